@@ -1,0 +1,84 @@
+"""Pins the CPU restatement (oracle/) against the Yjs 13.5.16 golden fixtures.
+
+The fixtures were produced by tests/golden/gen/gen_fixtures.js from the real Yjs bundle; the
+oracle must reproduce them byte for byte, in both client orders:
+  compat 136 (DS/SV sorted by client desc, Yjs 13.6 — the canonical form the engine emits) and
+  compat 135 (DS/SV in store-insertion order, exactly what Yjs 13.5.16 wrote).
+"""
+import json
+
+import pytest
+
+from oracle.yref import Doc, OracleError
+
+SETS = ("kat", "map", "array", "nested")
+
+
+def _cases(golden):
+    for s in SETS:
+        for c in golden[s]:
+            yield c
+
+
+def _apply(c, compat):
+    d = Doc(0x7FFFFFF0, compat)
+    for u in c["updates"]:
+        d.apply_update(bytes.fromhex(u))
+    return d
+
+
+@pytest.mark.parametrize("setname", SETS)
+def test_oracle_state_canonical(golden, setname):
+    for c in golden[setname]:
+        d = _apply(c, 136)
+        assert d.encode_state_as_update().hex() == c["state"], c["name"]
+        assert d.encode_state_vector().hex() == c["sv"], c["name"]
+
+
+@pytest.mark.parametrize("setname", SETS)
+def test_oracle_state_raw_13_5(golden, setname):
+    for c in golden[setname]:
+        d = _apply(c, 135)
+        assert d.encode_state_as_update().hex() == c["state_raw"], c["name"]
+        assert d.encode_state_vector().hex() == c["sv_raw"], c["name"]
+
+
+@pytest.mark.parametrize("setname", SETS)
+def test_oracle_json_and_deltas(golden, setname):
+    for c in golden[setname]:
+        d = _apply(c, 136)
+        for root, kind in c["roots"].items():
+            assert json.loads(d.root_json(root, kind)) == c["json"][root], (c["name"], root)
+        for df in c["diffs"]:
+            assert d.encode_state_as_update(bytes.fromhex(df["sv"])).hex() == df["update"], c["name"]
+
+
+def test_oracle_kats_literal():
+    # SURVEY.md App. A.6 literal bytes
+    d = Doc(1)
+    d.map_set("users", "user1", bytes([118, 1, 4]) + b"name" + bytes([119, 5]) + b"Alice")
+    assert list(d.encode_state_as_update()) == [1, 1, 1, 0, 40, 1, 5, 117, 115, 101, 114, 115, 5, 117, 115, 101, 114, 49, 1, 118, 1, 4, 110, 97, 109, 101, 119, 5, 65, 108, 105, 99, 101, 0]
+    assert list(d.encode_state_vector()) == [1, 1, 1]
+    e = Doc(3)
+    for i in range(5):
+        e.map_set("u", "x", bytes([125, i]))
+    assert list(e.encode_state_as_update()) == [1, 2, 3, 0, 33, 1, 1, 117, 1, 120, 4, 168, 3, 3, 1, 125, 4, 1, 3, 1, 0, 4]
+
+
+def test_oracle_rejects_garbage():
+    for bad in (b"", b"\x00", b"\x01\x05", bytes([1, 1, 1, 0, 40, 1]), b"\xff" * 8):
+        d = Doc(1)
+        with pytest.raises(OracleError):
+            d.apply_update(bad)
+
+
+def test_oracle_pending_reported():
+    a = Doc(1)
+    a.map_set("m", "k", bytes([125, 1]))
+    sv = a.encode_state_vector()
+    a.map_set("m", "k", bytes([125, 2]))
+    delta = a.encode_state_as_update(sv)
+    d = Doc(9)
+    with pytest.raises(OracleError) as ei:
+        d.apply_update(delta)
+    assert ei.value.code == -2
