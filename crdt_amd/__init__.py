@@ -1,0 +1,259 @@
+"""crdt_amd — MI355X-native batched Yjs merge engine (Python mirror of the `Y` surface).
+
+The reference (@ypear/crdt) talks to its CRDT engine only through the object injected as
+`router.options.Y` (reference crdt.js:175-180). This module exposes the same surface on top of
+the C ABI in include/ycrdt.h (libycrdt.so, hand-written gfx950 HIP kernels):
+
+    Doc()                         new Y.Doc()                      crdt.js:33,54,56,80,221
+    apply_update(doc, u8)         Y.applyUpdate(doc, u8)           crdt.js:35,56,58,85,294
+    apply_updates(doc, [u8])      n × Y.applyUpdate, one batch     crdt.js:79-98 (LevelDB replay)
+    encode_state_as_update(doc[, sv])  Y.encodeStateAsUpdate       crdt.js:56,260,288,347,443,...
+    encode_state_vector(doc)      Y.encodeStateVector(doc)         crdt.js:59,239,258,289
+
+Errors raise YcrdtError (the reference only reads `e.message`, crdt.js:38-39). There is no CPU
+fallback: importing works without a GPU, but every compute call needs the HIP device.
+"""
+import ctypes
+import os
+
+__all__ = [
+    "YcrdtError", "Engine", "Doc", "Batch", "MergeStats", "apply_update", "apply_updates",
+    "encode_state_as_update", "encode_state_vector", "default_engine", "library_path",
+]
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB = None
+
+YCRDT_OK = 0
+ERRORS = {
+    -1: "DECODE",
+    -2: "PENDING",
+    -3: "UNSUPPORTED",
+    -4: "CAPACITY",
+    -5: "DEVICE",
+    -6: "ARG",
+}
+
+
+class YcrdtError(Exception):
+    def __init__(self, code, message):
+        super().__init__(message)
+        self.code = code
+        self.kind = ERRORS.get(code, "UNKNOWN")
+
+
+class _Buf(ctypes.Structure):
+    _fields_ = [("ptr", ctypes.c_void_p), ("len", ctypes.c_size_t)]
+
+
+class _Out(ctypes.Structure):
+    _fields_ = [("ptr", ctypes.c_void_p), ("len", ctypes.c_size_t)]
+
+
+class MergeStats(ctypes.Structure):
+    _fields_ = [
+        ("in_bytes", ctypes.c_uint64),
+        ("items", ctypes.c_uint64),
+        ("structs", ctypes.c_uint64),
+        ("units", ctypes.c_uint64),
+        ("segments", ctypes.c_uint64),
+        ("out_structs", ctypes.c_uint64),
+        ("out_bytes", ctypes.c_uint64),
+        ("clients", ctypes.c_uint64),
+        ("device_ms", ctypes.c_double),
+    ]
+
+    def as_dict(self):
+        return {k: getattr(self, k) for k, _ in self._fields_}
+
+
+def library_path():
+    return os.path.join(_HERE, "libycrdt.so")
+
+
+EXPORTS = (
+    "ycrdt_engine_create", "ycrdt_engine_destroy", "ycrdt_engine_set_profiling", "ycrdt_engine_phase_times",
+    "ycrdt_doc_create", "ycrdt_doc_destroy", "ycrdt_apply_update", "ycrdt_apply_updates",
+    "ycrdt_encode_state_as_update", "ycrdt_encode_state_vector", "ycrdt_doc_last_stats",
+    "ycrdt_batch_stage", "ycrdt_batch_merge", "ycrdt_batch_result", "ycrdt_batch_destroy",
+    "ycrdt_free", "ycrdt_last_error", "ycrdt_version",
+)
+
+
+def lib():
+    """Loads libycrdt.so (built in-tree by __graft_entry__.build()); fails loudly if absent."""
+    global _LIB
+    if _LIB is not None:
+        return _LIB
+    path = library_path()
+    if not os.path.exists(path):
+        raise RuntimeError(f"{path} not built: run `python -c 'import __graft_entry__ as g; g.build()'`")
+    L = ctypes.CDLL(path)
+    vp, sz, u32, i32 = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint32, ctypes.c_int
+    P = ctypes.POINTER
+    L.ycrdt_engine_create.argtypes = [i32, i32, P(vp)]
+    L.ycrdt_engine_destroy.argtypes = [vp]
+    L.ycrdt_engine_set_profiling.argtypes = [vp, i32]
+    L.ycrdt_engine_phase_times.argtypes = [vp, P(ctypes.c_char_p), P(ctypes.c_double), i32]
+    L.ycrdt_doc_create.argtypes = [vp, u32, P(vp)]
+    L.ycrdt_doc_destroy.argtypes = [vp]
+    L.ycrdt_apply_update.argtypes = [vp, _Buf]
+    L.ycrdt_apply_updates.argtypes = [vp, P(_Buf), sz]
+    L.ycrdt_encode_state_as_update.argtypes = [vp, _Buf, P(_Out)]
+    L.ycrdt_encode_state_vector.argtypes = [vp, P(_Out)]
+    L.ycrdt_doc_last_stats.argtypes = [vp, P(MergeStats)]
+    L.ycrdt_batch_stage.argtypes = [vp, P(_Buf), sz, P(vp)]
+    L.ycrdt_batch_merge.argtypes = [vp, P(MergeStats)]
+    L.ycrdt_batch_result.argtypes = [vp, P(_Out), P(_Out)]
+    L.ycrdt_batch_destroy.argtypes = [vp]
+    L.ycrdt_free.argtypes = [P(_Out)]
+    L.ycrdt_last_error.restype = ctypes.c_char_p
+    L.ycrdt_version.restype = ctypes.c_char_p
+    _LIB = L
+    return L
+
+
+def _check(rc):
+    if rc != YCRDT_OK:
+        raise YcrdtError(rc, lib().ycrdt_last_error().decode(errors="replace"))
+
+
+def _bufs(updates):
+    keep = [bytes(u) for u in updates]
+    arr = (_Buf * max(1, len(keep)))()
+    for i, u in enumerate(keep):
+        arr[i].ptr = ctypes.cast(ctypes.c_char_p(u), ctypes.c_void_p)
+        arr[i].len = len(u)
+    return arr, keep
+
+
+def _take(out):
+    try:
+        return ctypes.string_at(out.ptr, out.len) if out.len else b""
+    finally:
+        lib().ycrdt_free(ctypes.byref(out))
+
+
+class Engine:
+    """One HIP device + stream + HBM workspace (compat 136 = Yjs 13.6 canonical client order)."""
+
+    def __init__(self, device=0, compat=136):
+        h = ctypes.c_void_p()
+        _check(lib().ycrdt_engine_create(device, compat, ctypes.byref(h)))
+        self._h = h
+
+    def close(self):
+        if getattr(self, "_h", None):
+            lib().ycrdt_engine_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def set_profiling(self, on=True):
+        _check(lib().ycrdt_engine_set_profiling(self._h, 1 if on else 0))
+
+    def phase_times(self):
+        names = (ctypes.c_char_p * 64)()
+        ms = (ctypes.c_double * 64)()
+        n = lib().ycrdt_engine_phase_times(self._h, names, ms, 64)
+        return [(names[i].decode(), ms[i]) for i in range(n)]
+
+
+_DEFAULT = None
+
+
+def default_engine():
+    global _DEFAULT
+    if _DEFAULT is None:
+        _DEFAULT = Engine(int(os.environ.get("YCRDT_DEVICE", "0")))
+    return _DEFAULT
+
+
+class Doc:
+    """Y.Doc backed by the GPU engine. The canonical encoded state lives in HBM."""
+
+    def __init__(self, client_id=None, engine=None):
+        self.engine = engine or default_engine()
+        h = ctypes.c_void_p()
+        cid = client_id if client_id is not None else int.from_bytes(os.urandom(4), "little")
+        _check(lib().ycrdt_doc_create(self.engine._h, cid, ctypes.byref(h)))
+        self._h = h
+        self.client_id = cid
+
+    def __del__(self):
+        if getattr(self, "_h", None):
+            lib().ycrdt_doc_destroy(self._h)
+            self._h = None
+
+    def apply_update(self, update: bytes):
+        u = bytes(update)
+        b = _Buf(ctypes.cast(ctypes.c_char_p(u), ctypes.c_void_p), len(u))
+        _check(lib().ycrdt_apply_update(self._h, b))
+
+    def apply_updates(self, updates):
+        arr, keep = _bufs(updates)
+        _check(lib().ycrdt_apply_updates(self._h, arr, len(keep)))
+
+    def encode_state_as_update(self, sv: bytes = b"") -> bytes:
+        s = bytes(sv or b"")
+        b = _Buf(ctypes.cast(ctypes.c_char_p(s), ctypes.c_void_p), len(s))
+        out = _Out()
+        _check(lib().ycrdt_encode_state_as_update(self._h, b, ctypes.byref(out)))
+        return _take(out)
+
+    def encode_state_vector(self) -> bytes:
+        out = _Out()
+        _check(lib().ycrdt_encode_state_vector(self._h, ctypes.byref(out)))
+        return _take(out)
+
+    def last_stats(self) -> MergeStats:
+        st = MergeStats()
+        _check(lib().ycrdt_doc_last_stats(self._h, ctypes.byref(st)))
+        return st
+
+
+class Batch:
+    """A set of updates staged in HBM; merge() runs the whole merge on the device."""
+
+    def __init__(self, updates, engine=None):
+        self.engine = engine or default_engine()
+        arr, keep = _bufs(updates)
+        h = ctypes.c_void_p()
+        _check(lib().ycrdt_batch_stage(self.engine._h, arr, len(keep), ctypes.byref(h)))
+        self._h = h
+
+    def __del__(self):
+        if getattr(self, "_h", None):
+            lib().ycrdt_batch_destroy(self._h)
+            self._h = None
+
+    def merge(self) -> MergeStats:
+        st = MergeStats()
+        _check(lib().ycrdt_batch_merge(self._h, ctypes.byref(st)))
+        return st
+
+    def result(self):
+        u, s = _Out(), _Out()
+        _check(lib().ycrdt_batch_result(self._h, ctypes.byref(u), ctypes.byref(s)))
+        return _take(u), _take(s)
+
+
+# ---- the `Y` functions the reference calls ---------------------------------------------------
+def apply_update(doc: Doc, update: bytes):
+    doc.apply_update(update)
+
+
+def apply_updates(doc: Doc, updates):
+    doc.apply_updates(updates)
+
+
+def encode_state_as_update(doc: Doc, sv: bytes = b"") -> bytes:
+    return doc.encode_state_as_update(sv)
+
+
+def encode_state_vector(doc: Doc) -> bytes:
+    return doc.encode_state_vector()

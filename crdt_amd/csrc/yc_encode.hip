@@ -1,0 +1,311 @@
+// yc_encode.hip — K7: state vector + (delta) re-encode of the merged store as a Yjs v1 update.
+//
+// Restates encodeStateAsUpdate (Y@22505 → writeClientsStructs Y@19025 → writeStructs Y@18809 →
+// Item.write Y@80416) and createDeleteSetFromStructStore + writeDeleteSet (Y@10800 / Y@11105):
+//   * client blocks are written in descending client order; a client is included when its state
+//     exceeds the target state vector, and its first struct is written with offset sv − clock;
+//   * the delete set is always the full store's runs of consecutive deleted structs, clients in
+//     descending order (Yjs 13.6 canonical order; 13.5.16 used store insertion order).
+// Every size is computed first (one lane per output struct / run / client), positions come from
+// exclusive scans, then a second pass writes the bytes.
+#include "yc_work.h"
+
+namespace yc {
+
+__device__ __forceinline__ uint32_t* ccol(const Work& w, uint32_t col) { return w.cc + (size_t)col * (w.cap_clients + 1); }
+
+__device__ __forceinline__ uint32_t unit_client(const Work& w, uint32_t nclients, uint32_t g) {
+  uint32_t lo = 0, hi = nclients;  // last c with cl_base[c] <= g
+  while (hi - lo > 1) { const uint32_t mid = (lo + hi) >> 1; if (w.cl_base[mid] <= g) lo = mid; else hi = mid; }
+  return lo;
+}
+
+__device__ __forceinline__ uint32_t copy_bytes(uint8_t* __restrict__ o, uint32_t p, const uint8_t* __restrict__ src, uint32_t n) {
+  for (uint32_t i = 0; i < n; ++i) o[p + i] = src[i];
+  return p + n;
+}
+
+// Encodes output struct `o` (segments [a,b)) at position p when WRITE, returns the size.
+template <bool WRITE>
+__device__ uint32_t encode_struct(const Work& w, uint32_t nclients, uint32_t o, uint8_t* __restrict__ out, uint32_t p0) {
+  const uint32_t a = w.o_first[o], b = w.o_first[o + 1];
+  const uint32_t cidx = w.g_cidx[a];
+  const uint64_t base = w.cl_base[cidx];
+  const uint32_t k0 = (uint32_t)(w.g_start[a] - base), k1 = (uint32_t)(w.g_start[b] - base);
+  const uint32_t cs = w.cl_start[cidx];
+  if (k1 <= cs) return 0;
+  const uint32_t off = cs > k0 ? cs - k0 : 0;
+  const uint32_t len = k1 - k0;
+  const uint32_t f = w.g_flags[a];
+  const uint32_t src = w.g_src[a];
+  uint32_t p = p0;
+  if (!(f & SEG_ITEM)) {  // GC.write
+    if (WRITE) { out[p++] = REF_GC; p = wr_vu(out, p, len - off); return p - p0; }
+    return 1 + vu_size(len - off);
+  }
+  const bool del = (f & SEG_DEL) != 0;
+  const uint32_t ref = del ? (uint32_t)REF_DELETED : (w.s_info[src] & 31u);
+  uint32_t oclient = 0, oclock = 0;
+  bool has_o = false;
+  if (off > 0) { has_o = true; oclient = w.cl_vals[cidx]; oclock = k0 + off - 1; }
+  else if (w.g_origin[a] != NONE) {
+    const uint32_t g = w.g_origin[a];
+    const uint32_t c = unit_client(w, nclients, g);
+    has_o = true;
+    oclient = w.cl_vals[c];
+    oclock = (uint32_t)(g - w.cl_base[c]);
+  }
+  bool has_r = false;
+  uint32_t rclient = 0, rclock = 0;
+  if (w.g_rorigin[a] != NONE) {
+    const uint32_t g = w.g_rorigin[a];
+    const uint32_t c = unit_client(w, nclients, g);
+    has_r = true;
+    rclient = w.cl_vals[c];
+    rclock = (uint32_t)(g - w.cl_base[c]);
+  }
+  const uint32_t info = ref | (has_o ? 0x80u : 0u) | (has_r ? 0x40u : 0u) | 0x20u;  // round 1: every item is a map entry
+  uint32_t size = 1;
+  if (WRITE) out[p++] = (uint8_t)info;
+  if (has_o) {
+    if (WRITE) { p = wr_vu(out, p, oclient); p = wr_vu(out, p, oclock); }
+    size += vu_size(oclient) + vu_size(oclock);
+  }
+  if (has_r) {
+    if (WRITE) { p = wr_vu(out, p, rclient); p = wr_vu(out, p, rclock); }
+    size += vu_size(rclient) + vu_size(rclock);
+  }
+  if (!has_o && !has_r) {  // parent info (root type name) + parentSub
+    const uint32_t pa = w.s_pa[src], pb = w.s_pb[src];
+    const uint32_t ps = w.s_psub[src], pl = w.s_psublen[src];
+    if (WRITE) {
+      out[p++] = 1;
+      p = copy_bytes(out, p, w.bytes + pa, pb);
+      p = copy_bytes(out, p, w.bytes + ps, pl);
+    }
+    size += 1 + pb + pl;
+  }
+  if (del) {
+    if (WRITE) p = wr_vu(out, p, len - off);
+    size += vu_size(len - off);
+  } else if (ref == REF_ANY || ref == REF_JSON) {
+    if (WRITE) p = wr_vu(out, p, len - off);
+    size += vu_size(len - off);
+    for (uint32_t s = a; s < b; ++s) {  // every live segment covers its whole (single-value) source
+      const uint32_t sr = w.g_src[s];
+      const uint32_t n = w.s_cend[sr] - w.s_celem[sr];
+      if (WRITE) p = copy_bytes(out, p, w.bytes + w.s_celem[sr], n);
+      size += n;
+    }
+  } else {  // Binary / Doc: one unit, verbatim content bytes
+    const uint32_t n = w.s_cend[src] - w.s_cpos[src];
+    if (WRITE) p = copy_bytes(out, p, w.bytes + w.s_cpos[src], n);
+    size += n;
+  }
+  return size;
+}
+
+__global__ __launch_bounds__(256) void k_out_sizes(Work w, uint32_t nout, uint32_t nclients) {
+  const uint32_t o = blockIdx.x * blockDim.x + threadIdx.x;
+  if (o > nout) return;
+  if (o == nout) { w.o_size[o] = 0; return; }
+  w.o_cidx[o] = w.g_cidx[w.o_first[o]];
+  w.o_size[o] = encode_struct<false>(w, nclients, o, nullptr, 0);
+}
+
+// runs of consecutive deleted segments (createDeleteSetFromStructStore)
+__device__ __forceinline__ bool seg_deleted(uint32_t f) { return (f & SEG_DEL) || !(f & SEG_ITEM); }
+__global__ void k_run_flags(Work w, uint32_t nsegs) {
+  const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
+  if (s > nsegs) return;
+  if (s == nsegs) { w.g_tmp[s] = 0; return; }
+  const bool d = seg_deleted(w.g_flags[s]);
+  const bool start = d && (s == 0 || w.g_cidx[s - 1] != w.g_cidx[s] || !seg_deleted(w.g_flags[s - 1]));
+  w.g_tmp[s] = start ? 1u : 0u;
+}
+__global__ void k_run_fill(Work w, uint32_t nsegs) {
+  const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= nsegs) return;
+  if (!seg_deleted(w.g_flags[s])) return;
+  const uint32_t rid = w.g_tmp2[s + 1] - 1;  // inclusive count of run starts up to s
+  const uint32_t units = w.g_start[s + 1] - w.g_start[s];
+  if (w.g_tmp2[s + 1] != w.g_tmp2[s]) {     // s starts run rid
+    w.r_seg[rid] = s;
+    atomicAdd(&ccol(w, CC_NRUNS)[w.g_cidx[s]], 1u);
+  }
+  atomicAdd(&w.r_len[rid], units);
+}
+__global__ void k_run_sizes(Work w, uint32_t nruns) {
+  const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r > nruns) return;
+  if (r == nruns) { w.r_size[r] = 0; return; }
+  const uint32_t s = w.r_seg[r];
+  const uint32_t clock = (uint32_t)(w.g_start[s] - w.cl_base[w.g_cidx[s]]);
+  w.r_size[r] = vu_size(clock) + vu_size(w.r_len[r]);
+}
+
+// per client: struct block + delete-set block + state-vector entry sizes
+__global__ void k_client_sizes(Work w, uint32_t nclients, uint32_t nout, uint32_t nruns) {
+  const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c > nclients) return;
+  uint32_t* first_out = ccol(w, CC_FIRST_OUT);
+  if (c == nclients) {
+    ccol(w, CC_BLK)[c] = 0; ccol(w, CC_DSBLK)[c] = 0; ccol(w, CC_SV)[c] = 0;
+    return;
+  }
+  // first output struct of client c (outputs are sorted by client)
+  const uint32_t fo = lower_bound_u32(w.o_cidx, nout, c);
+  const uint32_t eo = lower_bound_u32(w.o_cidx, nout, c + 1);
+  first_out[c] = fo;
+  const uint32_t state = w.cl_state[c];
+  const uint32_t cs = w.cl_start[c];
+  uint32_t blk = 0, nincl = 0, fi = eo;
+  if (state > cs && eo > fo) {
+    // first included output: the one containing clock cs
+    uint32_t lo = fo, hi = eo;
+    while (lo < hi) {
+      const uint32_t mid = (lo + hi) >> 1;
+      const uint32_t k1 = (uint32_t)(w.g_start[w.o_first[mid + 1]] - w.cl_base[c]);
+      if (k1 <= cs) lo = mid + 1; else hi = mid;
+    }
+    fi = lo;
+    nincl = eo - fi;
+    const uint32_t hdr = vu_size(nincl) + vu_size(w.cl_vals[c]) + vu_size(cs);
+    ccol(w, CC_HDR)[c] = hdr;
+    blk = hdr + (w.o_pos[eo] - w.o_pos[fi]);
+    atomicAdd(&w.ctr->pad[0], 1u);  // included clients
+  }
+  ccol(w, CC_FIRST_INCL)[c] = fi;
+  ccol(w, CC_NINCL)[c] = nincl;
+  ccol(w, CC_BLK)[c] = blk;
+  // delete-set block
+  const uint32_t nr = ccol(w, CC_NRUNS)[c];
+  uint32_t dsblk = 0;
+  if (nr) {
+    // first run of client c: runs are ordered by (client, clock)
+    uint32_t lo = 0, hi = nruns;
+    while (lo < hi) {
+      const uint32_t mid = (lo + hi) >> 1;
+      if (w.g_cidx[w.r_seg[mid]] < c) lo = mid + 1; else hi = mid;
+    }
+    ccol(w, CC_FIRST_RUN)[c] = lo;
+    dsblk = vu_size(w.cl_vals[c]) + vu_size(nr) + (w.r_pos[lo + nr] - w.r_pos[lo]);
+    atomicAdd(&w.ctr->pad[1], 1u);  // ds clients
+  }
+  ccol(w, CC_DSBLK)[c] = dsblk;
+  ccol(w, CC_SV)[c] = state ? vu_size(w.cl_vals[c]) + vu_size(state) : 0;
+  if (state) atomicAdd(&w.ctr->pad[2], 1u);  // sv entries
+}
+
+// reverse a per-client column so that an ascending scan yields descending-client positions
+__global__ void k_reverse(Work w, uint32_t nclients, uint32_t col) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i > nclients) return;
+  ccol(w, CC_REV)[i] = i < nclients ? ccol(w, col)[nclients - 1 - i] : 0;
+}
+__global__ void k_unreverse(Work w, uint32_t nclients, uint32_t col) {
+  const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c > nclients) return;
+  // position of client c = sum of blocks of clients > c = scan[nclients-1-c]; total at [nclients]
+  ccol(w, col)[c] = c < nclients ? ccol(w, CC_REVSCAN)[nclients - 1 - c] : ccol(w, CC_REVSCAN)[nclients];
+}
+
+__global__ void k_totals(Work w, uint32_t nclients) {
+  const uint32_t nincl = w.ctr->pad[0], nds = w.ctr->pad[1], nsv = w.ctr->pad[2];
+  const uint32_t sblk = ccol(w, CC_BLKPOS)[nclients];
+  const uint32_t sds = ccol(w, CC_DSPOS)[nclients];
+  const uint32_t ssv = ccol(w, CC_SVPOS)[nclients];
+  w.ctr->pad[3] = vu_size(nincl);                 // struct section header size
+  w.ctr->pad[4] = vu_size(nincl) + sblk;          // delete-set section start
+  w.ctr->out_bytes = vu_size(nincl) + sblk + vu_size(nds) + sds;
+  w.ctr->sv_bytes = vu_size(nsv) + ssv;
+}
+
+__global__ __launch_bounds__(256) void k_write_structs(Work w, uint32_t nout, uint32_t nclients) {
+  const uint32_t o = blockIdx.x * blockDim.x + threadIdx.x;
+  if (o >= nout) return;
+  if (w.o_size[o] == 0) return;
+  const uint32_t c = w.o_cidx[o];
+  const uint32_t fi = ccol(w, CC_FIRST_INCL)[c];
+  const uint32_t p = w.ctr->pad[3] + ccol(w, CC_BLKPOS)[c] + ccol(w, CC_HDR)[c] + (w.o_pos[o] - w.o_pos[fi]);
+  encode_struct<true>(w, nclients, o, w.out, p);
+}
+__global__ void k_write_clients(Work w, uint32_t nclients) {
+  const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c == 0) {
+    wr_vu(w.out, 0, w.ctr->pad[0]);
+    wr_vu(w.out, w.ctr->pad[4], w.ctr->pad[1]);
+    wr_vu(w.sv_out, 0, w.ctr->pad[2]);
+  }
+  if (c >= nclients) return;
+  if (ccol(w, CC_NINCL)[c]) {
+    uint32_t p = w.ctr->pad[3] + ccol(w, CC_BLKPOS)[c];
+    p = wr_vu(w.out, p, ccol(w, CC_NINCL)[c]);
+    p = wr_vu(w.out, p, w.cl_vals[c]);
+    wr_vu(w.out, p, w.cl_start[c]);
+  }
+  const uint32_t nr = ccol(w, CC_NRUNS)[c];
+  if (nr) {
+    const uint32_t dsbase = w.ctr->pad[4] + vu_size(w.ctr->pad[1]);
+    uint32_t p = dsbase + ccol(w, CC_DSPOS)[c];
+    p = wr_vu(w.out, p, w.cl_vals[c]);
+    wr_vu(w.out, p, nr);
+  }
+  if (w.cl_state[c]) {
+    uint32_t p = vu_size(w.ctr->pad[2]) + ccol(w, CC_SVPOS)[c];
+    p = wr_vu(w.sv_out, p, w.cl_vals[c]);
+    wr_vu(w.sv_out, p, w.cl_state[c]);
+  }
+}
+__global__ void k_write_runs(Work w, uint32_t nruns) {
+  const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= nruns) return;
+  const uint32_t s = w.r_seg[r];
+  const uint32_t c = w.g_cidx[s];
+  const uint32_t first = ccol(w, CC_FIRST_RUN)[c];
+  const uint32_t nr = ccol(w, CC_NRUNS)[c];
+  const uint32_t dsbase = w.ctr->pad[4] + vu_size(w.ctr->pad[1]);
+  uint32_t p = dsbase + ccol(w, CC_DSPOS)[c] + vu_size(w.cl_vals[c]) + vu_size(nr) + (w.r_pos[r] - w.r_pos[first]);
+  p = wr_vu(w.out, p, (uint32_t)(w.g_start[s] - w.cl_base[c]));
+  wr_vu(w.out, p, w.r_len[r]);
+}
+
+static void rev_scan(const Work& w, uint32_t nclients, uint32_t col_in, uint32_t col_out, hipStream_t s) {
+  const uint32_t grid = nclients / 256 + 1;
+  hipLaunchKernelGGL(k_reverse, dim3(grid), dim3(256), 0, s, w, nclients, col_in);
+  scan_u32(w.tmp, w.tmp_bytes, w.cc + (size_t)CC_REV * (w.cap_clients + 1), w.cc + (size_t)CC_REVSCAN * (w.cap_clients + 1),
+           nclients + 1, s);
+  hipLaunchKernelGGL(k_unreverse, dim3(grid), dim3(256), 0, s, w, nclients, col_out);
+}
+
+// Phase 1: sizes + layout (ends with out_bytes / sv_bytes in the counters)
+void launch_encode_sizes(const Work& w, uint32_t nsegs, uint32_t nclients, uint32_t nout, uint32_t* nruns_host, hipStream_t s) {
+  hipMemsetAsync(w.ctr->pad, 0, sizeof(uint32_t) * 8, s);
+  hipMemsetAsync(w.cc + (size_t)CC_NRUNS * (w.cap_clients + 1), 0, sizeof(uint32_t) * (w.cap_clients + 1), s);
+  hipLaunchKernelGGL(k_out_sizes, dim3(nout / 256 + 1), dim3(256), 0, s, w, nout, nclients);
+  scan_u32(w.tmp, w.tmp_bytes, w.o_size, w.o_pos, nout + 1, s);
+  // delete-set runs
+  hipLaunchKernelGGL(k_run_flags, dim3(nsegs / 256 + 1), dim3(256), 0, s, w, nsegs);
+  scan_u32(w.tmp, w.tmp_bytes, w.g_tmp, w.g_tmp2, nsegs + 1, s);
+  hipMemcpyAsync(nruns_host, w.g_tmp2 + nsegs, sizeof(uint32_t), hipMemcpyDeviceToHost, s);
+  hipStreamSynchronize(s);
+  const uint32_t nruns = *nruns_host;
+  hipMemsetAsync(w.r_len, 0, sizeof(uint32_t) * (nruns + 1), s);
+  if (nsegs) hipLaunchKernelGGL(k_run_fill, dim3((nsegs + 255) / 256), dim3(256), 0, s, w, nsegs);
+  hipLaunchKernelGGL(k_run_sizes, dim3(nruns / 256 + 1), dim3(256), 0, s, w, nruns);
+  scan_u32(w.tmp, w.tmp_bytes, w.r_size, w.r_pos, nruns + 1, s);
+  hipLaunchKernelGGL(k_client_sizes, dim3(nclients / 256 + 1), dim3(256), 0, s, w, nclients, nout, nruns);
+  rev_scan(w, nclients, CC_BLK, CC_BLKPOS, s);
+  rev_scan(w, nclients, CC_DSBLK, CC_DSPOS, s);
+  rev_scan(w, nclients, CC_SV, CC_SVPOS, s);
+  hipLaunchKernelGGL(k_totals, dim3(1), dim3(1), 0, s, w, nclients);
+}
+
+// Phase 2: write bytes (buffers sized from phase 1)
+void launch_encode_write(const Work& w, uint32_t nclients, uint32_t nout, uint32_t nruns, hipStream_t s) {
+  hipLaunchKernelGGL(k_write_clients, dim3(nclients / 256 + 1), dim3(256), 0, s, w, nclients);
+  if (nout) hipLaunchKernelGGL(k_write_structs, dim3((nout + 255) / 256), dim3(256), 0, s, w, nout, nclients);
+  if (nruns) hipLaunchKernelGGL(k_write_runs, dim3((nruns + 255) / 256), dim3(256), 0, s, w, nruns);
+}
+
+}  // namespace yc

@@ -1,0 +1,669 @@
+// yc_engine.hip — host orchestration of the batched merge + the C ABI (include/ycrdt.h).
+//
+// One engine = one HIP device + one stream + a grow-only set of HBM buffers. A merge runs the
+// decode → dedupe → delete-set → segmentation → map-winner → encode kernels back to back on the
+// engine stream; the host only reads a handful of counters at the sync points where the next
+// phase's size depends on data (struct count, unit count, segment count, output bytes).
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+#include <unordered_map>
+#include <algorithm>
+
+#include "yc_work.h"
+#include "../../include/ycrdt.h"
+
+using namespace yc;
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string& msg) {
+  g_err = msg;
+  return code;
+}
+
+#define HIPCHK(x)                                                                                    \
+  do {                                                                                               \
+    hipError_t _e = (x);                                                                             \
+    if (_e != hipSuccess) return fail(YCRDT_E_DEVICE, std::string("HIP error: ") + hipGetErrorString(_e) + " at " #x); \
+  } while (0)
+
+struct DevBuf {
+  void* p = nullptr;
+  size_t cap = 0;
+};
+
+bool grow(DevBuf& b, size_t bytes) {
+  if (bytes == 0) bytes = 16;
+  if (bytes <= b.cap) return true;
+  if (b.p) hipFree(b.p);
+  b.p = nullptr;
+  b.cap = 0;
+  size_t c = bytes + bytes / 4 + 256;
+  if (hipMalloc(&b.p, c) != hipSuccess) return false;
+  b.cap = c;
+  return true;
+}
+
+template <class T>
+T* take(std::vector<DevBuf>& v, size_t idx, size_t n, bool& ok) {
+  if (v.size() <= idx) v.resize(idx + 1);
+  if (!grow(v[idx], n * sizeof(T))) { ok = false; return nullptr; }
+  return (T*)v[idx].p;
+}
+
+uint32_t next_pow2(uint64_t v) {
+  uint64_t p = 1;
+  while (p < v) p <<= 1;
+  return (uint32_t)std::min<uint64_t>(p, 1ull << 31);
+}
+
+// decode a state vector (varuint n, (client, clock) × n)
+bool parse_sv(const uint8_t* p, size_t n, std::unordered_map<uint32_t, uint32_t>& out) {
+  size_t pos = 0;
+  auto vu = [&](uint32_t& v) -> bool {
+    uint32_t r = 0;
+    int shift = 0;
+    for (;;) {
+      if (pos >= n) return false;
+      uint32_t b = p[pos++];
+      if (shift < 32) r |= (b & 0x7fu) << shift;
+      shift += 7;
+      if (b < 0x80) { v = r; return true; }
+      if (shift > 35) return false;
+    }
+  };
+  uint32_t k;
+  if (!vu(k)) return false;
+  for (uint32_t i = 0; i < k; ++i) {
+    uint32_t c, cl;
+    if (!vu(c) || !vu(cl)) return false;
+    out[c] = cl;
+  }
+  return true;
+}
+
+enum Buf {
+  B_BYTES, B_META, B_CTR, B_MAIN, B_FINAL, B_SECB, B_GPRE, B_GEXIT, B_COPY, B_PATCH, B_DSSTART, B_SECT, B_SECSORT,
+  B_WCNT, B_WSEC, B_DS, B_DSLEN, B_DSSCAN, B_SCRATCH, B_TMP,
+  B_SPOS, B_SSEC, B_SLEN, B_SLENSCAN, B_SCLOCK, B_SCIDX, B_SINFO, B_SOC, B_SOK, B_SRC, B_SRK, B_SPA, B_SPB, B_SPS, B_SPL,
+  B_SCPOS, B_SCEND, B_SCELEM,
+  B_CLVALS, B_CLTMP, B_CLSTATE, B_CLBASE, B_CLSTART, B_CC,
+  B_UOWN, B_UFLAG, B_UMIN, B_UCUT, B_UWPRE,
+  B_GSTART, B_GCIDX, B_GSRC, B_GFLAGS, B_GORIG, B_GRORIG, B_GLINK, B_GKEY, B_GMAXC, B_GNEXT, B_GOUTID, B_GTMP, B_GTMP2,
+  B_KHASH, B_KROOT, B_KWIN,
+  B_OFIRST, B_OCIDX, B_OSIZE, B_OPOS, B_RSEG, B_RLEN, B_RSIZE, B_RPOS, B_OUT, B_SVOUT,
+  B_COUNT
+};
+
+}  // namespace
+
+struct ycrdt_engine {
+  int device = 0;
+  int compat = 136;
+  hipStream_t stream = nullptr;
+  std::vector<DevBuf> bufs;
+  Work w;
+  bool profiling = false;
+  std::vector<std::pair<const char*, hipEvent_t>> marks;
+  std::vector<std::pair<const char*, double>> phase_ms;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  std::vector<uint8_t> pinned_stage;
+  // result of the last merge
+  uint32_t out_bytes = 0, sv_bytes = 0;
+  ycrdt_merge_stats last{};
+};
+
+struct ycrdt_doc {
+  ycrdt_engine* e = nullptr;
+  uint32_t client_id = 0;
+  DevBuf state;          // canonical encoded state (Yjs v1 update) in HBM
+  size_t state_len = 0;  // 0 = empty doc
+  std::vector<uint8_t> sv;
+  ycrdt_merge_stats last{};
+};
+
+struct ycrdt_batch {
+  ycrdt_engine* e = nullptr;
+  DevBuf bytes, meta;
+  std::vector<uint32_t> uoff, ulen, ugroup;
+  std::vector<Group> groups;
+  uint32_t nbytes = 0;
+  uint64_t in_bytes = 0;
+  bool merged = false;
+};
+
+namespace {
+
+void mark(ycrdt_engine* e, const char* name) {
+  if (!e->profiling) return;
+  hipEvent_t ev;
+  hipEventCreate(&ev);
+  hipEventRecord(ev, e->stream);
+  e->marks.push_back({name, ev});
+}
+
+// Lays out n updates (64-byte aligned) + decode group table. `prefix` (device) is placed first.
+void layout(ycrdt_batch* b, const ycrdt_buf* ups, size_t n, size_t prefix_len) {
+  size_t total = prefix_len ? ((prefix_len + 63) & ~size_t(63)) : 0;
+  b->uoff.clear(); b->ulen.clear(); b->ugroup.clear(); b->groups.clear();
+  b->in_bytes = 0;
+  auto add = [&](size_t off, size_t len) {
+    b->uoff.push_back((uint32_t)off);
+    b->ulen.push_back((uint32_t)len);
+    b->ugroup.push_back((uint32_t)b->groups.size());
+    for (size_t g = 0; g < len; g += GROUP_BYTES) {
+      Group G;
+      G.start = (uint32_t)(off + g);
+      G.end = (uint32_t)std::min(off + len, off + g + GROUP_BYTES);
+      G.uend = (uint32_t)(off + len);
+      G.upd = (uint32_t)(b->uoff.size() - 1);
+      b->groups.push_back(G);
+    }
+    b->in_bytes += len;
+  };
+  if (prefix_len) add(0, prefix_len);
+  for (size_t i = 0; i < n; ++i) {
+    add(total, ups[i].len);
+    total += (ups[i].len + 63) & ~size_t(63);
+  }
+  b->uoff.push_back((uint32_t)total);
+  b->nbytes = (uint32_t)total;
+}
+
+int stage(ycrdt_batch* b, const ycrdt_buf* ups, size_t n, const DevBuf* prefix, size_t prefix_len) {
+  ycrdt_engine* e = b->e;
+  size_t total64 = 0;
+  for (size_t i = 0; i < n; ++i) total64 += ((ups[i].len + 63) & ~size_t(63));
+  total64 += prefix_len ? ((prefix_len + 63) & ~size_t(63)) : 0;
+  if (total64 >= 0xF0000000ull) return fail(YCRDT_E_CAPACITY, "batch larger than 3.75 GiB");
+  layout(b, ups, n, prefix_len);
+  if (!grow(b->bytes, (size_t)b->nbytes + 128)) return fail(YCRDT_E_DEVICE, "hipMalloc failed (batch bytes)");
+  // pack on the host, one H2D copy
+  e->pinned_stage.assign((size_t)b->nbytes - (prefix_len ? ((prefix_len + 63) & ~size_t(63)) : 0), 0);
+  size_t base = prefix_len ? ((prefix_len + 63) & ~size_t(63)) : 0;
+  const size_t nu0 = prefix_len ? 1 : 0;
+  for (size_t i = 0; i < n; ++i)
+    if (ups[i].len) memcpy(e->pinned_stage.data() + (b->uoff[nu0 + i] - base), ups[i].ptr, ups[i].len);
+  if (prefix_len) HIPCHK(hipMemcpyAsync(b->bytes.p, prefix->p, prefix_len, hipMemcpyDeviceToDevice, e->stream));
+  if (!e->pinned_stage.empty())
+    HIPCHK(hipMemcpyAsync((uint8_t*)b->bytes.p + base, e->pinned_stage.data(), e->pinned_stage.size(), hipMemcpyHostToDevice, e->stream));
+  // meta: uoff | ulen | ugroup | groups
+  const size_t nu = b->ulen.size();
+  const size_t meta_bytes = sizeof(uint32_t) * (nu + 1 + nu + nu) + sizeof(Group) * b->groups.size() + 64;
+  if (!grow(b->meta, meta_bytes)) return fail(YCRDT_E_DEVICE, "hipMalloc failed (meta)");
+  std::vector<uint8_t> meta(meta_bytes, 0);
+  size_t o = 0;
+  memcpy(meta.data() + o, b->uoff.data(), sizeof(uint32_t) * (nu + 1)); o += sizeof(uint32_t) * (nu + 1);
+  memcpy(meta.data() + o, b->ulen.data(), sizeof(uint32_t) * nu); o += sizeof(uint32_t) * nu;
+  memcpy(meta.data() + o, b->ugroup.data(), sizeof(uint32_t) * nu); o += sizeof(uint32_t) * nu;
+  o = (o + 15) & ~size_t(15);
+  if (!b->groups.empty()) memcpy(meta.data() + o, b->groups.data(), sizeof(Group) * b->groups.size());
+  HIPCHK(hipMemcpyAsync(b->meta.p, meta.data(), meta_bytes, hipMemcpyHostToDevice, e->stream));
+  HIPCHK(hipStreamSynchronize(e->stream));
+  b->merged = false;
+  return YCRDT_OK;
+}
+
+int map_err(uint32_t code, const char* where) {
+  switch (code) {
+    case ERR_DECODE: return fail(YCRDT_E_DECODE, std::string("Integer out of range! (malformed update, ") + where + ")");
+    case ERR_PENDING: return fail(YCRDT_E_PENDING, std::string("update has missing dependencies (pending) at ") + where);
+    case ERR_UNSUPPORTED: return fail(YCRDT_E_UNSUPPORTED, std::string("input outside the engine's current coverage (see DESIGN.md) at ") + where);
+    case ERR_CAPACITY: return fail(YCRDT_E_CAPACITY, std::string("capacity exceeded at ") + where);
+    default: return fail(YCRDT_E_DEVICE, "unknown device error");
+  }
+}
+
+// Reads the counters (sync) and returns an error if the device raised one.
+int check(ycrdt_engine* e, Counters& c, const char* where) {
+  HIPCHK(hipMemcpyAsync(&c, e->w.ctr, sizeof(Counters), hipMemcpyDeviceToHost, e->stream));
+  HIPCHK(hipStreamSynchronize(e->stream));
+  if (c.err) return map_err(c.err, where);
+  return YCRDT_OK;
+}
+
+// The whole batched merge. `target` (optional) selects a delta encode against a state vector.
+int run_merge(ycrdt_engine* e, ycrdt_batch* b, const std::unordered_map<uint32_t, uint32_t>* target) {
+  Work& w = e->w;
+  auto& V = e->bufs;
+  bool ok = true;
+  hipStream_t s = e->stream;
+  for (auto& m : e->marks) hipEventDestroy(m.second);
+  e->marks.clear();
+  e->phase_ms.clear();
+  HIPCHK(hipEventRecord(e->ev0, s));
+  mark(e, "start");
+  // ---- inputs
+  const uint32_t nu = (uint32_t)b->ulen.size();
+  w.bytes = (const uint8_t*)b->bytes.p;
+  w.nbytes = b->nbytes;
+  w.nupd = nu;
+  w.uoff = (const uint32_t*)b->meta.p;
+  w.ulen = w.uoff + nu + 1;
+  w.ugroup = w.ulen + nu;
+  {
+    size_t o = sizeof(uint32_t) * (nu + 1 + nu + nu);
+    o = (o + 15) & ~size_t(15);
+    w.groups = (const Group*)((const uint8_t*)b->meta.p + o);
+  }
+  w.ngroups = (uint32_t)b->groups.size();
+  const uint64_t B = (uint64_t)b->nbytes + 64;
+  const uint64_t nwords = B / 64 + 2;
+  w.cap_structs = (uint32_t)(B / 2 + 64);
+  w.cap_sections = (uint32_t)(B / 3 + 64);
+  w.cap_copy = w.ngroups + w.cap_sections + 64;
+  w.cap_patch = w.cap_structs;
+  w.cap_ds = (uint32_t)(B / 2 + 64);
+  // ---- decode buffers
+  w.ctr = take<Counters>(V, B_CTR, 1, ok);
+  w.main_bits = take<uint64_t>(V, B_MAIN, nwords, ok);
+  w.final_bits = take<uint64_t>(V, B_FINAL, nwords, ok);
+  w.sec_bits = take<uint64_t>(V, B_SECB, nwords, ok);
+  w.gpre = take<uint16_t>(V, B_GPRE, (size_t)(w.ngroups + 1) * (GROUP_LANES + 1), ok);
+  w.gexit = take<uint32_t>(V, B_GEXIT, w.ngroups + 1, ok);
+  w.copy = take<CopyTask>(V, B_COPY, w.cap_copy, ok);
+  w.patch = take<uint32_t>(V, B_PATCH, w.cap_patch, ok);
+  w.dsstart = take<uint32_t>(V, B_DSSTART, nu + 1, ok);
+  w.sections = take<Section>(V, B_SECT, w.cap_sections, ok);
+  w.sec_sorted = take<uint32_t>(V, B_SECSORT, w.cap_sections, ok);
+  w.wcnt = take<uint32_t>(V, B_WCNT, nwords + 1, ok);
+  w.wsec = take<uint32_t>(V, B_WSEC, nwords + 1, ok);
+  w.ds = take<DsRange>(V, B_DS, w.cap_ds, ok);
+  w.ds_len = take<uint32_t>(V, B_DSLEN, w.cap_ds + 1, ok);
+  w.ds_scan = take<uint64_t>(V, B_DSSCAN, w.cap_ds + 1, ok);
+  w.s_pos = take<uint32_t>(V, B_SPOS, w.cap_structs, ok);
+  w.s_sec = take<uint32_t>(V, B_SSEC, w.cap_structs, ok);
+  w.s_len = take<uint32_t>(V, B_SLEN, w.cap_structs + 1, ok);
+  w.s_lenscan = take<uint64_t>(V, B_SLENSCAN, w.cap_structs + 1, ok);
+  w.s_clock = take<uint32_t>(V, B_SCLOCK, w.cap_structs, ok);
+  w.s_cidx = take<uint32_t>(V, B_SCIDX, w.cap_structs, ok);
+  w.s_info = take<uint8_t>(V, B_SINFO, w.cap_structs, ok);
+  w.s_ocidx = take<uint32_t>(V, B_SOC, w.cap_structs, ok);
+  w.s_oclock = take<uint32_t>(V, B_SOK, w.cap_structs, ok);
+  w.s_rcidx = take<uint32_t>(V, B_SRC, w.cap_structs, ok);
+  w.s_rclock = take<uint32_t>(V, B_SRK, w.cap_structs, ok);
+  w.s_pa = take<uint32_t>(V, B_SPA, w.cap_structs, ok);
+  w.s_pb = take<uint32_t>(V, B_SPB, w.cap_structs, ok);
+  w.s_psub = take<uint32_t>(V, B_SPS, w.cap_structs, ok);
+  w.s_psublen = take<uint32_t>(V, B_SPL, w.cap_structs, ok);
+  w.s_cpos = take<uint32_t>(V, B_SCPOS, w.cap_structs, ok);
+  w.s_cend = take<uint32_t>(V, B_SCEND, w.cap_structs, ok);
+  w.s_celem = take<uint32_t>(V, B_SCELEM, w.cap_structs, ok);
+  w.cap_clients = w.cap_sections;
+  w.cl_vals = take<uint32_t>(V, B_CLVALS, w.cap_clients + 1, ok);
+  w.cl_tmp = take<uint32_t>(V, B_CLTMP, w.cap_clients + 1, ok);
+  w.cl_state = take<uint32_t>(V, B_CLSTATE, w.cap_clients + 1, ok);
+  w.cl_base = take<uint64_t>(V, B_CLBASE, w.cap_clients + 2, ok);
+  w.cl_start = take<uint32_t>(V, B_CLSTART, w.cap_clients + 1, ok);
+  w.scratch = take<uint32_t>(V, B_SCRATCH, std::max<uint64_t>(nwords + 2, w.cap_sections + 2), ok);
+  if (!ok) return fail(YCRDT_E_DEVICE, "hipMalloc failed (decode workspace)");
+  // rocPRIM scratch sized for the largest scan of this batch (units may grow it later)
+  {
+    size_t tb = prim_tmp_bytes(std::max<uint64_t>(B, 1024));
+    w.tmp = take<uint8_t>(V, B_TMP, tb, ok);
+    w.tmp_bytes = V[B_TMP].cap;
+  }
+  if (!ok) return fail(YCRDT_E_DEVICE, "hipMalloc failed (scan scratch)");
+  HIPCHK(hipMemsetAsync(w.ctr, 0, sizeof(Counters), s));
+  HIPCHK(hipMemsetAsync(w.final_bits, 0, nwords * 8, s));
+  HIPCHK(hipMemsetAsync(w.sec_bits, 0, nwords * 8, s));
+  // ---- K1 decode
+  mark(e, "decode.group_parse");
+  launch_group_parse(w, s);
+  mark(e, "decode.walker");
+  launch_walker(w, s);
+  mark(e, "decode.bitmap");
+  launch_build_final_bits(w, s);
+  launch_struct_positions(w, s);
+  Counters c;
+  int rc = check(e, c, "decode");
+  if (rc) return rc;
+  uint32_t nstructs = 0;
+  HIPCHK(hipMemcpyAsync(&nstructs, w.wcnt + (w.nbytes + 63) / 64, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+  HIPCHK(hipStreamSynchronize(s));
+  const uint32_t nsections = c.nsections;
+  mark(e, "decode.sections");
+  launch_section_clients(w, nsections, s);
+  launch_ds_decode(w, s);
+  uint32_t nclients = 0;
+  if (nsections) launch_client_table(w, nsections, &nclients, s);
+  mark(e, "decode.structs");
+  launch_struct_decode(w, nstructs, nsections, nclients, s);
+  HIPCHK(hipMemsetAsync(w.cl_start, 0, sizeof(uint32_t) * (nclients + 1), s));
+  launch_states(w, nstructs, nclients, s);
+  rc = check(e, c, "struct decode");
+  if (rc) return rc;
+  uint64_t nunits = 0;
+  HIPCHK(hipMemcpyAsync(&nunits, w.cl_base + nclients, sizeof(uint64_t), hipMemcpyDeviceToHost, s));
+  HIPCHK(hipStreamSynchronize(s));
+  if (nunits >= 0xF0000000ull) return fail(YCRDT_E_CAPACITY, "more than 2^32 units in one batch");
+  const uint32_t nds = std::min(c.nds, w.cap_ds);
+  // target state vector → per-client start clocks
+  if (target && !target->empty() && nclients) {
+    std::vector<uint32_t> vals(nclients), starts(nclients, 0);
+    HIPCHK(hipMemcpy(vals.data(), w.cl_vals, sizeof(uint32_t) * nclients, hipMemcpyDeviceToHost));
+    for (uint32_t i = 0; i < nclients; ++i) {
+      auto it = target->find(vals[i]);
+      if (it != target->end()) starts[i] = it->second;
+    }
+    HIPCHK(hipMemcpyAsync(w.cl_start, starts.data(), sizeof(uint32_t) * nclients, hipMemcpyHostToDevice, s));
+  }
+  // ---- per-unit / per-segment buffers
+  const uint64_t U = nunits;
+  const uint64_t uw = U / 64 + 2;
+  w.cap_units = U + 1;
+  w.u_owner = take<uint32_t>(V, B_UOWN, U + 1, ok);
+  w.u_flags = take<uint32_t>(V, B_UFLAG, U + 1, ok);
+  w.u_minchild = take<uint32_t>(V, B_UMIN, U + 1, ok);
+  w.u_cutbits = take<uint64_t>(V, B_UCUT, uw, ok);
+  w.u_wpre = take<uint32_t>(V, B_UWPRE, uw + 1, ok);
+  w.scratch = take<uint32_t>(V, B_SCRATCH, std::max<uint64_t>({nwords + 2, (uint64_t)w.cap_sections + 2, uw + 2, U + 2}), ok);
+  w.g_start = take<uint32_t>(V, B_GSTART, U + 2, ok);
+  w.g_cidx = take<uint32_t>(V, B_GCIDX, U + 1, ok);
+  w.g_src = take<uint32_t>(V, B_GSRC, U + 1, ok);
+  w.g_flags = take<uint32_t>(V, B_GFLAGS, U + 1, ok);
+  w.g_origin = take<uint32_t>(V, B_GORIG, U + 1, ok);
+  w.g_rorigin = take<uint32_t>(V, B_GRORIG, U + 1, ok);
+  w.g_link = take<uint32_t>(V, B_GLINK, U + 1, ok);
+  w.g_key = take<uint32_t>(V, B_GKEY, U + 1, ok);
+  w.g_maxchild = take<uint64_t>(V, B_GMAXC, U + 1, ok);
+  w.g_next = take<uint32_t>(V, B_GNEXT, U + 1, ok);
+  w.g_outid = take<uint32_t>(V, B_GOUTID, U + 2, ok);
+  w.g_tmp = take<uint32_t>(V, B_GTMP, U + 2, ok);
+  w.g_tmp2 = take<uint32_t>(V, B_GTMP2, U + 2, ok);
+  w.o_first = take<uint32_t>(V, B_OFIRST, U + 2, ok);
+  w.o_cidx = take<uint32_t>(V, B_OCIDX, U + 2, ok);
+  w.o_size = take<uint32_t>(V, B_OSIZE, U + 2, ok);
+  w.o_pos = take<uint32_t>(V, B_OPOS, U + 2, ok);
+  w.r_seg = take<uint32_t>(V, B_RSEG, U + 2, ok);
+  w.r_len = take<uint32_t>(V, B_RLEN, U + 2, ok);
+  w.r_size = take<uint32_t>(V, B_RSIZE, U + 2, ok);
+  w.r_pos = take<uint32_t>(V, B_RPOS, U + 2, ok);
+  w.cc = take<uint32_t>(V, B_CC, (size_t)CC_N * (w.cap_clients + 1), ok);
+  {
+    size_t tb = prim_tmp_bytes(std::max<uint64_t>({B, U + 2, 1024}));
+    w.tmp = take<uint8_t>(V, B_TMP, tb, ok);
+    w.tmp_bytes = V[B_TMP].cap;
+  }
+  if (!ok) return fail(YCRDT_E_DEVICE, "hipMalloc failed (unit workspace)");
+  // ---- K2..K5 units
+  mark(e, "merge.units");
+  if (U) launch_units(w, nstructs, nclients, nds, U, s);
+  mark(e, "merge.segments");
+  uint32_t nsegs = 0;
+  if (U) {
+    launch_segments(w, nclients, U, s);
+    rc = check(e, c, "segments");
+    if (rc) return rc;
+    nsegs = c.nsegs;
+  }
+  // keys
+  w.cap_keys = next_pow2(std::max<uint64_t>(2ull * nsegs, 64));
+  w.k_hash = take<uint64_t>(V, B_KHASH, w.cap_keys, ok);
+  w.k_rootmax = take<uint64_t>(V, B_KROOT, w.cap_keys, ok);
+  w.k_winner = take<uint32_t>(V, B_KWIN, w.cap_keys, ok);
+  if (!ok) return fail(YCRDT_E_DEVICE, "hipMalloc failed (key table)");
+  uint32_t nout = 0;
+  if (nsegs) {
+    mark(e, "merge.segment_props");
+    launch_segment_props(w, nsegs, nclients, U, s);
+    mark(e, "merge.keys");
+    run_key_resolution(w, nsegs, s);
+    mark(e, "merge.winner");
+    launch_map_winner(w, nsegs, s);
+    run_descent(w, nsegs, s);
+    mark(e, "merge.merge_flags");
+    launch_merge_flags(w, nsegs, s);
+    rc = check(e, c, "merge");
+    if (rc) return rc;
+    nout = c.nout;
+  }
+  // ---- K7 encode
+  mark(e, "encode.sizes");
+  uint32_t nruns = 0;
+  launch_encode_sizes(w, nsegs, nclients, nout, &nruns, s);
+  rc = check(e, c, "encode sizes");
+  if (rc) return rc;
+  w.out = take<uint8_t>(V, B_OUT, (size_t)c.out_bytes + 16, ok);
+  w.sv_out = take<uint8_t>(V, B_SVOUT, (size_t)c.sv_bytes + 16, ok);
+  if (!ok) return fail(YCRDT_E_DEVICE, "hipMalloc failed (output)");
+  mark(e, "encode.write");
+  launch_encode_write(w, nclients, nout, nruns, s);
+  mark(e, "end");
+  HIPCHK(hipEventRecord(e->ev1, s));
+  rc = check(e, c, "encode");
+  if (rc) return rc;
+  e->out_bytes = c.out_bytes;
+  e->sv_bytes = c.sv_bytes;
+  float ms = 0;
+  hipEventElapsedTime(&ms, e->ev0, e->ev1);
+  ycrdt_merge_stats& st = e->last;
+  st.in_bytes = b->in_bytes;
+  st.items = c.items;
+  st.structs = nstructs;
+  st.units = U;
+  st.segments = nsegs;
+  st.out_structs = nout;
+  st.out_bytes = c.out_bytes;
+  st.clients = nclients;
+  st.device_ms = ms;
+  if (e->profiling) {
+    for (size_t i = 0; i + 1 < e->marks.size(); ++i) {
+      float t = 0;
+      hipEventElapsedTime(&t, e->marks[i].second, e->marks[i + 1].second);
+      e->phase_ms.push_back({e->marks[i].first, (double)t});
+    }
+  }
+  return YCRDT_OK;
+}
+
+int empty_update(ycrdt_out* out) {
+  out->ptr = (uint8_t*)malloc(2);
+  out->ptr[0] = 0;
+  out->ptr[1] = 0;
+  out->len = 2;
+  return YCRDT_OK;
+}
+
+}  // namespace
+
+// =========================================================================================== C ABI
+extern "C" {
+
+const char* ycrdt_last_error(void) { return g_err.c_str(); }
+const char* ycrdt_version(void) { return "ycrdt-mi355x 0.1 (gfx950)"; }
+
+void ycrdt_free(ycrdt_out* o) {
+  if (o && o->ptr) free(o->ptr);
+  if (o) { o->ptr = nullptr; o->len = 0; }
+}
+
+int ycrdt_engine_create(int device, int compat, ycrdt_engine** out) {
+  if (!out) return fail(YCRDT_E_ARG, "null out");
+  *out = nullptr;
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || n == 0) return fail(YCRDT_E_DEVICE, "no HIP device available");
+  if (device < 0 || device >= n) return fail(YCRDT_E_DEVICE, "bad device ordinal");
+  HIPCHK(hipSetDevice(device));
+  auto* e = new ycrdt_engine();
+  e->device = device;
+  e->compat = compat == 135 ? 135 : 136;
+  if (hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess) { delete e; return fail(YCRDT_E_DEVICE, "stream"); }
+  hipEventCreate(&e->ev0);
+  hipEventCreate(&e->ev1);
+  e->bufs.resize(B_COUNT);
+  *out = e;
+  return YCRDT_OK;
+}
+
+void ycrdt_engine_destroy(ycrdt_engine* e) {
+  if (!e) return;
+  hipSetDevice(e->device);
+  hipStreamSynchronize(e->stream);
+  for (auto& b : e->bufs) if (b.p) hipFree(b.p);
+  for (auto& m : e->marks) hipEventDestroy(m.second);
+  hipEventDestroy(e->ev0);
+  hipEventDestroy(e->ev1);
+  hipStreamDestroy(e->stream);
+  delete e;
+}
+
+int ycrdt_engine_set_profiling(ycrdt_engine* e, int on) {
+  if (!e) return fail(YCRDT_E_ARG, "null engine");
+  e->profiling = on != 0;
+  return YCRDT_OK;
+}
+
+int ycrdt_engine_phase_times(ycrdt_engine* e, const char** names, double* ms, int cap) {
+  if (!e) return 0;
+  int n = 0;
+  for (auto& p : e->phase_ms) {
+    if (n >= cap) break;
+    names[n] = p.first;
+    ms[n] = p.second;
+    ++n;
+  }
+  return n;
+}
+
+int ycrdt_doc_create(ycrdt_engine* e, uint32_t client_id, ycrdt_doc** out) {
+  if (!e || !out) return fail(YCRDT_E_ARG, "null arg");
+  auto* d = new ycrdt_doc();
+  d->e = e;
+  d->client_id = client_id;
+  d->sv = {0};
+  *out = d;
+  return YCRDT_OK;
+}
+
+void ycrdt_doc_destroy(ycrdt_doc* d) {
+  if (!d) return;
+  hipSetDevice(d->e->device);
+  if (d->state.p) hipFree(d->state.p);
+  delete d;
+}
+
+int ycrdt_apply_updates(ycrdt_doc* d, const ycrdt_buf* ups, size_t n) {
+  if (!d || (!ups && n)) return fail(YCRDT_E_ARG, "null arg");
+  if (n == 0) return YCRDT_OK;
+  ycrdt_engine* e = d->e;
+  HIPCHK(hipSetDevice(e->device));
+  ycrdt_batch b;
+  b.e = e;
+  int rc = stage(&b, ups, n, d->state_len ? &d->state : nullptr, d->state_len);
+  if (rc == YCRDT_OK) rc = run_merge(e, &b, nullptr);
+  if (rc == YCRDT_OK) {
+    // the merged canonical state becomes the doc state; the host keeps the state vector
+    if (!grow(d->state, e->out_bytes + 16)) rc = fail(YCRDT_E_DEVICE, "hipMalloc failed (doc state)");
+    else {
+      hipMemcpyAsync(d->state.p, e->w.out, e->out_bytes, hipMemcpyDeviceToDevice, e->stream);
+      d->state_len = e->out_bytes;
+      d->sv.resize(e->sv_bytes);
+      hipMemcpyAsync(d->sv.data(), e->w.sv_out, e->sv_bytes, hipMemcpyDeviceToHost, e->stream);
+      hipStreamSynchronize(e->stream);
+      d->last = e->last;
+    }
+  }
+  if (b.bytes.p) hipFree(b.bytes.p);
+  if (b.meta.p) hipFree(b.meta.p);
+  return rc;
+}
+
+int ycrdt_apply_update(ycrdt_doc* d, ycrdt_buf update) { return ycrdt_apply_updates(d, &update, 1); }
+
+int ycrdt_encode_state_as_update(ycrdt_doc* d, ycrdt_buf sv, ycrdt_out* out) {
+  if (!d || !out) return fail(YCRDT_E_ARG, "null arg");
+  out->ptr = nullptr;
+  out->len = 0;
+  std::unordered_map<uint32_t, uint32_t> target;
+  if (sv.len && !parse_sv(sv.ptr, sv.len, target)) return fail(YCRDT_E_DECODE, "Integer out of range! (state vector)");
+  if (!d->state_len) return empty_update(out);
+  ycrdt_engine* e = d->e;
+  HIPCHK(hipSetDevice(e->device));
+  if (target.empty()) {
+    out->ptr = (uint8_t*)malloc(d->state_len);
+    out->len = d->state_len;
+    HIPCHK(hipMemcpy(out->ptr, d->state.p, d->state_len, hipMemcpyDeviceToHost));
+    return YCRDT_OK;
+  }
+  // delta: re-run the (idempotent) merge of the canonical state with per-client start clocks
+  ycrdt_batch b;
+  b.e = e;
+  int rc = stage(&b, nullptr, 0, &d->state, d->state_len);
+  if (rc == YCRDT_OK) rc = run_merge(e, &b, &target);
+  if (rc == YCRDT_OK) {
+    out->ptr = (uint8_t*)malloc(e->out_bytes);
+    out->len = e->out_bytes;
+    if (hipMemcpy(out->ptr, e->w.out, e->out_bytes, hipMemcpyDeviceToHost) != hipSuccess) rc = fail(YCRDT_E_DEVICE, "D2H");
+  }
+  if (b.bytes.p) hipFree(b.bytes.p);
+  if (b.meta.p) hipFree(b.meta.p);
+  return rc;
+}
+
+int ycrdt_encode_state_vector(ycrdt_doc* d, ycrdt_out* out) {
+  if (!d || !out) return fail(YCRDT_E_ARG, "null arg");
+  out->len = d->sv.size();
+  out->ptr = (uint8_t*)malloc(out->len ? out->len : 1);
+  if (out->len) memcpy(out->ptr, d->sv.data(), out->len);
+  return YCRDT_OK;
+}
+
+int ycrdt_doc_last_stats(ycrdt_doc* d, ycrdt_merge_stats* st) {
+  if (!d || !st) return fail(YCRDT_E_ARG, "null arg");
+  *st = d->last;
+  return YCRDT_OK;
+}
+
+int ycrdt_batch_stage(ycrdt_engine* e, const ycrdt_buf* ups, size_t n, ycrdt_batch** out) {
+  if (!e || !out || (!ups && n)) return fail(YCRDT_E_ARG, "null arg");
+  HIPCHK(hipSetDevice(e->device));
+  auto* b = new ycrdt_batch();
+  b->e = e;
+  int rc = stage(b, ups, n, nullptr, 0);
+  if (rc) { ycrdt_batch_destroy(b); return rc; }
+  *out = b;
+  return YCRDT_OK;
+}
+
+int ycrdt_batch_merge(ycrdt_batch* b, ycrdt_merge_stats* st) {
+  if (!b) return fail(YCRDT_E_ARG, "null batch");
+  HIPCHK(hipSetDevice(b->e->device));
+  int rc = run_merge(b->e, b, nullptr);
+  if (rc == YCRDT_OK) {
+    b->merged = true;
+    if (st) *st = b->e->last;
+  }
+  return rc;
+}
+
+int ycrdt_batch_result(ycrdt_batch* b, ycrdt_out* update, ycrdt_out* sv) {
+  if (!b || !b->merged) return fail(YCRDT_E_ARG, "batch not merged");
+  ycrdt_engine* e = b->e;
+  HIPCHK(hipSetDevice(e->device));
+  if (update) {
+    update->len = e->out_bytes;
+    update->ptr = (uint8_t*)malloc(update->len ? update->len : 1);
+    HIPCHK(hipMemcpy(update->ptr, e->w.out, update->len, hipMemcpyDeviceToHost));
+  }
+  if (sv) {
+    sv->len = e->sv_bytes;
+    sv->ptr = (uint8_t*)malloc(sv->len ? sv->len : 1);
+    HIPCHK(hipMemcpy(sv->ptr, e->w.sv_out, sv->len, hipMemcpyDeviceToHost));
+  }
+  return YCRDT_OK;
+}
+
+void ycrdt_batch_destroy(ycrdt_batch* b) {
+  if (!b) return;
+  hipSetDevice(b->e->device);
+  if (b->bytes.p) hipFree(b->bytes.p);
+  if (b->meta.p) hipFree(b->meta.p);
+  delete b;
+}
+
+}  // extern "C"

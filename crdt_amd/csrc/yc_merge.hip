@@ -1,0 +1,399 @@
+// yc_merge.hip — K2..K6: dedupe, delete sets, segmentation and the YMap winner on gfx950.
+//
+// All state is indexed by the dense *unit* index g = cl_base[client] + clock (one unit per
+// (client, clock) of the merged store), so every step below is a flat, coalesced pass:
+//   k_owner        dedupe (integrateStructs offset logic, Y@19963): each unit takes its struct
+//                  from the earliest update that carries it (atomicMin over struct index)
+//   k_ds_mark      delete-set application (readAndApplyDeleteSet, Y@11619) as unit flags
+//   k_refs         split points required by origin / rightOrigin references (getItemCleanEnd /
+//                  getItemCleanStart, Y@29100) + min child client per unit (list adjacency)
+//   k_cuts         struct boundaries -> bitmap; popcount scan -> segments
+//   k_seg_props    per-segment origin / rightOrigin / parent / flags
+//   k_keyjump      parent+parentSub resolution (Item.getMissing, Y@76507) by pointer jumping
+//   k_children     YATA for map entries (Item.integrate, Y@77594): children ordered by client ⇒
+//                  the rightmost entry is the max-client descent from the max-client root
+//   k_descend      pointer jumping along the max-client child
+//   k_overwrite    every non-rightmost entry of a key is deleted (typeMapSet / left.delete)
+//   k_merge_flags  Item.mergeWith (Y@79424) / tryToMergeWithLeft (Y@30960) as a pairwise
+//                  predicate over adjacent segments ⇒ canonical (maximally merged) structs
+#include "yc_work.h"
+
+namespace yc {
+
+constexpr uint32_t OWNER_UNITS_PER_LANE = 16;
+
+__device__ __forceinline__ uint32_t seg_of(const uint64_t* __restrict__ cut, const uint32_t* __restrict__ wpre, uint32_t g) {
+  return wpre[g >> 6] + (uint32_t)__popcll(cut[g >> 6] & ((2ull << (g & 63)) - 1)) - 1;
+}
+
+// --------------------------------------------------------------------------- owner / dedupe
+__global__ __launch_bounds__(256) void k_owner(Work w, uint32_t nstructs, uint64_t total_in) {
+  const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  uint64_t j = t * OWNER_UNITS_PER_LANE;
+  if (j >= total_in) return;
+  const uint64_t jend = min(j + OWNER_UNITS_PER_LANE, total_in);
+  const uint64_t* __restrict__ P = w.s_lenscan;
+  uint32_t lo = 0, hi = nstructs;  // last s with P[s] <= j
+  while (hi - lo > 1) { const uint32_t mid = (lo + hi) >> 1; if (P[mid] <= j) lo = mid; else hi = mid; }
+  uint32_t s = lo;
+  while (j < jend) {
+    while (P[s + 1] <= j) ++s;
+    const uint64_t send = min(jend, P[s + 1]);
+    const uint32_t ref = w.s_info[s] & 31u;
+    if (ref != REF_SKIP) {
+      const uint32_t cidx = w.s_cidx[s];
+      const uint64_t gb = w.cl_base[cidx] + w.s_clock[s] - P[s];
+      const uint32_t fl = ref == REF_DELETED ? UF_DEL : (ref == REF_GC ? (UF_GC | UF_DEL) : 0u);
+      for (; j < send; ++j) {
+        const uint32_t g = (uint32_t)(gb + j);
+        atomicMin(&w.u_owner[g], s);
+        if (fl) atomicOr(&w.u_flags[g], fl);
+      }
+    } else j = send;
+  }
+}
+
+// --------------------------------------------------------------------------- delete sets
+__global__ void k_ds_prep(Work w, uint32_t nds, uint32_t nclients) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= nds) { if (i == nds) w.ds_len[i] = 0; return; }
+  DsRange r = w.ds[i];
+  const uint32_t c = lower_bound_u32(w.cl_vals, nclients, r.client);
+  uint32_t len = r.len;
+  if (len == 0) { w.ds_len[i] = 0; return; }
+  if (c >= nclients || w.cl_vals[c] != r.client) { raise_err(&w.ctr->err, ERR_PENDING); w.ds_len[i] = 0; return; }
+  const uint64_t endc = (uint64_t)r.clock + len;
+  if (endc > w.cl_state[c]) { raise_err(&w.ctr->err, ERR_PENDING); len = r.clock < w.cl_state[c] ? w.cl_state[c] - r.clock : 0; }
+  r.client = c;
+  w.ds[i] = r;
+  w.ds_len[i] = len;
+}
+__global__ __launch_bounds__(256) void k_ds_mark(Work w, uint32_t nds, uint64_t total) {
+  const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  uint64_t j = t * OWNER_UNITS_PER_LANE;
+  if (j >= total) return;
+  const uint64_t jend = min(j + OWNER_UNITS_PER_LANE, total);
+  const uint64_t* __restrict__ P = w.ds_scan;
+  uint32_t lo = 0, hi = nds;
+  while (hi - lo > 1) { const uint32_t mid = (lo + hi) >> 1; if (P[mid] <= j) lo = mid; else hi = mid; }
+  uint32_t s = lo;
+  while (j < jend) {
+    while (P[s + 1] <= j) ++s;
+    const uint64_t send = min(jend, P[s + 1]);
+    const DsRange r = w.ds[s];
+    const uint64_t gb = w.cl_base[r.client] + r.clock - P[s];
+    for (; j < send; ++j) atomicOr(&w.u_flags[(uint32_t)(gb + j)], UF_DS);
+  }
+}
+
+// --------------------------------------------------------------------------- reference cuts
+__global__ void k_refs(Work w, uint32_t nstructs) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= nstructs) return;
+  const uint32_t oc = w.s_ocidx[i];
+  if (oc != NONE) {
+    const uint32_t k = w.s_oclock[i];
+    if (k >= w.cl_state[oc]) { raise_err(&w.ctr->err, ERR_PENDING); return; }
+    const uint32_t g = (uint32_t)(w.cl_base[oc] + k);
+    atomicMin(&w.u_minchild[g], w.s_cidx[i]);
+    if (k + 1 < w.cl_state[oc]) atomicOr(&w.u_flags[g + 1], UF_CUT);  // getItemCleanEnd(origin)
+  }
+  const uint32_t rc = w.s_rcidx[i];
+  if (rc != NONE) {
+    const uint32_t k = w.s_rclock[i];
+    if (k >= w.cl_state[rc]) { raise_err(&w.ctr->err, ERR_PENDING); return; }
+    atomicOr(&w.u_flags[(uint32_t)(w.cl_base[rc] + k)], UF_CUT);       // getItemCleanStart(rightOrigin)
+  }
+}
+
+// --------------------------------------------------------------------------- cuts -> segments
+__global__ __launch_bounds__(256) void k_cuts(Work w, uint64_t nunits) {
+  const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  bool cut = false;
+  if (g < nunits) {
+    const uint32_t own = w.u_owner[g];
+    if (own == NONE) {
+      raise_err(&w.ctr->err, ERR_PENDING);  // a gap in a client's clock range
+    } else {
+      const uint32_t f = w.u_flags[g];
+      cut = (f & UF_CUT) || g == 0;
+      const uint64_t first = w.cl_base[w.s_cidx[own]] + w.s_clock[own];
+      cut |= g == first;
+      if (g > 0) {
+        const uint32_t po = w.u_owner[g - 1];
+        const uint32_t pf = w.u_flags[g - 1];
+        cut |= po != own;
+        const bool d = (f & (UF_DEL | UF_DS)) != 0, pd = (pf & (UF_DEL | UF_DS)) != 0;
+        cut |= d != pd;
+        cut |= ((f ^ pf) & UF_GC) != 0;
+      }
+    }
+  }
+  const uint64_t word = __ballot(cut);
+  if ((threadIdx.x & 63) == 0 && g < nunits) w.u_cutbits[g >> 6] = word;
+}
+__global__ void k_client_cuts(Work w, uint32_t nclients) {
+  const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= nclients || w.cl_state[c] == 0) return;
+  const uint64_t g = w.cl_base[c];
+  atomicOr((unsigned long long*)&w.u_cutbits[g >> 6], 1ull << (g & 63));
+}
+__global__ void k_scatter_seg(Work w, uint32_t nwords, uint64_t nunits) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= nwords) return;
+  uint64_t x = w.u_cutbits[i];
+  uint32_t k = w.u_wpre[i];
+  while (x) {
+    const uint32_t bit = (uint32_t)__ffsll((long long)x) - 1;
+    x &= x - 1;
+    w.g_start[k++] = i * 64 + bit;
+  }
+  if (i == nwords - 1) w.g_start[w.u_wpre[nwords]] = (uint32_t)nunits;  // sentinel
+}
+
+void launch_units(const Work& w, uint32_t nstructs, uint32_t nclients, uint32_t nds, uint64_t nunits, hipStream_t s) {
+  hipMemsetAsync(w.u_owner, 0xFF, sizeof(uint32_t) * nunits, s);
+  hipMemsetAsync(w.u_flags, 0, sizeof(uint32_t) * nunits, s);
+  hipMemsetAsync(w.u_minchild, 0xFF, sizeof(uint32_t) * nunits, s);
+  // owner (needs total input units = s_lenscan[nstructs], read on device by the kernel bound)
+  uint64_t total_in = 0;
+  hipMemcpyAsync(&total_in, w.s_lenscan + nstructs, sizeof(uint64_t), hipMemcpyDeviceToHost, s);
+  hipStreamSynchronize(s);
+  if (total_in) {
+    const uint64_t lanes = (total_in + OWNER_UNITS_PER_LANE - 1) / OWNER_UNITS_PER_LANE;
+    hipLaunchKernelGGL(k_owner, dim3((uint32_t)((lanes + 255) / 256)), dim3(256), 0, s, w, nstructs, total_in);
+  }
+  if (nds) {
+    hipLaunchKernelGGL(k_ds_prep, dim3(nds / 256 + 1), dim3(256), 0, s, w, nds, nclients);
+    scan_u32_to_u64(w.tmp, w.tmp_bytes, w.ds_len, w.ds_scan, nds + 1, s);
+    uint64_t total_ds = 0;
+    hipMemcpyAsync(&total_ds, w.ds_scan + nds, sizeof(uint64_t), hipMemcpyDeviceToHost, s);
+    hipStreamSynchronize(s);
+    if (total_ds) {
+      const uint64_t lanes = (total_ds + OWNER_UNITS_PER_LANE - 1) / OWNER_UNITS_PER_LANE;
+      hipLaunchKernelGGL(k_ds_mark, dim3((uint32_t)((lanes + 255) / 256)), dim3(256), 0, s, w, nds, total_ds);
+    }
+  }
+  if (nstructs) hipLaunchKernelGGL(k_refs, dim3((nstructs + 255) / 256), dim3(256), 0, s, w, nstructs);
+}
+
+__global__ void k_popc_words(const uint64_t* __restrict__ bits, uint32_t* __restrict__ cnt, uint32_t n) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) cnt[i] = (uint32_t)__popcll(bits[i]);
+  else if (i == n) cnt[i] = 0;
+}
+
+void launch_segments(const Work& w, uint32_t nclients, uint64_t nunits, hipStream_t s) {
+  const uint32_t nwords = (uint32_t)((nunits + 63) / 64);
+  hipLaunchKernelGGL(k_cuts, dim3(nwords / 4 + 1), dim3(256), 0, s, w, nunits);
+  hipLaunchKernelGGL(k_client_cuts, dim3(nclients / 256 + 1), dim3(256), 0, s, w, nclients);
+  hipLaunchKernelGGL(k_popc_words, dim3(nwords / 256 + 1), dim3(256), 0, s, (const uint64_t*)w.u_cutbits, w.scratch, nwords);
+  scan_u32(w.tmp, w.tmp_bytes, w.scratch, w.u_wpre, nwords + 1, s);
+  hipLaunchKernelGGL(k_scatter_seg, dim3(nwords / 256 + 1), dim3(256), 0, s, w, nwords, nunits);
+  hipMemcpyAsync(&w.ctr->nsegs, w.u_wpre + nwords, sizeof(uint32_t), hipMemcpyDeviceToDevice, s);
+}
+
+// --------------------------------------------------------------------------- segment properties
+__device__ __forceinline__ uint64_t fnv_bytes(uint64_t h, const uint8_t* __restrict__ p, uint32_t n) {
+  for (uint32_t i = 0; i < n; ++i) { h ^= p[i]; h *= 1099511628211ull; }
+  return h;
+}
+__device__ __forceinline__ uint32_t key_insert(uint64_t* __restrict__ tab, uint32_t cap, uint64_t h) {
+  uint32_t slot = (uint32_t)(h ^ (h >> 29)) & (cap - 1);
+  for (uint32_t probe = 0; probe < cap; ++probe) {
+    const unsigned long long old = atomicCAS((unsigned long long*)&tab[slot], 0ull, (unsigned long long)h);
+    if (old == 0ull || old == h) return slot;
+    slot = (slot + 1) & (cap - 1);
+  }
+  return NONE;
+}
+
+__global__ __launch_bounds__(256) void k_seg_props(Work w, uint32_t nsegs) {
+  const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= nsegs) return;
+  const uint32_t g0 = w.g_start[s];
+  const uint32_t own = w.u_owner[g0];
+  const uint32_t cidx = w.s_cidx[own];
+  const uint32_t k0 = (uint32_t)(g0 - w.cl_base[cidx]);
+  const uint32_t f = w.u_flags[g0];
+  const uint32_t ref = w.s_info[own] & 31u;
+  uint32_t sf = 0;
+  if (f & (UF_DEL | UF_DS)) sf |= SEG_DEL;
+  if (f & UF_GC) sf |= SEG_GC;
+  if (ref != REF_GC) sf |= SEG_ITEM;
+  const bool expl = k0 == w.s_clock[own];
+  if (expl) sf |= SEG_EXPLICIT;
+  uint32_t origin = NONE, rorigin = NONE;
+  if (expl) {
+    if (w.s_ocidx[own] != NONE) origin = (uint32_t)(w.cl_base[w.s_ocidx[own]] + w.s_oclock[own]);
+  } else origin = g0 - 1;
+  if (w.s_rcidx[own] != NONE) rorigin = (uint32_t)(w.cl_base[w.s_rcidx[own]] + w.s_rclock[own]);
+  uint32_t key = NONE, link = s;
+  if ((sf & SEG_ITEM) && origin == NONE && rorigin == NONE) {
+    sf |= SEG_ROOT;
+    const uint32_t pa = w.s_pa[own], ps = w.s_psub[own];
+    if (pa == NONE || ps == NONE) { raise_err(&w.ctr->err, ERR_UNSUPPORTED); }
+    else {
+      uint64_t h = 1469598103934665603ull;
+      h = fnv_bytes(h, w.bytes + pa, w.s_pb[own]);
+      h = fnv_bytes(h, w.bytes + ps, w.s_psublen[own]);
+      if (h == 0) h = 1;
+      key = key_insert(w.k_hash, w.cap_keys, h);
+      if (key == NONE) raise_err(&w.ctr->err, ERR_CAPACITY);
+    }
+  } else if (sf & SEG_ITEM) {
+    link = seg_of(w.u_cutbits, w.u_wpre, origin != NONE ? origin : rorigin);
+  }
+  w.g_cidx[s] = cidx;
+  w.g_src[s] = own;
+  w.g_flags[s] = sf;
+  w.g_origin[s] = origin;
+  w.g_rorigin[s] = rorigin;
+  w.g_key[s] = key;
+  w.g_link[s] = link;
+}
+
+void launch_segment_props(const Work& w, uint32_t nsegs, uint32_t nclients, uint64_t nunits, hipStream_t s) {
+  hipMemsetAsync(w.k_hash, 0, sizeof(uint64_t) * w.cap_keys, s);
+  hipMemsetAsync(w.k_rootmax, 0, sizeof(uint64_t) * w.cap_keys, s);
+  hipMemsetAsync(w.g_maxchild, 0, sizeof(uint64_t) * nsegs, s);
+  if (nsegs) hipLaunchKernelGGL(k_seg_props, dim3((nsegs + 255) / 256), dim3(256), 0, s, w, nsegs);
+}
+
+// --------------------------------------------------------------------------- key resolution
+__global__ __launch_bounds__(256) void k_keyjump(Work w, uint32_t nsegs) {
+  const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= nsegs) return;
+  if (w.g_key[s] != NONE || !(w.g_flags[s] & SEG_ITEM)) return;
+  const uint32_t t = w.g_link[s];
+  const uint32_t kt = w.g_key[t];
+  if (kt != NONE) { w.g_key[s] = kt; w.ctr->changed = 1; return; }
+  const uint32_t tt = w.g_link[t];
+  if (tt != t) { w.g_link[s] = tt; w.ctr->changed = 1; }
+}
+
+uint32_t run_key_resolution(const Work& w, uint32_t nsegs, hipStream_t s) {
+  if (!nsegs) return 0;
+  uint32_t rounds = 0;
+  for (; rounds < 64; rounds += 2) {
+    hipMemsetAsync(&w.ctr->changed, 0, sizeof(uint32_t), s);
+    hipLaunchKernelGGL(k_keyjump, dim3((nsegs + 255) / 256), dim3(256), 0, s, w, nsegs);
+    hipLaunchKernelGGL(k_keyjump, dim3((nsegs + 255) / 256), dim3(256), 0, s, w, nsegs);
+    uint32_t changed = 0;
+    hipMemcpyAsync(&changed, &w.ctr->changed, sizeof(uint32_t), hipMemcpyDeviceToHost, s);
+    hipStreamSynchronize(s);
+    if (!changed) break;
+  }
+  return rounds;
+}
+
+// --------------------------------------------------------------------------- map winner
+__global__ __launch_bounds__(256) void k_children(Work w, uint32_t nsegs) {
+  const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= nsegs) return;
+  const uint32_t f = w.g_flags[s];
+  if (!(f & SEG_ITEM)) return;
+  const uint32_t key = w.g_key[s];
+  if (key == NONE) { raise_err(&w.ctr->err, ERR_DECODE); return; }  // origin chain without a root
+  const unsigned long long v = ((unsigned long long)(w.g_cidx[s] + 1) << 32) | s;
+  const uint32_t o = w.g_origin[s];
+  if (o != NONE) {
+    atomicMax((unsigned long long*)&w.g_maxchild[seg_of(w.u_cutbits, w.u_wpre, o)], v);
+  } else if (f & SEG_ROOT) {
+    atomicMax((unsigned long long*)&w.k_rootmax[key], v);
+  }
+}
+__global__ void k_next_init(Work w, uint32_t nsegs) {
+  const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= nsegs) return;
+  const uint64_t m = w.g_maxchild[s];
+  w.g_next[s] = m ? (uint32_t)m : s;
+}
+__global__ __launch_bounds__(256) void k_descend(Work w, uint32_t nsegs) {
+  const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= nsegs) return;
+  const uint32_t n = w.g_next[s];
+  const uint32_t nn = w.g_next[n];
+  if (nn != n) { w.g_next[s] = nn; w.ctr->changed = 1; }
+}
+__global__ void k_winner(Work w) {
+  const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= w.cap_keys) return;
+  const uint64_t r = w.k_rootmax[k];
+  w.k_winner[k] = r ? w.g_next[(uint32_t)r] : NONE;
+}
+__global__ void k_overwrite(Work w, uint32_t nsegs) {
+  const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= nsegs) return;
+  const uint32_t f = w.g_flags[s];
+  if (!(f & SEG_ITEM)) return;
+  if (w.k_winner[w.g_key[s]] != s) w.g_flags[s] = f | SEG_DEL;
+}
+
+void launch_map_winner(const Work& w, uint32_t nsegs, hipStream_t s) {
+  if (!nsegs) return;
+  hipLaunchKernelGGL(k_children, dim3((nsegs + 255) / 256), dim3(256), 0, s, w, nsegs);
+  hipLaunchKernelGGL(k_next_init, dim3((nsegs + 255) / 256), dim3(256), 0, s, w, nsegs);
+}
+
+uint32_t run_descent(const Work& w, uint32_t nsegs, hipStream_t s) {
+  if (!nsegs) return 0;
+  uint32_t rounds = 0;
+  for (; rounds < 64; rounds += 2) {
+    hipMemsetAsync(&w.ctr->changed, 0, sizeof(uint32_t), s);
+    hipLaunchKernelGGL(k_descend, dim3((nsegs + 255) / 256), dim3(256), 0, s, w, nsegs);
+    hipLaunchKernelGGL(k_descend, dim3((nsegs + 255) / 256), dim3(256), 0, s, w, nsegs);
+    uint32_t changed = 0;
+    hipMemcpyAsync(&changed, &w.ctr->changed, sizeof(uint32_t), hipMemcpyDeviceToHost, s);
+    hipStreamSynchronize(s);
+    if (!changed) break;
+  }
+  hipLaunchKernelGGL(k_winner, dim3(w.cap_keys / 256 + 1), dim3(256), 0, s, w);
+  hipLaunchKernelGGL(k_overwrite, dim3((nsegs + 255) / 256), dim3(256), 0, s, w, nsegs);
+  return rounds;
+}
+
+// --------------------------------------------------------------------------- merge flags
+__device__ __forceinline__ bool content_mergeable(uint32_t ref) {
+  return ref == REF_ANY || ref == REF_JSON || ref == REF_STRING;
+}
+__global__ __launch_bounds__(256) void k_merge_flags(Work w, uint32_t nsegs) {
+  const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
+  if (s > nsegs) return;
+  if (s == nsegs) { w.g_tmp[s] = 0; return; }
+  bool merge = false;
+  const uint32_t fr = w.g_flags[s];
+  if (s > 0 && w.g_cidx[s - 1] == w.g_cidx[s]) {
+    const uint32_t fl = w.g_flags[s - 1];
+    const uint32_t gs = w.g_start[s];
+    if ((fl & SEG_ITEM) == (fr & SEG_ITEM)) {
+      if (!(fr & SEG_ITEM)) merge = true;  // GC + GC
+      else if ((fl & SEG_DEL) == (fr & SEG_DEL) && w.g_origin[s] == gs - 1 && w.g_rorigin[s - 1] == w.g_rorigin[s] &&
+               w.u_minchild[gs - 1] >= w.g_cidx[s]) {
+        if (fr & SEG_DEL) merge = true;  // both become ContentDeleted after GC
+        else {
+          const uint32_t rl = w.s_info[w.g_src[s - 1]] & 31u, rr = w.s_info[w.g_src[s]] & 31u;
+          merge = rl == rr && content_mergeable(rr);
+        }
+      }
+    }
+  }
+  if (merge) w.g_flags[s] = fr | SEG_MERGE;
+  w.g_tmp[s] = merge ? 0u : 1u;
+}
+__global__ void k_out_first(Work w, uint32_t nsegs) {
+  const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= nsegs) return;
+  if (!(w.g_flags[s] & SEG_MERGE)) w.o_first[w.g_outid[s]] = s;
+  if (s == nsegs - 1) w.o_first[w.g_outid[nsegs]] = nsegs;  // sentinel
+}
+
+void launch_merge_flags(const Work& w, uint32_t nsegs, hipStream_t s) {
+  if (!nsegs) return;
+  hipLaunchKernelGGL(k_merge_flags, dim3(nsegs / 256 + 1), dim3(256), 0, s, w, nsegs);
+  scan_u32(w.tmp, w.tmp_bytes, w.g_tmp, w.g_outid, nsegs + 1, s);
+  hipLaunchKernelGGL(k_out_first, dim3((nsegs + 255) / 256), dim3(256), 0, s, w, nsegs);
+  hipMemcpyAsync(&w.ctr->nout, w.g_outid + nsegs, sizeof(uint32_t), hipMemcpyDeviceToDevice, s);
+}
+
+}  // namespace yc

@@ -1,0 +1,33 @@
+// yc_prims.hip — device-wide scan / sort primitives (rocPRIM) used between the engine's kernels.
+#include <cstring>
+#include <cstdlib>
+#include <rocprim/rocprim.hpp>
+#include "yc_work.h"
+
+namespace yc {
+
+size_t prim_tmp_bytes(uint64_t n) {
+  size_t a = 0, b = 0, c = 0;
+  rocprim::exclusive_scan(nullptr, a, (const uint32_t*)nullptr, (uint32_t*)nullptr, 0u, (size_t)n, rocprim::plus<uint32_t>());
+  rocprim::exclusive_scan(nullptr, b, (const uint32_t*)nullptr, (uint64_t*)nullptr, (uint64_t)0, (size_t)n, rocprim::plus<uint64_t>());
+  rocprim::radix_sort_keys(nullptr, c, (const uint32_t*)nullptr, (uint32_t*)nullptr, (size_t)n, 0, 32);
+  size_t m = a > b ? a : b;
+  return (m > c ? m : c) + 256;
+}
+
+void scan_u32(void* tmp, size_t tmpb, const uint32_t* in, uint32_t* out, uint64_t n, hipStream_t s) {
+  if (!n) return;
+  rocprim::exclusive_scan(tmp, tmpb, in, out, 0u, (size_t)n, rocprim::plus<uint32_t>(), s);
+}
+
+void scan_u32_to_u64(void* tmp, size_t tmpb, const uint32_t* in, uint64_t* out, uint64_t n, hipStream_t s) {
+  if (!n) return;
+  rocprim::exclusive_scan(tmp, tmpb, in, out, (uint64_t)0, (size_t)n, rocprim::plus<uint64_t>(), s);
+}
+
+void sort_u32(void* tmp, size_t tmpb, const uint32_t* in, uint32_t* out, uint64_t n, hipStream_t s) {
+  if (!n) return;
+  rocprim::radix_sort_keys(tmp, tmpb, in, out, (size_t)n, 0, 32, s);
+}
+
+}  // namespace yc

@@ -1,0 +1,193 @@
+// yc_work.h — device workspace of one batched merge and the host-side launch entry points.
+//
+// Every array lives in HBM for the lifetime of the engine (grow-only arena, no hipMalloc on the
+// merge path). Naming: B = batch bytes, G = decode groups, S = decoded structs, NC = clients,
+// U = units (one per (client, clock) in the merged store), NS = segments, NO = output structs.
+#pragma once
+#include "yc_common.h"
+
+namespace yc {
+
+struct Counters {            // device-side counters, read back at the few host sync points
+  uint32_t err;              // first error code (ERR_*)
+  uint32_t err_info;         // position / index that raised it
+  uint32_t nsections;        // appended by the walker
+  uint32_t ncopy;            // copy tasks
+  uint32_t npatch;           // desync patch positions
+  uint32_t nds;              // decoded delete-set ranges
+  uint32_t ndsclients;       // delete-set client headers
+  uint32_t nstructs;         // S
+  uint32_t nclients;         // NC
+  uint32_t nunits_lo;        // U (low 32 bits)
+  uint32_t nunits_hi;        // U (high bits; must be 0)
+  uint32_t nsegs;            // NS
+  uint32_t nout;             // NO
+  uint32_t changed;          // pointer-jumping convergence flag
+  uint32_t out_bytes;        // encoded output size
+  uint32_t sv_bytes;         // encoded state-vector size
+  uint32_t nkeys;            // distinct map keys
+  uint32_t nruns;            // delete-set runs in the output
+  uint32_t pad[14];          // encode scratch (see yc_encode.hip)
+  unsigned long long items;  // Σ clock lengths of Item + GC input structs (the throughput unit)
+};
+
+struct DsRange {             // one decoded (client, clock, len) delete-set range
+  uint32_t client;           // value; later rewritten to cidx
+  uint32_t clock;
+  uint32_t len;
+  uint32_t upd;
+};
+
+struct Work {
+  // ---- batch input
+  const uint8_t* bytes = nullptr;  // B bytes, every update starts at a 64-byte aligned offset
+  uint32_t nbytes = 0;
+  const uint32_t* uoff = nullptr;  // [nupd+1] update start offsets (aligned)
+  const uint32_t* ulen = nullptr;  // [nupd] real update lengths
+  const uint32_t* ugroup = nullptr;// [nupd] first decode group of each update
+  uint32_t nupd = 0;
+  const Group* groups = nullptr;   // [G]
+  uint32_t ngroups = 0;
+  // ---- capacities
+  uint32_t cap_structs = 0, cap_sections = 0, cap_copy = 0, cap_patch = 0, cap_ds = 0, cap_dsclients = 0;
+  uint64_t cap_units = 0;
+  // ---- decode
+  Counters* ctr = nullptr;
+  uint64_t* main_bits = nullptr;   // [B/64] speculative main-chain struct starts
+  uint64_t* final_bits = nullptr;  // [B/64] verified struct starts
+  uint64_t* sec_bits = nullptr;    // [B/64] first struct of every non-empty section
+  uint16_t* gpre = nullptr;        // [G*257] per-group prefix counts of main bits per chunk
+  uint32_t* gexit = nullptr;       // [G] first main-chain position >= group end
+  CopyTask* copy = nullptr;        // [cap_copy]
+  uint32_t* patch = nullptr;       // [cap_patch]
+  uint32_t* dsstart = nullptr;     // [nupd] byte position of the delete set
+  Section* sections = nullptr;     // [cap_sections] (walker order)
+  uint32_t* sec_sorted = nullptr;  // [cap_sections] section index by position rank
+  uint32_t* wcnt = nullptr;        // [B/64 + 1] popcount prefix of final_bits words
+  uint32_t* wsec = nullptr;        // [B/64 + 1] popcount prefix of sec_bits words
+  DsRange* ds = nullptr;           // [cap_ds]
+  uint32_t* ds_len = nullptr;      // [cap_ds+1] clipped lengths (scan input)
+  uint64_t* ds_scan = nullptr;     // [cap_ds+1]
+  uint32_t* dsclient_vals = nullptr; // [cap_dsclients] (client values seen in delete sets)
+  // ---- per struct (S)
+  uint32_t* s_pos = nullptr;
+  uint32_t* s_sec = nullptr;       // index into sections
+  uint32_t* s_len = nullptr;
+  uint64_t* s_lenscan = nullptr;   // [S+1] exclusive prefix of s_len
+  uint32_t* s_clock = nullptr;
+  uint32_t* s_cidx = nullptr;
+  uint8_t* s_info = nullptr;
+  uint32_t* s_ocidx = nullptr;     // origin client index (NONE = no origin)
+  uint32_t* s_oclock = nullptr;
+  uint32_t* s_rcidx = nullptr;     // right origin client index
+  uint32_t* s_rclock = nullptr;
+  uint32_t* s_pa = nullptr;        // parent name varString position (root) or NONE
+  uint32_t* s_pb = nullptr;        // parent name varString length
+  uint32_t* s_psub = nullptr;      // parentSub varString position or NONE
+  uint32_t* s_psublen = nullptr;
+  uint32_t* s_cpos = nullptr;      // content byte range
+  uint32_t* s_cend = nullptr;
+  uint32_t* s_celem = nullptr;     // position of first Any/JSON element (after the count varuint)
+  // ---- clients (NC)
+  uint32_t* cl_vals = nullptr;     // sorted distinct client ids [cap_sections]
+  uint32_t* cl_tmp = nullptr;      // sort scratch [cap_sections]
+  uint32_t* cl_state = nullptr;    // per client state (max end clock)
+  uint64_t* cl_base = nullptr;     // [NC+1] exclusive prefix of states (unit base)
+  uint32_t* cl_start = nullptr;    // per client start clock for diff encodes (sv); 0 = full
+  // ---- per unit (U)
+  uint32_t* u_owner = nullptr;
+  uint32_t* u_flags = nullptr;
+  uint32_t* u_minchild = nullptr;
+  uint64_t* u_cutbits = nullptr;   // [U/64+1]
+  uint32_t* u_wpre = nullptr;      // [U/64+2] popcount prefix of u_cutbits words
+  // ---- per segment (NS <= U)
+  uint32_t* g_start = nullptr;     // first unit (global unit index)
+  uint32_t* g_cidx = nullptr;
+  uint32_t* g_src = nullptr;       // owning struct
+  uint32_t* g_flags = nullptr;     // SEG_* flags
+  uint32_t* g_origin = nullptr;    // origin unit (global) or NONE
+  uint32_t* g_rorigin = nullptr;   // right-origin unit or NONE
+  uint32_t* g_link = nullptr;      // pointer-jumping link (key resolution)
+  uint32_t* g_key = nullptr;       // resolved key slot or NONE
+  uint64_t* g_maxchild = nullptr;  // (cidx<<32 | seg) of max-client child, 0 = none
+  uint32_t* g_next = nullptr;      // descent pointer / pointer jumping
+  uint32_t* g_outid = nullptr;     // output struct id (scan of !merge flags)
+  uint32_t* g_tmp = nullptr;       // scratch per segment
+  uint32_t* g_tmp2 = nullptr;
+  // ---- keys (hash table)
+  uint64_t* k_hash = nullptr;      // [cap_keys] open addressing table of 64-bit key hashes (0 = empty)
+  uint64_t* k_rootmax = nullptr;   // [cap_keys] (cidx<<32 | seg) of max-client root
+  uint32_t* k_winner = nullptr;    // [cap_keys] winning (rightmost) segment
+  uint32_t cap_keys = 0;
+  // ---- encode (NO <= NS)
+  uint32_t* o_first = nullptr;     // [NO+1] first segment of output struct (+ sentinel)
+  uint32_t* o_cidx = nullptr;      // client of output struct
+  uint32_t* o_size = nullptr;      // encoded size (0 = below the target state vector)
+  uint32_t* o_pos = nullptr;       // [NO+1] exclusive prefix of o_size
+  uint32_t* r_seg = nullptr;       // [runs] first segment of delete-set run
+  uint32_t* r_len = nullptr;       // [runs] run length in units
+  uint32_t* r_size = nullptr;      // [runs+1] encoded size of (clock,len)
+  uint32_t* r_pos = nullptr;       // [runs+1]
+  uint32_t* cc = nullptr;          // per-client scratch: CC_N arrays of (cap_clients+1)
+  uint32_t cap_clients = 0;
+  uint8_t* out = nullptr;          // encoded update
+  uint64_t cap_out = 0;
+  uint8_t* sv_out = nullptr;       // encoded state vector
+  uint32_t* scratch = nullptr;     // scan staging (max of all scan lengths)
+  // ---- rocPRIM scratch
+  void* tmp = nullptr;
+  size_t tmp_bytes = 0;
+};
+
+// per-client scratch arrays inside Work::cc
+enum : uint32_t {
+  CC_FIRST_OUT = 0, CC_FIRST_INCL, CC_NINCL, CC_HDR, CC_BLK, CC_BLKPOS, CC_NRUNS, CC_FIRST_RUN,
+  CC_DSBLK, CC_DSPOS, CC_SV, CC_SVPOS, CC_REV, CC_REVSCAN, CC_N
+};
+
+// segment flags
+enum : uint32_t {
+  SEG_DEL = 1u,        // deleted in the final state
+  SEG_GC = 2u,
+  SEG_EXPLICIT = 4u,   // segment starts at its source struct's first unit
+  SEG_ROOT = 8u,       // explicit parent (root name) + parentSub
+  SEG_MERGE = 16u,     // merges into the previous segment
+  SEG_ITEM = 32u,
+};
+// unit flags
+enum : uint32_t {
+  UF_DEL = 1u,         // source content is ContentDeleted
+  UF_GC = 2u,          // a GC struct covers the unit
+  UF_DS = 4u,          // a delete-set range covers the unit
+  UF_CUT = 8u,         // a struct boundary is required before this unit
+};
+
+// ---- launch entry points (yc_decode.hip / yc_merge.hip / yc_encode.hip / yc_prims.hip)
+void launch_group_parse(const Work& w, hipStream_t s);
+void launch_walker(const Work& w, hipStream_t s);
+void launch_build_final_bits(const Work& w, hipStream_t s);
+void launch_struct_positions(const Work& w, hipStream_t s);
+void launch_ds_decode(const Work& w, hipStream_t s);
+void launch_section_clients(const Work& w, uint32_t nsections, hipStream_t s);
+void launch_client_table(Work& w, uint32_t nsections, uint32_t* nclients_host, hipStream_t s);
+void launch_struct_decode(const Work& w, uint32_t nstructs, uint32_t nsections, uint32_t nclients, hipStream_t s);
+void launch_states(const Work& w, uint32_t nstructs, uint32_t nclients, hipStream_t s);
+
+void launch_units(const Work& w, uint32_t nstructs, uint32_t nclients, uint32_t nds, uint64_t nunits, hipStream_t s);
+void launch_segments(const Work& w, uint32_t nclients, uint64_t nunits, hipStream_t s);
+void launch_segment_props(const Work& w, uint32_t nsegs, uint32_t nclients, uint64_t nunits, hipStream_t s);
+uint32_t run_key_resolution(const Work& w, uint32_t nsegs, hipStream_t s);
+void launch_map_winner(const Work& w, uint32_t nsegs, hipStream_t s);
+uint32_t run_descent(const Work& w, uint32_t nsegs, hipStream_t s);
+void launch_merge_flags(const Work& w, uint32_t nsegs, hipStream_t s);
+
+void launch_encode_sizes(const Work& w, uint32_t nsegs, uint32_t nclients, uint32_t nout, uint32_t* nruns_host, hipStream_t s);
+void launch_encode_write(const Work& w, uint32_t nclients, uint32_t nout, uint32_t nruns, hipStream_t s);
+
+// rocPRIM wrappers (yc_prims.hip)
+size_t prim_tmp_bytes(uint64_t max_items);
+void scan_u32(void* tmp, size_t tmpb, const uint32_t* in, uint32_t* out, uint64_t n, hipStream_t s);          // exclusive
+void scan_u32_to_u64(void* tmp, size_t tmpb, const uint32_t* in, uint64_t* out, uint64_t n, hipStream_t s);   // exclusive
+void sort_u32(void* tmp, size_t tmpb, const uint32_t* in, uint32_t* out, uint64_t n, hipStream_t s);
+
+}  // namespace yc

@@ -1,0 +1,99 @@
+/* ycrdt.h — C ABI of the MI355X-native batched Yjs merge engine (libycrdt.so).
+ *
+ * This is the drop-in boundary for the path @ypear/crdt delegates to Yjs. The reference injects
+ * its CRDT engine through `router.options.Y` (reference crdt.js:175-180) and only ever calls the
+ * entry points listed below; each function cites the reference call sites it replaces. A Node
+ * N-API addon (crdt_amd/js) and a Python ctypes mirror (crdt_amd/__init__.py) are the callers.
+ *
+ * Conventions
+ *  - Inputs are borrowed for the duration of the call and copied (to HBM) before it returns.
+ *  - Outputs (ycrdt_out) are library-owned until ycrdt_free().
+ *  - Every function returns YCRDT_OK (0) or a negative YCRDT_E_* code; ycrdt_last_error() gives
+ *    the message (thread-local). Decode errors are atomic: the doc is unchanged (Yjs decodes the
+ *    whole struct section before integrating, Y@21330).
+ *  - Output byte order is Yjs 13.6 canonical (delete-set / state-vector clients sorted
+ *    descending); see DESIGN.md §Compat for the 13.5.16 insertion-order difference.
+ *  - There is no CPU fallback: without a usable HIP device every compute entry point fails
+ *    with YCRDT_E_DEVICE.
+ */
+#ifndef YCRDT_H
+#define YCRDT_H
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct ycrdt_engine ycrdt_engine;
+typedef struct ycrdt_doc ycrdt_doc;
+typedef struct ycrdt_batch ycrdt_batch;
+
+typedef struct { const uint8_t *ptr; size_t len; } ycrdt_buf; /* borrowed */
+typedef struct { uint8_t *ptr; size_t len; } ycrdt_out;       /* library-owned */
+
+enum {
+  YCRDT_OK = 0,
+  YCRDT_E_DECODE = -1,      /* malformed update (Yjs: Error('Integer out of range!')) */
+  YCRDT_E_PENDING = -2,     /* missing dependencies; Yjs would park the structs as pending */
+  YCRDT_E_UNSUPPORTED = -3, /* valid Yjs input outside the engine's coverage */
+  YCRDT_E_CAPACITY = -4,
+  YCRDT_E_DEVICE = -5,      /* no HIP device / HIP runtime error */
+  YCRDT_E_ARG = -6,
+};
+
+typedef struct {
+  uint64_t in_bytes;        /* bytes of all input updates */
+  uint64_t items;           /* Σ struct clock lengths of the inputs (Item + GC, Skip excluded) */
+  uint64_t structs;         /* decoded structs */
+  uint64_t units;           /* distinct (client, clock) units in the merged store */
+  uint64_t segments;        /* split-point segments */
+  uint64_t out_structs;     /* structs in the encoded state */
+  uint64_t out_bytes;       /* encoded update bytes */
+  uint64_t clients;
+  double device_ms;         /* device time of the merge (events on the engine stream) */
+} ycrdt_merge_stats;
+
+/* ---- engine ------------------------------------------------------------------------------ */
+/* device: HIP device ordinal. compat: 136 (default, Yjs 13.6 order) */
+int ycrdt_engine_create(int device, int compat, ycrdt_engine **out);
+void ycrdt_engine_destroy(ycrdt_engine *e);
+/* optional per-phase device timing (hipEvents on the engine stream) */
+int ycrdt_engine_set_profiling(ycrdt_engine *e, int on);
+/* fills up to `cap` (name, milliseconds) pairs of the last merge; returns the count */
+int ycrdt_engine_phase_times(ycrdt_engine *e, const char **names, double *ms, int cap);
+
+/* ---- Y.Doc ------------------------------------------------------------------------------- */
+/* new Y.Doc()  (crdt.js:33,54,56,80,221) */
+int ycrdt_doc_create(ycrdt_engine *e, uint32_t client_id, ycrdt_doc **out);
+void ycrdt_doc_destroy(ycrdt_doc *d);
+/* Y.applyUpdate(doc, u8)  (crdt.js:35,56,58,85,294) */
+int ycrdt_apply_update(ycrdt_doc *d, ycrdt_buf update);
+/* n sequential Y.applyUpdate calls, merged in one batch (LevelDB replay crdt.js:79-98, ingest) */
+int ycrdt_apply_updates(ycrdt_doc *d, const ycrdt_buf *ups, size_t n);
+/* Y.encodeStateAsUpdate(doc[, sv])  (crdt.js:56,260,288,347,383,443,471,505,533,560,585,611);
+ * sv.len == 0 ⇒ full state */
+int ycrdt_encode_state_as_update(ycrdt_doc *d, ycrdt_buf sv, ycrdt_out *out);
+/* Y.encodeStateVector(doc)  (crdt.js:59,239,258,289) */
+int ycrdt_encode_state_vector(ycrdt_doc *d, ycrdt_out *out);
+/* stats of the doc's last merge */
+int ycrdt_doc_last_stats(ycrdt_doc *d, ycrdt_merge_stats *st);
+
+/* ---- device-resident batches (ingest queue / benchmark) ---------------------------------- */
+/* Copies the updates into HBM. */
+int ycrdt_batch_stage(ycrdt_engine *e, const ycrdt_buf *ups, size_t n, ycrdt_batch **out);
+/* Merges the staged updates into a fresh doc entirely on the device; the encoded state stays in
+ * HBM. Equivalent to applying every update to a new Y.Doc and encodeStateAsUpdate(doc). */
+int ycrdt_batch_merge(ycrdt_batch *b, ycrdt_merge_stats *st);
+/* Copies the last merge result (encoded update and state vector) to the host. */
+int ycrdt_batch_result(ycrdt_batch *b, ycrdt_out *update, ycrdt_out *state_vector);
+void ycrdt_batch_destroy(ycrdt_batch *b);
+
+void ycrdt_free(ycrdt_out *o);
+const char *ycrdt_last_error(void);
+const char *ycrdt_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

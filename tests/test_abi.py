@@ -1,0 +1,20 @@
+"""CPU-side checks of the C ABI boundary: the library loads and exports every declared symbol."""
+import os
+import re
+
+import crdt_amd
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_header_symbols_exported():
+    hdr = open(os.path.join(ROOT, "include", "ycrdt.h")).read()
+    declared = set(re.findall(r"\b(ycrdt_[a-z_]+)\s*\(", hdr))
+    assert declared == set(crdt_amd.EXPORTS), declared ^ set(crdt_amd.EXPORTS)
+    L = crdt_amd.lib()
+    for sym in declared:
+        assert hasattr(L, sym), sym
+
+
+def test_version_string():
+    assert b"gfx950" in crdt_amd.lib().ycrdt_version()
