@@ -1,0 +1,56 @@
+"""Seeded synthetic replica-update workloads for tests and bench.py.
+
+Thin ctypes wrapper over crdt_amd/workload/ycw.cpp (built as crdt_amd/libycrdt_workload.so).
+"""
+import ctypes
+import json
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_L = None
+
+
+def _lib():
+    global _L
+    if _L is None:
+        L = ctypes.CDLL(os.path.join(_HERE, "libycrdt_workload.so"))
+        P = ctypes.POINTER
+        L.ycw_gen_map.argtypes = [
+            ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_double, ctypes.c_double, ctypes.c_int,
+            ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_int,
+            P(ctypes.c_void_p), P(ctypes.c_size_t), P(ctypes.c_void_p), P(ctypes.c_size_t), P(ctypes.c_void_p),
+        ]
+        L.ycw_free.argtypes = [ctypes.c_void_p]
+        _L = L
+    return _L
+
+
+# SURVEY.md §8(d)
+C1 = dict(n_keys=1000, n_replicas=2, ops_per_replica=10000, zipf_s=0.0, p_set=0.8, base_snapshot=False,
+          base_client=1, client_mode=1, value_mode=1, seed=42)
+C2 = dict(n_keys=100_000, n_replicas=1000, ops_per_replica=1000, zipf_s=1.1, p_set=0.8, base_snapshot=True,
+          base_client=1, client_mode=0, value_mode=0, seed=2)
+
+
+def gen_map(n_keys, n_replicas, ops_per_replica, zipf_s=1.1, p_set=0.8, base_snapshot=True, base_client=1,
+            client_mode=0, value_mode=0, seed=2, script=False):
+    """Returns (updates: list[bytes], script: dict|None)."""
+    L = _lib()
+    data, dlen, offs, nupd, sc = ctypes.c_void_p(), ctypes.c_size_t(), ctypes.c_void_p(), ctypes.c_size_t(), ctypes.c_void_p()
+    rc = L.ycw_gen_map(n_keys, n_replicas, ops_per_replica, zipf_s, p_set, 1 if base_snapshot else 0, base_client,
+                       client_mode, value_mode, seed, 1 if script else 0, ctypes.byref(data), ctypes.byref(dlen),
+                       ctypes.byref(offs), ctypes.byref(nupd), ctypes.byref(sc) if script else None)
+    if rc != 0:
+        raise ValueError("bad workload config")
+    try:
+        raw = ctypes.string_at(data.value, dlen.value) if dlen.value else b""
+        o = (ctypes.c_uint64 * (nupd.value + 1)).from_address(offs.value)
+        ups = [raw[o[i]:o[i + 1]] for i in range(nupd.value)]
+        js = json.loads(ctypes.string_at(sc.value).decode()) if script else None
+    finally:
+        L.ycw_free(data)
+        L.ycw_free(offs)
+        if script:
+            L.ycw_free(sc)
+    return ups, js
+
