@@ -19,7 +19,9 @@ constexpr uint32_t NONE = 0xFFFFFFFFu;
 constexpr uint32_t CHUNK = 64;
 constexpr uint32_t GROUP_LANES = 256;
 constexpr uint32_t GROUP_BYTES = CHUNK * GROUP_LANES;  // 16384
-constexpr uint32_t SPEC_MAX_STEPS = 4096;             // speculative parse work cap per struct
+constexpr uint32_t SPEC_STEPS_FAST = 4;               // speculative parse: first pass work cap (elements)
+constexpr uint32_t SPEC_MAX_STEPS = 1024;             // second pass (compacted); longer -> exact walker parse
+constexpr uint16_t STOPF = 0x8000;                    // table flag: chain stops at an unsized struct
 
 // content refs (low 5 bits of the info byte)
 enum : uint8_t {
@@ -53,7 +55,7 @@ struct Section {        // one client section of one update's struct section
   uint32_t pad;
 };
 
-struct CopyTask {       // "main-chain bits in [a,b) are true struct starts"
+struct CopyTask {       // verified chain segment: b struct starts along the chain from position a
   uint32_t a, b;
 };
 
@@ -94,15 +96,25 @@ __device__ __forceinline__ void skip_vi(const uint8_t* __restrict__ b, uint32_t&
   }
 }
 
+// A ContentJSON / ContentEmbed / ContentFormat value is JSON.stringify output, decoded by Yjs
+// with JSON.parse (Y@71000..): text that cannot start a JSON value (or is empty) makes Yjs throw,
+// so the decoder rejects it too. This also lets speculative parses of non-struct bytes fail fast.
+__device__ __forceinline__ bool json_start_ok(uint32_t c) {
+  return c == '{' || c == '[' || c == '"' || c == 't' || c == 'f' || c == 'n' || c == 'u' || c == '-' ||
+         (c >= '0' && c <= '9') || c == ' ' || c == '\t' || c == '\n' || c == '\r';
+}
+
 __device__ __forceinline__ void skip_bytes(uint32_t& p, uint32_t n, uint32_t end, bool& ok) {
   if (end - p < n) { ok = false; p = end; return; }
   p += n;
 }
 
-// readAny (L0@1937 B): iterative skip with an explicit container stack.
+// readAny (L0@1937 B): iterative skip with an explicit container stack of depth DEPTH (deeper
+// nesting fails the parse: speculative callers use a shallow stack, exact callers a deep one).
+template <int DEPTH>
 __device__ inline bool skip_any(const uint8_t* __restrict__ b, uint32_t& p, uint32_t end, uint32_t& steps) {
-  uint32_t rem[32];
-  uint8_t isobj[32];
+  uint32_t rem[DEPTH];
+  uint32_t objmask = 0;  // bit d set: level d is an object (key before each member)
   int d = 0;
   bool ok = true;
 #pragma unroll 1
@@ -121,9 +133,9 @@ __device__ inline bool skip_any(const uint8_t* __restrict__ b, uint32_t& p, uint
         uint32_t n = rd_vu(b, p, end, ok);
         if (!ok) return false;
         if (n > 0) {
-          if (d == 32) return false;
+          if (d == DEPTH) return false;
           rem[d] = n;
-          isobj[d] = tag == 118;
+          if (tag == 118) objmask |= 1u << d; else objmask &= ~(1u << d);
           ++d;
           if (tag == 118) { uint32_t k = rd_vu(b, p, end, ok); if (ok) skip_bytes(p, k, end, ok); }
           if (!ok) return false;
@@ -135,10 +147,11 @@ __device__ inline bool skip_any(const uint8_t* __restrict__ b, uint32_t& p, uint
     }
     if (!ok) return false;
     // a value completed: pop finished containers
+#pragma unroll 1
     for (;;) {
       if (d == 0) return true;
       if (--rem[d - 1] > 0) {
-        if (isobj[d - 1]) { uint32_t k = rd_vu(b, p, end, ok); if (ok) skip_bytes(p, k, end, ok); if (!ok) return false; }
+        if ((objmask >> (d - 1)) & 1u) { uint32_t k = rd_vu(b, p, end, ok); if (ok) skip_bytes(p, k, end, ok); if (!ok) return false; }
         break;  // next member value
       }
       --d;
@@ -162,18 +175,19 @@ struct StructView {
 };
 
 // Parses one struct starting at p. FULL fills `v`. Speculative callers pass a finite
-// step budget; exact callers pass 0xFFFFFFFF. Returns 1 = ok, 0 = malformed, -1 = budget hit.
-template <bool FULL>
+// step budget; exact callers pass 0xFFFFFFFF. Returns 1 = ok, 0 = malformed, -1 = budget hit,
+// -2 = ran past `end` (only distinguishable from 0 when `end` is not the update end).
+template <bool FULL, int DEPTH = 32>
 __device__ inline int parse_struct(const uint8_t* __restrict__ b, uint32_t& p, uint32_t end, uint32_t steps, StructView* v) {
   bool ok = true;
-  if (p >= end) return 0;
+  if (p >= end) return -2;
   uint32_t info = b[p++];
   uint32_t ref = info & 31u;
   if (FULL) { v->info = (uint8_t)info; v->ref = (uint8_t)ref; v->pkind = 0; v->has_psub = 0; v->nel = 0; }
   if (ref == REF_GC || ref == REF_SKIP) {
     uint32_t len = rd_vu(b, p, end, ok);
     if (FULL) { v->len = len; v->cpos = v->cend = p; }
-    return ok ? 1 : 0;
+    return ok ? 1 : (p >= end ? -2 : 0);
   }
   if (ref > REF_DOC) return 0;
   if (info & 0x80u) {
@@ -184,10 +198,10 @@ __device__ inline int parse_struct(const uint8_t* __restrict__ b, uint32_t& p, u
     uint32_t c = rd_vu(b, p, end, ok), k = rd_vu(b, p, end, ok);
     if (FULL) { v->rc = c; v->rk = k; }
   }
-  if (!ok) return 0;
+  if (!ok) return p >= end ? -2 : 0;
   if ((info & 0xC0u) == 0) {
     uint32_t pinfo = rd_vu(b, p, end, ok);
-    if (!ok) return 0;
+    if (!ok) return p >= end ? -2 : 0;
     if (pinfo == 1) {
       uint32_t st = p;
       uint32_t n = rd_vu(b, p, end, ok);
@@ -203,7 +217,7 @@ __device__ inline int parse_struct(const uint8_t* __restrict__ b, uint32_t& p, u
       if (ok) skip_bytes(p, n, end, ok);
       if (FULL) { v->has_psub = 1; v->psub_pos = st; v->psub_len = p - st; }
     }
-    if (!ok) return 0;
+    if (!ok) return p >= end ? -2 : 0;
   }
   uint32_t cpos = p;
   uint32_t len = 1;
@@ -216,13 +230,20 @@ __device__ inline int parse_struct(const uint8_t* __restrict__ b, uint32_t& p, u
         if (steps == 0) return -1;
         --steps;
         uint32_t k = rd_vu(b, p, end, ok);
+        if (ok && (k == 0 || (p < end && !json_start_ok(b[p])))) return 0;
         if (ok) skip_bytes(p, k, end, ok);
       }
       if (FULL) v->nel = n;
       if (ok && steps == 0) return -1;
       break;
     }
-    case REF_BINARY: case REF_EMBED: { uint32_t k = rd_vu(b, p, end, ok); if (ok) skip_bytes(p, k, end, ok); break; }
+    case REF_BINARY: { uint32_t k = rd_vu(b, p, end, ok); if (ok) skip_bytes(p, k, end, ok); break; }
+    case REF_EMBED: {
+      uint32_t k = rd_vu(b, p, end, ok);
+      if (ok && (k == 0 || (p < end && !json_start_ok(b[p])))) return 0;
+      if (ok) skip_bytes(p, k, end, ok);
+      break;
+    }
     case REF_STRING: {
       uint32_t k = rd_vu(b, p, end, ok);
       uint32_t st = p;
@@ -241,6 +262,7 @@ __device__ inline int parse_struct(const uint8_t* __restrict__ b, uint32_t& p, u
       uint32_t k = rd_vu(b, p, end, ok);
       if (ok) skip_bytes(p, k, end, ok);
       k = rd_vu(b, p, end, ok);
+      if (ok && (k == 0 || (p < end && !json_start_ok(b[p])))) return 0;
       if (ok) skip_bytes(p, k, end, ok);
       break;
     }
@@ -253,7 +275,7 @@ __device__ inline int parse_struct(const uint8_t* __restrict__ b, uint32_t& p, u
     case REF_ANY: {
       uint32_t n = rd_vu(b, p, end, ok);
       len = n;
-      for (uint32_t i = 0; i < n && ok; ++i) ok = skip_any(b, p, end, steps);
+      for (uint32_t i = 0; i < n && ok; ++i) ok = skip_any<DEPTH>(b, p, end, steps);
       if (!ok && steps == 0) return -1;
       if (FULL) v->nel = n;
       break;
@@ -261,13 +283,14 @@ __device__ inline int parse_struct(const uint8_t* __restrict__ b, uint32_t& p, u
     case REF_DOC: {
       uint32_t k = rd_vu(b, p, end, ok);
       if (ok) skip_bytes(p, k, end, ok);
-      if (ok) ok = skip_any(b, p, end, steps);
+      if (ok) ok = skip_any<DEPTH>(b, p, end, steps);
       if (!ok && steps == 0) return -1;
       break;
     }
     default: return 0;
   }
   if (FULL) { v->len = len; v->cpos = cpos; v->cend = p; }
+  if (!ok && p >= end) return -2;  // ran out of input (the struct may continue past `end`)
   return ok ? 1 : 0;
 }
 

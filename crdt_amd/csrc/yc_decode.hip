@@ -19,103 +19,147 @@
 
 namespace yc {
 
-// --------------------------------------------------------------------------- 1. group parse
-__global__ __launch_bounds__(256) void k_group_parse(const uint8_t* __restrict__ b, const Group* __restrict__ groups,
-                                                     uint64_t* __restrict__ main_bits, uint16_t* __restrict__ gpre,
-                                                     uint32_t* __restrict__ gexit) {
-  __shared__ uint64_t sbits[GROUP_LANES];
-  __shared__ uint32_t sexit[GROUP_LANES];
-  __shared__ uint8_t strunc[GROUP_LANES];
-  __shared__ uint32_t scnt[GROUP_LANES + 1];
+// --------------------------------------------------------------------------- 1. chain tables
+// For every byte position p of a group: nxt[p] = length of the struct that would start at p
+// (0 = not a struct, 1 = too long for the staged window), and the chain summaries
+// (first chain position at/after the end of p's chunk / block / group, number of chain positions
+// visited before it) computed by backward dynamic programming (list ranking) in LDS.
+constexpr uint32_t TL = 512;                    // lanes per table workgroup
+constexpr uint32_t HALO = 4096;                 // bytes staged past the group end
+constexpr uint32_t BLOCK = 1024;                // 16 chunks
+constexpr uint32_t LDS_NXT = 0, LDS_CEXIT = 32768, LDS_CCNT = 65536, LDS_BEXIT = 81920, LDS_BCNT = 114688;
+constexpr uint32_t LDS_TOTAL = 147456;
+// the pass-2 queue (<= 16K u16 offsets) lives in the cexit region, unused until phase B
+__device__ __forceinline__ uint16_t* ccnt16_alias(uint8_t* lds) { return (uint16_t*)(lds + LDS_CEXIT); }
+static_assert(GROUP_BYTES == 16384, "table layout assumes 16 KiB groups");
+
+__global__ __launch_bounds__(TL) void k_tables(const uint8_t* __restrict__ b, const Group* __restrict__ groups, Tables t) {
+  __shared__ __attribute__((aligned(16))) uint8_t lds[LDS_TOTAL];
+  uint16_t* nxt = (uint16_t*)(lds + LDS_NXT);
+  uint16_t* cexit = (uint16_t*)(lds + LDS_CEXIT);
+  uint8_t* ccnt = (uint8_t*)(lds + LDS_CCNT);
+  uint16_t* bexit = (uint16_t*)(lds + LDS_BEXIT);
+  uint16_t* bcnt = (uint16_t*)(lds + LDS_BCNT);
+  uint8_t* sb = lds + LDS_BEXIT;                // staged bytes overlay the block arrays (phase A only)
+  uint16_t* gexit = nxt;                        // group level overlays nxt / cexit (phase D)
+  uint16_t* gcnt = cexit;
   const Group G = groups[blockIdx.x];
-  const uint32_t lane = threadIdx.x;
-  const uint32_t nchunks = (G.end - G.start + CHUNK - 1) / CHUNK;
-  const uint32_t cs = G.start + lane * CHUNK;
-  uint64_t bits = 0;
-  uint32_t pos = cs;
-  uint8_t trunc = 0;
-  if (lane < nchunks) {
-    const uint32_t ce = min(cs + CHUNK, G.end);
-    while (pos < ce) {
-      // every position the chain visits is marked (also one that fails to parse: it may be the
-      // first byte after a section, which the walker needs to find as "the r-th position")
-      bits |= 1ull << (pos - cs);
-      uint32_t q = pos;
-      int r = parse_struct<false>(b, q, G.uend, SPEC_MAX_STEPS, nullptr);
-      if (r > 0) pos = q;
-      else if (r == 0) ++pos;          // not a struct start: restart one byte later
-      else { trunc = 1; break; }       // long struct: leave it to the exact stitcher
+  const uint32_t tid = threadIdx.x;
+  const uint32_t glen = G.end - G.start;
+  const uint32_t lim = min(G.uend, G.start + GROUP_BYTES + HALO);
+  const uint32_t slen = lim - G.start;
+  const bool window_cut = lim < G.uend;
+  // stage (16-byte vector loads; the batch buffer is padded)
+  for (uint32_t i = tid * 16; i < slen; i += TL * 16) *(uint4*)(sb + i) = *(const uint4*)(b + G.start + i);
+  __syncthreads();
+  // phase A: speculative parse at every byte position. Pass 1 uses a tiny work cap; positions that
+  // need more work are queued in LDS and re-parsed densely in pass 2, so one slow lane does not
+  // stall its whole wavefront.
+  __shared__ uint32_t qn;
+  uint16_t* queue = ccnt16_alias(lds);
+  if (tid == 0) qn = 0;
+  __syncthreads();
+  for (uint32_t o = tid; o < glen; o += TL) {
+    uint32_t q = o;
+    const int r = parse_struct<false, 4>(sb, q, slen, SPEC_STEPS_FAST, nullptr);
+    uint16_t d;
+    if (r > 0) d = (uint16_t)(q - o);
+    else if (r == -1) { d = 1; queue[atomicAdd(&qn, 1u)] = (uint16_t)o; }
+    else if (r == -2 && window_cut) d = 1;  // may continue past the staged window: exact parse later
+    else d = 0;
+    nxt[o] = d;
+  }
+  __syncthreads();
+  const uint32_t nq = qn;
+  for (uint32_t i = tid; i < nq; i += TL) {
+    const uint32_t o = queue[i];
+    uint32_t q = o;
+    const int r = parse_struct<false, 4>(sb, q, slen, SPEC_MAX_STEPS, nullptr);
+    nxt[o] = r > 0 ? (uint16_t)(q - o) : ((r == -1 || (r == -2 && window_cut)) ? (uint16_t)1 : (uint16_t)0);
+  }
+  __syncthreads();
+  // phase B: chunk level (one lane per chunk, backward over its 64 positions)
+  const uint32_t nchunks = (glen + CHUNK - 1) / CHUNK;
+  for (uint32_t c = tid; c < nchunks; c += TL) {
+    const uint32_t cs = c * CHUNK, ce = min(cs + CHUNK, glen);
+    for (int o = (int)ce - 1; o >= (int)cs; --o) {
+      const uint32_t d = nxt[o];
+      if (d == 1) { cexit[o] = (uint16_t)(o | STOPF); ccnt[o] = 0; continue; }
+      const uint32_t sx = d == 0 ? o + 1 : o + d;
+      if (sx >= ce) { cexit[o] = (uint16_t)sx; ccnt[o] = 1; }
+      else { cexit[o] = cexit[sx]; ccnt[o] = (uint8_t)(1 + ccnt[sx]); }
     }
   }
-  sbits[lane] = bits;
-  sexit[lane] = pos;
-  strunc[lane] = trunc;
   __syncthreads();
-  if (lane == 0) {
-    // stitch: one deterministic chain from the group start (exact where the lanes gave up)
-    uint32_t p = G.start;
-    for (uint32_t c = 0; c < nchunks; ++c) {
-      const uint32_t ccs = G.start + c * CHUNK;
-      const uint32_t cce = min(ccs + CHUNK, G.end);
-      const uint64_t cb = sbits[c];
-      uint64_t m = 0;
-      while (p < cce) {
-        const uint32_t off = p - ccs;
-        if ((cb >> off) & 1ull) {  // on chunk c's chain: adopt it
-          m |= cb & (~0ull << off);
-          p = sexit[c];
-          if (strunc[c]) {         // exact parse of the struct the lane skipped (already marked)
-            uint32_t q = p;
-            if (parse_struct<false>(b, q, G.uend, 0xFFFFFFFFu, nullptr) > 0) p = q;
-            else ++p;
-          }
-          continue;
-        }
-        m |= 1ull << off;
-        uint32_t q = p;
-        if (parse_struct<false>(b, q, G.uend, 0xFFFFFFFFu, nullptr) > 0) p = q;
-        else ++p;
-      }
-      sbits[c] = m;
+  // exits are stored as forward deltas from the position itself (|STOPF when the chain stops at a
+  // struct the tables could not size), so consumers never need the group origin
+  for (uint32_t o = tid; o < glen; o += TL) {
+    t.nxt[G.start + o] = nxt[o];
+    t.cexit[G.start + o] = (uint16_t)(((cexit[o] & 0x7FFFu) - o) | (cexit[o] & STOPF));
+    t.ccnt[G.start + o] = ccnt[o];
+  }
+  // phase C: block level (chunk s of every block, s = 15..0)
+  for (int s = 15; s >= 0; --s) {
+    for (uint32_t i = tid; i < 16 * CHUNK; i += TL) {
+      const uint32_t blk = i / CHUNK;
+      const uint32_t o = blk * BLOCK + (uint32_t)s * CHUNK + (i % CHUNK);
+      if (o >= glen) continue;
+      const uint32_t bend = min((blk + 1) * BLOCK, glen);
+      const uint32_t x = cexit[o];
+      if ((x & STOPF) || x >= bend) { bexit[o] = (uint16_t)x; bcnt[o] = ccnt[o]; }
+      else { bexit[o] = bexit[x]; bcnt[o] = (uint16_t)(ccnt[o] + bcnt[x]); }
     }
-    gexit[blockIdx.x] = p;
-  }
-  __syncthreads();
-  uint32_t cnt = 0;
-  if (lane < nchunks) {
-    main_bits[(G.start >> 6) + lane] = sbits[lane];
-    cnt = (uint32_t)__popcll(sbits[lane]);
-  }
-  scnt[lane] = cnt;
-  __syncthreads();
-  // inclusive Hillis-Steele scan over 256 counts
-  for (uint32_t off = 1; off < GROUP_LANES; off <<= 1) {
-    uint32_t v = lane >= off ? scnt[lane - off] : 0;
-    __syncthreads();
-    scnt[lane] += v;
     __syncthreads();
   }
-  uint16_t* pre = gpre + (size_t)blockIdx.x * (GROUP_LANES + 1);
-  pre[lane + 1] = (uint16_t)scnt[lane];
-  if (lane == 0) pre[0] = 0;
+  for (uint32_t o = tid; o < glen; o += TL) {
+    t.bexit[G.start + o] = (uint16_t)(((bexit[o] & 0x7FFFu) - o) | (bexit[o] & STOPF));
+    t.bcnt[G.start + o] = bcnt[o];
+  }
+  // phase D: group level (block s = 15..0); gexit/gcnt overlay nxt/cexit (already written out)
+  for (int s = 15; s >= 0; --s) {
+    for (uint32_t i = tid; i < BLOCK; i += TL) {
+      const uint32_t o = (uint32_t)s * BLOCK + i;
+      if (o >= glen) continue;
+      const uint32_t x = bexit[o];
+      if ((x & STOPF) || x >= glen) { gexit[o] = (uint16_t)x; gcnt[o] = bcnt[o]; }
+      else { gexit[o] = gexit[x]; gcnt[o] = (uint16_t)(bcnt[o] + gcnt[x]); }
+    }
+    __syncthreads();
+  }
+  for (uint32_t o = tid; o < glen; o += TL) {
+    t.gexit[G.start + o] = (uint16_t)(((gexit[o] & 0x7FFFu) - o) | (gexit[o] & STOPF));
+    t.gcnt[G.start + o] = gcnt[o];
+  }
 }
 
 void launch_group_parse(const Work& w, hipStream_t s) {
   if (w.ngroups == 0) return;
-  hipLaunchKernelGGL(k_group_parse, dim3(w.ngroups), dim3(GROUP_LANES), 0, s, w.bytes, w.groups, w.main_bits, w.gpre,
-                     w.gexit);
+  hipLaunchKernelGGL(k_tables, dim3(w.ngroups), dim3(TL), 0, s, w.bytes, w.groups, w.tab);
 }
 
 // --------------------------------------------------------------------------- 2. walker
-__device__ __forceinline__ uint32_t select_bit(uint64_t x, uint32_t n) {  // position of the n-th set bit
-  for (uint32_t i = 0; i < n; ++i) x &= x - 1;
-  return (uint32_t)__ffsll((long long)x) - 1;
+// One lane per update follows the true struct chain through the section headers: a whole group
+// per step while the current section continues past it (gexit/gcnt), descending to block /
+// chunk / struct granularity only where a section ends. It emits verified chain segments
+// (start, count) for k_mark and exact positions (long structs, final steps) as patches.
+__device__ __forceinline__ bool emit_seg(const Work& w, uint32_t x, uint32_t n) {
+  const uint32_t i = atomicAdd(&w.ctr->ncopy, 1u);
+  if (i >= w.cap_copy) { raise_err(&w.ctr->err, ERR_CAPACITY); return false; }
+  w.copy[i] = CopyTask{x, n};
+  return true;
+}
+__device__ __forceinline__ bool emit_patch(const Work& w, uint32_t p) {
+  const uint32_t i = atomicAdd(&w.ctr->npatch, 1u);
+  if (i >= w.cap_patch) { raise_err(&w.ctr->err, ERR_CAPACITY); return false; }
+  w.patch[i] = p;
+  return true;
 }
 
 __global__ __launch_bounds__(64) void k_walker(Work w) {
   const uint32_t u = blockIdx.x * blockDim.x + threadIdx.x;
   if (u >= w.nupd) return;
   const uint8_t* __restrict__ b = w.bytes;
+  const Tables& T = w.tab;
   const uint32_t ustart = w.uoff[u];
   const uint32_t uend = ustart + w.ulen[u];
   uint32_t* err = &w.ctr->err;
@@ -139,39 +183,40 @@ __global__ __launch_bounds__(64) void k_walker(Work w) {
     uint32_t r = n;
     while (r > 0) {
       if (p >= uend) { raise_err(err, ERR_DECODE); return; }
-      const uint32_t g = w.ugroup[u] + (p - ustart) / GROUP_BYTES;
-      const uint64_t wb = w.main_bits[p >> 6];
-      const uint32_t off = p & 63;
-      if ((wb >> off) & 1ull) {
-        const Group G = w.groups[g];
-        const uint16_t* pre = w.gpre + (size_t)g * (GROUP_LANES + 1);
-        const uint32_t c = (p - G.start) >> 6;
-        const uint32_t below = pre[c] + (uint32_t)__popcll(wb & ((1ull << off) - 1));
-        const uint32_t total = pre[GROUP_LANES];
-        const uint32_t k = total - below;
-        uint32_t pend;
-        if (k < r) {
-          pend = w.gexit[g];
-          r -= k;
-        } else {
-          const uint32_t target = below + r;
-          if (target == total) pend = w.gexit[g];
-          else {
-            uint32_t lo = 0, hi = GROUP_LANES;  // last chunk cc with pre[cc] <= target
-            while (hi - lo > 1) { uint32_t mid = (lo + hi) >> 1; if (pre[mid] <= target) lo = mid; else hi = mid; }
-            const uint64_t cw = w.main_bits[(G.start >> 6) + lo];
-            pend = G.start + lo * CHUNK + select_bit(cw, target - pre[lo]);
-          }
-          r = 0;
+      const uint32_t ge = T.gexit[p], gc = T.gcnt[p];
+      bool exact = false;
+      if (gc < r) {  // the section continues past this group (or past a long struct)
+        if (gc && !emit_seg(w, p, gc)) return;
+        r -= gc;
+        p += ge & 0x7FFFu;
+        exact = (ge & STOPF) != 0;
+      } else {       // the section ends inside this group: descend block -> chunk -> struct
+        uint32_t rr = r;
+        for (;;) {
+          const uint32_t be = T.bexit[p], bc = T.bcnt[p];
+          if ((be & STOPF) || bc >= rr) break;
+          if (!emit_seg(w, p, bc)) return;
+          rr -= bc;
+          p += be;
         }
-        const uint32_t ti = atomicAdd(&w.ctr->ncopy, 1u);
-        if (ti >= w.cap_copy) { raise_err(err, ERR_CAPACITY); return; }
-        w.copy[ti] = CopyTask{p, min(pend, G.end)};
-        p = pend;
-      } else {
-        const uint32_t pi = atomicAdd(&w.ctr->npatch, 1u);
-        if (pi >= w.cap_patch) { raise_err(err, ERR_CAPACITY); return; }
-        w.patch[pi] = p;
+        for (;;) {
+          const uint32_t ce = T.cexit[p], cc = T.ccnt[p];
+          if ((ce & STOPF) || cc >= rr) break;
+          if (!emit_seg(w, p, cc)) return;
+          rr -= cc;
+          p += ce;
+        }
+        while (rr > 0) {
+          const uint32_t d = T.nxt[p];
+          if (d == 1) { exact = true; break; }
+          if (d == 0 || !emit_patch(w, p)) { raise_err(err, ERR_DECODE); return; }
+          p += d;
+          --rr;
+        }
+        r = rr;
+      }
+      if (exact && r > 0) {  // a struct the tables could not size: parse it exactly
+        if (!emit_patch(w, p)) return;
         uint32_t q = p;
         if (parse_struct<false>(b, q, uend, 0xFFFFFFFFu, nullptr) <= 0) { raise_err(err, ERR_DECODE); w.ctr->err_info = p; return; }
         p = q;
@@ -188,33 +233,71 @@ void launch_walker(const Work& w, hipStream_t s) {
 }
 
 // --------------------------------------------------------------------------- 3. final bitmap
-__global__ __launch_bounds__(256) void k_copy(const CopyTask* __restrict__ tasks, const uint32_t* __restrict__ ntasks,
-                                              const uint64_t* __restrict__ main_bits, uint64_t* __restrict__ final_bits) {
-  const uint32_t lane = threadIdx.x & 63;
-  const uint32_t t = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-  if (t >= *ntasks) return;
-  const CopyTask T = tasks[t];
-  if (T.a >= T.b) return;
-  const uint32_t w0 = T.a >> 6, w1 = (T.b - 1) >> 6;
-  for (uint32_t wi = w0 + lane; wi <= w1; wi += 64) {
-    uint64_t m = ~0ull;
-    if (wi == w0) m &= ~0ull << (T.a & 63);
-    if (wi == w1 && (T.b & 63)) m &= (1ull << (T.b & 63)) - 1;
-    const uint64_t v = main_bits[wi] & m;
-    if (v) atomicOr((unsigned long long*)&final_bits[wi], (unsigned long long)v);
+// One wavefront per verified segment (x, n): block hops by lane 0, chunk hops by one lane per
+// block, then one lane per chunk walks nxt inside its 64-byte chunk and sets the bits of that
+// chunk's bitmap word with a single atomicOr.
+__global__ __launch_bounds__(256) void k_mark(Work w) {
+  __shared__ uint32_t s_bx[4][16], s_bn[4][16];          // block spans per wave
+  __shared__ uint32_t s_cx[4][256], s_cn[4][256];        // chunk spans per wave
+  __shared__ uint32_t s_nb[4], s_nc[4][16];
+  const uint32_t wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const uint32_t si = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const uint32_t nseg = min(w.ctr->ncopy, w.cap_copy);
+  const bool active = si < nseg;  // no early return: every wave reaches the barriers
+  CopyTask S{0, 0};
+  if (active) S = w.copy[si];
+  const Tables& T = w.tab;
+  if (lane == 0) {  // block spans of the segment (segments never cross a group)
+    uint32_t x = S.a, left = active ? S.b : 0, nb = 0;
+    while (left > 0 && nb < 16) {
+      const uint32_t take = min((uint32_t)T.bcnt[x], left);
+      s_bx[wv][nb] = x;
+      s_bn[wv][nb] = take;
+      ++nb;
+      left -= take;
+      if (left) x += T.bexit[x] & 0x7FFFu;
+    }
+    s_nb[wv] = nb;
+  }
+  __syncthreads();
+  const uint32_t nb = s_nb[wv];
+  if (lane < nb) {
+    uint32_t x = s_bx[wv][lane], left = s_bn[wv][lane], nc = 0;
+    while (left > 0 && nc < 16) {
+      const uint32_t cc = T.ccnt[x];
+      const uint32_t take = min(cc, left);
+      s_cx[wv][lane * 16 + nc] = x; s_cn[wv][lane * 16 + nc] = take; ++nc;
+      left -= take;
+      if (left) x += T.cexit[x] & 0x7FFFu;
+    }
+    s_nc[wv][lane] = nc;
+  }
+  __syncthreads();
+  for (uint32_t k = lane; k < nb * 16; k += 64) {
+    const uint32_t bi = k >> 4, ci = k & 15;
+    if (ci >= s_nc[wv][bi]) continue;
+    uint32_t x = s_cx[wv][k], left = s_cn[wv][k];
+    uint64_t m = 0;
+    const uint32_t word = x >> 6;
+    while (left > 0) {
+      m |= 1ull << (x & 63);
+      const uint32_t d = T.nxt[x];
+      x += d == 0 ? 1 : d;
+      --left;
+    }
+    atomicOr((unsigned long long*)&w.final_bits[word], (unsigned long long)m);
   }
 }
-__global__ void k_patch(const uint32_t* __restrict__ patch, const uint32_t* __restrict__ npatch, uint64_t* __restrict__ final_bits) {
+__global__ void k_patch(const uint32_t* __restrict__ patch, const uint32_t* __restrict__ npatch, uint32_t cap, uint64_t* __restrict__ final_bits) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= *npatch) return;
+  if (i >= min(*npatch, cap)) return;
   const uint32_t p = patch[i];
   atomicOr((unsigned long long*)&final_bits[p >> 6], 1ull << (p & 63));
 }
 
-void launch_build_final_bits(const Work& w, hipStream_t s) {
-  // launch over the capacities; kernels read the real counts from device memory
-  hipLaunchKernelGGL(k_copy, dim3((w.cap_copy + 3) / 4), dim3(256), 0, s, w.copy, &w.ctr->ncopy, w.main_bits, w.final_bits);
-  hipLaunchKernelGGL(k_patch, dim3((w.cap_patch + 255) / 256), dim3(256), 0, s, w.patch, &w.ctr->npatch, w.final_bits);
+void launch_build_final_bits(const Work& w, uint32_t nseg, uint32_t npatch, hipStream_t s) {
+  if (nseg) hipLaunchKernelGGL(k_mark, dim3((nseg + 3) / 4), dim3(256), 0, s, w);
+  if (npatch) hipLaunchKernelGGL(k_patch, dim3((npatch + 255) / 256), dim3(256), 0, s, w.patch, &w.ctr->npatch, w.cap_patch, w.final_bits);
 }
 
 // --------------------------------------------------------------------------- 4. struct positions
@@ -273,7 +356,10 @@ void launch_section_clients(const Work& w, uint32_t nsections, hipStream_t s) {
 }
 
 // --------------------------------------------------------------------------- 5. delete sets
-__device__ __forceinline__ uint32_t nth_lane(uint64_t mask, uint32_t n) { return select_bit(mask, n); }
+__device__ __forceinline__ uint32_t nth_lane(uint64_t x, uint32_t n) {  // position of the n-th set bit
+  for (uint32_t i = 0; i < n; ++i) x &= x - 1;
+  return (uint32_t)__ffsll((long long)x) - 1;
+}
 
 __global__ __launch_bounds__(256) void k_ds_decode(Work w) {
   const uint32_t lane = threadIdx.x & 63;
@@ -286,6 +372,10 @@ __global__ __launch_bounds__(256) void k_ds_decode(Work w) {
   uint32_t* err = &w.ctr->err;
   enum { PH_N = 0, PH_CLIENT = 1, PH_NR = 2, PH_PAIRS = 3, PH_DONE = 4 };
   uint32_t phase = PH_N, nclients = 0, client = 0, pairs_left = 0, pend_clock = 0;
+  // this update's private output region (every range needs >= 2 bytes): no shared counter
+  const uint32_t obase0 = w.ds_region[u];
+  const uint32_t oend = w.ds_region[u + 1];
+  uint32_t obase = obase0;
   uint32_t carry_val = 0, carry_shift = 0, carry_bytes = 0;
   const uint64_t lt_mask = (1ull << lane) - 1;
   for (uint32_t base = p0; base < end && phase != PH_DONE; base += 64) {
@@ -318,20 +408,18 @@ __global__ __launch_bounds__(256) void k_ds_decode(Work w) {
         const bool mine = ((term >> lane) & 1ull) && myk >= vi && myk < vi + take;
         const bool is_len = mine && ((pairs_left - (myk - vi)) & 1u);
         const uint64_t lm = __ballot(is_len);
-        uint32_t obase = 0;
-        if (lane == 0 && lm) obase = atomicAdd(&w.ctr->nds, (uint32_t)__popcll(lm));
-        obase = (uint32_t)__shfl((int)obase, 0);
         if (is_len) {
           const uint32_t idx = obase + (uint32_t)__popcll(lm & lt_mask);
-          if (idx < w.cap_ds) {
+          if (idx < oend) {
             DsRange r;
             r.client = client;
             r.clock = myk == vi ? pend_clock : prevval;
             r.len = val;
             r.upd = u;
-            w.ds[idx] = r;
+            w.ds_tmp[idx] = r;
           } else raise_err(err, ERR_CAPACITY);
         }
+        obase += (uint32_t)__popcll(lm);
         pairs_left -= take;
         vi += take;
         if (pairs_left & 1u) pend_clock = (uint32_t)__shfl((int)val, (int)nth_lane(term, vi - 1));
@@ -377,11 +465,33 @@ __global__ __launch_bounds__(256) void k_ds_decode(Work w) {
     }
   }
   if (phase != PH_DONE) raise_err(err, ERR_DECODE);  // truncated delete set
+  if (lane == 0) w.ds_count[u] = obase - obase0;
+}
+
+__global__ void k_ds_bound(Work w) {  // region size per update: (delete-set bytes + 1) / 2
+  const uint32_t u = blockIdx.x * blockDim.x + threadIdx.x;
+  if (u > w.nupd) return;
+  if (u == w.nupd) { w.scratch[u] = 0; w.ds_count[u] = 0; return; }
+  const uint32_t st = w.dsstart[u];
+  w.scratch[u] = st == NONE ? 0 : (w.uoff[u] + w.ulen[u] - st + 1) / 2;
+  w.ds_count[u] = 0;
+}
+__global__ void k_ds_compact(Work w) {  // one wave per update: region -> dense ds[]
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t u = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  if (u >= w.nupd) return;
+  const uint32_t n = w.ds_count[u], src = w.ds_region[u], dst = w.ds_dense_off[u];
+  for (uint32_t i = lane; i < n; i += 64) w.ds[dst + i] = w.ds_tmp[src + i];
+  if (u == w.nupd - 1 && lane == 0) w.ctr->nds = dst + n;
 }
 
 void launch_ds_decode(const Work& w, hipStream_t s) {
   if (w.nupd == 0) return;
+  hipLaunchKernelGGL(k_ds_bound, dim3(w.nupd / 256 + 1), dim3(256), 0, s, w);
+  scan_u32(w.tmp, w.tmp_bytes, w.scratch, w.ds_region, w.nupd + 1, s);
   hipLaunchKernelGGL(k_ds_decode, dim3((w.nupd + 3) / 4), dim3(256), 0, s, w);
+  scan_u32(w.tmp, w.tmp_bytes, w.ds_count, w.ds_dense_off, w.nupd + 1, s);
+  hipLaunchKernelGGL(k_ds_compact, dim3((w.nupd + 3) / 4), dim3(256), 0, s, w);
 }
 
 // --------------------------------------------------------------------------- client table
@@ -491,14 +601,14 @@ void launch_struct_decode(const Work& w, uint32_t nstructs, uint32_t nsections, 
 // --------------------------------------------------------------------------- client states
 __global__ void k_states(Work w, uint32_t nstructs) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  uint32_t items = 0;
-  if (i < nstructs && (w.s_info[i] & 31u) != REF_SKIP) {
-    atomicMax(&w.cl_state[w.s_cidx[i]], w.s_clock[i] + w.s_len[i]);
-    items = w.s_len[i];
+  if (i >= nstructs) return;
+  if ((w.s_info[i] & 31u) == REF_SKIP) {  // rare: Skip lengths are subtracted from the item count
+    atomicAdd(&w.ctr->items, (unsigned long long)w.s_len[i]);
+    return;
   }
-  // wave-level sum, one 64-bit atomic per wave
-  for (int off = 32; off > 0; off >>= 1) items += (uint32_t)__shfl_down((int)items, off);
-  if ((threadIdx.x & 63) == 0 && items) atomicAdd(&w.ctr->items, (unsigned long long)items);
+  // clocks grow along a section: only the last non-skip struct of a run can hold the max
+  const bool last = i + 1 == nstructs || w.s_sec[i + 1] != w.s_sec[i] || (w.s_info[i + 1] & 31u) == REF_SKIP;
+  if (last) atomicMax(&w.cl_state[w.s_cidx[i]], w.s_clock[i] + w.s_len[i]);
 }
 void launch_states(const Work& w, uint32_t nstructs, uint32_t nclients, hipStream_t s) {
   hipMemsetAsync(w.cl_state, 0, sizeof(uint32_t) * (nclients + 1), s);

@@ -126,22 +126,23 @@ __global__ void k_run_flags(Work w, uint32_t nsegs) {
 __global__ void k_run_fill(Work w, uint32_t nsegs) {
   const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
   if (s >= nsegs) return;
-  if (!seg_deleted(w.g_flags[s])) return;
+  const uint32_t f = w.g_flags[s];
+  if (!seg_deleted(f)) return;
   const uint32_t rid = w.g_tmp2[s + 1] - 1;  // inclusive count of run starts up to s
-  const uint32_t units = w.g_start[s + 1] - w.g_start[s];
-  if (w.g_tmp2[s + 1] != w.g_tmp2[s]) {     // s starts run rid
-    w.r_seg[rid] = s;
-    atomicAdd(&ccol(w, CC_NRUNS)[w.g_cidx[s]], 1u);
-  }
-  atomicAdd(&w.r_len[rid], units);
+  if (w.g_tmp2[s + 1] != w.g_tmp2[s]) w.r_seg[rid] = s;  // s starts run rid
+  // s ends run rid: the next segment is live or belongs to another client
+  const bool last = s + 1 == nsegs || w.g_cidx[s + 1] != w.g_cidx[s] || !seg_deleted(w.g_flags[s + 1]);
+  if (last) w.r_len[rid] = w.g_start[s + 1];  // end unit; the start is subtracted in k_run_sizes
 }
 __global__ void k_run_sizes(Work w, uint32_t nruns) {
   const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
   if (r > nruns) return;
   if (r == nruns) { w.r_size[r] = 0; return; }
   const uint32_t s = w.r_seg[r];
+  const uint32_t len = w.r_len[r] - w.g_start[s];
+  w.r_len[r] = len;
   const uint32_t clock = (uint32_t)(w.g_start[s] - w.cl_base[w.g_cidx[s]]);
-  w.r_size[r] = vu_size(clock) + vu_size(w.r_len[r]);
+  w.r_size[r] = vu_size(clock) + vu_size(len);
 }
 
 // per client: struct block + delete-set block + state-vector entry sizes
@@ -178,16 +179,21 @@ __global__ void k_client_sizes(Work w, uint32_t nclients, uint32_t nout, uint32_
   ccol(w, CC_FIRST_INCL)[c] = fi;
   ccol(w, CC_NINCL)[c] = nincl;
   ccol(w, CC_BLK)[c] = blk;
-  // delete-set block
-  const uint32_t nr = ccol(w, CC_NRUNS)[c];
+  // delete-set block: runs are ordered by (client, clock)
+  uint32_t lo = 0, hi = nruns;
+  while (lo < hi) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (w.g_cidx[w.r_seg[mid]] < c) lo = mid + 1; else hi = mid;
+  }
+  uint32_t lo2 = lo, hi2 = nruns;
+  while (lo2 < hi2) {
+    const uint32_t mid = (lo2 + hi2) >> 1;
+    if (w.g_cidx[w.r_seg[mid]] <= c) lo2 = mid + 1; else hi2 = mid;
+  }
+  const uint32_t nr = lo2 - lo;
+  ccol(w, CC_NRUNS)[c] = nr;
   uint32_t dsblk = 0;
   if (nr) {
-    // first run of client c: runs are ordered by (client, clock)
-    uint32_t lo = 0, hi = nruns;
-    while (lo < hi) {
-      const uint32_t mid = (lo + hi) >> 1;
-      if (w.g_cidx[w.r_seg[mid]] < c) lo = mid + 1; else hi = mid;
-    }
     ccol(w, CC_FIRST_RUN)[c] = lo;
     dsblk = vu_size(w.cl_vals[c]) + vu_size(nr) + (w.r_pos[lo + nr] - w.r_pos[lo]);
     atomicAdd(&w.ctr->pad[1], 1u);  // ds clients
@@ -290,7 +296,6 @@ void launch_encode_sizes(const Work& w, uint32_t nsegs, uint32_t nclients, uint3
   hipMemcpyAsync(nruns_host, w.g_tmp2 + nsegs, sizeof(uint32_t), hipMemcpyDeviceToHost, s);
   hipStreamSynchronize(s);
   const uint32_t nruns = *nruns_host;
-  hipMemsetAsync(w.r_len, 0, sizeof(uint32_t) * (nruns + 1), s);
   if (nsegs) hipLaunchKernelGGL(k_run_fill, dim3((nsegs + 255) / 256), dim3(256), 0, s, w, nsegs);
   hipLaunchKernelGGL(k_run_sizes, dim3(nruns / 256 + 1), dim3(256), 0, s, w, nruns);
   scan_u32(w.tmp, w.tmp_bytes, w.r_size, w.r_pos, nruns + 1, s);

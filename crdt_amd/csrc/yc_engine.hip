@@ -87,8 +87,9 @@ bool parse_sv(const uint8_t* p, size_t n, std::unordered_map<uint32_t, uint32_t>
 }
 
 enum Buf {
-  B_BYTES, B_META, B_CTR, B_MAIN, B_FINAL, B_SECB, B_GPRE, B_GEXIT, B_COPY, B_PATCH, B_DSSTART, B_SECT, B_SECSORT,
-  B_WCNT, B_WSEC, B_DS, B_DSLEN, B_DSSCAN, B_SCRATCH, B_TMP,
+  B_BYTES, B_META, B_CTR, B_TNXT, B_TCEXIT, B_TCCNT, B_TBEXIT, B_TBCNT, B_TGEXIT, B_TGCNT, B_FINAL, B_SECB, B_COPY,
+  B_PATCH, B_DSSTART, B_SECT, B_SECSORT,
+  B_WCNT, B_WSEC, B_DS, B_DSTMP, B_DSREG, B_DSCNT, B_DSOFF, B_DSLEN, B_DSSCAN, B_SCRATCH, B_TMP,
   B_SPOS, B_SSEC, B_SLEN, B_SLENSCAN, B_SCLOCK, B_SCIDX, B_SINFO, B_SOC, B_SOK, B_SRC, B_SRK, B_SPA, B_SPB, B_SPS, B_SPL,
   B_SCPOS, B_SCEND, B_SCELEM,
   B_CLVALS, B_CLTMP, B_CLSTATE, B_CLBASE, B_CLSTART, B_CC,
@@ -255,16 +256,20 @@ int run_merge(ycrdt_engine* e, ycrdt_batch* b, const std::unordered_map<uint32_t
   const uint64_t nwords = B / 64 + 2;
   w.cap_structs = (uint32_t)(B / 2 + 64);
   w.cap_sections = (uint32_t)(B / 3 + 64);
-  w.cap_copy = w.ngroups + w.cap_sections + 64;
+  w.cap_copy = w.ngroups + w.cap_structs + 64;  // every segment holds >= 1 struct
   w.cap_patch = w.cap_structs;
   w.cap_ds = (uint32_t)(B / 2 + 64);
   // ---- decode buffers
   w.ctr = take<Counters>(V, B_CTR, 1, ok);
-  w.main_bits = take<uint64_t>(V, B_MAIN, nwords, ok);
+  w.tab.nxt = take<uint16_t>(V, B_TNXT, B, ok);
+  w.tab.cexit = take<uint16_t>(V, B_TCEXIT, B, ok);
+  w.tab.ccnt = take<uint8_t>(V, B_TCCNT, B, ok);
+  w.tab.bexit = take<uint16_t>(V, B_TBEXIT, B, ok);
+  w.tab.bcnt = take<uint16_t>(V, B_TBCNT, B, ok);
+  w.tab.gexit = take<uint16_t>(V, B_TGEXIT, B, ok);
+  w.tab.gcnt = take<uint16_t>(V, B_TGCNT, B, ok);
   w.final_bits = take<uint64_t>(V, B_FINAL, nwords, ok);
   w.sec_bits = take<uint64_t>(V, B_SECB, nwords, ok);
-  w.gpre = take<uint16_t>(V, B_GPRE, (size_t)(w.ngroups + 1) * (GROUP_LANES + 1), ok);
-  w.gexit = take<uint32_t>(V, B_GEXIT, w.ngroups + 1, ok);
   w.copy = take<CopyTask>(V, B_COPY, w.cap_copy, ok);
   w.patch = take<uint32_t>(V, B_PATCH, w.cap_patch, ok);
   w.dsstart = take<uint32_t>(V, B_DSSTART, nu + 1, ok);
@@ -273,6 +278,10 @@ int run_merge(ycrdt_engine* e, ycrdt_batch* b, const std::unordered_map<uint32_t
   w.wcnt = take<uint32_t>(V, B_WCNT, nwords + 1, ok);
   w.wsec = take<uint32_t>(V, B_WSEC, nwords + 1, ok);
   w.ds = take<DsRange>(V, B_DS, w.cap_ds, ok);
+  w.ds_tmp = take<DsRange>(V, B_DSTMP, w.cap_ds, ok);
+  w.ds_region = take<uint32_t>(V, B_DSREG, nu + 2, ok);
+  w.ds_count = take<uint32_t>(V, B_DSCNT, nu + 2, ok);
+  w.ds_dense_off = take<uint32_t>(V, B_DSOFF, nu + 2, ok);
   w.ds_len = take<uint32_t>(V, B_DSLEN, w.cap_ds + 1, ok);
   w.ds_scan = take<uint64_t>(V, B_DSSCAN, w.cap_ds + 1, ok);
   w.s_pos = take<uint32_t>(V, B_SPOS, w.cap_structs, ok);
@@ -299,7 +308,7 @@ int run_merge(ycrdt_engine* e, ycrdt_batch* b, const std::unordered_map<uint32_t
   w.cl_state = take<uint32_t>(V, B_CLSTATE, w.cap_clients + 1, ok);
   w.cl_base = take<uint64_t>(V, B_CLBASE, w.cap_clients + 2, ok);
   w.cl_start = take<uint32_t>(V, B_CLSTART, w.cap_clients + 1, ok);
-  w.scratch = take<uint32_t>(V, B_SCRATCH, std::max<uint64_t>(nwords + 2, w.cap_sections + 2), ok);
+  w.scratch = take<uint32_t>(V, B_SCRATCH, std::max<uint64_t>({nwords + 2, (uint64_t)w.cap_sections + 2, (uint64_t)nu + 2}), ok);
   if (!ok) return fail(YCRDT_E_DEVICE, "hipMalloc failed (decode workspace)");
   // rocPRIM scratch sized for the largest scan of this batch (units may grow it later)
   {
@@ -312,16 +321,16 @@ int run_merge(ycrdt_engine* e, ycrdt_batch* b, const std::unordered_map<uint32_t
   HIPCHK(hipMemsetAsync(w.final_bits, 0, nwords * 8, s));
   HIPCHK(hipMemsetAsync(w.sec_bits, 0, nwords * 8, s));
   // ---- K1 decode
-  mark(e, "decode.group_parse");
+  mark(e, "decode.tables");
   launch_group_parse(w, s);
   mark(e, "decode.walker");
   launch_walker(w, s);
-  mark(e, "decode.bitmap");
-  launch_build_final_bits(w, s);
-  launch_struct_positions(w, s);
   Counters c;
   int rc = check(e, c, "decode");
   if (rc) return rc;
+  mark(e, "decode.bitmap");
+  launch_build_final_bits(w, std::min(c.ncopy, w.cap_copy), std::min(c.npatch, w.cap_patch), s);
+  launch_struct_positions(w, s);
   uint32_t nstructs = 0;
   HIPCHK(hipMemcpyAsync(&nstructs, w.wcnt + (w.nbytes + 63) / 64, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
   HIPCHK(hipStreamSynchronize(s));
@@ -443,7 +452,11 @@ int run_merge(ycrdt_engine* e, ycrdt_batch* b, const std::unordered_map<uint32_t
   hipEventElapsedTime(&ms, e->ev0, e->ev1);
   ycrdt_merge_stats& st = e->last;
   st.in_bytes = b->in_bytes;
-  st.items = c.items;
+  {
+    uint64_t total_len = 0;
+    hipMemcpy(&total_len, w.s_lenscan + nstructs, sizeof(uint64_t), hipMemcpyDeviceToHost);
+    st.items = nstructs ? total_len - c.items : 0;  // Item + GC clock lengths (Skip excluded)
+  }
   st.structs = nstructs;
   st.units = U;
   st.segments = nsegs;

@@ -82,7 +82,8 @@ __global__ __launch_bounds__(256) void k_ds_mark(Work w, uint32_t nds, uint64_t 
     const uint64_t send = min(jend, P[s + 1]);
     const DsRange r = w.ds[s];
     const uint64_t gb = w.cl_base[r.client] + r.clock - P[s];
-    for (; j < send; ++j) atomicOr(&w.u_flags[(uint32_t)(gb + j)], UF_DS);
+    // only UF_DS is written in this kernel: concurrent plain ORs of the same bit are harmless
+    for (; j < send; ++j) w.u_flags[(uint32_t)(gb + j)] |= UF_DS;
   }
 }
 
@@ -95,14 +96,18 @@ __global__ void k_refs(Work w, uint32_t nstructs) {
     const uint32_t k = w.s_oclock[i];
     if (k >= w.cl_state[oc]) { raise_err(&w.ctr->err, ERR_PENDING); return; }
     const uint32_t g = (uint32_t)(w.cl_base[oc] + k);
-    atomicMin(&w.u_minchild[g], w.s_cidx[i]);
-    if (k + 1 < w.cl_state[oc]) atomicOr(&w.u_flags[g + 1], UF_CUT);  // getItemCleanEnd(origin)
+    const uint32_t ci = w.s_cidx[i];
+    if (w.u_minchild[g] > ci) atomicMin(&w.u_minchild[g], ci);  // read first: hot origins are shared
+    // getItemCleanEnd(origin); only UF_CUT is written to u_flags in this kernel, so a plain
+    // read-modify-write that races with another writer of the same bit is harmless
+    if (k + 1 < w.cl_state[oc] && !(w.u_flags[g + 1] & UF_CUT)) w.u_flags[g + 1] |= UF_CUT;
   }
   const uint32_t rc = w.s_rcidx[i];
   if (rc != NONE) {
     const uint32_t k = w.s_rclock[i];
     if (k >= w.cl_state[rc]) { raise_err(&w.ctr->err, ERR_PENDING); return; }
-    atomicOr(&w.u_flags[(uint32_t)(w.cl_base[rc] + k)], UF_CUT);       // getItemCleanStart(rightOrigin)
+    const uint32_t g = (uint32_t)(w.cl_base[rc] + k);
+    if (!(w.u_flags[g] & UF_CUT)) w.u_flags[g] |= UF_CUT;              // getItemCleanStart(rightOrigin)
   }
 }
 
@@ -298,9 +303,11 @@ __global__ __launch_bounds__(256) void k_children(Work w, uint32_t nsegs) {
   const unsigned long long v = ((unsigned long long)(w.g_cidx[s] + 1) << 32) | s;
   const uint32_t o = w.g_origin[s];
   if (o != NONE) {
-    atomicMax((unsigned long long*)&w.g_maxchild[seg_of(w.u_cutbits, w.u_wpre, o)], v);
+    unsigned long long* dst = (unsigned long long*)&w.g_maxchild[seg_of(w.u_cutbits, w.u_wpre, o)];
+    if (*dst < v) atomicMax(dst, v);  // read first: the base entries of hot keys have ~1k children
   } else if (f & SEG_ROOT) {
-    atomicMax((unsigned long long*)&w.k_rootmax[key], v);
+    unsigned long long* dst = (unsigned long long*)&w.k_rootmax[key];
+    if (*dst < v) atomicMax(dst, v);
   }
 }
 __global__ void k_next_init(Work w, uint32_t nsegs) {

@@ -28,7 +28,7 @@ struct Counters {            // device-side counters, read back at the few host 
   uint32_t nkeys;            // distinct map keys
   uint32_t nruns;            // delete-set runs in the output
   uint32_t pad[14];          // encode scratch (see yc_encode.hip)
-  unsigned long long items;  // Σ clock lengths of Item + GC input structs (the throughput unit)
+  unsigned long long items;  // Σ clock lengths of Skip structs (items = Σ all lengths − this)
 };
 
 struct DsRange {             // one decoded (client, clock, len) delete-set range
@@ -36,6 +36,18 @@ struct DsRange {             // one decoded (client, clock, len) delete-set rang
   uint32_t clock;
   uint32_t len;
   uint32_t upd;
+};
+
+// Per-byte chain tables (written by k_tables, read by the walker and k_mark). Exits are forward
+// deltas from the position; STOPF marks a chain that stops at a struct the tables did not size.
+struct Tables {
+  uint16_t* nxt = nullptr;         // struct length starting here (0 = no struct, 1 = unsized)
+  uint16_t* cexit = nullptr;       // first chain position at/after the end of this 64-byte chunk
+  uint8_t* ccnt = nullptr;         // chain positions visited before it
+  uint16_t* bexit = nullptr;       // ... 1 KiB block
+  uint16_t* bcnt = nullptr;
+  uint16_t* gexit = nullptr;       // ... 16 KiB group
+  uint16_t* gcnt = nullptr;
 };
 
 struct Work {
@@ -53,19 +65,21 @@ struct Work {
   uint64_t cap_units = 0;
   // ---- decode
   Counters* ctr = nullptr;
-  uint64_t* main_bits = nullptr;   // [B/64] speculative main-chain struct starts
+  Tables tab;                      // per-byte chain tables [B]
   uint64_t* final_bits = nullptr;  // [B/64] verified struct starts
   uint64_t* sec_bits = nullptr;    // [B/64] first struct of every non-empty section
-  uint16_t* gpre = nullptr;        // [G*257] per-group prefix counts of main bits per chunk
-  uint32_t* gexit = nullptr;       // [G] first main-chain position >= group end
-  CopyTask* copy = nullptr;        // [cap_copy]
+  CopyTask* copy = nullptr;        // [cap_copy] verified chain segments (start, count)
   uint32_t* patch = nullptr;       // [cap_patch]
   uint32_t* dsstart = nullptr;     // [nupd] byte position of the delete set
   Section* sections = nullptr;     // [cap_sections] (walker order)
   uint32_t* sec_sorted = nullptr;  // [cap_sections] section index by position rank
   uint32_t* wcnt = nullptr;        // [B/64 + 1] popcount prefix of final_bits words
   uint32_t* wsec = nullptr;        // [B/64 + 1] popcount prefix of sec_bits words
-  DsRange* ds = nullptr;           // [cap_ds]
+  DsRange* ds = nullptr;           // [cap_ds] dense delete-set ranges
+  DsRange* ds_tmp = nullptr;       // [cap_ds] per-update regions (decode output)
+  uint32_t* ds_region = nullptr;   // [nupd+1] region offsets (scan of (ds bytes + 1) / 2)
+  uint32_t* ds_count = nullptr;    // [nupd+1] ranges decoded per update
+  uint32_t* ds_dense_off = nullptr;// [nupd+1] scan of ds_count
   uint32_t* ds_len = nullptr;      // [cap_ds+1] clipped lengths (scan input)
   uint64_t* ds_scan = nullptr;     // [cap_ds+1]
   uint32_t* dsclient_vals = nullptr; // [cap_dsclients] (client values seen in delete sets)
@@ -165,7 +179,7 @@ enum : uint32_t {
 // ---- launch entry points (yc_decode.hip / yc_merge.hip / yc_encode.hip / yc_prims.hip)
 void launch_group_parse(const Work& w, hipStream_t s);
 void launch_walker(const Work& w, hipStream_t s);
-void launch_build_final_bits(const Work& w, hipStream_t s);
+void launch_build_final_bits(const Work& w, uint32_t nseg, uint32_t npatch, hipStream_t s);
 void launch_struct_positions(const Work& w, hipStream_t s);
 void launch_ds_decode(const Work& w, hipStream_t s);
 void launch_section_clients(const Work& w, uint32_t nsections, hipStream_t s);

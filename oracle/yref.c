@@ -889,6 +889,15 @@ static void utf16_to_utf8(buf_t *b, const uint16_t *u, uint32_t n) {
   }
 }
 
+/* JSON.parse(readString()) of ContentJSON / ContentEmbed / ContentFormat values throws in Yjs on
+ * text that cannot start a JSON value (and on the empty string): treat as a decode error. */
+static int json_start_ok(const uint8_t *p, uint32_t k) {
+  if (k == 0) return 0;
+  uint8_t c = p[0];
+  return c == '{' || c == '[' || c == '"' || c == 't' || c == 'f' || c == 'n' || c == 'u' || c == '-' ||
+         (c >= '0' && c <= '9') || c == ' ' || c == '\t' || c == '\n' || c == '\r';
+}
+
 /* readItemContent (hi / ai table) */
 static int read_content(yo_doc *doc, dec_t *d, uint8_t info, ycontent *c) {
   memset(c, 0, sizeof *c);
@@ -901,7 +910,8 @@ static int read_content(yo_doc *doc, dec_t *d, uint8_t info, ycontent *c) {
       for (uint32_t i = 0; i < n && !d->err; i++) {
         st = d->pos;
         uint32_t k = dvu(d);
-        dbytes(d, k);
+        const uint8_t *js = dbytes(d, k);
+        if (!d->err && !json_start_ok(js, k)) d->err = 1;
         if (!d->err) el_push(c, ystr_dup(d->p + st, (uint32_t)(d->pos - st)));
       }
       break;
@@ -909,7 +919,8 @@ static int read_content(yo_doc *doc, dec_t *d, uint8_t info, ycontent *c) {
     case CT_BINARY: case CT_EMBED: {
       st = d->pos;
       uint32_t k = dvu(d);
-      dbytes(d, k);
+      const uint8_t *js = dbytes(d, k);
+      if (!d->err && c->ref == CT_EMBED && !json_start_ok(js, k)) d->err = 1;
       if (!d->err) c->raw = ystr_dup(d->p + st, (uint32_t)(d->pos - st));
       break;
     }
@@ -928,7 +939,8 @@ static int read_content(yo_doc *doc, dec_t *d, uint8_t info, ycontent *c) {
       uint32_t k = dvu(d);
       dbytes(d, k);
       k = dvu(d);
-      dbytes(d, k);
+      const uint8_t *js = dbytes(d, k);
+      if (!d->err && !json_start_ok(js, k)) d->err = 1;
       if (!d->err) c->raw = ystr_dup(d->p + st, (uint32_t)(d->pos - st));
       break;
     }

@@ -116,7 +116,7 @@ def test_gpu_c2_full_properties():
     b = crdt_amd.Batch(ups)
     st = b.merge()
     state, sv = b.result()
-    assert st.items == 900_000 - 0 or st.items > 0
+    assert st.items > 800_000
     # idempotence: the canonical state merged alone reproduces itself
     d = crdt_amd.Doc(client_id=0x7FFFFFF0)
     d.apply_update(state)
