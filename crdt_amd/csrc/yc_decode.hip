@@ -29,8 +29,6 @@ constexpr uint32_t HALO = 4096;                 // bytes staged past the group e
 constexpr uint32_t BLOCK = 1024;                // 16 chunks
 constexpr uint32_t LDS_NXT = 0, LDS_CEXIT = 32768, LDS_CCNT = 65536, LDS_BEXIT = 81920, LDS_BCNT = 114688;
 constexpr uint32_t LDS_TOTAL = 147456;
-// the pass-2 queue (<= 16K u16 offsets) lives in the cexit region, unused until phase B
-__device__ __forceinline__ uint16_t* ccnt16_alias(uint8_t* lds) { return (uint16_t*)(lds + LDS_CEXIT); }
 static_assert(GROUP_BYTES == 16384, "table layout assumes 16 KiB groups");
 
 __global__ __launch_bounds__(TL) void k_tables(const uint8_t* __restrict__ b, const Group* __restrict__ groups, Tables t) {
@@ -52,14 +50,52 @@ __global__ __launch_bounds__(TL) void k_tables(const uint8_t* __restrict__ b, co
   // stage (16-byte vector loads; the batch buffer is padded)
   for (uint32_t i = tid * 16; i < slen; i += TL * 16) *(uint4*)(sb + i) = *(const uint4*)(b + G.start + i);
   __syncthreads();
-  // phase A: speculative parse at every byte position. Pass 1 uses a tiny work cap; positions that
-  // need more work are queued in LDS and re-parsed densely in pass 2, so one slow lane does not
-  // stall its whole wavefront.
+  // phase A: speculative parse at every byte position.
+  //  A0: classify each position by its would-be info byte: non-structs (content ref > 10) and
+  //      GC / Skip (info + one varuint) are resolved on the spot;
+  //  A1: counting-sort the other candidates by (content ref, origin/rightOrigin/parentSub bits) so
+  //      the lanes of a wavefront take the same path through the (branch-heavy) parser;
+  //  A2: parse in sorted order under a tiny work cap, queueing the few that need more;
+  //  A3: re-parse the queued positions densely.
+  constexpr uint32_t NB = 72;  // content refs 1..9 x info>>5
+  __shared__ uint32_t bstart[NB + 1], bcursor[NB];
   __shared__ uint32_t qn;
-  uint16_t* queue = ccnt16_alias(lds);
+  uint16_t* sorted = (uint16_t*)(lds + LDS_CEXIT);  // cexit/ccnt are unused until phase B
+  uint16_t* queue = (uint16_t*)(lds + LDS_BCNT);    // staged bytes end below LDS_BCNT
+  static_assert(LDS_BEXIT + GROUP_BYTES + HALO <= LDS_BCNT, "staged window overlaps the queue");
+  for (uint32_t i = tid; i < NB; i += TL) bcursor[i] = 0;
   if (tid == 0) qn = 0;
   __syncthreads();
   for (uint32_t o = tid; o < glen; o += TL) {
+    const uint32_t info = sb[o];
+    const uint32_t ref = info & 31u;
+    uint16_t d = 0;
+    if (ref == REF_GC || ref == REF_SKIP) {
+      uint32_t q = o + 1;
+      bool okv = true;
+      rd_vu(sb, q, slen, okv);
+      d = okv ? (uint16_t)(q - o) : (window_cut && q >= slen ? (uint16_t)1 : (uint16_t)0);
+    } else if (ref <= REF_DOC) {
+      atomicAdd(&bcursor[(ref - 1) * 8 + (info >> 5)], 1u);
+    }
+    nxt[o] = d;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    uint32_t acc = 0;
+    for (uint32_t i = 0; i < NB; ++i) { const uint32_t c = bcursor[i]; bstart[i] = acc; bcursor[i] = acc; acc += c; }
+    bstart[NB] = acc;
+  }
+  __syncthreads();
+  for (uint32_t o = tid; o < glen; o += TL) {
+    const uint32_t info = sb[o];
+    const uint32_t ref = info & 31u;
+    if (ref >= 1 && ref <= REF_DOC) sorted[atomicAdd(&bcursor[(ref - 1) * 8 + (info >> 5)], 1u)] = (uint16_t)o;
+  }
+  __syncthreads();
+  const uint32_t ncand = bstart[NB];
+  for (uint32_t i = tid; i < ncand; i += TL) {
+    const uint32_t o = sorted[i];
     uint32_t q = o;
     const int r = parse_struct<false, 4>(sb, q, slen, SPEC_STEPS_FAST, nullptr);
     uint16_t d;
@@ -78,19 +114,36 @@ __global__ __launch_bounds__(TL) void k_tables(const uint8_t* __restrict__ b, co
     nxt[o] = r > 0 ? (uint16_t)(q - o) : ((r == -1 || (r == -2 && window_cut)) ? (uint16_t)1 : (uint16_t)0);
   }
   __syncthreads();
-  // phase B: chunk level (one lane per chunk, backward over its 64 positions)
-  const uint32_t nchunks = (glen + CHUNK - 1) / CHUNK;
-  for (uint32_t c = tid; c < nchunks; c += TL) {
-    const uint32_t cs = c * CHUNK, ce = min(cs + CHUNK, glen);
-    for (int o = (int)ce - 1; o >= (int)cs; --o) {
+  // phase B: chunk level by pointer doubling over all positions (6 rounds cover a 64-byte chunk),
+  // double-buffered through the block-array region (free again once the bytes are parsed); reads
+  // are mostly unit-stride across a wavefront, unlike a lane-per-chunk backward sweep.
+  {
+    uint16_t* e0 = cexit;
+    uint8_t* c0 = ccnt;
+    uint16_t* e1 = bexit;
+    uint8_t* c1 = (uint8_t*)bcnt;
+    for (uint32_t o = tid; o < glen; o += TL) {
       const uint32_t d = nxt[o];
-      if (d == 1) { cexit[o] = (uint16_t)(o | STOPF); ccnt[o] = 0; continue; }
-      const uint32_t sx = d == 0 ? o + 1 : o + d;
-      if (sx >= ce) { cexit[o] = (uint16_t)sx; ccnt[o] = 1; }
-      else { cexit[o] = cexit[sx]; ccnt[o] = (uint8_t)(1 + ccnt[sx]); }
+      if (d == 1) { e0[o] = (uint16_t)(o | STOPF); c0[o] = 0; }
+      else { e0[o] = (uint16_t)(d == 0 ? o + 1 : o + d); c0[o] = 1; }
     }
+    __syncthreads();
+#pragma unroll 1
+    for (int round = 0; round < 6; ++round) {
+      for (uint32_t o = tid; o < glen; o += TL) {
+        const uint32_t ce = min((o | (CHUNK - 1)) + 1, glen);
+        const uint32_t x = e0[o];
+        uint32_t ex = x, cx = c0[o];
+        if (!(x & STOPF) && x < ce) { ex = e0[x]; cx += c0[x]; }
+        e1[o] = (uint16_t)ex;
+        c1[o] = (uint8_t)cx;
+      }
+      __syncthreads();
+      uint16_t* te = e0; e0 = e1; e1 = te;
+      uint8_t* tc = c0; c0 = c1; c1 = tc;
+    }
+    static_assert(6 % 2 == 0, "an even number of rounds leaves the result in cexit/ccnt");
   }
-  __syncthreads();
   // exits are stored as forward deltas from the position itself (|STOPF when the chain stops at a
   // struct the tables could not size), so consumers never need the group origin
   for (uint32_t o = tid; o < glen; o += TL) {
