@@ -615,8 +615,17 @@ __global__ __launch_bounds__(256) void k_struct_decode(Work w, uint32_t nstructs
   w.s_oclock[i] = v.ok_;
   w.s_rcidx[i] = rc;
   w.s_rclock[i] = v.rk;
-  w.s_pa[i] = (item && v.pkind == 1) ? v.pa : NONE;
-  w.s_pb[i] = v.pb;
+  // parent: root type name (varString position/length) or parent item id (client index, clock)
+  uint32_t pk = item ? v.pkind : 0u, pa = NONE, pb = 0;
+  if (pk == 1) { pa = v.pa; pb = v.pb; }
+  else if (pk == 2) {
+    pa = find_cidx(w.cl_vals, nclients, v.pa);
+    pb = v.pb;
+    if (pa == NONE) { raise_err(err, ERR_PENDING); w.ctr->err_info = i; }
+  }
+  w.s_pk[i] = (uint8_t)pk;
+  w.s_pa[i] = pa;
+  w.s_pb[i] = pb;
   w.s_psub[i] = (item && v.has_psub) ? v.psub_pos : NONE;
   w.s_psublen[i] = v.psub_len;
   w.s_cpos[i] = v.cpos;
@@ -624,12 +633,6 @@ __global__ __launch_bounds__(256) void k_struct_decode(Work w, uint32_t nstructs
   uint32_t celem = v.cpos;
   if (v.ref == REF_ANY || v.ref == REF_JSON) celem += vu_size(v.nel);
   w.s_celem[i] = celem;
-  // coverage of the engine (round 1): root-level YMap entries
-  if (v.ref == REF_GC || v.ref == REF_STRING || v.ref == REF_EMBED || v.ref == REF_FORMAT || v.ref == REF_TYPE)
-    raise_err(err, ERR_UNSUPPORTED);
-  if (item && ((v.info & 0x40u) || v.pkind == 2)) raise_err(err, ERR_UNSUPPORTED);
-  if (item && v.pkind == 1 && !v.has_psub) raise_err(err, ERR_UNSUPPORTED);  // root YArray item
-  if (v.ref == REF_ANY && v.len > 1) raise_err(err, ERR_UNSUPPORTED);          // live map items are single values
 }
 
 __global__ void k_struct_clock(Work w, uint32_t nstructs) {

@@ -25,7 +25,58 @@ __device__ __forceinline__ uint32_t copy_bytes(uint8_t* __restrict__ o, uint32_t
   return p + n;
 }
 
-// Encodes output struct `o` (segments [a,b)) at position p when WRITE, returns the size.
+// Byte range of content elements [e0, e1) of struct `src` (ContentAny: lib0 `any` values,
+// ContentJSON: varStrings, ContentString: UTF-16 code units of the UTF-8 text; every other
+// content has length 1 and is copied whole). This is ContentX.splice (Y@70000..) as a byte slice.
+__device__ bool content_slice(const Work& w, uint32_t src, uint32_t e0, uint32_t e1, uint32_t& b0, uint32_t& b1) {
+  const uint32_t ref = w.s_info[src] & 31u;
+  const uint8_t* __restrict__ by = w.bytes;
+  const uint32_t end = w.s_cend[src];
+  if (ref == REF_ANY || ref == REF_JSON) {
+    uint32_t p = w.s_celem[src];
+    bool ok = true;
+    for (uint32_t i = 0; i < e1; ++i) {
+      if (i == e0) b0 = p;
+      if (ref == REF_ANY) {
+        uint32_t steps = 0xFFFFFFFFu;
+        ok = skip_any<32>(by, p, end, steps);
+      } else {
+        const uint32_t k = rd_vu(by, p, end, ok);
+        if (ok) skip_bytes(p, k, end, ok);
+      }
+      if (!ok) return false;
+    }
+    if (e0 == e1) b0 = p;
+    b1 = p;
+    return true;
+  }
+  if (ref == REF_STRING) {
+    uint32_t p = w.s_cpos[src];
+    bool ok = true;
+    rd_vu(by, p, end, ok);  // byte length prefix
+    if (!ok) return false;
+    uint32_t u = 0;  // UTF-16 units before p
+    b0 = e0 == 0 ? p : NONE;
+    while (p < end && u < e1) {
+      const uint32_t c = by[p];
+      const uint32_t n = c < 0x80u ? 1u : c < 0xE0u ? 2u : c < 0xF0u ? 3u : 4u;
+      const uint32_t du = n == 4 ? 2u : 1u;
+      if (u < e0 && u + du > e0) return false;  // a slice through a surrogate pair
+      if (u < e1 && u + du > e1) return false;
+      p += n;
+      u += du;
+      if (u == e0) b0 = p;
+    }
+    b1 = p;
+    return b0 != NONE && u == e1;
+  }
+  b0 = w.s_cpos[src];
+  b1 = end;
+  return true;
+}
+
+// Encodes output struct `o` (segments [a,b)) at position p when WRITE, returns the size
+// (Item.write Y@80416 / GC.write Y@68955 with the writeStructs offset, Y@18809).
 template <bool WRITE>
 __device__ uint32_t encode_struct(const Work& w, uint32_t nclients, uint32_t o, uint8_t* __restrict__ out, uint32_t p0) {
   const uint32_t a = w.o_first[o], b = w.o_first[o + 1];
@@ -64,7 +115,8 @@ __device__ uint32_t encode_struct(const Work& w, uint32_t nclients, uint32_t o, 
     rclient = w.cl_vals[c];
     rclock = (uint32_t)(g - w.cl_base[c]);
   }
-  const uint32_t info = ref | (has_o ? 0x80u : 0u) | (has_r ? 0x40u : 0u) | 0x20u;  // round 1: every item is a map entry
+  const bool psub = (f & SEG_PSUB) != 0;
+  const uint32_t info = ref | (has_o ? 0x80u : 0u) | (has_r ? 0x40u : 0u) | (psub ? 0x20u : 0u);
   uint32_t size = 1;
   if (WRITE) out[p++] = (uint8_t)info;
   if (has_o) {
@@ -75,29 +127,43 @@ __device__ uint32_t encode_struct(const Work& w, uint32_t nclients, uint32_t o, 
     if (WRITE) { p = wr_vu(out, p, rclient); p = wr_vu(out, p, rclock); }
     size += vu_size(rclient) + vu_size(rclock);
   }
-  if (!has_o && !has_r) {  // parent info (root type name) + parentSub
+  if (!has_o && !has_r) {  // parent info (root type name | parent item id) + parentSub
     const uint32_t pa = w.s_pa[src], pb = w.s_pb[src];
-    const uint32_t ps = w.s_psub[src], pl = w.s_psublen[src];
-    if (WRITE) {
-      out[p++] = 1;
-      p = copy_bytes(out, p, w.bytes + pa, pb);
-      p = copy_bytes(out, p, w.bytes + ps, pl);
+    if (w.s_pk[src] == 1) {
+      if (WRITE) { out[p++] = 1; p = copy_bytes(out, p, w.bytes + pa, pb); }
+      size += 1 + pb;
+    } else {
+      const uint32_t pc = w.cl_vals[pa];
+      if (WRITE) { out[p++] = 0; p = wr_vu(out, p, pc); p = wr_vu(out, p, pb); }
+      size += 1 + vu_size(pc) + vu_size(pb);
     }
-    size += 1 + pb + pl;
+    if (psub) {
+      const uint32_t ps = w.s_psub[src], pl = w.s_psublen[src];
+      if (WRITE) p = copy_bytes(out, p, w.bytes + ps, pl);
+      size += pl;
+    }
   }
   if (del) {
     if (WRITE) p = wr_vu(out, p, len - off);
     size += vu_size(len - off);
-  } else if (ref == REF_ANY || ref == REF_JSON) {
-    if (WRITE) p = wr_vu(out, p, len - off);
-    size += vu_size(len - off);
-    for (uint32_t s = a; s < b; ++s) {  // every live segment covers its whole (single-value) source
-      const uint32_t sr = w.g_src[s];
-      const uint32_t n = w.s_cend[sr] - w.s_celem[sr];
-      if (WRITE) p = copy_bytes(out, p, w.bytes + w.s_celem[sr], n);
-      size += n;
+  } else if (ref == REF_ANY || ref == REF_JSON || ref == REF_STRING) {
+    // elements of every segment from unit k0 + off on, sliced out of their source structs
+    uint32_t nbytes = 0;
+    for (uint32_t pass = 0; pass < (WRITE ? 2u : 1u); ++pass) {
+      if (pass == 1) p = wr_vu(out, p, ref == REF_STRING ? nbytes : len - off);
+      for (uint32_t s = a; s < b; ++s) {
+        const uint32_t sr = w.g_src[s];
+        const uint32_t sb = w.s_clock[sr];  // source struct's first clock
+        const uint32_t u0 = max((uint32_t)(w.g_start[s] - base), k0 + off), u1 = (uint32_t)(w.g_start[s + 1] - base);
+        if (u1 <= u0) continue;
+        uint32_t b0 = 0, b1 = 0;
+        if (!content_slice(w, sr, u0 - sb, u1 - sb, b0, b1)) { raise_err(&w.ctr->err, ERR_UNSUPPORTED); return size; }
+        if (pass == 1) p = copy_bytes(out, p, w.bytes + b0, b1 - b0);
+        else nbytes += b1 - b0;
+      }
     }
-  } else {  // Binary / Doc: one unit, verbatim content bytes
+    size += (ref == REF_STRING ? vu_size(nbytes) : vu_size(len - off)) + nbytes;
+  } else {  // Binary / Embed / Format / Type / Doc: one unit, verbatim content bytes
     const uint32_t n = w.s_cend[src] - w.s_cpos[src];
     if (WRITE) p = copy_bytes(out, p, w.bytes + w.s_cpos[src], n);
     size += n;

@@ -95,7 +95,8 @@ enum Buf {
   B_CLVALS, B_CLTMP, B_CLSTATE, B_CLBASE, B_CLSTART, B_CC,
   B_UOWN, B_UFLAG, B_UMIN, B_UCUT, B_UWPRE,
   B_GSTART, B_GCIDX, B_GSRC, B_GFLAGS, B_GORIG, B_GRORIG, B_GLINK, B_GKEY, B_GMAXC, B_GNEXT, B_GOUTID, B_GTMP, B_GTMP2,
-  B_KHASH, B_KROOT, B_KWIN,
+  B_KHASH, B_KROOT, B_KWIN, B_KPAR, B_KFLAG, B_SPK,
+  B_GRIGHT, B_YKEY, B_YKEYS, B_YSEG, B_YIOTA, B_YLSTART, B_YSTATE, B_YBEFORE, B_YCONFL, B_YSTACK,
   B_OFIRST, B_OCIDX, B_OSIZE, B_OPOS, B_RSEG, B_RLEN, B_RSIZE, B_RPOS, B_OUT, B_SVOUT,
   B_COUNT
 };
@@ -295,6 +296,7 @@ int run_merge(ycrdt_engine* e, ycrdt_batch* b, const std::unordered_map<uint32_t
   w.s_oclock = take<uint32_t>(V, B_SOK, w.cap_structs, ok);
   w.s_rcidx = take<uint32_t>(V, B_SRC, w.cap_structs, ok);
   w.s_rclock = take<uint32_t>(V, B_SRK, w.cap_structs, ok);
+  w.s_pk = take<uint8_t>(V, B_SPK, w.cap_structs, ok);
   w.s_pa = take<uint32_t>(V, B_SPA, w.cap_structs, ok);
   w.s_pb = take<uint32_t>(V, B_SPB, w.cap_structs, ok);
   w.s_psub = take<uint32_t>(V, B_SPS, w.cap_structs, ok);
@@ -384,6 +386,16 @@ int run_merge(ycrdt_engine* e, ycrdt_batch* b, const std::unordered_map<uint32_t
   w.g_outid = take<uint32_t>(V, B_GOUTID, U + 2, ok);
   w.g_tmp = take<uint32_t>(V, B_GTMP, U + 2, ok);
   w.g_tmp2 = take<uint32_t>(V, B_GTMP2, U + 2, ok);
+  w.g_right = take<uint32_t>(V, B_GRIGHT, U + 2, ok);
+  w.y_key = take<uint32_t>(V, B_YKEY, U + 2, ok);
+  w.y_keys = take<uint32_t>(V, B_YKEYS, U + 2, ok);
+  w.y_seg = take<uint32_t>(V, B_YSEG, U + 2, ok);
+  w.y_iota = take<uint32_t>(V, B_YIOTA, U + 2, ok);
+  w.y_lstart = take<uint32_t>(V, B_YLSTART, U + 2, ok);
+  w.y_state = take<uint32_t>(V, B_YSTATE, U + 2, ok);
+  w.y_before = take<uint32_t>(V, B_YBEFORE, U + 2, ok);
+  w.y_confl = take<uint32_t>(V, B_YCONFL, U + 2, ok);
+  w.y_stack = take<uint32_t>(V, B_YSTACK, U + 2, ok);
   w.o_first = take<uint32_t>(V, B_OFIRST, U + 2, ok);
   w.o_cidx = take<uint32_t>(V, B_OCIDX, U + 2, ok);
   w.o_size = take<uint32_t>(V, B_OSIZE, U + 2, ok);
@@ -415,6 +427,8 @@ int run_merge(ycrdt_engine* e, ycrdt_batch* b, const std::unordered_map<uint32_t
   w.k_hash = take<uint64_t>(V, B_KHASH, w.cap_keys, ok);
   w.k_rootmax = take<uint64_t>(V, B_KROOT, w.cap_keys, ok);
   w.k_winner = take<uint32_t>(V, B_KWIN, w.cap_keys, ok);
+  w.k_parent = take<uint32_t>(V, B_KPAR, w.cap_keys, ok);
+  w.k_flags = take<uint32_t>(V, B_KFLAG, w.cap_keys, ok);
   if (!ok) return fail(YCRDT_E_DEVICE, "hipMalloc failed (key table)");
   uint32_t nout = 0;
   if (nsegs) {
@@ -425,6 +439,10 @@ int run_merge(ycrdt_engine* e, ycrdt_batch* b, const std::unordered_map<uint32_t
     mark(e, "merge.winner");
     launch_map_winner(w, nsegs, s);
     run_descent(w, nsegs, s);
+    mark(e, "merge.dead_types");
+    run_dead_keys(w, nsegs, s);
+    mark(e, "merge.yata");
+    launch_yata(w, nsegs, s);
     mark(e, "merge.merge_flags");
     launch_merge_flags(w, nsegs, s);
     rc = check(e, c, "merge");

@@ -213,6 +213,16 @@ __device__ __forceinline__ uint32_t key_insert(uint64_t* __restrict__ tab, uint3
   return NONE;
 }
 
+__device__ __forceinline__ uint64_t fnv_u32(uint64_t h, uint32_t v) {
+  for (int i = 0; i < 4; ++i) { h ^= (v >> (8 * i)) & 0xFFu; h *= 1099511628211ull; }
+  return h;
+}
+
+// Per segment: item vs GC, origin / right origin units, parent list. A root segment (no origin,
+// no right origin) names its list: root type name or parent type item, plus the parentSub for
+// YMap entries; every other item inherits the list from its origin (else right origin) by
+// pointer jumping (Item.getMissing, Y@76507). An item whose origin / right origin is GC, or
+// whose parent item is GC, is integrated as GC (getMissing sets parent = null).
 __global__ __launch_bounds__(256) void k_seg_props(Work w, uint32_t nsegs) {
   const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
   if (s >= nsegs) return;
@@ -224,36 +234,58 @@ __global__ __launch_bounds__(256) void k_seg_props(Work w, uint32_t nsegs) {
   const uint32_t ref = w.s_info[own] & 31u;
   uint32_t sf = 0;
   if (f & (UF_DEL | UF_DS)) sf |= SEG_DEL;
-  if (f & UF_GC) sf |= SEG_GC;
-  if (ref != REF_GC) sf |= SEG_ITEM;
+  bool gc = (f & UF_GC) || ref == REF_GC;
   const bool expl = k0 == w.s_clock[own];
   if (expl) sf |= SEG_EXPLICIT;
   uint32_t origin = NONE, rorigin = NONE;
-  if (expl) {
-    if (w.s_ocidx[own] != NONE) origin = (uint32_t)(w.cl_base[w.s_ocidx[own]] + w.s_oclock[own]);
-  } else origin = g0 - 1;
-  if (w.s_rcidx[own] != NONE) rorigin = (uint32_t)(w.cl_base[w.s_rcidx[own]] + w.s_rclock[own]);
+  if (!gc) {
+    if (expl) {
+      if (w.s_ocidx[own] != NONE) origin = (uint32_t)(w.cl_base[w.s_ocidx[own]] + w.s_oclock[own]);
+    } else origin = g0 - 1;
+    if (w.s_rcidx[own] != NONE) rorigin = (uint32_t)(w.cl_base[w.s_rcidx[own]] + w.s_rclock[own]);
+    if ((origin != NONE && (w.u_flags[origin] & UF_GC)) || (rorigin != NONE && (w.u_flags[rorigin] & UF_GC))) gc = true;
+  }
   uint32_t key = NONE, link = s;
-  if ((sf & SEG_ITEM) && origin == NONE && rorigin == NONE) {
-    sf |= SEG_ROOT;
-    const uint32_t pa = w.s_pa[own], ps = w.s_psub[own];
-    if (pa == NONE || ps == NONE) { raise_err(&w.ctr->err, ERR_UNSUPPORTED); }
-    else {
-      uint64_t h = 1469598103934665603ull;
-      h = fnv_bytes(h, w.bytes + pa, w.s_pb[own]);
-      h = fnv_bytes(h, w.bytes + ps, w.s_psublen[own]);
+  if (!gc && origin == NONE && rorigin == NONE) {
+    const uint32_t pk = w.s_pk[own];
+    uint64_t h = 1469598103934665603ull;
+    uint32_t parent = NONE;
+    if (pk == 1) {
+      h = fnv_bytes(h, w.bytes + w.s_pa[own], w.s_pb[own]);
+    } else if (pk == 2) {
+      const uint32_t pc = w.s_pa[own], pclock = w.s_pb[own];
+      if (pc == NONE || pclock >= w.cl_state[pc]) { raise_err(&w.ctr->err, ERR_PENDING); gc = true; }
+      else {
+        parent = (uint32_t)(w.cl_base[pc] + pclock);
+        if (w.u_flags[parent] & UF_GC) gc = true;
+        h = fnv_u32(h ^ 0xA5u, parent);
+      }
+    } else {
+      raise_err(&w.ctr->err, ERR_DECODE);  // an item without origin, right origin or parent
+      gc = true;
+    }
+    if (!gc) {
+      const uint32_t ps = w.s_psub[own];
+      if (ps != NONE) { h = fnv_u32(h, 0x5Au); h = fnv_bytes(h, w.bytes + ps, w.s_psublen[own]); }
       if (h == 0) h = 1;
       key = key_insert(w.k_hash, w.cap_keys, h);
       if (key == NONE) raise_err(&w.ctr->err, ERR_CAPACITY);
+      else {
+        sf |= SEG_ROOT;
+        w.k_parent[key] = parent;  // every root of a list names the same parent
+        if (ps != NONE) atomicOr(&w.k_flags[key], KF_PSUB);
+      }
     }
-  } else if (sf & SEG_ITEM) {
+  } else if (!gc) {
     link = seg_of(w.u_cutbits, w.u_wpre, origin != NONE ? origin : rorigin);
   }
+  if (gc) sf |= SEG_GC | SEG_DEL;
+  else sf |= SEG_ITEM;
   w.g_cidx[s] = cidx;
   w.g_src[s] = own;
   w.g_flags[s] = sf;
-  w.g_origin[s] = origin;
-  w.g_rorigin[s] = rorigin;
+  w.g_origin[s] = gc ? NONE : origin;
+  w.g_rorigin[s] = gc ? NONE : rorigin;
   w.g_key[s] = key;
   w.g_link[s] = link;
 }
@@ -261,6 +293,8 @@ __global__ __launch_bounds__(256) void k_seg_props(Work w, uint32_t nsegs) {
 void launch_segment_props(const Work& w, uint32_t nsegs, uint32_t nclients, uint64_t nunits, hipStream_t s) {
   hipMemsetAsync(w.k_hash, 0, sizeof(uint64_t) * w.cap_keys, s);
   hipMemsetAsync(w.k_rootmax, 0, sizeof(uint64_t) * w.cap_keys, s);
+  hipMemsetAsync(w.k_flags, 0, sizeof(uint32_t) * w.cap_keys, s);
+  hipMemsetAsync(w.k_parent, 0xFF, sizeof(uint32_t) * w.cap_keys, s);
   hipMemsetAsync(w.g_maxchild, 0, sizeof(uint64_t) * nsegs, s);
   if (nsegs) hipLaunchKernelGGL(k_seg_props, dim3((nsegs + 255) / 256), dim3(256), 0, s, w, nsegs);
 }
@@ -277,6 +311,17 @@ __global__ __launch_bounds__(256) void k_keyjump(Work w, uint32_t nsegs) {
   if (tt != t) { w.g_link[s] = tt; w.ctr->changed = 1; }
 }
 
+// every item now knows its list: tag it YMap-entry (parentSub) or YArray member
+__global__ void k_seg_kind(Work w, uint32_t nsegs) {
+  const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= nsegs) return;
+  const uint32_t f = w.g_flags[s];
+  if (!(f & SEG_ITEM)) return;
+  const uint32_t key = w.g_key[s];
+  if (key == NONE) { raise_err(&w.ctr->err, ERR_DECODE); return; }  // origin chain without a root
+  w.g_flags[s] = f | ((w.k_flags[key] & KF_PSUB) ? SEG_PSUB : SEG_ARRAY);
+}
+
 uint32_t run_key_resolution(const Work& w, uint32_t nsegs, hipStream_t s) {
   if (!nsegs) return 0;
   uint32_t rounds = 0;
@@ -289,6 +334,7 @@ uint32_t run_key_resolution(const Work& w, uint32_t nsegs, hipStream_t s) {
     hipStreamSynchronize(s);
     if (!changed) break;
   }
+  hipLaunchKernelGGL(k_seg_kind, dim3((nsegs + 255) / 256), dim3(256), 0, s, w, nsegs);
   return rounds;
 }
 
@@ -297,9 +343,8 @@ __global__ __launch_bounds__(256) void k_children(Work w, uint32_t nsegs) {
   const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
   if (s >= nsegs) return;
   const uint32_t f = w.g_flags[s];
-  if (!(f & SEG_ITEM)) return;
+  if (!(f & SEG_PSUB)) return;
   const uint32_t key = w.g_key[s];
-  if (key == NONE) { raise_err(&w.ctr->err, ERR_DECODE); return; }  // origin chain without a root
   const unsigned long long v = ((unsigned long long)(w.g_cidx[s] + 1) << 32) | s;
   const uint32_t o = w.g_origin[s];
   if (o != NONE) {
@@ -333,7 +378,7 @@ __global__ void k_overwrite(Work w, uint32_t nsegs) {
   const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
   if (s >= nsegs) return;
   const uint32_t f = w.g_flags[s];
-  if (!(f & SEG_ITEM)) return;
+  if (!(f & SEG_PSUB)) return;
   if (w.k_winner[w.g_key[s]] != s) w.g_flags[s] = f | SEG_DEL;
 }
 
@@ -360,9 +405,56 @@ uint32_t run_descent(const Work& w, uint32_t nsegs, hipStream_t s) {
   return rounds;
 }
 
+// --------------------------------------------------------------------------- deleted parent types
+// ContentType.delete / gc (Y@73441): when a type's item is deleted, every item of that type is
+// deleted and garbage-collected into GC structs (Item.gc with parentGCd, Y@75928); nested types
+// recurse. A list is dead when its parent item is deleted / GC / not a type, or lies in a dead list.
+__global__ void k_dead_init(Work w) {
+  const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= w.cap_keys || w.k_hash[k] == 0) return;
+  const uint32_t pu = w.k_parent[k];
+  if (pu == NONE) return;
+  const uint32_t p = seg_of(w.u_cutbits, w.u_wpre, pu);
+  const uint32_t pf = w.g_flags[p];
+  const bool is_type = (w.s_info[w.g_src[p]] & 31u) == REF_TYPE;
+  if ((pf & SEG_DEL) || !(pf & SEG_ITEM) || !is_type) w.k_flags[k] |= KF_DEAD;
+}
+__global__ void k_dead_prop(Work w) {
+  const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= w.cap_keys || w.k_hash[k] == 0) return;
+  const uint32_t kf = w.k_flags[k];
+  const uint32_t pu = w.k_parent[k];
+  if ((kf & KF_DEAD) || pu == NONE) return;
+  const uint32_t pk = w.g_key[seg_of(w.u_cutbits, w.u_wpre, pu)];
+  if (pk != NONE && (w.k_flags[pk] & KF_DEAD)) { w.k_flags[k] = kf | KF_DEAD; w.ctr->changed = 1; }
+}
+__global__ void k_dead_apply(Work w, uint32_t nsegs) {
+  const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= nsegs) return;
+  const uint32_t f = w.g_flags[s];
+  if (!(f & SEG_ITEM)) return;
+  if (w.k_flags[w.g_key[s]] & KF_DEAD)
+    w.g_flags[s] = (f & ~(SEG_ITEM | SEG_ARRAY | SEG_PSUB | SEG_ROOT)) | SEG_GC | SEG_DEL;
+}
+
+void run_dead_keys(const Work& w, uint32_t nsegs, hipStream_t s) {
+  if (!nsegs) return;
+  const uint32_t kg = w.cap_keys / 256 + 1;
+  hipLaunchKernelGGL(k_dead_init, dim3(kg), dim3(256), 0, s, w);
+  for (int round = 0; round < 64; ++round) {
+    hipMemsetAsync(&w.ctr->changed, 0, sizeof(uint32_t), s);
+    hipLaunchKernelGGL(k_dead_prop, dim3(kg), dim3(256), 0, s, w);
+    uint32_t changed = 0;
+    hipMemcpyAsync(&changed, &w.ctr->changed, sizeof(uint32_t), hipMemcpyDeviceToHost, s);
+    hipStreamSynchronize(s);
+    if (!changed) break;
+  }
+  hipLaunchKernelGGL(k_dead_apply, dim3((nsegs + 255) / 256), dim3(256), 0, s, w, nsegs);
+}
+
 // --------------------------------------------------------------------------- merge flags
-__device__ __forceinline__ bool content_mergeable(uint32_t ref) {
-  return ref == REF_ANY || ref == REF_JSON || ref == REF_STRING;
+__device__ __forceinline__ bool content_mergeable(uint32_t ref) {  // ContentX.mergeWith
+  return ref == REF_ANY || ref == REF_JSON || ref == REF_STRING || ref == REF_DELETED;
 }
 __global__ __launch_bounds__(256) void k_merge_flags(Work w, uint32_t nsegs) {
   const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
@@ -376,7 +468,8 @@ __global__ __launch_bounds__(256) void k_merge_flags(Work w, uint32_t nsegs) {
     if ((fl & SEG_ITEM) == (fr & SEG_ITEM)) {
       if (!(fr & SEG_ITEM)) merge = true;  // GC + GC
       else if ((fl & SEG_DEL) == (fr & SEG_DEL) && w.g_origin[s] == gs - 1 && w.g_rorigin[s - 1] == w.g_rorigin[s] &&
-               w.u_minchild[gs - 1] >= w.g_cidx[s]) {
+               (fl & (SEG_ARRAY | SEG_PSUB)) == (fr & (SEG_ARRAY | SEG_PSUB)) &&
+               ((fr & SEG_ARRAY) ? w.g_right[s - 1] == s : w.u_minchild[gs - 1] >= w.g_cidx[s])) {
         if (fr & SEG_DEL) merge = true;  // both become ContentDeleted after GC
         else {
           const uint32_t rl = w.s_info[w.g_src[s - 1]] & 31u, rr = w.s_info[w.g_src[s]] & 31u;

@@ -11,8 +11,12 @@ size_t prim_tmp_bytes(uint64_t n) {
   rocprim::exclusive_scan(nullptr, a, (const uint32_t*)nullptr, (uint32_t*)nullptr, 0u, (size_t)n, rocprim::plus<uint32_t>());
   rocprim::exclusive_scan(nullptr, b, (const uint32_t*)nullptr, (uint64_t*)nullptr, (uint64_t)0, (size_t)n, rocprim::plus<uint64_t>());
   rocprim::radix_sort_keys(nullptr, c, (const uint32_t*)nullptr, (uint32_t*)nullptr, (size_t)n, 0, 32);
+  size_t d = 0;
+  rocprim::radix_sort_pairs(nullptr, d, (const uint32_t*)nullptr, (uint32_t*)nullptr, (const uint32_t*)nullptr,
+                            (uint32_t*)nullptr, (size_t)n, 0, 32);
   size_t m = a > b ? a : b;
-  return (m > c ? m : c) + 256;
+  m = m > c ? m : c;
+  return (m > d ? m : d) + 256;
 }
 
 void scan_u32(void* tmp, size_t tmpb, const uint32_t* in, uint32_t* out, uint64_t n, hipStream_t s) {
@@ -28,6 +32,12 @@ void scan_u32_to_u64(void* tmp, size_t tmpb, const uint32_t* in, uint64_t* out, 
 void sort_u32(void* tmp, size_t tmpb, const uint32_t* in, uint32_t* out, uint64_t n, hipStream_t s) {
   if (!n) return;
   rocprim::radix_sort_keys(tmp, tmpb, in, out, (size_t)n, 0, 32, s);
+}
+
+void sort_pairs_u32(void* tmp, size_t tmpb, const uint32_t* kin, uint32_t* kout, const uint32_t* vin, uint32_t* vout,
+                    uint64_t n, hipStream_t s) {
+  if (!n) return;
+  rocprim::radix_sort_pairs(tmp, tmpb, kin, kout, vin, vout, (size_t)n, 0, 32, s);
 }
 
 }  // namespace yc

@@ -95,8 +95,9 @@ struct Work {
   uint32_t* s_oclock = nullptr;
   uint32_t* s_rcidx = nullptr;     // right origin client index
   uint32_t* s_rclock = nullptr;
-  uint32_t* s_pa = nullptr;        // parent name varString position (root) or NONE
-  uint32_t* s_pb = nullptr;        // parent name varString length
+  uint8_t* s_pk = nullptr;         // parent kind: 0 inherited, 1 root type name, 2 parent item id
+  uint32_t* s_pa = nullptr;        // pk 1: name varString position; pk 2: parent client index
+  uint32_t* s_pb = nullptr;        // pk 1: name varString length;   pk 2: parent clock
   uint32_t* s_psub = nullptr;      // parentSub varString position or NONE
   uint32_t* s_psublen = nullptr;
   uint32_t* s_cpos = nullptr;      // content byte range
@@ -132,7 +133,20 @@ struct Work {
   uint64_t* k_hash = nullptr;      // [cap_keys] open addressing table of 64-bit key hashes (0 = empty)
   uint64_t* k_rootmax = nullptr;   // [cap_keys] (cidx<<32 | seg) of max-client root
   uint32_t* k_winner = nullptr;    // [cap_keys] winning (rightmost) segment
+  uint32_t* k_parent = nullptr;    // [cap_keys] parent type item unit (NONE = root type)
+  uint32_t* k_flags = nullptr;     // [cap_keys] KF_* flags
   uint32_t cap_keys = 0;
+  // ---- YArray lists (YATA integration, yc_yata.hip)
+  uint32_t* g_right = nullptr;     // [NS] right neighbour after integration (NONE = end of list)
+  uint32_t* y_key = nullptr;       // [NS] sort key: key slot of live array-list segments, NONE otherwise
+  uint32_t* y_keys = nullptr;      // [NS] sorted keys
+  uint32_t* y_seg = nullptr;       // [NS] segments sorted by (key slot, segment)
+  uint32_t* y_iota = nullptr;      // [NS] 0..NS-1 (sort values)
+  uint32_t* y_lstart = nullptr;    // [lists+1] first position of every list in y_seg
+  uint32_t* y_state = nullptr;     // [NS] integration state / stamps (per segment)
+  uint32_t* y_before = nullptr;    // [NS]
+  uint32_t* y_confl = nullptr;     // [NS]
+  uint32_t* y_stack = nullptr;     // [NS]
   // ---- encode (NO <= NS)
   uint32_t* o_first = nullptr;     // [NO+1] first segment of output struct (+ sentinel)
   uint32_t* o_cidx = nullptr;      // client of output struct
@@ -167,6 +181,13 @@ enum : uint32_t {
   SEG_ROOT = 8u,       // explicit parent (root name) + parentSub
   SEG_MERGE = 16u,     // merges into the previous segment
   SEG_ITEM = 32u,
+  SEG_ARRAY = 64u,     // member of a YArray list (no parentSub)
+  SEG_PSUB = 128u,     // member of a YMap entry list (parentSub)
+};
+// key flags
+enum : uint32_t {
+  KF_PSUB = 1u,        // the list is a YMap entry (items carry a parentSub)
+  KF_DEAD = 2u,        // the parent type item is deleted: every member becomes GC
 };
 // unit flags
 enum : uint32_t {
@@ -194,6 +215,8 @@ uint32_t run_key_resolution(const Work& w, uint32_t nsegs, hipStream_t s);
 void launch_map_winner(const Work& w, uint32_t nsegs, hipStream_t s);
 uint32_t run_descent(const Work& w, uint32_t nsegs, hipStream_t s);
 void launch_merge_flags(const Work& w, uint32_t nsegs, hipStream_t s);
+void run_dead_keys(const Work& w, uint32_t nsegs, hipStream_t s);
+uint32_t launch_yata(const Work& w, uint32_t nsegs, hipStream_t s);
 
 void launch_encode_sizes(const Work& w, uint32_t nsegs, uint32_t nclients, uint32_t nout, uint32_t* nruns_host, hipStream_t s);
 void launch_encode_write(const Work& w, uint32_t nclients, uint32_t nout, uint32_t nruns, hipStream_t s);
@@ -203,5 +226,7 @@ size_t prim_tmp_bytes(uint64_t max_items);
 void scan_u32(void* tmp, size_t tmpb, const uint32_t* in, uint32_t* out, uint64_t n, hipStream_t s);          // exclusive
 void scan_u32_to_u64(void* tmp, size_t tmpb, const uint32_t* in, uint64_t* out, uint64_t n, hipStream_t s);   // exclusive
 void sort_u32(void* tmp, size_t tmpb, const uint32_t* in, uint32_t* out, uint64_t n, hipStream_t s);
+void sort_pairs_u32(void* tmp, size_t tmpb, const uint32_t* kin, uint32_t* kout, const uint32_t* vin, uint32_t* vout,
+                    uint64_t n, hipStream_t s);
 
 }  // namespace yc

@@ -1,0 +1,135 @@
+// yc_yata.hip — K4: YArray YATA integration (Item.integrate conflict loop, Y@77594) on gfx950.
+//
+// Every live YArray list (root array or nested array, keyed by the list slot resolved in
+// yc_merge.hip) is integrated independently, so lists are the unit of parallelism:
+//   k_ykey / sort      segments of live array lists, radix-sorted by (list slot, segment) — a
+//                      stable sort, so each list's members stay in (client, clock) order
+//   k_ylist_*          list boundaries (flag + scan)
+//   k_yata             one wavefront per list runs the exact YATA loop over
+//                      segments in a causal order (depth-first on origin / right origin, the
+//                      "stack dive" of integrateStructs, Y@19963), producing the final right
+//                      neighbour of every segment (g_right) for Item.mergeWith adjacency.
+// A segment is a run of consecutive units of one client cut at every referenced unit, so the
+// loop's verdict on the first unit of a run holds for the whole run (SURVEY §7 hard part 1,
+// per-clock restatement) and the loop can step over segments instead of units.
+#include "yc_work.h"
+
+namespace yc {
+
+__device__ __forceinline__ uint32_t seg_of_unit(const Work& w, uint32_t g) {
+  return w.u_wpre[g >> 6] + (uint32_t)__popcll(w.u_cutbits[g >> 6] & ((2ull << (g & 63)) - 1)) - 1;
+}
+
+__global__ void k_ykey(Work w, uint32_t nsegs) {
+  const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= nsegs) return;
+  w.y_key[s] = (w.g_flags[s] & SEG_ARRAY) ? w.g_key[s] : NONE;
+  w.y_iota[s] = s;
+  w.g_right[s] = NONE;
+  w.y_state[s] = 0;
+}
+
+// flag list starts; y_before doubles as the flag array, y_confl receives the scan
+__global__ void k_ylist_flags(Work w, uint32_t nsegs) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i > nsegs) return;
+  if (i == nsegs) { w.y_before[i] = 0; return; }
+  const uint32_t k = w.y_keys[i];
+  w.y_before[i] = (k != NONE && (i == 0 || w.y_keys[i - 1] != k)) ? 1u : 0u;
+}
+__global__ void k_ylist_starts(Work w, uint32_t nsegs) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= nsegs) return;
+  const uint32_t k = w.y_keys[i];
+  if (k == NONE) return;
+  if (w.y_before[i]) w.y_lstart[w.y_confl[i]] = i;
+  if (i + 1 == nsegs || w.y_keys[i + 1] == NONE) w.y_lstart[w.y_confl[nsegs]] = i + 1;  // sentinel
+}
+
+// One wavefront per list; lane 0 runs the sequential loop (the lists of a batch run in parallel).
+__global__ __launch_bounds__(64) void k_yata(Work w, uint32_t nlists) {
+  const uint32_t l = blockIdx.x;
+  if (l >= nlists || threadIdx.x != 0) return;
+  const uint32_t a = w.y_lstart[l], b = w.y_lstart[l + 1];
+  const uint32_t key = w.y_keys[a];
+  uint32_t* __restrict__ right = w.g_right;
+  uint32_t* __restrict__ state = w.y_state;   // 0 = pending, 1 = on the stack, 2 = integrated
+  uint32_t* __restrict__ before = w.y_before; // itemsBeforeOrigin stamp
+  uint32_t* __restrict__ confl = w.y_confl;   // conflictingItems stamp
+  uint32_t* __restrict__ stack = w.y_stack + a;
+  uint32_t head = NONE;  // parent._start
+  uint32_t ctr = 0;      // stamps: every (integration, conflicting-set epoch) gets a fresh value
+  for (uint32_t i = a; i < b; ++i) {
+    const uint32_t s0 = w.y_seg[i];
+    if (state[s0] == 2) continue;
+    uint32_t sp = 0;
+    stack[sp++] = s0;
+    state[s0] = 1;
+    while (sp > 0) {
+      const uint32_t t = stack[sp - 1];
+      const uint32_t oU = w.g_origin[t], rU = w.g_rorigin[t];
+      const uint32_t oseg = oU != NONE ? seg_of_unit(w, oU) : NONE;
+      const uint32_t rseg = rU != NONE ? seg_of_unit(w, rU) : NONE;
+      uint32_t dep = NONE;
+      if (oseg != NONE && state[oseg] != 2) dep = oseg;
+      else if (rseg != NONE && state[rseg] != 2) dep = rseg;
+      if (dep != NONE) {
+        if (state[dep] == 1 || w.g_key[dep] != key || !(w.g_flags[dep] & SEG_ARRAY) || sp >= b - a) {
+          raise_err(&w.ctr->err, ERR_DECODE);  // a reference outside the list, or a cycle
+          return;
+        }
+        state[dep] = 1;
+        stack[sp++] = dep;
+        continue;
+      }
+      // ---- Item.integrate(t): YATA conflict resolution between origin and right origin
+      uint32_t left = oseg;
+      const uint32_t ct = w.g_cidx[t];
+      uint32_t o = left != NONE ? right[left] : head;
+      if (o != rseg) {
+        const uint32_t iter = ++ctr;
+        uint32_t ep = ++ctr;
+        while (o != NONE && o != rseg) {
+          before[o] = iter;
+          confl[o] = ep;
+          const uint32_t oo = w.g_origin[o];
+          if (oo == oU) {
+            if (w.g_cidx[o] < ct) { left = o; ep = ++ctr; }
+            else if (w.g_rorigin[o] == rU) break;
+          } else if (oo != NONE && before[seg_of_unit(w, oo)] == iter) {
+            if (confl[seg_of_unit(w, oo)] != ep) { left = o; ep = ++ctr; }
+          } else {
+            break;
+          }
+          o = right[o];
+        }
+      }
+      uint32_t r2;
+      if (left != NONE) { r2 = right[left]; right[left] = t; }
+      else { r2 = head; head = t; }
+      right[t] = r2;
+      state[t] = 2;
+      --sp;
+    }
+  }
+}
+
+uint32_t launch_yata(const Work& w, uint32_t nsegs, hipStream_t s) {
+  if (!nsegs) return 0;
+  const uint32_t grid = nsegs / 256 + 1;
+  hipLaunchKernelGGL(k_ykey, dim3(grid), dim3(256), 0, s, w, nsegs);
+  sort_pairs_u32(w.tmp, w.tmp_bytes, w.y_key, w.y_keys, w.y_iota, w.y_seg, nsegs, s);
+  hipLaunchKernelGGL(k_ylist_flags, dim3(grid), dim3(256), 0, s, w, nsegs);
+  scan_u32(w.tmp, w.tmp_bytes, w.y_before, w.y_confl, nsegs + 1, s);
+  uint32_t nlists = 0;
+  hipMemcpyAsync(&nlists, w.y_confl + nsegs, sizeof(uint32_t), hipMemcpyDeviceToHost, s);
+  hipStreamSynchronize(s);
+  if (!nlists) return 0;
+  hipLaunchKernelGGL(k_ylist_starts, dim3(grid), dim3(256), 0, s, w, nsegs);
+  hipMemsetAsync(w.y_before, 0, sizeof(uint32_t) * (nsegs + 1), s);  // stamps: 0 is never issued
+  hipMemsetAsync(w.y_confl, 0, sizeof(uint32_t) * (nsegs + 1), s);
+  hipLaunchKernelGGL(k_yata, dim3(nlists), dim3(64), 0, s, w, nlists);
+  return nlists;
+}
+
+}  // namespace yc
