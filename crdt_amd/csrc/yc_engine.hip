@@ -110,6 +110,7 @@ struct ycrdt_engine {
   std::vector<DevBuf> bufs;
   Work w;
   bool profiling = false;
+  bool debug_sync = false;
   std::vector<std::pair<const char*, hipEvent_t>> marks;
   std::vector<std::pair<const char*, double>> phase_ms;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
@@ -141,6 +142,10 @@ struct ycrdt_batch {
 namespace {
 
 void mark(ycrdt_engine* e, const char* name) {
+  if (e->debug_sync) {  // YCRDT_DEBUG_SYNC=1: attribute a device fault to the phase that raised it
+    const hipError_t er = hipStreamSynchronize(e->stream);
+    if (er != hipSuccess) fprintf(stderr, "[ycrdt] device error before phase %s: %s\n", name, hipGetErrorString(er));
+  }
   if (!e->profiling) return;
   hipEvent_t ev;
   hipEventCreate(&ev);
@@ -523,6 +528,7 @@ int ycrdt_engine_create(int device, int compat, ycrdt_engine** out) {
   auto* e = new ycrdt_engine();
   e->device = device;
   e->compat = compat == 135 ? 135 : 136;
+  e->debug_sync = getenv("YCRDT_DEBUG_SYNC") && getenv("YCRDT_DEBUG_SYNC")[0] == '1';
   if (hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess) { delete e; return fail(YCRDT_E_DEVICE, "stream"); }
   hipEventCreate(&e->ev0);
   hipEventCreate(&e->ev1);

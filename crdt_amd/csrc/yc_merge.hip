@@ -303,8 +303,16 @@ void launch_segment_props(const Work& w, uint32_t nsegs, uint32_t nclients, uint
 __global__ __launch_bounds__(256) void k_keyjump(Work w, uint32_t nsegs) {
   const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
   if (s >= nsegs) return;
-  if (w.g_key[s] != NONE || !(w.g_flags[s] & SEG_ITEM)) return;
+  const uint32_t f = w.g_flags[s];
+  if (w.g_key[s] != NONE || !(f & SEG_ITEM)) return;
   const uint32_t t = w.g_link[s];
+  if (!(w.g_flags[t] & SEG_ITEM)) {  // the origin chain ends in GC: getMissing drops the parent
+    w.g_flags[s] = (f & ~SEG_ITEM) | SEG_GC | SEG_DEL;
+    w.g_origin[s] = NONE;
+    w.g_rorigin[s] = NONE;
+    w.ctr->changed = 1;
+    return;
+  }
   const uint32_t kt = w.g_key[t];
   if (kt != NONE) { w.g_key[s] = kt; w.ctr->changed = 1; return; }
   const uint32_t tt = w.g_link[t];
@@ -433,7 +441,8 @@ __global__ void k_dead_apply(Work w, uint32_t nsegs) {
   if (s >= nsegs) return;
   const uint32_t f = w.g_flags[s];
   if (!(f & SEG_ITEM)) return;
-  if (w.k_flags[w.g_key[s]] & KF_DEAD)
+  const uint32_t key = w.g_key[s];
+  if (key == NONE || (w.k_flags[key] & KF_DEAD))
     w.g_flags[s] = (f & ~(SEG_ITEM | SEG_ARRAY | SEG_PSUB | SEG_ROOT)) | SEG_GC | SEG_DEL;
 }
 
