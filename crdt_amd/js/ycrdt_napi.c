@@ -1,0 +1,246 @@
+/* ycrdt_napi.c — Node-API addon over the C ABI (include/ycrdt.h).
+ *
+ * This is the reference-language host binding: @ypear/crdt loads its CRDT engine from
+ * `router.options.Y` (reference crdt.js:175-180), so a Node module exporting the Yjs functions
+ * the reference calls is the drop-in. crdt_amd/js/index.js builds that `Y` object on top of this
+ * binding. Plain C + node_api.h (NAPI 8, Node >= 12.22); no node-gyp needed:
+ *   gcc -shared -fPIC -I/usr/include/node ycrdt_napi.c -L.. -lycrdt -Wl,-rpath,'$ORIGIN/..'
+ * Errors from the engine become JS `Error`s carrying ycrdt_last_error() (the reference only reads
+ * e.message, crdt.js:38-39) and a numeric `code`.
+ */
+#define NAPI_VERSION 8
+#include <node_api.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "../../include/ycrdt.h"
+
+#define CHECK(env, call)                                                 \
+  do {                                                                   \
+    if ((call) != napi_ok) {                                             \
+      napi_throw_error((env), NULL, "ycrdt: N-API call failed: " #call); \
+      return NULL;                                                       \
+    }                                                                    \
+  } while (0)
+
+static ycrdt_engine *g_engine = NULL; /* one engine (HIP device + stream) per process */
+static int g_device = 0;
+
+static napi_value throw_rc(napi_env env, int rc) {
+  napi_value msg, err, code;
+  const char *m = ycrdt_last_error();
+  napi_create_string_utf8(env, m && m[0] ? m : "ycrdt error", NAPI_AUTO_LENGTH, &msg);
+  napi_create_error(env, NULL, msg, &err);
+  napi_create_int32(env, rc, &code);
+  napi_set_named_property(env, err, "code", code);
+  napi_throw(env, err);
+  return NULL;
+}
+
+static ycrdt_engine *engine(napi_env env) {
+  if (!g_engine) {
+    int rc = ycrdt_engine_create(g_device, 136, &g_engine);
+    if (rc != YCRDT_OK) {
+      g_engine = NULL;
+      throw_rc(env, rc);
+      return NULL;
+    }
+  }
+  return g_engine;
+}
+
+/* Uint8Array / Buffer argument → borrowed (ptr, len) */
+static int get_bytes(napi_env env, napi_value v, ycrdt_buf *out) {
+  bool is_ta = false;
+  napi_is_typedarray(env, v, &is_ta);
+  if (is_ta) {
+    napi_typedarray_type t;
+    size_t len, off;
+    void *data;
+    napi_value ab;
+    if (napi_get_typedarray_info(env, v, &t, &len, &data, &ab, &off) != napi_ok || t != napi_uint8_array) return 0;
+    out->ptr = (const uint8_t *)data;
+    out->len = len;
+    return 1;
+  }
+  bool is_buf = false;
+  napi_is_buffer(env, v, &is_buf);
+  if (is_buf) {
+    void *data;
+    size_t len;
+    if (napi_get_buffer_info(env, v, &data, &len) != napi_ok) return 0;
+    out->ptr = (const uint8_t *)data;
+    out->len = len;
+    return 1;
+  }
+  return 0;
+}
+
+
+static napi_value u8_from_out(napi_env env, ycrdt_out *o) {
+  napi_value ab, ta;
+  void *data = NULL;
+  size_t n = o->len;
+  CHECK(env, napi_create_arraybuffer(env, n, &data, &ab));
+  if (n) memcpy(data, o->ptr, n);
+  ycrdt_free(o);
+  CHECK(env, napi_create_typedarray(env, napi_uint8_array, n, ab, 0, &ta));
+  return ta;
+}
+
+static void doc_finalize(napi_env env, void *data, void *hint) {
+  (void)env;
+  (void)hint;
+  ycrdt_doc_destroy((ycrdt_doc *)data);
+}
+
+static ycrdt_doc *get_doc(napi_env env, napi_value v) {
+  void *p = NULL;
+  if (napi_get_value_external(env, v, &p) != napi_ok || !p) {
+    napi_throw_type_error(env, NULL, "ycrdt: expected a doc handle");
+    return NULL;
+  }
+  return (ycrdt_doc *)p;
+}
+
+/* setDevice(ordinal) — before the first engine use */
+static napi_value js_set_device(napi_env env, napi_callback_info info) {
+  size_t argc = 1;
+  napi_value argv[1];
+  CHECK(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+  int32_t dev = 0;
+  if (argc > 0) napi_get_value_int32(env, argv[0], &dev);
+  g_device = dev;
+  return NULL;
+}
+
+/* docCreate(clientId) → handle   (new Y.Doc(), crdt.js:33,54,56,80,221) */
+static napi_value js_doc_create(napi_env env, napi_callback_info info) {
+  size_t argc = 1;
+  napi_value argv[1], out;
+  CHECK(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+  uint32_t cid = 0;
+  if (argc > 0) napi_get_value_uint32(env, argv[0], &cid);
+  ycrdt_engine *e = engine(env);
+  if (!e) return NULL;
+  ycrdt_doc *d = NULL;
+  int rc = ycrdt_doc_create(e, cid, &d);
+  if (rc != YCRDT_OK) return throw_rc(env, rc);
+  CHECK(env, napi_create_external(env, d, doc_finalize, NULL, &out));
+  return out;
+}
+
+/* applyUpdates(doc, update | update[])   (Y.applyUpdate, crdt.js:35,56,58,85,294) */
+static napi_value js_apply_updates(napi_env env, napi_callback_info info) {
+  size_t argc = 2;
+  napi_value argv[2];
+  CHECK(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+  if (argc < 2) { napi_throw_type_error(env, NULL, "applyUpdates(doc, updates)"); return NULL; }
+  ycrdt_doc *d = get_doc(env, argv[0]);
+  if (!d) return NULL;
+  bool is_arr = false;
+  napi_is_array(env, argv[1], &is_arr);
+  if (!is_arr) {
+    ycrdt_buf b;
+    if (!get_bytes(env, argv[1], &b)) { napi_throw_type_error(env, NULL, "update must be a Uint8Array"); return NULL; }
+    int rc = ycrdt_apply_update(d, b);
+    return rc == YCRDT_OK ? NULL : throw_rc(env, rc);
+  }
+  uint32_t n = 0;
+  napi_get_array_length(env, argv[1], &n);
+  ycrdt_buf *bufs = (ycrdt_buf *)calloc(n ? n : 1, sizeof(ycrdt_buf));
+  for (uint32_t i = 0; i < n; ++i) {
+    napi_value el;
+    napi_get_element(env, argv[1], i, &el);
+    if (!get_bytes(env, el, &bufs[i])) {
+      free(bufs);
+      napi_throw_type_error(env, NULL, "updates must be Uint8Arrays");
+      return NULL;
+    }
+  }
+  int rc = ycrdt_apply_updates(d, bufs, n);
+  free(bufs);
+  return rc == YCRDT_OK ? NULL : throw_rc(env, rc);
+}
+
+/* encodeStateAsUpdate(doc[, sv])   (crdt.js:56,260,288,347,383,443,471,505,533,560,585,611) */
+static napi_value js_encode_state_as_update(napi_env env, napi_callback_info info) {
+  size_t argc = 2;
+  napi_value argv[2];
+  CHECK(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+  ycrdt_doc *d = argc > 0 ? get_doc(env, argv[0]) : NULL;
+  if (!d) return NULL;
+  ycrdt_buf sv = {NULL, 0};
+  if (argc > 1) {
+    napi_valuetype t;
+    napi_typeof(env, argv[1], &t);
+    if (t != napi_undefined && t != napi_null && !get_bytes(env, argv[1], &sv)) {
+      napi_throw_type_error(env, NULL, "state vector must be a Uint8Array");
+      return NULL;
+    }
+  }
+  ycrdt_out o = {NULL, 0};
+  int rc = ycrdt_encode_state_as_update(d, sv, &o);
+  if (rc != YCRDT_OK) return throw_rc(env, rc);
+  return u8_from_out(env, &o);
+}
+
+/* encodeStateVector(doc)   (crdt.js:59,239,258,289) */
+static napi_value js_encode_state_vector(napi_env env, napi_callback_info info) {
+  size_t argc = 1;
+  napi_value argv[1];
+  CHECK(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+  ycrdt_doc *d = argc > 0 ? get_doc(env, argv[0]) : NULL;
+  if (!d) return NULL;
+  ycrdt_out o = {NULL, 0};
+  int rc = ycrdt_encode_state_vector(d, &o);
+  if (rc != YCRDT_OK) return throw_rc(env, rc);
+  return u8_from_out(env, &o);
+}
+
+/* lastStats(doc) → {items, structs, units, segments, outBytes, deviceMs} */
+static napi_value js_last_stats(napi_env env, napi_callback_info info) {
+  size_t argc = 1;
+  napi_value argv[1], obj, v;
+  CHECK(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+  ycrdt_doc *d = argc > 0 ? get_doc(env, argv[0]) : NULL;
+  if (!d) return NULL;
+  ycrdt_merge_stats st;
+  int rc = ycrdt_doc_last_stats(d, &st);
+  if (rc != YCRDT_OK) return throw_rc(env, rc);
+  CHECK(env, napi_create_object(env, &obj));
+#define PUT(name, val) napi_create_double(env, (double)(val), &v); napi_set_named_property(env, obj, name, v)
+  PUT("inBytes", st.in_bytes);
+  PUT("items", st.items);
+  PUT("structs", st.structs);
+  PUT("units", st.units);
+  PUT("segments", st.segments);
+  PUT("outBytes", st.out_bytes);
+  PUT("clients", st.clients);
+  PUT("deviceMs", st.device_ms);
+#undef PUT
+  return obj;
+}
+
+static napi_value js_version(napi_env env, napi_callback_info info) {
+  (void)info;
+  napi_value s;
+  CHECK(env, napi_create_string_utf8(env, ycrdt_version(), NAPI_AUTO_LENGTH, &s));
+  return s;
+}
+
+static napi_value init(napi_env env, napi_value exports) {
+  napi_property_descriptor props[] = {
+      {"setDevice", NULL, js_set_device, NULL, NULL, NULL, napi_default, NULL},
+      {"docCreate", NULL, js_doc_create, NULL, NULL, NULL, napi_default, NULL},
+      {"applyUpdates", NULL, js_apply_updates, NULL, NULL, NULL, napi_default, NULL},
+      {"encodeStateAsUpdate", NULL, js_encode_state_as_update, NULL, NULL, NULL, napi_default, NULL},
+      {"encodeStateVector", NULL, js_encode_state_vector, NULL, NULL, NULL, napi_default, NULL},
+      {"lastStats", NULL, js_last_stats, NULL, NULL, NULL, napi_default, NULL},
+      {"version", NULL, js_version, NULL, NULL, NULL, napi_default, NULL},
+  };
+  napi_define_properties(env, exports, sizeof(props) / sizeof(props[0]), props);
+  return exports;
+}
+
+NAPI_MODULE(NODE_GYP_MODULE_NAME, init)

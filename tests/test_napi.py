@@ -1,0 +1,34 @@
+"""The reference-language boundary: the Node-API addon + `Y` facade (crdt_amd/js) that
+@ypear/crdt receives as router.options.Y (reference crdt.js:175-180)."""
+import os
+import shutil
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+NODE = shutil.which("node")
+pytestmark = pytest.mark.skipif(NODE is None, reason="node not installed")
+
+
+def _run(mode, timeout):
+    r = subprocess.run([NODE, os.path.join(ROOT, "tests", "js", "napi_check.js"), mode], capture_output=True, text=True,
+                       timeout=timeout)
+    assert r.returncode == 0, r.stdout + r.stderr
+    return r.stdout
+
+
+def test_napi_addon_loads_and_fails_loudly_without_gpu():
+    import crdt_amd
+
+    try:
+        crdt_amd.Engine()
+        pytest.skip("a GPU is present: the no-device behaviour is not observable")
+    except crdt_amd.YcrdtError:
+        pass
+    assert "napi cpu ok" in _run("cpu", 120)
+
+
+@pytest.mark.gpu
+def test_napi_golden_on_gpu():
+    assert "napi golden ok" in _run("golden", 300)
