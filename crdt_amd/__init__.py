@@ -9,6 +9,8 @@ the C ABI in include/ycrdt.h (libycrdt.so, hand-written gfx950 HIP kernels):
     apply_updates(doc, [u8])      n × Y.applyUpdate, one batch     crdt.js:79-98 (LevelDB replay)
     encode_state_as_update(doc[, sv])  Y.encodeStateAsUpdate       crdt.js:56,260,288,347,443,...
     encode_state_vector(doc)      Y.encodeStateVector(doc)         crdt.js:59,239,258,289
+    merge_updates([u8])           Y.mergeUpdates                   north_star (Y@39011)
+    diff_update(u8, sv)           Y.diffUpdate                     Y@40711
 
 Errors raise YcrdtError (the reference only reads `e.message`, crdt.js:38-39). There is no CPU
 fallback: importing works without a GPU, but every compute call needs the HIP device.
@@ -18,7 +20,7 @@ import os
 
 __all__ = [
     "YcrdtError", "Engine", "Doc", "Batch", "MergeStats", "apply_update", "apply_updates",
-    "encode_state_as_update", "encode_state_vector", "default_engine", "library_path",
+    "encode_state_as_update", "encode_state_vector", "merge_updates", "diff_update", "default_engine", "library_path",
 ]
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
@@ -76,7 +78,7 @@ EXPORTS = (
     "ycrdt_doc_create", "ycrdt_doc_destroy", "ycrdt_apply_update", "ycrdt_apply_updates",
     "ycrdt_encode_state_as_update", "ycrdt_encode_state_vector", "ycrdt_doc_last_stats",
     "ycrdt_batch_stage", "ycrdt_batch_merge", "ycrdt_batch_result", "ycrdt_batch_destroy",
-    "ycrdt_free", "ycrdt_last_error", "ycrdt_version",
+    "ycrdt_merge_updates", "ycrdt_diff_update", "ycrdt_free", "ycrdt_last_error", "ycrdt_version",
 )
 
 
@@ -106,6 +108,8 @@ def lib():
     L.ycrdt_batch_merge.argtypes = [vp, P(MergeStats)]
     L.ycrdt_batch_result.argtypes = [vp, P(_Out), P(_Out)]
     L.ycrdt_batch_destroy.argtypes = [vp]
+    L.ycrdt_merge_updates.argtypes = [vp, P(_Buf), sz, P(_Out)]
+    L.ycrdt_diff_update.argtypes = [vp, _Buf, _Buf, P(_Out)]
     L.ycrdt_free.argtypes = [P(_Out)]
     L.ycrdt_last_error.restype = ctypes.c_char_p
     L.ycrdt_version.restype = ctypes.c_char_p
@@ -257,3 +261,23 @@ def encode_state_as_update(doc: Doc, sv: bytes = b"") -> bytes:
 
 def encode_state_vector(doc: Doc) -> bytes:
     return doc.encode_state_vector()
+
+
+def merge_updates(updates, engine=None) -> bytes:
+    """Y.mergeUpdates(updates) on the GPU (lazy k-way struct merge + delete-set union)."""
+    eng = engine or default_engine()
+    arr, keep = _bufs(updates)
+    out = _Out()
+    _check(lib().ycrdt_merge_updates(eng._h, arr, len(keep), ctypes.byref(out)))
+    return _take(out)
+
+
+def diff_update(update: bytes, sv: bytes, engine=None) -> bytes:
+    """Y.diffUpdate(update, sv) on the GPU."""
+    eng = engine or default_engine()
+    u, v = bytes(update), bytes(sv)
+    bu = _Buf(ctypes.cast(ctypes.c_char_p(u), ctypes.c_void_p), len(u))
+    bv = _Buf(ctypes.cast(ctypes.c_char_p(v), ctypes.c_void_p), len(v))
+    out = _Out()
+    _check(lib().ycrdt_diff_update(eng._h, bu, bv, ctypes.byref(out)))
+    return _take(out)

@@ -298,6 +298,9 @@ __device__ inline int parse_struct(const uint8_t* __restrict__ b, uint32_t& p, u
 __device__ __forceinline__ uint32_t vu_size(uint32_t v) {
   return v < (1u << 7) ? 1 : v < (1u << 14) ? 2 : v < (1u << 21) ? 3 : v < (1u << 28) ? 4 : 5;
 }
+inline uint32_t vu_size_host(uint32_t v) {
+  return v < (1u << 7) ? 1 : v < (1u << 14) ? 2 : v < (1u << 21) ? 3 : v < (1u << 28) ? 4 : 5;
+}
 __device__ __forceinline__ uint32_t wr_vu(uint8_t* __restrict__ o, uint32_t p, uint32_t v) {
   while (v > 127u) { o[p++] = (uint8_t)(0x80u | (v & 0x7fu)); v >>= 7; }
   o[p++] = (uint8_t)v;

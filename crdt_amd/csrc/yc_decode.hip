@@ -223,6 +223,8 @@ __global__ __launch_bounds__(64) void k_walker(Work w) {
   if (!ok || nsec > (uend - p) / 3 + 1) { raise_err(err, ERR_DECODE); return; }
   const uint32_t sbase = atomicAdd(&w.ctr->nsections, nsec);
   if (sbase + nsec > w.cap_sections) { raise_err(err, ERR_CAPACITY); return; }
+  w.usec_start[u] = sbase;
+  w.usec_n[u] = nsec;
   for (uint32_t s = 0; s < nsec; ++s) {
     const uint32_t n = rd_vu(b, p, uend, ok);
     const uint32_t client = rd_vu(b, p, uend, ok);
@@ -603,13 +605,15 @@ __global__ __launch_bounds__(256) void k_struct_decode(Work w, uint32_t nstructs
   w.s_cidx[i] = sec.cidx;
   uint32_t oc = NONE, rc = NONE;
   const bool item = v.ref != REF_GC && v.ref != REF_SKIP;
+  // lazy mode (mergeUpdates / diffUpdate): references are copied, never resolved, so the raw
+  // client ids are kept (presence = info bits); integrate mode maps them to client indices
   if (item && (v.info & 0x80u)) {
-    oc = find_cidx(w.cl_vals, nclients, v.oc);
-    if (oc == NONE) { raise_err(err, ERR_PENDING); w.ctr->err_info = i; }
+    oc = w.lazy ? v.oc : find_cidx(w.cl_vals, nclients, v.oc);
+    if (oc == NONE && !w.lazy) { raise_err(err, ERR_PENDING); w.ctr->err_info = i; }
   }
   if (item && (v.info & 0x40u)) {
-    rc = find_cidx(w.cl_vals, nclients, v.rc);
-    if (rc == NONE) { raise_err(err, ERR_PENDING); w.ctr->err_info = i; }
+    rc = w.lazy ? v.rc : find_cidx(w.cl_vals, nclients, v.rc);
+    if (rc == NONE && !w.lazy) { raise_err(err, ERR_PENDING); w.ctr->err_info = i; }
   }
   w.s_ocidx[i] = oc;
   w.s_oclock[i] = v.ok_;
@@ -619,9 +623,9 @@ __global__ __launch_bounds__(256) void k_struct_decode(Work w, uint32_t nstructs
   uint32_t pk = item ? v.pkind : 0u, pa = NONE, pb = 0;
   if (pk == 1) { pa = v.pa; pb = v.pb; }
   else if (pk == 2) {
-    pa = find_cidx(w.cl_vals, nclients, v.pa);
+    pa = w.lazy ? v.pa : find_cidx(w.cl_vals, nclients, v.pa);
     pb = v.pb;
-    if (pa == NONE) { raise_err(err, ERR_PENDING); w.ctr->err_info = i; }
+    if (pa == NONE && !w.lazy) { raise_err(err, ERR_PENDING); w.ctr->err_info = i; }
   }
   w.s_pk[i] = (uint8_t)pk;
   w.s_pa[i] = pa;

@@ -25,56 +25,6 @@ __device__ __forceinline__ uint32_t copy_bytes(uint8_t* __restrict__ o, uint32_t
   return p + n;
 }
 
-// Byte range of content elements [e0, e1) of struct `src` (ContentAny: lib0 `any` values,
-// ContentJSON: varStrings, ContentString: UTF-16 code units of the UTF-8 text; every other
-// content has length 1 and is copied whole). This is ContentX.splice (Y@70000..) as a byte slice.
-__device__ bool content_slice(const Work& w, uint32_t src, uint32_t e0, uint32_t e1, uint32_t& b0, uint32_t& b1) {
-  const uint32_t ref = w.s_info[src] & 31u;
-  const uint8_t* __restrict__ by = w.bytes;
-  const uint32_t end = w.s_cend[src];
-  if (ref == REF_ANY || ref == REF_JSON) {
-    uint32_t p = w.s_celem[src];
-    bool ok = true;
-    for (uint32_t i = 0; i < e1; ++i) {
-      if (i == e0) b0 = p;
-      if (ref == REF_ANY) {
-        uint32_t steps = 0xFFFFFFFFu;
-        ok = skip_any<32>(by, p, end, steps);
-      } else {
-        const uint32_t k = rd_vu(by, p, end, ok);
-        if (ok) skip_bytes(p, k, end, ok);
-      }
-      if (!ok) return false;
-    }
-    if (e0 == e1) b0 = p;
-    b1 = p;
-    return true;
-  }
-  if (ref == REF_STRING) {
-    uint32_t p = w.s_cpos[src];
-    bool ok = true;
-    rd_vu(by, p, end, ok);  // byte length prefix
-    if (!ok) return false;
-    uint32_t u = 0;  // UTF-16 units before p
-    b0 = e0 == 0 ? p : NONE;
-    while (p < end && u < e1) {
-      const uint32_t c = by[p];
-      const uint32_t n = c < 0x80u ? 1u : c < 0xE0u ? 2u : c < 0xF0u ? 3u : 4u;
-      const uint32_t du = n == 4 ? 2u : 1u;
-      if (u < e0 && u + du > e0) return false;  // a slice through a surrogate pair
-      if (u < e1 && u + du > e1) return false;
-      p += n;
-      u += du;
-      if (u == e0) b0 = p;
-    }
-    b1 = p;
-    return b0 != NONE && u == e1;
-  }
-  b0 = w.s_cpos[src];
-  b1 = end;
-  return true;
-}
-
 // Encodes output struct `o` (segments [a,b)) at position p when WRITE, returns the size
 // (Item.write Y@80416 / GC.write Y@68955 with the writeStructs offset, Y@18809).
 template <bool WRITE>

@@ -96,6 +96,11 @@ enum Buf {
   B_UOWN, B_UFLAG, B_UMIN, B_UCUT, B_UWPRE,
   B_GSTART, B_GCIDX, B_GSRC, B_GFLAGS, B_GORIG, B_GRORIG, B_GLINK, B_GKEY, B_GMAXC, B_GNEXT, B_GOUTID, B_GTMP, B_GTMP2,
   B_KHASH, B_KROOT, B_KWIN, B_KPAR, B_KFLAG, B_SPK,
+  B_USEC, B_USECN,
+  B_LZKEY, B_LZKEYS, B_LZIOTA, B_LZSEC, B_LZRSTART, B_LZPREV, B_LZFIRST, B_LZCAP, B_LZEVBASE, B_LZEVN, B_LZFLAG,
+  B_LZLHI, B_LZLLO, B_EVKIND, B_EVSRC, B_EVCLOCK, B_EVLEN, B_EVSIZE, B_EVPOS, B_BLKSIZE, B_BLKPOS, B_SVC, B_SVK,
+  B_DSMKEY, B_DSMKEYS, B_DSMLEN, B_DSMLENS, B_DSMEND, B_DSMMAX, B_DSMFLAG, B_DSMRID, B_DRCLIENT, B_DRCLOCK, B_DREND,
+  B_DWFLAG, B_DWGID, B_DWGSTART, B_DWSIZE, B_DWPOS,
   B_GRIGHT, B_YKEY, B_YKEYS, B_YSEG, B_YIOTA, B_YLSTART, B_YSTATE, B_YBEFORE, B_YCONFL, B_YSTACK,
   B_OFIRST, B_OCIDX, B_OSIZE, B_OPOS, B_RSEG, B_RLEN, B_RSIZE, B_RPOS, B_OUT, B_SVOUT,
   B_COUNT
@@ -233,8 +238,14 @@ int check(ycrdt_engine* e, Counters& c, const char* where) {
   return YCRDT_OK;
 }
 
-// The whole batched merge. `target` (optional) selects a delta encode against a state vector.
-int run_merge(ycrdt_engine* e, ycrdt_batch* b, const std::unordered_map<uint32_t, uint32_t>* target) {
+struct Decoded {
+  uint32_t nstructs = 0, nsections = 0, nclients = 0, nds = 0;
+  uint64_t nunits = 0;
+};
+
+// K1: decode every update of the batch into the struct SoA (+ client table, delete-set ranges).
+// lazy = mergeUpdates / diffUpdate mode: references stay raw client ids, no client states.
+int run_decode(ycrdt_engine* e, ycrdt_batch* b, bool lazy, Decoded& D) {
   Work& w = e->w;
   auto& V = e->bufs;
   bool ok = true;
@@ -258,6 +269,7 @@ int run_merge(ycrdt_engine* e, ycrdt_batch* b, const std::unordered_map<uint32_t
     w.groups = (const Group*)((const uint8_t*)b->meta.p + o);
   }
   w.ngroups = (uint32_t)b->groups.size();
+  w.lazy = lazy ? 1u : 0u;
   const uint64_t B = (uint64_t)b->nbytes + 64;
   const uint64_t nwords = B / 64 + 2;
   w.cap_structs = (uint32_t)(B / 2 + 64);
@@ -316,6 +328,8 @@ int run_merge(ycrdt_engine* e, ycrdt_batch* b, const std::unordered_map<uint32_t
   w.cl_base = take<uint64_t>(V, B_CLBASE, w.cap_clients + 2, ok);
   w.cl_start = take<uint32_t>(V, B_CLSTART, w.cap_clients + 1, ok);
   w.scratch = take<uint32_t>(V, B_SCRATCH, std::max<uint64_t>({nwords + 2, (uint64_t)w.cap_sections + 2, (uint64_t)nu + 2}), ok);
+  w.usec_start = take<uint32_t>(V, B_USEC, nu + 1, ok);
+  w.usec_n = take<uint32_t>(V, B_USECN, nu + 1, ok);
   if (!ok) return fail(YCRDT_E_DEVICE, "hipMalloc failed (decode workspace)");
   // rocPRIM scratch sized for the largest scan of this batch (units may grow it later)
   {
@@ -350,14 +364,37 @@ int run_merge(ycrdt_engine* e, ycrdt_batch* b, const std::unordered_map<uint32_t
   mark(e, "decode.structs");
   launch_struct_decode(w, nstructs, nsections, nclients, s);
   HIPCHK(hipMemsetAsync(w.cl_start, 0, sizeof(uint32_t) * (nclients + 1), s));
-  launch_states(w, nstructs, nclients, s);
+  if (!lazy) launch_states(w, nstructs, nclients, s);
   rc = check(e, c, "struct decode");
   if (rc) return rc;
   uint64_t nunits = 0;
-  HIPCHK(hipMemcpyAsync(&nunits, w.cl_base + nclients, sizeof(uint64_t), hipMemcpyDeviceToHost, s));
-  HIPCHK(hipStreamSynchronize(s));
+  if (!lazy) {
+    HIPCHK(hipMemcpyAsync(&nunits, w.cl_base + nclients, sizeof(uint64_t), hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+  }
   if (nunits >= 0xF0000000ull) return fail(YCRDT_E_CAPACITY, "more than 2^32 units in one batch");
-  const uint32_t nds = std::min(c.nds, w.cap_ds);
+  D.nstructs = nstructs;
+  D.nsections = nsections;
+  D.nclients = nclients;
+  D.nds = std::min(c.nds, w.cap_ds);
+  D.nunits = nunits;
+  return YCRDT_OK;
+}
+
+// The whole batched merge. `target` (optional) selects a delta encode against a state vector.
+int run_merge(ycrdt_engine* e, ycrdt_batch* b, const std::unordered_map<uint32_t, uint32_t>* target) {
+  Work& w = e->w;
+  auto& V = e->bufs;
+  bool ok = true;
+  hipStream_t s = e->stream;
+  Decoded D;
+  int rc = run_decode(e, b, false, D);
+  if (rc) return rc;
+  Counters c;
+  const uint32_t nstructs = D.nstructs, nclients = D.nclients, nds = D.nds;
+  const uint64_t nunits = D.nunits;
+  const uint64_t B = (uint64_t)b->nbytes + 64;
+  const uint64_t nwords = B / 64 + 2;
   // target state vector → per-client start clocks
   if (target && !target->empty() && nclients) {
     std::vector<uint32_t> vals(nclients), starts(nclients, 0);
@@ -494,6 +531,118 @@ int run_merge(ycrdt_engine* e, ycrdt_batch* b, const std::unordered_map<uint32_t
       e->phase_ms.push_back({e->marks[i].first, (double)t});
     }
   }
+  return YCRDT_OK;
+}
+
+// mergeUpdates (merge = true) or diffUpdate (merge = false, target state vector given) of a
+// staged batch; the encoded update is copied to `out`.
+int run_lazy(ycrdt_engine* e, ycrdt_batch* b, bool merge, const std::vector<std::pair<uint32_t, uint32_t>>& sv,
+             ycrdt_out* out) {
+  Work& w = e->w;
+  auto& V = e->bufs;
+  bool ok = true;
+  hipStream_t s = e->stream;
+  Decoded D;
+  int rc = run_decode(e, b, true, D);
+  if (rc) return rc;
+  Counters c;
+  const uint64_t NSEC = D.nsections + 2, NC = D.nclients + 2;
+  const uint64_t NBLK = (merge ? D.nclients : D.nsections) + 2;
+  const uint64_t SLOTS = 2ull * D.nstructs + 2ull * NBLK + 4;
+  const uint64_t NDS = D.nds + 2;
+  w.lz_key = take<uint64_t>(V, B_LZKEY, NSEC, ok);
+  w.lz_keys = take<uint64_t>(V, B_LZKEYS, NSEC, ok);
+  w.lz_iota = take<uint32_t>(V, B_LZIOTA, NSEC, ok);
+  w.lz_sec = take<uint32_t>(V, B_LZSEC, NSEC, ok);
+  w.lz_rstart = take<uint32_t>(V, B_LZRSTART, NC, ok);
+  w.lz_prev = take<uint32_t>(V, B_LZPREV, NSEC, ok);
+  w.lz_first = take<uint32_t>(V, B_LZFIRST, NSEC, ok);
+  w.lz_cap = take<uint32_t>(V, B_LZCAP, NBLK, ok);
+  w.lz_evbase = take<uint32_t>(V, B_LZEVBASE, NBLK, ok);
+  w.lz_evn = take<uint32_t>(V, B_LZEVN, NBLK, ok);
+  w.lz_flag = take<uint32_t>(V, B_LZFLAG, NSEC, ok);
+  w.lz_leave_hi = take<uint32_t>(V, B_LZLHI, NSEC, ok);
+  w.lz_leave_lo = take<uint32_t>(V, B_LZLLO, NSEC, ok);
+  w.ev_kind = take<uint32_t>(V, B_EVKIND, SLOTS, ok);
+  w.ev_src = take<uint32_t>(V, B_EVSRC, SLOTS, ok);
+  w.ev_clock = take<uint32_t>(V, B_EVCLOCK, SLOTS, ok);
+  w.ev_len = take<uint32_t>(V, B_EVLEN, SLOTS, ok);
+  w.ev_size = take<uint32_t>(V, B_EVSIZE, SLOTS, ok);
+  w.ev_pos = take<uint32_t>(V, B_EVPOS, SLOTS, ok);
+  w.blk_size = take<uint32_t>(V, B_BLKSIZE, NBLK, ok);
+  w.blk_pos = take<uint32_t>(V, B_BLKPOS, NBLK, ok);
+  w.dsm_key = take<uint64_t>(V, B_DSMKEY, NDS, ok);
+  w.dsm_keys = take<uint64_t>(V, B_DSMKEYS, NDS, ok);
+  w.dsm_len = take<uint32_t>(V, B_DSMLEN, NDS, ok);
+  w.dsm_lens = take<uint32_t>(V, B_DSMLENS, NDS, ok);
+  w.dsm_end = take<uint64_t>(V, B_DSMEND, NDS, ok);
+  w.dsm_max = take<uint64_t>(V, B_DSMMAX, NDS, ok);
+  w.dsm_flag = take<uint32_t>(V, B_DSMFLAG, NDS, ok);
+  w.dsm_rid = take<uint32_t>(V, B_DSMRID, NDS, ok);
+  w.dr_client = take<uint32_t>(V, B_DRCLIENT, NDS, ok);
+  w.dr_clock = take<uint32_t>(V, B_DRCLOCK, NDS, ok);
+  w.dr_end = take<uint32_t>(V, B_DREND, NDS, ok);
+  w.dw_flag = take<uint32_t>(V, B_DWFLAG, NDS, ok);
+  w.dw_gid = take<uint32_t>(V, B_DWGID, NDS, ok);
+  w.dw_gstart = take<uint32_t>(V, B_DWGSTART, NDS, ok);
+  w.dw_size = take<uint32_t>(V, B_DWSIZE, NDS, ok);
+  w.dw_pos = take<uint32_t>(V, B_DWPOS, NDS, ok);
+  {
+    size_t tb = prim_tmp_bytes(std::max<uint64_t>({(uint64_t)b->nbytes + 64, SLOTS, NDS, 1024}));
+    w.tmp = take<uint8_t>(V, B_TMP, tb, ok);
+    w.tmp_bytes = V[B_TMP].cap;
+  }
+  uint32_t* svbuf = take<uint32_t>(V, B_SVC, 2 * sv.size() + 2, ok);
+  if (!ok) return fail(YCRDT_E_DEVICE, "hipMalloc failed (lazy merge workspace)");
+  if (merge) {
+    mark(e, "lazy.merge");
+    if (D.nsections) launch_lazy_merge(w, D.nsections, D.nclients, s);
+    else { w.lz_nblk = 0; w.lz_diff = 0; HIPCHK(hipMemsetAsync(w.lz_evbase, 0, sizeof(uint32_t) * 2, s)); }
+  } else {
+    std::vector<uint32_t> h(2 * sv.size() + 2, 0);
+    for (size_t i = 0; i < sv.size(); ++i) { h[i] = sv[i].first; h[sv.size() + i] = sv[i].second; }
+    HIPCHK(hipMemcpyAsync(svbuf, h.data(), sizeof(uint32_t) * h.size(), hipMemcpyHostToDevice, s));
+    w.sv_client = svbuf;
+    w.sv_clock = svbuf + sv.size();
+    w.sv_n = (uint32_t)sv.size();
+    mark(e, "lazy.diff");
+    if (D.nsections) launch_lazy_diff(w, D.nsections, s);
+    else { w.lz_nblk = 0; w.lz_diff = 1; HIPCHK(hipMemsetAsync(w.lz_evbase, 0, sizeof(uint32_t) * 2, s)); }
+  }
+  rc = check(e, c, merge ? "mergeUpdates" : "diffUpdate");
+  if (rc) return rc;
+  mark(e, "lazy.sizes");
+  uint32_t nslots = 0;
+  if (w.lz_nblk) launch_event_sizes(w, s, &nslots);
+  else HIPCHK(hipMemsetAsync(w.ctr->pad, 0, sizeof(uint32_t) * 8, s));
+  const uint32_t nr = launch_ds_runs(w, D.nds, merge, s);
+  const uint32_t dsbytes = launch_ds_write_sizes(w, nr, s);
+  rc = check(e, c, "lazy sizes");
+  if (rc) return rc;
+  uint32_t blk_total = 0;
+  if (w.lz_nblk) {
+    HIPCHK(hipMemcpyAsync(&blk_total, w.blk_pos + w.lz_nblk, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+  }
+  const uint32_t sbytes = vu_size_host(c.pad[0]) + blk_total;
+  const uint32_t total = sbytes + dsbytes;
+  w.out = take<uint8_t>(V, B_OUT, (size_t)total + 16, ok);
+  if (!ok) return fail(YCRDT_E_DEVICE, "hipMalloc failed (output)");
+  mark(e, "lazy.write");
+  if (w.lz_nblk) launch_lazy_write(w, nslots, nr, sbytes, s);
+  else {
+    const uint8_t zero[2] = {0, 0};
+    HIPCHK(hipMemcpyAsync(w.out, zero, 1, hipMemcpyHostToDevice, s));
+    if (nr) launch_lazy_write(w, 0, nr, sbytes, s);
+    else HIPCHK(hipMemcpyAsync(w.out + 1, zero, 1, hipMemcpyHostToDevice, s));
+  }
+  mark(e, "end");
+  HIPCHK(hipEventRecord(e->ev1, s));
+  rc = check(e, c, "lazy write");
+  if (rc) return rc;
+  out->len = total;
+  out->ptr = (uint8_t*)malloc(total ? total : 1);
+  HIPCHK(hipMemcpy(out->ptr, w.out, total, hipMemcpyDeviceToHost));
   return YCRDT_OK;
 }
 
@@ -693,6 +842,44 @@ int ycrdt_batch_result(ycrdt_batch* b, ycrdt_out* update, ycrdt_out* sv) {
     HIPCHK(hipMemcpy(sv->ptr, e->w.sv_out, sv->len, hipMemcpyDeviceToHost));
   }
   return YCRDT_OK;
+}
+
+int ycrdt_merge_updates(ycrdt_engine* e, const ycrdt_buf* ups, size_t n, ycrdt_out* out) {
+  if (!e || !out || (!ups && n)) return fail(YCRDT_E_ARG, "null arg");
+  out->ptr = nullptr;
+  out->len = 0;
+  if (n == 1) {  // mergeUpdatesV2 returns its single input unchanged (Y@39011)
+    out->len = ups[0].len;
+    out->ptr = (uint8_t*)malloc(out->len ? out->len : 1);
+    if (out->len) memcpy(out->ptr, ups[0].ptr, out->len);
+    return YCRDT_OK;
+  }
+  HIPCHK(hipSetDevice(e->device));
+  ycrdt_batch b;
+  b.e = e;
+  int rc = stage(&b, ups, n, nullptr, 0);
+  if (rc == YCRDT_OK) rc = run_lazy(e, &b, true, {}, out);
+  if (b.bytes.p) hipFree(b.bytes.p);
+  if (b.meta.p) hipFree(b.meta.p);
+  return rc;
+}
+
+int ycrdt_diff_update(ycrdt_engine* e, ycrdt_buf update, ycrdt_buf sv, ycrdt_out* out) {
+  if (!e || !out) return fail(YCRDT_E_ARG, "null arg");
+  out->ptr = nullptr;
+  out->len = 0;
+  std::unordered_map<uint32_t, uint32_t> m;
+  if (!parse_sv(sv.ptr, sv.len, m)) return fail(YCRDT_E_DECODE, "Integer out of range! (state vector)");
+  std::vector<std::pair<uint32_t, uint32_t>> v(m.begin(), m.end());
+  std::sort(v.begin(), v.end());
+  HIPCHK(hipSetDevice(e->device));
+  ycrdt_batch b;
+  b.e = e;
+  int rc = stage(&b, &update, 1, nullptr, 0);
+  if (rc == YCRDT_OK) rc = run_lazy(e, &b, false, v, out);
+  if (b.bytes.p) hipFree(b.bytes.p);
+  if (b.meta.p) hipFree(b.meta.p);
+  return rc;
 }
 
 void ycrdt_batch_destroy(ycrdt_batch* b) {

@@ -1,0 +1,535 @@
+// yc_lazy.hip — Y.mergeUpdates / Y.diffUpdate on gfx950 (lazy struct merge; no integration).
+//
+// Restates mergeUpdatesV2 (`ds`, Y@39011) and diffUpdateV2 (`us`, Y@40711) over the struct table
+// decoded by yc_decode.hip in lazy mode (references kept as raw client ids):
+//
+//   mergeUpdates  Yjs re-sorts its readers (one per update) before every step: client desc, clock
+//                 asc, stable. Structs of one client only ever meet structs of the same client,
+//                 so every client is an independent k-way merge — one wavefront per client —
+//                 EXCEPT for the tie order of readers sitting on the same clock: a stable sort
+//                 keeps the previous relative order, and the reader that moved last was the front
+//                 one, so ties go to the most recent arrival (arrival stamp = processing time).
+//                 A reader arrives at its section of client c when it leaves its previous
+//                 section (a higher client, processed earlier), so wavefronts run in client-desc
+//                 order and pick the arrival stamps of their readers up from the wavefronts of
+//                 the higher clients (decoupled look-back: a wave only waits on lower block ids).
+//   diffUpdate    a single reader: per section, the first non-Skip struct ending past the state
+//                 vector is written with an offset, every later struct of the section as is.
+//
+// Both produce "events" (struct, offset, length | GC | Skip) per output client block; a size pass,
+// scans and a write pass encode them with the lazy Item.write rules (parentSub only on items that
+// carry neither origin nor right origin, Y@36564). Delete sets: mergeDeleteSets + sortAndMerge
+// (`he`/`le`, Y@10486) as a sort + segmented running-max scan; diffUpdate copies its input's.
+#include "yc_work.h"
+
+namespace yc {
+
+constexpr uint32_t LZ_KMAX = 1024;  // readers (updates) per client handled in LDS
+constexpr uint32_t END = NONE;
+
+// ---------------------------------------------------------------- section order / reader runs
+// key = (client rank) << 32 | update, rank 0 = the highest client
+__global__ void k_lz_keys(Work w, uint32_t nsections, uint32_t nclients) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= nsections) return;
+  const Section s = w.sections[i];
+  w.lz_key[i] = ((uint64_t)(nclients - 1 - s.cidx) << 32) | s.upd;
+  w.lz_iota[i] = i;
+}
+__global__ void k_lz_runs(Work w, uint32_t nsections, uint32_t nclients) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= nsections) return;
+  const uint64_t k = w.lz_keys[i];
+  const uint32_t r = (uint32_t)(k >> 32);
+  if (i == 0 || (uint32_t)(w.lz_keys[i - 1] >> 32) != r) w.lz_rstart[r] = i;
+  if (i > 0 && w.lz_keys[i - 1] == k) raise_err(&w.ctr->err, ERR_UNSUPPORTED);  // two sections of one client in one update
+  if (i == nsections - 1) w.lz_rstart[nclients] = nsections;
+}
+// one lane per update: previous non-empty section (arrival source), client-desc check
+__device__ __forceinline__ uint32_t first_nonskip(const Work& w, uint32_t a, uint32_t n) {
+  for (uint32_t j = a; j < a + n; ++j)
+    if ((w.s_info[j] & 31u) != REF_SKIP) return j;
+  return END;
+}
+__global__ void k_lz_prev(Work w, uint32_t nupd) {
+  const uint32_t u = blockIdx.x * blockDim.x + threadIdx.x;
+  if (u >= nupd) return;
+  const uint32_t a = w.usec_start[u], b = a + w.usec_n[u];
+  uint32_t prev = NONE;
+  for (uint32_t i = a; i < b; ++i) {
+    const Section s = w.sections[i];
+    if (i > a && s.client >= w.sections[i - 1].client && s.n > 0) raise_err(&w.ctr->err, ERR_UNSUPPORTED);
+    w.lz_prev[i] = prev;
+    const uint32_t f = s.n ? first_nonskip(w, s.first_idx, s.n) : END;
+    w.lz_first[i] = f;
+    if (f != END) prev = i;
+  }
+}
+// per client: event capacity (every advance emits at most one struct and one Skip)
+__global__ void k_lz_cap(Work w, uint32_t nclients) {
+  const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r > nclients) return;
+  if (r == nclients) { w.lz_cap[r] = 0; return; }
+  uint32_t tot = 0;
+  for (uint32_t i = w.lz_rstart[r]; i < w.lz_rstart[r + 1]; ++i) tot += w.sections[w.lz_sec[i]].n;
+  w.lz_cap[r] = 2 * tot + 2;
+}
+
+// ---------------------------------------------------------------- the per-client lazy merge
+struct Cur {
+  uint32_t kind;   // REF_GC, REF_SKIP or 1 (item)
+  uint32_t src;    // source struct (items)
+  uint32_t clock;  // first clock (source clock + offset)
+  uint32_t len;
+};
+
+__global__ __launch_bounds__(64) void k_lz_merge(Work w, uint32_t nclients) {
+  __shared__ uint32_t rcur[LZ_KMAX], rend[LZ_KMAX], rhi[LZ_KMAX], rlo[LZ_KMAX];
+  const uint32_t r = blockIdx.x;  // client rank (descending client order)
+  const uint32_t lane = threadIdx.x;
+  const uint32_t a = w.lz_rstart[r], K = w.lz_rstart[r + 1] - a;
+  const uint32_t base = w.lz_evbase[r];
+  const uint32_t cap = w.lz_cap[r];
+  bool fail = K > LZ_KMAX;
+  if (fail && lane == 0) raise_err(&w.ctr->err, ERR_CAPACITY);
+  // ---- readers: first struct + arrival stamp (look back to the previous section's wave)
+  for (uint32_t k = lane; k < K && !fail; k += 64) {
+    const uint32_t sec = w.lz_sec[a + k];
+    const Section S = w.sections[sec];
+    rcur[k] = w.lz_first[sec];
+    rend[k] = S.first_idx + S.n;
+    const uint32_t p = w.lz_prev[sec];
+    if (p == NONE) { rhi[k] = 0; rlo[k] = 0xFFFFFFFFu - S.upd; }  // never moved: update order
+    else {
+      uint32_t spins = 0;
+      while (__hip_atomic_load(&w.lz_flag[p], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) == 0) {
+        __builtin_amdgcn_s_sleep(2);
+        if (++spins > (1u << 24)) { raise_err(&w.ctr->err, ERR_CAPACITY); break; }
+      }
+      rhi[k] = w.lz_leave_hi[p];
+      rlo[k] = w.lz_leave_lo[p];
+    }
+  }
+  __syncthreads();
+  const uint32_t rank_stamp = r + 1;
+  uint32_t step = 0, evn = 0;
+  Cur cur{0, NONE, 0, 0};
+  bool have = false;
+  auto emit = [&](const Cur& c) {
+    if (evn < cap) {
+      if (lane == 0) {
+        w.ev_kind[base + evn] = c.kind;
+        w.ev_src[base + evn] = c.src;
+        w.ev_clock[base + evn] = c.clock;
+        w.ev_len[base + evn] = c.len;
+      }
+      ++evn;
+    } else if (lane == 0) raise_err(&w.ctr->err, ERR_CAPACITY);
+  };
+  auto advance = [&](uint32_t t) {
+    uint32_t c = rcur[t] + 1;
+    const uint32_t e = rend[t];
+    while (c < e && (w.s_info[c] & 31u) == REF_SKIP) ++c;
+    ++step;
+    __syncthreads();
+    if (lane == 0) {
+      rcur[t] = c < e ? c : END;
+      rhi[t] = rank_stamp;
+      rlo[t] = step;
+    }
+    __syncthreads();
+  };
+  auto kind_of = [&](uint32_t s) -> uint32_t {
+    const uint32_t ref = w.s_info[s] & 31u;
+    return ref == REF_GC ? (uint32_t)REF_GC : ref == REF_SKIP ? (uint32_t)REF_SKIP : 1u;
+  };
+  const uint32_t max_iter = 4 * cap + 16;
+  for (uint32_t it = 0; !fail; ++it) {
+    if (it > max_iter) { if (lane == 0) raise_err(&w.ctr->err, ERR_CAPACITY); break; }
+    // front reader: min (clock), ties → latest arrival (max stamp)
+    uint32_t bk = NONE, bc = 0xFFFFFFFFu, bh = 0, bl = 0;
+    for (uint32_t k = lane; k < K; k += 64) {
+      const uint32_t s = rcur[k];
+      if (s == END) continue;
+      const uint32_t c = w.s_clock[s], h = rhi[k], l = rlo[k];
+      if (bk == NONE || c < bc || (c == bc && (h > bh || (h == bh && l > bl)))) { bk = k; bc = c; bh = h; bl = l; }
+    }
+    for (int off = 32; off > 0; off >>= 1) {
+      const uint32_t ok = __shfl_xor(bk, off), oc = __shfl_xor(bc, off), oh = __shfl_xor(bh, off), ol = __shfl_xor(bl, off);
+      if (ok != NONE && (bk == NONE || oc < bc || (oc == bc && (oh > bh || (oh == bh && ol > bl))))) { bk = ok; bc = oc; bh = oh; bl = ol; }
+    }
+    if (bk == NONE) break;  // every reader of this client is exhausted
+    const uint32_t t = bk;
+    uint32_t n = rcur[t];
+    if (have) {
+      bool skipped = false;
+      const uint32_t cend = cur.clock + cur.len;
+      while (n != END && w.s_clock[n] + w.s_len[n] <= cend) { advance(t); n = rcur[t]; skipped = true; }
+      if (n == END || (skipped && w.s_clock[n] > cend)) continue;
+      const uint32_t nclock = w.s_clock[n], nlen = w.s_len[n];
+      if (cend < nclock) {  // gap
+        if (cur.kind == REF_SKIP) cur.len = nclock + nlen - cur.clock;
+        else { emit(cur); cur = Cur{REF_SKIP, NONE, cend, nclock - cend}; }
+      } else {
+        const uint32_t diff = cend - nclock;
+        Cur nn{kind_of(n), n, nclock, nlen};
+        if (diff > 0) {
+          if (cur.kind == REF_SKIP) cur.len -= diff;
+          else { nn.clock += diff; nn.len -= diff; }  // sliceStruct
+        }
+        if (cur.kind == nn.kind && cur.kind != 1u) cur.len += nn.len;  // GC / Skip mergeWith
+        else { emit(cur); cur = nn; advance(t); }
+      }
+    } else {
+      cur = Cur{kind_of(n), n, w.s_clock[n], w.s_len[n]};
+      have = true;
+      advance(t);
+    }
+    // consecutive structs of the same reader are written without re-sorting
+    n = rcur[t];
+    while (n != END && w.s_clock[n] == cur.clock + cur.len && kind_of(n) != REF_SKIP) {
+      emit(cur);
+      cur = Cur{kind_of(n), n, w.s_clock[n], w.s_len[n]};
+      advance(t);
+      n = rcur[t];
+    }
+  }
+  if (have && !fail) emit(cur);
+  if (lane == 0) w.lz_evn[r] = evn;
+  // ---- publish the leave stamps of this client's sections
+  __syncthreads();
+  for (uint32_t k = lane; k < K && k < LZ_KMAX; k += 64) {
+    const uint32_t sec = w.lz_sec[a + k];
+    w.lz_leave_hi[sec] = rhi[k];
+    w.lz_leave_lo[sec] = rlo[k];
+    __hip_atomic_store(&w.lz_flag[sec], 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  if (fail) {  // never leave a dependent wave spinning
+    for (uint32_t k = lane; k < K; k += 64) __hip_atomic_store(&w.lz_flag[w.lz_sec[a + k]], 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
+// ---------------------------------------------------------------- diffUpdate events
+// one lane per section: the section's events live at lz_evbase[section]
+__global__ void k_lz_diff(Work w, uint32_t nsections) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= nsections) return;
+  const Section S = w.sections[i];
+  const uint32_t base = w.lz_evbase[i];
+  uint32_t svc = 0;  // target state of this client
+  {
+    uint32_t lo = 0, hi = w.sv_n;
+    while (lo < hi) { const uint32_t m = (lo + hi) >> 1; if (w.sv_client[m] < S.client) lo = m + 1; else hi = m; }
+    if (lo < w.sv_n && w.sv_client[lo] == S.client) svc = w.sv_clock[lo];
+  }
+  uint32_t evn = 0;
+  // first struct (non-Skip) that ends past the target state: binary search on the clocks
+  uint32_t lo = S.first_idx, hi = S.first_idx + S.n;
+  while (lo < hi) { const uint32_t m = (lo + hi) >> 1; if (w.s_clock[m] + w.s_len[m] <= svc) lo = m + 1; else hi = m; }
+  while (lo < S.first_idx + S.n && (w.s_info[lo] & 31u) == REF_SKIP) ++lo;
+  for (uint32_t j = lo; j < S.first_idx + S.n; ++j) {
+    const uint32_t ref = w.s_info[j] & 31u;
+    const uint32_t off = (j == lo && svc > w.s_clock[j]) ? svc - w.s_clock[j] : 0u;
+    w.ev_kind[base + evn] = ref == REF_GC ? (uint32_t)REF_GC : ref == REF_SKIP ? (uint32_t)REF_SKIP : 1u;
+    w.ev_src[base + evn] = j;
+    w.ev_clock[base + evn] = w.s_clock[j] + off;
+    w.ev_len[base + evn] = w.s_len[j] - off;
+    ++evn;
+  }
+  w.lz_evn[i] = evn;
+}
+__global__ void k_lz_diff_cap(Work w, uint32_t nsections) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i > nsections) return;
+  w.lz_cap[i] = i < nsections ? w.sections[i].n : 0u;
+}
+
+// ---------------------------------------------------------------- event encoding
+// Lazy Item.write (Y@80416 on a lazily read item): parentSub survives only on items that carry
+// neither origin nor right origin; an offset > 0 turns the origin into (client, clock + off - 1).
+template <bool WRITE>
+__device__ uint32_t encode_event(const Work& w, uint32_t client, uint32_t e, uint8_t* __restrict__ out, uint32_t p0) {
+  const uint32_t kind = w.ev_kind[e], len = w.ev_len[e];
+  uint32_t p = p0;
+  if (kind != 1u) {
+    if (WRITE) { out[p++] = (uint8_t)kind; p = wr_vu(out, p, len); return p - p0; }
+    return 1 + vu_size(len);
+  }
+  const uint32_t src = w.ev_src[e];
+  const uint32_t info0 = w.s_info[src];
+  const uint32_t ref = info0 & 31u;
+  const uint32_t off = w.ev_clock[e] - w.s_clock[src];
+  const bool root = (info0 & 0xC0u) == 0;
+  const bool has_o = off > 0 || (info0 & 0x80u);
+  const bool has_r = (info0 & 0x40u) != 0;
+  const bool psub = root && (info0 & 0x20u);
+  const uint32_t oc = off > 0 ? client : w.s_ocidx[src], ok = off > 0 ? w.s_clock[src] + off - 1 : w.s_oclock[src];
+  uint32_t size = 1;
+  if (WRITE) out[p++] = (uint8_t)(ref | (has_o ? 0x80u : 0u) | (has_r ? 0x40u : 0u) | (psub ? 0x20u : 0u));
+  if (has_o) {
+    if (WRITE) { p = wr_vu(out, p, oc); p = wr_vu(out, p, ok); }
+    size += vu_size(oc) + vu_size(ok);
+  }
+  if (has_r) {
+    const uint32_t rc = w.s_rcidx[src], rk = w.s_rclock[src];
+    if (WRITE) { p = wr_vu(out, p, rc); p = wr_vu(out, p, rk); }
+    size += vu_size(rc) + vu_size(rk);
+  }
+  if (!has_o && !has_r) {
+    const uint32_t pa = w.s_pa[src], pb = w.s_pb[src];
+    if (w.s_pk[src] == 1) {
+      if (WRITE) { out[p++] = 1; for (uint32_t i = 0; i < pb; ++i) out[p++] = w.bytes[pa + i]; }
+      size += 1 + pb;
+    } else {
+      if (WRITE) { out[p++] = 0; p = wr_vu(out, p, pa); p = wr_vu(out, p, pb); }
+      size += 1 + vu_size(pa) + vu_size(pb);
+    }
+    if (psub) {
+      const uint32_t ps = w.s_psub[src], pl = w.s_psublen[src];
+      if (WRITE) for (uint32_t i = 0; i < pl; ++i) out[p++] = w.bytes[ps + i];
+      size += pl;
+    }
+  }
+  if (ref == REF_DELETED) {
+    if (WRITE) p = wr_vu(out, p, len);
+    size += vu_size(len);
+  } else if (ref == REF_ANY || ref == REF_JSON || ref == REF_STRING) {
+    uint32_t b0 = 0, b1 = 0;
+    if (!content_slice(w, src, off, off + len, b0, b1)) { raise_err(&w.ctr->err, ERR_UNSUPPORTED); return size; }
+    const uint32_t pre = ref == REF_STRING ? b1 - b0 : len;
+    if (WRITE) { p = wr_vu(out, p, pre); for (uint32_t i = b0; i < b1; ++i) out[p++] = w.bytes[i]; }
+    size += vu_size(pre) + (b1 - b0);
+  } else {
+    const uint32_t n = w.s_cend[src] - w.s_cpos[src];
+    if (WRITE) for (uint32_t i = 0; i < n; ++i) out[p++] = w.bytes[w.s_cpos[src] + i];
+    size += n;
+  }
+  return size;
+}
+
+// block b (client rank for merge, section for diff): its client id
+__device__ __forceinline__ uint32_t blk_client(const Work& w, uint32_t b) {
+  return w.lz_diff ? w.sections[b].client : w.cl_vals[w.lz_nblk - 1 - b];
+}
+// event slots [evbase[b], evbase[b] + cap[b]); slots past evn[b] are empty
+__global__ __launch_bounds__(256) void k_ev_sizes(Work w, uint32_t nslots) {
+  const uint32_t e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e > nslots) return;
+  if (e == nslots) { w.ev_size[e] = 0; return; }
+  const uint32_t b = upper_bound_u32(w.lz_evbase, w.lz_nblk, e) - 1;
+  w.ev_size[e] = (e - w.lz_evbase[b] < w.lz_evn[b]) ? encode_event<false>(w, blk_client(w, b), e, nullptr, 0) : 0u;
+}
+__global__ void k_blk_sizes(Work w, uint32_t nblk) {
+  const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b > nblk) return;
+  if (b == nblk) { w.blk_size[b] = 0; return; }
+  const uint32_t n = w.lz_evn[b];
+  uint32_t sz = 0;
+  if (n) {
+    const uint32_t e0 = w.lz_evbase[b];
+    sz = vu_size(n) + vu_size(blk_client(w, b)) + vu_size(w.ev_clock[e0]) + (w.ev_pos[e0 + n] - w.ev_pos[e0]);
+    atomicAdd(&w.ctr->pad[0], 1u);
+  }
+  w.blk_size[b] = sz;
+}
+__global__ __launch_bounds__(256) void k_ev_write(Work w, uint32_t nslots) {
+  const uint32_t e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= nslots) return;
+  const uint32_t b = upper_bound_u32(w.lz_evbase, w.lz_nblk, e) - 1;
+  const uint32_t e0 = w.lz_evbase[b], n = w.lz_evn[b];
+  if (e - e0 >= n) return;
+  const uint32_t client = blk_client(w, b);
+  const uint32_t hdr = vu_size(n) + vu_size(client) + vu_size(w.ev_clock[e0]);
+  const uint32_t p = vu_size(w.ctr->pad[0]) + w.blk_pos[b] + hdr + (w.ev_pos[e] - w.ev_pos[e0]);
+  encode_event<true>(w, client, e, w.out, p);
+}
+__global__ void k_blk_write(Work w, uint32_t nblk) {
+  const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b == 0) wr_vu(w.out, 0, w.ctr->pad[0]);
+  if (b >= nblk) return;
+  const uint32_t n = w.lz_evn[b];
+  if (!n) return;
+  uint32_t p = vu_size(w.ctr->pad[0]) + w.blk_pos[b];
+  p = wr_vu(w.out, p, n);
+  p = wr_vu(w.out, p, blk_client(w, b));
+  wr_vu(w.out, p, w.ev_clock[w.lz_evbase[b]]);
+}
+
+// ---------------------------------------------------------------- delete sets
+// merge: sort (client desc, clock asc), running max of range ends per client, runs
+__global__ void k_dsm_keys(Work w, uint32_t nds) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= nds) return;
+  const DsRange d = w.ds[i];
+  w.dsm_key[i] = ((uint64_t)(~d.client) << 32) | d.clock;
+  w.dsm_len[i] = d.len;
+}
+__global__ void k_dsm_ends(Work w, uint32_t nds) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= nds) return;
+  const uint64_t k = w.dsm_keys[i];
+  w.dsm_end[i] = (k & 0xFFFFFFFF00000000ull) | (uint64_t)((uint32_t)k + w.dsm_lens[i]);
+}
+// run starts (sortAndMergeDeleteSet: merge while s.clock + s.len >= r.clock)
+__global__ void k_dsm_flags(Work w, uint32_t nds) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i > nds) return;
+  if (i == nds) { w.dsm_flag[i] = 0; return; }
+  const uint64_t k = w.dsm_keys[i];
+  bool st = i == 0 || (w.dsm_keys[i - 1] >> 32) != (k >> 32) || (uint32_t)w.dsm_max[i - 1] < (uint32_t)k;
+  w.dsm_flag[i] = st ? 1u : 0u;
+}
+__global__ void k_dsm_runs(Work w, uint32_t nds) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= nds) return;
+  const uint32_t rid = w.dsm_rid[i] + w.dsm_flag[i] - 1;  // inclusive count of run starts - 1
+  const uint64_t k = w.dsm_keys[i];
+  if (w.dsm_flag[i]) { w.dr_client[rid] = ~(uint32_t)(k >> 32); w.dr_clock[rid] = (uint32_t)k; }
+  if (i + 1 == nds || w.dsm_flag[i + 1]) w.dr_end[rid] = (uint32_t)w.dsm_max[i];
+}
+// diff: the input's ranges unmerged, clients in descending order (13.6 canonical), wire order
+// within a client
+__global__ void k_dsd_keys(Work w, uint32_t nds) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= nds) return;
+  w.dsm_key[i] = ((uint64_t)(~w.ds[i].client) << 32) | i;
+  w.dsm_len[i] = i;
+}
+__global__ void k_dsd_runs(Work w, uint32_t nds) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= nds) return;
+  const DsRange d = w.ds[w.dsm_lens[i]];
+  w.dr_client[i] = d.client;
+  w.dr_clock[i] = d.clock;
+  w.dr_end[i] = d.clock + d.len;
+}
+
+// writeDeleteSet (Y@11105 `fe`): runs grouped by client in output order
+__global__ void k_dw_flags(Work w, uint32_t nr) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i > nr) return;
+  w.dw_flag[i] = (i < nr && (i == 0 || w.dr_client[i] != w.dr_client[i - 1])) ? 1u : 0u;
+}
+__global__ void k_dw_gstart(Work w, uint32_t nr) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= nr) return;
+  if (w.dw_flag[i]) w.dw_gstart[w.dw_gid[i]] = i;
+  if (i == nr - 1) w.dw_gstart[w.dw_gid[nr]] = nr;
+}
+__global__ void k_dw_sizes(Work w, uint32_t nr) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i > nr) return;
+  if (i == nr) { w.dw_size[i] = 0; return; }
+  const uint32_t clock = w.dr_clock[i], len = w.dr_end[i] - clock;
+  uint32_t sz = vu_size(clock) + vu_size(len);
+  if (w.dw_flag[i]) {
+    const uint32_t g = w.dw_gid[i];
+    sz += vu_size(w.dr_client[i]) + vu_size(w.dw_gstart[g + 1] - w.dw_gstart[g]);
+  }
+  w.dw_size[i] = sz;
+}
+__global__ void k_dw_write(Work w, uint32_t nr, uint32_t dsbase) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t ng = w.dw_gid[nr];
+  if (i == 0) wr_vu(w.out, dsbase, ng);
+  if (i >= nr) return;
+  uint32_t p = dsbase + vu_size(ng) + w.dw_pos[i];
+  if (w.dw_flag[i]) {
+    const uint32_t g = w.dw_gid[i];
+    p = wr_vu(w.out, p, w.dr_client[i]);
+    p = wr_vu(w.out, p, w.dw_gstart[g + 1] - w.dw_gstart[g]);
+  }
+  const uint32_t clock = w.dr_clock[i];
+  p = wr_vu(w.out, p, clock);
+  wr_vu(w.out, p, w.dr_end[i] - clock);
+}
+
+// ---------------------------------------------------------------- host side
+static inline uint32_t G(uint64_t n) { return (uint32_t)(n / 256 + 1); }
+
+// Reader order + per-client merge (mergeUpdates) → events
+void launch_lazy_merge(Work& w, uint32_t nsections, uint32_t nclients, hipStream_t s) {
+  w.lz_diff = 0;
+  w.lz_nblk = nclients;
+  hipLaunchKernelGGL(k_lz_keys, dim3(G(nsections)), dim3(256), 0, s, w, nsections, nclients);
+  sort_pairs_u64_u32(w.tmp, w.tmp_bytes, w.lz_key, w.lz_keys, w.lz_iota, w.lz_sec, nsections, s);
+  hipLaunchKernelGGL(k_lz_runs, dim3(G(nsections)), dim3(256), 0, s, w, nsections, nclients);
+  hipLaunchKernelGGL(k_lz_prev, dim3(G(w.nupd)), dim3(256), 0, s, w, w.nupd);
+  hipLaunchKernelGGL(k_lz_cap, dim3(G(nclients + 1)), dim3(256), 0, s, w, nclients);
+  scan_u32(w.tmp, w.tmp_bytes, w.lz_cap, w.lz_evbase, nclients + 1, s);
+  hipMemsetAsync(w.lz_flag, 0, sizeof(uint32_t) * (nsections + 1), s);
+  hipLaunchKernelGGL(k_lz_merge, dim3(nclients), dim3(64), 0, s, w, nclients);
+}
+
+// diffUpdate: one block per section of the single input update
+void launch_lazy_diff(Work& w, uint32_t nsections, hipStream_t s) {
+  w.lz_diff = 1;
+  w.lz_nblk = nsections;
+  hipLaunchKernelGGL(k_lz_diff_cap, dim3(G(nsections + 1)), dim3(256), 0, s, w, nsections);
+  scan_u32(w.tmp, w.tmp_bytes, w.lz_cap, w.lz_evbase, nsections + 1, s);
+  hipLaunchKernelGGL(k_lz_diff, dim3(G(nsections)), dim3(256), 0, s, w, nsections);
+}
+
+// events → struct-section sizes (returns total via counters: pad[0] = non-empty blocks)
+uint32_t launch_event_sizes(Work& w, hipStream_t s, uint32_t* nslots_out) {
+  uint32_t nslots = 0;
+  hipMemcpyAsync(&nslots, w.lz_evbase + w.lz_nblk, sizeof(uint32_t), hipMemcpyDeviceToHost, s);
+  hipStreamSynchronize(s);
+  *nslots_out = nslots;
+  hipMemsetAsync(w.ctr->pad, 0, sizeof(uint32_t) * 8, s);
+  hipLaunchKernelGGL(k_ev_sizes, dim3(G(nslots + 1)), dim3(256), 0, s, w, nslots);
+  scan_u32(w.tmp, w.tmp_bytes, w.ev_size, w.ev_pos, nslots + 1, s);
+  hipLaunchKernelGGL(k_blk_sizes, dim3(G(w.lz_nblk + 1)), dim3(256), 0, s, w, w.lz_nblk);
+  scan_u32(w.tmp, w.tmp_bytes, w.blk_size, w.blk_pos, w.lz_nblk + 1, s);
+  return nslots;
+}
+
+// delete-set runs: merge (union of all inputs) or diff (the input's own)
+uint32_t launch_ds_runs(Work& w, uint32_t nds, bool merge, hipStream_t s) {
+  if (!nds) return 0;
+  if (!merge) {
+    hipLaunchKernelGGL(k_dsd_keys, dim3(G(nds)), dim3(256), 0, s, w, nds);
+    sort_pairs_u64_u32(w.tmp, w.tmp_bytes, w.dsm_key, w.dsm_keys, w.dsm_len, w.dsm_lens, nds, s);
+    hipLaunchKernelGGL(k_dsd_runs, dim3(G(nds)), dim3(256), 0, s, w, nds);
+    return nds;
+  }
+  hipLaunchKernelGGL(k_dsm_keys, dim3(G(nds)), dim3(256), 0, s, w, nds);
+  sort_pairs_u64_u32(w.tmp, w.tmp_bytes, w.dsm_key, w.dsm_keys, w.dsm_len, w.dsm_lens, nds, s);
+  hipLaunchKernelGGL(k_dsm_ends, dim3(G(nds)), dim3(256), 0, s, w, nds);
+  scan_segmax_u64(w.tmp, w.tmp_bytes, w.dsm_end, w.dsm_max, nds, s);
+  hipLaunchKernelGGL(k_dsm_flags, dim3(G(nds + 1)), dim3(256), 0, s, w, nds);
+  scan_u32(w.tmp, w.tmp_bytes, w.dsm_flag, w.dsm_rid, nds + 1, s);
+  hipLaunchKernelGGL(k_dsm_runs, dim3(G(nds)), dim3(256), 0, s, w, nds);
+  uint32_t nr = 0;
+  hipMemcpyAsync(&nr, w.dsm_rid + nds, sizeof(uint32_t), hipMemcpyDeviceToHost, s);
+  hipStreamSynchronize(s);
+  return nr;
+}
+
+// delete-set sizes (returns the encoded DS byte count)
+uint32_t launch_ds_write_sizes(Work& w, uint32_t nr, hipStream_t s) {
+  if (!nr) return 1;  // varuint 0
+  hipLaunchKernelGGL(k_dw_flags, dim3(G(nr + 1)), dim3(256), 0, s, w, nr);
+  scan_u32(w.tmp, w.tmp_bytes, w.dw_flag, w.dw_gid, nr + 1, s);
+  hipLaunchKernelGGL(k_dw_gstart, dim3(G(nr)), dim3(256), 0, s, w, nr);
+  hipLaunchKernelGGL(k_dw_sizes, dim3(G(nr + 1)), dim3(256), 0, s, w, nr);
+  scan_u32(w.tmp, w.tmp_bytes, w.dw_size, w.dw_pos, nr + 1, s);
+  uint32_t v[2] = {0, 0};
+  hipMemcpyAsync(&v[0], w.dw_gid + nr, sizeof(uint32_t), hipMemcpyDeviceToHost, s);
+  hipMemcpyAsync(&v[1], w.dw_pos + nr, sizeof(uint32_t), hipMemcpyDeviceToHost, s);
+  hipStreamSynchronize(s);
+  return vu_size_host(v[0]) + v[1];
+}
+
+void launch_lazy_write(Work& w, uint32_t nslots, uint32_t nr, uint32_t dsbase, hipStream_t s) {
+  hipLaunchKernelGGL(k_blk_write, dim3(G(w.lz_nblk)), dim3(256), 0, s, w, w.lz_nblk);
+  if (nslots) hipLaunchKernelGGL(k_ev_write, dim3(G(nslots)), dim3(256), 0, s, w, nslots);
+  if (nr) hipLaunchKernelGGL(k_dw_write, dim3(G(nr)), dim3(256), 0, s, w, nr, dsbase);
+  else {
+    const uint8_t zero = 0;
+    hipMemcpyAsync(w.out + dsbase, &zero, 1, hipMemcpyHostToDevice, s);
+    hipStreamSynchronize(s);
+  }
+}
+
+}  // namespace yc

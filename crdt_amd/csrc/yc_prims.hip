@@ -6,6 +6,12 @@
 
 namespace yc {
 
+struct SegMax64 {  // max of packed (segment << 32 | value) within a segment; a new segment restarts
+  __host__ __device__ uint64_t operator()(uint64_t a, uint64_t b) const {
+    return (a >> 32) == (b >> 32) ? (a > b ? a : b) : b;
+  }
+};
+
 size_t prim_tmp_bytes(uint64_t n) {
   size_t a = 0, b = 0, c = 0;
   rocprim::exclusive_scan(nullptr, a, (const uint32_t*)nullptr, (uint32_t*)nullptr, 0u, (size_t)n, rocprim::plus<uint32_t>());
@@ -14,9 +20,15 @@ size_t prim_tmp_bytes(uint64_t n) {
   size_t d = 0;
   rocprim::radix_sort_pairs(nullptr, d, (const uint32_t*)nullptr, (uint32_t*)nullptr, (const uint32_t*)nullptr,
                             (uint32_t*)nullptr, (size_t)n, 0, 32);
+  size_t e = 0, f = 0;
+  rocprim::radix_sort_pairs(nullptr, e, (const uint64_t*)nullptr, (uint64_t*)nullptr, (const uint32_t*)nullptr,
+                            (uint32_t*)nullptr, (size_t)n, 0, 64);
+  rocprim::inclusive_scan(nullptr, f, (const uint64_t*)nullptr, (uint64_t*)nullptr, (size_t)n, SegMax64());
   size_t m = a > b ? a : b;
   m = m > c ? m : c;
-  return (m > d ? m : d) + 256;
+  m = m > d ? m : d;
+  m = m > e ? m : e;
+  return (m > f ? m : f) + 256;
 }
 
 void scan_u32(void* tmp, size_t tmpb, const uint32_t* in, uint32_t* out, uint64_t n, hipStream_t s) {
@@ -38,6 +50,17 @@ void sort_pairs_u32(void* tmp, size_t tmpb, const uint32_t* kin, uint32_t* kout,
                     uint64_t n, hipStream_t s) {
   if (!n) return;
   rocprim::radix_sort_pairs(tmp, tmpb, kin, kout, vin, vout, (size_t)n, 0, 32, s);
+}
+
+void sort_pairs_u64_u32(void* tmp, size_t tmpb, const uint64_t* kin, uint64_t* kout, const uint32_t* vin, uint32_t* vout,
+                        uint64_t n, hipStream_t s) {
+  if (!n) return;
+  rocprim::radix_sort_pairs(tmp, tmpb, kin, kout, vin, vout, (size_t)n, 0, 64, s);
+}
+
+void scan_segmax_u64(void* tmp, size_t tmpb, const uint64_t* in, uint64_t* out, uint64_t n, hipStream_t s) {
+  if (!n) return;
+  rocprim::inclusive_scan(tmp, tmpb, in, out, (size_t)n, SegMax64(), s);
 }
 
 }  // namespace yc

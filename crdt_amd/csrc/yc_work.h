@@ -58,6 +58,7 @@ struct Work {
   const uint32_t* ulen = nullptr;  // [nupd] real update lengths
   const uint32_t* ugroup = nullptr;// [nupd] first decode group of each update
   uint32_t nupd = 0;
+  uint32_t lazy = 0;               // 1: mergeUpdates / diffUpdate decode (references kept raw)
   const Group* groups = nullptr;   // [G]
   uint32_t ngroups = 0;
   // ---- capacities
@@ -147,6 +148,50 @@ struct Work {
   uint32_t* y_before = nullptr;    // [NS]
   uint32_t* y_confl = nullptr;     // [NS]
   uint32_t* y_stack = nullptr;     // [NS]
+  // ---- lazy merge (mergeUpdates / diffUpdate, yc_lazy.hip)
+  uint32_t* usec_start = nullptr;  // [nupd] first section of every update (walker order)
+  uint32_t* usec_n = nullptr;      // [nupd] sections of every update
+  uint64_t* lz_key = nullptr;      // [sections] (client rank, update)
+  uint64_t* lz_keys = nullptr;     // sorted
+  uint32_t* lz_iota = nullptr;
+  uint32_t* lz_sec = nullptr;      // sections sorted by (client desc, update)
+  uint32_t* lz_rstart = nullptr;   // [NC+1] readers of every client rank
+  uint32_t* lz_prev = nullptr;     // [sections] previous non-empty section of the same update
+  uint32_t* lz_first = nullptr;    // [sections] first non-Skip struct
+  uint32_t* lz_cap = nullptr;      // [blocks+1] event slots per output block
+  uint32_t* lz_evbase = nullptr;   // [blocks+1] exclusive scan of lz_cap
+  uint32_t* lz_evn = nullptr;      // [blocks] events emitted
+  uint32_t* lz_flag = nullptr;     // [sections] leave stamp published
+  uint32_t* lz_leave_hi = nullptr; // [sections] leave stamp (client rank + 1, step)
+  uint32_t* lz_leave_lo = nullptr;
+  uint32_t lz_nblk = 0, lz_diff = 0;
+  uint32_t* ev_kind = nullptr;     // [slots] REF_GC | REF_SKIP | 1 (item)
+  uint32_t* ev_src = nullptr;
+  uint32_t* ev_clock = nullptr;
+  uint32_t* ev_len = nullptr;
+  uint32_t* ev_size = nullptr;     // [slots+1]
+  uint32_t* ev_pos = nullptr;      // [slots+1]
+  uint32_t* blk_size = nullptr;    // [blocks+1]
+  uint32_t* blk_pos = nullptr;     // [blocks+1]
+  const uint32_t* sv_client = nullptr;  // diff target state vector, sorted by client
+  const uint32_t* sv_clock = nullptr;
+  uint32_t sv_n = 0;
+  uint64_t* dsm_key = nullptr;     // [ds] (~client, clock)
+  uint64_t* dsm_keys = nullptr;
+  uint32_t* dsm_len = nullptr;
+  uint32_t* dsm_lens = nullptr;
+  uint64_t* dsm_end = nullptr;     // (~client, clock + len)
+  uint64_t* dsm_max = nullptr;     // segmented running max
+  uint32_t* dsm_flag = nullptr;    // [ds+1]
+  uint32_t* dsm_rid = nullptr;     // [ds+1]
+  uint32_t* dr_client = nullptr;   // [runs] delete-set runs in output order
+  uint32_t* dr_clock = nullptr;
+  uint32_t* dr_end = nullptr;
+  uint32_t* dw_flag = nullptr;     // [runs+1]
+  uint32_t* dw_gid = nullptr;      // [runs+1]
+  uint32_t* dw_gstart = nullptr;   // [runs+1]
+  uint32_t* dw_size = nullptr;     // [runs+1]
+  uint32_t* dw_pos = nullptr;      // [runs+1]
   // ---- encode (NO <= NS)
   uint32_t* o_first = nullptr;     // [NO+1] first segment of output struct (+ sentinel)
   uint32_t* o_cidx = nullptr;      // client of output struct
@@ -166,6 +211,56 @@ struct Work {
   void* tmp = nullptr;
   size_t tmp_bytes = 0;
 };
+
+// Byte range of content elements [e0, e1) of struct `src` (ContentAny: lib0 `any` values,
+// ContentJSON: varStrings, ContentString: UTF-16 code units of the UTF-8 text; every other
+// content has length 1 and is copied whole). This is ContentX.splice (Y@70000..) as a byte slice.
+__device__ inline bool content_slice(const Work& w, uint32_t src, uint32_t e0, uint32_t e1, uint32_t& b0, uint32_t& b1) {
+  const uint32_t ref = w.s_info[src] & 31u;
+  const uint8_t* __restrict__ by = w.bytes;
+  const uint32_t end = w.s_cend[src];
+  if (ref == REF_ANY || ref == REF_JSON) {
+    uint32_t p = w.s_celem[src];
+    bool ok = true;
+    for (uint32_t i = 0; i < e1; ++i) {
+      if (i == e0) b0 = p;
+      if (ref == REF_ANY) {
+        uint32_t steps = 0xFFFFFFFFu;
+        ok = skip_any<32>(by, p, end, steps);
+      } else {
+        const uint32_t k = rd_vu(by, p, end, ok);
+        if (ok) skip_bytes(p, k, end, ok);
+      }
+      if (!ok) return false;
+    }
+    if (e0 == e1) b0 = p;
+    b1 = p;
+    return true;
+  }
+  if (ref == REF_STRING) {
+    uint32_t p = w.s_cpos[src];
+    bool ok = true;
+    rd_vu(by, p, end, ok);  // byte length prefix
+    if (!ok) return false;
+    uint32_t u = 0;  // UTF-16 units before p
+    b0 = e0 == 0 ? p : NONE;
+    while (p < end && u < e1) {
+      const uint32_t c = by[p];
+      const uint32_t n = c < 0x80u ? 1u : c < 0xE0u ? 2u : c < 0xF0u ? 3u : 4u;
+      const uint32_t du = n == 4 ? 2u : 1u;
+      if (u < e0 && u + du > e0) return false;  // a slice through a surrogate pair
+      if (u < e1 && u + du > e1) return false;
+      p += n;
+      u += du;
+      if (u == e0) b0 = p;
+    }
+    b1 = p;
+    return b0 != NONE && u == e1;
+  }
+  b0 = w.s_cpos[src];
+  b1 = end;
+  return true;
+}
 
 // per-client scratch arrays inside Work::cc
 enum : uint32_t {
@@ -228,5 +323,17 @@ void scan_u32_to_u64(void* tmp, size_t tmpb, const uint32_t* in, uint64_t* out, 
 void sort_u32(void* tmp, size_t tmpb, const uint32_t* in, uint32_t* out, uint64_t n, hipStream_t s);
 void sort_pairs_u32(void* tmp, size_t tmpb, const uint32_t* kin, uint32_t* kout, const uint32_t* vin, uint32_t* vout,
                     uint64_t n, hipStream_t s);
+void sort_pairs_u64_u32(void* tmp, size_t tmpb, const uint64_t* kin, uint64_t* kout, const uint32_t* vin, uint32_t* vout,
+                        uint64_t n, hipStream_t s);
+// inclusive scan with "max within equal high words" (segmented running max of packed values)
+void scan_segmax_u64(void* tmp, size_t tmpb, const uint64_t* in, uint64_t* out, uint64_t n, hipStream_t s);
+
+// lazy merge (yc_lazy.hip)
+void launch_lazy_merge(Work& w, uint32_t nsections, uint32_t nclients, hipStream_t s);
+void launch_lazy_diff(Work& w, uint32_t nsections, hipStream_t s);
+uint32_t launch_event_sizes(Work& w, hipStream_t s, uint32_t* nslots_out);
+uint32_t launch_ds_runs(Work& w, uint32_t nds, bool merge, hipStream_t s);
+uint32_t launch_ds_write_sizes(Work& w, uint32_t nr, hipStream_t s);
+void launch_lazy_write(Work& w, uint32_t nslots, uint32_t nr, uint32_t dsbase, hipStream_t s);
 
 }  // namespace yc

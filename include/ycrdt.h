@@ -79,6 +79,14 @@ int ycrdt_encode_state_vector(ycrdt_doc *d, ycrdt_out *out);
 /* stats of the doc's last merge */
 int ycrdt_doc_last_stats(ycrdt_doc *d, ycrdt_merge_stats *st);
 
+/* Y.mergeUpdates(updates) — north_star; Yjs-internal for pending structs (Y@39011). Lazy k-way
+ * merge of the updates' structs (no integration), delete sets unioned. One input is returned
+ * unchanged, as Yjs does. */
+int ycrdt_merge_updates(ycrdt_engine *e, const ycrdt_buf *ups, size_t n, ycrdt_out *out);
+/* Y.diffUpdate(update, sv) (Y@40711): the structs of `update` missing from state vector `sv`,
+ * with the update's delete set. */
+int ycrdt_diff_update(ycrdt_engine *e, ycrdt_buf update, ycrdt_buf sv, ycrdt_out *out);
+
 /* ---- device-resident batches (ingest queue / benchmark) ---------------------------------- */
 /* Copies the updates into HBM. */
 int ycrdt_batch_stage(ycrdt_engine *e, const ycrdt_buf *ups, size_t n, ycrdt_batch **out);
