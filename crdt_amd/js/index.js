@@ -4,7 +4,8 @@
 //   const Y = require('crdt_amd/js');  router.updateOptions({ Y });
 //
 // Exposes the Yjs functions the reference calls (SURVEY.md §8(b)): new Y.Doc(), Y.applyUpdate,
-// Y.encodeStateAsUpdate(doc[, sv]), Y.encodeStateVector, plus the batch entry Y.applyUpdates.
+// Y.encodeStateAsUpdate(doc[, sv]), Y.encodeStateVector, Y.mergeUpdates, Y.diffUpdate, plus the
+// batch entry Y.applyUpdates.
 // Errors are thrown as Error objects whose `message` carries the engine's text (crdt.js:38-39
 // only reads e.message). There is no CPU fallback: without an MI355X every call throws.
 'use strict';
@@ -48,6 +49,8 @@ module.exports = {
   applyUpdates,
   encodeStateAsUpdate,
   encodeStateVector,
+  mergeUpdates: (updates) => binding.mergeUpdates(updates),
+  diffUpdate: (update, sv) => binding.diffUpdate(update, sv),
   lastStats: (doc) => binding.lastStats(doc._h),
   version: binding.version,
   setDevice: binding.setDevice,

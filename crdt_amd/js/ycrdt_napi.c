@@ -222,6 +222,49 @@ static napi_value js_last_stats(napi_env env, napi_callback_info info) {
   return obj;
 }
 
+/* mergeUpdates(update[]) → Uint8Array   (Y.mergeUpdates, north_star / Y@39011) */
+static napi_value js_merge_updates(napi_env env, napi_callback_info info) {
+  size_t argc = 1;
+  napi_value argv[1];
+  CHECK(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+  bool is_arr = false;
+  if (argc > 0) napi_is_array(env, argv[0], &is_arr);
+  if (!is_arr) { napi_throw_type_error(env, NULL, "mergeUpdates(updates[])"); return NULL; }
+  ycrdt_engine *e = engine(env);
+  if (!e) return NULL;
+  uint32_t n = 0;
+  napi_get_array_length(env, argv[0], &n);
+  ycrdt_buf *bufs = (ycrdt_buf *)calloc(n ? n : 1, sizeof(ycrdt_buf));
+  for (uint32_t i = 0; i < n; ++i) {
+    napi_value el;
+    napi_get_element(env, argv[0], i, &el);
+    if (!get_bytes(env, el, &bufs[i])) { free(bufs); napi_throw_type_error(env, NULL, "updates must be Uint8Arrays"); return NULL; }
+  }
+  ycrdt_out o = {NULL, 0};
+  int rc = ycrdt_merge_updates(e, bufs, n, &o);
+  free(bufs);
+  if (rc != YCRDT_OK) return throw_rc(env, rc);
+  return u8_from_out(env, &o);
+}
+
+/* diffUpdate(update, sv) → Uint8Array   (Y.diffUpdate, Y@40711) */
+static napi_value js_diff_update(napi_env env, napi_callback_info info) {
+  size_t argc = 2;
+  napi_value argv[2];
+  CHECK(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+  ycrdt_buf u, sv;
+  if (argc < 2 || !get_bytes(env, argv[0], &u) || !get_bytes(env, argv[1], &sv)) {
+    napi_throw_type_error(env, NULL, "diffUpdate(update, stateVector)");
+    return NULL;
+  }
+  ycrdt_engine *e = engine(env);
+  if (!e) return NULL;
+  ycrdt_out o = {NULL, 0};
+  int rc = ycrdt_diff_update(e, u, sv, &o);
+  if (rc != YCRDT_OK) return throw_rc(env, rc);
+  return u8_from_out(env, &o);
+}
+
 static napi_value js_version(napi_env env, napi_callback_info info) {
   (void)info;
   napi_value s;
@@ -236,6 +279,8 @@ static napi_value init(napi_env env, napi_value exports) {
       {"applyUpdates", NULL, js_apply_updates, NULL, NULL, NULL, napi_default, NULL},
       {"encodeStateAsUpdate", NULL, js_encode_state_as_update, NULL, NULL, NULL, napi_default, NULL},
       {"encodeStateVector", NULL, js_encode_state_vector, NULL, NULL, NULL, napi_default, NULL},
+      {"mergeUpdates", NULL, js_merge_updates, NULL, NULL, NULL, napi_default, NULL},
+      {"diffUpdate", NULL, js_diff_update, NULL, NULL, NULL, napi_default, NULL},
       {"lastStats", NULL, js_last_stats, NULL, NULL, NULL, napi_default, NULL},
       {"version", NULL, js_version, NULL, NULL, NULL, napi_default, NULL},
   };

@@ -13,7 +13,7 @@ const hex = (u) => Buffer.from(u).toString('hex');
 const unhex = (h) => new Uint8Array(Buffer.from(h, 'hex'));
 
 const mode = process.argv[2] || 'cpu';
-for (const f of ['Doc', 'applyUpdate', 'applyUpdates', 'encodeStateAsUpdate', 'encodeStateVector']) {
+for (const f of ['Doc', 'applyUpdate', 'applyUpdates', 'encodeStateAsUpdate', 'encodeStateVector', 'mergeUpdates', 'diffUpdate']) {
   assert.strictEqual(typeof Y[f], 'function', f);
 }
 assert.ok(/gfx950/.test(Y.version()));
@@ -34,6 +34,7 @@ if (mode === 'cpu') {
       assert.strictEqual(hex(Y.encodeStateAsUpdate(d)), c.state, c.name);
       assert.strictEqual(hex(Y.encodeStateVector(d)), c.sv, c.name);
       for (const df of c.diffs) assert.strictEqual(hex(Y.encodeStateAsUpdate(d, unhex(df.sv))), df.update, c.name);
+      assert.strictEqual(hex(Y.mergeUpdates(c.updates.map(unhex))), c.updates.length > 1 ? c.merged : c.merged_raw, c.name);
       n++;
     }
   }

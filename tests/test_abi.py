@@ -18,3 +18,12 @@ def test_header_symbols_exported():
 
 def test_version_string():
     assert b"gfx950" in crdt_amd.lib().ycrdt_version()
+
+
+def test_library_is_fresh():
+    """libycrdt.so must be rebuilt after every source edit (the GPU box runs the in-tree build)."""
+    so = os.path.getmtime(os.path.join(ROOT, "crdt_amd", "libycrdt.so"))
+    src = os.path.join(ROOT, "crdt_amd", "csrc")
+    for f in os.listdir(src):
+        if f.endswith((".hip", ".h")):
+            assert os.path.getmtime(os.path.join(src, f)) <= so, f"{f} is newer than libycrdt.so: rebuild"
