@@ -31,7 +31,10 @@ constexpr uint32_t LDS_NXT = 0, LDS_CEXIT = 32768, LDS_CCNT = 65536, LDS_BEXIT =
 constexpr uint32_t LDS_TOTAL = 147456;
 static_assert(GROUP_BYTES == 16384, "table layout assumes 16 KiB groups");
 
-__global__ __launch_bounds__(TL) void k_tables(const uint8_t* __restrict__ b, const Group* __restrict__ groups, Tables t) {
+__global__ __launch_bounds__(TL) void k_tables(Work w) {
+  const uint8_t* __restrict__ b = w.bytes;
+  const Group* __restrict__ groups = w.groups;
+  const Tables& t = w.tab;
   __shared__ __attribute__((aligned(16))) uint8_t lds[LDS_TOTAL];
   uint16_t* nxt = (uint16_t*)(lds + LDS_NXT);
   uint16_t* cexit = (uint16_t*)(lds + LDS_CEXIT);
@@ -144,6 +147,94 @@ __global__ __launch_bounds__(TL) void k_tables(const uint8_t* __restrict__ b, co
     }
     static_assert(6 % 2 == 0, "an even number of rounds leaves the result in cexit/ccnt");
   }
+  // ---- an update that fits in one group is walked right here (its tables never leave LDS): lane 0
+  // follows the true chain through the section headers by chunk exits, queueing (position, count)
+  // chain pieces, then every lane marks its pieces' struct starts into an LDS copy of the final
+  // bitmap (the update owns its 64-byte-aligned words exclusively) — k_walker / k_mark skip it.
+  if (G.start == w.uoff[G.upd] && G.end == G.uend) {
+    uint64_t* bm = (uint64_t*)(lds + LDS_BEXIT);           // 256 words (bexit/bcnt are free again)
+    uint32_t* task = (uint32_t*)(lds + LDS_BEXIT + 2048);  // (position << 8 | count)
+    constexpr uint32_t MAXTASK = (LDS_TOTAL - LDS_BEXIT - 2048) / 4;
+    __shared__ uint32_t ntask;
+    const uint32_t nwords_g = (glen + 63) / 64;
+    for (uint32_t i = tid; i < nwords_g; i += TL) bm[i] = 0;
+    if (tid == 0) ntask = 0;
+    __syncthreads();
+    if (tid == 0) {
+      const uint32_t u = G.upd, uend = G.uend;
+      uint32_t* err = &w.ctr->err;
+      w.dsstart[u] = NONE;
+      bool ok = true;
+      uint32_t p = G.start;
+      uint32_t nt = 0;
+      const uint32_t nsec = rd_vu(b, p, uend, ok);
+      if (!ok || nsec > (uend - p) / 3 + 1) { raise_err(err, ERR_DECODE); goto done; }
+      {
+        const uint32_t sbase = atomicAdd(&w.ctr->nsections, nsec);
+        if (sbase + nsec > w.cap_sections) { raise_err(err, ERR_CAPACITY); goto done; }
+        w.usec_start[u] = sbase;
+        w.usec_n[u] = nsec;
+        for (uint32_t sct = 0; sct < nsec; ++sct) {
+          const uint32_t n = rd_vu(b, p, uend, ok);
+          const uint32_t client = rd_vu(b, p, uend, ok);
+          const uint32_t clock = rd_vu(b, p, uend, ok);
+          if (!ok || n > uend - p) { raise_err(err, ERR_DECODE); goto done; }
+          Section sec;
+          sec.upd = u; sec.n = n; sec.client = client; sec.clock = clock;
+          sec.first_pos = n ? p : NONE; sec.cidx = NONE; sec.first_idx = NONE; sec.pad = 0;
+          w.sections[sbase + sct] = sec;
+          if (n) atomicOr((unsigned long long*)&w.sec_bits[p >> 6], 1ull << (p & 63));
+          uint32_t r = n;
+          uint32_t o = p - G.start;
+          while (r > 0) {
+            if (o >= glen) { raise_err(err, ERR_DECODE); goto done; }
+            for (;;) {  // whole chunk pieces of the chain
+              const uint32_t ce = cexit[o], cc = ccnt[o];
+              if ((ce & STOPF) || cc >= r || cc == 0) break;
+              if (nt >= MAXTASK) { raise_err(err, ERR_CAPACITY); goto done; }
+              task[nt++] = (o << 8) | cc;
+              r -= cc;
+              o = ce;
+              if (o >= glen) break;
+            }
+            if (r == 0) break;
+            if (o >= glen) { raise_err(err, ERR_DECODE); goto done; }
+            // one struct: sized by the table, or parsed exactly (long / unsized struct)
+            const uint32_t d = nxt[o];
+            uint32_t q = G.start + o;
+            if (d == 1) {
+              if (parse_struct<false>(b, q, uend, 0xFFFFFFFFu, nullptr) <= 0) { raise_err(err, ERR_DECODE); w.ctr->err_info = G.start + o; goto done; }
+            } else if (d == 0) { raise_err(err, ERR_DECODE); goto done; }
+            else q += d;
+            atomicOr((unsigned long long*)&bm[o >> 6], 1ull << (o & 63));
+            o = q - G.start;
+            --r;
+          }
+          p = G.start + o;
+        }
+        w.dsstart[u] = p;
+      }
+    done:
+      ntask = nt;
+    }
+    __syncthreads();
+    const uint32_t nt = ntask;
+    for (uint32_t i = tid; i < nt; i += TL) {
+      uint32_t x = task[i] >> 8, left = task[i] & 0xFFu;
+      const uint32_t word = x >> 6;
+      uint64_t m = 0;
+      while (left > 0) {
+        m |= 1ull << (x & 63);
+        const uint32_t d = nxt[x];
+        x += d == 0 ? 1 : d;
+        --left;
+      }
+      atomicOr((unsigned long long*)&bm[word], (unsigned long long)m);
+    }
+    __syncthreads();
+    for (uint32_t i = tid; i < nwords_g; i += TL) w.final_bits[(G.start >> 6) + i] = bm[i];
+    return;
+  }
   // exits are stored as forward deltas from the position itself (|STOPF when the chain stops at a
   // struct the tables could not size), so consumers never need the group origin
   for (uint32_t o = tid; o < glen; o += TL) {
@@ -187,7 +278,7 @@ __global__ __launch_bounds__(TL) void k_tables(const uint8_t* __restrict__ b, co
 
 void launch_group_parse(const Work& w, hipStream_t s) {
   if (w.ngroups == 0) return;
-  hipLaunchKernelGGL(k_tables, dim3(w.ngroups), dim3(TL), 0, s, w.bytes, w.groups, w.tab);
+  hipLaunchKernelGGL(k_tables, dim3(w.ngroups), dim3(TL), 0, s, w);
 }
 
 // --------------------------------------------------------------------------- 2. walker
@@ -208,83 +299,134 @@ __device__ __forceinline__ bool emit_patch(const Work& w, uint32_t p) {
   return true;
 }
 
+// One wavefront per multi-group update. The header / descent logic runs uniformly on every lane
+// (lane 0 stores); the group-to-group jumps of a long section are speculated 64 groups at a time:
+// lane j takes the exit S_j of the chain that starts at its group's first byte; the true chain
+// enters group j+1 at S_j as soon as it has synchronised with that chain inside group j, which
+// lane j checks by looking up the exit of its (true) entry. The first lane that fails still knows
+// its true exit, so a failed speculation costs one group, exactly the sequential step.
 __global__ __launch_bounds__(64) void k_walker(Work w) {
-  const uint32_t u = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t u = blockIdx.x;
+  const uint32_t lane = threadIdx.x;
   if (u >= w.nupd) return;
+  if (w.ulen[u] > 0 && w.ulen[u] <= GROUP_BYTES) return;  // walked inside k_tables
   const uint8_t* __restrict__ b = w.bytes;
   const Tables& T = w.tab;
   const uint32_t ustart = w.uoff[u];
   const uint32_t uend = ustart + w.ulen[u];
+  const uint32_t ngu = (w.ulen[u] + GROUP_BYTES - 1) / GROUP_BYTES;
   uint32_t* err = &w.ctr->err;
-  w.dsstart[u] = NONE;
+  const bool L0 = lane == 0;
+  if (L0) w.dsstart[u] = NONE;
   uint32_t p = ustart;
   bool ok = true;
   const uint32_t nsec = rd_vu(b, p, uend, ok);
-  if (!ok || nsec > (uend - p) / 3 + 1) { raise_err(err, ERR_DECODE); return; }
-  const uint32_t sbase = atomicAdd(&w.ctr->nsections, nsec);
-  if (sbase + nsec > w.cap_sections) { raise_err(err, ERR_CAPACITY); return; }
-  w.usec_start[u] = sbase;
-  w.usec_n[u] = nsec;
-  for (uint32_t s = 0; s < nsec; ++s) {
+  if (!ok || nsec > (uend - p) / 3 + 1) { if (L0) raise_err(err, ERR_DECODE); return; }
+  uint32_t sbase = 0;
+  if (L0) sbase = atomicAdd(&w.ctr->nsections, nsec);
+  sbase = __shfl(sbase, 0);
+  if (sbase + nsec > w.cap_sections) { if (L0) raise_err(err, ERR_CAPACITY); return; }
+  if (L0) { w.usec_start[u] = sbase; w.usec_n[u] = nsec; }
+  for (uint32_t sct = 0; sct < nsec; ++sct) {
     const uint32_t n = rd_vu(b, p, uend, ok);
     const uint32_t client = rd_vu(b, p, uend, ok);
     const uint32_t clock = rd_vu(b, p, uend, ok);
-    if (!ok || n > uend - p) { raise_err(err, ERR_DECODE); return; }
-    Section sec;
-    sec.upd = u; sec.n = n; sec.client = client; sec.clock = clock;
-    sec.first_pos = n ? p : NONE; sec.cidx = NONE; sec.first_idx = NONE; sec.pad = 0;
-    w.sections[sbase + s] = sec;
-    if (n) atomicOr((unsigned long long*)&w.sec_bits[p >> 6], 1ull << (p & 63));
+    if (!ok || n > uend - p) { if (L0) raise_err(err, ERR_DECODE); return; }
+    if (L0) {
+      Section sec;
+      sec.upd = u; sec.n = n; sec.client = client; sec.clock = clock;
+      sec.first_pos = n ? p : NONE; sec.cidx = NONE; sec.first_idx = NONE; sec.pad = 0;
+      w.sections[sbase + sct] = sec;
+      if (n) atomicOr((unsigned long long*)&w.sec_bits[p >> 6], 1ull << (p & 63));
+    }
     uint32_t r = n;
     while (r > 0) {
-      if (p >= uend) { raise_err(err, ERR_DECODE); return; }
-      const uint32_t ge = T.gexit[p], gc = T.gcnt[p];
+      if (p >= uend) { if (L0) raise_err(err, ERR_DECODE); return; }
       bool exact = false;
-      if (gc < r) {  // the section continues past this group (or past a long struct)
-        if (gc && !emit_seg(w, p, gc)) return;
-        r -= gc;
-        p += ge & 0x7FFFu;
-        exact = (ge & STOPF) != 0;
-      } else {       // the section ends inside this group: descend block -> chunk -> struct
+      if (T.gcnt[p] < r) {  // the section continues past this group: speculate 64 groups ahead
+        const uint32_t gi = (p - ustart) / GROUP_BYTES + lane;
+        uint32_t S = NONE;
+        if (gi < ngu) {
+          const uint32_t gs = ustart + gi * GROUP_BYTES;
+          const uint32_t x = T.gexit[gs];
+          if (!(x & STOPF)) S = gs + (x & 0x7FFFu);
+        }
+        uint32_t E = __shfl_up(S, 1);
+        if (lane == 0) E = p;
+        uint32_t X = NONE, C = 0;
+        bool stop = true;
+        if (E != NONE && E < uend && gi < ngu) {
+          const uint32_t ge = T.gexit[E];
+          C = T.gcnt[E];
+          X = E + (ge & 0x7FFFu);
+          stop = (ge & STOPF) != 0;
+        }
+        const bool good = !stop && X == S;
+        const uint64_t bad = __ballot(!good);
+        const uint32_t f = bad ? (uint32_t)__ffsll((long long)bad) - 1 : 63u;  // lanes 0..f hold true entries
+        // inclusive count scan over lanes 0..f
+        uint32_t incl = lane <= f ? C : 0u;
+        for (uint32_t off = 1; off < 64; off <<= 1) {
+          const uint32_t v = __shfl_up(incl, off);
+          if (lane >= off) incl += v;
+        }
+        const uint32_t excl = incl - (lane <= f ? C : 0u);
+        const uint64_t ends = __ballot(lane <= f && incl >= r);
+        if (ends) {  // the section ends in the group of lane j
+          const uint32_t j = (uint32_t)__ffsll((long long)ends) - 1;
+          if (lane < j && C && !emit_seg(w, E, C)) return;
+          r -= __shfl(excl, j);
+          p = __shfl(E, j);
+        } else {
+          if (lane <= f && C && !emit_seg(w, E, C)) return;
+          r -= __shfl(incl, f);
+          p = __shfl(X, f);
+          exact = __shfl(stop ? 1u : 0u, f) != 0;
+          if (p == NONE) { if (L0) raise_err(err, ERR_DECODE); return; }
+          if (!exact) continue;
+        }
+      }
+      if (!exact) {  // the section ends inside this group: descend block -> chunk -> struct
         uint32_t rr = r;
         for (;;) {
           const uint32_t be = T.bexit[p], bc = T.bcnt[p];
           if ((be & STOPF) || bc >= rr) break;
-          if (!emit_seg(w, p, bc)) return;
+          if (L0 && !emit_seg(w, p, bc)) return;
           rr -= bc;
           p += be;
         }
         for (;;) {
           const uint32_t ce = T.cexit[p], cc = T.ccnt[p];
           if ((ce & STOPF) || cc >= rr) break;
-          if (!emit_seg(w, p, cc)) return;
+          if (L0 && !emit_seg(w, p, cc)) return;
           rr -= cc;
           p += ce;
         }
         while (rr > 0) {
           const uint32_t d = T.nxt[p];
           if (d == 1) { exact = true; break; }
-          if (d == 0 || !emit_patch(w, p)) { raise_err(err, ERR_DECODE); return; }
+          if (d == 0) { if (L0) raise_err(err, ERR_DECODE); return; }
+          if (L0 && !emit_patch(w, p)) return;
           p += d;
           --rr;
         }
         r = rr;
       }
       if (exact && r > 0) {  // a struct the tables could not size: parse it exactly
-        if (!emit_patch(w, p)) return;
+        if (L0 && !emit_patch(w, p)) return;
         uint32_t q = p;
-        if (parse_struct<false>(b, q, uend, 0xFFFFFFFFu, nullptr) <= 0) { raise_err(err, ERR_DECODE); w.ctr->err_info = p; return; }
+        if (parse_struct<false>(b, q, uend, 0xFFFFFFFFu, nullptr) <= 0) { if (L0) { raise_err(err, ERR_DECODE); w.ctr->err_info = p; } return; }
         p = q;
         --r;
       }
     }
   }
-  w.dsstart[u] = p;
+  if (L0) w.dsstart[u] = p;
 }
 
 void launch_walker(const Work& w, hipStream_t s) {
   if (w.nupd == 0) return;
-  hipLaunchKernelGGL(k_walker, dim3((w.nupd + 63) / 64), dim3(64), 0, s, w);
+  hipLaunchKernelGGL(k_walker, dim3(w.nupd), dim3(64), 0, s, w);
 }
 
 // --------------------------------------------------------------------------- 3. final bitmap

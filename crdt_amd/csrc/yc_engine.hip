@@ -424,7 +424,6 @@ int run_merge(ycrdt_engine* e, ycrdt_batch* b, const std::unordered_map<uint32_t
   w.g_link = take<uint32_t>(V, B_GLINK, U + 1, ok);
   w.g_key = take<uint32_t>(V, B_GKEY, U + 1, ok);
   w.g_maxchild = take<uint64_t>(V, B_GMAXC, U + 1, ok);
-  w.g_next = take<uint32_t>(V, B_GNEXT, U + 1, ok);
   w.g_outid = take<uint32_t>(V, B_GOUTID, U + 2, ok);
   w.g_tmp = take<uint32_t>(V, B_GTMP, U + 2, ok);
   w.g_tmp2 = take<uint32_t>(V, B_GTMP2, U + 2, ok);
@@ -484,7 +483,10 @@ int run_merge(ycrdt_engine* e, ycrdt_batch* b, const std::unordered_map<uint32_t
     mark(e, "merge.dead_types");
     run_dead_keys(w, nsegs, s);
     mark(e, "merge.yata");
-    launch_yata(w, nsegs, s);
+    uint32_t narray = 0;  // read after the descent / dead-type rounds (already synchronised)
+    HIPCHK(hipMemcpyAsync(&narray, &w.ctr->narray, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    launch_yata(w, nsegs, narray, s);
     mark(e, "merge.merge_flags");
     launch_merge_flags(w, nsegs, s);
     rc = check(e, c, "merge");

@@ -9,10 +9,11 @@
 //                  getItemCleanStart, Y@29100) + min child client per unit (list adjacency)
 //   k_cuts         struct boundaries -> bitmap; popcount scan -> segments
 //   k_seg_props    per-segment origin / rightOrigin / parent / flags
-//   k_keyjump      parent+parentSub resolution (Item.getMissing, Y@76507) by pointer jumping
+//   k_keyfind      parent+parentSub resolution (Item.getMissing, Y@76507): climb the origin chain
+//                  with path halving
 //   k_children     YATA for map entries (Item.integrate, Y@77594): children ordered by client ⇒
 //                  the rightmost entry is the max-client descent from the max-client root
-//   k_descend      pointer jumping along the max-client child
+//   k_winner_walk  per key: descend along the max-client child to the rightmost entry
 //   k_overwrite    every non-rightmost entry of a key is deleted (typeMapSet / left.delete)
 //   k_merge_flags  Item.mergeWith (Y@79424) / tryToMergeWithLeft (Y@30960) as a pairwise
 //                  predicate over adjacent segments ⇒ canonical (maximally merged) structs
@@ -300,25 +301,6 @@ void launch_segment_props(const Work& w, uint32_t nsegs, uint32_t nclients, uint
 }
 
 // --------------------------------------------------------------------------- key resolution
-__global__ __launch_bounds__(256) void k_keyjump(Work w, uint32_t nsegs) {
-  const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
-  if (s >= nsegs) return;
-  const uint32_t f = w.g_flags[s];
-  if (w.g_key[s] != NONE || !(f & SEG_ITEM)) return;
-  const uint32_t t = w.g_link[s];
-  if (!(w.g_flags[t] & SEG_ITEM)) {  // the origin chain ends in GC: getMissing drops the parent
-    w.g_flags[s] = (f & ~SEG_ITEM) | SEG_GC | SEG_DEL;
-    w.g_origin[s] = NONE;
-    w.g_rorigin[s] = NONE;
-    w.ctr->changed = 1;
-    return;
-  }
-  const uint32_t kt = w.g_key[t];
-  if (kt != NONE) { w.g_key[s] = kt; w.ctr->changed = 1; return; }
-  const uint32_t tt = w.g_link[t];
-  if (tt != t) { w.g_link[s] = tt; w.ctr->changed = 1; }
-}
-
 // every item now knows its list: tag it YMap-entry (parentSub) or YArray member
 __global__ void k_seg_kind(Work w, uint32_t nsegs) {
   const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
@@ -327,23 +309,42 @@ __global__ void k_seg_kind(Work w, uint32_t nsegs) {
   if (!(f & SEG_ITEM)) return;
   const uint32_t key = w.g_key[s];
   if (key == NONE) { raise_err(&w.ctr->err, ERR_DECODE); return; }  // origin chain without a root
-  w.g_flags[s] = f | ((w.k_flags[key] & KF_PSUB) ? SEG_PSUB : SEG_ARRAY);
+  const bool arr = !(w.k_flags[key] & KF_PSUB);
+  w.g_flags[s] = f | (arr ? SEG_ARRAY : SEG_PSUB);
+  if (arr) atomicAdd(&w.ctr->narray, 1u);
+}
+
+// One pass instead of host-driven pointer-jumping rounds: every unresolved item climbs its origin
+// chain to the first segment that knows its list, halving the path it walks (link[x] ← link[link[x]]
+// is monotone: it only ever points further up the same chain, so concurrent halving is safe).
+__global__ __launch_bounds__(256) void k_keyfind(Work w, uint32_t nsegs) {
+  const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= nsegs) return;
+  const uint32_t f = w.g_flags[s];
+  if (w.g_key[s] != NONE || !(f & SEG_ITEM)) return;
+  uint32_t x = w.g_link[s];
+  for (uint32_t it = 0; it < (1u << 22); ++it) {
+    if (!(w.g_flags[x] & SEG_ITEM)) {  // the origin chain ends in GC: getMissing drops the parent
+      w.g_flags[s] = (f & ~SEG_ITEM) | SEG_GC | SEG_DEL;
+      w.g_origin[s] = NONE;
+      w.g_rorigin[s] = NONE;
+      return;
+    }
+    const uint32_t k = w.g_key[x];
+    if (k != NONE) { w.g_key[s] = k; return; }
+    const uint32_t y = w.g_link[x];
+    if (y == x) return;  // a chain without a root: k_seg_kind reports it
+    const uint32_t z = w.g_link[y];
+    if (z != y) w.g_link[x] = z;
+    x = y;
+  }
 }
 
 uint32_t run_key_resolution(const Work& w, uint32_t nsegs, hipStream_t s) {
   if (!nsegs) return 0;
-  uint32_t rounds = 0;
-  for (; rounds < 64; rounds += 2) {
-    hipMemsetAsync(&w.ctr->changed, 0, sizeof(uint32_t), s);
-    hipLaunchKernelGGL(k_keyjump, dim3((nsegs + 255) / 256), dim3(256), 0, s, w, nsegs);
-    hipLaunchKernelGGL(k_keyjump, dim3((nsegs + 255) / 256), dim3(256), 0, s, w, nsegs);
-    uint32_t changed = 0;
-    hipMemcpyAsync(&changed, &w.ctr->changed, sizeof(uint32_t), hipMemcpyDeviceToHost, s);
-    hipStreamSynchronize(s);
-    if (!changed) break;
-  }
+  hipLaunchKernelGGL(k_keyfind, dim3((nsegs + 255) / 256), dim3(256), 0, s, w, nsegs);
   hipLaunchKernelGGL(k_seg_kind, dim3((nsegs + 255) / 256), dim3(256), 0, s, w, nsegs);
-  return rounds;
+  return 1;
 }
 
 // --------------------------------------------------------------------------- map winner
@@ -363,24 +364,20 @@ __global__ __launch_bounds__(256) void k_children(Work w, uint32_t nsegs) {
     if (*dst < v) atomicMax(dst, v);
   }
 }
-__global__ void k_next_init(Work w, uint32_t nsegs) {
-  const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
-  if (s >= nsegs) return;
-  const uint64_t m = w.g_maxchild[s];
-  w.g_next[s] = m ? (uint32_t)m : s;
-}
-__global__ __launch_bounds__(256) void k_descend(Work w, uint32_t nsegs) {
-  const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
-  if (s >= nsegs) return;
-  const uint32_t n = w.g_next[s];
-  const uint32_t nn = w.g_next[n];
-  if (nn != n) { w.g_next[s] = nn; w.ctr->changed = 1; }
-}
-__global__ void k_winner(Work w) {
+// the key's value is the rightmost entry: descend from the max-client root through the max-client
+// child until a leaf (YATA order of an origin-only tree, SURVEY.md §7 hard part 2)
+__global__ void k_winner_walk(Work w) {
   const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
   if (k >= w.cap_keys) return;
   const uint64_t r = w.k_rootmax[k];
-  w.k_winner[k] = r ? w.g_next[(uint32_t)r] : NONE;
+  if (!r) { w.k_winner[k] = NONE; return; }
+  uint32_t x = (uint32_t)r;
+  for (uint32_t it = 0; it < (1u << 24); ++it) {
+    const uint64_t m = w.g_maxchild[x];
+    if (!m) break;
+    x = (uint32_t)m;
+  }
+  w.k_winner[k] = x;
 }
 __global__ void k_overwrite(Work w, uint32_t nsegs) {
   const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
@@ -393,24 +390,13 @@ __global__ void k_overwrite(Work w, uint32_t nsegs) {
 void launch_map_winner(const Work& w, uint32_t nsegs, hipStream_t s) {
   if (!nsegs) return;
   hipLaunchKernelGGL(k_children, dim3((nsegs + 255) / 256), dim3(256), 0, s, w, nsegs);
-  hipLaunchKernelGGL(k_next_init, dim3((nsegs + 255) / 256), dim3(256), 0, s, w, nsegs);
 }
 
 uint32_t run_descent(const Work& w, uint32_t nsegs, hipStream_t s) {
   if (!nsegs) return 0;
-  uint32_t rounds = 0;
-  for (; rounds < 64; rounds += 2) {
-    hipMemsetAsync(&w.ctr->changed, 0, sizeof(uint32_t), s);
-    hipLaunchKernelGGL(k_descend, dim3((nsegs + 255) / 256), dim3(256), 0, s, w, nsegs);
-    hipLaunchKernelGGL(k_descend, dim3((nsegs + 255) / 256), dim3(256), 0, s, w, nsegs);
-    uint32_t changed = 0;
-    hipMemcpyAsync(&changed, &w.ctr->changed, sizeof(uint32_t), hipMemcpyDeviceToHost, s);
-    hipStreamSynchronize(s);
-    if (!changed) break;
-  }
-  hipLaunchKernelGGL(k_winner, dim3(w.cap_keys / 256 + 1), dim3(256), 0, s, w);
+  hipLaunchKernelGGL(k_winner_walk, dim3(w.cap_keys / 256 + 1), dim3(256), 0, s, w);
   hipLaunchKernelGGL(k_overwrite, dim3((nsegs + 255) / 256), dim3(256), 0, s, w, nsegs);
-  return rounds;
+  return 1;
 }
 
 // --------------------------------------------------------------------------- deleted parent types

@@ -27,7 +27,8 @@ struct Counters {            // device-side counters, read back at the few host 
   uint32_t sv_bytes;         // encoded state-vector size
   uint32_t nkeys;            // distinct map keys
   uint32_t nruns;            // delete-set runs in the output
-  uint32_t pad[14];          // encode scratch (see yc_encode.hip)
+  uint32_t narray;           // YArray list members (segments)
+  uint32_t pad[13];          // encode scratch (see yc_encode.hip)
   unsigned long long items;  // Σ clock lengths of Skip structs (items = Σ all lengths − this)
 };
 
@@ -219,6 +220,11 @@ __device__ inline bool content_slice(const Work& w, uint32_t src, uint32_t e0, u
   const uint32_t ref = w.s_info[src] & 31u;
   const uint8_t* __restrict__ by = w.bytes;
   const uint32_t end = w.s_cend[src];
+  if (e0 == 0 && e1 == w.s_len[src] && (ref == REF_ANY || ref == REF_JSON)) {  // the whole content
+    b0 = w.s_celem[src];
+    b1 = end;
+    return true;
+  }
   if (ref == REF_ANY || ref == REF_JSON) {
     uint32_t p = w.s_celem[src];
     bool ok = true;
@@ -311,7 +317,7 @@ void launch_map_winner(const Work& w, uint32_t nsegs, hipStream_t s);
 uint32_t run_descent(const Work& w, uint32_t nsegs, hipStream_t s);
 void launch_merge_flags(const Work& w, uint32_t nsegs, hipStream_t s);
 void run_dead_keys(const Work& w, uint32_t nsegs, hipStream_t s);
-uint32_t launch_yata(const Work& w, uint32_t nsegs, hipStream_t s);
+uint32_t launch_yata(const Work& w, uint32_t nsegs, uint32_t narray, hipStream_t s);
 
 void launch_encode_sizes(const Work& w, uint32_t nsegs, uint32_t nclients, uint32_t nout, uint32_t* nruns_host, hipStream_t s);
 void launch_encode_write(const Work& w, uint32_t nclients, uint32_t nout, uint32_t nruns, hipStream_t s);
