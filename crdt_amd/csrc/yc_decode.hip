@@ -46,6 +46,7 @@ __global__ __launch_bounds__(TL) void k_tables(Work w) {
   uint16_t* gcnt = cexit;
   const Group G = groups[blockIdx.x];
   const uint32_t tid = threadIdx.x;
+  if (w.dbg && tid == 0) w.dbg[blockIdx.x * 8 + 0] = clock64();
   const uint32_t glen = G.end - G.start;
   const uint32_t lim = min(G.uend, G.start + GROUP_BYTES + HALO);
   const uint32_t slen = lim - G.start;
@@ -53,6 +54,7 @@ __global__ __launch_bounds__(TL) void k_tables(Work w) {
   // stage (16-byte vector loads; the batch buffer is padded)
   for (uint32_t i = tid * 16; i < slen; i += TL * 16) *(uint4*)(sb + i) = *(const uint4*)(b + G.start + i);
   __syncthreads();
+  if (w.dbg && tid == 0) w.dbg[blockIdx.x * 8 + 1] = clock64();
   // phase A: speculative parse at every byte position.
   //  A0: classify each position by its would-be info byte: non-structs (content ref > 10) and
   //      GC / Skip (info + one varuint) are resolved on the spot;
@@ -97,6 +99,7 @@ __global__ __launch_bounds__(TL) void k_tables(Work w) {
   }
   __syncthreads();
   const uint32_t ncand = bstart[NB];
+  if (w.dbg && tid == 0) w.dbg[blockIdx.x * 8 + 2] = clock64();
   for (uint32_t i = tid; i < ncand; i += TL) {
     const uint32_t o = sorted[i];
     uint32_t q = o;
@@ -110,6 +113,7 @@ __global__ __launch_bounds__(TL) void k_tables(Work w) {
   }
   __syncthreads();
   const uint32_t nq = qn;
+  if (w.dbg && tid == 0) w.dbg[blockIdx.x * 8 + 3] = clock64();
   for (uint32_t i = tid; i < nq; i += TL) {
     const uint32_t o = queue[i];
     uint32_t q = o;
@@ -147,6 +151,7 @@ __global__ __launch_bounds__(TL) void k_tables(Work w) {
     }
     static_assert(6 % 2 == 0, "an even number of rounds leaves the result in cexit/ccnt");
   }
+  if (w.dbg && tid == 0) w.dbg[blockIdx.x * 8 + 4] = clock64();
   // ---- an update that fits in one group is walked right here (its tables never leave LDS): lane 0
   // follows the true chain through the section headers by chunk exits, queueing (position, count)
   // chain pieces, then every lane marks its pieces' struct starts into an LDS copy of the final
@@ -233,6 +238,7 @@ __global__ __launch_bounds__(TL) void k_tables(Work w) {
     }
     __syncthreads();
     for (uint32_t i = tid; i < nwords_g; i += TL) w.final_bits[(G.start >> 6) + i] = bm[i];
+  if (w.dbg && tid == 0) w.dbg[blockIdx.x * 8 + 5] = clock64();
     return;
   }
   // exits are stored as forward deltas from the position itself (|STOPF when the chain stops at a

@@ -96,7 +96,7 @@ enum Buf {
   B_UOWN, B_UFLAG, B_UMIN, B_UCUT, B_UWPRE,
   B_GSTART, B_GCIDX, B_GSRC, B_GFLAGS, B_GORIG, B_GRORIG, B_GLINK, B_GKEY, B_GMAXC, B_GNEXT, B_GOUTID, B_GTMP, B_GTMP2,
   B_KHASH, B_KROOT, B_KWIN, B_KPAR, B_KFLAG, B_SPK,
-  B_USEC, B_USECN,
+  B_USEC, B_USECN, B_DBG,
   B_LZKEY, B_LZKEYS, B_LZIOTA, B_LZSEC, B_LZRSTART, B_LZPREV, B_LZFIRST, B_LZCAP, B_LZEVBASE, B_LZEVN, B_LZFLAG,
   B_LZLHI, B_LZLLO, B_EVKIND, B_EVSRC, B_EVCLOCK, B_EVLEN, B_EVSIZE, B_EVPOS, B_BLKSIZE, B_BLKPOS, B_SVC, B_SVK,
   B_DSMKEY, B_DSMKEYS, B_DSMLEN, B_DSMLENS, B_DSMEND, B_DSMMAX, B_DSMFLAG, B_DSMRID, B_DRCLIENT, B_DRCLOCK, B_DREND,
@@ -343,7 +343,24 @@ int run_decode(ycrdt_engine* e, ycrdt_batch* b, bool lazy, Decoded& D) {
   HIPCHK(hipMemsetAsync(w.sec_bits, 0, nwords * 8, s));
   // ---- K1 decode
   mark(e, "decode.tables");
+  static const bool dbg_tables = getenv("YCRDT_DEBUG_TABLES") && getenv("YCRDT_DEBUG_TABLES")[0] == '1';
+  w.dbg = dbg_tables ? take<unsigned long long>(V, B_DBG, (size_t)w.ngroups * 8 + 8, ok) : nullptr;
+  if (w.dbg) HIPCHK(hipMemsetAsync(w.dbg, 0, sizeof(unsigned long long) * ((size_t)w.ngroups * 8 + 8), s));
   launch_group_parse(w, s);
+  if (w.dbg) {
+    HIPCHK(hipStreamSynchronize(s));
+    std::vector<unsigned long long> h((size_t)w.ngroups * 8);
+    HIPCHK(hipMemcpy(h.data(), w.dbg, sizeof(unsigned long long) * h.size(), hipMemcpyDeviceToHost));
+    double acc[8] = {0};
+    uint32_t n = 0;
+    for (uint32_t g = 0; g < w.ngroups; ++g) {
+      if (!h[g * 8 + 5]) continue;  // multi-group path
+      ++n;
+      for (int k = 1; k <= 5; ++k) acc[k] += (double)(h[g * 8 + k] - h[g * 8 + k - 1]);
+    }
+    fprintf(stderr, "[ycrdt] k_tables cycles per group (%u single-group): stage %.0f  classify+count %.0f  parse %.0f  requeue+B %.0f  walk %.0f\n",
+            n, acc[1] / n, acc[2] / n, acc[3] / n, acc[4] / n, acc[5] / n);
+  }
   mark(e, "decode.walker");
   launch_walker(w, s);
   Counters c;

@@ -60,6 +60,7 @@ struct Work {
   const uint32_t* ugroup = nullptr;// [nupd] first decode group of each update
   uint32_t nupd = 0;
   uint32_t lazy = 0;               // 1: mergeUpdates / diffUpdate decode (references kept raw)
+  unsigned long long* dbg = nullptr; // YCRDT_DEBUG_TABLES=1: per-group phase timestamps of k_tables
   const Group* groups = nullptr;   // [G]
   uint32_t ngroups = 0;
   // ---- capacities
