@@ -133,7 +133,7 @@ __device__ inline bool skip_any(const uint8_t* __restrict__ b, uint32_t& p, uint
         uint32_t n = rd_vu(b, p, end, ok);
         if (!ok) return false;
         if (n > 0) {
-          if (d == DEPTH) return false;
+          if (d == DEPTH) { steps = 0; return false; }  // too deep: "unknown" (-1), never "malformed"
           rem[d] = n;
           if (tag == 118) objmask |= 1u << d; else objmask &= ~(1u << d);
           ++d;

@@ -15,6 +15,8 @@
 //   5. k_ds_decode     one wavefront per update decodes the delete set, a pure varuint stream, with a
 //                      ballot of terminal bytes + in-register gathers (wavefront prefix scan).
 //   6. k_struct_decode one lane per struct: full field decode into the SoA struct table.
+#include <algorithm>
+
 #include "yc_work.h"
 
 namespace yc {
@@ -444,9 +446,11 @@ __global__ __launch_bounds__(256) void k_mark(Work w) {
   __shared__ uint32_t s_cx[4][256], s_cn[4][256];        // chunk spans per wave
   __shared__ uint32_t s_nb[4], s_nc[4][16];
   const uint32_t wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const uint32_t si = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-  const uint32_t nseg = min(w.ctr->ncopy, w.cap_copy);
-  const bool active = si < nseg;  // no early return: every wave reaches the barriers
+  const uint32_t nseg = min(w.ctr->ncopy, w.cap_copy);  // read on the device: no host sync
+  // block-stride loop; the trip count depends on blockIdx only, so every wave reaches the barriers
+  for (uint32_t blk = blockIdx.x; blk * 4 < nseg; blk += gridDim.x) {
+  const uint32_t si = blk * 4 + wv;
+  const bool active = si < nseg;
   CopyTask S{0, 0};
   if (active) S = w.copy[si];
   const Tables& T = w.tab;
@@ -490,17 +494,23 @@ __global__ __launch_bounds__(256) void k_mark(Work w) {
     }
     atomicOr((unsigned long long*)&w.final_bits[word], (unsigned long long)m);
   }
+  __syncthreads();  // the LDS span lists are reused by the next iteration
+  }
 }
 __global__ void k_patch(const uint32_t* __restrict__ patch, const uint32_t* __restrict__ npatch, uint32_t cap, uint64_t* __restrict__ final_bits) {
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= min(*npatch, cap)) return;
-  const uint32_t p = patch[i];
-  atomicOr((unsigned long long*)&final_bits[p >> 6], 1ull << (p & 63));
+  const uint32_t n = min(*npatch, cap);
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    const uint32_t p = patch[i];
+    atomicOr((unsigned long long*)&final_bits[p >> 6], 1ull << (p & 63));
+  }
 }
 
-void launch_build_final_bits(const Work& w, uint32_t nseg, uint32_t npatch, hipStream_t s) {
-  if (nseg) hipLaunchKernelGGL(k_mark, dim3((nseg + 3) / 4), dim3(256), 0, s, w);
-  if (npatch) hipLaunchKernelGGL(k_patch, dim3((npatch + 255) / 256), dim3(256), 0, s, w.patch, &w.ctr->npatch, w.cap_patch, w.final_bits);
+// segment / patch counts are read on the device (grid-stride), so the walker needs no host sync
+void launch_build_final_bits(const Work& w, hipStream_t s) {
+  const uint32_t grid = std::min<uint32_t>(w.ngroups * 4 + 64, 8192);
+  hipLaunchKernelGGL(k_mark, dim3(grid), dim3(256), 0, s, w);
+  hipLaunchKernelGGL(k_patch, dim3(std::min<uint32_t>(w.ngroups * 4 + 64, 4096)), dim3(256), 0, s, w.patch, &w.ctr->npatch,
+                     w.cap_patch, w.final_bits);
 }
 
 // --------------------------------------------------------------------------- 4. struct positions
@@ -713,12 +723,13 @@ __global__ void k_unique_scatter(const uint32_t* __restrict__ v, const uint32_t*
   if (i < n && (i == 0 || v[i] != v[i - 1])) out[pre[i]] = v[i];
   if (i == n) *nout = pre[n];
 }
-__global__ void k_section_cidx(Section* __restrict__ sec, uint32_t n, const uint32_t* __restrict__ cl, uint32_t nc) {
+__global__ void k_section_cidx(Section* __restrict__ sec, uint32_t n, const uint32_t* __restrict__ cl, const uint32_t* nc) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < n) sec[i].cidx = lower_bound_u32(cl, nc, sec[i].client);
+  if (i < n) sec[i].cidx = lower_bound_u32(cl, *nc, sec[i].client);
 }
 
-void launch_client_table(Work& w, uint32_t nsections, uint32_t* nclients_host, hipStream_t s) {
+// NC stays on the device (ctr->nclients) until the struct-decode counter read
+void launch_client_table(Work& w, uint32_t nsections, hipStream_t s) {
   const uint32_t grid = nsections / 256 + 1;
   hipLaunchKernelGGL(k_gather_sec_clients, dim3(grid), dim3(256), 0, s, w.sections, nsections, w.cl_tmp);
   sort_u32(w.tmp, w.tmp_bytes, w.cl_tmp, w.cl_vals, nsections, s);
@@ -727,9 +738,7 @@ void launch_client_table(Work& w, uint32_t nsections, uint32_t* nclients_host, h
   // compact in place is unsafe; use cl_state as scratch output, then copy back
   hipLaunchKernelGGL(k_unique_scatter, dim3(grid), dim3(256), 0, s, w.cl_vals, w.cl_tmp, nsections, w.cl_state, &w.ctr->nclients);
   hipMemcpyAsync(w.cl_vals, w.cl_state, sizeof(uint32_t) * nsections, hipMemcpyDeviceToDevice, s);
-  hipMemcpyAsync(nclients_host, &w.ctr->nclients, sizeof(uint32_t), hipMemcpyDeviceToHost, s);
-  hipStreamSynchronize(s);
-  hipLaunchKernelGGL(k_section_cidx, dim3(grid), dim3(256), 0, s, w.sections, nsections, w.cl_vals, *nclients_host);
+  hipLaunchKernelGGL(k_section_cidx, dim3(grid), dim3(256), 0, s, w.sections, nsections, w.cl_vals, &w.ctr->nclients);
 }
 
 // --------------------------------------------------------------------------- 6. struct decode
@@ -738,9 +747,10 @@ __device__ __forceinline__ uint32_t find_cidx(const uint32_t* __restrict__ cl, u
   return (i < nc && cl[i] == client) ? i : NONE;
 }
 
-__global__ __launch_bounds__(256) void k_struct_decode(Work w, uint32_t nstructs, uint32_t nclients) {
+__global__ __launch_bounds__(256) void k_struct_decode(Work w, uint32_t nstructs) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= nstructs) return;
+  const uint32_t nclients = w.ctr->nclients;
   uint32_t* err = &w.ctr->err;
   const uint32_t p0 = w.s_pos[i];
   const Section sec = w.sections[w.s_sec[i]];
@@ -775,6 +785,7 @@ __global__ __launch_bounds__(256) void k_struct_decode(Work w, uint32_t nstructs
     pb = v.pb;
     if (pa == NONE && !w.lazy) { raise_err(err, ERR_PENDING); w.ctr->err_info = i; }
   }
+  if (pk != 0 && !v.has_psub) w.ctr->narray_roots = 1;  // a YArray list may exist (flag, plain store)
   w.s_pk[i] = (uint8_t)pk;
   w.s_pa[i] = pa;
   w.s_pb[i] = pb;
@@ -798,10 +809,10 @@ __global__ void k_struct_clock(Work w, uint32_t nstructs) {
   w.s_clock[i] = (uint32_t)clock;
 }
 
-void launch_struct_decode(const Work& w, uint32_t nstructs, uint32_t nsections, uint32_t nclients, hipStream_t s) {
+void launch_struct_decode(const Work& w, uint32_t nstructs, hipStream_t s) {
   if (!nstructs) return;
   hipLaunchKernelGGL(k_struct_sec, dim3((nstructs + 255) / 256), dim3(256), 0, s, w, nstructs);
-  hipLaunchKernelGGL(k_struct_decode, dim3((nstructs + 255) / 256), dim3(256), 0, s, w, nstructs, nclients);
+  hipLaunchKernelGGL(k_struct_decode, dim3((nstructs + 255) / 256), dim3(256), 0, s, w, nstructs);
   scan_u32_to_u64(w.tmp, w.tmp_bytes, w.s_len, w.s_lenscan, nstructs + 1, s);
   hipLaunchKernelGGL(k_struct_clock, dim3((nstructs + 255) / 256), dim3(256), 0, s, w, nstructs);
 }
@@ -818,10 +829,16 @@ __global__ void k_states(Work w, uint32_t nstructs) {
   const bool last = i + 1 == nstructs || w.s_sec[i + 1] != w.s_sec[i] || (w.s_info[i + 1] & 31u) == REF_SKIP;
   if (last) atomicMax(&w.cl_state[w.s_cidx[i]], w.s_clock[i] + w.s_len[i]);
 }
-void launch_states(const Work& w, uint32_t nstructs, uint32_t nclients, hipStream_t s) {
-  hipMemsetAsync(w.cl_state, 0, sizeof(uint32_t) * (nclients + 1), s);
+__global__ void k_state_totals(Work w, uint32_t nstructs) {  // U and Σ input lengths into the counters
+  w.ctr->units = w.cl_base[w.ctr->nclients];
+  w.ctr->in_len = w.s_lenscan[nstructs];
+}
+// NC <= nsections: the states are zero past NC, so a scan over nsections + 1 entries gives cl_base
+void launch_states(const Work& w, uint32_t nstructs, uint32_t nsections, hipStream_t s) {
+  hipMemsetAsync(w.cl_state, 0, sizeof(uint32_t) * (nsections + 1), s);
   if (nstructs) hipLaunchKernelGGL(k_states, dim3((nstructs + 255) / 256), dim3(256), 0, s, w, nstructs);
-  scan_u32_to_u64(w.tmp, w.tmp_bytes, w.cl_state, w.cl_base, nclients + 1, s);
+  scan_u32_to_u64(w.tmp, w.tmp_bytes, w.cl_state, w.cl_base, nsections + 1, s);
+  hipLaunchKernelGGL(k_state_totals, dim3(1), dim3(1), 0, s, w, nstructs);
 }
 
 }  // namespace yc

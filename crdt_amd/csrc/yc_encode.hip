@@ -121,10 +121,11 @@ __device__ uint32_t encode_struct(const Work& w, uint32_t nclients, uint32_t o, 
   return size;
 }
 
-__global__ __launch_bounds__(256) void k_out_sizes(Work w, uint32_t nout, uint32_t nclients) {
+// NO (ctr->nout) and the run count (g_tmp2[NS]) stay on the device: grids and scans cover NS + 1
+__global__ __launch_bounds__(256) void k_out_sizes(Work w, uint32_t nsegs, uint32_t nclients) {
   const uint32_t o = blockIdx.x * blockDim.x + threadIdx.x;
-  if (o > nout) return;
-  if (o == nout) { w.o_size[o] = 0; return; }
+  if (o > nsegs) return;
+  if (o >= w.ctr->nout) { w.o_size[o] = 0; return; }
   w.o_cidx[o] = w.g_cidx[w.o_first[o]];
   w.o_size[o] = encode_struct<false>(w, nclients, o, nullptr, 0);
 }
@@ -150,10 +151,10 @@ __global__ void k_run_fill(Work w, uint32_t nsegs) {
   const bool last = s + 1 == nsegs || w.g_cidx[s + 1] != w.g_cidx[s] || !seg_deleted(w.g_flags[s + 1]);
   if (last) w.r_len[rid] = w.g_start[s + 1];  // end unit; the start is subtracted in k_run_sizes
 }
-__global__ void k_run_sizes(Work w, uint32_t nruns) {
+__global__ void k_run_sizes(Work w, uint32_t nsegs) {
   const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
-  if (r > nruns) return;
-  if (r == nruns) { w.r_size[r] = 0; return; }
+  if (r > nsegs) return;
+  if (r >= w.g_tmp2[nsegs]) { w.r_size[r] = 0; return; }
   const uint32_t s = w.r_seg[r];
   const uint32_t len = w.r_len[r] - w.g_start[s];
   w.r_len[r] = len;
@@ -162,9 +163,10 @@ __global__ void k_run_sizes(Work w, uint32_t nruns) {
 }
 
 // per client: struct block + delete-set block + state-vector entry sizes
-__global__ void k_client_sizes(Work w, uint32_t nclients, uint32_t nout, uint32_t nruns) {
+__global__ void k_client_sizes(Work w, uint32_t nclients, uint32_t nsegs) {
   const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
   if (c > nclients) return;
+  const uint32_t nout = w.ctr->nout, nruns = w.g_tmp2[nsegs];
   uint32_t* first_out = ccol(w, CC_FIRST_OUT);
   if (c == nclients) {
     ccol(w, CC_BLK)[c] = 0; ccol(w, CC_DSBLK)[c] = 0; ccol(w, CC_SV)[c] = 0;
@@ -241,11 +243,13 @@ __global__ void k_totals(Work w, uint32_t nclients) {
   w.ctr->pad[4] = vu_size(nincl) + sblk;          // delete-set section start
   w.ctr->out_bytes = vu_size(nincl) + sblk + vu_size(nds) + sds;
   w.ctr->sv_bytes = vu_size(nsv) + ssv;
+  // the output buffers were sized from a bound before the sizes were known; never write past them
+  if (w.ctr->out_bytes > w.cap_out || w.ctr->sv_bytes > w.cap_sv) { w.ctr->pad[5] = 1; raise_err(&w.ctr->err, ERR_CAPACITY); }
 }
 
-__global__ __launch_bounds__(256) void k_write_structs(Work w, uint32_t nout, uint32_t nclients) {
+__global__ __launch_bounds__(256) void k_write_structs(Work w, uint32_t nsegs, uint32_t nclients) {
   const uint32_t o = blockIdx.x * blockDim.x + threadIdx.x;
-  if (o >= nout) return;
+  if (o >= w.ctr->nout || w.ctr->pad[5]) return;
   if (w.o_size[o] == 0) return;
   const uint32_t c = w.o_cidx[o];
   const uint32_t fi = ccol(w, CC_FIRST_INCL)[c];
@@ -254,6 +258,7 @@ __global__ __launch_bounds__(256) void k_write_structs(Work w, uint32_t nout, ui
 }
 __global__ void k_write_clients(Work w, uint32_t nclients) {
   const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (w.ctr->pad[5]) return;
   if (c == 0) {
     wr_vu(w.out, 0, w.ctr->pad[0]);
     wr_vu(w.out, w.ctr->pad[4], w.ctr->pad[1]);
@@ -279,9 +284,9 @@ __global__ void k_write_clients(Work w, uint32_t nclients) {
     wr_vu(w.sv_out, p, w.cl_state[c]);
   }
 }
-__global__ void k_write_runs(Work w, uint32_t nruns) {
+__global__ void k_write_runs(Work w, uint32_t nsegs) {
   const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
-  if (r >= nruns) return;
+  if (r >= w.g_tmp2[nsegs] || w.ctr->pad[5]) return;
   const uint32_t s = w.r_seg[r];
   const uint32_t c = w.g_cidx[s];
   const uint32_t first = ccol(w, CC_FIRST_RUN)[c];
@@ -300,33 +305,34 @@ static void rev_scan(const Work& w, uint32_t nclients, uint32_t col_in, uint32_t
   hipLaunchKernelGGL(k_unreverse, dim3(grid), dim3(256), 0, s, w, nclients, col_out);
 }
 
-// Phase 1: sizes + layout (ends with out_bytes / sv_bytes in the counters)
-void launch_encode_sizes(const Work& w, uint32_t nsegs, uint32_t nclients, uint32_t nout, uint32_t* nruns_host, hipStream_t s) {
+// Phase 1: sizes + layout (ends with out_bytes / sv_bytes in the counters). No host sync: the
+// output / run counts are read on the device, grids and scans are sized for NS + 1 entries.
+void launch_encode_sizes(const Work& w, uint32_t nsegs, uint32_t nclients, hipStream_t s) {
   hipMemsetAsync(w.ctr->pad, 0, sizeof(uint32_t) * 8, s);
   hipMemsetAsync(w.cc + (size_t)CC_NRUNS * (w.cap_clients + 1), 0, sizeof(uint32_t) * (w.cap_clients + 1), s);
-  hipLaunchKernelGGL(k_out_sizes, dim3(nout / 256 + 1), dim3(256), 0, s, w, nout, nclients);
-  scan_u32(w.tmp, w.tmp_bytes, w.o_size, w.o_pos, nout + 1, s);
+  const uint32_t grid = nsegs / 256 + 1;
+  hipLaunchKernelGGL(k_out_sizes, dim3(grid), dim3(256), 0, s, w, nsegs, nclients);
+  scan_u32(w.tmp, w.tmp_bytes, w.o_size, w.o_pos, nsegs + 1, s);
   // delete-set runs
-  hipLaunchKernelGGL(k_run_flags, dim3(nsegs / 256 + 1), dim3(256), 0, s, w, nsegs);
+  hipLaunchKernelGGL(k_run_flags, dim3(grid), dim3(256), 0, s, w, nsegs);
   scan_u32(w.tmp, w.tmp_bytes, w.g_tmp, w.g_tmp2, nsegs + 1, s);
-  hipMemcpyAsync(nruns_host, w.g_tmp2 + nsegs, sizeof(uint32_t), hipMemcpyDeviceToHost, s);
-  hipStreamSynchronize(s);
-  const uint32_t nruns = *nruns_host;
   if (nsegs) hipLaunchKernelGGL(k_run_fill, dim3((nsegs + 255) / 256), dim3(256), 0, s, w, nsegs);
-  hipLaunchKernelGGL(k_run_sizes, dim3(nruns / 256 + 1), dim3(256), 0, s, w, nruns);
-  scan_u32(w.tmp, w.tmp_bytes, w.r_size, w.r_pos, nruns + 1, s);
-  hipLaunchKernelGGL(k_client_sizes, dim3(nclients / 256 + 1), dim3(256), 0, s, w, nclients, nout, nruns);
+  hipLaunchKernelGGL(k_run_sizes, dim3(grid), dim3(256), 0, s, w, nsegs);
+  scan_u32(w.tmp, w.tmp_bytes, w.r_size, w.r_pos, nsegs + 1, s);
+  hipLaunchKernelGGL(k_client_sizes, dim3(nclients / 256 + 1), dim3(256), 0, s, w, nclients, nsegs);
   rev_scan(w, nclients, CC_BLK, CC_BLKPOS, s);
   rev_scan(w, nclients, CC_DSBLK, CC_DSPOS, s);
   rev_scan(w, nclients, CC_SV, CC_SVPOS, s);
   hipLaunchKernelGGL(k_totals, dim3(1), dim3(1), 0, s, w, nclients);
 }
 
-// Phase 2: write bytes (buffers sized from phase 1)
-void launch_encode_write(const Work& w, uint32_t nclients, uint32_t nout, uint32_t nruns, hipStream_t s) {
+// Phase 2: write bytes (buffers sized from a bound, checked in k_totals)
+void launch_encode_write(const Work& w, uint32_t nsegs, uint32_t nclients, hipStream_t s) {
   hipLaunchKernelGGL(k_write_clients, dim3(nclients / 256 + 1), dim3(256), 0, s, w, nclients);
-  if (nout) hipLaunchKernelGGL(k_write_structs, dim3((nout + 255) / 256), dim3(256), 0, s, w, nout, nclients);
-  if (nruns) hipLaunchKernelGGL(k_write_runs, dim3((nruns + 255) / 256), dim3(256), 0, s, w, nruns);
+  if (nsegs) {
+    hipLaunchKernelGGL(k_write_structs, dim3((nsegs + 255) / 256), dim3(256), 0, s, w, nsegs, nclients);
+    hipLaunchKernelGGL(k_write_runs, dim3((nsegs + 255) / 256), dim3(256), 0, s, w, nsegs);
+  }
 }
 
 }  // namespace yc

@@ -240,7 +240,8 @@ int check(ycrdt_engine* e, Counters& c, const char* where) {
 
 struct Decoded {
   uint32_t nstructs = 0, nsections = 0, nclients = 0, nds = 0;
-  uint64_t nunits = 0;
+  uint64_t nunits = 0, in_len = 0;
+  uint32_t array_roots = 0;  // 1: some item names a parent without a parentSub (a YArray may exist)
 };
 
 // K1: decode every update of the batch into the struct SoA (+ client table, delete-set ranges).
@@ -363,32 +364,29 @@ int run_decode(ycrdt_engine* e, ycrdt_batch* b, bool lazy, Decoded& D) {
   }
   mark(e, "decode.walker");
   launch_walker(w, s);
+  mark(e, "decode.bitmap");
+  launch_build_final_bits(w, s);
+  launch_struct_positions(w, s);
+  HIPCHK(hipMemcpyAsync(&w.ctr->nstructs, w.wcnt + (w.nbytes + 63) / 64, sizeof(uint32_t), hipMemcpyDeviceToDevice, s));
   Counters c;
   int rc = check(e, c, "decode");
   if (rc) return rc;
-  mark(e, "decode.bitmap");
-  launch_build_final_bits(w, std::min(c.ncopy, w.cap_copy), std::min(c.npatch, w.cap_patch), s);
-  launch_struct_positions(w, s);
-  uint32_t nstructs = 0;
-  HIPCHK(hipMemcpyAsync(&nstructs, w.wcnt + (w.nbytes + 63) / 64, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
-  HIPCHK(hipStreamSynchronize(s));
+  const uint32_t nstructs = c.nstructs;
   const uint32_t nsections = c.nsections;
   mark(e, "decode.sections");
   launch_section_clients(w, nsections, s);
   launch_ds_decode(w, s);
-  uint32_t nclients = 0;
-  if (nsections) launch_client_table(w, nsections, &nclients, s);
+  if (nsections) launch_client_table(w, nsections, s);
   mark(e, "decode.structs");
-  launch_struct_decode(w, nstructs, nsections, nclients, s);
-  HIPCHK(hipMemsetAsync(w.cl_start, 0, sizeof(uint32_t) * (nclients + 1), s));
-  if (!lazy) launch_states(w, nstructs, nclients, s);
+  launch_struct_decode(w, nstructs, s);
+  HIPCHK(hipMemsetAsync(w.cl_start, 0, sizeof(uint32_t) * (nsections + 1), s));
+  if (!lazy) launch_states(w, nstructs, nsections, s);
   rc = check(e, c, "struct decode");
   if (rc) return rc;
-  uint64_t nunits = 0;
-  if (!lazy) {
-    HIPCHK(hipMemcpyAsync(&nunits, w.cl_base + nclients, sizeof(uint64_t), hipMemcpyDeviceToHost, s));
-    HIPCHK(hipStreamSynchronize(s));
-  }
+  const uint32_t nclients = c.nclients;
+  const uint64_t nunits = lazy ? 0 : c.units;
+  D.in_len = c.in_len;
+  D.array_roots = c.narray_roots;
   if (nunits >= 0xF0000000ull) return fail(YCRDT_E_CAPACITY, "more than 2^32 units in one batch");
   D.nstructs = nstructs;
   D.nsections = nsections;
@@ -500,42 +498,40 @@ int run_merge(ycrdt_engine* e, ycrdt_batch* b, const std::unordered_map<uint32_t
     mark(e, "merge.dead_types");
     run_dead_keys(w, nsegs, s);
     mark(e, "merge.yata");
-    uint32_t narray = 0;  // read after the descent / dead-type rounds (already synchronised)
-    HIPCHK(hipMemcpyAsync(&narray, &w.ctr->narray, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
-    HIPCHK(hipStreamSynchronize(s));
+    uint32_t narray = 0;  // YArray members; only read when the decode saw a possible array root
+    if (D.array_roots) {
+      HIPCHK(hipMemcpyAsync(&narray, &w.ctr->narray, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+      HIPCHK(hipStreamSynchronize(s));
+    }
     launch_yata(w, nsegs, narray, s);
     mark(e, "merge.merge_flags");
     launch_merge_flags(w, nsegs, s);
-    rc = check(e, c, "merge");
-    if (rc) return rc;
-    nout = c.nout;
   }
-  // ---- K7 encode
-  mark(e, "encode.sizes");
-  uint32_t nruns = 0;
-  launch_encode_sizes(w, nsegs, nclients, nout, &nruns, s);
-  rc = check(e, c, "encode sizes");
-  if (rc) return rc;
-  w.out = take<uint8_t>(V, B_OUT, (size_t)c.out_bytes + 16, ok);
-  w.sv_out = take<uint8_t>(V, B_SVOUT, (size_t)c.sv_bytes + 16, ok);
+  // ---- K7 encode. Output bound: every output struct adds at most 37 bytes of header (info,
+  // origin, right origin, parent, length prefix) to content bytes sliced from the input, every
+  // delete-set run at most 10, every client block / state-vector entry at most 15 + 10.
+  if (!nsegs) HIPCHK(hipMemsetAsync(&w.ctr->nout, 0, sizeof(uint32_t), s));
+  w.cap_out = (uint64_t)b->nbytes + 48ull * nsegs + 32ull * nclients + 64;
+  w.cap_sv = 16ull + 10ull * nclients;
+  w.out = take<uint8_t>(V, B_OUT, (size_t)w.cap_out + 16, ok);
+  w.sv_out = take<uint8_t>(V, B_SVOUT, (size_t)w.cap_sv + 16, ok);
   if (!ok) return fail(YCRDT_E_DEVICE, "hipMalloc failed (output)");
+  mark(e, "encode.sizes");
+  launch_encode_sizes(w, nsegs, nclients, s);
   mark(e, "encode.write");
-  launch_encode_write(w, nclients, nout, nruns, s);
+  launch_encode_write(w, nsegs, nclients, s);
   mark(e, "end");
   HIPCHK(hipEventRecord(e->ev1, s));
-  rc = check(e, c, "encode");
+  rc = check(e, c, "merge / encode");
   if (rc) return rc;
+  nout = nsegs ? c.nout : 0;
   e->out_bytes = c.out_bytes;
   e->sv_bytes = c.sv_bytes;
   float ms = 0;
   hipEventElapsedTime(&ms, e->ev0, e->ev1);
   ycrdt_merge_stats& st = e->last;
   st.in_bytes = b->in_bytes;
-  {
-    uint64_t total_len = 0;
-    hipMemcpy(&total_len, w.s_lenscan + nstructs, sizeof(uint64_t), hipMemcpyDeviceToHost);
-    st.items = nstructs ? total_len - c.items : 0;  // Item + GC clock lengths (Skip excluded)
-  }
+  st.items = nstructs ? D.in_len - c.items : 0;  // Item + GC clock lengths (Skip excluded)
   st.structs = nstructs;
   st.units = U;
   st.segments = nsegs;

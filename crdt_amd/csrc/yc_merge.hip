@@ -17,6 +17,8 @@
 //   k_overwrite    every non-rightmost entry of a key is deleted (typeMapSet / left.delete)
 //   k_merge_flags  Item.mergeWith (Y@79424) / tryToMergeWithLeft (Y@30960) as a pairwise
 //                  predicate over adjacent segments ⇒ canonical (maximally merged) structs
+#include <algorithm>
+
 #include "yc_work.h"
 
 namespace yc {
@@ -28,29 +30,32 @@ __device__ __forceinline__ uint32_t seg_of(const uint64_t* __restrict__ cut, con
 }
 
 // --------------------------------------------------------------------------- owner / dedupe
-__global__ __launch_bounds__(256) void k_owner(Work w, uint32_t nstructs, uint64_t total_in) {
-  const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  uint64_t j = t * OWNER_UNITS_PER_LANE;
-  if (j >= total_in) return;
-  const uint64_t jend = min(j + OWNER_UNITS_PER_LANE, total_in);
+// grid-stride over the Σ input clock lengths (read on the device: no host sync for the bound)
+__global__ __launch_bounds__(256) void k_owner(Work w, uint32_t nstructs) {
+  const uint64_t total_in = w.s_lenscan[nstructs];
+  const uint64_t nlanes = (total_in + OWNER_UNITS_PER_LANE - 1) / OWNER_UNITS_PER_LANE;
   const uint64_t* __restrict__ P = w.s_lenscan;
-  uint32_t lo = 0, hi = nstructs;  // last s with P[s] <= j
-  while (hi - lo > 1) { const uint32_t mid = (lo + hi) >> 1; if (P[mid] <= j) lo = mid; else hi = mid; }
-  uint32_t s = lo;
-  while (j < jend) {
-    while (P[s + 1] <= j) ++s;
-    const uint64_t send = min(jend, P[s + 1]);
-    const uint32_t ref = w.s_info[s] & 31u;
-    if (ref != REF_SKIP) {
-      const uint32_t cidx = w.s_cidx[s];
-      const uint64_t gb = w.cl_base[cidx] + w.s_clock[s] - P[s];
-      const uint32_t fl = ref == REF_DELETED ? UF_DEL : (ref == REF_GC ? (UF_GC | UF_DEL) : 0u);
-      for (; j < send; ++j) {
-        const uint32_t g = (uint32_t)(gb + j);
-        atomicMin(&w.u_owner[g], s);
-        if (fl) atomicOr(&w.u_flags[g], fl);
-      }
-    } else j = send;
+  for (uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; t < nlanes; t += (uint64_t)gridDim.x * blockDim.x) {
+    uint64_t j = t * OWNER_UNITS_PER_LANE;
+    const uint64_t jend = min(j + OWNER_UNITS_PER_LANE, total_in);
+    uint32_t lo = 0, hi = nstructs;  // last s with P[s] <= j
+    while (hi - lo > 1) { const uint32_t mid = (lo + hi) >> 1; if (P[mid] <= j) lo = mid; else hi = mid; }
+    uint32_t s = lo;
+    while (j < jend) {
+      while (P[s + 1] <= j) ++s;
+      const uint64_t send = min(jend, P[s + 1]);
+      const uint32_t ref = w.s_info[s] & 31u;
+      if (ref != REF_SKIP) {
+        const uint32_t cidx = w.s_cidx[s];
+        const uint64_t gb = w.cl_base[cidx] + w.s_clock[s] - P[s];
+        const uint32_t fl = ref == REF_DELETED ? UF_DEL : (ref == REF_GC ? (UF_GC | UF_DEL) : 0u);
+        for (; j < send; ++j) {
+          const uint32_t g = (uint32_t)(gb + j);
+          atomicMin(&w.u_owner[g], s);
+          if (fl) atomicOr(&w.u_flags[g], fl);
+        }
+      } else j = send;
+    }
   }
 }
 
@@ -69,22 +74,24 @@ __global__ void k_ds_prep(Work w, uint32_t nds, uint32_t nclients) {
   w.ds[i] = r;
   w.ds_len[i] = len;
 }
-__global__ __launch_bounds__(256) void k_ds_mark(Work w, uint32_t nds, uint64_t total) {
-  const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  uint64_t j = t * OWNER_UNITS_PER_LANE;
-  if (j >= total) return;
-  const uint64_t jend = min(j + OWNER_UNITS_PER_LANE, total);
+__global__ __launch_bounds__(256) void k_ds_mark(Work w, uint32_t nds) {
+  const uint64_t total = w.ds_scan[nds];
+  const uint64_t nlanes = (total + OWNER_UNITS_PER_LANE - 1) / OWNER_UNITS_PER_LANE;
   const uint64_t* __restrict__ P = w.ds_scan;
-  uint32_t lo = 0, hi = nds;
-  while (hi - lo > 1) { const uint32_t mid = (lo + hi) >> 1; if (P[mid] <= j) lo = mid; else hi = mid; }
-  uint32_t s = lo;
-  while (j < jend) {
-    while (P[s + 1] <= j) ++s;
-    const uint64_t send = min(jend, P[s + 1]);
-    const DsRange r = w.ds[s];
-    const uint64_t gb = w.cl_base[r.client] + r.clock - P[s];
-    // only UF_DS is written in this kernel: concurrent plain ORs of the same bit are harmless
-    for (; j < send; ++j) w.u_flags[(uint32_t)(gb + j)] |= UF_DS;
+  for (uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; t < nlanes; t += (uint64_t)gridDim.x * blockDim.x) {
+    uint64_t j = t * OWNER_UNITS_PER_LANE;
+    const uint64_t jend = min(j + OWNER_UNITS_PER_LANE, total);
+    uint32_t lo = 0, hi = nds;
+    while (hi - lo > 1) { const uint32_t mid = (lo + hi) >> 1; if (P[mid] <= j) lo = mid; else hi = mid; }
+    uint32_t s = lo;
+    while (j < jend) {
+      while (P[s + 1] <= j) ++s;
+      const uint64_t send = min(jend, P[s + 1]);
+      const DsRange r = w.ds[s];
+      const uint64_t gb = w.cl_base[r.client] + r.clock - P[s];
+      // only UF_DS is written in this kernel: concurrent plain ORs of the same bit are harmless
+      for (; j < send; ++j) w.u_flags[(uint32_t)(gb + j)] |= UF_DS;
+    }
   }
 }
 
@@ -161,24 +168,14 @@ void launch_units(const Work& w, uint32_t nstructs, uint32_t nclients, uint32_t 
   hipMemsetAsync(w.u_owner, 0xFF, sizeof(uint32_t) * nunits, s);
   hipMemsetAsync(w.u_flags, 0, sizeof(uint32_t) * nunits, s);
   hipMemsetAsync(w.u_minchild, 0xFF, sizeof(uint32_t) * nunits, s);
-  // owner (needs total input units = s_lenscan[nstructs], read on device by the kernel bound)
-  uint64_t total_in = 0;
-  hipMemcpyAsync(&total_in, w.s_lenscan + nstructs, sizeof(uint64_t), hipMemcpyDeviceToHost, s);
-  hipStreamSynchronize(s);
-  if (total_in) {
-    const uint64_t lanes = (total_in + OWNER_UNITS_PER_LANE - 1) / OWNER_UNITS_PER_LANE;
-    hipLaunchKernelGGL(k_owner, dim3((uint32_t)((lanes + 255) / 256)), dim3(256), 0, s, w, nstructs, total_in);
-  }
+  // the unit counts these kernels cover (Σ input lengths, Σ delete-set lengths) are read on the
+  // device; the grids are sized for one pass over the merged store and stride beyond it
+  const uint32_t grid = (uint32_t)std::min<uint64_t>(nunits / (OWNER_UNITS_PER_LANE * 256) + 1, 8192);
+  if (nstructs) hipLaunchKernelGGL(k_owner, dim3(grid), dim3(256), 0, s, w, nstructs);
   if (nds) {
     hipLaunchKernelGGL(k_ds_prep, dim3(nds / 256 + 1), dim3(256), 0, s, w, nds, nclients);
     scan_u32_to_u64(w.tmp, w.tmp_bytes, w.ds_len, w.ds_scan, nds + 1, s);
-    uint64_t total_ds = 0;
-    hipMemcpyAsync(&total_ds, w.ds_scan + nds, sizeof(uint64_t), hipMemcpyDeviceToHost, s);
-    hipStreamSynchronize(s);
-    if (total_ds) {
-      const uint64_t lanes = (total_ds + OWNER_UNITS_PER_LANE - 1) / OWNER_UNITS_PER_LANE;
-      hipLaunchKernelGGL(k_ds_mark, dim3((uint32_t)((lanes + 255) / 256)), dim3(256), 0, s, w, nds, total_ds);
-    }
+    hipLaunchKernelGGL(k_ds_mark, dim3(grid), dim3(256), 0, s, w, nds);
   }
   if (nstructs) hipLaunchKernelGGL(k_refs, dim3((nstructs + 255) / 256), dim3(256), 0, s, w, nstructs);
 }
@@ -413,14 +410,20 @@ __global__ void k_dead_init(Work w) {
   const bool is_type = (w.s_info[w.g_src[p]] & 31u) == REF_TYPE;
   if ((pf & SEG_DEL) || !(pf & SEG_ITEM) || !is_type) w.k_flags[k] |= KF_DEAD;
 }
-__global__ void k_dead_prop(Work w) {
+// every list climbs its chain of parent lists (nesting depth) to the first dead one, if any;
+// KF_DEAD only ever gets set, so reading a flag another lane is setting is safe
+__global__ void k_dead_climb(Work w) {
   const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
-  if (k >= w.cap_keys || w.k_hash[k] == 0) return;
-  const uint32_t kf = w.k_flags[k];
-  const uint32_t pu = w.k_parent[k];
-  if ((kf & KF_DEAD) || pu == NONE) return;
-  const uint32_t pk = w.g_key[seg_of(w.u_cutbits, w.u_wpre, pu)];
-  if (pk != NONE && (w.k_flags[pk] & KF_DEAD)) { w.k_flags[k] = kf | KF_DEAD; w.ctr->changed = 1; }
+  if (k >= w.cap_keys || w.k_hash[k] == 0 || (w.k_flags[k] & KF_DEAD)) return;
+  uint32_t x = k;
+  for (uint32_t depth = 0; depth < (1u << 20); ++depth) {
+    const uint32_t pu = w.k_parent[x];
+    if (pu == NONE) return;  // a root type: alive
+    const uint32_t pk = w.g_key[seg_of(w.u_cutbits, w.u_wpre, pu)];
+    if (pk == NONE) return;
+    if (w.k_flags[pk] & KF_DEAD) { atomicOr(&w.k_flags[k], KF_DEAD); return; }
+    x = pk;
+  }
 }
 __global__ void k_dead_apply(Work w, uint32_t nsegs) {
   const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
@@ -436,14 +439,7 @@ void run_dead_keys(const Work& w, uint32_t nsegs, hipStream_t s) {
   if (!nsegs) return;
   const uint32_t kg = w.cap_keys / 256 + 1;
   hipLaunchKernelGGL(k_dead_init, dim3(kg), dim3(256), 0, s, w);
-  for (int round = 0; round < 64; ++round) {
-    hipMemsetAsync(&w.ctr->changed, 0, sizeof(uint32_t), s);
-    hipLaunchKernelGGL(k_dead_prop, dim3(kg), dim3(256), 0, s, w);
-    uint32_t changed = 0;
-    hipMemcpyAsync(&changed, &w.ctr->changed, sizeof(uint32_t), hipMemcpyDeviceToHost, s);
-    hipStreamSynchronize(s);
-    if (!changed) break;
-  }
+  hipLaunchKernelGGL(k_dead_climb, dim3(kg), dim3(256), 0, s, w);
   hipLaunchKernelGGL(k_dead_apply, dim3((nsegs + 255) / 256), dim3(256), 0, s, w, nsegs);
 }
 

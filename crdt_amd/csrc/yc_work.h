@@ -28,8 +28,11 @@ struct Counters {            // device-side counters, read back at the few host 
   uint32_t nkeys;            // distinct map keys
   uint32_t nruns;            // delete-set runs in the output
   uint32_t narray;           // YArray list members (segments)
-  uint32_t pad[13];          // encode scratch (see yc_encode.hip)
+  uint32_t narray_roots;     // 1: a decoded item may root a YArray list (parent given, no parentSub)
+  uint32_t pad[12];          // encode scratch (see yc_encode.hip)
   unsigned long long items;  // Σ clock lengths of Skip structs (items = Σ all lengths − this)
+  unsigned long long units;  // U = cl_base[NC] (copied on the device before a counter read)
+  unsigned long long in_len; // Σ input clock lengths = s_lenscan[S] (same)
 };
 
 struct DsRange {             // one decoded (client, clock, len) delete-set range
@@ -207,6 +210,7 @@ struct Work {
   uint32_t cap_clients = 0;
   uint8_t* out = nullptr;          // encoded update
   uint64_t cap_out = 0;
+  uint64_t cap_sv = 0;
   uint8_t* sv_out = nullptr;       // encoded state vector
   uint32_t* scratch = nullptr;     // scan staging (max of all scan lengths)
   // ---- rocPRIM scratch
@@ -302,13 +306,13 @@ enum : uint32_t {
 // ---- launch entry points (yc_decode.hip / yc_merge.hip / yc_encode.hip / yc_prims.hip)
 void launch_group_parse(const Work& w, hipStream_t s);
 void launch_walker(const Work& w, hipStream_t s);
-void launch_build_final_bits(const Work& w, uint32_t nseg, uint32_t npatch, hipStream_t s);
+void launch_build_final_bits(const Work& w, hipStream_t s);
 void launch_struct_positions(const Work& w, hipStream_t s);
 void launch_ds_decode(const Work& w, hipStream_t s);
 void launch_section_clients(const Work& w, uint32_t nsections, hipStream_t s);
-void launch_client_table(Work& w, uint32_t nsections, uint32_t* nclients_host, hipStream_t s);
-void launch_struct_decode(const Work& w, uint32_t nstructs, uint32_t nsections, uint32_t nclients, hipStream_t s);
-void launch_states(const Work& w, uint32_t nstructs, uint32_t nclients, hipStream_t s);
+void launch_client_table(Work& w, uint32_t nsections, hipStream_t s);
+void launch_struct_decode(const Work& w, uint32_t nstructs, hipStream_t s);
+void launch_states(const Work& w, uint32_t nstructs, uint32_t nsections, hipStream_t s);
 
 void launch_units(const Work& w, uint32_t nstructs, uint32_t nclients, uint32_t nds, uint64_t nunits, hipStream_t s);
 void launch_segments(const Work& w, uint32_t nclients, uint64_t nunits, hipStream_t s);
@@ -320,8 +324,8 @@ void launch_merge_flags(const Work& w, uint32_t nsegs, hipStream_t s);
 void run_dead_keys(const Work& w, uint32_t nsegs, hipStream_t s);
 uint32_t launch_yata(const Work& w, uint32_t nsegs, uint32_t narray, hipStream_t s);
 
-void launch_encode_sizes(const Work& w, uint32_t nsegs, uint32_t nclients, uint32_t nout, uint32_t* nruns_host, hipStream_t s);
-void launch_encode_write(const Work& w, uint32_t nclients, uint32_t nout, uint32_t nruns, hipStream_t s);
+void launch_encode_sizes(const Work& w, uint32_t nsegs, uint32_t nclients, hipStream_t s);
+void launch_encode_write(const Work& w, uint32_t nsegs, uint32_t nclients, hipStream_t s);
 
 // rocPRIM wrappers (yc_prims.hip)
 size_t prim_tmp_bytes(uint64_t max_items);
