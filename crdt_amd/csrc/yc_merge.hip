@@ -104,8 +104,6 @@ __global__ void k_refs(Work w, uint32_t nstructs) {
     const uint32_t k = w.s_oclock[i];
     if (k >= w.cl_state[oc]) { raise_err(&w.ctr->err, ERR_PENDING); return; }
     const uint32_t g = (uint32_t)(w.cl_base[oc] + k);
-    const uint32_t ci = w.s_cidx[i];
-    if (w.u_minchild[g] > ci) atomicMin(&w.u_minchild[g], ci);  // read first: hot origins are shared
     // getItemCleanEnd(origin); only UF_CUT is written to u_flags in this kernel, so a plain
     // read-modify-write that races with another writer of the same bit is harmless
     if (k + 1 < w.cl_state[oc] && !(w.u_flags[g + 1] & UF_CUT)) w.u_flags[g + 1] |= UF_CUT;
@@ -345,17 +343,25 @@ uint32_t run_key_resolution(const Work& w, uint32_t nsegs, hipStream_t s) {
 }
 
 // --------------------------------------------------------------------------- map winner
-__global__ __launch_bounds__(256) void k_children(Work w, uint32_t nsegs) {
-  const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
-  if (s >= nsegs) return;
+// Per YMap entry: max-client child of its origin (the winner descent) and min-client child of its
+// origin unit (YATA puts it right after the origin: merge adjacency). The base entry of a hot key
+// has a child from every replica, and contended device-scope atomics serialise at the memory side,
+// so every lane reads first and the segments (sorted by client) run in three launches: the top
+// clients first (they settle every max), then the bottom ones (they settle every min), then the
+// rest, which then finds almost every slot already decided and issues no atomic.
+__global__ __launch_bounds__(256) void k_children(Work w, uint32_t lo, uint32_t hi) {
+  const uint32_t s = lo + blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= hi) return;
   const uint32_t f = w.g_flags[s];
   if (!(f & SEG_PSUB)) return;
   const uint32_t key = w.g_key[s];
-  const unsigned long long v = ((unsigned long long)(w.g_cidx[s] + 1) << 32) | s;
+  const uint32_t cidx = w.g_cidx[s];
+  const unsigned long long v = ((unsigned long long)(cidx + 1) << 32) | s;
   const uint32_t o = w.g_origin[s];
   if (o != NONE) {
+    if (w.u_minchild[o] > cidx) atomicMin(&w.u_minchild[o], cidx);
     unsigned long long* dst = (unsigned long long*)&w.g_maxchild[seg_of(w.u_cutbits, w.u_wpre, o)];
-    if (*dst < v) atomicMax(dst, v);  // read first: the base entries of hot keys have ~1k children
+    if (*dst < v) atomicMax(dst, v);
   } else if (f & SEG_ROOT) {
     unsigned long long* dst = (unsigned long long*)&w.k_rootmax[key];
     if (*dst < v) atomicMax(dst, v);
@@ -386,7 +392,10 @@ __global__ void k_overwrite(Work w, uint32_t nsegs) {
 
 void launch_map_winner(const Work& w, uint32_t nsegs, hipStream_t s) {
   if (!nsegs) return;
-  hipLaunchKernelGGL(k_children, dim3((nsegs + 255) / 256), dim3(256), 0, s, w, nsegs);
+  const uint32_t a = nsegs / 16, b = nsegs - nsegs / 16;
+  const uint32_t ranges[3][2] = {{b, nsegs}, {0, a}, {a, b}};
+  for (auto& r : ranges)
+    if (r[1] > r[0]) hipLaunchKernelGGL(k_children, dim3((r[1] - r[0] + 255) / 256), dim3(256), 0, s, w, r[0], r[1]);
 }
 
 uint32_t run_descent(const Work& w, uint32_t nsegs, hipStream_t s) {
