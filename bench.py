@@ -18,6 +18,8 @@ data-path collective ⇒ "scaling": "weak". torch.distributed (RCCL) is used onl
 and the max-over-ranks of the step time.
 """
 import argparse
+import csv
+import glob
 import json
 import os
 import sys
@@ -81,15 +83,21 @@ def main():
             dist.all_reduce(t)
             torch.cuda.synchronize()
 
-    # ---- timed region: K merges, inputs resident in HBM
+    # ---- timed region: K merges, inputs resident in HBM. The engine's phase events stay on: they
+    # time the dominant kernel live, on the engine stream it runs on (roofline below).
+    eng.set_profiling(True)
+    phase_acc = {}
     barrier()
     t0 = time.perf_counter()
     dev_ms = 0.0
     for _ in range(args.steps):
         st = batch.merge()  # synchronous: returns after the device finished
         dev_ms += st.device_ms
+        for name, ms in eng.phase_times():
+            phase_acc[name] = phase_acc.get(name, 0.0) + ms
     barrier()
     t1 = time.perf_counter()
+    eng.set_profiling(False)
     dt = t1 - t0
     if dist is not None:
         import torch
@@ -104,32 +112,52 @@ def main():
         items_step = float(st.items)
     ms_per_step = dt * 1e3 / args.steps
     value = items_step * args.steps / dt
+    phases = [(n, m / args.steps) for n, m in phase_acc.items()]
 
-    # ---- per-phase device times (events on the engine stream), one extra profiled merge
-    eng.set_profiling(True)
-    batch.merge()
-    phases = eng.phase_times()
-    eng.set_profiling(False)
-
+    # ---- roofline of the dominant kernel. k_tables (K1 chain tables) is the largest single-kernel
+    # phase; its algorithmic traffic is the input bytes it parses, read once (SURVEY.md §8(d):
+    # B_in), and its duration is the HIP-event time of the "decode.tables" phase, which holds that
+    # one launch. `traffic` is the HBM bytes per launch from the committed rocprofv3 PMC pass
+    # (2 x FETCH_SIZE + WRITE_SIZE, gfx950 correction; scripts/pmc.sh + scripts/pmc_summary.py).
+    ph = dict(phases)
+    k_ms = ph.get("decode.tables", 0.0)
+    alg = in_bytes
+    traffic, traffic_src = None, None
+    pmc = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_c2_pmc.csv")))
+    if pmc:
+        with open(pmc[-1]) as f:
+            for r in csv.DictReader(f):
+                if r["kernel"] == "yc::k_tables":
+                    traffic = int(float(r["hbm_bytes"]))
+                    traffic_src = os.path.basename(pmc[-1])
+    achieved = alg / (k_ms * 1e-3) / 1e9 if k_ms > 0 else 0.0
+    dominant = max(phases, key=lambda p: p[1]) if phases else ("merge", st.device_ms)
+    roofline = {
+        "bound": "hbm",
+        "kernel": "yc::k_tables",
+        "achieved": round(achieved, 2),
+        "peak": HBM_PEAK_GBS,
+        "unit": "GB/s",
+        "frac": round(achieved / HBM_PEAK_GBS, 5),
+        "traffic": traffic,
+        "traffic_unit": "HBM bytes per launch",
+        "traffic_source": traffic_src,
+        "alg_bytes_per_launch": alg,
+        "avg_launch_ms": round(k_ms, 4),
+        "largest_phase": {"name": dominant[0], "ms": round(dominant[1], 4)},
+    }
     # algorithmic bytes of the whole merge: B_in + B_out + 64·S
     b_alg = in_bytes + len(out_update) + len(out_sv) + 64 * st.structs
-    roofline = None
-    kern = os.environ.get("YCRDT_ROOFLINE_JSON")
-    if kern and os.path.exists(kern):
-        with open(kern) as f:
-            roofline = json.load(f)
-    if roofline is None:
-        dominant = max(phases, key=lambda p: p[1]) if phases else ("merge", st.device_ms)
-        roofline = {
-            "bound": "hbm",
-            "kernel": "whole merge pipeline (per-kernel rocprof summary in profiles/)",
-            "achieved": round(b_alg / (st.device_ms * 1e-3) / 1e9, 2),
-            "peak": HBM_PEAK_GBS,
-            "unit": "GB/s",
-            "frac": round(b_alg / (st.device_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 5),
-            "traffic": None,
-            "dominant_phase": {"name": dominant[0], "ms": round(dominant[1], 4)},
-        }
+
+    # ---- end to end (host buffers in, host buffers out): pack + H2D + merge + D2H; never `value`
+    e2e_steps = 3
+    e0 = time.perf_counter()
+    for _ in range(e2e_steps):
+        b2 = crdt_amd.Batch(updates, eng)
+        b2.merge()
+        b2.result()
+        del b2
+    e2e_ms = (time.perf_counter() - e0) * 1e3 / e2e_steps
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -185,6 +213,9 @@ def main():
             "parallelism": f"doc-sharded x{world}",
         },
         "device_ms_per_step": round(dev_ms / args.steps, 4),
+        "unique_items_per_step_per_gpu": st.units,
+        "end_to_end": {"ms_per_step": round(e2e_ms, 3), "items_per_s": round(st.items / (e2e_ms * 1e-3), 1),
+                       "includes": "host pack + H2D + merge + D2H of the update and state vector, 1 GPU"},
         "pipeline_roofline": {
             "b_alg_bytes": b_alg,
             "achieved_GBs": round(b_alg / (ms_per_step * 1e-3) / 1e9, 2),

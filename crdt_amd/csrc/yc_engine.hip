@@ -116,7 +116,8 @@ struct ycrdt_engine {
   Work w;
   bool profiling = false;
   bool debug_sync = false;
-  std::vector<std::pair<const char*, hipEvent_t>> marks;
+  std::vector<std::pair<const char*, hipEvent_t>> marks;  // this merge's phase marks
+  std::vector<hipEvent_t> event_pool;                     // reused across merges (no create per mark)
   std::vector<std::pair<const char*, double>> phase_ms;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   std::vector<uint8_t> pinned_stage;
@@ -152,8 +153,12 @@ void mark(ycrdt_engine* e, const char* name) {
     if (er != hipSuccess) fprintf(stderr, "[ycrdt] device error before phase %s: %s\n", name, hipGetErrorString(er));
   }
   if (!e->profiling) return;
-  hipEvent_t ev;
-  hipEventCreate(&ev);
+  if (e->marks.size() == e->event_pool.size()) {
+    hipEvent_t ev;
+    if (hipEventCreate(&ev) != hipSuccess) return;
+    e->event_pool.push_back(ev);
+  }
+  hipEvent_t ev = e->event_pool[e->marks.size()];
   hipEventRecord(ev, e->stream);
   e->marks.push_back({name, ev});
 }
@@ -251,7 +256,6 @@ int run_decode(ycrdt_engine* e, ycrdt_batch* b, bool lazy, Decoded& D) {
   auto& V = e->bufs;
   bool ok = true;
   hipStream_t s = e->stream;
-  for (auto& m : e->marks) hipEventDestroy(m.second);
   e->marks.clear();
   e->phase_ms.clear();
   HIPCHK(hipEventRecord(e->ev0, s));
@@ -706,7 +710,7 @@ void ycrdt_engine_destroy(ycrdt_engine* e) {
   hipSetDevice(e->device);
   hipStreamSynchronize(e->stream);
   for (auto& b : e->bufs) if (b.p) hipFree(b.p);
-  for (auto& m : e->marks) hipEventDestroy(m.second);
+  for (auto& ev : e->event_pool) hipEventDestroy(ev);
   hipEventDestroy(e->ev0);
   hipEventDestroy(e->ev1);
   hipStreamDestroy(e->stream);
