@@ -21,16 +21,89 @@
 
 namespace yc {
 
-// --------------------------------------------------------------------------- 1. chain tables
-// For every byte position p of a group: nxt[p] = length of the struct that would start at p
-// (0 = not a struct, 1 = too long for the staged window), and the chain summaries
-// (first chain position at/after the end of p's chunk / block / group, number of chain positions
-// visited before it) computed by backward dynamic programming (list ranking) in LDS.
+// --------------------------------------------------------------------------- 1a. speculative parse
+// nxt[p] for every byte position p of every group: the length of the struct that would start at
+// p (0 = not a struct, 1 = not sized here: over the work cap, or too long for the 15-bit table
+// positions — the walkers parse those exactly). One 256-lane workgroup per 4 KiB slice, reading
+// the bytes through the caches (no LDS staging), so many workgroups share a CU and hide the
+// latency of the byte-serial parse. Positions are counting-sorted by their would-be info byte
+// (content ref x origin/rightOrigin/parentSub bits) so the lanes of a wavefront take the same
+// path through the branch-heavy parser; a tiny work cap first, the few over it re-parsed densely.
+constexpr uint32_t PSLICE = 4096;               // bytes per parse workgroup
+constexpr uint32_t PL = 256;                    // lanes per parse workgroup
+constexpr uint32_t NB = 72;                     // content refs 1..9 x info>>5
+
+__global__ __launch_bounds__(PL) void k_parse(Work w) {
+  const uint8_t* __restrict__ b = w.bytes;
+  const Group G = w.groups[blockIdx.x / (GROUP_BYTES / PSLICE)];
+  const uint32_t s0 = G.start + (blockIdx.x % (GROUP_BYTES / PSLICE)) * PSLICE;
+  if (s0 >= G.end) return;
+  const uint32_t len = min(G.end - s0, PSLICE), uend = G.uend;
+  uint16_t* __restrict__ out = w.tab.nxt + s0;
+  __shared__ uint32_t bstart[NB + 1], bcursor[NB], qn;
+  __shared__ uint16_t sorted[PSLICE], queue[PSLICE];
+  const uint32_t tid = threadIdx.x;
+  for (uint32_t i = tid; i < NB; i += PL) bcursor[i] = 0;
+  if (tid == 0) qn = 0;
+  __syncthreads();
+  for (uint32_t o = tid; o < len; o += PL) {  // GC / Skip (info + one varuint) resolved on the spot
+    const uint32_t info = b[s0 + o];
+    const uint32_t ref = info & 31u;
+    uint16_t d = 0;
+    if (ref == REF_GC || ref == REF_SKIP) {
+      uint32_t q = s0 + o + 1;
+      bool okv = true;
+      rd_vu(b, q, uend, okv);
+      d = okv ? (uint16_t)(q - s0 - o) : (uint16_t)0;
+    } else if (ref <= REF_DOC) {
+      atomicAdd(&bcursor[(ref - 1) * 8 + (info >> 5)], 1u);
+    }
+    out[o] = d;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    uint32_t acc = 0;
+    for (uint32_t i = 0; i < NB; ++i) { const uint32_t c = bcursor[i]; bstart[i] = acc; bcursor[i] = acc; acc += c; }
+    bstart[NB] = acc;
+  }
+  __syncthreads();
+  for (uint32_t o = tid; o < len; o += PL) {
+    const uint32_t info = b[s0 + o];
+    const uint32_t ref = info & 31u;
+    if (ref >= 1 && ref <= REF_DOC) sorted[atomicAdd(&bcursor[(ref - 1) * 8 + (info >> 5)], 1u)] = (uint16_t)o;
+  }
+  __syncthreads();
+  const uint32_t ncand = bstart[NB];
+  for (uint32_t i = tid; i < ncand; i += PL) {
+    const uint32_t o = sorted[i];
+    uint32_t q = s0 + o;
+    const int r = parse_struct<false, 4>(b, q, uend, SPEC_STEPS_FAST, nullptr);
+    uint16_t d = 0;
+    if (r > 0) d = q - s0 - o < 0x10000u ? (uint16_t)(q - s0 - o) : (uint16_t)1;
+    else if (r == -1) { d = 1; queue[atomicAdd(&qn, 1u)] = (uint16_t)o; }
+    out[o] = d;
+  }
+  __syncthreads();
+  const uint32_t nq = qn;
+  for (uint32_t i = tid; i < nq; i += PL) {
+    const uint32_t o = queue[i];
+    uint32_t q = s0 + o;
+    const int r = parse_struct<false, 4>(b, q, uend, SPEC_MAX_STEPS, nullptr);
+    out[o] = r > 0 ? (q - s0 - o < 0x10000u ? (uint16_t)(q - s0 - o) : (uint16_t)1) : (r == -1 ? (uint16_t)1 : (uint16_t)0);
+  }
+}
+
+// --------------------------------------------------------------------------- 1b. chain tables
+// For every byte position p of a group, from nxt: the chain summaries (first chain position
+// at/after the end of p's chunk / block / group, number of chain positions visited before it)
+// computed by backward dynamic programming (list ranking) in LDS. Table positions are 15 bits
+// (STOPF marks a chain that stops at a struct the tables could not size).
 constexpr uint32_t TL = 512;                    // lanes per table workgroup
-constexpr uint32_t HALO = 4096;                 // bytes staged past the group end
 constexpr uint32_t BLOCK = 1024;                // 16 chunks
 constexpr uint32_t LDS_NXT = 0, LDS_CEXIT = 32768, LDS_CCNT = 65536, LDS_BEXIT = 81920, LDS_BCNT = 114688;
-constexpr uint32_t LDS_TOTAL = 147456;
+constexpr uint32_t LDS_BM = 147456, LDS_TASK = LDS_BM + 2048;  // single-group walk: bitmap words, pieces
+constexpr uint32_t MAXTASK = 2048;
+constexpr uint32_t LDS_TOTAL = LDS_TASK + 4 * MAXTASK;             // 157,696 B of the 160 KiB
 static_assert(GROUP_BYTES == 16384, "table layout assumes 16 KiB groups");
 
 __global__ __launch_bounds__(TL) void k_tables(Work w) {
@@ -43,86 +116,15 @@ __global__ __launch_bounds__(TL) void k_tables(Work w) {
   uint8_t* ccnt = (uint8_t*)(lds + LDS_CCNT);
   uint16_t* bexit = (uint16_t*)(lds + LDS_BEXIT);
   uint16_t* bcnt = (uint16_t*)(lds + LDS_BCNT);
-  uint8_t* sb = lds + LDS_BEXIT;                // staged bytes overlay the block arrays (phase A only)
   uint16_t* gexit = nxt;                        // group level overlays nxt / cexit (phase D)
   uint16_t* gcnt = cexit;
   const Group G = groups[blockIdx.x];
   const uint32_t tid = threadIdx.x;
   if (w.dbg && tid == 0) w.dbg[blockIdx.x * 8 + 0] = clock64();
   const uint32_t glen = G.end - G.start;
-  const uint32_t lim = min(G.uend, G.start + GROUP_BYTES + HALO);
-  const uint32_t slen = lim - G.start;
-  const bool window_cut = lim < G.uend;
-  // stage (16-byte vector loads; the batch buffer is padded)
-  for (uint32_t i = tid * 16; i < slen; i += TL * 16) *(uint4*)(sb + i) = *(const uint4*)(b + G.start + i);
+  for (uint32_t o = tid; o < glen; o += TL) nxt[o] = t.nxt[G.start + o];
   __syncthreads();
-  if (w.dbg && tid == 0) w.dbg[blockIdx.x * 8 + 1] = clock64();
-  // phase A: speculative parse at every byte position.
-  //  A0: classify each position by its would-be info byte: non-structs (content ref > 10) and
-  //      GC / Skip (info + one varuint) are resolved on the spot;
-  //  A1: counting-sort the other candidates by (content ref, origin/rightOrigin/parentSub bits) so
-  //      the lanes of a wavefront take the same path through the (branch-heavy) parser;
-  //  A2: parse in sorted order under a tiny work cap, queueing the few that need more;
-  //  A3: re-parse the queued positions densely.
-  constexpr uint32_t NB = 72;  // content refs 1..9 x info>>5
-  __shared__ uint32_t bstart[NB + 1], bcursor[NB];
-  __shared__ uint32_t qn;
-  uint16_t* sorted = (uint16_t*)(lds + LDS_CEXIT);  // cexit/ccnt are unused until phase B
-  uint16_t* queue = (uint16_t*)(lds + LDS_BCNT);    // staged bytes end below LDS_BCNT
-  static_assert(LDS_BEXIT + GROUP_BYTES + HALO <= LDS_BCNT, "staged window overlaps the queue");
-  for (uint32_t i = tid; i < NB; i += TL) bcursor[i] = 0;
-  if (tid == 0) qn = 0;
-  __syncthreads();
-  for (uint32_t o = tid; o < glen; o += TL) {
-    const uint32_t info = sb[o];
-    const uint32_t ref = info & 31u;
-    uint16_t d = 0;
-    if (ref == REF_GC || ref == REF_SKIP) {
-      uint32_t q = o + 1;
-      bool okv = true;
-      rd_vu(sb, q, slen, okv);
-      d = okv ? (uint16_t)(q - o) : (window_cut && q >= slen ? (uint16_t)1 : (uint16_t)0);
-    } else if (ref <= REF_DOC) {
-      atomicAdd(&bcursor[(ref - 1) * 8 + (info >> 5)], 1u);
-    }
-    nxt[o] = d;
-  }
-  __syncthreads();
-  if (tid == 0) {
-    uint32_t acc = 0;
-    for (uint32_t i = 0; i < NB; ++i) { const uint32_t c = bcursor[i]; bstart[i] = acc; bcursor[i] = acc; acc += c; }
-    bstart[NB] = acc;
-  }
-  __syncthreads();
-  for (uint32_t o = tid; o < glen; o += TL) {
-    const uint32_t info = sb[o];
-    const uint32_t ref = info & 31u;
-    if (ref >= 1 && ref <= REF_DOC) sorted[atomicAdd(&bcursor[(ref - 1) * 8 + (info >> 5)], 1u)] = (uint16_t)o;
-  }
-  __syncthreads();
-  const uint32_t ncand = bstart[NB];
-  if (w.dbg && tid == 0) w.dbg[blockIdx.x * 8 + 2] = clock64();
-  for (uint32_t i = tid; i < ncand; i += TL) {
-    const uint32_t o = sorted[i];
-    uint32_t q = o;
-    const int r = parse_struct<false, 4>(sb, q, slen, SPEC_STEPS_FAST, nullptr);
-    uint16_t d;
-    if (r > 0) d = (uint16_t)(q - o);
-    else if (r == -1) { d = 1; queue[atomicAdd(&qn, 1u)] = (uint16_t)o; }
-    else if (r == -2 && window_cut) d = 1;  // may continue past the staged window: exact parse later
-    else d = 0;
-    nxt[o] = d;
-  }
-  __syncthreads();
-  const uint32_t nq = qn;
-  if (w.dbg && tid == 0) w.dbg[blockIdx.x * 8 + 3] = clock64();
-  for (uint32_t i = tid; i < nq; i += TL) {
-    const uint32_t o = queue[i];
-    uint32_t q = o;
-    const int r = parse_struct<false, 4>(sb, q, slen, SPEC_MAX_STEPS, nullptr);
-    nxt[o] = r > 0 ? (uint16_t)(q - o) : ((r == -1 || (r == -2 && window_cut)) ? (uint16_t)1 : (uint16_t)0);
-  }
-  __syncthreads();
+  if (w.dbg && tid == 0) { w.dbg[blockIdx.x * 8 + 1] = w.dbg[blockIdx.x * 8 + 2] = w.dbg[blockIdx.x * 8 + 3] = clock64(); }
   // phase B: chunk level by pointer doubling over all positions (6 rounds cover a 64-byte chunk),
   // double-buffered through the block-array region (free again once the bytes are parsed); reads
   // are mostly unit-stride across a wavefront, unlike a lane-per-chunk backward sweep.
@@ -133,7 +135,7 @@ __global__ __launch_bounds__(TL) void k_tables(Work w) {
     uint8_t* c1 = (uint8_t*)bcnt;
     for (uint32_t o = tid; o < glen; o += TL) {
       const uint32_t d = nxt[o];
-      if (d == 1) { e0[o] = (uint16_t)(o | STOPF); c0[o] = 0; }
+      if (d == 1 || o + d >= STOPF) { e0[o] = (uint16_t)(o | STOPF); c0[o] = 0; }  // sized by an exact parse
       else { e0[o] = (uint16_t)(d == 0 ? o + 1 : o + d); c0[o] = 1; }
     }
     __syncthreads();
@@ -153,15 +155,28 @@ __global__ __launch_bounds__(TL) void k_tables(Work w) {
     }
     static_assert(6 % 2 == 0, "an even number of rounds leaves the result in cexit/ccnt");
   }
+  // phase C: block level (chunk s of every block, s = 15..0), from the chunk level
+  for (int s = 15; s >= 0; --s) {
+    for (uint32_t i = tid; i < 16 * CHUNK; i += TL) {
+      const uint32_t blk = i / CHUNK;
+      const uint32_t o = blk * BLOCK + (uint32_t)s * CHUNK + (i % CHUNK);
+      if (o >= glen) continue;
+      const uint32_t bend = min((blk + 1) * BLOCK, glen);
+      const uint32_t x = cexit[o];
+      if ((x & STOPF) || x >= bend) { bexit[o] = (uint16_t)x; bcnt[o] = ccnt[o]; }
+      else { bexit[o] = bexit[x]; bcnt[o] = (uint16_t)(ccnt[o] + bcnt[x]); }
+    }
+    __syncthreads();
+  }
   if (w.dbg && tid == 0) w.dbg[blockIdx.x * 8 + 4] = clock64();
   // ---- an update that fits in one group is walked right here (its tables never leave LDS): lane 0
-  // follows the true chain through the section headers by chunk exits, queueing (position, count)
-  // chain pieces, then every lane marks its pieces' struct starts into an LDS copy of the final
-  // bitmap (the update owns its 64-byte-aligned words exclusively) — k_walker / k_mark skip it.
+  // follows the true chain through the section headers by block exits (1 KiB per step), then chunk
+  // exits, queueing (position, count) chain pieces; then one lane per piece marks its struct starts
+  // into an LDS copy of the final bitmap (the update owns its 64-byte-aligned words exclusively) —
+  // k_walker / k_mark skip it.
   if (G.start == w.uoff[G.upd] && G.end == G.uend) {
-    uint64_t* bm = (uint64_t*)(lds + LDS_BEXIT);           // 256 words (bexit/bcnt are free again)
-    uint32_t* task = (uint32_t*)(lds + LDS_BEXIT + 2048);  // (position << 8 | count)
-    constexpr uint32_t MAXTASK = (LDS_TOTAL - LDS_BEXIT - 2048) / 4;
+    uint64_t* bm = (uint64_t*)(lds + LDS_BM);   // 256 words
+    uint32_t* task = (uint32_t*)(lds + LDS_TASK);  // (position << 11 | count), count <= 1024
     __shared__ uint32_t ntask;
     const uint32_t nwords_g = (glen + 63) / 64;
     for (uint32_t i = tid; i < nwords_g; i += TL) bm[i] = 0;
@@ -174,6 +189,15 @@ __global__ __launch_bounds__(TL) void k_tables(Work w) {
       bool ok = true;
       uint32_t p = G.start;
       uint32_t nt = 0;
+      // a chain piece: queued while there is room, else marked right here (many tiny sections)
+      auto piece = [&](uint32_t o, uint32_t cnt) {
+        if (nt < MAXTASK) { task[nt++] = (o << 11) | cnt; return; }
+        for (uint32_t k = 0; k < cnt; ++k) {
+          bm[o >> 6] |= 1ull << (o & 63);
+          const uint32_t d = nxt[o];
+          o += d == 0 ? 1 : d;
+        }
+      };
       const uint32_t nsec = rd_vu(b, p, uend, ok);
       if (!ok || nsec > (uend - p) / 3 + 1) { raise_err(err, ERR_DECODE); goto done; }
       {
@@ -195,11 +219,19 @@ __global__ __launch_bounds__(TL) void k_tables(Work w) {
           uint32_t o = p - G.start;
           while (r > 0) {
             if (o >= glen) { raise_err(err, ERR_DECODE); goto done; }
-            for (;;) {  // whole chunk pieces of the chain
+            for (;;) {  // whole block pieces of the chain
+              const uint32_t be = bexit[o], bc = bcnt[o];
+              if ((be & STOPF) || bc >= r || bc == 0) break;
+              piece(o, bc);
+              r -= bc;
+              o = be;
+              if (o >= glen) break;
+            }
+            if (r == 0 || o >= glen) continue;
+            for (;;) {  // whole chunk pieces
               const uint32_t ce = cexit[o], cc = ccnt[o];
               if ((ce & STOPF) || cc >= r || cc == 0) break;
-              if (nt >= MAXTASK) { raise_err(err, ERR_CAPACITY); goto done; }
-              task[nt++] = (o << 8) | cc;
+              piece(o, cc);
               r -= cc;
               o = ce;
               if (o >= glen) break;
@@ -213,7 +245,7 @@ __global__ __launch_bounds__(TL) void k_tables(Work w) {
               if (parse_struct<false>(b, q, uend, 0xFFFFFFFFu, nullptr) <= 0) { raise_err(err, ERR_DECODE); w.ctr->err_info = G.start + o; goto done; }
             } else if (d == 0) { raise_err(err, ERR_DECODE); goto done; }
             else q += d;
-            atomicOr((unsigned long long*)&bm[o >> 6], 1ull << (o & 63));
+            bm[o >> 6] |= 1ull << (o & 63);
             o = q - G.start;
             --r;
           }
@@ -227,10 +259,11 @@ __global__ __launch_bounds__(TL) void k_tables(Work w) {
     __syncthreads();
     const uint32_t nt = ntask;
     for (uint32_t i = tid; i < nt; i += TL) {
-      uint32_t x = task[i] >> 8, left = task[i] & 0xFFu;
-      const uint32_t word = x >> 6;
+      uint32_t x = task[i] >> 11, left = task[i] & 0x7FFu;
+      uint32_t word = x >> 6;
       uint64_t m = 0;
       while (left > 0) {
+        if ((x >> 6) != word) { atomicOr((unsigned long long*)&bm[word], (unsigned long long)m); word = x >> 6; m = 0; }
         m |= 1ull << (x & 63);
         const uint32_t d = nxt[x];
         x += d == 0 ? 1 : d;
@@ -240,28 +273,14 @@ __global__ __launch_bounds__(TL) void k_tables(Work w) {
     }
     __syncthreads();
     for (uint32_t i = tid; i < nwords_g; i += TL) w.final_bits[(G.start >> 6) + i] = bm[i];
-  if (w.dbg && tid == 0) w.dbg[blockIdx.x * 8 + 5] = clock64();
+    if (w.dbg && tid == 0) w.dbg[blockIdx.x * 8 + 5] = clock64();
     return;
   }
   // exits are stored as forward deltas from the position itself (|STOPF when the chain stops at a
   // struct the tables could not size), so consumers never need the group origin
   for (uint32_t o = tid; o < glen; o += TL) {
-    t.nxt[G.start + o] = nxt[o];
     t.cexit[G.start + o] = (uint16_t)(((cexit[o] & 0x7FFFu) - o) | (cexit[o] & STOPF));
     t.ccnt[G.start + o] = ccnt[o];
-  }
-  // phase C: block level (chunk s of every block, s = 15..0)
-  for (int s = 15; s >= 0; --s) {
-    for (uint32_t i = tid; i < 16 * CHUNK; i += TL) {
-      const uint32_t blk = i / CHUNK;
-      const uint32_t o = blk * BLOCK + (uint32_t)s * CHUNK + (i % CHUNK);
-      if (o >= glen) continue;
-      const uint32_t bend = min((blk + 1) * BLOCK, glen);
-      const uint32_t x = cexit[o];
-      if ((x & STOPF) || x >= bend) { bexit[o] = (uint16_t)x; bcnt[o] = ccnt[o]; }
-      else { bexit[o] = bexit[x]; bcnt[o] = (uint16_t)(ccnt[o] + bcnt[x]); }
-    }
-    __syncthreads();
   }
   for (uint32_t o = tid; o < glen; o += TL) {
     t.bexit[G.start + o] = (uint16_t)(((bexit[o] & 0x7FFFu) - o) | (bexit[o] & STOPF));
@@ -286,6 +305,7 @@ __global__ __launch_bounds__(TL) void k_tables(Work w) {
 
 void launch_group_parse(const Work& w, hipStream_t s) {
   if (w.ngroups == 0) return;
+  hipLaunchKernelGGL(k_parse, dim3(w.ngroups * (GROUP_BYTES / PSLICE)), dim3(PL), 0, s, w);
   hipLaunchKernelGGL(k_tables, dim3(w.ngroups), dim3(TL), 0, s, w);
 }
 
