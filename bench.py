@@ -114,27 +114,27 @@ def main():
     value = items_step * args.steps / dt
     phases = [(n, m / args.steps) for n, m in phase_acc.items()]
 
-    # ---- roofline of the dominant kernel. k_tables (K1 chain tables) is the largest single-kernel
-    # phase; its algorithmic traffic is the input bytes it parses, read once (SURVEY.md §8(d):
-    # B_in), and its duration is the HIP-event time of the "decode.tables" phase, which holds that
-    # one launch. `traffic` is the HBM bytes per launch from the committed rocprofv3 PMC pass
+    # ---- roofline of the dominant kernel. k_parse (K1 speculative parse at every input byte) is the
+    # largest single-kernel phase; its algorithmic traffic is the input bytes it parses, read once
+    # (B_in), and its duration is the HIP-event time of the "decode.parse" phase,
+    # which holds that one launch. `traffic` is the HBM bytes per launch from the committed rocprofv3 PMC pass
     # (2 x FETCH_SIZE + WRITE_SIZE, gfx950 correction; scripts/pmc.sh + scripts/pmc_summary.py).
     ph = dict(phases)
-    k_ms = ph.get("decode.tables", 0.0)
+    k_ms = ph.get("decode.parse", 0.0)
     alg = in_bytes
     traffic, traffic_src = None, None
     pmc = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_c2_pmc.csv")))
     if pmc:
         with open(pmc[-1]) as f:
             for r in csv.DictReader(f):
-                if r["kernel"] == "yc::k_tables":
+                if r["kernel"] == "yc::k_parse":
                     traffic = int(float(r["hbm_bytes"]))
                     traffic_src = os.path.basename(pmc[-1])
     achieved = alg / (k_ms * 1e-3) / 1e9 if k_ms > 0 else 0.0
     dominant = max(phases, key=lambda p: p[1]) if phases else ("merge", st.device_ms)
     roofline = {
         "bound": "hbm",
-        "kernel": "yc::k_tables",
+        "kernel": "yc::k_parse",
         "achieved": round(achieved, 2),
         "peak": HBM_PEAK_GBS,
         "unit": "GB/s",

@@ -304,9 +304,10 @@ __global__ __launch_bounds__(TL) void k_tables(Work w) {
 }
 
 void launch_group_parse(const Work& w, hipStream_t s) {
-  if (w.ngroups == 0) return;
-  hipLaunchKernelGGL(k_parse, dim3(w.ngroups * (GROUP_BYTES / PSLICE)), dim3(PL), 0, s, w);
-  hipLaunchKernelGGL(k_tables, dim3(w.ngroups), dim3(TL), 0, s, w);
+  if (w.ngroups) hipLaunchKernelGGL(k_parse, dim3(w.ngroups * (GROUP_BYTES / PSLICE)), dim3(PL), 0, s, w);
+}
+void launch_group_tables(const Work& w, hipStream_t s) {
+  if (w.ngroups) hipLaunchKernelGGL(k_tables, dim3(w.ngroups), dim3(TL), 0, s, w);
 }
 
 // --------------------------------------------------------------------------- 2. walker

@@ -347,11 +347,13 @@ int run_decode(ycrdt_engine* e, ycrdt_batch* b, bool lazy, Decoded& D) {
   HIPCHK(hipMemsetAsync(w.final_bits, 0, nwords * 8, s));
   HIPCHK(hipMemsetAsync(w.sec_bits, 0, nwords * 8, s));
   // ---- K1 decode
-  mark(e, "decode.tables");
+  mark(e, "decode.parse");
   static const bool dbg_tables = getenv("YCRDT_DEBUG_TABLES") && getenv("YCRDT_DEBUG_TABLES")[0] == '1';
   w.dbg = dbg_tables ? take<unsigned long long>(V, B_DBG, (size_t)w.ngroups * 8 + 8, ok) : nullptr;
   if (w.dbg) HIPCHK(hipMemsetAsync(w.dbg, 0, sizeof(unsigned long long) * ((size_t)w.ngroups * 8 + 8), s));
   launch_group_parse(w, s);
+  mark(e, "decode.tables");
+  launch_group_tables(w, s);
   if (w.dbg) {
     HIPCHK(hipStreamSynchronize(s));
     std::vector<unsigned long long> h((size_t)w.ngroups * 8);

@@ -304,7 +304,8 @@ enum : uint32_t {
 };
 
 // ---- launch entry points (yc_decode.hip / yc_merge.hip / yc_encode.hip / yc_prims.hip)
-void launch_group_parse(const Work& w, hipStream_t s);
+void launch_group_parse(const Work& w, hipStream_t s);   // k_parse: nxt at every byte
+void launch_group_tables(const Work& w, hipStream_t s);  // k_tables: chain exits (+ single-group walk)
 void launch_walker(const Work& w, hipStream_t s);
 void launch_build_final_bits(const Work& w, hipStream_t s);
 void launch_struct_positions(const Work& w, hipStream_t s);
