@@ -27,11 +27,128 @@ namespace yc {
 // positions — the walkers parse those exactly). One 256-lane workgroup per 4 KiB slice, reading
 // the bytes through the caches (no LDS staging), so many workgroups share a CU and hide the
 // latency of the byte-serial parse. Positions are counting-sorted by their would-be info byte
-// (content ref x origin/rightOrigin/parentSub bits) so the lanes of a wavefront take the same
-// path through the branch-heavy parser; a tiny work cap first, the few over it re-parsed densely.
+// (content ref x origin/rightOrigin/parentSub bits) and sized by spec_len one class per wavefront;
+// what the sizer hands over is re-parsed by parse_struct under a work cap.
 constexpr uint32_t PSLICE = 4096;               // bytes per parse workgroup
 constexpr uint32_t PL = 256;                    // lanes per parse workgroup
 constexpr uint32_t NB = 72;                     // content refs 1..9 x info>>5
+
+// ---- the speculative struct sizer (k_parse). Exact on every valid struct; on other bytes it only
+// has to be deterministic: the walkers follow nxt from true struct starts only, and every struct
+// on the true chain is re-parsed exactly by k_struct_decode, which reports a malformed one.
+// The info byte's class (content ref, origin / right origin / parentSub bits) is wave-uniform
+// (positions are tiled per class), so the field layout costs scalar branches, and varuints are
+// read branch-free from an 8-byte register window.
+__device__ __forceinline__ uint64_t win8(const uint8_t* __restrict__ b, uint32_t p) {
+  const uint32_t* d = (const uint32_t*)(b + (p & ~3u));  // the batch buffer is padded past its end
+  return ((uint64_t)d[0] | ((uint64_t)d[1] << 32)) >> ((p & 3u) * 8);
+}
+__device__ __forceinline__ uint32_t vu_fast(const uint8_t* __restrict__ b, uint32_t& p, uint32_t end, bool& ok) {
+  const uint64_t w = win8(b, p);
+  const uint64_t t = ~w & 0x8080808080ull;  // terminal bytes among the first five
+  const uint32_t len = t ? ((uint32_t)__builtin_ctzll(t) >> 3) + 1 : 6u;
+  uint64_t v = (w & 0x7full) | ((w >> 1) & (0x7full << 7)) | ((w >> 2) & (0x7full << 14)) | ((w >> 3) & (0x7full << 21)) |
+               ((w >> 4) & (0x7full << 28));
+  v &= len >= 5 ? ~0ull : ((1ull << (7 * len)) - 1);
+  ok = ok && len <= 5 && end - p >= len && p < end;
+  p += len;
+  return (uint32_t)v;  // lib0 0.2.42 accumulates in 32 bits
+}
+__device__ __forceinline__ void skip_n(uint32_t& p, uint32_t n, uint32_t end, bool& ok) {
+  const bool f = p <= end && n <= end - p;
+  ok = ok && f;
+  p = f ? p + n : end;
+}
+// one `any` value (L0@1937) that is not a container; false: a container, or more than this sizer does
+__device__ __forceinline__ bool any_simple(const uint8_t* __restrict__ b, uint32_t& p, uint32_t end, bool& ok) {
+  if (p >= end) { ok = false; return true; }
+  const uint32_t tag = b[p++];
+  switch (tag) {
+    case 127: case 126: case 121: case 120: return true;
+    case 125: {  // varInt
+      const uint64_t t = ~win8(b, p) & 0x8080808080ull;
+      const uint32_t len = t ? ((uint32_t)__builtin_ctzll(t) >> 3) + 1
+                             : (p + 5 < end && b[p + 5] < 0x80u ? 6u : (p + 6 < end && b[p + 6] < 0x80u ? 7u : 8u));
+      ok = ok && len <= 7 && end - p >= len;  // skip_vi: a first byte and up to six more
+      p += len;
+      return true;
+    }
+    case 124: skip_n(p, 4, end, ok); return true;
+    case 123: case 122: skip_n(p, 8, end, ok); return true;
+    case 119: case 116: { const uint32_t n = vu_fast(b, p, end, ok); skip_n(p, n, end, ok); return true; }
+    case 118: case 117: return false;
+    default: ok = false; return true;
+  }
+}
+constexpr uint32_t SIZER_MAX_ELEMS = 16;
+// struct length, 0 = not a struct, 1 = hand over to parse_struct (many elements, deep nesting, Doc)
+__device__ __forceinline__ uint32_t spec_len(const uint8_t* __restrict__ b, uint32_t pos, uint32_t end, uint32_t cls) {
+  const uint32_t ref = cls / 8 + 1, bits = (cls % 8) << 5;
+  bool ok = true;
+  uint32_t p = pos + 1;
+  if (bits & 0x80u) { vu_fast(b, p, end, ok); vu_fast(b, p, end, ok); }
+  if (bits & 0x40u) { vu_fast(b, p, end, ok); vu_fast(b, p, end, ok); }
+  if (!(bits & 0xC0u)) {
+    const uint32_t pinfo = vu_fast(b, p, end, ok);
+    if (pinfo == 1) { const uint32_t n = vu_fast(b, p, end, ok); skip_n(p, n, end, ok); }
+    else { vu_fast(b, p, end, ok); vu_fast(b, p, end, ok); }
+    if (bits & 0x20u) { const uint32_t n = vu_fast(b, p, end, ok); skip_n(p, n, end, ok); }
+  }
+  switch (ref) {
+    case REF_DELETED: vu_fast(b, p, end, ok); break;
+    case REF_BINARY: case REF_STRING: { const uint32_t n = vu_fast(b, p, end, ok); skip_n(p, n, end, ok); break; }
+    case REF_EMBED: {
+      const uint32_t n = vu_fast(b, p, end, ok);
+      ok = ok && n > 0 && p < end && json_start_ok(b[p]);
+      skip_n(p, n, end, ok);
+      break;
+    }
+    case REF_FORMAT: {
+      uint32_t n = vu_fast(b, p, end, ok);
+      skip_n(p, n, end, ok);
+      n = vu_fast(b, p, end, ok);
+      ok = ok && n > 0 && p < end && json_start_ok(b[p]);
+      skip_n(p, n, end, ok);
+      break;
+    }
+    case REF_TYPE: {
+      const uint32_t tr = vu_fast(b, p, end, ok);
+      if (tr == 3 || tr == 5) { const uint32_t n = vu_fast(b, p, end, ok); skip_n(p, n, end, ok); }
+      ok = ok && tr <= 6;
+      break;
+    }
+    case REF_JSON: {
+      const uint32_t n = vu_fast(b, p, end, ok);
+      if (ok && n > SIZER_MAX_ELEMS) return 1;
+      for (uint32_t i = 0; i < n && ok; ++i) {
+        const uint32_t k = vu_fast(b, p, end, ok);
+        ok = ok && k > 0 && p < end && json_start_ok(b[p]);
+        skip_n(p, k, end, ok);
+      }
+      break;
+    }
+    case REF_ANY: {
+      const uint32_t n = vu_fast(b, p, end, ok);
+      if (ok && n > SIZER_MAX_ELEMS) return 1;
+      for (uint32_t i = 0; i < n && ok; ++i) {
+        const uint32_t q0 = p;
+        if (any_simple(b, p, end, ok)) continue;
+        // a container one level deep with simple members; anything deeper goes to parse_struct
+        const bool obj = b[q0] == 118;
+        const uint32_t m = vu_fast(b, p, end, ok);
+        if (ok && m > SIZER_MAX_ELEMS) return 1;
+        for (uint32_t j = 0; j < m && ok; ++j) {
+          if (obj) { const uint32_t k = vu_fast(b, p, end, ok); skip_n(p, k, end, ok); }
+          if (!any_simple(b, p, end, ok)) return ok ? 1u : 0u;
+        }
+      }
+      break;
+    }
+    default: return 1;  // ContentDoc
+  }
+  if (!ok) return 0;
+  return p - pos < 0x10000u ? p - pos : 1u;
+}
 
 __global__ __launch_bounds__(PL) void k_parse(Work w) {
   const uint8_t* __restrict__ b = w.bytes;
@@ -40,9 +157,9 @@ __global__ __launch_bounds__(PL) void k_parse(Work w) {
   if (s0 >= G.end) return;
   const uint32_t len = min(G.end - s0, PSLICE), uend = G.uend;
   uint16_t* __restrict__ out = w.tab.nxt + s0;
-  __shared__ uint32_t bstart[NB + 1], bcursor[NB], qn;
+  __shared__ uint32_t bstart[NB + 1], bcursor[NB], tstart[NB + 1], qn;
   __shared__ uint16_t sorted[PSLICE], queue[PSLICE];
-  const uint32_t tid = threadIdx.x;
+  const uint32_t tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   for (uint32_t i = tid; i < NB; i += PL) bcursor[i] = 0;
   if (tid == 0) qn = 0;
   __syncthreads();
@@ -61,10 +178,14 @@ __global__ __launch_bounds__(PL) void k_parse(Work w) {
     out[o] = d;
   }
   __syncthreads();
-  if (tid == 0) {
-    uint32_t acc = 0;
-    for (uint32_t i = 0; i < NB; ++i) { const uint32_t c = bcursor[i]; bstart[i] = acc; bcursor[i] = acc; acc += c; }
-    bstart[NB] = acc;
+  if (tid == 0) {  // class starts, and 64-position tiles per class
+    uint32_t acc = 0, tiles = 0;
+    for (uint32_t i = 0; i < NB; ++i) {
+      const uint32_t c = bcursor[i];
+      bstart[i] = acc; bcursor[i] = acc; tstart[i] = tiles;
+      acc += c; tiles += (c + 63) / 64;
+    }
+    bstart[NB] = acc; tstart[NB] = tiles;
   }
   __syncthreads();
   for (uint32_t o = tid; o < len; o += PL) {
@@ -73,18 +194,22 @@ __global__ __launch_bounds__(PL) void k_parse(Work w) {
     if (ref >= 1 && ref <= REF_DOC) sorted[atomicAdd(&bcursor[(ref - 1) * 8 + (info >> 5)], 1u)] = (uint16_t)o;
   }
   __syncthreads();
-  const uint32_t ncand = bstart[NB];
-  for (uint32_t i = tid; i < ncand; i += PL) {
-    const uint32_t o = sorted[i];
-    uint32_t q = s0 + o;
-    const int r = parse_struct<false, 4>(b, q, uend, SPEC_STEPS_FAST, nullptr);
-    uint16_t d = 0;
-    if (r > 0) d = q - s0 - o < 0x10000u ? (uint16_t)(q - s0 - o) : (uint16_t)1;
-    else if (r == -1) { d = 1; queue[atomicAdd(&qn, 1u)] = (uint16_t)o; }
-    out[o] = d;
+  // every wavefront sizes tiles of ONE class: the class is a scalar for the whole parse
+  const uint32_t ntiles = tstart[NB];
+  for (uint32_t t = wave; t < ntiles; t += PL / 64) {
+    uint32_t lo = 0, hi = NB;  // last class c with tstart[c] <= t
+    while (hi - lo > 1) { const uint32_t m = (lo + hi) >> 1; if (tstart[m] <= t) lo = m; else hi = m; }
+    const uint32_t c = __builtin_amdgcn_readfirstlane(lo);
+    const uint32_t i = bstart[c] + (t - tstart[c]) * 64 + lane;
+    if (i < bstart[c + 1]) {
+      const uint32_t o = sorted[i];
+      const uint32_t d = spec_len(b, s0 + o, uend, c);
+      if (d == 1) queue[atomicAdd(&qn, 1u)] = (uint16_t)o;
+      out[o] = (uint16_t)d;
+    }
   }
   __syncthreads();
-  const uint32_t nq = qn;
+  const uint32_t nq = qn;  // the general parser under a work cap for what the sizer handed over
   for (uint32_t i = tid; i < nq; i += PL) {
     const uint32_t o = queue[i];
     uint32_t q = s0 + o;
