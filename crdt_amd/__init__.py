@@ -79,6 +79,8 @@ EXPORTS = (
     "ycrdt_encode_state_as_update", "ycrdt_encode_state_vector", "ycrdt_doc_last_stats",
     "ycrdt_batch_stage", "ycrdt_batch_merge", "ycrdt_batch_result", "ycrdt_batch_destroy",
     "ycrdt_merge_updates", "ycrdt_diff_update", "ycrdt_free", "ycrdt_last_error", "ycrdt_version",
+    "ycrdt_doc_json", "ycrdt_map_set", "ycrdt_map_set_type", "ycrdt_map_delete", "ycrdt_array_insert",
+    "ycrdt_array_delete", "ycrdt_doc_client_id",
 )
 
 
@@ -111,6 +113,14 @@ def lib():
     L.ycrdt_merge_updates.argtypes = [vp, P(_Buf), sz, P(_Out)]
     L.ycrdt_diff_update.argtypes = [vp, _Buf, _Buf, P(_Out)]
     L.ycrdt_free.argtypes = [P(_Out)]
+    cs = ctypes.c_char_p
+    L.ycrdt_doc_json.argtypes = [vp, cs, i32, P(_Out)]
+    L.ycrdt_map_set.argtypes = [vp, cs, cs, cs, ctypes.c_char_p, sz]
+    L.ycrdt_map_set_type.argtypes = [vp, cs, cs, cs, u32]
+    L.ycrdt_map_delete.argtypes = [vp, cs, cs, cs]
+    L.ycrdt_array_insert.argtypes = [vp, cs, cs, u32, ctypes.c_char_p, sz, u32]
+    L.ycrdt_array_delete.argtypes = [vp, cs, cs, u32, u32]
+    L.ycrdt_doc_client_id.argtypes = [vp, P(u32)]
     L.ycrdt_last_error.restype = ctypes.c_char_p
     L.ycrdt_version.restype = ctypes.c_char_p
     _LIB = L
@@ -129,6 +139,10 @@ def _bufs(updates):
         arr[i].ptr = ctypes.cast(ctypes.c_char_p(u), ctypes.c_void_p)
         arr[i].len = len(u)
     return arr, keep
+
+
+def _opt(s):
+    return None if s is None else s.encode()
 
 
 def _take(out):
@@ -218,6 +232,32 @@ class Doc:
         st = MergeStats()
         _check(lib().ycrdt_doc_last_stats(self._h, ctypes.byref(st)))
         return st
+
+    # ---- crdt.c materialisation + local ops (same signatures as oracle/yref.py's Doc) ----------
+    # `parent_key` addresses the shared type stored in root map `root` under that key.
+    def root_json(self, name: str, kind: str) -> str:
+        """YMap.toJSON / YArray.toJSON of root `name` (kind "map" | "array") as JSON text."""
+        out = _Out()
+        _check(lib().ycrdt_doc_json(self._h, name.encode(), 0 if kind == "map" else 1, ctypes.byref(out)))
+        return _take(out).decode()
+
+    def map_set(self, root: str, key: str, any_bytes: bytes, parent_key: str = None):
+        a = bytes(any_bytes)
+        _check(lib().ycrdt_map_set(self._h, root.encode(), _opt(parent_key), key.encode(), a, len(a)))
+
+    def map_set_type(self, root: str, key: str, type_ref: int = 0, parent_key: str = None):
+        """YMap.set(key, new Y.Array()) (type_ref 0) / new Y.Map() (1)."""
+        _check(lib().ycrdt_map_set_type(self._h, root.encode(), _opt(parent_key), key.encode(), type_ref))
+
+    def map_delete(self, root: str, key: str, parent_key: str = None):
+        _check(lib().ycrdt_map_delete(self._h, root.encode(), _opt(parent_key), key.encode()))
+
+    def array_insert(self, root: str, index: int, anys: list, parent_key: str = None):
+        a = b"".join(bytes(x) for x in anys)
+        _check(lib().ycrdt_array_insert(self._h, root.encode(), _opt(parent_key), index, a, len(a), len(anys)))
+
+    def array_delete(self, root: str, index: int, length: int, parent_key: str = None):
+        _check(lib().ycrdt_array_delete(self._h, root.encode(), _opt(parent_key), index, length))
 
 
 class Batch:

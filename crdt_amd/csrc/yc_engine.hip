@@ -12,6 +12,7 @@
 #include <algorithm>
 
 #include "yc_work.h"
+#include "yc_host.h"
 #include "../../include/ycrdt.h"
 
 using namespace yc;
@@ -103,6 +104,7 @@ enum Buf {
   B_DWFLAG, B_DWGID, B_DWGSTART, B_DWSIZE, B_DWPOS,
   B_GRIGHT, B_YKEY, B_YKEYS, B_YSEG, B_YIOTA, B_YLSTART, B_YSTATE, B_YBEFORE, B_YCONFL, B_YSTACK,
   B_OFIRST, B_OCIDX, B_OSIZE, B_OPOS, B_RSEG, B_RLEN, B_RSIZE, B_RPOS, B_OUT, B_SVOUT,
+  B_VKMAP, B_VKREP, B_VKEYS, B_VNKEYS, B_VPOS, B_VD0, B_VN0, B_VD1, B_VN1, B_VORDER, B_VSEGS,
   B_COUNT
 };
 
@@ -123,6 +125,7 @@ struct ycrdt_engine {
   std::vector<uint8_t> pinned_stage;
   // result of the last merge
   uint32_t out_bytes = 0, sv_bytes = 0;
+  uint32_t nsegs = 0, nlists = 0;  // segments / YArray lists of the last merge (the view reads them)
   ycrdt_merge_stats last{};
 };
 
@@ -133,6 +136,7 @@ struct ycrdt_doc {
   size_t state_len = 0;  // 0 = empty doc
   std::vector<uint8_t> sv;
   ycrdt_merge_stats last{};
+  HostView view;         // materialised view of `state` (crdt.c), rebuilt lazily after a change
 };
 
 struct ycrdt_batch {
@@ -493,6 +497,8 @@ int run_merge(ycrdt_engine* e, ycrdt_batch* b, const std::unordered_map<uint32_t
   w.k_flags = take<uint32_t>(V, B_KFLAG, w.cap_keys, ok);
   if (!ok) return fail(YCRDT_E_DEVICE, "hipMalloc failed (key table)");
   uint32_t nout = 0;
+  e->nsegs = nsegs;
+  e->nlists = 0;
   if (nsegs) {
     mark(e, "merge.segment_props");
     launch_segment_props(w, nsegs, nclients, U, s);
@@ -509,7 +515,7 @@ int run_merge(ycrdt_engine* e, ycrdt_batch* b, const std::unordered_map<uint32_t
       HIPCHK(hipMemcpyAsync(&narray, &w.ctr->narray, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
       HIPCHK(hipStreamSynchronize(s));
     }
-    launch_yata(w, nsegs, narray, s);
+    e->nlists = launch_yata(w, nsegs, narray, s);
     mark(e, "merge.merge_flags");
     launch_merge_flags(w, nsegs, s);
   }
@@ -552,6 +558,54 @@ int run_merge(ycrdt_engine* e, ycrdt_batch* b, const std::unordered_map<uint32_t
       e->phase_ms.push_back({e->marks[i].first, (double)t});
     }
   }
+  return YCRDT_OK;
+}
+
+// K8: materialised view of the doc state just merged into the engine's workspace (yc_view.hip),
+// copied to the host with the state bytes its byte ranges point into.
+int run_view(ycrdt_engine* e, ycrdt_batch* b, HostView& hv) {
+  Work& w = e->w;
+  auto& V = e->bufs;
+  bool ok = true;
+  hipStream_t s = e->stream;
+  const uint32_t nsegs = e->nsegs, nlists = e->nlists;
+  uint32_t narr = 0;
+  if (nlists) {
+    HIPCHK(hipMemcpyAsync(&narr, w.y_lstart + nlists, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+  }
+  ViewBufs vb;
+  const size_t ck = std::max<uint32_t>(w.cap_keys, 1);
+  vb.kmap = take<uint32_t>(V, B_VKMAP, ck, ok);
+  vb.krep = take<uint32_t>(V, B_VKREP, ck, ok);
+  vb.keys = take<ViewKey>(V, B_VKEYS, ck, ok);
+  vb.nkeys = take<uint32_t>(V, B_VNKEYS, 4, ok);
+  vb.pos_of = take<uint32_t>(V, B_VPOS, (size_t)nsegs + 1, ok);
+  vb.d0 = take<uint32_t>(V, B_VD0, (size_t)narr + 1, ok);
+  vb.n0 = take<uint32_t>(V, B_VN0, (size_t)narr + 1, ok);
+  vb.d1 = take<uint32_t>(V, B_VD1, (size_t)narr + 1, ok);
+  vb.n1 = take<uint32_t>(V, B_VN1, (size_t)narr + 1, ok);
+  vb.order = take<uint32_t>(V, B_VORDER, (size_t)narr + 1, ok);
+  vb.segs = take<ViewSeg>(V, B_VSEGS, (size_t)narr + 1, ok);
+  if (!ok) return fail(YCRDT_E_DEVICE, "hipMalloc failed (view)");
+  hv.keys.clear();
+  hv.segs.clear();
+  hv.bytes.assign(b->nbytes, 0);
+  if (nsegs) {
+    launch_view(w, vb, nsegs, nlists, narr, s);
+    Counters c;
+    int rc = check(e, c, "view");
+    if (rc) return rc;
+    uint32_t nkeys = 0;
+    HIPCHK(hipMemcpy(&nkeys, vb.nkeys, sizeof(uint32_t), hipMemcpyDeviceToHost));
+    hv.keys.resize(nkeys);
+    hv.segs.resize(narr);
+    if (nkeys) HIPCHK(hipMemcpy(hv.keys.data(), vb.keys, sizeof(ViewKey) * nkeys, hipMemcpyDeviceToHost));
+    if (narr) HIPCHK(hipMemcpy(hv.segs.data(), vb.segs, sizeof(ViewSeg) * narr, hipMemcpyDeviceToHost));
+  }
+  if (b->nbytes) HIPCHK(hipMemcpy(hv.bytes.data(), b->bytes.p, b->nbytes, hipMemcpyDeviceToHost));
+  hv.index();
+  hv.valid = true;
   return YCRDT_OK;
 }
 
@@ -773,6 +827,7 @@ int ycrdt_apply_updates(ycrdt_doc* d, const ycrdt_buf* ups, size_t n) {
       hipMemcpyAsync(d->sv.data(), e->w.sv_out, e->sv_bytes, hipMemcpyDeviceToHost, e->stream);
       hipStreamSynchronize(e->stream);
       d->last = e->last;
+      d->view.valid = false;
     }
   }
   if (b.bytes.p) hipFree(b.bytes.p);
@@ -909,6 +964,141 @@ void ycrdt_batch_destroy(ycrdt_batch* b) {
   if (b->bytes.p) hipFree(b->bytes.p);
   if (b->meta.p) hipFree(b->meta.p);
   delete b;
+}
+
+// ---- crdt.c materialisation + local ops (yc_view.hip, yc_host.cpp)
+
+static int ensure_view(ycrdt_doc* d) {
+  if (d->view.valid) return YCRDT_OK;
+  if (!d->state_len) {
+    d->view = HostView();
+    d->view.valid = true;
+    return YCRDT_OK;
+  }
+  ycrdt_engine* e = d->e;
+  HIPCHK(hipSetDevice(e->device));
+  ycrdt_batch b;
+  b.e = e;
+  int rc = stage(&b, nullptr, 0, &d->state, d->state_len);
+  if (rc == YCRDT_OK) rc = run_merge(e, &b, nullptr);  // idempotent on the canonical state
+  if (rc == YCRDT_OK) rc = run_view(e, &b, d->view);
+  if (b.bytes.p) hipFree(b.bytes.p);
+  if (b.meta.p) hipFree(b.meta.p);
+  return rc;
+}
+
+static uint32_t next_clock(ycrdt_doc* d) {
+  std::unordered_map<uint32_t, uint32_t> sv;
+  parse_sv(d->sv.data(), d->sv.size(), sv);
+  auto it = sv.find(d->client_id);
+  return it == sv.end() ? 0u : it->second;
+}
+
+static int apply_local(ycrdt_doc* d, const std::vector<uint8_t>& u) {
+  ycrdt_buf b{u.data(), u.size()};
+  return ycrdt_apply_updates(d, &b, 1);
+}
+
+static OpTarget target_of(const char* root, const char* parent_key) {
+  OpTarget t;
+  t.root = root;
+  t.nested = parent_key != nullptr;
+  if (parent_key) t.key = parent_key;
+  return t;
+}
+
+int ycrdt_doc_json(ycrdt_doc* d, const char* root, int kind, ycrdt_out* out) {
+  if (!d || !root || !out || kind < 0 || kind > 1) return fail(YCRDT_E_ARG, "bad arg");
+  out->ptr = nullptr;
+  out->len = 0;
+  int rc = ensure_view(d);
+  if (rc) return rc;
+  std::string j, err;
+  if (!view_root_json(d->view, root, kind, j, err)) return fail(YCRDT_E_DECODE, err);
+  out->len = j.size();
+  out->ptr = (uint8_t*)malloc(j.size() + 1);
+  memcpy(out->ptr, j.data(), j.size());
+  out->ptr[j.size()] = 0;
+  return YCRDT_OK;
+}
+
+int ycrdt_map_set(ycrdt_doc* d, const char* root, const char* parent_key, const char* key, const uint8_t* any,
+                  size_t anylen) {
+  if (!d || !root || !key || (!any && anylen)) return fail(YCRDT_E_ARG, "null arg");
+  if (!any_values_ok(any, anylen, 1)) return fail(YCRDT_E_ARG, "bad any value");
+  int rc = ensure_view(d);
+  if (rc) return rc;
+  std::vector<uint8_t> content{1};  // ContentAny([value])
+  content.insert(content.end(), any, any + anylen);
+  std::vector<uint8_t> u;
+  std::string err;
+  rc = encode_map_set(d->view, target_of(root, parent_key), key, d->client_id, next_clock(d), 8, content.data(),
+                      content.size(), u, err);
+  if (rc) return fail(rc, err);
+  return apply_local(d, u);
+}
+
+int ycrdt_map_set_type(ycrdt_doc* d, const char* root, const char* parent_key, const char* key, uint32_t type_ref) {
+  if (!d || !root || !key || type_ref > 1) return fail(YCRDT_E_ARG, "bad arg (type_ref: 0 = YArray, 1 = YMap)");
+  int rc = ensure_view(d);
+  if (rc) return rc;
+  std::vector<uint8_t> content{(uint8_t)type_ref};  // ContentType: writeTypeRef
+  std::vector<uint8_t> u;
+  std::string err;
+  rc = encode_map_set(d->view, target_of(root, parent_key), key, d->client_id, next_clock(d), 7, content.data(),
+                      content.size(), u, err);
+  if (rc) return fail(rc, err);
+  return apply_local(d, u);
+}
+
+int ycrdt_map_delete(ycrdt_doc* d, const char* root, const char* parent_key, const char* key) {
+  if (!d || !root || !key) return fail(YCRDT_E_ARG, "null arg");
+  int rc = ensure_view(d);
+  if (rc) return rc;
+  std::vector<uint8_t> u;
+  std::string err;
+  bool nothing = false;
+  rc = encode_map_delete(d->view, target_of(root, parent_key), key, u, nothing, err);
+  if (rc) return fail(rc, err);
+  return nothing ? YCRDT_OK : apply_local(d, u);
+}
+
+int ycrdt_array_insert(ycrdt_doc* d, const char* root, const char* parent_key, uint32_t index, const uint8_t* anys,
+                       size_t len, uint32_t count) {
+  if (!d || !root || (!anys && len)) return fail(YCRDT_E_ARG, "null arg");
+  if (!any_values_ok(anys, len, count)) return fail(YCRDT_E_ARG, "bad any value");
+  int rc = ensure_view(d);
+  if (rc) return rc;
+  std::vector<uint8_t> u;
+  std::string err;
+  bool nothing = false;
+  rc = encode_array_insert(d->view, target_of(root, parent_key), index, anys, len, count, d->client_id, next_clock(d), u,
+                           nothing, err);
+  if (rc) return fail(rc, err);
+  return nothing ? YCRDT_OK : apply_local(d, u);
+}
+
+int ycrdt_array_delete(ycrdt_doc* d, const char* root, const char* parent_key, uint32_t index, uint32_t length) {
+  if (!d || !root) return fail(YCRDT_E_ARG, "null arg");
+  int rc = ensure_view(d);
+  if (rc) return rc;
+  std::vector<uint8_t> u;
+  std::string err;
+  bool nothing = false;
+  rc = encode_array_delete(d->view, target_of(root, parent_key), index, length, u, nothing, err);
+  // like Yjs, what exists is deleted even when the range runs past the end (then it throws)
+  if (!nothing && !u.empty()) {
+    const int rc2 = apply_local(d, u);
+    if (rc2) return rc2;
+  }
+  if (rc) return fail(rc, err);
+  return YCRDT_OK;
+}
+
+int ycrdt_doc_client_id(ycrdt_doc* d, uint32_t* out) {
+  if (!d || !out) return fail(YCRDT_E_ARG, "null arg");
+  *out = d->client_id;
+  return YCRDT_OK;
 }
 
 }  // extern "C"

@@ -5,6 +5,7 @@
 // U = units (one per (client, clock) in the merged store), NS = segments, NO = output structs.
 #pragma once
 #include "yc_common.h"
+#include "yc_view.h"
 
 namespace yc {
 
@@ -302,6 +303,19 @@ enum : uint32_t {
   UF_DS = 4u,          // a delete-set range covers the unit
   UF_CUT = 8u,         // a struct boundary is required before this unit
 };
+
+// ---- materialised view (yc_view.hip), copied to the host as is
+struct ViewBufs {
+  uint32_t* kmap = nullptr;  // [cap_keys] slot -> ViewKey index
+  uint32_t* krep = nullptr;  // [cap_keys] a root member segment
+  ViewKey* keys = nullptr;   // [cap_keys]
+  uint32_t* nkeys = nullptr;
+  uint32_t* pos_of = nullptr;// [NS] segment -> sorted member position
+  uint32_t *d0 = nullptr, *n0 = nullptr, *d1 = nullptr, *n1 = nullptr;  // [narr] list ranking
+  uint32_t* order = nullptr; // [narr] members in document order
+  ViewSeg* segs = nullptr;   // [narr]
+};
+void launch_view(const Work& w, const ViewBufs& v, uint32_t nsegs, uint32_t nlists, uint32_t narr, hipStream_t s);
 
 // ---- launch entry points (yc_decode.hip / yc_merge.hip / yc_encode.hip / yc_prims.hip)
 void launch_group_parse(const Work& w, hipStream_t s);   // k_parse: nxt at every byte

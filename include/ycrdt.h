@@ -87,6 +87,32 @@ int ycrdt_merge_updates(ycrdt_engine *e, const ycrdt_buf *ups, size_t n, ycrdt_o
  * with the update's delete set. */
 int ycrdt_diff_update(ycrdt_engine *e, ycrdt_buf update, ycrdt_buf sv, ycrdt_out *out);
 
+/* ---- crdt.c materialisation and local ops ------------------------------------------------
+ * A "target" is root type `root`, or (parent_key != NULL) the shared type stored in root YMap
+ * `root` under `parent_key` (crdt.js nests one YArray per map key, crdt.js:423-430).
+ * The device computes map winners and list order (a view of the merged state); the host
+ * decodes values and writes each local op as a one-struct Yjs v1 update, applied like a remote
+ * one, so the doc's bytes match a Yjs doc that performed the same ops. */
+/* YMap.toJSON / YArray.toJSON of a root (kind 0 = map, 1 = array) as JSON.stringify text
+ * (crdt.js:202,214,304,372,494,528,555,581,607; YMap.toJSON Y@51558, typeListToArray Y@46408) */
+int ycrdt_doc_json(ycrdt_doc *d, const char *root, int kind, ycrdt_out *out);
+/* YMap.set(key, value) with a lib0 `any` value (crdt.js:375,434; typeMapSet Y@49334) */
+int ycrdt_map_set(ycrdt_doc *d, const char *root, const char *parent_key, const char *key, const uint8_t *any,
+                  size_t anylen);
+/* YMap.set(key, new Y.Array()) (type_ref 0) / new Y.Map() (1)  (crdt.js:423) */
+int ycrdt_map_set_type(ycrdt_doc *d, const char *root, const char *parent_key, const char *key, uint32_t type_ref);
+/* YMap.delete(key)  (crdt.js:465; typeMapDelete Y@49261) */
+int ycrdt_map_delete(ycrdt_doc *d, const char *root, const char *parent_key, const char *key);
+/* YArray.insert(index, values) / push / unshift with `count` concatenated lib0 `any` values
+ * (crdt.js:426-428,527,554,580; typeListInsertGenerics Y@48365). "Length exceeded!" past the end. */
+int ycrdt_array_insert(ycrdt_doc *d, const char *root, const char *parent_key, uint32_t index, const uint8_t *anys,
+                       size_t len, uint32_t count);
+/* YArray.delete(index, length)  (crdt.js:429,606; typeListDelete Y@48835). Like Yjs, deletes
+ * what exists and then fails with "Length exceeded!" when the range runs past the end. */
+int ycrdt_array_delete(ycrdt_doc *d, const char *root, const char *parent_key, uint32_t index, uint32_t length);
+/* doc.clientID */
+int ycrdt_doc_client_id(ycrdt_doc *d, uint32_t *out);
+
 /* ---- device-resident batches (ingest queue / benchmark) ---------------------------------- */
 /* Copies the updates into HBM. */
 int ycrdt_batch_stage(ycrdt_engine *e, const ycrdt_buf *ups, size_t n, ycrdt_batch **out);

@@ -82,3 +82,31 @@ def test_oracle_pending_reported():
     with pytest.raises(OracleError) as ei:
         d.apply_update(delta)
     assert ei.value.code == -2
+
+
+def test_oracle_local_ops_pinned():
+    """The oracle's local ops (typeMapSet / typeListInsertGenerics / typeListDelete restated) replay
+    the root-type Yjs op scripts of tests/golden/ops.json byte for byte after every step."""
+    import json
+    import os
+
+    with open(os.path.join(os.path.dirname(__file__), "golden", "ops.json")) as f:
+        cases = [c for c in json.load(f)["cases"] if c["name"].startswith("ops_root_")]
+    assert len(cases) == 20
+    for c in cases:
+        d = Doc(c["client"])
+        for i, s in enumerate(c["steps"]):
+            op = s["op"]
+            if op == "apply":
+                d.apply_update(bytes.fromhex(s["update"]))
+            elif op == "map_set":
+                d.map_set(s["root"], s["key"], bytes.fromhex(s["any"]))
+            elif op == "map_delete":
+                d.map_delete(s["root"], s["key"])
+            elif op == "array_insert":
+                d.array_insert(s["root"], s["index"], [bytes.fromhex(a) for a in s["anys"]])
+            elif op == "array_delete":
+                d.array_delete(s["root"], s["index"], s["length"])
+            assert d.encode_state_as_update().hex() == s["state"], (c["name"], i, op)
+        assert json.loads(d.root_json("users", "map")) == c["json"]["users"], c["name"]
+        assert json.loads(d.root_json("messages", "array")) == c["json"]["messages"], c["name"]
