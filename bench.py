@@ -39,9 +39,90 @@ def parse():
     p.add_argument("--workload", default="c2", choices=["c2", "c1"])
     p.add_argument("--replicas", type=int, default=None, help="override replica count (default: config)")
     p.add_argument("--no-cpu-baseline", action="store_true")
-    p.add_argument("--cpu-replicas", type=int, default=1000, help="replicas in the CPU-baseline sample")
+    p.add_argument("--cpu-replicas", type=int, default=300,
+                   help="replicas in the Yjs CPU-baseline sample (bounded: ~10 s of Yjs work)")
+    p.add_argument("--port-replicas", type=int, default=1000, help="replicas in the oracle-port timing sample")
     p.add_argument("--profile-phases", action="store_true")
     return p.parse_args()
+
+
+def _sample(cfg, n_replicas, updates, gen_map):
+    c = dict(cfg)
+    c["n_replicas"] = min(n_replicas, cfg["n_replicas"])
+    return updates if c["n_replicas"] == cfg["n_replicas"] else gen_map(**c)[0], c["n_replicas"]
+
+
+def cpu_baselines(args, cfg, updates, out_update, st, eng, gen_map):
+    """The reference path timed on this box's host cores, beside the GPU number (never `value`).
+
+    kind "reference": Yjs 13.5.16 itself (the library @ypear/crdt delegates to), in Node, on one
+    core, over a bounded sample of the same workload (scripts/yjs_baseline.js); its output is
+    checked against the GPU merge of the same sample (sha256 of the canonical update).
+    `port`: the oracle's sequential C restatement (oracle/yref.c) on the full batch, also 1 core.
+    """
+    import hashlib
+    import shutil
+    import struct
+    import subprocess
+    import tempfile
+
+    import crdt_amd
+    from oracle.yref import Doc as ODoc
+
+    res = None
+    node = shutil.which("node")
+    sups, nrep = _sample(cfg, args.cpu_replicas, updates, gen_map)
+    b = crdt_amd.Batch(sups, eng)
+    sst = b.merge()
+    gpu_out = b.result()[0]
+    del b
+    if node:
+        with tempfile.NamedTemporaryFile(suffix=".bin", delete=False) as f:
+            f.write(struct.pack("<I", len(sups)))
+            for u in sups:
+                f.write(struct.pack("<I", len(u)))
+                f.write(u)
+            fname = f.name
+        try:
+            r = subprocess.run([node, "--max-old-space-size=16384", os.path.join(ROOT, "scripts", "yjs_baseline.js"), fname],
+                               capture_output=True, text=True, timeout=240)
+            y = json.loads(r.stdout.strip().splitlines()[-1]) if r.returncode == 0 and r.stdout.strip() else None
+        finally:
+            os.unlink(fname)
+        if y and y.get("available"):
+            res = {
+                "value": round(sst.items / (y["ms"] * 1e-3), 1),
+                "unit": "items/s",
+                "cores": 1,
+                "kind": "reference",
+                "sample": f"C2 base + {nrep} replicas x {cfg['ops_per_replica']} ops ({sst.items} items): Yjs "
+                          f"{y['yjs']} / lib0 {y['lib0']} in Node {y['node']}, for u of batch: Y.applyUpdate(doc, u); "
+                          f"Y.encodeStateAsUpdate(doc), {y['ms'] / 1e3:.2f} s",
+                "parity": y["out_sha256"] == hashlib.sha256(gpu_out).hexdigest(),
+            }
+    if res is None:
+        res = {"value": None, "unit": "items/s", "cores": 1, "kind": "reference",
+               "sample": "reference baseline unavailable (no Node or no Yjs on this machine)"}
+    # the sequential C restatement (oracle/yref.c) on the full batch
+    pups, prep = _sample(cfg, args.port_replicas, updates, gen_map)
+    d = ODoc(0x7FFFFFF0)
+    c0 = time.perf_counter()
+    for u in pups:
+        d.apply_update(u)
+    ref = d.encode_state_as_update()
+    c1 = time.perf_counter()
+    pitems = st.items if pups is updates else None
+    if pitems is None:
+        b2 = crdt_amd.Batch(pups, eng)
+        pitems = b2.merge().items
+        del b2
+    res["port"] = {
+        "value": round(pitems / (c1 - c0), 1), "unit": "items/s", "cores": 1, "kind": "port",
+        "sample": f"C2 base + {prep} replicas x {cfg['ops_per_replica']} ops ({pitems} items), oracle/yref.c "
+                  f"sequential Yjs restatement, {c1 - c0:.2f} s",
+        "parity": (ref == out_update) if pups is updates else None,
+    }
+    return res
 
 
 def main():
@@ -161,33 +242,7 @@ def main():
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        from oracle.yref import Doc as ODoc
-
-        ccfg = dict(cfg)
-        ccfg["n_replicas"] = min(args.cpu_replicas, cfg["n_replicas"])
-        cups, _ = gen_map(**ccfg) if ccfg["n_replicas"] != cfg["n_replicas"] else (updates, None)
-        d = ODoc(0x7FFFFFF0)
-        c0 = time.perf_counter()
-        for u in cups:
-            d.apply_update(u)
-        ref = d.encode_state_as_update()
-        c1 = time.perf_counter()
-        citems = st.items if cups is updates else None
-        if citems is None:
-            b2 = crdt_amd.Batch(cups, eng)
-            citems = b2.merge().items
-            del b2
-        cpu = {
-            "value": round(citems / (c1 - c0), 1),
-            "unit": "items/s",
-            "cores": 1,
-            "kind": "port",
-            "sample": f"C2 base + {ccfg['n_replicas']} replicas x {cfg['ops_per_replica']} ops ({citems} items), "
-                      f"oracle/yref.c sequential Yjs restatement, {c1 - c0:.2f} s",
-        }
-        if cups is updates:
-            cpu["parity"] = ref == out_update
-
+        cpu = cpu_baselines(args, cfg, updates, out_update, st, eng, gen_map)
     line = {
         "metric": "CRDT items merged/sec at 1/2/4/8 MI355X + % of HBM roofline",
         "value": round(value, 1),

@@ -80,7 +80,7 @@ EXPORTS = (
     "ycrdt_batch_stage", "ycrdt_batch_merge", "ycrdt_batch_result", "ycrdt_batch_destroy",
     "ycrdt_merge_updates", "ycrdt_diff_update", "ycrdt_free", "ycrdt_last_error", "ycrdt_version",
     "ycrdt_doc_json", "ycrdt_map_set", "ycrdt_map_set_type", "ycrdt_map_delete", "ycrdt_array_insert",
-    "ycrdt_array_delete", "ycrdt_doc_client_id",
+    "ycrdt_array_delete", "ycrdt_doc_client_id", "ycrdt_map_type_at",
 )
 
 
@@ -115,6 +115,7 @@ def lib():
     L.ycrdt_free.argtypes = [P(_Out)]
     cs = ctypes.c_char_p
     L.ycrdt_doc_json.argtypes = [vp, cs, i32, P(_Out)]
+    L.ycrdt_map_type_at.argtypes = [vp, cs, cs, P(i32)]
     L.ycrdt_map_set.argtypes = [vp, cs, cs, cs, ctypes.c_char_p, sz]
     L.ycrdt_map_set_type.argtypes = [vp, cs, cs, cs, u32]
     L.ycrdt_map_delete.argtypes = [vp, cs, cs, cs]
@@ -240,6 +241,12 @@ class Doc:
         out = _Out()
         _check(lib().ycrdt_doc_json(self._h, name.encode(), 0 if kind == "map" else 1, ctypes.byref(out)))
         return _take(out).decode()
+
+    def map_type_at(self, root: str, key: str) -> int:
+        """type ref of the shared type under root map `root`[key] (0 YArray, 1 YMap), -1 if none."""
+        t = ctypes.c_int32()
+        _check(lib().ycrdt_map_type_at(self._h, root.encode(), key.encode(), ctypes.byref(t)))
+        return t.value
 
     def map_set(self, root: str, key: str, any_bytes: bytes, parent_key: str = None):
         a = bytes(any_bytes)

@@ -1022,6 +1022,14 @@ int ycrdt_doc_json(ycrdt_doc* d, const char* root, int kind, ycrdt_out* out) {
   return YCRDT_OK;
 }
 
+int ycrdt_map_type_at(ycrdt_doc* d, const char* root, const char* key, int32_t* type_ref) {
+  if (!d || !root || !key || !type_ref) return fail(YCRDT_E_ARG, "null arg");
+  int rc = ensure_view(d);
+  if (rc) return rc;
+  *type_ref = view_type_at(d->view, root, key);
+  return YCRDT_OK;
+}
+
 int ycrdt_map_set(ycrdt_doc* d, const char* root, const char* parent_key, const char* key, const uint8_t* any,
                   size_t anylen) {
   if (!d || !root || !key || (!any && anylen)) return fail(YCRDT_E_ARG, "null arg");

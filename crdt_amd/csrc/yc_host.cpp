@@ -465,6 +465,14 @@ const ViewKey* HostView::child_list(uint32_t unit, const std::string* psub) cons
   return nullptr;
 }
 
+int view_type_at(const HostView& v, const std::string& root, const std::string& key) {
+  const ViewKey* e = v.root_list(root, &key);
+  if (!e || e->win.client == VNONE || (e->win.flags & VS_DELETED) || e->win.ref != R_TYPE) return -1;
+  Rd r{v.bytes.data(), e->win.b0, e->win.b1};
+  const uint32_t tr = r.vu();
+  return r.ok ? (int)tr : -1;
+}
+
 bool view_root_json(const HostView& v, const std::string& name, int kind, std::string& out, std::string& err) {
   JsonCtx c{v};
   out.clear();

@@ -30,6 +30,10 @@ struct HostView {
 // toJSON of root `name`: kind 0 = YMap, 1 = YArray (JSON.stringify text)
 bool view_root_json(const HostView& v, const std::string& name, int kind, std::string& out, std::string& err);
 
+// type_ref of the live shared type stored in root map `root` under `key` (YMap.get returning a
+// Y.AbstractType), or -1 when the key holds a plain value or nothing
+int view_type_at(const HostView& v, const std::string& root, const std::string& key);
+
 // Where a local op writes: a root type, or the type stored in root map `root` under `key`.
 struct OpTarget {
   std::string root;

@@ -272,6 +272,161 @@ static napi_value js_version(napi_env env, napi_callback_info info) {
   return s;
 }
 
+/* ---- crdt.c materialisation and local ops (YMap / YArray methods of the facade) ------------ */
+/* JS string (or null/undefined → NULL when `opt`) into a malloc'd UTF-8 buffer; 0 on a type error */
+static int get_str(napi_env env, napi_value v, char **out, int opt) {
+  napi_valuetype t;
+  napi_typeof(env, v, &t);
+  *out = NULL;
+  if (opt && (t == napi_undefined || t == napi_null)) return 1;
+  if (t != napi_string) return 0;
+  size_t n = 0;
+  if (napi_get_value_string_utf8(env, v, NULL, 0, &n) != napi_ok) return 0;
+  *out = (char *)malloc(n + 1);
+  if (napi_get_value_string_utf8(env, v, *out, n + 1, &n) != napi_ok) { free(*out); *out = NULL; return 0; }
+  return 1;
+}
+
+typedef struct { ycrdt_doc *d; char *root, *pkey, *key; } op_args;
+
+/* (doc, root, parentKey|null[, key]) — the target of every view/local-op call */
+static int op_target(napi_env env, napi_value *argv, size_t argc, int want_key, op_args *a) {
+  memset(a, 0, sizeof(*a));
+  if (argc < (size_t)(3 + want_key)) { napi_throw_type_error(env, NULL, "ycrdt: missing arguments"); return 0; }
+  a->d = get_doc(env, argv[0]);
+  if (!a->d) return 0;
+  if (!get_str(env, argv[1], &a->root, 0) || !get_str(env, argv[2], &a->pkey, 1) ||
+      (want_key && !get_str(env, argv[3], &a->key, 0))) {
+    free(a->root); free(a->pkey);
+    napi_throw_type_error(env, NULL, "ycrdt: type name and keys must be strings");
+    return 0;
+  }
+  return 1;
+}
+static void op_free(op_args *a) { free(a->root); free(a->pkey); free(a->key); }
+
+/* docJson(doc, root, kind) → JSON text of YMap.toJSON (kind 0) / YArray.toJSON (kind 1)
+ * (crdt.js:202,214,304,372,494,528,555,581,607) */
+static napi_value js_doc_json(napi_env env, napi_callback_info info) {
+  size_t argc = 3;
+  napi_value argv[3], s;
+  CHECK(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+  ycrdt_doc *d = argc > 2 ? get_doc(env, argv[0]) : NULL;
+  if (!d) return NULL;
+  char *root = NULL;
+  int32_t kind = 0;
+  if (!get_str(env, argv[1], &root, 0) || napi_get_value_int32(env, argv[2], &kind) != napi_ok) {
+    free(root);
+    napi_throw_type_error(env, NULL, "docJson(doc, root, kind)");
+    return NULL;
+  }
+  ycrdt_out o = {NULL, 0};
+  int rc = ycrdt_doc_json(d, root, kind, &o);
+  free(root);
+  if (rc != YCRDT_OK) return throw_rc(env, rc);
+  CHECK(env, napi_create_string_utf8(env, (const char *)o.ptr, o.len, &s));
+  ycrdt_free(&o);
+  return s;
+}
+
+/* mapSet(doc, root, parentKey, key, anyBytes)   (YMap.set, crdt.js:375,434) */
+static napi_value js_map_set(napi_env env, napi_callback_info info) {
+  size_t argc = 5;
+  napi_value argv[5];
+  CHECK(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+  op_args a;
+  if (!op_target(env, argv, argc, 1, &a)) return NULL;
+  ycrdt_buf v;
+  int rc = YCRDT_E_ARG;
+  if (argc > 4 && get_bytes(env, argv[4], &v)) rc = ycrdt_map_set(a.d, a.root, a.pkey, a.key, v.ptr, v.len);
+  else { op_free(&a); napi_throw_type_error(env, NULL, "mapSet: value must be lib0 any bytes"); return NULL; }
+  op_free(&a);
+  return rc == YCRDT_OK ? NULL : throw_rc(env, rc);
+}
+
+/* mapSetType(doc, root, parentKey, key, typeRef)   (YMap.set(key, new Y.Array()), crdt.js:423) */
+static napi_value js_map_set_type(napi_env env, napi_callback_info info) {
+  size_t argc = 5;
+  napi_value argv[5];
+  CHECK(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+  op_args a;
+  if (!op_target(env, argv, argc, 1, &a)) return NULL;
+  uint32_t tr = 0;
+  if (argc > 4) napi_get_value_uint32(env, argv[4], &tr);
+  int rc = ycrdt_map_set_type(a.d, a.root, a.pkey, a.key, tr);
+  op_free(&a);
+  return rc == YCRDT_OK ? NULL : throw_rc(env, rc);
+}
+
+/* mapDelete(doc, root, parentKey, key)   (YMap.delete, crdt.js:465) */
+static napi_value js_map_delete(napi_env env, napi_callback_info info) {
+  size_t argc = 4;
+  napi_value argv[4];
+  CHECK(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+  op_args a;
+  if (!op_target(env, argv, argc, 1, &a)) return NULL;
+  int rc = ycrdt_map_delete(a.d, a.root, a.pkey, a.key);
+  op_free(&a);
+  return rc == YCRDT_OK ? NULL : throw_rc(env, rc);
+}
+
+/* arrayInsert(doc, root, parentKey, index, anysBytes, count)   (insert/push/unshift, crdt.js:426-428,527,554,580) */
+static napi_value js_array_insert(napi_env env, napi_callback_info info) {
+  size_t argc = 6;
+  napi_value argv[6];
+  CHECK(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+  op_args a;
+  if (!op_target(env, argv, argc, 0, &a)) return NULL;
+  uint32_t index = 0, count = 0;
+  ycrdt_buf v;
+  if (argc < 6 || napi_get_value_uint32(env, argv[3], &index) != napi_ok || !get_bytes(env, argv[4], &v) ||
+      napi_get_value_uint32(env, argv[5], &count) != napi_ok) {
+    op_free(&a);
+    napi_throw_type_error(env, NULL, "arrayInsert(doc, root, parentKey, index, anys, count)");
+    return NULL;
+  }
+  int rc = ycrdt_array_insert(a.d, a.root, a.pkey, index, v.ptr, v.len, count);
+  op_free(&a);
+  return rc == YCRDT_OK ? NULL : throw_rc(env, rc);
+}
+
+/* arrayDelete(doc, root, parentKey, index, length)   (YArray.delete, crdt.js:429,606) */
+static napi_value js_array_delete(napi_env env, napi_callback_info info) {
+  size_t argc = 5;
+  napi_value argv[5];
+  CHECK(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+  op_args a;
+  if (!op_target(env, argv, argc, 0, &a)) return NULL;
+  uint32_t index = 0, length = 0;
+  if (argc < 5 || napi_get_value_uint32(env, argv[3], &index) != napi_ok ||
+      napi_get_value_uint32(env, argv[4], &length) != napi_ok) {
+    op_free(&a);
+    napi_throw_type_error(env, NULL, "arrayDelete(doc, root, parentKey, index, length)");
+    return NULL;
+  }
+  int rc = ycrdt_array_delete(a.d, a.root, a.pkey, index, length);
+  op_free(&a);
+  return rc == YCRDT_OK ? NULL : throw_rc(env, rc);
+}
+
+/* mapTypeAt(doc, root, key) → type ref of the shared type under root[key], -1 if none (YMap.get) */
+static napi_value js_map_type_at(napi_env env, napi_callback_info info) {
+  size_t argc = 3;
+  napi_value argv[4], v;
+  CHECK(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+  if (argc < 3) { napi_throw_type_error(env, NULL, "mapTypeAt(doc, root, key)"); return NULL; }
+  napi_get_null(env, &argv[3]);
+  napi_value args[4] = {argv[0], argv[1], argv[3], argv[2]};  /* (doc, root, null, key) */
+  op_args a;
+  if (!op_target(env, args, 4, 1, &a)) return NULL;
+  int32_t tr = -1;
+  int rc = ycrdt_map_type_at(a.d, a.root, a.key, &tr);
+  op_free(&a);
+  if (rc != YCRDT_OK) return throw_rc(env, rc);
+  CHECK(env, napi_create_int32(env, tr, &v));
+  return v;
+}
+
 static napi_value init(napi_env env, napi_value exports) {
   napi_property_descriptor props[] = {
       {"setDevice", NULL, js_set_device, NULL, NULL, NULL, napi_default, NULL},
@@ -283,6 +438,13 @@ static napi_value init(napi_env env, napi_value exports) {
       {"diffUpdate", NULL, js_diff_update, NULL, NULL, NULL, napi_default, NULL},
       {"lastStats", NULL, js_last_stats, NULL, NULL, NULL, napi_default, NULL},
       {"version", NULL, js_version, NULL, NULL, NULL, napi_default, NULL},
+      {"mapTypeAt", NULL, js_map_type_at, NULL, NULL, NULL, napi_default, NULL},
+      {"docJson", NULL, js_doc_json, NULL, NULL, NULL, napi_default, NULL},
+      {"mapSet", NULL, js_map_set, NULL, NULL, NULL, napi_default, NULL},
+      {"mapSetType", NULL, js_map_set_type, NULL, NULL, NULL, napi_default, NULL},
+      {"mapDelete", NULL, js_map_delete, NULL, NULL, NULL, napi_default, NULL},
+      {"arrayInsert", NULL, js_array_insert, NULL, NULL, NULL, napi_default, NULL},
+      {"arrayDelete", NULL, js_array_delete, NULL, NULL, NULL, napi_default, NULL},
   };
   napi_define_properties(env, exports, sizeof(props) / sizeof(props[0]), props);
   return exports;

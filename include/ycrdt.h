@@ -96,6 +96,9 @@ int ycrdt_diff_update(ycrdt_engine *e, ycrdt_buf update, ycrdt_buf sv, ycrdt_out
 /* YMap.toJSON / YArray.toJSON of a root (kind 0 = map, 1 = array) as JSON.stringify text
  * (crdt.js:202,214,304,372,494,528,555,581,607; YMap.toJSON Y@51558, typeListToArray Y@46408) */
 int ycrdt_doc_json(ycrdt_doc *d, const char *root, int kind, ycrdt_out *out);
+/* YMap.get(key) of root map `root`: *type_ref = the type ref (0 YArray, 1 YMap, ...) when the
+ * key holds a live shared type, else -1 (a plain value or nothing)  (crdt.js:423-424) */
+int ycrdt_map_type_at(ycrdt_doc *d, const char *root, const char *key, int32_t *type_ref);
 /* YMap.set(key, value) with a lib0 `any` value (crdt.js:375,434; typeMapSet Y@49334) */
 int ycrdt_map_set(ycrdt_doc *d, const char *root, const char *parent_key, const char *key, const uint8_t *any,
                   size_t anylen);

@@ -1,0 +1,87 @@
+#!/usr/bin/env node
+// CPU baseline leg of bench.py: the reference path — Yjs itself — timed in Node on this machine's
+// host cores (SURVEY.md §8(d)). Never part of the product; only bench.py runs it.
+//
+// The Yjs that @ypear/crdt would call is the machine's installed copy: this image ships Yjs
+// 13.5.16 + lib0 0.2.42 inside JupyterLab's static bundle (SURVEY.md §4.1), loaded in place by
+// tests/golden/gen/load_yjs.js. If it is absent the script prints {"available": false}.
+//
+// Usage: node yjs_baseline.js <batch file> [workers]
+//   batch file = u32le count, then per update u32le length + bytes (bench.py writes it)
+// Single-doc workloads run on ONE core (Yjs integrates a doc on one thread; SURVEY.md §8(d)):
+// `for u of batch: Y.applyUpdate(doc, u)` then `Y.encodeStateAsUpdate(doc)`, timed with
+// process.hrtime.bigint() around that loop only. With workers > 1 (doc fleets), each
+// worker_thread merges its own copy of the batch as an independent doc and the rate is the sum.
+'use strict';
+const fs = require('fs');
+const path = require('path');
+const crypto = require('crypto');
+const { Worker, isMainThread, parentPort, workerData } = require('worker_threads');
+
+function readBatch(file) {
+  const b = fs.readFileSync(file);
+  const n = b.readUInt32LE(0);
+  const ups = [];
+  let p = 4;
+  for (let i = 0; i < n; i++) {
+    const len = b.readUInt32LE(p);
+    p += 4;
+    ups.push(new Uint8Array(b.buffer, b.byteOffset + p, len));
+    p += len;
+  }
+  return ups;
+}
+
+function runOnce(Y, ups) {
+  const doc = new Y.Doc();
+  doc.clientID = 0x7ffffff0;
+  const t0 = process.hrtime.bigint();
+  for (const u of ups) Y.applyUpdate(doc, u);
+  const out = Y.encodeStateAsUpdate(doc);
+  const t1 = process.hrtime.bigint();
+  return { ms: Number(t1 - t0) / 1e6, out };
+}
+
+function load() {
+  try {
+    const { loadYjs } = require(path.join(__dirname, '..', 'tests', 'golden', 'gen', 'load_yjs.js'));
+    return loadYjs();
+  } catch (e) {
+    return null;
+  }
+}
+
+if (isMainThread) {
+  const file = process.argv[2];
+  const workers = Math.max(1, parseInt(process.argv[3] || '1', 10));
+  const Y = load();
+  if (!Y) {
+    console.log(JSON.stringify({ available: false, reason: 'Yjs bundle not found on this machine' }));
+    process.exit(0);
+  }
+  const ups = readBatch(file);
+  if (workers === 1) {
+    const r = runOnce(Y, ups);
+    const { canonicalUpdate } = require(path.join(__dirname, '..', 'tests', 'golden', 'gen', 'v1.js'));
+    const canon = canonicalUpdate(r.out);
+    console.log(JSON.stringify({
+      available: true, yjs: '13.5.16', lib0: '0.2.42', node: process.version, workers: 1,
+      ms: r.ms, out_bytes: r.out.length, out_sha256: crypto.createHash('sha256').update(canon).digest('hex'),
+    }));
+  } else {
+    let done = 0, maxMs = 0;
+    for (let w = 0; w < workers; w++) {
+      const wk = new Worker(__filename, { workerData: { file } });
+      wk.on('message', (m) => {
+        maxMs = Math.max(maxMs, m.ms);
+        if (++done === workers) {
+          console.log(JSON.stringify({ available: true, yjs: '13.5.16', lib0: '0.2.42', node: process.version, workers, ms: maxMs }));
+        }
+      });
+    }
+  }
+} else {
+  const Y = load();
+  const r = runOnce(Y, readBatch(workerData.file));
+  parentPort.postMessage({ ms: r.ms });
+}

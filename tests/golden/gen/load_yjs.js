@@ -1,4 +1,6 @@
-// Fixture-generation helper (TEST INFRASTRUCTURE ONLY — never shipped, never run on the GPU box).
+// Fixture-generation helper (TEST INFRASTRUCTURE ONLY — never part of the product). Also used by
+// scripts/yjs_baseline.js, bench.py's CPU-baseline leg, which times the machine's OWN installed
+// Yjs copy (the same image on the GPU box); no Yjs code is shipped with this repository.
 //
 // Loads the Yjs 13.5.16 + lib0 0.2.42 bundle that ships inside this container's JupyterLab
 // static assets (SURVEY.md §4.1, §8(c)). No Yjs code lives in this repository: this file is a

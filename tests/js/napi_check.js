@@ -2,6 +2,9 @@
 // Drives the N-API `Y` facade (crdt_amd/js). Modes:
 //   cpu     — the addon loads, exports the Y surface, and fails loudly without a GPU
 //   golden  — every golden case through Y.applyUpdate / Y.encodeStateAsUpdate / encodeStateVector
+//   ops     — every Yjs 13.5.16 local-op script (tests/golden/ops.json) through the YMap / YArray
+//             facade crdt.js uses (getMap/getArray, set/delete, set(key, new Y.Array()), push /
+//             unshift / insert / delete, toJSON / toArray, observe), byte-identical after every step
 'use strict';
 const fs = require('fs');
 const path = require('path');
@@ -13,16 +16,68 @@ const hex = (u) => Buffer.from(u).toString('hex');
 const unhex = (h) => new Uint8Array(Buffer.from(h, 'hex'));
 
 const mode = process.argv[2] || 'cpu';
+const { encodeAny, decodeAny } = require(path.join(ROOT, 'crdt_amd', 'js', 'any.js'));
+const opsCases = () => JSON.parse(fs.readFileSync(path.join(ROOT, 'tests', 'golden', 'ops.json'))).cases;
 for (const f of ['Doc', 'applyUpdate', 'applyUpdates', 'encodeStateAsUpdate', 'encodeStateVector', 'mergeUpdates', 'diffUpdate']) {
   assert.strictEqual(typeof Y[f], 'function', f);
 }
 assert.ok(/gfx950/.test(Y.version()));
+for (const f of ['getMap', 'getArray', 'transact']) assert.strictEqual(typeof Y.Doc.prototype[f], 'function', f);
+for (const f of ['set', 'get', 'has', 'delete', 'toJSON', 'observe', 'unobserve']) assert.strictEqual(typeof Y.Map.prototype[f], 'function', f);
+for (const f of ['insert', 'push', 'unshift', 'delete', 'toJSON', 'toArray', 'observe', 'unobserve']) assert.strictEqual(typeof Y.Array.prototype[f], 'function', f);
 if (mode === 'cpu') {
+  // the lib0 any codec against every value Yjs 13.5.16 wrote in the op scripts
+  let nv = 0;
+  for (const c of opsCases()) {
+    for (const s of c.steps) {
+      for (const a of s.any ? [s.any] : s.anys || []) {
+        const vals = decodeAny(unhex(a));
+        assert.strictEqual(vals.length, 1);
+        assert.strictEqual(hex(encodeAny(vals)), a, 'any codec ' + a);
+        nv++;
+      }
+    }
+  }
+  console.log('any codec ok:', nv, 'values');
   let threw = null;
   try { new Y.Doc(); } catch (e) { threw = e; }
   assert.ok(threw instanceof Error, 'no device: new Y.Doc() must throw');
   assert.ok(/device/i.test(threw.message), threw.message);
   console.log('napi cpu ok:', threw.message);
+} else if (mode === 'ops') {
+  let n = 0, events = 0;
+  for (const c of opsCases()) {
+    const d = new Y.Doc({ clientID: c.client });
+    const users = d.getMap('users');
+    const msgs = d.getArray('messages');
+    users.observe((ev) => { events++; assert.ok(ev.keysChanged.size > 0 && ev.target === users); });
+    c.steps.forEach((s, i) => {
+      const tgt = () => (s.parent_key ? users.get(s.parent_key) : d.getArray(s.root));
+      if (s.op === 'apply') Y.applyUpdate(d, unhex(s.update));
+      else if (s.op === 'map_set') d.getMap(s.root).set(s.key, decodeAny(unhex(s.any))[0]);
+      else if (s.op === 'map_set_type') {
+        const a = new Y.Array();
+        assert.strictEqual(d.getMap(s.root).set(s.key, a), a);
+        assert.ok(users.get(s.key) instanceof Y.Array);
+      } else if (s.op === 'map_delete') d.getMap(s.root).delete(s.key);
+      else if (s.op === 'array_insert') {
+        const arr = tgt();
+        assert.ok(arr instanceof Y.Array, c.name + ' step ' + i);
+        const vals = s.anys.map((a) => decodeAny(unhex(a))[0]);
+        const L = arr.length;
+        if (s.index === L && i % 2) arr.push(vals);
+        else if (s.index === 0 && i % 2) arr.unshift(vals);
+        else d.transact(() => arr.insert(s.index, vals));
+      } else if (s.op === 'array_delete') tgt().delete(s.index, s.length);
+      else throw new Error(s.op);
+      assert.strictEqual(hex(Y.encodeStateAsUpdate(d)), s.state, c.name + ' step ' + i + ' ' + s.op);
+    });
+    assert.deepStrictEqual(JSON.parse(JSON.stringify(users.toJSON())), c.json.users, c.name);
+    assert.deepStrictEqual(JSON.parse(JSON.stringify(msgs.toArray())), c.json.messages, c.name);
+    n++;
+  }
+  assert.ok(events > 0, 'YMap observers fired');
+  console.log('napi ops ok:', n, 'scripts,', events, 'map events');
 } else {
   let n = 0;
   for (const set of ['kat', 'map', 'array', 'nested']) {

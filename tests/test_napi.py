@@ -26,9 +26,16 @@ def test_napi_addon_loads_and_fails_loudly_without_gpu():
         pytest.skip("a GPU is present: the no-device behaviour is not observable")
     except crdt_amd.YcrdtError:
         pass
-    assert "napi cpu ok" in _run("cpu", 120)
+    out = _run("cpu", 120)
+    assert "napi cpu ok" in out and "any codec ok" in out
 
 
 @pytest.mark.gpu
 def test_napi_golden_on_gpu():
     assert "napi golden ok" in _run("golden", 300)
+
+
+@pytest.mark.gpu
+def test_napi_facade_ops_on_gpu():
+    """The crdt.js-facing YMap / YArray facade replays every recorded Yjs op script byte-exactly."""
+    assert "napi ops ok" in _run("ops", 300)
