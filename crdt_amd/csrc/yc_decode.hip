@@ -31,6 +31,11 @@ namespace yc {
 // what the sizer hands over is re-parsed by parse_struct under a work cap.
 constexpr uint32_t PSLICE = 4096;               // bytes per parse workgroup
 constexpr uint32_t PL = 256;                    // lanes per parse workgroup
+// work cap of the general parser on what the sizer handed over. Most of the queue is garbage
+// positions whose would-be element count is large; a long chain of dependent reads there stalls
+// the whole workgroup, and a true struct over the cap is parsed exactly by the walkers.
+constexpr uint32_t PARSE_QUEUE_STEPS = 96;
+constexpr uint32_t PHALO = 1024;                // bytes staged past the slice (structs crossing its end)
 constexpr uint32_t NB = 72;                     // content refs 1..9 x info>>5
 
 // ---- the speculative struct sizer (k_parse). Exact on every valid struct; on other bytes it only
@@ -43,8 +48,25 @@ __device__ __forceinline__ uint64_t win8(const uint8_t* __restrict__ b, uint32_t
   const uint32_t* d = (const uint32_t*)(b + (p & ~3u));  // the batch buffer is padded past its end
   return ((uint64_t)d[0] | ((uint64_t)d[1] << 32)) >> ((p & 3u) * 8);
 }
-__device__ __forceinline__ uint32_t vu_fast(const uint8_t* __restrict__ b, uint32_t& p, uint32_t end, bool& ok) {
-  const uint64_t w = win8(b, p);
+// Byte sources for the sizer: the slice's bytes staged in LDS (plus a halo past its end), with
+// a fallback to the batch buffer (through the caches) for reads beyond the staged window.
+struct LdsSrc {
+  const uint8_t* __restrict__ b;
+  const uint32_t* lw;  // staged words of [s0, wend)
+  uint32_t s0, wlen;   // wlen = wend - s0
+  __device__ __forceinline__ uint32_t u8(uint32_t p) const {
+    const uint32_t o = p - s0;
+    return o < wlen ? (lw[o >> 2] >> ((o & 3u) * 8)) & 0xFFu : (uint32_t)b[p];
+  }
+  __device__ __forceinline__ uint64_t w8(uint32_t p) const {
+    const uint32_t o = p - s0;
+    if (o + 8 <= wlen) return ((uint64_t)lw[o >> 2] | ((uint64_t)lw[(o >> 2) + 1] << 32)) >> ((o & 3u) * 8);
+    return win8(b, p);
+  }
+};
+template <class S>
+__device__ __forceinline__ uint32_t vu_fast(const S& b, uint32_t& p, uint32_t end, bool& ok) {
+  const uint64_t w = b.w8(p);
   const uint64_t t = ~w & 0x8080808080ull;  // terminal bytes among the first five
   const uint32_t len = t ? ((uint32_t)__builtin_ctzll(t) >> 3) + 1 : 6u;
   uint64_t v = (w & 0x7full) | ((w >> 1) & (0x7full << 7)) | ((w >> 2) & (0x7full << 14)) | ((w >> 3) & (0x7full << 21)) |
@@ -60,15 +82,16 @@ __device__ __forceinline__ void skip_n(uint32_t& p, uint32_t n, uint32_t end, bo
   p = f ? p + n : end;
 }
 // one `any` value (L0@1937) that is not a container; false: a container, or more than this sizer does
-__device__ __forceinline__ bool any_simple(const uint8_t* __restrict__ b, uint32_t& p, uint32_t end, bool& ok) {
+template <class S>
+__device__ __forceinline__ bool any_simple(const S& b, uint32_t& p, uint32_t end, bool& ok) {
   if (p >= end) { ok = false; return true; }
-  const uint32_t tag = b[p++];
+  const uint32_t tag = b.u8(p++);
   switch (tag) {
     case 127: case 126: case 121: case 120: return true;
     case 125: {  // varInt
-      const uint64_t t = ~win8(b, p) & 0x8080808080ull;
+      const uint64_t t = ~b.w8(p) & 0x8080808080ull;
       const uint32_t len = t ? ((uint32_t)__builtin_ctzll(t) >> 3) + 1
-                             : (p + 5 < end && b[p + 5] < 0x80u ? 6u : (p + 6 < end && b[p + 6] < 0x80u ? 7u : 8u));
+                             : (p + 5 < end && b.u8(p + 5) < 0x80u ? 6u : (p + 6 < end && b.u8(p + 6) < 0x80u ? 7u : 8u));
       ok = ok && len <= 7 && end - p >= len;  // skip_vi: a first byte and up to six more
       p += len;
       return true;
@@ -82,7 +105,8 @@ __device__ __forceinline__ bool any_simple(const uint8_t* __restrict__ b, uint32
 }
 constexpr uint32_t SIZER_MAX_ELEMS = 16;
 // struct length, 0 = not a struct, 1 = hand over to parse_struct (many elements, deep nesting, Doc)
-__device__ __forceinline__ uint32_t spec_len(const uint8_t* __restrict__ b, uint32_t pos, uint32_t end, uint32_t cls) {
+template <class S>
+__device__ __forceinline__ uint32_t spec_len(const S& b, uint32_t pos, uint32_t end, uint32_t cls) {
   const uint32_t ref = cls / 8 + 1, bits = (cls % 8) << 5;
   bool ok = true;
   uint32_t p = pos + 1;
@@ -99,7 +123,7 @@ __device__ __forceinline__ uint32_t spec_len(const uint8_t* __restrict__ b, uint
     case REF_BINARY: case REF_STRING: { const uint32_t n = vu_fast(b, p, end, ok); skip_n(p, n, end, ok); break; }
     case REF_EMBED: {
       const uint32_t n = vu_fast(b, p, end, ok);
-      ok = ok && n > 0 && p < end && json_start_ok(b[p]);
+      ok = ok && n > 0 && p < end && json_start_ok(b.u8(p));
       skip_n(p, n, end, ok);
       break;
     }
@@ -107,7 +131,7 @@ __device__ __forceinline__ uint32_t spec_len(const uint8_t* __restrict__ b, uint
       uint32_t n = vu_fast(b, p, end, ok);
       skip_n(p, n, end, ok);
       n = vu_fast(b, p, end, ok);
-      ok = ok && n > 0 && p < end && json_start_ok(b[p]);
+      ok = ok && n > 0 && p < end && json_start_ok(b.u8(p));
       skip_n(p, n, end, ok);
       break;
     }
@@ -122,7 +146,7 @@ __device__ __forceinline__ uint32_t spec_len(const uint8_t* __restrict__ b, uint
       if (ok && n > SIZER_MAX_ELEMS) return 1;
       for (uint32_t i = 0; i < n && ok; ++i) {
         const uint32_t k = vu_fast(b, p, end, ok);
-        ok = ok && k > 0 && p < end && json_start_ok(b[p]);
+        ok = ok && k > 0 && p < end && json_start_ok(b.u8(p));
         skip_n(p, k, end, ok);
       }
       break;
@@ -134,7 +158,7 @@ __device__ __forceinline__ uint32_t spec_len(const uint8_t* __restrict__ b, uint
         const uint32_t q0 = p;
         if (any_simple(b, p, end, ok)) continue;
         // a container one level deep with simple members; anything deeper goes to parse_struct
-        const bool obj = b[q0] == 118;
+        const bool obj = b.u8(q0) == 118;
         const uint32_t m = vu_fast(b, p, end, ok);
         if (ok && m > SIZER_MAX_ELEMS) return 1;
         for (uint32_t j = 0; j < m && ok; ++j) {
@@ -155,16 +179,24 @@ __global__ __launch_bounds__(PL) void k_parse(Work w) {
   const Group G = w.groups[blockIdx.x / (GROUP_BYTES / PSLICE)];
   const uint32_t s0 = G.start + (blockIdx.x % (GROUP_BYTES / PSLICE)) * PSLICE;
   if (s0 >= G.end) return;
+  unsigned long long* dbg = w.dbg ? w.dbg + (size_t)w.ngroups * 8 + (size_t)blockIdx.x * 8 : nullptr;
+  if (dbg && threadIdx.x == 0) { dbg[0] = wall_clock64(); dbg[1] = clock64(); }
   const uint32_t len = min(G.end - s0, PSLICE), uend = G.uend;
   uint16_t* __restrict__ out = w.tab.nxt + s0;
   __shared__ uint32_t bstart[NB + 1], bcursor[NB], tstart[NB + 1], qn;
   __shared__ uint16_t sorted[PSLICE], queue[PSLICE];
+  __shared__ uint32_t lw[(PSLICE + PHALO) / 4 + 2];
   const uint32_t tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  // stage the slice + halo in LDS: the byte-serial varuint chains then wait on LDS, not on L2
+  const uint32_t wlen = min(uend - s0, PSLICE + PHALO);
+  const uint32_t* __restrict__ gw = (const uint32_t*)(b + s0);  // s0 is 64-byte aligned
+  for (uint32_t i = tid; i < (wlen + 3) / 4; i += PL) lw[i] = gw[i];
+  const LdsSrc src{b, lw, s0, wlen};
   for (uint32_t i = tid; i < NB; i += PL) bcursor[i] = 0;
   if (tid == 0) qn = 0;
   __syncthreads();
   for (uint32_t o = tid; o < len; o += PL) {  // GC / Skip (info + one varuint) resolved on the spot
-    const uint32_t info = b[s0 + o];
+    const uint32_t info = (lw[o >> 2] >> ((o & 3u) * 8)) & 0xFFu;
     const uint32_t ref = info & 31u;
     uint16_t d = 0;
     if (ref == REF_GC || ref == REF_SKIP) {
@@ -178,6 +210,7 @@ __global__ __launch_bounds__(PL) void k_parse(Work w) {
     out[o] = d;
   }
   __syncthreads();
+  if (dbg && tid == 0) dbg[2] = clock64();
   if (tid == 0) {  // class starts, and 64-position tiles per class
     uint32_t acc = 0, tiles = 0;
     for (uint32_t i = 0; i < NB; ++i) {
@@ -189,11 +222,12 @@ __global__ __launch_bounds__(PL) void k_parse(Work w) {
   }
   __syncthreads();
   for (uint32_t o = tid; o < len; o += PL) {
-    const uint32_t info = b[s0 + o];
+    const uint32_t info = (lw[o >> 2] >> ((o & 3u) * 8)) & 0xFFu;
     const uint32_t ref = info & 31u;
     if (ref >= 1 && ref <= REF_DOC) sorted[atomicAdd(&bcursor[(ref - 1) * 8 + (info >> 5)], 1u)] = (uint16_t)o;
   }
   __syncthreads();
+  if (dbg && tid == 0) dbg[3] = clock64();
   // every wavefront sizes tiles of ONE class: the class is a scalar for the whole parse
   const uint32_t ntiles = tstart[NB];
   for (uint32_t t = wave; t < ntiles; t += PL / 64) {
@@ -203,21 +237,25 @@ __global__ __launch_bounds__(PL) void k_parse(Work w) {
     const uint32_t i = bstart[c] + (t - tstart[c]) * 64 + lane;
     if (i < bstart[c + 1]) {
       const uint32_t o = sorted[i];
-      const uint32_t d = spec_len(b, s0 + o, uend, c);
+      const uint32_t d = spec_len(src, s0 + o, uend, c);
       if (d == 1) queue[atomicAdd(&qn, 1u)] = (uint16_t)o;
       out[o] = (uint16_t)d;
     }
   }
   __syncthreads();
+  if (dbg && tid == 0) dbg[4] = clock64();
   const uint32_t nq = qn;  // the general parser under a work cap for what the sizer handed over
   for (uint32_t i = tid; i < nq; i += PL) {
     const uint32_t o = queue[i];
     uint32_t q = s0 + o;
-    const int r = parse_struct<false, 4>(b, q, uend, SPEC_MAX_STEPS, nullptr);
+    const int r = parse_struct<false, 4>(b, q, uend, PARSE_QUEUE_STEPS, nullptr);
     out[o] = r > 0 ? (q - s0 - o < 0x10000u ? (uint16_t)(q - s0 - o) : (uint16_t)1) : (r == -1 ? (uint16_t)1 : (uint16_t)0);
   }
+  if (dbg) {
+    __syncthreads();
+    if (tid == 0) { dbg[5] = clock64(); dbg[6] = wall_clock64(); dbg[7] = ((unsigned long long)nq << 32) | ntiles; }
+  }
 }
-
 // --------------------------------------------------------------------------- 1b. chain tables
 // For every byte position p of a group, from nxt: the chain summaries (first chain position
 // at/after the end of p's chunk / block / group, number of chain positions visited before it)

@@ -353,8 +353,9 @@ int run_decode(ycrdt_engine* e, ycrdt_batch* b, bool lazy, Decoded& D) {
   // ---- K1 decode
   mark(e, "decode.parse");
   static const bool dbg_tables = getenv("YCRDT_DEBUG_TABLES") && getenv("YCRDT_DEBUG_TABLES")[0] == '1';
-  w.dbg = dbg_tables ? take<unsigned long long>(V, B_DBG, (size_t)w.ngroups * 8 + 8, ok) : nullptr;
-  if (w.dbg) HIPCHK(hipMemsetAsync(w.dbg, 0, sizeof(unsigned long long) * ((size_t)w.ngroups * 8 + 8), s));
+  const size_t ndbg = (size_t)w.ngroups * 8 + (size_t)w.ngroups * (GROUP_BYTES / 4096) * 8 + 8;
+  w.dbg = dbg_tables ? take<unsigned long long>(V, B_DBG, ndbg, ok) : nullptr;
+  if (w.dbg) HIPCHK(hipMemsetAsync(w.dbg, 0, sizeof(unsigned long long) * ndbg, s));
   launch_group_parse(w, s);
   mark(e, "decode.tables");
   launch_group_tables(w, s);
@@ -371,6 +372,32 @@ int run_decode(ycrdt_engine* e, ycrdt_batch* b, bool lazy, Decoded& D) {
     }
     fprintf(stderr, "[ycrdt] k_tables cycles per group (%u single-group): stage %.0f  classify+count %.0f  parse %.0f  requeue+B %.0f  walk %.0f\n",
             n, acc[1] / n, acc[2] / n, acc[3] / n, acc[4] / n, acc[5] / n);
+    // k_parse: per-slice phase cycles (wave 0) and the spread of slice lifetimes (wall clock, 100 MHz)
+    const size_t ns = (size_t)w.ngroups * (GROUP_BYTES / 4096);
+    std::vector<unsigned long long> q(ns * 8);
+    HIPCHK(hipMemcpy(q.data(), w.dbg + (size_t)w.ngroups * 8, sizeof(unsigned long long) * q.size(), hipMemcpyDeviceToHost));
+    double pa[6] = {0};
+    std::vector<std::pair<double, size_t>> life;
+    unsigned long long t0 = ~0ull, t1 = 0;
+    for (size_t i = 0; i < ns; ++i) {
+      if (!q[i * 8 + 6]) continue;
+      for (int k = 2; k <= 5; ++k) pa[k] += (double)(q[i * 8 + k] - q[i * 8 + k - 1]);
+      life.push_back({(double)(q[i * 8 + 6] - q[i * 8]), i});
+      t0 = std::min(t0, q[i * 8]); t1 = std::max(t1, q[i * 8 + 6]);
+    }
+    std::sort(life.begin(), life.end());
+    const size_t m = life.size();
+    if (m) {
+      fprintf(stderr, "[ycrdt] k_parse %zu slices: cycles pass1 %.0f  classes %.0f  tiles %.0f  queue %.0f | life us p50 %.2f p90 %.2f p99 %.2f max %.2f | span %.2f us\n",
+              m, pa[2] / m, pa[3] / m, pa[4] / m, pa[5] / m, life[m / 2].first / 100.0, life[m * 9 / 10].first / 100.0,
+              life[m * 99 / 100].first / 100.0, life[m - 1].first / 100.0, (double)(t1 - t0) / 100.0);
+      for (size_t j = m - 3; j < m && j < m; ++j) {
+        const size_t i = life[j].second;
+        fprintf(stderr, "[ycrdt]   slow slice %zu: %.2f us  nq %llu ntiles %llu  cycles %llu %llu %llu %llu\n", i, life[j].first / 100.0,
+                q[i * 8 + 7] >> 32, q[i * 8 + 7] & 0xFFFFFFFFull, q[i * 8 + 2] - q[i * 8 + 1], q[i * 8 + 3] - q[i * 8 + 2],
+                q[i * 8 + 4] - q[i * 8 + 3], q[i * 8 + 5] - q[i * 8 + 4]);
+      }
+    }
   }
   mark(e, "decode.walker");
   launch_walker(w, s);
