@@ -35,7 +35,8 @@ constexpr uint32_t PL = 256;                    // lanes per parse workgroup
 // positions whose would-be element count is large; a long chain of dependent reads there stalls
 // the whole workgroup, and a true struct over the cap is parsed exactly by the walkers.
 constexpr uint32_t PARSE_QUEUE_STEPS = 96;
-constexpr uint32_t PHALO = 1024;                // bytes staged past the slice (structs crossing its end)
+constexpr uint32_t PHALO = 1024;
+constexpr uint32_t PQUEUE = 1024;              // general-parser queue entries per slice                // bytes staged past the slice (structs crossing its end)
 constexpr uint32_t NB = 72;                     // content refs 1..9 x info>>5
 
 // ---- the speculative struct sizer (k_parse). Exact on every valid struct; on other bytes it only
@@ -184,7 +185,7 @@ __global__ __launch_bounds__(PL) void k_parse(Work w) {
   const uint32_t len = min(G.end - s0, PSLICE), uend = G.uend;
   uint16_t* __restrict__ out = w.tab.nxt + s0;
   __shared__ uint32_t bstart[NB + 1], bcursor[NB], tstart[NB + 1], qn;
-  __shared__ uint16_t sorted[PSLICE], queue[PSLICE];
+  __shared__ uint16_t sorted[PSLICE], queue[PQUEUE];
   __shared__ uint32_t lw[(PSLICE + PHALO) / 4 + 2];
   const uint32_t tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   // stage the slice + halo in LDS: the byte-serial varuint chains then wait on LDS, not on L2
@@ -211,14 +212,22 @@ __global__ __launch_bounds__(PL) void k_parse(Work w) {
   }
   __syncthreads();
   if (dbg && tid == 0) dbg[2] = clock64();
-  if (tid == 0) {  // class starts, and 64-position tiles per class
+  if (wave == 0) {  // class starts and 64-position tiles per class: a wavefront scan over NB classes
     uint32_t acc = 0, tiles = 0;
-    for (uint32_t i = 0; i < NB; ++i) {
-      const uint32_t c = bcursor[i];
-      bstart[i] = acc; bcursor[i] = acc; tstart[i] = tiles;
-      acc += c; tiles += (c + 63) / 64;
+    for (uint32_t base = 0; base < NB; base += 64) {
+      const uint32_t i = base + lane;
+      const uint32_t c = i < NB ? bcursor[i] : 0u, tc = (c + 63) / 64;
+      uint32_t x = c, y = tc;  // inclusive scans
+#pragma unroll
+      for (uint32_t d = 1; d < 64; d <<= 1) {
+        const uint32_t xo = __shfl_up(x, d), yo = __shfl_up(y, d);
+        if (lane >= d) { x += xo; y += yo; }
+      }
+      if (i < NB) { bstart[i] = acc + x - c; bcursor[i] = acc + x - c; tstart[i] = tiles + y - tc; }
+      acc += __shfl(x, 63);
+      tiles += __shfl(y, 63);
     }
-    bstart[NB] = acc; tstart[NB] = tiles;
+    if (lane == 0) { bstart[NB] = acc; tstart[NB] = tiles; }
   }
   __syncthreads();
   for (uint32_t o = tid; o < len; o += PL) {
@@ -238,13 +247,16 @@ __global__ __launch_bounds__(PL) void k_parse(Work w) {
     if (i < bstart[c + 1]) {
       const uint32_t o = sorted[i];
       const uint32_t d = spec_len(src, s0 + o, uend, c);
-      if (d == 1) queue[atomicAdd(&qn, 1u)] = (uint16_t)o;
+      if (d == 1) {  // over the queue's capacity the position stays handed over (1) to the walkers
+        const uint32_t k = atomicAdd(&qn, 1u);
+        if (k < PQUEUE) queue[k] = (uint16_t)o;
+      }
       out[o] = (uint16_t)d;
     }
   }
   __syncthreads();
   if (dbg && tid == 0) dbg[4] = clock64();
-  const uint32_t nq = qn;  // the general parser under a work cap for what the sizer handed over
+  const uint32_t nq = min(qn, PQUEUE);  // the general parser under a work cap for what the sizer handed over
   for (uint32_t i = tid; i < nq; i += PL) {
     const uint32_t o = queue[i];
     uint32_t q = s0 + o;
