@@ -16,6 +16,7 @@
 //                      ballot of terminal bytes + in-register gathers (wavefront prefix scan).
 //   6. k_struct_decode one lane per struct: full field decode into the SoA struct table.
 #include <algorithm>
+#include <cstdlib>
 
 #include "yc_work.h"
 

@@ -543,6 +543,12 @@ int run_merge(ycrdt_engine* e, ycrdt_batch* b, const std::unordered_map<uint32_t
       HIPCHK(hipStreamSynchronize(s));
     }
     e->nlists = launch_yata(w, nsegs, narray, s);
+    if (w.dbg && e->nlists) {
+      unsigned long long h[3];
+      HIPCHK(hipStreamSynchronize(s));
+      HIPCHK(hipMemcpy(h, w.dbg + (size_t)w.ngroups * 8 + (size_t)w.ngroups * (GROUP_BYTES / 4096) * 8, sizeof(h), hipMemcpyDeviceToHost));
+      fprintf(stderr, "[ycrdt] k_yata: %u lists, %llu integrations, %llu conflict-scan steps, %llu stack dives\n", e->nlists, h[0], h[1], h[2]);
+    }
     mark(e, "merge.merge_flags");
     launch_merge_flags(w, nsegs, s);
   }

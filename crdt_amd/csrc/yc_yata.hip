@@ -58,6 +58,7 @@ __global__ __launch_bounds__(64) void k_yata(Work w, uint32_t nlists) {
   uint32_t* __restrict__ confl = w.y_confl;   // conflictingItems stamp
   uint32_t* __restrict__ stack = w.y_stack + a;
   uint32_t head = NONE;  // parent._start
+  unsigned long long nscan = 0, ndive = 0, nint = 0;  // YCRDT_DEBUG_TABLES statistics
   uint32_t ctr = 0;      // stamps: every (integration, conflicting-set epoch) gets a fresh value
   for (uint32_t i = a; i < b; ++i) {
     const uint32_t s0 = w.y_seg[i];
@@ -80,6 +81,7 @@ __global__ __launch_bounds__(64) void k_yata(Work w, uint32_t nlists) {
         }
         state[dep] = 1;
         stack[sp++] = dep;
+        ++ndive;
         continue;
       }
       // ---- Item.integrate(t): YATA conflict resolution between origin and right origin
@@ -90,6 +92,7 @@ __global__ __launch_bounds__(64) void k_yata(Work w, uint32_t nlists) {
         const uint32_t iter = ++ctr;
         uint32_t ep = ++ctr;
         while (o != NONE && o != rseg) {
+          ++nscan;
           before[o] = iter;
           confl[o] = ep;
           const uint32_t oo = w.g_origin[o];
@@ -109,8 +112,15 @@ __global__ __launch_bounds__(64) void k_yata(Work w, uint32_t nlists) {
       else { r2 = head; head = t; }
       right[t] = r2;
       state[t] = 2;
+      ++nint;
       --sp;
     }
+  }
+  if (w.dbg) {
+    unsigned long long* d = w.dbg + (size_t)w.ngroups * 8 + (size_t)w.ngroups * (GROUP_BYTES / 4096) * 8;
+    atomicAdd(d + 0, nint);
+    atomicAdd(d + 1, nscan);
+    atomicAdd(d + 2, ndive);
   }
 }
 
