@@ -59,6 +59,13 @@ struct CopyTask {       // verified chain segment: b struct starts along the cha
   uint32_t a, b;
 };
 
+// count the lanes of a wavefront for which `pred` holds with ONE atomic (the first such lane adds
+// the popcount): per-lane atomics on one counter address serialise at the memory side
+__device__ __forceinline__ void wave_count_add(uint32_t* ctr, bool pred) {
+  const unsigned long long m = __ballot(pred);
+  if (m && (threadIdx.x & 63u) == (uint32_t)__ffsll((long long)m) - 1) atomicAdd(ctr, (uint32_t)__popcll(m));
+}
+
 __device__ __forceinline__ void raise_err(uint32_t* err, uint32_t code) {
   atomicCAS(err, 0u, code);
 }

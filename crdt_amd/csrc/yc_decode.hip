@@ -274,7 +274,7 @@ __global__ __launch_bounds__(PL) void k_parse(Work w) {
 // at/after the end of p's chunk / block / group, number of chain positions visited before it)
 // computed by backward dynamic programming (list ranking) in LDS. Table positions are 15 bits
 // (STOPF marks a chain that stops at a struct the tables could not size).
-constexpr uint32_t TL = 512;                    // lanes per table workgroup
+constexpr uint32_t TL = 1024;                   // lanes per table workgroup
 constexpr uint32_t BLOCK = 1024;                // 16 chunks
 constexpr uint32_t LDS_NXT = 0, LDS_CEXIT = 32768, LDS_CCNT = 65536, LDS_BEXIT = 81920, LDS_BCNT = 114688;
 constexpr uint32_t LDS_BM = 147456, LDS_TASK = LDS_BM + 2048;  // single-group walk: bitmap words, pieces

@@ -162,6 +162,25 @@ __global__ void k_run_sizes(Work w, uint32_t nsegs) {
   w.r_size[r] = vu_size(clock) + vu_size(len);
 }
 
+// per client: first output struct and first delete-set run, from the boundaries of the (client-
+// sorted) output and run arrays — one parallel pass instead of per-client binary searches, whose
+// ~80 dependent loads per lane made the per-client pass latency-bound
+__global__ void k_client_bounds(Work w, uint32_t nclients, uint32_t nsegs) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i > nsegs) return;
+  const uint32_t nout = w.ctr->nout, nruns = w.g_tmp2[nsegs];
+  if (i <= nout) {
+    const int64_t a = i == 0 ? -1 : (int64_t)w.o_cidx[i - 1];
+    const int64_t b = i == nout ? (int64_t)nclients : (int64_t)w.o_cidx[i];
+    for (int64_t c = a + 1; c <= b; ++c) ccol(w, CC_FIRST_OUT)[c] = i;
+  }
+  if (i <= nruns) {
+    const int64_t a = i == 0 ? -1 : (int64_t)w.g_cidx[w.r_seg[i - 1]];
+    const int64_t b = i == nruns ? (int64_t)nclients : (int64_t)w.g_cidx[w.r_seg[i]];
+    for (int64_t c = a + 1; c <= b; ++c) ccol(w, CC_RUN_LO)[c] = i;
+  }
+}
+
 // per client: struct block + delete-set block + state-vector entry sizes
 __global__ void k_client_sizes(Work w, uint32_t nclients, uint32_t nsegs) {
   const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
@@ -172,16 +191,15 @@ __global__ void k_client_sizes(Work w, uint32_t nclients, uint32_t nsegs) {
     ccol(w, CC_BLK)[c] = 0; ccol(w, CC_DSBLK)[c] = 0; ccol(w, CC_SV)[c] = 0;
     return;
   }
-  // first output struct of client c (outputs are sorted by client)
-  const uint32_t fo = lower_bound_u32(w.o_cidx, nout, c);
-  const uint32_t eo = lower_bound_u32(w.o_cidx, nout, c + 1);
-  first_out[c] = fo;
+  // first output struct of client c and of the next client (outputs are sorted by client)
+  const uint32_t fo = first_out[c], eo = first_out[c + 1];
   const uint32_t state = w.cl_state[c];
   const uint32_t cs = w.cl_start[c];
   uint32_t blk = 0, nincl = 0, fi = eo;
-  if (state > cs && eo > fo) {
+  const bool incl = state > cs && eo > fo;
+  if (incl) {
     // first included output: the one containing clock cs
-    uint32_t lo = fo, hi = eo;
+    uint32_t lo = fo, hi = cs == 0 ? fo : eo;  // a full-state encode starts at the first output
     while (lo < hi) {
       const uint32_t mid = (lo + hi) >> 1;
       const uint32_t k1 = (uint32_t)(w.g_start[w.o_first[mid + 1]] - w.cl_base[c]);
@@ -192,33 +210,23 @@ __global__ void k_client_sizes(Work w, uint32_t nclients, uint32_t nsegs) {
     const uint32_t hdr = vu_size(nincl) + vu_size(w.cl_vals[c]) + vu_size(cs);
     ccol(w, CC_HDR)[c] = hdr;
     blk = hdr + (w.o_pos[eo] - w.o_pos[fi]);
-    atomicAdd(&w.ctr->pad[0], 1u);  // included clients
   }
   ccol(w, CC_FIRST_INCL)[c] = fi;
   ccol(w, CC_NINCL)[c] = nincl;
   ccol(w, CC_BLK)[c] = blk;
   // delete-set block: runs are ordered by (client, clock)
-  uint32_t lo = 0, hi = nruns;
-  while (lo < hi) {
-    const uint32_t mid = (lo + hi) >> 1;
-    if (w.g_cidx[w.r_seg[mid]] < c) lo = mid + 1; else hi = mid;
-  }
-  uint32_t lo2 = lo, hi2 = nruns;
-  while (lo2 < hi2) {
-    const uint32_t mid = (lo2 + hi2) >> 1;
-    if (w.g_cidx[w.r_seg[mid]] <= c) lo2 = mid + 1; else hi2 = mid;
-  }
-  const uint32_t nr = lo2 - lo;
+  const uint32_t lo = ccol(w, CC_RUN_LO)[c], nr = ccol(w, CC_RUN_LO)[c + 1] - lo;
   ccol(w, CC_NRUNS)[c] = nr;
   uint32_t dsblk = 0;
   if (nr) {
     ccol(w, CC_FIRST_RUN)[c] = lo;
     dsblk = vu_size(w.cl_vals[c]) + vu_size(nr) + (w.r_pos[lo + nr] - w.r_pos[lo]);
-    atomicAdd(&w.ctr->pad[1], 1u);  // ds clients
   }
   ccol(w, CC_DSBLK)[c] = dsblk;
   ccol(w, CC_SV)[c] = state ? vu_size(w.cl_vals[c]) + vu_size(state) : 0;
-  if (state) atomicAdd(&w.ctr->pad[2], 1u);  // sv entries
+  wave_count_add(&w.ctr->pad[0], incl);        // included clients
+  wave_count_add(&w.ctr->pad[1], nr != 0);     // ds clients
+  wave_count_add(&w.ctr->pad[2], state != 0);  // sv entries
 }
 
 // reverse a per-client column so that an ascending scan yields descending-client positions
@@ -319,6 +327,7 @@ void launch_encode_sizes(const Work& w, uint32_t nsegs, uint32_t nclients, hipSt
   if (nsegs) hipLaunchKernelGGL(k_run_fill, dim3((nsegs + 255) / 256), dim3(256), 0, s, w, nsegs);
   hipLaunchKernelGGL(k_run_sizes, dim3(grid), dim3(256), 0, s, w, nsegs);
   scan_u32(w.tmp, w.tmp_bytes, w.r_size, w.r_pos, nsegs + 1, s);
+  hipLaunchKernelGGL(k_client_bounds, dim3(grid), dim3(256), 0, s, w, nclients, nsegs);
   hipLaunchKernelGGL(k_client_sizes, dim3(nclients / 256 + 1), dim3(256), 0, s, w, nclients, nsegs);
   rev_scan(w, nclients, CC_BLK, CC_BLKPOS, s);
   rev_scan(w, nclients, CC_DSBLK, CC_DSPOS, s);

@@ -328,9 +328,9 @@ __global__ void k_blk_sizes(Work w, uint32_t nblk) {
   if (n) {
     const uint32_t e0 = w.lz_evbase[b];
     sz = vu_size(n) + vu_size(blk_client(w, b)) + vu_size(w.ev_clock[e0]) + (w.ev_pos[e0 + n] - w.ev_pos[e0]);
-    atomicAdd(&w.ctr->pad[0], 1u);
   }
   w.blk_size[b] = sz;
+  wave_count_add(&w.ctr->pad[0], n != 0);
 }
 __global__ __launch_bounds__(256) void k_ev_write(Work w, uint32_t nslots) {
   const uint32_t e = blockIdx.x * blockDim.x + threadIdx.x;

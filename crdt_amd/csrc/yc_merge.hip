@@ -301,12 +301,16 @@ __global__ void k_seg_kind(Work w, uint32_t nsegs) {
   const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
   if (s >= nsegs) return;
   const uint32_t f = w.g_flags[s];
-  if (!(f & SEG_ITEM)) return;
-  const uint32_t key = w.g_key[s];
-  if (key == NONE) { raise_err(&w.ctr->err, ERR_DECODE); return; }  // origin chain without a root
-  const bool arr = !(w.k_flags[key] & KF_PSUB);
-  w.g_flags[s] = f | (arr ? SEG_ARRAY : SEG_PSUB);
-  if (arr) atomicAdd(&w.ctr->narray, 1u);
+  bool arr = false;
+  if (f & SEG_ITEM) {
+    const uint32_t key = w.g_key[s];
+    if (key == NONE) raise_err(&w.ctr->err, ERR_DECODE);  // origin chain without a root
+    else {
+      arr = !(w.k_flags[key] & KF_PSUB);
+      w.g_flags[s] = f | (arr ? SEG_ARRAY : SEG_PSUB);
+    }
+  }
+  wave_count_add(&w.ctr->narray, arr);
 }
 
 // One pass instead of host-driven pointer-jumping rounds: every unresolved item climbs its origin

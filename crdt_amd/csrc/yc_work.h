@@ -277,7 +277,7 @@ __device__ inline bool content_slice(const Work& w, uint32_t src, uint32_t e0, u
 // per-client scratch arrays inside Work::cc
 enum : uint32_t {
   CC_FIRST_OUT = 0, CC_FIRST_INCL, CC_NINCL, CC_HDR, CC_BLK, CC_BLKPOS, CC_NRUNS, CC_FIRST_RUN,
-  CC_DSBLK, CC_DSPOS, CC_SV, CC_SVPOS, CC_REV, CC_REVSCAN, CC_N
+  CC_DSBLK, CC_DSPOS, CC_SV, CC_SVPOS, CC_REV, CC_REVSCAN, CC_RUN_LO, CC_N
 };
 
 // segment flags
