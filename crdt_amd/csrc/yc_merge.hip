@@ -23,7 +23,7 @@
 
 namespace yc {
 
-constexpr uint32_t OWNER_UNITS_PER_LANE = 16;
+constexpr uint32_t OWNER_UNITS_PER_LANE = 2;
 
 __device__ __forceinline__ uint32_t seg_of(const uint64_t* __restrict__ cut, const uint32_t* __restrict__ wpre, uint32_t g) {
   return wpre[g >> 6] + (uint32_t)__popcll(cut[g >> 6] & ((2ull << (g & 63)) - 1)) - 1;
