@@ -229,17 +229,20 @@ __global__ void k_client_sizes(Work w, uint32_t nclients, uint32_t nsegs) {
   wave_count_add(&w.ctr->pad[2], state != 0);  // sv entries
 }
 
-// reverse a per-client column so that an ascending scan yields descending-client positions
-__global__ void k_reverse(Work w, uint32_t nclients, uint32_t col) {
+// reverse the three per-client size columns (structs, delete set, state vector) so that ascending
+// scans yield descending-client positions; one launch each way for all three
+__global__ void k_reverse3(Work w, uint32_t nclients) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i > nclients) return;
-  ccol(w, CC_REV)[i] = i < nclients ? ccol(w, col)[nclients - 1 - i] : 0;
+  const uint32_t src[3] = {CC_BLK, CC_DSBLK, CC_SV}, dst[3] = {CC_REV, CC_REV2, CC_REV3};
+  for (int k = 0; k < 3; ++k) ccol(w, dst[k])[i] = i < nclients ? ccol(w, src[k])[nclients - 1 - i] : 0;
 }
-__global__ void k_unreverse(Work w, uint32_t nclients, uint32_t col) {
+__global__ void k_unreverse3(Work w, uint32_t nclients) {
   const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
   if (c > nclients) return;
   // position of client c = sum of blocks of clients > c = scan[nclients-1-c]; total at [nclients]
-  ccol(w, col)[c] = c < nclients ? ccol(w, CC_REVSCAN)[nclients - 1 - c] : ccol(w, CC_REVSCAN)[nclients];
+  const uint32_t src[3] = {CC_REVSCAN, CC_REVSCAN2, CC_REVSCAN3}, dst[3] = {CC_BLKPOS, CC_DSPOS, CC_SVPOS};
+  for (int k = 0; k < 3; ++k) ccol(w, dst[k])[c] = ccol(w, src[k])[c < nclients ? nclients - 1 - c : nclients];
 }
 
 __global__ void k_totals(Work w, uint32_t nclients) {
@@ -305,19 +308,20 @@ __global__ void k_write_runs(Work w, uint32_t nsegs) {
   wr_vu(w.out, p, w.r_len[r]);
 }
 
-static void rev_scan(const Work& w, uint32_t nclients, uint32_t col_in, uint32_t col_out, hipStream_t s) {
+static void rev_scans(const Work& w, uint32_t nclients, hipStream_t s) {
   const uint32_t grid = nclients / 256 + 1;
-  hipLaunchKernelGGL(k_reverse, dim3(grid), dim3(256), 0, s, w, nclients, col_in);
-  scan_u32(w.tmp, w.tmp_bytes, w.cc + (size_t)CC_REV * (w.cap_clients + 1), w.cc + (size_t)CC_REVSCAN * (w.cap_clients + 1),
-           nclients + 1, s);
-  hipLaunchKernelGGL(k_unreverse, dim3(grid), dim3(256), 0, s, w, nclients, col_out);
+  hipLaunchKernelGGL(k_reverse3, dim3(grid), dim3(256), 0, s, w, nclients);
+  const uint32_t cols[3][2] = {{CC_REV, CC_REVSCAN}, {CC_REV2, CC_REVSCAN2}, {CC_REV3, CC_REVSCAN3}};
+  for (auto& c : cols)
+    scan_u32(w.tmp, w.tmp_bytes, w.cc + (size_t)c[0] * (w.cap_clients + 1), w.cc + (size_t)c[1] * (w.cap_clients + 1),
+             nclients + 1, s);
+  hipLaunchKernelGGL(k_unreverse3, dim3(grid), dim3(256), 0, s, w, nclients);
 }
 
 // Phase 1: sizes + layout (ends with out_bytes / sv_bytes in the counters). No host sync: the
 // output / run counts are read on the device, grids and scans are sized for NS + 1 entries.
 void launch_encode_sizes(const Work& w, uint32_t nsegs, uint32_t nclients, hipStream_t s) {
-  hipMemsetAsync(w.ctr->pad, 0, sizeof(uint32_t) * 8, s);
-  hipMemsetAsync(w.cc + (size_t)CC_NRUNS * (w.cap_clients + 1), 0, sizeof(uint32_t) * (w.cap_clients + 1), s);
+  fill_u32_multi({{w.ctr->pad, 8, 0u}, {w.cc + (size_t)CC_NRUNS * (w.cap_clients + 1), (uint64_t)w.cap_clients + 1, 0u}}, s);
   const uint32_t grid = nsegs / 256 + 1;
   hipLaunchKernelGGL(k_out_sizes, dim3(grid), dim3(256), 0, s, w, nsegs, nclients);
   scan_u32(w.tmp, w.tmp_bytes, w.o_size, w.o_pos, nsegs + 1, s);
@@ -329,9 +333,7 @@ void launch_encode_sizes(const Work& w, uint32_t nsegs, uint32_t nclients, hipSt
   scan_u32(w.tmp, w.tmp_bytes, w.r_size, w.r_pos, nsegs + 1, s);
   hipLaunchKernelGGL(k_client_bounds, dim3(grid), dim3(256), 0, s, w, nclients, nsegs);
   hipLaunchKernelGGL(k_client_sizes, dim3(nclients / 256 + 1), dim3(256), 0, s, w, nclients, nsegs);
-  rev_scan(w, nclients, CC_BLK, CC_BLKPOS, s);
-  rev_scan(w, nclients, CC_DSBLK, CC_DSPOS, s);
-  rev_scan(w, nclients, CC_SV, CC_SVPOS, s);
+  rev_scans(w, nclients, s);
   hipLaunchKernelGGL(k_totals, dim3(1), dim3(1), 0, s, w, nclients);
 }
 

@@ -347,9 +347,10 @@ int run_decode(ycrdt_engine* e, ycrdt_batch* b, bool lazy, Decoded& D) {
     w.tmp_bytes = V[B_TMP].cap;
   }
   if (!ok) return fail(YCRDT_E_DEVICE, "hipMalloc failed (scan scratch)");
-  HIPCHK(hipMemsetAsync(w.ctr, 0, sizeof(Counters), s));
-  HIPCHK(hipMemsetAsync(w.final_bits, 0, nwords * 8, s));
-  HIPCHK(hipMemsetAsync(w.sec_bits, 0, nwords * 8, s));
+  static_assert(sizeof(Counters) % 4 == 0, "counters are filled as words");
+  fill_u32_multi({{(uint32_t*)w.ctr, sizeof(Counters) / 4, 0u},
+                  {(uint32_t*)w.final_bits, (uint64_t)nwords * 2, 0u},
+                  {(uint32_t*)w.sec_bits, (uint64_t)nwords * 2, 0u}}, s);
   // ---- K1 decode
   mark(e, "decode.parse");
   static const bool dbg_tables = getenv("YCRDT_DEBUG_TABLES") && getenv("YCRDT_DEBUG_TABLES")[0] == '1';

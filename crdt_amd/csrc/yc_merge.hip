@@ -163,9 +163,7 @@ __global__ void k_scatter_seg(Work w, uint32_t nwords, uint64_t nunits) {
 }
 
 void launch_units(const Work& w, uint32_t nstructs, uint32_t nclients, uint32_t nds, uint64_t nunits, hipStream_t s) {
-  hipMemsetAsync(w.u_owner, 0xFF, sizeof(uint32_t) * nunits, s);
-  hipMemsetAsync(w.u_flags, 0, sizeof(uint32_t) * nunits, s);
-  hipMemsetAsync(w.u_minchild, 0xFF, sizeof(uint32_t) * nunits, s);
+  fill_u32_multi({{w.u_owner, nunits, NONE}, {w.u_flags, nunits, 0u}, {w.u_minchild, nunits, NONE}}, s);
   // the unit counts these kernels cover (Σ input lengths, Σ delete-set lengths) are read on the
   // device; the grids are sized for one pass over the merged store and stride beyond it
   const uint32_t grid = (uint32_t)std::min<uint64_t>(nunits / (OWNER_UNITS_PER_LANE * 256) + 1, 8192);
@@ -287,11 +285,11 @@ __global__ __launch_bounds__(256) void k_seg_props(Work w, uint32_t nsegs) {
 }
 
 void launch_segment_props(const Work& w, uint32_t nsegs, uint32_t nclients, uint64_t nunits, hipStream_t s) {
-  hipMemsetAsync(w.k_hash, 0, sizeof(uint64_t) * w.cap_keys, s);
-  hipMemsetAsync(w.k_rootmax, 0, sizeof(uint64_t) * w.cap_keys, s);
-  hipMemsetAsync(w.k_flags, 0, sizeof(uint32_t) * w.cap_keys, s);
-  hipMemsetAsync(w.k_parent, 0xFF, sizeof(uint32_t) * w.cap_keys, s);
-  hipMemsetAsync(w.g_maxchild, 0, sizeof(uint64_t) * nsegs, s);
+  fill_u32_multi({{(uint32_t*)w.k_hash, (uint64_t)w.cap_keys * 2, 0u},
+                  {(uint32_t*)w.k_rootmax, (uint64_t)w.cap_keys * 2, 0u},
+                  {w.k_flags, w.cap_keys, 0u},
+                  {w.k_parent, w.cap_keys, NONE},
+                  {(uint32_t*)w.g_maxchild, (uint64_t)nsegs * 2, 0u}}, s);
   if (nsegs) hipLaunchKernelGGL(k_seg_props, dim3((nsegs + 255) / 256), dim3(256), 0, s, w, nsegs);
 }
 

@@ -1,4 +1,5 @@
 // yc_prims.hip — device-wide scan / sort primitives (rocPRIM) used between the engine's kernels.
+#include <algorithm>
 #include <cstring>
 #include <cstdlib>
 #include <rocprim/rocprim.hpp>
@@ -11,6 +12,31 @@ struct SegMax64 {  // max of packed (segment << 32 | value) within a segment; a 
     return (a >> 32) == (b >> 32) ? (a > b ? a : b) : b;
   }
 };
+
+// several u32 fills in one launch (blockIdx.y = fill): each hipMemsetAsync is its own ~4.5 us
+// dispatch, and a merge issues a dozen of them
+__global__ void k_fill_multi(FillBatch b) {
+  const FillDesc d = b.d[blockIdx.y];
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < d.n; i += (uint64_t)gridDim.x * blockDim.x)
+    d.p[i] = d.v;
+}
+
+void fill_u32_multi(std::initializer_list<FillDesc> fills, hipStream_t s) {
+  FillBatch b{};
+  uint64_t nmax = 0;
+  for (const FillDesc& f : fills) {
+    if (!f.n) continue;
+    if (b.count == FILL_MAX) {  // more than one batch: flush
+      hipLaunchKernelGGL(k_fill_multi, dim3((uint32_t)std::min<uint64_t>(nmax / 256 + 1, 2048), b.count), dim3(256), 0, s, b);
+      b.count = 0;
+      nmax = 0;
+    }
+    b.d[b.count++] = f;
+    nmax = std::max(nmax, f.n);
+  }
+  if (b.count)
+    hipLaunchKernelGGL(k_fill_multi, dim3((uint32_t)std::min<uint64_t>(nmax / 256 + 1, 2048), b.count), dim3(256), 0, s, b);
+}
 
 size_t prim_tmp_bytes(uint64_t n) {
   size_t a = 0, b = 0, c = 0;

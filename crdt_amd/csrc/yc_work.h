@@ -4,6 +4,7 @@
 // merge path). Naming: B = batch bytes, G = decode groups, S = decoded structs, NC = clients,
 // U = units (one per (client, clock) in the merged store), NS = segments, NO = output structs.
 #pragma once
+#include <initializer_list>
 #include "yc_common.h"
 #include "yc_view.h"
 
@@ -277,7 +278,7 @@ __device__ inline bool content_slice(const Work& w, uint32_t src, uint32_t e0, u
 // per-client scratch arrays inside Work::cc
 enum : uint32_t {
   CC_FIRST_OUT = 0, CC_FIRST_INCL, CC_NINCL, CC_HDR, CC_BLK, CC_BLKPOS, CC_NRUNS, CC_FIRST_RUN,
-  CC_DSBLK, CC_DSPOS, CC_SV, CC_SVPOS, CC_REV, CC_REVSCAN, CC_RUN_LO, CC_N
+  CC_DSBLK, CC_DSPOS, CC_SV, CC_SVPOS, CC_REV, CC_REVSCAN, CC_RUN_LO, CC_REV2, CC_REVSCAN2, CC_REV3, CC_REVSCAN3, CC_N
 };
 
 // segment flags
@@ -347,6 +348,11 @@ size_t prim_tmp_bytes(uint64_t max_items);
 void scan_u32(void* tmp, size_t tmpb, const uint32_t* in, uint32_t* out, uint64_t n, hipStream_t s);          // exclusive
 void scan_u32_to_u64(void* tmp, size_t tmpb, const uint32_t* in, uint64_t* out, uint64_t n, hipStream_t s);   // exclusive
 void sort_u32(void* tmp, size_t tmpb, const uint32_t* in, uint32_t* out, uint64_t n, hipStream_t s);
+// batched u32 fills (n in 32-bit words)
+struct FillDesc { uint32_t* p; uint64_t n; uint32_t v; };
+constexpr uint32_t FILL_MAX = 8;
+struct FillBatch { FillDesc d[FILL_MAX]; uint32_t count; };
+void fill_u32_multi(std::initializer_list<FillDesc> fills, hipStream_t s);
 void sort_pairs_u32(void* tmp, size_t tmpb, const uint32_t* kin, uint32_t* kout, const uint32_t* vin, uint32_t* vout,
                     uint64_t n, hipStream_t s);
 void sort_pairs_u64_u32(void* tmp, size_t tmpb, const uint64_t* kin, uint64_t* kout, const uint32_t* vin, uint32_t* vout,
