@@ -281,7 +281,7 @@ void map_json(JsonCtx& c, uint32_t parent_unit, std::string& o) {
   if (it != v.by_parent.end()) {
     for (uint32_t ki : it->second) {
       const ViewKey& K = v.keys[ki];
-      if (!(K.flags & VK_PSUB) || K.win.client == VNONE || (K.win.flags & VS_DELETED) || !(K.win.flags & VS_ITEM)) continue;
+      if (!(K.flags & VK_PSUB) || !(K.win.flags & VS_SET) || (K.win.flags & VS_DELETED) || !(K.win.flags & VS_ITEM)) continue;
       std::vector<std::pair<bool, std::string>> el;
       seg_elements(c, K.win, el, true);
       if (el.empty() || !el.back().first) continue;
@@ -353,7 +353,14 @@ void w_str(std::vector<uint8_t>& o, const std::string& s) {
   o.insert(o.end(), s.begin(), s.end());
 }
 
-struct Id { uint32_t client = VNONE, clock = 0; bool some() const { return client != VNONE; } };
+// an item id; `set` marks presence (client ids use all 32 bits: 0xFFFFFFFF is a valid client)
+struct Id {
+  uint32_t client = 0, clock = 0;
+  bool set = false;
+  Id() = default;
+  Id(uint32_t c, uint32_t k) : client(c), clock(k), set(true) {}
+  bool some() const { return set; }
+};
 
 // Parent of the op's target type: root name, or the type item stored under root map `key`
 struct ParentRef {
@@ -365,7 +372,7 @@ struct ParentRef {
 int resolve_parent(const HostView& v, const OpTarget& t, uint32_t want_type, ParentRef& pr, std::string& err) {
   if (!t.nested) { pr.root = true; pr.unit = VNONE; return YCRDT_OK; }
   const ViewKey* e = v.root_list(t.root, &t.key);
-  if (!e || e->win.client == VNONE || (e->win.flags & VS_DELETED) || e->win.ref != R_TYPE) {
+  if (!e || !(e->win.flags & VS_SET) || (e->win.flags & VS_DELETED) || e->win.ref != R_TYPE) {
     err = "no shared type at " + t.root + "." + t.key;
     return YCRDT_E_ARG;
   }
@@ -467,7 +474,7 @@ const ViewKey* HostView::child_list(uint32_t unit, const std::string* psub) cons
 
 int view_type_at(const HostView& v, const std::string& root, const std::string& key) {
   const ViewKey* e = v.root_list(root, &key);
-  if (!e || e->win.client == VNONE || (e->win.flags & VS_DELETED) || e->win.ref != R_TYPE) return -1;
+  if (!e || !(e->win.flags & VS_SET) || (e->win.flags & VS_DELETED) || e->win.ref != R_TYPE) return -1;
   Rd r{v.bytes.data(), e->win.b0, e->win.b1};
   const uint32_t tr = r.vu();
   return r.ok ? (int)tr : -1;
@@ -487,7 +494,7 @@ bool view_root_json(const HostView& v, const std::string& name, int kind, std::s
         if (!(K.flags & VK_PSUB) || K.name_len != name.size() ||
             memcmp(v.bytes.data() + K.name_pos, name.data(), name.size()) != 0)
           continue;
-        if (K.win.client == VNONE || (K.win.flags & VS_DELETED) || !(K.win.flags & VS_ITEM)) continue;
+        if (!(K.win.flags & VS_SET) || (K.win.flags & VS_DELETED) || !(K.win.flags & VS_ITEM)) continue;
         std::vector<std::pair<bool, std::string>> el;
         seg_elements(c, K.win, el, true);
         if (el.empty() || !el.back().first) continue;
@@ -519,7 +526,7 @@ int encode_map_set(const HostView& v, const OpTarget& t, const std::string& key,
   // typeMapSet: left = parent._map.get(key) (the entry's rightmost item, deleted or not)
   const ViewKey* e = target_list(v, t, pr, &key);
   Id origin;
-  if (e && e->win.client != VNONE) origin = {e->win.client, e->win.clock + e->win.len - 1};
+  if (e && (e->win.flags & VS_SET)) origin = {e->win.client, e->win.clock + e->win.len - 1};
   write_item_update(out, client, clock, content_ref, origin, Id{}, t, pr, &key, content, content_len);
   return YCRDT_OK;
 }
@@ -530,7 +537,7 @@ int encode_map_delete(const HostView& v, const OpTarget& t, const std::string& k
   int rc = resolve_parent(v, t, 1, pr, err);
   if (rc) return rc;
   const ViewKey* e = target_list(v, t, pr, &key);
-  nothing = !e || e->win.client == VNONE || (e->win.flags & VS_DELETED);
+  nothing = !e || !(e->win.flags & VS_SET) || (e->win.flags & VS_DELETED);
   if (nothing) return YCRDT_OK;
   write_ds_update(out, {{e->win.client, e->win.clock, e->win.len}});
   return YCRDT_OK;

@@ -5,7 +5,9 @@
 
 namespace yc {
 
-enum : uint32_t { VS_DELETED = 1u, VS_COUNTABLE = 2u, VS_ITEM = 4u };
+// VS_SET: the record holds a struct (client ids use all 32 bits, so no client value can mark
+// an empty record)
+enum : uint32_t { VS_DELETED = 1u, VS_COUNTABLE = 2u, VS_ITEM = 4u, VS_SET = 8u };
 constexpr uint32_t VK_PSUB = 1u;    // ViewKey::flags: a YMap entry
 constexpr uint32_t VNONE = 0xFFFFFFFFu;
 struct ViewSeg {             // one item run of a list (or a YMap entry's value: its last element)
@@ -21,7 +23,7 @@ struct ViewKey {             // one live list: a YMap entry (KF_PSUB) or a YArra
   uint32_t name_pos, name_len;   // root type name (root lists)
   uint32_t psub_pos, psub_len;   // YMap entry key
   uint32_t seg0, nseg;       // YArray: members in document order, ViewSeg [seg0, seg0 + nseg)
-  ViewSeg win;               // YMap entry: the winning item's value (client NONE = none)
+  ViewSeg win;               // YMap entry: the winning item's value (flags without VS_SET = none)
 };
 
 }  // namespace yc

@@ -34,7 +34,7 @@ __device__ void fill_seg(const Work& w, uint32_t s, bool last_only, ViewSeg& v) 
   v.len = g1 - g0;
   v.unit = g0;
   v.ref = ref;
-  v.flags = ((f & SEG_DEL) ? VS_DELETED : 0u) | (countable_ref(ref) ? VS_COUNTABLE : 0u) | ((f & SEG_ITEM) ? VS_ITEM : 0u);
+  v.flags = VS_SET | ((f & SEG_DEL) ? VS_DELETED : 0u) | (countable_ref(ref) ? VS_COUNTABLE : 0u) | ((f & SEG_ITEM) ? VS_ITEM : 0u);
   v.b0 = v.b1 = 0;
   if ((f & SEG_DEL) || !(f & SEG_ITEM)) return;
   const uint32_t e1 = clock + v.len - w.s_clock[own];
