@@ -20,6 +20,15 @@ __device__ __forceinline__ uint32_t unit_client(const Work& w, uint32_t nclients
   return lo;
 }
 
+// client of unit g, trying the likely candidates first (the segment's own client: an origin inside
+// a split struct; the source struct's origin / right-origin client) before the binary search,
+// which costs ~10 dependent loads per call
+__device__ __forceinline__ uint32_t unit_client_hint(const Work& w, uint32_t nclients, uint32_t g, uint32_t c0, uint32_t c1) {
+  if (c0 < nclients && g >= w.cl_base[c0] && g < w.cl_base[c0 + 1]) return c0;
+  if (c1 < nclients && g >= w.cl_base[c1] && g < w.cl_base[c1 + 1]) return c1;
+  return unit_client(w, nclients, g);
+}
+
 __device__ __forceinline__ uint32_t copy_bytes(uint8_t* __restrict__ o, uint32_t p, const uint8_t* __restrict__ src, uint32_t n) {
   for (uint32_t i = 0; i < n; ++i) o[p + i] = src[i];
   return p + n;
@@ -51,7 +60,7 @@ __device__ uint32_t encode_struct(const Work& w, uint32_t nclients, uint32_t o, 
   if (off > 0) { has_o = true; oclient = w.cl_vals[cidx]; oclock = k0 + off - 1; }
   else if (w.g_origin[a] != NONE) {
     const uint32_t g = w.g_origin[a];
-    const uint32_t c = unit_client(w, nclients, g);
+    const uint32_t c = unit_client_hint(w, nclients, g, cidx, w.s_ocidx[src]);
     has_o = true;
     oclient = w.cl_vals[c];
     oclock = (uint32_t)(g - w.cl_base[c]);
@@ -60,7 +69,7 @@ __device__ uint32_t encode_struct(const Work& w, uint32_t nclients, uint32_t o, 
   uint32_t rclient = 0, rclock = 0;
   if (w.g_rorigin[a] != NONE) {
     const uint32_t g = w.g_rorigin[a];
-    const uint32_t c = unit_client(w, nclients, g);
+    const uint32_t c = unit_client_hint(w, nclients, g, w.s_rcidx[src], cidx);
     has_r = true;
     rclient = w.cl_vals[c];
     rclock = (uint32_t)(g - w.cl_base[c]);
