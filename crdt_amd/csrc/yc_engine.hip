@@ -543,7 +543,7 @@ int run_merge(ycrdt_engine* e, ycrdt_batch* b, const std::unordered_map<uint32_t
       HIPCHK(hipMemcpyAsync(&narray, &w.ctr->narray, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
       HIPCHK(hipStreamSynchronize(s));
     }
-    e->nlists = launch_yata(w, nsegs, narray, s);
+    e->nlists = launch_yata(w, nsegs, narray, nclients, s);
     if (w.dbg && e->nlists) {
       unsigned long long h[3];
       HIPCHK(hipStreamSynchronize(s));

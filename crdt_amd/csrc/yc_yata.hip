@@ -12,6 +12,8 @@
 // A segment is a run of consecutive units of one client cut at every referenced unit, so the
 // loop's verdict on the first unit of a run holds for the whole run (SURVEY §7 hard part 1,
 // per-clock restatement) and the loop can step over segments instead of units.
+#include <cstdlib>
+
 #include "yc_work.h"
 
 namespace yc {
@@ -47,10 +49,11 @@ __global__ void k_ylist_starts(Work w, uint32_t nsegs) {
 }
 
 // One wavefront per list; lane 0 runs the sequential loop (the lists of a batch run in parallel).
-__global__ __launch_bounds__(64) void k_yata(Work w, uint32_t nlists) {
+__global__ __launch_bounds__(64) void k_yata(Work w, uint32_t nlists, uint32_t nmin) {
   const uint32_t l = blockIdx.x;
   if (l >= nlists || threadIdx.x != 0) return;
   const uint32_t a = w.y_lstart[l], b = w.y_lstart[l + 1];
+  if (b - a < nmin) return;  // integrated in LDS by k_yata_lds
   const uint32_t key = w.y_keys[a];
   uint32_t* __restrict__ right = w.g_right;
   uint32_t* __restrict__ state = w.y_state;   // 0 = pending, 1 = on the stack, 2 = integrated
@@ -124,12 +127,128 @@ __global__ __launch_bounds__(64) void k_yata(Work w, uint32_t nlists) {
   }
 }
 
+// ---- LDS-resident YATA for lists of at most CAP segments: the same loop over list-local u16
+// indices, every array it touches staged in LDS (12 bytes per segment), so each conflict-scan step
+// waits on LDS instead of on L2 (~470 ns per step for the global kernel on a 13 K-segment list).
+//   lo / lr   local index of the origin / right-origin segment (L_NONE: none, L_OUT: outside the
+//             list — an error once it is needed). Origin units are the last unit of their segment
+//             and right-origin units the first (k_refs cuts there), so comparing segments is
+//             comparing the units the global kernel compares.
+//   rt        right neighbour; cs = client index (14 bits) | state << 14 (0 pending, 1 on the
+//             stack, 2 integrated) — the four u16 of a segment are one 8-byte record, so a scan
+//             step is one LDS read (the next record is fetched while this one is examined);
+//             bf / cf the itemsBeforeOrigin / conflictingItems stamps (u16 pair, all cleared when
+//             the counter could wrap inside the next integration).
+// The dependency stack lives in global memory (y_stack); lists longer than CAP, or batches with
+// 16 K clients or more, take k_yata.
+constexpr uint32_t L_NONE = 0xFFFFu, L_OUT = 0xFFFEu;
+constexpr uint32_t YL_SMALL = 1024, YL_LARGE = 13312;  // 12 B x 13312 = 156 KiB of LDS
+
+__device__ __forceinline__ uint32_t local_of(const Work& w, uint32_t a, uint32_t n, uint32_t g) {
+  uint32_t lo = 0, hi = n;  // y_seg[a, a + n) is sorted (stable sort of the identity)
+  while (lo < hi) { const uint32_t m = (lo + hi) >> 1; if (w.y_seg[a + m] < g) lo = m + 1; else hi = m; }
+  return lo < n && w.y_seg[a + lo] == g ? lo : L_OUT;
+}
+
+struct __attribute__((aligned(8))) YRec { uint16_t lo, lr, rt, cs; };  // one ds_read_b64 per scan step
+struct __attribute__((aligned(4))) YStamp { uint16_t bf, cf; };
+
+template <uint32_t CAP>
+__global__ void k_yata_lds(Work w, uint32_t nlists, uint32_t nmin) {
+  const uint32_t l = blockIdx.x;
+  if (l >= nlists) return;
+  const uint32_t a = w.y_lstart[l], n = w.y_lstart[l + 1] - a;
+  if (n < nmin || n > CAP) return;
+  __shared__ YRec rec[CAP];
+  __shared__ YStamp stp[CAP];
+  for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) {
+    const uint32_t g = w.y_seg[a + i];
+    const uint32_t oU = w.g_origin[g], rU = w.g_rorigin[g];
+    YRec r;
+    r.lo = (uint16_t)(oU == NONE ? L_NONE : local_of(w, a, n, seg_of_unit(w, oU)));
+    r.lr = (uint16_t)(rU == NONE ? L_NONE : local_of(w, a, n, seg_of_unit(w, rU)));
+    r.rt = (uint16_t)L_NONE;
+    r.cs = (uint16_t)w.g_cidx[g];
+    rec[i] = r;
+    stp[i] = YStamp{0, 0};
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t* __restrict__ stack = w.y_stack + a;
+    uint32_t head = L_NONE, ctr = 0;
+    const uint32_t wrap = 0xFFFFu - n - 3;  // an integration issues at most n + 2 stamps
+    auto st = [&](uint32_t i) { return (uint32_t)rec[i].cs >> 14; };
+    auto set_st = [&](uint32_t i, uint32_t v) { rec[i].cs = (uint16_t)((rec[i].cs & 0x3FFFu) | (v << 14)); };
+    for (uint32_t i0 = 0; i0 < n; ++i0) {
+      if (st(i0) == 2) continue;
+      uint32_t sp = 0;
+      stack[sp++] = i0;
+      set_st(i0, 1);
+      while (sp > 0) {
+        const uint32_t t = stack[sp - 1];
+        const YRec T = rec[t];
+        const uint32_t os = T.lo, rs = T.lr;
+        uint32_t dep = L_NONE;
+        if (os != L_NONE && (os == L_OUT || st(os) != 2)) dep = os;
+        else if (rs != L_NONE && (rs == L_OUT || st(rs) != 2)) dep = rs;
+        if (dep != L_NONE) {
+          if (dep == L_OUT || st(dep) == 1 || sp >= n) { raise_err(&w.ctr->err, ERR_DECODE); return; }
+          set_st(dep, 1);
+          stack[sp++] = dep;
+          continue;
+        }
+        if (ctr > wrap) {  // clear the stamps before the counter can wrap
+          for (uint32_t k = 0; k < n; ++k) stp[k] = YStamp{0, 0};
+          ctr = 0;
+        }
+        uint32_t left = os;
+        const uint32_t ct = T.cs & 0x3FFFu;
+        uint32_t o = left != L_NONE ? rec[left].rt : head;
+        if (o != rs) {
+          const uint32_t iter = ++ctr;
+          uint32_t ep = ++ctr;
+          YRec R = o != L_NONE ? rec[o] : YRec{0, 0, 0, 0};
+          while (o != L_NONE && o != rs) {
+            stp[o] = YStamp{(uint16_t)iter, (uint16_t)ep};
+            const uint32_t next = R.rt;
+            const YRec RN = next != L_NONE ? rec[next] : YRec{0, 0, 0, 0};  // prefetch the next step
+            const uint32_t oo = R.lo;
+            if (oo == os) {
+              if ((R.cs & 0x3FFFu) < ct) { left = o; ep = ++ctr; }
+              else if (R.lr == rs) break;
+            } else if (oo != L_NONE && oo != L_OUT) {
+              const YStamp S = stp[oo];
+              if (S.bf != iter) break;
+              if (S.cf != ep) { left = o; ep = ++ctr; }
+            } else {
+              break;
+            }
+            o = next;
+            R = RN;
+          }
+        }
+        uint32_t r2;
+        if (left != L_NONE) { r2 = rec[left].rt; rec[left].rt = (uint16_t)t; }
+        else { r2 = head; head = t; }
+        rec[t].rt = (uint16_t)r2;
+        set_st(t, 2);
+        --sp;
+      }
+    }
+  }
+  __syncthreads();
+  for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) {
+    const uint32_t r = rec[i].rt;
+    w.g_right[w.y_seg[a + i]] = r == L_NONE ? NONE : w.y_seg[a + r];
+  }
+}
+
 __global__ void k_ynone(Work w, uint32_t nsegs) {  // no array lists: every right neighbour is NONE
   const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
   if (s < nsegs) w.g_right[s] = NONE;
 }
 
-uint32_t launch_yata(const Work& w, uint32_t nsegs, uint32_t narray, hipStream_t s) {
+uint32_t launch_yata(const Work& w, uint32_t nsegs, uint32_t narray, uint32_t nclients, hipStream_t s) {
   if (!nsegs) return 0;
   const uint32_t grid = nsegs / 256 + 1;
   if (!narray) { hipLaunchKernelGGL(k_ynone, dim3(grid), dim3(256), 0, s, w, nsegs); return 0; }
@@ -144,7 +263,13 @@ uint32_t launch_yata(const Work& w, uint32_t nsegs, uint32_t narray, hipStream_t
   hipLaunchKernelGGL(k_ylist_starts, dim3(grid), dim3(256), 0, s, w, nsegs);
   hipMemsetAsync(w.y_before, 0, sizeof(uint32_t) * (nsegs + 1), s);  // stamps: 0 is never issued
   hipMemsetAsync(w.y_confl, 0, sizeof(uint32_t) * (nsegs + 1), s);
-  hipLaunchKernelGGL(k_yata, dim3(nlists), dim3(64), 0, s, w, nlists);
+  if (nclients < 16384 && !getenv("YCRDT_YATA_GLOBAL")) {  // client index in 14 bits
+    hipLaunchKernelGGL(k_yata_lds<YL_SMALL>, dim3(nlists), dim3(64), 0, s, w, nlists, 1u);
+    hipLaunchKernelGGL(k_yata_lds<YL_LARGE>, dim3(nlists), dim3(256), 0, s, w, nlists, YL_SMALL + 1);
+    hipLaunchKernelGGL(k_yata, dim3(nlists), dim3(64), 0, s, w, nlists, YL_LARGE + 1);
+  } else {
+    hipLaunchKernelGGL(k_yata, dim3(nlists), dim3(64), 0, s, w, nlists, 0u);
+  }
   return nlists;
 }
 
