@@ -205,7 +205,10 @@ class Doc:
 
     def __del__(self):
         if getattr(self, "_h", None):
-            lib().ycrdt_doc_destroy(self._h)
+            try:
+                lib().ycrdt_doc_destroy(self._h)
+            except Exception:  # interpreter teardown: module globals already cleared
+                pass
             self._h = None
 
     def apply_update(self, update: bytes):
@@ -279,7 +282,10 @@ class Batch:
 
     def __del__(self):
         if getattr(self, "_h", None):
-            lib().ycrdt_batch_destroy(self._h)
+            try:
+                lib().ycrdt_batch_destroy(self._h)
+            except Exception:  # interpreter teardown: module globals already cleared
+                pass
             self._h = None
 
     def merge(self) -> MergeStats:

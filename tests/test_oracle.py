@@ -110,3 +110,25 @@ def test_oracle_local_ops_pinned():
             assert d.encode_state_as_update().hex() == s["state"], (c["name"], i, op)
         assert json.loads(d.root_json("users", "map")) == c["json"]["users"], c["name"]
         assert json.loads(d.root_json("messages", "array")) == c["json"]["messages"], c["name"]
+
+
+def test_oracle_config_fixtures():
+    """Reduced-scale C3 / C4 / C5 cases played through Yjs 13.5.16 (tests/golden/configs.json)."""
+    import json as _json
+    import os as _os
+
+    from oracle.yref import Doc as _Doc
+
+    with open(_os.path.join(_os.path.dirname(__file__), "golden", "configs.json")) as f:
+        cases = _json.load(f)["cases"]
+    for c in cases:
+        d = _Doc(0x7FFFFFF0)
+        for u in c["updates"]:
+            d.apply_update(bytes.fromhex(u))
+        assert d.encode_state_as_update().hex() == c["state"], c["name"]
+        assert d.encode_state_vector().hex() == c["sv"], c["name"]
+        for df in c["diffs"]:
+            assert d.encode_state_as_update(bytes.fromhex(df["sv"])).hex() == df["update"], c["name"]
+        for root, val in c["json"].items():
+            kind = "array" if isinstance(val, list) else "map"
+            assert _json.loads(d.root_json(root, kind)) == val, (c["name"], root)
