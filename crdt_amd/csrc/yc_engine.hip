@@ -251,6 +251,7 @@ struct Decoded {
   uint32_t nstructs = 0, nsections = 0, nclients = 0, nds = 0;
   uint64_t nunits = 0, in_len = 0;
   uint32_t array_roots = 0;  // 1: some item names a parent without a parentSub (a YArray may exist)
+  uint32_t nested = 0;       // 1: some item names a parent item (nested types: dead-type pass needed)
 };
 
 // K1: decode every update of the batch into the struct SoA (+ client table, delete-set ranges).
@@ -425,6 +426,7 @@ int run_decode(ycrdt_engine* e, ycrdt_batch* b, bool lazy, Decoded& D) {
   const uint64_t nunits = lazy ? 0 : c.units;
   D.in_len = c.in_len;
   D.array_roots = c.narray_roots;
+  D.nested = c.nested;
   if (nunits >= 0xF0000000ull) return fail(YCRDT_E_CAPACITY, "more than 2^32 units in one batch");
   D.nstructs = nstructs;
   D.nsections = nsections;
@@ -536,7 +538,7 @@ int run_merge(ycrdt_engine* e, ycrdt_batch* b, const std::unordered_map<uint32_t
     launch_map_winner(w, nsegs, s);
     run_descent(w, nsegs, s);
     mark(e, "merge.dead_types");
-    run_dead_keys(w, nsegs, s);
+    if (D.nested) run_dead_keys(w, nsegs, s);  // only lists under a parent item can die with it
     mark(e, "merge.yata");
     uint32_t narray = 0;  // YArray members; only read when the decode saw a possible array root
     if (D.array_roots) {

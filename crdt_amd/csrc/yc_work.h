@@ -31,6 +31,7 @@ struct Counters {            // device-side counters, read back at the few host 
   uint32_t nruns;            // delete-set runs in the output
   uint32_t narray;           // YArray list members (segments)
   uint32_t narray_roots;     // 1: a decoded item may root a YArray list (parent given, no parentSub)
+  uint32_t nested;           // 1: a decoded item names a parent ITEM (nested types exist)
   uint32_t pad[12];          // encode scratch (see yc_encode.hip)
   unsigned long long items;  // Σ clock lengths of Skip structs (items = Σ all lengths − this)
   unsigned long long units;  // U = cl_base[NC] (copied on the device before a counter read)

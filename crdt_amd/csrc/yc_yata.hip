@@ -243,15 +243,10 @@ __global__ void k_yata_lds(Work w, uint32_t nlists, uint32_t nmin) {
   }
 }
 
-__global__ void k_ynone(Work w, uint32_t nsegs) {  // no array lists: every right neighbour is NONE
-  const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
-  if (s < nsegs) w.g_right[s] = NONE;
-}
-
 uint32_t launch_yata(const Work& w, uint32_t nsegs, uint32_t narray, uint32_t nclients, hipStream_t s) {
   if (!nsegs) return 0;
   const uint32_t grid = nsegs / 256 + 1;
-  if (!narray) { hipLaunchKernelGGL(k_ynone, dim3(grid), dim3(256), 0, s, w, nsegs); return 0; }
+  if (!narray) return 0;  // g_right is only read for YArray members (merge predicate, view)
   hipLaunchKernelGGL(k_ykey, dim3(grid), dim3(256), 0, s, w, nsegs);
   sort_pairs_u32(w.tmp, w.tmp_bytes, w.y_key, w.y_keys, w.y_iota, w.y_seg, nsegs, s);
   hipLaunchKernelGGL(k_ylist_flags, dim3(grid), dim3(256), 0, s, w, nsegs);
