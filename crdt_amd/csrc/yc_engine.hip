@@ -105,6 +105,7 @@ enum Buf {
   B_GRIGHT, B_YKEY, B_YKEYS, B_YSEG, B_YIOTA, B_YLSTART, B_YSTATE, B_YBEFORE, B_YCONFL, B_YSTACK,
   B_OFIRST, B_OCIDX, B_OSIZE, B_OPOS, B_RSEG, B_RLEN, B_RSIZE, B_RPOS, B_OUT, B_SVOUT,
   B_VKMAP, B_VKREP, B_VKEYS, B_VNKEYS, B_VPOS, B_VD0, B_VN0, B_VD1, B_VN1, B_VORDER, B_VSEGS,
+  B_SCRATCH2, B_TMP2,
   B_COUNT
 };
 
@@ -114,6 +115,8 @@ struct ycrdt_engine {
   int device = 0;
   int compat = 136;
   hipStream_t stream = nullptr;
+  hipStream_t side = nullptr;        // delete-set decode overlaps the client table / struct decode
+  hipEvent_t side_done = nullptr;
   std::vector<DevBuf> bufs;
   Work w;
   bool profiling = false;
@@ -413,13 +416,24 @@ int run_decode(ycrdt_engine* e, ycrdt_batch* b, bool lazy, Decoded& D) {
   const uint32_t nstructs = c.nstructs;
   const uint32_t nsections = c.nsections;
   mark(e, "decode.sections");
+  {  // the delete sets decode on the side stream (own scratch / scan space) while the client
+     // table and the struct table are built; both streams only read what the sync above published
+    Work wd = w;
+    bool okd = true;
+    wd.scratch = take<uint32_t>(V, B_SCRATCH2, (uint64_t)w.nupd + 2, okd);
+    wd.tmp = take<uint8_t>(V, B_TMP2, prim_tmp_bytes((uint64_t)w.nupd + 2), okd);
+    wd.tmp_bytes = V[B_TMP2].cap;
+    if (!okd) return fail(YCRDT_E_DEVICE, "hipMalloc failed (delete-set scratch)");
+    launch_ds_decode(wd, e->side);
+    HIPCHK(hipEventRecord(e->side_done, e->side));
+  }
   launch_section_clients(w, nsections, s);
-  launch_ds_decode(w, s);
   if (nsections) launch_client_table(w, nsections, s);
   mark(e, "decode.structs");
   launch_struct_decode(w, nstructs, s);
   HIPCHK(hipMemsetAsync(w.cl_start, 0, sizeof(uint32_t) * (nsections + 1), s));
   if (!lazy) launch_states(w, nstructs, nsections, s);
+  HIPCHK(hipStreamWaitEvent(s, e->side_done, 0));
   rc = check(e, c, "struct decode");
   if (rc) return rc;
   const uint32_t nclients = c.nclients;
@@ -790,6 +804,8 @@ int ycrdt_engine_create(int device, int compat, ycrdt_engine** out) {
   e->compat = compat == 135 ? 135 : 136;
   e->debug_sync = getenv("YCRDT_DEBUG_SYNC") && getenv("YCRDT_DEBUG_SYNC")[0] == '1';
   if (hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess) { delete e; return fail(YCRDT_E_DEVICE, "stream"); }
+  if (hipStreamCreateWithFlags(&e->side, hipStreamNonBlocking) != hipSuccess) { delete e; return fail(YCRDT_E_DEVICE, "stream"); }
+  hipEventCreateWithFlags(&e->side_done, hipEventDisableTiming);
   hipEventCreate(&e->ev0);
   hipEventCreate(&e->ev1);
   e->bufs.resize(B_COUNT);
@@ -805,6 +821,9 @@ void ycrdt_engine_destroy(ycrdt_engine* e) {
   for (auto& ev : e->event_pool) hipEventDestroy(ev);
   hipEventDestroy(e->ev0);
   hipEventDestroy(e->ev1);
+  hipStreamSynchronize(e->side);
+  hipEventDestroy(e->side_done);
+  hipStreamDestroy(e->side);
   hipStreamDestroy(e->stream);
   delete e;
 }
