@@ -329,17 +329,22 @@ static void rev_scans(const Work& w, uint32_t nclients, hipStream_t s) {
 
 // Phase 1: sizes + layout (ends with out_bytes / sv_bytes in the counters). No host sync: the
 // output / run counts are read on the device, grids and scans are sized for NS + 1 entries.
-void launch_encode_sizes(const Work& w, uint32_t nsegs, uint32_t nclients, hipStream_t s) {
+void launch_encode_sizes(const Work& w, uint32_t nsegs, uint32_t nclients, hipStream_t s, hipStream_t side,
+                         hipEvent_t ev_fork, hipEvent_t ev_join, void* tmp2, size_t tmp2_bytes) {
   fill_u32_multi({{w.ctr->pad, 8, 0u}, {w.cc + (size_t)CC_NRUNS * (w.cap_clients + 1), (uint64_t)w.cap_clients + 1, 0u}}, s);
   const uint32_t grid = nsegs / 256 + 1;
+  // delete-set runs (side stream) || output struct sizes (main stream)
+  hipEventRecord(ev_fork, s);
+  hipStreamWaitEvent(side, ev_fork, 0);
+  hipLaunchKernelGGL(k_run_flags, dim3(grid), dim3(256), 0, side, w, nsegs);
+  scan_u32(tmp2, tmp2_bytes, w.g_tmp, w.g_tmp2, nsegs + 1, side);
+  if (nsegs) hipLaunchKernelGGL(k_run_fill, dim3((nsegs + 255) / 256), dim3(256), 0, side, w, nsegs);
+  hipLaunchKernelGGL(k_run_sizes, dim3(grid), dim3(256), 0, side, w, nsegs);
+  scan_u32(tmp2, tmp2_bytes, w.r_size, w.r_pos, nsegs + 1, side);
+  hipEventRecord(ev_join, side);
   hipLaunchKernelGGL(k_out_sizes, dim3(grid), dim3(256), 0, s, w, nsegs, nclients);
   scan_u32(w.tmp, w.tmp_bytes, w.o_size, w.o_pos, nsegs + 1, s);
-  // delete-set runs
-  hipLaunchKernelGGL(k_run_flags, dim3(grid), dim3(256), 0, s, w, nsegs);
-  scan_u32(w.tmp, w.tmp_bytes, w.g_tmp, w.g_tmp2, nsegs + 1, s);
-  if (nsegs) hipLaunchKernelGGL(k_run_fill, dim3((nsegs + 255) / 256), dim3(256), 0, s, w, nsegs);
-  hipLaunchKernelGGL(k_run_sizes, dim3(grid), dim3(256), 0, s, w, nsegs);
-  scan_u32(w.tmp, w.tmp_bytes, w.r_size, w.r_pos, nsegs + 1, s);
+  hipStreamWaitEvent(s, ev_join, 0);
   hipLaunchKernelGGL(k_client_bounds, dim3(grid), dim3(256), 0, s, w, nclients, nsegs);
   hipLaunchKernelGGL(k_client_sizes, dim3(nclients / 256 + 1), dim3(256), 0, s, w, nclients, nsegs);
   rev_scans(w, nclients, s);

@@ -116,7 +116,7 @@ struct ycrdt_engine {
   int compat = 136;
   hipStream_t stream = nullptr;
   hipStream_t side = nullptr;        // delete-set decode overlaps the client table / struct decode
-  hipEvent_t side_done = nullptr;
+  hipEvent_t side_done = nullptr, side_fork = nullptr;
   std::vector<DevBuf> bufs;
   Work w;
   bool profiling = false;
@@ -578,8 +578,10 @@ int run_merge(ycrdt_engine* e, ycrdt_batch* b, const std::unordered_map<uint32_t
   w.out = take<uint8_t>(V, B_OUT, (size_t)w.cap_out + 16, ok);
   w.sv_out = take<uint8_t>(V, B_SVOUT, (size_t)w.cap_sv + 16, ok);
   if (!ok) return fail(YCRDT_E_DEVICE, "hipMalloc failed (output)");
+  uint8_t* tmp2 = take<uint8_t>(V, B_TMP2, prim_tmp_bytes((uint64_t)nsegs + 2), ok);
+  if (!ok) return fail(YCRDT_E_DEVICE, "hipMalloc failed (scan space)");
   mark(e, "encode.sizes");
-  launch_encode_sizes(w, nsegs, nclients, s);
+  launch_encode_sizes(w, nsegs, nclients, s, e->side, e->side_fork, e->side_done, tmp2, V[B_TMP2].cap);
   mark(e, "encode.write");
   launch_encode_write(w, nsegs, nclients, s);
   mark(e, "end");
@@ -806,6 +808,7 @@ int ycrdt_engine_create(int device, int compat, ycrdt_engine** out) {
   if (hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess) { delete e; return fail(YCRDT_E_DEVICE, "stream"); }
   if (hipStreamCreateWithFlags(&e->side, hipStreamNonBlocking) != hipSuccess) { delete e; return fail(YCRDT_E_DEVICE, "stream"); }
   hipEventCreateWithFlags(&e->side_done, hipEventDisableTiming);
+  hipEventCreateWithFlags(&e->side_fork, hipEventDisableTiming);
   hipEventCreate(&e->ev0);
   hipEventCreate(&e->ev1);
   e->bufs.resize(B_COUNT);
@@ -823,6 +826,7 @@ void ycrdt_engine_destroy(ycrdt_engine* e) {
   hipEventDestroy(e->ev1);
   hipStreamSynchronize(e->side);
   hipEventDestroy(e->side_done);
+  hipEventDestroy(e->side_fork);
   hipStreamDestroy(e->side);
   hipStreamDestroy(e->stream);
   delete e;

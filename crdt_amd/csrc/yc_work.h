@@ -341,7 +341,9 @@ void launch_merge_flags(const Work& w, uint32_t nsegs, hipStream_t s);
 void run_dead_keys(const Work& w, uint32_t nsegs, hipStream_t s);
 uint32_t launch_yata(const Work& w, uint32_t nsegs, uint32_t narray, uint32_t nclients, hipStream_t s);
 
-void launch_encode_sizes(const Work& w, uint32_t nsegs, uint32_t nclients, hipStream_t s);
+// side / ev_fork / ev_join / tmp2: the delete-set run chain runs on `side` with its own scan space
+void launch_encode_sizes(const Work& w, uint32_t nsegs, uint32_t nclients, hipStream_t s, hipStream_t side,
+                         hipEvent_t ev_fork, hipEvent_t ev_join, void* tmp2, size_t tmp2_bytes);
 void launch_encode_write(const Work& w, uint32_t nsegs, uint32_t nclients, hipStream_t s);
 
 // rocPRIM wrappers (yc_prims.hip)
