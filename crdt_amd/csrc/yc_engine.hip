@@ -492,7 +492,7 @@ int run_merge(ycrdt_engine* e, ycrdt_batch* b, const std::unordered_map<uint32_t
   w.g_rorigin = take<uint32_t>(V, B_GRORIG, U + 1, ok);
   w.g_link = take<uint32_t>(V, B_GLINK, U + 1, ok);
   w.g_key = take<uint32_t>(V, B_GKEY, U + 1, ok);
-  w.g_maxchild = take<uint64_t>(V, B_GMAXC, U + 1, ok);
+  w.g_maxchild = take<uint32_t>(V, B_GMAXC, U + 1, ok);
   w.g_outid = take<uint32_t>(V, B_GOUTID, U + 2, ok);
   w.g_tmp = take<uint32_t>(V, B_GTMP, U + 2, ok);
   w.g_tmp2 = take<uint32_t>(V, B_GTMP2, U + 2, ok);
@@ -535,7 +535,7 @@ int run_merge(ycrdt_engine* e, ycrdt_batch* b, const std::unordered_map<uint32_t
   // keys
   w.cap_keys = next_pow2(std::max<uint64_t>(2ull * nsegs, 64));
   w.k_hash = take<uint64_t>(V, B_KHASH, w.cap_keys, ok);
-  w.k_rootmax = take<uint64_t>(V, B_KROOT, w.cap_keys, ok);
+  w.k_rootmax = take<uint32_t>(V, B_KROOT, w.cap_keys, ok);
   w.k_winner = take<uint32_t>(V, B_KWIN, w.cap_keys, ok);
   w.k_parent = take<uint32_t>(V, B_KPAR, w.cap_keys, ok);
   w.k_flags = take<uint32_t>(V, B_KFLAG, w.cap_keys, ok);

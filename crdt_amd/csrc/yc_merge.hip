@@ -286,10 +286,10 @@ __global__ __launch_bounds__(256) void k_seg_props(Work w, uint32_t nsegs) {
 
 void launch_segment_props(const Work& w, uint32_t nsegs, uint32_t nclients, uint64_t nunits, hipStream_t s) {
   fill_u32_multi({{(uint32_t*)w.k_hash, (uint64_t)w.cap_keys * 2, 0u},
-                  {(uint32_t*)w.k_rootmax, (uint64_t)w.cap_keys * 2, 0u},
+                  {w.k_rootmax, (uint64_t)w.cap_keys, 0u},
                   {w.k_flags, w.cap_keys, 0u},
                   {w.k_parent, w.cap_keys, NONE},
-                  {(uint32_t*)w.g_maxchild, (uint64_t)nsegs * 2, 0u}}, s);
+                  {w.g_maxchild, (uint64_t)nsegs, 0u}}, s);
   if (nsegs) hipLaunchKernelGGL(k_seg_props, dim3((nsegs + 255) / 256), dim3(256), 0, s, w, nsegs);
 }
 
@@ -358,14 +358,16 @@ __global__ __launch_bounds__(256) void k_children(Work w, uint32_t lo, uint32_t 
   if (!(f & SEG_PSUB)) return;
   const uint32_t key = w.g_key[s];
   const uint32_t cidx = w.g_cidx[s];
-  const unsigned long long v = ((unsigned long long)(cidx + 1) << 32) | s;
+  // segments are numbered in (client index, clock) order, so the max (client, segment) child is
+  // the max segment: a u32 atomicMax of s + 1 (u64 atomics issue at well under half the rate)
+  const uint32_t v = s + 1;
   const uint32_t o = w.g_origin[s];
   if (o != NONE) {
     if (w.u_minchild[o] > cidx) atomicMin(&w.u_minchild[o], cidx);
-    unsigned long long* dst = (unsigned long long*)&w.g_maxchild[seg_of(w.u_cutbits, w.u_wpre, o)];
+    uint32_t* dst = &w.g_maxchild[seg_of(w.u_cutbits, w.u_wpre, o)];
     if (*dst < v) atomicMax(dst, v);
   } else if (f & SEG_ROOT) {
-    unsigned long long* dst = (unsigned long long*)&w.k_rootmax[key];
+    uint32_t* dst = &w.k_rootmax[key];
     if (*dst < v) atomicMax(dst, v);
   }
 }
@@ -374,13 +376,13 @@ __global__ __launch_bounds__(256) void k_children(Work w, uint32_t lo, uint32_t 
 __global__ void k_winner_walk(Work w) {
   const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
   if (k >= w.cap_keys) return;
-  const uint64_t r = w.k_rootmax[k];
+  const uint32_t r = w.k_rootmax[k];
   if (!r) { w.k_winner[k] = NONE; return; }
-  uint32_t x = (uint32_t)r;
+  uint32_t x = r - 1;
   for (uint32_t it = 0; it < (1u << 24); ++it) {
-    const uint64_t m = w.g_maxchild[x];
+    const uint32_t m = w.g_maxchild[x];
     if (!m) break;
-    x = (uint32_t)m;
+    x = m - 1;
   }
   w.k_winner[k] = x;
 }

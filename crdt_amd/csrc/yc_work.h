@@ -133,14 +133,14 @@ struct Work {
   uint32_t* g_rorigin = nullptr;   // right-origin unit or NONE
   uint32_t* g_link = nullptr;      // pointer-jumping link (key resolution)
   uint32_t* g_key = nullptr;       // resolved key slot or NONE
-  uint64_t* g_maxchild = nullptr;  // (cidx<<32 | seg) of max-client child, 0 = none
+  uint32_t* g_maxchild = nullptr;  // seg + 1 of the max-client child (segments are in client order), 0 = none
   uint32_t* g_next = nullptr;      // descent pointer / pointer jumping
   uint32_t* g_outid = nullptr;     // output struct id (scan of !merge flags)
   uint32_t* g_tmp = nullptr;       // scratch per segment
   uint32_t* g_tmp2 = nullptr;
   // ---- keys (hash table)
   uint64_t* k_hash = nullptr;      // [cap_keys] open addressing table of 64-bit key hashes (0 = empty)
-  uint64_t* k_rootmax = nullptr;   // [cap_keys] (cidx<<32 | seg) of max-client root
+  uint32_t* k_rootmax = nullptr;   // [cap_keys] seg + 1 of the max-client root, 0 = none
   uint32_t* k_winner = nullptr;    // [cap_keys] winning (rightmost) segment
   uint32_t* k_parent = nullptr;    // [cap_keys] parent type item unit (NONE = root type)
   uint32_t* k_flags = nullptr;     // [cap_keys] KF_* flags
