@@ -11,6 +11,7 @@ the C ABI in include/ycrdt.h (libycrdt.so, hand-written gfx950 HIP kernels):
     encode_state_vector(doc)      Y.encodeStateVector(doc)         crdt.js:59,239,258,289
     merge_updates([u8])           Y.mergeUpdates                   north_star (Y@39011)
     diff_update(u8, sv)           Y.diffUpdate                     Y@40711
+    diff_updates(u8s, svs)        n x Y.diffUpdate, one batched pass (crdt.js:286-291 sync responder)
 
 Errors raise YcrdtError (the reference only reads `e.message`, crdt.js:38-39). There is no CPU
 fallback: importing works without a GPU, but every compute call needs the HIP device.
@@ -20,7 +21,7 @@ import os
 
 __all__ = [
     "YcrdtError", "Engine", "Doc", "Batch", "MergeStats", "apply_update", "apply_updates",
-    "encode_state_as_update", "encode_state_vector", "merge_updates", "diff_update", "default_engine", "library_path",
+    "encode_state_as_update", "encode_state_vector", "merge_updates", "diff_update", "diff_updates", "default_engine", "library_path",
 ]
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
@@ -78,7 +79,7 @@ EXPORTS = (
     "ycrdt_doc_create", "ycrdt_doc_destroy", "ycrdt_apply_update", "ycrdt_apply_updates",
     "ycrdt_encode_state_as_update", "ycrdt_encode_state_vector", "ycrdt_doc_last_stats",
     "ycrdt_batch_stage", "ycrdt_batch_merge", "ycrdt_batch_result", "ycrdt_batch_destroy",
-    "ycrdt_merge_updates", "ycrdt_diff_update", "ycrdt_free", "ycrdt_last_error", "ycrdt_version",
+    "ycrdt_merge_updates", "ycrdt_diff_update", "ycrdt_diff_updates", "ycrdt_free", "ycrdt_last_error", "ycrdt_version",
     "ycrdt_doc_json", "ycrdt_map_set", "ycrdt_map_set_type", "ycrdt_map_delete", "ycrdt_array_insert",
     "ycrdt_array_delete", "ycrdt_doc_client_id", "ycrdt_map_type_at",
 )
@@ -112,6 +113,7 @@ def lib():
     L.ycrdt_batch_destroy.argtypes = [vp]
     L.ycrdt_merge_updates.argtypes = [vp, P(_Buf), sz, P(_Out)]
     L.ycrdt_diff_update.argtypes = [vp, _Buf, _Buf, P(_Out)]
+    L.ycrdt_diff_updates.argtypes = [vp, P(_Buf), P(_Buf), sz, P(_Out)]
     L.ycrdt_free.argtypes = [P(_Out)]
     cs = ctypes.c_char_p
     L.ycrdt_doc_json.argtypes = [vp, cs, i32, P(_Out)]
@@ -334,3 +336,16 @@ def diff_update(update: bytes, sv: bytes, engine=None) -> bytes:
     out = _Out()
     _check(lib().ycrdt_diff_update(eng._h, bu, bv, ctypes.byref(out)))
     return _take(out)
+
+
+def diff_updates(updates, svs, engine=None) -> list:
+    """[Y.diffUpdate(u, sv) for u, sv in zip(updates, svs)] in one batched GPU pass (the sync
+    responder of crdt.js:286-291 batched across peers / topics)."""
+    eng = engine or default_engine()
+    if len(updates) != len(svs):
+        raise ValueError("diff_updates: one state vector per update")
+    ua, ukeep = _bufs(updates)
+    va, vkeep = _bufs(svs)
+    outs = (_Out * max(len(ukeep), 1))()
+    _check(lib().ycrdt_diff_updates(eng._h, ua, va, len(ukeep), outs))
+    return [_take(outs[i]) for i in range(len(ukeep))]

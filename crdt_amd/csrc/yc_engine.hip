@@ -663,9 +663,65 @@ int run_view(ycrdt_engine* e, ycrdt_batch* b, HostView& hv) {
 
 // mergeUpdates (merge = true) or diffUpdate (merge = false, target state vector given) of a
 // staged batch; the encoded update is copied to `out`.
-int run_lazy(ycrdt_engine* e, ycrdt_batch* b, bool merge, const std::vector<std::pair<uint32_t, uint32_t>>& sv,
-             ycrdt_out* out) {
+void put_vu(std::vector<uint8_t>& o, uint32_t v) {
+  while (v >= 0x80u) { o.push_back((uint8_t)(v | 0x80u)); v >>= 7; }
+  o.push_back((uint8_t)v);
+}
+
+// Per-update outputs of a multi diff: [varuint blocks][its sections' blocks, in byte order]
+// [varuint delete-set clients][its delete-set groups]. Sections are appended by the walkers per
+// update (updates interleave), delete-set rows were sorted by (update, client desc).
+int split_multi(ycrdt_engine* e, const Decoded& D, uint32_t nr, uint32_t sbytes, uint32_t total,
+                std::vector<std::vector<uint8_t>>& outs) {
   Work& w = e->w;
+  const uint32_t nsec = D.nsections;
+  std::vector<uint8_t> all(total);
+  std::vector<Section> sec(nsec);
+  std::vector<uint32_t> evn(nsec), bpos(nsec + 1), dflag(nr), dpos(nr + 1);
+  std::vector<uint64_t> dkey(nr);
+  HIPCHK(hipMemcpy(all.data(), w.out, total, hipMemcpyDeviceToHost));
+  if (nsec) {
+    HIPCHK(hipMemcpy(sec.data(), w.sections, sizeof(Section) * nsec, hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(evn.data(), w.lz_evn, sizeof(uint32_t) * nsec, hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(bpos.data(), w.blk_pos, sizeof(uint32_t) * (nsec + 1), hipMemcpyDeviceToHost));
+  }
+  if (nr) {
+    HIPCHK(hipMemcpy(dflag.data(), w.dw_flag, sizeof(uint32_t) * nr, hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(dpos.data(), w.dw_pos, sizeof(uint32_t) * (nr + 1), hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(dkey.data(), w.dsm_keys, sizeof(uint64_t) * nr, hipMemcpyDeviceToHost));
+  }
+  const uint32_t nupd = w.nupd;
+  std::vector<std::vector<uint32_t>> by_upd(nupd);
+  for (uint32_t i = 0; i < nsec; ++i) {
+    if (sec[i].upd >= nupd) return fail(YCRDT_E_DEVICE, "diff batch: section of an unknown update");
+    if (evn[i]) by_upd[sec[i].upd].push_back(i);
+  }
+  outs.assign(nupd, {});
+  uint32_t r = 0;
+  for (uint32_t u = 0; u < nupd; ++u) {
+    auto& idx = by_upd[u];
+    std::sort(idx.begin(), idx.end(), [&](uint32_t a, uint32_t b) { return sec[a].first_pos < sec[b].first_pos; });
+    std::vector<uint8_t>& o = outs[u];
+    put_vu(o, (uint32_t)idx.size());
+    for (uint32_t i : idx) o.insert(o.end(), all.begin() + bpos[i], all.begin() + bpos[i + 1]);
+    const uint32_t r0 = r;
+    uint32_t ng = 0;
+    while (r < nr && (uint32_t)(dkey[r] >> 32) == u) { ng += dflag[r]; ++r; }
+    put_vu(o, ng);
+    o.insert(o.end(), all.begin() + sbytes + dpos[r0], all.begin() + sbytes + dpos[r]);
+  }
+  if (r != nr) return fail(YCRDT_E_DEVICE, "diff batch: delete-set rows out of update order");
+  return YCRDT_OK;
+}
+
+// With sv_off (diff only): update u is diffed against sv[sv_off[u] .. sv_off[u+1]) and `multi`
+// receives one encoded update per input update (the kernels write header-less block and
+// delete-set bytes; the per-update headers are written here while the bytes are split).
+int run_lazy(ycrdt_engine* e, ycrdt_batch* b, bool merge, const std::vector<std::pair<uint32_t, uint32_t>>& sv,
+             ycrdt_out* out, const std::vector<uint32_t>* sv_off = nullptr,
+             std::vector<std::vector<uint8_t>>* multi = nullptr) {
+  Work& w = e->w;
+  w.lz_multi = 0;
   auto& V = e->bufs;
   bool ok = true;
   hipStream_t s = e->stream;
@@ -719,19 +775,23 @@ int run_lazy(ycrdt_engine* e, ycrdt_batch* b, bool merge, const std::vector<std:
     w.tmp = take<uint8_t>(V, B_TMP, tb, ok);
     w.tmp_bytes = V[B_TMP].cap;
   }
-  uint32_t* svbuf = take<uint32_t>(V, B_SVC, 2 * sv.size() + 2, ok);
+  const size_t nsvo = sv_off ? sv_off->size() : 0;
+  uint32_t* svbuf = take<uint32_t>(V, B_SVC, 2 * sv.size() + nsvo + 2, ok);
   if (!ok) return fail(YCRDT_E_DEVICE, "hipMalloc failed (lazy merge workspace)");
   if (merge) {
     mark(e, "lazy.merge");
     if (D.nsections) launch_lazy_merge(w, D.nsections, D.nclients, s);
     else { w.lz_nblk = 0; w.lz_diff = 0; HIPCHK(hipMemsetAsync(w.lz_evbase, 0, sizeof(uint32_t) * 2, s)); }
   } else {
-    std::vector<uint32_t> h(2 * sv.size() + 2, 0);
+    std::vector<uint32_t> h(2 * sv.size() + nsvo + 2, 0);
     for (size_t i = 0; i < sv.size(); ++i) { h[i] = sv[i].first; h[sv.size() + i] = sv[i].second; }
+    for (size_t i = 0; i < nsvo; ++i) h[2 * sv.size() + i] = (*sv_off)[i];
     HIPCHK(hipMemcpyAsync(svbuf, h.data(), sizeof(uint32_t) * h.size(), hipMemcpyHostToDevice, s));
     w.sv_client = svbuf;
     w.sv_clock = svbuf + sv.size();
     w.sv_n = (uint32_t)sv.size();
+    w.sv_off = sv_off ? svbuf + 2 * sv.size() : nullptr;
+    w.lz_multi = sv_off ? 1u : 0u;
     mark(e, "lazy.diff");
     if (D.nsections) launch_lazy_diff(w, D.nsections, s);
     else { w.lz_nblk = 0; w.lz_diff = 1; HIPCHK(hipMemsetAsync(w.lz_evbase, 0, sizeof(uint32_t) * 2, s)); }
@@ -767,6 +827,7 @@ int run_lazy(ycrdt_engine* e, ycrdt_batch* b, bool merge, const std::vector<std:
   HIPCHK(hipEventRecord(e->ev1, s));
   rc = check(e, c, "lazy write");
   if (rc) return rc;
+  if (multi) return split_multi(e, D, nr, sbytes, total, *multi);
   out->len = total;
   out->ptr = (uint8_t*)malloc(total ? total : 1);
   HIPCHK(hipMemcpy(out->ptr, w.out, total, hipMemcpyDeviceToHost));
@@ -1015,6 +1076,37 @@ int ycrdt_diff_update(ycrdt_engine* e, ycrdt_buf update, ycrdt_buf sv, ycrdt_out
   if (b.bytes.p) hipFree(b.bytes.p);
   if (b.meta.p) hipFree(b.meta.p);
   return rc;
+}
+
+int ycrdt_diff_updates(ycrdt_engine* e, const ycrdt_buf* updates, const ycrdt_buf* svs, size_t n, ycrdt_out* outs) {
+  if (!e || (n && (!updates || !svs || !outs))) return fail(YCRDT_E_ARG, "null arg");
+  for (size_t i = 0; i < n; ++i) { outs[i].ptr = nullptr; outs[i].len = 0; }
+  if (!n) return YCRDT_OK;
+  std::vector<std::pair<uint32_t, uint32_t>> v;
+  std::vector<uint32_t> off(n + 1, 0);
+  for (size_t i = 0; i < n; ++i) {
+    std::unordered_map<uint32_t, uint32_t> m;
+    if (!parse_sv(svs[i].ptr, svs[i].len, m)) return fail(YCRDT_E_DECODE, "Integer out of range! (state vector)");
+    const size_t v0 = v.size();
+    v.insert(v.end(), m.begin(), m.end());
+    std::sort(v.begin() + v0, v.end());
+    off[i + 1] = (uint32_t)v.size();
+  }
+  HIPCHK(hipSetDevice(e->device));
+  ycrdt_batch b;
+  b.e = e;
+  std::vector<std::vector<uint8_t>> res;
+  int rc = stage(&b, updates, n, nullptr, 0);
+  if (rc == YCRDT_OK) rc = run_lazy(e, &b, false, v, nullptr, &off, &res);
+  if (b.bytes.p) hipFree(b.bytes.p);
+  if (b.meta.p) hipFree(b.meta.p);
+  if (rc) return rc;
+  for (size_t i = 0; i < n; ++i) {
+    outs[i].len = res[i].size();
+    outs[i].ptr = (uint8_t*)malloc(res[i].size() ? res[i].size() : 1);
+    if (!res[i].empty()) memcpy(outs[i].ptr, res[i].data(), res[i].size());
+  }
+  return YCRDT_OK;
 }
 
 void ycrdt_batch_destroy(ycrdt_batch* b) {

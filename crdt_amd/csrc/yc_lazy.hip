@@ -216,11 +216,12 @@ __global__ void k_lz_diff(Work w, uint32_t nsections) {
   if (i >= nsections) return;
   const Section S = w.sections[i];
   const uint32_t base = w.lz_evbase[i];
-  uint32_t svc = 0;  // target state of this client
+  uint32_t svc = 0;  // target state of this client (lz_multi: in this update's own state vector)
   {
-    uint32_t lo = 0, hi = w.sv_n;
+    const uint32_t sv0 = w.lz_multi ? w.sv_off[S.upd] : 0u, sv1 = w.lz_multi ? w.sv_off[S.upd + 1] : w.sv_n;
+    uint32_t lo = sv0, hi = sv1;
     while (lo < hi) { const uint32_t m = (lo + hi) >> 1; if (w.sv_client[m] < S.client) lo = m + 1; else hi = m; }
-    if (lo < w.sv_n && w.sv_client[lo] == S.client) svc = w.sv_clock[lo];
+    if (lo < sv1 && w.sv_client[lo] == S.client) svc = w.sv_clock[lo];
   }
   uint32_t evn = 0;
   // first struct (non-Skip) that ends past the target state: binary search on the clocks
@@ -340,16 +341,17 @@ __global__ __launch_bounds__(256) void k_ev_write(Work w, uint32_t nslots) {
   if (e - e0 >= n) return;
   const uint32_t client = blk_client(w, b);
   const uint32_t hdr = vu_size(n) + vu_size(client) + vu_size(w.ev_clock[e0]);
-  const uint32_t p = vu_size(w.ctr->pad[0]) + w.blk_pos[b] + hdr + (w.ev_pos[e] - w.ev_pos[e0]);
+  const uint32_t hoff = w.lz_multi ? 0u : vu_size(w.ctr->pad[0]);  // lz_multi: the host writes per-update headers
+  const uint32_t p = hoff + w.blk_pos[b] + hdr + (w.ev_pos[e] - w.ev_pos[e0]);
   encode_event<true>(w, client, e, w.out, p);
 }
 __global__ void k_blk_write(Work w, uint32_t nblk) {
   const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
-  if (b == 0) wr_vu(w.out, 0, w.ctr->pad[0]);
+  if (b == 0 && !w.lz_multi) wr_vu(w.out, 0, w.ctr->pad[0]);
   if (b >= nblk) return;
   const uint32_t n = w.lz_evn[b];
   if (!n) return;
-  uint32_t p = vu_size(w.ctr->pad[0]) + w.blk_pos[b];
+  uint32_t p = (w.lz_multi ? 0u : vu_size(w.ctr->pad[0])) + w.blk_pos[b];
   p = wr_vu(w.out, p, n);
   p = wr_vu(w.out, p, blk_client(w, b));
   wr_vu(w.out, p, w.ev_clock[w.lz_evbase[b]]);
@@ -392,7 +394,8 @@ __global__ void k_dsm_runs(Work w, uint32_t nds) {
 __global__ void k_dsd_keys(Work w, uint32_t nds) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= nds) return;
-  w.dsm_key[i] = ((uint64_t)(~w.ds[i].client) << 32) | i;
+  // lz_multi: (update, client desc); the radix sort is stable, so wire order survives within a client
+  w.dsm_key[i] = w.lz_multi ? ((uint64_t)w.ds[i].upd << 32 | (uint32_t)~w.ds[i].client) : ((uint64_t)(~w.ds[i].client) << 32) | i;
   w.dsm_len[i] = i;
 }
 __global__ void k_dsd_runs(Work w, uint32_t nds) {
@@ -408,7 +411,8 @@ __global__ void k_dsd_runs(Work w, uint32_t nds) {
 __global__ void k_dw_flags(Work w, uint32_t nr) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i > nr) return;
-  w.dw_flag[i] = (i < nr && (i == 0 || w.dr_client[i] != w.dr_client[i - 1])) ? 1u : 0u;
+  const bool brk = i > 0 && i < nr && w.lz_multi && (w.dsm_keys[i] >> 32) != (w.dsm_keys[i - 1] >> 32);  // next update
+  w.dw_flag[i] = (i < nr && (i == 0 || brk || w.dr_client[i] != w.dr_client[i - 1])) ? 1u : 0u;
 }
 __global__ void k_dw_gstart(Work w, uint32_t nr) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -431,9 +435,9 @@ __global__ void k_dw_sizes(Work w, uint32_t nr) {
 __global__ void k_dw_write(Work w, uint32_t nr, uint32_t dsbase) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t ng = w.dw_gid[nr];
-  if (i == 0) wr_vu(w.out, dsbase, ng);
+  if (i == 0 && !w.lz_multi) wr_vu(w.out, dsbase, ng);
   if (i >= nr) return;
-  uint32_t p = dsbase + vu_size(ng) + w.dw_pos[i];
+  uint32_t p = dsbase + (w.lz_multi ? 0u : vu_size(ng)) + w.dw_pos[i];
   if (w.dw_flag[i]) {
     const uint32_t g = w.dw_gid[i];
     p = wr_vu(w.out, p, w.dr_client[i]);

@@ -173,6 +173,7 @@ struct Work {
   uint32_t* lz_leave_hi = nullptr; // [sections] leave stamp (client rank + 1, step)
   uint32_t* lz_leave_lo = nullptr;
   uint32_t lz_nblk = 0, lz_diff = 0;
+  uint32_t lz_multi = 0;            // 1: one diffUpdate per input update (sync responder batch); no global headers
   uint32_t* ev_kind = nullptr;     // [slots] REF_GC | REF_SKIP | 1 (item)
   uint32_t* ev_src = nullptr;
   uint32_t* ev_clock = nullptr;
@@ -184,6 +185,7 @@ struct Work {
   const uint32_t* sv_client = nullptr;  // diff target state vector, sorted by client
   const uint32_t* sv_clock = nullptr;
   uint32_t sv_n = 0;
+  const uint32_t* sv_off = nullptr; // lz_multi: [nupd+1] each update's range of (sv_client, sv_clock)
   uint64_t* dsm_key = nullptr;     // [ds] (~client, clock)
   uint64_t* dsm_keys = nullptr;
   uint32_t* dsm_len = nullptr;

@@ -86,6 +86,12 @@ int ycrdt_merge_updates(ycrdt_engine *e, const ycrdt_buf *ups, size_t n, ycrdt_o
 /* Y.diffUpdate(update, sv) (Y@40711): the structs of `update` missing from state vector `sv`,
  * with the update's delete set. */
 int ycrdt_diff_update(ycrdt_engine *e, ycrdt_buf update, ycrdt_buf sv, ycrdt_out *out);
+/* n independent Y.diffUpdate(updates[i], svs[i]) in ONE batched device pass: the sync responder
+ * of crdt.js:286-291 (`Y.encodeStateAsUpdate(doc, peerStateVector)` per joining peer) batched
+ * across peers and topics. outs[i] is byte-identical to
+ * ycrdt_diff_update(updates[i], svs[i]); each must be released with ycrdt_free. A malformed
+ * update or state vector fails the whole batch (no output is produced). */
+int ycrdt_diff_updates(ycrdt_engine *e, const ycrdt_buf *updates, const ycrdt_buf *svs, size_t n, ycrdt_out *outs);
 
 /* ---- crdt.c materialisation and local ops ------------------------------------------------
  * A "target" is root type `root`, or (parent_key != NULL) the shared type stored in root YMap
