@@ -39,6 +39,8 @@ def parse():
     p.add_argument("--workload", default="c2", choices=["c2", "c1"])
     p.add_argument("--replicas", type=int, default=None, help="override replica count (default: config)")
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--fleet-pairs", type=int, default=20000,
+                   help="C5-shaped sync-responder leg: (doc state, peer SV) pairs in one batched diff (0 = off)")
     p.add_argument("--cpu-replicas", type=int, default=300,
                    help="replicas in the Yjs CPU-baseline sample (bounded: ~10 s of Yjs work)")
     p.add_argument("--port-replicas", type=int, default=1000, help="replicas in the oracle-port timing sample")
@@ -122,6 +124,60 @@ def cpu_baselines(args, cfg, updates, out_update, st, eng, gen_map):
                   f"sequential Yjs restatement, {c1 - c0:.2f} s",
         "parity": (ref == out_update) if pups is updates else None,
     }
+    return res
+
+
+def fleet_sync_leg(eng, n_pairs):
+    """Batched sync responder: n_pairs (doc state, lagging
+    peer state vector) pairs from the reduced C5 fixtures (60 docs of 2-4 clients, Yjs-generated),
+    cycled to n_pairs, answered with ONE ycrdt_diff_updates call (host buffers in and out, PCIe and
+    per-pair host split included). Beside it: Yjs 13.5.16's Y.diffUpdate over the same pairs in Node
+    on one core, outputs compared (sha256 of the canonical updates)."""
+    import hashlib
+    import shutil
+    import struct
+    import subprocess
+    import tempfile
+
+    import crdt_amd
+
+    with open(os.path.join(ROOT, "tests", "golden", "configs.json")) as f:
+        cases = [c for c in json.load(f)["cases"] if c["name"].startswith("c5_")]
+    base = []
+    for c in cases:
+        st = bytes.fromhex(c["state"])
+        base += [(st, bytes.fromhex(df["sv"])) for df in c["diffs"]] + [(st, b"\x00")]
+    pairs = [base[i % len(base)] for i in range(n_pairs)]
+    ups, svs = [p[0] for p in pairs], [p[1] for p in pairs]
+    crdt_amd.diff_updates(ups[:64], svs[:64], eng)  # warm
+    reps = 3
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        outs = crdt_amd.diff_updates(ups, svs, eng)
+    gpu_ms = (time.perf_counter() - t0) * 1e3 / reps
+    res = {"pairs": n_pairs, "docs": len(cases), "in_bytes": sum(map(len, ups)) + sum(map(len, svs)),
+           "out_bytes": sum(map(len, outs)), "ms": round(gpu_ms, 3), "pairs_per_s": round(n_pairs / (gpu_ms * 1e-3), 1),
+           "includes": "host pack + H2D + lazy decode + diff + encode + D2H + per-pair split, 1 GPU", "yjs": None}
+    node = shutil.which("node")
+    if node:
+        with tempfile.NamedTemporaryFile(suffix=".bin", delete=False) as f:
+            f.write(struct.pack("<I", 2 * n_pairs))
+            for u, v in pairs:
+                f.write(struct.pack("<I", len(u)) + u + struct.pack("<I", len(v)) + v)
+            fname = f.name
+        try:
+            r = subprocess.run([node, os.path.join(ROOT, "scripts", "yjs_baseline.js"), fname, "diff"],
+                               capture_output=True, text=True, timeout=240)
+            y = json.loads(r.stdout.strip().splitlines()[-1]) if r.returncode == 0 and r.stdout.strip() else None
+        finally:
+            os.unlink(fname)
+        if y and y.get("available"):
+            h = hashlib.sha256()
+            for o in outs:
+                h.update(o)
+            res["yjs"] = {"pairs_per_s": round(y["pairs"] / (y["ms"] * 1e-3), 1), "cores": 1, "kind": "reference",
+                          "ms": round(y["ms"], 2), "parity": y["out_sha256"] == h.hexdigest(),
+                          "sample": f"Yjs {y['yjs']} Y.diffUpdate over the same {y['pairs']} pairs in Node {y['node']}"}
     return res
 
 
@@ -243,6 +299,9 @@ def main():
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baselines(args, cfg, updates, out_update, st, eng, gen_map)
+    fleet = None
+    if rank == 0 and world == 1 and args.fleet_pairs > 0:
+        fleet = fleet_sync_leg(eng, args.fleet_pairs)
     line = {
         "metric": "CRDT items merged/sec at 1/2/4/8 MI355X + % of HBM roofline",
         "value": round(value, 1),
@@ -278,6 +337,7 @@ def main():
         },
         "roofline": roofline,
         "cpu_baseline": cpu,
+        "fleet_sync": fleet,
         "phases_ms": {n: round(m, 4) for n, m in phases},
     }
     if rank == 0:

@@ -234,6 +234,9 @@ module.exports = {
   encodeStateVector,
   mergeUpdates: (updates) => binding.mergeUpdates(updates),
   diffUpdate: (update, sv) => binding.diffUpdate(update, sv),
+  // batch entry (not in Yjs): [Y.diffUpdate(u, sv) for each pair] in one device pass — the sync
+  // responder (crdt.js:286-291) answering many joining peers / topics at once
+  diffUpdates: (updates, svs) => binding.diffUpdates(updates, svs),
   lastStats: (doc) => binding.lastStats(doc._h),
   version: binding.version,
   setDevice: binding.setDevice,

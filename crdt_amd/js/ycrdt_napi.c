@@ -265,6 +265,47 @@ static napi_value js_diff_update(napi_env env, napi_callback_info info) {
   return u8_from_out(env, &o);
 }
 
+/* diffUpdates(update[], sv[]) → Uint8Array[]   (n x Y.diffUpdate in one batched device pass: the
+ * sync responder of crdt.js:286-291 across peers / topics) */
+static int get_buf_array(napi_env env, napi_value arr, ycrdt_buf **out, uint32_t *n) {
+  bool is_arr = false;
+  napi_is_array(env, arr, &is_arr);
+  if (!is_arr) return 0;
+  napi_get_array_length(env, arr, n);
+  *out = (ycrdt_buf *)calloc(*n ? *n : 1, sizeof(ycrdt_buf));
+  for (uint32_t i = 0; i < *n; ++i) {
+    napi_value el;
+    napi_get_element(env, arr, i, &el);
+    if (!get_bytes(env, el, &(*out)[i])) { free(*out); *out = NULL; return 0; }
+  }
+  return 1;
+}
+static napi_value js_diff_updates(napi_env env, napi_callback_info info) {
+  size_t argc = 2;
+  napi_value argv[2];
+  CHECK(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+  ycrdt_buf *ups = NULL, *svs = NULL;
+  uint32_t n = 0, m = 0;
+  if (argc < 2 || !get_buf_array(env, argv[0], &ups, &n) || !get_buf_array(env, argv[1], &svs, &m) || n != m) {
+    free(ups);
+    free(svs);
+    napi_throw_type_error(env, NULL, "diffUpdates(updates[], stateVectors[]) with one state vector per update");
+    return NULL;
+  }
+  ycrdt_engine *e = engine(env);
+  if (!e) { free(ups); free(svs); return NULL; }
+  ycrdt_out *outs = (ycrdt_out *)calloc(n ? n : 1, sizeof(ycrdt_out));
+  int rc = ycrdt_diff_updates(e, ups, svs, n, outs);
+  free(ups);
+  free(svs);
+  if (rc != YCRDT_OK) { free(outs); return throw_rc(env, rc); }
+  napi_value arr;
+  napi_create_array_with_length(env, n, &arr);
+  for (uint32_t i = 0; i < n; ++i) napi_set_element(env, arr, i, u8_from_out(env, &outs[i]));
+  free(outs);
+  return arr;
+}
+
 static napi_value js_version(napi_env env, napi_callback_info info) {
   (void)info;
   napi_value s;
@@ -436,6 +477,7 @@ static napi_value init(napi_env env, napi_value exports) {
       {"encodeStateVector", NULL, js_encode_state_vector, NULL, NULL, NULL, napi_default, NULL},
       {"mergeUpdates", NULL, js_merge_updates, NULL, NULL, NULL, napi_default, NULL},
       {"diffUpdate", NULL, js_diff_update, NULL, NULL, NULL, napi_default, NULL},
+      {"diffUpdates", NULL, js_diff_updates, NULL, NULL, NULL, napi_default, NULL},
       {"lastStats", NULL, js_last_stats, NULL, NULL, NULL, napi_default, NULL},
       {"version", NULL, js_version, NULL, NULL, NULL, napi_default, NULL},
       {"mapTypeAt", NULL, js_map_type_at, NULL, NULL, NULL, napi_default, NULL},

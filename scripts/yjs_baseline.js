@@ -7,6 +7,7 @@
 // tests/golden/gen/load_yjs.js. If it is absent the script prints {"available": false}.
 //
 // Usage: node yjs_baseline.js <batch file> [workers]
+//        node yjs_baseline.js <pairs file> diff   (update, state vector) alternating: Y.diffUpdate each
 //   batch file = u32le count, then per update u32le length + bytes (bench.py writes it)
 // Single-doc workloads run on ONE core (Yjs integrates a doc on one thread; SURVEY.md §8(d)):
 // `for u of batch: Y.applyUpdate(doc, u)` then `Y.encodeStateAsUpdate(doc)`, timed with
@@ -60,6 +61,21 @@ if (isMainThread) {
     process.exit(0);
   }
   const ups = readBatch(file);
+  if (process.argv[3] === 'diff') {  // sync responder: (update, sv) pairs, Y.diffUpdate each, one core
+    const { canonicalUpdate } = require(path.join(__dirname, '..', 'tests', 'golden', 'gen', 'v1.js'));
+    const outs = [];
+    const t0 = process.hrtime.bigint();
+    for (let i = 0; i + 1 < ups.length; i += 2) outs.push(Y.diffUpdate(ups[i], ups[i + 1]));
+    const t1 = process.hrtime.bigint();
+    const h = crypto.createHash('sha256');
+    let bytes = 0;
+    for (const o of outs) { h.update(canonicalUpdate(o)); bytes += o.length; }
+    console.log(JSON.stringify({
+      available: true, yjs: '13.5.16', lib0: '0.2.42', node: process.version, workers: 1,
+      ms: Number(t1 - t0) / 1e6, pairs: outs.length, out_bytes: bytes, out_sha256: h.digest('hex'),
+    }));
+    process.exit(0);
+  }
   if (workers === 1) {
     const r = runOnce(Y, ups);
     const { canonicalUpdate } = require(path.join(__dirname, '..', 'tests', 'golden', 'gen', 'v1.js'));

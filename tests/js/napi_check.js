@@ -18,7 +18,7 @@ const unhex = (h) => new Uint8Array(Buffer.from(h, 'hex'));
 const mode = process.argv[2] || 'cpu';
 const { encodeAny, decodeAny } = require(path.join(ROOT, 'crdt_amd', 'js', 'any.js'));
 const opsCases = () => JSON.parse(fs.readFileSync(path.join(ROOT, 'tests', 'golden', 'ops.json'))).cases;
-for (const f of ['Doc', 'applyUpdate', 'applyUpdates', 'encodeStateAsUpdate', 'encodeStateVector', 'mergeUpdates', 'diffUpdate']) {
+for (const f of ['Doc', 'applyUpdate', 'applyUpdates', 'encodeStateAsUpdate', 'encodeStateVector', 'mergeUpdates', 'diffUpdate', 'diffUpdates']) {
   assert.strictEqual(typeof Y[f], 'function', f);
 }
 assert.ok(/gfx950/.test(Y.version()));
@@ -80,6 +80,7 @@ if (mode === 'cpu') {
   console.log('napi ops ok:', n, 'scripts,', events, 'map events');
 } else {
   let n = 0;
+  const dsrc = [], dsv = [];
   for (const set of ['kat', 'map', 'array', 'nested']) {
     const cases = JSON.parse(fs.readFileSync(path.join(ROOT, 'tests', 'golden', set + '.json'))).cases;
     for (const c of cases) {
@@ -90,11 +91,18 @@ if (mode === 'cpu') {
       assert.strictEqual(hex(Y.encodeStateVector(d)), c.sv, c.name);
       for (const df of c.diffs) assert.strictEqual(hex(Y.encodeStateAsUpdate(d, unhex(df.sv))), df.update, c.name);
       assert.strictEqual(hex(Y.mergeUpdates(c.updates.map(unhex))), c.updates.length > 1 ? c.merged : c.merged_raw, c.name);
+      const st = Y.encodeStateAsUpdate(d);
+      for (const df of c.diffs) { dsrc.push(st); dsv.push(unhex(df.sv)); }
+      dsrc.push(st); dsv.push(new Uint8Array([0]));
       n++;
     }
   }
+  // the batched sync responder: every (doc state, peer state vector) pair in one call
+  const batch = Y.diffUpdates(dsrc, dsv);
+  assert.strictEqual(batch.length, dsrc.length);
+  for (let i = 0; i < dsrc.length; i++) assert.strictEqual(hex(batch[i]), hex(Y.diffUpdate(dsrc[i], dsv[i])), 'diffUpdates ' + i);
   let threw = null;
   try { Y.applyUpdate(new Y.Doc(), new Uint8Array([0xff, 0xff])); } catch (e) { threw = e; }
   assert.ok(threw && /Integer out of range/.test(threw.message), 'malformed update must throw like Yjs');
-  console.log('napi golden ok:', n, 'cases');
+  console.log('napi golden ok:', n, 'cases,', dsrc.length, 'batched diffs');
 }
