@@ -81,7 +81,7 @@ EXPORTS = (
     "ycrdt_batch_stage", "ycrdt_batch_merge", "ycrdt_batch_result", "ycrdt_batch_destroy",
     "ycrdt_merge_updates", "ycrdt_diff_update", "ycrdt_diff_updates", "ycrdt_free", "ycrdt_last_error", "ycrdt_version",
     "ycrdt_doc_json", "ycrdt_map_set", "ycrdt_map_set_type", "ycrdt_map_delete", "ycrdt_array_insert",
-    "ycrdt_array_delete", "ycrdt_doc_client_id", "ycrdt_map_type_at",
+    "ycrdt_array_delete", "ycrdt_doc_client_id", "ycrdt_map_type_at", "ycrdt_doc_take_local_update",
 )
 
 
@@ -114,6 +114,7 @@ def lib():
     L.ycrdt_merge_updates.argtypes = [vp, P(_Buf), sz, P(_Out)]
     L.ycrdt_diff_update.argtypes = [vp, _Buf, _Buf, P(_Out)]
     L.ycrdt_diff_updates.argtypes = [vp, P(_Buf), P(_Buf), sz, P(_Out)]
+    L.ycrdt_doc_take_local_update.argtypes = [vp, P(_Out)]
     L.ycrdt_free.argtypes = [P(_Out)]
     cs = ctypes.c_char_p
     L.ycrdt_doc_json.argtypes = [vp, cs, i32, P(_Out)]
@@ -267,6 +268,12 @@ class Doc:
     def array_insert(self, root: str, index: int, anys: list, parent_key: str = None):
         a = b"".join(bytes(x) for x in anys)
         _check(lib().ycrdt_array_insert(self._h, root.encode(), _opt(parent_key), index, a, len(a), len(anys)))
+
+    def take_local_update(self) -> bytes:
+        """The local ops since the previous call as one update (incremental wire delta)."""
+        out = _Out()
+        _check(lib().ycrdt_doc_take_local_update(self._h, ctypes.byref(out)))
+        return _take(out)
 
     def array_delete(self, root: str, index: int, length: int, parent_key: str = None):
         _check(lib().ycrdt_array_delete(self._h, root.encode(), _opt(parent_key), index, length))

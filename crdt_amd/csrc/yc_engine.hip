@@ -140,6 +140,7 @@ struct ycrdt_doc {
   std::vector<uint8_t> sv;
   ycrdt_merge_stats last{};
   HostView view;         // materialised view of `state` (crdt.c), rebuilt lazily after a change
+  std::vector<std::vector<uint8_t>> local;  // local-op updates since the last ycrdt_doc_take_local_update
 };
 
 struct ycrdt_batch {
@@ -1147,7 +1148,27 @@ static uint32_t next_clock(ycrdt_doc* d) {
 
 static int apply_local(ycrdt_doc* d, const std::vector<uint8_t>& u) {
   ycrdt_buf b{u.data(), u.size()};
-  return ycrdt_apply_updates(d, &b, 1);
+  const int rc = ycrdt_apply_updates(d, &b, 1);
+  if (rc == YCRDT_OK) d->local.push_back(u);  // the op's own update: the incremental wire delta
+  return rc;
+}
+
+int ycrdt_doc_take_local_update(ycrdt_doc* d, ycrdt_out* out) {
+  if (!d || !out) return fail(YCRDT_E_ARG, "null arg");
+  out->ptr = nullptr;
+  out->len = 0;
+  std::vector<std::vector<uint8_t>> ops;
+  ops.swap(d->local);
+  if (ops.empty()) return empty_update(out);
+  if (ops.size() == 1) {  // Y.mergeUpdates returns a single input unchanged
+    out->len = ops[0].size();
+    out->ptr = (uint8_t*)malloc(out->len);
+    memcpy(out->ptr, ops[0].data(), out->len);
+    return YCRDT_OK;
+  }
+  std::vector<ycrdt_buf> bufs;
+  for (const auto& u : ops) bufs.push_back(ycrdt_buf{u.data(), u.size()});
+  return ycrdt_merge_updates(d->e, bufs.data(), bufs.size(), out);  // one update for the transaction
 }
 
 static OpTarget target_of(const char* root, const char* parent_key) {

@@ -237,6 +237,9 @@ module.exports = {
   // batch entry (not in Yjs): [Y.diffUpdate(u, sv) for each pair] in one device pass — the sync
   // responder (crdt.js:286-291) answering many joining peers / topics at once
   diffUpdates: (updates, svs) => binding.diffUpdates(updates, svs),
+  // opt-in incremental local-op encode (not in Yjs): the doc's local ops since the previous call as
+  // one update, instead of re-encoding the whole doc after every op (crdt.js:347,383,443,...)
+  takeLocalUpdate: (doc) => binding.takeLocalUpdate(doc._h),
   lastStats: (doc) => binding.lastStats(doc._h),
   version: binding.version,
   setDevice: binding.setDevice,

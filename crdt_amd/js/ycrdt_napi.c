@@ -198,6 +198,19 @@ static napi_value js_encode_state_vector(napi_env env, napi_callback_info info) 
   return u8_from_out(env, &o);
 }
 
+/* takeLocalUpdate(doc) → Uint8Array: the local ops since the previous call as one update */
+static napi_value js_take_local_update(napi_env env, napi_callback_info info) {
+  size_t argc = 1;
+  napi_value argv[1];
+  CHECK(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+  ycrdt_doc *d = argc > 0 ? get_doc(env, argv[0]) : NULL;
+  if (!d) return NULL;
+  ycrdt_out o = {NULL, 0};
+  int rc = ycrdt_doc_take_local_update(d, &o);
+  if (rc != YCRDT_OK) return throw_rc(env, rc);
+  return u8_from_out(env, &o);
+}
+
 /* lastStats(doc) → {items, structs, units, segments, outBytes, deviceMs} */
 static napi_value js_last_stats(napi_env env, napi_callback_info info) {
   size_t argc = 1;
@@ -478,6 +491,7 @@ static napi_value init(napi_env env, napi_value exports) {
       {"mergeUpdates", NULL, js_merge_updates, NULL, NULL, NULL, napi_default, NULL},
       {"diffUpdate", NULL, js_diff_update, NULL, NULL, NULL, napi_default, NULL},
       {"diffUpdates", NULL, js_diff_updates, NULL, NULL, NULL, napi_default, NULL},
+      {"takeLocalUpdate", NULL, js_take_local_update, NULL, NULL, NULL, napi_default, NULL},
       {"lastStats", NULL, js_last_stats, NULL, NULL, NULL, napi_default, NULL},
       {"version", NULL, js_version, NULL, NULL, NULL, napi_default, NULL},
       {"mapTypeAt", NULL, js_map_type_at, NULL, NULL, NULL, napi_default, NULL},

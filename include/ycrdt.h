@@ -121,6 +121,13 @@ int ycrdt_array_insert(ycrdt_doc *d, const char *root, const char *parent_key, u
 int ycrdt_array_delete(ycrdt_doc *d, const char *root, const char *parent_key, uint32_t index, uint32_t length);
 /* doc.clientID */
 int ycrdt_doc_client_id(ycrdt_doc *d, uint32_t *out);
+/* Incremental local-op encode: the updates of the local ops
+ * (ycrdt_map_* / ycrdt_array_*) applied since the previous call, as ONE update (Y.mergeUpdates of
+ * them; a single op's own update is returned as is; none = the empty update). crdt.js broadcasts
+ * Y.encodeStateAsUpdate(doc) after every local op (crdt.js:347,383,443,471,505,533,560,585,611);
+ * this delta is wire-compatible (Y.applyUpdate accepts it) but changes the bytes on the wire, so a
+ * host opts in. Remote updates applied in between are not part of it. */
+int ycrdt_doc_take_local_update(ycrdt_doc *d, ycrdt_out *out);
 
 /* ---- device-resident batches (ingest queue / benchmark) ---------------------------------- */
 /* Copies the updates into HBM. */

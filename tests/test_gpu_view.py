@@ -86,3 +86,29 @@ def test_gpu_local_op_errors():
         d.array_insert("users", 0, [b"\x7d\x01"], parent_key="nolist")  # no shared type there
     d.map_delete("users", "absent")  # a no-op, no struct written
     assert json.loads(d.root_json("users", "map")) == {}
+
+
+@pytest.mark.parametrize("every", [1, 3])
+def test_gpu_local_delta_replay(every):
+    """Incremental local-op encode (ycrdt_doc_take_local_update): a peer that receives only the
+    local-op deltas (one op, or the merge of up to `every` ops) plus the same remote updates
+    reaches the Yjs-recorded state bytes, wherever a delta has been delivered."""
+    for c in _ops()[::3]:
+        a = crdt_amd.Doc(client_id=c["client"])
+        b = crdt_amd.Doc(client_id=0x7FFFFFF1)
+        pending = 0
+        for i, s in enumerate(c["steps"]):
+            _step(a, s)
+            if s["op"] == "apply":
+                if pending:
+                    b.apply_update(a.take_local_update())
+                    pending = 0
+                b.apply_update(bytes.fromhex(s["update"]))
+            else:
+                pending += 1
+                if pending >= every or i == len(c["steps"]) - 1:
+                    b.apply_update(a.take_local_update())
+                    pending = 0
+            if not pending:
+                assert b.encode_state_as_update().hex() == s["state"], (c["name"], i, s["op"])
+        assert a.take_local_update() == b"\x00\x00"  # nothing new since the last take
