@@ -137,11 +137,23 @@ def _check(rc):
 
 
 def _bufs(updates):
+    """ycrdt_buf[] over the updates: one joined blob (kept alive on the array) and the pointer /
+    length columns filled with numpy — per-element ctypes assignment costs ~1.5 us per buffer."""
+    import numpy as np
+
     keep = [bytes(u) for u in updates]
-    arr = (_Buf * max(1, len(keep)))()
-    for i, u in enumerate(keep):
-        arr[i].ptr = ctypes.cast(ctypes.c_char_p(u), ctypes.c_void_p)
-        arr[i].len = len(u)
+    n = len(keep)
+    arr = (_Buf * max(1, n))()
+    if n:
+        blob = b"".join(keep)
+        arr._blob = blob
+        lens = np.fromiter(map(len, keep), dtype=np.uint64, count=n)
+        offs = np.zeros(n, dtype=np.uint64)
+        np.cumsum(lens[:-1], out=offs[1:])
+        base = ctypes.cast(ctypes.c_char_p(blob), ctypes.c_void_p).value or 0
+        cols = np.frombuffer(arr, dtype=np.uint64).reshape(-1, 2)  # {ptr, len} per ycrdt_buf
+        cols[:n, 0] = offs + np.uint64(base)
+        cols[:n, 1] = lens
     return arr, keep
 
 
