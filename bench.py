@@ -155,9 +155,14 @@ def fleet_sync_leg(eng, n_pairs):
     for _ in range(reps):
         outs = crdt_amd.diff_updates(ups, svs, eng)
     gpu_ms = (time.perf_counter() - t0) * 1e3 / reps
+    eng.set_profiling(True)  # one more pass with the engine's phase events: the device-side share
+    crdt_amd.diff_updates(ups, svs, eng)
+    phases = eng.phase_times()
+    eng.set_profiling(False)
     res = {"pairs": n_pairs, "docs": len(cases), "in_bytes": sum(map(len, ups)) + sum(map(len, svs)),
            "out_bytes": sum(map(len, outs)), "ms": round(gpu_ms, 3), "pairs_per_s": round(n_pairs / (gpu_ms * 1e-3), 1),
-           "includes": "host pack + H2D + lazy decode + diff + encode + D2H + per-pair split, 1 GPU", "yjs": None}
+           "includes": "host pack + H2D + lazy decode + diff + encode + D2H + per-pair split, 1 GPU",
+           "engine_phases_ms": {n: round(m, 4) for n, m in phases}, "yjs": None}
     node = shutil.which("node")
     if node:
         with tempfile.NamedTemporaryFile(suffix=".bin", delete=False) as f:

@@ -828,6 +828,13 @@ int run_lazy(ycrdt_engine* e, ycrdt_batch* b, bool merge, const std::vector<std:
   HIPCHK(hipEventRecord(e->ev1, s));
   rc = check(e, c, "lazy write");
   if (rc) return rc;
+  if (e->profiling) {  // phase times of the lazy pipeline (stage .. last kernel, host syncs included)
+    for (size_t i = 0; i + 1 < e->marks.size(); ++i) {
+      float t = 0;
+      hipEventElapsedTime(&t, e->marks[i].second, e->marks[i + 1].second);
+      e->phase_ms.push_back({e->marks[i].first, (double)t});
+    }
+  }
   if (multi) return split_multi(e, D, nr, sbytes, total, *multi);
   out->len = total;
   out->ptr = (uint8_t*)malloc(total ? total : 1);
