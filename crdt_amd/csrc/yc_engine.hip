@@ -115,6 +115,7 @@ struct ycrdt_engine {
   int device = 0;
   int compat = 136;
   hipStream_t stream = nullptr;
+  ycrdt_batch* scratch = nullptr;    // staging batch of the one-shot calls (apply / encode / merge / diff)
   hipStream_t side = nullptr;        // delete-set decode overlaps the client table / struct decode
   hipEvent_t side_done = nullptr, side_fork = nullptr;
   std::vector<DevBuf> bufs;
@@ -154,6 +155,14 @@ struct ycrdt_batch {
 };
 
 namespace {
+
+ycrdt_batch& scratch_batch(ycrdt_engine* e) {
+  if (!e->scratch) {
+    e->scratch = new ycrdt_batch();
+    e->scratch->e = e;
+  }
+  return *e->scratch;
+}
 
 void mark(ycrdt_engine* e, const char* name) {
   if (e->debug_sync) {  // YCRDT_DEBUG_SYNC=1: attribute a device fault to the phase that raised it
@@ -890,6 +899,11 @@ void ycrdt_engine_destroy(ycrdt_engine* e) {
   hipSetDevice(e->device);
   hipStreamSynchronize(e->stream);
   for (auto& b : e->bufs) if (b.p) hipFree(b.p);
+  if (e->scratch) {
+    if (e->scratch->bytes.p) hipFree(e->scratch->bytes.p);
+    if (e->scratch->meta.p) hipFree(e->scratch->meta.p);
+    delete e->scratch;
+  }
   for (auto& ev : e->event_pool) hipEventDestroy(ev);
   hipEventDestroy(e->ev0);
   hipEventDestroy(e->ev1);
@@ -941,8 +955,7 @@ int ycrdt_apply_updates(ycrdt_doc* d, const ycrdt_buf* ups, size_t n) {
   if (n == 0) return YCRDT_OK;
   ycrdt_engine* e = d->e;
   HIPCHK(hipSetDevice(e->device));
-  ycrdt_batch b;
-  b.e = e;
+  ycrdt_batch& b = scratch_batch(e);  // engine-owned: no hipMalloc / hipFree per call
   int rc = stage(&b, ups, n, d->state_len ? &d->state : nullptr, d->state_len);
   if (rc == YCRDT_OK) rc = run_merge(e, &b, nullptr);
   if (rc == YCRDT_OK) {
@@ -958,8 +971,6 @@ int ycrdt_apply_updates(ycrdt_doc* d, const ycrdt_buf* ups, size_t n) {
       d->view.valid = false;
     }
   }
-  if (b.bytes.p) hipFree(b.bytes.p);
-  if (b.meta.p) hipFree(b.meta.p);
   return rc;
 }
 
@@ -981,8 +992,7 @@ int ycrdt_encode_state_as_update(ycrdt_doc* d, ycrdt_buf sv, ycrdt_out* out) {
     return YCRDT_OK;
   }
   // delta: re-run the (idempotent) merge of the canonical state with per-client start clocks
-  ycrdt_batch b;
-  b.e = e;
+  ycrdt_batch& b = scratch_batch(e);  // engine-owned: no hipMalloc / hipFree per call
   int rc = stage(&b, nullptr, 0, &d->state, d->state_len);
   if (rc == YCRDT_OK) rc = run_merge(e, &b, &target);
   if (rc == YCRDT_OK) {
@@ -990,8 +1000,6 @@ int ycrdt_encode_state_as_update(ycrdt_doc* d, ycrdt_buf sv, ycrdt_out* out) {
     out->len = e->out_bytes;
     if (hipMemcpy(out->ptr, e->w.out, e->out_bytes, hipMemcpyDeviceToHost) != hipSuccess) rc = fail(YCRDT_E_DEVICE, "D2H");
   }
-  if (b.bytes.p) hipFree(b.bytes.p);
-  if (b.meta.p) hipFree(b.meta.p);
   return rc;
 }
 
@@ -1059,12 +1067,9 @@ int ycrdt_merge_updates(ycrdt_engine* e, const ycrdt_buf* ups, size_t n, ycrdt_o
     return YCRDT_OK;
   }
   HIPCHK(hipSetDevice(e->device));
-  ycrdt_batch b;
-  b.e = e;
+  ycrdt_batch& b = scratch_batch(e);  // engine-owned: no hipMalloc / hipFree per call
   int rc = stage(&b, ups, n, nullptr, 0);
   if (rc == YCRDT_OK) rc = run_lazy(e, &b, true, {}, out);
-  if (b.bytes.p) hipFree(b.bytes.p);
-  if (b.meta.p) hipFree(b.meta.p);
   return rc;
 }
 
@@ -1077,12 +1082,9 @@ int ycrdt_diff_update(ycrdt_engine* e, ycrdt_buf update, ycrdt_buf sv, ycrdt_out
   std::vector<std::pair<uint32_t, uint32_t>> v(m.begin(), m.end());
   std::sort(v.begin(), v.end());
   HIPCHK(hipSetDevice(e->device));
-  ycrdt_batch b;
-  b.e = e;
+  ycrdt_batch& b = scratch_batch(e);  // engine-owned: no hipMalloc / hipFree per call
   int rc = stage(&b, &update, 1, nullptr, 0);
   if (rc == YCRDT_OK) rc = run_lazy(e, &b, false, v, out);
-  if (b.bytes.p) hipFree(b.bytes.p);
-  if (b.meta.p) hipFree(b.meta.p);
   return rc;
 }
 
@@ -1101,13 +1103,10 @@ int ycrdt_diff_updates(ycrdt_engine* e, const ycrdt_buf* updates, const ycrdt_bu
     off[i + 1] = (uint32_t)v.size();
   }
   HIPCHK(hipSetDevice(e->device));
-  ycrdt_batch b;
-  b.e = e;
+  ycrdt_batch& b = scratch_batch(e);  // engine-owned: no hipMalloc / hipFree per call
   std::vector<std::vector<uint8_t>> res;
   int rc = stage(&b, updates, n, nullptr, 0);
   if (rc == YCRDT_OK) rc = run_lazy(e, &b, false, v, nullptr, &off, &res);
-  if (b.bytes.p) hipFree(b.bytes.p);
-  if (b.meta.p) hipFree(b.meta.p);
   if (rc) return rc;
   for (size_t i = 0; i < n; ++i) {
     outs[i].len = res[i].size();
@@ -1136,13 +1135,10 @@ static int ensure_view(ycrdt_doc* d) {
   }
   ycrdt_engine* e = d->e;
   HIPCHK(hipSetDevice(e->device));
-  ycrdt_batch b;
-  b.e = e;
+  ycrdt_batch& b = scratch_batch(e);  // engine-owned: no hipMalloc / hipFree per call
   int rc = stage(&b, nullptr, 0, &d->state, d->state_len);
   if (rc == YCRDT_OK) rc = run_merge(e, &b, nullptr);  // idempotent on the canonical state
   if (rc == YCRDT_OK) rc = run_view(e, &b, d->view);
-  if (b.bytes.p) hipFree(b.bytes.p);
-  if (b.meta.p) hipFree(b.meta.p);
   return rc;
 }
 
