@@ -27,3 +27,18 @@ def test_library_is_fresh():
     for f in os.listdir(src):
         if f.endswith((".hip", ".h")):
             assert os.path.getmtime(os.path.join(src, f)) <= so, f"{f} is newer than libycrdt.so: rebuild"
+
+
+def test_buf_arrays_point_at_the_inputs():
+    """The mirror's ycrdt_buf[] (one joined blob, numpy-filled columns) addresses every input,
+    empty ones included."""
+    import ctypes
+
+    ups = [b"", b"\x00\x00", bytes(range(200)), b"", b"\x01" * 7]
+    arr, keep = crdt_amd._bufs(ups)
+    assert len(keep) == len(ups)
+    for i, u in enumerate(ups):
+        assert arr[i].len == len(u)
+        assert ctypes.string_at(arr[i].ptr, arr[i].len) == u
+    empty, k = crdt_amd._bufs([])
+    assert k == [] and len(empty) == 1
