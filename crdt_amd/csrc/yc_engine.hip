@@ -10,6 +10,7 @@
 #include <vector>
 #include <unordered_map>
 #include <algorithm>
+#include <memory>
 
 #include "yc_work.h"
 #include "yc_host.h"
@@ -673,54 +674,74 @@ int run_view(ycrdt_engine* e, ycrdt_batch* b, HostView& hv) {
 
 // mergeUpdates (merge = true) or diffUpdate (merge = false, target state vector given) of a
 // staged batch; the encoded update is copied to `out`.
-void put_vu(std::vector<uint8_t>& o, uint32_t v) {
-  while (v >= 0x80u) { o.push_back((uint8_t)(v | 0x80u)); v >>= 7; }
-  o.push_back((uint8_t)v);
-}
-
 // Per-update outputs of a multi diff: [varuint blocks][its sections' blocks, in byte order]
 // [varuint delete-set clients][its delete-set groups]. Sections are appended by the walkers per
 // update (updates interleave), delete-set rows were sorted by (update, client desc).
-int split_multi(ycrdt_engine* e, const Decoded& D, uint32_t nr, uint32_t sbytes, uint32_t total,
-                std::vector<std::vector<uint8_t>>& outs) {
+int split_multi(ycrdt_engine* e, const Decoded& D, uint32_t nr, uint32_t sbytes, uint32_t total, ycrdt_out* outs) {
   Work& w = e->w;
   const uint32_t nsec = D.nsections;
-  std::vector<uint8_t> all(total);
+  std::unique_ptr<uint8_t[]> all(new uint8_t[total ? total : 1]);
   std::vector<Section> sec(nsec);
   std::vector<uint32_t> evn(nsec), bpos(nsec + 1), dflag(nr), dpos(nr + 1);
   std::vector<uint64_t> dkey(nr);
-  HIPCHK(hipMemcpy(all.data(), w.out, total, hipMemcpyDeviceToHost));
+  if (total) HIPCHK(hipMemcpyAsync(all.get(), w.out, total, hipMemcpyDeviceToHost, e->stream));
   if (nsec) {
-    HIPCHK(hipMemcpy(sec.data(), w.sections, sizeof(Section) * nsec, hipMemcpyDeviceToHost));
-    HIPCHK(hipMemcpy(evn.data(), w.lz_evn, sizeof(uint32_t) * nsec, hipMemcpyDeviceToHost));
-    HIPCHK(hipMemcpy(bpos.data(), w.blk_pos, sizeof(uint32_t) * (nsec + 1), hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpyAsync(sec.data(), w.sections, sizeof(Section) * nsec, hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(hipMemcpyAsync(evn.data(), w.lz_evn, sizeof(uint32_t) * nsec, hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(hipMemcpyAsync(bpos.data(), w.blk_pos, sizeof(uint32_t) * (nsec + 1), hipMemcpyDeviceToHost, e->stream));
   }
   if (nr) {
-    HIPCHK(hipMemcpy(dflag.data(), w.dw_flag, sizeof(uint32_t) * nr, hipMemcpyDeviceToHost));
-    HIPCHK(hipMemcpy(dpos.data(), w.dw_pos, sizeof(uint32_t) * (nr + 1), hipMemcpyDeviceToHost));
-    HIPCHK(hipMemcpy(dkey.data(), w.dsm_keys, sizeof(uint64_t) * nr, hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpyAsync(dflag.data(), w.dw_flag, sizeof(uint32_t) * nr, hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(hipMemcpyAsync(dpos.data(), w.dw_pos, sizeof(uint32_t) * (nr + 1), hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(hipMemcpyAsync(dkey.data(), w.dsm_keys, sizeof(uint64_t) * nr, hipMemcpyDeviceToHost, e->stream));
   }
+  HIPCHK(hipStreamSynchronize(e->stream));
   const uint32_t nupd = w.nupd;
-  std::vector<std::vector<uint32_t>> by_upd(nupd);
+  // non-empty sections grouped by update (counting sort), in byte order within an update
+  std::vector<uint32_t> cnt(nupd + 1, 0), idx;
   for (uint32_t i = 0; i < nsec; ++i) {
     if (sec[i].upd >= nupd) return fail(YCRDT_E_DEVICE, "diff batch: section of an unknown update");
-    if (evn[i]) by_upd[sec[i].upd].push_back(i);
+    if (evn[i]) ++cnt[sec[i].upd + 1];
   }
-  outs.assign(nupd, {});
+  for (uint32_t u = 0; u < nupd; ++u) cnt[u + 1] += cnt[u];
+  idx.resize(cnt[nupd]);
+  {
+    std::vector<uint32_t> cur(cnt.begin(), cnt.end() - 1);
+    for (uint32_t i = 0; i < nsec; ++i)
+      if (evn[i]) idx[cur[sec[i].upd]++] = i;
+  }
+  uint8_t hdr[2][5];
+  auto vu = [](uint8_t* o, uint32_t v) {
+    uint32_t n = 0;
+    while (v >= 0x80u) { o[n++] = (uint8_t)(v | 0x80u); v >>= 7; }
+    o[n++] = (uint8_t)v;
+    return n;
+  };
   uint32_t r = 0;
   for (uint32_t u = 0; u < nupd; ++u) {
-    auto& idx = by_upd[u];
-    std::sort(idx.begin(), idx.end(), [&](uint32_t a, uint32_t b) { return sec[a].first_pos < sec[b].first_pos; });
-    std::vector<uint8_t>& o = outs[u];
-    put_vu(o, (uint32_t)idx.size());
-    for (uint32_t i : idx) o.insert(o.end(), all.begin() + bpos[i], all.begin() + bpos[i + 1]);
+    uint32_t* a = idx.data() + cnt[u];
+    uint32_t* b = idx.data() + cnt[u + 1];
+    std::sort(a, b, [&](uint32_t x, uint32_t y) { return sec[x].first_pos < sec[y].first_pos; });
+    uint32_t blk = 0;
+    for (uint32_t* q = a; q < b; ++q) blk += bpos[*q + 1] - bpos[*q];
     const uint32_t r0 = r;
     uint32_t ng = 0;
     while (r < nr && (uint32_t)(dkey[r] >> 32) == u) { ng += dflag[r]; ++r; }
-    put_vu(o, ng);
-    o.insert(o.end(), all.begin() + sbytes + dpos[r0], all.begin() + sbytes + dpos[r]);
+    const uint32_t h0 = vu(hdr[0], (uint32_t)(b - a)), h1 = vu(hdr[1], ng);
+    const size_t len = (size_t)h0 + blk + h1 + (dpos[r] - dpos[r0]);
+    uint8_t* o = (uint8_t*)malloc(len);
+    size_t p = 0;
+    memcpy(o, hdr[0], h0); p += h0;
+    for (uint32_t* q = a; q < b; ++q) { memcpy(o + p, all.get() + bpos[*q], bpos[*q + 1] - bpos[*q]); p += bpos[*q + 1] - bpos[*q]; }
+    memcpy(o + p, hdr[1], h1); p += h1;
+    memcpy(o + p, all.get() + sbytes + dpos[r0], dpos[r] - dpos[r0]);
+    outs[u].ptr = o;
+    outs[u].len = len;
   }
-  if (r != nr) return fail(YCRDT_E_DEVICE, "diff batch: delete-set rows out of update order");
+  if (r != nr) {
+    for (uint32_t u = 0; u < nupd; ++u) { free(outs[u].ptr); outs[u].ptr = nullptr; outs[u].len = 0; }
+    return fail(YCRDT_E_DEVICE, "diff batch: delete-set rows out of update order");
+  }
   return YCRDT_OK;
 }
 
@@ -729,7 +750,7 @@ int split_multi(ycrdt_engine* e, const Decoded& D, uint32_t nr, uint32_t sbytes,
 // delete-set bytes; the per-update headers are written here while the bytes are split).
 int run_lazy(ycrdt_engine* e, ycrdt_batch* b, bool merge, const std::vector<std::pair<uint32_t, uint32_t>>& sv,
              ycrdt_out* out, const std::vector<uint32_t>* sv_off = nullptr,
-             std::vector<std::vector<uint8_t>>* multi = nullptr) {
+             ycrdt_out* multi = nullptr) {
   Work& w = e->w;
   w.lz_multi = 0;
   auto& V = e->bufs;
@@ -844,7 +865,7 @@ int run_lazy(ycrdt_engine* e, ycrdt_batch* b, bool merge, const std::vector<std:
       e->phase_ms.push_back({e->marks[i].first, (double)t});
     }
   }
-  if (multi) return split_multi(e, D, nr, sbytes, total, *multi);
+  if (multi) return split_multi(e, D, nr, sbytes, total, multi);
   out->len = total;
   out->ptr = (uint8_t*)malloc(total ? total : 1);
   HIPCHK(hipMemcpy(out->ptr, w.out, total, hipMemcpyDeviceToHost));
@@ -1104,16 +1125,9 @@ int ycrdt_diff_updates(ycrdt_engine* e, const ycrdt_buf* updates, const ycrdt_bu
   }
   HIPCHK(hipSetDevice(e->device));
   ycrdt_batch& b = scratch_batch(e);  // engine-owned: no hipMalloc / hipFree per call
-  std::vector<std::vector<uint8_t>> res;
   int rc = stage(&b, updates, n, nullptr, 0);
-  if (rc == YCRDT_OK) rc = run_lazy(e, &b, false, v, nullptr, &off, &res);
-  if (rc) return rc;
-  for (size_t i = 0; i < n; ++i) {
-    outs[i].len = res[i].size();
-    outs[i].ptr = (uint8_t*)malloc(res[i].size() ? res[i].size() : 1);
-    if (!res[i].empty()) memcpy(outs[i].ptr, res[i].data(), res[i].size());
-  }
-  return YCRDT_OK;
+  if (rc == YCRDT_OK) rc = run_lazy(e, &b, false, v, nullptr, &off, outs);
+  return rc;
 }
 
 void ycrdt_batch_destroy(ycrdt_batch* b) {
