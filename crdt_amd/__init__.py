@@ -82,7 +82,10 @@ EXPORTS = (
     "ycrdt_merge_updates", "ycrdt_diff_update", "ycrdt_diff_updates", "ycrdt_free", "ycrdt_last_error", "ycrdt_version",
     "ycrdt_doc_json", "ycrdt_map_set", "ycrdt_map_set_type", "ycrdt_map_delete", "ycrdt_array_insert",
     "ycrdt_array_delete", "ycrdt_doc_client_id", "ycrdt_map_type_at", "ycrdt_doc_take_local_update",
+    "ycrdt_doc_flush", "ycrdt_doc_pending", "ycrdt_doc_track_local", "ycrdt_validate_update", "ycrdt_debug_replay",
 )
+
+MERGE_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p)
 
 
 def lib():
@@ -115,6 +118,11 @@ def lib():
     L.ycrdt_diff_update.argtypes = [vp, _Buf, _Buf, P(_Out)]
     L.ycrdt_diff_updates.argtypes = [vp, P(_Buf), P(_Buf), sz, P(_Out)]
     L.ycrdt_doc_take_local_update.argtypes = [vp, P(_Out)]
+    L.ycrdt_doc_flush.argtypes = [vp]
+    L.ycrdt_doc_pending.argtypes = [vp, P(i32), P(i32)]
+    L.ycrdt_doc_track_local.argtypes = [vp, i32]
+    L.ycrdt_validate_update.argtypes = [_Buf, P(i32)]
+    L.ycrdt_debug_replay.argtypes = [P(_Buf), sz, MERGE_FN, vp, P(_Out), P(_Out), P(_Out)]
     L.ycrdt_free.argtypes = [P(_Out)]
     cs = ctypes.c_char_p
     L.ycrdt_doc_json.argtypes = [vp, cs, i32, P(_Out)]
@@ -247,6 +255,20 @@ class Doc:
         _check(lib().ycrdt_encode_state_vector(self._h, ctypes.byref(out)))
         return _take(out)
 
+    def flush(self):
+        """Runs the deferred Y.applyUpdate calls now (every read does this implicitly)."""
+        _check(lib().ycrdt_doc_flush(self._h))
+
+    def pending(self):
+        """(structs, delete_set): whether Yjs would hold store.pendingStructs / store.pendingDs."""
+        a, b = ctypes.c_int(), ctypes.c_int()
+        _check(lib().ycrdt_doc_pending(self._h, ctypes.byref(a), ctypes.byref(b)))
+        return bool(a.value), bool(b.value)
+
+    def track_local(self, on=True):
+        """Record local-op updates for take_local_update (off until this or the first take)."""
+        _check(lib().ycrdt_doc_track_local(self._h, 1 if on else 0))
+
     def last_stats(self) -> MergeStats:
         st = MergeStats()
         _check(lib().ycrdt_doc_last_stats(self._h, ctypes.byref(st)))
@@ -355,6 +377,41 @@ def diff_update(update: bytes, sv: bytes, engine=None) -> bytes:
     out = _Out()
     _check(lib().ycrdt_diff_update(eng._h, bu, bv, ctypes.byref(out)))
     return _take(out)
+
+
+def validate_update(update: bytes):
+    """Host-side validation of one update (no GPU): (ok, structs_ok)."""
+    u = bytes(update)
+    b = _Buf(ctypes.cast(ctypes.c_char_p(u), ctypes.c_void_p), len(u))
+    so = ctypes.c_int()
+    rc = lib().ycrdt_validate_update(b, ctypes.byref(so))
+    return rc == YCRDT_OK, bool(so.value)
+
+
+def debug_replay(updates, merge):
+    """Test hook (no GPU): replays Y.applyUpdate x n on struct headers with `merge(list[bytes]) ->
+    bytes` as Y.mergeUpdates; returns (state vector ascending, pending update, pending delete set)."""
+    keep = []
+
+    def cb(_ctx, ups, n, out):
+        try:
+            arr = ctypes.cast(ups, ctypes.POINTER(_Buf))
+            ins = [ctypes.string_at(arr[i].ptr, arr[i].len) if arr[i].len else b"" for i in range(n)]
+            res = bytes(merge(ins))
+            buf = ctypes.create_string_buffer(res, max(1, len(res)))
+            keep.append(buf)
+            o = ctypes.cast(out, ctypes.POINTER(_Out))
+            o[0].ptr = ctypes.cast(buf, ctypes.c_void_p)
+            o[0].len = len(res)
+            return 0
+        except Exception:  # noqa: BLE001 — surfaces as an error code in the replay
+            return -6
+
+    fn = MERGE_FN(cb)
+    arr, kept = _bufs(updates)
+    sv, p, pd = _Out(), _Out(), _Out()
+    _check(lib().ycrdt_debug_replay(arr, len(kept), fn, None, ctypes.byref(sv), ctypes.byref(p), ctypes.byref(pd)))
+    return _take(sv), _take(p), _take(pd)
 
 
 def diff_updates(updates, svs, engine=None) -> list:

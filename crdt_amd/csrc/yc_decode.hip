@@ -964,11 +964,11 @@ __global__ __launch_bounds__(256) void k_struct_decode(Work w, uint32_t nstructs
   // client ids are kept (presence = info bits); integrate mode maps them to client indices
   if (item && (v.info & 0x80u)) {
     oc = w.lazy ? v.oc : find_cidx(w.cl_vals, nclients, v.oc);
-    if (oc == NONE && !w.lazy) { raise_err(err, ERR_PENDING); w.ctr->err_info = i; }
+    if (oc == NONE && !w.lazy) oc = UNKNOWN;  // k_refs decides (pending unless capped away)
   }
   if (item && (v.info & 0x40u)) {
     rc = w.lazy ? v.rc : find_cidx(w.cl_vals, nclients, v.rc);
-    if (rc == NONE && !w.lazy) { raise_err(err, ERR_PENDING); w.ctr->err_info = i; }
+    if (rc == NONE && !w.lazy) rc = UNKNOWN;
   }
   w.s_ocidx[i] = oc;
   w.s_oclock[i] = v.ok_;
@@ -980,7 +980,7 @@ __global__ __launch_bounds__(256) void k_struct_decode(Work w, uint32_t nstructs
   else if (pk == 2) {
     pa = w.lazy ? v.pa : find_cidx(w.cl_vals, nclients, v.pa);
     pb = v.pb;
-    if (pa == NONE && !w.lazy) { raise_err(err, ERR_PENDING); w.ctr->err_info = i; }
+    if (pa == NONE && !w.lazy) pa = UNKNOWN;
   }
   if (pk != 0 && !v.has_psub) w.ctr->narray_roots = 1;  // a YArray list may exist (flag, plain store)
   if (pk == 2) w.ctr->nested = 1;                        // a nested type's list (flag, plain store)
@@ -1027,6 +1027,15 @@ __global__ void k_states(Work w, uint32_t nstructs) {
   const bool last = i + 1 == nstructs || w.s_sec[i + 1] != w.s_sec[i] || (w.s_info[i + 1] & 31u) == REF_SKIP;
   if (last) atomicMax(&w.cl_state[w.s_cidx[i]], w.s_clock[i] + w.s_len[i]);
 }
+// Yjs pending structs (yc_ingest.h): every client is integrated up to its cap only
+__global__ void k_apply_caps(Work w) {
+  const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= w.ctr->nclients) return;
+  const uint32_t v = w.cl_vals[c];
+  const uint32_t i = lower_bound_u32(w.cap_client, w.ncaps, v);
+  const uint32_t cap = (i < w.ncaps && w.cap_client[i] == v) ? w.cap_clock[i] : 0u;
+  if (w.cl_state[c] > cap) w.cl_state[c] = cap;
+}
 __global__ void k_state_totals(Work w, uint32_t nstructs) {  // U and Σ input lengths into the counters
   w.ctr->units = w.cl_base[w.ctr->nclients];
   w.ctr->in_len = w.s_lenscan[nstructs];
@@ -1035,6 +1044,7 @@ __global__ void k_state_totals(Work w, uint32_t nstructs) {  // U and Σ input l
 void launch_states(const Work& w, uint32_t nstructs, uint32_t nsections, hipStream_t s) {
   hipMemsetAsync(w.cl_state, 0, sizeof(uint32_t) * (nsections + 1), s);
   if (nstructs) hipLaunchKernelGGL(k_states, dim3((nstructs + 255) / 256), dim3(256), 0, s, w, nstructs);
+  if (w.capped && nsections) hipLaunchKernelGGL(k_apply_caps, dim3(nsections / 256 + 1), dim3(256), 0, s, w);
   scan_u32_to_u64(w.tmp, w.tmp_bytes, w.cl_state, w.cl_base, nsections + 1, s);
   hipLaunchKernelGGL(k_state_totals, dim3(1), dim3(1), 0, s, w, nstructs);
 }

@@ -14,6 +14,8 @@
 
 #include "yc_work.h"
 #include "yc_host.h"
+#include "yc_ingest.h"
+#include <thread>
 #include "../../include/ycrdt.h"
 
 using namespace yc;
@@ -106,7 +108,7 @@ enum Buf {
   B_GRIGHT, B_YKEY, B_YKEYS, B_YSEG, B_YIOTA, B_YLSTART, B_YSTATE, B_YBEFORE, B_YCONFL, B_YSTACK,
   B_OFIRST, B_OCIDX, B_OSIZE, B_OPOS, B_RSEG, B_RLEN, B_RSIZE, B_RPOS, B_OUT, B_SVOUT,
   B_VKMAP, B_VKREP, B_VKEYS, B_VNKEYS, B_VPOS, B_VD0, B_VN0, B_VD1, B_VN1, B_VORDER, B_VSEGS,
-  B_SCRATCH2, B_TMP2,
+  B_SCRATCH2, B_TMP2, B_CAPS,
   B_COUNT
 };
 
@@ -128,7 +130,9 @@ struct ycrdt_engine {
   std::vector<std::pair<const char*, double>> phase_ms;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   std::vector<uint8_t> pinned_stage;
-  // result of the last merge
+  // result of the last merge (e->w.out / e->w.sv_out): ws_owner is the batch that produced it
+  // (nullptr after any other call), so ycrdt_batch_result never returns another call's bytes
+  const void* ws_owner = nullptr;
   uint32_t out_bytes = 0, sv_bytes = 0;
   uint32_t nsegs = 0, nlists = 0;  // segments / YArray lists of the last merge (the view reads them)
   ycrdt_merge_stats last{};
@@ -142,7 +146,15 @@ struct ycrdt_doc {
   std::vector<uint8_t> sv;
   ycrdt_merge_stats last{};
   HostView view;         // materialised view of `state` (crdt.c), rebuilt lazily after a change
+  // Y.applyUpdate is deferred: validated updates wait here and are merged in one
+  // batch by the next read (encode*, toJSON, get, local op). n sequential applies cost one merge.
+  struct Queued { std::vector<uint8_t> bytes; bool local; };
+  std::vector<Queued> queue;
+  size_t queue_bytes = 0;
+  IngestState ing;       // Yjs pendingStructs / pendingDs / store client order (yc_ingest.h)
+  bool track_local = false;                 // ycrdt_doc_track_local: record local-op updates
   std::vector<std::vector<uint8_t>> local;  // local-op updates since the last ycrdt_doc_take_local_update
+  size_t local_bytes = 0;
 };
 
 struct ycrdt_batch {
@@ -461,12 +473,29 @@ int run_decode(ycrdt_engine* e, ycrdt_batch* b, bool lazy, Decoded& D) {
   return YCRDT_OK;
 }
 
-// The whole batched merge. `target` (optional) selects a delta encode against a state vector.
-int run_merge(ycrdt_engine* e, ycrdt_batch* b, const std::unordered_map<uint32_t, uint32_t>* target) {
+// The whole batched merge. `target` (optional) selects a delta encode against a state vector;
+// `caps` (optional) integrates every client only up to its cap (Yjs pending structs, yc_ingest.h).
+int run_merge(ycrdt_engine* e, ycrdt_batch* b, const std::unordered_map<uint32_t, uint32_t>* target,
+              const ClockMap* caps = nullptr) {
   Work& w = e->w;
   auto& V = e->bufs;
   bool ok = true;
   hipStream_t s = e->stream;
+  e->ws_owner = nullptr;
+  w.capped = 0;
+  w.ncaps = 0;
+  if (caps) {
+    uint32_t* cb = take<uint32_t>(V, B_CAPS, 2 * caps->size() + 2, ok);
+    if (!ok) return fail(YCRDT_E_DEVICE, "hipMalloc failed (caps)");
+    std::vector<uint32_t> h(2 * caps->size() + 2, 0);
+    size_t i = 0;
+    for (const auto& kv : *caps) { h[i] = kv.first; h[caps->size() + i] = kv.second; ++i; }
+    HIPCHK(hipMemcpyAsync(cb, h.data(), sizeof(uint32_t) * h.size(), hipMemcpyHostToDevice, s));
+    w.cap_client = cb;
+    w.cap_clock = cb + caps->size();
+    w.ncaps = (uint32_t)caps->size();
+    w.capped = 1;
+  }
   Decoded D;
   int rc = run_decode(e, b, false, D);
   if (rc) return rc;
@@ -534,7 +563,8 @@ int run_merge(ycrdt_engine* e, ycrdt_batch* b, const std::unordered_map<uint32_t
   if (!ok) return fail(YCRDT_E_DEVICE, "hipMalloc failed (unit workspace)");
   // ---- K2..K5 units
   mark(e, "merge.units");
-  if (U) launch_units(w, nstructs, nclients, nds, U, s);
+  // with no units, delete-set ranges still have to be checked: each one is pending (pendingDs)
+  if (U || nds) launch_units(w, nstructs, nclients, nds, U, s);
   mark(e, "merge.segments");
   uint32_t nsegs = 0;
   if (U) {
@@ -729,7 +759,11 @@ int split_multi(ycrdt_engine* e, const Decoded& D, uint32_t nr, uint32_t sbytes,
     while (r < nr && (uint32_t)(dkey[r] >> 32) == u) { ng += dflag[r]; ++r; }
     const uint32_t h0 = vu(hdr[0], (uint32_t)(b - a)), h1 = vu(hdr[1], ng);
     const size_t len = (size_t)h0 + blk + h1 + (dpos[r] - dpos[r0]);
-    uint8_t* o = (uint8_t*)malloc(len);
+    uint8_t* o = (uint8_t*)malloc(len ? len : 1);
+    if (!o) {
+      for (uint32_t k = 0; k < u; ++k) { free(outs[k].ptr); outs[k].ptr = nullptr; outs[k].len = 0; }
+      return fail(YCRDT_E_CAPACITY, "diff batch: host allocation failed");
+    }
     size_t p = 0;
     memcpy(o, hdr[0], h0); p += h0;
     for (uint32_t* q = a; q < b; ++q) { memcpy(o + p, all.get() + bpos[*q], bpos[*q + 1] - bpos[*q]); p += bpos[*q + 1] - bpos[*q]; }
@@ -753,6 +787,8 @@ int run_lazy(ycrdt_engine* e, ycrdt_batch* b, bool merge, const std::vector<std:
              ycrdt_out* multi = nullptr) {
   Work& w = e->w;
   w.lz_multi = 0;
+  w.capped = 0;
+  e->ws_owner = nullptr;
   auto& V = e->bufs;
   bool ok = true;
   hipStream_t s = e->stream;
@@ -868,6 +904,7 @@ int run_lazy(ycrdt_engine* e, ycrdt_batch* b, bool merge, const std::vector<std:
   if (multi) return split_multi(e, D, nr, sbytes, total, multi);
   out->len = total;
   out->ptr = (uint8_t*)malloc(total ? total : 1);
+  if (!out->ptr) { out->len = 0; return fail(YCRDT_E_CAPACITY, "host allocation failed"); }
   HIPCHK(hipMemcpy(out->ptr, w.out, total, hipMemcpyDeviceToHost));
   return YCRDT_OK;
 }
@@ -967,35 +1004,171 @@ int ycrdt_doc_create(ycrdt_engine* e, uint32_t client_id, ycrdt_doc** out) {
 void ycrdt_doc_destroy(ycrdt_doc* d) {
   if (!d) return;
   hipSetDevice(d->e->device);
+  if (d->e->ws_owner == d) d->e->ws_owner = nullptr;
   if (d->state.p) hipFree(d->state.p);
   delete d;
 }
 
+}  // extern "C"
+
+namespace {
+
+constexpr size_t QUEUE_FLUSH_BYTES = size_t(1) << 30;  // deferred updates past this are merged at once
+
+// Merges `extra` (host updates) behind the doc's state in one device pass and makes the result the
+// doc's state. caps: integrate only below the per-client caps (the pending path).
+int commit_merge(ycrdt_doc* d, const std::vector<ycrdt_buf>& extra, const ClockMap* caps) {
+  ycrdt_engine* e = d->e;
+  ycrdt_batch& b = scratch_batch(e);  // engine-owned: no hipMalloc / hipFree per call
+  int rc = stage(&b, extra.data(), extra.size(), d->state_len ? &d->state : nullptr, d->state_len);
+  if (rc == YCRDT_OK) rc = run_merge(e, &b, nullptr, caps);
+  if (rc) return rc;
+  if (!grow(d->state, e->out_bytes + 16)) return fail(YCRDT_E_DEVICE, "hipMalloc failed (doc state)");
+  HIPCHK(hipMemcpyAsync(d->state.p, e->w.out, e->out_bytes, hipMemcpyDeviceToDevice, e->stream));
+  d->state_len = e->out_bytes;
+  d->sv.resize(e->sv_bytes);
+  HIPCHK(hipMemcpyAsync(d->sv.data(), e->w.sv_out, e->sv_bytes, hipMemcpyDeviceToHost, e->stream));
+  HIPCHK(hipStreamSynchronize(e->stream));
+  d->last = e->last;
+  d->view.valid = false;
+  e->ws_owner = d;  // the workspace now holds this doc's merged store (ensure_view reuses it)
+  return YCRDT_OK;
+}
+
+// Y.mergeUpdates of host buffers on the device (the pending path's merges)
+int lazy_merge_host(ycrdt_engine* e, const std::vector<const std::vector<uint8_t>*>& ins, std::vector<uint8_t>& out) {
+  std::vector<ycrdt_buf> bufs;
+  for (const auto* v : ins) bufs.push_back(ycrdt_buf{v->data(), v->size()});
+  ycrdt_out o{nullptr, 0};
+  const int rc = ycrdt_merge_updates(e, bufs.data(), bufs.size(), &o);
+  if (rc) return rc;
+  out.assign(o.ptr, o.ptr + o.len);
+  ycrdt_free(&o);
+  return YCRDT_OK;
+}
+
+// Runs the deferred Y.applyUpdate calls. Fast path: no pending state before, and the device merge
+// of (state ∪ queue) finds every dependency — then sequential Yjs ends with nothing pending either
+// (every parked struct is retried once the client it waits on advances), so the merge IS the
+// result. Otherwise the queue is replayed through Yjs's readUpdateV2 on struct headers
+// (yc_ingest.cpp), which yields the pending structs / delete set byte for byte and the state every
+// client reaches; one capped device merge then integrates exactly that.
+int flush(ycrdt_doc* d) {
+  if (d->queue.empty()) return YCRDT_OK;
+  ycrdt_engine* e = d->e;
+  HIPCHK(hipSetDevice(e->device));
+  std::vector<ycrdt_buf> bufs;
+  for (const auto& q : d->queue) bufs.push_back(ycrdt_buf{q.bytes.data(), q.bytes.size()});
+  if (!d->ing.has_pending && !d->ing.has_ds && e->compat != 135) {
+    const int rc = commit_merge(d, bufs, nullptr);
+    if (rc != YCRDT_E_PENDING) {
+      if (rc == YCRDT_OK) { d->queue.clear(); d->queue_bytes = 0; }
+      return rc;
+    }
+  }
+  IngestState S = d->ing;
+  S.state.clear();
+  if (!parse_state_vector(d->sv.data(), d->sv.size(), S.state)) return fail(YCRDT_E_DEVICE, "internal: doc state vector");
+  const MergeFn mf = [e](const std::vector<const std::vector<uint8_t>*>& ins, std::vector<uint8_t>& out) {
+    return lazy_merge_host(e, ins, out);
+  };
+  std::string err;
+  for (const auto& q : d->queue) {
+    const int rc = read_update(S, q.bytes.data(), q.bytes.size(), q.local, mf, err);
+    if (rc) return fail(rc, err);
+  }
+  if (d->ing.has_pending) bufs.push_back(ycrdt_buf{d->ing.pending.data(), d->ing.pending.size()});
+  if (d->ing.has_ds) bufs.push_back(ycrdt_buf{d->ing.pending_ds.data(), d->ing.pending_ds.size()});
+  int rc = commit_merge(d, bufs, &S.state);
+  if (rc) return rc;
+  ClockMap got;
+  parse_state_vector(d->sv.data(), d->sv.size(), got);
+  for (auto it = S.state.begin(); it != S.state.end();) it = it->second ? std::next(it) : S.state.erase(it);
+  if (got != S.state) return fail(YCRDT_E_DEVICE, "internal: capped merge disagrees with the pending emulation");
+  d->ing = std::move(S);
+  d->queue.clear();
+  d->queue_bytes = 0;
+  return YCRDT_OK;
+}
+
+void enqueue(ycrdt_doc* d, const uint8_t* p, size_t n, bool local) {
+  d->queue.push_back(ycrdt_doc::Queued{std::vector<uint8_t>(p, p + n), local});
+  d->queue_bytes += n;
+  d->view.valid = false;
+}
+
+// 13.5.16 writes the state vector in store insertion order (Y@22723)
+void sv_in_order(const ycrdt_doc* d, std::vector<uint8_t>& out) {
+  ClockMap st;
+  parse_state_vector(d->sv.data(), d->sv.size(), st);
+  out.clear();
+  uint32_t n = 0;
+  std::vector<uint8_t> body;
+  for (const uint32_t c : d->ing.order) {
+    const auto it = st.find(c);
+    if (it == st.end() || !it->second) continue;
+    put_vu(body, c);
+    put_vu(body, it->second);
+    ++n;
+  }
+  put_vu(out, n);
+  out.insert(out.end(), body.begin(), body.end());
+}
+
+}  // namespace
+
+extern "C" {
+
+// Y.applyUpdate × n. Each update is validated now (Yjs decodes the struct section before it
+// changes anything, and throws on malformed input); the merge itself is deferred to the next read.
 int ycrdt_apply_updates(ycrdt_doc* d, const ycrdt_buf* ups, size_t n) {
   if (!d || (!ups && n)) return fail(YCRDT_E_ARG, "null arg");
   if (n == 0) return YCRDT_OK;
-  ycrdt_engine* e = d->e;
-  HIPCHK(hipSetDevice(e->device));
-  ycrdt_batch& b = scratch_batch(e);  // engine-owned: no hipMalloc / hipFree per call
-  int rc = stage(&b, ups, n, d->state_len ? &d->state : nullptr, d->state_len);
-  if (rc == YCRDT_OK) rc = run_merge(e, &b, nullptr);
-  if (rc == YCRDT_OK) {
-    // the merged canonical state becomes the doc state; the host keeps the state vector
-    if (!grow(d->state, e->out_bytes + 16)) rc = fail(YCRDT_E_DEVICE, "hipMalloc failed (doc state)");
-    else {
-      hipMemcpyAsync(d->state.p, e->w.out, e->out_bytes, hipMemcpyDeviceToDevice, e->stream);
-      d->state_len = e->out_bytes;
-      d->sv.resize(e->sv_bytes);
-      hipMemcpyAsync(d->sv.data(), e->w.sv_out, e->sv_bytes, hipMemcpyDeviceToHost, e->stream);
-      hipStreamSynchronize(e->stream);
-      d->last = e->last;
-      d->view.valid = false;
-    }
+  std::vector<UpdScan> sc(n);
+  std::vector<char> ok(n, 0);
+  size_t total = 0;
+  for (size_t i = 0; i < n; ++i) total += ups[i].len;
+  const size_t nt = total > (size_t(4) << 20) && n > 1 ? std::min<size_t>({n, 16, std::max(1u, std::thread::hardware_concurrency())}) : 1;
+  auto work = [&](size_t t) {
+    for (size_t i = t; i < n; i += nt) ok[i] = scan_update(ups[i].ptr, ups[i].len, false, sc[i]) ? 1 : 0;
+  };
+  if (nt > 1) {
+    std::vector<std::thread> th;
+    for (size_t t = 0; t < nt; ++t) th.emplace_back(work, t);
+    for (auto& t : th) t.join();
+  } else {
+    work(0);
   }
-  return rc;
+  for (size_t i = 0; i < n; ++i) {
+    if (!ok[i]) {
+      // Yjs integrates a well-formed struct section and the delete-set ranges read before the error
+      if (sc[i].structs_ok) {
+        const std::vector<uint8_t> r = repaired_update(ups[i].ptr, sc[i]);
+        enqueue(d, r.data(), r.size(), false);
+      }
+      return fail(YCRDT_E_DECODE, "Integer out of range! (malformed update " + std::to_string(i) + ")");
+    }
+    enqueue(d, ups[i].ptr, ups[i].len, false);
+  }
+  if (d->queue_bytes > QUEUE_FLUSH_BYTES) return flush(d);
+  return YCRDT_OK;
 }
 
 int ycrdt_apply_update(ycrdt_doc* d, ycrdt_buf update) { return ycrdt_apply_updates(d, &update, 1); }
+
+int ycrdt_doc_flush(ycrdt_doc* d) {
+  if (!d) return fail(YCRDT_E_ARG, "null doc");
+  return flush(d);
+}
+
+int ycrdt_doc_pending(ycrdt_doc* d, int* structs, int* delete_set) {
+  if (!d) return fail(YCRDT_E_ARG, "null doc");
+  const int rc = flush(d);
+  if (rc) return rc;
+  if (structs) *structs = d->ing.has_pending ? 1 : 0;
+  if (delete_set) *delete_set = d->ing.has_ds ? 1 : 0;
+  return YCRDT_OK;
+}
 
 int ycrdt_encode_state_as_update(ycrdt_doc* d, ycrdt_buf sv, ycrdt_out* out) {
   if (!d || !out) return fail(YCRDT_E_ARG, "null arg");
@@ -1003,37 +1176,68 @@ int ycrdt_encode_state_as_update(ycrdt_doc* d, ycrdt_buf sv, ycrdt_out* out) {
   out->len = 0;
   std::unordered_map<uint32_t, uint32_t> target;
   if (sv.len && !parse_sv(sv.ptr, sv.len, target)) return fail(YCRDT_E_DECODE, "Integer out of range! (state vector)");
-  if (!d->state_len) return empty_update(out);
+  int rc = flush(d);
+  if (rc) return rc;
   ycrdt_engine* e = d->e;
   HIPCHK(hipSetDevice(e->device));
-  if (target.empty()) {
-    out->ptr = (uint8_t*)malloc(d->state_len);
-    out->len = d->state_len;
-    HIPCHK(hipMemcpy(out->ptr, d->state.p, d->state_len, hipMemcpyDeviceToHost));
+  // writeStateAsUpdate (the integrated store)
+  std::vector<uint8_t> main;
+  if (!d->state_len) {
+    main = {0, 0};
+  } else if (target.empty()) {
+    main.resize(d->state_len);
+    HIPCHK(hipMemcpy(main.data(), d->state.p, d->state_len, hipMemcpyDeviceToHost));
+  } else {  // delta: re-run the (idempotent) merge of the canonical state with per-client start clocks
+    ycrdt_batch& b = scratch_batch(e);
+    rc = stage(&b, nullptr, 0, &d->state, d->state_len);
+    if (rc == YCRDT_OK) rc = run_merge(e, &b, &target);
+    if (rc) return rc;
+    main.resize(e->out_bytes);
+    HIPCHK(hipMemcpy(main.data(), e->w.out, e->out_bytes, hipMemcpyDeviceToHost));
+  }
+  if (!d->ing.has_pending && !d->ing.has_ds) {
+    out->len = main.size();
+    out->ptr = (uint8_t*)malloc(out->len);
+    if (!out->ptr) return fail(YCRDT_E_CAPACITY, "host allocation failed");
+    memcpy(out->ptr, main.data(), out->len);
     return YCRDT_OK;
   }
-  // delta: re-run the (idempotent) merge of the canonical state with per-client start clocks
-  ycrdt_batch& b = scratch_batch(e);  // engine-owned: no hipMalloc / hipFree per call
-  int rc = stage(&b, nullptr, 0, &d->state, d->state_len);
-  if (rc == YCRDT_OK) rc = run_merge(e, &b, &target);
-  if (rc == YCRDT_OK) {
-    out->ptr = (uint8_t*)malloc(e->out_bytes);
-    out->len = e->out_bytes;
-    if (hipMemcpy(out->ptr, e->w.out, e->out_bytes, hipMemcpyDeviceToHost) != hipSuccess) rc = fail(YCRDT_E_DEVICE, "D2H");
+  // encodeStateAsUpdateV2 (Y@22155): mergeUpdates([main, pendingDs, diffUpdate(pending, sv)])
+  std::vector<ycrdt_buf> parts{ycrdt_buf{main.data(), main.size()}};
+  if (d->ing.has_ds) parts.push_back(ycrdt_buf{d->ing.pending_ds.data(), d->ing.pending_ds.size()});
+  ycrdt_out pd{nullptr, 0};
+  if (d->ing.has_pending) {
+    static const uint8_t empty_sv[1] = {0};
+    const ycrdt_buf svb = sv.len ? sv : ycrdt_buf{empty_sv, 1};
+    rc = ycrdt_diff_update(e, ycrdt_buf{d->ing.pending.data(), d->ing.pending.size()}, svb, &pd);
+    if (rc) return rc;
+    parts.push_back(ycrdt_buf{pd.ptr, pd.len});
   }
+  rc = ycrdt_merge_updates(e, parts.data(), parts.size(), out);
+  ycrdt_free(&pd);
   return rc;
 }
 
 int ycrdt_encode_state_vector(ycrdt_doc* d, ycrdt_out* out) {
   if (!d || !out) return fail(YCRDT_E_ARG, "null arg");
-  out->len = d->sv.size();
+  out->ptr = nullptr;
+  out->len = 0;
+  const int rc = flush(d);
+  if (rc) return rc;
+  std::vector<uint8_t> ordered;
+  const std::vector<uint8_t>* src = &d->sv;
+  if (d->e->compat == 135) { sv_in_order(d, ordered); src = &ordered; }
+  out->len = src->size();
   out->ptr = (uint8_t*)malloc(out->len ? out->len : 1);
-  if (out->len) memcpy(out->ptr, d->sv.data(), out->len);
+  if (!out->ptr) { out->len = 0; return fail(YCRDT_E_CAPACITY, "host allocation failed"); }
+  if (out->len) memcpy(out->ptr, src->data(), out->len);
   return YCRDT_OK;
 }
 
 int ycrdt_doc_last_stats(ycrdt_doc* d, ycrdt_merge_stats* st) {
   if (!d || !st) return fail(YCRDT_E_ARG, "null arg");
+  const int rc = flush(d);
+  if (rc) return rc;
   *st = d->last;
   return YCRDT_OK;
 }
@@ -1055,6 +1259,7 @@ int ycrdt_batch_merge(ycrdt_batch* b, ycrdt_merge_stats* st) {
   int rc = run_merge(b->e, b, nullptr);
   if (rc == YCRDT_OK) {
     b->merged = true;
+    b->e->ws_owner = b;
     if (st) *st = b->e->last;
   }
   return rc;
@@ -1063,15 +1268,21 @@ int ycrdt_batch_merge(ycrdt_batch* b, ycrdt_merge_stats* st) {
 int ycrdt_batch_result(ycrdt_batch* b, ycrdt_out* update, ycrdt_out* sv) {
   if (!b || !b->merged) return fail(YCRDT_E_ARG, "batch not merged");
   ycrdt_engine* e = b->e;
+  // the result lives in the engine workspace until the next engine call overwrites it
+  if (e->ws_owner != b) return fail(YCRDT_E_ARG, "batch result no longer available (another engine call ran since ycrdt_batch_merge)");
   HIPCHK(hipSetDevice(e->device));
+  if (update) { update->ptr = nullptr; update->len = 0; }
+  if (sv) { sv->ptr = nullptr; sv->len = 0; }
   if (update) {
+    update->ptr = (uint8_t*)malloc(e->out_bytes ? e->out_bytes : 1);
+    if (!update->ptr) return fail(YCRDT_E_CAPACITY, "host allocation failed");
     update->len = e->out_bytes;
-    update->ptr = (uint8_t*)malloc(update->len ? update->len : 1);
     HIPCHK(hipMemcpy(update->ptr, e->w.out, update->len, hipMemcpyDeviceToHost));
   }
   if (sv) {
+    sv->ptr = (uint8_t*)malloc(e->sv_bytes ? e->sv_bytes : 1);
+    if (!sv->ptr) { ycrdt_free(update); return fail(YCRDT_E_CAPACITY, "host allocation failed"); }
     sv->len = e->sv_bytes;
-    sv->ptr = (uint8_t*)malloc(sv->len ? sv->len : 1);
     HIPCHK(hipMemcpy(sv->ptr, e->w.sv_out, sv->len, hipMemcpyDeviceToHost));
   }
   return YCRDT_OK;
@@ -1133,6 +1344,7 @@ int ycrdt_diff_updates(ycrdt_engine* e, const ycrdt_buf* updates, const ycrdt_bu
 void ycrdt_batch_destroy(ycrdt_batch* b) {
   if (!b) return;
   hipSetDevice(b->e->device);
+  if (b->e->ws_owner == b) b->e->ws_owner = nullptr;
   if (b->bytes.p) hipFree(b->bytes.p);
   if (b->meta.p) hipFree(b->meta.p);
   delete b;
@@ -1141,6 +1353,8 @@ void ycrdt_batch_destroy(ycrdt_batch* b) {
 // ---- crdt.c materialisation + local ops (yc_view.hip, yc_host.cpp)
 
 static int ensure_view(ycrdt_doc* d) {
+  int rc = flush(d);
+  if (rc) return rc;
   if (d->view.valid) return YCRDT_OK;
   if (!d->state_len) {
     d->view = HostView();
@@ -1150,10 +1364,13 @@ static int ensure_view(ycrdt_doc* d) {
   ycrdt_engine* e = d->e;
   HIPCHK(hipSetDevice(e->device));
   ycrdt_batch& b = scratch_batch(e);  // engine-owned: no hipMalloc / hipFree per call
-  int rc = stage(&b, nullptr, 0, &d->state, d->state_len);
-  if (rc == YCRDT_OK) rc = run_merge(e, &b, nullptr);  // idempotent on the canonical state
-  if (rc == YCRDT_OK) rc = run_view(e, &b, d->view);
-  return rc;
+  if (e->ws_owner != d) {  // the workspace no longer holds this doc's merge: redo it (idempotent)
+    rc = stage(&b, nullptr, 0, &d->state, d->state_len);
+    if (rc == YCRDT_OK) rc = run_merge(e, &b, nullptr);
+    if (rc) return rc;
+    e->ws_owner = d;
+  }
+  return run_view(e, &b, d->view);
 }
 
 static uint32_t next_clock(ycrdt_doc* d) {
@@ -1163,29 +1380,53 @@ static uint32_t next_clock(ycrdt_doc* d) {
   return it == sv.end() ? 0u : it->second;
 }
 
+// A local op's update joins the ingest queue as a local transaction (no pending retry / pendingDs
+// pass, like Yjs's local transact) and, when the host opted in, the incremental-delta list.
 static int apply_local(ycrdt_doc* d, const std::vector<uint8_t>& u) {
-  ycrdt_buf b{u.data(), u.size()};
-  const int rc = ycrdt_apply_updates(d, &b, 1);
-  if (rc == YCRDT_OK) d->local.push_back(u);  // the op's own update: the incremental wire delta
-  return rc;
+  enqueue(d, u.data(), u.size(), true);
+  if (!d->track_local) return YCRDT_OK;
+  d->local.push_back(u);
+  d->local_bytes += u.size();
+  if (d->local.size() > 4096 || d->local_bytes > (size_t(64) << 20)) {  // bound the list: fold it into one update
+    std::vector<ycrdt_buf> bufs;
+    for (const auto& x : d->local) bufs.push_back(ycrdt_buf{x.data(), x.size()});
+    ycrdt_out o{nullptr, 0};
+    const int rc = ycrdt_merge_updates(d->e, bufs.data(), bufs.size(), &o);
+    if (rc) return rc;
+    d->local.assign(1, std::vector<uint8_t>(o.ptr, o.ptr + o.len));
+    d->local_bytes = o.len;
+    ycrdt_free(&o);
+  }
+  return YCRDT_OK;
+}
+
+int ycrdt_doc_track_local(ycrdt_doc* d, int on) {
+  if (!d) return fail(YCRDT_E_ARG, "null doc");
+  d->track_local = on != 0;
+  if (!on) { d->local.clear(); d->local_bytes = 0; }
+  return YCRDT_OK;
 }
 
 int ycrdt_doc_take_local_update(ycrdt_doc* d, ycrdt_out* out) {
   if (!d || !out) return fail(YCRDT_E_ARG, "null arg");
   out->ptr = nullptr;
   out->len = 0;
-  std::vector<std::vector<uint8_t>> ops;
-  ops.swap(d->local);
+  d->track_local = true;  // from now on local ops are recorded for the next take
+  const std::vector<std::vector<uint8_t>>& ops = d->local;
   if (ops.empty()) return empty_update(out);
+  int rc = YCRDT_OK;
   if (ops.size() == 1) {  // Y.mergeUpdates returns a single input unchanged
+    out->ptr = (uint8_t*)malloc(ops[0].size() ? ops[0].size() : 1);
+    if (!out->ptr) return fail(YCRDT_E_CAPACITY, "host allocation failed");
     out->len = ops[0].size();
-    out->ptr = (uint8_t*)malloc(out->len);
     memcpy(out->ptr, ops[0].data(), out->len);
-    return YCRDT_OK;
+  } else {
+    std::vector<ycrdt_buf> bufs;
+    for (const auto& u : ops) bufs.push_back(ycrdt_buf{u.data(), u.size()});
+    rc = ycrdt_merge_updates(d->e, bufs.data(), bufs.size(), out);  // one update for the transaction
   }
-  std::vector<ycrdt_buf> bufs;
-  for (const auto& u : ops) bufs.push_back(ycrdt_buf{u.data(), u.size()});
-  return ycrdt_merge_updates(d->e, bufs.data(), bufs.size(), out);  // one update for the transaction
+  if (rc == YCRDT_OK) { d->local.clear(); d->local_bytes = 0; }  // on failure the ops stay for the next take
+  return rc;
 }
 
 static OpTarget target_of(const char* root, const char* parent_key) {
@@ -1290,6 +1531,54 @@ int ycrdt_array_delete(ycrdt_doc* d, const char* root, const char* parent_key, u
   }
   if (rc) return fail(rc, err);
   return YCRDT_OK;
+}
+
+int ycrdt_validate_update(ycrdt_buf update, int* structs_ok) {
+  UpdScan sc;
+  const bool ok = scan_update(update.ptr, update.len, false, sc);
+  if (structs_ok) *structs_ok = sc.structs_ok ? 1 : 0;
+  return ok ? YCRDT_OK : fail(YCRDT_E_DECODE, "Integer out of range!");
+}
+
+static int out_copy(ycrdt_out* o, const std::vector<uint8_t>& v) {
+  if (!o) return YCRDT_OK;
+  o->ptr = (uint8_t*)malloc(v.size() ? v.size() : 1);
+  if (!o->ptr) { o->len = 0; return fail(YCRDT_E_CAPACITY, "host allocation failed"); }
+  o->len = v.size();
+  if (!v.empty()) memcpy(o->ptr, v.data(), v.size());
+  return YCRDT_OK;
+}
+
+int ycrdt_debug_replay(const ycrdt_buf* ups, size_t n, ycrdt_merge_fn merge, void* ctx, ycrdt_out* sv, ycrdt_out* pending,
+                       ycrdt_out* pending_ds) {
+  if ((!ups && n) || !merge) return fail(YCRDT_E_ARG, "null arg");
+  IngestState S;
+  const MergeFn mf = [merge, ctx](const std::vector<const std::vector<uint8_t>*>& ins, std::vector<uint8_t>& out) -> int {
+    std::vector<ycrdt_buf> b;
+    for (const auto* v : ins) b.push_back(ycrdt_buf{v->data(), v->size()});
+    ycrdt_out o{nullptr, 0};
+    const int rc = merge(ctx, b.data(), b.size(), &o);
+    if (rc) return rc;
+    out.assign(o.ptr, o.ptr + o.len);
+    return (int)YCRDT_OK;
+  };
+  std::string err;
+  for (size_t i = 0; i < n; ++i) {
+    UpdScan sc;
+    if (!scan_update(ups[i].ptr, ups[i].len, false, sc)) return fail(YCRDT_E_DECODE, "Integer out of range!");
+    const int rc = read_update(S, ups[i].ptr, ups[i].len, false, mf, err);
+    if (rc) return fail(rc, err);
+  }
+  std::vector<uint8_t> s;
+  uint32_t k = 0;
+  std::vector<uint8_t> body;
+  for (const auto& kv : S.state) { put_vu(body, kv.first); put_vu(body, kv.second); ++k; }
+  put_vu(s, k);
+  s.insert(s.end(), body.begin(), body.end());
+  int rc = out_copy(sv, s);
+  if (!rc) rc = out_copy(pending, S.has_pending ? S.pending : std::vector<uint8_t>());
+  if (!rc) rc = out_copy(pending_ds, S.has_ds ? S.pending_ds : std::vector<uint8_t>());
+  return rc;
 }
 
 int ycrdt_doc_client_id(ycrdt_doc* d, uint32_t* out) {

@@ -47,13 +47,17 @@ __global__ __launch_bounds__(256) void k_owner(Work w, uint32_t nstructs) {
       const uint32_t ref = w.s_info[s] & 31u;
       if (ref != REF_SKIP) {
         const uint32_t cidx = w.s_cidx[s];
-        const uint64_t gb = w.cl_base[cidx] + w.s_clock[s] - P[s];
+        const uint32_t clock = w.s_clock[s], st = w.cl_state[cidx];
+        const uint64_t gb = w.cl_base[cidx] + clock - P[s];
         const uint32_t fl = ref == REF_DELETED ? UF_DEL : (ref == REF_GC ? (UF_GC | UF_DEL) : 0u);
-        for (; j < send; ++j) {
+        // units at or past the client's (capped) state stay out of the store
+        const uint64_t lim = min(send, P[s] + (st > clock ? (uint64_t)(st - clock) : 0ull));
+        for (; j < lim; ++j) {
           const uint32_t g = (uint32_t)(gb + j);
           atomicMin(&w.u_owner[g], s);
           if (fl) atomicOr(&w.u_flags[g], fl);
         }
+        j = send;
       } else j = send;
     }
   }
@@ -67,9 +71,11 @@ __global__ void k_ds_prep(Work w, uint32_t nds, uint32_t nclients) {
   const uint32_t c = lower_bound_u32(w.cl_vals, nclients, r.client);
   uint32_t len = r.len;
   if (len == 0) { w.ds_len[i] = 0; return; }
-  if (c >= nclients || w.cl_vals[c] != r.client) { raise_err(&w.ctr->err, ERR_PENDING); w.ds_len[i] = 0; return; }
+  // a range past the known state is Yjs's pendingDs: an error here (the host then takes the pending
+  // path), clipped silently when the host already computed the caps
+  if (c >= nclients || w.cl_vals[c] != r.client) { if (!w.capped) raise_err(&w.ctr->err, ERR_PENDING); w.ds_len[i] = 0; return; }
   const uint64_t endc = (uint64_t)r.clock + len;
-  if (endc > w.cl_state[c]) { raise_err(&w.ctr->err, ERR_PENDING); len = r.clock < w.cl_state[c] ? w.cl_state[c] - r.clock : 0; }
+  if (endc > w.cl_state[c]) { if (!w.capped) raise_err(&w.ctr->err, ERR_PENDING); len = r.clock < w.cl_state[c] ? w.cl_state[c] - r.clock : 0; }
   r.client = c;
   w.ds[i] = r;
   w.ds_len[i] = len;
@@ -99,10 +105,13 @@ __global__ __launch_bounds__(256) void k_ds_mark(Work w, uint32_t nds) {
 __global__ void k_refs(Work w, uint32_t nstructs) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= nstructs) return;
+  if (w.s_clock[i] >= w.cl_state[w.s_cidx[i]] || (w.s_info[i] & 31u) == REF_SKIP) return;  // not integrated
+  // Item.getMissing (Y@76507): every reference of an integrated struct must be in the store
+  if (w.s_pk[i] == 2 && (w.s_pa[i] == UNKNOWN || w.s_pb[i] >= w.cl_state[w.s_pa[i]])) { raise_err(&w.ctr->err, ERR_PENDING); return; }
   const uint32_t oc = w.s_ocidx[i];
   if (oc != NONE) {
     const uint32_t k = w.s_oclock[i];
-    if (k >= w.cl_state[oc]) { raise_err(&w.ctr->err, ERR_PENDING); return; }
+    if (oc == UNKNOWN || k >= w.cl_state[oc]) { raise_err(&w.ctr->err, ERR_PENDING); return; }
     const uint32_t g = (uint32_t)(w.cl_base[oc] + k);
     // getItemCleanEnd(origin); only UF_CUT is written to u_flags in this kernel, so a plain
     // read-modify-write that races with another writer of the same bit is harmless
@@ -111,7 +120,7 @@ __global__ void k_refs(Work w, uint32_t nstructs) {
   const uint32_t rc = w.s_rcidx[i];
   if (rc != NONE) {
     const uint32_t k = w.s_rclock[i];
-    if (k >= w.cl_state[rc]) { raise_err(&w.ctr->err, ERR_PENDING); return; }
+    if (rc == UNKNOWN || k >= w.cl_state[rc]) { raise_err(&w.ctr->err, ERR_PENDING); return; }
     const uint32_t g = (uint32_t)(w.cl_base[rc] + k);
     if (!(w.u_flags[g] & UF_CUT)) w.u_flags[g] |= UF_CUT;              // getItemCleanStart(rightOrigin)
   }
@@ -248,7 +257,7 @@ __global__ __launch_bounds__(256) void k_seg_props(Work w, uint32_t nsegs) {
       h = fnv_bytes(h, w.bytes + w.s_pa[own], w.s_pb[own]);
     } else if (pk == 2) {
       const uint32_t pc = w.s_pa[own], pclock = w.s_pb[own];
-      if (pc == NONE || pclock >= w.cl_state[pc]) { raise_err(&w.ctr->err, ERR_PENDING); gc = true; }
+      if (pc == NONE || pc == UNKNOWN || pclock >= w.cl_state[pc]) { raise_err(&w.ctr->err, ERR_PENDING); gc = true; }
       else {
         parent = (uint32_t)(w.cl_base[pc] + pclock);
         if (w.u_flags[parent] & UF_GC) gc = true;

@@ -1,0 +1,259 @@
+// yc_parse.h — the Yjs v1 / lib0 byte grammar, shared by the gfx950 decoder and the host-side
+// update scanner (yc_ingest.cpp), so that both refuse exactly the same inputs.
+//
+// Compiled by hipcc (as part of yc_common.h, __host__ __device__) and by g++ (plain inline).
+#pragma once
+#include <cstdint>
+
+#if defined(__HIP__) || defined(__HIPCC__)
+#define YC_HD __host__ __device__
+#define YC_HDI __host__ __device__ __forceinline__
+#else
+#define YC_HD
+#define YC_HDI inline __attribute__((always_inline))
+#endif
+
+namespace yc {
+
+// content refs (low 5 bits of the info byte)
+enum : uint8_t {
+  REF_GC = 0, REF_DELETED = 1, REF_JSON = 2, REF_BINARY = 3, REF_STRING = 4, REF_EMBED = 5,
+  REF_FORMAT = 6, REF_TYPE = 7, REF_ANY = 8, REF_DOC = 9, REF_SKIP = 10
+};
+
+// ---------------------------------------------------------------- lib0 readers (L0@1937)
+// readVarUint: 7-bit groups with 32-bit shift-or accumulation (lib0 0.2.42). A 6th
+// continuation byte or running past `end` is "Integer out of range!".
+YC_HDI uint32_t rd_vu(const uint8_t* __restrict__ b, uint32_t& p, uint32_t end, bool& ok) {
+  uint32_t v = 0;
+  uint32_t shift = 0;
+#pragma unroll 1
+  for (;;) {
+    if (p >= end) { ok = false; return 0; }
+    uint32_t r = b[p++];
+    if (shift < 32) v |= (r & 0x7fu) << shift;
+    shift += 7;
+    if (r < 0x80u) return v;
+    if (shift > 35) { ok = false; return 0; }
+  }
+}
+
+// readVarInt: sign bit 0x40 in the first byte, 6+7k bits, error past 41 bits.
+YC_HDI void skip_vi(const uint8_t* __restrict__ b, uint32_t& p, uint32_t end, bool& ok) {
+  if (p >= end) { ok = false; return; }
+  uint32_t r = b[p++];
+  if (!(r & 0x80u)) return;
+  uint32_t shift = 6;
+#pragma unroll 1
+  for (;;) {
+    if (p >= end) { ok = false; return; }
+    r = b[p++];
+    shift += 7;
+    if (r < 0x80u) return;
+    if (shift > 41) { ok = false; return; }
+  }
+}
+
+// A ContentJSON / ContentEmbed / ContentFormat value is JSON.stringify output, decoded by Yjs
+// with JSON.parse (Y@71000..): text that cannot start a JSON value (or is empty) makes Yjs throw,
+// so the decoder rejects it too. This also lets speculative parses of non-struct bytes fail fast.
+YC_HDI bool json_start_ok(uint32_t c) {
+  return c == '{' || c == '[' || c == '"' || c == 't' || c == 'f' || c == 'n' || c == 'u' || c == '-' ||
+         (c >= '0' && c <= '9') || c == ' ' || c == '\t' || c == '\n' || c == '\r';
+}
+
+YC_HDI void skip_bytes(uint32_t& p, uint32_t n, uint32_t end, bool& ok) {
+  if (end - p < n) { ok = false; p = end; return; }
+  p += n;
+}
+
+// readAny (L0@1937 B): iterative skip with an explicit container stack of depth DEPTH (deeper
+// nesting fails the parse: speculative callers use a shallow stack, exact callers a deep one).
+template <int DEPTH>
+YC_HD inline bool skip_any(const uint8_t* __restrict__ b, uint32_t& p, uint32_t end, uint32_t& steps) {
+  uint32_t rem[DEPTH];
+  uint32_t objmask = 0;  // bit d set: level d is an object (key before each member)
+  int d = 0;
+  bool ok = true;
+#pragma unroll 1
+  for (;;) {
+    if (steps == 0) return false;
+    --steps;
+    if (p >= end) return false;
+    uint32_t tag = b[p++];
+    switch (tag) {
+      case 127: case 126: case 121: case 120: break;
+      case 125: skip_vi(b, p, end, ok); break;
+      case 124: skip_bytes(p, 4, end, ok); break;
+      case 123: case 122: skip_bytes(p, 8, end, ok); break;
+      case 119: case 116: { uint32_t n = rd_vu(b, p, end, ok); if (ok) skip_bytes(p, n, end, ok); break; }
+      case 118: case 117: {
+        uint32_t n = rd_vu(b, p, end, ok);
+        if (!ok) return false;
+        if (n > 0) {
+          if (d == DEPTH) { steps = 0; return false; }  // too deep: "unknown" (-1), never "malformed"
+          rem[d] = n;
+          if (tag == 118) objmask |= 1u << d; else objmask &= ~(1u << d);
+          ++d;
+          if (tag == 118) { uint32_t k = rd_vu(b, p, end, ok); if (ok) skip_bytes(p, k, end, ok); }
+          if (!ok) return false;
+          continue;  // read the first member value
+        }
+        break;
+      }
+      default: return false;
+    }
+    if (!ok) return false;
+    // a value completed: pop finished containers
+#pragma unroll 1
+    for (;;) {
+      if (d == 0) return true;
+      if (--rem[d - 1] > 0) {
+        if ((objmask >> (d - 1)) & 1u) { uint32_t k = rd_vu(b, p, end, ok); if (ok) skip_bytes(p, k, end, ok); if (!ok) return false; }
+        break;  // next member value
+      }
+      --d;
+    }
+  }
+}
+
+// Decoded view of one struct (Y@19286 readClientsStructRefs + readItemContent).
+struct StructView {
+  uint8_t info;
+  uint8_t ref;
+  uint8_t pkind;       // 0 none, 1 root name, 2 parent id
+  uint8_t has_psub;
+  uint32_t len;        // clock length
+  uint32_t oc, ok_;    // origin (client, clock) valid if info&0x80
+  uint32_t rc, rk;     // right origin valid if info&0x40
+  uint32_t pa, pb;     // root name: (pos of varString, byte length incl. prefix) | parent id (client, clock)
+  uint32_t psub_pos, psub_len;  // varString (incl. length prefix)
+  uint32_t cpos, cend; // content bytes [cpos, cend)
+  uint32_t nel;        // Any/JSON element count
+};
+
+// Parses one struct starting at p. FULL fills `v`. Speculative callers pass a finite
+// step budget; exact callers pass 0xFFFFFFFF. Returns 1 = ok, 0 = malformed, -1 = budget hit,
+// -2 = ran past `end` (only distinguishable from 0 when `end` is not the update end).
+template <bool FULL, int DEPTH = 32>
+YC_HD inline int parse_struct(const uint8_t* __restrict__ b, uint32_t& p, uint32_t end, uint32_t steps, StructView* v) {
+  bool ok = true;
+  if (p >= end) return -2;
+  uint32_t info = b[p++];
+  uint32_t ref = info & 31u;
+  if (FULL) { v->info = (uint8_t)info; v->ref = (uint8_t)ref; v->pkind = 0; v->has_psub = 0; v->nel = 0; }
+  if (ref == REF_GC || ref == REF_SKIP) {
+    uint32_t len = rd_vu(b, p, end, ok);
+    if (FULL) { v->len = len; v->cpos = v->cend = p; }
+    return ok ? 1 : (p >= end ? -2 : 0);
+  }
+  if (ref > REF_DOC) return 0;
+  if (info & 0x80u) {
+    uint32_t c = rd_vu(b, p, end, ok), k = rd_vu(b, p, end, ok);
+    if (FULL) { v->oc = c; v->ok_ = k; }
+  }
+  if (info & 0x40u) {
+    uint32_t c = rd_vu(b, p, end, ok), k = rd_vu(b, p, end, ok);
+    if (FULL) { v->rc = c; v->rk = k; }
+  }
+  if (!ok) return p >= end ? -2 : 0;
+  if ((info & 0xC0u) == 0) {
+    uint32_t pinfo = rd_vu(b, p, end, ok);
+    if (!ok) return p >= end ? -2 : 0;
+    if (pinfo == 1) {
+      uint32_t st = p;
+      uint32_t n = rd_vu(b, p, end, ok);
+      if (ok) skip_bytes(p, n, end, ok);
+      if (FULL) { v->pkind = 1; v->pa = st; v->pb = p - st; }
+    } else {
+      uint32_t c = rd_vu(b, p, end, ok), k = rd_vu(b, p, end, ok);
+      if (FULL) { v->pkind = 2; v->pa = c; v->pb = k; }
+    }
+    if (info & 0x20u) {
+      uint32_t st = p;
+      uint32_t n = rd_vu(b, p, end, ok);
+      if (ok) skip_bytes(p, n, end, ok);
+      if (FULL) { v->has_psub = 1; v->psub_pos = st; v->psub_len = p - st; }
+    }
+    if (!ok) return p >= end ? -2 : 0;
+  }
+  uint32_t cpos = p;
+  uint32_t len = 1;
+  switch (ref) {
+    case REF_DELETED: len = rd_vu(b, p, end, ok); break;
+    case REF_JSON: {
+      uint32_t n = rd_vu(b, p, end, ok);
+      len = n;
+      for (uint32_t i = 0; i < n && ok; ++i) {
+        if (steps == 0) return -1;
+        --steps;
+        uint32_t k = rd_vu(b, p, end, ok);
+        if (ok && (k == 0 || (p < end && !json_start_ok(b[p])))) return 0;
+        if (ok) skip_bytes(p, k, end, ok);
+      }
+      if (FULL) v->nel = n;
+      if (ok && steps == 0) return -1;
+      break;
+    }
+    case REF_BINARY: { uint32_t k = rd_vu(b, p, end, ok); if (ok) skip_bytes(p, k, end, ok); break; }
+    case REF_EMBED: {
+      uint32_t k = rd_vu(b, p, end, ok);
+      if (ok && (k == 0 || (p < end && !json_start_ok(b[p])))) return 0;
+      if (ok) skip_bytes(p, k, end, ok);
+      break;
+    }
+    case REF_STRING: {
+      uint32_t k = rd_vu(b, p, end, ok);
+      uint32_t st = p;
+      if (ok) skip_bytes(p, k, end, ok);
+      if (ok && FULL) {  // ContentString length counts UTF-16 code units
+        uint32_t u = 0;
+        for (uint32_t i = st; i < st + k; ++i) {
+          uint32_t c = b[i];
+          if ((c & 0xC0u) != 0x80u) u += (c >= 0xF0u) ? 2u : 1u;
+        }
+        len = u;
+      }
+      break;
+    }
+    case REF_FORMAT: {
+      uint32_t k = rd_vu(b, p, end, ok);
+      if (ok) skip_bytes(p, k, end, ok);
+      k = rd_vu(b, p, end, ok);
+      if (ok && (k == 0 || (p < end && !json_start_ok(b[p])))) return 0;
+      if (ok) skip_bytes(p, k, end, ok);
+      break;
+    }
+    case REF_TYPE: {
+      uint32_t tr = rd_vu(b, p, end, ok);
+      if (ok && (tr == 3 || tr == 5)) { uint32_t k = rd_vu(b, p, end, ok); if (ok) skip_bytes(p, k, end, ok); }
+      if (tr > 6) ok = false;
+      break;
+    }
+    case REF_ANY: {
+      uint32_t n = rd_vu(b, p, end, ok);
+      len = n;
+      for (uint32_t i = 0; i < n && ok; ++i) ok = skip_any<DEPTH>(b, p, end, steps);
+      if (!ok && steps == 0) return -1;
+      if (FULL) v->nel = n;
+      break;
+    }
+    case REF_DOC: {
+      uint32_t k = rd_vu(b, p, end, ok);
+      if (ok) skip_bytes(p, k, end, ok);
+      if (ok) ok = skip_any<DEPTH>(b, p, end, steps);
+      if (!ok && steps == 0) return -1;
+      break;
+    }
+    default: return 0;
+  }
+  if (FULL) { v->len = len; v->cpos = cpos; v->cend = p; }
+  if (!ok && p >= end) return -2;  // ran out of input (the struct may continue past `end`)
+  return ok ? 1 : 0;
+}
+
+YC_HDI uint32_t vu_size_host(uint32_t v) {
+  return v < (1u << 7) ? 1 : v < (1u << 14) ? 2 : v < (1u << 21) ? 3 : v < (1u << 28) ? 4 : 5;
+}
+
+}  // namespace yc

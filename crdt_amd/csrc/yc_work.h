@@ -118,6 +118,12 @@ struct Work {
   uint32_t* cl_state = nullptr;    // per client state (max end clock)
   uint64_t* cl_base = nullptr;     // [NC+1] exclusive prefix of states (unit base)
   uint32_t* cl_start = nullptr;    // per client start clock for diff encodes (sv); 0 = full
+  // per-client integration caps (Yjs pending structs, yc_ingest.h): sorted (client, cap) pairs;
+  // units at or past a client's cap are left out of the merge and delete-set ranges clipped to it
+  const uint32_t* cap_client = nullptr;
+  const uint32_t* cap_clock = nullptr;
+  uint32_t ncaps = 0;
+  uint32_t capped = 0;             // 1: caps given (clip silently); 0: anything missing is ERR_PENDING
   // ---- per unit (U)
   uint32_t* u_owner = nullptr;
   uint32_t* u_flags = nullptr;

@@ -240,6 +240,7 @@ module.exports = {
   // opt-in incremental local-op encode (not in Yjs): the doc's local ops since the previous call as
   // one update, instead of re-encoding the whole doc after every op (crdt.js:347,383,443,...)
   takeLocalUpdate: (doc) => binding.takeLocalUpdate(doc._h),
+  trackLocalUpdates: (doc, on = true) => binding.trackLocalUpdates(doc._h, on),
   lastStats: (doc) => binding.lastStats(doc._h),
   version: binding.version,
   setDevice: binding.setDevice,

@@ -211,6 +211,20 @@ static napi_value js_take_local_update(napi_env env, napi_callback_info info) {
   return u8_from_out(env, &o);
 }
 
+/* trackLocalUpdates(doc[, on = true]): record local-op updates for takeLocalUpdate (opt-in) */
+static napi_value js_track_local(napi_env env, napi_callback_info info) {
+  size_t argc = 2;
+  napi_value argv[2];
+  CHECK(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+  ycrdt_doc *d = argc > 0 ? get_doc(env, argv[0]) : NULL;
+  if (!d) return NULL;
+  bool on = true;
+  if (argc > 1) CHECK(env, napi_get_value_bool(env, argv[1], &on));
+  int rc = ycrdt_doc_track_local(d, on ? 1 : 0);
+  if (rc != YCRDT_OK) return throw_rc(env, rc);
+  return NULL;
+}
+
 /* lastStats(doc) → {items, structs, units, segments, outBytes, deviceMs} */
 static napi_value js_last_stats(napi_env env, napi_callback_info info) {
   size_t argc = 1;
@@ -492,6 +506,7 @@ static napi_value init(napi_env env, napi_value exports) {
       {"diffUpdate", NULL, js_diff_update, NULL, NULL, NULL, napi_default, NULL},
       {"diffUpdates", NULL, js_diff_updates, NULL, NULL, NULL, napi_default, NULL},
       {"takeLocalUpdate", NULL, js_take_local_update, NULL, NULL, NULL, napi_default, NULL},
+      {"trackLocalUpdates", NULL, js_track_local, NULL, NULL, NULL, napi_default, NULL},
       {"lastStats", NULL, js_last_stats, NULL, NULL, NULL, napi_default, NULL},
       {"version", NULL, js_version, NULL, NULL, NULL, napi_default, NULL},
       {"mapTypeAt", NULL, js_map_type_at, NULL, NULL, NULL, napi_default, NULL},

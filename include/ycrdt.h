@@ -35,7 +35,7 @@ typedef struct { uint8_t *ptr; size_t len; } ycrdt_out;       /* library-owned *
 enum {
   YCRDT_OK = 0,
   YCRDT_E_DECODE = -1,      /* malformed update (Yjs: Error('Integer out of range!')) */
-  YCRDT_E_PENDING = -2,     /* missing dependencies; Yjs would park the structs as pending */
+  YCRDT_E_PENDING = -2,     /* internal: missing dependencies seen by a merge that must have none */
   YCRDT_E_UNSUPPORTED = -3, /* valid Yjs input outside the engine's coverage */
   YCRDT_E_CAPACITY = -4,
   YCRDT_E_DEVICE = -5,      /* no HIP device / HIP runtime error */
@@ -67,10 +67,23 @@ int ycrdt_engine_phase_times(ycrdt_engine *e, const char **names, double *ms, in
 /* new Y.Doc()  (crdt.js:33,54,56,80,221) */
 int ycrdt_doc_create(ycrdt_engine *e, uint32_t client_id, ycrdt_doc **out);
 void ycrdt_doc_destroy(ycrdt_doc *d);
-/* Y.applyUpdate(doc, u8)  (crdt.js:35,56,58,85,294) */
+/* Y.applyUpdate(doc, u8)  (crdt.js:35,56,58,85,294). Yjs semantics, including missing
+ * dependencies: structs whose dependencies are unknown are parked (Yjs store.pendingStructs /
+ * pendingDs, readUpdateV2 Y@21330), retried when a later update supplies them, and emitted by
+ * ycrdt_encode_state_as_update exactly as Yjs does. The update is validated now (a malformed one
+ * fails with YCRDT_E_DECODE: the doc is unchanged if the struct section is malformed; a malformed
+ * delete set keeps the structs and the ranges read before the error, as in Yjs); the merge itself
+ * is DEFERRED to the next read of the doc (encode*, json, map_type_at, a local op, flush), so a
+ * burst of n applies costs one batched merge (crdt.js:294 onData bursts, crdt.js:79-98 replay). */
 int ycrdt_apply_update(ycrdt_doc *d, ycrdt_buf update);
-/* n sequential Y.applyUpdate calls, merged in one batch (LevelDB replay crdt.js:79-98, ingest) */
+/* n sequential Y.applyUpdate calls (LevelDB replay crdt.js:79-98, ingest); stops at the first
+ * malformed update, as a loop of Y.applyUpdate would. */
 int ycrdt_apply_updates(ycrdt_doc *d, const ycrdt_buf *ups, size_t n);
+/* Runs the deferred applies now (every read does this implicitly). */
+int ycrdt_doc_flush(ycrdt_doc *d);
+/* Whether Yjs would hold pending structs (store.pendingStructs) / a pending delete set
+ * (store.pendingDs) for this doc. */
+int ycrdt_doc_pending(ycrdt_doc *d, int *structs, int *delete_set);
 /* Y.encodeStateAsUpdate(doc[, sv])  (crdt.js:56,260,288,347,383,443,471,505,533,560,585,611);
  * sv.len == 0 ⇒ full state */
 int ycrdt_encode_state_as_update(ycrdt_doc *d, ycrdt_buf sv, ycrdt_out *out);
@@ -128,6 +141,9 @@ int ycrdt_doc_client_id(ycrdt_doc *d, uint32_t *out);
  * this delta is wire-compatible (Y.applyUpdate accepts it) but changes the bytes on the wire, so a
  * host opts in. Remote updates applied in between are not part of it. */
 int ycrdt_doc_take_local_update(ycrdt_doc *d, ycrdt_out *out);
+/* Starts (on != 0) or stops recording local-op updates for ycrdt_doc_take_local_update. Off by
+ * default; the first take turns it on. A long untaken list is folded into one update. */
+int ycrdt_doc_track_local(ycrdt_doc *d, int on);
 
 /* ---- device-resident batches (ingest queue / benchmark) ---------------------------------- */
 /* Copies the updates into HBM. */
@@ -135,9 +151,23 @@ int ycrdt_batch_stage(ycrdt_engine *e, const ycrdt_buf *ups, size_t n, ycrdt_bat
 /* Merges the staged updates into a fresh doc entirely on the device; the encoded state stays in
  * HBM. Equivalent to applying every update to a new Y.Doc and encodeStateAsUpdate(doc). */
 int ycrdt_batch_merge(ycrdt_batch *b, ycrdt_merge_stats *st);
-/* Copies the last merge result (encoded update and state vector) to the host. */
+/* Copies the merge result (encoded update and state vector) to the host. The result lives in the
+ * engine workspace: any other engine call in between makes this fail with YCRDT_E_ARG. */
 int ycrdt_batch_result(ycrdt_batch *b, ycrdt_out *update, ycrdt_out *state_vector);
 void ycrdt_batch_destroy(ycrdt_batch *b);
+
+/* ---- host-only entry points (no HIP device needed) ---------------------------------------- */
+/* The validation Y.applyUpdate runs before queueing an update: YCRDT_OK, or YCRDT_E_DECODE with
+ * *structs_ok = 1 when only the delete set is malformed (Yjs then keeps the structs). */
+int ycrdt_validate_update(ycrdt_buf update, int *structs_ok);
+/* Test hook for the pending-struct emulation (yc_ingest.cpp): replays n Y.applyUpdate calls into
+ * an empty doc on struct headers only, with Y.mergeUpdates supplied by the caller (`merge` fills
+ * *out with caller-owned bytes that must stay valid until it returns). Outputs the store's state
+ * vector (clients ascending), the pending-structs update (len 0 = none) and the pending delete set
+ * (len 0 = none); release them with ycrdt_free. */
+typedef int (*ycrdt_merge_fn)(void *ctx, const ycrdt_buf *ups, size_t n, ycrdt_out *out);
+int ycrdt_debug_replay(const ycrdt_buf *ups, size_t n, ycrdt_merge_fn merge, void *ctx, ycrdt_out *sv,
+                       ycrdt_out *pending, ycrdt_out *pending_ds);
 
 void ycrdt_free(ycrdt_out *o);
 const char *ycrdt_last_error(void);

@@ -1,6 +1,6 @@
 """GPU edge cases of the merge path, each checked against the CPU oracle (oracle/yref.c).
 
-Empty and ragged batches, malformed and pending input (atomic refusal, doc unchanged), structs
+Empty and ragged batches, malformed input (atomic refusal, doc unchanged), pending input, structs
 longer than the sizer's 15-bit tables and longer than a 16 KiB decode group, client ids at the
 ends of the u32 range, unicode keys / values, delete-set-only updates, duplicates and many tiny
 updates. Reference semantics: Y.applyUpdate / Y.encodeStateAsUpdate (crdt.js:35,56,294 / 347).
@@ -65,11 +65,26 @@ def test_malformed_is_refused_atomically():
     for bad in (b"\xff\xff", good[:-3], good[:5], b"\x01\x01\x07\x00\x28\x01"):
         with pytest.raises(crdt_amd.YcrdtError) as ei:
             d.apply_update(bad)
-        assert ei.value.kind in ("DECODE", "PENDING")
+        assert ei.value.kind == "DECODE"
         assert d.encode_state_as_update() == before  # the doc is unchanged
 
 
-def test_pending_is_refused_atomically():
+def test_malformed_delete_set_keeps_structs():
+    """Yjs decodes and integrates the struct section before it reads the delete set (Y@21330): an
+    update whose delete set is cut off throws, but its structs stay in the doc."""
+    a = ODoc(7)
+    a.map_set("users", "k", any_int(5))
+    good = a.encode_state_as_update()
+    d = crdt_amd.Doc(client_id=1)
+    with pytest.raises(crdt_amd.YcrdtError) as ei:
+        d.apply_update(good[:-1])
+    assert ei.value.kind == "DECODE"
+    assert d.encode_state_as_update() == good
+
+
+def test_missing_dependencies_are_pending_not_refused():
+    """Y.applyUpdate of an update whose predecessor is missing parks it (Yjs pendingStructs); the
+    predecessor then integrates both (the exact bytes while pending: test_gpu_pending.py)."""
     a = ODoc(9)
     a.map_set("users", "x", any_int(1))
     u1 = a.encode_state_as_update()
@@ -77,11 +92,12 @@ def test_pending_is_refused_atomically():
     a.map_set("users", "x", any_int(2))
     u2 = a.encode_state_as_update(sv1)  # depends on u1
     d = crdt_amd.Doc(client_id=1)
-    with pytest.raises(crdt_amd.YcrdtError) as ei:
-        d.apply_update(u2)
-    assert ei.value.kind == "PENDING"
-    assert d.encode_state_as_update() == b"\x00\x00"
-    d.apply_updates([u2, u1])  # one batch: the merge is order independent
+    d.apply_update(u2)
+    # the delta carries the full delete set: x=1 (clock 0), not integrated yet, is a pending range
+    assert d.pending() == (True, True)
+    assert d.encode_state_vector() == b"\x00"
+    d.apply_update(u1)
+    assert d.pending() == (False, False)
     ref = ODoc(1)
     ref.apply_update(u1)
     ref.apply_update(u2)

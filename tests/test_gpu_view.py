@@ -95,6 +95,7 @@ def test_gpu_local_delta_replay(every):
     reaches the Yjs-recorded state bytes, wherever a delta has been delivered."""
     for c in _ops()[::3]:
         a = crdt_amd.Doc(client_id=c["client"])
+        a.track_local(True)  # the host opted in to delta broadcast
         b = crdt_amd.Doc(client_id=0x7FFFFFF1)
         pending = 0
         for i, s in enumerate(c["steps"]):
@@ -112,3 +113,17 @@ def test_gpu_local_delta_replay(every):
             if not pending:
                 assert b.encode_state_as_update().hex() == s["state"], (c["name"], i, s["op"])
         assert a.take_local_update() == b"\x00\x00"  # nothing new since the last take
+
+
+def test_local_ops_untracked_stay_bounded():
+    """Without delta tracking, local ops record nothing (the list used to grow for the
+    doc's lifetime); a take then turns tracking on for the ops that follow."""
+    d = crdt_amd.Doc(client_id=77)
+    for i in range(50):
+        d.map_set("users", f"k{i % 5}", bytes([125, i]))
+    assert d.take_local_update() == b"\x00\x00"
+    d.map_set("users", "k0", bytes([125, 99]))
+    u = d.take_local_update()
+    peer = crdt_amd.Doc(client_id=78)
+    peer.apply_update(u)
+    assert peer.pending()[0]  # the op's origin is an item the peer never received
