@@ -127,6 +127,36 @@ def cpu_baselines(args, cfg, updates, out_update, st, eng, gen_map):
     return res
 
 
+def apply_loop_leg(eng, updates, out_update):
+    """crdt.js's own ingest shape (onData per message crdt.js:294, LevelDB replay crdt.js:79-98):
+    one Y.applyUpdate call per update of the C2 batch through the C ABI (host buffers), then ONE
+    read (Y.encodeStateAsUpdate). Each apply validates on the host and queues; the read merges the
+    whole queue in one device pass, so the loop costs about one merge, not 1,001. Output compared
+    with the batched merge's."""
+    import crdt_amd
+
+    reps = 3
+    loop_ms = read_ms = 0.0
+    same = True
+    for _ in range(reps):
+        d = crdt_amd.Doc(client_id=0x7FFFFFF0, engine=eng)
+        t0 = time.perf_counter()
+        for u in updates:
+            d.apply_update(u)
+        t1 = time.perf_counter()
+        got = d.encode_state_as_update()
+        t2 = time.perf_counter()
+        loop_ms += (t1 - t0) * 1e3
+        read_ms += (t2 - t1) * 1e3
+        same = same and got == out_update
+        del d
+    loop_ms /= reps
+    read_ms /= reps
+    return {"applies": len(updates), "apply_calls_ms": round(loop_ms, 3), "first_read_ms": round(read_ms, 3),
+            "total_ms": round(loop_ms + read_ms, 3), "merges": 1, "parity": same,
+            "includes": "per call: ctypes + host validation + queue copy; read: H2D + one merge + D2H"}
+
+
 def fleet_sync_leg(eng, n_pairs):
     """Batched sync responder: n_pairs (doc state, lagging
     peer state vector) pairs from the reduced C5 fixtures (60 docs of 2-4 clients, Yjs-generated),
@@ -307,6 +337,7 @@ def main():
     fleet = None
     if rank == 0 and world == 1 and args.fleet_pairs > 0:
         fleet = fleet_sync_leg(eng, args.fleet_pairs)
+    loop = apply_loop_leg(eng, updates, out_update) if rank == 0 and world == 1 else None
     line = {
         "metric": "CRDT items merged/sec at 1/2/4/8 MI355X + % of HBM roofline",
         "value": round(value, 1),
@@ -343,6 +374,7 @@ def main():
         "roofline": roofline,
         "cpu_baseline": cpu,
         "fleet_sync": fleet,
+        "apply_loop": loop,
         "phases_ms": {n: round(m, 4) for n, m in phases},
     }
     if rank == 0:

@@ -106,6 +106,8 @@ enum Buf {
   B_DSMKEY, B_DSMKEYS, B_DSMLEN, B_DSMLENS, B_DSMEND, B_DSMMAX, B_DSMFLAG, B_DSMRID, B_DRCLIENT, B_DRCLOCK, B_DREND,
   B_DWFLAG, B_DWGID, B_DWGSTART, B_DWSIZE, B_DWPOS,
   B_GRIGHT, B_YKEY, B_YKEYS, B_YSEG, B_YIOTA, B_YLSTART, B_YSTATE, B_YBEFORE, B_YCONFL, B_YSTACK,
+  B_TKEY, B_TKEYS, B_TSEG, B_TPOS, B_TGSTART, B_TNEXT, B_TDONE, B_TFIRST, B_TNSIB, B_TJUMP, B_TBIG,
+  B_TPRV, B_TMPRV, B_TMTAIL, B_TTREP, B_TOTAIL,
   B_OFIRST, B_OCIDX, B_OSIZE, B_OPOS, B_RSEG, B_RLEN, B_RSIZE, B_RPOS, B_OUT, B_SVOUT,
   B_VKMAP, B_VKREP, B_VKEYS, B_VNKEYS, B_VPOS, B_VD0, B_VN0, B_VD1, B_VN1, B_VORDER, B_VSEGS,
   B_SCRATCH2, B_TMP2, B_CAPS,
@@ -546,6 +548,22 @@ int run_merge(ycrdt_engine* e, ycrdt_batch* b, const std::unordered_map<uint32_t
   w.y_before = take<uint32_t>(V, B_YBEFORE, U + 2, ok);
   w.y_confl = take<uint32_t>(V, B_YCONFL, U + 2, ok);
   w.y_stack = take<uint32_t>(V, B_YSTACK, U + 2, ok);
+  w.t_key = take<uint32_t>(V, B_TKEY, U + 2, ok);
+  w.t_keys = take<uint32_t>(V, B_TKEYS, U + 2, ok);
+  w.t_seg = take<uint32_t>(V, B_TSEG, U + 2, ok);
+  w.t_pos = take<uint32_t>(V, B_TPOS, U + 2, ok);
+  w.t_gstart = take<uint32_t>(V, B_TGSTART, U + 2, ok);
+  w.t_next = take<uint32_t>(V, B_TNEXT, U + 2, ok);
+  w.t_done = take<uint32_t>(V, B_TDONE, U + 2, ok);
+  w.t_first = take<uint32_t>(V, B_TFIRST, U + 2, ok);
+  w.t_nsib = take<uint32_t>(V, B_TNSIB, U + 2, ok);
+  w.t_jump = take<uint32_t>(V, B_TJUMP, U + 2, ok);
+  w.t_big = take<uint32_t>(V, B_TBIG, U + 2, ok);
+  w.t_prv = take<uint32_t>(V, B_TPRV, U + 2, ok);
+  w.t_mprv = take<uint32_t>(V, B_TMPRV, U + 2, ok);
+  w.t_mtail = take<uint32_t>(V, B_TMTAIL, U + 2, ok);
+  w.t_trep = take<uint32_t>(V, B_TTREP, U + 2, ok);
+  w.t_otail = take<uint32_t>(V, B_TOTAIL, U + 2, ok);
   w.o_first = take<uint32_t>(V, B_OFIRST, U + 2, ok);
   w.o_cidx = take<uint32_t>(V, B_OCIDX, U + 2, ok);
   w.o_size = take<uint32_t>(V, B_OSIZE, U + 2, ok);

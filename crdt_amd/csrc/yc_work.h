@@ -31,6 +31,8 @@ struct Counters {            // device-side counters, read back at the few host 
   uint32_t nruns;            // delete-set runs in the output
   uint32_t narray;           // YArray list members (segments)
   uint32_t narray_roots;     // 1: a decoded item may root a YArray list (parent given, no parentSub)
+  uint32_t tgroups;          // sibling groups of the YArray origin trees (yc_yata.hip)
+  uint32_t tbig;             // groups too large for one lane
   uint32_t nested;           // 1: a decoded item names a parent ITEM (nested types exist)
   uint32_t pad[12];          // encode scratch (see yc_encode.hip)
   unsigned long long items;  // Σ clock lengths of Skip structs (items = Σ all lengths − this)
@@ -162,6 +164,23 @@ struct Work {
   uint32_t* y_before = nullptr;    // [NS]
   uint32_t* y_confl = nullptr;     // [NS]
   uint32_t* y_stack = nullptr;     // [NS]
+  // ---- parallel YATA as an origin-tree pre-order (yc_yata.hip)
+  uint32_t* t_key = nullptr;       // [NS] sibling-group key: origin segment, or NS + list slot for roots; NONE = not in a list
+  uint32_t* t_keys = nullptr;      // [NS] sorted keys
+  uint32_t* t_seg = nullptr;       // [NS] segments sorted by (group, segment): siblings in client order
+  uint32_t* t_pos = nullptr;       // [NS] segment -> sorted position
+  uint32_t* t_gstart = nullptr;    // [groups+1] first sorted position of every sibling group
+  uint32_t* t_next = nullptr;      // [NS] next sibling (sorted position) after the sibling loops
+  uint32_t* t_done = nullptr;      // [NS] sibling-loop state (0 pending, 1 on the stack, 2 placed)
+  uint32_t* t_first = nullptr;     // [NS] first child segment of every segment (NONE = leaf)
+  uint32_t* t_nsib = nullptr;      // [NS] next sibling segment (NONE = last child)
+  uint32_t* t_jump = nullptr;      // [NS] climbing link: an ancestor with the same "next in pre-order"
+  uint32_t* t_big = nullptr;       // [groups] ids of the groups too large for one lane
+  uint32_t* t_prv = nullptr;       // [NS] previous sibling (sorted position) during the loops
+  uint32_t* t_mprv = nullptr;      // [NS] previous member of the same right-origin group
+  uint32_t* t_mtail = nullptr;     // [NS] last member of the group whose right origin is this sibling
+  uint32_t* t_otail = nullptr;     // [NS] last member of the outside-right-origin group anchored here
+  uint32_t* t_trep = nullptr;      // [NS] anchor of the member's right-origin group
   // ---- lazy merge (mergeUpdates / diffUpdate, yc_lazy.hip)
   uint32_t* usec_start = nullptr;  // [nupd] first section of every update (walker order)
   uint32_t* usec_n = nullptr;      // [nupd] sections of every update

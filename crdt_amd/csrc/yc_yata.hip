@@ -13,6 +13,7 @@
 // loop's verdict on the first unit of a run holds for the whole run (SURVEY §7 hard part 1,
 // per-clock restatement) and the loop can step over segments instead of units.
 #include <cstdlib>
+#include <cstring>
 
 #include "yc_work.h"
 
@@ -243,6 +244,333 @@ __global__ void k_yata_lds(Work w, uint32_t nlists, uint32_t nmin) {
   }
 }
 
+// ============================================================================================
+// Parallel YATA: the list as a pre-order walk of the origin tree.
+// In the final Yjs list the origin-descendants of every item form one contiguous block right
+// after it: the B.1 loop only ever leaves an item after a whole sibling block (left moves through
+// a block's descendants once it is set on the block's root) or right after its origin, and it only
+// stops at a block start (the right origin, a same-origin sibling) or past the origin's block. So
+// the list is a pre-order walk of the origin tree whose children — items with the same origin
+// (segment), each carrying its block — are ordered by the B.1 loop run over the children alone:
+//   scan the siblings from the first until c's right origin (if that is a sibling; else to the
+//   end): left := o when o.client < c.client, else stop when o.rightOrigin == c.rightOrigin.
+// scripts/yata_tree_proto.py checks this against the sequential loop on per-clock items of 234
+// seeded / golden histories. Sibling groups are independent: a group of <= TSMALL children runs on
+// one lane, larger ones on one workgroup with the group staged in LDS (<= TLDS) or read from
+// global memory (sib_loop below: the B.1 scan evaluated backwards). The pre-order successor (g_right) is
+// the first child, else the next sibling of the nearest ancestor-or-self that has one: one
+// climbing pass with path halving.
+constexpr uint32_t TSMALL = 16, TLDS = 6144;  // 20 B per member in LDS
+
+__global__ void k_tkey(Work w, uint32_t nsegs) {
+  const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= nsegs) return;
+  uint32_t key = NONE, p = NONE;
+  if (w.g_flags[s] & SEG_ARRAY) {
+    const uint32_t list = w.g_key[s];
+    const uint32_t o = w.g_origin[s], r = w.g_rorigin[s];
+    if (o != NONE) {
+      p = seg_of_unit(w, o);
+      if (!(w.g_flags[p] & SEG_ARRAY) || w.g_key[p] != list) raise_err(&w.ctr->err, ERR_DECODE);  // outside the list
+    }
+    if (r != NONE) {
+      const uint32_t rs = seg_of_unit(w, r);
+      if (!(w.g_flags[rs] & SEG_ARRAY) || w.g_key[rs] != list) raise_err(&w.ctr->err, ERR_DECODE);
+    }
+    key = p != NONE ? p : nsegs + list;
+  }
+  w.t_key[s] = key;
+  w.t_first[s] = NONE;
+  w.t_nsib[s] = NONE;
+  w.t_jump[s] = p;
+}
+// group starts: t_done = flags, t_next = their exclusive scan (both re-initialised afterwards)
+__global__ void k_tgroup_flags(Work w, uint32_t nsegs) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i > nsegs) return;
+  const uint32_t k = i < nsegs ? w.t_keys[i] : NONE;
+  w.t_done[i] = (k != NONE && (i == 0 || w.t_keys[i - 1] != k)) ? 1u : 0u;
+}
+__global__ void k_tgroup_starts(Work w, uint32_t nsegs) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i == nsegs) w.ctr->tgroups = w.t_next[nsegs];
+  if (i >= nsegs) return;
+  const uint32_t k = w.t_keys[i];
+  if (k == NONE) return;
+  w.t_pos[w.t_seg[i]] = i;
+  if (w.t_done[i]) w.t_gstart[w.t_next[i]] = i;
+  if (i + 1 == nsegs || w.t_keys[i + 1] == NONE) w.t_gstart[w.t_next[nsegs]] = i + 1;  // sentinel
+}
+// per sorted position: client index, right-origin unit, sorted position of a sibling right origin
+// (y_state / y_before / y_confl are free once the list table is built)
+__global__ void k_tprep(Work w, uint32_t nsegs) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= nsegs) return;
+  w.t_done[i] = 0;
+  w.t_next[i] = NONE;
+  w.t_prv[i] = NONE;
+  w.t_mprv[i] = NONE;
+  w.t_mtail[i] = NONE;
+  w.t_otail[i] = NONE;
+  const uint32_t k = w.t_keys[i];
+  if (k == NONE) return;
+  const uint32_t s = w.t_seg[i];
+  const uint32_t r = w.g_rorigin[s];
+  uint32_t rp = NONE;
+  if (r != NONE) {
+    const uint32_t rs = seg_of_unit(w, r);
+    if (w.t_key[rs] == k) rp = w.t_pos[rs];
+  }
+  w.y_state[i] = w.g_cidx[s];
+  w.y_before[i] = r;
+  w.y_confl[i] = rp;
+}
+
+// One sibling group (local indices 0..n-1 in ascending client order). The forward B.1 scan
+//   from the first sibling until c's right origin: left := o when o.client < c.client, else stop
+//   at o when o.rightOrigin == c.rightOrigin
+// is evaluated backwards: the members of one right-origin group always stand in ascending client
+// order (the stop rule puts every newcomer before the group's first higher client and after its
+// lower ones), so the stop is the group's next higher-client member already placed (its member
+// list is walked from the top), else the right-origin sibling, else the end; left is then the
+// nearest lower-client sibling before the stop. Integrating in ascending client order makes both
+// walks O(1) in practice (scripts/yata_tree_proto.py: 49 backward steps where the forward scans
+// take 151 k on the same groups, identical orders).
+constexpr uint32_t TOUT = 0x8000u;  // LDS trep flag (bit 31 in global memory): the anchor is the first member of an outside right origin
+template <class A>
+__device__ uint32_t sib_loop(A& a, uint32_t n, uint32_t* __restrict__ stack, uint32_t* err) {
+  uint32_t head = NONE, tail = NONE;
+  for (uint32_t i0 = 0; i0 < n; ++i0) {
+    if (a.done(i0) == 2) continue;
+    uint32_t sp = 0;
+    stack[sp++] = i0;
+    a.set_done(i0, 1);
+    while (sp > 0) {
+      const uint32_t c = stack[sp - 1];
+      const uint32_t rp = a.rpos(c);
+      if (rp != NONE && a.done(rp) != 2) {  // the right origin is a sibling: place it first
+        if (a.done(rp) == 1 || sp >= n) { raise_err(err, ERR_DECODE); return NONE; }
+        a.set_done(rp, 1);
+        stack[sp++] = rp;
+        continue;
+      }
+      bool out = false;
+      const uint32_t cc = a.cid(c), ta = a.trep(c, out);
+      // member list of c's right-origin group, walked from its top (highest client) down; a group
+      // is anchored at its right-origin sibling (mtail) or, for a right origin outside the group,
+      // at its first member (otail: a member can anchor both kinds)
+      uint32_t m = out ? a.otail(ta) : a.mtail(ta), succ = NONE;
+      while (m != NONE && a.cid(m) > cc) { succ = m; m = a.mprv(m); }
+      a.set_mprv(c, m);
+      if (succ != NONE) a.set_mprv(succ, c);
+      else if (out) a.set_otail(ta, c);
+      else a.set_mtail(ta, c);
+      const uint32_t stop = succ != NONE ? succ : rp;
+      uint32_t left = stop != NONE ? a.prv(stop) : tail;
+      while (left != NONE && a.cid(left) >= cc) left = a.prv(left);
+      const uint32_t nx = left != NONE ? a.next(left) : head;
+      a.set_prv(c, left);
+      a.set_next(c, nx);
+      if (left != NONE) a.set_next(left, c); else head = c;
+      if (nx != NONE) a.set_prv(nx, c); else tail = c;
+      a.set_done(c, 2);
+      --sp;
+    }
+  }
+  return head;
+}
+struct SibGlobal {  // a group read in place (sorted positions base..base+n); links hold positions
+  const Work& w;
+  uint32_t base;
+  __device__ static uint32_t loc(uint32_t x, uint32_t b) { return x == NONE ? NONE : x - b; }
+  __device__ static uint32_t glo(uint32_t x, uint32_t b) { return x == NONE ? NONE : x + b; }
+  __device__ uint32_t done(uint32_t i) const { return w.t_done[base + i]; }
+  __device__ void set_done(uint32_t i, uint32_t v) { w.t_done[base + i] = v; }
+  __device__ uint32_t rpos(uint32_t i) const { return loc(w.y_confl[base + i], base); }
+  __device__ uint32_t trep(uint32_t i, bool& out) const { const uint32_t t = w.t_trep[base + i]; out = (t >> 31) != 0; return (t & 0x7FFFFFFFu) - base; }
+  __device__ uint32_t cid(uint32_t i) const { return w.y_state[base + i]; }
+  __device__ uint32_t next(uint32_t i) const { return loc(w.t_next[base + i], base); }
+  __device__ void set_next(uint32_t i, uint32_t v) { w.t_next[base + i] = glo(v, base); }
+  __device__ uint32_t prv(uint32_t i) const { return loc(w.t_prv[base + i], base); }
+  __device__ void set_prv(uint32_t i, uint32_t v) { w.t_prv[base + i] = glo(v, base); }
+  __device__ uint32_t mprv(uint32_t i) const { return loc(w.t_mprv[base + i], base); }
+  __device__ void set_mprv(uint32_t i, uint32_t v) { w.t_mprv[base + i] = glo(v, base); }
+  __device__ uint32_t mtail(uint32_t i) const { return loc(w.t_mtail[base + i], base); }
+  __device__ void set_mtail(uint32_t i, uint32_t v) { w.t_mtail[base + i] = glo(v, base); }
+  __device__ uint32_t otail(uint32_t i) const { return loc(w.t_otail[base + i], base); }
+  __device__ void set_otail(uint32_t i, uint32_t v) { w.t_otail[base + i] = glo(v, base); }
+};
+struct __attribute__((aligned(4))) SibRec { uint32_t cid; uint16_t rpos, trep, nxt, prv, mprv, mtail, otail, pad; };
+constexpr uint16_t S_NONE = 0xFFFFu;
+struct SibLds {  // a group staged in LDS (n <= TLDS)
+  SibRec* rec;
+  uint8_t* st;
+  __device__ static uint32_t w32(uint16_t x) { return x == S_NONE ? NONE : x; }
+  __device__ static uint16_t w16(uint32_t x) { return x == NONE ? S_NONE : (uint16_t)x; }
+  __device__ uint32_t done(uint32_t i) const { return st[i]; }
+  __device__ void set_done(uint32_t i, uint32_t v) { st[i] = (uint8_t)v; }
+  __device__ uint32_t rpos(uint32_t i) const { return w32(rec[i].rpos); }
+  __device__ uint32_t trep(uint32_t i, bool& out) const { out = (rec[i].trep & TOUT) != 0; return rec[i].trep & ~TOUT; }
+  __device__ uint32_t cid(uint32_t i) const { return rec[i].cid; }
+  __device__ uint32_t next(uint32_t i) const { return w32(rec[i].nxt); }
+  __device__ void set_next(uint32_t i, uint32_t v) { rec[i].nxt = w16(v); }
+  __device__ uint32_t prv(uint32_t i) const { return w32(rec[i].prv); }
+  __device__ void set_prv(uint32_t i, uint32_t v) { rec[i].prv = w16(v); }
+  __device__ uint32_t mprv(uint32_t i) const { return w32(rec[i].mprv); }
+  __device__ void set_mprv(uint32_t i, uint32_t v) { rec[i].mprv = w16(v); }
+  __device__ uint32_t mtail(uint32_t i) const { return w32(rec[i].mtail); }
+  __device__ void set_mtail(uint32_t i, uint32_t v) { rec[i].mtail = w16(v); }
+  __device__ uint32_t otail(uint32_t i) const { return w32(rec[i].otail); }
+  __device__ void set_otail(uint32_t i, uint32_t v) { rec[i].otail = w16(v); }
+};
+
+// sibling order -> first child / next sibling (segment indices)
+__device__ __forceinline__ void sib_publish(const Work& w, uint32_t a, uint32_t n, uint32_t nsegs, uint32_t head) {
+  const uint32_t key = w.t_keys[a];
+  if (key < nsegs && head != NONE) w.t_first[key] = w.t_seg[a + head];
+}
+// right-origin group anchor of every member: the right-origin sibling itself, or (a right origin
+// outside the group, or none) the first member with the same right-origin unit
+__device__ __forceinline__ void sib_anchors_small(const Work& w, uint32_t a, uint32_t n) {
+  for (uint32_t i = 0; i < n; ++i) {
+    uint32_t t = w.y_confl[a + i];
+    if (t == NONE) {
+      const uint32_t r = w.y_before[a + i];
+      t = a + i;
+      for (uint32_t j = 0; j < i; ++j)
+        if (w.y_confl[a + j] == NONE && w.y_before[a + j] == r) { t = a + j; break; }
+      t |= 0x80000000u;
+    }
+    w.t_trep[a + i] = t;
+  }
+}
+
+__global__ void k_tsib_small(Work w, uint32_t nsegs) {
+  const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= w.ctr->tgroups) return;
+  const uint32_t a = w.t_gstart[g], n = w.t_gstart[g + 1] - a;
+  if (n > TSMALL) {
+    w.t_big[atomicAdd(&w.ctr->tbig, 1u)] = g;
+    return;
+  }
+  uint32_t head = 0;
+  if (n > 1) {
+    sib_anchors_small(w, a, n);
+    SibGlobal acc{w, a};
+    head = sib_loop(acc, n, w.y_stack + a, &w.ctr->err);
+  }
+  sib_publish(w, a, n, nsegs, head);
+  for (uint32_t i = 0; i < n; ++i) {
+    const uint32_t x = n == 1 ? NONE : w.t_next[a + i];
+    w.t_nsib[w.t_seg[a + i]] = x == NONE ? NONE : w.t_seg[x];
+  }
+}
+// one workgroup per large group: anchors of outside right origins through an LDS hash table,
+// the group staged in LDS when it fits (else read in place); lane 0 runs the loop
+constexpr uint32_t THASH = 2048;
+__global__ __launch_bounds__(256) void k_tsib_big(Work w, uint32_t nsegs) {
+  const uint32_t g = w.t_big[blockIdx.x];
+  const uint32_t a = w.t_gstart[g], n = w.t_gstart[g + 1] - a;
+  __shared__ SibRec rec[TLDS];
+  __shared__ uint8_t st[TLDS];
+  __shared__ uint32_t hkey[THASH], hval[THASH];
+  __shared__ uint32_t head_s;
+  for (uint32_t i = threadIdx.x; i < THASH; i += blockDim.x) { hkey[i] = NONE; hval[i] = NONE; }
+  __syncthreads();
+  // anchors: the first member (lowest position) of every outside right-origin unit
+  for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) {
+    if (w.y_confl[a + i] != NONE) continue;
+    const uint32_t r = w.y_before[a + i];
+    uint32_t slot = (r * 2654435761u) & (THASH - 1);
+    for (uint32_t probe = 0;; ++probe) {
+      if (probe == THASH) { raise_err(&w.ctr->err, ERR_CAPACITY); break; }
+      const uint32_t old = atomicCAS(&hkey[slot], NONE, r);
+      if (old == NONE || old == r) { atomicMin(&hval[slot], i); break; }
+      slot = (slot + 1) & (THASH - 1);
+    }
+  }
+  __syncthreads();
+  for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) {
+    uint32_t t = w.y_confl[a + i];
+    if (t == NONE) {
+      const uint32_t r = w.y_before[a + i];
+      uint32_t slot = (r * 2654435761u) & (THASH - 1);
+      for (uint32_t probe = 0; probe < THASH && hkey[slot] != r; ++probe) slot = (slot + 1) & (THASH - 1);
+      t = (hkey[slot] == r ? a + hval[slot] : a + i) | 0x80000000u;
+    }
+    w.t_trep[a + i] = t;
+  }
+  __syncthreads();
+  if (n <= TLDS) {
+    for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) {
+      const uint32_t rp = w.y_confl[a + i];
+      const uint32_t t = w.t_trep[a + i];
+      rec[i] = SibRec{w.y_state[a + i], (uint16_t)(rp == NONE ? S_NONE : rp - a),
+                      (uint16_t)(((t & 0x7FFFFFFFu) - a) | ((t >> 31) ? TOUT : 0u)), S_NONE, S_NONE, S_NONE, S_NONE, S_NONE, 0};
+      st[i] = 0;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      SibLds acc{rec, st};
+      head_s = sib_loop(acc, n, w.y_stack + a, &w.ctr->err);
+    }
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) {
+      const uint32_t x = rec[i].nxt;
+      w.t_nsib[w.t_seg[a + i]] = x == S_NONE ? NONE : w.t_seg[a + x];
+    }
+  } else {
+    if (threadIdx.x == 0) {
+      SibGlobal acc{w, a};
+      head_s = sib_loop(acc, n, w.y_stack + a, &w.ctr->err);
+    }
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) {
+      const uint32_t x = w.t_next[a + i];
+      w.t_nsib[w.t_seg[a + i]] = x == NONE ? NONE : w.t_seg[x];
+    }
+  }
+  if (threadIdx.x == 0 && head_s != NONE) sib_publish(w, a, n, nsegs, head_s);
+}
+// pre-order successor: first child, else the next sibling of the nearest ancestor-or-self with one
+__global__ __launch_bounds__(256) void k_tclimb(Work w, uint32_t nsegs) {
+  const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= nsegs || !(w.g_flags[s] & SEG_ARRAY)) return;
+  const uint32_t fc = w.t_first[s];
+  if (fc != NONE) { w.g_right[s] = fc; return; }
+  uint32_t y = s, res = NONE;
+  for (uint32_t it = 0; it < (1u << 26); ++it) {
+    const uint32_t ns = w.t_nsib[y];
+    if (ns != NONE) { res = ns; break; }
+    const uint32_t z = w.t_jump[y];  // an ancestor whose answer is y's (every node between has no next sibling)
+    if (z == NONE) break;            // a last child of the list's root: the end of the list
+    if (w.t_nsib[z] == NONE) {       // path halving: y inherits z's link
+      const uint32_t zz = w.t_jump[z];
+      if (zz != z) w.t_jump[y] = zz;
+    }
+    y = z;
+  }
+  w.g_right[s] = res;
+}
+
+uint32_t launch_yata_tree(const Work& w, uint32_t nsegs, hipStream_t s) {
+  const uint32_t grid = nsegs / 256 + 1;
+  hipLaunchKernelGGL(k_tkey, dim3(grid), dim3(256), 0, s, w, nsegs);
+  sort_pairs_u32(w.tmp, w.tmp_bytes, w.t_key, w.t_keys, w.y_iota, w.t_seg, nsegs, s);
+  hipLaunchKernelGGL(k_tgroup_flags, dim3(grid), dim3(256), 0, s, w, nsegs);
+  scan_u32(w.tmp, w.tmp_bytes, w.t_done, w.t_next, nsegs + 1, s);
+  hipMemsetAsync(&w.ctr->tbig, 0, sizeof(uint32_t), s);
+  hipLaunchKernelGGL(k_tgroup_starts, dim3(grid), dim3(256), 0, s, w, nsegs);
+  hipLaunchKernelGGL(k_tprep, dim3(grid), dim3(256), 0, s, w, nsegs);
+  hipLaunchKernelGGL(k_tsib_small, dim3(grid), dim3(256), 0, s, w, nsegs);
+  uint32_t nbig = 0;
+  hipMemcpyAsync(&nbig, &w.ctr->tbig, sizeof(uint32_t), hipMemcpyDeviceToHost, s);
+  hipStreamSynchronize(s);
+  if (nbig) hipLaunchKernelGGL(k_tsib_big, dim3(nbig), dim3(256), 0, s, w, nsegs);
+  hipLaunchKernelGGL(k_tclimb, dim3(grid), dim3(256), 0, s, w, nsegs);
+  return nbig;
+}
+
 uint32_t launch_yata(const Work& w, uint32_t nsegs, uint32_t narray, uint32_t nclients, hipStream_t s) {
   if (!nsegs) return 0;
   const uint32_t grid = nsegs / 256 + 1;
@@ -256,6 +584,11 @@ uint32_t launch_yata(const Work& w, uint32_t nsegs, uint32_t narray, uint32_t nc
   hipStreamSynchronize(s);
   if (!nlists) return 0;
   hipLaunchKernelGGL(k_ylist_starts, dim3(grid), dim3(256), 0, s, w, nsegs);
+  static const bool seq = getenv("YCRDT_YATA") && !strcmp(getenv("YCRDT_YATA"), "seq");
+  if (!seq && (uint64_t)nsegs * 5 < 0xFFFFFFF0ull) {  // sibling keys NS + list slot stay below NONE
+    launch_yata_tree(w, nsegs, s);
+    return nlists;
+  }
   hipMemsetAsync(w.y_before, 0, sizeof(uint32_t) * (nsegs + 1), s);  // stamps: 0 is never issued
   hipMemsetAsync(w.y_confl, 0, sizeof(uint32_t) * (nsegs + 1), s);
   if (nclients < 16384 && !getenv("YCRDT_YATA_GLOBAL")) {  // client index in 14 bits
