@@ -45,6 +45,8 @@ def parse():
                    help="replicas in the Yjs CPU-baseline sample (bounded: ~10 s of Yjs work)")
     p.add_argument("--port-replicas", type=int, default=1000, help="replicas in the oracle-port timing sample")
     p.add_argument("--profile-phases", action="store_true")
+    p.add_argument("--c3-items", type=int, default=10_000_000,
+                   help="C3 leg: YArray 'messages', 256 replicas x 16 rounds, this many values (0 = off)")
     return p.parse_args()
 
 
@@ -155,6 +157,101 @@ def apply_loop_leg(eng, updates, out_update):
     return {"applies": len(updates), "apply_calls_ms": round(loop_ms, 3), "first_read_ms": round(read_ms, 3),
             "total_ms": round(loop_ms + read_ms, 3), "merges": 1, "parity": same,
             "includes": "per call: ctypes + host validation + queue copy; read: H2D + one merge + D2H"}
+
+
+def _yjs_time(ups, timeout=240):
+    """Yjs 13.5.16 in Node on one core over a batch (scripts/yjs_baseline.js): (ms, sha256) or None."""
+    import shutil
+    import struct
+    import subprocess
+    import tempfile
+
+    node = shutil.which("node")
+    if not node:
+        return None
+    with tempfile.NamedTemporaryFile(suffix=".bin", delete=False) as f:
+        f.write(struct.pack("<I", len(ups)))
+        for u in ups:
+            f.write(struct.pack("<I", len(u)))
+            f.write(u)
+        fname = f.name
+    try:
+        r = subprocess.run([node, "--max-old-space-size=16384", os.path.join(ROOT, "scripts", "yjs_baseline.js"), fname],
+                           capture_output=True, text=True, timeout=timeout)
+        y = json.loads(r.stdout.strip().splitlines()[-1]) if r.returncode == 0 and r.stdout.strip() else None
+    finally:
+        os.unlink(fname)
+    return y if y and y.get("available") else None
+
+
+def c3_leg(eng, n_items, steps=3):
+    """BASELINE.json configs[2] (C3): YArray 'messages', 256 replicas doing push / unshift / insert /
+    cut over 16 rounds (crdt_amd/workload/ycw_array.cpp), every replica's per-round update merged
+    in one batch (4,096 updates). Properties at full size: the reversed batch and the merge of the
+    output give the same bytes. Beside it, on bounded samples of the same generator: the oracle
+    port (oracle/yref.c, 1 core) and Yjs 13.5.16 in Node (1 core), outputs compared."""
+    import hashlib
+
+    import crdt_amd
+    from crdt_amd.workload import gen_array
+    from oracle.yref import Doc as ODoc
+
+    g0 = time.perf_counter()
+    ups, gst = gen_array(256, 16, n_items, 3)
+    gen_s = time.perf_counter() - g0
+    b = crdt_amd.Batch(ups, eng)
+    st = b.merge()  # warm-up
+    eng.set_profiling(True)
+    acc, t0 = {}, time.perf_counter()
+    for _ in range(steps):
+        st = b.merge()
+        for n, m in eng.phase_times():
+            acc[n] = acc.get(n, 0.0) + m
+    wall = (time.perf_counter() - t0) / steps
+    eng.set_profiling(False)
+    out = b.result()[0]
+    del b
+    rb = crdt_amd.Batch(list(reversed(ups)), eng)
+    rb.merge()
+    rev_ok = rb.result()[0] == out
+    del rb
+    ib = crdt_amd.Batch([out], eng)
+    ib.merge()
+    idem_ok = ib.result()[0] == out
+    del ib
+    res = {"workload": "C3: YArray 'messages', 256 replicas x 16 rounds, push 40% / unshift 15% / insert 30% / cut 15%",
+           "updates": len(ups), "input_bytes": sum(map(len, ups)), "items": st.items, "structs": st.structs,
+           "segments": st.segments, "output_bytes": len(out), "ms_per_merge": round(wall * 1e3, 3),
+           "device_ms": round(st.device_ms, 3), "items_per_s": round(st.items / wall, 1),
+           "phases_ms": {n: round(m / steps, 3) for n, m in acc.items()},
+           "order_independent": rev_ok, "idempotent": idem_ok, "generate_s": round(gen_s, 2)}
+    # the oracle port and Yjs on bounded samples of the same generator
+    for key, n, runner in (("port", 1_000_000, "port"), ("yjs", 200_000, "yjs")):
+        sups, sst = gen_array(256, 16, n, 3)
+        gb = crdt_amd.Batch(sups, eng)
+        gst2 = gb.merge()
+        t0 = time.perf_counter()
+        for _ in range(3):
+            gst2 = gb.merge()
+        gms = (time.perf_counter() - t0) * 1e3 / 3
+        gout = gb.result()[0]
+        del gb
+        if runner == "port":
+            d = ODoc(0x7FFFFFF0)
+            c0 = time.perf_counter()
+            for u in sups:
+                d.apply_update(u)
+            ref = d.encode_state_as_update()
+            cms = (time.perf_counter() - c0) * 1e3
+            res[key] = {"items": gst2.items, "cpu_ms": round(cms, 1), "gpu_ms": round(gms, 2), "cores": 1, "kind": "port",
+                        "parity": ref == gout, "sample": f"{n} values, oracle/yref.c sequential Yjs restatement"}
+        else:
+            y = _yjs_time(sups)
+            if y:
+                res[key] = {"items": gst2.items, "cpu_ms": round(y["ms"], 1), "gpu_ms": round(gms, 2), "cores": 1,
+                            "kind": "reference", "parity": y["out_sha256"] == hashlib.sha256(gout).hexdigest(),
+                            "sample": f"{n} values, Yjs {y['yjs']} in Node {y['node']}"}
+    return res
 
 
 def fleet_sync_leg(eng, n_pairs):
@@ -338,6 +435,7 @@ def main():
     if rank == 0 and world == 1 and args.fleet_pairs > 0:
         fleet = fleet_sync_leg(eng, args.fleet_pairs)
     loop = apply_loop_leg(eng, updates, out_update) if rank == 0 and world == 1 else None
+    c3 = c3_leg(eng, args.c3_items) if rank == 0 and world == 1 and args.c3_items > 0 else None
     line = {
         "metric": "CRDT items merged/sec at 1/2/4/8 MI355X + % of HBM roofline",
         "value": round(value, 1),
@@ -375,6 +473,7 @@ def main():
         "cpu_baseline": cpu,
         "fleet_sync": fleet,
         "apply_loop": loop,
+        "c3": c3,
         "phases_ms": {n: round(m, 4) for n, m in phases},
     }
     if rank == 0:

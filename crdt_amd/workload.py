@@ -1,4 +1,4 @@
-"""Seeded synthetic replica-update workloads (SURVEY.md §8(d) C1 / C2) for tests and bench.py.
+"""Seeded synthetic replica-update workloads (SURVEY.md §8(d) C1 / C2 / C3) for tests and bench.py.
 
 Thin ctypes wrapper over crdt_amd/workload/ycw.cpp (built as crdt_amd/libycrdt_workload.so).
 """
@@ -20,6 +20,9 @@ def _lib():
             ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_int,
             P(ctypes.c_void_p), P(ctypes.c_size_t), P(ctypes.c_void_p), P(ctypes.c_size_t), P(ctypes.c_void_p),
         ]
+        L.ycw_gen_array.argtypes = [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_uint32,
+                                    P(ctypes.c_void_p), P(ctypes.c_size_t), P(ctypes.c_void_p), P(ctypes.c_size_t),
+                                    P(ctypes.c_uint64), P(ctypes.c_void_p), P(ctypes.c_size_t)]
         L.ycw_free.argtypes = [ctypes.c_void_p]
         _L = L
     return _L
@@ -30,6 +33,34 @@ C1 = dict(n_keys=1000, n_replicas=2, ops_per_replica=10000, zipf_s=0.0, p_set=0.
           base_client=1, client_mode=1, value_mode=1, seed=42)
 C2 = dict(n_keys=100_000, n_replicas=1000, ops_per_replica=1000, zipf_s=1.1, p_set=0.8, base_snapshot=True,
           base_client=1, client_mode=0, value_mode=0, seed=2)
+C3 = dict(n_replicas=256, rounds=16, items=10_000_000, seed=3)
+
+
+def gen_array(n_replicas=256, rounds=16, items=10_000_000, seed=3, order=False):
+    """C3-shaped YArray workload (crdt_amd/workload/ycw_array.cpp): every replica's per-round wire
+    update. Returns (updates: list[bytes], stats: dict); with order=True stats["order"] lists the
+    final live values as (client, clock) in the generator's list order."""
+    L = _lib()
+    data, dlen, offs, nupd = ctypes.c_void_p(), ctypes.c_size_t(), ctypes.c_void_p(), ctypes.c_size_t()
+    st = (ctypes.c_uint64 * 4)()
+    op, no = ctypes.c_void_p(), ctypes.c_size_t()
+    rc = L.ycw_gen_array(n_replicas, rounds, items, seed, ctypes.byref(data), ctypes.byref(dlen), ctypes.byref(offs),
+                         ctypes.byref(nupd), st, ctypes.byref(op) if order else None, ctypes.byref(no) if order else None)
+    if rc != 0:
+        raise ValueError("bad workload config")
+    try:
+        raw = ctypes.string_at(data.value, dlen.value) if dlen.value else b""
+        o = (ctypes.c_uint64 * (nupd.value + 1)).from_address(offs.value)
+        ups = [raw[o[i]:o[i + 1]] for i in range(nupd.value)]
+        stats = {"ops": st[0], "items": st[1], "deleted": st[2], "length": st[3]}
+        if order:
+            a = (ctypes.c_uint32 * (2 * no.value + 1)).from_address(op.value)
+            stats["order"] = [(a[2 * i], a[2 * i + 1]) for i in range(no.value)]
+            L.ycw_free(op)
+    finally:
+        L.ycw_free(data)
+        L.ycw_free(offs)
+    return ups, stats
 
 
 def gen_map(n_keys, n_replicas, ops_per_replica, zipf_s=1.1, p_set=0.8, base_snapshot=True, base_client=1,
