@@ -83,6 +83,7 @@ EXPORTS = (
     "ycrdt_doc_json", "ycrdt_map_set", "ycrdt_map_set_type", "ycrdt_map_delete", "ycrdt_array_insert",
     "ycrdt_array_delete", "ycrdt_doc_client_id", "ycrdt_map_type_at", "ycrdt_doc_take_local_update",
     "ycrdt_doc_flush", "ycrdt_doc_pending", "ycrdt_doc_track_local", "ycrdt_validate_update", "ycrdt_debug_replay",
+    "ycrdt_batch_stage_docs", "ycrdt_batch_result_docs", "ycrdt_merge_docs",
 )
 
 MERGE_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p)
@@ -122,6 +123,9 @@ def lib():
     L.ycrdt_doc_pending.argtypes = [vp, P(i32), P(i32)]
     L.ycrdt_doc_track_local.argtypes = [vp, i32]
     L.ycrdt_validate_update.argtypes = [_Buf, P(i32)]
+    L.ycrdt_batch_stage_docs.argtypes = [vp, P(_Buf), P(u32), sz, u32, P(vp)]
+    L.ycrdt_batch_result_docs.argtypes = [vp, P(_Out), P(_Out)]
+    L.ycrdt_merge_docs.argtypes = [vp, P(_Buf), P(u32), sz, u32, P(_Out), P(_Out)]
     L.ycrdt_debug_replay.argtypes = [P(_Buf), sz, MERGE_FN, vp, P(_Out), P(_Out), P(_Out)]
     L.ycrdt_free.argtypes = [P(_Out)]
     cs = ctypes.c_char_p
@@ -313,14 +317,32 @@ class Doc:
         _check(lib().ycrdt_array_delete(self._h, root.encode(), _opt(parent_key), index, length))
 
 
-class Batch:
-    """A set of updates staged in HBM; merge() runs the whole merge on the device."""
+def _docs_arrays(docs):
+    ups, doc_of = [], []
+    for d, us in enumerate(docs):
+        ups.extend(us)
+        doc_of.extend([d] * len(us))
+    arr, keep = _bufs(ups)
+    do = (ctypes.c_uint32 * max(1, len(doc_of)))(*doc_of)
+    return arr, keep, do
 
-    def __init__(self, updates, engine=None):
+
+class Batch:
+    """A set of updates staged in HBM; merge() runs the whole merge on the device. With
+    `docs=[[u8, ...], ...]` instead of `updates` the batch holds many independent documents
+    (ycrdt_batch_stage_docs) merged in the same device pass; result_docs() splits them."""
+
+    def __init__(self, updates=None, engine=None, docs=None):
         self.engine = engine or default_engine()
-        arr, keep = _bufs(updates)
         h = ctypes.c_void_p()
-        _check(lib().ycrdt_batch_stage(self.engine._h, arr, len(keep), ctypes.byref(h)))
+        self.ndocs = 1
+        if docs is not None:
+            arr, keep, do = _docs_arrays(docs)
+            self.ndocs = max(1, len(docs))
+            _check(lib().ycrdt_batch_stage_docs(self.engine._h, arr, do, len(keep), self.ndocs, ctypes.byref(h)))
+        else:
+            arr, keep = _bufs(updates)
+            _check(lib().ycrdt_batch_stage(self.engine._h, arr, len(keep), ctypes.byref(h)))
         self._h = h
 
     def __del__(self):
@@ -340,6 +362,23 @@ class Batch:
         u, s = _Out(), _Out()
         _check(lib().ycrdt_batch_result(self._h, ctypes.byref(u), ctypes.byref(s)))
         return _take(u), _take(s)
+
+    def result_docs(self):
+        """[(encoded update, state vector)] per document of a multi-document batch."""
+        us, ss = (_Out * self.ndocs)(), (_Out * self.ndocs)()
+        _check(lib().ycrdt_batch_result_docs(self._h, us, ss))
+        return [(_take(us[i]), _take(ss[i])) for i in range(self.ndocs)]
+
+
+def merge_docs(docs, engine=None):
+    """Many independent documents' update lists merged in ONE device pass (ycrdt_merge_docs):
+    [(encodeStateAsUpdate, encodeStateVector)] of a fresh doc per list."""
+    eng = engine or default_engine()
+    arr, keep, do = _docs_arrays(docs)
+    n = max(1, len(docs))
+    us, ss = (_Out * n)(), (_Out * n)()
+    _check(lib().ycrdt_merge_docs(eng._h, arr, do, len(keep), n, us, ss))
+    return [(_take(us[i]), _take(ss[i])) for i in range(len(docs))]
 
 
 # ---- the `Y` functions the reference calls ---------------------------------------------------

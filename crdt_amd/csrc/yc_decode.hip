@@ -924,10 +924,45 @@ __global__ void k_section_cidx(Section* __restrict__ sec, uint32_t n, const uint
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i < n) sec[i].cidx = lower_bound_u32(cl, *nc, sec[i].client);
 }
+// multi-document batches: clients are (doc, client) pairs, sorted by doc then client id
+__global__ void k_gather_sec_keys(Work w, uint32_t n) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) { w.cl_key2[i] = ((uint64_t)w.udoc[w.sections[i].upd] << 32) | w.sections[i].client; w.cl_tmp[i] = i; }
+}
+__global__ void k_unique_keys(Work w, uint32_t n) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) w.scratch[i] = (i == 0 || w.cl_key[i] != w.cl_key[i - 1]) ? 1u : 0u;
+  else if (i == n) w.scratch[i] = 0;
+}
+__global__ void k_unique_keys_scatter(Work w, uint32_t n) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n && (i == 0 || w.cl_key[i] != w.cl_key[i - 1])) {
+    const uint64_t k = w.cl_key[i];
+    const uint32_t c = w.cl_tmp[i];
+    w.cl_key2[c] = k;
+    w.cl_vals[c] = (uint32_t)k;
+    w.cl_doc[c] = (uint32_t)(k >> 32);
+  }
+  if (i == n) w.ctr->nclients = w.cl_tmp[n];
+}
+__global__ void k_section_cidx_multi(Work w, uint32_t n) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) w.sections[i].cidx = find_client(w, w.ctr->nclients, w.udoc[w.sections[i].upd], w.sections[i].client);
+}
 
 // NC stays on the device (ctr->nclients) until the struct-decode counter read
 void launch_client_table(Work& w, uint32_t nsections, hipStream_t s) {
   const uint32_t grid = nsections / 256 + 1;
+  if (w.udoc) {
+    hipLaunchKernelGGL(k_gather_sec_keys, dim3(grid), dim3(256), 0, s, w, nsections);
+    sort_pairs_u64_u32(w.tmp, w.tmp_bytes, w.cl_key2, w.cl_key, w.cl_tmp, w.cl_state, nsections, s);
+    hipLaunchKernelGGL(k_unique_keys, dim3(grid), dim3(256), 0, s, w, nsections);
+    scan_u32(w.tmp, w.tmp_bytes, w.scratch, w.cl_tmp, nsections + 1, s);
+    hipLaunchKernelGGL(k_unique_keys_scatter, dim3(grid), dim3(256), 0, s, w, nsections);
+    hipMemcpyAsync(w.cl_key, w.cl_key2, sizeof(uint64_t) * nsections, hipMemcpyDeviceToDevice, s);
+    hipLaunchKernelGGL(k_section_cidx_multi, dim3(grid), dim3(256), 0, s, w, nsections);
+    return;
+  }
   hipLaunchKernelGGL(k_gather_sec_clients, dim3(grid), dim3(256), 0, s, w.sections, nsections, w.cl_tmp);
   sort_u32(w.tmp, w.tmp_bytes, w.cl_tmp, w.cl_vals, nsections, s);
   hipLaunchKernelGGL(k_unique_flags, dim3(grid), dim3(256), 0, s, w.cl_vals, nsections, w.scratch);
@@ -939,10 +974,6 @@ void launch_client_table(Work& w, uint32_t nsections, hipStream_t s) {
 }
 
 // --------------------------------------------------------------------------- 6. struct decode
-__device__ __forceinline__ uint32_t find_cidx(const uint32_t* __restrict__ cl, uint32_t nc, uint32_t client) {
-  const uint32_t i = lower_bound_u32(cl, nc, client);
-  return (i < nc && cl[i] == client) ? i : NONE;
-}
 
 __global__ __launch_bounds__(256) void k_struct_decode(Work w, uint32_t nstructs) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -952,6 +983,7 @@ __global__ __launch_bounds__(256) void k_struct_decode(Work w, uint32_t nstructs
   const uint32_t p0 = w.s_pos[i];
   const Section sec = w.sections[w.s_sec[i]];
   const uint32_t uend = w.uoff[sec.upd] + w.ulen[sec.upd];
+  const uint32_t doc = doc_of_update(w, sec.upd);
   StructView v;
   uint32_t p = p0;
   if (parse_struct<true>(w.bytes, p, uend, 0xFFFFFFFFu, &v) <= 0) { raise_err(err, ERR_DECODE); return; }
@@ -963,11 +995,11 @@ __global__ __launch_bounds__(256) void k_struct_decode(Work w, uint32_t nstructs
   // lazy mode (mergeUpdates / diffUpdate): references are copied, never resolved, so the raw
   // client ids are kept (presence = info bits); integrate mode maps them to client indices
   if (item && (v.info & 0x80u)) {
-    oc = w.lazy ? v.oc : find_cidx(w.cl_vals, nclients, v.oc);
+    oc = w.lazy ? v.oc : find_client(w, nclients, doc, v.oc);
     if (oc == NONE && !w.lazy) oc = UNKNOWN;  // k_refs decides (pending unless capped away)
   }
   if (item && (v.info & 0x40u)) {
-    rc = w.lazy ? v.rc : find_cidx(w.cl_vals, nclients, v.rc);
+    rc = w.lazy ? v.rc : find_client(w, nclients, doc, v.rc);
     if (rc == NONE && !w.lazy) rc = UNKNOWN;
   }
   w.s_ocidx[i] = oc;
@@ -978,7 +1010,7 @@ __global__ __launch_bounds__(256) void k_struct_decode(Work w, uint32_t nstructs
   uint32_t pk = item ? v.pkind : 0u, pa = NONE, pb = 0;
   if (pk == 1) { pa = v.pa; pb = v.pb; }
   else if (pk == 2) {
-    pa = w.lazy ? v.pa : find_cidx(w.cl_vals, nclients, v.pa);
+    pa = w.lazy ? v.pa : find_client(w, nclients, doc, v.pa);
     pb = v.pb;
     if (pa == NONE && !w.lazy) pa = UNKNOWN;
   }

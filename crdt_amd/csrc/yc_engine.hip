@@ -110,7 +110,7 @@ enum Buf {
   B_TPRV, B_TMPRV, B_TMTAIL, B_TTREP, B_TOTAIL,
   B_OFIRST, B_OCIDX, B_OSIZE, B_OPOS, B_RSEG, B_RLEN, B_RSIZE, B_RPOS, B_OUT, B_SVOUT,
   B_VKMAP, B_VKREP, B_VKEYS, B_VNKEYS, B_VPOS, B_VD0, B_VN0, B_VD1, B_VN1, B_VORDER, B_VSEGS,
-  B_SCRATCH2, B_TMP2, B_CAPS,
+  B_SCRATCH2, B_TMP2, B_CAPS, B_CLKEY, B_CLKEY2, B_CLDOC,
   B_COUNT
 };
 
@@ -163,6 +163,9 @@ struct ycrdt_batch {
   ycrdt_engine* e = nullptr;
   DevBuf bytes, meta;
   std::vector<uint32_t> uoff, ulen, ugroup;
+  std::vector<uint32_t> udoc;   // multi-document batch: document of every staged update
+  uint32_t ndocs = 1;
+  size_t udoc_off = 0;          // byte offset of udoc in `meta`
   std::vector<Group> groups;
   uint32_t nbytes = 0;
   uint64_t in_bytes = 0;
@@ -223,7 +226,8 @@ void layout(ycrdt_batch* b, const ycrdt_buf* ups, size_t n, size_t prefix_len) {
   b->nbytes = (uint32_t)total;
 }
 
-int stage(ycrdt_batch* b, const ycrdt_buf* ups, size_t n, const DevBuf* prefix, size_t prefix_len) {
+int stage(ycrdt_batch* b, const ycrdt_buf* ups, size_t n, const DevBuf* prefix, size_t prefix_len,
+          const uint32_t* doc_of = nullptr, uint32_t ndocs = 1) {
   ycrdt_engine* e = b->e;
   size_t total64 = 0;
   for (size_t i = 0; i < n; ++i) total64 += ((ups[i].len + 63) & ~size_t(63));
@@ -242,7 +246,16 @@ int stage(ycrdt_batch* b, const ycrdt_buf* ups, size_t n, const DevBuf* prefix, 
     HIPCHK(hipMemcpyAsync((uint8_t*)b->bytes.p + base, e->pinned_stage.data(), e->pinned_stage.size(), hipMemcpyHostToDevice, e->stream));
   // meta: uoff | ulen | ugroup | groups
   const size_t nu = b->ulen.size();
-  const size_t meta_bytes = sizeof(uint32_t) * (nu + 1 + nu + nu) + sizeof(Group) * b->groups.size() + 64;
+  b->ndocs = doc_of && ndocs > 1 ? ndocs : 1;
+  b->udoc.clear();
+  if (b->ndocs > 1) {
+    if (prefix_len) return fail(YCRDT_E_ARG, "internal: multi-document batch with a state prefix");
+    b->udoc.assign(doc_of, doc_of + n);
+    for (const uint32_t d : b->udoc)
+      if (d >= b->ndocs) return fail(YCRDT_E_ARG, "document index out of range");
+  }
+  const size_t meta_bytes = sizeof(uint32_t) * (nu + 1 + nu + nu) + sizeof(Group) * b->groups.size() + 64 +
+                            sizeof(uint32_t) * b->udoc.size() + 16;
   if (!grow(b->meta, meta_bytes)) return fail(YCRDT_E_DEVICE, "hipMalloc failed (meta)");
   std::vector<uint8_t> meta(meta_bytes, 0);
   size_t o = 0;
@@ -251,6 +264,10 @@ int stage(ycrdt_batch* b, const ycrdt_buf* ups, size_t n, const DevBuf* prefix, 
   memcpy(meta.data() + o, b->ugroup.data(), sizeof(uint32_t) * nu); o += sizeof(uint32_t) * nu;
   o = (o + 15) & ~size_t(15);
   if (!b->groups.empty()) memcpy(meta.data() + o, b->groups.data(), sizeof(Group) * b->groups.size());
+  o += sizeof(Group) * b->groups.size();
+  o = (o + 15) & ~size_t(15);
+  b->udoc_off = o;
+  if (!b->udoc.empty()) memcpy(meta.data() + o, b->udoc.data(), sizeof(uint32_t) * b->udoc.size());
   HIPCHK(hipMemcpyAsync(b->meta.p, meta.data(), meta_bytes, hipMemcpyHostToDevice, e->stream));
   HIPCHK(hipStreamSynchronize(e->stream));
   b->merged = false;
@@ -307,6 +324,8 @@ int run_decode(ycrdt_engine* e, ycrdt_batch* b, bool lazy, Decoded& D) {
     w.groups = (const Group*)((const uint8_t*)b->meta.p + o);
   }
   w.ngroups = (uint32_t)b->groups.size();
+  w.udoc = b->ndocs > 1 ? (const uint32_t*)((const uint8_t*)b->meta.p + b->udoc_off) : nullptr;
+  w.ndocs = b->ndocs;
   w.lazy = lazy ? 1u : 0u;
   const uint64_t B = (uint64_t)b->nbytes + 64;
   const uint64_t nwords = B / 64 + 2;
@@ -361,6 +380,9 @@ int run_decode(ycrdt_engine* e, ycrdt_batch* b, bool lazy, Decoded& D) {
   w.s_celem = take<uint32_t>(V, B_SCELEM, w.cap_structs, ok);
   w.cap_clients = w.cap_sections;
   w.cl_vals = take<uint32_t>(V, B_CLVALS, w.cap_clients + 1, ok);
+  w.cl_key = take<uint64_t>(V, B_CLKEY, w.cap_clients + 1, ok);
+  w.cl_key2 = take<uint64_t>(V, B_CLKEY2, w.cap_clients + 1, ok);
+  w.cl_doc = take<uint32_t>(V, B_CLDOC, w.cap_clients + 1, ok);
   w.cl_tmp = take<uint32_t>(V, B_CLTMP, w.cap_clients + 1, ok);
   w.cl_state = take<uint32_t>(V, B_CLSTATE, w.cap_clients + 1, ok);
   w.cl_base = take<uint64_t>(V, B_CLBASE, w.cap_clients + 2, ok);
@@ -927,6 +949,67 @@ int run_lazy(ycrdt_engine* e, ycrdt_batch* b, bool merge, const std::vector<std:
   return YCRDT_OK;
 }
 
+// Multi-document merge result, split per document on the host. The encoder lays clients out in
+// descending (document, client) order, so every document's struct blocks, delete-set blocks and
+// state-vector entries are contiguous; each document's update is its blocks behind its own
+// varuint counts (writeClientsStructs / writeDeleteSet / writeStateVector headers).
+int split_docs(ycrdt_engine* e, uint32_t ndocs, ycrdt_out* outs, ycrdt_out* svs) {
+  Work& w = e->w;
+  const uint32_t nc = (uint32_t)e->last.clients;
+  const size_t stride = (size_t)w.cap_clients + 1;
+  std::vector<uint32_t> doc(nc), blk(nc), blkpos(nc), nincl(nc), dsblk(nc), dspos(nc), nruns(nc), sv(nc), svpos(nc);
+  std::vector<uint8_t> all(e->out_bytes), svall(e->sv_bytes);
+  Counters c;
+  hipStream_t s = e->stream;
+  HIPCHK(hipMemcpyAsync(&c, w.ctr, sizeof(Counters), hipMemcpyDeviceToHost, s));
+  if (nc) {
+    HIPCHK(hipMemcpyAsync(doc.data(), w.cl_doc, sizeof(uint32_t) * nc, hipMemcpyDeviceToHost, s));
+    const std::pair<uint32_t, std::vector<uint32_t>*> cols[] = {{CC_BLK, &blk}, {CC_BLKPOS, &blkpos}, {CC_NINCL, &nincl},
+                                                                 {CC_DSBLK, &dsblk}, {CC_DSPOS, &dspos}, {CC_NRUNS, &nruns},
+                                                                 {CC_SV, &sv}, {CC_SVPOS, &svpos}};
+    for (const auto& col : cols)
+      HIPCHK(hipMemcpyAsync(col.second->data(), w.cc + col.first * stride, sizeof(uint32_t) * nc, hipMemcpyDeviceToHost, s));
+  }
+  if (!all.empty()) HIPCHK(hipMemcpyAsync(all.data(), w.out, all.size(), hipMemcpyDeviceToHost, s));
+  if (!svall.empty()) HIPCHK(hipMemcpyAsync(svall.data(), w.sv_out, svall.size(), hipMemcpyDeviceToHost, s));
+  HIPCHK(hipStreamSynchronize(s));
+  const uint32_t sbase = c.pad[3], dsbase = c.pad[4] + vu_size_host(c.pad[1]), svbase = vu_size_host(c.pad[2]);
+  struct Rng { uint32_t lo = 0xFFFFFFFFu, hi = 0, n = 0; void add(uint32_t a, uint32_t len, bool in) { if (!in) return; lo = std::min(lo, a); hi = std::max(hi, a + len); ++n; } };
+  std::vector<Rng> rs(ndocs), rd(ndocs), rv(ndocs);
+  for (uint32_t i = 0; i < nc; ++i) {
+    const uint32_t d = doc[i];
+    if (d >= ndocs) return fail(YCRDT_E_DEVICE, "internal: client of an unknown document");
+    rs[d].add(blkpos[i], blk[i], nincl[i] != 0);
+    rd[d].add(dspos[i], dsblk[i], nruns[i] != 0);
+    rv[d].add(svpos[i], sv[i], sv[i] != 0);
+  }
+  auto put = [](std::vector<uint8_t>& o, uint32_t v) {
+    while (v > 127u) { o.push_back((uint8_t)(0x80u | (v & 0x7fu))); v >>= 7; }
+    o.push_back((uint8_t)v);
+  };
+  for (uint32_t d = 0; d < ndocs; ++d) {
+    std::vector<uint8_t> o;
+    put(o, rs[d].n);
+    if (rs[d].n) o.insert(o.end(), all.begin() + sbase + rs[d].lo, all.begin() + sbase + rs[d].hi);
+    put(o, rd[d].n);
+    if (rd[d].n) o.insert(o.end(), all.begin() + dsbase + rd[d].lo, all.begin() + dsbase + rd[d].hi);
+    outs[d].ptr = (uint8_t*)malloc(o.size());
+    if (!outs[d].ptr) return fail(YCRDT_E_CAPACITY, "host allocation failed");
+    outs[d].len = o.size();
+    memcpy(outs[d].ptr, o.data(), o.size());
+    if (svs) {
+      std::vector<uint8_t> v;
+      put(v, rv[d].n);
+      if (rv[d].n) v.insert(v.end(), svall.begin() + svbase + rv[d].lo, svall.begin() + svbase + rv[d].hi);
+      svs[d].ptr = (uint8_t*)malloc(v.size());
+      if (!svs[d].ptr) return fail(YCRDT_E_CAPACITY, "host allocation failed");
+      svs[d].len = v.size();
+      memcpy(svs[d].ptr, v.data(), v.size());
+    }
+  }
+  return YCRDT_OK;
+}
+
 int empty_update(ycrdt_out* out) {
   out->ptr = (uint8_t*)malloc(2);
   out->ptr[0] = 0;
@@ -1269,6 +1352,48 @@ int ycrdt_batch_stage(ycrdt_engine* e, const ycrdt_buf* ups, size_t n, ycrdt_bat
   if (rc) { ycrdt_batch_destroy(b); return rc; }
   *out = b;
   return YCRDT_OK;
+}
+
+int ycrdt_batch_stage_docs(ycrdt_engine* e, const ycrdt_buf* ups, const uint32_t* doc_of, size_t n, uint32_t ndocs,
+                           ycrdt_batch** out) {
+  if (!e || !out || (n && (!ups || !doc_of)) || !ndocs) return fail(YCRDT_E_ARG, "null arg");
+  HIPCHK(hipSetDevice(e->device));
+  auto* b = new ycrdt_batch();
+  b->e = e;
+  int rc = stage(b, ups, n, nullptr, 0, doc_of, ndocs);
+  if (rc) { ycrdt_batch_destroy(b); return rc; }
+  b->ndocs = ndocs;
+  *out = b;
+  return YCRDT_OK;
+}
+
+int ycrdt_batch_result_docs(ycrdt_batch* b, ycrdt_out* updates, ycrdt_out* svs) {
+  if (!b || !b->merged || !updates) return fail(YCRDT_E_ARG, "batch not merged");
+  ycrdt_engine* e = b->e;
+  if (e->ws_owner != b) return fail(YCRDT_E_ARG, "batch result no longer available (another engine call ran since ycrdt_batch_merge)");
+  HIPCHK(hipSetDevice(e->device));
+  for (uint32_t d = 0; d < b->ndocs; ++d) { updates[d] = ycrdt_out{nullptr, 0}; if (svs) svs[d] = ycrdt_out{nullptr, 0}; }
+  if (b->ndocs == 1) return ycrdt_batch_result(b, updates, svs);
+  const int rc = split_docs(e, b->ndocs, updates, svs);
+  if (rc) for (uint32_t d = 0; d < b->ndocs; ++d) { ycrdt_free(&updates[d]); if (svs) ycrdt_free(&svs[d]); }
+  return rc;
+}
+
+int ycrdt_merge_docs(ycrdt_engine* e, const ycrdt_buf* ups, const uint32_t* doc_of, size_t n, uint32_t ndocs,
+                     ycrdt_out* updates, ycrdt_out* svs) {
+  if (!e || !updates || (n && (!ups || !doc_of)) || !ndocs) return fail(YCRDT_E_ARG, "null arg");
+  HIPCHK(hipSetDevice(e->device));
+  ycrdt_batch& b = scratch_batch(e);
+  int rc = stage(&b, ups, n, nullptr, 0, doc_of, ndocs);
+  if (rc == YCRDT_OK) rc = run_merge(e, &b, nullptr);
+  if (rc) return rc;
+  b.merged = true;
+  e->ws_owner = &b;
+  const uint32_t nd = b.ndocs;
+  b.ndocs = ndocs;
+  rc = ycrdt_batch_result_docs(&b, updates, svs);
+  b.ndocs = nd;
+  return rc;
 }
 
 int ycrdt_batch_merge(ycrdt_batch* b, ycrdt_merge_stats* st) {

@@ -68,12 +68,12 @@ __global__ void k_ds_prep(Work w, uint32_t nds, uint32_t nclients) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= nds) { if (i == nds) w.ds_len[i] = 0; return; }
   DsRange r = w.ds[i];
-  const uint32_t c = lower_bound_u32(w.cl_vals, nclients, r.client);
+  const uint32_t c = find_client(w, nclients, doc_of_update(w, r.upd), r.client);
   uint32_t len = r.len;
   if (len == 0) { w.ds_len[i] = 0; return; }
   // a range past the known state is Yjs's pendingDs: an error here (the host then takes the pending
   // path), clipped silently when the host already computed the caps
-  if (c >= nclients || w.cl_vals[c] != r.client) { if (!w.capped) raise_err(&w.ctr->err, ERR_PENDING); w.ds_len[i] = 0; return; }
+  if (c == NONE) { if (!w.capped) raise_err(&w.ctr->err, ERR_PENDING); w.ds_len[i] = 0; return; }
   const uint64_t endc = (uint64_t)r.clock + len;
   if (endc > w.cl_state[c]) { if (!w.capped) raise_err(&w.ctr->err, ERR_PENDING); len = r.clock < w.cl_state[c] ? w.cl_state[c] - r.clock : 0; }
   r.client = c;
@@ -254,6 +254,7 @@ __global__ __launch_bounds__(256) void k_seg_props(Work w, uint32_t nsegs) {
     uint64_t h = 1469598103934665603ull;
     uint32_t parent = NONE;
     if (pk == 1) {
+      if (w.udoc) h = fnv_u32(h ^ 0x3Cu, w.cl_doc[cidx]);  // root types are per document
       h = fnv_bytes(h, w.bytes + w.s_pa[own], w.s_pb[own]);
     } else if (pk == 2) {
       const uint32_t pc = w.s_pa[own], pclock = w.s_pb[own];

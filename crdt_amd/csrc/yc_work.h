@@ -67,6 +67,8 @@ struct Work {
   const uint32_t* ulen = nullptr;  // [nupd] real update lengths
   const uint32_t* ugroup = nullptr;// [nupd] first decode group of each update
   uint32_t nupd = 0;
+  const uint32_t* udoc = nullptr;  // [nupd] document of every update (multi-document batches); nullptr = one doc
+  uint32_t ndocs = 1;
   uint32_t lazy = 0;               // 1: mergeUpdates / diffUpdate decode (references kept raw)
   unsigned long long* dbg = nullptr; // YCRDT_DEBUG_TABLES=1: per-group phase timestamps of k_tables
   const Group* groups = nullptr;   // [G]
@@ -116,6 +118,9 @@ struct Work {
   uint32_t* s_celem = nullptr;     // position of first Any/JSON element (after the count varuint)
   // ---- clients (NC)
   uint32_t* cl_vals = nullptr;     // sorted distinct client ids [cap_sections]
+  uint64_t* cl_key = nullptr;      // multi-doc: sorted distinct (doc << 32 | client) keys; cl_vals = their low words
+  uint64_t* cl_key2 = nullptr;     // multi-doc sort scratch
+  uint32_t* cl_doc = nullptr;      // document of every client index (multi-doc)
   uint32_t* cl_tmp = nullptr;      // sort scratch [cap_sections]
   uint32_t* cl_state = nullptr;    // per client state (max end clock)
   uint64_t* cl_base = nullptr;     // [NC+1] exclusive prefix of states (unit base)
@@ -247,6 +252,20 @@ struct Work {
   void* tmp = nullptr;
   size_t tmp_bytes = 0;
 };
+
+// client index of (document, client id); NONE if the batch has no such client. Multi-document
+// batches index clients by (doc, client), so every per-client structure stays per document.
+__device__ __forceinline__ uint32_t find_client(const Work& w, uint32_t nclients, uint32_t doc, uint32_t client) {
+  if (!w.udoc) {
+    const uint32_t i = lower_bound_u32(w.cl_vals, nclients, client);
+    return (i < nclients && w.cl_vals[i] == client) ? i : NONE;
+  }
+  const uint64_t key = ((uint64_t)doc << 32) | client;
+  uint32_t lo = 0, hi = nclients;
+  while (lo < hi) { const uint32_t m = (lo + hi) >> 1; if (w.cl_key[m] < key) lo = m + 1; else hi = m; }
+  return (lo < nclients && w.cl_key[lo] == key) ? lo : NONE;
+}
+__device__ __forceinline__ uint32_t doc_of_update(const Work& w, uint32_t upd) { return w.udoc ? w.udoc[upd] : 0u; }
 
 // Byte range of content elements [e0, e1) of struct `src` (ContentAny: lib0 `any` values,
 // ContentJSON: varStrings, ContentString: UTF-16 code units of the UTF-8 text; every other

@@ -155,6 +155,17 @@ int ycrdt_batch_merge(ycrdt_batch *b, ycrdt_merge_stats *st);
  * engine workspace: any other engine call in between makes this fail with YCRDT_E_ARG. */
 int ycrdt_batch_result(ycrdt_batch *b, ycrdt_out *update, ycrdt_out *state_vector);
 void ycrdt_batch_destroy(ycrdt_batch *b);
+/* Multi-document batches (C5 fleets: one Y.Doc per topic, crdt.js:235; and many independent replica
+ * sets per device pass): update i belongs to document doc_of[i] < ndocs. One device pass merges
+ * every document on its own (clients, lists and delete sets never mix across documents); the
+ * result of document d equals merging its updates alone. */
+int ycrdt_batch_stage_docs(ycrdt_engine *e, const ycrdt_buf *ups, const uint32_t *doc_of, size_t n, uint32_t ndocs,
+                           ycrdt_batch **out);
+/* updates[ndocs] (and state_vectors[ndocs] unless NULL) receive every document's encoded state */
+int ycrdt_batch_result_docs(ycrdt_batch *b, ycrdt_out *updates, ycrdt_out *state_vectors);
+/* one-shot form of the two above (host buffers in and out) */
+int ycrdt_merge_docs(ycrdt_engine *e, const ycrdt_buf *ups, const uint32_t *doc_of, size_t n, uint32_t ndocs,
+                     ycrdt_out *updates, ycrdt_out *state_vectors);
 
 /* ---- host-only entry points (no HIP device needed) ---------------------------------------- */
 /* The validation Y.applyUpdate runs before queueing an update: YCRDT_OK, or YCRDT_E_DECODE with
