@@ -1,20 +1,23 @@
 #!/usr/bin/env python3
-"""Benchmark: CRDT items merged/sec on MI355X (BASELINE.json metric) — config C2.
+"""Benchmark: CRDT items merged/sec on MI355X (BASELINE.json metric) — config C2, at scale.
 
 Workload (BASELINE.json configs[1]): one YMap 'users' with 100k hot keys
-(Zipf s=1.1), a base snapshot of every key by one client, then 1,000 replicas × 1,000 concurrent
-set/delete ops with no gossip; the input batch is the base update plus every replica's
+(Zipf s=1.1), a base snapshot of every key by one client, then 1,000 replicas x 1,000 concurrent
+set/delete ops with no gossip; a document's input is the base update plus every replica's
 encodeStateAsUpdate(replica, baseSV) — 1,001 Yjs v1 updates, ≈13.5 MB, ≈0.9 M items.
 
-A step = one batched merge of that batch on the device (decode → dedupe → delete sets → YMap
-winner → canonical re-encode), inputs already resident in HBM, output left in HBM. It is exactly
-what `for u in batch: Y.applyUpdate(doc, u)` followed by `Y.encodeStateAsUpdate(doc)` computes
-(byte-identical; tests/test_gpu_parity.py). Items = Σ struct clock lengths of the inputs (Item +
-GC, Skip excluded), the SURVEY §8(d) unit.
+A step = one device pass that merges `--docs` (default 112) such documents — independent replica
+sets with different seeds, ≥ 100 M items — as a multi-document batch (ycrdt_batch_stage_docs:
+decode → dedupe → delete sets → YMap winner → canonical re-encode per document), inputs already
+resident in HBM, outputs left in HBM. Each document's result is exactly what `for u in doc:
+Y.applyUpdate(d, u)` followed by `Y.encodeStateAsUpdate(d)` computes (byte-identical;
+tests/test_gpu_parity.py, tests/test_gpu_multidoc.py). Items = Σ struct clock lengths of the
+inputs (Item + GC, Skip excluded), the SURVEY §8(d) unit. `single_doc` keeps the one-document
+step of round 1 for continuity.
 
 Multi-GPU: one process per GPU; the path shards by document (north_star: "partitioned ... by
-document/topic"), so every rank merges its own independent C2 document (seed + rank) with no
-data-path collective ⇒ "scaling": "weak". torch.distributed (RCCL) is used only for the barrier
+document/topic"), so every rank merges its own independent documents (seeds offset per rank) with
+no data-path collective ⇒ "scaling": "weak". torch.distributed (RCCL) is used only for the barrier
 and the max-over-ranks of the step time.
 """
 import argparse
@@ -37,6 +40,8 @@ def parse():
     p.add_argument("--steps", type=int, default=20)
     p.add_argument("--warmup", type=int, default=3)
     p.add_argument("--workload", default="c2", choices=["c2", "c1"])
+    p.add_argument("--docs", type=int, default=112,
+                   help="independent documents of the workload merged per step in one device pass (>= 100 M items)")
     p.add_argument("--replicas", type=int, default=None, help="override replica count (default: config)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--fleet-pairs", type=int, default=20000,
@@ -333,16 +338,30 @@ def main():
     cfg = dict(C2 if args.workload == "c2" else C1)
     if args.replicas:
         cfg["n_replicas"] = args.replicas
-    cfg["seed"] = cfg["seed"] + rank  # independent document per rank
-    updates, _ = gen_map(**cfg)
-    in_bytes = sum(len(u) for u in updates)
+    # every rank merges its own documents (weak scaling); document 0 of rank 0 is the pinned C2
+    seeds = [cfg["seed"] + rank * 100_003 + i * 1_009 for i in range(max(1, args.docs))]
+    from concurrent.futures import ThreadPoolExecutor
+
+    with ThreadPoolExecutor(16) as ex:
+        docs = list(ex.map(lambda sd: gen_map(**dict(cfg, seed=sd))[0], seeds))
+    cfg["seed"] = seeds[0]
+    updates = docs[0]
+    ndocs = len(docs)
+    in_bytes = sum(len(u) for d in docs for u in d)
 
     eng = crdt_amd.Engine(device=local if world > 1 else int(os.environ.get("YCRDT_DEVICE", "0")))
-    batch = crdt_amd.Batch(updates, eng)
+    batch = crdt_amd.Batch(docs=docs, engine=eng) if ndocs > 1 else crdt_amd.Batch(updates, eng)
     st = None
     for _ in range(max(1, args.warmup)):
         st = batch.merge()
-    out_update, out_sv = batch.result()
+    if ndocs > 1:
+        results = batch.result_docs()
+        out_update, out_sv = results[0]
+        out_bytes = sum(len(u) + len(v) for u, v in results)
+        del results
+    else:
+        out_update, out_sv = batch.result()
+        out_bytes = len(out_update) + len(out_sv)
 
     def barrier():
         if dist is not None:
@@ -416,21 +435,38 @@ def main():
         "largest_phase": {"name": dominant[0], "ms": round(dominant[1], 4)},
     }
     # algorithmic bytes of the whole merge: B_in + B_out + 64·S
-    b_alg = in_bytes + len(out_update) + len(out_sv) + 64 * st.structs
+    b_alg = in_bytes + out_bytes + 64 * st.structs
+    steps_items = st.items
 
-    # ---- end to end (host buffers in, host buffers out): pack + H2D + merge + D2H; never `value`
-    e2e_steps = 3
+    # ---- end to end (host buffers in, host buffers out): pack + H2D + merge + D2H + per-document
+    # split; never `value`
+    e2e_steps = 2
     e0 = time.perf_counter()
     for _ in range(e2e_steps):
-        b2 = crdt_amd.Batch(updates, eng)
+        b2 = crdt_amd.Batch(docs=docs, engine=eng) if ndocs > 1 else crdt_amd.Batch(updates, eng)
         b2.merge()
-        b2.result()
+        if ndocs > 1:
+            b2.result_docs()
+        else:
+            b2.result()
         del b2
     e2e_ms = (time.perf_counter() - e0) * 1e3 / e2e_steps
+    del batch
+    # ---- one C2 document per step (the round-1 headline shape), for continuity
+    single = None
+    if ndocs > 1 and rank == 0:
+        sb = crdt_amd.Batch(updates, eng)
+        sst = sb.merge()
+        s0 = time.perf_counter()
+        for _ in range(10):
+            sst = sb.merge()
+        sms = (time.perf_counter() - s0) * 1e3 / 10
+        single = {"ms_per_step": round(sms, 4), "items_per_step": sst.items, "items_per_s": round(sst.items / (sms * 1e-3), 1)}
+        del sb
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baselines(args, cfg, updates, out_update, st, eng, gen_map)
+        cpu = cpu_baselines(args, cfg, updates, out_update, crdt_amd.Batch(updates, eng).merge(), eng, gen_map)
     fleet = None
     if rank == 0 and world == 1 and args.fleet_pairs > 0:
         fleet = fleet_sync_leg(eng, args.fleet_pairs)
@@ -450,20 +486,24 @@ def main():
         "dtype": "u8/u32 (integer byte-stream + index work)",
         "data": "synthetic (seeded C2 generator, pinned byte-exact against Yjs 13.5.16)",
         "config": {
-            "workload": f"{args.workload.upper()}: YMap 'users', {cfg['n_keys']} keys, {cfg['n_replicas']} replicas x "
-                        f"{cfg['ops_per_replica']} set/del ops" + (", base snapshot" if cfg["base_snapshot"] else ""),
-            "updates_per_step": len(updates),
+            "workload": f"{args.workload.upper()} x {ndocs} documents per step, one device pass: YMap 'users', "
+                        f"{cfg['n_keys']} keys, {cfg['n_replicas']} replicas x {cfg['ops_per_replica']} set/del ops per "
+                        "document" + (", base snapshot" if cfg["base_snapshot"] else ""),
+            "docs_per_step": ndocs,
+            "updates_per_step": sum(len(d) for d in docs),
             "input_bytes": in_bytes,
             "items_per_step_per_gpu": st.items,
             "structs": st.structs,
             "segments": st.segments,
-            "output_bytes": len(out_update),
+            "output_bytes": out_bytes,
             "parallelism": f"doc-sharded x{world}",
         },
+        "single_doc": single,
         "device_ms_per_step": round(dev_ms / args.steps, 4),
         "unique_items_per_step_per_gpu": st.units,
-        "end_to_end": {"ms_per_step": round(e2e_ms, 3), "items_per_s": round(st.items / (e2e_ms * 1e-3), 1),
-                       "includes": "host pack + H2D + merge + D2H of the update and state vector, 1 GPU"},
+        "end_to_end": {"ms_per_step": round(e2e_ms, 3), "items_per_s": round(steps_items / (e2e_ms * 1e-3), 1),
+                       "includes": "host pack + H2D + merge + D2H of every document's update and state vector "
+                                   "(split per document on the host), 1 GPU"},
         "pipeline_roofline": {
             "b_alg_bytes": b_alg,
             "achieved_GBs": round(b_alg / (ms_per_step * 1e-3) / 1e9, 2),

@@ -749,14 +749,19 @@ __global__ void k_struct_sec(Work w, uint32_t nstructs) {
   w.s_sec[i] = w.sec_sorted[rank_incl(w.sec_bits, w.wsec, p) - 1];
 }
 
-void launch_struct_positions(const Work& w, hipStream_t s) {
+// before the count sync: struct / section-start counts (popcount prefix of the bitmaps)
+void launch_struct_count(const Work& w, hipStream_t s) {
   const uint32_t nwords = (w.nbytes + 63) / 64;
   hipLaunchKernelGGL(k_popc, dim3(nwords / 256 + 1), dim3(256), 0, s, w.final_bits, w.scratch, nwords);
   scan_u32(w.tmp, w.tmp_bytes, w.scratch, w.wcnt, nwords + 1, s);
-  hipLaunchKernelGGL(k_scatter_pos, dim3(nwords / 256 + 1), dim3(256), 0, s, w.final_bits, w.wcnt, nwords, w.s_pos,
-                     w.cap_structs, &w.ctr->err);
   hipLaunchKernelGGL(k_popc, dim3(nwords / 256 + 1), dim3(256), 0, s, w.sec_bits, w.scratch, nwords);
   scan_u32(w.tmp, w.tmp_bytes, w.scratch, w.wsec, nwords + 1, s);
+}
+// after it (the struct table is sized from the count): dense struct positions
+void launch_struct_scatter(const Work& w, hipStream_t s) {
+  const uint32_t nwords = (w.nbytes + 63) / 64;
+  hipLaunchKernelGGL(k_scatter_pos, dim3(nwords / 256 + 1), dim3(256), 0, s, w.final_bits, w.wcnt, nwords, w.s_pos,
+                     w.cap_structs, &w.ctr->err);
 }
 
 // called once the section count is known on the host
@@ -895,10 +900,15 @@ __global__ void k_ds_compact(Work w) {  // one wave per update: region -> dense 
   if (u == w.nupd - 1 && lane == 0) w.ctr->nds = dst + n;
 }
 
-void launch_ds_decode(const Work& w, hipStream_t s) {
+// delete-set regions (before the count sync: the range arrays are sized from their total)
+void launch_ds_bound(const Work& w, hipStream_t s) {
   if (w.nupd == 0) return;
   hipLaunchKernelGGL(k_ds_bound, dim3(w.nupd / 256 + 1), dim3(256), 0, s, w);
   scan_u32(w.tmp, w.tmp_bytes, w.scratch, w.ds_region, w.nupd + 1, s);
+  hipMemcpyAsync(&w.ctr->ds_region, w.ds_region + w.nupd, sizeof(uint32_t), hipMemcpyDeviceToDevice, s);
+}
+void launch_ds_decode(const Work& w, hipStream_t s) {
+  if (w.nupd == 0) return;
   hipLaunchKernelGGL(k_ds_decode, dim3((w.nupd + 3) / 4), dim3(256), 0, s, w);
   scan_u32(w.tmp, w.tmp_bytes, w.ds_count, w.ds_dense_off, w.nupd + 1, s);
   hipLaunchKernelGGL(k_ds_compact, dim3((w.nupd + 3) / 4), dim3(256), 0, s, w);

@@ -5,7 +5,8 @@
 //   * client blocks are written in descending client order; a client is included when its state
 //     exceeds the target state vector, and its first struct is written with offset sv − clock;
 //   * the delete set is always the full store's runs of consecutive deleted structs, clients in
-//     descending order (Yjs 13.6 canonical order; 13.5.16 used store insertion order).
+//     descending order (Yjs 13.6 canonical order) or, with cl_emit (compat 135), in the store's
+//     client insertion order (13.5.16 iterates store.clients, Y@10800), as is the state vector.
 // Every size is computed first (one lane per output struct / run / client), positions come from
 // exclusive scans, then a second pass writes the bytes.
 #include "yc_work.h"
@@ -239,19 +240,26 @@ __global__ void k_client_sizes(Work w, uint32_t nclients, uint32_t nsegs) {
 }
 
 // reverse the three per-client size columns (structs, delete set, state vector) so that ascending
-// scans yield descending-client positions; one launch each way for all three
+// scans yield descending-client positions; one launch each way for all three. With cl_emit
+// (compat 135) the delete-set and state-vector columns follow the store insertion order instead.
+__device__ __forceinline__ uint32_t emit_slot_client(const Work& w, uint32_t nclients, int k, uint32_t i) {
+  return (k > 0 && w.cl_emit) ? w.cl_emit[i] : nclients - 1 - i;
+}
 __global__ void k_reverse3(Work w, uint32_t nclients) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i > nclients) return;
   const uint32_t src[3] = {CC_BLK, CC_DSBLK, CC_SV}, dst[3] = {CC_REV, CC_REV2, CC_REV3};
-  for (int k = 0; k < 3; ++k) ccol(w, dst[k])[i] = i < nclients ? ccol(w, src[k])[nclients - 1 - i] : 0;
+  for (int k = 0; k < 3; ++k) ccol(w, dst[k])[i] = i < nclients ? ccol(w, src[k])[emit_slot_client(w, nclients, k, i)] : 0;
 }
 __global__ void k_unreverse3(Work w, uint32_t nclients) {
   const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
   if (c > nclients) return;
-  // position of client c = sum of blocks of clients > c = scan[nclients-1-c]; total at [nclients]
+  // position of client c = sum of the blocks written before it = scan[slot of c]; total at [nclients]
   const uint32_t src[3] = {CC_REVSCAN, CC_REVSCAN2, CC_REVSCAN3}, dst[3] = {CC_BLKPOS, CC_DSPOS, CC_SVPOS};
-  for (int k = 0; k < 3; ++k) ccol(w, dst[k])[c] = ccol(w, src[k])[c < nclients ? nclients - 1 - c : nclients];
+  for (int k = 0; k < 3; ++k) {
+    const uint32_t slot = c == nclients ? nclients : (k > 0 && w.cl_emit) ? w.cl_slot[c] : nclients - 1 - c;
+    ccol(w, dst[k])[c] = ccol(w, src[k])[slot];
+  }
 }
 
 __global__ void k_totals(Work w, uint32_t nclients) {

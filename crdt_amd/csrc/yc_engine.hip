@@ -110,7 +110,7 @@ enum Buf {
   B_TPRV, B_TMPRV, B_TMTAIL, B_TTREP, B_TOTAIL,
   B_OFIRST, B_OCIDX, B_OSIZE, B_OPOS, B_RSEG, B_RLEN, B_RSIZE, B_RPOS, B_OUT, B_SVOUT,
   B_VKMAP, B_VKREP, B_VKEYS, B_VNKEYS, B_VPOS, B_VD0, B_VN0, B_VD1, B_VN1, B_VORDER, B_VSEGS,
-  B_SCRATCH2, B_TMP2, B_CAPS, B_CLKEY, B_CLKEY2, B_CLDOC,
+  B_SCRATCH2, B_TMP2, B_CAPS, B_CLKEY, B_CLKEY2, B_CLDOC, B_DSFA, B_EMIT,
   B_COUNT
 };
 
@@ -301,7 +301,7 @@ struct Decoded {
 
 // K1: decode every update of the batch into the struct SoA (+ client table, delete-set ranges).
 // lazy = mergeUpdates / diffUpdate mode: references stay raw client ids, no client states.
-int run_decode(ycrdt_engine* e, ycrdt_batch* b, bool lazy, Decoded& D) {
+int run_decode(ycrdt_engine* e, ycrdt_batch* b, bool lazy, Decoded& D, bool generous = false) {
   Work& w = e->w;
   auto& V = e->bufs;
   bool ok = true;
@@ -329,11 +329,17 @@ int run_decode(ycrdt_engine* e, ycrdt_batch* b, bool lazy, Decoded& D) {
   w.lazy = lazy ? 1u : 0u;
   const uint64_t B = (uint64_t)b->nbytes + 64;
   const uint64_t nwords = B / 64 + 2;
-  w.cap_structs = (uint32_t)(B / 2 + 64);
-  w.cap_sections = (uint32_t)(B / 3 + 64);
-  w.cap_copy = w.ngroups + w.cap_structs + 64;  // every segment holds >= 1 struct
-  w.cap_patch = w.cap_structs;
-  w.cap_ds = (uint32_t)(B / 2 + 64);
+  // The walker's outputs are sized from estimates (a capacity overflow reruns the decode with the
+  // worst-case bounds); the struct table, the client table and the delete-set ranges are sized
+  // after the count sync from the real counts, so the workspace follows the content, not B.
+  const uint64_t est_sec = generous ? B / 3 + 64 : std::min<uint64_t>(B / 3 + 64, (uint64_t)nu * 16 + B / 256 + 4096);
+  const uint64_t est_copy = generous ? w.ngroups + B / 2 + 64 : std::min<uint64_t>(w.ngroups + B / 2 + 64, (uint64_t)w.ngroups * 64 + B / 16 + 4096);
+  const uint64_t est_patch = generous ? B / 2 + 64 : std::min<uint64_t>(B / 2 + 64, B / 16 + 4096);
+  w.cap_sections = (uint32_t)est_sec;
+  w.cap_copy = (uint32_t)est_copy;
+  w.cap_patch = (uint32_t)est_patch;
+  w.cap_structs = 0;
+  w.cap_ds = 0;
   // ---- decode buffers
   w.ctr = take<Counters>(V, B_CTR, 1, ok);
   w.tab.nxt = take<uint16_t>(V, B_TNXT, B, ok);
@@ -352,42 +358,11 @@ int run_decode(ycrdt_engine* e, ycrdt_batch* b, bool lazy, Decoded& D) {
   w.sec_sorted = take<uint32_t>(V, B_SECSORT, w.cap_sections, ok);
   w.wcnt = take<uint32_t>(V, B_WCNT, nwords + 1, ok);
   w.wsec = take<uint32_t>(V, B_WSEC, nwords + 1, ok);
-  w.ds = take<DsRange>(V, B_DS, w.cap_ds, ok);
-  w.ds_tmp = take<DsRange>(V, B_DSTMP, w.cap_ds, ok);
   w.ds_region = take<uint32_t>(V, B_DSREG, nu + 2, ok);
   w.ds_count = take<uint32_t>(V, B_DSCNT, nu + 2, ok);
   w.ds_dense_off = take<uint32_t>(V, B_DSOFF, nu + 2, ok);
-  w.ds_len = take<uint32_t>(V, B_DSLEN, w.cap_ds + 1, ok);
-  w.ds_scan = take<uint64_t>(V, B_DSSCAN, w.cap_ds + 1, ok);
-  w.s_pos = take<uint32_t>(V, B_SPOS, w.cap_structs, ok);
-  w.s_sec = take<uint32_t>(V, B_SSEC, w.cap_structs, ok);
-  w.s_len = take<uint32_t>(V, B_SLEN, w.cap_structs + 1, ok);
-  w.s_lenscan = take<uint64_t>(V, B_SLENSCAN, w.cap_structs + 1, ok);
-  w.s_clock = take<uint32_t>(V, B_SCLOCK, w.cap_structs, ok);
-  w.s_cidx = take<uint32_t>(V, B_SCIDX, w.cap_structs, ok);
-  w.s_info = take<uint8_t>(V, B_SINFO, w.cap_structs, ok);
-  w.s_ocidx = take<uint32_t>(V, B_SOC, w.cap_structs, ok);
-  w.s_oclock = take<uint32_t>(V, B_SOK, w.cap_structs, ok);
-  w.s_rcidx = take<uint32_t>(V, B_SRC, w.cap_structs, ok);
-  w.s_rclock = take<uint32_t>(V, B_SRK, w.cap_structs, ok);
-  w.s_pk = take<uint8_t>(V, B_SPK, w.cap_structs, ok);
-  w.s_pa = take<uint32_t>(V, B_SPA, w.cap_structs, ok);
-  w.s_pb = take<uint32_t>(V, B_SPB, w.cap_structs, ok);
-  w.s_psub = take<uint32_t>(V, B_SPS, w.cap_structs, ok);
-  w.s_psublen = take<uint32_t>(V, B_SPL, w.cap_structs, ok);
-  w.s_cpos = take<uint32_t>(V, B_SCPOS, w.cap_structs, ok);
-  w.s_cend = take<uint32_t>(V, B_SCEND, w.cap_structs, ok);
-  w.s_celem = take<uint32_t>(V, B_SCELEM, w.cap_structs, ok);
   w.cap_clients = w.cap_sections;
-  w.cl_vals = take<uint32_t>(V, B_CLVALS, w.cap_clients + 1, ok);
-  w.cl_key = take<uint64_t>(V, B_CLKEY, w.cap_clients + 1, ok);
-  w.cl_key2 = take<uint64_t>(V, B_CLKEY2, w.cap_clients + 1, ok);
-  w.cl_doc = take<uint32_t>(V, B_CLDOC, w.cap_clients + 1, ok);
-  w.cl_tmp = take<uint32_t>(V, B_CLTMP, w.cap_clients + 1, ok);
-  w.cl_state = take<uint32_t>(V, B_CLSTATE, w.cap_clients + 1, ok);
-  w.cl_base = take<uint64_t>(V, B_CLBASE, w.cap_clients + 2, ok);
-  w.cl_start = take<uint32_t>(V, B_CLSTART, w.cap_clients + 1, ok);
-  w.scratch = take<uint32_t>(V, B_SCRATCH, std::max<uint64_t>({nwords + 2, (uint64_t)w.cap_sections + 2, (uint64_t)nu + 2}), ok);
+  w.scratch = take<uint32_t>(V, B_SCRATCH, std::max<uint64_t>({nwords + 2, (uint64_t)w.cap_sections + 66, (uint64_t)nu + 2}), ok);
   w.usec_start = take<uint32_t>(V, B_USEC, nu + 1, ok);
   w.usec_n = take<uint32_t>(V, B_USECN, nu + 1, ok);
   if (!ok) return fail(YCRDT_E_DEVICE, "hipMalloc failed (decode workspace)");
@@ -455,13 +430,52 @@ int run_decode(ycrdt_engine* e, ycrdt_batch* b, bool lazy, Decoded& D) {
   launch_walker(w, s);
   mark(e, "decode.bitmap");
   launch_build_final_bits(w, s);
-  launch_struct_positions(w, s);
+  launch_struct_count(w, s);
+  launch_ds_bound(w, s);
   HIPCHK(hipMemcpyAsync(&w.ctr->nstructs, w.wcnt + (w.nbytes + 63) / 64, sizeof(uint32_t), hipMemcpyDeviceToDevice, s));
   Counters c;
   int rc = check(e, c, "decode");
+  if (rc == YCRDT_E_CAPACITY && !generous) return run_decode(e, b, lazy, D, true);  // past the estimates
   if (rc) return rc;
   const uint32_t nstructs = c.nstructs;
   const uint32_t nsections = c.nsections;
+  // ---- tables sized from the counts
+  w.cap_structs = nstructs + 64;
+  w.cap_ds = c.ds_region + 64;
+  w.cap_clients = nsections + 64;
+  w.ds = take<DsRange>(V, B_DS, w.cap_ds, ok);
+  w.ds_tmp = take<DsRange>(V, B_DSTMP, w.cap_ds, ok);
+  w.ds_len = take<uint32_t>(V, B_DSLEN, w.cap_ds + 1, ok);
+  w.ds_scan = take<uint64_t>(V, B_DSSCAN, w.cap_ds + 1, ok);
+  w.s_pos = take<uint32_t>(V, B_SPOS, w.cap_structs, ok);
+  w.s_sec = take<uint32_t>(V, B_SSEC, w.cap_structs, ok);
+  w.s_len = take<uint32_t>(V, B_SLEN, w.cap_structs + 1, ok);
+  w.s_lenscan = take<uint64_t>(V, B_SLENSCAN, w.cap_structs + 1, ok);
+  w.s_clock = take<uint32_t>(V, B_SCLOCK, w.cap_structs, ok);
+  w.s_cidx = take<uint32_t>(V, B_SCIDX, w.cap_structs, ok);
+  w.s_info = take<uint8_t>(V, B_SINFO, w.cap_structs, ok);
+  w.s_ocidx = take<uint32_t>(V, B_SOC, w.cap_structs, ok);
+  w.s_oclock = take<uint32_t>(V, B_SOK, w.cap_structs, ok);
+  w.s_rcidx = take<uint32_t>(V, B_SRC, w.cap_structs, ok);
+  w.s_rclock = take<uint32_t>(V, B_SRK, w.cap_structs, ok);
+  w.s_pk = take<uint8_t>(V, B_SPK, w.cap_structs, ok);
+  w.s_pa = take<uint32_t>(V, B_SPA, w.cap_structs, ok);
+  w.s_pb = take<uint32_t>(V, B_SPB, w.cap_structs, ok);
+  w.s_psub = take<uint32_t>(V, B_SPS, w.cap_structs, ok);
+  w.s_psublen = take<uint32_t>(V, B_SPL, w.cap_structs, ok);
+  w.s_cpos = take<uint32_t>(V, B_SCPOS, w.cap_structs, ok);
+  w.s_cend = take<uint32_t>(V, B_SCEND, w.cap_structs, ok);
+  w.s_celem = take<uint32_t>(V, B_SCELEM, w.cap_structs, ok);
+  w.cl_vals = take<uint32_t>(V, B_CLVALS, w.cap_clients + 1, ok);
+  w.cl_key = take<uint64_t>(V, B_CLKEY, w.cap_clients + 1, ok);
+  w.cl_key2 = take<uint64_t>(V, B_CLKEY2, w.cap_clients + 1, ok);
+  w.cl_doc = take<uint32_t>(V, B_CLDOC, w.cap_clients + 1, ok);
+  w.cl_tmp = take<uint32_t>(V, B_CLTMP, w.cap_clients + 1, ok);
+  w.cl_state = take<uint32_t>(V, B_CLSTATE, w.cap_clients + 1, ok);
+  w.cl_base = take<uint64_t>(V, B_CLBASE, w.cap_clients + 2, ok);
+  w.cl_start = take<uint32_t>(V, B_CLSTART, w.cap_clients + 1, ok);
+  if (!ok) return fail(YCRDT_E_DEVICE, "hipMalloc failed (struct table)");
+  launch_struct_scatter(w, s);
   mark(e, "decode.sections");
   {  // the delete sets decode on the side stream (own scratch / scan space) while the client
      // table and the struct table are built; both streams only read what the sync above published
@@ -499,8 +513,9 @@ int run_decode(ycrdt_engine* e, ycrdt_batch* b, bool lazy, Decoded& D) {
 
 // The whole batched merge. `target` (optional) selects a delta encode against a state vector;
 // `caps` (optional) integrates every client only up to its cap (Yjs pending structs, yc_ingest.h).
+// `order` (compat 135): the doc store's client insertion order, the delete-set / state-vector order.
 int run_merge(ycrdt_engine* e, ycrdt_batch* b, const std::unordered_map<uint32_t, uint32_t>* target,
-              const ClockMap* caps = nullptr) {
+              const ClockMap* caps = nullptr, const std::vector<uint32_t>* order = nullptr) {
   Work& w = e->w;
   auto& V = e->bufs;
   bool ok = true;
@@ -529,9 +544,31 @@ int run_merge(ycrdt_engine* e, ycrdt_batch* b, const std::unordered_map<uint32_t
   const uint64_t B = (uint64_t)b->nbytes + 64;
   const uint64_t nwords = B / 64 + 2;
   // target state vector → per-client start clocks
-  if (target && !target->empty() && nclients) {
-    std::vector<uint32_t> vals(nclients), starts(nclients, 0);
+  std::vector<uint32_t> vals;
+  if (((target && !target->empty()) || order) && nclients) {
+    vals.resize(nclients);
     HIPCHK(hipMemcpy(vals.data(), w.cl_vals, sizeof(uint32_t) * nclients, hipMemcpyDeviceToHost));
+  }
+  w.cl_emit = w.cl_slot = nullptr;
+  if (order && nclients) {  // slots: store clients in insertion order, then the rest (no blocks to write)
+    std::unordered_map<uint32_t, uint32_t> rank;
+    for (size_t i = 0; i < order->size(); ++i) rank.emplace((*order)[i], (uint32_t)i);
+    std::vector<uint32_t> h(2 * (size_t)nclients);
+    for (uint32_t c = 0; c < nclients; ++c) h[c] = c;
+    std::stable_sort(h.begin(), h.begin() + nclients, [&](uint32_t a, uint32_t b2) {
+      const auto ia = rank.find(vals[a]), ib = rank.find(vals[b2]);
+      const uint32_t ra = ia == rank.end() ? UINT32_MAX : ia->second, rb = ib == rank.end() ? UINT32_MAX : ib->second;
+      return ra < rb;
+    });
+    for (uint32_t i = 0; i < nclients; ++i) h[nclients + h[i]] = i;
+    uint32_t* eb = take<uint32_t>(V, B_EMIT, h.size(), ok);
+    if (!ok) return fail(YCRDT_E_DEVICE, "hipMalloc failed (client order)");
+    HIPCHK(hipMemcpyAsync(eb, h.data(), sizeof(uint32_t) * h.size(), hipMemcpyHostToDevice, s));
+    w.cl_emit = eb;
+    w.cl_slot = eb + nclients;
+  }
+  if (target && !target->empty() && nclients) {
+    std::vector<uint32_t> starts(nclients, 0);
     for (uint32_t i = 0; i < nclients; ++i) {
       auto it = target->find(vals[i]);
       if (it != target->end()) starts[i] = it->second;
@@ -547,7 +584,7 @@ int run_merge(ycrdt_engine* e, ycrdt_batch* b, const std::unordered_map<uint32_t
   w.u_minchild = take<uint32_t>(V, B_UMIN, U + 1, ok);
   w.u_cutbits = take<uint64_t>(V, B_UCUT, uw, ok);
   w.u_wpre = take<uint32_t>(V, B_UWPRE, uw + 1, ok);
-  w.scratch = take<uint32_t>(V, B_SCRATCH, std::max<uint64_t>({nwords + 2, (uint64_t)w.cap_sections + 2, uw + 2, U + 2}), ok);
+  w.scratch = take<uint32_t>(V, B_SCRATCH, std::max<uint64_t>({nwords + 2, (uint64_t)w.cap_sections + 66, uw + 2, U + 2}), ok);
   w.g_start = take<uint32_t>(V, B_GSTART, U + 2, ok);
   w.g_cidx = take<uint32_t>(V, B_GCIDX, U + 1, ok);
   w.g_src = take<uint32_t>(V, B_GSRC, U + 1, ok);
@@ -828,6 +865,7 @@ int run_lazy(ycrdt_engine* e, ycrdt_batch* b, bool merge, const std::vector<std:
   Work& w = e->w;
   w.lz_multi = 0;
   w.capped = 0;
+  w.ds_first = e->compat == 135 ? 1u : 0u;
   e->ws_owner = nullptr;
   auto& V = e->bufs;
   bool ok = true;
@@ -877,6 +915,7 @@ int run_lazy(ycrdt_engine* e, ycrdt_batch* b, bool merge, const std::vector<std:
   w.dw_gstart = take<uint32_t>(V, B_DWGSTART, NDS, ok);
   w.dw_size = take<uint32_t>(V, B_DWSIZE, NDS, ok);
   w.dw_pos = take<uint32_t>(V, B_DWPOS, NDS, ok);
+  w.ds_fa = w.ds_first ? take<uint32_t>(V, B_DSFA, NDS, ok) : nullptr;
   {
     size_t tb = prim_tmp_bytes(std::max<uint64_t>({(uint64_t)b->nbytes + 64, SLOTS, NDS, 1024}));
     w.tmp = take<uint8_t>(V, B_TMP, tb, ok);
@@ -1118,11 +1157,12 @@ constexpr size_t QUEUE_FLUSH_BYTES = size_t(1) << 30;  // deferred updates past 
 
 // Merges `extra` (host updates) behind the doc's state in one device pass and makes the result the
 // doc's state. caps: integrate only below the per-client caps (the pending path).
-int commit_merge(ycrdt_doc* d, const std::vector<ycrdt_buf>& extra, const ClockMap* caps) {
+int commit_merge(ycrdt_doc* d, const std::vector<ycrdt_buf>& extra, const ClockMap* caps,
+                 const std::vector<uint32_t>* order = nullptr) {
   ycrdt_engine* e = d->e;
   ycrdt_batch& b = scratch_batch(e);  // engine-owned: no hipMalloc / hipFree per call
   int rc = stage(&b, extra.data(), extra.size(), d->state_len ? &d->state : nullptr, d->state_len);
-  if (rc == YCRDT_OK) rc = run_merge(e, &b, nullptr, caps);
+  if (rc == YCRDT_OK) rc = run_merge(e, &b, nullptr, caps, order);
   if (rc) return rc;
   if (!grow(d->state, e->out_bytes + 16)) return fail(YCRDT_E_DEVICE, "hipMalloc failed (doc state)");
   HIPCHK(hipMemcpyAsync(d->state.p, e->w.out, e->out_bytes, hipMemcpyDeviceToDevice, e->stream));
@@ -1180,7 +1220,8 @@ int flush(ycrdt_doc* d) {
   }
   if (d->ing.has_pending) bufs.push_back(ycrdt_buf{d->ing.pending.data(), d->ing.pending.size()});
   if (d->ing.has_ds) bufs.push_back(ycrdt_buf{d->ing.pending_ds.data(), d->ing.pending_ds.size()});
-  int rc = commit_merge(d, bufs, &S.state);
+  // compat 135: the stored state is written with the store's client order (what 13.5.16 emits)
+  int rc = commit_merge(d, bufs, &S.state, e->compat == 135 ? &S.order : nullptr);
   if (rc) return rc;
   ClockMap got;
   parse_state_vector(d->sv.data(), d->sv.size(), got);
@@ -1196,24 +1237,6 @@ void enqueue(ycrdt_doc* d, const uint8_t* p, size_t n, bool local) {
   d->queue.push_back(ycrdt_doc::Queued{std::vector<uint8_t>(p, p + n), local});
   d->queue_bytes += n;
   d->view.valid = false;
-}
-
-// 13.5.16 writes the state vector in store insertion order (Y@22723)
-void sv_in_order(const ycrdt_doc* d, std::vector<uint8_t>& out) {
-  ClockMap st;
-  parse_state_vector(d->sv.data(), d->sv.size(), st);
-  out.clear();
-  uint32_t n = 0;
-  std::vector<uint8_t> body;
-  for (const uint32_t c : d->ing.order) {
-    const auto it = st.find(c);
-    if (it == st.end() || !it->second) continue;
-    put_vu(body, c);
-    put_vu(body, it->second);
-    ++n;
-  }
-  put_vu(out, n);
-  out.insert(out.end(), body.begin(), body.end());
 }
 
 }  // namespace
@@ -1291,7 +1314,7 @@ int ycrdt_encode_state_as_update(ycrdt_doc* d, ycrdt_buf sv, ycrdt_out* out) {
   } else {  // delta: re-run the (idempotent) merge of the canonical state with per-client start clocks
     ycrdt_batch& b = scratch_batch(e);
     rc = stage(&b, nullptr, 0, &d->state, d->state_len);
-    if (rc == YCRDT_OK) rc = run_merge(e, &b, &target);
+    if (rc == YCRDT_OK) rc = run_merge(e, &b, &target, nullptr, e->compat == 135 ? &d->ing.order : nullptr);
     if (rc) return rc;
     main.resize(e->out_bytes);
     HIPCHK(hipMemcpy(main.data(), e->w.out, e->out_bytes, hipMemcpyDeviceToHost));
@@ -1325,9 +1348,7 @@ int ycrdt_encode_state_vector(ycrdt_doc* d, ycrdt_out* out) {
   out->len = 0;
   const int rc = flush(d);
   if (rc) return rc;
-  std::vector<uint8_t> ordered;
-  const std::vector<uint8_t>* src = &d->sv;
-  if (d->e->compat == 135) { sv_in_order(d, ordered); src = &ordered; }
+  const std::vector<uint8_t>* src = &d->sv;  // device-written: descending, or store order (compat 135)
   out->len = src->size();
   out->ptr = (uint8_t*)malloc(out->len ? out->len : 1);
   if (!out->ptr) { out->len = 0; return fail(YCRDT_E_CAPACITY, "host allocation failed"); }

@@ -363,7 +363,7 @@ __global__ void k_dsm_keys(Work w, uint32_t nds) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= nds) return;
   const DsRange d = w.ds[i];
-  w.dsm_key[i] = ((uint64_t)(~d.client) << 32) | d.clock;
+  w.dsm_key[i] = ((uint64_t)(w.ds_first ? w.ds_fa[i] : ~d.client) << 32) | d.clock;
   w.dsm_len[i] = d.len;
 }
 __global__ void k_dsm_ends(Work w, uint32_t nds) {
@@ -386,7 +386,10 @@ __global__ void k_dsm_runs(Work w, uint32_t nds) {
   if (i >= nds) return;
   const uint32_t rid = w.dsm_rid[i] + w.dsm_flag[i] - 1;  // inclusive count of run starts - 1
   const uint64_t k = w.dsm_keys[i];
-  if (w.dsm_flag[i]) { w.dr_client[rid] = ~(uint32_t)(k >> 32); w.dr_clock[rid] = (uint32_t)k; }
+  if (w.dsm_flag[i]) {
+    w.dr_client[rid] = w.ds_first ? w.ds[(uint32_t)(k >> 32)].client : ~(uint32_t)(k >> 32);
+    w.dr_clock[rid] = (uint32_t)k;
+  }
   if (i + 1 == nds || w.dsm_flag[i + 1]) w.dr_end[rid] = (uint32_t)w.dsm_max[i];
 }
 // diff: the input's ranges unmerged, clients in descending order (13.6 canonical), wire order
@@ -394,8 +397,13 @@ __global__ void k_dsm_runs(Work w, uint32_t nds) {
 __global__ void k_dsd_keys(Work w, uint32_t nds) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= nds) return;
-  // lz_multi: (update, client desc); the radix sort is stable, so wire order survives within a client
-  w.dsm_key[i] = w.lz_multi ? ((uint64_t)w.ds[i].upd << 32 | (uint32_t)~w.ds[i].client) : ((uint64_t)(~w.ds[i].client) << 32) | i;
+  // lz_multi: (update, client desc); the radix sort is stable, so wire order survives within a client.
+  // compat 135: first-appearance client order (the range's first-range index; per update for multi)
+  const DsRange d = w.ds[i];
+  if (w.ds_first)
+    w.dsm_key[i] = w.lz_multi ? ((uint64_t)d.upd << 32 | (w.ds_fa[i] - w.ds_dense_off[d.upd])) : ((uint64_t)w.ds_fa[i] << 32) | i;
+  else
+    w.dsm_key[i] = w.lz_multi ? ((uint64_t)d.upd << 32 | (uint32_t)~d.client) : ((uint64_t)(~d.client) << 32) | i;
   w.dsm_len[i] = i;
 }
 __global__ void k_dsd_runs(Work w, uint32_t nds) {
@@ -405,6 +413,26 @@ __global__ void k_dsd_runs(Work w, uint32_t nds) {
   w.dr_client[i] = d.client;
   w.dr_clock[i] = d.clock;
   w.dr_end[i] = d.clock + d.len;
+}
+
+// first appearance of every range's client (compat 135): stable sort by (scope, client), then each
+// range takes the smallest original index of its group (the group head, by a running max of heads)
+__global__ void k_fa_keys(Work w, uint32_t nds) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= nds) return;
+  const DsRange d = w.ds[i];
+  w.dsm_key[i] = w.lz_multi ? ((uint64_t)d.upd << 32 | d.client) : (uint64_t)d.client;
+  w.dsm_len[i] = i;
+}
+__global__ void k_fa_heads(Work w, uint32_t nds) {
+  const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= nds) return;
+  w.dsm_end[p] = (p == 0 || w.dsm_keys[p] != w.dsm_keys[p - 1]) ? p : 0;
+}
+__global__ void k_fa_set(Work w, uint32_t nds) {
+  const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= nds) return;
+  w.ds_fa[w.dsm_lens[p]] = w.dsm_lens[(uint32_t)w.dsm_max[p]];
 }
 
 // writeDeleteSet (Y@11105 `fe`): runs grouped by client in output order
@@ -491,6 +519,13 @@ uint32_t launch_event_sizes(Work& w, hipStream_t s, uint32_t* nslots_out) {
 // delete-set runs: merge (union of all inputs) or diff (the input's own)
 uint32_t launch_ds_runs(Work& w, uint32_t nds, bool merge, hipStream_t s) {
   if (!nds) return 0;
+  if (w.ds_first) {
+    hipLaunchKernelGGL(k_fa_keys, dim3(G(nds)), dim3(256), 0, s, w, nds);
+    sort_pairs_u64_u32(w.tmp, w.tmp_bytes, w.dsm_key, w.dsm_keys, w.dsm_len, w.dsm_lens, nds, s);
+    hipLaunchKernelGGL(k_fa_heads, dim3(G(nds)), dim3(256), 0, s, w, nds);
+    scan_segmax_u64(w.tmp, w.tmp_bytes, w.dsm_end, w.dsm_max, nds, s);  // high words 0: a plain running max
+    hipLaunchKernelGGL(k_fa_set, dim3(G(nds)), dim3(256), 0, s, w, nds);
+  }
   if (!merge) {
     hipLaunchKernelGGL(k_dsd_keys, dim3(G(nds)), dim3(256), 0, s, w, nds);
     sort_pairs_u64_u32(w.tmp, w.tmp_bytes, w.dsm_key, w.dsm_keys, w.dsm_len, w.dsm_lens, nds, s);

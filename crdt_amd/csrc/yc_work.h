@@ -33,6 +33,7 @@ struct Counters {            // device-side counters, read back at the few host 
   uint32_t narray_roots;     // 1: a decoded item may root a YArray list (parent given, no parentSub)
   uint32_t tgroups;          // sibling groups of the YArray origin trees (yc_yata.hip)
   uint32_t tbig;             // groups too large for one lane
+  uint32_t ds_region;        // Σ per-update delete-set regions (sizes the range arrays)
   uint32_t nested;           // 1: a decoded item names a parent ITEM (nested types exist)
   uint32_t pad[12];          // encode scratch (see yc_encode.hip)
   unsigned long long items;  // Σ clock lengths of Skip structs (items = Σ all lengths − this)
@@ -232,6 +233,11 @@ struct Work {
   uint32_t* dw_gstart = nullptr;   // [runs+1]
   uint32_t* dw_size = nullptr;     // [runs+1]
   uint32_t* dw_pos = nullptr;      // [runs+1]
+  // Yjs 13.5.16 (compat 135) writes a delete set's clients in Map insertion order: first appearance
+  // (readDeleteSet / mergeDeleteSets, per update for a multi diff). ds_fa[i] = index of the first
+  // range of range i's client; keys then carry ds_fa instead of ~client.
+  uint32_t ds_first = 0;
+  uint32_t* ds_fa = nullptr;       // [ds]
   // ---- encode (NO <= NS)
   uint32_t* o_first = nullptr;     // [NO+1] first segment of output struct (+ sentinel)
   uint32_t* o_cidx = nullptr;      // client of output struct
@@ -242,6 +248,10 @@ struct Work {
   uint32_t* r_size = nullptr;      // [runs+1] encoded size of (clock,len)
   uint32_t* r_pos = nullptr;       // [runs+1]
   uint32_t* cc = nullptr;          // per-client scratch: CC_N arrays of (cap_clients+1)
+  // compat 135: delete-set / state-vector client order = the doc store's insertion order.
+  // cl_emit[slot] = client table index written at that slot, cl_slot = its inverse (null: desc)
+  const uint32_t* cl_emit = nullptr;
+  const uint32_t* cl_slot = nullptr;
   uint32_t cap_clients = 0;
   uint8_t* out = nullptr;          // encoded update
   uint64_t cap_out = 0;
@@ -370,7 +380,9 @@ void launch_group_parse(const Work& w, hipStream_t s);   // k_parse: nxt at ever
 void launch_group_tables(const Work& w, hipStream_t s);  // k_tables: chain exits (+ single-group walk)
 void launch_walker(const Work& w, hipStream_t s);
 void launch_build_final_bits(const Work& w, hipStream_t s);
-void launch_struct_positions(const Work& w, hipStream_t s);
+void launch_struct_count(const Work& w, hipStream_t s);
+void launch_struct_scatter(const Work& w, hipStream_t s);
+void launch_ds_bound(const Work& w, hipStream_t s);
 void launch_ds_decode(const Work& w, hipStream_t s);
 void launch_section_clients(const Work& w, uint32_t nsections, hipStream_t s);
 void launch_client_table(Work& w, uint32_t nsections, hipStream_t s);
