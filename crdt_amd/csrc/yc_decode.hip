@@ -511,9 +511,9 @@ __device__ __forceinline__ bool emit_patch(const Work& w, uint32_t p) {
 // lane j checks by looking up the exit of its (true) entry. The first lane that fails still knows
 // its true exit, so a failed speculation costs one group, exactly the sequential step.
 __global__ __launch_bounds__(64) void k_walker(Work w) {
-  const uint32_t u = blockIdx.x;
+  if (blockIdx.x >= w.nbig) return;
+  const uint32_t u = w.ulist[blockIdx.x];
   const uint32_t lane = threadIdx.x;
-  if (u >= w.nupd) return;
   if (w.ulen[u] > 0 && w.ulen[u] <= GROUP_BYTES) return;  // walked inside k_tables
   const uint8_t* __restrict__ b = w.bytes;
   const Tables& T = w.tab;
@@ -629,9 +629,55 @@ __global__ __launch_bounds__(64) void k_walker(Work w) {
   if (L0) w.dsstart[u] = p;
 }
 
+// Direct path: one lane per small update parses it exactly, struct by struct, and writes the
+// update's struct-start words of the final bitmap itself (updates are 64-byte aligned, so the
+// words are the lane's own: plain stores, each word once, as the lane moves forward).
+__global__ __launch_bounds__(256) void k_direct(Work w) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= w.nsmall) return;
+  const uint32_t u = w.ulist[w.nbig + i];
+  const uint8_t* __restrict__ b = w.bytes;
+  const uint32_t ustart = w.uoff[u], uend = ustart + w.ulen[u];
+  uint32_t* err = &w.ctr->err;
+  w.dsstart[u] = NONE;
+  bool ok = true;
+  uint32_t p = ustart;
+  const uint32_t nsec = rd_vu(b, p, uend, ok);
+  if (!ok || nsec > (uend - p) / 3 + 1) { raise_err(err, ERR_DECODE); return; }
+  const uint32_t sbase = atomicAdd(&w.ctr->nsections, nsec);
+  if (sbase + nsec > w.cap_sections) { raise_err(err, ERR_CAPACITY); return; }
+  w.usec_start[u] = sbase;
+  w.usec_n[u] = nsec;
+  uint32_t word = NONE;
+  uint64_t m = 0;
+  for (uint32_t sct = 0; sct < nsec; ++sct) {
+    const uint32_t n = rd_vu(b, p, uend, ok);
+    const uint32_t client = rd_vu(b, p, uend, ok);
+    const uint32_t clock = rd_vu(b, p, uend, ok);
+    if (!ok || n > uend - p) { raise_err(err, ERR_DECODE); return; }
+    Section sec;
+    sec.upd = u; sec.n = n; sec.client = client; sec.clock = clock;
+    sec.first_pos = n ? p : NONE; sec.cidx = NONE; sec.first_idx = NONE; sec.pad = 0;
+    w.sections[sbase + sct] = sec;
+    if (n) atomicOr((unsigned long long*)&w.sec_bits[p >> 6], 1ull << (p & 63));
+    for (uint32_t k = 0; k < n; ++k) {
+      if ((p >> 6) != word) {
+        if (word != NONE) w.final_bits[word] = m;
+        word = p >> 6;
+        m = 0;
+      }
+      m |= 1ull << (p & 63);
+      const uint32_t at = p;
+      if (parse_struct<false>(b, p, uend, 0xFFFFFFFFu, nullptr) <= 0) { raise_err(err, ERR_DECODE); w.ctr->err_info = at; return; }
+    }
+  }
+  if (word != NONE) w.final_bits[word] = m;
+  w.dsstart[u] = p;
+}
+
 void launch_walker(const Work& w, hipStream_t s) {
-  if (w.nupd == 0) return;
-  hipLaunchKernelGGL(k_walker, dim3(w.nupd), dim3(64), 0, s, w);
+  if (w.nbig) hipLaunchKernelGGL(k_walker, dim3(w.nbig), dim3(64), 0, s, w);
+  if (w.nsmall) hipLaunchKernelGGL(k_direct, dim3((w.nsmall + 255) / 256), dim3(256), 0, s, w);
 }
 
 // --------------------------------------------------------------------------- 3. final bitmap

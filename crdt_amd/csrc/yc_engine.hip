@@ -166,6 +166,9 @@ struct ycrdt_batch {
   std::vector<uint32_t> udoc;   // multi-document batch: document of every staged update
   uint32_t ndocs = 1;
   size_t udoc_off = 0;          // byte offset of udoc in `meta`
+  std::vector<uint32_t> ulist;  // updates parsed through the chain tables, then the direct ones
+  uint32_t nbig = 0;
+  size_t ulist_off = 0;
   std::vector<Group> groups;
   uint32_t nbytes = 0;
   uint64_t in_bytes = 0;
@@ -198,22 +201,48 @@ void mark(ycrdt_engine* e, const char* name) {
   e->marks.push_back({name, ev});
 }
 
-// Lays out n updates (64-byte aligned) + decode group table. `prefix` (device) is placed first.
+// Small updates are parsed directly, one lane per update walking its structs exactly (no speculative
+// tables), when there are many of them: a wavefront then parses 64 updates side by side and the
+// batch is read about once. A few small updates, and every large one, take the table path
+// (k_parse / k_tables / k_walker), whose latency does not grow with the update. YCRDT_DECODE=
+// tables|direct forces one path for small updates (tests cover both).
+constexpr size_t DIRECT_MAX_BYTES = GROUP_BYTES;  // an update the direct lane walks whole
+constexpr size_t DIRECT_TINY_BYTES = 1024;         // always direct (a handful of structs)
+constexpr size_t DIRECT_MIN_COUNT = 1024;          // enough small updates to fill wavefronts
+
+// Lays out n updates (64-byte aligned, so every update owns its bitmap words) + decode group table.
+// `prefix` (device) is placed first.
 void layout(ycrdt_batch* b, const ycrdt_buf* ups, size_t n, size_t prefix_len) {
   size_t total = prefix_len ? ((prefix_len + 63) & ~size_t(63)) : 0;
-  b->uoff.clear(); b->ulen.clear(); b->ugroup.clear(); b->groups.clear();
+  b->uoff.clear(); b->ulen.clear(); b->ugroup.clear(); b->groups.clear(); b->ulist.clear();
   b->in_bytes = 0;
+  const char* mode = getenv("YCRDT_DECODE");
+  const int force = mode && !strcmp(mode, "tables") ? 1 : mode && !strcmp(mode, "direct") ? 2 : 0;
+  size_t nsmall = 0;
+  for (size_t i = 0; i < n; ++i) nsmall += ups[i].len <= DIRECT_MAX_BYTES;
+  auto direct = [&](size_t len) {
+    if (len > DIRECT_MAX_BYTES || force == 1) return false;
+    return force == 2 || nsmall >= DIRECT_MIN_COUNT || len <= DIRECT_TINY_BYTES;
+  };
+  std::vector<uint32_t> small;
   auto add = [&](size_t off, size_t len) {
+    const uint32_t u = (uint32_t)b->uoff.size();
     b->uoff.push_back((uint32_t)off);
     b->ulen.push_back((uint32_t)len);
-    b->ugroup.push_back((uint32_t)b->groups.size());
-    for (size_t g = 0; g < len; g += GROUP_BYTES) {
-      Group G;
-      G.start = (uint32_t)(off + g);
-      G.end = (uint32_t)std::min(off + len, off + g + GROUP_BYTES);
-      G.uend = (uint32_t)(off + len);
-      G.upd = (uint32_t)(b->uoff.size() - 1);
-      b->groups.push_back(G);
+    if (len && direct(len)) {
+      b->ugroup.push_back(NONE);
+      small.push_back(u);
+    } else {
+      b->ugroup.push_back((uint32_t)b->groups.size());
+      b->ulist.push_back(u);
+      for (size_t g = 0; g < len; g += GROUP_BYTES) {
+        Group G;
+        G.start = (uint32_t)(off + g);
+        G.end = (uint32_t)std::min(off + len, off + g + GROUP_BYTES);
+        G.uend = (uint32_t)(off + len);
+        G.upd = u;
+        b->groups.push_back(G);
+      }
     }
     b->in_bytes += len;
   };
@@ -222,6 +251,8 @@ void layout(ycrdt_batch* b, const ycrdt_buf* ups, size_t n, size_t prefix_len) {
     add(total, ups[i].len);
     total += (ups[i].len + 63) & ~size_t(63);
   }
+  b->nbig = (uint32_t)b->ulist.size();
+  b->ulist.insert(b->ulist.end(), small.begin(), small.end());
   b->uoff.push_back((uint32_t)total);
   b->nbytes = (uint32_t)total;
 }
@@ -255,7 +286,7 @@ int stage(ycrdt_batch* b, const ycrdt_buf* ups, size_t n, const DevBuf* prefix, 
       if (d >= b->ndocs) return fail(YCRDT_E_ARG, "document index out of range");
   }
   const size_t meta_bytes = sizeof(uint32_t) * (nu + 1 + nu + nu) + sizeof(Group) * b->groups.size() + 64 +
-                            sizeof(uint32_t) * b->udoc.size() + 16;
+                            sizeof(uint32_t) * b->udoc.size() + 16 + sizeof(uint32_t) * b->ulist.size() + 16;
   if (!grow(b->meta, meta_bytes)) return fail(YCRDT_E_DEVICE, "hipMalloc failed (meta)");
   std::vector<uint8_t> meta(meta_bytes, 0);
   size_t o = 0;
@@ -268,6 +299,10 @@ int stage(ycrdt_batch* b, const ycrdt_buf* ups, size_t n, const DevBuf* prefix, 
   o = (o + 15) & ~size_t(15);
   b->udoc_off = o;
   if (!b->udoc.empty()) memcpy(meta.data() + o, b->udoc.data(), sizeof(uint32_t) * b->udoc.size());
+  o += sizeof(uint32_t) * b->udoc.size();
+  o = (o + 15) & ~size_t(15);
+  b->ulist_off = o;
+  if (!b->ulist.empty()) memcpy(meta.data() + o, b->ulist.data(), sizeof(uint32_t) * b->ulist.size());
   HIPCHK(hipMemcpyAsync(b->meta.p, meta.data(), meta_bytes, hipMemcpyHostToDevice, e->stream));
   HIPCHK(hipStreamSynchronize(e->stream));
   b->merged = false;
@@ -326,6 +361,9 @@ int run_decode(ycrdt_engine* e, ycrdt_batch* b, bool lazy, Decoded& D, bool gene
   w.ngroups = (uint32_t)b->groups.size();
   w.udoc = b->ndocs > 1 ? (const uint32_t*)((const uint8_t*)b->meta.p + b->udoc_off) : nullptr;
   w.ndocs = b->ndocs;
+  w.ulist = (const uint32_t*)((const uint8_t*)b->meta.p + b->ulist_off);
+  w.nbig = b->nbig;
+  w.nsmall = (uint32_t)b->ulist.size() - b->nbig;
   w.lazy = lazy ? 1u : 0u;
   const uint64_t B = (uint64_t)b->nbytes + 64;
   const uint64_t nwords = B / 64 + 2;

@@ -70,6 +70,8 @@ struct Work {
   uint32_t nupd = 0;
   const uint32_t* udoc = nullptr;  // [nupd] document of every update (multi-document batches); nullptr = one doc
   uint32_t ndocs = 1;
+  const uint32_t* ulist = nullptr; // [nbig] updates on the table path, then [nsmall] parsed directly
+  uint32_t nbig = 0, nsmall = 0;
   uint32_t lazy = 0;               // 1: mergeUpdates / diffUpdate decode (references kept raw)
   unsigned long long* dbg = nullptr; // YCRDT_DEBUG_TABLES=1: per-group phase timestamps of k_tables
   const Group* groups = nullptr;   // [G]

@@ -1,0 +1,71 @@
+"""Both decode paths for small updates give the same bytes.
+
+A batch with many small updates is parsed directly (one lane per update walks its structs,
+k_direct); few small updates and every large one take the speculative chain-table path (k_parse /
+k_tables / k_walker). YCRDT_DECODE forces one path for every update of at most 16 KiB; both must
+match the Yjs fixtures and the oracle byte for byte, and report the same malformed input.
+"""
+import pytest
+
+crdt_amd = pytest.importorskip("crdt_amd")
+
+pytestmark = pytest.mark.gpu
+MODES = ("tables", "direct")
+
+
+@pytest.mark.parametrize("mode", MODES)
+def test_paths_golden(golden, mode, monkeypatch):
+    monkeypatch.setenv("YCRDT_DECODE", mode)
+    for setname in ("kat", "map", "array", "nested"):
+        for c in golden[setname]:
+            d = crdt_amd.Doc(client_id=0x7FFFFFF0)
+            d.apply_updates([bytes.fromhex(u) for u in c["updates"]])
+            assert d.encode_state_as_update().hex() == c["state"], (mode, c["name"])
+            assert d.encode_state_vector().hex() == c["sv"], (mode, c["name"])
+            ups = [bytes.fromhex(u) for u in c["updates"]]
+            want = c["merged"] if len(ups) > 1 else c["merged_raw"]
+            assert crdt_amd.merge_updates(ups).hex() == want, (mode, c["name"])
+
+
+@pytest.mark.parametrize("mode", MODES)
+def test_paths_generated_vs_oracle(mode, monkeypatch):
+    from crdt_amd.workload import C2, gen_map
+    from oracle.yref import Doc as ODoc
+
+    monkeypatch.setenv("YCRDT_DECODE", mode)
+    cfg = dict(C2)
+    cfg.update(n_keys=2000, n_replicas=300, ops_per_replica=200)
+    ups, _ = gen_map(**cfg)
+    o = ODoc(0x7FFFFFF0)
+    for u in ups:
+        o.apply_update(u)
+    b = crdt_amd.Batch(ups)
+    b.merge()
+    assert b.result() == (o.encode_state_as_update(), o.encode_state_vector())
+
+
+@pytest.mark.parametrize("mode", MODES)
+def test_paths_array_vs_oracle(mode, monkeypatch):
+    from tests.histories import array_history
+    from oracle.yref import Doc as ODoc
+
+    monkeypatch.setenv("YCRDT_DECODE", mode)
+    states, wire = array_history(77, n_replicas=6, rounds=4, ops=10, with_map=True)
+    ups = states + wire
+    o = ODoc(0x7FFFFFF0)
+    for u in ups:
+        o.apply_update(u)
+    b = crdt_amd.Batch(ups)
+    b.merge()
+    assert b.result() == (o.encode_state_as_update(), o.encode_state_vector())
+
+
+@pytest.mark.parametrize("mode", MODES)
+def test_paths_malformed(golden, mode, monkeypatch):
+    """A truncated update in a batch fails the merge on both paths (Yjs throws on it)."""
+    monkeypatch.setenv("YCRDT_DECODE", mode)
+    good = [bytes.fromhex(u) for u in golden["map"][0]["updates"]]
+    bad = good[0][: max(3, len(good[0]) // 2)]
+    b = crdt_amd.Batch(good + [bad])
+    with pytest.raises(crdt_amd.YcrdtError):
+        b.merge()
