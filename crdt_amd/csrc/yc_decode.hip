@@ -631,14 +631,37 @@ __global__ __launch_bounds__(64) void k_walker(Work w) {
 
 // Direct path: one lane per small update parses it exactly, struct by struct, and writes the
 // update's struct-start words of the final bitmap itself (updates are 64-byte aligned, so the
-// words are the lane's own: plain stores, each word once, as the lane moves forward).
-__global__ __launch_bounds__(256) void k_direct(Work w) {
+// words are the lane's own: plain stores, each word once, as the lane moves forward). Each lane
+// reads its update through a private LDS window of DW bytes, refilled with 16-byte loads when
+// fewer than DREFILL bytes are left: the byte-serial parse then waits on LDS, not on L2 / HBM
+// (a wavefront touches 64 different updates, far more lines than L1 keeps). Structs are sized by
+// the speculative sizer (exact on valid structs); what it hands over is parsed by parse_struct.
+constexpr uint32_t DW = 128;                    // window bytes per lane
+constexpr uint32_t DSTRIDE = DW / 4 + 4;        // words per lane slot (16-byte padded)
+constexpr uint32_t DREFILL = 48;
+constexpr uint32_t DL = 256;                    // lanes per direct workgroup
+// the exact parser out of line: inlined, its nested-`any` walker multiplies the register demand
+// of the lane loop (one wavefront per SIMD), and it only runs on the few handed-over structs
+__device__ __attribute__((noinline)) uint32_t exact_len(const uint8_t* __restrict__ b, uint32_t p, uint32_t end) {
+  uint32_t q = p;
+  return parse_struct<false>(b, q, end, 0xFFFFFFFFu, nullptr) > 0 ? q - p : 0u;
+}
+__global__ __launch_bounds__(DL) void k_direct(Work w) {
+  __shared__ __attribute__((aligned(16))) uint32_t win[DL * DSTRIDE];
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= w.nsmall) return;
   const uint32_t u = w.ulist[w.nbig + i];
   const uint8_t* __restrict__ b = w.bytes;
   const uint32_t ustart = w.uoff[u], uend = ustart + w.ulen[u];
   uint32_t* err = &w.ctr->err;
+  uint32_t* slot = win + threadIdx.x * DSTRIDE;
+  LdsSrc src{b, slot, 0, 0};
+  auto refill = [&](uint32_t p) {
+    src.s0 = p & ~15u;
+    src.wlen = min(DW, (uend + 15u - src.s0) & ~15u);
+    const uint4* g = (const uint4*)(b + src.s0);
+    for (uint32_t k = 0; k < src.wlen / 16; ++k) ((uint4*)slot)[k] = g[k];
+  };
   w.dsstart[u] = NONE;
   bool ok = true;
   uint32_t p = ustart;
@@ -648,10 +671,11 @@ __global__ __launch_bounds__(256) void k_direct(Work w) {
   if (sbase + nsec > w.cap_sections) { raise_err(err, ERR_CAPACITY); return; }
   w.usec_start[u] = sbase;
   w.usec_n[u] = nsec;
+  refill(p);
   uint32_t word = NONE;
   uint64_t m = 0;
   for (uint32_t sct = 0; sct < nsec; ++sct) {
-    const uint32_t n = rd_vu(b, p, uend, ok);
+    const uint32_t n = rd_vu(b, p, uend, ok);  // headers: the walkers' exact reader
     const uint32_t client = rd_vu(b, p, uend, ok);
     const uint32_t clock = rd_vu(b, p, uend, ok);
     if (!ok || n > uend - p) { raise_err(err, ERR_DECODE); return; }
@@ -661,14 +685,29 @@ __global__ __launch_bounds__(256) void k_direct(Work w) {
     w.sections[sbase + sct] = sec;
     if (n) atomicOr((unsigned long long*)&w.sec_bits[p >> 6], 1ull << (p & 63));
     for (uint32_t k = 0; k < n; ++k) {
+      if (p >= uend) { raise_err(err, ERR_DECODE); w.ctr->err_info = p; return; }
       if ((p >> 6) != word) {
         if (word != NONE) w.final_bits[word] = m;
         word = p >> 6;
         m = 0;
       }
       m |= 1ull << (p & 63);
-      const uint32_t at = p;
-      if (parse_struct<false>(b, p, uend, 0xFFFFFFFFu, nullptr) <= 0) { raise_err(err, ERR_DECODE); w.ctr->err_info = at; return; }
+      if (p - src.s0 + DREFILL > src.wlen) refill(p);
+      const uint32_t info = src.u8(p), ref = info & 31u;
+      uint32_t d = 0;
+      if (ref == REF_GC || ref == REF_SKIP) {
+        uint32_t q = p + 1;
+        bool okv = true;
+        vu_fast(src, q, uend, okv);
+        d = okv ? q - p : 0u;
+      } else if (ref >= 1 && ref <= REF_DOC) {
+        d = spec_len(src, p, uend, (ref - 1) * 8 + (info >> 5));
+      }
+      if (d <= 1) {  // handed over (long / deep / Doc), or not sized: the exact parser decides
+        d = exact_len(b, p, uend);
+        if (!d) { raise_err(err, ERR_DECODE); w.ctr->err_info = p; return; }
+      }
+      p += d;
     }
   }
   if (word != NONE) w.final_bits[word] = m;
@@ -677,7 +716,7 @@ __global__ __launch_bounds__(256) void k_direct(Work w) {
 
 void launch_walker(const Work& w, hipStream_t s) {
   if (w.nbig) hipLaunchKernelGGL(k_walker, dim3(w.nbig), dim3(64), 0, s, w);
-  if (w.nsmall) hipLaunchKernelGGL(k_direct, dim3((w.nsmall + 255) / 256), dim3(256), 0, s, w);
+  if (w.nsmall) hipLaunchKernelGGL(k_direct, dim3((w.nsmall + DL - 1) / DL), dim3(DL), 0, s, w);
 }
 
 // --------------------------------------------------------------------------- 3. final bitmap

@@ -98,7 +98,7 @@ enum Buf {
   B_SCPOS, B_SCEND, B_SCELEM,
   B_CLVALS, B_CLTMP, B_CLSTATE, B_CLBASE, B_CLSTART, B_CC,
   B_UOWN, B_UFLAG, B_UMIN, B_UCUT, B_UWPRE,
-  B_GSTART, B_GCIDX, B_GSRC, B_GFLAGS, B_GORIG, B_GRORIG, B_GLINK, B_GKEY, B_GMAXC, B_GNEXT, B_GOUTID, B_GTMP, B_GTMP2,
+  B_GSTART, B_GCIDX, B_GSRC, B_GFLAGS, B_GORIG, B_GRORIG, B_GLINK, B_GOSEG, B_GKEY, B_GMAXC, B_GNEXT, B_GOUTID, B_GTMP, B_GTMP2,
   B_KHASH, B_KROOT, B_KWIN, B_KPAR, B_KFLAG, B_SPK,
   B_USEC, B_USECN, B_DBG,
   B_LZKEY, B_LZKEYS, B_LZIOTA, B_LZSEC, B_LZRSTART, B_LZPREV, B_LZFIRST, B_LZCAP, B_LZEVBASE, B_LZEVN, B_LZFLAG,
@@ -630,6 +630,7 @@ int run_merge(ycrdt_engine* e, ycrdt_batch* b, const std::unordered_map<uint32_t
   w.g_origin = take<uint32_t>(V, B_GORIG, U + 1, ok);
   w.g_rorigin = take<uint32_t>(V, B_GRORIG, U + 1, ok);
   w.g_link = take<uint32_t>(V, B_GLINK, U + 1, ok);
+  w.g_oseg = take<uint32_t>(V, B_GOSEG, U + 1, ok);
   w.g_key = take<uint32_t>(V, B_GKEY, U + 1, ok);
   w.g_maxchild = take<uint32_t>(V, B_GMAXC, U + 1, ok);
   w.g_outid = take<uint32_t>(V, B_GOUTID, U + 2, ok);

@@ -283,6 +283,7 @@ __global__ __launch_bounds__(256) void k_seg_props(Work w, uint32_t nsegs) {
   } else if (!gc) {
     link = seg_of(w.u_cutbits, w.u_wpre, origin != NONE ? origin : rorigin);
   }
+  w.g_oseg[s] = (!gc && origin != NONE) ? link : NONE;  // link = the origin's segment here
   if (gc) sf |= SEG_GC | SEG_DEL;
   else sf |= SEG_ITEM;
   w.g_cidx[s] = cidx;
@@ -356,30 +357,31 @@ uint32_t run_key_resolution(const Work& w, uint32_t nsegs, hipStream_t s) {
 
 // --------------------------------------------------------------------------- map winner
 // Per YMap entry: max-client child of its origin (the winner descent) and min-client child of its
-// origin unit (YATA puts it right after the origin: merge adjacency). The base entry of a hot key
-// has a child from every replica, and contended device-scope atomics serialise at the memory side,
-// so every lane reads first and the segments (sorted by client) run in three launches: the top
-// clients first (they settle every max), then the bottom ones (they settle every min), then the
-// rest, which then finds almost every slot already decided and issues no atomic.
-__global__ __launch_bounds__(256) void k_children(Work w, uint32_t lo, uint32_t hi) {
+// origin unit (YATA puts it right after the origin: merge adjacency). Both are device-scope
+// atomics, which execute at the memory side, one request per lane; so every lane reads first and
+// issues only an improving atomic. Segments are numbered in (client index, clock) order, so the
+// max child is the max segment and the min child the min client: the max pass sweeps the segments
+// in descending slices and the min pass in ascending ones — the first slice holding a child of an
+// origin settles it, and the children in later slices read a better value and issue nothing.
+constexpr uint32_t CHILD_SLICES = 8;
+__global__ __launch_bounds__(256) void k_children_max(Work w, uint32_t lo, uint32_t hi) {
   const uint32_t s = lo + blockIdx.x * blockDim.x + threadIdx.x;
   if (s >= hi) return;
   const uint32_t f = w.g_flags[s];
   if (!(f & SEG_PSUB)) return;
-  const uint32_t key = w.g_key[s];
-  const uint32_t cidx = w.g_cidx[s];
-  // segments are numbered in (client index, clock) order, so the max (client, segment) child is
-  // the max segment: a u32 atomicMax of s + 1 (u64 atomics issue at well under half the rate)
-  const uint32_t v = s + 1;
+  const uint32_t v = s + 1;  // a u32 atomicMax of s + 1 (u64 atomics issue at well under half the rate)
+  const uint32_t os = w.g_oseg[s];
+  uint32_t* dst = os != NONE ? &w.g_maxchild[os] : (f & SEG_ROOT) ? &w.k_rootmax[w.g_key[s]] : nullptr;
+  if (dst && *dst < v) atomicMax(dst, v);
+}
+__global__ __launch_bounds__(256) void k_children_min(Work w, uint32_t lo, uint32_t hi) {
+  const uint32_t s = lo + blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= hi) return;
+  if (!(w.g_flags[s] & SEG_PSUB)) return;
   const uint32_t o = w.g_origin[s];
-  if (o != NONE) {
-    if (w.u_minchild[o] > cidx) atomicMin(&w.u_minchild[o], cidx);
-    uint32_t* dst = &w.g_maxchild[seg_of(w.u_cutbits, w.u_wpre, o)];
-    if (*dst < v) atomicMax(dst, v);
-  } else if (f & SEG_ROOT) {
-    uint32_t* dst = &w.k_rootmax[key];
-    if (*dst < v) atomicMax(dst, v);
-  }
+  if (o == NONE) return;
+  const uint32_t cidx = w.g_cidx[s];
+  if (w.u_minchild[o] > cidx) atomicMin(&w.u_minchild[o], cidx);
 }
 // the key's value is the rightmost entry: descend from the max-client root through the max-client
 // child until a leaf (YATA order of an origin-only tree, SURVEY.md §7 hard part 2)
@@ -406,10 +408,16 @@ __global__ void k_overwrite(Work w, uint32_t nsegs) {
 
 void launch_map_winner(const Work& w, uint32_t nsegs, hipStream_t s) {
   if (!nsegs) return;
-  const uint32_t a = nsegs / 16, b = nsegs - nsegs / 16;
-  const uint32_t ranges[3][2] = {{b, nsegs}, {0, a}, {a, b}};
-  for (auto& r : ranges)
-    if (r[1] > r[0]) hipLaunchKernelGGL(k_children, dim3((r[1] - r[0] + 255) / 256), dim3(256), 0, s, w, r[0], r[1]);
+  const uint32_t k = nsegs < (1u << 16) ? 1u : CHILD_SLICES;  // small merges: one launch each
+  const uint32_t step = (nsegs + k - 1) / k;
+  for (uint32_t i = 0; i < k; ++i) {  // descending slices
+    const uint32_t hi = nsegs - std::min(nsegs, i * step), lo = hi - std::min(hi, step);
+    if (hi > lo) hipLaunchKernelGGL(k_children_max, dim3((hi - lo + 255) / 256), dim3(256), 0, s, w, lo, hi);
+  }
+  for (uint32_t i = 0; i < k; ++i) {  // ascending slices
+    const uint32_t lo = std::min(nsegs, i * step), hi = std::min(nsegs, lo + step);
+    if (hi > lo) hipLaunchKernelGGL(k_children_min, dim3((hi - lo + 255) / 256), dim3(256), 0, s, w, lo, hi);
+  }
 }
 
 uint32_t run_descent(const Work& w, uint32_t nsegs, hipStream_t s) {

@@ -117,6 +117,16 @@ YC_HD inline bool skip_any(const uint8_t* __restrict__ b, uint32_t& p, uint32_t 
   }
 }
 
+// Out of line: the container stack costs DEPTH registers wherever skip_any is inlined, so struct
+// parsers take scalar values inline and hand containers to this call.
+// (State goes in and out by value: taking the caller's cursor by address would put it in scratch.)
+struct AnySkip { uint32_t p, steps, ok; };
+template <int DEPTH>
+YC_HD __attribute__((noinline)) AnySkip skip_any_nl(const uint8_t* __restrict__ b, uint32_t p, uint32_t end, uint32_t steps) {
+  const bool ok = skip_any<DEPTH>(b, p, end, steps);
+  return AnySkip{p, steps, ok ? 1u : 0u};
+}
+
 // Decoded view of one struct (Y@19286 readClientsStructRefs + readItemContent).
 struct StructView {
   uint8_t info;
@@ -233,7 +243,25 @@ YC_HD inline int parse_struct(const uint8_t* __restrict__ b, uint32_t& p, uint32
     case REF_ANY: {
       uint32_t n = rd_vu(b, p, end, ok);
       len = n;
-      for (uint32_t i = 0; i < n && ok; ++i) ok = skip_any<DEPTH>(b, p, end, steps);
+      for (uint32_t i = 0; i < n && ok; ++i) {
+        const uint32_t tag = p < end ? b[p] : 0u;
+        if (p < end && steps > 0 && tag >= 116u && tag <= 127u && tag != 117u && tag != 118u) {  // a scalar: skip_any's one step
+          --steps;
+          ++p;
+          switch (tag) {
+            case 125: skip_vi(b, p, end, ok); break;
+            case 124: skip_bytes(p, 4, end, ok); break;
+            case 123: case 122: skip_bytes(p, 8, end, ok); break;
+            case 119: case 116: { const uint32_t k = rd_vu(b, p, end, ok); if (ok) skip_bytes(p, k, end, ok); break; }
+            default: break;  // 127 undefined, 126 null, 121 false, 120 true
+          }
+        } else {
+          const AnySkip r = skip_any_nl<DEPTH>(b, p, end, steps);
+          p = r.p;
+          steps = r.steps;
+          ok = r.ok != 0;
+        }
+      }
       if (!ok && steps == 0) return -1;
       if (FULL) v->nel = n;
       break;
@@ -241,7 +269,12 @@ YC_HD inline int parse_struct(const uint8_t* __restrict__ b, uint32_t& p, uint32
     case REF_DOC: {
       uint32_t k = rd_vu(b, p, end, ok);
       if (ok) skip_bytes(p, k, end, ok);
-      if (ok) ok = skip_any<DEPTH>(b, p, end, steps);
+      if (ok) {
+        const AnySkip r = skip_any_nl<DEPTH>(b, p, end, steps);
+        p = r.p;
+        steps = r.steps;
+        ok = r.ok != 0;
+      }
       if (!ok && steps == 0) return -1;
       break;
     }

@@ -148,6 +148,7 @@ struct Work {
   uint32_t* g_origin = nullptr;    // origin unit (global) or NONE
   uint32_t* g_rorigin = nullptr;   // right-origin unit or NONE
   uint32_t* g_link = nullptr;      // pointer-jumping link (key resolution)
+  uint32_t* g_oseg = nullptr;      // segment holding the origin unit (NONE: no origin / GC)
   uint32_t* g_key = nullptr;       // resolved key slot or NONE
   uint32_t* g_maxchild = nullptr;  // seg + 1 of the max-client child (segments are in client order), 0 = none
   uint32_t* g_next = nullptr;      // descent pointer / pointer jumping
@@ -282,17 +283,32 @@ __device__ __forceinline__ uint32_t doc_of_update(const Work& w, uint32_t upd) {
 // Byte range of content elements [e0, e1) of struct `src` (ContentAny: lib0 `any` values,
 // ContentJSON: varStrings, ContentString: UTF-16 code units of the UTF-8 text; every other
 // content has length 1 and is copied whole). This is ContentX.splice (Y@70000..) as a byte slice.
-__device__ inline bool content_slice(const Work& w, uint32_t src, uint32_t e0, uint32_t e1, uint32_t& b0, uint32_t& b1) {
+// The element walk is out of line: inlined, the nested-`any` skipper multiplies the register
+// demand (and so cuts the occupancy) of every kernel that encodes structs, for a path that only
+// split structs take. The whole-content case stays inline.
+// (Plain values in, the range packed in a register pair out: a reference to Work or an
+// out-parameter would make every caller spill them to scratch memory on every path.)
+static __device__ __attribute__((noinline)) uint64_t content_slice_walk(const uint8_t* __restrict__ by, uint32_t ref, uint32_t celem,
+                                                                        uint32_t cpos, uint32_t end, uint32_t e0, uint32_t e1);
+__device__ __forceinline__ bool content_slice(const Work& w, uint32_t src, uint32_t e0, uint32_t e1, uint32_t& b0, uint32_t& b1) {
   const uint32_t ref = w.s_info[src] & 31u;
-  const uint8_t* __restrict__ by = w.bytes;
-  const uint32_t end = w.s_cend[src];
   if (e0 == 0 && e1 == w.s_len[src] && (ref == REF_ANY || ref == REF_JSON)) {  // the whole content
     b0 = w.s_celem[src];
-    b1 = end;
+    b1 = w.s_cend[src];
     return true;
   }
+  const uint64_t r = content_slice_walk(w.bytes, ref, w.s_celem[src], w.s_cpos[src], w.s_cend[src], e0, e1);
+  if (r == ~0ull) return false;
+  b0 = (uint32_t)r;
+  b1 = (uint32_t)(r >> 32);
+  return true;
+}
+static __device__ __attribute__((noinline)) uint64_t content_slice_walk(const uint8_t* __restrict__ by, uint32_t ref, uint32_t celem,
+                                                                        uint32_t cpos, uint32_t end, uint32_t e0, uint32_t e1) {
+  uint32_t b0 = 0, b1 = 0;
+  const bool got = [&]() -> bool {
   if (ref == REF_ANY || ref == REF_JSON) {
-    uint32_t p = w.s_celem[src];
+    uint32_t p = celem;
     bool ok = true;
     for (uint32_t i = 0; i < e1; ++i) {
       if (i == e0) b0 = p;
@@ -310,7 +326,7 @@ __device__ inline bool content_slice(const Work& w, uint32_t src, uint32_t e0, u
     return true;
   }
   if (ref == REF_STRING) {
-    uint32_t p = w.s_cpos[src];
+    uint32_t p = cpos;
     bool ok = true;
     rd_vu(by, p, end, ok);  // byte length prefix
     if (!ok) return false;
@@ -329,9 +345,11 @@ __device__ inline bool content_slice(const Work& w, uint32_t src, uint32_t e0, u
     b1 = p;
     return b0 != NONE && u == e1;
   }
-  b0 = w.s_cpos[src];
+  b0 = cpos;
   b1 = end;
   return true;
+  }();
+  return got ? ((uint64_t)b1 << 32) | b0 : ~0ull;
 }
 
 // per-client scratch arrays inside Work::cc
