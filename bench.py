@@ -50,6 +50,7 @@ def parse():
                    help="replicas in the Yjs CPU-baseline sample (bounded: ~10 s of Yjs work)")
     p.add_argument("--port-replicas", type=int, default=1000, help="replicas in the oracle-port timing sample")
     p.add_argument("--profile-phases", action="store_true")
+    p.add_argument("--no-per-op", action="store_true", help="skip the crdt.js per-op leg")
     p.add_argument("--c3-items", type=int, default=10_000_000,
                    help="C3 leg: YArray 'messages', 256 replicas x 16 rounds, this many values (0 = off)")
     return p.parse_args()
@@ -162,6 +163,69 @@ def apply_loop_leg(eng, updates, out_update):
     return {"applies": len(updates), "apply_calls_ms": round(loop_ms, 3), "first_read_ms": round(read_ms, 3),
             "total_ms": round(loop_ms + read_ms, 3), "merges": 1, "parity": same,
             "includes": "per call: ctypes + host validation + queue copy; read: H2D + one merge + D2H"}
+
+
+def _any_str(v: str) -> bytes:
+    """lib0 `any` encoding of one string (tag 119, varString)."""
+    b = v.encode()
+    n, out = len(b), bytearray([119])
+    while n > 0x7F:
+        out.append(0x80 | (n & 0x7F))
+        n >>= 7
+    out.append(n)
+    return bytes(out) + b
+
+
+def per_op_leg(eng, n_ops_list=(500, 2000)):
+    """crdt.js's per-op path (SURVEY.md §6 'crdt.js end-to-end', crdt.js:433-445, 294-305): peer A
+    does one YMap set (every 5th op a delete) and encodes its FULL state (crdt.js sends
+    Y.encodeStateAsUpdate(y.doc) per op); peer B applies it and rebuilds its crdt.c cache
+    (toJSON of the root). Reported as ops/s next to the same loop in Yjs 13.5.16 (Node, one core,
+    scripts/yjs_baseline.js perop), final states compared byte for byte."""
+    import hashlib
+    import crdt_amd
+
+    res = {}
+    for n_ops in n_ops_list:
+        a = crdt_amd.Doc(client_id=1, engine=eng)
+        b = crdt_amd.Doc(client_id=2, engine=eng)
+        a.track_local(False)
+        t0 = time.perf_counter()
+        for i in range(n_ops):
+            key = "user%d" % (i % 100)
+            if i % 5 == 4:
+                a.map_delete("users", key)
+            else:
+                a.map_set("users", key, _any_str("v%d" % i))
+            u = a.encode_state_as_update()
+            b.apply_update(u)
+            b.root_json("users", "map")
+        dt = time.perf_counter() - t0
+        final = b.encode_state_as_update()
+        r = {"ops": n_ops, "ms": round(dt * 1e3, 2), "ops_per_s": round(n_ops / dt, 1),
+             "includes": "A: set/delete + full encodeStateAsUpdate; B: applyUpdate + toJSON (crdt.c), ctypes, 1 GPU"}
+        y = _yjs_perop(n_ops)
+        if y:
+            from tests.v1util import canonical_update
+            r["yjs"] = {"ops_per_s": round(n_ops / (y["ms"] * 1e-3), 1), "cores": 1, "kind": "reference",
+                        "parity": y["state_sha256"] == hashlib.sha256(canonical_update(final)).hexdigest(),
+                        "sample": f"the same loop in Yjs {y['yjs']} / Node {y['node']}"}
+        res[str(n_ops)] = r
+        del a, b
+    return res
+
+
+def _yjs_perop(n_ops, timeout=240):
+    import shutil
+    import subprocess
+
+    node = shutil.which("node")
+    if not node:
+        return None
+    r = subprocess.run([node, os.path.join(ROOT, "scripts", "yjs_baseline.js"), str(n_ops), "perop"],
+                       capture_output=True, text=True, timeout=timeout)
+    y = json.loads(r.stdout.strip().splitlines()[-1]) if r.returncode == 0 and r.stdout.strip() else None
+    return y if y and y.get("available") else None
 
 
 def _yjs_time(ups, timeout=240):
@@ -471,6 +535,7 @@ def main():
     if rank == 0 and world == 1 and args.fleet_pairs > 0:
         fleet = fleet_sync_leg(eng, args.fleet_pairs)
     loop = apply_loop_leg(eng, updates, out_update) if rank == 0 and world == 1 else None
+    per_op = per_op_leg(eng) if rank == 0 and world == 1 and not args.no_per_op else None
     c3 = c3_leg(eng, args.c3_items) if rank == 0 and world == 1 and args.c3_items > 0 else None
     line = {
         "metric": "CRDT items merged/sec at 1/2/4/8 MI355X + % of HBM roofline",
@@ -513,6 +578,7 @@ def main():
         "cpu_baseline": cpu,
         "fleet_sync": fleet,
         "apply_loop": loop,
+        "per_op": per_op,
         "c3": c3,
         "phases_ms": {n: round(m, 4) for n, m in phases},
     }

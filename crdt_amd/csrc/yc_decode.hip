@@ -1089,12 +1089,14 @@ __global__ __launch_bounds__(256) void k_struct_decode(Work w, uint32_t nstructs
   const bool item = v.ref != REF_GC && v.ref != REF_SKIP;
   // lazy mode (mergeUpdates / diffUpdate): references are copied, never resolved, so the raw
   // client ids are kept (presence = info bits); integrate mode maps them to client indices
+  // references to the struct's own client (the common case: a client's consecutive inserts) take
+  // the section's client index instead of a binary search over the client table
   if (item && (v.info & 0x80u)) {
-    oc = w.lazy ? v.oc : find_client(w, nclients, doc, v.oc);
+    oc = w.lazy ? v.oc : v.oc == sec.client ? sec.cidx : find_client(w, nclients, doc, v.oc);
     if (oc == NONE && !w.lazy) oc = UNKNOWN;  // k_refs decides (pending unless capped away)
   }
   if (item && (v.info & 0x40u)) {
-    rc = w.lazy ? v.rc : find_client(w, nclients, doc, v.rc);
+    rc = w.lazy ? v.rc : v.rc == sec.client ? sec.cidx : find_client(w, nclients, doc, v.rc);
     if (rc == NONE && !w.lazy) rc = UNKNOWN;
   }
   w.s_ocidx[i] = oc;
@@ -1105,7 +1107,7 @@ __global__ __launch_bounds__(256) void k_struct_decode(Work w, uint32_t nstructs
   uint32_t pk = item ? v.pkind : 0u, pa = NONE, pb = 0;
   if (pk == 1) { pa = v.pa; pb = v.pb; }
   else if (pk == 2) {
-    pa = w.lazy ? v.pa : find_client(w, nclients, doc, v.pa);
+    pa = w.lazy ? v.pa : v.pa == sec.client ? sec.cidx : find_client(w, nclients, doc, v.pa);
     pb = v.pb;
     if (pa == NONE && !w.lazy) pa = UNKNOWN;
   }

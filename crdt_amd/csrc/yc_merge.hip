@@ -18,6 +18,7 @@
 //   k_merge_flags  Item.mergeWith (Y@79424) / tryToMergeWithLeft (Y@30960) as a pairwise
 //                  predicate over adjacent segments ⇒ canonical (maximally merged) structs
 #include <algorithm>
+#include <cstdlib>
 
 #include "yc_work.h"
 
@@ -357,31 +358,25 @@ uint32_t run_key_resolution(const Work& w, uint32_t nsegs, hipStream_t s) {
 
 // --------------------------------------------------------------------------- map winner
 // Per YMap entry: max-client child of its origin (the winner descent) and min-client child of its
-// origin unit (YATA puts it right after the origin: merge adjacency). Both are device-scope
-// atomics, which execute at the memory side, one request per lane; so every lane reads first and
-// issues only an improving atomic. Segments are numbered in (client index, clock) order, so the
-// max child is the max segment and the min child the min client: the max pass sweeps the segments
-// in descending slices and the min pass in ascending ones — the first slice holding a child of an
-// origin settles it, and the children in later slices read a better value and issue nothing.
-constexpr uint32_t CHILD_SLICES = 8;
-__global__ __launch_bounds__(256) void k_children_max(Work w, uint32_t lo, uint32_t hi) {
-  const uint32_t s = lo + blockIdx.x * blockDim.x + threadIdx.x;
-  if (s >= hi) return;
+// origin unit (YATA puts it right after the origin: merge adjacency). Segments are numbered in
+// (client index, clock) order, so the max child is the max segment (a u32 atomicMax of s + 1; u64
+// atomics issue at well under half the rate) and the min child the min client index. Both are
+// fire-and-forget device-scope atomics: they execute at the memory side and the lane never waits,
+// whereas reading the slot first to skip a useless atomic is a dependent random load that costs
+// more than the atomic it saves (measured on the 112-document C2 batch: 26 ms read-then-atomic vs
+// 13.6 ms plain atomics for this phase).
+__global__ __launch_bounds__(256) void k_children(Work w, uint32_t nsegs) {
+  const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= nsegs) return;
   const uint32_t f = w.g_flags[s];
   if (!(f & SEG_PSUB)) return;
-  const uint32_t v = s + 1;  // a u32 atomicMax of s + 1 (u64 atomics issue at well under half the rate)
   const uint32_t os = w.g_oseg[s];
-  uint32_t* dst = os != NONE ? &w.g_maxchild[os] : (f & SEG_ROOT) ? &w.k_rootmax[w.g_key[s]] : nullptr;
-  if (dst && *dst < v) atomicMax(dst, v);
-}
-__global__ __launch_bounds__(256) void k_children_min(Work w, uint32_t lo, uint32_t hi) {
-  const uint32_t s = lo + blockIdx.x * blockDim.x + threadIdx.x;
-  if (s >= hi) return;
-  if (!(w.g_flags[s] & SEG_PSUB)) return;
-  const uint32_t o = w.g_origin[s];
-  if (o == NONE) return;
-  const uint32_t cidx = w.g_cidx[s];
-  if (w.u_minchild[o] > cidx) atomicMin(&w.u_minchild[o], cidx);
+  if (os != NONE) {
+    atomicMax(&w.g_maxchild[os], s + 1);
+    atomicMin(&w.u_minchild[w.g_origin[s]], w.g_cidx[s]);
+  } else if (f & SEG_ROOT) {
+    atomicMax(&w.k_rootmax[w.g_key[s]], s + 1);
+  }
 }
 // the key's value is the rightmost entry: descend from the max-client root through the max-client
 // child until a leaf (YATA order of an origin-only tree, SURVEY.md §7 hard part 2)
@@ -407,17 +402,7 @@ __global__ void k_overwrite(Work w, uint32_t nsegs) {
 }
 
 void launch_map_winner(const Work& w, uint32_t nsegs, hipStream_t s) {
-  if (!nsegs) return;
-  const uint32_t k = nsegs < (1u << 16) ? 1u : CHILD_SLICES;  // small merges: one launch each
-  const uint32_t step = (nsegs + k - 1) / k;
-  for (uint32_t i = 0; i < k; ++i) {  // descending slices
-    const uint32_t hi = nsegs - std::min(nsegs, i * step), lo = hi - std::min(hi, step);
-    if (hi > lo) hipLaunchKernelGGL(k_children_max, dim3((hi - lo + 255) / 256), dim3(256), 0, s, w, lo, hi);
-  }
-  for (uint32_t i = 0; i < k; ++i) {  // ascending slices
-    const uint32_t lo = std::min(nsegs, i * step), hi = std::min(nsegs, lo + step);
-    if (hi > lo) hipLaunchKernelGGL(k_children_min, dim3((hi - lo + 255) / 256), dim3(256), 0, s, w, lo, hi);
-  }
+  if (nsegs) hipLaunchKernelGGL(k_children, dim3((nsegs + 255) / 256), dim3(256), 0, s, w, nsegs);
 }
 
 uint32_t run_descent(const Work& w, uint32_t nsegs, hipStream_t s) {

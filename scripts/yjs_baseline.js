@@ -8,6 +8,7 @@
 //
 // Usage: node yjs_baseline.js <batch file> [workers]
 //        node yjs_baseline.js <pairs file> diff   (update, state vector) alternating: Y.diffUpdate each
+//        node yjs_baseline.js <n ops> perop       crdt.js per-op path (bench.py per_op_leg)
 //   batch file = u32le count, then per update u32le length + bytes (bench.py writes it)
 // Single-doc workloads run on ONE core (Yjs integrates a doc on one thread; SURVEY.md §8(d)):
 // `for u of batch: Y.applyUpdate(doc, u)` then `Y.encodeStateAsUpdate(doc)`, timed with
@@ -58,6 +59,28 @@ if (isMainThread) {
   const Y = load();
   if (!Y) {
     console.log(JSON.stringify({ available: false, reason: 'Yjs bundle not found on this machine' }));
+    process.exit(0);
+  }
+  if (process.argv[3] === 'perop') {  // crdt.js per-op path: A set/delete + full encode, B apply + toJSON
+    const { canonicalUpdate } = require(path.join(__dirname, '..', 'tests', 'golden', 'gen', 'v1.js'));
+    const n = parseInt(file, 10);
+    const a = new Y.Doc(); a.clientID = 1;
+    const b = new Y.Doc(); b.clientID = 2;
+    const ma = a.getMap('users'), mb = b.getMap('users');
+    const t0 = process.hrtime.bigint();
+    for (let i = 0; i < n; i++) {
+      const key = 'user' + (i % 100);
+      if (i % 5 === 4) ma.delete(key); else ma.set(key, 'v' + i);
+      const u = Y.encodeStateAsUpdate(a);
+      Y.applyUpdate(b, u);
+      mb.toJSON();
+    }
+    const t1 = process.hrtime.bigint();
+    const st = canonicalUpdate(Y.encodeStateAsUpdate(b));
+    console.log(JSON.stringify({
+      available: true, yjs: '13.5.16', lib0: '0.2.42', node: process.version, workers: 1, ops: n,
+      ms: Number(t1 - t0) / 1e6, state_sha256: crypto.createHash('sha256').update(st).digest('hex'),
+    }));
     process.exit(0);
   }
   const ups = readBatch(file);
