@@ -51,6 +51,8 @@ def parse():
     p.add_argument("--port-replicas", type=int, default=1000, help="replicas in the oracle-port timing sample")
     p.add_argument("--profile-phases", action="store_true")
     p.add_argument("--no-per-op", action="store_true", help="skip the crdt.js per-op leg")
+    p.add_argument("--only-headline", action="store_true",
+                   help="time the headline merge only (no side legs): rocprof averages then match the bench line")
     p.add_argument("--c3-items", type=int, default=10_000_000,
                    help="C3 leg: YArray 'messages', 256 replicas x 16 rounds, this many values (0 = off)")
     return p.parse_args()
@@ -466,27 +468,29 @@ def main():
     value = items_step * args.steps / dt
     phases = [(n, m / args.steps) for n, m in phase_acc.items()]
 
-    # ---- roofline of the dominant kernel. k_parse (K1 speculative parse at every input byte) is the
-    # largest single-kernel phase; its algorithmic traffic is the input bytes it parses, read once
-    # (B_in), and its duration is the HIP-event time of the "decode.parse" phase,
-    # which holds that one launch. `traffic` is the HBM bytes per launch from the committed rocprofv3 PMC pass
-    # (2 x FETCH_SIZE + WRITE_SIZE, gfx950 correction; scripts/pmc.sh + scripts/pmc_summary.py).
+    # ---- roofline of the dominant kernel: k_children (YMap winner / merge adjacency), the longest
+    # single-kernel phase of the C2 merge ("merge.winner" holds exactly that one launch; its HIP
+    # events are recorded on the engine stream the kernel runs on). Algorithmic bytes per segment
+    # (DESIGN.md §Roofline): flags, origin segment, origin unit and client index read once (16 B)
+    # plus two 4-byte read-modify-write atomics (max child, min child: 8 B) = 24 B. `traffic` is the
+    # HBM bytes per launch from the committed rocprofv3 PMC pass (2 x FETCH_SIZE + WRITE_SIZE,
+    # gfx950 correction; scripts/pmc.sh + scripts/pmc_summary.py).
     ph = dict(phases)
-    k_ms = ph.get("decode.parse", 0.0)
-    alg = in_bytes
+    k_ms = ph.get("merge.winner", 0.0)
+    alg = 24 * st.segments
     traffic, traffic_src = None, None
     pmc = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_c2_pmc.csv")))
     if pmc:
         with open(pmc[-1]) as f:
             for r in csv.DictReader(f):
-                if r["kernel"] == "yc::k_parse":
+                if r["kernel"] == "yc::k_children":
                     traffic = int(float(r["hbm_bytes"]))
                     traffic_src = os.path.basename(pmc[-1])
     achieved = alg / (k_ms * 1e-3) / 1e9 if k_ms > 0 else 0.0
     dominant = max(phases, key=lambda p: p[1]) if phases else ("merge", st.device_ms)
     roofline = {
         "bound": "hbm",
-        "kernel": "yc::k_parse",
+        "kernel": "yc::k_children",
         "achieved": round(achieved, 2),
         "peak": HBM_PEAK_GBS,
         "unit": "GB/s",
@@ -495,6 +499,7 @@ def main():
         "traffic_unit": "HBM bytes per launch",
         "traffic_source": traffic_src,
         "alg_bytes_per_launch": alg,
+        "alg_bytes_per_unit": "24 B per segment",
         "avg_launch_ms": round(k_ms, 4),
         "largest_phase": {"name": dominant[0], "ms": round(dominant[1], 4)},
     }
@@ -504,7 +509,7 @@ def main():
 
     # ---- end to end (host buffers in, host buffers out): pack + H2D + merge + D2H + per-document
     # split; never `value`
-    e2e_steps = 2
+    e2e_steps = 0 if args.only_headline else 2
     e0 = time.perf_counter()
     for _ in range(e2e_steps):
         b2 = crdt_amd.Batch(docs=docs, engine=eng) if ndocs > 1 else crdt_amd.Batch(updates, eng)
@@ -514,11 +519,11 @@ def main():
         else:
             b2.result()
         del b2
-    e2e_ms = (time.perf_counter() - e0) * 1e3 / e2e_steps
+    e2e_ms = (time.perf_counter() - e0) * 1e3 / max(1, e2e_steps)
     del batch
     # ---- one C2 document per step (the round-1 headline shape), for continuity
     single = None
-    if ndocs > 1 and rank == 0:
+    if ndocs > 1 and rank == 0 and not args.only_headline:
         sb = crdt_amd.Batch(updates, eng)
         sst = sb.merge()
         s0 = time.perf_counter()
@@ -529,14 +534,15 @@ def main():
         del sb
 
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and not args.only_headline:
         cpu = cpu_baselines(args, cfg, updates, out_update, crdt_amd.Batch(updates, eng).merge(), eng, gen_map)
     fleet = None
-    if rank == 0 and world == 1 and args.fleet_pairs > 0:
+    if rank == 0 and world == 1 and args.fleet_pairs > 0 and not args.only_headline:
         fleet = fleet_sync_leg(eng, args.fleet_pairs)
-    loop = apply_loop_leg(eng, updates, out_update) if rank == 0 and world == 1 else None
-    per_op = per_op_leg(eng) if rank == 0 and world == 1 and not args.no_per_op else None
-    c3 = c3_leg(eng, args.c3_items) if rank == 0 and world == 1 and args.c3_items > 0 else None
+    side = rank == 0 and world == 1 and not args.only_headline
+    loop = apply_loop_leg(eng, updates, out_update) if side else None
+    per_op = per_op_leg(eng) if side and not args.no_per_op else None
+    c3 = c3_leg(eng, args.c3_items) if side and args.c3_items > 0 else None
     line = {
         "metric": "CRDT items merged/sec at 1/2/4/8 MI355X + % of HBM roofline",
         "value": round(value, 1),
@@ -568,7 +574,7 @@ def main():
         "unique_items_per_step_per_gpu": st.units,
         "end_to_end": {"ms_per_step": round(e2e_ms, 3), "items_per_s": round(steps_items / (e2e_ms * 1e-3), 1),
                        "includes": "host pack + H2D + merge + D2H of every document's update and state vector "
-                                   "(split per document on the host), 1 GPU"},
+                                   "(split per document on the host), 1 GPU"} if e2e_steps else None,
         "pipeline_roofline": {
             "b_alg_bytes": b_alg,
             "achieved_GBs": round(b_alg / (ms_per_step * 1e-3) / 1e9, 2),

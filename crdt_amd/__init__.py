@@ -84,6 +84,7 @@ EXPORTS = (
     "ycrdt_array_delete", "ycrdt_doc_client_id", "ycrdt_map_type_at", "ycrdt_doc_take_local_update",
     "ycrdt_doc_flush", "ycrdt_doc_pending", "ycrdt_doc_track_local", "ycrdt_validate_update", "ycrdt_debug_replay",
     "ycrdt_batch_stage_docs", "ycrdt_batch_result_docs", "ycrdt_merge_docs",
+    "ycrdt_map_get", "ycrdt_map_size", "ycrdt_array_length", "ycrdt_array_get",
 )
 
 MERGE_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p)
@@ -137,6 +138,10 @@ def lib():
     L.ycrdt_array_insert.argtypes = [vp, cs, cs, u32, ctypes.c_char_p, sz, u32]
     L.ycrdt_array_delete.argtypes = [vp, cs, cs, u32, u32]
     L.ycrdt_doc_client_id.argtypes = [vp, P(u32)]
+    L.ycrdt_map_get.argtypes = [vp, cs, cs, cs, P(i32), P(_Out)]
+    L.ycrdt_map_size.argtypes = [vp, cs, cs, P(u32)]
+    L.ycrdt_array_length.argtypes = [vp, cs, cs, P(ctypes.c_uint64)]
+    L.ycrdt_array_get.argtypes = [vp, cs, cs, ctypes.c_uint64, P(i32), P(_Out)]
     L.ycrdt_last_error.restype = ctypes.c_char_p
     L.ycrdt_version.restype = ctypes.c_char_p
     _LIB = L
@@ -291,6 +296,27 @@ class Doc:
         t = ctypes.c_int32()
         _check(lib().ycrdt_map_type_at(self._h, root.encode(), key.encode(), ctypes.byref(t)))
         return t.value
+
+    def map_get(self, root: str, key: str, parent_key: str = None):
+        """YMap.get without a toJSON of the map: (state, json) — state 0 absent, 1 value, 2 undefined."""
+        st, out = ctypes.c_int32(), _Out()
+        _check(lib().ycrdt_map_get(self._h, root.encode(), _opt(parent_key), key.encode(), ctypes.byref(st), ctypes.byref(out)))
+        return st.value, _take(out).decode()
+
+    def map_size(self, root: str, parent_key: str = None) -> int:
+        n = ctypes.c_uint32()
+        _check(lib().ycrdt_map_size(self._h, root.encode(), _opt(parent_key), ctypes.byref(n)))
+        return n.value
+
+    def array_length(self, root: str, parent_key: str = None) -> int:
+        n = ctypes.c_uint64()
+        _check(lib().ycrdt_array_length(self._h, root.encode(), _opt(parent_key), ctypes.byref(n)))
+        return n.value
+
+    def array_get(self, root: str, index: int, parent_key: str = None):
+        st, out = ctypes.c_int32(), _Out()
+        _check(lib().ycrdt_array_get(self._h, root.encode(), _opt(parent_key), index, ctypes.byref(st), ctypes.byref(out)))
+        return st.value, _take(out).decode()
 
     def map_set(self, root: str, key: str, any_bytes: bytes, parent_key: str = None):
         a = bytes(any_bytes)

@@ -716,6 +716,8 @@ __global__ __launch_bounds__(DL) void k_direct(Work w) {
 
 void launch_walker(const Work& w, hipStream_t s) {
   if (w.nbig) hipLaunchKernelGGL(k_walker, dim3(w.nbig), dim3(64), 0, s, w);
+}
+void launch_direct(const Work& w, hipStream_t s) {
   if (w.nsmall) hipLaunchKernelGGL(k_direct, dim3((w.nsmall + DL - 1) / DL), dim3(DL), 0, s, w);
 }
 

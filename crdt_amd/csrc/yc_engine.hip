@@ -466,6 +466,8 @@ int run_decode(ycrdt_engine* e, ycrdt_batch* b, bool lazy, Decoded& D, bool gene
   }
   mark(e, "decode.walker");
   launch_walker(w, s);
+  mark(e, "decode.direct");
+  launch_direct(w, s);
   mark(e, "decode.bitmap");
   launch_build_final_bits(w, s);
   launch_struct_count(w, s);
@@ -705,8 +707,9 @@ int run_merge(ycrdt_engine* e, ycrdt_batch* b, const std::unordered_map<uint32_t
     launch_segment_props(w, nsegs, nclients, U, s);
     mark(e, "merge.keys");
     run_key_resolution(w, nsegs, s);
-    mark(e, "merge.winner");
+    mark(e, "merge.winner");  // k_children alone (bench.py's roofline kernel)
     launch_map_winner(w, nsegs, s);
+    mark(e, "merge.descent");
     run_descent(w, nsegs, s);
     mark(e, "merge.dead_types");
     if (D.nested) run_dead_keys(w, nsegs, s);  // only lists under a parent item can die with it
@@ -1734,6 +1737,54 @@ int ycrdt_array_delete(ycrdt_doc* d, const char* root, const char* parent_key, u
   }
   if (rc) return fail(rc, err);
   return YCRDT_OK;
+}
+
+// Per-key reads (YMap.get / has / size, YArray.length / get): the view's hash index, no JSON of
+// the whole type. The first read after a change merges the queue and rebuilds the view, as toJSON.
+static int read_out(const std::string& j, ycrdt_out* out) {
+  out->len = j.size();
+  out->ptr = (uint8_t*)malloc(j.size() + 1);
+  if (!out->ptr) { out->len = 0; return fail(YCRDT_E_CAPACITY, "host allocation failed"); }
+  memcpy(out->ptr, j.data(), j.size());
+  return YCRDT_OK;
+}
+
+int ycrdt_map_get(ycrdt_doc* d, const char* root, const char* parent_key, const char* key, int* state, ycrdt_out* json) {
+  if (!d || !root || !key || !state || !json) return fail(YCRDT_E_ARG, "null arg");
+  json->ptr = nullptr;
+  json->len = 0;
+  const int rc = ensure_view(d);
+  if (rc) return rc;
+  std::string j;
+  view_map_get(d->view, target_of(root, parent_key), key, *state, j);
+  return read_out(j, json);
+}
+
+int ycrdt_map_size(ycrdt_doc* d, const char* root, const char* parent_key, uint32_t* size) {
+  if (!d || !root || !size) return fail(YCRDT_E_ARG, "null arg");
+  const int rc = ensure_view(d);
+  if (rc) return rc;
+  *size = view_map_size(d->view, target_of(root, parent_key));
+  return YCRDT_OK;
+}
+
+int ycrdt_array_length(ycrdt_doc* d, const char* root, const char* parent_key, uint64_t* length) {
+  if (!d || !root || !length) return fail(YCRDT_E_ARG, "null arg");
+  const int rc = ensure_view(d);
+  if (rc) return rc;
+  *length = view_array_length(d->view, target_of(root, parent_key));
+  return YCRDT_OK;
+}
+
+int ycrdt_array_get(ycrdt_doc* d, const char* root, const char* parent_key, uint64_t index, int* state, ycrdt_out* json) {
+  if (!d || !root || !state || !json) return fail(YCRDT_E_ARG, "null arg");
+  json->ptr = nullptr;
+  json->len = 0;
+  const int rc = ensure_view(d);
+  if (rc) return rc;
+  std::string j;
+  view_array_get(d->view, target_of(root, parent_key), index, *state, j);
+  return read_out(j, json);
 }
 
 int ycrdt_validate_update(ycrdt_buf update, int* structs_ok) {

@@ -437,39 +437,52 @@ bool visible(const ViewSeg& s) { return (s.flags & VS_ITEM) && !(s.flags & VS_DE
 
 }  // namespace
 
+namespace {
+std::string entry_key(uint32_t parent_unit, const uint8_t* name, uint32_t name_len, const uint8_t* psub, uint32_t psub_len,
+                      bool has_psub) {
+  std::string k;
+  k.reserve(10 + name_len + psub_len);
+  k.append((const char*)&parent_unit, 4);
+  k.append((const char*)name, name_len);
+  k.push_back('\0');
+  k.push_back(has_psub ? 'P' : 'A');
+  k.append((const char*)psub, psub_len);
+  return k;
+}
+}  // namespace
+
 void HostView::index() {
   by_parent.clear();
+  entry.clear();
+  root_entries.clear();
   for (uint32_t i = 0; i < keys.size(); ++i) by_parent[keys[i].parent_unit].push_back(i);
-  for (auto& kv : by_parent)  // deterministic member order: by entry name, then slot
+  for (auto& kv : by_parent) {  // deterministic member order: by entry name, then slot
     std::sort(kv.second.begin(), kv.second.end(), [&](uint32_t a, uint32_t b) {
       const std::string sa = str(keys[a].psub_pos, keys[a].psub_len), sb = str(keys[b].psub_pos, keys[b].psub_len);
       return sa != sb ? sa < sb : keys[a].slot < keys[b].slot;
     });
+    // the first list (lowest slot) of every (parent, name, entry) is the one the lookups return
+    for (uint32_t ki : kv.second) {
+      const ViewKey& K = keys[ki];
+      const bool root = K.parent_unit == VNONE, ps = (K.flags & VK_PSUB) != 0;
+      entry.emplace(entry_key(K.parent_unit, root ? bytes.data() + K.name_pos : nullptr, root ? K.name_len : 0,
+                              bytes.data() + K.psub_pos, ps ? K.psub_len : 0, ps),
+                    ki);
+      if (root && ps) root_entries[str(K.name_pos, K.name_len)].push_back(ki);
+    }
+  }
 }
 
 const ViewKey* HostView::root_list(const std::string& name, const std::string* psub) const {
-  auto it = by_parent.find(VNONE);
-  if (it == by_parent.end()) return nullptr;
-  for (uint32_t ki : it->second) {
-    const ViewKey& K = keys[ki];
-    if (K.name_len != name.size() || memcmp(bytes.data() + K.name_pos, name.data(), name.size()) != 0) continue;
-    if (!psub) { if (!(K.flags & VK_PSUB)) return &K; continue; }
-    if ((K.flags & VK_PSUB) && K.psub_len == psub->size() && memcmp(bytes.data() + K.psub_pos, psub->data(), psub->size()) == 0)
-      return &K;
-  }
-  return nullptr;
+  const auto it = entry.find(entry_key(VNONE, (const uint8_t*)name.data(), (uint32_t)name.size(),
+                                       psub ? (const uint8_t*)psub->data() : nullptr, psub ? (uint32_t)psub->size() : 0, psub != nullptr));
+  return it == entry.end() ? nullptr : &keys[it->second];
 }
 
 const ViewKey* HostView::child_list(uint32_t unit, const std::string* psub) const {
-  auto it = by_parent.find(unit);
-  if (it == by_parent.end()) return nullptr;
-  for (uint32_t ki : it->second) {
-    const ViewKey& K = keys[ki];
-    if (!psub) { if (!(K.flags & VK_PSUB)) return &K; continue; }
-    if ((K.flags & VK_PSUB) && K.psub_len == psub->size() && memcmp(bytes.data() + K.psub_pos, psub->data(), psub->size()) == 0)
-      return &K;
-  }
-  return nullptr;
+  const auto it = entry.find(entry_key(unit, nullptr, 0, psub ? (const uint8_t*)psub->data() : nullptr,
+                                       psub ? (uint32_t)psub->size() : 0, psub != nullptr));
+  return it == entry.end() ? nullptr : &keys[it->second];
 }
 
 int view_type_at(const HostView& v, const std::string& root, const std::string& key) {
@@ -487,13 +500,10 @@ bool view_root_json(const HostView& v, const std::string& name, int kind, std::s
     // root map entries: every root list named `name` with a parentSub
     out.push_back('{');
     bool first = true;
-    auto it = v.by_parent.find(VNONE);
-    if (it != v.by_parent.end())
+    auto it = v.root_entries.find(name);
+    if (it != v.root_entries.end())
       for (uint32_t ki : it->second) {
         const ViewKey& K = v.keys[ki];
-        if (!(K.flags & VK_PSUB) || K.name_len != name.size() ||
-            memcmp(v.bytes.data() + K.name_pos, name.data(), name.size()) != 0)
-          continue;
         if (!(K.win.flags & VS_SET) || (K.win.flags & VS_DELETED) || !(K.win.flags & VS_ITEM)) continue;
         std::vector<std::pair<bool, std::string>> el;
         seg_elements(c, K.win, el, true);
@@ -509,6 +519,79 @@ bool view_root_json(const HostView& v, const std::string& name, int kind, std::s
   }
   array_json(c, v.root_list(name, nullptr), out);
   return true;
+}
+
+namespace {
+// the list a read addresses (nullptr: it does not exist), `want` = 1 YMap, 0 YArray
+const ViewKey* read_list(const HostView& v, const OpTarget& t, uint32_t want, const std::string* psub) {
+  ParentRef pr;
+  std::string err;
+  if (resolve_parent(v, t, want, pr, err) != YCRDT_OK) return nullptr;
+  return target_list(v, t, pr, psub);
+}
+}  // namespace
+
+void view_map_get(const HostView& v, const OpTarget& t, const std::string& key, int& state, std::string& json) {
+  state = 0;
+  json.clear();
+  const ViewKey* K = read_list(v, t, 1, &key);
+  if (!K || !(K->win.flags & VS_SET) || (K->win.flags & VS_DELETED) || !(K->win.flags & VS_ITEM)) return;
+  // typeMapGet (Y@49897): the last element of the entry's winning item
+  JsonCtx c{v};
+  std::vector<std::pair<bool, std::string>> el;
+  seg_elements(c, K->win, el, true);
+  if (el.empty()) return;
+  state = el.back().first ? 1 : 2;
+  if (state == 1) json = el.back().second;
+}
+
+uint32_t view_map_size(const HostView& v, const OpTarget& t) {
+  uint32_t n = 0;
+  auto count = [&](const ViewKey& K) {
+    if ((K.flags & VK_PSUB) && (K.win.flags & VS_SET) && !(K.win.flags & VS_DELETED) && (K.win.flags & VS_ITEM)) ++n;
+  };
+  if (!t.nested) {
+    const auto it = v.root_entries.find(t.root);
+    if (it != v.root_entries.end())
+      for (uint32_t ki : it->second) count(v.keys[ki]);
+    return n;
+  }
+  ParentRef pr;
+  std::string err;
+  if (resolve_parent(v, t, 1, pr, err) != YCRDT_OK) return 0;
+  const auto it = v.by_parent.find(pr.unit);
+  if (it != v.by_parent.end())
+    for (uint32_t ki : it->second) count(v.keys[ki]);
+  return n;
+}
+
+uint64_t view_array_length(const HostView& v, const OpTarget& t) {
+  const ViewKey* L = read_list(v, t, 0, nullptr);
+  uint64_t n = 0;
+  if (L)
+    for (uint32_t i = 0; i < L->nseg; ++i)
+      if (visible(v.segs[L->seg0 + i])) n += v.segs[L->seg0 + i].len;
+  return n;
+}
+
+void view_array_get(const HostView& v, const OpTarget& t, uint64_t index, int& state, std::string& json) {
+  state = 0;
+  json.clear();
+  const ViewKey* L = read_list(v, t, 0, nullptr);
+  if (!L) return;
+  for (uint32_t i = 0; i < L->nseg; ++i) {
+    const ViewSeg& s = v.segs[L->seg0 + i];
+    if (!visible(s)) continue;
+    if (index >= s.len) { index -= s.len; continue; }
+    JsonCtx c{v};
+    std::vector<std::pair<bool, std::string>> el;
+    seg_elements(c, s, el, false);
+    if (index >= el.size()) return;
+    // YArray.get of an `undefined` element: toJSON writes null there, get returns undefined
+    state = el[index].first ? 1 : 2;
+    if (state == 1) json = el[index].second;
+    return;
+  }
 }
 
 bool any_values_ok(const uint8_t* p, size_t n, uint32_t count) {

@@ -17,6 +17,10 @@ struct HostView {
   std::vector<ViewSeg> segs;
   std::vector<uint8_t> bytes;  // the merged doc state the byte ranges point into
   std::unordered_map<uint32_t, std::vector<uint32_t>> by_parent;  // parent unit (VNONE = root) -> keys
+  // (parent, root name, entry key | array) -> list: the per-key lookups of YMap.get / has and the
+  // local ops, O(1) instead of a scan of the parent's lists
+  std::unordered_map<std::string, uint32_t> entry;
+  std::unordered_map<std::string, std::vector<uint32_t>> root_entries;  // root name -> its YMap entries
   bool valid = false;
 
   void index();
@@ -40,6 +44,14 @@ struct OpTarget {
   bool nested = false;
   std::string key;
 };
+
+// Per-key reads of the view (YMap.get / has / size, YArray.length / get) without building the
+// type's JSON: state 0 = absent, 1 = present (`json` holds the value), 2 = present but `undefined`
+// (YMap.has is true, toJSON drops it). A nested target whose type does not exist reads as empty.
+void view_map_get(const HostView& v, const OpTarget& t, const std::string& key, int& state, std::string& json);
+uint32_t view_map_size(const HostView& v, const OpTarget& t);
+uint64_t view_array_length(const HostView& v, const OpTarget& t);
+void view_array_get(const HostView& v, const OpTarget& t, uint64_t index, int& state, std::string& json);
 
 // Local ops as one Yjs v1 update each (client, clock = the doc's next clock for its client).
 // Values are lib0 `any` encodings (concatenated for inserts). Return 0 or a YCRDT_E_* code with

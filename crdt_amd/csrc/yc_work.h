@@ -399,6 +399,7 @@ void launch_view(const Work& w, const ViewBufs& v, uint32_t nsegs, uint32_t nlis
 void launch_group_parse(const Work& w, hipStream_t s);   // k_parse: nxt at every byte
 void launch_group_tables(const Work& w, hipStream_t s);  // k_tables: chain exits (+ single-group walk)
 void launch_walker(const Work& w, hipStream_t s);
+void launch_direct(const Work& w, hipStream_t s);
 void launch_build_final_bits(const Work& w, hipStream_t s);
 void launch_struct_count(const Work& w, hipStream_t s);
 void launch_struct_scatter(const Work& w, hipStream_t s);

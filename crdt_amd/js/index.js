@@ -99,14 +99,16 @@ class YMap extends AbstractType {
     const v = JSON.parse(binding.docJson(h, this._root, 0))[this._pkey];
     return v && typeof v === 'object' && !Array.isArray(v) ? v : {};
   }
-  has(key) { return Object.prototype.hasOwnProperty.call(this.toJSON(), key); }
+  // per-key reads go to the view's hash index (no toJSON of the whole map per call)
+  has(key) { return binding.mapHas(this._bound(), this._root, this._pkey, key); }
   get(key) {
     const h = this._bound();
     if (this._pkey === null) {
       const tr = binding.mapTypeAt(h, this._root, key);
       if (tr === TYPE_ARRAY || tr === TYPE_MAP) return this.doc._nested(this._root, key, tr);
     }
-    return this.toJSON()[key];
+    const j = binding.mapGet(h, this._root, this._pkey, key);
+    return j === undefined ? undefined : JSON.parse(j);
   }
   set(key, value) {
     const h = this._bound();
@@ -129,7 +131,7 @@ class YMap extends AbstractType {
   delete(key) { const h = this._bound(); mutate(this.doc, () => binding.mapDelete(h, this._root, this._pkey, key)); }
   forEach(f) { const j = this.toJSON(); for (const k of Object.keys(j)) f(j[k], k, this); }
   keys() { return Object.keys(this.toJSON())[Symbol.iterator](); }
-  get size() { return Object.keys(this.toJSON()).length; }
+  get size() { return binding.mapSize(this._bound(), this._root, this._pkey); }
 }
 
 class YArray extends AbstractType {
@@ -141,8 +143,12 @@ class YArray extends AbstractType {
     return Array.isArray(v) ? v : [];
   }
   toArray() { return this.toJSON(); }
-  get length() { return this.toJSON().length; }
-  get(index) { return this.toJSON()[index]; }
+  get length() { return this.doc ? binding.arrayLength(this._bound(), this._root, this._pkey) : this._prelim.length; }
+  get(index) {
+    if (!this.doc) return this._prelim[index];
+    const j = binding.arrayGet(this._bound(), this._root, this._pkey, index);
+    return j === undefined ? undefined : JSON.parse(j);
+  }
   insert(index, content) {
     if (!this.doc) { this._prelim.splice(index, 0, ...content); return; }
     const h = this._bound();

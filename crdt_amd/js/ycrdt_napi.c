@@ -495,6 +495,95 @@ static napi_value js_map_type_at(napi_env env, napi_callback_info info) {
   return v;
 }
 
+/* per-key reads: JSON text, or undefined when absent / `undefined` (state 0 / 2); mapHas → bool */
+static napi_value read_result(napi_env env, int rc, int state, ycrdt_out *o, int want_has) {
+  napi_value v;
+  if (rc != YCRDT_OK) return throw_rc(env, rc);
+  if (want_has) CHECK(env, napi_get_boolean(env, state != 0, &v));
+  else if (state == 1) CHECK(env, napi_create_string_utf8(env, (const char *)o->ptr, o->len, &v));
+  else CHECK(env, napi_get_undefined(env, &v));
+  ycrdt_free(o);
+  return v;
+}
+
+/* mapGet(doc, root, parentKey, key) → JSON text | undefined   (YMap.get, crdt.js:424) */
+static napi_value js_map_get(napi_env env, napi_callback_info info) {
+  size_t argc = 4;
+  napi_value argv[4];
+  CHECK(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+  op_args a;
+  if (!op_target(env, argv, argc, 1, &a)) return NULL;
+  int state = 0;
+  ycrdt_out o = {NULL, 0};
+  int rc = ycrdt_map_get(a.d, a.root, a.pkey, a.key, &state, &o);
+  op_free(&a);
+  return read_result(env, rc, state, &o, 0);
+}
+
+/* mapHas(doc, root, parentKey, key) → bool   (YMap.has, crdt.js:423) */
+static napi_value js_map_has(napi_env env, napi_callback_info info) {
+  size_t argc = 4;
+  napi_value argv[4];
+  CHECK(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+  op_args a;
+  if (!op_target(env, argv, argc, 1, &a)) return NULL;
+  int state = 0;
+  ycrdt_out o = {NULL, 0};
+  int rc = ycrdt_map_get(a.d, a.root, a.pkey, a.key, &state, &o);
+  op_free(&a);
+  return read_result(env, rc, state, &o, 1);
+}
+
+/* mapSize(doc, root, parentKey) → number   (YMap.size) */
+static napi_value js_map_size(napi_env env, napi_callback_info info) {
+  size_t argc = 3;
+  napi_value argv[3], v;
+  CHECK(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+  op_args a;
+  if (!op_target(env, argv, argc, 0, &a)) return NULL;
+  uint32_t n = 0;
+  int rc = ycrdt_map_size(a.d, a.root, a.pkey, &n);
+  op_free(&a);
+  if (rc != YCRDT_OK) return throw_rc(env, rc);
+  CHECK(env, napi_create_uint32(env, n, &v));
+  return v;
+}
+
+/* arrayLength(doc, root, parentKey) → number   (YArray.length; push, crdt.js:427) */
+static napi_value js_array_length(napi_env env, napi_callback_info info) {
+  size_t argc = 3;
+  napi_value argv[3], v;
+  CHECK(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+  op_args a;
+  if (!op_target(env, argv, argc, 0, &a)) return NULL;
+  uint64_t n = 0;
+  int rc = ycrdt_array_length(a.d, a.root, a.pkey, &n);
+  op_free(&a);
+  if (rc != YCRDT_OK) return throw_rc(env, rc);
+  CHECK(env, napi_create_double(env, (double)n, &v));
+  return v;
+}
+
+/* arrayGet(doc, root, parentKey, index) → JSON text | undefined   (YArray.get) */
+static napi_value js_array_get(napi_env env, napi_callback_info info) {
+  size_t argc = 4;
+  napi_value argv[4];
+  CHECK(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+  op_args a;
+  if (!op_target(env, argv, argc, 0, &a)) return NULL;
+  int64_t index = 0;
+  if (argc < 4 || napi_get_value_int64(env, argv[3], &index) != napi_ok) {
+    op_free(&a);
+    napi_throw_type_error(env, NULL, "arrayGet(doc, root, parentKey, index)");
+    return NULL;
+  }
+  int state = 0;
+  ycrdt_out o = {NULL, 0};
+  int rc = index < 0 ? YCRDT_OK : ycrdt_array_get(a.d, a.root, a.pkey, (uint64_t)index, &state, &o);
+  op_free(&a);
+  return read_result(env, rc, state, &o, 0);
+}
+
 static napi_value init(napi_env env, napi_value exports) {
   napi_property_descriptor props[] = {
       {"setDevice", NULL, js_set_device, NULL, NULL, NULL, napi_default, NULL},
@@ -516,6 +605,11 @@ static napi_value init(napi_env env, napi_value exports) {
       {"mapDelete", NULL, js_map_delete, NULL, NULL, NULL, napi_default, NULL},
       {"arrayInsert", NULL, js_array_insert, NULL, NULL, NULL, napi_default, NULL},
       {"arrayDelete", NULL, js_array_delete, NULL, NULL, NULL, napi_default, NULL},
+      {"mapGet", NULL, js_map_get, NULL, NULL, NULL, napi_default, NULL},
+      {"mapHas", NULL, js_map_has, NULL, NULL, NULL, napi_default, NULL},
+      {"mapSize", NULL, js_map_size, NULL, NULL, NULL, napi_default, NULL},
+      {"arrayLength", NULL, js_array_length, NULL, NULL, NULL, napi_default, NULL},
+      {"arrayGet", NULL, js_array_get, NULL, NULL, NULL, napi_default, NULL},
   };
   napi_define_properties(env, exports, sizeof(props) / sizeof(props[0]), props);
   return exports;

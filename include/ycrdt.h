@@ -134,6 +134,15 @@ int ycrdt_array_insert(ycrdt_doc *d, const char *root, const char *parent_key, u
 int ycrdt_array_delete(ycrdt_doc *d, const char *root, const char *parent_key, uint32_t index, uint32_t length);
 /* doc.clientID */
 int ycrdt_doc_client_id(ycrdt_doc *d, uint32_t *out);
+/* Per-key reads of the materialised view, replacing a full toJSON per call (facade YMap.get / has /
+ * size, YArray.length / get; crdt.js:423-424 `h[name].has(key)` / `.get(key)`, push's length):
+ * state 0 = absent, 1 = present (`json` = JSON text of the value), 2 = present, value `undefined`.
+ * `json` is always allocated (free with ycrdt_free). A nested target whose type does not exist
+ * reads as empty. */
+int ycrdt_map_get(ycrdt_doc *d, const char *root, const char *parent_key, const char *key, int *state, ycrdt_out *json);
+int ycrdt_map_size(ycrdt_doc *d, const char *root, const char *parent_key, uint32_t *size);
+int ycrdt_array_length(ycrdt_doc *d, const char *root, const char *parent_key, uint64_t *length);
+int ycrdt_array_get(ycrdt_doc *d, const char *root, const char *parent_key, uint64_t index, int *state, ycrdt_out *json);
 /* Incremental local-op encode: the updates of the local ops
  * (ycrdt_map_* / ycrdt_array_*) applied since the previous call, as ONE update (Y.mergeUpdates of
  * them; a single op's own update is returned as is; none = the empty update). crdt.js broadcasts

@@ -7,7 +7,7 @@ tag=${1:-run}
 shift
 out=gpurun_out/pmc_$tag
 mkdir -p $out
-B="bench.py --steps 3 --warmup 1 --no-cpu-baseline --fleet-pairs 0 --c3-items 0 $*"
+B="bench.py --steps 3 --warmup 1 --only-headline $*"
 timeout -s KILL 300 rocprofv3 --kernel-trace --stats --output-format csv -d $out/stats -o stats -- python3 $B > $out/stats.log 2>&1 || exit 1
 echo "stats ok"
 timeout -s KILL 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_WAVE_CYCLES SQ_BUSY_CYCLES --output-format csv -d $out/sq -o sq -- python3 $B > $out/sq.log 2>&1 || exit 1
