@@ -84,7 +84,7 @@ EXPORTS = (
     "ycrdt_array_delete", "ycrdt_doc_client_id", "ycrdt_map_type_at", "ycrdt_doc_take_local_update",
     "ycrdt_doc_flush", "ycrdt_doc_pending", "ycrdt_doc_track_local", "ycrdt_validate_update", "ycrdt_debug_replay",
     "ycrdt_batch_stage_docs", "ycrdt_batch_result_docs", "ycrdt_merge_docs",
-    "ycrdt_map_get", "ycrdt_map_size", "ycrdt_array_length", "ycrdt_array_get",
+    "ycrdt_map_get", "ycrdt_map_size", "ycrdt_array_length", "ycrdt_array_get", "ycrdt_apply_updates_multi",
 )
 
 MERGE_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p)
@@ -139,6 +139,7 @@ def lib():
     L.ycrdt_array_delete.argtypes = [vp, cs, cs, u32, u32]
     L.ycrdt_doc_client_id.argtypes = [vp, P(u32)]
     L.ycrdt_map_get.argtypes = [vp, cs, cs, cs, P(i32), P(_Out)]
+    L.ycrdt_apply_updates_multi.argtypes = [vp, P(vp), P(_Buf), sz]
     L.ycrdt_map_size.argtypes = [vp, cs, cs, P(u32)]
     L.ycrdt_array_length.argtypes = [vp, cs, cs, P(ctypes.c_uint64)]
     L.ycrdt_array_get.argtypes = [vp, cs, cs, ctypes.c_uint64, P(i32), P(_Out)]
@@ -422,6 +423,17 @@ def encode_state_as_update(doc: Doc, sv: bytes = b"") -> bytes:
 
 def encode_state_vector(doc: Doc) -> bytes:
     return doc.encode_state_vector()
+
+
+def apply_updates_multi(docs, updates, engine=None):
+    """Y.applyUpdate(docs[i], updates[i]) for every i — a fleet ingest batch — merged in one device
+    pass for every document with nothing pending (ycrdt_apply_updates_multi)."""
+    if len(docs) != len(updates):
+        raise ValueError("one document per update")
+    eng = engine or (docs[0].engine if docs else default_engine())
+    arr, keep = _bufs(updates)
+    hs = (ctypes.c_void_p * max(1, len(docs)))(*[d._h.value for d in docs])
+    _check(lib().ycrdt_apply_updates_multi(eng._h, hs, arr, len(keep)))
 
 
 def merge_updates(updates, engine=None) -> bytes:

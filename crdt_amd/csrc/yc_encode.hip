@@ -368,4 +368,39 @@ void launch_encode_write(const Work& w, uint32_t nsegs, uint32_t nclients, hipSt
   }
 }
 
+// Per-document byte ranges of a multi-document encode. Clients are laid out in (document, client)
+// descending order, so each document's struct blocks, delete-set blocks and state-vector entries
+// are contiguous: rng[9d + 0..8] = struct (lo, hi, clients), delete set (lo, hi, clients),
+// state vector (lo, hi, entries), relative to each section's first block.
+__global__ void k_doc_ranges_init(uint32_t* rng, uint32_t ndocs) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < 9 * ndocs) rng[i] = (i % 3 == 0) ? 0xFFFFFFFFu : 0u;
+}
+__global__ void k_doc_ranges(Work w, uint32_t nclients, uint32_t ndocs, uint32_t* rng) {
+  const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= nclients) return;
+  const uint32_t d = w.cl_doc[c];
+  if (d >= ndocs) { raise_err(&w.ctr->err, ERR_DECODE); return; }
+  uint32_t* r = rng + 9 * (size_t)d;
+  if (ccol(w, CC_NINCL)[c]) {
+    atomicMin(&r[0], ccol(w, CC_BLKPOS)[c]);
+    atomicMax(&r[1], ccol(w, CC_BLKPOS)[c] + ccol(w, CC_BLK)[c]);
+    atomicAdd(&r[2], 1u);
+  }
+  if (ccol(w, CC_NRUNS)[c]) {
+    atomicMin(&r[3], ccol(w, CC_DSPOS)[c]);
+    atomicMax(&r[4], ccol(w, CC_DSPOS)[c] + ccol(w, CC_DSBLK)[c]);
+    atomicAdd(&r[5], 1u);
+  }
+  if (ccol(w, CC_SV)[c]) {
+    atomicMin(&r[6], ccol(w, CC_SVPOS)[c]);
+    atomicMax(&r[7], ccol(w, CC_SVPOS)[c] + ccol(w, CC_SV)[c]);
+    atomicAdd(&r[8], 1u);
+  }
+}
+void launch_doc_ranges(const Work& w, uint32_t nclients, uint32_t ndocs, uint32_t* rng, hipStream_t s) {
+  hipLaunchKernelGGL(k_doc_ranges_init, dim3(9 * ndocs / 256 + 1), dim3(256), 0, s, rng, ndocs);
+  if (nclients) hipLaunchKernelGGL(k_doc_ranges, dim3(nclients / 256 + 1), dim3(256), 0, s, w, nclients, ndocs, rng);
+}
+
 }  // namespace yc

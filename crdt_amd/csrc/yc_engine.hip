@@ -38,6 +38,41 @@ int fail(int code, const std::string& msg) {
 struct DevBuf {
   void* p = nullptr;
   size_t cap = 0;
+  bool arena = false;  // a block of the engine's doc-state arena (Arena::release), not a hipMalloc
+};
+
+// Doc states live in an engine-owned HBM arena: 64 MiB slabs carved into power-of-two blocks
+// (256 B .. 1 MiB) with a free list per size class; larger states get their own hipMalloc. A fleet
+// of 100k+ small documents then costs a few slab allocations instead of one hipMalloc per doc.
+struct Arena {
+  static constexpr size_t MIN_SHIFT = 8, MAX_SHIFT = 20, SLAB = size_t(64) << 20;
+  std::vector<void*> slabs;
+  std::vector<void*> free_[MAX_SHIFT - MIN_SHIFT + 1];
+  uint8_t* cur = nullptr;
+  size_t left = 0;
+  static int cls(size_t bytes) {
+    int c = 0;
+    while ((size_t(1) << (MIN_SHIFT + c)) < bytes) ++c;
+    return c;
+  }
+  void* alloc(size_t bytes, size_t& cap) {
+    const int c = cls(bytes);
+    cap = size_t(1) << (MIN_SHIFT + c);
+    if (!free_[c].empty()) { void* p = free_[c].back(); free_[c].pop_back(); return p; }
+    if (left < cap) {
+      void* s = nullptr;
+      if (hipMalloc(&s, SLAB) != hipSuccess) return nullptr;
+      slabs.push_back(s);
+      cur = (uint8_t*)s;
+      left = SLAB;  // the tail of the previous slab (< one block) is abandoned
+    }
+    void* p = cur;
+    cur += cap;
+    left -= cap;
+    return p;
+  }
+  void release(void* p, size_t cap) { free_[cls(cap)].push_back(p); }
+  ~Arena() { for (void* s : slabs) hipFree(s); }
 };
 
 bool grow(DevBuf& b, size_t bytes) {
@@ -110,7 +145,7 @@ enum Buf {
   B_TPRV, B_TMPRV, B_TMTAIL, B_TTREP, B_TOTAIL,
   B_OFIRST, B_OCIDX, B_OSIZE, B_OPOS, B_RSEG, B_RLEN, B_RSIZE, B_RPOS, B_OUT, B_SVOUT,
   B_VKMAP, B_VKREP, B_VKEYS, B_VNKEYS, B_VPOS, B_VD0, B_VN0, B_VD1, B_VN1, B_VORDER, B_VSEGS,
-  B_SCRATCH2, B_TMP2, B_CAPS, B_CLKEY, B_CLKEY2, B_CLDOC, B_DSFA, B_EMIT,
+  B_SCRATCH2, B_TMP2, B_CAPS, B_CLKEY, B_CLKEY2, B_CLDOC, B_DSFA, B_EMIT, B_DOCRNG,
   B_COUNT
 };
 
@@ -138,7 +173,23 @@ struct ycrdt_engine {
   uint32_t out_bytes = 0, sv_bytes = 0;
   uint32_t nsegs = 0, nlists = 0;  // segments / YArray lists of the last merge (the view reads them)
   ycrdt_merge_stats last{};
+  Arena arena;                      // doc states (grow_state)
 };
+
+// a doc state buffer of at least `bytes` (contents not kept)
+bool grow_state(ycrdt_engine* e, DevBuf& b, size_t bytes) {
+  if (bytes == 0) bytes = 16;
+  if (bytes <= b.cap) return true;
+  if (b.p) { if (b.arena) e->arena.release(b.p, b.cap); else hipFree(b.p); }
+  b = DevBuf();
+  if (bytes <= (size_t(1) << Arena::MAX_SHIFT)) {
+    b.p = e->arena.alloc(bytes, b.cap);
+    b.arena = b.p != nullptr;
+    if (!b.p) b.cap = 0;
+    return b.p != nullptr;
+  }
+  return grow(b, bytes);
+}
 
 struct ycrdt_doc {
   ycrdt_engine* e = nullptr;
@@ -161,7 +212,7 @@ struct ycrdt_doc {
 
 struct ycrdt_batch {
   ycrdt_engine* e = nullptr;
-  DevBuf bytes, meta;
+  DevBuf bytes, meta, pieces;
   std::vector<uint32_t> uoff, ulen, ugroup;
   std::vector<uint32_t> udoc;   // multi-document batch: document of every staged update
   uint32_t ndocs = 1;
@@ -210,22 +261,33 @@ constexpr size_t DIRECT_MAX_BYTES = GROUP_BYTES;  // an update the direct lane w
 constexpr size_t DIRECT_TINY_BYTES = 1024;         // always direct (a handful of structs)
 constexpr size_t DIRECT_MIN_COUNT = 1024;          // enough small updates to fill wavefronts
 
-// Lays out n updates (64-byte aligned, so every update owns its bitmap words) + decode group table.
-// `prefix` (device) is placed first.
-void layout(ycrdt_batch* b, const ycrdt_buf* ups, size_t n, size_t prefix_len) {
-  size_t total = prefix_len ? ((prefix_len + 63) & ~size_t(63)) : 0;
+// One staged input: host bytes, or a device buffer (a doc state already in HBM).
+struct Src {
+  const uint8_t* p;
+  size_t len;
+  bool dev;
+};
+
+// Lays out the sources (64-byte aligned, so every update owns its bitmap words; device sources
+// first, then the host ones in one contiguous region) + decode group table.
+void layout(ycrdt_batch* b, const std::vector<Src>& src, std::vector<uint32_t>& order) {
   b->uoff.clear(); b->ulen.clear(); b->ugroup.clear(); b->groups.clear(); b->ulist.clear();
   b->in_bytes = 0;
   const char* mode = getenv("YCRDT_DECODE");
   const int force = mode && !strcmp(mode, "tables") ? 1 : mode && !strcmp(mode, "direct") ? 2 : 0;
   size_t nsmall = 0;
-  for (size_t i = 0; i < n; ++i) nsmall += ups[i].len <= DIRECT_MAX_BYTES;
+  for (const Src& x : src) nsmall += x.len <= DIRECT_MAX_BYTES;
   auto direct = [&](size_t len) {
     if (len > DIRECT_MAX_BYTES || force == 1) return false;
     return force == 2 || nsmall >= DIRECT_MIN_COUNT || len <= DIRECT_TINY_BYTES;
   };
+  order.clear();
+  for (size_t i = 0; i < src.size(); ++i) if (src[i].dev) order.push_back((uint32_t)i);
+  for (size_t i = 0; i < src.size(); ++i) if (!src[i].dev) order.push_back((uint32_t)i);
   std::vector<uint32_t> small;
-  auto add = [&](size_t off, size_t len) {
+  size_t total = 0;
+  for (const uint32_t i : order) {
+    const size_t off = total, len = src[i].len;
     const uint32_t u = (uint32_t)b->uoff.size();
     b->uoff.push_back((uint32_t)off);
     b->ulen.push_back((uint32_t)len);
@@ -245,11 +307,7 @@ void layout(ycrdt_batch* b, const ycrdt_buf* ups, size_t n, size_t prefix_len) {
       }
     }
     b->in_bytes += len;
-  };
-  if (prefix_len) add(0, prefix_len);
-  for (size_t i = 0; i < n; ++i) {
-    add(total, ups[i].len);
-    total += (ups[i].len + 63) & ~size_t(63);
+    total += (len + 63) & ~size_t(63);
   }
   b->nbig = (uint32_t)b->ulist.size();
   b->ulist.insert(b->ulist.end(), small.begin(), small.end());
@@ -257,33 +315,45 @@ void layout(ycrdt_batch* b, const ycrdt_buf* ups, size_t n, size_t prefix_len) {
   b->nbytes = (uint32_t)total;
 }
 
-int stage(ycrdt_batch* b, const ycrdt_buf* ups, size_t n, const DevBuf* prefix, size_t prefix_len,
-          const uint32_t* doc_of = nullptr, uint32_t ndocs = 1) {
+// Stages the sources into the batch buffer: the host region in one H2D copy, device sources by
+// one piece-copy launch. doc_of (one per source) makes it a multi-document batch.
+int stage_srcs(ycrdt_batch* b, const std::vector<Src>& src, const uint32_t* doc_of = nullptr, uint32_t ndocs = 1) {
   ycrdt_engine* e = b->e;
   size_t total64 = 0;
-  for (size_t i = 0; i < n; ++i) total64 += ((ups[i].len + 63) & ~size_t(63));
-  total64 += prefix_len ? ((prefix_len + 63) & ~size_t(63)) : 0;
+  for (const Src& x : src) total64 += ((x.len + 63) & ~size_t(63));
   if (total64 >= 0xF0000000ull) return fail(YCRDT_E_CAPACITY, "batch larger than 3.75 GiB");
-  layout(b, ups, n, prefix_len);
+  std::vector<uint32_t> order;
+  layout(b, src, order);
   if (!grow(b->bytes, (size_t)b->nbytes + 128)) return fail(YCRDT_E_DEVICE, "hipMalloc failed (batch bytes)");
-  // pack on the host, one H2D copy
-  e->pinned_stage.assign((size_t)b->nbytes - (prefix_len ? ((prefix_len + 63) & ~size_t(63)) : 0), 0);
-  size_t base = prefix_len ? ((prefix_len + 63) & ~size_t(63)) : 0;
-  const size_t nu0 = prefix_len ? 1 : 0;
-  for (size_t i = 0; i < n; ++i)
-    if (ups[i].len) memcpy(e->pinned_stage.data() + (b->uoff[nu0 + i] - base), ups[i].ptr, ups[i].len);
-  if (prefix_len) HIPCHK(hipMemcpyAsync(b->bytes.p, prefix->p, prefix_len, hipMemcpyDeviceToDevice, e->stream));
-  if (!e->pinned_stage.empty())
-    HIPCHK(hipMemcpyAsync((uint8_t*)b->bytes.p + base, e->pinned_stage.data(), e->pinned_stage.size(), hipMemcpyHostToDevice, e->stream));
-  // meta: uoff | ulen | ugroup | groups
   const size_t nu = b->ulen.size();
+  size_t ndev = 0;
+  while (ndev < nu && src[order[ndev]].dev) ++ndev;
+  const size_t host0 = ndev < nu ? b->uoff[ndev] : b->nbytes;
+  e->pinned_stage.assign((size_t)b->nbytes - host0, 0);
+  for (size_t u = ndev; u < nu; ++u)
+    if (b->ulen[u]) memcpy(e->pinned_stage.data() + (b->uoff[u] - host0), src[order[u]].p, b->ulen[u]);
+  if (!e->pinned_stage.empty())
+    HIPCHK(hipMemcpyAsync((uint8_t*)b->bytes.p + host0, e->pinned_stage.data(), e->pinned_stage.size(), hipMemcpyHostToDevice, e->stream));
+  if (ndev == 1) {
+    if (b->ulen[0]) HIPCHK(hipMemcpyAsync(b->bytes.p, src[order[0]].p, b->ulen[0], hipMemcpyDeviceToDevice, e->stream));
+  } else if (ndev > 1) {
+    std::vector<Piece> pc;
+    pc.reserve(ndev);
+    for (size_t u = 0; u < ndev; ++u)
+      if (b->ulen[u]) pc.push_back(Piece{src[order[u]].p, (uint8_t*)b->bytes.p + b->uoff[u], b->ulen[u], {0}});
+    if (!grow(b->pieces, sizeof(Piece) * (pc.size() + 1))) return fail(YCRDT_E_DEVICE, "hipMalloc failed (pieces)");
+    HIPCHK(hipMemcpyAsync(b->pieces.p, pc.data(), sizeof(Piece) * pc.size(), hipMemcpyHostToDevice, e->stream));
+    copy_pieces((const Piece*)b->pieces.p, (uint32_t)pc.size(), e->stream);
+  }
+  // meta: uoff | ulen | ugroup | groups | udoc | ulist
   b->ndocs = doc_of && ndocs > 1 ? ndocs : 1;
   b->udoc.clear();
   if (b->ndocs > 1) {
-    if (prefix_len) return fail(YCRDT_E_ARG, "internal: multi-document batch with a state prefix");
-    b->udoc.assign(doc_of, doc_of + n);
-    for (const uint32_t d : b->udoc)
-      if (d >= b->ndocs) return fail(YCRDT_E_ARG, "document index out of range");
+    b->udoc.resize(nu);
+    for (size_t u = 0; u < nu; ++u) {
+      b->udoc[u] = doc_of[order[u]];
+      if (b->udoc[u] >= b->ndocs) return fail(YCRDT_E_ARG, "document index out of range");
+    }
   }
   const size_t meta_bytes = sizeof(uint32_t) * (nu + 1 + nu + nu) + sizeof(Group) * b->groups.size() + 64 +
                             sizeof(uint32_t) * b->udoc.size() + 16 + sizeof(uint32_t) * b->ulist.size() + 16;
@@ -307,6 +377,17 @@ int stage(ycrdt_batch* b, const ycrdt_buf* ups, size_t n, const DevBuf* prefix, 
   HIPCHK(hipStreamSynchronize(e->stream));
   b->merged = false;
   return YCRDT_OK;
+}
+
+// n host updates, optionally behind a device-resident doc state (`prefix`, the first update)
+int stage(ycrdt_batch* b, const ycrdt_buf* ups, size_t n, const DevBuf* prefix, size_t prefix_len,
+          const uint32_t* doc_of = nullptr, uint32_t ndocs = 1) {
+  if (prefix_len && doc_of && ndocs > 1) return fail(YCRDT_E_ARG, "internal: multi-document batch with a state prefix");
+  std::vector<Src> src;
+  src.reserve(n + 1);
+  if (prefix_len) src.push_back(Src{(const uint8_t*)prefix->p, prefix_len, true});
+  for (size_t i = 0; i < n; ++i) src.push_back(Src{ups[i].ptr, ups[i].len, false});
+  return stage_srcs(b, src, doc_of, ndocs);
 }
 
 int map_err(uint32_t code, const char* where) {
@@ -1141,6 +1222,7 @@ void ycrdt_engine_destroy(ycrdt_engine* e) {
   for (auto& b : e->bufs) if (b.p) hipFree(b.p);
   if (e->scratch) {
     if (e->scratch->bytes.p) hipFree(e->scratch->bytes.p);
+    if (e->scratch->pieces.p) hipFree(e->scratch->pieces.p);
     if (e->scratch->meta.p) hipFree(e->scratch->meta.p);
     delete e->scratch;
   }
@@ -1187,7 +1269,7 @@ void ycrdt_doc_destroy(ycrdt_doc* d) {
   if (!d) return;
   hipSetDevice(d->e->device);
   if (d->e->ws_owner == d) d->e->ws_owner = nullptr;
-  if (d->state.p) hipFree(d->state.p);
+  if (d->state.p) { if (d->state.arena) d->e->arena.release(d->state.p, d->state.cap); else hipFree(d->state.p); }
   delete d;
 }
 
@@ -1206,7 +1288,7 @@ int commit_merge(ycrdt_doc* d, const std::vector<ycrdt_buf>& extra, const ClockM
   int rc = stage(&b, extra.data(), extra.size(), d->state_len ? &d->state : nullptr, d->state_len);
   if (rc == YCRDT_OK) rc = run_merge(e, &b, nullptr, caps, order);
   if (rc) return rc;
-  if (!grow(d->state, e->out_bytes + 16)) return fail(YCRDT_E_DEVICE, "hipMalloc failed (doc state)");
+  if (!grow_state(e, d->state, e->out_bytes + 16)) return fail(YCRDT_E_DEVICE, "hipMalloc failed (doc state)");
   HIPCHK(hipMemcpyAsync(d->state.p, e->w.out, e->out_bytes, hipMemcpyDeviceToDevice, e->stream));
   d->state_len = e->out_bytes;
   d->sv.resize(e->sv_bytes);
@@ -1281,6 +1363,99 @@ void enqueue(ycrdt_doc* d, const uint8_t* p, size_t n, bool local) {
   d->view.valid = false;
 }
 
+// Multi-document flush (ycrdt_apply_updates_multi): the documents on the fast path (nothing
+// pending, 13.6 client order) are merged in ONE device pass — each document's state (HBM, read in
+// place) and its queued updates form one multi-document batch (yc_work.h: (doc, client) keys) —
+// and the result is split back into each document's arena block on the device, headers written
+// inline (k_doc_ranges + copy_pieces): no per-document merge, copy or hipMalloc. A missing
+// dependency anywhere sends every document through its own flush (the pending emulation is per
+// document), as does any document on the slow path.
+int flush_multi(ycrdt_engine* e, const std::vector<ycrdt_doc*>& docs) {
+  std::vector<ycrdt_doc*> fast;
+  for (ycrdt_doc* d : docs) {
+    if (d->queue.empty()) continue;
+    if (!d->ing.has_pending && !d->ing.has_ds && e->compat != 135) fast.push_back(d);
+    else if (const int rc = flush(d)) return rc;
+  }
+  if (fast.size() < 2) return fast.empty() ? YCRDT_OK : flush(fast[0]);
+  HIPCHK(hipSetDevice(e->device));
+  const uint32_t nd = (uint32_t)fast.size();
+  std::vector<Src> src;
+  std::vector<uint32_t> doc_of;
+  for (uint32_t j = 0; j < nd; ++j) {
+    ycrdt_doc* d = fast[j];
+    if (d->state_len) { src.push_back(Src{(const uint8_t*)d->state.p, d->state_len, true}); doc_of.push_back(j); }
+    for (const auto& q : d->queue) { src.push_back(Src{q.bytes.data(), q.bytes.size(), false}); doc_of.push_back(j); }
+  }
+  ycrdt_batch& b = scratch_batch(e);
+  int rc = stage_srcs(&b, src, doc_of.data(), nd);
+  if (rc == YCRDT_OK) rc = run_merge(e, &b, nullptr);
+  if (rc == YCRDT_E_PENDING) {
+    for (ycrdt_doc* d : fast)
+      if (const int r2 = flush(d)) return r2;
+    return YCRDT_OK;
+  }
+  if (rc) return rc;
+  // per-document ranges of the encode, then every document's state assembled on the device
+  Work& w = e->w;
+  auto& V = e->bufs;
+  bool ok = true;
+  uint32_t* rng = take<uint32_t>(V, B_DOCRNG, 9 * (size_t)nd + 9, ok);
+  if (!ok) return fail(YCRDT_E_DEVICE, "hipMalloc failed (document ranges)");
+  hipStream_t s = e->stream;
+  launch_doc_ranges(w, (uint32_t)e->last.clients, nd, rng, s);
+  std::vector<uint32_t> r(9 * (size_t)nd);
+  std::vector<uint8_t> svall(e->sv_bytes);
+  Counters c;
+  HIPCHK(hipMemcpyAsync(r.data(), rng, sizeof(uint32_t) * r.size(), hipMemcpyDeviceToHost, s));
+  if (!svall.empty()) HIPCHK(hipMemcpyAsync(svall.data(), w.sv_out, svall.size(), hipMemcpyDeviceToHost, s));
+  HIPCHK(hipMemcpyAsync(&c, w.ctr, sizeof(Counters), hipMemcpyDeviceToHost, s));
+  HIPCHK(hipStreamSynchronize(s));
+  if (c.err) return map_err(c.err, "document split");
+  const uint32_t sbase = c.pad[3], dsbase = c.pad[4] + vu_size_host(c.pad[1]), svbase = vu_size_host(c.pad[2]);
+  std::vector<Piece> pc;
+  pc.reserve(4 * (size_t)nd);
+  std::vector<size_t> len(nd);
+  auto hdr = [](Piece& P, uint32_t v) {
+    P.src = nullptr;
+    P.len = 0;
+    while (v > 127u) { P.inl[P.len++] = (uint8_t)(0x80u | (v & 0x7fu)); v >>= 7; }
+    P.inl[P.len++] = (uint8_t)v;
+  };
+  for (uint32_t j = 0; j < nd; ++j) {
+    const uint32_t* x = &r[9 * (size_t)j];
+    const uint32_t ns = x[2] ? x[1] - x[0] : 0, ndb = x[5] ? x[4] - x[3] : 0;
+    len[j] = vu_size_host(x[2]) + ns + vu_size_host(x[5]) + ndb;
+    ycrdt_doc* d = fast[j];
+    if (!grow_state(e, d->state, len[j] + 16)) return fail(YCRDT_E_DEVICE, "hipMalloc failed (doc state)");
+    uint8_t* dst = (uint8_t*)d->state.p;
+    Piece P{};
+    hdr(P, x[2]); P.dst = dst; dst += P.len; pc.push_back(P);
+    if (ns) { pc.push_back(Piece{w.out + sbase + x[0], dst, ns, {0}}); dst += ns; }
+    hdr(P, x[5]); P.dst = dst; dst += P.len; pc.push_back(P);
+    if (ndb) pc.push_back(Piece{w.out + dsbase + x[3], dst, ndb, {0}});
+    // state vector: its entries (host copy of the encode's state vector section)
+    std::vector<uint8_t> sv;
+    put_vu(sv, x[8]);
+    if (x[8]) sv.insert(sv.end(), svall.begin() + svbase + x[6], svall.begin() + svbase + x[7]);
+    d->sv.swap(sv);
+  }
+  if (!grow(b.pieces, sizeof(Piece) * (pc.size() + 1))) return fail(YCRDT_E_DEVICE, "hipMalloc failed (pieces)");
+  HIPCHK(hipMemcpyAsync(b.pieces.p, pc.data(), sizeof(Piece) * pc.size(), hipMemcpyHostToDevice, s));
+  copy_pieces((const Piece*)b.pieces.p, (uint32_t)pc.size(), s);
+  HIPCHK(hipStreamSynchronize(s));
+  for (uint32_t j = 0; j < nd; ++j) {
+    ycrdt_doc* d = fast[j];
+    d->state_len = len[j];
+    d->last = e->last;  // the whole pass
+    d->view.valid = false;
+    d->queue.clear();
+    d->queue_bytes = 0;
+  }
+  e->ws_owner = nullptr;  // the workspace holds many documents: a view re-merges its own
+  return YCRDT_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -1321,6 +1496,52 @@ int ycrdt_apply_updates(ycrdt_doc* d, const ycrdt_buf* ups, size_t n) {
 }
 
 int ycrdt_apply_update(ycrdt_doc* d, ycrdt_buf update) { return ycrdt_apply_updates(d, &update, 1); }
+
+// Y.applyUpdate(docs[i], ups[i]) for i = 0..n-1 (a fleet ingest batch: many documents, any number
+// of updates each), validated like ycrdt_apply_updates and then merged at once: one device pass
+// for every document on the fast path (flush_multi).
+int ycrdt_apply_updates_multi(ycrdt_engine* e, ycrdt_doc* const* docs, const ycrdt_buf* ups, size_t n) {
+  if (!e || (n && (!docs || !ups))) return fail(YCRDT_E_ARG, "null arg");
+  for (size_t i = 0; i < n; ++i)
+    if (!docs[i] || docs[i]->e != e) return fail(YCRDT_E_ARG, "document of another engine (or null) at " + std::to_string(i));
+  std::vector<UpdScan> sc(n);
+  std::vector<char> ok(n, 0);
+  size_t total = 0;
+  for (size_t i = 0; i < n; ++i) total += ups[i].len;
+  const size_t nt = total > (size_t(4) << 20) && n > 1 ? std::min<size_t>({n, 16, std::max(1u, std::thread::hardware_concurrency())}) : 1;
+  auto work = [&](size_t t) {
+    for (size_t i = t; i < n; i += nt) ok[i] = scan_update(ups[i].ptr, ups[i].len, false, sc[i]) ? 1 : 0;
+  };
+  if (nt > 1) {
+    std::vector<std::thread> th;
+    for (size_t t = 0; t < nt; ++t) th.emplace_back(work, t);
+    for (auto& t : th) t.join();
+  } else {
+    work(0);
+  }
+  std::vector<ycrdt_doc*> touched;
+  int rc = YCRDT_OK;
+  std::string err;
+  for (size_t i = 0; i < n; ++i) {
+    ycrdt_doc* d = docs[i];
+    touched.push_back(d);
+    if (!ok[i]) {  // sequential semantics: what came before is applied, then Yjs throws
+      if (sc[i].structs_ok) {
+        const std::vector<uint8_t> r = repaired_update(ups[i].ptr, sc[i]);
+        enqueue(d, r.data(), r.size(), false);
+      }
+      rc = YCRDT_E_DECODE;
+      err = "Integer out of range! (malformed update " + std::to_string(i) + ")";
+      break;
+    }
+    enqueue(d, ups[i].ptr, ups[i].len, false);
+  }
+  std::sort(touched.begin(), touched.end());
+  touched.erase(std::unique(touched.begin(), touched.end()), touched.end());
+  const int frc = flush_multi(e, touched);
+  if (rc) return fail(rc, err);
+  return frc;
+}
 
 int ycrdt_doc_flush(ycrdt_doc* d) {
   if (!d) return fail(YCRDT_E_ARG, "null doc");
@@ -1552,6 +1773,7 @@ void ycrdt_batch_destroy(ycrdt_batch* b) {
   hipSetDevice(b->e->device);
   if (b->e->ws_owner == b) b->e->ws_owner = nullptr;
   if (b->bytes.p) hipFree(b->bytes.p);
+  if (b->pieces.p) hipFree(b->pieces.p);
   if (b->meta.p) hipFree(b->meta.p);
   delete b;
 }

@@ -287,6 +287,7 @@ __global__ __launch_bounds__(256) void k_seg_props(Work w, uint32_t nsegs) {
   w.g_oseg[s] = (!gc && origin != NONE) ? link : NONE;  // link = the origin's segment here
   if (gc) sf |= SEG_GC | SEG_DEL;
   else sf |= SEG_ITEM;
+  if (!gc && expl && origin != NONE && w.s_ocidx[own] < NONE - 1 && cidx < w.s_ocidx[own]) sf |= SEG_OLOW;
   w.g_cidx[s] = cidx;
   w.g_src[s] = own;
   w.g_flags[s] = sf;
@@ -357,14 +358,15 @@ uint32_t run_key_resolution(const Work& w, uint32_t nsegs, hipStream_t s) {
 }
 
 // --------------------------------------------------------------------------- map winner
-// Per YMap entry: max-client child of its origin (the winner descent) and min-client child of its
-// origin unit (YATA puts it right after the origin: merge adjacency). Segments are numbered in
-// (client index, clock) order, so the max child is the max segment (a u32 atomicMax of s + 1; u64
-// atomics issue at well under half the rate) and the min child the min client index. Both are
-// fire-and-forget device-scope atomics: they execute at the memory side and the lane never waits,
-// whereas reading the slot first to skip a useless atomic is a dependent random load that costs
-// more than the atomic it saves (measured on the 112-document C2 batch: 26 ms read-then-atomic vs
-// 13.6 ms plain atomics for this phase).
+// Per YMap entry: the max-client child of its origin (the winner descent: YATA orders siblings by
+// client, Item.integrate Y@77594) and whether its origin unit has a child of a lower client than
+// the unit's own (then the origin's own-client successor is not adjacent to it: no merge).
+// Segments are numbered in (client index, clock) order, so the max child is the max segment: a
+// fire-and-forget u32 atomicMax of s + 1 (u64 atomics issue at well under half the rate; reading
+// the slot first to skip a useless atomic is a dependent random load that costs more than the
+// atomic: 26 ms vs 13.6 ms measured on the 112-document C2 batch). The adjacency test needs no
+// minimum at all: a lower-client child only marks its origin (idempotent plain store), and most
+// children never store (C2: replicas above the base client, chains within one client).
 __global__ __launch_bounds__(256) void k_children(Work w, uint32_t nsegs) {
   const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
   if (s >= nsegs) return;
@@ -373,7 +375,7 @@ __global__ __launch_bounds__(256) void k_children(Work w, uint32_t nsegs) {
   const uint32_t os = w.g_oseg[s];
   if (os != NONE) {
     atomicMax(&w.g_maxchild[os], s + 1);
-    atomicMin(&w.u_minchild[w.g_origin[s]], w.g_cidx[s]);
+    if (f & SEG_OLOW) w.u_minchild[w.g_origin[s]] = 0u;
   } else if (f & SEG_ROOT) {
     atomicMax(&w.k_rootmax[w.g_key[s]], s + 1);
   }
@@ -476,7 +478,7 @@ __global__ __launch_bounds__(256) void k_merge_flags(Work w, uint32_t nsegs) {
       if (!(fr & SEG_ITEM)) merge = true;  // GC + GC
       else if ((fl & SEG_DEL) == (fr & SEG_DEL) && w.g_origin[s] == gs - 1 && w.g_rorigin[s - 1] == w.g_rorigin[s] &&
                (fl & (SEG_ARRAY | SEG_PSUB)) == (fr & (SEG_ARRAY | SEG_PSUB)) &&
-               ((fr & SEG_ARRAY) ? w.g_right[s - 1] == s : w.u_minchild[gs - 1] >= w.g_cidx[s])) {
+               ((fr & SEG_ARRAY) ? w.g_right[s - 1] == s : w.u_minchild[gs - 1] != 0u)) {
         if (fr & SEG_DEL) merge = true;  // both become ContentDeleted after GC
         else {
           const uint32_t rl = w.s_info[w.g_src[s - 1]] & 31u, rr = w.s_info[w.g_src[s]] & 31u;

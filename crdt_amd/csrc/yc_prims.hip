@@ -89,4 +89,22 @@ void scan_segmax_u64(void* tmp, size_t tmpb, const uint64_t* in, uint64_t* out, 
   rocprim::inclusive_scan(tmp, tmpb, in, out, (size_t)n, SegMax64(), s);
 }
 
+// Byte pieces (device -> device, or a few inline bytes) in one launch: one wavefront per piece.
+// Doc states are gathered into a multi-document batch and a multi-document result is split back
+// into the documents' arena blocks this way (ycrdt_apply_updates_multi), instead of one
+// hipMemcpyAsync per document.
+__global__ __launch_bounds__(256) void k_copy_pieces(const Piece* __restrict__ pieces, uint32_t n) {
+  const uint32_t i = (blockIdx.x * blockDim.x + threadIdx.x) >> 6, lane = threadIdx.x & 63;
+  if (i >= n) return;
+  const Piece P = pieces[i];
+  if (!P.src) {
+    if (lane < P.len) P.dst[lane] = P.inl[lane];
+    return;
+  }
+  for (uint32_t k = lane; k < P.len; k += 64) P.dst[k] = P.src[k];
+}
+void copy_pieces(const Piece* pieces, uint32_t n, hipStream_t s) {
+  if (n) hipLaunchKernelGGL(k_copy_pieces, dim3((n + 3) / 4), dim3(256), 0, s, pieces, n);
+}
+
 }  // namespace yc

@@ -137,7 +137,7 @@ struct Work {
   // ---- per unit (U)
   uint32_t* u_owner = nullptr;
   uint32_t* u_flags = nullptr;
-  uint32_t* u_minchild = nullptr;
+  uint32_t* u_minchild = nullptr;  // 0 = some YMap child of this unit has a lower client than the unit (merge blocked)
   uint64_t* u_cutbits = nullptr;   // [U/64+1]
   uint32_t* u_wpre = nullptr;      // [U/64+2] popcount prefix of u_cutbits words
   // ---- per segment (NS <= U)
@@ -368,6 +368,8 @@ enum : uint32_t {
   SEG_ITEM = 32u,
   SEG_ARRAY = 64u,     // member of a YArray list (no parentSub)
   SEG_PSUB = 128u,     // member of a YMap entry list (parentSub)
+  SEG_OLOW = 256u,     // its client index is below its origin's (a YATA sibling placed before the
+                       // origin's own-client successor: that successor cannot merge, k_children)
 };
 // key flags
 enum : uint32_t {
@@ -430,6 +432,16 @@ size_t prim_tmp_bytes(uint64_t max_items);
 void scan_u32(void* tmp, size_t tmpb, const uint32_t* in, uint32_t* out, uint64_t n, hipStream_t s);          // exclusive
 void scan_u32_to_u64(void* tmp, size_t tmpb, const uint32_t* in, uint64_t* out, uint64_t n, hipStream_t s);   // exclusive
 void sort_u32(void* tmp, size_t tmpb, const uint32_t* in, uint32_t* out, uint64_t n, hipStream_t s);
+// device byte pieces: copy `len` bytes src -> dst, or (src == nullptr) write inl[0..len) (len <= 8)
+struct Piece {
+  const uint8_t* src;
+  uint8_t* dst;
+  uint32_t len;
+  uint8_t inl[8];
+};
+void copy_pieces(const Piece* pieces, uint32_t n, hipStream_t s);
+// per-document (lo, hi, n) of the struct / delete-set / state-vector sections of a multi-document encode
+void launch_doc_ranges(const Work& w, uint32_t nclients, uint32_t ndocs, uint32_t* rng, hipStream_t s);
 // batched u32 fills (n in 32-bit words)
 struct FillDesc { uint32_t* p; uint64_t n; uint32_t v; };
 constexpr uint32_t FILL_MAX = 8;

@@ -79,6 +79,14 @@ int ycrdt_apply_update(ycrdt_doc *d, ycrdt_buf update);
 /* n sequential Y.applyUpdate calls (LevelDB replay crdt.js:79-98, ingest); stops at the first
  * malformed update, as a loop of Y.applyUpdate would. */
 int ycrdt_apply_updates(ycrdt_doc *d, const ycrdt_buf *ups, size_t n);
+/* Fleet ingest (crdt.js:235 one doc per topic, crdt.js:294 onData per message):
+ * Y.applyUpdate(docs[i], ups[i]) for i = 0..n-1, validated as ycrdt_apply_updates, then merged in
+ * this call — ONE device pass for every document that has nothing pending (multi-document batch,
+ * results split back into each document's HBM state on the device). Documents with pending
+ * structs / delete ranges, or an engine with compat 135, take their own flush. All documents must
+ * belong to `e`. A malformed update i: updates before it are applied (and merged), then
+ * YCRDT_E_DECODE. */
+int ycrdt_apply_updates_multi(ycrdt_engine *e, ycrdt_doc *const *docs, const ycrdt_buf *ups, size_t n);
 /* Runs the deferred applies now (every read does this implicitly). */
 int ycrdt_doc_flush(ycrdt_doc *d);
 /* Whether Yjs would hold pending structs (store.pendingStructs) / a pending delete set

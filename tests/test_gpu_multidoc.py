@@ -53,3 +53,88 @@ def test_multidoc_shared_clients_and_batch_api():
     assert st.items == sum(crdt_amd.Batch(d).merge().items for d in docs)
     with pytest.raises(crdt_amd.YcrdtError):  # other merges ran since: the workspace is not mb's any more
         mb.result_docs()
+
+
+# ---------------------------------------------------------------- fleet ingest (apply_updates_multi)
+def _interleaved(cases, rng):
+    """(doc index, update) pairs of every case, interleaved across documents, per-doc order kept."""
+    queues = [[bytes.fromhex(u) for u in c["updates"]] for c in cases]
+    pos = [0] * len(queues)
+    out = []
+    live = [i for i, q in enumerate(queues) if q]
+    while live:
+        i = rng.choice(live)
+        out.append((i, queues[i][pos[i]]))
+        pos[i] += 1
+        if pos[i] == len(queues[i]):
+            live.remove(i)
+    return out
+
+
+def test_apply_multi_golden_fleet(golden):
+    """Every golden case is one document; all their updates arrive interleaved in ONE call."""
+    cases = [c for s in ("kat", "map", "array", "nested") for c in golden[s]]
+    docs = [crdt_amd.Doc(client_id=0x7FFFFFF0) for _ in cases]
+    pairs = _interleaved(cases, random.Random(3))
+    crdt_amd.apply_updates_multi([docs[i] for i, _ in pairs], [u for _, u in pairs])
+    for c, d in zip(cases, docs):
+        assert d.encode_state_as_update().hex() == c["state"], c["name"]
+        assert d.encode_state_vector().hex() == c["sv"], c["name"]
+        for name, kind in c["roots"].items():
+            assert json.loads(d.root_json(name, kind)) == c["json"][name], c["name"]
+
+
+def test_apply_multi_in_rounds_and_reads_between(golden):
+    """Several ingest calls on the same fleet, reads and local ops in between (state stays in HBM)."""
+    cases = [c for s in ("map", "nested") for c in golden[s]][:30]
+    docs = [crdt_amd.Doc(client_id=0x7FFFFFF0) for _ in cases]
+    pairs = _interleaved(cases, random.Random(5))
+    k = len(pairs) // 3
+    for part in (pairs[:k], pairs[k:2 * k], pairs[2 * k:]):
+        crdt_amd.apply_updates_multi([docs[i] for i, _ in part], [u for _, u in part])
+        for d in docs[::7]:
+            d.encode_state_vector()
+    for c, d in zip(cases, docs):
+        assert d.encode_state_as_update().hex() == c["state"], c["name"]
+
+
+def test_apply_multi_pending_docs_fall_back():
+    """Out-of-order deltas (Yjs pending structs) in the fleet: each such document takes its own
+    pending emulation, the others still merge together; every read equals Yjs's after the batch."""
+    with open(os.path.join(ROOT, "tests", "golden", "pending.json")) as f:
+        cases = json.load(f)["cases"][:24]
+    docs = [crdt_amd.Doc(client_id=0x7FFFFFF0) for _ in cases]
+    pairs = _interleaved(cases, random.Random(9))
+    crdt_amd.apply_updates_multi([docs[i] for i, _ in pairs], [u for _, u in pairs])
+    for c, d in zip(cases, docs):
+        st = c["steps"][-1]
+        assert d.pending() == (st["pending"], st["pending_ds"]), c["name"]
+        assert d.encode_state_as_update().hex() == st["state"], c["name"]
+
+
+def test_apply_multi_c5_fleet_large():
+    """A C5-shaped fleet: 20k documents of 2-3 small replica updates each, one ingest call."""
+    from crdt_amd.workload import gen_map
+
+    base = [gen_map(n_keys=20, n_replicas=2 + s % 2, ops_per_replica=4, seed=700 + s)[0] for s in range(50)]
+    n_docs = 20000
+    fleet = [base[i % len(base)] for i in range(n_docs)]
+    docs = [crdt_amd.Doc(client_id=0x7FFFFFF0) for _ in range(n_docs)]
+    idx, ups = [], []
+    for i, us in enumerate(fleet):
+        for u in us:
+            idx.append(i)
+            ups.append(u)
+    crdt_amd.apply_updates_multi([docs[i] for i in idx], ups)
+    want = crdt_amd.merge_docs(base)
+    for i in range(0, n_docs, 997):
+        assert (docs[i].encode_state_as_update(), docs[i].encode_state_vector()) == want[i % len(base)], i
+
+
+def test_apply_multi_malformed_applies_prefix(golden):
+    c = golden["map"][0]
+    ups = [bytes.fromhex(u) for u in c["updates"]]
+    d1, d2 = crdt_amd.Doc(client_id=1), crdt_amd.Doc(client_id=2)
+    with pytest.raises(crdt_amd.YcrdtError):
+        crdt_amd.apply_updates_multi([d1] * len(ups) + [d2], ups + [b"\x05\x01"])
+    assert d1.encode_state_as_update().hex() == c["state"]
