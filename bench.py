@@ -51,6 +51,7 @@ def parse():
     p.add_argument("--port-replicas", type=int, default=1000, help="replicas in the oracle-port timing sample")
     p.add_argument("--profile-phases", action="store_true")
     p.add_argument("--no-per-op", action="store_true", help="skip the crdt.js per-op leg")
+    p.add_argument("--fleet-docs", type=int, default=100_000, help="documents in the C5 fleet-ingest leg (0 = skip)")
     p.add_argument("--only-headline", action="store_true",
                    help="time the headline merge only (no side legs): rocprof averages then match the bench line")
     p.add_argument("--c3-items", type=int, default=10_000_000,
@@ -325,6 +326,83 @@ def c3_leg(eng, n_items, steps=3):
     return res
 
 
+def fleet_ingest_leg(eng, n_docs):
+    """C5 fleet ingest (crdt.js:235 one Y.Doc per topic, crdt.js:294 Y.applyUpdate per message):
+    n_docs documents, each receiving the replica updates of one of the C5 fixtures (Yjs-generated,
+    tests/golden/configs.json, cycled), all applied with ONE ycrdt_apply_updates_multi call (host
+    buffers in, one device pass, every document's state left in HBM). Parity: every document's
+    encodeStateAsUpdate / encodeStateVector equals the fixture's Yjs state. Beside it: Yjs 13.5.16
+    in Node, worker_threads on W cores (each worker applies and encodes its share of the documents),
+    final states compared (sha256 over the canonical states in document order)."""
+    import hashlib
+
+    import crdt_amd
+
+    with open(os.path.join(ROOT, "tests", "golden", "configs.json")) as f:
+        cases = [c for c in json.load(f)["cases"] if c["name"].startswith("c5_")]
+    base = [[bytes.fromhex(u) for u in c["updates"]] for c in cases]
+    idx, ups = [], []
+    for d in range(n_docs):
+        for u in base[d % len(base)]:
+            idx.append(d)
+            ups.append(u)
+    in_bytes = sum(len(u) for u in ups)
+    reps, ms = 2, []
+    docs = None
+    for _ in range(reps):
+        docs = [crdt_amd.Doc(client_id=0x7FFFFFF0, engine=eng) for _ in range(n_docs)]
+        t0 = time.perf_counter()
+        crdt_amd.apply_updates_multi([docs[i] for i in idx], ups, engine=eng)
+        ms.append((time.perf_counter() - t0) * 1e3)
+    gpu_ms = min(ms)
+    parity = True
+    h = hashlib.sha256()
+    from tests.v1util import canonical_update
+    for d in range(n_docs):
+        c = cases[d % len(cases)]
+        st = docs[d].encode_state_as_update()
+        h.update(hashlib.sha256(canonical_update(st)).digest())
+        if d < len(cases) or d % 4099 == 0:
+            parity = parity and st.hex() == c["state"] and docs[d].encode_state_vector().hex() == c["sv"]
+    res = {"docs": n_docs, "updates": len(ups), "in_bytes": in_bytes, "ms": round(gpu_ms, 2),
+           "docs_per_s": round(n_docs / (gpu_ms * 1e-3), 1), "updates_per_s": round(len(ups) / (gpu_ms * 1e-3), 1),
+           "calls": 1, "parity": parity,
+           "includes": "ctypes + host validation + H2D + one multi-document merge + per-document split in HBM, 1 GPU"}
+    y = _yjs_fleet(idx, ups, n_docs)
+    if y:
+        res["yjs"] = {"docs_per_s": round(n_docs / (y["ms"] * 1e-3), 1), "workers": y["workers"], "kind": "reference",
+                      "cores": y["workers"], "ms": round(y["ms"], 2), "parity": y["state_sha256"] == h.hexdigest(),
+                      "sample": f"Yjs {y['yjs']} in Node {y['node']}, worker_threads W={y['workers']} (os.cpus() = "
+                                f"{y['cpus']}, capped at the box's CPU share), each: new Y.Doc + Y.applyUpdate per "
+                                "update + Y.encodeStateAsUpdate per document"}
+    del docs
+    return res
+
+
+def _yjs_fleet(idx, ups, n_docs, timeout=400):
+    import shutil
+    import struct
+    import subprocess
+    import tempfile
+
+    node = shutil.which("node")
+    if not node:
+        return None
+    with tempfile.NamedTemporaryFile(suffix=".bin", delete=False) as f:
+        f.write(struct.pack("<I", len(ups)))
+        for d, u in zip(idx, ups):
+            f.write(struct.pack("<II", d, len(u)) + u)
+        fname = f.name
+    try:
+        w = str(int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1))
+        r = subprocess.run([node, os.path.join(ROOT, "scripts", "yjs_baseline.js"), fname, "fleet", w, str(n_docs)],
+                           capture_output=True, text=True, timeout=timeout)
+        y = json.loads(r.stdout.strip().splitlines()[-1]) if r.returncode == 0 and r.stdout.strip() else None
+    finally:
+        os.unlink(fname)
+    return y if y and y.get("available") else None
+
+
 def fleet_sync_leg(eng, n_pairs):
     """Batched sync responder: n_pairs (doc state, lagging
     peer state vector) pairs from the reduced C5 fixtures (60 docs of 2-4 clients, Yjs-generated),
@@ -539,6 +617,9 @@ def main():
     fleet = None
     if rank == 0 and world == 1 and args.fleet_pairs > 0 and not args.only_headline:
         fleet = fleet_sync_leg(eng, args.fleet_pairs)
+    ingest = None
+    if rank == 0 and world == 1 and args.fleet_docs > 0 and not args.only_headline:
+        ingest = fleet_ingest_leg(eng, args.fleet_docs)
     side = rank == 0 and world == 1 and not args.only_headline
     loop = apply_loop_leg(eng, updates, out_update) if side else None
     per_op = per_op_leg(eng) if side and not args.no_per_op else None
@@ -583,6 +664,7 @@ def main():
         "roofline": roofline,
         "cpu_baseline": cpu,
         "fleet_sync": fleet,
+        "fleet_ingest": ingest,
         "apply_loop": loop,
         "per_op": per_op,
         "c3": c3,

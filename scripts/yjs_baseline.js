@@ -9,6 +9,7 @@
 // Usage: node yjs_baseline.js <batch file> [workers]
 //        node yjs_baseline.js <pairs file> diff   (update, state vector) alternating: Y.diffUpdate each
 //        node yjs_baseline.js <n ops> perop       crdt.js per-op path (bench.py per_op_leg)
+//        node yjs_baseline.js <fleet file> fleet W nDocs   C5 fleet ingest on W worker_threads
 //   batch file = u32le count, then per update u32le length + bytes (bench.py writes it)
 // Single-doc workloads run on ONE core (Yjs integrates a doc on one thread; SURVEY.md §8(d)):
 // `for u of batch: Y.applyUpdate(doc, u)` then `Y.encodeStateAsUpdate(doc)`, timed with
@@ -60,6 +61,26 @@ if (isMainThread) {
   if (!Y) {
     console.log(JSON.stringify({ available: false, reason: 'Yjs bundle not found on this machine' }));
     process.exit(0);
+  }
+  if (process.argv[3] === 'fleet') {  // C5 fleet ingest: (doc, update) pairs, W worker_threads
+    const W = Math.max(1, parseInt(process.argv[4] || '1', 10));
+    const nDocs = parseInt(process.argv[5], 10);
+    let done = 0, maxMs = 0;
+    const hashes = new Array(W);
+    for (let w = 0; w < W; w++) {
+      const wk = new Worker(__filename, { workerData: { fleet: file, w, W, nDocs } });
+      wk.on('message', (m) => {
+        hashes[w] = m.states;
+        maxMs = Math.max(maxMs, m.ms);
+        if (++done === W) {
+          const h = crypto.createHash('sha256');
+          for (let d = 0; d < nDocs; d++) h.update(Buffer.from(hashes[d % W][Math.floor(d / W)], 'hex'));
+          console.log(JSON.stringify({ available: true, yjs: '13.5.16', lib0: '0.2.42', node: process.version,
+            workers: W, cpus: require('os').cpus().length, ms: maxMs, state_sha256: h.digest('hex') }));
+        }
+      });
+    }
+    return;
   }
   if (process.argv[3] === 'perop') {  // crdt.js per-op path: A set/delete + full encode, B apply + toJSON
     const { canonicalUpdate } = require(path.join(__dirname, '..', 'tests', 'golden', 'gen', 'v1.js'));
@@ -119,6 +140,33 @@ if (isMainThread) {
       });
     }
   }
+} else if (workerData.fleet) {  // fleet worker: documents d with d % W == w
+  const Y = load();
+  const { canonicalUpdate } = require(path.join(__dirname, '..', 'tests', 'golden', 'gen', 'v1.js'));
+  const b = fs.readFileSync(workerData.fleet);
+  const n = b.readUInt32LE(0);
+  const { w, W, nDocs } = workerData;
+  const docs = new Map();
+  let p = 4;
+  const mine = [];
+  for (let i = 0; i < n; i++) {
+    const d = b.readUInt32LE(p), len = b.readUInt32LE(p + 4);
+    if (d % W === w) mine.push([d, new Uint8Array(b.buffer, b.byteOffset + p + 8, len)]);
+    p += 8 + len;
+  }
+  const t0 = process.hrtime.bigint();  // the worker's own work: applies + encodes (load / parse excluded)
+  for (const [d, u] of mine) {
+    let doc = docs.get(d);
+    if (!doc) { doc = new Y.Doc(); doc.clientID = 0x7ffffff0; docs.set(d, doc); }
+    Y.applyUpdate(doc, u);
+  }
+  const states = [];
+  for (let d = w; d < nDocs; d += W) {
+    const doc = docs.get(d) || new Y.Doc();
+    states.push(Y.encodeStateAsUpdate(doc));
+  }
+  const ms = Number(process.hrtime.bigint() - t0) / 1e6;
+  parentPort.postMessage({ ms, states: states.map((st) => crypto.createHash('sha256').update(canonicalUpdate(st)).digest('hex')) });
 } else {
   const Y = load();
   const r = runOnce(Y, readBatch(workerData.file));
