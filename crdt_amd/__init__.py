@@ -85,6 +85,8 @@ EXPORTS = (
     "ycrdt_doc_flush", "ycrdt_doc_pending", "ycrdt_doc_track_local", "ycrdt_validate_update", "ycrdt_debug_replay",
     "ycrdt_batch_stage_docs", "ycrdt_batch_result_docs", "ycrdt_merge_docs",
     "ycrdt_map_get", "ycrdt_map_size", "ycrdt_array_length", "ycrdt_array_get", "ycrdt_apply_updates_multi",
+    "ycrdt_comm_unique_id", "ycrdt_comm_create", "ycrdt_comm_destroy", "ycrdt_batch_merge_sharded",
+    "ycrdt_comm_sv_allreduce_max", "ycrdt_comm_ds_allgather",
 )
 
 MERGE_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p)
@@ -140,6 +142,12 @@ def lib():
     L.ycrdt_doc_client_id.argtypes = [vp, P(u32)]
     L.ycrdt_map_get.argtypes = [vp, cs, cs, cs, P(i32), P(_Out)]
     L.ycrdt_apply_updates_multi.argtypes = [vp, P(vp), P(_Buf), sz]
+    L.ycrdt_comm_unique_id.argtypes = [ctypes.c_char_p]
+    L.ycrdt_comm_create.argtypes = [vp, i32, i32, ctypes.c_char_p, P(vp)]
+    L.ycrdt_comm_destroy.argtypes = [vp]
+    L.ycrdt_batch_merge_sharded.argtypes = [vp, vp, u32, P(MergeStats)]
+    L.ycrdt_comm_sv_allreduce_max.argtypes = [vp, vp, _Buf, P(_Out)]
+    L.ycrdt_comm_ds_allgather.argtypes = [vp, vp, _Buf, P(_Out)]
     L.ycrdt_map_size.argtypes = [vp, cs, cs, P(u32)]
     L.ycrdt_array_length.argtypes = [vp, cs, cs, P(ctypes.c_uint64)]
     L.ycrdt_array_get.argtypes = [vp, cs, cs, ctypes.c_uint64, P(i32), P(_Out)]
@@ -385,6 +393,13 @@ class Batch:
         _check(lib().ycrdt_batch_merge(self._h, ctypes.byref(st)))
         return st
 
+    def merge_sharded(self, nshards: int, comm: "Comm" = None) -> MergeStats:
+        """Key-hash sharded merge (C4): every logical shard on this GPU (comm None) or this rank's
+        shard with the flag words summed over RCCL. Same bytes as merge()."""
+        st = MergeStats()
+        _check(lib().ycrdt_batch_merge_sharded(self._h, comm._h if comm else None, nshards, ctypes.byref(st)))
+        return st
+
     def result(self):
         u, s = _Out(), _Out()
         _check(lib().ycrdt_batch_result(self._h, ctypes.byref(u), ctypes.byref(s)))
@@ -423,6 +438,45 @@ def encode_state_as_update(doc: Doc, sv: bytes = b"") -> bytes:
 
 def encode_state_vector(doc: Doc) -> bytes:
     return doc.encode_state_vector()
+
+
+class Comm:
+    """RCCL communicator inside libycrdt (one rank per GPU): Comm.unique_id() on rank 0, the bytes
+    handed to every rank by any channel, then Comm(engine, nranks, rank, uid) on each."""
+
+    @staticmethod
+    def unique_id() -> bytes:
+        buf = ctypes.create_string_buffer(128)
+        _check(lib().ycrdt_comm_unique_id(buf))
+        return buf.raw
+
+    def __init__(self, engine, nranks: int, rank: int, uid: bytes):
+        h = ctypes.c_void_p()
+        _check(lib().ycrdt_comm_create(engine._h, nranks, rank, bytes(uid), ctypes.byref(h)))
+        self._h, self.engine, self.nranks, self.rank = h, engine, nranks, rank
+
+    def close(self):
+        if getattr(self, "_h", None):
+            lib().ycrdt_comm_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def sv_allreduce_max(self, sv: bytes) -> bytes:
+        out = _Out()
+        b = bytes(sv)
+        _check(lib().ycrdt_comm_sv_allreduce_max(self._h, self.engine._h, _Buf(ctypes.cast(ctypes.c_char_p(b), ctypes.c_void_p), len(b)), ctypes.byref(out)))
+        return _take(out)
+
+    def ds_allgather(self, update: bytes) -> bytes:
+        out = _Out()
+        b = bytes(update)
+        _check(lib().ycrdt_comm_ds_allgather(self._h, self.engine._h, _Buf(ctypes.cast(ctypes.c_char_p(b), ctypes.c_void_p), len(b)), ctypes.byref(out)))
+        return _take(out)
 
 
 def apply_updates_multi(docs, updates, engine=None):

@@ -15,6 +15,7 @@
 #include "yc_work.h"
 #include "yc_host.h"
 #include "yc_ingest.h"
+#include "yc_comm.h"
 #include <thread>
 #include "../../include/ycrdt.h"
 
@@ -145,7 +146,7 @@ enum Buf {
   B_TPRV, B_TMPRV, B_TMTAIL, B_TTREP, B_TOTAIL,
   B_OFIRST, B_OCIDX, B_OSIZE, B_OPOS, B_RSEG, B_RLEN, B_RSIZE, B_RPOS, B_OUT, B_SVOUT,
   B_VKMAP, B_VKREP, B_VKEYS, B_VNKEYS, B_VPOS, B_VD0, B_VN0, B_VD1, B_VN1, B_VORDER, B_VSEGS,
-  B_SCRATCH2, B_TMP2, B_CAPS, B_CLKEY, B_CLKEY2, B_CLDOC, B_DSFA, B_EMIT, B_DOCRNG,
+  B_SCRATCH2, B_TMP2, B_CAPS, B_CLKEY, B_CLKEY2, B_CLDOC, B_DSFA, B_EMIT, B_DOCRNG, B_KSHARD, B_SOWNER, B_GFLAGS0, B_GFACC,
   B_COUNT
 };
 
@@ -635,8 +636,19 @@ int run_decode(ycrdt_engine* e, ycrdt_batch* b, bool lazy, Decoded& D, bool gene
 // The whole batched merge. `target` (optional) selects a delta encode against a state vector;
 // `caps` (optional) integrates every client only up to its cap (Yjs pending structs, yc_ingest.h).
 // `order` (compat 135): the doc store's client insertion order, the delete-set / state-vector order.
+// `sh`: key-hash shards of one document (all of them on this GPU, or this rank's over RCCL).
+struct ShardSpec {
+  uint32_t nshards = 1;
+  int32_t shard = -1;  // -1: every shard in turn (logical shards on one GPU)
+  ycrdt_comm* comm = nullptr;
+};
+int comm_allreduce_sum_u32(ycrdt_comm* c, uint32_t* buf, size_t n, hipStream_t s) {
+  std::string err;
+  if (yc::comm_allreduce_u32(c, buf, n, false, s, err)) return fail(YCRDT_E_DEVICE, err);
+  return YCRDT_OK;
+}
 int run_merge(ycrdt_engine* e, ycrdt_batch* b, const std::unordered_map<uint32_t, uint32_t>* target,
-              const ClockMap* caps = nullptr, const std::vector<uint32_t>* order = nullptr) {
+              const ClockMap* caps = nullptr, const std::vector<uint32_t>* order = nullptr, const ShardSpec* sh = nullptr) {
   Work& w = e->w;
   auto& V = e->bufs;
   bool ok = true;
@@ -788,27 +800,68 @@ int run_merge(ycrdt_engine* e, ycrdt_batch* b, const std::unordered_map<uint32_t
     launch_segment_props(w, nsegs, nclients, U, s);
     mark(e, "merge.keys");
     run_key_resolution(w, nsegs, s);
-    mark(e, "merge.winner");  // k_children alone (bench.py's roofline kernel)
-    launch_map_winner(w, nsegs, s);
-    mark(e, "merge.descent");
-    run_descent(w, nsegs, s);
-    mark(e, "merge.dead_types");
-    if (D.nested) run_dead_keys(w, nsegs, s);  // only lists under a parent item can die with it
-    mark(e, "merge.yata");
     uint32_t narray = 0;  // YArray members; only read when the decode saw a possible array root
     if (D.array_roots) {
       HIPCHK(hipMemcpyAsync(&narray, &w.ctr->narray, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
       HIPCHK(hipStreamSynchronize(s));
     }
-    e->nlists = launch_yata(w, nsegs, narray, nclients, s);
-    if (w.dbg && e->nlists) {
-      unsigned long long h[3];
-      HIPCHK(hipStreamSynchronize(s));
-      HIPCHK(hipMemcpy(h, w.dbg + (size_t)w.ngroups * 8 + (size_t)w.ngroups * (GROUP_BYTES / 4096) * 8, sizeof(h), hipMemcpyDeviceToHost));
-      fprintf(stderr, "[ycrdt] k_yata: %u lists, %llu integrations, %llu conflict-scan steps, %llu stack dives\n", e->nlists, h[0], h[1], h[2]);
+    // the integrate phases: once, or once per key-hash shard (sh: C4 sharding, §6 of DESIGN.md)
+    uint8_t* owner = nullptr;
+    uint32_t *gflags0 = nullptr, *acc = nullptr;
+    uint32_t first = 0, last = 1;
+    if (sh) {
+      uint32_t* key_shard = take<uint32_t>(V, B_KSHARD, w.cap_keys + 1, ok);
+      owner = take<uint8_t>(V, B_SOWNER, (size_t)nsegs + 16, ok);
+      gflags0 = take<uint32_t>(V, B_GFLAGS0, (size_t)nsegs + 1, ok);
+      acc = take<uint32_t>(V, B_GFACC, (size_t)nsegs + 1, ok);
+      if (!ok) return fail(YCRDT_E_DEVICE, "hipMalloc failed (shards)");
+      mark(e, "shard.owners");
+      launch_key_shards(w, nsegs, sh->nshards, key_shard, owner, s);
+      HIPCHK(hipMemcpyAsync(gflags0, w.g_flags, sizeof(uint32_t) * nsegs, hipMemcpyDeviceToDevice, s));
+      HIPCHK(hipMemsetAsync(acc, 0, sizeof(uint32_t) * (nsegs + 1), s));
+      first = sh->shard < 0 ? 0u : (uint32_t)sh->shard;
+      last = sh->shard < 0 ? sh->nshards : first + 1;
     }
-    mark(e, "merge.merge_flags");
-    launch_merge_flags(w, nsegs, s);
+    for (uint32_t shard = first; shard < last; ++shard) {
+      if (sh) {
+        if (shard != first) {  // a logical shard after the first: the pristine flags, fresh winner slots
+          HIPCHK(hipMemcpyAsync(w.g_flags, gflags0, sizeof(uint32_t) * nsegs, hipMemcpyDeviceToDevice, s));
+          fill_u32_multi({{w.g_maxchild, (uint64_t)nsegs, 0u}, {w.k_rootmax, (uint64_t)w.cap_keys, 0u}}, s);
+        }
+        launch_shard_mask(w, nsegs, owner, shard, s);
+      }
+      mark(e, "merge.winner");  // k_children alone (bench.py's roofline kernel)
+      launch_map_winner(w, nsegs, s);
+      mark(e, "merge.descent");
+      run_descent(w, nsegs, s);
+      mark(e, "merge.dead_types");
+      if (D.nested) run_dead_keys(w, nsegs, s);  // only lists under a parent item can die with it
+      mark(e, "merge.yata");
+      e->nlists = launch_yata(w, nsegs, narray, nclients, s);
+      if (w.dbg && e->nlists) {
+        unsigned long long h[3];
+        HIPCHK(hipStreamSynchronize(s));
+        HIPCHK(hipMemcpy(h, w.dbg + (size_t)w.ngroups * 8 + (size_t)w.ngroups * (GROUP_BYTES / 4096) * 8, sizeof(h), hipMemcpyDeviceToHost));
+        fprintf(stderr, "[ycrdt] k_yata: %u lists, %llu integrations, %llu conflict-scan steps, %llu stack dives\n", e->nlists, h[0], h[1], h[2]);
+      }
+      mark(e, "merge.merge_flags");
+      if (!sh) {
+        launch_merge_flags(w, nsegs, s);
+      } else {
+        launch_merge_flags_only(w, nsegs, s);
+        launch_shard_export(w, nsegs, owner, shard, acc, s);
+      }
+    }
+    if (sh) {  // combine: every segment's flags come from its owner (RCCL sum across GPUs)
+      mark(e, "shard.exchange");
+      if (sh->comm) {
+        const int rc2 = comm_allreduce_sum_u32(sh->comm, acc, nsegs, s);
+        if (rc2) return rc2;
+      }
+      HIPCHK(hipMemcpyAsync(w.g_flags, acc, sizeof(uint32_t) * nsegs, hipMemcpyDeviceToDevice, s));
+      launch_merge_final(w, nsegs, s);
+      e->nlists = 0;  // the view is not built from a sharded merge
+    }
   }
   // ---- K7 encode. Output bound: every output struct adds at most 37 bytes of header (info,
   // origin, right origin, parent, length prefix) to content bytes sliced from the input, every
@@ -1690,6 +1743,73 @@ int ycrdt_batch_merge(ycrdt_batch* b, ycrdt_merge_stats* st) {
     if (st) *st = b->e->last;
   }
   return rc;
+}
+
+int ycrdt_comm_unique_id(uint8_t id[YCRDT_COMM_ID_BYTES]) {
+  if (!id) return fail(YCRDT_E_ARG, "null arg");
+  std::string err;
+  if (yc::comm_unique_id(id, err)) return fail(YCRDT_E_DEVICE, err);
+  return YCRDT_OK;
+}
+
+int ycrdt_comm_create(ycrdt_engine* e, int nranks, int rank, const uint8_t id[YCRDT_COMM_ID_BYTES], ycrdt_comm** out) {
+  if (!e || !id || !out) return fail(YCRDT_E_ARG, "null arg");
+  std::string err;
+  *out = yc::comm_create(e->device, nranks, rank, id, err);
+  if (!*out) return fail(YCRDT_E_DEVICE, err);
+  return YCRDT_OK;
+}
+
+void ycrdt_comm_destroy(ycrdt_comm* c) { yc::comm_destroy(c); }
+
+int ycrdt_batch_merge_sharded(ycrdt_batch* b, ycrdt_comm* comm, uint32_t nshards, ycrdt_merge_stats* st) {
+  if (!b || !nshards || nshards > 255) return fail(YCRDT_E_ARG, "bad batch / shard count (1..255)");
+  if (b->ndocs > 1) return fail(YCRDT_E_ARG, "sharded merge of a multi-document batch");
+  ShardSpec sh;
+  sh.nshards = nshards;
+  if (comm) {
+    if ((uint32_t)yc::comm_size(comm) != nshards) return fail(YCRDT_E_ARG, "nshards must equal the communicator size");
+    sh.shard = yc::comm_rank(comm);
+    sh.comm = comm;
+  }
+  HIPCHK(hipSetDevice(b->e->device));
+  int rc = run_merge(b->e, b, nullptr, nullptr, nullptr, &sh);
+  if (rc == YCRDT_OK) {
+    b->merged = true;
+    b->e->ws_owner = b;
+    if (st) *st = b->e->last;
+  }
+  return rc;
+}
+
+int ycrdt_comm_sv_allreduce_max(ycrdt_comm* c, ycrdt_engine* e, ycrdt_buf sv, ycrdt_out* out) {
+  if (!c || !e || !out || (sv.len && !sv.ptr)) return fail(YCRDT_E_ARG, "null arg");
+  out->ptr = nullptr;
+  out->len = 0;
+  HIPCHK(hipSetDevice(e->device));
+  std::string err;
+  std::vector<uint8_t> o;
+  const int r = yc::comm_sv_allreduce_max(c, sv.ptr, sv.len, e->stream, o, err);
+  if (r) return fail(r == -2 ? YCRDT_E_DECODE : YCRDT_E_DEVICE, err);
+  out->len = o.size();
+  out->ptr = (uint8_t*)malloc(o.size() ? o.size() : 1);
+  if (!out->ptr) { out->len = 0; return fail(YCRDT_E_CAPACITY, "host allocation failed"); }
+  memcpy(out->ptr, o.data(), o.size());
+  return YCRDT_OK;
+}
+
+int ycrdt_comm_ds_allgather(ycrdt_comm* c, ycrdt_engine* e, ycrdt_buf update, ycrdt_out* out) {
+  if (!c || !e || !out || (update.len && !update.ptr)) return fail(YCRDT_E_ARG, "null arg");
+  out->ptr = nullptr;
+  out->len = 0;
+  HIPCHK(hipSetDevice(e->device));
+  std::string err;
+  std::vector<std::vector<uint8_t>> parts;
+  if (yc::comm_allgather_updates(c, update.ptr, update.len, e->stream, parts, err)) return fail(YCRDT_E_DEVICE, err);
+  // the union: Y.mergeUpdates of the gathered updates on this engine (delete sets: sort + segmented max)
+  std::vector<ycrdt_buf> bufs;
+  for (const auto& p : parts) bufs.push_back(ycrdt_buf{p.data(), p.size()});
+  return ycrdt_merge_updates(e, bufs.data(), bufs.size(), out);
 }
 
 int ycrdt_batch_result(ycrdt_batch* b, ycrdt_out* update, ycrdt_out* sv) {

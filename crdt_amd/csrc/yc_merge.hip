@@ -497,6 +497,91 @@ __global__ void k_out_first(Work w, uint32_t nsegs) {
   if (s == nsegs - 1) w.o_first[w.g_outid[nsegs]] = nsegs;  // sentinel
 }
 
+// ---- key-hash sharding of one document (C4). Every list — a YMap entry, a
+// YArray — and every mergeWith adjacency lives inside ONE top-level entry of a root type (nested
+// lists hang below their parent item's entry), so the integrate phases (map winner, dead types,
+// YATA, item merge flags) are shard-local once each segment is owned by hash(top-level list) %
+// shards. A shard runs them with the other shards' segments masked out (no YMap / YArray role),
+// exports its own segments' final flags, and the flag words of all shards are summed (exactly one
+// owner per segment; RCCL all-reduce across GPUs). GC runs merge regardless of lists, so their
+// merge flags are settled afterwards on the combined flags (k_merge_final).
+__device__ __forceinline__ uint32_t shard_of_hash(uint64_t h, uint32_t n) {
+  h ^= h >> 33;
+  h *= 0xff51afd7ed558ccdull;
+  h ^= h >> 33;
+  return (uint32_t)(h % n);
+}
+__global__ void k_key_shard(Work w, uint32_t nshards, uint32_t* __restrict__ key_shard) {
+  const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= w.cap_keys) return;
+  if (w.k_hash[k] == 0) { key_shard[k] = 0; return; }
+  uint32_t x = k;  // climb to the top-level list: parent item -> the list that holds it
+  for (uint32_t depth = 0; depth < (1u << 20); ++depth) {
+    const uint32_t pu = w.k_parent[x];
+    if (pu == NONE) break;
+    const uint32_t pk = w.g_key[seg_of(w.u_cutbits, w.u_wpre, pu)];
+    if (pk == NONE || pk == x) break;
+    x = pk;
+  }
+  key_shard[k] = shard_of_hash(w.k_hash[x], nshards);
+}
+__global__ void k_seg_shard(Work w, uint32_t nsegs, const uint32_t* __restrict__ key_shard, uint8_t* __restrict__ owner) {
+  const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= nsegs) return;
+  const uint32_t key = w.g_key[s];
+  owner[s] = key == NONE ? 0 : (uint8_t)key_shard[key];  // keyless (GC) segments: shard 0
+}
+__global__ void k_shard_mask(Work w, uint32_t nsegs, const uint8_t* __restrict__ owner, uint32_t shard) {
+  const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= nsegs || owner[s] == shard) return;
+  w.g_flags[s] &= ~(SEG_PSUB | SEG_ARRAY | SEG_ROOT);
+}
+__global__ void k_shard_export(Work w, uint32_t nsegs, const uint8_t* __restrict__ owner, uint32_t shard, uint32_t* __restrict__ acc) {
+  const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= nsegs || owner[s] != shard) return;
+  acc[s] = w.g_flags[s];
+}
+__global__ void k_merge_final(Work w, uint32_t nsegs) {
+  const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
+  if (s > nsegs) return;
+  if (s == nsegs) { w.g_tmp[s] = 0; return; }
+  uint32_t f = w.g_flags[s];
+  if (!(f & SEG_ITEM)) {  // GC + GC merge (only the MERGE bit changes, so neighbours read ITEM safely)
+    const bool m = s > 0 && w.g_cidx[s - 1] == w.g_cidx[s] && !(w.g_flags[s - 1] & SEG_ITEM);
+    const uint32_t g = m ? (f | SEG_MERGE) : (f & ~SEG_MERGE);
+    if (g != f) w.g_flags[s] = g;
+    f = g;
+  }
+  w.g_tmp[s] = (f & SEG_MERGE) ? 0u : 1u;
+}
+void launch_key_shards(const Work& w, uint32_t nsegs, uint32_t nshards, uint32_t* key_shard, uint8_t* owner, hipStream_t s) {
+  hipLaunchKernelGGL(k_key_shard, dim3(w.cap_keys / 256 + 1), dim3(256), 0, s, w, nshards, key_shard);
+  if (nsegs) hipLaunchKernelGGL(k_seg_shard, dim3(nsegs / 256 + 1), dim3(256), 0, s, w, nsegs, key_shard, owner);
+}
+void launch_shard_mask(const Work& w, uint32_t nsegs, const uint8_t* owner, uint32_t shard, hipStream_t s) {
+  if (nsegs) hipLaunchKernelGGL(k_shard_mask, dim3(nsegs / 256 + 1), dim3(256), 0, s, w, nsegs, owner, shard);
+}
+void launch_shard_export(const Work& w, uint32_t nsegs, const uint8_t* owner, uint32_t shard, uint32_t* acc, hipStream_t s) {
+  if (nsegs) hipLaunchKernelGGL(k_shard_export, dim3(nsegs / 256 + 1), dim3(256), 0, s, w, nsegs, owner, shard, acc);
+}
+// the combined flags are in place: settle GC merges, then the output-struct numbering
+void launch_merge_final(const Work& w, uint32_t nsegs, hipStream_t s) {
+  if (!nsegs) return;
+  hipLaunchKernelGGL(k_merge_final, dim3(nsegs / 256 + 1), dim3(256), 0, s, w, nsegs);
+  launch_merge_tail(w, nsegs, s);
+}
+
+// the item-merge predicate only (a shard's part); launch_merge_tail numbers the output structs
+void launch_merge_flags_only(const Work& w, uint32_t nsegs, hipStream_t s) {
+  if (nsegs) hipLaunchKernelGGL(k_merge_flags, dim3(nsegs / 256 + 1), dim3(256), 0, s, w, nsegs);
+}
+void launch_merge_tail(const Work& w, uint32_t nsegs, hipStream_t s) {
+  if (!nsegs) return;
+  scan_u32(w.tmp, w.tmp_bytes, w.g_tmp, w.g_outid, nsegs + 1, s);
+  hipLaunchKernelGGL(k_out_first, dim3((nsegs + 255) / 256), dim3(256), 0, s, w, nsegs);
+  hipMemcpyAsync(&w.ctr->nout, w.g_outid + nsegs, sizeof(uint32_t), hipMemcpyDeviceToDevice, s);
+}
+
 void launch_merge_flags(const Work& w, uint32_t nsegs, hipStream_t s) {
   if (!nsegs) return;
   hipLaunchKernelGGL(k_merge_flags, dim3(nsegs / 256 + 1), dim3(256), 0, s, w, nsegs);

@@ -419,6 +419,13 @@ uint32_t run_key_resolution(const Work& w, uint32_t nsegs, hipStream_t s);
 void launch_map_winner(const Work& w, uint32_t nsegs, hipStream_t s);
 uint32_t run_descent(const Work& w, uint32_t nsegs, hipStream_t s);
 void launch_merge_flags(const Work& w, uint32_t nsegs, hipStream_t s);
+void launch_merge_flags_only(const Work& w, uint32_t nsegs, hipStream_t s);
+void launch_merge_tail(const Work& w, uint32_t nsegs, hipStream_t s);
+// key-hash shards of one document (yc_merge.hip)
+void launch_key_shards(const Work& w, uint32_t nsegs, uint32_t nshards, uint32_t* key_shard, uint8_t* owner, hipStream_t s);
+void launch_shard_mask(const Work& w, uint32_t nsegs, const uint8_t* owner, uint32_t shard, hipStream_t s);
+void launch_shard_export(const Work& w, uint32_t nsegs, const uint8_t* owner, uint32_t shard, uint32_t* acc, hipStream_t s);
+void launch_merge_final(const Work& w, uint32_t nsegs, hipStream_t s);
 void run_dead_keys(const Work& w, uint32_t nsegs, hipStream_t s);
 uint32_t launch_yata(const Work& w, uint32_t nsegs, uint32_t narray, uint32_t nclients, hipStream_t s);
 

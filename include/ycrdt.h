@@ -28,6 +28,8 @@ extern "C" {
 typedef struct ycrdt_engine ycrdt_engine;
 typedef struct ycrdt_doc ycrdt_doc;
 typedef struct ycrdt_batch ycrdt_batch;
+typedef struct ycrdt_comm ycrdt_comm; /* RCCL communicator (multi-GPU exchanges) */
+#define YCRDT_COMM_ID_BYTES 128
 
 typedef struct { const uint8_t *ptr; size_t len; } ycrdt_buf; /* borrowed */
 typedef struct { uint8_t *ptr; size_t len; } ycrdt_out;       /* library-owned */
@@ -196,6 +198,26 @@ int ycrdt_validate_update(ycrdt_buf update, int *structs_ok);
 typedef int (*ycrdt_merge_fn)(void *ctx, const ycrdt_buf *ups, size_t n, ycrdt_out *out);
 int ycrdt_debug_replay(const ycrdt_buf *ups, size_t n, ycrdt_merge_fn merge, void *ctx, ycrdt_out *sv,
                        ycrdt_out *pending, ycrdt_out *pending_ds);
+
+/* ---- multi-GPU: RCCL over xGMI inside the library, one rank per GPU.
+ * Rank 0 creates the unique id; the caller hands those bytes to every rank (any channel), then each
+ * rank creates its communicator on its engine's device. */
+int ycrdt_comm_unique_id(uint8_t id[YCRDT_COMM_ID_BYTES]);
+int ycrdt_comm_create(ycrdt_engine *e, int nranks, int rank, const uint8_t id[YCRDT_COMM_ID_BYTES], ycrdt_comm **out);
+void ycrdt_comm_destroy(ycrdt_comm *c);
+/* Key-hash sharded merge of ONE document (C4): every rank stages the same updates; the integrate
+ * phases (map winner, YATA, dead types, merge adjacency) run for the rank's shard only — lists
+ * owned by hash(top-level entry) % nshards — and the per-segment flag words are summed over RCCL;
+ * every rank then encodes the full result. comm == NULL: all nshards logical shards run in turn on
+ * this GPU (the partition check: byte-identical to ycrdt_batch_merge). Read the result with
+ * ycrdt_batch_result. */
+int ycrdt_batch_merge_sharded(ycrdt_batch *b, ycrdt_comm *comm, uint32_t nshards, ycrdt_merge_stats *st);
+/* State vector of the union of what the ranks hold of one document (crdt.js:239,289 exchange):
+ * all-gather + max per client, descending client order. */
+int ycrdt_comm_sv_allreduce_max(ycrdt_comm *c, ycrdt_engine *e, ycrdt_buf sv, ycrdt_out *out);
+/* Delete sets of all ranks (each a delete-set-only or full update) all-gathered and merged with the
+ * engine's HIP mergeUpdates (the delete-set union): every rank receives the same update. */
+int ycrdt_comm_ds_allgather(ycrdt_comm *c, ycrdt_engine *e, ycrdt_buf update, ycrdt_out *out);
 
 void ycrdt_free(ycrdt_out *o);
 const char *ycrdt_last_error(void);

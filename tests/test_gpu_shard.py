@@ -1,0 +1,110 @@
+"""Key-hash sharding of ONE document (config C4): the integrate phases run per shard
+(lists owned by hash(top-level entry) % shards, other shards' segments masked), the per-segment
+flag words are combined, and the encode runs on the combined flags. Every shard count must give
+the unsharded bytes — on the Yjs fixtures (golden sets, the C3 / C4 config cases) and on a C4-shaped
+history generated here (nested YArrays under YMap keys, overwrites that GC whole arrays, concurrent
+pushes / inserts / deletes). The RCCL path runs at world size 1 on the one-GPU box (the identity
+all-reduce); world-size-2 partition / exchange logic is covered on CPU by tests/test_shard_cpu.py."""
+import json
+import os
+import random
+
+import pytest
+
+crdt_amd = pytest.importorskip("crdt_amd")
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _merge(ups, nshards=None, comm=None):
+    b = crdt_amd.Batch(ups)
+    if nshards is None:
+        b.merge()
+    else:
+        b.merge_sharded(nshards, comm)
+    return b.result()
+
+
+def test_shards_golden_and_configs(golden):
+    with open(os.path.join(ROOT, "tests", "golden", "configs.json")) as f:
+        cfg = [c for c in json.load(f)["cases"] if not c["name"].startswith("c5_")]
+    cases = [c for s in ("kat", "map", "array", "nested") for c in golden[s]] + cfg
+    for c in cases:
+        ups = [bytes.fromhex(u) for u in c["updates"]]
+        for n in (1, 2, 3, 8):
+            st, sv = _merge(ups, n)
+            assert st.hex() == c["state"], (c["name"], n)
+            assert sv.hex() == c["sv"], (c["name"], n)
+
+
+def _any_int(v):
+    return bytes([125, v & 0x3F]) if 0 <= v < 64 else bytes([119, 1, 0x61 + v % 26])
+
+
+def c4_history(seed, n_rep=8, n_keys=24, rounds=4, ops=25):
+    """C4-shaped: replicas on YMap 'docs' whose keys hold nested YArrays; local ops through the
+    engine (byte-identical Yjs structs), deltas gossiped after every round."""
+    rng = random.Random(seed)
+    reps = [crdt_amd.Doc(client_id=1000 + 7 * i) for i in range(n_rep)]
+    for d in reps:
+        d.track_local(True)
+    log = []
+    for _ in range(rounds):
+        for d in reps:
+            for _ in range(ops):
+                key = "d%d" % rng.randrange(n_keys)
+                if d.map_type_at("docs", key) != 0 or rng.random() < 0.08:
+                    d.map_set_type("docs", key, 0)  # new (or overwriting) nested array
+                n = d.array_length("docs", parent_key=key)
+                x = rng.random()
+                if x < 0.6 or n == 0:
+                    d.array_insert("docs", rng.randrange(n + 1), [_any_int(rng.randrange(100)) for _ in range(1 + rng.randrange(3))], parent_key=key)
+                elif x < 0.85:
+                    d.array_insert("docs", n, [_any_int(rng.randrange(100))], parent_key=key)
+                else:
+                    i = rng.randrange(n)
+                    d.array_delete("docs", i, min(n - i, 1 + rng.randrange(2)), parent_key=key)
+        deltas = [d.take_local_update() for d in reps]
+        log += [u for u in deltas if u]
+        for i, d in enumerate(reps):
+            for j, u in enumerate(deltas):
+                if i != j and u and rng.random() < 0.7:
+                    d.apply_update(u)
+    return log
+
+
+@pytest.mark.parametrize("seed", [1, 2, 3])
+def test_shards_generated_c4(seed):
+    ups = c4_history(seed, n_rep=6 + 2 * seed, n_keys=16 * seed)
+    want = _merge(ups)
+    for n in (2, 5, 16):
+        assert _merge(ups, n) == want, n
+    random.Random(seed).shuffle(ups)
+    assert _merge(ups, 3) == want
+
+
+def test_shards_c2_generated():
+    from crdt_amd.workload import C2, gen_map
+
+    cfg = dict(C2)
+    cfg.update(n_keys=3000, n_replicas=60, ops_per_replica=200)
+    ups, _ = gen_map(**cfg)
+    want = _merge(ups)
+    assert _merge(ups, 4) == want
+
+
+def test_rccl_world1_exchanges(golden):
+    """The native RCCL path at world size 1: the sharded merge, the SV all-reduce and the DS
+    all-gather through libycrdt's communicator."""
+    eng = crdt_amd.default_engine()
+    comm = crdt_amd.Comm(eng, 1, 0, crdt_amd.Comm.unique_id())
+    try:
+        for c in golden["nested"][:20] + golden["array"][:10]:
+            ups = [bytes.fromhex(u) for u in c["updates"]]
+            assert _merge(ups, 1, comm) == (bytes.fromhex(c["state"]), bytes.fromhex(c["sv"])), c["name"]
+            assert comm.sv_allreduce_max(bytes.fromhex(c["sv_raw"])).hex() == c["sv"], c["name"]
+            st = bytes.fromhex(c["state"])
+            assert comm.ds_allgather(st) == st, c["name"]
+    finally:
+        comm.close()
