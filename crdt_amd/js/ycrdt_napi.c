@@ -39,7 +39,9 @@ static napi_value throw_rc(napi_env env, int rc) {
 
 static ycrdt_engine *engine(napi_env env) {
   if (!g_engine) {
-    int rc = ycrdt_engine_create(g_device, 136, &g_engine);
+    /* YCRDT_COMPAT=135: Yjs 13.5.16 client order in delete sets / state vectors (include/ycrdt.h) */
+    const char *cv = getenv("YCRDT_COMPAT");
+    int rc = ycrdt_engine_create(g_device, cv && atoi(cv) == 135 ? 135 : 136, &g_engine);
     if (rc != YCRDT_OK) {
       g_engine = NULL;
       throw_rc(env, rc);

@@ -5,6 +5,7 @@
 //   ops     — every Yjs 13.5.16 local-op script (tests/golden/ops.json) through the YMap / YArray
 //             facade crdt.js uses (getMap/getArray, set/delete, set(key, new Y.Array()), push /
 //             unshift / insert / delete, toJSON / toArray, observe), byte-identical after every step
+//   trace   — the crdt.js-driven Y call traces (tests/golden/crdtjs_traces.json), YCRDT_COMPAT=135
 'use strict';
 const fs = require('fs');
 const path = require('path');
@@ -78,6 +79,58 @@ if (mode === 'cpu') {
   }
   assert.ok(events > 0, 'YMap observers fired');
   console.log('napi ops ok:', n, 'scripts,', events, 'map events');
+} else if (mode === 'trace') {
+  // crdt.js-driven traces (tests/golden/crdtjs_traces.json, gen_crdtjs_traces.js): every Y call
+  // crdt.js made on every peer, replayed in order; every wire update / state vector byte-equal
+  // (run with YCRDT_COMPAT=135: Yjs 13.5.16's own bytes) and every toJSON / get / has deep-equal —
+  // the values crdt.c is built from (crdt.js:297-305, 372, 494, ...)
+  const cases = JSON.parse(fs.readFileSync(path.join(ROOT, 'tests', 'golden', 'crdtjs_traces.json'))).cases;
+  const norm = (v) => (v === undefined ? undefined : JSON.parse(JSON.stringify(v)));
+  const val = (r) => (r.undef ? undefined : r.v);
+  let nwire = 0, njson = 0, ncalls = 0;
+  for (const c of cases) {
+    const docs = {};
+    const typeOf = (ref) => {
+      const d = docs[ref.doc];
+      if (ref.key === undefined) return ref.kind === 'map' ? d.getMap(ref.root) : d.getArray(ref.root);
+      return d.getMap(ref.root).get(ref.key);
+    };
+    c.calls.forEach((x, i) => {
+      const tag = c.name + ' #' + i + ' ' + x.op;
+      const m = x.op.split('.')[1];
+      switch (x.op) {
+        case 'doc': docs[x.doc] = new Y.Doc({ clientID: x.client }); break;
+        case 'getMap': docs[x.doc].getMap(x.name); break;
+        case 'getArray': docs[x.doc].getArray(x.name); break;
+        case 'transact': case 'api': case 'crdt.c': break;  // execBatch's async callback: its ops follow on their own
+        case 'applyUpdate': Y.applyUpdate(docs[x.doc], unhex(x.update)); break;
+        case 'encodeStateAsUpdate':
+          assert.strictEqual(hex(Y.encodeStateAsUpdate(docs[x.doc], x.sv ? unhex(x.sv) : undefined)), x.result, tag);
+          nwire++;
+          break;
+        case 'encodeStateVector': assert.strictEqual(hex(Y.encodeStateVector(docs[x.doc])), x.result, tag); break;
+        case 'map.set': typeOf(x.ref).set(x.key, x.type ? new Y.Array() : val(x.value)); break;
+        case 'map.get': {
+          const r = typeOf(x.ref).get(x.key);
+          if (x.result.type) assert.ok(r instanceof Y.Array || r instanceof Y.Map, tag);
+          else assert.deepStrictEqual(norm(r), norm(val(x.result)), tag);
+          break;
+        }
+        case 'map.has': assert.strictEqual(typeOf(x.ref).has(...x.args), val(x.result), tag); break;
+        case 'map.toJSON': case 'array.toJSON': case 'array.toArray':
+          assert.deepStrictEqual(norm(typeOf(x.ref)[m]()), norm(val(x.result)), tag);
+          njson++;
+          break;
+        case 'map.delete': case 'array.push': case 'array.unshift': case 'array.insert': case 'array.delete':
+          typeOf(x.ref)[m](...x.args);
+          break;
+        case 'array.length': assert.strictEqual(typeOf(x.ref).length, x.result, tag); break;
+        default: throw new Error('unknown recorded call ' + x.op);
+      }
+      ncalls++;
+    });
+  }
+  console.log('napi trace ok:', cases.length, 'crdt.js scenarios,', ncalls, 'calls,', nwire, 'wire updates,', njson, 'toJSON');
 } else {
   let n = 0;
   const dsrc = [], dsv = [];

@@ -11,9 +11,9 @@ NODE = shutil.which("node")
 pytestmark = pytest.mark.skipif(NODE is None, reason="node not installed")
 
 
-def _run(mode, timeout):
+def _run(mode, timeout, env=None):
     r = subprocess.run([NODE, os.path.join(ROOT, "tests", "js", "napi_check.js"), mode], capture_output=True, text=True,
-                       timeout=timeout)
+                       timeout=timeout, env=dict(os.environ, **(env or {})))
     assert r.returncode == 0, r.stdout + r.stderr
     return r.stdout
 
@@ -39,3 +39,12 @@ def test_napi_golden_on_gpu():
 def test_napi_facade_ops_on_gpu():
     """The crdt.js-facing YMap / YArray facade replays every recorded Yjs op script byte-exactly."""
     assert "napi ops ok" in _run("ops", 300)
+
+
+@pytest.mark.gpu
+def test_napi_crdtjs_traces_on_gpu():
+    """crdt.js's own Y call sequence (recorded from crdt.js on a fake router, 2-4 peers, set / del /
+    push / insert / unshift / cut / execBatch): every wire update and state vector is Yjs 13.5.16's
+    raw bytes (compat 135) and every toJSON / get / has the same value (crdt.c, D1 / D7)."""
+    out = _run("trace", 600, {"YCRDT_COMPAT": "135"})
+    assert "napi trace ok" in out
