@@ -13,8 +13,8 @@
 // replays the call log through crdt_amd/js on the GPU and compares every result.
 //
 // crdt.js needs Node >= 14 (optional chaining, SURVEY D11); a lowered copy is written to a temp
-// directory with the five `?.` sites rewritten (exact text matches, or the script fails), next to a
-// stub `level` module (RAM mode: never called).
+// directory with the five `?.` sites rewritten (exact text matches, or the script fails), next to an
+// in-memory `level` module; two scenarios persist one peer in it and restart it (LevelDB replay).
 //
 // Usage: node gen_crdtjs_traces.js <out_dir>   → <out_dir>/crdtjs_traces.json
 'use strict';
@@ -44,8 +44,27 @@ function loweredCrdt() {
   if (src.includes('?.')) throw new Error('an optional chain is left');
   const dir = fs.mkdtempSync(path.join(os.tmpdir(), 'crdtjs-'));
   fs.mkdirSync(path.join(dir, 'node_modules', 'level'), { recursive: true });
-  fs.writeFileSync(path.join(dir, 'node_modules', 'level', 'index.js'),
-    "module.exports = () => { throw new Error('leveldb not used by the trace run'); };\n");
+  // in-memory LevelDB (SURVEY.md §4: get / batch / createReadStream({gt, lt}) / close, notFound
+  // errors flagged), shared across crdt.js restarts through a process-global map
+  fs.writeFileSync(path.join(dir, 'node_modules', 'level', 'index.js'), `
+const { EventEmitter } = require('events');
+const stores = global.__fakeLevel || (global.__fakeLevel = new Map());
+module.exports = function level(p) {
+  let m = stores.get(p);
+  if (!m) stores.set(p, (m = new Map()));
+  return {
+    async get(k) { if (!m.has(k)) { const e = new Error('NotFound: ' + k); e.notFound = true; throw e; } return m.get(k); },
+    async put(k, v) { m.set(k, Buffer.from(v)); },
+    async batch(ops) { for (const o of ops) { if (o.type === 'put') m.set(o.key, Buffer.from(o.value)); else m.delete(o.key); } },
+    createReadStream({ gt, lt }) {
+      const e = new EventEmitter();
+      setImmediate(() => { for (const k of [...m.keys()].sort()) if (k > gt && k < lt) e.emit('data', { key: k, value: m.get(k) }); e.emit('end'); });
+      return e;
+    },
+    async close() {},
+  };
+};
+`);
   fs.writeFileSync(path.join(dir, 'crdt.js'), src);
   return { dir, crdt: require(path.join(dir, 'crdt.js')) };
 }
@@ -167,15 +186,24 @@ function rng(seed) {
 
 const snap = (peer, api) => log.push({ op: 'crdt.c', peer, c: JSON.parse(JSON.stringify(api.c)) });
 
-// one scenario: `npeers` crdt.js instances on one topic, `nops` seeded API calls
-async function scenario(crdt, seed, npeers, nops) {
+// one scenario: `npeers` crdt.js instances on one topic, `nops` seeded API calls. With `persist`,
+// peer 0 stores every update in (fake) LevelDB (CRDTPersistence.storeUpdate validates it through two
+// scratch docs, crdt.js:30-75) and, after 2/3 of the ops, restarts from it: getYDoc replays every
+// stored update into a fresh doc (crdt.js:79-98) and the cache is rebuilt from the 'ix' map.
+async function scenario(crdt, seed, npeers, nops, persist = false) {
   const start = log.length;
   const bus = new Map();
   const g = rng(seed);
   const peers = [];
-  for (let i = 0; i < npeers; i++) peers.push(await crdt(makeRouter(bus, 'u' + i, 'pk' + i), { topic: 'trace' + seed }));
+  const opts = (i) => (persist && i === 0 ? { topic: 'trace' + seed, leveldb: 'lvl' + seed } : { topic: 'trace' + seed });
+  for (let i = 0; i < npeers; i++) peers.push(await crdt(makeRouter(bus, 'u' + i, 'pk' + i), opts(i)));
   const val = () => { const k = g.int(5); return k === 0 ? g.int(1000) : k === 1 ? 'v' + g.int(100) : k === 2 ? { n: g.int(9), s: 'x' } : k === 3 ? [g.int(5), 'y'] : g.r() < 0.5; };
   for (let i = 0; i < nops; i++) {
+    if (persist && i === Math.floor((2 * nops) / 3)) {  // restart peer 0 from its LevelDB
+      log.push({ op: 'api', peer: 0, n: i, restart: true });
+      peers[0] = await crdt(makeRouter(bus, 'u0', 'pk0'), opts(0));
+      snap(0, peers[0]);
+    }
     const p = g.int(npeers), api = peers[p];
     const x = g.r();
     log.push({ op: 'api', peer: p, n: i });
@@ -201,19 +229,22 @@ async function scenario(crdt, seed, npeers, nops) {
     await new Promise((res) => setImmediate(res));
     for (let q = 0; q < npeers; q++) snap(q, peers[q]);
   }
-  return { name: `crdtjs_s${seed}_p${npeers}_n${nops}`, peers: npeers, calls: log.slice(start) };
+  return { name: `crdtjs_s${seed}_p${npeers}_n${nops}` + (persist ? '_leveldb' : ''), peers: npeers, calls: log.slice(start) };
 }
 
 async function main() {
   const out = process.argv[2] || path.join(__dirname, '..');
-  const { crdt } = loweredCrdt();
+  const { dir, crdt } = loweredCrdt();
+  process.chdir(dir);  // CRDTPersistence mkdirs its storage path
+  let t = 1700000000000;
+  Date.now = () => t++;  // LevelDB keys carry Date.now(): distinct, ordered, reproducible
   const origLog = console.log;
   console.log = () => {};  // crdt.js logs every update
   const cases = [];
   try {
-    for (const [seed, np, n] of [[1, 2, 60], [2, 3, 80], [3, 2, 150], [4, 4, 60]]) {
+    for (const [seed, np, n, persist] of [[1, 2, 60], [2, 3, 80], [3, 2, 150], [4, 4, 60], [5, 2, 90, true], [6, 3, 60, true]]) {
       log.length = 0;
-      cases.push(await scenario(crdt, seed, np, n));
+      cases.push(await scenario(crdt, seed, np, n, persist));
     }
   } finally {
     console.log = origLog;
