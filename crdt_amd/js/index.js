@@ -8,7 +8,7 @@
 //   YMap set / get / has / delete / toJSON / observe / unobserve,
 //   YArray insert / push / unshift / delete / toJSON / toArray / length / observe / unobserve,
 //   Y.applyUpdate, Y.encodeStateAsUpdate(doc[, sv]), Y.encodeStateVector, Y.mergeUpdates,
-//   Y.diffUpdate, plus the batch entry Y.applyUpdates.
+//   Y.diffUpdate, plus the batch entries Y.applyUpdates (one doc) and Y.applyUpdatesMulti (a fleet).
 // Every local op is written by the engine as the Yjs v1 struct a Yjs doc would create, so the
 // doc's bytes stay identical to Yjs's (tests/js/napi_check.js `ops`). Values go through the
 // lib0 `any` codec (any.js). toJSON reads the device-materialised view (map winners, list order).
@@ -217,6 +217,12 @@ function applyUpdate(doc, update) {
   mutate(doc, () => binding.applyUpdates(doc._h, update));
 }
 
+// fleet ingest: Y.applyUpdate(docs[i], updates[i]) for every i, one device pass (not in Yjs)
+function applyUpdatesMulti(docs, updates) {
+  const before = docs.map((d) => snapshotObserved(d));
+  binding.applyUpdatesMulti(docs.map((d) => d._h), updates);
+  docs.forEach((d, i) => fireObservers(d, before[i], false));
+}
 function applyUpdates(doc, updates) {
   mutate(doc, () => binding.applyUpdates(doc._h, updates));
 }
@@ -236,6 +242,7 @@ module.exports = {
   AbstractType,
   applyUpdate,
   applyUpdates,
+  applyUpdatesMulti,
   encodeStateAsUpdate,
   encodeStateVector,
   mergeUpdates: (updates) => binding.mergeUpdates(updates),

@@ -166,6 +166,38 @@ static napi_value js_apply_updates(napi_env env, napi_callback_info info) {
 }
 
 /* encodeStateAsUpdate(doc[, sv])   (crdt.js:56,260,288,347,383,443,471,505,533,560,585,611) */
+/* applyUpdatesMulti(docs[], updates[]) — Y.applyUpdate(docs[i], updates[i]) for a fleet, merged in
+ * one device pass (ycrdt_apply_updates_multi; crdt.js:235 one doc per topic, :294 onData) */
+static napi_value js_apply_updates_multi(napi_env env, napi_callback_info info) {
+  size_t argc = 2;
+  napi_value argv[2];
+  CHECK(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+  bool a0 = false, a1 = false;
+  if (argc >= 2) { napi_is_array(env, argv[0], &a0); napi_is_array(env, argv[1], &a1); }
+  uint32_t n = 0, m = 0;
+  if (a0) napi_get_array_length(env, argv[0], &n);
+  if (a1) napi_get_array_length(env, argv[1], &m);
+  if (!a0 || !a1 || n != m) { napi_throw_type_error(env, NULL, "applyUpdatesMulti(docs[], updates[]) of equal length"); return NULL; }
+  ycrdt_engine *e = engine(env);
+  if (!e) return NULL;
+  ycrdt_doc **docs = (ycrdt_doc **)calloc(n ? n : 1, sizeof(ycrdt_doc *));
+  ycrdt_buf *bufs = (ycrdt_buf *)calloc(n ? n : 1, sizeof(ycrdt_buf));
+  for (uint32_t i = 0; i < n; ++i) {
+    napi_value d, u;
+    napi_get_element(env, argv[0], i, &d);
+    napi_get_element(env, argv[1], i, &u);
+    docs[i] = get_doc(env, d);
+    if (!docs[i] || !get_bytes(env, u, &bufs[i])) {
+      free(docs); free(bufs);
+      if (docs[i]) napi_throw_type_error(env, NULL, "updates must be Uint8Arrays");
+      return NULL;
+    }
+  }
+  int rc = ycrdt_apply_updates_multi(e, docs, bufs, n);
+  free(docs); free(bufs);
+  return rc == YCRDT_OK ? NULL : throw_rc(env, rc);
+}
+
 static napi_value js_encode_state_as_update(napi_env env, napi_callback_info info) {
   size_t argc = 2;
   napi_value argv[2];
@@ -591,6 +623,7 @@ static napi_value init(napi_env env, napi_value exports) {
       {"setDevice", NULL, js_set_device, NULL, NULL, NULL, napi_default, NULL},
       {"docCreate", NULL, js_doc_create, NULL, NULL, NULL, napi_default, NULL},
       {"applyUpdates", NULL, js_apply_updates, NULL, NULL, NULL, napi_default, NULL},
+      {"applyUpdatesMulti", NULL, js_apply_updates_multi, NULL, NULL, NULL, napi_default, NULL},
       {"encodeStateAsUpdate", NULL, js_encode_state_as_update, NULL, NULL, NULL, napi_default, NULL},
       {"encodeStateVector", NULL, js_encode_state_vector, NULL, NULL, NULL, napi_default, NULL},
       {"mergeUpdates", NULL, js_merge_updates, NULL, NULL, NULL, napi_default, NULL},

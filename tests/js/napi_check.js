@@ -19,7 +19,7 @@ const unhex = (h) => new Uint8Array(Buffer.from(h, 'hex'));
 const mode = process.argv[2] || 'cpu';
 const { encodeAny, decodeAny } = require(path.join(ROOT, 'crdt_amd', 'js', 'any.js'));
 const opsCases = () => JSON.parse(fs.readFileSync(path.join(ROOT, 'tests', 'golden', 'ops.json'))).cases;
-for (const f of ['Doc', 'applyUpdate', 'applyUpdates', 'encodeStateAsUpdate', 'encodeStateVector', 'mergeUpdates', 'diffUpdate', 'diffUpdates']) {
+for (const f of ['Doc', 'applyUpdate', 'applyUpdates', 'applyUpdatesMulti', 'encodeStateAsUpdate', 'encodeStateVector', 'mergeUpdates', 'diffUpdate', 'diffUpdates']) {
   assert.strictEqual(typeof Y[f], 'function', f);
 }
 assert.ok(/gfx950/.test(Y.version()));
@@ -150,6 +150,17 @@ if (mode === 'cpu') {
       n++;
     }
   }
+  // fleet ingest: every golden case is a document, all their updates in ONE Y.applyUpdatesMulti
+  const fleet = [], fdocs = [], fups = [];
+  for (const set of ['kat', 'map', 'array', 'nested']) {
+    for (const c of JSON.parse(fs.readFileSync(path.join(ROOT, 'tests', 'golden', set + '.json'))).cases) {
+      const d = new Y.Doc({ clientID: 0x7ffffff0 });
+      fleet.push([d, c]);
+      for (const u of c.updates) { fdocs.push(d); fups.push(unhex(u)); }
+    }
+  }
+  Y.applyUpdatesMulti(fdocs, fups);
+  for (const [d, c] of fleet) assert.strictEqual(hex(Y.encodeStateAsUpdate(d)), c.state, 'applyUpdatesMulti ' + c.name);
   // the batched sync responder: every (doc state, peer state vector) pair in one call
   const batch = Y.diffUpdates(dsrc, dsv);
   assert.strictEqual(batch.length, dsrc.length);
