@@ -52,6 +52,9 @@ def parse():
     p.add_argument("--profile-phases", action="store_true")
     p.add_argument("--no-per-op", action="store_true", help="skip the crdt.js per-op leg")
     p.add_argument("--fleet-docs", type=int, default=100_000, help="documents in the C5 fleet-ingest leg (0 = skip)")
+    p.add_argument("--no-c4", action="store_true", help="skip the single-GPU C4 leg")
+    p.add_argument("--c4-sharded", action="store_true",
+                   help="with --gpus N > 1: C4 key-hash sharded across the ranks over RCCL (opt-in)")
     p.add_argument("--only-headline", action="store_true",
                    help="time the headline merge only (no side legs): rocprof averages then match the bench line")
     p.add_argument("--c3-items", type=int, default=10_000_000,
@@ -324,6 +327,70 @@ def c3_leg(eng, n_items, steps=3):
                             "kind": "reference", "parity": y["out_sha256"] == hashlib.sha256(gout).hexdigest(),
                             "sample": f"{n} values, Yjs {y['yjs']} in Node {y['node']}"}
     return res
+
+
+def c4_leg(eng, reps=3):
+    """C4 (BASELINE configs[3], nested YArrays under YMap keys) on one GPU: the full document
+    (crdt_amd/workload C4: 2 000 replicas x 10 000 ops on 100 k nested arrays, ~47 M items, base
+    snapshot, overwrites that GC whole arrays, deletes) merged in one device pass, and the same
+    merge as 8 logical key-hash shards (each shard's integrate phases run in turn, flag words summed
+    as the RCCL all-reduce would) — byte-identical to the unsharded result."""
+    import crdt_amd
+    from crdt_amd.workload import C4, gen_nested
+
+    t0 = time.perf_counter()
+    ups, st = gen_nested(**C4)
+    gen_s = time.perf_counter() - t0
+    b = crdt_amd.Batch(ups, eng)
+    b.merge()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        s1 = b.merge()
+    ms = (time.perf_counter() - t0) * 1e3 / reps
+    full = b.result()
+    eng.set_profiling(True)
+    b.merge()
+    phases = {n: round(m, 3) for n, m in eng.phase_times()}
+    eng.set_profiling(False)
+    t0 = time.perf_counter()
+    b.merge_sharded(8)
+    sh_ms = (time.perf_counter() - t0) * 1e3
+    same = b.result() == full
+    return {"workload": "C4: YMap 'docs' of 100 000 nested YArrays, 2 000 replicas x 10 000 ops (push 93 %, "
+                        "overwrite with a new array 2 %, delete 5 %), base snapshot",
+            "updates": len(ups), "input_bytes": sum(len(u) for u in ups), "items": s1.items, "structs": s1.structs,
+            "segments": s1.segments, "output_bytes": len(full[0]), "ms_per_merge": round(ms, 3),
+            "items_per_s": round(s1.items / (ms * 1e-3), 1), "phases_ms": phases,
+            "sharded_8_logical": {"ms": round(sh_ms, 3), "identical": same,
+                                  "includes": "8 x (mask + winner + dead types + YATA + merge flags + export), "
+                                              "sum, GC merge settle, one encode, on this GPU"},
+            "generate_s": round(gen_s, 2)}
+
+
+def c4_sharded_leg(eng, world, rank, dist, reps=3):
+    """C4 key-hash sharded across the ranks (one GPU each): every rank stages the same C4 updates,
+    runs its shard's integrate phases, and the flag words are summed over RCCL inside libycrdt."""
+    import crdt_amd
+    from crdt_amd.workload import C4, gen_nested
+
+    ups, st = gen_nested(**C4)
+    uid = [crdt_amd.Comm.unique_id() if rank == 0 else None]
+    dist.broadcast_object_list(uid, src=0)
+    comm = crdt_amd.Comm(eng, world, rank, uid[0])
+    try:
+        b = crdt_amd.Batch(ups, eng)
+        b.merge_sharded(world, comm)
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            s1 = b.merge_sharded(world, comm)
+        ms = (time.perf_counter() - t0) * 1e3 / reps
+        full = b.result()
+        b.merge()
+        same = b.result() == full
+    finally:
+        comm.close()
+    return {"ranks": world, "ms_per_merge": round(ms, 3), "items": s1.items,
+            "items_per_s": round(s1.items / (ms * 1e-3), 1), "identical_to_unsharded": same}
 
 
 def fleet_ingest_leg(eng, n_docs):
@@ -624,6 +691,8 @@ def main():
     loop = apply_loop_leg(eng, updates, out_update) if side else None
     per_op = per_op_leg(eng) if side and not args.no_per_op else None
     c3 = c3_leg(eng, args.c3_items) if side and args.c3_items > 0 else None
+    c4 = c4_leg(eng) if side and not args.no_c4 else None
+    c4s = c4_sharded_leg(eng, world, rank, dist) if dist is not None and args.c4_sharded else None
     line = {
         "metric": "CRDT items merged/sec at 1/2/4/8 MI355X + % of HBM roofline",
         "value": round(value, 1),
@@ -668,6 +737,8 @@ def main():
         "apply_loop": loop,
         "per_op": per_op,
         "c3": c3,
+        "c4": c4,
+        "c4_sharded": c4s,
         "phases_ms": {n: round(m, 4) for n, m in phases},
     }
     if rank == 0:

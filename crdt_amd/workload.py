@@ -23,6 +23,9 @@ def _lib():
         L.ycw_gen_array.argtypes = [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_uint32,
                                     P(ctypes.c_void_p), P(ctypes.c_size_t), P(ctypes.c_void_p), P(ctypes.c_size_t),
                                     P(ctypes.c_uint64), P(ctypes.c_void_p), P(ctypes.c_size_t)]
+        L.ycw_gen_nested.argtypes = [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_double,
+                                     ctypes.c_double, ctypes.c_uint32, P(ctypes.c_void_p), P(ctypes.c_size_t),
+                                     P(ctypes.c_void_p), P(ctypes.c_size_t), P(ctypes.c_uint64)]
         L.ycw_free.argtypes = [ctypes.c_void_p]
         _L = L
     return _L
@@ -34,6 +37,29 @@ C1 = dict(n_keys=1000, n_replicas=2, ops_per_replica=10000, zipf_s=0.0, p_set=0.
 C2 = dict(n_keys=100_000, n_replicas=1000, ops_per_replica=1000, zipf_s=1.1, p_set=0.8, base_snapshot=True,
           base_client=1, client_mode=0, value_mode=0, seed=2)
 C3 = dict(n_replicas=256, rounds=16, items=10_000_000, seed=3)
+# C4 (nested YArrays under YMap keys): 100k keys, 2 000 replicas x 10 000 ops ~= 50 M items per
+# document; BASELINE's 100 M items is two such documents' worth per GPU pair, key-hash sharded
+C4 = dict(n_replicas=2000, n_keys=100_000, pushes=10_000, init_len=4, p_over=0.02, p_del=0.05, seed=4)
+
+
+def gen_nested(n_replicas, n_keys, pushes, init_len=4, p_over=0.02, p_del=0.05, seed=4):
+    """C4-shaped workload (crdt_amd/workload/ycw_nested.cpp): the base snapshot + one update per
+    replica. Returns (updates: list[bytes], stats: dict(items, structs, deletes))."""
+    L = _lib()
+    data, dlen, offs, nupd = ctypes.c_void_p(), ctypes.c_size_t(), ctypes.c_void_p(), ctypes.c_size_t()
+    st = (ctypes.c_uint64 * 3)()
+    rc = L.ycw_gen_nested(n_replicas, n_keys, pushes, init_len, p_over, p_del, seed, ctypes.byref(data),
+                          ctypes.byref(dlen), ctypes.byref(offs), ctypes.byref(nupd), st)
+    if rc != 0:
+        raise ValueError("bad workload config")
+    try:
+        raw = ctypes.string_at(data.value, dlen.value) if dlen.value else b""
+        o = (ctypes.c_uint64 * (nupd.value + 1)).from_address(offs.value)
+        ups = [raw[o[i]:o[i + 1]] for i in range(nupd.value)]
+    finally:
+        L.ycw_free(data)
+        L.ycw_free(offs)
+    return ups, {"items": st[0], "structs": st[1], "deletes": st[2]}
 
 
 def gen_array(n_replicas=256, rounds=16, items=10_000_000, seed=3, order=False):

@@ -108,3 +108,41 @@ def test_rccl_world1_exchanges(golden):
             assert comm.ds_allgather(st) == st, c["name"]
     finally:
         comm.close()
+
+
+def test_c4_generated_vs_oracle_and_shards():
+    """The C4 generator (crdt_amd/workload/ycw_nested.cpp) at reduced scale: GPU merge equals the
+    oracle's state, and 8 key-hash shards equal the unsharded merge."""
+    from crdt_amd.workload import gen_nested
+    from oracle.yref import Doc as ODoc
+
+    ups, st = gen_nested(60, 2000, 300, seed=11)
+    o = ODoc(0x7FFFFFF0)
+    for u in ups:
+        o.apply_update(u)
+    want = (o.encode_state_as_update(), o.encode_state_vector())
+    assert _merge(ups) == want
+    assert _merge(ups, 8) == want
+    d = crdt_amd.Doc(client_id=0x7FFFFFF0)
+    d.apply_updates(ups)
+    assert json.loads(d.root_json("docs", "map")) == json.loads(o.root_json("docs", "map"))
+
+
+def test_c4_full_size_shards_properties():
+    """Full-size C4 (≈47 M items, 2 000 replicas, 100 k nested arrays): 4 key-hash shards give the
+    unsharded bytes; the merge is order-independent and idempotent."""
+    from crdt_amd.workload import C4, gen_nested
+
+    ups, st = gen_nested(**C4)
+    b = crdt_amd.Batch(ups)
+    s1 = b.merge()
+    full = b.result()
+    assert s1.items > 40_000_000
+    b.merge_sharded(4)
+    assert b.result() == full
+    r = crdt_amd.Batch(list(reversed(ups)))
+    r.merge()
+    assert r.result() == full
+    i = crdt_amd.Batch([full[0]] + ups[:100])
+    i.merge()
+    assert i.result() == full
