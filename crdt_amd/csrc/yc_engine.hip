@@ -568,7 +568,6 @@ int run_decode(ycrdt_engine* e, ycrdt_batch* b, bool lazy, Decoded& D, bool gene
   w.ds = take<DsRange>(V, B_DS, w.cap_ds, ok);
   w.ds_tmp = take<DsRange>(V, B_DSTMP, w.cap_ds, ok);
   w.ds_len = take<uint32_t>(V, B_DSLEN, w.cap_ds + 1, ok);
-  w.ds_scan = take<uint64_t>(V, B_DSSCAN, w.cap_ds + 1, ok);
   w.s_pos = take<uint32_t>(V, B_SPOS, w.cap_structs, ok);
   w.s_sec = take<uint32_t>(V, B_SSEC, w.cap_structs, ok);
   w.s_len = take<uint32_t>(V, B_SLEN, w.cap_structs + 1, ok);

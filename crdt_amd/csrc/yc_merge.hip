@@ -24,42 +24,49 @@
 
 namespace yc {
 
-constexpr uint32_t OWNER_UNITS_PER_LANE = 2;
 
 __device__ __forceinline__ uint32_t seg_of(const uint64_t* __restrict__ cut, const uint32_t* __restrict__ wpre, uint32_t g) {
   return wpre[g >> 6] + (uint32_t)__popcll(cut[g >> 6] & ((2ull << (g & 63)) - 1)) - 1;
 }
 
 // --------------------------------------------------------------------------- owner / dedupe
-// grid-stride over the Σ input clock lengths (read on the device: no host sync for the bound)
+// One lane per struct (one per delete-set range below): a struct's units are consecutive in the
+// merged store, so a wave's atomics on short structs hit consecutive addresses; structs longer than
+// LONG_UNITS are covered by the whole wavefront, one at a time. (A lane per unit pair had to find
+// its struct by a binary search over all structs: ~27 dependent loads per lane at C2 x 112.)
+constexpr uint32_t LONG_UNITS = 32;
+__device__ __forceinline__ uint64_t shfl64(uint64_t v, int l) {
+  return ((uint64_t)(uint32_t)__shfl((uint32_t)(v >> 32), l) << 32) | (uint32_t)__shfl((uint32_t)v, l);
+}
 __global__ __launch_bounds__(256) void k_owner(Work w, uint32_t nstructs) {
-  const uint64_t total_in = w.s_lenscan[nstructs];
-  const uint64_t nlanes = (total_in + OWNER_UNITS_PER_LANE - 1) / OWNER_UNITS_PER_LANE;
-  const uint64_t* __restrict__ P = w.s_lenscan;
-  for (uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; t < nlanes; t += (uint64_t)gridDim.x * blockDim.x) {
-    uint64_t j = t * OWNER_UNITS_PER_LANE;
-    const uint64_t jend = min(j + OWNER_UNITS_PER_LANE, total_in);
-    uint32_t lo = 0, hi = nstructs;  // last s with P[s] <= j
-    while (hi - lo > 1) { const uint32_t mid = (lo + hi) >> 1; if (P[mid] <= j) lo = mid; else hi = mid; }
-    uint32_t s = lo;
-    while (j < jend) {
-      while (P[s + 1] <= j) ++s;
-      const uint64_t send = min(jend, P[s + 1]);
-      const uint32_t ref = w.s_info[s] & 31u;
-      if (ref != REF_SKIP) {
-        const uint32_t cidx = w.s_cidx[s];
-        const uint32_t clock = w.s_clock[s], st = w.cl_state[cidx];
-        const uint64_t gb = w.cl_base[cidx] + clock - P[s];
-        const uint32_t fl = ref == REF_DELETED ? UF_DEL : (ref == REF_GC ? (UF_GC | UF_DEL) : 0u);
-        // units at or past the client's (capped) state stay out of the store
-        const uint64_t lim = min(send, P[s] + (st > clock ? (uint64_t)(st - clock) : 0ull));
-        for (; j < lim; ++j) {
-          const uint32_t g = (uint32_t)(gb + j);
-          atomicMin(&w.u_owner[g], s);
-          if (fl) atomicOr(&w.u_flags[g], fl);
-        }
-        j = send;
-      } else j = send;
+  const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t lane = threadIdx.x & 63;
+  uint64_t gb = 0;
+  uint32_t n = 0, fl = 0;
+  if (s < nstructs) {
+    const uint32_t ref = w.s_info[s] & 31u;
+    if (ref != REF_SKIP) {
+      const uint32_t cidx = w.s_cidx[s];
+      const uint32_t clock = w.s_clock[s], st = w.cl_state[cidx];
+      // units at or past the client's (capped) state stay out of the store
+      n = st > clock ? min(w.s_len[s], st - clock) : 0u;
+      gb = w.cl_base[cidx] + clock;
+      fl = ref == REF_DELETED ? UF_DEL : (ref == REF_GC ? (UF_GC | UF_DEL) : 0u);
+    }
+  }
+  const bool lng = n > LONG_UNITS;
+  if (!lng)
+    for (uint32_t k = 0; k < n; ++k) {
+      atomicMin(&w.u_owner[(uint32_t)(gb + k)], s);
+      if (fl) atomicOr(&w.u_flags[(uint32_t)(gb + k)], fl);
+    }
+  for (uint64_t m = __ballot(lng); m; m &= m - 1) {
+    const int L = __ffsll((long long)m) - 1;
+    const uint64_t g0 = shfl64(gb, L);
+    const uint32_t nl = __shfl(n, L), fll = __shfl(fl, L), sl = __shfl(s, L);
+    for (uint32_t k = lane; k < nl; k += 64) {
+      atomicMin(&w.u_owner[(uint32_t)(g0 + k)], sl);
+      if (fll) atomicOr(&w.u_flags[(uint32_t)(g0 + k)], fll);
     }
   }
 }
@@ -81,24 +88,24 @@ __global__ void k_ds_prep(Work w, uint32_t nds, uint32_t nclients) {
   w.ds[i] = r;
   w.ds_len[i] = len;
 }
+// only UF_DS is written in this kernel: concurrent plain ORs of the same bit are harmless
 __global__ __launch_bounds__(256) void k_ds_mark(Work w, uint32_t nds) {
-  const uint64_t total = w.ds_scan[nds];
-  const uint64_t nlanes = (total + OWNER_UNITS_PER_LANE - 1) / OWNER_UNITS_PER_LANE;
-  const uint64_t* __restrict__ P = w.ds_scan;
-  for (uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; t < nlanes; t += (uint64_t)gridDim.x * blockDim.x) {
-    uint64_t j = t * OWNER_UNITS_PER_LANE;
-    const uint64_t jend = min(j + OWNER_UNITS_PER_LANE, total);
-    uint32_t lo = 0, hi = nds;
-    while (hi - lo > 1) { const uint32_t mid = (lo + hi) >> 1; if (P[mid] <= j) lo = mid; else hi = mid; }
-    uint32_t s = lo;
-    while (j < jend) {
-      while (P[s + 1] <= j) ++s;
-      const uint64_t send = min(jend, P[s + 1]);
-      const DsRange r = w.ds[s];
-      const uint64_t gb = w.cl_base[r.client] + r.clock - P[s];
-      // only UF_DS is written in this kernel: concurrent plain ORs of the same bit are harmless
-      for (; j < send; ++j) w.u_flags[(uint32_t)(gb + j)] |= UF_DS;
-    }
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t lane = threadIdx.x & 63;
+  uint64_t gb = 0;
+  uint32_t n = 0;
+  if (i < nds) {
+    n = w.ds_len[i];
+    if (n) { const DsRange r = w.ds[i]; gb = w.cl_base[r.client] + r.clock; }
+  }
+  const bool lng = n > LONG_UNITS;
+  if (!lng)
+    for (uint32_t k = 0; k < n; ++k) w.u_flags[(uint32_t)(gb + k)] |= UF_DS;
+  for (uint64_t m = __ballot(lng); m; m &= m - 1) {
+    const int L = __ffsll((long long)m) - 1;
+    const uint64_t g0 = shfl64(gb, L);
+    const uint32_t nl = __shfl(n, L);
+    for (uint32_t k = lane; k < nl; k += 64) w.u_flags[(uint32_t)(g0 + k)] |= UF_DS;
   }
 }
 
@@ -174,14 +181,10 @@ __global__ void k_scatter_seg(Work w, uint32_t nwords, uint64_t nunits) {
 
 void launch_units(const Work& w, uint32_t nstructs, uint32_t nclients, uint32_t nds, uint64_t nunits, hipStream_t s) {
   fill_u32_multi({{w.u_owner, nunits, NONE}, {w.u_flags, nunits, 0u}, {w.u_minchild, nunits, NONE}}, s);
-  // the unit counts these kernels cover (Σ input lengths, Σ delete-set lengths) are read on the
-  // device; the grids are sized for one pass over the merged store and stride beyond it
-  const uint32_t grid = (uint32_t)std::min<uint64_t>(nunits / (OWNER_UNITS_PER_LANE * 256) + 1, 8192);
-  if (nstructs) hipLaunchKernelGGL(k_owner, dim3(grid), dim3(256), 0, s, w, nstructs);
+  if (nstructs) hipLaunchKernelGGL(k_owner, dim3((nstructs + 255) / 256), dim3(256), 0, s, w, nstructs);
   if (nds) {
     hipLaunchKernelGGL(k_ds_prep, dim3(nds / 256 + 1), dim3(256), 0, s, w, nds, nclients);
-    scan_u32_to_u64(w.tmp, w.tmp_bytes, w.ds_len, w.ds_scan, nds + 1, s);
-    hipLaunchKernelGGL(k_ds_mark, dim3(grid), dim3(256), 0, s, w, nds);
+    hipLaunchKernelGGL(k_ds_mark, dim3((nds + 255) / 256), dim3(256), 0, s, w, nds);
   }
   if (nstructs) hipLaunchKernelGGL(k_refs, dim3((nstructs + 255) / 256), dim3(256), 0, s, w, nstructs);
 }
