@@ -414,6 +414,7 @@ struct Decoded {
   uint64_t nunits = 0, in_len = 0;
   uint32_t array_roots = 0;  // 1: some item names a parent without a parentSub (a YArray may exist)
   uint32_t nested = 0;       // 1: some item names a parent item (nested types: dead-type pass needed)
+  uint32_t nroots = 0;       // items with an explicit parent (key table bound)
 };
 
 // K1: decode every update of the batch into the struct SoA (+ client table, delete-set ranges).
@@ -623,6 +624,7 @@ int run_decode(ycrdt_engine* e, ycrdt_batch* b, bool lazy, Decoded& D, bool gene
   D.in_len = c.in_len;
   D.array_roots = c.narray_roots;
   D.nested = c.nested;
+  D.nroots = c.nroots;
   if (nunits >= 0xF0000000ull) return fail(YCRDT_E_CAPACITY, "more than 2^32 units in one batch");
   D.nstructs = nstructs;
   D.nsections = nsections;
@@ -784,7 +786,9 @@ int run_merge(ycrdt_engine* e, ycrdt_batch* b, const std::unordered_map<uint32_t
     nsegs = c.nsegs;
   }
   // keys
-  w.cap_keys = next_pow2(std::max<uint64_t>(2ull * nsegs, 64));
+  // every list is rooted by an explicit-parent item (a key per root struct at most): the table is
+  // sized from those, not from every segment
+  w.cap_keys = next_pow2(std::max<uint64_t>(2ull * std::min<uint64_t>(D.nroots, nsegs), 64));
   w.k_hash = take<uint64_t>(V, B_KHASH, w.cap_keys, ok);
   w.k_rootmax = take<uint32_t>(V, B_KROOT, w.cap_keys, ok);
   w.k_winner = take<uint32_t>(V, B_KWIN, w.cap_keys, ok);
