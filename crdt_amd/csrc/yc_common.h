@@ -16,14 +16,9 @@ constexpr uint32_t NONE = 0xFFFFFFFFu;
 constexpr uint32_t UNKNOWN = 0xFFFFFFFEu;  // a reference to a client no update of the batch carries
 
 // ---------------------------------------------------------------- decode geometry
-// A "group" is a ≤16 KiB slice of one update parsed by one 256-lane workgroup; each lane owns
-// a 64-byte chunk and speculatively parses the struct chain that starts at the chunk start.
-constexpr uint32_t CHUNK = 64;
-constexpr uint32_t GROUP_LANES = 256;
-constexpr uint32_t GROUP_BYTES = CHUNK * GROUP_LANES;  // 16384
-constexpr uint32_t SPEC_STEPS_FAST = 4;               // speculative parse: first pass work cap (elements)
-constexpr uint32_t SPEC_MAX_STEPS = 1024;             // second pass (compacted); longer -> exact walker parse
-constexpr uint16_t STOPF = 0x8000;                    // table flag: chain stops at an unsized struct
+// A large update is cut into chunks of SCHUNK bytes (64-byte aligned, so a chunk owns its words of
+// the per-byte bitmaps); one lane per chunk follows the struct chain from the chunk's first byte.
+constexpr uint32_t SCHUNK = 1024;
 
 
 // error codes raised on device (first error wins via atomicCAS on the error word)
@@ -35,9 +30,9 @@ enum : uint32_t {
   ERR_CAPACITY = 4,     // internal capacity exceeded
 };
 
-struct Group {          // one decode group
+struct Group {          // one decode chunk of a large update
   uint32_t start, end;  // byte range [start,end) inside the batch buffer (start 64-byte aligned)
-  uint32_t uend;        // end of the group's update (parses never read past it)
+  uint32_t uend;        // end of the chunk's update (parses never read past it)
   uint32_t upd;         // update index
 };
 
@@ -50,10 +45,6 @@ struct Section {        // one client section of one update's struct section
   uint32_t cidx;        // dense client index (filled later)
   uint32_t first_idx;   // global struct index of first struct
   uint32_t pad;
-};
-
-struct CopyTask {       // verified chain segment: b struct starts along the chain from position a
-  uint32_t a, b;
 };
 
 // count the lanes of a wavefront for which `pred` holds with ONE atomic (the first such lane adds

@@ -1,20 +1,24 @@
 // yc_decode.hip — K1: decode of Yjs v1 updates on gfx950.
 //
 // Replaces lib0's sequential readers + readClientsStructRefs (Y@19286) / readDeleteSet
-// (Y@11105) with a byte-parallel decode:
-//   1. k_group_parse   one 256-lane workgroup per 16 KiB group; every lane speculatively parses the
-//                      struct chain starting at its 64-byte chunk, lane 0 stitches the chunk chains
-//                      into one deterministic "main chain" bitmap (1 bit per byte of input; a bit
-//                      marks every position the chain visits: next(p) on success, p+1 on failure).
-//                      From any true struct start the chain IS the true struct sequence.
-//   2. k_walker        one lane per update follows the true chain through section headers, jumping a
-//                      whole group per step while it is on the main chain (popcount of the bitmap),
-//                      parsing exactly only where it is off the chain (after headers).
-//   3. k_copy/k_patch  verified main-chain ranges + exact positions -> final struct-start bitmap.
-//   4. k_struct_pos    popcount prefix (scan) -> dense struct index for every struct start.
-//   5. k_ds_decode     one wavefront per update decodes the delete set, a pure varuint stream, with a
+// (Y@11105) with a parallel decode. Small updates (most of a fleet / gossip batch) take the direct
+// path; large ones (snapshots) the chunk path:
+//   1. k_direct        one lane per small update parses it exactly through a private LDS window
+//                      and writes its words of the struct-start bitmap.
+//   1'. k_spec         one lane per 1 KiB chunk of a large update follows the all-struct chain
+//                      (next(p) = p + struct length, p + 1 where no struct parses) from the chunk's
+//                      first byte and marks every position it visits (spec_bits) and its exit.
+//                      Such a chain synchronises with the true struct sequence within a few structs
+//                      of any start, and from a true struct start on it IS the true sequence.
+//   2'. k_walk         one wavefront per large update follows the true sequence through the
+//                      section headers 64 chunks per step: lane j enters chunk j at the exit of
+//                      chunk j-1's chain, parses exactly until it meets its own chunk's chain and
+//                      counts the rest by popcount; the first lane whose true exit differs from
+//                      its chain's exit ends the step (a failed speculation costs one chunk).
+//   3. k_struct_pos    popcount prefix (scan) -> dense struct index for every struct start.
+//   4. k_ds_decode     one wavefront per update decodes the delete set, a pure varuint stream, with a
 //                      ballot of terminal bytes + in-register gathers (wavefront prefix scan).
-//   6. k_struct_decode one lane per struct: full field decode into the SoA struct table.
+//   5. k_struct_decode one lane per struct: full field decode into the SoA struct table.
 #include <algorithm>
 #include <cstdlib>
 
@@ -22,29 +26,10 @@
 
 namespace yc {
 
-// --------------------------------------------------------------------------- 1a. speculative parse
-// nxt[p] for every byte position p of every group: the length of the struct that would start at
-// p (0 = not a struct, 1 = not sized here: over the work cap, or too long for the 15-bit table
-// positions — the walkers parse those exactly). One 256-lane workgroup per 4 KiB slice, reading
-// the bytes through the caches (no LDS staging), so many workgroups share a CU and hide the
-// latency of the byte-serial parse. Positions are counting-sorted by their would-be info byte
-// (content ref x origin/rightOrigin/parentSub bits) and sized by spec_len one class per wavefront;
-// what the sizer hands over is re-parsed by parse_struct under a work cap.
-constexpr uint32_t PSLICE = 4096;               // bytes per parse workgroup
-constexpr uint32_t PL = 256;                    // lanes per parse workgroup
-// work cap of the general parser on what the sizer handed over. Most of the queue is garbage
-// positions whose would-be element count is large; a long chain of dependent reads there stalls
-// the whole workgroup, and a true struct over the cap is parsed exactly by the walkers.
-constexpr uint32_t PARSE_QUEUE_STEPS = 96;
-constexpr uint32_t PHALO = 1024;
-constexpr uint32_t PQUEUE = 1024;              // general-parser queue entries per slice                // bytes staged past the slice (structs crossing its end)
-constexpr uint32_t NB = 72;                     // content refs 1..9 x info>>5
-
-// ---- the speculative struct sizer (k_parse). Exact on every valid struct; on other bytes it only
-// has to be deterministic: the walkers follow nxt from true struct starts only, and every struct
-// on the true chain is re-parsed exactly by k_struct_decode, which reports a malformed one.
-// The info byte's class (content ref, origin / right origin / parentSub bits) is wave-uniform
-// (positions are tiled per class), so the field layout costs scalar branches, and varuints are
+// --------------------------------------------------------------------------- 1. struct sizer
+// The speculative struct sizer. Exact on every valid struct; on other bytes it only has to be
+// deterministic: chains are trusted only from true struct starts on, and every struct on the true
+// sequence is re-parsed exactly by k_struct_decode, which reports a malformed one. Varuints are
 // read branch-free from an 8-byte register window.
 __device__ __forceinline__ uint64_t win8(const uint8_t* __restrict__ b, uint32_t p) {
   const uint32_t* d = (const uint32_t*)(b + (p & ~3u));  // the batch buffer is padded past its end
@@ -176,459 +161,6 @@ __device__ __forceinline__ uint32_t spec_len(const S& b, uint32_t pos, uint32_t 
   return p - pos < 0x10000u ? p - pos : 1u;
 }
 
-__global__ __launch_bounds__(PL) void k_parse(Work w) {
-  const uint8_t* __restrict__ b = w.bytes;
-  const Group G = w.groups[blockIdx.x / (GROUP_BYTES / PSLICE)];
-  const uint32_t s0 = G.start + (blockIdx.x % (GROUP_BYTES / PSLICE)) * PSLICE;
-  if (s0 >= G.end) return;
-  unsigned long long* dbg = w.dbg ? w.dbg + (size_t)w.ngroups * 8 + (size_t)blockIdx.x * 8 : nullptr;
-  if (dbg && threadIdx.x == 0) { dbg[0] = wall_clock64(); dbg[1] = clock64(); }
-  const uint32_t len = min(G.end - s0, PSLICE), uend = G.uend;
-  uint16_t* __restrict__ out = w.tab.nxt + s0;
-  __shared__ uint32_t bstart[NB + 1], bcursor[NB], tstart[NB + 1], qn;
-  __shared__ uint16_t sorted[PSLICE], queue[PQUEUE];
-  __shared__ uint32_t lw[(PSLICE + PHALO) / 4 + 2];
-  const uint32_t tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-  // stage the slice + halo in LDS: the byte-serial varuint chains then wait on LDS, not on L2
-  const uint32_t wlen = min(uend - s0, PSLICE + PHALO);
-  const uint32_t* __restrict__ gw = (const uint32_t*)(b + s0);  // s0 is 64-byte aligned
-  for (uint32_t i = tid; i < (wlen + 3) / 4; i += PL) lw[i] = gw[i];
-  const LdsSrc src{b, lw, s0, wlen};
-  for (uint32_t i = tid; i < NB; i += PL) bcursor[i] = 0;
-  if (tid == 0) qn = 0;
-  __syncthreads();
-  for (uint32_t o = tid; o < len; o += PL) {  // GC / Skip (info + one varuint) resolved on the spot
-    const uint32_t info = (lw[o >> 2] >> ((o & 3u) * 8)) & 0xFFu;
-    const uint32_t ref = info & 31u;
-    uint16_t d = 0;
-    if (ref == REF_GC || ref == REF_SKIP) {
-      uint32_t q = s0 + o + 1;
-      bool okv = true;
-      rd_vu(b, q, uend, okv);
-      d = okv ? (uint16_t)(q - s0 - o) : (uint16_t)0;
-    } else if (ref <= REF_DOC) {
-      atomicAdd(&bcursor[(ref - 1) * 8 + (info >> 5)], 1u);
-    }
-    out[o] = d;
-  }
-  __syncthreads();
-  if (dbg && tid == 0) dbg[2] = clock64();
-  if (wave == 0) {  // class starts and 64-position tiles per class: a wavefront scan over NB classes
-    uint32_t acc = 0, tiles = 0;
-    for (uint32_t base = 0; base < NB; base += 64) {
-      const uint32_t i = base + lane;
-      const uint32_t c = i < NB ? bcursor[i] : 0u, tc = (c + 63) / 64;
-      uint32_t x = c, y = tc;  // inclusive scans
-#pragma unroll
-      for (uint32_t d = 1; d < 64; d <<= 1) {
-        const uint32_t xo = __shfl_up(x, d), yo = __shfl_up(y, d);
-        if (lane >= d) { x += xo; y += yo; }
-      }
-      if (i < NB) { bstart[i] = acc + x - c; bcursor[i] = acc + x - c; tstart[i] = tiles + y - tc; }
-      acc += __shfl(x, 63);
-      tiles += __shfl(y, 63);
-    }
-    if (lane == 0) { bstart[NB] = acc; tstart[NB] = tiles; }
-  }
-  __syncthreads();
-  for (uint32_t o = tid; o < len; o += PL) {
-    const uint32_t info = (lw[o >> 2] >> ((o & 3u) * 8)) & 0xFFu;
-    const uint32_t ref = info & 31u;
-    if (ref >= 1 && ref <= REF_DOC) sorted[atomicAdd(&bcursor[(ref - 1) * 8 + (info >> 5)], 1u)] = (uint16_t)o;
-  }
-  __syncthreads();
-  if (dbg && tid == 0) dbg[3] = clock64();
-  // every wavefront sizes tiles of ONE class: the class is a scalar for the whole parse
-  const uint32_t ntiles = tstart[NB];
-  for (uint32_t t = wave; t < ntiles; t += PL / 64) {
-    uint32_t lo = 0, hi = NB;  // last class c with tstart[c] <= t
-    while (hi - lo > 1) { const uint32_t m = (lo + hi) >> 1; if (tstart[m] <= t) lo = m; else hi = m; }
-    const uint32_t c = __builtin_amdgcn_readfirstlane(lo);
-    const uint32_t i = bstart[c] + (t - tstart[c]) * 64 + lane;
-    if (i < bstart[c + 1]) {
-      const uint32_t o = sorted[i];
-      const uint32_t d = spec_len(src, s0 + o, uend, c);
-      if (d == 1) {  // over the queue's capacity the position stays handed over (1) to the walkers
-        const uint32_t k = atomicAdd(&qn, 1u);
-        if (k < PQUEUE) queue[k] = (uint16_t)o;
-      }
-      out[o] = (uint16_t)d;
-    }
-  }
-  __syncthreads();
-  if (dbg && tid == 0) dbg[4] = clock64();
-  const uint32_t nq = min(qn, PQUEUE);  // the general parser under a work cap for what the sizer handed over
-  for (uint32_t i = tid; i < nq; i += PL) {
-    const uint32_t o = queue[i];
-    uint32_t q = s0 + o;
-    const int r = parse_struct<false, 4>(b, q, uend, PARSE_QUEUE_STEPS, nullptr);
-    out[o] = r > 0 ? (q - s0 - o < 0x10000u ? (uint16_t)(q - s0 - o) : (uint16_t)1) : (r == -1 ? (uint16_t)1 : (uint16_t)0);
-  }
-  if (dbg) {
-    __syncthreads();
-    if (tid == 0) { dbg[5] = clock64(); dbg[6] = wall_clock64(); dbg[7] = ((unsigned long long)nq << 32) | ntiles; }
-  }
-}
-// --------------------------------------------------------------------------- 1b. chain tables
-// For every byte position p of a group, from nxt: the chain summaries (first chain position
-// at/after the end of p's chunk / block / group, number of chain positions visited before it)
-// computed by backward dynamic programming (list ranking) in LDS. Table positions are 15 bits
-// (STOPF marks a chain that stops at a struct the tables could not size).
-constexpr uint32_t TL = 1024;                   // lanes per table workgroup
-constexpr uint32_t BLOCK = 1024;                // 16 chunks
-constexpr uint32_t LDS_NXT = 0, LDS_CEXIT = 32768, LDS_CCNT = 65536, LDS_BEXIT = 81920, LDS_BCNT = 114688;
-constexpr uint32_t LDS_BM = 147456, LDS_TASK = LDS_BM + 2048;  // single-group walk: bitmap words, pieces
-constexpr uint32_t MAXTASK = 2048;
-constexpr uint32_t LDS_TOTAL = LDS_TASK + 4 * MAXTASK;             // 157,696 B of the 160 KiB
-static_assert(GROUP_BYTES == 16384, "table layout assumes 16 KiB groups");
-
-__global__ __launch_bounds__(TL) void k_tables(Work w) {
-  const uint8_t* __restrict__ b = w.bytes;
-  const Group* __restrict__ groups = w.groups;
-  const Tables& t = w.tab;
-  __shared__ __attribute__((aligned(16))) uint8_t lds[LDS_TOTAL];
-  uint16_t* nxt = (uint16_t*)(lds + LDS_NXT);
-  uint16_t* cexit = (uint16_t*)(lds + LDS_CEXIT);
-  uint8_t* ccnt = (uint8_t*)(lds + LDS_CCNT);
-  uint16_t* bexit = (uint16_t*)(lds + LDS_BEXIT);
-  uint16_t* bcnt = (uint16_t*)(lds + LDS_BCNT);
-  uint16_t* gexit = nxt;                        // group level overlays nxt / cexit (phase D)
-  uint16_t* gcnt = cexit;
-  const Group G = groups[blockIdx.x];
-  const uint32_t tid = threadIdx.x;
-  if (w.dbg && tid == 0) w.dbg[blockIdx.x * 8 + 0] = clock64();
-  const uint32_t glen = G.end - G.start;
-  for (uint32_t o = tid; o < glen; o += TL) nxt[o] = t.nxt[G.start + o];
-  __syncthreads();
-  if (w.dbg && tid == 0) { w.dbg[blockIdx.x * 8 + 1] = w.dbg[blockIdx.x * 8 + 2] = w.dbg[blockIdx.x * 8 + 3] = clock64(); }
-  // phase B: chunk level by pointer doubling over all positions (6 rounds cover a 64-byte chunk),
-  // double-buffered through the block-array region (free again once the bytes are parsed); reads
-  // are mostly unit-stride across a wavefront, unlike a lane-per-chunk backward sweep.
-  {
-    uint16_t* e0 = cexit;
-    uint8_t* c0 = ccnt;
-    uint16_t* e1 = bexit;
-    uint8_t* c1 = (uint8_t*)bcnt;
-    for (uint32_t o = tid; o < glen; o += TL) {
-      const uint32_t d = nxt[o];
-      if (d == 1 || o + d >= STOPF) { e0[o] = (uint16_t)(o | STOPF); c0[o] = 0; }  // sized by an exact parse
-      else { e0[o] = (uint16_t)(d == 0 ? o + 1 : o + d); c0[o] = 1; }
-    }
-    __syncthreads();
-#pragma unroll 1
-    for (int round = 0; round < 6; ++round) {
-      for (uint32_t o = tid; o < glen; o += TL) {
-        const uint32_t ce = min((o | (CHUNK - 1)) + 1, glen);
-        const uint32_t x = e0[o];
-        uint32_t ex = x, cx = c0[o];
-        if (!(x & STOPF) && x < ce) { ex = e0[x]; cx += c0[x]; }
-        e1[o] = (uint16_t)ex;
-        c1[o] = (uint8_t)cx;
-      }
-      __syncthreads();
-      uint16_t* te = e0; e0 = e1; e1 = te;
-      uint8_t* tc = c0; c0 = c1; c1 = tc;
-    }
-    static_assert(6 % 2 == 0, "an even number of rounds leaves the result in cexit/ccnt");
-  }
-  // phase C: block level (chunk s of every block, s = 15..0), from the chunk level
-  for (int s = 15; s >= 0; --s) {
-    for (uint32_t i = tid; i < 16 * CHUNK; i += TL) {
-      const uint32_t blk = i / CHUNK;
-      const uint32_t o = blk * BLOCK + (uint32_t)s * CHUNK + (i % CHUNK);
-      if (o >= glen) continue;
-      const uint32_t bend = min((blk + 1) * BLOCK, glen);
-      const uint32_t x = cexit[o];
-      if ((x & STOPF) || x >= bend) { bexit[o] = (uint16_t)x; bcnt[o] = ccnt[o]; }
-      else { bexit[o] = bexit[x]; bcnt[o] = (uint16_t)(ccnt[o] + bcnt[x]); }
-    }
-    __syncthreads();
-  }
-  if (w.dbg && tid == 0) w.dbg[blockIdx.x * 8 + 4] = clock64();
-  // ---- an update that fits in one group is walked right here (its tables never leave LDS): lane 0
-  // follows the true chain through the section headers by block exits (1 KiB per step), then chunk
-  // exits, queueing (position, count) chain pieces; then one lane per piece marks its struct starts
-  // into an LDS copy of the final bitmap (the update owns its 64-byte-aligned words exclusively) —
-  // k_walker / k_mark skip it.
-  if (G.start == w.uoff[G.upd] && G.end == G.uend) {
-    uint64_t* bm = (uint64_t*)(lds + LDS_BM);   // 256 words
-    uint32_t* task = (uint32_t*)(lds + LDS_TASK);  // (position << 11 | count), count <= 1024
-    __shared__ uint32_t ntask;
-    const uint32_t nwords_g = (glen + 63) / 64;
-    for (uint32_t i = tid; i < nwords_g; i += TL) bm[i] = 0;
-    if (tid == 0) ntask = 0;
-    __syncthreads();
-    if (tid == 0) {
-      const uint32_t u = G.upd, uend = G.uend;
-      uint32_t* err = &w.ctr->err;
-      w.dsstart[u] = NONE;
-      bool ok = true;
-      uint32_t p = G.start;
-      uint32_t nt = 0;
-      // a chain piece: queued while there is room, else marked right here (many tiny sections)
-      auto piece = [&](uint32_t o, uint32_t cnt) {
-        if (nt < MAXTASK) { task[nt++] = (o << 11) | cnt; return; }
-        for (uint32_t k = 0; k < cnt; ++k) {
-          bm[o >> 6] |= 1ull << (o & 63);
-          const uint32_t d = nxt[o];
-          o += d == 0 ? 1 : d;
-        }
-      };
-      const uint32_t nsec = rd_vu(b, p, uend, ok);
-      if (!ok || nsec > (uend - p) / 3 + 1) { raise_err(err, ERR_DECODE); goto done; }
-      {
-        const uint32_t sbase = atomicAdd(&w.ctr->nsections, nsec);
-        if (sbase + nsec > w.cap_sections) { raise_err(err, ERR_CAPACITY); goto done; }
-        w.usec_start[u] = sbase;
-        w.usec_n[u] = nsec;
-        for (uint32_t sct = 0; sct < nsec; ++sct) {
-          const uint32_t n = rd_vu(b, p, uend, ok);
-          const uint32_t client = rd_vu(b, p, uend, ok);
-          const uint32_t clock = rd_vu(b, p, uend, ok);
-          if (!ok || n > uend - p) { raise_err(err, ERR_DECODE); goto done; }
-          Section sec;
-          sec.upd = u; sec.n = n; sec.client = client; sec.clock = clock;
-          sec.first_pos = n ? p : NONE; sec.cidx = NONE; sec.first_idx = NONE; sec.pad = 0;
-          w.sections[sbase + sct] = sec;
-          if (n) atomicOr((unsigned long long*)&w.sec_bits[p >> 6], 1ull << (p & 63));
-          uint32_t r = n;
-          uint32_t o = p - G.start;
-          while (r > 0) {
-            if (o >= glen) { raise_err(err, ERR_DECODE); goto done; }
-            for (;;) {  // whole block pieces of the chain
-              const uint32_t be = bexit[o], bc = bcnt[o];
-              if ((be & STOPF) || bc >= r || bc == 0) break;
-              piece(o, bc);
-              r -= bc;
-              o = be;
-              if (o >= glen) break;
-            }
-            if (r == 0 || o >= glen) continue;
-            for (;;) {  // whole chunk pieces
-              const uint32_t ce = cexit[o], cc = ccnt[o];
-              if ((ce & STOPF) || cc >= r || cc == 0) break;
-              piece(o, cc);
-              r -= cc;
-              o = ce;
-              if (o >= glen) break;
-            }
-            if (r == 0) break;
-            if (o >= glen) { raise_err(err, ERR_DECODE); goto done; }
-            // one struct: sized by the table, or parsed exactly (long / unsized struct)
-            const uint32_t d = nxt[o];
-            uint32_t q = G.start + o;
-            if (d == 1) {
-              if (parse_struct<false>(b, q, uend, 0xFFFFFFFFu, nullptr) <= 0) { raise_err(err, ERR_DECODE); w.ctr->err_info = G.start + o; goto done; }
-            } else if (d == 0) { raise_err(err, ERR_DECODE); goto done; }
-            else q += d;
-            bm[o >> 6] |= 1ull << (o & 63);
-            o = q - G.start;
-            --r;
-          }
-          p = G.start + o;
-        }
-        w.dsstart[u] = p;
-      }
-    done:
-      ntask = nt;
-    }
-    __syncthreads();
-    const uint32_t nt = ntask;
-    for (uint32_t i = tid; i < nt; i += TL) {
-      uint32_t x = task[i] >> 11, left = task[i] & 0x7FFu;
-      uint32_t word = x >> 6;
-      uint64_t m = 0;
-      while (left > 0) {
-        if ((x >> 6) != word) { atomicOr((unsigned long long*)&bm[word], (unsigned long long)m); word = x >> 6; m = 0; }
-        m |= 1ull << (x & 63);
-        const uint32_t d = nxt[x];
-        x += d == 0 ? 1 : d;
-        --left;
-      }
-      atomicOr((unsigned long long*)&bm[word], (unsigned long long)m);
-    }
-    __syncthreads();
-    for (uint32_t i = tid; i < nwords_g; i += TL) w.final_bits[(G.start >> 6) + i] = bm[i];
-    if (w.dbg && tid == 0) w.dbg[blockIdx.x * 8 + 5] = clock64();
-    return;
-  }
-  // exits are stored as forward deltas from the position itself (|STOPF when the chain stops at a
-  // struct the tables could not size), so consumers never need the group origin
-  for (uint32_t o = tid; o < glen; o += TL) {
-    t.cexit[G.start + o] = (uint16_t)(((cexit[o] & 0x7FFFu) - o) | (cexit[o] & STOPF));
-    t.ccnt[G.start + o] = ccnt[o];
-  }
-  for (uint32_t o = tid; o < glen; o += TL) {
-    t.bexit[G.start + o] = (uint16_t)(((bexit[o] & 0x7FFFu) - o) | (bexit[o] & STOPF));
-    t.bcnt[G.start + o] = bcnt[o];
-  }
-  // phase D: group level (block s = 15..0); gexit/gcnt overlay nxt/cexit (already written out)
-  for (int s = 15; s >= 0; --s) {
-    for (uint32_t i = tid; i < BLOCK; i += TL) {
-      const uint32_t o = (uint32_t)s * BLOCK + i;
-      if (o >= glen) continue;
-      const uint32_t x = bexit[o];
-      if ((x & STOPF) || x >= glen) { gexit[o] = (uint16_t)x; gcnt[o] = bcnt[o]; }
-      else { gexit[o] = gexit[x]; gcnt[o] = (uint16_t)(bcnt[o] + gcnt[x]); }
-    }
-    __syncthreads();
-  }
-  for (uint32_t o = tid; o < glen; o += TL) {
-    t.gexit[G.start + o] = (uint16_t)(((gexit[o] & 0x7FFFu) - o) | (gexit[o] & STOPF));
-    t.gcnt[G.start + o] = gcnt[o];
-  }
-}
-
-void launch_group_parse(const Work& w, hipStream_t s) {
-  if (w.ngroups) hipLaunchKernelGGL(k_parse, dim3(w.ngroups * (GROUP_BYTES / PSLICE)), dim3(PL), 0, s, w);
-}
-void launch_group_tables(const Work& w, hipStream_t s) {
-  if (w.ngroups) hipLaunchKernelGGL(k_tables, dim3(w.ngroups), dim3(TL), 0, s, w);
-}
-
-// --------------------------------------------------------------------------- 2. walker
-// One lane per update follows the true struct chain through the section headers: a whole group
-// per step while the current section continues past it (gexit/gcnt), descending to block /
-// chunk / struct granularity only where a section ends. It emits verified chain segments
-// (start, count) for k_mark and exact positions (long structs, final steps) as patches.
-__device__ __forceinline__ bool emit_seg(const Work& w, uint32_t x, uint32_t n) {
-  const uint32_t i = atomicAdd(&w.ctr->ncopy, 1u);
-  if (i >= w.cap_copy) { raise_err(&w.ctr->err, ERR_CAPACITY); return false; }
-  w.copy[i] = CopyTask{x, n};
-  return true;
-}
-__device__ __forceinline__ bool emit_patch(const Work& w, uint32_t p) {
-  const uint32_t i = atomicAdd(&w.ctr->npatch, 1u);
-  if (i >= w.cap_patch) { raise_err(&w.ctr->err, ERR_CAPACITY); return false; }
-  w.patch[i] = p;
-  return true;
-}
-
-// One wavefront per multi-group update. The header / descent logic runs uniformly on every lane
-// (lane 0 stores); the group-to-group jumps of a long section are speculated 64 groups at a time:
-// lane j takes the exit S_j of the chain that starts at its group's first byte; the true chain
-// enters group j+1 at S_j as soon as it has synchronised with that chain inside group j, which
-// lane j checks by looking up the exit of its (true) entry. The first lane that fails still knows
-// its true exit, so a failed speculation costs one group, exactly the sequential step.
-__global__ __launch_bounds__(64) void k_walker(Work w) {
-  if (blockIdx.x >= w.nbig) return;
-  const uint32_t u = w.ulist[blockIdx.x];
-  const uint32_t lane = threadIdx.x;
-  if (w.ulen[u] > 0 && w.ulen[u] <= GROUP_BYTES) return;  // walked inside k_tables
-  const uint8_t* __restrict__ b = w.bytes;
-  const Tables& T = w.tab;
-  const uint32_t ustart = w.uoff[u];
-  const uint32_t uend = ustart + w.ulen[u];
-  const uint32_t ngu = (w.ulen[u] + GROUP_BYTES - 1) / GROUP_BYTES;
-  uint32_t* err = &w.ctr->err;
-  const bool L0 = lane == 0;
-  if (L0) w.dsstart[u] = NONE;
-  uint32_t p = ustart;
-  bool ok = true;
-  const uint32_t nsec = rd_vu(b, p, uend, ok);
-  if (!ok || nsec > (uend - p) / 3 + 1) { if (L0) raise_err(err, ERR_DECODE); return; }
-  uint32_t sbase = 0;
-  if (L0) sbase = atomicAdd(&w.ctr->nsections, nsec);
-  sbase = __shfl(sbase, 0);
-  if (sbase + nsec > w.cap_sections) { if (L0) raise_err(err, ERR_CAPACITY); return; }
-  if (L0) { w.usec_start[u] = sbase; w.usec_n[u] = nsec; }
-  for (uint32_t sct = 0; sct < nsec; ++sct) {
-    const uint32_t n = rd_vu(b, p, uend, ok);
-    const uint32_t client = rd_vu(b, p, uend, ok);
-    const uint32_t clock = rd_vu(b, p, uend, ok);
-    if (!ok || n > uend - p) { if (L0) raise_err(err, ERR_DECODE); return; }
-    if (L0) {
-      Section sec;
-      sec.upd = u; sec.n = n; sec.client = client; sec.clock = clock;
-      sec.first_pos = n ? p : NONE; sec.cidx = NONE; sec.first_idx = NONE; sec.pad = 0;
-      w.sections[sbase + sct] = sec;
-      if (n) atomicOr((unsigned long long*)&w.sec_bits[p >> 6], 1ull << (p & 63));
-    }
-    uint32_t r = n;
-    while (r > 0) {
-      if (p >= uend) { if (L0) raise_err(err, ERR_DECODE); return; }
-      bool exact = false;
-      if (T.gcnt[p] < r) {  // the section continues past this group: speculate 64 groups ahead
-        const uint32_t gi = (p - ustart) / GROUP_BYTES + lane;
-        uint32_t S = NONE;
-        if (gi < ngu) {
-          const uint32_t gs = ustart + gi * GROUP_BYTES;
-          const uint32_t x = T.gexit[gs];
-          if (!(x & STOPF)) S = gs + (x & 0x7FFFu);
-        }
-        uint32_t E = __shfl_up(S, 1);
-        if (lane == 0) E = p;
-        uint32_t X = NONE, C = 0;
-        bool stop = true;
-        if (E != NONE && E < uend && gi < ngu) {
-          const uint32_t ge = T.gexit[E];
-          C = T.gcnt[E];
-          X = E + (ge & 0x7FFFu);
-          stop = (ge & STOPF) != 0;
-        }
-        const bool good = !stop && X == S;
-        const uint64_t bad = __ballot(!good);
-        const uint32_t f = bad ? (uint32_t)__ffsll((long long)bad) - 1 : 63u;  // lanes 0..f hold true entries
-        // inclusive count scan over lanes 0..f
-        uint32_t incl = lane <= f ? C : 0u;
-        for (uint32_t off = 1; off < 64; off <<= 1) {
-          const uint32_t v = __shfl_up(incl, off);
-          if (lane >= off) incl += v;
-        }
-        const uint32_t excl = incl - (lane <= f ? C : 0u);
-        const uint64_t ends = __ballot(lane <= f && incl >= r);
-        if (ends) {  // the section ends in the group of lane j
-          const uint32_t j = (uint32_t)__ffsll((long long)ends) - 1;
-          if (lane < j && C && !emit_seg(w, E, C)) return;
-          r -= __shfl(excl, j);
-          p = __shfl(E, j);
-        } else {
-          if (lane <= f && C && !emit_seg(w, E, C)) return;
-          r -= __shfl(incl, f);
-          p = __shfl(X, f);
-          exact = __shfl(stop ? 1u : 0u, f) != 0;
-          if (p == NONE) { if (L0) raise_err(err, ERR_DECODE); return; }
-          if (!exact) continue;
-        }
-      }
-      if (!exact) {  // the section ends inside this group: descend block -> chunk -> struct
-        uint32_t rr = r;
-        for (;;) {
-          const uint32_t be = T.bexit[p], bc = T.bcnt[p];
-          if ((be & STOPF) || bc >= rr) break;
-          if (L0 && !emit_seg(w, p, bc)) return;
-          rr -= bc;
-          p += be;
-        }
-        for (;;) {
-          const uint32_t ce = T.cexit[p], cc = T.ccnt[p];
-          if ((ce & STOPF) || cc >= rr) break;
-          if (L0 && !emit_seg(w, p, cc)) return;
-          rr -= cc;
-          p += ce;
-        }
-        while (rr > 0) {
-          const uint32_t d = T.nxt[p];
-          if (d == 1) { exact = true; break; }
-          if (d == 0) { if (L0) raise_err(err, ERR_DECODE); return; }
-          if (L0 && !emit_patch(w, p)) return;
-          p += d;
-          --rr;
-        }
-        r = rr;
-      }
-      if (exact && r > 0) {  // a struct the tables could not size: parse it exactly
-        if (L0 && !emit_patch(w, p)) return;
-        uint32_t q = p;
-        if (parse_struct<false>(b, q, uend, 0xFFFFFFFFu, nullptr) <= 0) { if (L0) { raise_err(err, ERR_DECODE); w.ctr->err_info = p; } return; }
-        p = q;
-        --r;
-      }
-    }
-  }
-  if (L0) w.dsstart[u] = p;
-}
-
 // Direct path: one lane per small update parses it exactly, struct by struct, and writes the
 // update's struct-start words of the final bitmap itself (updates are 64-byte aligned, so the
 // words are the lane's own: plain stores, each word once, as the lane moves forward). Each lane
@@ -714,90 +246,274 @@ __global__ __launch_bounds__(DL) void k_direct(Work w) {
   w.dsstart[u] = p;
 }
 
-void launch_walker(const Work& w, hipStream_t s) {
-  if (w.nbig) hipLaunchKernelGGL(k_walker, dim3(w.nbig), dim3(64), 0, s, w);
+
+// --------------------------------------------------------------------------- 1'. chunk chains
+// Struct length at p on the all-struct chain, 0 where no struct parses (the chain then steps one
+// byte). The chunk chains and the walker use this one function, so chains that meet stay together.
+template <class S>
+__device__ __forceinline__ uint32_t chain_len(const S& src, const uint8_t* __restrict__ b, uint32_t p, uint32_t uend) {
+  const uint32_t info = src.u8(p), ref = info & 31u;
+  uint32_t d = 0;
+  if (ref == REF_GC || ref == REF_SKIP) {
+    uint32_t q = p + 1;
+    bool okv = true;
+    vu_fast(src, q, uend, okv);
+    d = okv ? q - p : 0u;
+  } else if (ref >= 1 && ref <= REF_DOC) {
+    d = spec_len(src, p, uend, (ref - 1) * 8 + (info >> 5));
+    if (d == 1) d = exact_len(b, p, uend);  // handed over (long / deep / Doc)
+  }
+  return d;
+}
+struct GlobalSrc {
+  const uint8_t* __restrict__ b;
+  __device__ __forceinline__ uint32_t u8(uint32_t p) const { return b[p]; }
+  __device__ __forceinline__ uint64_t w8(uint32_t p) const { return win8(b, p); }
+};
+__device__ __forceinline__ uint32_t chain_step(const uint8_t* __restrict__ b, uint32_t p, uint32_t uend) {
+  const uint32_t d = chain_len(GlobalSrc{b}, b, p, uend);
+  return p + (d ? d : 1u);
+}
+
+// One lane per chunk (SCHUNK bytes of a large update): the chain from the chunk's first byte, every
+// visited position inside the chunk set in spec_bits (the lane owns the chunk's words: chunks and
+// updates are 64-byte aligned) and the first position at / past the chunk end in cexit. The bytes
+// come through the lane's LDS window, as in k_direct.
+__global__ __launch_bounds__(DL) void k_spec(Work w) {
+  __shared__ __attribute__((aligned(16))) uint32_t win[DL * DSTRIDE];
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= w.ngroups) return;
+  const Group G = w.groups[i];
+  const uint8_t* __restrict__ b = w.bytes;
+  const uint32_t uend = G.uend;
+  uint32_t* slot = win + threadIdx.x * DSTRIDE;
+  LdsSrc src{b, slot, 0, 0};
+  auto refill = [&](uint32_t p) {
+    src.s0 = p & ~15u;
+    src.wlen = min(DW, (uend + 15u - src.s0) & ~15u);
+    const uint4* g = (const uint4*)(b + src.s0);
+    for (uint32_t k = 0; k < src.wlen / 16; ++k) ((uint4*)slot)[k] = g[k];
+  };
+  uint64_t* __restrict__ spec = w.spec_bits;
+  uint32_t p = G.start, word = G.start >> 6;
+  uint64_t m = 0;
+  refill(p);
+  while (p < G.end) {
+    if ((p >> 6) != word) {
+      spec[word] = m;
+      m = 0;
+      while (++word < (p >> 6)) spec[word] = 0;
+    }
+    m |= 1ull << (p & 63);
+    if (p - src.s0 + DREFILL > src.wlen) refill(p);
+    const uint32_t d = chain_len(src, b, p, uend);
+    p += d ? d : 1u;
+  }
+  const uint32_t wend = (G.end + 63) >> 6;
+  spec[word] = m;
+  while (++word < wend) spec[word] = 0;
+  w.cexit[i] = p;
+}
+
+// One lane per chunk re-enters it where the previous chunk's chain leaves (xin of chunk j-1): from
+// there the chain is followed until it meets the chunk's own chain, and the chunk's words of
+// spec_bits are rewritten to that one chain (walked positions, then the own chain from the meeting
+// point); its exit goes to xout. A chain meets the true struct sequence within ~100 bytes of its
+// start in the median (C2 snapshots: 90 % within 400 bytes), so after one round nearly every
+// chunk's chain is the true sequence from its first struct on; a second round (xin / xout
+// swapped) re-enters the few chunks behind a chunk whose chain had not met it, and the walker
+// finds its entries on the chains. A chunk the chain jumps over entirely (one long struct) gets no
+// positions. The first chunk of an update keeps its chain (the walker enters it after the update /
+// section headers).
+__global__ __launch_bounds__(256) void k_sync(Work w, const uint32_t* __restrict__ xin, uint32_t* __restrict__ xout) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= w.ngroups) return;
+  const Group G = w.groups[i];
+  uint32_t X = xin[i];
+  if (G.start != w.uoff[G.upd]) {  // chunks of one update are consecutive
+    const uint8_t* __restrict__ b = w.bytes;
+    uint64_t* __restrict__ spec = w.spec_bits;
+    const uint32_t E = xin[i - 1];
+    uint32_t q = E, word = G.start >> 6;
+    uint64_t m = 0;
+    while (q < G.end && !((spec[q >> 6] >> (q & 63)) & 1ull)) {
+      while ((q >> 6) != word) { spec[word] = m; m = 0; ++word; }
+      m |= 1ull << (q & 63);
+      q = chain_step(b, q, G.uend);
+    }
+    if (q < G.end) {  // met the own chain at q: keep its positions from q on
+      while ((q >> 6) != word) { spec[word] = m; m = 0; ++word; }
+      spec[word] = m | (spec[word] & (~0ull << (q & 63)));
+    } else {
+      const uint32_t wend = (G.end + 63) >> 6;
+      for (; word < wend; ++word) { spec[word] = m; m = 0; }
+      X = q;
+    }
+  }
+  xout[i] = X;
+}
+
+// ---- bitmap ranges [a, e) (e > a): count, OR into the final bitmap, and select
+__device__ __forceinline__ uint64_t range_word(const uint64_t* __restrict__ bits, uint32_t wd, uint32_t a, uint32_t e) {
+  uint64_t x = bits[wd];
+  if (wd == (a >> 6)) x &= ~0ull << (a & 63);
+  if (wd == ((e - 1) >> 6)) x &= ~0ull >> (63 - ((e - 1) & 63));
+  return x;
+}
+__device__ __forceinline__ uint32_t popc_range(const uint64_t* __restrict__ bits, uint32_t a, uint32_t e) {
+  uint32_t n = 0;
+  if (a < e)
+    for (uint32_t wd = a >> 6; wd <= (e - 1) >> 6; ++wd) n += (uint32_t)__popcll(range_word(bits, wd, a, e));
+  return n;
+}
+__device__ __forceinline__ void or_range(uint64_t* __restrict__ fin, const uint64_t* __restrict__ bits, uint32_t a, uint32_t e) {
+  if (a < e)
+    for (uint32_t wd = a >> 6; wd <= (e - 1) >> 6; ++wd) {
+      const uint64_t x = range_word(bits, wd, a, e);
+      if (x) atomicOr((unsigned long long*)&fin[wd], (unsigned long long)x);
+    }
+}
+// the n-th (n >= 1) set bit at or after a (the caller has counted at least n)
+__device__ __forceinline__ uint32_t select_from(const uint64_t* __restrict__ bits, uint32_t a, uint32_t n) {
+  uint32_t wd = a >> 6;
+  uint64_t x = bits[wd] & (~0ull << (a & 63));
+  for (;;) {
+    const uint32_t c = (uint32_t)__popcll(x);
+    if (c >= n) break;
+    n -= c;
+    x = bits[++wd];
+  }
+  for (uint32_t k = 1; k < n; ++k) x &= x - 1;
+  return wd * 64 + (uint32_t)__ffsll((long long)x) - 1;
+}
+// cnt true structs from x, set in the final bitmap (sections of one update may share a word);
+// returns the position after the last
+__device__ __forceinline__ uint32_t mark_exact(const Work& w, uint32_t x, uint32_t cnt, uint32_t uend) {
+  uint32_t word = NONE;
+  uint64_t m = 0;
+  for (uint32_t k = 0; k < cnt; ++k) {
+    if ((x >> 6) != word) {
+      if (m) atomicOr((unsigned long long*)&w.final_bits[word], (unsigned long long)m);
+      word = x >> 6;
+      m = 0;
+    }
+    m |= 1ull << (x & 63);
+    x = chain_step(w.bytes, x, uend);
+  }
+  if (m) atomicOr((unsigned long long*)&w.final_bits[word], (unsigned long long)m);
+  return x;
+}
+
+// One wavefront per large update follows its true struct sequence through the section headers.
+// Per step lane j takes chunk cj + j (cj = the chunk of the current position p): its entry E is p
+// (lane 0) or the chain exit of the previous chunk; it parses exactly from E until it meets its
+// chunk's chain (then the rest of the chunk's true structs are the chain's positions: a popcount)
+// or leaves the chunk. Lanes up to the first one whose true exit differs from its chain's exit
+// have true entries; the step takes their chunks, or stops in the chunk where the section ends.
+__global__ __launch_bounds__(64) void k_walk(Work w) {
+  if (blockIdx.x >= w.nbig) return;
+  const uint32_t u = w.ulist[blockIdx.x];
+  const uint32_t lane = threadIdx.x;
+  const uint8_t* __restrict__ b = w.bytes;
+  const uint64_t* __restrict__ spec = w.spec_bits;
+  const uint32_t ustart = w.uoff[u], uend = ustart + w.ulen[u];
+  const uint32_t c0 = w.ugroup[u], nch = (w.ulen[u] + SCHUNK - 1) / SCHUNK;
+  uint32_t* err = &w.ctr->err;
+  const bool L0 = lane == 0;
+  if (L0) w.dsstart[u] = NONE;
+  if (w.ulen[u] == 0) { if (L0) raise_err(err, ERR_DECODE); return; }
+  uint32_t p = ustart;
+  bool ok = true;
+  const uint32_t nsec = rd_vu(b, p, uend, ok);
+  if (!ok || nsec > (uend - p) / 3 + 1) { if (L0) raise_err(err, ERR_DECODE); return; }
+  uint32_t sbase = 0;
+  if (L0) sbase = atomicAdd(&w.ctr->nsections, nsec);
+  sbase = __shfl(sbase, 0);
+  if (sbase + nsec > w.cap_sections) { if (L0) raise_err(err, ERR_CAPACITY); return; }
+  if (L0) { w.usec_start[u] = sbase; w.usec_n[u] = nsec; }
+  for (uint32_t sct = 0; sct < nsec; ++sct) {
+    const uint32_t n = rd_vu(b, p, uend, ok);
+    const uint32_t client = rd_vu(b, p, uend, ok);
+    const uint32_t clock = rd_vu(b, p, uend, ok);
+    if (!ok || n > uend - p) { if (L0) raise_err(err, ERR_DECODE); return; }
+    if (L0) {
+      Section sec;
+      sec.upd = u; sec.n = n; sec.client = client; sec.clock = clock;
+      sec.first_pos = n ? p : NONE; sec.cidx = NONE; sec.first_idx = NONE; sec.pad = 0;
+      w.sections[sbase + sct] = sec;
+      if (n) atomicOr((unsigned long long*)&w.sec_bits[p >> 6], 1ull << (p & 63));
+    }
+    uint32_t r = n;
+    while (r > 0) {
+      if (p >= uend) { if (L0) { raise_err(err, ERR_DECODE); w.ctr->err_info = p; } return; }
+      const uint32_t j = (p - ustart) / SCHUNK + lane;
+      const bool valid = j < nch;
+      const uint32_t ce = valid ? min(ustart + (j + 1) * SCHUNK, uend) : 0u;
+      const uint32_t S = valid ? w.cexit[c0 + j] : NONE;  // after the two k_sync rounds
+      uint32_t E = __shfl_up(S, 1);
+      if (L0) E = p;
+      uint32_t q = E, k = 0;
+      bool merged = false;
+      if (valid) {
+        while (q < ce && !((spec[q >> 6] >> (q & 63)) & 1ull)) { q = chain_step(b, q, uend); ++k; }
+        merged = q < ce;
+      }
+      const uint32_t C = k + (merged ? popc_range(spec, q, ce) : 0u);
+      const uint32_t X = merged ? S : q;  // the true exit, given the entry
+      const uint64_t bad = __ballot(!(valid && X == S));
+      const uint32_t f = bad ? (uint32_t)__ffsll((long long)bad) - 1 : 63u;  // lanes 0..f hold true entries
+      uint32_t incl = lane <= f ? C : 0u;
+      for (uint32_t off = 1; off < 64; off <<= 1) {
+        const uint32_t v = __shfl_up(incl, off);
+        if (lane >= off) incl += v;
+      }
+      const uint32_t excl = incl - (lane <= f ? C : 0u);
+      const uint64_t ends = __ballot(lane <= f && valid && incl >= r);
+      if (ends) {  // the section ends in lane jl's chunk
+        const uint32_t jl = (uint32_t)__ffsll((long long)ends) - 1;
+        uint32_t np = 0;
+        if (lane < jl) {
+          mark_exact(w, E, k, uend);
+          if (merged) or_range(w.final_bits, spec, q, ce);
+        } else if (lane == jl) {
+          const uint32_t rr = r - excl;
+          if (rr <= k) {
+            np = mark_exact(w, E, rr, uend);
+          } else {
+            mark_exact(w, E, k, uend);
+            const uint32_t L = select_from(spec, q, rr - k);
+            or_range(w.final_bits, spec, q, L + 1);
+            np = chain_step(b, L, uend);
+          }
+        }
+        p = __shfl(np, jl);
+        r = 0;
+      } else {
+        if (lane <= f) {
+          mark_exact(w, E, k, uend);
+          if (merged) or_range(w.final_bits, spec, q, ce);
+        }
+        r -= __shfl(incl, f);
+        p = __shfl(X, f);  // NONE / past the update when the section runs past its end
+      }
+    }
+  }
+  if (L0) w.dsstart[u] = p;
+}
+
+void launch_chunks(const Work& w, hipStream_t s) {
+  if (w.ngroups) hipLaunchKernelGGL(k_spec, dim3((w.ngroups + DL - 1) / DL), dim3(DL), 0, s, w);
+  if (w.ngroups) {
+    hipLaunchKernelGGL(k_sync, dim3((w.ngroups + 255) / 256), dim3(256), 0, s, w, (const uint32_t*)w.cexit, w.sexit);
+    hipLaunchKernelGGL(k_sync, dim3((w.ngroups + 255) / 256), dim3(256), 0, s, w, (const uint32_t*)w.sexit, w.cexit);
+  }
+  if (w.nbig) hipLaunchKernelGGL(k_walk, dim3(w.nbig), dim3(64), 0, s, w);
 }
 void launch_direct(const Work& w, hipStream_t s) {
   if (w.nsmall) hipLaunchKernelGGL(k_direct, dim3((w.nsmall + DL - 1) / DL), dim3(DL), 0, s, w);
 }
 
-// --------------------------------------------------------------------------- 3. final bitmap
-// One wavefront per verified segment (x, n): block hops by lane 0, chunk hops by one lane per
-// block, then one lane per chunk walks nxt inside its 64-byte chunk and sets the bits of that
-// chunk's bitmap word with a single atomicOr.
-__global__ __launch_bounds__(256) void k_mark(Work w) {
-  __shared__ uint32_t s_bx[4][16], s_bn[4][16];          // block spans per wave
-  __shared__ uint32_t s_cx[4][256], s_cn[4][256];        // chunk spans per wave
-  __shared__ uint32_t s_nb[4], s_nc[4][16];
-  const uint32_t wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const uint32_t nseg = min(w.ctr->ncopy, w.cap_copy);  // read on the device: no host sync
-  // block-stride loop; the trip count depends on blockIdx only, so every wave reaches the barriers
-  for (uint32_t blk = blockIdx.x; blk * 4 < nseg; blk += gridDim.x) {
-  const uint32_t si = blk * 4 + wv;
-  const bool active = si < nseg;
-  CopyTask S{0, 0};
-  if (active) S = w.copy[si];
-  const Tables& T = w.tab;
-  if (lane == 0) {  // block spans of the segment (segments never cross a group)
-    uint32_t x = S.a, left = active ? S.b : 0, nb = 0;
-    while (left > 0 && nb < 16) {
-      const uint32_t take = min((uint32_t)T.bcnt[x], left);
-      s_bx[wv][nb] = x;
-      s_bn[wv][nb] = take;
-      ++nb;
-      left -= take;
-      if (left) x += T.bexit[x] & 0x7FFFu;
-    }
-    s_nb[wv] = nb;
-  }
-  __syncthreads();
-  const uint32_t nb = s_nb[wv];
-  if (lane < nb) {
-    uint32_t x = s_bx[wv][lane], left = s_bn[wv][lane], nc = 0;
-    while (left > 0 && nc < 16) {
-      const uint32_t cc = T.ccnt[x];
-      const uint32_t take = min(cc, left);
-      s_cx[wv][lane * 16 + nc] = x; s_cn[wv][lane * 16 + nc] = take; ++nc;
-      left -= take;
-      if (left) x += T.cexit[x] & 0x7FFFu;
-    }
-    s_nc[wv][lane] = nc;
-  }
-  __syncthreads();
-  for (uint32_t k = lane; k < nb * 16; k += 64) {
-    const uint32_t bi = k >> 4, ci = k & 15;
-    if (ci >= s_nc[wv][bi]) continue;
-    uint32_t x = s_cx[wv][k], left = s_cn[wv][k];
-    uint64_t m = 0;
-    const uint32_t word = x >> 6;
-    while (left > 0) {
-      m |= 1ull << (x & 63);
-      const uint32_t d = T.nxt[x];
-      x += d == 0 ? 1 : d;
-      --left;
-    }
-    atomicOr((unsigned long long*)&w.final_bits[word], (unsigned long long)m);
-  }
-  __syncthreads();  // the LDS span lists are reused by the next iteration
-  }
-}
-__global__ void k_patch(const uint32_t* __restrict__ patch, const uint32_t* __restrict__ npatch, uint32_t cap, uint64_t* __restrict__ final_bits) {
-  const uint32_t n = min(*npatch, cap);
-  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
-    const uint32_t p = patch[i];
-    atomicOr((unsigned long long*)&final_bits[p >> 6], 1ull << (p & 63));
-  }
-}
-
-// segment / patch counts are read on the device (grid-stride), so the walker needs no host sync
-void launch_build_final_bits(const Work& w, hipStream_t s) {
-  const uint32_t grid = std::min<uint32_t>(w.ngroups * 4 + 64, 8192);
-  hipLaunchKernelGGL(k_mark, dim3(grid), dim3(256), 0, s, w);
-  hipLaunchKernelGGL(k_patch, dim3(std::min<uint32_t>(w.ngroups * 4 + 64, 4096)), dim3(256), 0, s, w.patch, &w.ctr->npatch,
-                     w.cap_patch, w.final_bits);
-}
-
-// --------------------------------------------------------------------------- 4. struct positions
+// --------------------------------------------------------------------------- 3. struct positions
 __global__ void k_popc(const uint64_t* __restrict__ bits, uint32_t* __restrict__ cnt, uint32_t nwords) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i < nwords) cnt[i] = (uint32_t)__popcll(bits[i]);
@@ -1068,6 +784,20 @@ void launch_client_table(Work& w, uint32_t nsections, hipStream_t s) {
   hipLaunchKernelGGL(k_unique_scatter, dim3(grid), dim3(256), 0, s, w.cl_vals, w.cl_tmp, nsections, w.cl_state, &w.ctr->nclients);
   hipMemcpyAsync(w.cl_vals, w.cl_state, sizeof(uint32_t) * nsections, hipMemcpyDeviceToDevice, s);
   hipLaunchKernelGGL(k_section_cidx, dim3(grid), dim3(256), 0, s, w.sections, nsections, w.cl_vals, &w.ctr->nclients);
+}
+
+// the client hash (find_client), from the finished client table; slots were filled with ~0
+__global__ void k_client_hash(Work w, uint64_t* __restrict__ key, uint32_t* __restrict__ val, uint32_t mask) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= w.ctr->nclients) return;
+  const uint64_t k = w.udoc ? w.cl_key[i] : (uint64_t)w.cl_vals[i];
+  for (uint32_t slot = (uint32_t)client_hash(k) & mask;; slot = (slot + 1) & mask) {
+    const unsigned long long old = atomicCAS((unsigned long long*)&key[slot], ~0ull, (unsigned long long)k);
+    if (old == ~0ull || old == k) { val[slot] = i; return; }  // keys are distinct
+  }
+}
+void launch_client_hash(const Work& w, uint64_t* key, uint32_t* val, uint32_t mask, hipStream_t s) {
+  hipLaunchKernelGGL(k_client_hash, dim3((mask + 1) / 512 + 1), dim3(256), 0, s, w, key, val, mask);
 }
 
 // --------------------------------------------------------------------------- 6. struct decode

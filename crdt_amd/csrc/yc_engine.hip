@@ -127,8 +127,8 @@ bool parse_sv(const uint8_t* p, size_t n, std::unordered_map<uint32_t, uint32_t>
 }
 
 enum Buf {
-  B_BYTES, B_META, B_CTR, B_TNXT, B_TCEXIT, B_TCCNT, B_TBEXIT, B_TBCNT, B_TGEXIT, B_TGCNT, B_FINAL, B_SECB, B_COPY,
-  B_PATCH, B_DSSTART, B_SECT, B_SECSORT,
+  B_BYTES, B_META, B_CTR, B_SPECB, B_CEXIT, B_SEXIT, B_FINAL, B_SECB,
+  B_DSSTART, B_SECT, B_SECSORT,
   B_WCNT, B_WSEC, B_DS, B_DSTMP, B_DSREG, B_DSCNT, B_DSOFF, B_DSLEN, B_DSSCAN, B_SCRATCH, B_TMP,
   B_SPOS, B_SSEC, B_SLEN, B_SLENSCAN, B_SCLOCK, B_SCIDX, B_SINFO, B_SOC, B_SOK, B_SRC, B_SRK, B_SPA, B_SPB, B_SPS, B_SPL,
   B_SCPOS, B_SCEND, B_SCELEM,
@@ -146,7 +146,7 @@ enum Buf {
   B_TPRV, B_TMPRV, B_TMTAIL, B_TTREP, B_TOTAIL,
   B_OFIRST, B_OCIDX, B_OSIZE, B_OPOS, B_RSEG, B_RLEN, B_RSIZE, B_RPOS, B_OUT, B_SVOUT,
   B_VKMAP, B_VKREP, B_VKEYS, B_VNKEYS, B_VPOS, B_VD0, B_VN0, B_VD1, B_VN1, B_VORDER, B_VSEGS,
-  B_SCRATCH2, B_TMP2, B_CAPS, B_CLKEY, B_CLKEY2, B_CLDOC, B_DSFA, B_EMIT, B_DOCRNG, B_KSHARD, B_SOWNER, B_GFLAGS0, B_GFACC,
+  B_SCRATCH2, B_TMP2, B_CAPS, B_CLKEY, B_CLKEY2, B_CHKEY, B_CHVAL, B_CLDOC, B_DSFA, B_EMIT, B_DOCRNG, B_KSHARD, B_SOWNER, B_GFLAGS0, B_GFACC,
   B_COUNT
 };
 
@@ -253,12 +253,12 @@ void mark(ycrdt_engine* e, const char* name) {
   e->marks.push_back({name, ev});
 }
 
-// Small updates are parsed directly, one lane per update walking its structs exactly (no speculative
-// tables), when there are many of them: a wavefront then parses 64 updates side by side and the
-// batch is read about once. A few small updates, and every large one, take the table path
-// (k_parse / k_tables / k_walker), whose latency does not grow with the update. YCRDT_DECODE=
-// tables|direct forces one path for small updates (tests cover both).
-constexpr size_t DIRECT_MAX_BYTES = GROUP_BYTES;  // an update the direct lane walks whole
+// Small updates are parsed directly, one lane per update walking its structs exactly, when there
+// are many of them: a wavefront then parses 64 updates side by side and the batch is read about
+// once. A few small updates, and every large one, take the chunk path (k_spec / k_walk), whose
+// latency grows with the update only by one wavefront step per 64 KiB. YCRDT_DECODE=chunks|direct
+// forces one path for small updates (tests cover both; "tables" is the older name of "chunks").
+constexpr size_t DIRECT_MAX_BYTES = 16384;         // an update the direct lane walks whole
 constexpr size_t DIRECT_TINY_BYTES = 1024;         // always direct (a handful of structs)
 constexpr size_t DIRECT_MIN_COUNT = 1024;          // enough small updates to fill wavefronts
 
@@ -275,7 +275,7 @@ void layout(ycrdt_batch* b, const std::vector<Src>& src, std::vector<uint32_t>& 
   b->uoff.clear(); b->ulen.clear(); b->ugroup.clear(); b->groups.clear(); b->ulist.clear();
   b->in_bytes = 0;
   const char* mode = getenv("YCRDT_DECODE");
-  const int force = mode && !strcmp(mode, "tables") ? 1 : mode && !strcmp(mode, "direct") ? 2 : 0;
+  const int force = mode && (!strcmp(mode, "chunks") || !strcmp(mode, "tables")) ? 1 : mode && !strcmp(mode, "direct") ? 2 : 0;
   size_t nsmall = 0;
   for (const Src& x : src) nsmall += x.len <= DIRECT_MAX_BYTES;
   auto direct = [&](size_t len) {
@@ -298,10 +298,10 @@ void layout(ycrdt_batch* b, const std::vector<Src>& src, std::vector<uint32_t>& 
     } else {
       b->ugroup.push_back((uint32_t)b->groups.size());
       b->ulist.push_back(u);
-      for (size_t g = 0; g < len; g += GROUP_BYTES) {
+      for (size_t g = 0; g < len; g += SCHUNK) {
         Group G;
         G.start = (uint32_t)(off + g);
-        G.end = (uint32_t)std::min(off + len, off + g + GROUP_BYTES);
+        G.end = (uint32_t)std::min(off + len, off + g + SCHUNK);
         G.uend = (uint32_t)(off + len);
         G.upd = u;
         b->groups.push_back(G);
@@ -450,30 +450,20 @@ int run_decode(ycrdt_engine* e, ycrdt_batch* b, bool lazy, Decoded& D, bool gene
   w.lazy = lazy ? 1u : 0u;
   const uint64_t B = (uint64_t)b->nbytes + 64;
   const uint64_t nwords = B / 64 + 2;
-  // The walker's outputs are sized from estimates (a capacity overflow reruns the decode with the
-  // worst-case bounds); the struct table, the client table and the delete-set ranges are sized
+  // The section table is sized from an estimate (a capacity overflow reruns the decode with the
+  // worst-case bound); the struct table, the client table and the delete-set ranges are sized
   // after the count sync from the real counts, so the workspace follows the content, not B.
   const uint64_t est_sec = generous ? B / 3 + 64 : std::min<uint64_t>(B / 3 + 64, (uint64_t)nu * 16 + B / 256 + 4096);
-  const uint64_t est_copy = generous ? w.ngroups + B / 2 + 64 : std::min<uint64_t>(w.ngroups + B / 2 + 64, (uint64_t)w.ngroups * 64 + B / 16 + 4096);
-  const uint64_t est_patch = generous ? B / 2 + 64 : std::min<uint64_t>(B / 2 + 64, B / 16 + 4096);
   w.cap_sections = (uint32_t)est_sec;
-  w.cap_copy = (uint32_t)est_copy;
-  w.cap_patch = (uint32_t)est_patch;
   w.cap_structs = 0;
   w.cap_ds = 0;
   // ---- decode buffers
   w.ctr = take<Counters>(V, B_CTR, 1, ok);
-  w.tab.nxt = take<uint16_t>(V, B_TNXT, B, ok);
-  w.tab.cexit = take<uint16_t>(V, B_TCEXIT, B, ok);
-  w.tab.ccnt = take<uint8_t>(V, B_TCCNT, B, ok);
-  w.tab.bexit = take<uint16_t>(V, B_TBEXIT, B, ok);
-  w.tab.bcnt = take<uint16_t>(V, B_TBCNT, B, ok);
-  w.tab.gexit = take<uint16_t>(V, B_TGEXIT, B, ok);
-  w.tab.gcnt = take<uint16_t>(V, B_TGCNT, B, ok);
+  w.spec_bits = take<uint64_t>(V, B_SPECB, nwords, ok);
+  w.cexit = take<uint32_t>(V, B_CEXIT, (uint64_t)w.ngroups + 1, ok);
+  w.sexit = take<uint32_t>(V, B_SEXIT, (uint64_t)w.ngroups + 1, ok);
   w.final_bits = take<uint64_t>(V, B_FINAL, nwords, ok);
   w.sec_bits = take<uint64_t>(V, B_SECB, nwords, ok);
-  w.copy = take<CopyTask>(V, B_COPY, w.cap_copy, ok);
-  w.patch = take<uint32_t>(V, B_PATCH, w.cap_patch, ok);
   w.dsstart = take<uint32_t>(V, B_DSSTART, nu + 1, ok);
   w.sections = take<Section>(V, B_SECT, w.cap_sections, ok);
   w.sec_sorted = take<uint32_t>(V, B_SECSORT, w.cap_sections, ok);
@@ -498,61 +488,19 @@ int run_decode(ycrdt_engine* e, ycrdt_batch* b, bool lazy, Decoded& D, bool gene
   fill_u32_multi({{(uint32_t*)w.ctr, sizeof(Counters) / 4, 0u},
                   {(uint32_t*)w.final_bits, (uint64_t)nwords * 2, 0u},
                   {(uint32_t*)w.sec_bits, (uint64_t)nwords * 2, 0u}}, s);
+  static const bool dbg_yata = getenv("YCRDT_DEBUG_YATA") && getenv("YCRDT_DEBUG_YATA")[0] == '1';
+  w.dbg = dbg_yata ? take<unsigned long long>(V, B_DBG, 8, ok) : nullptr;
+  if (w.dbg) HIPCHK(hipMemsetAsync(w.dbg, 0, 64, s));
   // ---- K1 decode
-  mark(e, "decode.parse");
-  static const bool dbg_tables = getenv("YCRDT_DEBUG_TABLES") && getenv("YCRDT_DEBUG_TABLES")[0] == '1';
-  const size_t ndbg = (size_t)w.ngroups * 8 + (size_t)w.ngroups * (GROUP_BYTES / 4096) * 8 + 8;
-  w.dbg = dbg_tables ? take<unsigned long long>(V, B_DBG, ndbg, ok) : nullptr;
-  if (w.dbg) HIPCHK(hipMemsetAsync(w.dbg, 0, sizeof(unsigned long long) * ndbg, s));
-  launch_group_parse(w, s);
-  mark(e, "decode.tables");
-  launch_group_tables(w, s);
-  if (w.dbg) {
-    HIPCHK(hipStreamSynchronize(s));
-    std::vector<unsigned long long> h((size_t)w.ngroups * 8);
-    HIPCHK(hipMemcpy(h.data(), w.dbg, sizeof(unsigned long long) * h.size(), hipMemcpyDeviceToHost));
-    double acc[8] = {0};
-    uint32_t n = 0;
-    for (uint32_t g = 0; g < w.ngroups; ++g) {
-      if (!h[g * 8 + 5]) continue;  // multi-group path
-      ++n;
-      for (int k = 1; k <= 5; ++k) acc[k] += (double)(h[g * 8 + k] - h[g * 8 + k - 1]);
-    }
-    fprintf(stderr, "[ycrdt] k_tables cycles per group (%u single-group): stage %.0f  classify+count %.0f  parse %.0f  requeue+B %.0f  walk %.0f\n",
-            n, acc[1] / n, acc[2] / n, acc[3] / n, acc[4] / n, acc[5] / n);
-    // k_parse: per-slice phase cycles (wave 0) and the spread of slice lifetimes (wall clock, 100 MHz)
-    const size_t ns = (size_t)w.ngroups * (GROUP_BYTES / 4096);
-    std::vector<unsigned long long> q(ns * 8);
-    HIPCHK(hipMemcpy(q.data(), w.dbg + (size_t)w.ngroups * 8, sizeof(unsigned long long) * q.size(), hipMemcpyDeviceToHost));
-    double pa[6] = {0};
-    std::vector<std::pair<double, size_t>> life;
-    unsigned long long t0 = ~0ull, t1 = 0;
-    for (size_t i = 0; i < ns; ++i) {
-      if (!q[i * 8 + 6]) continue;
-      for (int k = 2; k <= 5; ++k) pa[k] += (double)(q[i * 8 + k] - q[i * 8 + k - 1]);
-      life.push_back({(double)(q[i * 8 + 6] - q[i * 8]), i});
-      t0 = std::min(t0, q[i * 8]); t1 = std::max(t1, q[i * 8 + 6]);
-    }
-    std::sort(life.begin(), life.end());
-    const size_t m = life.size();
-    if (m) {
-      fprintf(stderr, "[ycrdt] k_parse %zu slices: cycles pass1 %.0f  classes %.0f  tiles %.0f  queue %.0f | life us p50 %.2f p90 %.2f p99 %.2f max %.2f | span %.2f us\n",
-              m, pa[2] / m, pa[3] / m, pa[4] / m, pa[5] / m, life[m / 2].first / 100.0, life[m * 9 / 10].first / 100.0,
-              life[m * 99 / 100].first / 100.0, life[m - 1].first / 100.0, (double)(t1 - t0) / 100.0);
-      for (size_t j = m - 3; j < m && j < m; ++j) {
-        const size_t i = life[j].second;
-        fprintf(stderr, "[ycrdt]   slow slice %zu: %.2f us  nq %llu ntiles %llu  cycles %llu %llu %llu %llu\n", i, life[j].first / 100.0,
-                q[i * 8 + 7] >> 32, q[i * 8 + 7] & 0xFFFFFFFFull, q[i * 8 + 2] - q[i * 8 + 1], q[i * 8 + 3] - q[i * 8 + 2],
-                q[i * 8 + 4] - q[i * 8 + 3], q[i * 8 + 5] - q[i * 8 + 4]);
-      }
-    }
-  }
-  mark(e, "decode.walker");
-  launch_walker(w, s);
+  // large updates (chunk path, mostly latency-bound) on the side stream, beside k_direct
   mark(e, "decode.direct");
+  HIPCHK(hipEventRecord(e->side_fork, s));
+  HIPCHK(hipStreamWaitEvent(e->side, e->side_fork, 0));
+  launch_chunks(w, e->side);
+  HIPCHK(hipEventRecord(e->side_done, e->side));
   launch_direct(w, s);
+  HIPCHK(hipStreamWaitEvent(s, e->side_done, 0));
   mark(e, "decode.bitmap");
-  launch_build_final_bits(w, s);
   launch_struct_count(w, s);
   launch_ds_bound(w, s);
   HIPCHK(hipMemcpyAsync(&w.ctr->nstructs, w.wcnt + (w.nbytes + 63) / 64, sizeof(uint32_t), hipMemcpyDeviceToDevice, s));
@@ -589,6 +537,10 @@ int run_decode(ycrdt_engine* e, ycrdt_batch* b, bool lazy, Decoded& D, bool gene
   w.s_cend = take<uint32_t>(V, B_SCEND, w.cap_structs, ok);
   w.s_celem = take<uint32_t>(V, B_SCELEM, w.cap_structs, ok);
   w.cl_vals = take<uint32_t>(V, B_CLVALS, w.cap_clients + 1, ok);
+  w.ch_key = nullptr;  // find_client binary-searches until the hash is built below
+  const uint32_t ch_slots = (uint32_t)next_pow2(std::max<uint64_t>(2ull * (nsections + 1), 64));
+  uint64_t* ch_key = take<uint64_t>(V, B_CHKEY, ch_slots, ok);
+  uint32_t* ch_val = take<uint32_t>(V, B_CHVAL, ch_slots, ok);
   w.cl_key = take<uint64_t>(V, B_CLKEY, w.cap_clients + 1, ok);
   w.cl_key2 = take<uint64_t>(V, B_CLKEY2, w.cap_clients + 1, ok);
   w.cl_doc = take<uint32_t>(V, B_CLDOC, w.cap_clients + 1, ok);
@@ -611,7 +563,14 @@ int run_decode(ycrdt_engine* e, ycrdt_batch* b, bool lazy, Decoded& D, bool gene
     HIPCHK(hipEventRecord(e->side_done, e->side));
   }
   launch_section_clients(w, nsections, s);
-  if (nsections) launch_client_table(w, nsections, s);
+  if (nsections) {
+    launch_client_table(w, nsections, s);
+    fill_u32_multi({{(uint32_t*)ch_key, 2ull * ch_slots, 0xFFFFFFFFu}}, s);
+    launch_client_hash(w, ch_key, ch_val, ch_slots - 1, s);
+    w.ch_key = ch_key;
+    w.ch_val = ch_val;
+    w.ch_mask = ch_slots - 1;
+  }
   mark(e, "decode.structs");
   launch_struct_decode(w, nstructs, s);
   HIPCHK(hipMemsetAsync(w.cl_start, 0, sizeof(uint32_t) * (nsections + 1), s));
@@ -844,7 +803,7 @@ int run_merge(ycrdt_engine* e, ycrdt_batch* b, const std::unordered_map<uint32_t
       if (w.dbg && e->nlists) {
         unsigned long long h[3];
         HIPCHK(hipStreamSynchronize(s));
-        HIPCHK(hipMemcpy(h, w.dbg + (size_t)w.ngroups * 8 + (size_t)w.ngroups * (GROUP_BYTES / 4096) * 8, sizeof(h), hipMemcpyDeviceToHost));
+        HIPCHK(hipMemcpy(h, w.dbg, sizeof(h), hipMemcpyDeviceToHost));
         fprintf(stderr, "[ycrdt] k_yata: %u lists, %llu integrations, %llu conflict-scan steps, %llu stack dives\n", e->nlists, h[0], h[1], h[2]);
       }
       mark(e, "merge.merge_flags");

@@ -14,8 +14,6 @@ struct Counters {            // device-side counters, read back at the few host 
   uint32_t err;              // first error code (ERR_*)
   uint32_t err_info;         // position / index that raised it
   uint32_t nsections;        // appended by the walker
-  uint32_t ncopy;            // copy tasks
-  uint32_t npatch;           // desync patch positions
   uint32_t nds;              // decoded delete-set ranges
   uint32_t ndsclients;       // delete-set client headers
   uint32_t nstructs;         // S
@@ -49,44 +47,32 @@ struct DsRange {             // one decoded (client, clock, len) delete-set rang
   uint32_t upd;
 };
 
-// Per-byte chain tables (written by k_tables, read by the walker and k_mark). Exits are forward
-// deltas from the position; STOPF marks a chain that stops at a struct the tables did not size.
-struct Tables {
-  uint16_t* nxt = nullptr;         // struct length starting here (0 = no struct, 1 = unsized)
-  uint16_t* cexit = nullptr;       // first chain position at/after the end of this 64-byte chunk
-  uint8_t* ccnt = nullptr;         // chain positions visited before it
-  uint16_t* bexit = nullptr;       // ... 1 KiB block
-  uint16_t* bcnt = nullptr;
-  uint16_t* gexit = nullptr;       // ... 16 KiB group
-  uint16_t* gcnt = nullptr;
-};
-
 struct Work {
   // ---- batch input
   const uint8_t* bytes = nullptr;  // B bytes, every update starts at a 64-byte aligned offset
   uint32_t nbytes = 0;
   const uint32_t* uoff = nullptr;  // [nupd+1] update start offsets (aligned)
   const uint32_t* ulen = nullptr;  // [nupd] real update lengths
-  const uint32_t* ugroup = nullptr;// [nupd] first decode group of each update
+  const uint32_t* ugroup = nullptr;// [nupd] first decode chunk of each large update
   uint32_t nupd = 0;
   const uint32_t* udoc = nullptr;  // [nupd] document of every update (multi-document batches); nullptr = one doc
   uint32_t ndocs = 1;
-  const uint32_t* ulist = nullptr; // [nbig] updates on the table path, then [nsmall] parsed directly
+  const uint32_t* ulist = nullptr; // [nbig] updates on the chunk path, then [nsmall] parsed directly
   uint32_t nbig = 0, nsmall = 0;
   uint32_t lazy = 0;               // 1: mergeUpdates / diffUpdate decode (references kept raw)
-  unsigned long long* dbg = nullptr; // YCRDT_DEBUG_TABLES=1: per-group phase timestamps of k_tables
-  const Group* groups = nullptr;   // [G]
+  unsigned long long* dbg = nullptr; // YCRDT_DEBUG_YATA=1: k_yata work counters
+  const Group* groups = nullptr;   // [G] chunks of the large updates
   uint32_t ngroups = 0;
   // ---- capacities
-  uint32_t cap_structs = 0, cap_sections = 0, cap_copy = 0, cap_patch = 0, cap_ds = 0, cap_dsclients = 0;
+  uint32_t cap_structs = 0, cap_sections = 0, cap_ds = 0, cap_dsclients = 0;
   uint64_t cap_units = 0;
   // ---- decode
   Counters* ctr = nullptr;
-  Tables tab;                      // per-byte chain tables [B]
+  uint64_t* spec_bits = nullptr;   // [B/64] positions visited by the chunk chains (large updates)
+  uint32_t* cexit = nullptr;       // [G] first chain position at / past each chunk's end
+  uint32_t* sexit = nullptr;       // [G] the same after k_sync's first round (the second writes cexit)
   uint64_t* final_bits = nullptr;  // [B/64] verified struct starts
   uint64_t* sec_bits = nullptr;    // [B/64] first struct of every non-empty section
-  CopyTask* copy = nullptr;        // [cap_copy] verified chain segments (start, count)
-  uint32_t* patch = nullptr;       // [cap_patch]
   uint32_t* dsstart = nullptr;     // [nupd] byte position of the delete set
   Section* sections = nullptr;     // [cap_sections] (walker order)
   uint32_t* sec_sorted = nullptr;  // [cap_sections] section index by position rank
@@ -124,6 +110,9 @@ struct Work {
   uint32_t* cl_vals = nullptr;     // sorted distinct client ids [cap_sections]
   uint64_t* cl_key = nullptr;      // multi-doc: sorted distinct (doc << 32 | client) keys; cl_vals = their low words
   uint64_t* cl_key2 = nullptr;     // multi-doc sort scratch
+  uint64_t* ch_key = nullptr;      // client hash: (doc << 32 | client) per slot, ~0 = empty (null until built)
+  uint32_t* ch_val = nullptr;      // client hash: client index per slot
+  uint32_t ch_mask = 0;            // slots - 1 (a power of two >= 2 x the clients)
   uint32_t* cl_doc = nullptr;      // document of every client index (multi-doc)
   uint32_t* cl_tmp = nullptr;      // sort scratch [cap_sections]
   uint32_t* cl_state = nullptr;    // per client state (max end clock)
@@ -269,7 +258,22 @@ struct Work {
 
 // client index of (document, client id); NONE if the batch has no such client. Multi-document
 // batches index clients by (doc, client), so every per-client structure stays per document.
+__device__ __forceinline__ uint64_t client_hash(uint64_t k) {  // splitmix64 finaliser
+  k ^= k >> 30; k *= 0xBF58476D1CE4E5B9ull;
+  k ^= k >> 27; k *= 0x94D049BB133111EBull;
+  return k ^ (k >> 31);
+}
+// client index of (doc, client) or NONE: one or two probes of the client hash once it is built
+// (decode builds it right after the client table), a binary search over the sorted table before
 __device__ __forceinline__ uint32_t find_client(const Work& w, uint32_t nclients, uint32_t doc, uint32_t client) {
+  if (w.ch_key) {
+    const uint64_t key = w.udoc ? (((uint64_t)doc << 32) | client) : (uint64_t)client;
+    for (uint32_t slot = (uint32_t)client_hash(key) & w.ch_mask;; slot = (slot + 1) & w.ch_mask) {
+      const uint64_t k = w.ch_key[slot];
+      if (k == key) return w.ch_val[slot];
+      if (k == ~0ull) return NONE;
+    }
+  }
   if (!w.udoc) {
     const uint32_t i = lower_bound_u32(w.cl_vals, nclients, client);
     return (i < nclients && w.cl_vals[i] == client) ? i : NONE;
@@ -399,11 +403,9 @@ struct ViewBufs {
 void launch_view(const Work& w, const ViewBufs& v, uint32_t nsegs, uint32_t nlists, uint32_t narr, hipStream_t s);
 
 // ---- launch entry points (yc_decode.hip / yc_merge.hip / yc_encode.hip / yc_prims.hip)
-void launch_group_parse(const Work& w, hipStream_t s);   // k_parse: nxt at every byte
-void launch_group_tables(const Work& w, hipStream_t s);  // k_tables: chain exits (+ single-group walk)
-void launch_walker(const Work& w, hipStream_t s);
-void launch_direct(const Work& w, hipStream_t s);
-void launch_build_final_bits(const Work& w, hipStream_t s);
+void launch_chunks(const Work& w, hipStream_t s);  // k_spec + k_walk: large updates
+void launch_direct(const Work& w, hipStream_t s);  // k_direct: small updates
+void launch_client_hash(const Work& w, uint64_t* key, uint32_t* val, uint32_t mask, hipStream_t s);
 void launch_struct_count(const Work& w, hipStream_t s);
 void launch_struct_scatter(const Work& w, hipStream_t s);
 void launch_ds_bound(const Work& w, hipStream_t s);

@@ -121,7 +121,7 @@ __global__ __launch_bounds__(64) void k_yata(Work w, uint32_t nlists, uint32_t n
     }
   }
   if (w.dbg) {
-    unsigned long long* d = w.dbg + (size_t)w.ngroups * 8 + (size_t)w.ngroups * (GROUP_BYTES / 4096) * 8;
+    unsigned long long* d = w.dbg;
     atomicAdd(d + 0, nint);
     atomicAdd(d + 1, nscan);
     atomicAdd(d + 2, ndive);

@@ -1,8 +1,8 @@
 """Both decode paths for small updates give the same bytes.
 
 A batch with many small updates is parsed directly (one lane per update walks its structs,
-k_direct); few small updates and every large one take the speculative chain-table path (k_parse /
-k_tables / k_walker). YCRDT_DECODE forces one path for every update of at most 16 KiB; both must
+k_direct); few small updates and every large one take the chunk path (k_spec / k_walk).
+YCRDT_DECODE forces one path for every update of at most 16 KiB; both must
 match the Yjs fixtures and the oracle byte for byte, and report the same malformed input.
 """
 import pytest
@@ -10,7 +10,7 @@ import pytest
 crdt_amd = pytest.importorskip("crdt_amd")
 
 pytestmark = pytest.mark.gpu
-MODES = ("tables", "direct")
+MODES = ("chunks", "direct")
 
 
 @pytest.mark.parametrize("mode", MODES)
