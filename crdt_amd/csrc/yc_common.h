@@ -19,6 +19,7 @@ constexpr uint32_t UNKNOWN = 0xFFFFFFFEu;  // a reference to a client no update 
 // A large update is cut into chunks of SCHUNK bytes (64-byte aligned, so a chunk owns its words of
 // the per-byte bitmaps); one lane per chunk follows the struct chain from the chunk's first byte.
 constexpr uint32_t SCHUNK = 1024;
+constexpr uint32_t XK = 64;  // entry offsets per chunk in the exit table (yc_decode.hip k_xtab)
 
 
 // error codes raised on device (first error wins via atomicCAS on the error word)

@@ -10,11 +10,14 @@
 //                      first byte and marks every position it visits (spec_bits) and its exit.
 //                      Such a chain synchronises with the true struct sequence within a few structs
 //                      of any start, and from a true struct start on it IS the true sequence.
+//                      It also tabulates, for the first XK entry offsets, where the chain from
+//                      that entry leaves the chunk (periodic streams hold chains of several
+//                      phases that never meet).
 //   2'. k_walk         one wavefront per large update follows the true sequence through the
-//                      section headers 64 chunks per step: lane j enters chunk j at the exit of
-//                      chunk j-1's chain, parses exactly until it meets its own chunk's chain and
-//                      counts the rest by popcount; the first lane whose true exit differs from
-//                      its chain's exit ends the step (a failed speculation costs one chunk).
+//                      section headers 64 chunks per step: lane j's entry comes from composing the
+//                      exit tables of the chunks before it; it parses exactly until it meets its
+//                      chunk's chain and counts the rest by popcount; the first lane whose true
+//                      exit differs from the predicted one ends the step.
 //   3. k_struct_pos    popcount prefix (scan) -> dense struct index for every struct start.
 //   4. k_ds_decode     one wavefront per update decodes the delete set, a pure varuint stream, with a
 //                      ballot of terminal bytes + in-register gathers (wavefront prefix scan).
@@ -353,6 +356,81 @@ __global__ __launch_bounds__(256) void k_sync(Work w, const uint32_t* __restrict
   xout[i] = X;
 }
 
+
+// Fallback for updates whose chunk chains lock into a wrong phase (the walker gave up on them:
+// periodic struct streams, e.g. a snapshot of identical structs, hold chains of several phases
+// that never meet, so the previous chunk's chain exit is no entry into the next chunk). For each
+// chunk of such an update one wavefront tabulates, for every entry offset e < XK, the chain from
+// start + e: where it leaves the chunk and how many positions it visits inside. Lane e walks
+// offset e over the chunk staged in LDS; every visited position records (lane, step) in an LDS
+// word, and a lane landing on a recorded position has merged into that lane's chain (same exit,
+// the rest of its count). Merged lanes stop, so a wavefront costs about one chunk walk however
+// many phases there are. The walker composes the tables to enter every chunk at its true struct.
+constexpr uint32_t SW = SCHUNK / 64;  // bitmap words per chunk
+constexpr uint32_t XHALO = 256;       // staged bytes past the chunk end
+constexpr uint32_t XFAR = 0xFFFFu;    // exit table: 64 KiB or more past the chunk end
+__global__ __launch_bounds__(64) void k_xtab(Work w) {
+  __shared__ __attribute__((aligned(16))) uint32_t cb[(SCHUNK + XHALO) / 4];
+  __shared__ uint32_t rec[SCHUNK];  // (lane << 16) | step of the first visit, NONE: unvisited
+  __shared__ uint32_t res_exit[64], res_cnt[64], res_done[64];
+  const uint32_t e = threadIdx.x, nx = w.ctr->xchunks;
+  for (uint32_t t = blockIdx.x; t < nx; t += gridDim.x) {
+  const uint32_t i = w.xlist[t];
+  const Group G = w.groups[i];
+  const uint8_t* __restrict__ b = w.bytes;
+  const uint32_t uend = G.uend, cs = G.start;
+  const uint32_t wlen = min(SCHUNK + XHALO, (uend + 15u - cs) & ~15u);
+  for (uint32_t k = e; k < wlen / 16; k += 64) ((uint4*)cb)[k] = ((const uint4*)(b + cs))[k];
+  for (uint32_t k = e; k < SCHUNK; k += 64) rec[k] = NONE;
+  if (e == 0) w.tentry[i] = NONE;
+  __syncthreads();
+  const LdsSrc src{b, cb, cs, wlen};
+  uint32_t q = cs + e, k = 0, tgt = NONE, tidx = 0;
+  bool active = true;
+  for (;;) {
+    bool claim = false;
+    if (active) {
+      if (q >= G.end) active = false;
+      else {
+        const uint32_t v = rec[q - cs];
+        if (v != NONE) { tgt = v >> 16; tidx = v & 0xFFFFu; active = false; }
+        else { rec[q - cs] = (e << 16) | k; claim = true; }
+      }
+    }
+    __syncthreads();
+    if (claim) {  // two lanes on one position in the same step: the last writer keeps it
+      const uint32_t v = rec[q - cs];
+      if ((v >> 16) != e) { tgt = v >> 16; tidx = v & 0xFFFFu; active = false; }
+      else {
+        const uint32_t d = chain_len(src, b, q, uend);
+        q += d ? d : 1u;
+        ++k;
+      }
+    }
+    if (!__ballot(active)) break;
+    __syncthreads();
+  }
+  // resolve merges: a merged lane takes its target's exit and the target's count from the merge
+  res_done[e] = tgt == NONE ? 1u : 0u;
+  res_exit[e] = q;
+  res_cnt[e] = k;
+  __syncthreads();
+  for (uint32_t round = 0; round < 64; ++round) {
+    bool mine = false;
+    uint32_t x = 0, c = 0;
+    if (!res_done[e] && res_done[tgt]) { x = res_exit[tgt]; c = k + res_cnt[tgt] - tidx; mine = true; }
+    __syncthreads();
+    if (mine) { res_exit[e] = x; res_cnt[e] = c; res_done[e] = 1u; }
+    __syncthreads();
+    if (__ballot(!res_done[e]) == 0) break;
+  }
+  const uint32_t x = res_exit[e];
+  const uint32_t dx = res_done[e] ? min(x - G.end, XFAR) : XFAR;
+  w.xtab[(size_t)i * XK + e] = (min(res_cnt[e], 0xFFFFu) << 16) | dx;
+  __syncthreads();
+  }
+}
+
 // ---- bitmap ranges [a, e) (e > a): count, OR into the final bitmap, and select
 __device__ __forceinline__ uint64_t range_word(const uint64_t* __restrict__ bits, uint32_t wd, uint32_t a, uint32_t e) {
   uint64_t x = bits[wd];
@@ -386,33 +464,29 @@ __device__ __forceinline__ uint32_t select_from(const uint64_t* __restrict__ bit
   for (uint32_t k = 1; k < n; ++k) x &= x - 1;
   return wd * 64 + (uint32_t)__ffsll((long long)x) - 1;
 }
-// cnt true structs from x, set in the final bitmap (sections of one update may share a word);
-// returns the position after the last
-__device__ __forceinline__ uint32_t mark_exact(const Work& w, uint32_t x, uint32_t cnt, uint32_t uend) {
-  uint32_t word = NONE;
-  uint64_t m = 0;
-  for (uint32_t k = 0; k < cnt; ++k) {
-    if ((x >> 6) != word) {
-      if (m) atomicOr((unsigned long long*)&w.final_bits[word], (unsigned long long)m);
-      word = x >> 6;
-      m = 0;
-    }
-    m |= 1ull << (x & 63);
-    x = chain_step(w.bytes, x, uend);
-  }
-  if (m) atomicOr((unsigned long long*)&w.final_bits[word], (unsigned long long)m);
-  return x;
-}
-
 // One wavefront per large update follows its true struct sequence through the section headers.
-// Per step lane j takes chunk cj + j (cj = the chunk of the current position p): its entry E is p
-// (lane 0) or the chain exit of the previous chunk; it parses exactly from E until it meets its
-// chunk's chain (then the rest of the chunk's true structs are the chain's positions: a popcount)
-// or leaves the chunk. Lanes up to the first one whose true exit differs from its chain's exit
-// have true entries; the step takes their chunks, or stops in the chunk where the section ends.
+// Per step lane j takes chunk cj + j (cj = the chunk of the current position p). Entries: lane 0
+// enters at p; lane 0 composes the chunks' exit tables from p for as long as each entry offset is
+// tabulated (lanes up to L get their true entries and exits), beyond that lane j enters at the
+// exit of chunk j-1's chain 0 (speculative). Each lane parses exactly from its entry through its
+// LDS window, recording the positions, until it meets its chunk's chain 0 (then the rest of the
+// chunk's true structs are chain 0's positions: a popcount) or leaves the chunk. Lanes up to the
+// first one whose true exit differs from the predicted one have true entries; the step takes
+// their chunks, or stops in the chunk where the section ends.
+__device__ __forceinline__ void or_words(uint64_t* __restrict__ fin, uint32_t w0, const uint64_t* __restrict__ m, uint32_t nw) {
+  for (uint32_t k = 0; k < nw; ++k)
+    if (m[k]) atomicOr((unsigned long long*)&fin[w0 + k], (unsigned long long)m[k]);
+}
+template <bool TABLES>
 __global__ __launch_bounds__(64) void k_walk(Work w) {
+  __shared__ __attribute__((aligned(16))) uint32_t win[64 * DSTRIDE];
+  __shared__ uint64_t walked[64 * (SW + 1)];
+  __shared__ uint64_t chain0[64 * (SW + 1)];
+  __shared__ __attribute__((aligned(16))) uint32_t tab[TABLES ? 64 * XK : 4];
+  __shared__ uint32_t ent[65], cnt[64], nknown;
   if (blockIdx.x >= w.nbig) return;
   const uint32_t u = w.ulist[blockIdx.x];
+  if (TABLES && !w.ufail[u]) return;
   const uint32_t lane = threadIdx.x;
   const uint8_t* __restrict__ b = w.bytes;
   const uint64_t* __restrict__ spec = w.spec_bits;
@@ -420,6 +494,16 @@ __global__ __launch_bounds__(64) void k_walk(Work w) {
   const uint32_t c0 = w.ugroup[u], nch = (w.ulen[u] + SCHUNK - 1) / SCHUNK;
   uint32_t* err = &w.ctr->err;
   const bool L0 = lane == 0;
+  uint32_t* slot = win + lane * DSTRIDE;
+  uint64_t* mw = walked + lane * (SW + 1);
+  uint64_t* mc = chain0 + lane * (SW + 1);
+  LdsSrc src{b, slot, 0, 0};
+  auto refill = [&](uint32_t p) {
+    src.s0 = p & ~15u;
+    src.wlen = min(DW, (uend + 15u - src.s0) & ~15u);
+    const uint4* g = (const uint4*)(b + src.s0);
+    for (uint32_t k = 0; k < src.wlen / 16; ++k) ((uint4*)slot)[k] = g[k];
+  };
   if (L0) w.dsstart[u] = NONE;
   if (w.ulen[u] == 0) { if (L0) raise_err(err, ERR_DECODE); return; }
   uint32_t p = ustart;
@@ -427,10 +511,19 @@ __global__ __launch_bounds__(64) void k_walk(Work w) {
   const uint32_t nsec = rd_vu(b, p, uend, ok);
   if (!ok || nsec > (uend - p) / 3 + 1) { if (L0) raise_err(err, ERR_DECODE); return; }
   uint32_t sbase = 0;
-  if (L0) sbase = atomicAdd(&w.ctr->nsections, nsec);
+  if (TABLES) sbase = w.usec_start[u];  // the speculative walk gave up on this update: same sections
+  else if (L0) sbase = atomicAdd(&w.ctr->nsections, nsec);
   sbase = __shfl(sbase, 0);
   if (sbase + nsec > w.cap_sections) { if (L0) raise_err(err, ERR_CAPACITY); return; }
-  if (L0) { w.usec_start[u] = sbase; w.usec_n[u] = nsec; }
+  if (L0 && !TABLES) { w.usec_start[u] = sbase; w.usec_n[u] = nsec; }
+  auto hand_over = [&]() {  // to the exit tables: flag the update, list its chunks
+    uint32_t base = 0;
+    if (L0) { w.ufail[u] = 1u; base = atomicAdd(&w.ctr->xchunks, nch); }
+    base = __shfl(base, 0);
+    for (uint32_t k = lane; k < nch; k += 64) w.xlist[base + k] = c0 + k;
+  };
+  if (!TABLES && w.force_xtab) { hand_over(); return; }
+  uint32_t steps = 0, fails = 0;
   for (uint32_t sct = 0; sct < nsec; ++sct) {
     const uint32_t n = rd_vu(b, p, uend, ok);
     const uint32_t client = rd_vu(b, p, uend, ok);
@@ -446,21 +539,64 @@ __global__ __launch_bounds__(64) void k_walk(Work w) {
     uint32_t r = n;
     while (r > 0) {
       if (p >= uend) { if (L0) { raise_err(err, ERR_DECODE); w.ctr->err_info = p; } return; }
-      const uint32_t j = (p - ustart) / SCHUNK + lane;
+      const uint32_t j0 = (p - ustart) / SCHUNK, j = j0 + lane;
       const bool valid = j < nch;
-      const uint32_t ce = valid ? min(ustart + (j + 1) * SCHUNK, uend) : 0u;
-      const uint32_t S = valid ? w.cexit[c0 + j] : NONE;  // after the two k_sync rounds
+      const uint32_t cs = ustart + j * SCHUNK;
+      const uint32_t ce = valid ? min(cs + SCHUNK, uend) : 0u;
+      if (valid) {
+        if (TABLES) {
+          const uint4* xt = (const uint4*)(w.xtab + (size_t)(c0 + j) * XK);
+          for (uint32_t k = 0; k < XK / 4; ++k) ((uint4*)(tab + lane * XK))[k] = xt[k];
+        }
+        for (uint32_t k = 0; k <= SW; ++k) { mc[k] = k < SW ? spec[(cs >> 6) + k] : 0ull; mw[k] = 0; }
+      }
+      if (!TABLES && L0) nknown = 0;
+      __syncthreads();
+      if (TABLES && L0) {  // compose the exit tables from p
+        uint32_t E = p, L = 0;
+        for (uint32_t l = 0; l < 64 && j0 + l < nch; ++l) {
+          const uint32_t s_l = ustart + (j0 + l) * SCHUNK, e_l = min(s_l + SCHUNK, uend);
+          const uint32_t off = E - s_l;
+          if (off >= XK) break;
+          const uint32_t v = tab[l * XK + off];
+          if ((v & 0xFFFFu) == XFAR) break;
+          E = e_l + (v & 0xFFFFu);
+          ent[l + 1] = E;
+          cnt[l] = v >> 16;
+          L = l + 1;
+        }
+        nknown = L;
+      }
+      __syncthreads();
+      const uint32_t L = nknown;
+      const uint32_t CX = valid ? w.cexit[c0 + j] : NONE;   // chain 0's exit
+      const uint32_t S = valid && lane < L ? ent[lane + 1] : CX;  // predicted exit
       uint32_t E = __shfl_up(S, 1);
       if (L0) E = p;
+      // lanes below L hold a tabulated chunk: their count is known and their positions are
+      // marked later (k_xmark from the entry); the others parse exactly from their entry
+      const bool tabbed = TABLES && valid && lane < L;
+      auto walk = [&](uint32_t q0, uint32_t limit, uint32_t& kk) {  // exact, until chain 0 / limit
+        uint32_t q = q0;
+        if (q < ce) refill(q);
+        while (q < ce && kk < limit && !((mc[(q - cs) >> 6] >> (q & 63)) & 1ull)) {
+          mw[(q - cs) >> 6] |= 1ull << (q & 63);
+          if (q - src.s0 + DREFILL > src.wlen) refill(q);
+          const uint32_t d = chain_len(src, b, q, uend);
+          q += d ? d : 1u;
+          ++kk;
+        }
+        return q;
+      };
       uint32_t q = E, k = 0;
       bool merged = false;
-      if (valid) {
-        while (q < ce && !((spec[q >> 6] >> (q & 63)) & 1ull)) { q = chain_step(b, q, uend); ++k; }
+      if (valid && E >= cs && !tabbed) {
+        q = walk(E, NONE, k);
         merged = q < ce;
       }
-      const uint32_t C = k + (merged ? popc_range(spec, q, ce) : 0u);
-      const uint32_t X = merged ? S : q;  // the true exit, given the entry
-      const uint64_t bad = __ballot(!(valid && X == S));
+      const uint32_t C = tabbed ? cnt[lane] : k + (merged ? popc_range(spec, q, ce) : 0u);
+      const uint32_t X = tabbed ? S : merged ? CX : q;  // the true exit, given the entry
+      const uint64_t bad = __ballot(!(valid && E >= cs && X == S));
       const uint32_t f = bad ? (uint32_t)__ffsll((long long)bad) - 1 : 63u;  // lanes 0..f hold true entries
       uint32_t incl = lane <= f ? C : 0u;
       for (uint32_t off = 1; off < 64; off <<= 1) {
@@ -469,45 +605,111 @@ __global__ __launch_bounds__(64) void k_walk(Work w) {
       }
       const uint32_t excl = incl - (lane <= f ? C : 0u);
       const uint64_t ends = __ballot(lane <= f && valid && incl >= r);
+      const uint32_t nw = valid ? (ce - cs + 63) >> 6 : 0u;
+      // chains locked into a wrong phase fail one speculation per step: hand the update to the
+      // exit tables (k_xtab + k_walk<true>); the marks made so far are true and are made again
+      ++steps;
+      if (!TABLES && !ends && f < 63 && j0 + f + 1 < nch && ++fails >= 4 && fails * 4 > steps) {
+        hand_over();
+        return;
+      }
+      auto mark_all = [&]() {
+        if (tabbed) w.tentry[c0 + j] = E;
+        else {
+          or_words(w.final_bits, cs >> 6, mw, nw);
+          if (merged) or_range(w.final_bits, spec, q, ce);
+        }
+      };
       if (ends) {  // the section ends in lane jl's chunk
         const uint32_t jl = (uint32_t)__ffsll((long long)ends) - 1;
         uint32_t np = 0;
         if (lane < jl) {
-          mark_exact(w, E, k, uend);
-          if (merged) or_range(w.final_bits, spec, q, ce);
+          mark_all();
         } else if (lane == jl) {
           const uint32_t rr = r - excl;
-          if (rr <= k) {
-            np = mark_exact(w, E, rr, uend);
-          } else {
-            mark_exact(w, E, k, uend);
-            const uint32_t L = select_from(spec, q, rr - k);
-            or_range(w.final_bits, spec, q, L + 1);
-            np = chain_step(b, L, uend);
+          if (tabbed) {  // parse the rr structs exactly (all inside the chunk: the count says so)
+            uint32_t kk = 0;
+            for (uint32_t x = 0; x <= SW; ++x) mc[x] = 0;
+            walk(E, rr, kk);
           }
+          uint32_t Lp;
+          if (tabbed || rr <= k) {  // the rr-th walked position is the section's last struct
+            Lp = select_from(mw, 0, rr) + cs;  // mw is indexed from the chunk start
+            const uint32_t lw = (Lp - cs) >> 6;
+            for (uint32_t x = 0; x < nw; ++x) {
+              const uint64_t v = x < lw ? mw[x] : x == lw ? mw[x] & (~0ull >> (63 - (Lp & 63))) : 0ull;
+              if (v) atomicOr((unsigned long long*)&w.final_bits[(cs >> 6) + x], (unsigned long long)v);
+            }
+          } else {
+            or_words(w.final_bits, cs >> 6, mw, nw);
+            Lp = select_from(spec, q, rr - k);
+            or_range(w.final_bits, spec, q, Lp + 1);
+          }
+          np = chain_step(b, Lp, uend);
         }
         p = __shfl(np, jl);
         r = 0;
       } else {
-        if (lane <= f) {
-          mark_exact(w, E, k, uend);
-          if (merged) or_range(w.final_bits, spec, q, ce);
-        }
+        if (lane <= f) mark_all();
         r -= __shfl(incl, f);
         p = __shfl(X, f);  // NONE / past the update when the section runs past its end
       }
+      __syncthreads();
     }
   }
   if (L0) w.dsstart[u] = p;
 }
 
+// Positions of the chunks the table walk entered without parsing (tentry): one lane per chunk
+// parses exactly from the entry to the chunk end through its LDS window and marks them.
+__global__ __launch_bounds__(DL) void k_xmark(Work w) {
+  __shared__ __attribute__((aligned(16))) uint32_t win[DL * DSTRIDE];
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= w.ctr->xchunks) return;
+  const uint32_t i = w.xlist[t];
+  const Group G = w.groups[i];
+  uint32_t p = w.tentry[i];
+  if (p == NONE) return;
+  const uint8_t* __restrict__ b = w.bytes;
+  const uint32_t uend = G.uend;
+  uint32_t* slot = win + threadIdx.x * DSTRIDE;
+  LdsSrc src{b, slot, 0, 0};
+  auto refill = [&](uint32_t x) {
+    src.s0 = x & ~15u;
+    src.wlen = min(DW, (uend + 15u - src.s0) & ~15u);
+    const uint4* g = (const uint4*)(b + src.s0);
+    for (uint32_t k = 0; k < src.wlen / 16; ++k) ((uint4*)slot)[k] = g[k];
+  };
+  refill(p);
+  uint32_t word = p >> 6;
+  uint64_t m = 0;
+  while (p < G.end) {
+    if ((p >> 6) != word) {
+      if (m) atomicOr((unsigned long long*)&w.final_bits[word], (unsigned long long)m);
+      word = p >> 6;
+      m = 0;
+    }
+    m |= 1ull << (p & 63);
+    if (p - src.s0 + DREFILL > src.wlen) refill(p);
+    const uint32_t d = chain_len(src, b, p, uend);
+    p += d ? d : 1u;
+  }
+  if (m) atomicOr((unsigned long long*)&w.final_bits[word], (unsigned long long)m);
+}
+
 void launch_chunks(const Work& w, hipStream_t s) {
-  if (w.ngroups) hipLaunchKernelGGL(k_spec, dim3((w.ngroups + DL - 1) / DL), dim3(DL), 0, s, w);
   if (w.ngroups) {
+    hipLaunchKernelGGL(k_spec, dim3((w.ngroups + DL - 1) / DL), dim3(DL), 0, s, w);
     hipLaunchKernelGGL(k_sync, dim3((w.ngroups + 255) / 256), dim3(256), 0, s, w, (const uint32_t*)w.cexit, w.sexit);
     hipLaunchKernelGGL(k_sync, dim3((w.ngroups + 255) / 256), dim3(256), 0, s, w, (const uint32_t*)w.sexit, w.cexit);
   }
-  if (w.nbig) hipLaunchKernelGGL(k_walk, dim3(w.nbig), dim3(64), 0, s, w);
+  if (w.nbig) {
+    hipLaunchKernelGGL(k_walk<false>, dim3(w.nbig), dim3(64), 0, s, w);
+    // the table path, for updates the speculative walk handed over (grid-stride over xlist)
+    hipLaunchKernelGGL(k_xtab, dim3(std::min(w.ngroups, 4096u)), dim3(64), 0, s, w);
+    hipLaunchKernelGGL(k_walk<true>, dim3(w.nbig), dim3(64), 0, s, w);
+    hipLaunchKernelGGL(k_xmark, dim3((w.ngroups + DL - 1) / DL), dim3(DL), 0, s, w);
+  }
 }
 void launch_direct(const Work& w, hipStream_t s) {
   if (w.nsmall) hipLaunchKernelGGL(k_direct, dim3((w.nsmall + DL - 1) / DL), dim3(DL), 0, s, w);

@@ -136,7 +136,7 @@ enum Buf {
   B_UOWN, B_UFLAG, B_UMIN, B_UCUT, B_UWPRE,
   B_GSTART, B_GCIDX, B_GSRC, B_GFLAGS, B_GORIG, B_GRORIG, B_GLINK, B_GOSEG, B_GKEY, B_GMAXC, B_GNEXT, B_GOUTID, B_GTMP, B_GTMP2,
   B_KHASH, B_KROOT, B_KWIN, B_KPAR, B_KFLAG, B_SPK,
-  B_USEC, B_USECN, B_DBG,
+  B_USEC, B_USECN, B_DBG, B_XTAB, B_UFAIL, B_TENTRY, B_XLIST,
   B_LZKEY, B_LZKEYS, B_LZIOTA, B_LZSEC, B_LZRSTART, B_LZPREV, B_LZFIRST, B_LZCAP, B_LZEVBASE, B_LZEVN, B_LZFLAG,
   B_LZLHI, B_LZLLO, B_EVKIND, B_EVSRC, B_EVCLOCK, B_EVLEN, B_EVSIZE, B_EVPOS, B_BLKSIZE, B_BLKPOS, B_SVC, B_SVK,
   B_DSMKEY, B_DSMKEYS, B_DSMLEN, B_DSMLENS, B_DSMEND, B_DSMMAX, B_DSMFLAG, B_DSMRID, B_DRCLIENT, B_DRCLOCK, B_DREND,
@@ -257,7 +257,8 @@ void mark(ycrdt_engine* e, const char* name) {
 // are many of them: a wavefront then parses 64 updates side by side and the batch is read about
 // once. A few small updates, and every large one, take the chunk path (k_spec / k_walk), whose
 // latency grows with the update only by one wavefront step per 64 KiB. YCRDT_DECODE=chunks|direct
-// forces one path for small updates (tests cover both; "tables" is the older name of "chunks").
+// forces one path for small updates (tests cover both; "tables" is the older name of "chunks");
+// xtab = chunks, and every large update walked through the exit tables (yc_decode.hip k_xtab).
 constexpr size_t DIRECT_MAX_BYTES = 16384;         // an update the direct lane walks whole
 constexpr size_t DIRECT_TINY_BYTES = 1024;         // always direct (a handful of structs)
 constexpr size_t DIRECT_MIN_COUNT = 1024;          // enough small updates to fill wavefronts
@@ -275,7 +276,8 @@ void layout(ycrdt_batch* b, const std::vector<Src>& src, std::vector<uint32_t>& 
   b->uoff.clear(); b->ulen.clear(); b->ugroup.clear(); b->groups.clear(); b->ulist.clear();
   b->in_bytes = 0;
   const char* mode = getenv("YCRDT_DECODE");
-  const int force = mode && (!strcmp(mode, "chunks") || !strcmp(mode, "tables")) ? 1 : mode && !strcmp(mode, "direct") ? 2 : 0;
+  const int force = mode && (!strcmp(mode, "chunks") || !strcmp(mode, "tables") || !strcmp(mode, "xtab")) ? 1
+                    : mode && !strcmp(mode, "direct") ? 2 : 0;
   size_t nsmall = 0;
   for (const Src& x : src) nsmall += x.len <= DIRECT_MAX_BYTES;
   auto direct = [&](size_t len) {
@@ -448,6 +450,10 @@ int run_decode(ycrdt_engine* e, ycrdt_batch* b, bool lazy, Decoded& D, bool gene
   w.nbig = b->nbig;
   w.nsmall = (uint32_t)b->ulist.size() - b->nbig;
   w.lazy = lazy ? 1u : 0u;
+  {
+    const char* mode = getenv("YCRDT_DECODE");
+    w.force_xtab = mode && !strcmp(mode, "xtab") ? 1u : 0u;
+  }
   const uint64_t B = (uint64_t)b->nbytes + 64;
   const uint64_t nwords = B / 64 + 2;
   // The section table is sized from an estimate (a capacity overflow reruns the decode with the
@@ -462,6 +468,10 @@ int run_decode(ycrdt_engine* e, ycrdt_batch* b, bool lazy, Decoded& D, bool gene
   w.spec_bits = take<uint64_t>(V, B_SPECB, nwords, ok);
   w.cexit = take<uint32_t>(V, B_CEXIT, (uint64_t)w.ngroups + 1, ok);
   w.sexit = take<uint32_t>(V, B_SEXIT, (uint64_t)w.ngroups + 1, ok);
+  w.xtab = take<uint32_t>(V, B_XTAB, ((uint64_t)w.ngroups + 1) * XK, ok);
+  w.tentry = take<uint32_t>(V, B_TENTRY, (uint64_t)w.ngroups + 1, ok);
+  w.xlist = take<uint32_t>(V, B_XLIST, (uint64_t)w.ngroups + 1, ok);
+  w.ufail = take<uint32_t>(V, B_UFAIL, nu + 1, ok);
   w.final_bits = take<uint64_t>(V, B_FINAL, nwords, ok);
   w.sec_bits = take<uint64_t>(V, B_SECB, nwords, ok);
   w.dsstart = take<uint32_t>(V, B_DSSTART, nu + 1, ok);
@@ -486,6 +496,7 @@ int run_decode(ycrdt_engine* e, ycrdt_batch* b, bool lazy, Decoded& D, bool gene
   if (!ok) return fail(YCRDT_E_DEVICE, "hipMalloc failed (scan scratch)");
   static_assert(sizeof(Counters) % 4 == 0, "counters are filled as words");
   fill_u32_multi({{(uint32_t*)w.ctr, sizeof(Counters) / 4, 0u},
+                  {w.ufail, (uint64_t)nu + 1, 0u},
                   {(uint32_t*)w.final_bits, (uint64_t)nwords * 2, 0u},
                   {(uint32_t*)w.sec_bits, (uint64_t)nwords * 2, 0u}}, s);
   static const bool dbg_yata = getenv("YCRDT_DEBUG_YATA") && getenv("YCRDT_DEBUG_YATA")[0] == '1';

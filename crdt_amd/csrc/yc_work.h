@@ -14,6 +14,7 @@ struct Counters {            // device-side counters, read back at the few host 
   uint32_t err;              // first error code (ERR_*)
   uint32_t err_info;         // position / index that raised it
   uint32_t nsections;        // appended by the walker
+  uint32_t xchunks;          // chunks of updates handed to the exit tables (xlist)
   uint32_t nds;              // decoded delete-set ranges
   uint32_t ndsclients;       // delete-set client headers
   uint32_t nstructs;         // S
@@ -59,6 +60,7 @@ struct Work {
   uint32_t ndocs = 1;
   const uint32_t* ulist = nullptr; // [nbig] updates on the chunk path, then [nsmall] parsed directly
   uint32_t nbig = 0, nsmall = 0;
+  uint32_t force_xtab = 0;         // YCRDT_DECODE=xtab: every large update takes the exit-table walk (tests)
   uint32_t lazy = 0;               // 1: mergeUpdates / diffUpdate decode (references kept raw)
   unsigned long long* dbg = nullptr; // YCRDT_DEBUG_YATA=1: k_yata work counters
   const Group* groups = nullptr;   // [G] chunks of the large updates
@@ -71,6 +73,10 @@ struct Work {
   uint64_t* spec_bits = nullptr;   // [B/64] positions visited by the chunk chains (large updates)
   uint32_t* cexit = nullptr;       // [G] first chain position at / past each chunk's end
   uint32_t* sexit = nullptr;       // [G] the same after k_sync's first round (the second writes cexit)
+  uint32_t* xtab = nullptr;        // [G x XK] locked updates only, per entry offset: count << 16 | exit - chunk end
+  uint32_t* tentry = nullptr;      // [G] locked updates: true entry of a chunk the table walk did not parse
+  uint32_t* xlist = nullptr;       // [G] the chunks of the locked updates (k_xtab / k_xmark work list)
+  uint32_t* ufail = nullptr;       // [nupd] 1: the speculative walk gave up (locked chain phases), tables next
   uint64_t* final_bits = nullptr;  // [B/64] verified struct starts
   uint64_t* sec_bits = nullptr;    // [B/64] first struct of every non-empty section
   uint32_t* dsstart = nullptr;     // [nupd] byte position of the delete set

@@ -466,21 +466,49 @@ __global__ void k_tsib_small(Work w, uint32_t nsegs) {
   }
 }
 // one workgroup per large group: anchors of outside right origins through an LDS hash table,
-// the group staged in LDS when it fits (else read in place); lane 0 runs the loop
-constexpr uint32_t THASH = 2048;
+// the group staged in LDS when it fits (else collapsed into chains, else read in place); lane 0
+// runs the loop
+constexpr uint32_t THASH = 2048, HNONE = 0xFFFFFFFEu;  // the "no right origin" key (units < HNONE)
+
+// Chains. Members c_1..c_m at consecutive sorted positions (one client, ascending clocks) with
+// rightOrigin(c_k) = c_{k-1}, where no other member names c_1..c_{m-1} as its right origin, are
+// placed by sib_loop as one contiguous block c_m .. c_1: c_k is integrated right
+// after c_{k-1} (nothing else can dive into an unreferenced member), lands immediately before it
+// (its right-origin group is {c_k}; prv(c_{k-1}) has a lower client), and no later member can
+// stop inside the block (its stop would be a referenced interior member) or step left into it
+// (a walk from the right crosses the block whole: one client). So the loop runs over chains as
+// single members — cid of the client, right origin and anchor of c_1, referenced by c_m — and the
+// block is expanded afterwards. The C3 list head (≈790 k unshifts, all origin = the list root)
+// collapses to one member per (replica, round).
+__device__ __forceinline__ uint32_t block_excl_scan256(uint32_t v, uint32_t* sh, uint32_t& total) {
+  const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  uint32_t x = v;
+  for (uint32_t d = 1; d < 64; d <<= 1) {
+    const uint32_t y = __shfl_up(x, d, 64);
+    if (lane >= d) x += y;
+  }
+  if (lane == 63) sh[wv] = x;
+  __syncthreads();
+  uint32_t off = 0;
+  for (uint32_t k = 0; k < wv; ++k) off += sh[k];
+  total = sh[0] + sh[1] + sh[2] + sh[3];
+  __syncthreads();
+  return off + x - v;
+}
+
 __global__ __launch_bounds__(256) void k_tsib_big(Work w, uint32_t nsegs) {
   const uint32_t g = w.t_big[blockIdx.x];
   const uint32_t a = w.t_gstart[g], n = w.t_gstart[g + 1] - a;
   __shared__ SibRec rec[TLDS];
   __shared__ uint8_t st[TLDS];
   __shared__ uint32_t hkey[THASH], hval[THASH];
-  __shared__ uint32_t head_s;
+  __shared__ uint32_t head_s, scan_sh[4];
   for (uint32_t i = threadIdx.x; i < THASH; i += blockDim.x) { hkey[i] = NONE; hval[i] = NONE; }
   __syncthreads();
   // anchors: the first member (lowest position) of every outside right-origin unit
   for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) {
     if (w.y_confl[a + i] != NONE) continue;
-    const uint32_t r = w.y_before[a + i];
+    const uint32_t r0 = w.y_before[a + i], r = r0 == NONE ? HNONE : r0;
     uint32_t slot = (r * 2654435761u) & (THASH - 1);
     for (uint32_t probe = 0;; ++probe) {
       if (probe == THASH) { raise_err(&w.ctr->err, ERR_CAPACITY); break; }
@@ -493,7 +521,7 @@ __global__ __launch_bounds__(256) void k_tsib_big(Work w, uint32_t nsegs) {
   for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) {
     uint32_t t = w.y_confl[a + i];
     if (t == NONE) {
-      const uint32_t r = w.y_before[a + i];
+      const uint32_t r0 = w.y_before[a + i], r = r0 == NONE ? HNONE : r0;
       uint32_t slot = (r * 2654435761u) & (THASH - 1);
       for (uint32_t probe = 0; probe < THASH && hkey[slot] != r; ++probe) slot = (slot + 1) & (THASH - 1);
       t = (hkey[slot] == r ? a + hval[slot] : a + i) | 0x80000000u;
@@ -501,6 +529,80 @@ __global__ __launch_bounds__(256) void k_tsib_big(Work w, uint32_t nsegs) {
     w.t_trep[a + i] = t;
   }
   __syncthreads();
+  uint32_t nn = NONE;  // member count after collapsing chains (n > TLDS only)
+  if (n > TLDS) {
+    // t_mtail / t_prv / t_next hold NONE here (k_tprep) and serve as scratch:
+    //   t_mtail[p] = 0   p is named as right origin by a member other than its chain successor
+    //   t_prv[i]         the chain (node) of position i;  t_next[k]  first position of node k
+    for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) {
+      const uint32_t rp = w.y_confl[a + i];
+      if (rp == NONE) continue;
+      const uint32_t p = rp - a;
+      if (!(p + 1 == i && w.y_state[a + i] == w.y_state[a + p])) w.t_mtail[a + p] = 0;
+    }
+    __syncthreads();
+    uint32_t carry = 0;
+    for (uint32_t base = 0; base < n; base += blockDim.x) {
+      const uint32_t i = base + threadIdx.x;
+      uint32_t first = 0;
+      if (i < n) {
+        const bool link = i > 0 && w.y_confl[a + i] == a + i - 1 && w.y_state[a + i] == w.y_state[a + i - 1] &&
+                          w.t_mtail[a + i - 1] == NONE;
+        first = link ? 0u : 1u;
+      }
+      uint32_t tot;
+      const uint32_t ex = block_excl_scan256(first, scan_sh, tot);
+      if (i < n) {
+        const uint32_t k = carry + ex + first - 1;
+        w.t_prv[a + i] = k;
+        if (first) w.t_next[a + k] = i;
+      }
+      carry += tot;
+    }
+    nn = carry;
+    __syncthreads();
+    if (nn > TLDS) {  // no room in LDS even collapsed: restore the scratch, run in place
+      for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) {
+        w.t_mtail[a + i] = NONE;
+        w.t_prv[a + i] = NONE;
+        w.t_next[a + i] = NONE;
+      }
+      __syncthreads();
+    }
+  }
+  if (nn != NONE && nn <= TLDS) {
+    const uint32_t* node = w.t_prv + a;
+    const uint32_t* nfirst = w.t_next + a;
+    for (uint32_t k = threadIdx.x; k < nn; k += blockDim.x) {
+      const uint32_t f = nfirst[k];
+      const uint32_t rp = w.y_confl[a + f];
+      const uint32_t t = w.t_trep[a + f];
+      const uint32_t tq = node[(t & 0x7FFFFFFFu) - a];
+      rec[k] = SibRec{w.y_state[a + f], (uint16_t)(rp == NONE ? S_NONE : node[rp - a]),
+                      (uint16_t)(tq | ((t >> 31) ? TOUT : 0u)), S_NONE, S_NONE, S_NONE, S_NONE, S_NONE, 0};
+      st[k] = 0;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      SibLds acc{rec, st};
+      head_s = sib_loop(acc, nn, w.y_stack + a, &w.ctr->err);
+    }
+    __syncthreads();
+    // expand: node k spans positions nfirst[k] .. nfirst[k + 1] - 1, listed from the last down
+    auto leftmost = [&](uint32_t k) { return (k + 1 < nn ? nfirst[k + 1] : n) - 1; };
+    for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) {
+      const uint32_t k = node[i];
+      uint32_t nx;
+      if (i > nfirst[k]) nx = i - 1;
+      else {
+        const uint32_t kn = rec[k].nxt;
+        nx = kn == S_NONE ? NONE : leftmost(kn);
+      }
+      w.t_nsib[w.t_seg[a + i]] = nx == NONE ? NONE : w.t_seg[a + nx];
+    }
+    if (threadIdx.x == 0 && head_s != NONE) sib_publish(w, a, n, nsegs, leftmost(head_s));
+    return;
+  }
   if (n <= TLDS) {
     for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) {
       const uint32_t rp = w.y_confl[a + i];

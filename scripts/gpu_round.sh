@@ -22,4 +22,5 @@ fi
 if [[ $what == all || $what == prof ]]; then
   export TMPDIR=/tmp
   step prof 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline --fleet-pairs 0
+  rm -f gpurun_out/prof/run_kernel_trace.csv
 fi

@@ -168,16 +168,89 @@ def tree_yata(units):
     return out, steps
 
 
+def tree_yata_chains(units):
+    """tree_yata with every sibling group collapsed into chains first (yc_yata.hip k_tsib_big):
+    kids at consecutive ascending (client, clock) positions c_1..c_m of one client with
+    rightOrigin(c_k) = c_{k-1}, no other kid naming c_1..c_{m-1} as right origin, run through the
+    sibling loop as one member (client, right origin of c_1) and expand to c_m .. c_1."""
+    children = {}
+    for u, (o, _) in units.items():
+        children.setdefault(o, []).append(u)
+    ordered = {}
+    nchains = 0
+    for p, kids in children.items():
+        kids = sorted(kids)
+        pos = {k: i for i, k in enumerate(kids)}
+        ext = set()
+        for i, k in enumerate(kids):
+            r = units[k][1]
+            if r in pos and not (pos[r] + 1 == i and r[0] == k[0]):
+                ext.add(pos[r])
+        node_of, firsts = [], []
+        for i, k in enumerate(kids):
+            r = units[k][1]
+            link = i > 0 and units[k][1] == kids[i - 1] and r[0] == k[0] and (i - 1) not in ext
+            if not link:
+                firsts.append(i)
+            node_of.append(len(firsts) - 1)
+        nn = len(firsts)
+        nchains += nn
+        client = [kids[firsts[x]][0] for x in range(nn)]
+        rn = []
+        for x in range(nn):
+            r = units[kids[firsts[x]]][1]
+            rn.append(("in", node_of[pos[r]]) if r in pos else ("out", r))
+        lst = []
+        done = set()
+        for x0 in range(nn):
+            if x0 in done:
+                continue
+            stack = [x0]
+            while stack:
+                x = stack[-1]
+                kind, r = rn[x]
+                if kind == "in" and r not in done:
+                    stack.append(r)
+                    continue
+                left = -1
+                for i, o in enumerate(lst):
+                    if kind == "in" and o == r:
+                        break
+                    if client[o] < client[x]:
+                        left = i
+                    elif rn[o] == rn[x]:
+                        break
+                lst.insert(left + 1, x)
+                done.add(x)
+                stack.pop()
+        out = []
+        for x in lst:
+            end = firsts[x + 1] if x + 1 < nn else len(kids)
+            out.extend(kids[i] for i in range(end - 1, firsts[x] - 1, -1))
+        ordered[p] = out
+    out = []
+    stack = [iter(ordered.get(None, []))]
+    while stack:
+        x = next(stack[-1], None)
+        if x is None:
+            stack.pop()
+            continue
+        out.append(x)
+        if x in ordered:
+            stack.append(iter(ordered[x]))
+    return out, nchains
+
+
 def main():
     from tests.histories import array_history
 
     n = int(sys.argv[1]) if len(sys.argv) > 1 else 60
-    tot = [0, 0, 0]
+    tot = [0, 0, 0, 0]
     for seed in range(n):
         reps = 2 + seed % 7
         states, wire = array_history(7000 + seed, n_replicas=reps, rounds=2 + seed % 4, ops=3 + seed % 9)
         check(states + wire, f"seed {seed}", tot)
-    print(f"{n} histories agree; scan steps: B.1 ascending {tot[0]}, descending {tot[1]}, tree sibling loops {tot[2]}")
+    print(f"{n} histories agree; scan steps: B.1 ascending {tot[0]}, descending {tot[1]}, tree sibling loops {tot[2]}; units absorbed into chains {tot[3]}")
     import json
     ncase = 0
     for name in ("array", "nested", "configs"):
@@ -185,7 +258,7 @@ def main():
             for c in json.load(f)["cases"]:
                 check([bytes.fromhex(u) for u in c["updates"]], c["name"], tot)
                 ncase += 1
-    print(f"+ {ncase} golden cases agree; scan steps: B.1 ascending {tot[0]}, descending {tot[1]}, tree sibling loops {tot[2]}")
+    print(f"+ {ncase} golden cases agree; scan steps: B.1 ascending {tot[0]}, descending {tot[1]}, tree sibling loops {tot[2]}; units absorbed into chains {tot[3]}")
 
 
 def check(updates, name, tot):
@@ -195,8 +268,11 @@ def check(updates, name, tot):
         a, sa = seq_yata(units)
         b, sb = seq_yata(units, descending=True)
         c, sc = tree_yata(units)
+        d, nchain = tree_yata_chains(units)
         assert a == b, f"{name}: the loop depends on the causal order"
         assert a == c, f"{name}: tree order differs ({len(units)} units)"
+        assert a == d, f"{name}: chain-collapsed order differs ({len(units)} units, {nchain} chains)"
+        tot[3] += len(units) - nchain
         tot[0] += sa
         tot[1] += sb
         tot[2] += sc

@@ -113,3 +113,35 @@ def test_batch_of_large_and_small():
         small.append(o.encode_state_as_update())
     d, ref = _merge_both(snaps + small)
     _same(d, ref)
+
+
+def _periodic_snapshot(n, seed):
+    """One client writing n map entries of identical encoded size (one section): the struct stream
+    is periodic, so chunk chains can settle into a phase that never meets the true one."""
+    d = ODoc(7)
+    for k in range(n):
+        d.map_set("users", f"k{k:06d}", any_int(1000 + (k * 7919 + seed) % 9000))
+    return d.encode_state_as_update()
+
+
+@pytest.mark.parametrize("mode", ["auto", "xtab"])
+def test_periodic_struct_streams(mode, monkeypatch):
+    """Periodic snapshots (the C4 base: identical type items, then identical elements) hand the
+    walk over to the exit tables (k_xtab): byte-exact either way, and with every large update of
+    the other chunk-path cases forced through the tables."""
+    if mode == "xtab":
+        monkeypatch.setenv("YCRDT_DECODE", "xtab")
+    from crdt_amd.workload import gen_nested
+
+    ups, _ = gen_nested(40, 3000, 60, seed=9)
+    assert len(ups[0]) > 64 * 1024
+    for batch in ([ups[0]], ups, [_periodic_snapshot(20000, 3)]):
+        d, ref = _merge_both(batch)
+        _same(d, ref)
+    if mode == "xtab":
+        for n_clients, per_client in ((900, 3), (60, 40)):
+            d, ref = _merge_both([_snapshot(n_clients, per_client, n_clients)])
+            _same(d, ref)
+        snap = _snapshot(40, 4, 7, value=lambda rng2: any_str("x" * rng2.choice([1, 900, 1023, 1025, 5000, 70_000])))
+        d, ref = _merge_both([snap])
+        _same(d, ref)

@@ -54,3 +54,34 @@ def test_gpu_yata_tree_equals_sequential_kernel():
     env = dict(os.environ, YCRDT_YATA="seq")
     r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=200)
     assert r.returncode == 0 and r.stdout.strip().endswith("ok"), r.stderr[-2000:]
+
+
+@pytest.mark.parametrize("reps,rounds,items,seed", [(64, 4, 200_000, 11), (4096, 2, 60_000, 5)])
+def test_gpu_yata_large_sibling_group(reps, rounds, items, seed):
+    """C3-generator histories whose list head carries a sibling group larger than one workgroup's
+    LDS (every unshift has the list root as origin): (64, 4) collapses it into per-(replica, round)
+    chains (k_tsib_big); (4096, 2) leaves too many chains for LDS and runs in place. Byte-exact
+    against the oracle, and the list order is the generator's independent origin-tree order."""
+    from crdt_amd.workload import gen_array
+    from oracle.yref import Doc as ODoc
+    from tests.test_workload_c3 import _any_json
+    from oracle.ymerge import ITEM, Dec, lazy_structs
+
+    ups, st = gen_array(reps, rounds, items, seed, order=True)
+    heads = sum(1 for u in ups for s in lazy_structs(Dec(u)) if s.kind == ITEM and s.origin is None)
+    assert heads > 6144  # the root sibling group exceeds k_tsib_big's LDS staging
+    ref = ODoc(0x7FFFFFF0)
+    for u in ups:
+        ref.apply_update(u)
+    b = crdt_amd.Batch(ups)
+    b.merge()
+    assert b.result()[0] == ref.encode_state_as_update()
+    vals = {}
+    for u in ups:
+        for s in lazy_structs(Dec(u)):
+            if s.kind == ITEM:
+                for i, raw in enumerate(s.content):
+                    vals[(s.client, s.clock + i)] = _any_json(raw, 0)[0]
+    d = crdt_amd.Doc(client_id=0x7FFFFFF0)
+    d.apply_updates(ups)
+    assert json.loads(d.root_json("messages", "array")) == [vals[k] for k in st["order"]]
