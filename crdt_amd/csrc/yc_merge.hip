@@ -296,7 +296,8 @@ __global__ __launch_bounds__(256) void k_seg_props(Work w, uint32_t nsegs) {
   w.g_flags[s] = sf;
   w.g_origin[s] = gc ? NONE : origin;
   w.g_rorigin[s] = gc ? NONE : rorigin;
-  w.g_key[s] = key;
+  // a root's key carries its list kind in bit 31 until k_seg_kind (k_keyfind copies it whole)
+  w.g_key[s] = key != NONE && w.s_psub[own] != NONE ? key | KEY_PSUB : key;
   w.g_link[s] = link;
 }
 
@@ -311,16 +312,18 @@ void launch_segment_props(const Work& w, uint32_t nsegs, uint32_t nclients, uint
 
 // --------------------------------------------------------------------------- key resolution
 // every item now knows its list: tag it YMap-entry (parentSub) or YArray member
+// (the kind rides in bit 31 of the key the item copied from its root: no gather of the key flags)
 __global__ void k_seg_kind(Work w, uint32_t nsegs) {
   const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
   if (s >= nsegs) return;
   const uint32_t f = w.g_flags[s];
   bool arr = false;
   if (f & SEG_ITEM) {
-    const uint32_t key = w.g_key[s];
-    if (key == NONE) raise_err(&w.ctr->err, ERR_DECODE);  // origin chain without a root
+    const uint32_t kv = w.g_key[s];
+    if (kv == NONE) raise_err(&w.ctr->err, ERR_DECODE);  // origin chain without a root
     else {
-      arr = !(w.k_flags[key] & KF_PSUB);
+      arr = !(kv & KEY_PSUB);
+      w.g_key[s] = kv & ~KEY_PSUB;
       w.g_flags[s] = f | (arr ? SEG_ARRAY : SEG_PSUB);
     }
   }
@@ -397,13 +400,14 @@ __global__ void k_winner_walk(Work w) {
     x = m - 1;
   }
   w.k_winner[k] = x;
+  w.g_flags[x] |= SEG_WIN;  // one winner per key: the only writer of x's flags in this kernel
 }
+// every entry item but the winner is deleted (overwritten): a flag test, no gather of the key's winner
 __global__ void k_overwrite(Work w, uint32_t nsegs) {
   const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
   if (s >= nsegs) return;
   const uint32_t f = w.g_flags[s];
-  if (!(f & SEG_PSUB)) return;
-  if (w.k_winner[w.g_key[s]] != s) w.g_flags[s] = f | SEG_DEL;
+  if ((f & (SEG_PSUB | SEG_WIN)) == SEG_PSUB) w.g_flags[s] = f | SEG_DEL;
 }
 
 void launch_map_winner(const Work& w, uint32_t nsegs, hipStream_t s) {

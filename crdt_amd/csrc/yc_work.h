@@ -381,7 +381,10 @@ enum : uint32_t {
   SEG_PSUB = 128u,     // member of a YMap entry list (parentSub)
   SEG_OLOW = 256u,     // its client index is below its origin's (a YATA sibling placed before the
                        // origin's own-client successor: that successor cannot merge, k_children)
+  SEG_WIN = 512u,      // the value of its YMap entry (k_winner_walk); every other entry item is deleted
 };
+// bit 31 of g_key between k_seg_props and k_seg_kind: the list is a YMap entry (key slots < 2^31)
+constexpr uint32_t KEY_PSUB = 0x80000000u;
 // key flags
 enum : uint32_t {
   KF_PSUB = 1u,        // the list is a YMap entry (items carry a parentSub)
