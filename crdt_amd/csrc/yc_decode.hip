@@ -38,6 +38,10 @@ __device__ __forceinline__ uint64_t win8(const uint8_t* __restrict__ b, uint32_t
   const uint32_t* d = (const uint32_t*)(b + (p & ~3u));  // the batch buffer is padded past its end
   return ((uint64_t)d[0] | ((uint64_t)d[1] << 32)) >> ((p & 3u) * 8);
 }
+__device__ __forceinline__ uint32_t win4(const uint8_t* __restrict__ b, uint32_t p) {
+  const uint32_t* d = (const uint32_t*)(b + (p & ~3u));  // the batch buffer is padded past its end
+  return __builtin_amdgcn_alignbyte(d[1], d[0], p & 3u);  // v_alignbyte_b32: the shift counts bytes
+}
 // Byte sources for the sizer: the slice's bytes staged in LDS (plus a halo past its end), with
 // a fallback to the batch buffer (through the caches) for reads beyond the staged window.
 struct LdsSrc {
@@ -53,18 +57,32 @@ struct LdsSrc {
     if (o + 8 <= wlen) return ((uint64_t)lw[o >> 2] | ((uint64_t)lw[(o >> 2) + 1] << 32)) >> ((o & 3u) * 8);
     return win8(b, p);
   }
+  __device__ __forceinline__ uint32_t w4(uint32_t p) const {
+    const uint32_t o = p - s0;
+    if (o + 4 <= wlen) return __builtin_amdgcn_alignbyte(lw[(o >> 2) + 1], lw[o >> 2], o & 3u);
+    return win4(b, p);
+  }
 };
+// varuint from a 4-byte window (+ the fifth byte when the first four all continue): one funnel
+// shift and a 7-bit-group compaction in 32-bit arithmetic; lib0 0.2.42 accumulates in 32 bits,
+// so the fifth byte contributes its low four bits
 template <class S>
 __device__ __forceinline__ uint32_t vu_fast(const S& b, uint32_t& p, uint32_t end, bool& ok) {
-  const uint64_t w = b.w8(p);
-  const uint64_t t = ~w & 0x8080808080ull;  // terminal bytes among the first five
-  const uint32_t len = t ? ((uint32_t)__builtin_ctzll(t) >> 3) + 1 : 6u;
-  uint64_t v = (w & 0x7full) | ((w >> 1) & (0x7full << 7)) | ((w >> 2) & (0x7full << 14)) | ((w >> 3) & (0x7full << 21)) |
-               ((w >> 4) & (0x7full << 28));
-  v &= len >= 5 ? ~0ull : ((1ull << (7 * len)) - 1);
+  const uint32_t w = b.w4(p);
+  const uint32_t t = ~w & 0x80808080u;  // terminal bytes among the first four
+  uint32_t v = (w & 0x7fu) | ((w >> 1) & 0x3f80u) | ((w >> 2) & 0x1fc000u) | ((w >> 3) & 0xfe00000u);
+  uint32_t len;
+  if (t) {
+    len = ((uint32_t)__builtin_ctz(t) >> 3) + 1;
+    v &= len >= 4 ? 0x0FFFFFFFu : ((1u << (7 * len)) - 1u);
+  } else {
+    const uint32_t b4 = b.u8(p + 4);
+    len = b4 < 0x80u ? 5u : 6u;
+    v |= b4 << 28;
+  }
   ok = ok && len <= 5 && end - p >= len && p < end;
   p += len;
-  return (uint32_t)v;  // lib0 0.2.42 accumulates in 32 bits
+  return v;
 }
 __device__ __forceinline__ void skip_n(uint32_t& p, uint32_t n, uint32_t end, bool& ok) {
   const bool f = p <= end && n <= end - p;
@@ -272,6 +290,26 @@ struct GlobalSrc {
   const uint8_t* __restrict__ b;
   __device__ __forceinline__ uint32_t u8(uint32_t p) const { return b[p]; }
   __device__ __forceinline__ uint64_t w8(uint32_t p) const { return win8(b, p); }
+  __device__ __forceinline__ uint32_t w4(uint32_t p) const { return win4(b, p); }
+};
+// parse_struct's byte source for the exact decode: varuints / varInts read word-wide from the
+// batch buffer instead of byte by byte (the same values and the same accept / reject)
+struct FastSrc {
+  const uint8_t* __restrict__ b;
+  __device__ __forceinline__ uint32_t u8(uint32_t p) const { return b[p]; }
+  __device__ __forceinline__ uint64_t w8(uint32_t p) const { return win8(b, p); }
+  __device__ __forceinline__ uint32_t w4(uint32_t p) const { return win4(b, p); }
+  __device__ __forceinline__ uint32_t vu(uint32_t& p, uint32_t end, bool& ok) const {
+    if (p >= end) { ok = false; return 0; }
+    return vu_fast(*this, p, end, ok);
+  }
+  __device__ __forceinline__ void svi(uint32_t& p, uint32_t end, bool& ok) const {  // readVarInt: at most 7 bytes
+    if (p >= end) { ok = false; return; }
+    const uint64_t t = ~win8(b, p) & 0x80808080808080ull;
+    const uint32_t len = t ? ((uint32_t)__builtin_ctzll(t) >> 3) + 1 : 8u;
+    ok = ok && len <= 7 && end - p >= len;
+    p = ok ? p + len : end;
+  }
 };
 __device__ __forceinline__ uint32_t chain_step(const uint8_t* __restrict__ b, uint32_t p, uint32_t uend) {
   const uint32_t d = chain_len(GlobalSrc{b}, b, p, uend);
@@ -1015,7 +1053,7 @@ __global__ __launch_bounds__(256) void k_struct_decode(Work w, uint32_t nstructs
   const uint32_t doc = doc_of_update(w, sec.upd);
   StructView v;
   uint32_t p = p0;
-  if (parse_struct<true>(w.bytes, p, uend, 0xFFFFFFFFu, &v) <= 0) { raise_err(err, ERR_DECODE); return; }
+  if (parse_struct<true, 32, FastSrc>(FastSrc{w.bytes}, p, uend, 0xFFFFFFFFu, &v) <= 0) { raise_err(err, ERR_DECODE); return; }
   w.s_len[i] = v.len;
   w.s_info[i] = v.info;
   w.s_cidx[i] = sec.cidx;

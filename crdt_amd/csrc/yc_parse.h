@@ -142,46 +142,55 @@ struct StructView {
   uint32_t nel;        // Any/JSON element count
 };
 
+// Byte sources for parse_struct: the lib0 readers over a plain pointer (host and device); the
+// device decoder passes a source with word-wide varuint reads (yc_decode.hip FastSrc).
+struct RawSrc {
+  const uint8_t* __restrict__ b;
+  YC_HDI uint32_t u8(uint32_t p) const { return b[p]; }
+  YC_HDI uint32_t vu(uint32_t& p, uint32_t end, bool& ok) const { return rd_vu(b, p, end, ok); }
+  YC_HDI void svi(uint32_t& p, uint32_t end, bool& ok) const { skip_vi(b, p, end, ok); }
+};
+
 // Parses one struct starting at p. FULL fills `v`. Speculative callers pass a finite
 // step budget; exact callers pass 0xFFFFFFFF. Returns 1 = ok, 0 = malformed, -1 = budget hit,
 // -2 = ran past `end` (only distinguishable from 0 when `end` is not the update end).
-template <bool FULL, int DEPTH = 32>
-YC_HD inline int parse_struct(const uint8_t* __restrict__ b, uint32_t& p, uint32_t end, uint32_t steps, StructView* v) {
+template <bool FULL, int DEPTH = 32, class Src = RawSrc>
+YC_HD inline int parse_struct(const Src& b, uint32_t& p, uint32_t end, uint32_t steps, StructView* v) {
   bool ok = true;
   if (p >= end) return -2;
-  uint32_t info = b[p++];
+  uint32_t info = b.u8(p++);
   uint32_t ref = info & 31u;
   if (FULL) { v->info = (uint8_t)info; v->ref = (uint8_t)ref; v->pkind = 0; v->has_psub = 0; v->nel = 0; }
   if (ref == REF_GC || ref == REF_SKIP) {
-    uint32_t len = rd_vu(b, p, end, ok);
+    uint32_t len = b.vu(p, end, ok);
     if (FULL) { v->len = len; v->cpos = v->cend = p; }
     return ok ? 1 : (p >= end ? -2 : 0);
   }
   if (ref > REF_DOC) return 0;
   if (info & 0x80u) {
-    uint32_t c = rd_vu(b, p, end, ok), k = rd_vu(b, p, end, ok);
+    uint32_t c = b.vu(p, end, ok), k = b.vu(p, end, ok);
     if (FULL) { v->oc = c; v->ok_ = k; }
   }
   if (info & 0x40u) {
-    uint32_t c = rd_vu(b, p, end, ok), k = rd_vu(b, p, end, ok);
+    uint32_t c = b.vu(p, end, ok), k = b.vu(p, end, ok);
     if (FULL) { v->rc = c; v->rk = k; }
   }
   if (!ok) return p >= end ? -2 : 0;
   if ((info & 0xC0u) == 0) {
-    uint32_t pinfo = rd_vu(b, p, end, ok);
+    uint32_t pinfo = b.vu(p, end, ok);
     if (!ok) return p >= end ? -2 : 0;
     if (pinfo == 1) {
       uint32_t st = p;
-      uint32_t n = rd_vu(b, p, end, ok);
+      uint32_t n = b.vu(p, end, ok);
       if (ok) skip_bytes(p, n, end, ok);
       if (FULL) { v->pkind = 1; v->pa = st; v->pb = p - st; }
     } else {
-      uint32_t c = rd_vu(b, p, end, ok), k = rd_vu(b, p, end, ok);
+      uint32_t c = b.vu(p, end, ok), k = b.vu(p, end, ok);
       if (FULL) { v->pkind = 2; v->pa = c; v->pb = k; }
     }
     if (info & 0x20u) {
       uint32_t st = p;
-      uint32_t n = rd_vu(b, p, end, ok);
+      uint32_t n = b.vu(p, end, ok);
       if (ok) skip_bytes(p, n, end, ok);
       if (FULL) { v->has_psub = 1; v->psub_pos = st; v->psub_len = p - st; }
     }
@@ -190,36 +199,36 @@ YC_HD inline int parse_struct(const uint8_t* __restrict__ b, uint32_t& p, uint32
   uint32_t cpos = p;
   uint32_t len = 1;
   switch (ref) {
-    case REF_DELETED: len = rd_vu(b, p, end, ok); break;
+    case REF_DELETED: len = b.vu(p, end, ok); break;
     case REF_JSON: {
-      uint32_t n = rd_vu(b, p, end, ok);
+      uint32_t n = b.vu(p, end, ok);
       len = n;
       for (uint32_t i = 0; i < n && ok; ++i) {
         if (steps == 0) return -1;
         --steps;
-        uint32_t k = rd_vu(b, p, end, ok);
-        if (ok && (k == 0 || (p < end && !json_start_ok(b[p])))) return 0;
+        uint32_t k = b.vu(p, end, ok);
+        if (ok && (k == 0 || (p < end && !json_start_ok(b.u8(p))))) return 0;
         if (ok) skip_bytes(p, k, end, ok);
       }
       if (FULL) v->nel = n;
       if (ok && steps == 0) return -1;
       break;
     }
-    case REF_BINARY: { uint32_t k = rd_vu(b, p, end, ok); if (ok) skip_bytes(p, k, end, ok); break; }
+    case REF_BINARY: { uint32_t k = b.vu(p, end, ok); if (ok) skip_bytes(p, k, end, ok); break; }
     case REF_EMBED: {
-      uint32_t k = rd_vu(b, p, end, ok);
-      if (ok && (k == 0 || (p < end && !json_start_ok(b[p])))) return 0;
+      uint32_t k = b.vu(p, end, ok);
+      if (ok && (k == 0 || (p < end && !json_start_ok(b.u8(p))))) return 0;
       if (ok) skip_bytes(p, k, end, ok);
       break;
     }
     case REF_STRING: {
-      uint32_t k = rd_vu(b, p, end, ok);
+      uint32_t k = b.vu(p, end, ok);
       uint32_t st = p;
       if (ok) skip_bytes(p, k, end, ok);
       if (ok && FULL) {  // ContentString length counts UTF-16 code units
         uint32_t u = 0;
         for (uint32_t i = st; i < st + k; ++i) {
-          uint32_t c = b[i];
+          uint32_t c = b.u8(i);
           if ((c & 0xC0u) != 0x80u) u += (c >= 0xF0u) ? 2u : 1u;
         }
         len = u;
@@ -227,36 +236,36 @@ YC_HD inline int parse_struct(const uint8_t* __restrict__ b, uint32_t& p, uint32
       break;
     }
     case REF_FORMAT: {
-      uint32_t k = rd_vu(b, p, end, ok);
+      uint32_t k = b.vu(p, end, ok);
       if (ok) skip_bytes(p, k, end, ok);
-      k = rd_vu(b, p, end, ok);
-      if (ok && (k == 0 || (p < end && !json_start_ok(b[p])))) return 0;
+      k = b.vu(p, end, ok);
+      if (ok && (k == 0 || (p < end && !json_start_ok(b.u8(p))))) return 0;
       if (ok) skip_bytes(p, k, end, ok);
       break;
     }
     case REF_TYPE: {
-      uint32_t tr = rd_vu(b, p, end, ok);
-      if (ok && (tr == 3 || tr == 5)) { uint32_t k = rd_vu(b, p, end, ok); if (ok) skip_bytes(p, k, end, ok); }
+      uint32_t tr = b.vu(p, end, ok);
+      if (ok && (tr == 3 || tr == 5)) { uint32_t k = b.vu(p, end, ok); if (ok) skip_bytes(p, k, end, ok); }
       if (tr > 6) ok = false;
       break;
     }
     case REF_ANY: {
-      uint32_t n = rd_vu(b, p, end, ok);
+      uint32_t n = b.vu(p, end, ok);
       len = n;
       for (uint32_t i = 0; i < n && ok; ++i) {
-        const uint32_t tag = p < end ? b[p] : 0u;
+        const uint32_t tag = p < end ? b.u8(p) : 0u;
         if (p < end && steps > 0 && tag >= 116u && tag <= 127u && tag != 117u && tag != 118u) {  // a scalar: skip_any's one step
           --steps;
           ++p;
           switch (tag) {
-            case 125: skip_vi(b, p, end, ok); break;
+            case 125: b.svi(p, end, ok); break;
             case 124: skip_bytes(p, 4, end, ok); break;
             case 123: case 122: skip_bytes(p, 8, end, ok); break;
-            case 119: case 116: { const uint32_t k = rd_vu(b, p, end, ok); if (ok) skip_bytes(p, k, end, ok); break; }
+            case 119: case 116: { const uint32_t k = b.vu(p, end, ok); if (ok) skip_bytes(p, k, end, ok); break; }
             default: break;  // 127 undefined, 126 null, 121 false, 120 true
           }
         } else {
-          const AnySkip r = skip_any_nl<DEPTH>(b, p, end, steps);
+          const AnySkip r = skip_any_nl<DEPTH>(b.b, p, end, steps);
           p = r.p;
           steps = r.steps;
           ok = r.ok != 0;
@@ -267,10 +276,10 @@ YC_HD inline int parse_struct(const uint8_t* __restrict__ b, uint32_t& p, uint32
       break;
     }
     case REF_DOC: {
-      uint32_t k = rd_vu(b, p, end, ok);
+      uint32_t k = b.vu(p, end, ok);
       if (ok) skip_bytes(p, k, end, ok);
       if (ok) {
-        const AnySkip r = skip_any_nl<DEPTH>(b, p, end, steps);
+        const AnySkip r = skip_any_nl<DEPTH>(b.b, p, end, steps);
         p = r.p;
         steps = r.steps;
         ok = r.ok != 0;
@@ -283,6 +292,11 @@ YC_HD inline int parse_struct(const uint8_t* __restrict__ b, uint32_t& p, uint32
   if (FULL) { v->len = len; v->cpos = cpos; v->cend = p; }
   if (!ok && p >= end) return -2;  // ran out of input (the struct may continue past `end`)
   return ok ? 1 : 0;
+}
+
+template <bool FULL, int DEPTH = 32>
+YC_HD inline int parse_struct(const uint8_t* __restrict__ b, uint32_t& p, uint32_t end, uint32_t steps, StructView* v) {
+  return parse_struct<FULL, DEPTH, RawSrc>(RawSrc{b}, p, end, steps, v);
 }
 
 YC_HDI uint32_t vu_size_host(uint32_t v) {

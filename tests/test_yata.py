@@ -38,7 +38,7 @@ def test_oracle_matches_yjs_many_replicas(i):
 @pytest.mark.parametrize("i", range(6))
 def test_tree_order_equals_sequential_loop(i):
     c = _cases()[i]
-    tot = [0, 0, 0]
+    tot = [0, 0, 0, 0]
     proto.check([bytes.fromhex(u) for u in c["updates"]], c["name"], tot)
     assert tot[2] < tot[0]  # the sibling loops scan less than the whole-list loop
 
@@ -46,7 +46,7 @@ def test_tree_order_equals_sequential_loop(i):
 def test_tree_order_on_seeded_histories():
     from tests.histories import array_history
 
-    tot = [0, 0, 0]
+    tot = [0, 0, 0, 0]
     for seed in range(25):
         states, wire = array_history(7100 + seed, n_replicas=2 + seed % 9, rounds=2 + seed % 4, ops=3 + seed % 9)
         proto.check(states + wire, f"seed {seed}", tot)
