@@ -595,6 +595,12 @@ __global__ __launch_bounds__(64) void k_walk(Work w) {
         for (uint32_t l = 0; l < 64 && j0 + l < nch; ++l) {
           const uint32_t s_l = ustart + (j0 + l) * SCHUNK, e_l = min(s_l + SCHUNK, uend);
           const uint32_t off = E - s_l;
+          if (E >= e_l) {  // a long struct jumps over the whole chunk: no structs in it
+            ent[l + 1] = E;
+            cnt[l] = 0;
+            L = l + 1;
+            continue;
+          }
           if (off >= XK) break;
           const uint32_t v = tab[l * XK + off];
           if ((v & 0xFFFFu) == XFAR) break;
@@ -644,10 +650,12 @@ __global__ __launch_bounds__(64) void k_walk(Work w) {
       const uint32_t excl = incl - (lane <= f ? C : 0u);
       const uint64_t ends = __ballot(lane <= f && valid && incl >= r);
       const uint32_t nw = valid ? (ce - cs + 63) >> 6 : 0u;
-      // chains locked into a wrong phase fail one speculation per step: hand the update to the
-      // exit tables (k_xtab + k_walk<true>); the marks made so far are true and are made again
+      // chains locked into a wrong phase fail (nearly) every speculation: hand the update to the
+      // exit tables (k_xtab + k_walk<true>); the marks made so far are true and are made again.
+      // A failure where the true exit jumps past the next chunk (a long struct) is no sign of it.
       ++steps;
-      if (!TABLES && !ends && f < 63 && j0 + f + 1 < nch && ++fails >= 4 && fails * 4 > steps) {
+      const uint32_t Xf = __shfl(X, f), cef = __shfl(ce, f);
+      if (!TABLES && !ends && f < 63 && j0 + f + 1 < nch && Xf < cef + SCHUNK && ++fails >= 6 && fails * 4 > steps * 3) {
         hand_over();
         return;
       }

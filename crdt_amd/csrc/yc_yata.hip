@@ -506,27 +506,44 @@ __global__ __launch_bounds__(256) void k_tsib_big(Work w, uint32_t nsegs) {
   for (uint32_t i = threadIdx.x; i < THASH; i += blockDim.x) { hkey[i] = NONE; hval[i] = NONE; }
   __syncthreads();
   // anchors: the first member (lowest position) of every outside right-origin unit
-  for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) {
-    if (w.y_confl[a + i] != NONE) continue;
-    const uint32_t r0 = w.y_before[a + i], r = r0 == NONE ? HNONE : r0;
-    uint32_t slot = (r * 2654435761u) & (THASH - 1);
-    for (uint32_t probe = 0;; ++probe) {
-      if (probe == THASH) { raise_err(&w.ctr->err, ERR_CAPACITY); break; }
-      const uint32_t old = atomicCAS(&hkey[slot], NONE, r);
-      if (old == NONE || old == r) { atomicMin(&hval[slot], i); break; }
-      slot = (slot + 1) & (THASH - 1);
+  // (loops over the members take 4 coalesced elements per lane per round: their loads are
+  // independent, so a huge group costs rounds of bandwidth, not rounds of latency)
+  constexpr uint32_t U4 = 4;
+  for (uint32_t i0 = threadIdx.x; i0 < n; i0 += blockDim.x * U4) {
+    uint32_t rc[U4];
+#pragma unroll
+    for (uint32_t u = 0; u < U4; ++u) { const uint32_t i = i0 + u * blockDim.x; rc[u] = i < n ? w.y_confl[a + i] : 0u; }
+#pragma unroll
+    for (uint32_t u = 0; u < U4; ++u) {
+      const uint32_t i = i0 + u * blockDim.x;
+      if (i >= n || rc[u] != NONE) continue;
+      const uint32_t r0 = w.y_before[a + i], r = r0 == NONE ? HNONE : r0;
+      uint32_t slot = (r * 2654435761u) & (THASH - 1);
+      for (uint32_t probe = 0;; ++probe) {
+        if (probe == THASH) { raise_err(&w.ctr->err, ERR_CAPACITY); break; }
+        const uint32_t old = atomicCAS(&hkey[slot], NONE, r);
+        if (old == NONE || old == r) { atomicMin(&hval[slot], i); break; }
+        slot = (slot + 1) & (THASH - 1);
+      }
     }
   }
   __syncthreads();
-  for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) {
-    uint32_t t = w.y_confl[a + i];
-    if (t == NONE) {
-      const uint32_t r0 = w.y_before[a + i], r = r0 == NONE ? HNONE : r0;
-      uint32_t slot = (r * 2654435761u) & (THASH - 1);
-      for (uint32_t probe = 0; probe < THASH && hkey[slot] != r; ++probe) slot = (slot + 1) & (THASH - 1);
-      t = (hkey[slot] == r ? a + hval[slot] : a + i) | 0x80000000u;
+  for (uint32_t i0 = threadIdx.x; i0 < n; i0 += blockDim.x * U4) {
+    uint32_t t[U4];
+#pragma unroll
+    for (uint32_t u = 0; u < U4; ++u) { const uint32_t i = i0 + u * blockDim.x; t[u] = i < n ? w.y_confl[a + i] : 0u; }
+#pragma unroll
+    for (uint32_t u = 0; u < U4; ++u) {
+      const uint32_t i = i0 + u * blockDim.x;
+      if (i >= n) continue;
+      if (t[u] == NONE) {
+        const uint32_t r0 = w.y_before[a + i], r = r0 == NONE ? HNONE : r0;
+        uint32_t slot = (r * 2654435761u) & (THASH - 1);
+        for (uint32_t probe = 0; probe < THASH && hkey[slot] != r; ++probe) slot = (slot + 1) & (THASH - 1);
+        t[u] = (hkey[slot] == r ? a + hval[slot] : a + i) | 0x80000000u;
+      }
+      w.t_trep[a + i] = t[u];
     }
-    w.t_trep[a + i] = t;
   }
   __syncthreads();
   uint32_t nn = NONE;  // member count after collapsing chains (n > TLDS only)
@@ -534,28 +551,47 @@ __global__ __launch_bounds__(256) void k_tsib_big(Work w, uint32_t nsegs) {
     // t_mtail / t_prv / t_next hold NONE here (k_tprep) and serve as scratch:
     //   t_mtail[p] = 0   p is named as right origin by a member other than its chain successor
     //   t_prv[i]         the chain (node) of position i;  t_next[k]  first position of node k
-    for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) {
-      const uint32_t rp = w.y_confl[a + i];
-      if (rp == NONE) continue;
-      const uint32_t p = rp - a;
-      if (!(p + 1 == i && w.y_state[a + i] == w.y_state[a + p])) w.t_mtail[a + p] = 0;
+    for (uint32_t i0 = threadIdx.x; i0 < n; i0 += blockDim.x * U4) {
+      uint32_t rp[U4], ci[U4], cp[U4];
+#pragma unroll
+      for (uint32_t u = 0; u < U4; ++u) { const uint32_t i = i0 + u * blockDim.x; rp[u] = i < n ? w.y_confl[a + i] : NONE; }
+#pragma unroll
+      for (uint32_t u = 0; u < U4; ++u) {
+        const uint32_t i = i0 + u * blockDim.x;
+        const bool chk = rp[u] != NONE && rp[u] - a + 1 == i;  // a chain link candidate: compare clients
+        ci[u] = chk ? w.y_state[a + i] : 0u;
+        cp[u] = chk ? w.y_state[rp[u]] : 1u;
+      }
+#pragma unroll
+      for (uint32_t u = 0; u < U4; ++u)
+        if (rp[u] != NONE && ci[u] != cp[u]) w.t_mtail[rp[u]] = 0;
     }
     __syncthreads();
+    // chain numbering: CU consecutive positions per lane per round (vector-width loads, one
+    // workgroup scan per 256 x CU positions)
+    constexpr uint32_t CU = 8;
     uint32_t carry = 0;
-    for (uint32_t base = 0; base < n; base += blockDim.x) {
-      const uint32_t i = base + threadIdx.x;
-      uint32_t first = 0;
-      if (i < n) {
-        const bool link = i > 0 && w.y_confl[a + i] == a + i - 1 && w.y_state[a + i] == w.y_state[a + i - 1] &&
-                          w.t_mtail[a + i - 1] == NONE;
-        first = link ? 0u : 1u;
+    for (uint32_t base = 0; base < n; base += blockDim.x * CU) {
+      const uint32_t i0 = base + threadIdx.x * CU;
+      uint32_t fm = 0, cnt = 0;  // bit u: position i0 + u starts a chain
+#pragma unroll
+      for (uint32_t u = 0; u < CU; ++u) {
+        const uint32_t i = i0 + u;
+        if (i < n) {
+          const bool link = i > 0 && w.y_confl[a + i] == a + i - 1 && w.y_state[a + i] == w.y_state[a + i - 1] &&
+                            w.t_mtail[a + i - 1] == NONE;
+          if (!link) { fm |= 1u << u; ++cnt; }
+        }
       }
       uint32_t tot;
-      const uint32_t ex = block_excl_scan256(first, scan_sh, tot);
-      if (i < n) {
-        const uint32_t k = carry + ex + first - 1;
-        w.t_prv[a + i] = k;
-        if (first) w.t_next[a + k] = i;
+      uint32_t k = carry + block_excl_scan256(cnt, scan_sh, tot);  // chains started before i0
+#pragma unroll
+      for (uint32_t u = 0; u < CU; ++u) {
+        const uint32_t i = i0 + u;
+        if (i < n) {
+          if ((fm >> u) & 1u) { w.t_next[a + k] = i; ++k; }
+          w.t_prv[a + i] = k - 1;
+        }
       }
       carry += tot;
     }
@@ -590,15 +626,30 @@ __global__ __launch_bounds__(256) void k_tsib_big(Work w, uint32_t nsegs) {
     __syncthreads();
     // expand: node k spans positions nfirst[k] .. nfirst[k + 1] - 1, listed from the last down
     auto leftmost = [&](uint32_t k) { return (k + 1 < nn ? nfirst[k + 1] : n) - 1; };
-    for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) {
-      const uint32_t k = node[i];
-      uint32_t nx;
-      if (i > nfirst[k]) nx = i - 1;
-      else {
-        const uint32_t kn = rec[k].nxt;
-        nx = kn == S_NONE ? NONE : leftmost(kn);
+    for (uint32_t i0 = threadIdx.x; i0 < n; i0 += blockDim.x * U4) {
+      uint32_t k[U4], f[U4], nx[U4], sg[U4], sx[U4];
+#pragma unroll
+      for (uint32_t u = 0; u < U4; ++u) { const uint32_t i = i0 + u * blockDim.x; k[u] = i < n ? node[i] : 0u; }
+#pragma unroll
+      for (uint32_t u = 0; u < U4; ++u) f[u] = nfirst[k[u]];
+#pragma unroll
+      for (uint32_t u = 0; u < U4; ++u) {
+        const uint32_t i = i0 + u * blockDim.x;
+        if (i > f[u]) nx[u] = i - 1;
+        else {
+          const uint32_t kn = rec[k[u]].nxt;
+          nx[u] = kn == S_NONE ? NONE : leftmost(kn);
+        }
       }
-      w.t_nsib[w.t_seg[a + i]] = nx == NONE ? NONE : w.t_seg[a + nx];
+#pragma unroll
+      for (uint32_t u = 0; u < U4; ++u) {
+        const uint32_t i = i0 + u * blockDim.x;
+        sg[u] = i < n ? w.t_seg[a + i] : 0u;
+        sx[u] = i < n && nx[u] != NONE ? w.t_seg[a + nx[u]] : NONE;
+      }
+#pragma unroll
+      for (uint32_t u = 0; u < U4; ++u)
+        if (i0 + u * blockDim.x < n) w.t_nsib[sg[u]] = sx[u];
     }
     if (threadIdx.x == 0 && head_s != NONE) sib_publish(w, a, n, nsegs, leftmost(head_s));
     return;
