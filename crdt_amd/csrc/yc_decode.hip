@@ -529,7 +529,8 @@ __global__ __launch_bounds__(64) void k_walk(Work w) {
   const uint8_t* __restrict__ b = w.bytes;
   const uint64_t* __restrict__ spec = w.spec_bits;
   const uint32_t ustart = w.uoff[u], uend = ustart + w.ulen[u];
-  const uint32_t c0 = w.ugroup[u], nch = (w.ulen[u] + SCHUNK - 1) / SCHUNK;
+  const uint32_t CH = w.schunk;
+  const uint32_t c0 = w.ugroup[u], nch = (w.ulen[u] + CH - 1) / CH;
   uint32_t* err = &w.ctr->err;
   const bool L0 = lane == 0;
   uint32_t* slot = win + lane * DSTRIDE;
@@ -577,23 +578,24 @@ __global__ __launch_bounds__(64) void k_walk(Work w) {
     uint32_t r = n;
     while (r > 0) {
       if (p >= uend) { if (L0) { raise_err(err, ERR_DECODE); w.ctr->err_info = p; } return; }
-      const uint32_t j0 = (p - ustart) / SCHUNK, j = j0 + lane;
+      const uint32_t j0 = (p - ustart) / CH, j = j0 + lane;
       const bool valid = j < nch;
-      const uint32_t cs = ustart + j * SCHUNK;
-      const uint32_t ce = valid ? min(cs + SCHUNK, uend) : 0u;
+      const uint32_t cs = ustart + j * CH;
+      const uint32_t ce = valid ? min(cs + CH, uend) : 0u;
       if (valid) {
         if (TABLES) {
           const uint4* xt = (const uint4*)(w.xtab + (size_t)(c0 + j) * XK);
           for (uint32_t k = 0; k < XK / 4; ++k) ((uint4*)(tab + lane * XK))[k] = xt[k];
         }
-        for (uint32_t k = 0; k <= SW; ++k) { mc[k] = k < SW ? spec[(cs >> 6) + k] : 0ull; mw[k] = 0; }
+        const uint32_t nwc = (ce - cs + 63) >> 6;  // the chunk's words of spec_bits (no further)
+        for (uint32_t k = 0; k <= SW; ++k) { mc[k] = k < nwc ? spec[(cs >> 6) + k] : 0ull; mw[k] = 0; }
       }
       if (!TABLES && L0) nknown = 0;
       __syncthreads();
       if (TABLES && L0) {  // compose the exit tables from p
         uint32_t E = p, L = 0;
         for (uint32_t l = 0; l < 64 && j0 + l < nch; ++l) {
-          const uint32_t s_l = ustart + (j0 + l) * SCHUNK, e_l = min(s_l + SCHUNK, uend);
+          const uint32_t s_l = ustart + (j0 + l) * CH, e_l = min(s_l + CH, uend);
           const uint32_t off = E - s_l;
           if (E >= e_l) {  // a long struct jumps over the whole chunk: no structs in it
             ent[l + 1] = E;
@@ -655,7 +657,7 @@ __global__ __launch_bounds__(64) void k_walk(Work w) {
       // A failure where the true exit jumps past the next chunk (a long struct) is no sign of it.
       ++steps;
       const uint32_t Xf = __shfl(X, f), cef = __shfl(ce, f);
-      if (!TABLES && !ends && f < 63 && j0 + f + 1 < nch && Xf < cef + SCHUNK && ++fails >= 6 && fails * 4 > steps * 3) {
+      if (!TABLES && !ends && f < 63 && j0 + f + 1 < nch && Xf < cef + CH && ++fails >= 6 && fails * 4 > steps * 3) {
         hand_over();
         return;
       }

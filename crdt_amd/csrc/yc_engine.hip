@@ -220,6 +220,7 @@ struct ycrdt_batch {
   size_t udoc_off = 0;          // byte offset of udoc in `meta`
   std::vector<uint32_t> ulist;  // updates parsed through the chain tables, then the direct ones
   uint32_t nbig = 0;
+  uint32_t schunk = SCHUNK;     // chunk bytes of the large updates (layout)
   size_t ulist_off = 0;
   std::vector<Group> groups;
   uint32_t nbytes = 0;
@@ -262,6 +263,8 @@ void mark(ycrdt_engine* e, const char* name) {
 constexpr size_t DIRECT_MAX_BYTES = 16384;         // an update the direct lane walks whole
 constexpr size_t DIRECT_TINY_BYTES = 1024;         // always direct (a handful of structs)
 constexpr size_t DIRECT_MIN_COUNT = 1024;          // enough small updates to fill wavefronts
+constexpr size_t SMALL_BATCH_BYTES = size_t(1) << 20;  // chunk-path bytes up to which chunks are short
+constexpr uint32_t SCHUNK_SMALL = 256;
 
 // One staged input: host bytes, or a device buffer (a doc state already in HBM).
 struct Src {
@@ -284,6 +287,15 @@ void layout(ycrdt_batch* b, const std::vector<Src>& src, std::vector<uint32_t>& 
     if (len > DIRECT_MAX_BYTES || force == 1) return false;
     return force == 2 || nsmall >= DIRECT_MIN_COUNT || len <= DIRECT_TINY_BYTES;
   };
+  // chunk size: a lane walks its chunk serially, so a batch with little chunk-path input (a doc
+  // state and a few updates: the per-op path) takes short chunks; big ones the full SCHUNK
+  // (short enough that the walker's 64 lanes still span the largest update in one step)
+  size_t big_bytes = 0, big_max = 0;
+  for (const Src& x : src)
+    if (x.len && !direct(x.len)) { big_bytes += x.len; big_max = std::max(big_max, x.len); }
+  b->schunk = SCHUNK;
+  if (big_bytes <= SMALL_BATCH_BYTES)
+    while (b->schunk > SCHUNK_SMALL && (size_t)(b->schunk / 2) * 64 >= big_max) b->schunk /= 2;
   order.clear();
   for (size_t i = 0; i < src.size(); ++i) if (src[i].dev) order.push_back((uint32_t)i);
   for (size_t i = 0; i < src.size(); ++i) if (!src[i].dev) order.push_back((uint32_t)i);
@@ -300,10 +312,10 @@ void layout(ycrdt_batch* b, const std::vector<Src>& src, std::vector<uint32_t>& 
     } else {
       b->ugroup.push_back((uint32_t)b->groups.size());
       b->ulist.push_back(u);
-      for (size_t g = 0; g < len; g += SCHUNK) {
+      for (size_t g = 0; g < len; g += b->schunk) {
         Group G;
         G.start = (uint32_t)(off + g);
-        G.end = (uint32_t)std::min(off + len, off + g + SCHUNK);
+        G.end = (uint32_t)std::min(off + len, off + g + b->schunk);
         G.uend = (uint32_t)(off + len);
         G.upd = u;
         b->groups.push_back(G);
@@ -448,6 +460,7 @@ int run_decode(ycrdt_engine* e, ycrdt_batch* b, bool lazy, Decoded& D, bool gene
   w.ndocs = b->ndocs;
   w.ulist = (const uint32_t*)((const uint8_t*)b->meta.p + b->ulist_off);
   w.nbig = b->nbig;
+  w.schunk = b->schunk;
   w.nsmall = (uint32_t)b->ulist.size() - b->nbig;
   w.lazy = lazy ? 1u : 0u;
   {

@@ -60,6 +60,7 @@ struct Work {
   uint32_t ndocs = 1;
   const uint32_t* ulist = nullptr; // [nbig] updates on the chunk path, then [nsmall] parsed directly
   uint32_t nbig = 0, nsmall = 0;
+  uint32_t schunk = SCHUNK;        // chunk bytes of this batch's large updates (<= SCHUNK)
   uint32_t force_xtab = 0;         // YCRDT_DECODE=xtab: every large update takes the exit-table walk (tests)
   uint32_t lazy = 0;               // 1: mergeUpdates / diffUpdate decode (references kept raw)
   unsigned long long* dbg = nullptr; // YCRDT_DEBUG_YATA=1: k_yata work counters
