@@ -819,7 +819,7 @@ int run_merge(ycrdt_engine* e, ycrdt_batch* b, const std::unordered_map<uint32_t
       mark(e, "merge.winner");  // k_children alone (bench.py's roofline kernel)
       launch_map_winner(w, nsegs, s);
       mark(e, "merge.descent");
-      run_descent(w, nsegs, s);
+      run_descent(w, nsegs, s, !D.nested);  // no dead-type pass: merge flags apply the overwrite
       mark(e, "merge.dead_types");
       if (D.nested) run_dead_keys(w, nsegs, s);  // only lists under a parent item can die with it
       mark(e, "merge.yata");
@@ -832,9 +832,9 @@ int run_merge(ycrdt_engine* e, ycrdt_batch* b, const std::unordered_map<uint32_t
       }
       mark(e, "merge.merge_flags");
       if (!sh) {
-        launch_merge_flags(w, nsegs, s);
+        launch_merge_flags(w, nsegs, s, !D.nested);
       } else {
-        launch_merge_flags_only(w, nsegs, s);
+        launch_merge_flags_only(w, nsegs, s, !D.nested);
         launch_shard_export(w, nsegs, owner, shard, acc, s);
       }
     }

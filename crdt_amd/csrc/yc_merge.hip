@@ -414,10 +414,10 @@ void launch_map_winner(const Work& w, uint32_t nsegs, hipStream_t s) {
   if (nsegs) hipLaunchKernelGGL(k_children, dim3((nsegs + 255) / 256), dim3(256), 0, s, w, nsegs);
 }
 
-uint32_t run_descent(const Work& w, uint32_t nsegs, hipStream_t s) {
+uint32_t run_descent(const Work& w, uint32_t nsegs, hipStream_t s, bool fold) {
   if (!nsegs) return 0;
   hipLaunchKernelGGL(k_winner_walk, dim3(w.cap_keys / 256 + 1), dim3(256), 0, s, w);
-  hipLaunchKernelGGL(k_overwrite, dim3((nsegs + 255) / 256), dim3(256), 0, s, w, nsegs);
+  if (!fold) hipLaunchKernelGGL(k_overwrite, dim3((nsegs + 255) / 256), dim3(256), 0, s, w, nsegs);
   return 1;
 }
 
@@ -472,14 +472,19 @@ void run_dead_keys(const Work& w, uint32_t nsegs, hipStream_t s) {
 __device__ __forceinline__ bool content_mergeable(uint32_t ref) {  // ContentX.mergeWith
   return ref == REF_ANY || ref == REF_JSON || ref == REF_STRING || ref == REF_DELETED;
 }
-__global__ __launch_bounds__(256) void k_merge_flags(Work w, uint32_t nsegs) {
+// fold = 1: k_overwrite's deletion of the entry items that are not their key's winner is applied
+// here, on the flags as they are read (when no dead-type pass sits between the two)
+__device__ __forceinline__ uint32_t overwritten(uint32_t f, uint32_t fold) {
+  return (fold && (f & (SEG_PSUB | SEG_WIN)) == SEG_PSUB) ? f | SEG_DEL : f;
+}
+__global__ __launch_bounds__(256) void k_merge_flags(Work w, uint32_t nsegs, uint32_t fold) {
   const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
   if (s > nsegs) return;
   if (s == nsegs) { w.g_tmp[s] = 0; return; }
   bool merge = false;
-  const uint32_t fr = w.g_flags[s];
+  const uint32_t f0 = w.g_flags[s], fr = overwritten(f0, fold);
   if (s > 0 && w.g_cidx[s - 1] == w.g_cidx[s]) {
-    const uint32_t fl = w.g_flags[s - 1];
+    const uint32_t fl = overwritten(w.g_flags[s - 1], fold);
     const uint32_t gs = w.g_start[s];
     if ((fl & SEG_ITEM) == (fr & SEG_ITEM)) {
       if (!(fr & SEG_ITEM)) merge = true;  // GC + GC
@@ -494,7 +499,8 @@ __global__ __launch_bounds__(256) void k_merge_flags(Work w, uint32_t nsegs) {
       }
     }
   }
-  if (merge) w.g_flags[s] = fr | SEG_MERGE;
+  const uint32_t f1 = merge ? fr | SEG_MERGE : fr;
+  if (f1 != f0) w.g_flags[s] = f1;
   w.g_tmp[s] = merge ? 0u : 1u;
 }
 __global__ void k_out_first(Work w, uint32_t nsegs) {
@@ -579,8 +585,8 @@ void launch_merge_final(const Work& w, uint32_t nsegs, hipStream_t s) {
 }
 
 // the item-merge predicate only (a shard's part); launch_merge_tail numbers the output structs
-void launch_merge_flags_only(const Work& w, uint32_t nsegs, hipStream_t s) {
-  if (nsegs) hipLaunchKernelGGL(k_merge_flags, dim3(nsegs / 256 + 1), dim3(256), 0, s, w, nsegs);
+void launch_merge_flags_only(const Work& w, uint32_t nsegs, hipStream_t s, bool fold) {
+  if (nsegs) hipLaunchKernelGGL(k_merge_flags, dim3(nsegs / 256 + 1), dim3(256), 0, s, w, nsegs, fold ? 1u : 0u);
 }
 void launch_merge_tail(const Work& w, uint32_t nsegs, hipStream_t s) {
   if (!nsegs) return;
@@ -589,9 +595,9 @@ void launch_merge_tail(const Work& w, uint32_t nsegs, hipStream_t s) {
   hipMemcpyAsync(&w.ctr->nout, w.g_outid + nsegs, sizeof(uint32_t), hipMemcpyDeviceToDevice, s);
 }
 
-void launch_merge_flags(const Work& w, uint32_t nsegs, hipStream_t s) {
+void launch_merge_flags(const Work& w, uint32_t nsegs, hipStream_t s, bool fold) {
   if (!nsegs) return;
-  hipLaunchKernelGGL(k_merge_flags, dim3(nsegs / 256 + 1), dim3(256), 0, s, w, nsegs);
+  hipLaunchKernelGGL(k_merge_flags, dim3(nsegs / 256 + 1), dim3(256), 0, s, w, nsegs, fold ? 1u : 0u);
   scan_u32(w.tmp, w.tmp_bytes, w.g_tmp, w.g_outid, nsegs + 1, s);
   hipLaunchKernelGGL(k_out_first, dim3((nsegs + 255) / 256), dim3(256), 0, s, w, nsegs);
   hipMemcpyAsync(&w.ctr->nout, w.g_outid + nsegs, sizeof(uint32_t), hipMemcpyDeviceToDevice, s);

@@ -430,9 +430,9 @@ void launch_segments(const Work& w, uint32_t nclients, uint64_t nunits, hipStrea
 void launch_segment_props(const Work& w, uint32_t nsegs, uint32_t nclients, uint64_t nunits, hipStream_t s);
 uint32_t run_key_resolution(const Work& w, uint32_t nsegs, hipStream_t s);
 void launch_map_winner(const Work& w, uint32_t nsegs, hipStream_t s);
-uint32_t run_descent(const Work& w, uint32_t nsegs, hipStream_t s);
-void launch_merge_flags(const Work& w, uint32_t nsegs, hipStream_t s);
-void launch_merge_flags_only(const Work& w, uint32_t nsegs, hipStream_t s);
+uint32_t run_descent(const Work& w, uint32_t nsegs, hipStream_t s, bool fold_overwrite);
+void launch_merge_flags(const Work& w, uint32_t nsegs, hipStream_t s, bool fold_overwrite);
+void launch_merge_flags_only(const Work& w, uint32_t nsegs, hipStream_t s, bool fold_overwrite);
 void launch_merge_tail(const Work& w, uint32_t nsegs, hipStream_t s);
 // key-hash shards of one document (yc_merge.hip)
 void launch_key_shards(const Work& w, uint32_t nsegs, uint32_t nshards, uint32_t* key_shard, uint8_t* owner, hipStream_t s);
