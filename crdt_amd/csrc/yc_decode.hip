@@ -112,10 +112,71 @@ __device__ __forceinline__ bool any_simple(const S& b, uint32_t& p, uint32_t end
   }
 }
 constexpr uint32_t SIZER_MAX_ELEMS = 16;
+// Length of the varuint at p (1..5 bytes), 0 when its fifth byte still continues.
+template <class S>
+__device__ __forceinline__ uint32_t vu_len(const S& b, uint32_t p) {
+  const uint32_t t = ~b.w4(p) & 0x80808080u;
+  return t ? ((uint32_t)__builtin_ctz(t) >> 3) + 1 : (b.u8(p + 4) < 0x80u ? 5u : 0u);
+}
+// The sizer's fast path for the commonest struct shapes — an item placed by origin and / or right
+// origin (no parent info) whose content is Deleted, String, or Any with one scalar value (a map
+// set, a list insert): the ids are only skipped (terminal bytes, no value), so a struct step issues
+// a fraction of the general path's instructions. Exact lengths on valid structs, as spec_len;
+// NONE: another shape or anything spec_len must judge (running past `end`, long varInts).
+template <class S>
+__device__ __forceinline__ uint32_t spec_len_common(const S& b, uint32_t pos, uint32_t end, uint32_t ref, uint32_t bits) {
+  uint32_t p = pos + 1;
+  const uint32_t nid = ((bits >> 7) & 1u) * 2u + ((bits >> 6) & 1u) * 2u;  // origin / right origin: 2 varuints each
+  for (uint32_t k = 0; k < nid; ++k) {
+    const uint32_t l = vu_len(b, p);
+    if (!l) return NONE;
+    p += l;
+  }
+  if (ref == REF_ANY) {
+    const uint32_t w = b.w4(p);
+    if ((w & 0xFFu) != 1u) return NONE;  // one element
+    const uint32_t tag = (w >> 8) & 0xFFu;
+    p += 2;
+    if (tag == 125) {  // varInt: a first byte and up to three more here
+      const uint32_t t = ~b.w4(p) & 0x80808080u;
+      if (!t) return NONE;
+      p += ((uint32_t)__builtin_ctz(t) >> 3) + 1;
+    } else if (tag == 119) {  // string
+      const uint32_t l = vu_len(b, p);
+      if (!l || l > 4) return NONE;
+      const uint32_t n = b.w4(p) & 0x7Fu;
+      if (l > 1) return NONE;  // short strings only (one length byte)
+      p += 1 + n;
+    } else if (tag == 120 || tag == 121 || tag == 126 || tag == 127) {
+    } else if (tag == 124) {
+      p += 4;
+    } else if (tag == 123 || tag == 122) {
+      p += 8;
+    } else {
+      return NONE;
+    }
+  } else {  // Deleted: a length; String: a byte length and the bytes
+    const uint32_t w = b.w4(p);
+    const uint32_t t = ~w & 0x80808080u;
+    if (!t) return NONE;
+    const uint32_t l = ((uint32_t)__builtin_ctz(t) >> 3) + 1;
+    if (ref == REF_STRING) {
+      const uint32_t n = (w & 0x7fu) | ((w >> 1) & 0x3f80u) | ((w >> 2) & 0x1fc000u) | ((w >> 3) & 0xfe00000u);
+      p += l + (n & (l >= 4 ? 0x0FFFFFFFu : ((1u << (7 * l)) - 1u)));
+    } else {
+      p += l;
+    }
+  }
+  return p <= end && p - pos < 0x10000u ? p - pos : NONE;
+}
 // struct length, 0 = not a struct, 1 = hand over to parse_struct (many elements, deep nesting, Doc)
 template <class S>
 __device__ __forceinline__ uint32_t spec_len(const S& b, uint32_t pos, uint32_t end, uint32_t cls) {
   const uint32_t ref = cls / 8 + 1, bits = (cls % 8) << 5;
+  if ((bits & 0xC0u) && (ref == REF_ANY || ref == REF_STRING || ref == REF_DELETED)) {
+    const uint32_t d = spec_len_common(b, pos, end, ref, bits);
+    if (d != NONE) return d;
+  }
   bool ok = true;
   uint32_t p = pos + 1;
   if (bits & 0x80u) { vu_fast(b, p, end, ok); vu_fast(b, p, end, ok); }
@@ -193,6 +254,16 @@ constexpr uint32_t DW = 128;                    // window bytes per lane
 constexpr uint32_t DSTRIDE = DW / 4 + 4;        // words per lane slot (16-byte padded)
 constexpr uint32_t DREFILL = 48;
 constexpr uint32_t DL = 256;                    // lanes per direct workgroup
+// A window refill: all DW/16 loads issued before the first LDS store, so a refill costs one
+// memory round trip (a loop bounded by wlen waited on each load in turn). The batch buffer is
+// padded past its end, and bytes past wlen are never taken from the window.
+__device__ __forceinline__ void fill_window(uint32_t* slot, const uint4* __restrict__ g) {
+  uint4 v[DW / 16];
+#pragma unroll
+  for (uint32_t k = 0; k < DW / 16; ++k) v[k] = g[k];
+#pragma unroll
+  for (uint32_t k = 0; k < DW / 16; ++k) ((uint4*)slot)[k] = v[k];
+}
 // the exact parser out of line: inlined, its nested-`any` walker multiplies the register demand
 // of the lane loop (one wavefront per SIMD), and it only runs on the few handed-over structs
 __device__ __attribute__((noinline)) uint32_t exact_len(const uint8_t* __restrict__ b, uint32_t p, uint32_t end) {
@@ -213,7 +284,7 @@ __global__ __launch_bounds__(DL) void k_direct(Work w) {
     src.s0 = p & ~15u;
     src.wlen = min(DW, (uend + 15u - src.s0) & ~15u);
     const uint4* g = (const uint4*)(b + src.s0);
-    for (uint32_t k = 0; k < src.wlen / 16; ++k) ((uint4*)slot)[k] = g[k];
+    fill_window(slot, g);
   };
   w.dsstart[u] = NONE;
   bool ok = true;
@@ -333,7 +404,7 @@ __global__ __launch_bounds__(DL) void k_spec(Work w) {
     src.s0 = p & ~15u;
     src.wlen = min(DW, (uend + 15u - src.s0) & ~15u);
     const uint4* g = (const uint4*)(b + src.s0);
-    for (uint32_t k = 0; k < src.wlen / 16; ++k) ((uint4*)slot)[k] = g[k];
+    fill_window(slot, g);
   };
   uint64_t* __restrict__ spec = w.spec_bits;
   uint32_t p = G.start, word = G.start >> 6;
@@ -541,7 +612,7 @@ __global__ __launch_bounds__(64) void k_walk(Work w) {
     src.s0 = p & ~15u;
     src.wlen = min(DW, (uend + 15u - src.s0) & ~15u);
     const uint4* g = (const uint4*)(b + src.s0);
-    for (uint32_t k = 0; k < src.wlen / 16; ++k) ((uint4*)slot)[k] = g[k];
+    fill_window(slot, g);
   };
   if (L0) w.dsstart[u] = NONE;
   if (w.ulen[u] == 0) { if (L0) raise_err(err, ERR_DECODE); return; }
@@ -726,7 +797,7 @@ __global__ __launch_bounds__(DL) void k_xmark(Work w) {
     src.s0 = x & ~15u;
     src.wlen = min(DW, (uend + 15u - src.s0) & ~15u);
     const uint4* g = (const uint4*)(b + src.s0);
-    for (uint32_t k = 0; k < src.wlen / 16; ++k) ((uint4*)slot)[k] = g[k];
+    fill_window(slot, g);
   };
   refill(p);
   uint32_t word = p >> 6;
