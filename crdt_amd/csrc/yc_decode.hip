@@ -363,6 +363,45 @@ struct GlobalSrc {
   __device__ __forceinline__ uint64_t w8(uint32_t p) const { return win8(b, p); }
   __device__ __forceinline__ uint32_t w4(uint32_t p) const { return win4(b, p); }
 };
+// parse_struct's source for k_struct_decode: the struct's first bytes staged in the lane's LDS
+// window by one round of loads (SW_WIN bytes from the 16-byte line holding its start), the rest of
+// a longer struct read from the batch buffer; varuints / varInts word-wide as in FastSrc. The
+// field-by-field parse then waits on LDS instead of on one memory round trip per field.
+constexpr uint32_t SD_WIN = 64, SD_STRIDE = SD_WIN / 4 + 4;
+struct WinSrc {
+  const uint8_t* __restrict__ b;
+  const uint32_t* lw;
+  uint32_t s0;
+  __device__ __forceinline__ uint32_t u8(uint32_t p) const {
+    const uint32_t o = p - s0;
+    return o < SD_WIN ? (lw[o >> 2] >> ((o & 3u) * 8)) & 0xFFu : (uint32_t)b[p];
+  }
+  __device__ __forceinline__ uint32_t w4(uint32_t p) const {
+    const uint32_t o = p - s0;
+    if (o + 4 <= SD_WIN) return __builtin_amdgcn_alignbyte(lw[(o >> 2) + 1], lw[o >> 2], o & 3u);
+    return win4(b, p);
+  }
+  __device__ __forceinline__ uint64_t w8(uint32_t p) const {
+    const uint32_t o = p - s0;
+    if (o + 8 <= SD_WIN) {
+      const uint32_t i = o >> 2, sh = o & 3u;
+      const uint32_t lo = __builtin_amdgcn_alignbyte(lw[i + 1], lw[i], sh), hi = __builtin_amdgcn_alignbyte(lw[i + 2], lw[i + 1], sh);
+      return (uint64_t)lo | ((uint64_t)hi << 32);
+    }
+    return win8(b, p);
+  }
+  __device__ __forceinline__ uint32_t vu(uint32_t& p, uint32_t end, bool& ok) const {
+    if (p >= end) { ok = false; return 0; }
+    return vu_fast(*this, p, end, ok);
+  }
+  __device__ __forceinline__ void svi(uint32_t& p, uint32_t end, bool& ok) const {  // readVarInt: at most 7 bytes
+    if (p >= end) { ok = false; return; }
+    const uint64_t t = ~w8(p) & 0x80808080808080ull;
+    const uint32_t len = t ? ((uint32_t)__builtin_ctzll(t) >> 3) + 1 : 8u;
+    ok = ok && len <= 7 && end - p >= len;
+    p = ok ? p + len : end;
+  }
+};
 // parse_struct's byte source for the exact decode: varuints / varInts read word-wide from the
 // batch buffer instead of byte by byte (the same values and the same accept / reject)
 struct FastSrc {
@@ -1132,9 +1171,20 @@ __global__ __launch_bounds__(256) void k_struct_decode(Work w, uint32_t nstructs
   const Section sec = w.sections[w.s_sec[i]];
   const uint32_t uend = w.uoff[sec.upd] + w.ulen[sec.upd];
   const uint32_t doc = doc_of_update(w, sec.upd);
+  __shared__ __attribute__((aligned(16))) uint32_t win[256 * SD_STRIDE];
+  uint32_t* slot = win + threadIdx.x * SD_STRIDE;
+  const uint32_t s0 = p0 & ~15u;
+  {
+    const uint4* g = (const uint4*)(w.bytes + s0);  // the batch buffer is padded past its end
+    uint4 v4[SD_WIN / 16];
+#pragma unroll
+    for (uint32_t k = 0; k < SD_WIN / 16; ++k) v4[k] = g[k];
+#pragma unroll
+    for (uint32_t k = 0; k < SD_WIN / 16; ++k) ((uint4*)slot)[k] = v4[k];
+  }
   StructView v;
   uint32_t p = p0;
-  if (parse_struct<true, 32, FastSrc>(FastSrc{w.bytes}, p, uend, 0xFFFFFFFFu, &v) <= 0) { raise_err(err, ERR_DECODE); return; }
+  if (parse_struct<true, 32, WinSrc>(WinSrc{w.bytes, slot, s0}, p, uend, 0xFFFFFFFFu, &v) <= 0) { raise_err(err, ERR_DECODE); return; }
   w.s_len[i] = v.len;
   w.s_info[i] = v.info;
   w.s_cidx[i] = sec.cidx;
