@@ -39,41 +39,50 @@ __device__ __forceinline__ uint32_t copy_bytes(uint8_t* __restrict__ o, uint32_t
 // (Item.write Y@80416 / GC.write Y@68955 with the writeStructs offset, Y@18809).
 template <bool WRITE>
 __device__ uint32_t encode_struct(const Work& w, uint32_t nclients, uint32_t o, uint8_t* __restrict__ out, uint32_t p0) {
+  // The columns a struct can need are loaded in three dependent rounds — its first segment's row,
+  // then its source struct's and its client's, then the reference clients' — each round issued
+  // whole before anything branches on it, instead of one memory round trip per field.
   const uint32_t a = w.o_first[o], b = w.o_first[o + 1];
-  const uint32_t cidx = w.g_cidx[a];
-  const uint64_t base = w.cl_base[cidx];
-  const uint32_t k0 = (uint32_t)(w.g_start[a] - base), k1 = (uint32_t)(w.g_start[b] - base);
-  const uint32_t cs = w.cl_start[cidx];
+  const uint32_t cidx = w.g_cidx[a], ga = w.g_start[a], gb = w.g_start[b], f = w.g_flags[a], src = w.g_src[a];
+  const uint32_t go = w.g_origin[a], gr = w.g_rorigin[a];
+  const uint64_t base = w.cl_base[cidx], base1 = w.cl_base[cidx + 1];
+  const uint32_t cs = w.cl_start[cidx], cval = w.cl_vals[cidx];
+  const uint32_t info0 = w.s_info[src], soc = w.s_ocidx[src], src_rc = w.s_rcidx[src];
+  const uint32_t sclk = w.s_clock[src], slen = w.s_len[src], scel = w.s_celem[src], scend = w.s_cend[src];
+  const uint32_t k0 = (uint32_t)(ga - base), k1 = (uint32_t)(gb - base);
   if (k1 <= cs) return 0;
   const uint32_t off = cs > k0 ? cs - k0 : 0;
   const uint32_t len = k1 - k0;
-  const uint32_t f = w.g_flags[a];
-  const uint32_t src = w.g_src[a];
   uint32_t p = p0;
   if (!(f & SEG_ITEM)) {  // GC.write
     if (WRITE) { out[p++] = REF_GC; p = wr_vu(out, p, len - off); return p - p0; }
     return 1 + vu_size(len - off);
   }
   const bool del = (f & SEG_DEL) != 0;
-  const uint32_t ref = del ? (uint32_t)REF_DELETED : (w.s_info[src] & 31u);
+  const uint32_t ref = del ? (uint32_t)REF_DELETED : (info0 & 31u);
+  // the reference clients: the segment's own client first (an origin inside a split struct), then
+  // the source struct's recorded origin / right-origin client, a binary search last
+  auto client_of = [&](uint32_t g, uint32_t hint) -> uint32_t {
+    if (g >= base && g < base1) return cidx;
+    if (hint < nclients && g >= w.cl_base[hint] && g < w.cl_base[hint + 1]) return hint;
+    return unit_client(w, nclients, g);
+  };
   uint32_t oclient = 0, oclock = 0;
   bool has_o = false;
-  if (off > 0) { has_o = true; oclient = w.cl_vals[cidx]; oclock = k0 + off - 1; }
-  else if (w.g_origin[a] != NONE) {
-    const uint32_t g = w.g_origin[a];
-    const uint32_t c = unit_client_hint(w, nclients, g, cidx, w.s_ocidx[src]);
+  if (off > 0) { has_o = true; oclient = cval; oclock = k0 + off - 1; }
+  else if (go != NONE) {
+    const uint32_t c = client_of(go, soc);
     has_o = true;
-    oclient = w.cl_vals[c];
-    oclock = (uint32_t)(g - w.cl_base[c]);
+    oclient = c == cidx ? cval : w.cl_vals[c];
+    oclock = (uint32_t)(go - (c == cidx ? base : w.cl_base[c]));
   }
   bool has_r = false;
   uint32_t rclient = 0, rclock = 0;
-  if (w.g_rorigin[a] != NONE) {
-    const uint32_t g = w.g_rorigin[a];
-    const uint32_t c = unit_client_hint(w, nclients, g, w.s_rcidx[src], cidx);
+  if (gr != NONE) {
+    const uint32_t c = client_of(gr, src_rc);
     has_r = true;
-    rclient = w.cl_vals[c];
-    rclock = (uint32_t)(g - w.cl_base[c]);
+    rclient = c == cidx ? cval : w.cl_vals[c];
+    rclock = (uint32_t)(gr - (c == cidx ? base : w.cl_base[c]));
   }
   const bool psub = (f & SEG_PSUB) != 0;
   const uint32_t info = ref | (has_o ? 0x80u : 0u) | (has_r ? 0x40u : 0u) | (psub ? 0x20u : 0u);
@@ -106,6 +115,11 @@ __device__ uint32_t encode_struct(const Work& w, uint32_t nclients, uint32_t o, 
   if (del) {
     if (WRITE) p = wr_vu(out, p, len - off);
     size += vu_size(len - off);
+  } else if ((ref == REF_ANY || ref == REF_JSON) && b == a + 1 && off == 0 && k0 == sclk && len == slen) {
+    // the whole content of one source struct (the common case): its element bytes verbatim
+    const uint32_t nbytes = scend - scel;
+    if (WRITE) { p = wr_vu(out, p, len); p = copy_bytes(out, p, w.bytes + scel, nbytes); }
+    size += vu_size(len) + nbytes;
   } else if (ref == REF_ANY || ref == REF_JSON || ref == REF_STRING) {
     // elements of every segment from unit k0 + off on, sliced out of their source structs
     uint32_t nbytes = 0;
