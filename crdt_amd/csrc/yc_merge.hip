@@ -233,23 +233,26 @@ __device__ __forceinline__ uint64_t fnv_u32(uint64_t h, uint32_t v) {
 __global__ __launch_bounds__(256) void k_seg_props(Work w, uint32_t nsegs) {
   const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
   if (s >= nsegs) return;
+  // the source struct's columns in one round of loads (the right-origin clock is unwritten when
+  // there is none: read, never used), then the client bases
   const uint32_t g0 = w.g_start[s];
   const uint32_t own = w.u_owner[g0];
-  const uint32_t cidx = w.s_cidx[own];
-  const uint32_t k0 = (uint32_t)(g0 - w.cl_base[cidx]);
   const uint32_t f = w.u_flags[g0];
-  const uint32_t ref = w.s_info[own] & 31u;
+  const uint32_t cidx = w.s_cidx[own], ref = w.s_info[own] & 31u, sclk = w.s_clock[own];
+  const uint32_t socx = w.s_ocidx[own], socl = w.s_oclock[own], srcx = w.s_rcidx[own], srcl = w.s_rclock[own];
+  const uint64_t ob = socx < NONE - 1 ? w.cl_base[socx] : 0ull, rb = srcx < NONE - 1 ? w.cl_base[srcx] : 0ull;
+  const uint32_t k0 = (uint32_t)(g0 - w.cl_base[cidx]);
   uint32_t sf = 0;
   if (f & (UF_DEL | UF_DS)) sf |= SEG_DEL;
-  bool gc = (f & UF_GC) || ref == REF_GC;
-  const bool expl = k0 == w.s_clock[own];
+  bool gc = (f & UF_GC) || ref == REF_GC || socx == UNKNOWN || srcx == UNKNOWN;  // (unknown: k_refs raised PENDING)
+  const bool expl = k0 == sclk;
   if (expl) sf |= SEG_EXPLICIT;
   uint32_t origin = NONE, rorigin = NONE;
   if (!gc) {
     if (expl) {
-      if (w.s_ocidx[own] != NONE) origin = (uint32_t)(w.cl_base[w.s_ocidx[own]] + w.s_oclock[own]);
+      if (socx != NONE) origin = (uint32_t)(ob + socl);
     } else origin = g0 - 1;
-    if (w.s_rcidx[own] != NONE) rorigin = (uint32_t)(w.cl_base[w.s_rcidx[own]] + w.s_rclock[own]);
+    if (srcx != NONE) rorigin = (uint32_t)(rb + srcl);
     if ((origin != NONE && (w.u_flags[origin] & UF_GC)) || (rorigin != NONE && (w.u_flags[rorigin] & UF_GC))) gc = true;
   }
   uint32_t key = NONE, link = s;
