@@ -339,19 +339,18 @@ __global__ void k_seg_kind(Work w, uint32_t nsegs) {
 __global__ __launch_bounds__(256) void k_keyfind(Work w, uint32_t nsegs) {
   const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
   if (s >= nsegs) return;
-  const uint32_t f = w.g_flags[s];
-  if (w.g_key[s] != NONE || !(f & SEG_ITEM)) return;
+  const uint32_t f = w.g_flags[s], k_s = w.g_key[s];
   uint32_t x = w.g_link[s];
+  if (k_s != NONE || !(f & SEG_ITEM)) return;
   for (uint32_t it = 0; it < (1u << 22); ++it) {
-    if (!(w.g_flags[x] & SEG_ITEM)) {  // the origin chain ends in GC: getMissing drops the parent
+    const uint32_t fx = w.g_flags[x], k = w.g_key[x], y = w.g_link[x];  // one round of loads per hop
+    if (!(fx & SEG_ITEM)) {  // the origin chain ends in GC: getMissing drops the parent
       w.g_flags[s] = (f & ~SEG_ITEM) | SEG_GC | SEG_DEL;
       w.g_origin[s] = NONE;
       w.g_rorigin[s] = NONE;
       return;
     }
-    const uint32_t k = w.g_key[x];
     if (k != NONE) { w.g_key[s] = k; return; }
-    const uint32_t y = w.g_link[x];
     if (y == x) return;  // a chain without a root: k_seg_kind reports it
     const uint32_t z = w.g_link[y];
     if (z != y) w.g_link[x] = z;
