@@ -879,19 +879,33 @@ __global__ void k_popc(const uint64_t* __restrict__ bits, uint32_t* __restrict__
   if (i < nwords) cnt[i] = (uint32_t)__popcll(bits[i]);
   else if (i == nwords) cnt[i] = 0;
 }
-__global__ void k_scatter_pos(const uint64_t* __restrict__ bits, const uint32_t* __restrict__ pre, uint32_t nwords,
-                              uint32_t* __restrict__ out, uint32_t cap, uint32_t* err) {
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= nwords) return;
-  uint64_t x = bits[i];
-  uint32_t k = pre[i];
-  while (x) {
-    const uint32_t bit = (uint32_t)__ffsll((long long)x) - 1;
-    x &= x - 1;
-    if (k >= cap) { raise_err(err, ERR_CAPACITY); return; }
-    out[k++] = i * 64 + bit;
+// Dense positions of the set bits. A workgroup's 256 words stage their positions in LDS (each
+// lane writes its word's bits at its prefix offset) and the workgroup stores them as one
+// contiguous run: coalesced stores instead of every lane storing its ~5 positions at its own
+// offset, one divergent store per bit of the word with the most.
+constexpr uint32_t SCAT_LDS = 4096;
+__global__ __launch_bounds__(256) void k_scatter_pos(const uint64_t* __restrict__ bits, const uint32_t* __restrict__ pre, uint32_t nwords,
+                                                     uint32_t* __restrict__ out, uint32_t cap, uint32_t* err) {
+  __shared__ uint32_t buf[SCAT_LDS];
+  const uint32_t i0 = blockIdx.x * 256, i = i0 + threadIdx.x;
+  if (i0 >= nwords) return;
+  const uint32_t iend = min(i0 + 256, nwords);
+  const uint32_t base = pre[i0], total = pre[iend] - base;
+  if (base + total > cap) {
+    if (threadIdx.x == 0) raise_err(err, ERR_CAPACITY);
+    return;
   }
+  uint64_t x = i < nwords ? bits[i] : 0ull;
+  uint32_t k = i < nwords ? pre[i] : 0u;
+  if (total > SCAT_LDS) {  // a dense stretch: every lane stores its own positions
+    for (; x; x &= x - 1) out[k++] = i * 64 + (uint32_t)__ffsll((long long)x) - 1;
+    return;
+  }
+  for (k -= base; x; x &= x - 1) buf[k++] = i * 64 + (uint32_t)__ffsll((long long)x) - 1;
+  __syncthreads();
+  for (uint32_t t = threadIdx.x; t < total; t += 256) out[base + t] = buf[t];
 }
+
 __device__ __forceinline__ uint32_t rank_incl(const uint64_t* __restrict__ bits, const uint32_t* __restrict__ pre, uint32_t p) {
   return pre[p >> 6] + (uint32_t)__popcll(bits[p >> 6] & (((2ull << (p & 63)) - 1)));  // bits <= p
 }
