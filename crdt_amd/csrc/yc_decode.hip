@@ -316,7 +316,7 @@ __global__ __launch_bounds__(DL) void k_direct(Work w) {
         m = 0;
       }
       m |= 1ull << (p & 63);
-      if (p - src.s0 + DREFILL > src.wlen) refill(p);
+      if (__ballot(p - src.s0 + DREFILL > src.wlen)) refill(p);  // the whole wavefront at once: one stall, not one per lane
       const uint32_t info = src.u8(p), ref = info & 31u;
       uint32_t d = 0;
       if (ref == REF_GC || ref == REF_SKIP) {
@@ -456,7 +456,7 @@ __global__ __launch_bounds__(DL) void k_spec(Work w) {
       while (++word < (p >> 6)) spec[word] = 0;
     }
     m |= 1ull << (p & 63);
-    if (p - src.s0 + DREFILL > src.wlen) refill(p);
+    if (__ballot(p - src.s0 + DREFILL > src.wlen)) refill(p);  // the whole wavefront at once: one stall, not one per lane
     const uint32_t d = chain_len(src, b, p, uend);
     p += d ? d : 1u;
   }
