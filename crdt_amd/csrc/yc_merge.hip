@@ -44,13 +44,13 @@ __global__ __launch_bounds__(256) void k_owner(Work w, uint32_t nstructs) {
   uint64_t gb = 0;
   uint32_t n = 0, fl = 0;
   if (s < nstructs) {
-    const uint32_t ref = w.s_info[s] & 31u;
+    const uint32_t ref = w.s_info[s] & 31u, cidx = w.s_cidx[s], clock = w.s_clock[s], len = w.s_len[s];
+    const uint32_t st = w.cl_state[cidx];
+    const uint64_t cb = w.cl_base[cidx];
     if (ref != REF_SKIP) {
-      const uint32_t cidx = w.s_cidx[s];
-      const uint32_t clock = w.s_clock[s], st = w.cl_state[cidx];
       // units at or past the client's (capped) state stay out of the store
-      n = st > clock ? min(w.s_len[s], st - clock) : 0u;
-      gb = w.cl_base[cidx] + clock;
+      n = st > clock ? min(len, st - clock) : 0u;
+      gb = cb + clock;
       fl = ref == REF_DELETED ? UF_DEL : (ref == REF_GC ? (UF_GC | UF_DEL) : 0u);
     }
   }
@@ -113,28 +113,29 @@ __global__ __launch_bounds__(256) void k_ds_mark(Work w, uint32_t nds) {
 __global__ void k_refs(Work w, uint32_t nstructs) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= nstructs) return;
-  if (w.s_clock[i] >= w.cl_state[w.s_cidx[i]] || (w.s_info[i] & 31u) == REF_SKIP) return;  // not integrated
+  // the struct's columns in one round of loads (the right-origin clock and the parent are written
+  // only where present: read, used behind their presence tests), then the clients' states
+  const uint32_t clock = w.s_clock[i], cidx = w.s_cidx[i], ref = w.s_info[i] & 31u, pk = w.s_pk[i];
+  const uint32_t oc = w.s_ocidx[i], ok_ = w.s_oclock[i], rc = w.s_rcidx[i], rk = w.s_rclock[i];
+  const bool ov = oc < NONE - 1, rv = rc < NONE - 1;
+  const uint32_t st = w.cl_state[cidx], ost = ov ? w.cl_state[oc] : 0u, rst = rv ? w.cl_state[rc] : 0u;
+  const uint64_t ob = ov ? w.cl_base[oc] : 0ull, rb = rv ? w.cl_base[rc] : 0ull;
+  if (clock >= st || ref == REF_SKIP) return;  // not integrated
   // Item.getMissing (Y@76507): every reference of an integrated struct must be in the store
-  if (w.s_pk[i] == 2 && (w.s_pa[i] == UNKNOWN || w.s_pb[i] >= w.cl_state[w.s_pa[i]])) { raise_err(&w.ctr->err, ERR_PENDING); return; }
-  const uint32_t oc = w.s_ocidx[i];
+  if (pk == 2 && (w.s_pa[i] == UNKNOWN || w.s_pb[i] >= w.cl_state[w.s_pa[i]])) { raise_err(&w.ctr->err, ERR_PENDING); return; }
   if (oc != NONE) {
-    const uint32_t k = w.s_oclock[i];
-    if (oc == UNKNOWN || k >= w.cl_state[oc]) { raise_err(&w.ctr->err, ERR_PENDING); return; }
-    const uint32_t g = (uint32_t)(w.cl_base[oc] + k);
+    if (oc == UNKNOWN || ok_ >= ost) { raise_err(&w.ctr->err, ERR_PENDING); return; }
+    const uint32_t g = (uint32_t)(ob + ok_);
     // getItemCleanEnd(origin); only UF_CUT is written to u_flags in this kernel, so a plain
     // read-modify-write that races with another writer of the same bit is harmless
-    if (k + 1 < w.cl_state[oc] && !(w.u_flags[g + 1] & UF_CUT)) w.u_flags[g + 1] |= UF_CUT;
+    if (ok_ + 1 < ost && !(w.u_flags[g + 1] & UF_CUT)) w.u_flags[g + 1] |= UF_CUT;
   }
-  const uint32_t rc = w.s_rcidx[i];
   if (rc != NONE) {
-    const uint32_t k = w.s_rclock[i];
-    if (rc == UNKNOWN || k >= w.cl_state[rc]) { raise_err(&w.ctr->err, ERR_PENDING); return; }
-    const uint32_t g = (uint32_t)(w.cl_base[rc] + k);
+    if (rc == UNKNOWN || rk >= rst) { raise_err(&w.ctr->err, ERR_PENDING); return; }
+    const uint32_t g = (uint32_t)(rb + rk);
     if (!(w.u_flags[g] & UF_CUT)) w.u_flags[g] |= UF_CUT;              // getItemCleanStart(rightOrigin)
   }
 }
-
-// --------------------------------------------------------------------------- cuts -> segments
 __global__ __launch_bounds__(256) void k_cuts(Work w, uint64_t nunits) {
   const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   bool cut = false;
