@@ -514,7 +514,8 @@ def fleet_sync_leg(eng, n_pairs):
                 f.write(struct.pack("<I", len(u)) + u + struct.pack("<I", len(v)) + v)
             fname = f.name
         try:
-            r = subprocess.run([node, os.path.join(ROOT, "scripts", "yjs_baseline.js"), fname, "diff"],
+            wd = str(int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1))
+            r = subprocess.run([node, os.path.join(ROOT, "scripts", "yjs_baseline.js"), fname, "diff", wd],
                                capture_output=True, text=True, timeout=240)
             y = json.loads(r.stdout.strip().splitlines()[-1]) if r.returncode == 0 and r.stdout.strip() else None
         finally:
@@ -523,9 +524,10 @@ def fleet_sync_leg(eng, n_pairs):
             h = hashlib.sha256()
             for o in outs:
                 h.update(o)
-            res["yjs"] = {"pairs_per_s": round(y["pairs"] / (y["ms"] * 1e-3), 1), "cores": 1, "kind": "reference",
+            res["yjs"] = {"pairs_per_s": round(y["pairs"] / (y["ms"] * 1e-3), 1), "cores": y["workers"], "kind": "reference",
                           "ms": round(y["ms"], 2), "parity": y["out_sha256"] == h.hexdigest(),
-                          "sample": f"Yjs {y['yjs']} Y.diffUpdate over the same {y['pairs']} pairs in Node {y['node']}"}
+                          "sample": f"Yjs {y['yjs']} Y.diffUpdate over the same {y['pairs']} pairs in Node {y['node']}, "
+                                    f"worker_threads W={y['workers']} (os.cpus() = {y.get('cpus', 1)}, capped at the box's CPU share)"}
     return res
 
 

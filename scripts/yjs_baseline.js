@@ -7,7 +7,8 @@
 // tests/golden/gen/load_yjs.js. If it is absent the script prints {"available": false}.
 //
 // Usage: node yjs_baseline.js <batch file> [workers]
-//        node yjs_baseline.js <pairs file> diff   (update, state vector) alternating: Y.diffUpdate each
+//        node yjs_baseline.js <pairs file> diff [W]   (update, state vector) alternating: Y.diffUpdate each,
+//                                                   on W worker_threads
 //        node yjs_baseline.js <n ops> perop       crdt.js per-op path (bench.py per_op_leg)
 //        node yjs_baseline.js <fleet file> fleet W nDocs   C5 fleet ingest on W worker_threads
 //   batch file = u32le count, then per update u32le length + bytes (bench.py writes it)
@@ -105,6 +106,30 @@ if (isMainThread) {
     process.exit(0);
   }
   const ups = readBatch(file);
+  const dw = process.argv[3] === 'diff' ? Math.max(1, parseInt(process.argv[4] || '1', 10)) : 1;
+  if (dw > 1) {  // sync responder on W worker_threads: pair i answered by worker i % W
+    const { canonicalUpdate } = require(path.join(__dirname, '..', 'tests', 'golden', 'gen', 'v1.js'));
+    const npairs = Math.floor(ups.length / 2);
+    const outs = new Array(npairs);
+    let done = 0, maxMs = 0;
+    for (let w = 0; w < dw; w++) {
+      const wk = new Worker(__filename, { workerData: { diff: file, w, W: dw } });
+      wk.on('message', (m) => {
+        maxMs = Math.max(maxMs, m.ms);
+        m.outs.forEach((o, k) => { outs[w + k * dw] = Buffer.from(o); });
+        if (++done === dw) {
+          const h = crypto.createHash('sha256');
+          let bytes = 0;
+          for (const o of outs) { h.update(canonicalUpdate(o)); bytes += o.length; }
+          console.log(JSON.stringify({
+            available: true, yjs: '13.5.16', lib0: '0.2.42', node: process.version, workers: dw,
+            cpus: require('os').cpus().length, ms: maxMs, pairs: npairs, out_bytes: bytes, out_sha256: h.digest('hex'),
+          }));
+        }
+      });
+    }
+    return;
+  }
   if (process.argv[3] === 'diff') {  // sync responder: (update, sv) pairs, Y.diffUpdate each, one core
     const { canonicalUpdate } = require(path.join(__dirname, '..', 'tests', 'golden', 'gen', 'v1.js'));
     const outs = [];
@@ -140,6 +165,15 @@ if (isMainThread) {
       });
     }
   }
+} else if (workerData.diff) {  // sync-responder worker: pairs i with i % W == w
+  const Y = load();
+  const ups = readBatch(workerData.diff);
+  const { w, W } = workerData;
+  const outs = [];
+  const t0 = process.hrtime.bigint();  // the worker's own Y.diffUpdate calls (load / parse excluded)
+  for (let i = w; 2 * i + 1 < ups.length; i += W) outs.push(Y.diffUpdate(ups[2 * i], ups[2 * i + 1]));
+  const ms = Number(process.hrtime.bigint() - t0) / 1e6;
+  parentPort.postMessage({ ms, outs });
 } else if (workerData.fleet) {  // fleet worker: documents d with d % W == w
   const Y = load();
   const { canonicalUpdate } = require(path.join(__dirname, '..', 'tests', 'golden', 'gen', 'v1.js'));
