@@ -55,6 +55,18 @@ __device__ __forceinline__ void wave_count_add(uint32_t* ctr, bool pred) {
   if (m && (threadIdx.x & 63u) == (uint32_t)__ffsll((long long)m) - 1) atomicAdd(ctr, (uint32_t)__popcll(m));
 }
 
+// the same over NSHARD counter words picked by workgroup: one counter word takes ≈88 atomics per
+// µs (MI355X_MICROARCH.md, dequeue row), so a kernel where most wavefronts count would serialise
+// on it; the reader sums the shards
+constexpr uint32_t NSHARD = 64;
+__device__ __forceinline__ void wave_count_add_sharded(uint32_t* shards, bool pred) {
+  wave_count_add(shards + (blockIdx.x & (NSHARD - 1)), pred);
+}
+// a 0 -> 1 flag any lane may raise: plain stores (they merge in L2; no memory-side atomic)
+__device__ __forceinline__ void wave_flag(uint32_t* flag, bool pred) {
+  if (__ballot(pred) && (threadIdx.x & 63u) == 0) *flag = 1u;
+}
+
 __device__ __forceinline__ void raise_err(uint32_t* err, uint32_t code) {
   atomicCAS(err, 0u, code);
 }

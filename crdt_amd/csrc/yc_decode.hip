@@ -1233,7 +1233,7 @@ __global__ __launch_bounds__(256) void k_struct_decode(Work w, uint32_t nstructs
   }
   if (pk != 0 && !v.has_psub) w.ctr->narray_roots = 1;  // a YArray list may exist (flag, plain store)
   if (pk == 2) w.ctr->nested = 1;                        // a nested type's list (flag, plain store)
-  wave_count_add(&w.ctr->nroots, pk != 0);
+  wave_count_add_sharded(w.ctr->nroots_sh, pk != 0);
   w.s_pk[i] = (uint8_t)pk;
   if (pk != 0) {
     w.s_pa[i] = pa;

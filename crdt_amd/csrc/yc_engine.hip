@@ -607,7 +607,8 @@ int run_decode(ycrdt_engine* e, ycrdt_batch* b, bool lazy, Decoded& D, bool gene
   D.in_len = c.in_len;
   D.array_roots = c.narray_roots;
   D.nested = c.nested;
-  D.nroots = c.nroots;
+  D.nroots = 0;
+  for (uint32_t k = 0; k < NSHARD; ++k) D.nroots += c.nroots_sh[k];
   if (nunits >= 0xF0000000ull) return fail(YCRDT_E_CAPACITY, "more than 2^32 units in one batch");
   D.nstructs = nstructs;
   D.nsections = nsections;

@@ -331,7 +331,7 @@ __global__ void k_seg_kind(Work w, uint32_t nsegs) {
       w.g_flags[s] = f | (arr ? SEG_ARRAY : SEG_PSUB);
     }
   }
-  wave_count_add(&w.ctr->narray, arr);
+  wave_flag(&w.ctr->narray, arr);  // read as zero / non-zero (launch_yata)
 }
 
 // One pass instead of host-driven pointer-jumping rounds: every unresolved item climbs its origin

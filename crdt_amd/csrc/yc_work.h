@@ -34,6 +34,7 @@ struct Counters {            // device-side counters, read back at the few host 
   uint32_t tbig;             // groups too large for one lane
   uint32_t ds_region;        // Σ per-update delete-set regions (sizes the range arrays)
   uint32_t nested;           // 1: a decoded item names a parent ITEM (nested types exist)
+  uint32_t nroots_sh[NSHARD]; // items with an explicit parent, sharded by workgroup (summed on the host)
   uint32_t nroots;           // items with an explicit parent (bound on the distinct lists: key table size)
   uint32_t pad[12];          // encode scratch (see yc_encode.hip)
   unsigned long long items;  // Σ clock lengths of Skip structs (items = Σ all lengths − this)
