@@ -496,14 +496,19 @@ __device__ __forceinline__ uint32_t block_excl_scan256(uint32_t v, uint32_t* sh,
   return off + x - v;
 }
 
+// CAP: LDS capacity in members, HS: anchor hash slots. MID = the variant for groups of at most
+// CAP members (a small LDS footprint, several workgroups per CU); the other takes the rest.
+constexpr uint32_t TMID = 1024;
+template <uint32_t CAP, uint32_t HS, bool MID>
 __global__ __launch_bounds__(256) void k_tsib_big(Work w, uint32_t nsegs) {
   const uint32_t g = w.t_big[blockIdx.x];
   const uint32_t a = w.t_gstart[g], n = w.t_gstart[g + 1] - a;
-  __shared__ SibRec rec[TLDS];
-  __shared__ uint8_t st[TLDS];
-  __shared__ uint32_t hkey[THASH], hval[THASH];
+  if (MID ? n > CAP : n <= TMID) return;
+  __shared__ SibRec rec[CAP];
+  __shared__ uint8_t st[CAP];
+  __shared__ uint32_t hkey[HS], hval[HS];
   __shared__ uint32_t head_s, scan_sh[4];
-  for (uint32_t i = threadIdx.x; i < THASH; i += blockDim.x) { hkey[i] = NONE; hval[i] = NONE; }
+  for (uint32_t i = threadIdx.x; i < HS; i += blockDim.x) { hkey[i] = NONE; hval[i] = NONE; }
   __syncthreads();
   // anchors: the first member (lowest position) of every outside right-origin unit
   // (loops over the members take 4 coalesced elements per lane per round: their loads are
@@ -518,12 +523,12 @@ __global__ __launch_bounds__(256) void k_tsib_big(Work w, uint32_t nsegs) {
       const uint32_t i = i0 + u * blockDim.x;
       if (i >= n || rc[u] != NONE) continue;
       const uint32_t r0 = w.y_before[a + i], r = r0 == NONE ? HNONE : r0;
-      uint32_t slot = (r * 2654435761u) & (THASH - 1);
+      uint32_t slot = (r * 2654435761u) & (HS - 1);
       for (uint32_t probe = 0;; ++probe) {
-        if (probe == THASH) { raise_err(&w.ctr->err, ERR_CAPACITY); break; }
+        if (probe == HS) { raise_err(&w.ctr->err, ERR_CAPACITY); break; }
         const uint32_t old = atomicCAS(&hkey[slot], NONE, r);
         if (old == NONE || old == r) { atomicMin(&hval[slot], i); break; }
-        slot = (slot + 1) & (THASH - 1);
+        slot = (slot + 1) & (HS - 1);
       }
     }
   }
@@ -538,16 +543,16 @@ __global__ __launch_bounds__(256) void k_tsib_big(Work w, uint32_t nsegs) {
       if (i >= n) continue;
       if (t[u] == NONE) {
         const uint32_t r0 = w.y_before[a + i], r = r0 == NONE ? HNONE : r0;
-        uint32_t slot = (r * 2654435761u) & (THASH - 1);
-        for (uint32_t probe = 0; probe < THASH && hkey[slot] != r; ++probe) slot = (slot + 1) & (THASH - 1);
+        uint32_t slot = (r * 2654435761u) & (HS - 1);
+        for (uint32_t probe = 0; probe < HS && hkey[slot] != r; ++probe) slot = (slot + 1) & (HS - 1);
         t[u] = (hkey[slot] == r ? a + hval[slot] : a + i) | 0x80000000u;
       }
       w.t_trep[a + i] = t[u];
     }
   }
   __syncthreads();
-  uint32_t nn = NONE;  // member count after collapsing chains (n > TLDS only)
-  if (n > TLDS) {
+  uint32_t nn = NONE;  // member count after collapsing chains (n > CAP only)
+  if (n > CAP) {
     // t_mtail / t_prv / t_next hold NONE here (k_tprep) and serve as scratch:
     //   t_mtail[p] = 0   p is named as right origin by a member other than its chain successor
     //   t_prv[i]         the chain (node) of position i;  t_next[k]  first position of node k
@@ -597,7 +602,7 @@ __global__ __launch_bounds__(256) void k_tsib_big(Work w, uint32_t nsegs) {
     }
     nn = carry;
     __syncthreads();
-    if (nn > TLDS) {  // no room in LDS even collapsed: restore the scratch, run in place
+    if (nn > CAP) {  // no room in LDS even collapsed: restore the scratch, run in place
       for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) {
         w.t_mtail[a + i] = NONE;
         w.t_prv[a + i] = NONE;
@@ -606,7 +611,7 @@ __global__ __launch_bounds__(256) void k_tsib_big(Work w, uint32_t nsegs) {
       __syncthreads();
     }
   }
-  if (nn != NONE && nn <= TLDS) {
+  if (nn != NONE && nn <= CAP) {
     const uint32_t* node = w.t_prv + a;
     const uint32_t* nfirst = w.t_next + a;
     for (uint32_t k = threadIdx.x; k < nn; k += blockDim.x) {
@@ -654,7 +659,7 @@ __global__ __launch_bounds__(256) void k_tsib_big(Work w, uint32_t nsegs) {
     if (threadIdx.x == 0 && head_s != NONE) sib_publish(w, a, n, nsegs, leftmost(head_s));
     return;
   }
-  if (n <= TLDS) {
+  if (n <= CAP) {
     for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) {
       const uint32_t rp = w.y_confl[a + i];
       const uint32_t t = w.t_trep[a + i];
@@ -719,7 +724,10 @@ uint32_t launch_yata_tree(const Work& w, uint32_t nsegs, hipStream_t s) {
   uint32_t nbig = 0;
   hipMemcpyAsync(&nbig, &w.ctr->tbig, sizeof(uint32_t), hipMemcpyDeviceToHost, s);
   hipStreamSynchronize(s);
-  if (nbig) hipLaunchKernelGGL(k_tsib_big, dim3(nbig), dim3(256), 0, s, w, nsegs);
+  if (nbig) {
+    hipLaunchKernelGGL((k_tsib_big<TMID, 2048, true>), dim3(nbig), dim3(256), 0, s, w, nsegs);
+    hipLaunchKernelGGL((k_tsib_big<TLDS, THASH, false>), dim3(nbig), dim3(256), 0, s, w, nsegs);
+  }
   hipLaunchKernelGGL(k_tclimb, dim3(grid), dim3(256), 0, s, w, nsegs);
   return nbig;
 }
