@@ -767,7 +767,7 @@ __global__ __launch_bounds__(64) void k_walk(Work w) {
       // A failure where the true exit jumps past the next chunk (a long struct) is no sign of it.
       ++steps;
       const uint32_t Xf = __shfl(X, f), cef = __shfl(ce, f);
-      if (!TABLES && !ends && f < 63 && j0 + f + 1 < nch && Xf < cef + CH && ++fails >= 6 && fails * 4 > steps * 3) {
+      if (!TABLES && !ends && f < 63 && j0 + f + 1 < nch && Xf < cef + CH && ++fails >= 4 && fails * 4 > steps * 3) {
         hand_over();
         return;
       }
