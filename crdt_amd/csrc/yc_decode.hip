@@ -1181,21 +1181,20 @@ __global__ __launch_bounds__(256) void k_struct_decode(Work w, uint32_t nstructs
   if (i >= nstructs) return;
   const uint32_t nclients = w.ctr->nclients;
   uint32_t* err = &w.ctr->err;
-  const uint32_t p0 = w.s_pos[i];
-  const Section sec = w.sections[w.s_sec[i]];
-  const uint32_t uend = w.uoff[sec.upd] + w.ulen[sec.upd];
-  const uint32_t doc = doc_of_update(w, sec.upd);
+  const uint32_t p0 = w.s_pos[i], si = w.s_sec[i];
+  // the struct's bytes (they depend on its position only) are fetched beside its section record
   __shared__ __attribute__((aligned(16))) uint32_t win[256 * SD_STRIDE];
   uint32_t* slot = win + threadIdx.x * SD_STRIDE;
   const uint32_t s0 = p0 & ~15u;
-  {
-    const uint4* g = (const uint4*)(w.bytes + s0);  // the batch buffer is padded past its end
-    uint4 v4[SD_WIN / 16];
+  const uint4* g = (const uint4*)(w.bytes + s0);  // the batch buffer is padded past its end
+  uint4 v4[SD_WIN / 16];
 #pragma unroll
-    for (uint32_t k = 0; k < SD_WIN / 16; ++k) v4[k] = g[k];
+  for (uint32_t k = 0; k < SD_WIN / 16; ++k) v4[k] = g[k];
+  const Section sec = w.sections[si];
 #pragma unroll
-    for (uint32_t k = 0; k < SD_WIN / 16; ++k) ((uint4*)slot)[k] = v4[k];
-  }
+  for (uint32_t k = 0; k < SD_WIN / 16; ++k) ((uint4*)slot)[k] = v4[k];
+  const uint32_t uend = w.uoff[sec.upd] + w.ulen[sec.upd];
+  const uint32_t doc = doc_of_update(w, sec.upd);
   StructView v;
   uint32_t p = p0;
   if (parse_struct<true, 32, WinSrc>(WinSrc{w.bytes, slot, s0}, p, uend, 0xFFFFFFFFu, &v) <= 0) { raise_err(err, ERR_DECODE); return; }

@@ -67,14 +67,22 @@ __device__ uint32_t encode_struct(const Work& w, uint32_t nclients, uint32_t o, 
     if (hint < nclients && g >= w.cl_base[hint] && g < w.cl_base[hint + 1]) return hint;
     return unit_client(w, nclients, g);
   };
+  // the origin's likely client (the source struct's recorded one): its base, end and id together
+  const bool sh = soc < nclients;
+  const uint64_t hb0 = sh ? w.cl_base[soc] : 0ull, hb1 = sh ? w.cl_base[soc + 1] : 0ull;
+  const uint32_t hval = sh ? w.cl_vals[soc] : 0u;
   uint32_t oclient = 0, oclock = 0;
   bool has_o = false;
   if (off > 0) { has_o = true; oclient = cval; oclock = k0 + off - 1; }
   else if (go != NONE) {
-    const uint32_t c = client_of(go, soc);
     has_o = true;
-    oclient = c == cidx ? cval : w.cl_vals[c];
-    oclock = (uint32_t)(go - (c == cidx ? base : w.cl_base[c]));
+    if (go >= base && go < base1) { oclient = cval; oclock = (uint32_t)(go - base); }
+    else if (sh && go >= hb0 && go < hb1) { oclient = hval; oclock = (uint32_t)(go - hb0); }
+    else {
+      const uint32_t c = unit_client(w, nclients, go);
+      oclient = w.cl_vals[c];
+      oclock = (uint32_t)(go - w.cl_base[c]);
+    }
   }
   bool has_r = false;
   uint32_t rclient = 0, rclock = 0;
