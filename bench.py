@@ -633,6 +633,11 @@ def main():
                 if r["kernel"] == "yc::k_children":
                     traffic = int(float(r["hbm_bytes"]))
                     traffic_src = os.path.basename(pmc[-1])
+    # the whole merge's counter traffic from the same PMC pass (sum over its kernels, per merge)
+    pipe_traffic = None
+    if pmc:
+        with open(pmc[-1]) as f:
+            pipe_traffic = int(sum(float(r["hbm_bytes"]) for r in csv.DictReader(f)))
     achieved = alg / (k_ms * 1e-3) / 1e9 if k_ms > 0 else 0.0
     dominant = max(phases, key=lambda p: p[1]) if phases else ("merge", st.device_ms)
     roofline = {
@@ -731,6 +736,12 @@ def main():
             "b_alg_bytes": b_alg,
             "achieved_GBs": round(b_alg / (ms_per_step * 1e-3) / 1e9, 2),
             "frac": round(b_alg / (ms_per_step * 1e-3) / 1e9 / HBM_PEAK_GBS, 5),
+            # HBM / fabric bytes the merge actually moves (PMC, every kernel of one merge) over this
+            # step time: how busy the memory system is, against the algorithmic bytes above
+            "traffic_bytes": pipe_traffic,
+            "traffic_GBs": round(pipe_traffic / (ms_per_step * 1e-3) / 1e9, 2) if pipe_traffic else None,
+            "traffic_frac": round(pipe_traffic / (ms_per_step * 1e-3) / 1e9 / HBM_PEAK_GBS, 4) if pipe_traffic else None,
+            "traffic_source": traffic_src,
         },
         "roofline": roofline,
         "cpu_baseline": cpu,
