@@ -39,6 +39,9 @@ out2 = b2.result()[0]
 del b2
 b3 = crdt_amd.Batch([out], eng)
 b3.merge()
+t3 = time.time()
+b3.merge()
+print(f"the merged state as one update: {1e3 * (time.time() - t3):.1f} ms", flush=True)
 out3 = b3.result()[0]
 del b3
 print(f"output {len(out) / 1e6:.1f} MB; order independent {out == out2}; idempotent {out == out3}", flush=True)
