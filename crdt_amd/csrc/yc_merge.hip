@@ -88,7 +88,11 @@ __global__ void k_ds_prep(Work w, uint32_t nds, uint32_t nclients) {
   w.ds[i] = r;
   w.ds_len[i] = len;
 }
-// only UF_DS is written in this kernel: concurrent plain ORs of the same bit are harmless
+// UF_DS and UF_CUT own a byte of the unit's flag word each, so their writers store that byte
+// (no read-modify-write round trip); concurrent stores of the same byte write the same value
+__device__ __forceinline__ void set_flag_byte(uint32_t* u_flags, uint32_t g, uint32_t byte) {
+  reinterpret_cast<uint8_t*>(u_flags)[(size_t)g * 4 + byte] = 1;
+}
 __global__ __launch_bounds__(256) void k_ds_mark(Work w, uint32_t nds) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t lane = threadIdx.x & 63;
@@ -100,12 +104,12 @@ __global__ __launch_bounds__(256) void k_ds_mark(Work w, uint32_t nds) {
   }
   const bool lng = n > LONG_UNITS;
   if (!lng)
-    for (uint32_t k = 0; k < n; ++k) w.u_flags[(uint32_t)(gb + k)] |= UF_DS;
+    for (uint32_t k = 0; k < n; ++k) set_flag_byte(w.u_flags, (uint32_t)(gb + k), 1);
   for (uint64_t m = __ballot(lng); m; m &= m - 1) {
     const int L = __ffsll((long long)m) - 1;
     const uint64_t g0 = shfl64(gb, L);
     const uint32_t nl = __shfl(n, L);
-    for (uint32_t k = lane; k < nl; k += 64) w.u_flags[(uint32_t)(g0 + k)] |= UF_DS;
+    for (uint32_t k = lane; k < nl; k += 64) set_flag_byte(w.u_flags, (uint32_t)(g0 + k), 1);
   }
 }
 
@@ -126,14 +130,12 @@ __global__ void k_refs(Work w, uint32_t nstructs) {
   if (oc != NONE) {
     if (oc == UNKNOWN || ok_ >= ost) { raise_err(&w.ctr->err, ERR_PENDING); return; }
     const uint32_t g = (uint32_t)(ob + ok_);
-    // getItemCleanEnd(origin); only UF_CUT is written to u_flags in this kernel, so a plain
-    // read-modify-write that races with another writer of the same bit is harmless
-    if (ok_ + 1 < ost && !(w.u_flags[g + 1] & UF_CUT)) w.u_flags[g + 1] |= UF_CUT;
+    if (ok_ + 1 < ost) set_flag_byte(w.u_flags, g + 1, 2);  // getItemCleanEnd(origin)
   }
   if (rc != NONE) {
     if (rc == UNKNOWN || rk >= rst) { raise_err(&w.ctr->err, ERR_PENDING); return; }
     const uint32_t g = (uint32_t)(rb + rk);
-    if (!(w.u_flags[g] & UF_CUT)) w.u_flags[g] |= UF_CUT;              // getItemCleanStart(rightOrigin)
+    set_flag_byte(w.u_flags, g, 2);                          // getItemCleanStart(rightOrigin)
   }
 }
 __global__ __launch_bounds__(256) void k_cuts(Work w, uint64_t nunits) {

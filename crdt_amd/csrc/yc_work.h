@@ -396,8 +396,8 @@ enum : uint32_t {
 enum : uint32_t {
   UF_DEL = 1u,         // source content is ContentDeleted
   UF_GC = 2u,          // a GC struct covers the unit
-  UF_DS = 4u,          // a delete-set range covers the unit
-  UF_CUT = 8u,         // a struct boundary is required before this unit
+  UF_DS = 0x100u,      // a delete-set range covers the unit (byte 1: set by a plain byte store)
+  UF_CUT = 0x10000u,   // a struct boundary is required before this unit (byte 2: plain byte store)
 };
 
 // ---- materialised view (yc_view.hip), copied to the host as is
