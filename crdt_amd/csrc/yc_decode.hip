@@ -1063,7 +1063,11 @@ __global__ __launch_bounds__(256) void k_ds_decode(Work w) {
 __global__ void k_ds_bound(Work w) {  // region size per update: (delete-set bytes + 1) / 2
   const uint32_t u = blockIdx.x * blockDim.x + threadIdx.x;
   if (u > w.nupd) return;
-  if (u == w.nupd) { w.scratch[u] = 0; w.ds_count[u] = 0; return; }
+  if (u == w.nupd) {
+    w.scratch[u] = 0; w.ds_count[u] = 0;
+    w.ctr->nstructs = w.wcnt[(w.nbytes + 63) / 64];  // launch_struct_count's total (no copy launch)
+    return;
+  }
   const uint32_t st = w.dsstart[u];
   w.scratch[u] = st == NONE ? 0 : (w.uoff[u] + w.ulen[u] - st + 1) / 2;
   w.ds_count[u] = 0;
@@ -1292,8 +1296,8 @@ __global__ void k_state_totals(Work w, uint32_t nstructs) {  // U and Σ input l
   w.ctr->in_len = w.s_lenscan[nstructs];
 }
 // NC <= nsections: the states are zero past NC, so a scan over nsections + 1 entries gives cl_base
+// cl_state must be zero on entry (the caller's fill)
 void launch_states(const Work& w, uint32_t nstructs, uint32_t nsections, hipStream_t s) {
-  hipMemsetAsync(w.cl_state, 0, sizeof(uint32_t) * (nsections + 1), s);
   if (nstructs) hipLaunchKernelGGL(k_states, dim3((nstructs + 255) / 256), dim3(256), 0, s, w, nstructs);
   if (w.capped && nsections) hipLaunchKernelGGL(k_apply_caps, dim3(nsections / 256 + 1), dim3(256), 0, s, w);
   scan_u32_to_u64(w.tmp, w.tmp_bytes, w.cl_state, w.cl_base, nsections + 1, s);

@@ -200,6 +200,7 @@ struct ycrdt_doc {
   std::vector<uint8_t> sv;
   ycrdt_merge_stats last{};
   HostView view;         // materialised view of `state` (crdt.c), rebuilt lazily after a change
+  bool wants_view = false;  // a view was read once: build it beside every merge (crdt.js reads after each op)
   // Y.applyUpdate is deferred: validated updates wait here and are merged in one
   // batch by the next read (encode*, toJSON, get, local op). n sequential applies cost one merge.
   struct Queued { std::vector<uint8_t> bytes; bool local; };
@@ -527,7 +528,7 @@ int run_decode(ycrdt_engine* e, ycrdt_batch* b, bool lazy, Decoded& D, bool gene
   mark(e, "decode.bitmap");
   launch_struct_count(w, s);
   launch_ds_bound(w, s);
-  HIPCHK(hipMemcpyAsync(&w.ctr->nstructs, w.wcnt + (w.nbytes + 63) / 64, sizeof(uint32_t), hipMemcpyDeviceToDevice, s));
+  if (!w.nupd) HIPCHK(hipMemcpyAsync(&w.ctr->nstructs, w.wcnt + (w.nbytes + 63) / 64, sizeof(uint32_t), hipMemcpyDeviceToDevice, s));
   Counters c;
   int rc = check(e, c, "decode");
   if (rc == YCRDT_E_CAPACITY && !generous) return run_decode(e, b, lazy, D, true);  // past the estimates
@@ -597,8 +598,12 @@ int run_decode(ycrdt_engine* e, ycrdt_batch* b, bool lazy, Decoded& D, bool gene
   }
   mark(e, "decode.structs");
   launch_struct_decode(w, nstructs, s);
-  HIPCHK(hipMemsetAsync(w.cl_start, 0, sizeof(uint32_t) * (nsections + 1), s));
-  if (!lazy) launch_states(w, nstructs, nsections, s);
+  if (!lazy) {
+    fill_u32_multi({{w.cl_start, (uint64_t)nsections + 1, 0u}, {w.cl_state, (uint64_t)nsections + 1, 0u}}, s);
+    launch_states(w, nstructs, nsections, s);
+  } else {
+    HIPCHK(hipMemsetAsync(w.cl_start, 0, sizeof(uint32_t) * (nsections + 1), s));
+  }
   HIPCHK(hipStreamWaitEvent(s, e->side_done, 0));
   rc = check(e, c, "struct decode");
   if (rc) return rc;
@@ -1337,6 +1342,9 @@ int commit_merge(ycrdt_doc* d, const std::vector<ycrdt_buf>& extra, const ClockM
   d->last = e->last;
   d->view.valid = false;
   e->ws_owner = d;  // the workspace now holds this doc's merged store (ensure_view reuses it)
+  // a doc that is read through its view (local ops, toJSON, get) takes the view now, while the
+  // workspace holds its merge: another doc's merge in between would otherwise force a re-merge
+  if (d->wants_view) return run_view(e, &b, d->view);
   return YCRDT_OK;
 }
 
@@ -1888,6 +1896,7 @@ void ycrdt_batch_destroy(ycrdt_batch* b) {
 // ---- crdt.c materialisation + local ops (yc_view.hip, yc_host.cpp)
 
 static int ensure_view(ycrdt_doc* d) {
+  d->wants_view = true;
   int rc = flush(d);
   if (rc) return rc;
   if (d->view.valid) return YCRDT_OK;

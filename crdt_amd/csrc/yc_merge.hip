@@ -171,6 +171,7 @@ __global__ void k_client_cuts(Work w, uint32_t nclients) {
 }
 __global__ void k_scatter_seg(Work w, uint32_t nwords, uint64_t nunits) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i == 0) w.ctr->nsegs = w.u_wpre[nwords];  // the scan's total (no copy launch)
   if (i >= nwords) return;
   uint64_t x = w.u_cutbits[i];
   uint32_t k = w.u_wpre[i];
@@ -205,7 +206,6 @@ void launch_segments(const Work& w, uint32_t nclients, uint64_t nunits, hipStrea
   hipLaunchKernelGGL(k_popc_words, dim3(nwords / 256 + 1), dim3(256), 0, s, (const uint64_t*)w.u_cutbits, w.scratch, nwords);
   scan_u32(w.tmp, w.tmp_bytes, w.scratch, w.u_wpre, nwords + 1, s);
   hipLaunchKernelGGL(k_scatter_seg, dim3(nwords / 256 + 1), dim3(256), 0, s, w, nwords, nunits);
-  hipMemcpyAsync(&w.ctr->nsegs, w.u_wpre + nwords, sizeof(uint32_t), hipMemcpyDeviceToDevice, s);
 }
 
 // --------------------------------------------------------------------------- segment properties
@@ -512,7 +512,11 @@ __global__ void k_out_first(Work w, uint32_t nsegs) {
   const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
   if (s >= nsegs) return;
   if (!(w.g_flags[s] & SEG_MERGE)) w.o_first[w.g_outid[s]] = s;
-  if (s == nsegs - 1) w.o_first[w.g_outid[nsegs]] = nsegs;  // sentinel
+  if (s == nsegs - 1) {
+    const uint32_t nout = w.g_outid[nsegs];
+    w.o_first[nout] = nsegs;  // sentinel
+    w.ctr->nout = nout;
+  }
 }
 
 // ---- key-hash sharding of one document (C4). Every list — a YMap entry, a
@@ -597,7 +601,6 @@ void launch_merge_tail(const Work& w, uint32_t nsegs, hipStream_t s) {
   if (!nsegs) return;
   scan_u32(w.tmp, w.tmp_bytes, w.g_tmp, w.g_outid, nsegs + 1, s);
   hipLaunchKernelGGL(k_out_first, dim3((nsegs + 255) / 256), dim3(256), 0, s, w, nsegs);
-  hipMemcpyAsync(&w.ctr->nout, w.g_outid + nsegs, sizeof(uint32_t), hipMemcpyDeviceToDevice, s);
 }
 
 void launch_merge_flags(const Work& w, uint32_t nsegs, hipStream_t s, bool fold) {
@@ -605,7 +608,6 @@ void launch_merge_flags(const Work& w, uint32_t nsegs, hipStream_t s, bool fold)
   hipLaunchKernelGGL(k_merge_flags, dim3(nsegs / 256 + 1), dim3(256), 0, s, w, nsegs, fold ? 1u : 0u);
   scan_u32(w.tmp, w.tmp_bytes, w.g_tmp, w.g_outid, nsegs + 1, s);
   hipLaunchKernelGGL(k_out_first, dim3((nsegs + 255) / 256), dim3(256), 0, s, w, nsegs);
-  hipMemcpyAsync(&w.ctr->nout, w.g_outid + nsegs, sizeof(uint32_t), hipMemcpyDeviceToDevice, s);
 }
 
 }  // namespace yc
