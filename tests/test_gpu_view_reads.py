@@ -75,3 +75,37 @@ def test_reads_after_local_ops():
     assert d.array_length("docs", parent_key="list") == 10
     assert [json.loads(d.array_get("docs", i, parent_key="list")[1]) for i in range(10)] == list(range(10))
     _check_doc(d, {"users": "map"}, "local")
+
+
+def test_two_docs_one_engine_per_op_loop():
+    """crdt.js's per-op loop (bench.py per_op_leg) with both peers writing, on ONE engine: every
+    merge of one doc takes the engine workspace from the other, and a doc read through its view
+    gets the view built beside its merge (yc_engine.hip commit_merge). Both peers' toJSON, per-key
+    reads and encoded states match the oracle's two docs fed the same calls."""
+    from oracle.yref import Doc as ODoc
+    from tests.v1util import canonical_update
+
+    eng = crdt_amd.default_engine()
+    g = [crdt_amd.Doc(client_id=1, engine=eng), crdt_amd.Doc(client_id=2, engine=eng)]
+    o = [ODoc(client_id=1), ODoc(client_id=2)]
+    for i in range(60):
+        w, r = i % 2, 1 - i % 2  # the writer alternates
+        key = "user%d" % (i % 9)
+        if i % 5 == 4:
+            g[w].map_delete("users", key)
+            o[w].map_delete("users", key)
+        else:
+            v = _any_str("v%d" % i)
+            g[w].map_set("users", key, v)
+            o[w].map_set("users", key, v)
+        u = g[w].encode_state_as_update()
+        assert canonical_update(u) == canonical_update(o[w].encode_state_as_update()), i
+        g[r].apply_update(u)
+        o[r].apply_update(u)
+        for d, od in zip(g, o):
+            assert json.loads(d.root_json("users", "map")) == json.loads(od.root_json("users", "map")), i
+        st, j = g[r].map_get("users", key)
+        want = json.loads(o[r].root_json("users", "map")).get(key)
+        assert (json.loads(j) if st == 1 else None) == want, i
+    _check_doc(g[0], {"users": "map"}, "peer0")
+    _check_doc(g[1], {"users": "map"}, "peer1")
