@@ -1201,7 +1201,7 @@ int split_docs(ycrdt_engine* e, uint32_t ndocs, ycrdt_out* outs, ycrdt_out* svs)
     put(o, rd[d].n);
     if (rd[d].n) o.insert(o.end(), all.begin() + dsbase + rd[d].lo, all.begin() + dsbase + rd[d].hi);
     outs[d].ptr = (uint8_t*)malloc(o.size());
-    if (!outs[d].ptr) return fail(YCRDT_E_CAPACITY, "host allocation failed");
+    if (!outs[d].ptr) return fail(YCRDT_E_CAPACITY, "host allocation failed");  // the caller frees the rest
     outs[d].len = o.size();
     memcpy(outs[d].ptr, o.data(), o.size());
     if (svs) {
@@ -1219,6 +1219,7 @@ int split_docs(ycrdt_engine* e, uint32_t ndocs, ycrdt_out* outs, ycrdt_out* svs)
 
 int empty_update(ycrdt_out* out) {
   out->ptr = (uint8_t*)malloc(2);
+  if (!out->ptr) { out->len = 0; return fail(YCRDT_E_CAPACITY, "host allocation failed"); }
   out->ptr[0] = 0;
   out->ptr[1] = 0;
   out->len = 2;
