@@ -57,13 +57,50 @@ size_t prim_tmp_bytes(uint64_t n) {
   return (m > f ? m : f) + 256;
 }
 
+// A small exclusive scan in one workgroup and one launch (rocPRIM's look-back scan is two: state
+// init + scan). Small merges (the per-op path: a doc state and an update) are launch-bound, and a
+// merge runs a dozen scans. Each lane sums a contiguous run, the 1 024 run sums are scanned in LDS,
+// each lane writes its run's prefixes; a lane reads in[i] before it writes out[i] and runs are
+// disjoint, so in == out is safe. Same results as rocprim::exclusive_scan (wrapping plus).
+constexpr uint32_t SMALL_SCAN_LANES = 1024, SMALL_SCAN_MAX = SMALL_SCAN_LANES * 16;
+template <class T>
+__global__ __launch_bounds__(SMALL_SCAN_LANES) void k_scan_small(const uint32_t* in, T* out, uint32_t n) {
+  __shared__ T part[SMALL_SCAN_LANES];
+  const uint32_t t = threadIdx.x, per = (n + SMALL_SCAN_LANES - 1) / SMALL_SCAN_LANES;
+  const uint32_t a = min(n, t * per), b = min(n, a + per);
+  T sum = 0;
+  for (uint32_t i = a; i < b; ++i) sum += (T)in[i];
+  part[t] = sum;
+  __syncthreads();
+  for (uint32_t off = 1; off < SMALL_SCAN_LANES; off <<= 1) {
+    const T v = t >= off ? part[t - off] : (T)0;
+    __syncthreads();
+    part[t] += v;
+    __syncthreads();
+  }
+  T run = part[t] - sum;
+  for (uint32_t i = a; i < b; ++i) {
+    const T x = (T)in[i];
+    out[i] = run;
+    run += x;
+  }
+}
+
 void scan_u32(void* tmp, size_t tmpb, const uint32_t* in, uint32_t* out, uint64_t n, hipStream_t s) {
   if (!n) return;
+  if (n <= SMALL_SCAN_MAX) {
+    hipLaunchKernelGGL(k_scan_small<uint32_t>, dim3(1), dim3(SMALL_SCAN_LANES), 0, s, in, out, (uint32_t)n);
+    return;
+  }
   rocprim::exclusive_scan(tmp, tmpb, in, out, 0u, (size_t)n, rocprim::plus<uint32_t>(), s);
 }
 
 void scan_u32_to_u64(void* tmp, size_t tmpb, const uint32_t* in, uint64_t* out, uint64_t n, hipStream_t s) {
   if (!n) return;
+  if (n <= SMALL_SCAN_MAX) {
+    hipLaunchKernelGGL(k_scan_small<uint64_t>, dim3(1), dim3(SMALL_SCAN_LANES), 0, s, in, out, (uint32_t)n);
+    return;
+  }
   rocprim::exclusive_scan(tmp, tmpb, in, out, (uint64_t)0, (size_t)n, rocprim::plus<uint64_t>(), s);
 }
 
