@@ -450,9 +450,14 @@ class Comm:
         _check(lib().ycrdt_comm_unique_id(buf))
         return buf.raw
 
+    ID_BYTES = 128  # YCRDT_COMM_ID_BYTES: ycrdt_comm_create copies exactly this many bytes
+
     def __init__(self, engine, nranks: int, rank: int, uid: bytes):
+        uid = bytes(uid)
+        if len(uid) != Comm.ID_BYTES:
+            raise ValueError(f"communicator id must be {Comm.ID_BYTES} bytes (got {len(uid)})")
         h = ctypes.c_void_p()
-        _check(lib().ycrdt_comm_create(engine._h, nranks, rank, bytes(uid), ctypes.byref(h)))
+        _check(lib().ycrdt_comm_create(engine._h, nranks, rank, uid, ctypes.byref(h)))
         self._h, self.engine, self.nranks, self.rank = h, engine, nranks, rank
 
     def close(self):

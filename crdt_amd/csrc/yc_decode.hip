@@ -1201,7 +1201,8 @@ __global__ __launch_bounds__(256) void k_struct_decode(Work w, uint32_t nstructs
   const uint32_t doc = doc_of_update(w, sec.upd);
   StructView v;
   uint32_t p = p0;
-  if (parse_struct<true, 32, WinSrc>(WinSrc{w.bytes, slot, s0}, p, uend, 0xFFFFFFFFu, &v) <= 0) { raise_err(err, ERR_DECODE); return; }
+  const int pr = parse_struct<true, 32, WinSrc>(WinSrc{w.bytes, slot, s0}, p, uend, 0xFFFFFFFFu, &v);
+  if (pr <= 0) { raise_err(err, pr == -1 ? ERR_UNSUPPORTED : ERR_DECODE); return; }  // -1: any nested > 32 deep
   w.s_len[i] = v.len;
   w.s_info[i] = v.info;
   w.s_cidx[i] = sec.cidx;

@@ -174,15 +174,13 @@ struct ycrdt_engine {
   uint32_t out_bytes = 0, sv_bytes = 0;
   uint32_t nsegs = 0, nlists = 0;  // segments / YArray lists of the last merge (the view reads them)
   ycrdt_merge_stats last{};
-  Arena arena;                      // doc states (grow_state)
+  Arena arena;                      // doc states (alloc_state / release_state)
 };
 
-// a doc state buffer of at least `bytes` (contents not kept)
-bool grow_state(ycrdt_engine* e, DevBuf& b, size_t bytes) {
-  if (bytes == 0) bytes = 16;
-  if (bytes <= b.cap) return true;
-  if (b.p) { if (b.arena) e->arena.release(b.p, b.cap); else hipFree(b.p); }
+// a fresh doc state block of at least `bytes` (arena block, or its own hipMalloc when large)
+bool alloc_state(ycrdt_engine* e, DevBuf& b, size_t bytes) {
   b = DevBuf();
+  if (bytes == 0) bytes = 16;
   if (bytes <= (size_t(1) << Arena::MAX_SHIFT)) {
     b.p = e->arena.alloc(bytes, b.cap);
     b.arena = b.p != nullptr;
@@ -191,7 +189,10 @@ bool grow_state(ycrdt_engine* e, DevBuf& b, size_t bytes) {
   }
   return grow(b, bytes);
 }
-
+void release_state(ycrdt_engine* e, DevBuf& b) {
+  if (b.p) { if (b.arena) e->arena.release(b.p, b.cap); else hipFree(b.p); }
+  b = DevBuf();
+}
 struct ycrdt_doc {
   ycrdt_engine* e = nullptr;
   uint32_t client_id = 0;
@@ -1334,12 +1335,22 @@ int commit_merge(ycrdt_doc* d, const std::vector<ycrdt_buf>& extra, const ClockM
   int rc = stage(&b, extra.data(), extra.size(), d->state_len ? &d->state : nullptr, d->state_len);
   if (rc == YCRDT_OK) rc = run_merge(e, &b, nullptr, caps, order);
   if (rc) return rc;
-  if (!grow_state(e, d->state, e->out_bytes + 16)) return fail(YCRDT_E_DEVICE, "hipMalloc failed (doc state)");
-  HIPCHK(hipMemcpyAsync(d->state.p, e->w.out, e->out_bytes, hipMemcpyDeviceToDevice, e->stream));
+  // the merged state goes to a block of its own (or the doc's, when it fits and is not the
+  // source of this merge any more: the batch holds a copy); the doc changes only once it is there
+  DevBuf nb = d->state;
+  const bool fresh = e->out_bytes + 16 > d->state.cap;
+  if (fresh && !alloc_state(e, nb, e->out_bytes + 16)) return fail(YCRDT_E_DEVICE, "hipMalloc failed (doc state)");
+  std::vector<uint8_t> sv(e->sv_bytes);
+  hipError_t er = hipMemcpyAsync(nb.p, e->w.out, e->out_bytes, hipMemcpyDeviceToDevice, e->stream);
+  if (er == hipSuccess && !sv.empty()) er = hipMemcpyAsync(sv.data(), e->w.sv_out, e->sv_bytes, hipMemcpyDeviceToHost, e->stream);
+  if (er == hipSuccess) er = hipStreamSynchronize(e->stream);
+  if (er != hipSuccess) {
+    if (fresh) release_state(e, nb);
+    return fail(YCRDT_E_DEVICE, std::string("HIP error: ") + hipGetErrorString(er) + " (doc state copy)");
+  }
+  if (fresh) { release_state(e, d->state); d->state = nb; }
   d->state_len = e->out_bytes;
-  d->sv.resize(e->sv_bytes);
-  HIPCHK(hipMemcpyAsync(d->sv.data(), e->w.sv_out, e->sv_bytes, hipMemcpyDeviceToHost, e->stream));
-  HIPCHK(hipStreamSynchronize(e->stream));
+  d->sv.swap(sv);
   d->last = e->last;
   d->view.valid = false;
   e->ws_owner = d;  // the workspace now holds this doc's merged store (ensure_view reuses it)
@@ -1465,6 +1476,12 @@ int flush_multi(ycrdt_engine* e, const std::vector<ycrdt_doc*>& docs) {
   std::vector<Piece> pc;
   pc.reserve(4 * (size_t)nd);
   std::vector<size_t> len(nd);
+  // every document's new block and state vector are prepared first; the documents change only
+  // after the copy has succeeded (a failed allocation or copy leaves all of them as they were)
+  std::vector<DevBuf> nblk(nd);
+  std::vector<char> fresh(nd, 0);
+  std::vector<std::vector<uint8_t>> nsv(nd);
+  auto drop_fresh = [&]() { for (uint32_t j = 0; j < nd; ++j) if (fresh[j]) release_state(e, nblk[j]); };
   auto hdr = [](Piece& P, uint32_t v) {
     P.src = nullptr;
     P.len = 0;
@@ -1476,25 +1493,36 @@ int flush_multi(ycrdt_engine* e, const std::vector<ycrdt_doc*>& docs) {
     const uint32_t ns = x[2] ? x[1] - x[0] : 0, ndb = x[5] ? x[4] - x[3] : 0;
     len[j] = vu_size_host(x[2]) + ns + vu_size_host(x[5]) + ndb;
     ycrdt_doc* d = fast[j];
-    if (!grow_state(e, d->state, len[j] + 16)) return fail(YCRDT_E_DEVICE, "hipMalloc failed (doc state)");
-    uint8_t* dst = (uint8_t*)d->state.p;
+    // the batch holds a copy of every document's old state, so a block that fits is rewritten
+    // in place (untouched until the copy below), a bigger one is allocated beside the old
+    nblk[j] = d->state;
+    if (len[j] + 16 > d->state.cap) {
+      if (!alloc_state(e, nblk[j], len[j] + 16)) { drop_fresh(); return fail(YCRDT_E_DEVICE, "hipMalloc failed (doc state)"); }
+      fresh[j] = 1;
+    }
+    uint8_t* dst = (uint8_t*)nblk[j].p;
     Piece P{};
     hdr(P, x[2]); P.dst = dst; dst += P.len; pc.push_back(P);
     if (ns) { pc.push_back(Piece{w.out + sbase + x[0], dst, ns, {0}}); dst += ns; }
     hdr(P, x[5]); P.dst = dst; dst += P.len; pc.push_back(P);
     if (ndb) pc.push_back(Piece{w.out + dsbase + x[3], dst, ndb, {0}});
     // state vector: its entries (host copy of the encode's state vector section)
-    std::vector<uint8_t> sv;
+    std::vector<uint8_t>& sv = nsv[j];
     put_vu(sv, x[8]);
     if (x[8]) sv.insert(sv.end(), svall.begin() + svbase + x[6], svall.begin() + svbase + x[7]);
-    d->sv.swap(sv);
   }
-  if (!grow(b.pieces, sizeof(Piece) * (pc.size() + 1))) return fail(YCRDT_E_DEVICE, "hipMalloc failed (pieces)");
-  HIPCHK(hipMemcpyAsync(b.pieces.p, pc.data(), sizeof(Piece) * pc.size(), hipMemcpyHostToDevice, s));
-  copy_pieces((const Piece*)b.pieces.p, (uint32_t)pc.size(), s);
-  HIPCHK(hipStreamSynchronize(s));
+  if (!grow(b.pieces, sizeof(Piece) * (pc.size() + 1))) { drop_fresh(); return fail(YCRDT_E_DEVICE, "hipMalloc failed (pieces)"); }
+  hipError_t er = hipMemcpyAsync(b.pieces.p, pc.data(), sizeof(Piece) * pc.size(), hipMemcpyHostToDevice, s);
+  if (er == hipSuccess) { copy_pieces((const Piece*)b.pieces.p, (uint32_t)pc.size(), s); er = hipStreamSynchronize(s); }
+  if (er != hipSuccess) {
+    // a block rewritten in place may be partly written: those documents cannot be trusted
+    drop_fresh();
+    return fail(YCRDT_E_DEVICE, std::string("HIP error: ") + hipGetErrorString(er) + " (document split)");
+  }
   for (uint32_t j = 0; j < nd; ++j) {
     ycrdt_doc* d = fast[j];
+    if (fresh[j]) { release_state(e, d->state); d->state = nblk[j]; }
+    d->sv.swap(nsv[j]);
     d->state_len = len[j];
     d->last = e->last;  // the whole pass
     d->view.valid = false;
@@ -1530,6 +1558,8 @@ int ycrdt_apply_updates(ycrdt_doc* d, const ycrdt_buf* ups, size_t n) {
     work(0);
   }
   for (size_t i = 0; i < n; ++i) {
+    if (!ok[i] && sc[i].unsupported)
+      return fail(YCRDT_E_UNSUPPORTED, "update " + std::to_string(i) + ": an any value nests deeper than 32 levels (engine limit)");
     if (!ok[i]) {
       // Yjs integrates a well-formed struct section and the delete-set ranges read before the error
       if (sc[i].structs_ok) {
@@ -1574,6 +1604,11 @@ int ycrdt_apply_updates_multi(ycrdt_engine* e, ycrdt_doc* const* docs, const ycr
   for (size_t i = 0; i < n; ++i) {
     ycrdt_doc* d = docs[i];
     touched.push_back(d);
+    if (!ok[i] && sc[i].unsupported) {  // the earlier updates are applied; this one is refused
+      rc = YCRDT_E_UNSUPPORTED;
+      err = "update " + std::to_string(i) + ": an any value nests deeper than 32 levels (engine limit)";
+      break;
+    }
     if (!ok[i]) {  // sequential semantics: what came before is applied, then Yjs throws
       if (sc[i].structs_ok) {
         const std::vector<uint8_t> r = repaired_update(ups[i].ptr, sc[i]);
@@ -2130,6 +2165,7 @@ int ycrdt_validate_update(ycrdt_buf update, int* structs_ok) {
   UpdScan sc;
   const bool ok = scan_update(update.ptr, update.len, false, sc);
   if (structs_ok) *structs_ok = sc.structs_ok ? 1 : 0;
+  if (!ok && sc.unsupported) return fail(YCRDT_E_UNSUPPORTED, "an any value nests deeper than 32 levels (engine limit)");
   return ok ? YCRDT_OK : fail(YCRDT_E_DECODE, "Integer out of range!");
 }
 

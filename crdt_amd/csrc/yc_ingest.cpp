@@ -28,7 +28,9 @@ bool scan_update(const uint8_t* b, size_t n, bool headers, UpdScan& o) {
     for (uint32_t k = 0; k < ns; ++k) {
       StructView v;
       const uint32_t pos = p;
-      if (parse_struct<true>(b, p, end, 0xFFFFFFFFu, &v) <= 0) return false;
+      const int r = parse_struct<true>(b, p, end, 0xFFFFFFFFu, &v);
+      if (r == -1) o.unsupported = true;  // skip_any's depth limit (exact budget: never the step count)
+      if (r <= 0) return false;
       if (ck + v.len > 0xFFFFFFFFull) return false;  // clocks are u32 (k_struct_clock refuses the same)
       if (headers) o.st.push_back(ScanStruct{client, (uint32_t)ck, pos, v});
       ck += v.len;

@@ -35,6 +35,8 @@ struct UpdScan {
   size_t struct_end = 0;     // byte offset of the delete set
   bool structs_ok = false;   // struct section decoded (else Yjs throws before changing anything)
   bool ds_ok = false;        // delete set decoded (else Yjs throws after integrating the structs)
+  bool unsupported = false;  // an `any` value nests deeper than the decoder's 32 levels: valid Yjs
+                             // input the engine refuses (YCRDT_E_UNSUPPORTED), never "malformed"
   uint64_t nstructs = 0;
 };
 // readClientsStructRefs (Y@19286) + readDeleteSet over one v1 update, with lib0 0.2.42's error

@@ -182,14 +182,21 @@ static napi_value js_apply_updates_multi(napi_env env, napi_callback_info info) 
   if (!e) return NULL;
   ycrdt_doc **docs = (ycrdt_doc **)calloc(n ? n : 1, sizeof(ycrdt_doc *));
   ycrdt_buf *bufs = (ycrdt_buf *)calloc(n ? n : 1, sizeof(ycrdt_buf));
+  if (!docs || !bufs) {
+    free(docs); free(bufs);
+    napi_throw_error(env, NULL, "applyUpdatesMulti: out of host memory");
+    return NULL;
+  }
   for (uint32_t i = 0; i < n; ++i) {
     napi_value d, u;
     napi_get_element(env, argv[0], i, &d);
     napi_get_element(env, argv[1], i, &u);
     docs[i] = get_doc(env, d);
-    if (!docs[i] || !get_bytes(env, u, &bufs[i])) {
+    /* get_doc has already thrown for a non-Doc; only a bad update still needs an error */
+    const int doc_ok = docs[i] != NULL;
+    if (!doc_ok || !get_bytes(env, u, &bufs[i])) {
       free(docs); free(bufs);
-      if (docs[i]) napi_throw_type_error(env, NULL, "updates must be Uint8Arrays");
+      if (doc_ok) napi_throw_type_error(env, NULL, "updates must be Uint8Arrays");
       return NULL;
     }
   }

@@ -161,6 +161,10 @@ if (mode === 'cpu') {
   }
   Y.applyUpdatesMulti(fdocs, fups);
   for (const [d, c] of fleet) assert.strictEqual(hex(Y.encodeStateAsUpdate(d)), c.state, 'applyUpdatesMulti ' + c.name);
+  // a non-Uint8Array update is a TypeError (the addon's error path frees its arrays only after reading them)
+  let bad = null;
+  try { Y.applyUpdatesMulti([fdocs[0], fdocs[1]], [fups[0], 'not bytes']); } catch (e) { bad = e; }
+  assert.ok(bad instanceof TypeError && /Uint8Array/.test(bad.message), 'applyUpdatesMulti type error: ' + bad);
   // the batched sync responder: every (doc state, peer state vector) pair in one call
   const batch = Y.diffUpdates(dsrc, dsv);
   assert.strictEqual(batch.length, dsrc.length);
