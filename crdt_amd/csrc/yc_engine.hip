@@ -298,6 +298,10 @@ void layout(ycrdt_batch* b, const std::vector<Src>& src, std::vector<uint32_t>& 
   b->schunk = SCHUNK;
   if (big_bytes <= SMALL_BATCH_BYTES)
     while (b->schunk > SCHUNK_SMALL && (size_t)(b->schunk / 2) * 64 >= big_max) b->schunk /= 2;
+  if (const char* cs = getenv("YCRDT_SCHUNK")) {  // experiments: a fixed chunk size (64-byte multiple)
+    const uint32_t v = (uint32_t)atoi(cs);
+    if (v >= 64 && v <= SCHUNK && v % 64 == 0) b->schunk = v;
+  }
   order.clear();
   for (size_t i = 0; i < src.size(); ++i) if (src[i].dev) order.push_back((uint32_t)i);
   for (size_t i = 0; i < src.size(); ++i) if (!src[i].dev) order.push_back((uint32_t)i);
@@ -791,7 +795,7 @@ int run_merge(ycrdt_engine* e, ycrdt_batch* b, const std::unordered_map<uint32_t
   if (nsegs) {
     mark(e, "merge.segment_props");
     launch_segment_props(w, nsegs, nclients, U, s);
-    mark(e, "merge.keys");
+    mark(e, "merge.resolve");  // k_resolve alone
     run_key_resolution(w, nsegs, s);
     uint32_t narray = 0;  // YArray members; only read when the decode saw a possible array root
     if (D.array_roots) {
@@ -817,14 +821,11 @@ int run_merge(ycrdt_engine* e, ycrdt_batch* b, const std::unordered_map<uint32_t
     }
     for (uint32_t shard = first; shard < last; ++shard) {
       if (sh) {
-        if (shard != first) {  // a logical shard after the first: the pristine flags, fresh winner slots
-          HIPCHK(hipMemcpyAsync(w.g_flags, gflags0, sizeof(uint32_t) * nsegs, hipMemcpyDeviceToDevice, s));
-          fill_u32_multi({{w.g_maxchild, (uint64_t)nsegs, 0u}, {w.k_rootmax, (uint64_t)w.cap_keys, 0u}}, s);
-        }
+        // a logical shard after the first: the pristine flags (the winner slots were settled for
+        // every list in k_resolve: a list's children never leave its shard)
+        if (shard != first) HIPCHK(hipMemcpyAsync(w.g_flags, gflags0, sizeof(uint32_t) * nsegs, hipMemcpyDeviceToDevice, s));
         launch_shard_mask(w, nsegs, owner, shard, s);
       }
-      mark(e, "merge.winner");  // k_children alone (bench.py's roofline kernel)
-      launch_map_winner(w, nsegs, s);
       mark(e, "merge.descent");
       run_descent(w, nsegs, s, !D.nested);  // no dead-type pass: merge flags apply the overwrite
       mark(e, "merge.dead_types");

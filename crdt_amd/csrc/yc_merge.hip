@@ -8,11 +8,12 @@
 //   k_refs         split points required by origin / rightOrigin references (getItemCleanEnd /
 //                  getItemCleanStart, Y@29100) + min child client per unit (list adjacency)
 //   k_cuts         struct boundaries -> bitmap; popcount scan -> segments
-//   k_seg_props    per-segment origin / rightOrigin / parent / flags
-//   k_keyfind      parent+parentSub resolution (Item.getMissing, Y@76507): climb the origin chain
-//                  with path halving
-//   k_children     YATA for map entries (Item.integrate, Y@77594): children ordered by client ⇒
-//                  the rightmost entry is the max-client descent from the max-client root
+//   k_seg_props    per-segment origin / rightOrigin / parent / flags; first pass of the YMap
+//                  winner reduction (plain stores of a child into its origin's slot)
+//   k_resolve      parent+parentSub resolution (Item.getMissing, Y@76507): climb the origin chain
+//                  with path halving; list kind; YATA for map entries (Item.integrate, Y@77594):
+//                  children ordered by client ⇒ the rightmost entry is the max-client descent from
+//                  the max-client root (settling pass of the max-child reduction)
 //   k_winner_walk  per key: descend along the max-client child to the rightmost entry
 //   k_overwrite    every non-rightmost entry of a key is deleted (typeMapSet / left.delete)
 //   k_merge_flags  Item.mergeWith (Y@79424) / tryToMergeWithLeft (Y@30960) as a pairwise
@@ -256,7 +257,9 @@ __global__ __launch_bounds__(256) void k_seg_props(Work w, uint32_t nsegs) {
       if (socx != NONE) origin = (uint32_t)(ob + socl);
     } else origin = g0 - 1;
     if (srcx != NONE) rorigin = (uint32_t)(rb + srcl);
-    if ((origin != NONE && (w.u_flags[origin] & UF_GC)) || (rorigin != NONE && (w.u_flags[rorigin] & UF_GC))) gc = true;
+    // an item whose origin is GC becomes GC in k_resolve (its first hop lands on the GC segment,
+    // Item.getMissing drops the parent); only a right origin needs the unit's flag here
+    if (rorigin != NONE && (w.u_flags[rorigin] & UF_GC)) gc = true;
   }
   uint32_t key = NONE, link = s;
   if (!gc && origin == NONE && rorigin == NONE) {
@@ -296,14 +299,29 @@ __global__ __launch_bounds__(256) void k_seg_props(Work w, uint32_t nsegs) {
   w.g_oseg[s] = (!gc && origin != NONE) ? link : NONE;  // link = the origin's segment here
   if (gc) sf |= SEG_GC | SEG_DEL;
   else sf |= SEG_ITEM;
-  if (!gc && expl && origin != NONE && w.s_ocidx[own] < NONE - 1 && cidx < w.s_ocidx[own]) sf |= SEG_OLOW;
+  const bool olow = !gc && expl && origin != NONE && socx < NONE - 1 && cidx < socx;
+  if (olow) sf |= SEG_OLOW;
+  // The YMap winner's max-client child / max-client root, first pass: a plain store of s + 1 into
+  // the origin's (the key's) slot — one of the children lands there; k_resolve then raises the
+  // slot with an atomicMax only where a child finds it below itself. Plain scattered stores merge
+  // in L2 where the one-atomic-per-segment form (98 M memory-side atomics on the C2 batch, 4.9 ms)
+  // was bound by the chip's atomic rate. Every item stores: its kind (YMap entry / YArray member)
+  // is only known after k_resolve, and a YArray origin's slot is never read. A lower-client child
+  // marks its origin unit (no merge with the origin's own-client successor; read for entries only).
+  if (!gc && origin != NONE) {
+    w.g_maxchild[link] = s + 1;
+    if (olow) w.u_minchild[origin] = 0u;
+  } else if (key != NONE) {
+    w.k_rootmax[key] = s + 1;
+  }
   w.g_cidx[s] = cidx;
   w.g_src[s] = own;
   w.g_flags[s] = sf;
   w.g_origin[s] = gc ? NONE : origin;
   w.g_rorigin[s] = gc ? NONE : rorigin;
-  // a root's key carries its list kind in bit 31 until k_seg_kind (k_keyfind copies it whole)
-  w.g_key[s] = key != NONE && w.s_psub[own] != NONE ? key | KEY_PSUB : key;
+  // a root's key carries its list kind in bit 31 (k_resolve copies it whole down the chains and
+  // writes the final keys, without the bit, to g_key); the chains are climbed over g_tmp
+  w.g_tmp[s] = key != NONE && w.s_psub[own] != NONE ? key | KEY_PSUB : key;
   w.g_link[s] = link;
 }
 
@@ -317,80 +335,73 @@ void launch_segment_props(const Work& w, uint32_t nsegs, uint32_t nclients, uint
 }
 
 // --------------------------------------------------------------------------- key resolution
-// every item now knows its list: tag it YMap-entry (parentSub) or YArray member
-// (the kind rides in bit 31 of the key the item copied from its root: no gather of the key flags)
-__global__ void k_seg_kind(Work w, uint32_t nsegs) {
+// One pass (Item.getMissing, Y@76507): every item that is not a list root climbs its origin chain
+// to the first segment that knows its list, halving the path it walks (link[x] <- link[link[x]] is
+// monotone: it only ever points further up the same chain, so concurrent halving is safe). The
+// climb reads the keys of k_seg_props (g_tmp, with the list kind in bit 31); a resolved item
+// publishes its key there for later climbers and writes its final key (bit cleared) to g_key, so
+// no climber ever reads a key whose kind bit is gone. The item is then tagged YMap entry
+// (parentSub) or YArray member, and a YMap entry settles its origin's max-client child slot (the
+// second pass of the winner reduction begun in k_seg_props: an atomicMax only where the slot is
+// below itself — segments are numbered in client order, so the max child is the max segment).
+__global__ __launch_bounds__(256) void k_resolve(Work w, uint32_t nsegs) {
   const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
   if (s >= nsegs) return;
-  const uint32_t f = w.g_flags[s];
+  uint32_t f = w.g_flags[s];
+  uint32_t kv = w.g_tmp[s];
   bool arr = false;
   if (f & SEG_ITEM) {
-    const uint32_t kv = w.g_key[s];
-    if (kv == NONE) raise_err(&w.ctr->err, ERR_DECODE);  // origin chain without a root
-    else {
-      arr = !(kv & KEY_PSUB);
-      w.g_key[s] = kv & ~KEY_PSUB;
-      w.g_flags[s] = f | (arr ? SEG_ARRAY : SEG_PSUB);
+    if (kv == NONE) {  // not a root: climb
+      uint32_t x = w.g_link[s];
+      bool done = false;
+      for (uint32_t it = 0; it < (1u << 26); ++it) {
+        const uint32_t fx = w.g_flags[x], k = w.g_tmp[x], y = w.g_link[x];  // one round of loads per hop
+        if (!(fx & SEG_ITEM)) {  // the origin chain ends in GC: getMissing drops the parent
+          f = (f & ~SEG_ITEM) | SEG_GC | SEG_DEL;
+          w.g_flags[s] = f;
+          w.g_origin[s] = NONE;
+          w.g_rorigin[s] = NONE;
+          done = true;
+          break;
+        }
+        if (k != NONE) { kv = k; w.g_tmp[s] = k; done = true; break; }
+        if (y == x) { done = true; break; }  // a chain without a root: reported below
+        const uint32_t z = w.g_link[y];
+        if (z != y) w.g_link[x] = z;
+        x = y;
+      }
+      if (!done) raise_err(&w.ctr->err, ERR_CAPACITY);  // a chain longer than any batch can hold
+    }
+    if (f & SEG_ITEM) {
+      if (kv == NONE) raise_err(&w.ctr->err, ERR_DECODE);  // origin chain without a root
+      else {
+        arr = !(kv & KEY_PSUB);
+        f |= arr ? SEG_ARRAY : SEG_PSUB;
+        w.g_flags[s] = f;
+        if (!arr) {  // the winner reduction's settling pass (k_seg_props stored one child)
+          const uint32_t os = w.g_oseg[s];
+          uint32_t* slot = os != NONE ? &w.g_maxchild[os] : (f & SEG_ROOT) ? &w.k_rootmax[kv & ~KEY_PSUB] : nullptr;
+          if (slot && *slot < s + 1) atomicMax(slot, s + 1);
+        }
+      }
     }
   }
+  w.g_key[s] = (f & SEG_ITEM) && kv != NONE ? kv & ~KEY_PSUB : NONE;
   wave_flag(&w.ctr->narray, arr);  // read as zero / non-zero (launch_yata)
-}
-
-// One pass instead of host-driven pointer-jumping rounds: every unresolved item climbs its origin
-// chain to the first segment that knows its list, halving the path it walks (link[x] ← link[link[x]]
-// is monotone: it only ever points further up the same chain, so concurrent halving is safe).
-__global__ __launch_bounds__(256) void k_keyfind(Work w, uint32_t nsegs) {
-  const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
-  if (s >= nsegs) return;
-  const uint32_t f = w.g_flags[s], k_s = w.g_key[s];
-  uint32_t x = w.g_link[s];
-  if (k_s != NONE || !(f & SEG_ITEM)) return;
-  for (uint32_t it = 0; it < (1u << 22); ++it) {
-    const uint32_t fx = w.g_flags[x], k = w.g_key[x], y = w.g_link[x];  // one round of loads per hop
-    if (!(fx & SEG_ITEM)) {  // the origin chain ends in GC: getMissing drops the parent
-      w.g_flags[s] = (f & ~SEG_ITEM) | SEG_GC | SEG_DEL;
-      w.g_origin[s] = NONE;
-      w.g_rorigin[s] = NONE;
-      return;
-    }
-    if (k != NONE) { w.g_key[s] = k; return; }
-    if (y == x) return;  // a chain without a root: k_seg_kind reports it
-    const uint32_t z = w.g_link[y];
-    if (z != y) w.g_link[x] = z;
-    x = y;
-  }
 }
 
 uint32_t run_key_resolution(const Work& w, uint32_t nsegs, hipStream_t s) {
   if (!nsegs) return 0;
-  hipLaunchKernelGGL(k_keyfind, dim3((nsegs + 255) / 256), dim3(256), 0, s, w, nsegs);
-  hipLaunchKernelGGL(k_seg_kind, dim3((nsegs + 255) / 256), dim3(256), 0, s, w, nsegs);
+  hipLaunchKernelGGL(k_resolve, dim3((nsegs + 255) / 256), dim3(256), 0, s, w, nsegs);
   return 1;
 }
 
 // --------------------------------------------------------------------------- map winner
 // Per YMap entry: the max-client child of its origin (the winner descent: YATA orders siblings by
-// client, Item.integrate Y@77594) and whether its origin unit has a child of a lower client than
-// the unit's own (then the origin's own-client successor is not adjacent to it: no merge).
-// Segments are numbered in (client index, clock) order, so the max child is the max segment: a
-// fire-and-forget u32 atomicMax of s + 1 (u64 atomics issue at well under half the rate; reading
-// the slot first to skip a useless atomic is a dependent random load that costs more than the
-// atomic: 26 ms vs 13.6 ms measured on the 112-document C2 batch). The adjacency test needs no
-// minimum at all: a lower-client child only marks its origin (idempotent plain store), and most
-// children never store (C2: replicas above the base client, chains within one client).
-__global__ __launch_bounds__(256) void k_children(Work w, uint32_t nsegs) {
-  const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
-  if (s >= nsegs) return;
-  const uint32_t f = w.g_flags[s];
-  if (!(f & SEG_PSUB)) return;
-  const uint32_t os = w.g_oseg[s];
-  if (os != NONE) {
-    atomicMax(&w.g_maxchild[os], s + 1);
-    if (f & SEG_OLOW) w.u_minchild[w.g_origin[s]] = 0u;
-  } else if (f & SEG_ROOT) {
-    atomicMax(&w.k_rootmax[w.g_key[s]], s + 1);
-  }
-}
+// client, Item.integrate Y@77594) — computed by k_seg_props + k_resolve above — and whether its
+// origin unit has a child of a lower client than the unit's own (then the origin's own-client
+// successor is not adjacent to it: no merge; marked in k_seg_props).
+void launch_map_winner(const Work& w, uint32_t nsegs, hipStream_t s) {}
 // the key's value is the rightmost entry: descend from the max-client root through the max-client
 // child until a leaf (YATA order of an origin-only tree, SURVEY.md §7 hard part 2)
 __global__ void k_winner_walk(Work w) {
@@ -415,9 +426,6 @@ __global__ void k_overwrite(Work w, uint32_t nsegs) {
   if ((f & (SEG_PSUB | SEG_WIN)) == SEG_PSUB) w.g_flags[s] = f | SEG_DEL;
 }
 
-void launch_map_winner(const Work& w, uint32_t nsegs, hipStream_t s) {
-  if (nsegs) hipLaunchKernelGGL(k_children, dim3((nsegs + 255) / 256), dim3(256), 0, s, w, nsegs);
-}
 
 uint32_t run_descent(const Work& w, uint32_t nsegs, hipStream_t s, bool fold) {
   if (!nsegs) return 0;

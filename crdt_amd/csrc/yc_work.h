@@ -382,10 +382,11 @@ enum : uint32_t {
   SEG_ARRAY = 64u,     // member of a YArray list (no parentSub)
   SEG_PSUB = 128u,     // member of a YMap entry list (parentSub)
   SEG_OLOW = 256u,     // its client index is below its origin's (a YATA sibling placed before the
-                       // origin's own-client successor: that successor cannot merge, k_children)
+                       // origin's own-client successor: that successor cannot merge, k_seg_props)
   SEG_WIN = 512u,      // the value of its YMap entry (k_winner_walk); every other entry item is deleted
 };
-// bit 31 of g_key between k_seg_props and k_seg_kind: the list is a YMap entry (key slots < 2^31)
+// bit 31 of the climbing keys (g_tmp) between k_seg_props and k_resolve: the list is a YMap entry
+// (key slots < 2^31); g_key holds the final slots without it
 constexpr uint32_t KEY_PSUB = 0x80000000u;
 // key flags
 enum : uint32_t {
