@@ -1088,9 +1088,12 @@ void launch_ds_bound(const Work& w, hipStream_t s) {
   scan_u32(w.tmp, w.tmp_bytes, w.scratch, w.ds_region, w.nupd + 1, s);
   hipMemcpyAsync(&w.ctr->ds_region, w.ds_region + w.nupd, sizeof(uint32_t), hipMemcpyDeviceToDevice, s);
 }
+// the integrate path reads the ranges in their per-update regions (k_ds_apply); mergeUpdates /
+// diffUpdate (lazy) sort them, so there they are compacted into the dense table
 void launch_ds_decode(const Work& w, hipStream_t s) {
   if (w.nupd == 0) return;
   hipLaunchKernelGGL(k_ds_decode, dim3((w.nupd + 3) / 4), dim3(256), 0, s, w);
+  if (!w.lazy) return;
   scan_u32(w.tmp, w.tmp_bytes, w.ds_count, w.ds_dense_off, w.nupd + 1, s);
   hipLaunchKernelGGL(k_ds_compact, dim3((w.nupd + 3) / 4), dim3(256), 0, s, w);
 }

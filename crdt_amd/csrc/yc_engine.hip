@@ -302,6 +302,10 @@ void layout(ycrdt_batch* b, const std::vector<Src>& src, std::vector<uint32_t>& 
     const uint32_t v = (uint32_t)atoi(cs);
     if (v >= 64 && v <= SCHUNK && v % 64 == 0) b->schunk = v;
   }
+  if (const char* cs = getenv("YCRDT_SCHUNK")) {  // experiments: a fixed chunk size (64-byte multiple)
+    const uint32_t v = (uint32_t)atoi(cs);
+    if (v >= 64 && v <= SCHUNK && v % 64 == 0) b->schunk = v;
+  }
   order.clear();
   for (size_t i = 0; i < src.size(); ++i) if (src[i].dev) order.push_back((uint32_t)i);
   for (size_t i = 0; i < src.size(); ++i) if (!src[i].dev) order.push_back((uint32_t)i);
@@ -623,7 +627,9 @@ int run_decode(ycrdt_engine* e, ycrdt_batch* b, bool lazy, Decoded& D, bool gene
   D.nstructs = nstructs;
   D.nsections = nsections;
   D.nclients = nclients;
-  D.nds = std::min(c.nds, w.cap_ds);
+  // lazy: the compacted range count; integrate: the ranges stay in their regions (a nonzero
+  // region total says there may be some, k_ds_apply reads each update's count)
+  D.nds = lazy ? std::min(c.nds, w.cap_ds) : c.ds_region;
   D.nunits = nunits;
   return YCRDT_OK;
 }
@@ -720,7 +726,6 @@ int run_merge(ycrdt_engine* e, ycrdt_batch* b, const std::unordered_map<uint32_t
   w.g_origin = take<uint32_t>(V, B_GORIG, U + 1, ok);
   w.g_rorigin = take<uint32_t>(V, B_GRORIG, U + 1, ok);
   w.g_link = take<uint32_t>(V, B_GLINK, U + 1, ok);
-  w.g_oseg = take<uint32_t>(V, B_GOSEG, U + 1, ok);
   w.g_key = take<uint32_t>(V, B_GKEY, U + 1, ok);
   w.g_maxchild = take<uint32_t>(V, B_GMAXC, U + 1, ok);
   w.g_outid = take<uint32_t>(V, B_GOUTID, U + 2, ok);

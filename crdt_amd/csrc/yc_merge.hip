@@ -4,7 +4,7 @@
 // (client, clock) of the merged store), so every step below is a flat, coalesced pass:
 //   k_owner        dedupe (integrateStructs offset logic, Y@19963): each unit takes its struct
 //                  from the earliest update that carries it (atomicMin over struct index)
-//   k_ds_mark      delete-set application (readAndApplyDeleteSet, Y@11619) as unit flags
+//   k_ds_apply     delete-set application (readAndApplyDeleteSet, Y@11619) as unit flags
 //   k_refs         split points required by origin / rightOrigin references (getItemCleanEnd /
 //                  getItemCleanStart, Y@29100) + min child client per unit (list adjacency)
 //   k_cuts         struct boundaries -> bitmap; popcount scan -> segments
@@ -73,44 +73,53 @@ __global__ __launch_bounds__(256) void k_owner(Work w, uint32_t nstructs) {
 }
 
 // --------------------------------------------------------------------------- delete sets
-__global__ void k_ds_prep(Work w, uint32_t nds, uint32_t nclients) {
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= nds) { if (i == nds) w.ds_len[i] = 0; return; }
-  DsRange r = w.ds[i];
-  const uint32_t c = find_client(w, nclients, doc_of_update(w, r.upd), r.client);
-  uint32_t len = r.len;
-  if (len == 0) { w.ds_len[i] = 0; return; }
-  // a range past the known state is Yjs's pendingDs: an error here (the host then takes the pending
-  // path), clipped silently when the host already computed the caps
-  if (c == NONE) { if (!w.capped) raise_err(&w.ctr->err, ERR_PENDING); w.ds_len[i] = 0; return; }
-  const uint64_t endc = (uint64_t)r.clock + len;
-  if (endc > w.cl_state[c]) { if (!w.capped) raise_err(&w.ctr->err, ERR_PENDING); len = r.clock < w.cl_state[c] ? w.cl_state[c] - r.clock : 0; }
-  r.client = c;
-  w.ds[i] = r;
-  w.ds_len[i] = len;
-}
 // UF_DS and UF_CUT own a byte of the unit's flag word each, so their writers store that byte
 // (no read-modify-write round trip); concurrent stores of the same byte write the same value
 __device__ __forceinline__ void set_flag_byte(uint32_t* u_flags, uint32_t g, uint32_t byte) {
   reinterpret_cast<uint8_t*>(u_flags)[(size_t)g * 4 + byte] = 1;
 }
-__global__ __launch_bounds__(256) void k_ds_mark(Work w, uint32_t nds) {
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+// The delete sets of a merge, straight from the decoder's per-update regions (no compaction): one
+// wavefront per update resolves its ranges' clients, clips them to the known states (pendingDs)
+// and marks the units (the prep and mark passes above in one, for the integrate path)
+__global__ __launch_bounds__(256) void k_ds_apply(Work w, uint32_t nclients) {
   const uint32_t lane = threadIdx.x & 63;
-  uint64_t gb = 0;
-  uint32_t n = 0;
-  if (i < nds) {
-    n = w.ds_len[i];
-    if (n) { const DsRange r = w.ds[i]; gb = w.cl_base[r.client] + r.clock; }
-  }
-  const bool lng = n > LONG_UNITS;
-  if (!lng)
-    for (uint32_t k = 0; k < n; ++k) set_flag_byte(w.u_flags, (uint32_t)(gb + k), 1);
-  for (uint64_t m = __ballot(lng); m; m &= m - 1) {
-    const int L = __ffsll((long long)m) - 1;
-    const uint64_t g0 = shfl64(gb, L);
-    const uint32_t nl = __shfl(n, L);
-    for (uint32_t k = lane; k < nl; k += 64) set_flag_byte(w.u_flags, (uint32_t)(g0 + k), 1);
+  const uint32_t u = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  if (u >= w.nupd) return;
+  const uint32_t n = w.ds_count[u], base = w.ds_region[u];
+  const uint32_t doc = doc_of_update(w, u);
+  for (uint32_t i0 = 0; i0 < n; i0 += 64) {
+    const uint32_t i = i0 + lane;
+    uint64_t gb = 0;
+    uint32_t len = 0;
+    if (i < n) {
+      const DsRange r = w.ds_tmp[base + i];
+      len = r.len;
+      if (len) {
+        const uint32_t c = find_client(w, nclients, doc, r.client);
+        // a range past the known state is Yjs's pendingDs: an error here (the host then takes the
+        // pending path), clipped silently when the host already computed the caps
+        if (c == NONE) {
+          if (!w.capped) raise_err(&w.ctr->err, ERR_PENDING);
+          len = 0;
+        } else {
+          const uint32_t st = w.cl_state[c];
+          if ((uint64_t)r.clock + len > st) {
+            if (!w.capped) raise_err(&w.ctr->err, ERR_PENDING);
+            len = r.clock < st ? st - r.clock : 0;
+          }
+          gb = w.cl_base[c] + r.clock;
+        }
+      }
+    }
+    const bool lng = len > LONG_UNITS;
+    if (!lng)
+      for (uint32_t k = 0; k < len; ++k) set_flag_byte(w.u_flags, (uint32_t)(gb + k), 1);
+    for (uint64_t m = __ballot(lng); m; m &= m - 1) {
+      const int L = __ffsll((long long)m) - 1;
+      const uint64_t g0 = shfl64(gb, L);
+      const uint32_t nl = __shfl(len, L);
+      for (uint32_t k = lane; k < nl; k += 64) set_flag_byte(w.u_flags, (uint32_t)(g0 + k), 1);
+    }
   }
 }
 
@@ -147,10 +156,10 @@ __global__ __launch_bounds__(256) void k_cuts(Work w, uint64_t nunits) {
     if (own == NONE) {
       raise_err(&w.ctr->err, ERR_PENDING);  // a gap in a client's clock range
     } else {
+      // a struct's first unit needs no test of its own: the unit before it (if any) has another
+      // owner — units of one struct are consecutive — and so does a client's first unit
       const uint32_t f = w.u_flags[g];
       cut = (f & UF_CUT) || g == 0;
-      const uint64_t first = w.cl_base[w.s_cidx[own]] + w.s_clock[own];
-      cut |= g == first;
       if (g > 0) {
         const uint32_t po = w.u_owner[g - 1];
         const uint32_t pf = w.u_flags[g - 1];
@@ -163,12 +172,6 @@ __global__ __launch_bounds__(256) void k_cuts(Work w, uint64_t nunits) {
   }
   const uint64_t word = __ballot(cut);
   if ((threadIdx.x & 63) == 0 && g < nunits) w.u_cutbits[g >> 6] = word;
-}
-__global__ void k_client_cuts(Work w, uint32_t nclients) {
-  const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= nclients || w.cl_state[c] == 0) return;
-  const uint64_t g = w.cl_base[c];
-  atomicOr((unsigned long long*)&w.u_cutbits[g >> 6], 1ull << (g & 63));
 }
 __global__ void k_scatter_seg(Work w, uint32_t nwords, uint64_t nunits) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -187,10 +190,7 @@ __global__ void k_scatter_seg(Work w, uint32_t nwords, uint64_t nunits) {
 void launch_units(const Work& w, uint32_t nstructs, uint32_t nclients, uint32_t nds, uint64_t nunits, hipStream_t s) {
   fill_u32_multi({{w.u_owner, nunits, NONE}, {w.u_flags, nunits, 0u}, {w.u_minchild, nunits, NONE}}, s);
   if (nstructs) hipLaunchKernelGGL(k_owner, dim3((nstructs + 255) / 256), dim3(256), 0, s, w, nstructs);
-  if (nds) {
-    hipLaunchKernelGGL(k_ds_prep, dim3(nds / 256 + 1), dim3(256), 0, s, w, nds, nclients);
-    hipLaunchKernelGGL(k_ds_mark, dim3((nds + 255) / 256), dim3(256), 0, s, w, nds);
-  }
+  if (nds && w.nupd) hipLaunchKernelGGL(k_ds_apply, dim3((w.nupd + 3) / 4), dim3(256), 0, s, w, nclients);
   if (nstructs) hipLaunchKernelGGL(k_refs, dim3((nstructs + 255) / 256), dim3(256), 0, s, w, nstructs);
 }
 
@@ -203,7 +203,6 @@ __global__ void k_popc_words(const uint64_t* __restrict__ bits, uint32_t* __rest
 void launch_segments(const Work& w, uint32_t nclients, uint64_t nunits, hipStream_t s) {
   const uint32_t nwords = (uint32_t)((nunits + 63) / 64);
   hipLaunchKernelGGL(k_cuts, dim3(nwords / 4 + 1), dim3(256), 0, s, w, nunits);
-  hipLaunchKernelGGL(k_client_cuts, dim3(nclients / 256 + 1), dim3(256), 0, s, w, nclients);
   hipLaunchKernelGGL(k_popc_words, dim3(nwords / 256 + 1), dim3(256), 0, s, (const uint64_t*)w.u_cutbits, w.scratch, nwords);
   scan_u32(w.tmp, w.tmp_bytes, w.scratch, w.u_wpre, nwords + 1, s);
   hipLaunchKernelGGL(k_scatter_seg, dim3(nwords / 256 + 1), dim3(256), 0, s, w, nwords, nunits);
@@ -296,7 +295,6 @@ __global__ __launch_bounds__(256) void k_seg_props(Work w, uint32_t nsegs) {
   } else if (!gc) {
     link = seg_of(w.u_cutbits, w.u_wpre, origin != NONE ? origin : rorigin);
   }
-  w.g_oseg[s] = (!gc && origin != NONE) ? link : NONE;  // link = the origin's segment here
   if (gc) sf |= SEG_GC | SEG_DEL;
   else sf |= SEG_ITEM;
   const bool olow = !gc && expl && origin != NONE && socx < NONE - 1 && cidx < socx;
@@ -379,8 +377,10 @@ __global__ __launch_bounds__(256) void k_resolve(Work w, uint32_t nsegs) {
         f |= arr ? SEG_ARRAY : SEG_PSUB;
         w.g_flags[s] = f;
         if (!arr) {  // the winner reduction's settling pass (k_seg_props stored one child)
-          const uint32_t os = w.g_oseg[s];
-          uint32_t* slot = os != NONE ? &w.g_maxchild[os] : (f & SEG_ROOT) ? &w.k_rootmax[kv & ~KEY_PSUB] : nullptr;
+          // the origin's segment (k_seg_props stored into the same slot: its link)
+          const uint32_t og = w.g_origin[s];
+          uint32_t* slot = og != NONE ? &w.g_maxchild[seg_of(w.u_cutbits, w.u_wpre, og)]
+                           : (f & SEG_ROOT) ? &w.k_rootmax[kv & ~KEY_PSUB] : nullptr;
           if (slot && *slot < s + 1) atomicMax(slot, s + 1);
         }
       }

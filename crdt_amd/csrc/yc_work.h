@@ -146,7 +146,6 @@ struct Work {
   uint32_t* g_origin = nullptr;    // origin unit (global) or NONE
   uint32_t* g_rorigin = nullptr;   // right-origin unit or NONE
   uint32_t* g_link = nullptr;      // pointer-jumping link (key resolution)
-  uint32_t* g_oseg = nullptr;      // segment holding the origin unit (NONE: no origin / GC)
   uint32_t* g_key = nullptr;       // resolved key slot or NONE
   uint32_t* g_maxchild = nullptr;  // seg + 1 of the max-client child (segments are in client order), 0 = none
   uint32_t* g_next = nullptr;      // descent pointer / pointer jumping

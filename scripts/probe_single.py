@@ -11,7 +11,12 @@ import crdt_amd  # noqa: E402
 from crdt_amd.workload import C2, gen_map  # noqa: E402
 
 reps = int(sys.argv[1]) if len(sys.argv) > 1 else 20
+subset = sys.argv[2] if len(sys.argv) > 2 else "all"  # all | base | replicas
 ups = gen_map(**C2)[0]
+if subset == "base":
+    ups = ups[:1]
+elif subset == "replicas":
+    ups = ups[1:]
 eng = crdt_amd.Engine()
 b = crdt_amd.Batch(ups, eng)
 st = b.merge()
