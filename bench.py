@@ -59,6 +59,9 @@ def parse():
                    help="time the headline merge only (no side legs): rocprof averages then match the bench line")
     p.add_argument("--c3-items", type=int, default=10_000_000,
                    help="C3 leg: YArray 'messages', 256 replicas x 16 rounds, this many values (0 = off)")
+    p.add_argument("--billion", type=int, default=0, metavar="DOCS",
+                   help="opt-in leg: DOCS distinct C2 documents (1120 = 1.0 B items, ~15 GB of updates) merged in ONE "
+                        "ycrdt_batch_merge (multi-window batch), with its HBM footprint and properties; skips the side legs")
     return p.parse_args()
 
 
@@ -327,6 +330,54 @@ def c3_leg(eng, n_items, steps=3):
                             "kind": "reference", "parity": y["out_sha256"] == hashlib.sha256(gout).hexdigest(),
                             "sample": f"{n} values, Yjs {y['yjs']} in Node {y['node']}"}
     return res
+
+
+def billion_leg(eng, cfg, gen_map, n_docs, reps=3):
+    """north_star 'bit-exact Yjs merge of >= 1 B CRDT items': n_docs distinct C2 documents (seeds
+    disjoint from the headline's) merged in ONE ycrdt_batch_merge — a batch of ~15 GB laid out in
+    4 GiB windows (yc_work.h) — timed with its inputs resident in HBM. Properties at full size:
+    three documents merged alone (forward and reversed update order) give their bytes in the big
+    merge; the merge of all outputs as one batch returns them unchanged (idempotence)."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    import crdt_amd
+
+    seeds = [cfg["seed"] + 7_000_003 + i * 1_009 for i in range(n_docs)]
+    g0 = time.perf_counter()
+    with ThreadPoolExecutor(16) as ex:
+        docs = list(ex.map(lambda sd: gen_map(**dict(cfg, seed=sd))[0], seeds))
+    gen_s = time.perf_counter() - g0
+    in_bytes = sum(len(u) for d in docs for u in d)
+    s0 = time.perf_counter()
+    b = crdt_amd.Batch(docs=docs, engine=eng)
+    stage_s = time.perf_counter() - s0
+    st = b.merge()  # first merge: workspace allocation
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        st = b.merge()
+    ms = (time.perf_counter() - t0) * 1e3 / reps
+    hbm = eng.device_bytes()
+    outs = [u for u, _ in b.result_docs()]
+    out_bytes = sum(map(len, outs))
+    del b
+    alone = True
+    for k in (0, n_docs // 2, n_docs - 1):
+        for ups in (docs[k], list(reversed(docs[k]))):
+            sb = crdt_amd.Batch(ups, eng)
+            sb.merge()
+            alone = alone and sb.result()[0] == outs[k]
+            del sb
+    ib = crdt_amd.Batch(docs=[[o] for o in outs], engine=eng)
+    ist = ib.merge()
+    idem = [u for u, _ in ib.result_docs()] == outs
+    del ib
+    return {"docs": n_docs, "updates": sum(map(len, docs)), "input_bytes": in_bytes, "items": st.items,
+            "structs": st.structs, "segments": st.segments, "output_bytes": out_bytes, "merges": 1,
+            "ms_per_merge": round(ms, 2), "items_per_s": round(st.items / (ms * 1e-3), 1),
+            "windows": (in_bytes >> 32) + 1, "hbm_footprint_bytes": hbm,
+            "alone_equal_fwd_and_reversed": alone, "idempotent": idem, "idempotence_merge_items": ist.items,
+            "generate_s": round(gen_s, 1), "stage_s": round(stage_s, 1),
+            "includes": "one multi-document device pass, inputs resident in HBM (staging and D2H not timed)"}
 
 
 def c4_leg(eng, reps=3):
@@ -661,7 +712,7 @@ def main():
 
     # ---- end to end (host buffers in, host buffers out): pack + H2D + merge + D2H + per-document
     # split; never `value`
-    e2e_steps = 0 if args.only_headline else 2
+    e2e_steps = 0 if args.only_headline or args.billion else 2
     e0 = time.perf_counter()
     for _ in range(e2e_steps):
         b2 = crdt_amd.Batch(docs=docs, engine=eng) if ndocs > 1 else crdt_amd.Batch(updates, eng)
@@ -675,7 +726,7 @@ def main():
     del batch
     # ---- one C2 document per step (the round-1 headline shape), for continuity
     single = None
-    if ndocs > 1 and rank == 0 and not args.only_headline:
+    if ndocs > 1 and rank == 0 and not args.only_headline and not args.billion:
         sb = crdt_amd.Batch(updates, eng)
         sst = sb.merge()
         s0 = time.perf_counter()
@@ -686,20 +737,21 @@ def main():
         del sb
 
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline and not args.only_headline:
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and not args.only_headline and not args.billion:
         cpu = cpu_baselines(args, cfg, updates, out_update, crdt_amd.Batch(updates, eng).merge(), eng, gen_map)
     fleet = None
-    if rank == 0 and world == 1 and args.fleet_pairs > 0 and not args.only_headline:
+    if rank == 0 and world == 1 and args.fleet_pairs > 0 and not args.only_headline and not args.billion:
         fleet = fleet_sync_leg(eng, args.fleet_pairs)
     ingest = None
-    if rank == 0 and world == 1 and args.fleet_docs > 0 and not args.only_headline:
+    if rank == 0 and world == 1 and args.fleet_docs > 0 and not args.only_headline and not args.billion:
         ingest = fleet_ingest_leg(eng, args.fleet_docs)
-    side = rank == 0 and world == 1 and not args.only_headline
+    side = rank == 0 and world == 1 and not args.only_headline and not args.billion
     loop = apply_loop_leg(eng, updates, out_update) if side else None
     per_op = per_op_leg(eng) if side and not args.no_per_op else None
     c3 = c3_leg(eng, args.c3_items) if side and args.c3_items > 0 else None
     c4 = c4_leg(eng) if side and not args.no_c4 else None
     c4s = c4_sharded_leg(eng, world, rank, dist) if dist is not None and args.c4_sharded else None
+    billion = billion_leg(eng, cfg, gen_map, args.billion) if args.billion and rank == 0 else None
     line = {
         "metric": "CRDT items merged/sec at 1/2/4/8 MI355X + % of HBM roofline",
         "value": round(value, 1),
@@ -752,6 +804,7 @@ def main():
         "c3": c3,
         "c4": c4,
         "c4_sharded": c4s,
+        "billion": billion,
         "phases_ms": {n: round(m, 4) for n, m in phases},
     }
     if rank == 0:

@@ -80,6 +80,12 @@ __device__ __forceinline__ uint32_t wr_vu(uint8_t* __restrict__ o, uint32_t p, u
   o[p++] = (uint8_t)v;
   return p;
 }
+// the same at a 64-bit output position (the integrate encoder: outputs past 4 GiB)
+__device__ __forceinline__ uint64_t wr_vu(uint8_t* __restrict__ o, uint64_t p, uint32_t v) {
+  while (v > 127u) { o[p++] = (uint8_t)(0x80u | (v & 0x7fu)); v >>= 7; }
+  o[p++] = (uint8_t)v;
+  return p;
+}
 
 __device__ __forceinline__ uint32_t lower_bound_u32(const uint32_t* __restrict__ a, uint32_t n, uint32_t key) {
   uint32_t lo = 0, hi = n;

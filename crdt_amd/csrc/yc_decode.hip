@@ -275,7 +275,10 @@ __global__ __launch_bounds__(DL) void k_direct(Work w) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= w.nsmall) return;
   const uint32_t u = w.ulist[w.nbig + i];
-  const uint8_t* __restrict__ b = w.bytes;
+  const uint32_t uw = upd_win(w, u);  // positions below are relative to the update's window
+  const uint8_t* __restrict__ b = win_bytes(w, uw);
+  uint64_t* __restrict__ fbits = win_words(w.final_bits, uw);
+  uint64_t* __restrict__ sbits = win_words(w.sec_bits, uw);
   const uint32_t ustart = w.uoff[u], uend = ustart + w.ulen[u];
   uint32_t* err = &w.ctr->err;
   uint32_t* slot = win + threadIdx.x * DSTRIDE;
@@ -307,11 +310,11 @@ __global__ __launch_bounds__(DL) void k_direct(Work w) {
     sec.upd = u; sec.n = n; sec.client = client; sec.clock = clock;
     sec.first_pos = n ? p : NONE; sec.cidx = NONE; sec.first_idx = NONE; sec.pad = 0;
     w.sections[sbase + sct] = sec;
-    if (n) atomicOr((unsigned long long*)&w.sec_bits[p >> 6], 1ull << (p & 63));
+    if (n) atomicOr((unsigned long long*)&sbits[p >> 6], 1ull << (p & 63));
     for (uint32_t k = 0; k < n; ++k) {
       if (p >= uend) { raise_err(err, ERR_DECODE); w.ctr->err_info = p; return; }
       if ((p >> 6) != word) {
-        if (word != NONE) w.final_bits[word] = m;
+        if (word != NONE) fbits[word] = m;
         word = p >> 6;
         m = 0;
       }
@@ -334,7 +337,7 @@ __global__ __launch_bounds__(DL) void k_direct(Work w) {
       p += d;
     }
   }
-  if (word != NONE) w.final_bits[word] = m;
+  if (word != NONE) fbits[word] = m;
   w.dsstart[u] = p;
 }
 
@@ -435,7 +438,8 @@ __global__ __launch_bounds__(DL) void k_spec(Work w) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= w.ngroups) return;
   const Group G = w.groups[i];
-  const uint8_t* __restrict__ b = w.bytes;
+  const uint32_t uw = upd_win(w, G.upd);
+  const uint8_t* __restrict__ b = win_bytes(w, uw);
   const uint32_t uend = G.uend;
   uint32_t* slot = win + threadIdx.x * DSTRIDE;
   LdsSrc src{b, slot, 0, 0};
@@ -445,7 +449,7 @@ __global__ __launch_bounds__(DL) void k_spec(Work w) {
     const uint4* g = (const uint4*)(b + src.s0);
     fill_window(slot, g);
   };
-  uint64_t* __restrict__ spec = w.spec_bits;
+  uint64_t* __restrict__ spec = win_words(w.spec_bits, uw);
   uint32_t p = G.start, word = G.start >> 6;
   uint64_t m = 0;
   refill(p);
@@ -482,8 +486,9 @@ __global__ __launch_bounds__(256) void k_sync(Work w, const uint32_t* __restrict
   const Group G = w.groups[i];
   uint32_t X = xin[i];
   if (G.start != w.uoff[G.upd]) {  // chunks of one update are consecutive
-    const uint8_t* __restrict__ b = w.bytes;
-    uint64_t* __restrict__ spec = w.spec_bits;
+    const uint32_t uw = upd_win(w, G.upd);
+    const uint8_t* __restrict__ b = win_bytes(w, uw);
+    uint64_t* __restrict__ spec = win_words(w.spec_bits, uw);
     const uint32_t E = xin[i - 1];
     uint32_t q = E, word = G.start >> 6;
     uint64_t m = 0;
@@ -525,7 +530,7 @@ __global__ __launch_bounds__(64) void k_xtab(Work w) {
   for (uint32_t t = blockIdx.x; t < nx; t += gridDim.x) {
   const uint32_t i = w.xlist[t];
   const Group G = w.groups[i];
-  const uint8_t* __restrict__ b = w.bytes;
+  const uint8_t* __restrict__ b = win_bytes(w, upd_win(w, G.upd));
   const uint32_t uend = G.uend, cs = G.start;
   const uint32_t wlen = min(SCHUNK + XHALO, (uend + 15u - cs) & ~15u);
   for (uint32_t k = e; k < wlen / 16; k += 64) ((uint4*)cb)[k] = ((const uint4*)(b + cs))[k];
@@ -636,8 +641,11 @@ __global__ __launch_bounds__(64) void k_walk(Work w) {
   const uint32_t u = w.ulist[blockIdx.x];
   if (TABLES && !w.ufail[u]) return;
   const uint32_t lane = threadIdx.x;
-  const uint8_t* __restrict__ b = w.bytes;
-  const uint64_t* __restrict__ spec = w.spec_bits;
+  const uint32_t uw = upd_win(w, u);  // positions below are relative to the update's window
+  const uint8_t* __restrict__ b = win_bytes(w, uw);
+  const uint64_t* __restrict__ spec = win_words(w.spec_bits, uw);
+  uint64_t* __restrict__ fbits = win_words(w.final_bits, uw);
+  uint64_t* __restrict__ sbits = win_words(w.sec_bits, uw);
   const uint32_t ustart = w.uoff[u], uend = ustart + w.ulen[u];
   const uint32_t CH = w.schunk;
   const uint32_t c0 = w.ugroup[u], nch = (w.ulen[u] + CH - 1) / CH;
@@ -683,7 +691,7 @@ __global__ __launch_bounds__(64) void k_walk(Work w) {
       sec.upd = u; sec.n = n; sec.client = client; sec.clock = clock;
       sec.first_pos = n ? p : NONE; sec.cidx = NONE; sec.first_idx = NONE; sec.pad = 0;
       w.sections[sbase + sct] = sec;
-      if (n) atomicOr((unsigned long long*)&w.sec_bits[p >> 6], 1ull << (p & 63));
+      if (n) atomicOr((unsigned long long*)&sbits[p >> 6], 1ull << (p & 63));
     }
     uint32_t r = n;
     while (r > 0) {
@@ -774,8 +782,8 @@ __global__ __launch_bounds__(64) void k_walk(Work w) {
       auto mark_all = [&]() {
         if (tabbed) w.tentry[c0 + j] = E;
         else {
-          or_words(w.final_bits, cs >> 6, mw, nw);
-          if (merged) or_range(w.final_bits, spec, q, ce);
+          or_words(fbits, cs >> 6, mw, nw);
+          if (merged) or_range(fbits, spec, q, ce);
         }
       };
       if (ends) {  // the section ends in lane jl's chunk
@@ -796,12 +804,12 @@ __global__ __launch_bounds__(64) void k_walk(Work w) {
             const uint32_t lw = (Lp - cs) >> 6;
             for (uint32_t x = 0; x < nw; ++x) {
               const uint64_t v = x < lw ? mw[x] : x == lw ? mw[x] & (~0ull >> (63 - (Lp & 63))) : 0ull;
-              if (v) atomicOr((unsigned long long*)&w.final_bits[(cs >> 6) + x], (unsigned long long)v);
+              if (v) atomicOr((unsigned long long*)&fbits[(cs >> 6) + x], (unsigned long long)v);
             }
           } else {
-            or_words(w.final_bits, cs >> 6, mw, nw);
+            or_words(fbits, cs >> 6, mw, nw);
             Lp = select_from(spec, q, rr - k);
-            or_range(w.final_bits, spec, q, Lp + 1);
+            or_range(fbits, spec, q, Lp + 1);
           }
           np = chain_step(b, Lp, uend);
         }
@@ -828,7 +836,9 @@ __global__ __launch_bounds__(DL) void k_xmark(Work w) {
   const Group G = w.groups[i];
   uint32_t p = w.tentry[i];
   if (p == NONE) return;
-  const uint8_t* __restrict__ b = w.bytes;
+  const uint32_t uw = upd_win(w, G.upd);
+  const uint8_t* __restrict__ b = win_bytes(w, uw);
+  uint64_t* __restrict__ fbits = win_words(w.final_bits, uw);
   const uint32_t uend = G.uend;
   uint32_t* slot = win + threadIdx.x * DSTRIDE;
   LdsSrc src{b, slot, 0, 0};
@@ -843,7 +853,7 @@ __global__ __launch_bounds__(DL) void k_xmark(Work w) {
   uint64_t m = 0;
   while (p < G.end) {
     if ((p >> 6) != word) {
-      if (m) atomicOr((unsigned long long*)&w.final_bits[word], (unsigned long long)m);
+      if (m) atomicOr((unsigned long long*)&fbits[word], (unsigned long long)m);
       word = p >> 6;
       m = 0;
     }
@@ -852,7 +862,7 @@ __global__ __launch_bounds__(DL) void k_xmark(Work w) {
     const uint32_t d = chain_len(src, b, p, uend);
     p += d ? d : 1u;
   }
-  if (m) atomicOr((unsigned long long*)&w.final_bits[word], (unsigned long long)m);
+  if (m) atomicOr((unsigned long long*)&fbits[word], (unsigned long long)m);
 }
 
 void launch_chunks(const Work& w, hipStream_t s) {
@@ -885,7 +895,8 @@ __global__ void k_popc(const uint64_t* __restrict__ bits, uint32_t* __restrict__
 // offset, one divergent store per bit of the word with the most.
 constexpr uint32_t SCAT_LDS = 4096;
 __global__ __launch_bounds__(256) void k_scatter_pos(const uint64_t* __restrict__ bits, const uint32_t* __restrict__ pre, uint32_t nwords,
-                                                     uint32_t* __restrict__ out, uint32_t cap, uint32_t* err) {
+                                                     uint32_t* __restrict__ out, uint32_t cap, uint32_t* err, uint8_t* __restrict__ swin,
+                                                     uint32_t shift) {
   __shared__ uint32_t buf[SCAT_LDS];
   const uint32_t i0 = blockIdx.x * 256, i = i0 + threadIdx.x;
   if (i0 >= nwords) return;
@@ -897,11 +908,19 @@ __global__ __launch_bounds__(256) void k_scatter_pos(const uint64_t* __restrict_
   }
   uint64_t x = i < nwords ? bits[i] : 0ull;
   uint32_t k = i < nwords ? pre[i] : 0u;
+  // positions within the window; a multi-window batch records the window (a workgroup's 256
+  // words never straddle a window: windows are 2^14 words or more)
+  const uint64_t wmask = (1ull << shift) - 1;
+  if (swin) {
+    const uint8_t wn = (uint8_t)(((uint64_t)i0 * 64) >> shift);
+    for (uint32_t t = threadIdx.x; t < total; t += 256) swin[base + t] = wn;
+  }
+  const uint32_t rel = (uint32_t)(((uint64_t)i * 64) & wmask);
   if (total > SCAT_LDS) {  // a dense stretch: every lane stores its own positions
-    for (; x; x &= x - 1) out[k++] = i * 64 + (uint32_t)__ffsll((long long)x) - 1;
+    for (; x; x &= x - 1) out[k++] = rel + (uint32_t)__ffsll((long long)x) - 1;
     return;
   }
-  for (k -= base; x; x &= x - 1) buf[k++] = i * 64 + (uint32_t)__ffsll((long long)x) - 1;
+  for (k -= base; x; x &= x - 1) buf[k++] = rel + (uint32_t)__ffsll((long long)x) - 1;
   __syncthreads();
   for (uint32_t t = threadIdx.x; t < total; t += 256) out[base + t] = buf[t];
 }
@@ -914,16 +933,17 @@ __global__ void k_section_rank(Work w, uint32_t nsections) {
   if (i >= nsections) return;
   Section* sec = &w.sections[i];
   if (sec->n == 0) return;
-  const uint32_t p = sec->first_pos;
-  if (!((w.final_bits[p >> 6] >> (p & 63)) & 1ull)) { raise_err(&w.ctr->err, ERR_DECODE); return; }
-  sec->first_idx = rank_incl(w.final_bits, w.wcnt, p) - 1;
-  w.sec_sorted[rank_incl(w.sec_bits, w.wsec, p) - 1] = i;
+  const uint32_t p = sec->first_pos, uw = upd_win(w, sec->upd);  // (bitmap words and prefixes of its window)
+  const uint64_t* fbits = win_words(w.final_bits, uw);
+  if (!((fbits[p >> 6] >> (p & 63)) & 1ull)) { raise_err(&w.ctr->err, ERR_DECODE); return; }
+  sec->first_idx = rank_incl(fbits, win_words(w.wcnt, uw), p) - 1;
+  w.sec_sorted[rank_incl(win_words(w.sec_bits, uw), win_words(w.wsec, uw), p) - 1] = i;
 }
 __global__ void k_struct_sec(Work w, uint32_t nstructs) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= nstructs) return;
-  const uint32_t p = w.s_pos[i];
-  w.s_sec[i] = w.sec_sorted[rank_incl(w.sec_bits, w.wsec, p) - 1];
+  const uint32_t p = w.s_pos[i], uw = w.nwin > 1 ? w.s_win[i] : 0u;
+  w.s_sec[i] = w.sec_sorted[rank_incl(win_words(w.sec_bits, uw), win_words(w.wsec, uw), p) - 1];
 }
 
 // before the count sync: struct / section-start counts (popcount prefix of the bitmaps)
@@ -938,7 +958,7 @@ void launch_struct_count(const Work& w, hipStream_t s) {
 void launch_struct_scatter(const Work& w, hipStream_t s) {
   const uint32_t nwords = (w.nbytes + 63) / 64;
   hipLaunchKernelGGL(k_scatter_pos, dim3(nwords / 256 + 1), dim3(256), 0, s, w.final_bits, w.wcnt, nwords, w.s_pos,
-                     w.cap_structs, &w.ctr->err);
+                     w.cap_structs, &w.ctr->err, w.nwin > 1 ? w.s_win : nullptr, w.win_shift);
 }
 
 // called once the section count is known on the host
@@ -959,7 +979,7 @@ __global__ __launch_bounds__(256) void k_ds_decode(Work w) {
   if (u >= w.nupd) return;
   const uint32_t p0 = w.dsstart[u];
   if (p0 == NONE) return;
-  const uint8_t* __restrict__ b = w.bytes;
+  const uint8_t* __restrict__ b = win_bytes(w, upd_win(w, u));
   const uint32_t end = w.uoff[u] + w.ulen[u];
   uint32_t* err = &w.ctr->err;
   enum { PH_N = 0, PH_CLIENT = 1, PH_NR = 2, PH_PAIRS = 3, PH_DONE = 4 };
@@ -1193,7 +1213,8 @@ __global__ __launch_bounds__(256) void k_struct_decode(Work w, uint32_t nstructs
   __shared__ __attribute__((aligned(16))) uint32_t win[256 * SD_STRIDE];
   uint32_t* slot = win + threadIdx.x * SD_STRIDE;
   const uint32_t s0 = p0 & ~15u;
-  const uint4* g = (const uint4*)(w.bytes + s0);  // the batch buffer is padded past its end
+  const uint8_t* __restrict__ bw = struct_bytes(w, i);  // the struct's window
+  const uint4* g = (const uint4*)(bw + s0);  // the batch buffer is padded past its end
   uint4 v4[SD_WIN / 16];
 #pragma unroll
   for (uint32_t k = 0; k < SD_WIN / 16; ++k) v4[k] = g[k];
@@ -1204,7 +1225,7 @@ __global__ __launch_bounds__(256) void k_struct_decode(Work w, uint32_t nstructs
   const uint32_t doc = doc_of_update(w, sec.upd);
   StructView v;
   uint32_t p = p0;
-  const int pr = parse_struct<true, 32, WinSrc>(WinSrc{w.bytes, slot, s0}, p, uend, 0xFFFFFFFFu, &v);
+  const int pr = parse_struct<true, 32, WinSrc>(WinSrc{bw, slot, s0}, p, uend, 0xFFFFFFFFu, &v);
   if (pr <= 0) { raise_err(err, pr == -1 ? ERR_UNSUPPORTED : ERR_DECODE); return; }  // -1: any nested > 32 deep
   w.s_len[i] = v.len;
   w.s_info[i] = v.info;

@@ -14,6 +14,7 @@
 namespace yc {
 
 __device__ __forceinline__ uint32_t* ccol(const Work& w, uint32_t col) { return w.cc + (size_t)col * (w.cap_clients + 1); }
+__device__ __forceinline__ uint64_t* ccol64(const Work& w, uint32_t col) { return w.cc64 + (size_t)col * (w.cap_clients + 1); }
 
 __device__ __forceinline__ uint32_t unit_client(const Work& w, uint32_t nclients, uint32_t g) {
   uint32_t lo = 0, hi = nclients;  // last c with cl_base[c] <= g
@@ -30,7 +31,7 @@ __device__ __forceinline__ uint32_t unit_client_hint(const Work& w, uint32_t ncl
   return unit_client(w, nclients, g);
 }
 
-__device__ __forceinline__ uint32_t copy_bytes(uint8_t* __restrict__ o, uint32_t p, const uint8_t* __restrict__ src, uint32_t n) {
+__device__ __forceinline__ uint64_t copy_bytes(uint8_t* __restrict__ o, uint64_t p, const uint8_t* __restrict__ src, uint32_t n) {
   for (uint32_t i = 0; i < n; ++i) o[p + i] = src[i];
   return p + n;
 }
@@ -38,7 +39,7 @@ __device__ __forceinline__ uint32_t copy_bytes(uint8_t* __restrict__ o, uint32_t
 // Encodes output struct `o` (segments [a,b)) at position p when WRITE, returns the size
 // (Item.write Y@80416 / GC.write Y@68955 with the writeStructs offset, Y@18809).
 template <bool WRITE>
-__device__ uint32_t encode_struct(const Work& w, uint32_t nclients, uint32_t o, uint8_t* __restrict__ out, uint32_t p0) {
+__device__ uint32_t encode_struct(const Work& w, uint32_t nclients, uint32_t o, uint8_t* __restrict__ out, uint64_t p0) {
   // The columns a struct can need are loaded in three dependent rounds — its first segment's row,
   // then its source struct's and its client's, then the reference clients' — each round issued
   // whole before anything branches on it, instead of one memory round trip per field.
@@ -49,13 +50,14 @@ __device__ uint32_t encode_struct(const Work& w, uint32_t nclients, uint32_t o, 
   const uint32_t cs = w.cl_start[cidx], cval = w.cl_vals[cidx];
   const uint32_t info0 = w.s_info[src], soc = w.s_ocidx[src], src_rc = w.s_rcidx[src];
   const uint32_t sclk = w.s_clock[src], slen = w.s_len[src], scel = w.s_celem[src], scend = w.s_cend[src];
+  const uint8_t* __restrict__ sb = struct_bytes(w, src);  // the source struct's window
   const uint32_t k0 = (uint32_t)(ga - base), k1 = (uint32_t)(gb - base);
   if (k1 <= cs) return 0;
   const uint32_t off = cs > k0 ? cs - k0 : 0;
   const uint32_t len = k1 - k0;
-  uint32_t p = p0;
+  uint64_t p = p0;
   if (!(f & SEG_ITEM)) {  // GC.write
-    if (WRITE) { out[p++] = REF_GC; p = wr_vu(out, p, len - off); return p - p0; }
+    if (WRITE) { out[p++] = REF_GC; p = wr_vu(out, p, len - off); return (uint32_t)(p - p0); }
     return 1 + vu_size(len - off);
   }
   const bool del = (f & SEG_DEL) != 0;
@@ -107,7 +109,7 @@ __device__ uint32_t encode_struct(const Work& w, uint32_t nclients, uint32_t o, 
   if (!has_o && !has_r) {  // parent info (root type name | parent item id) + parentSub
     const uint32_t pa = w.s_pa[src], pb = w.s_pb[src];
     if (w.s_pk[src] == 1) {
-      if (WRITE) { out[p++] = 1; p = copy_bytes(out, p, w.bytes + pa, pb); }
+      if (WRITE) { out[p++] = 1; p = copy_bytes(out, p, sb + pa, pb); }
       size += 1 + pb;
     } else {
       const uint32_t pc = w.cl_vals[pa];
@@ -116,7 +118,7 @@ __device__ uint32_t encode_struct(const Work& w, uint32_t nclients, uint32_t o, 
     }
     if (psub) {
       const uint32_t ps = w.s_psub[src], pl = w.s_psublen[src];
-      if (WRITE) p = copy_bytes(out, p, w.bytes + ps, pl);
+      if (WRITE) p = copy_bytes(out, p, sb + ps, pl);
       size += pl;
     }
   }
@@ -126,7 +128,7 @@ __device__ uint32_t encode_struct(const Work& w, uint32_t nclients, uint32_t o, 
   } else if ((ref == REF_ANY || ref == REF_JSON) && b == a + 1 && off == 0 && k0 == sclk && len == slen) {
     // the whole content of one source struct (the common case): its element bytes verbatim
     const uint32_t nbytes = scend - scel;
-    if (WRITE) { p = wr_vu(out, p, len); p = copy_bytes(out, p, w.bytes + scel, nbytes); }
+    if (WRITE) { p = wr_vu(out, p, len); p = copy_bytes(out, p, sb + scel, nbytes); }
     size += vu_size(len) + nbytes;
   } else if (ref == REF_ANY || ref == REF_JSON || ref == REF_STRING) {
     // elements of every segment from unit k0 + off on, sliced out of their source structs
@@ -140,14 +142,14 @@ __device__ uint32_t encode_struct(const Work& w, uint32_t nclients, uint32_t o, 
         if (u1 <= u0) continue;
         uint32_t b0 = 0, b1 = 0;
         if (!content_slice(w, sr, u0 - sb, u1 - sb, b0, b1)) { raise_err(&w.ctr->err, ERR_UNSUPPORTED); return size; }
-        if (pass == 1) p = copy_bytes(out, p, w.bytes + b0, b1 - b0);
+        if (pass == 1) p = copy_bytes(out, p, struct_bytes(w, sr) + b0, b1 - b0);
         else nbytes += b1 - b0;
       }
     }
     size += (ref == REF_STRING ? vu_size(nbytes) : vu_size(len - off)) + nbytes;
   } else {  // Binary / Embed / Format / Type / Doc: one unit, verbatim content bytes
     const uint32_t n = w.s_cend[src] - w.s_cpos[src];
-    if (WRITE) p = copy_bytes(out, p, w.bytes + w.s_cpos[src], n);
+    if (WRITE) p = copy_bytes(out, p, sb + w.s_cpos[src], n);
     size += n;
   }
   return size;
@@ -277,24 +279,25 @@ __global__ void k_unreverse3(Work w, uint32_t nclients) {
   const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
   if (c > nclients) return;
   // position of client c = sum of the blocks written before it = scan[slot of c]; total at [nclients]
-  const uint32_t src[3] = {CC_REVSCAN, CC_REVSCAN2, CC_REVSCAN3}, dst[3] = {CC_BLKPOS, CC_DSPOS, CC_SVPOS};
+  // (64-bit: the sections of a merge past 4 GiB)
+  const uint32_t src[3] = {CC64_SCAN, CC64_SCAN2, CC64_SCAN3}, dst[3] = {CC64_BLKPOS, CC64_DSPOS, CC64_SVPOS};
   for (int k = 0; k < 3; ++k) {
     const uint32_t slot = c == nclients ? nclients : (k > 0 && w.cl_emit) ? w.cl_slot[c] : nclients - 1 - c;
-    ccol(w, dst[k])[c] = ccol(w, src[k])[slot];
+    ccol64(w, dst[k])[c] = ccol64(w, src[k])[slot];
   }
 }
 
 __global__ void k_totals(Work w, uint32_t nclients) {
   const uint32_t nincl = w.ctr->pad[0], nds = w.ctr->pad[1], nsv = w.ctr->pad[2];
-  const uint32_t sblk = ccol(w, CC_BLKPOS)[nclients];
-  const uint32_t sds = ccol(w, CC_DSPOS)[nclients];
-  const uint32_t ssv = ccol(w, CC_SVPOS)[nclients];
+  const uint64_t sblk = ccol64(w, CC64_BLKPOS)[nclients];
+  const uint64_t sds = ccol64(w, CC64_DSPOS)[nclients];
+  const uint64_t ssv = ccol64(w, CC64_SVPOS)[nclients];
   w.ctr->pad[3] = vu_size(nincl);                 // struct section header size
-  w.ctr->pad[4] = vu_size(nincl) + sblk;          // delete-set section start
-  w.ctr->out_bytes = vu_size(nincl) + sblk + vu_size(nds) + sds;
-  w.ctr->sv_bytes = vu_size(nsv) + ssv;
+  w.ctr->ds_base = vu_size(nincl) + sblk;         // delete-set section start
+  w.ctr->out_total = vu_size(nincl) + sblk + vu_size(nds) + sds;
+  w.ctr->sv_bytes = (uint32_t)(vu_size(nsv) + ssv);
   // the output buffers were sized from a bound before the sizes were known; never write past them
-  if (w.ctr->out_bytes > w.cap_out || w.ctr->sv_bytes > w.cap_sv) { w.ctr->pad[5] = 1; raise_err(&w.ctr->err, ERR_CAPACITY); }
+  if (w.ctr->out_total > w.cap_out || vu_size(nsv) + ssv > w.cap_sv) { w.ctr->pad[5] = 1; raise_err(&w.ctr->err, ERR_CAPACITY); }
 }
 
 __global__ __launch_bounds__(256) void k_write_structs(Work w, uint32_t nsegs, uint32_t nclients) {
@@ -303,33 +306,34 @@ __global__ __launch_bounds__(256) void k_write_structs(Work w, uint32_t nsegs, u
   if (w.o_size[o] == 0) return;
   const uint32_t c = w.o_cidx[o];
   const uint32_t fi = ccol(w, CC_FIRST_INCL)[c];
-  const uint32_t p = w.ctr->pad[3] + ccol(w, CC_BLKPOS)[c] + ccol(w, CC_HDR)[c] + (w.o_pos[o] - w.o_pos[fi]);
+  // (o_pos wraps at 2^32: differences within one client's block are exact)
+  const uint64_t p = w.ctr->pad[3] + ccol64(w, CC64_BLKPOS)[c] + ccol(w, CC_HDR)[c] + (uint32_t)(w.o_pos[o] - w.o_pos[fi]);
   encode_struct<true>(w, nclients, o, w.out, p);
 }
 __global__ void k_write_clients(Work w, uint32_t nclients) {
   const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
   if (w.ctr->pad[5]) return;
   if (c == 0) {
-    wr_vu(w.out, 0, w.ctr->pad[0]);
-    wr_vu(w.out, w.ctr->pad[4], w.ctr->pad[1]);
-    wr_vu(w.sv_out, 0, w.ctr->pad[2]);
+    wr_vu(w.out, (uint64_t)0, w.ctr->pad[0]);
+    wr_vu(w.out, (uint64_t)w.ctr->ds_base, w.ctr->pad[1]);
+    wr_vu(w.sv_out, (uint64_t)0, w.ctr->pad[2]);
   }
   if (c >= nclients) return;
   if (ccol(w, CC_NINCL)[c]) {
-    uint32_t p = w.ctr->pad[3] + ccol(w, CC_BLKPOS)[c];
+    uint64_t p = w.ctr->pad[3] + ccol64(w, CC64_BLKPOS)[c];
     p = wr_vu(w.out, p, ccol(w, CC_NINCL)[c]);
     p = wr_vu(w.out, p, w.cl_vals[c]);
     wr_vu(w.out, p, w.cl_start[c]);
   }
   const uint32_t nr = ccol(w, CC_NRUNS)[c];
   if (nr) {
-    const uint32_t dsbase = w.ctr->pad[4] + vu_size(w.ctr->pad[1]);
-    uint32_t p = dsbase + ccol(w, CC_DSPOS)[c];
+    const uint64_t dsbase = w.ctr->ds_base + vu_size(w.ctr->pad[1]);
+    uint64_t p = dsbase + ccol64(w, CC64_DSPOS)[c];
     p = wr_vu(w.out, p, w.cl_vals[c]);
     wr_vu(w.out, p, nr);
   }
   if (w.cl_state[c]) {
-    uint32_t p = vu_size(w.ctr->pad[2]) + ccol(w, CC_SVPOS)[c];
+    uint64_t p = vu_size(w.ctr->pad[2]) + ccol64(w, CC64_SVPOS)[c];
     p = wr_vu(w.sv_out, p, w.cl_vals[c]);
     wr_vu(w.sv_out, p, w.cl_state[c]);
   }
@@ -341,8 +345,8 @@ __global__ void k_write_runs(Work w, uint32_t nsegs) {
   const uint32_t c = w.g_cidx[s];
   const uint32_t first = ccol(w, CC_FIRST_RUN)[c];
   const uint32_t nr = ccol(w, CC_NRUNS)[c];
-  const uint32_t dsbase = w.ctr->pad[4] + vu_size(w.ctr->pad[1]);
-  uint32_t p = dsbase + ccol(w, CC_DSPOS)[c] + vu_size(w.cl_vals[c]) + vu_size(nr) + (w.r_pos[r] - w.r_pos[first]);
+  const uint64_t dsbase = w.ctr->ds_base + vu_size(w.ctr->pad[1]);
+  uint64_t p = dsbase + ccol64(w, CC64_DSPOS)[c] + vu_size(w.cl_vals[c]) + vu_size(nr) + (uint32_t)(w.r_pos[r] - w.r_pos[first]);
   p = wr_vu(w.out, p, (uint32_t)(w.g_start[s] - w.cl_base[c]));
   wr_vu(w.out, p, w.r_len[r]);
 }
@@ -350,10 +354,10 @@ __global__ void k_write_runs(Work w, uint32_t nsegs) {
 static void rev_scans(const Work& w, uint32_t nclients, hipStream_t s) {
   const uint32_t grid = nclients / 256 + 1;
   hipLaunchKernelGGL(k_reverse3, dim3(grid), dim3(256), 0, s, w, nclients);
-  const uint32_t cols[3][2] = {{CC_REV, CC_REVSCAN}, {CC_REV2, CC_REVSCAN2}, {CC_REV3, CC_REVSCAN3}};
+  const uint32_t cols[3][2] = {{CC_REV, CC64_SCAN}, {CC_REV2, CC64_SCAN2}, {CC_REV3, CC64_SCAN3}};
   for (auto& c : cols)
-    scan_u32(w.tmp, w.tmp_bytes, w.cc + (size_t)c[0] * (w.cap_clients + 1), w.cc + (size_t)c[1] * (w.cap_clients + 1),
-             nclients + 1, s);
+    scan_u32_to_u64(w.tmp, w.tmp_bytes, w.cc + (size_t)c[0] * (w.cap_clients + 1), w.cc64 + (size_t)c[1] * (w.cap_clients + 1),
+                    nclients + 1, s);
   hipLaunchKernelGGL(k_unreverse3, dim3(grid), dim3(256), 0, s, w, nclients);
 }
 
@@ -394,33 +398,33 @@ void launch_encode_write(const Work& w, uint32_t nsegs, uint32_t nclients, hipSt
 // descending order, so each document's struct blocks, delete-set blocks and state-vector entries
 // are contiguous: rng[9d + 0..8] = struct (lo, hi, clients), delete set (lo, hi, clients),
 // state vector (lo, hi, entries), relative to each section's first block.
-__global__ void k_doc_ranges_init(uint32_t* rng, uint32_t ndocs) {
+__global__ void k_doc_ranges_init(unsigned long long* rng, uint32_t ndocs) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < 9 * ndocs) rng[i] = (i % 3 == 0) ? 0xFFFFFFFFu : 0u;
+  if (i < 9 * ndocs) rng[i] = (i % 3 == 0) ? ~0ull : 0ull;
 }
-__global__ void k_doc_ranges(Work w, uint32_t nclients, uint32_t ndocs, uint32_t* rng) {
+__global__ void k_doc_ranges(Work w, uint32_t nclients, uint32_t ndocs, unsigned long long* rng) {
   const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= nclients) return;
   const uint32_t d = w.cl_doc[c];
   if (d >= ndocs) { raise_err(&w.ctr->err, ERR_DECODE); return; }
-  uint32_t* r = rng + 9 * (size_t)d;
+  unsigned long long* r = rng + 9 * (size_t)d;
   if (ccol(w, CC_NINCL)[c]) {
-    atomicMin(&r[0], ccol(w, CC_BLKPOS)[c]);
-    atomicMax(&r[1], ccol(w, CC_BLKPOS)[c] + ccol(w, CC_BLK)[c]);
-    atomicAdd(&r[2], 1u);
+    atomicMin(&r[0], (unsigned long long)ccol64(w, CC64_BLKPOS)[c]);
+    atomicMax(&r[1], (unsigned long long)(ccol64(w, CC64_BLKPOS)[c] + ccol(w, CC_BLK)[c]));
+    atomicAdd(&r[2], 1ull);
   }
   if (ccol(w, CC_NRUNS)[c]) {
-    atomicMin(&r[3], ccol(w, CC_DSPOS)[c]);
-    atomicMax(&r[4], ccol(w, CC_DSPOS)[c] + ccol(w, CC_DSBLK)[c]);
-    atomicAdd(&r[5], 1u);
+    atomicMin(&r[3], (unsigned long long)ccol64(w, CC64_DSPOS)[c]);
+    atomicMax(&r[4], (unsigned long long)(ccol64(w, CC64_DSPOS)[c] + ccol(w, CC_DSBLK)[c]));
+    atomicAdd(&r[5], 1ull);
   }
   if (ccol(w, CC_SV)[c]) {
-    atomicMin(&r[6], ccol(w, CC_SVPOS)[c]);
-    atomicMax(&r[7], ccol(w, CC_SVPOS)[c] + ccol(w, CC_SV)[c]);
-    atomicAdd(&r[8], 1u);
+    atomicMin(&r[6], (unsigned long long)ccol64(w, CC64_SVPOS)[c]);
+    atomicMax(&r[7], (unsigned long long)(ccol64(w, CC64_SVPOS)[c] + ccol(w, CC_SV)[c]));
+    atomicAdd(&r[8], 1ull);
   }
 }
-void launch_doc_ranges(const Work& w, uint32_t nclients, uint32_t ndocs, uint32_t* rng, hipStream_t s) {
+void launch_doc_ranges(const Work& w, uint32_t nclients, uint32_t ndocs, unsigned long long* rng, hipStream_t s) {
   hipLaunchKernelGGL(k_doc_ranges_init, dim3(9 * ndocs / 256 + 1), dim3(256), 0, s, rng, ndocs);
   if (nclients) hipLaunchKernelGGL(k_doc_ranges, dim3(nclients / 256 + 1), dim3(256), 0, s, w, nclients, ndocs, rng);
 }

@@ -76,16 +76,37 @@ struct Arena {
   ~Arena() { for (void* s : slabs) hipFree(s); }
 };
 
+thread_local size_t g_failed_alloc = 0;  // the request of the last failed hipMalloc (error messages)
 bool grow(DevBuf& b, size_t bytes) {
   if (bytes == 0) bytes = 16;
   if (bytes <= b.cap) return true;
   if (b.p) hipFree(b.p);
   b.p = nullptr;
   b.cap = 0;
-  size_t c = bytes + bytes / 4 + 256;
-  if (hipMalloc(&b.p, c) != hipSuccess) return false;
+  // 25 % headroom for the next batch; past 1 GiB (billion-item merges, where the workspace is a
+  // large share of HBM) 3 %
+  size_t c = bytes + (bytes > (size_t(1) << 30) ? bytes / 32 : bytes / 4) + 256;
+  if (hipMalloc(&b.p, c) != hipSuccess) {
+    (void)hipGetLastError();
+    if (hipMalloc(&b.p, bytes + 256) != hipSuccess) {  // without the headroom
+      (void)hipGetLastError();
+      b.p = nullptr;
+      g_failed_alloc = bytes;
+      return false;
+    }
+    c = bytes + 256;
+  }
   b.cap = c;
   return true;
+}
+// "hipMalloc failed (what)" with the request and the device's free / total memory
+std::string oom(const char* what) {
+  size_t fr = 0, tot = 0;
+  (void)hipMemGetInfo(&fr, &tot);
+  char buf[256];
+  snprintf(buf, sizeof buf, "hipMalloc failed (%s): request %.2f GB, device free %.2f of %.2f GB", what,
+           g_failed_alloc / 1e9, fr / 1e9, tot / 1e9);
+  return buf;
 }
 
 template <class T>
@@ -132,7 +153,7 @@ enum Buf {
   B_WCNT, B_WSEC, B_DS, B_DSTMP, B_DSREG, B_DSCNT, B_DSOFF, B_DSLEN, B_DSSCAN, B_SCRATCH, B_TMP,
   B_SPOS, B_SSEC, B_SLEN, B_SLENSCAN, B_SCLOCK, B_SCIDX, B_SINFO, B_SOC, B_SOK, B_SRC, B_SRK, B_SPA, B_SPB, B_SPS, B_SPL,
   B_SCPOS, B_SCEND, B_SCELEM,
-  B_CLVALS, B_CLTMP, B_CLSTATE, B_CLBASE, B_CLSTART, B_CC,
+  B_CLVALS, B_CLTMP, B_CLSTATE, B_CLBASE, B_CLSTART, B_CC, B_CC64, B_SWIN,
   B_UOWN, B_UFLAG, B_UMIN, B_UCUT, B_UWPRE,
   B_GSTART, B_GCIDX, B_GSRC, B_GFLAGS, B_GORIG, B_GRORIG, B_GLINK, B_GOSEG, B_GKEY, B_GMAXC, B_GNEXT, B_GOUTID, B_GTMP, B_GTMP2,
   B_KHASH, B_KROOT, B_KWIN, B_KPAR, B_KFLAG, B_SPK,
@@ -171,7 +192,8 @@ struct ycrdt_engine {
   // result of the last merge (e->w.out / e->w.sv_out): ws_owner is the batch that produced it
   // (nullptr after any other call), so ycrdt_batch_result never returns another call's bytes
   const void* ws_owner = nullptr;
-  uint32_t out_bytes = 0, sv_bytes = 0;
+  uint64_t out_bytes = 0;
+  uint32_t sv_bytes = 0;
   uint32_t nsegs = 0, nlists = 0;  // segments / YArray lists of the last merge (the view reads them)
   ycrdt_merge_stats last{};
   Arena arena;                      // doc states (alloc_state / release_state)
@@ -216,7 +238,11 @@ struct ycrdt_doc {
 struct ycrdt_batch {
   ycrdt_engine* e = nullptr;
   DevBuf bytes, meta, pieces;
-  std::vector<uint32_t> uoff, ulen, ugroup;
+  std::vector<uint32_t> uoff, ulen, ugroup;  // uoff: within the update's window (yc_work.h WIN_SHIFT)
+  std::vector<uint32_t> uwin;   // window of every staged update
+  uint32_t nwin = 1;
+  uint32_t win_shift = WIN_SHIFT;
+  size_t uwin_off = 0;          // byte offset of uwin in `meta` (multi-window batches)
   std::vector<uint32_t> udoc;   // multi-document batch: document of every staged update
   uint32_t ndocs = 1;
   size_t udoc_off = 0;          // byte offset of udoc in `meta`
@@ -225,7 +251,7 @@ struct ycrdt_batch {
   uint32_t schunk = SCHUNK;     // chunk bytes of the large updates (layout)
   size_t ulist_off = 0;
   std::vector<Group> groups;
-  uint32_t nbytes = 0;
+  uint64_t nbytes = 0;          // span of the batch buffer (windows before the last are 2^32 bytes)
   uint64_t in_bytes = 0;
   bool merged = false;
 };
@@ -278,7 +304,7 @@ struct Src {
 // Lays out the sources (64-byte aligned, so every update owns its bitmap words; device sources
 // first, then the host ones in one contiguous region) + decode group table.
 void layout(ycrdt_batch* b, const std::vector<Src>& src, std::vector<uint32_t>& order) {
-  b->uoff.clear(); b->ulen.clear(); b->ugroup.clear(); b->groups.clear(); b->ulist.clear();
+  b->uoff.clear(); b->ulen.clear(); b->ugroup.clear(); b->groups.clear(); b->ulist.clear(); b->uwin.clear();
   b->in_bytes = 0;
   const char* mode = getenv("YCRDT_DECODE");
   const int force = mode && (!strcmp(mode, "chunks") || !strcmp(mode, "tables") || !strcmp(mode, "xtab")) ? 1
@@ -310,11 +336,20 @@ void layout(ycrdt_batch* b, const std::vector<Src>& src, std::vector<uint32_t>& 
   for (size_t i = 0; i < src.size(); ++i) if (src[i].dev) order.push_back((uint32_t)i);
   for (size_t i = 0; i < src.size(); ++i) if (!src[i].dev) order.push_back((uint32_t)i);
   std::vector<uint32_t> small;
-  size_t total = 0;
+  b->win_shift = WIN_SHIFT;
+  if (const char* ws = getenv("YCRDT_WIN_SHIFT")) {  // tests: small windows (every multi-window path on MBs)
+    const int v = atoi(ws);
+    if (v >= 20 && v <= 32) b->win_shift = (uint32_t)v;
+  }
+  const uint64_t wuse = win_use(b->win_shift);
+  uint64_t total = 0, win = 0;  // total: bytes used in window `win`
   for (const uint32_t i : order) {
-    const size_t off = total, len = src[i].len;
+    const size_t len = src[i].len, len64 = (len + 63) & ~size_t(63);
+    if (total && total + len64 > wuse) { ++win; total = 0; }  // an update never straddles windows
+    const uint64_t off = total;
     const uint32_t u = (uint32_t)b->uoff.size();
     b->uoff.push_back((uint32_t)off);
+    b->uwin.push_back((uint32_t)win);
     b->ulen.push_back((uint32_t)len);
     if (len && direct(len)) {
       b->ugroup.push_back(NONE);
@@ -332,31 +367,35 @@ void layout(ycrdt_batch* b, const std::vector<Src>& src, std::vector<uint32_t>& 
       }
     }
     b->in_bytes += len;
-    total += (len + 63) & ~size_t(63);
+    total += len64;
   }
   b->nbig = (uint32_t)b->ulist.size();
   b->ulist.insert(b->ulist.end(), small.begin(), small.end());
   b->uoff.push_back((uint32_t)total);
-  b->nbytes = (uint32_t)total;
+  b->nwin = (uint32_t)win + 1;
+  b->nbytes = (win << b->win_shift) + total;
 }
+// absolute byte offset of staged update u in the batch buffer
+uint64_t uabs(const ycrdt_batch* b, size_t u) { return ((uint64_t)b->uwin[u] << b->win_shift) + b->uoff[u]; }
 
 // Stages the sources into the batch buffer: the host region in one H2D copy, device sources by
 // one piece-copy launch. doc_of (one per source) makes it a multi-document batch.
 int stage_srcs(ycrdt_batch* b, const std::vector<Src>& src, const uint32_t* doc_of = nullptr, uint32_t ndocs = 1) {
   ycrdt_engine* e = b->e;
-  size_t total64 = 0;
-  for (const Src& x : src) total64 += ((x.len + 63) & ~size_t(63));
-  if (total64 >= 0xF0000000ull) return fail(YCRDT_E_CAPACITY, "batch larger than 3.75 GiB");
   std::vector<uint32_t> order;
   layout(b, src, order);
-  if (!grow(b->bytes, (size_t)b->nbytes + 128)) return fail(YCRDT_E_DEVICE, "hipMalloc failed (batch bytes)");
+  for (const Src& x : src)
+    if (((x.len + 63) & ~size_t(63)) > win_use(b->win_shift)) return fail(YCRDT_E_CAPACITY, "an update larger than 4 GiB");
+  if (b->nwin > 255) return fail(YCRDT_E_CAPACITY, "batch larger than 255 windows of 4 GiB");
+  if (!grow(b->bytes, (size_t)b->nbytes + 128)) return fail(YCRDT_E_DEVICE, oom("batch bytes"));
   const size_t nu = b->ulen.size();
   size_t ndev = 0;
   while (ndev < nu && src[order[ndev]].dev) ++ndev;
-  const size_t host0 = ndev < nu ? b->uoff[ndev] : b->nbytes;
-  e->pinned_stage.assign((size_t)b->nbytes - host0, 0);
+  // the host updates in one H2D copy of their span (window gaps included)
+  const uint64_t host0 = ndev < nu ? uabs(b, ndev) : b->nbytes;
+  e->pinned_stage.assign((size_t)(b->nbytes - host0), 0);
   for (size_t u = ndev; u < nu; ++u)
-    if (b->ulen[u]) memcpy(e->pinned_stage.data() + (b->uoff[u] - host0), src[order[u]].p, b->ulen[u]);
+    if (b->ulen[u]) memcpy(e->pinned_stage.data() + (uabs(b, u) - host0), src[order[u]].p, b->ulen[u]);
   if (!e->pinned_stage.empty())
     HIPCHK(hipMemcpyAsync((uint8_t*)b->bytes.p + host0, e->pinned_stage.data(), e->pinned_stage.size(), hipMemcpyHostToDevice, e->stream));
   if (ndev == 1) {
@@ -365,8 +404,8 @@ int stage_srcs(ycrdt_batch* b, const std::vector<Src>& src, const uint32_t* doc_
     std::vector<Piece> pc;
     pc.reserve(ndev);
     for (size_t u = 0; u < ndev; ++u)
-      if (b->ulen[u]) pc.push_back(Piece{src[order[u]].p, (uint8_t*)b->bytes.p + b->uoff[u], b->ulen[u], {0}});
-    if (!grow(b->pieces, sizeof(Piece) * (pc.size() + 1))) return fail(YCRDT_E_DEVICE, "hipMalloc failed (pieces)");
+      if (b->ulen[u]) pc.push_back(Piece{src[order[u]].p, (uint8_t*)b->bytes.p + uabs(b, u), b->ulen[u], {0}});
+    if (!grow(b->pieces, sizeof(Piece) * (pc.size() + 1))) return fail(YCRDT_E_DEVICE, oom("pieces"));
     HIPCHK(hipMemcpyAsync(b->pieces.p, pc.data(), sizeof(Piece) * pc.size(), hipMemcpyHostToDevice, e->stream));
     copy_pieces((const Piece*)b->pieces.p, (uint32_t)pc.size(), e->stream);
   }
@@ -381,8 +420,9 @@ int stage_srcs(ycrdt_batch* b, const std::vector<Src>& src, const uint32_t* doc_
     }
   }
   const size_t meta_bytes = sizeof(uint32_t) * (nu + 1 + nu + nu) + sizeof(Group) * b->groups.size() + 64 +
-                            sizeof(uint32_t) * b->udoc.size() + 16 + sizeof(uint32_t) * b->ulist.size() + 16;
-  if (!grow(b->meta, meta_bytes)) return fail(YCRDT_E_DEVICE, "hipMalloc failed (meta)");
+                            sizeof(uint32_t) * b->udoc.size() + 16 + sizeof(uint32_t) * b->ulist.size() + 16 +
+                            sizeof(uint32_t) * b->uwin.size() + 16;
+  if (!grow(b->meta, meta_bytes)) return fail(YCRDT_E_DEVICE, oom("meta"));
   std::vector<uint8_t> meta(meta_bytes, 0);
   size_t o = 0;
   memcpy(meta.data() + o, b->uoff.data(), sizeof(uint32_t) * (nu + 1)); o += sizeof(uint32_t) * (nu + 1);
@@ -398,6 +438,10 @@ int stage_srcs(ycrdt_batch* b, const std::vector<Src>& src, const uint32_t* doc_
   o = (o + 15) & ~size_t(15);
   b->ulist_off = o;
   if (!b->ulist.empty()) memcpy(meta.data() + o, b->ulist.data(), sizeof(uint32_t) * b->ulist.size());
+  o += sizeof(uint32_t) * b->ulist.size();
+  o = (o + 15) & ~size_t(15);
+  b->uwin_off = o;
+  if (!b->uwin.empty()) memcpy(meta.data() + o, b->uwin.data(), sizeof(uint32_t) * b->uwin.size());
   HIPCHK(hipMemcpyAsync(b->meta.p, meta.data(), meta_bytes, hipMemcpyHostToDevice, e->stream));
   HIPCHK(hipStreamSynchronize(e->stream));
   b->merged = false;
@@ -456,6 +500,9 @@ int run_decode(ycrdt_engine* e, ycrdt_batch* b, bool lazy, Decoded& D, bool gene
   const uint32_t nu = (uint32_t)b->ulen.size();
   w.bytes = (const uint8_t*)b->bytes.p;
   w.nbytes = b->nbytes;
+  w.nwin = b->nwin;
+  w.win_shift = b->win_shift;
+  w.uwin = b->nwin > 1 ? (const uint32_t*)((const uint8_t*)b->meta.p + b->uwin_off) : nullptr;
   w.nupd = nu;
   w.uoff = (const uint32_t*)b->meta.p;
   w.ulen = w.uoff + nu + 1;
@@ -482,7 +529,8 @@ int run_decode(ycrdt_engine* e, ycrdt_batch* b, bool lazy, Decoded& D, bool gene
   // The section table is sized from an estimate (a capacity overflow reruns the decode with the
   // worst-case bound); the struct table, the client table and the delete-set ranges are sized
   // after the count sync from the real counts, so the workspace follows the content, not B.
-  const uint64_t est_sec = generous ? B / 3 + 64 : std::min<uint64_t>(B / 3 + 64, (uint64_t)nu * 16 + B / 256 + 4096);
+  const uint64_t est_sec = std::min<uint64_t>(generous ? B / 3 + 64 : std::min<uint64_t>(B / 3 + 64, (uint64_t)nu * 16 + B / 256 + 4096),
+                                              0x7FFFFFFFull);
   w.cap_sections = (uint32_t)est_sec;
   w.cap_structs = 0;
   w.cap_ds = 0;
@@ -509,14 +557,14 @@ int run_decode(ycrdt_engine* e, ycrdt_batch* b, bool lazy, Decoded& D, bool gene
   w.scratch = take<uint32_t>(V, B_SCRATCH, std::max<uint64_t>({nwords + 2, (uint64_t)w.cap_sections + 66, (uint64_t)nu + 2}), ok);
   w.usec_start = take<uint32_t>(V, B_USEC, nu + 1, ok);
   w.usec_n = take<uint32_t>(V, B_USECN, nu + 1, ok);
-  if (!ok) return fail(YCRDT_E_DEVICE, "hipMalloc failed (decode workspace)");
+  if (!ok) return fail(YCRDT_E_DEVICE, oom("decode workspace"));
   // rocPRIM scratch sized for the largest scan of this batch (units may grow it later)
   {
     size_t tb = prim_tmp_bytes(std::max<uint64_t>(B, 1024));
     w.tmp = take<uint8_t>(V, B_TMP, tb, ok);
     w.tmp_bytes = V[B_TMP].cap;
   }
-  if (!ok) return fail(YCRDT_E_DEVICE, "hipMalloc failed (scan scratch)");
+  if (!ok) return fail(YCRDT_E_DEVICE, oom("scan scratch"));
   static_assert(sizeof(Counters) % 4 == 0, "counters are filled as words");
   fill_u32_multi({{(uint32_t*)w.ctr, sizeof(Counters) / 4, 0u},
                   {w.ufail, (uint64_t)nu + 1, 0u},
@@ -548,10 +596,11 @@ int run_decode(ycrdt_engine* e, ycrdt_batch* b, bool lazy, Decoded& D, bool gene
   w.cap_structs = nstructs + 64;
   w.cap_ds = c.ds_region + 64;
   w.cap_clients = nsections + 64;
-  w.ds = take<DsRange>(V, B_DS, w.cap_ds, ok);
+  w.ds = lazy ? take<DsRange>(V, B_DS, w.cap_ds, ok) : nullptr;  // dense ranges: mergeUpdates / diffUpdate only
   w.ds_tmp = take<DsRange>(V, B_DSTMP, w.cap_ds, ok);
-  w.ds_len = take<uint32_t>(V, B_DSLEN, w.cap_ds + 1, ok);
+  w.ds_len = nullptr;  // (no per-range length column: k_ds_apply clips in registers)
   w.s_pos = take<uint32_t>(V, B_SPOS, w.cap_structs, ok);
+  w.s_win = b->nwin > 1 ? take<uint8_t>(V, B_SWIN, w.cap_structs, ok) : nullptr;
   w.s_sec = take<uint32_t>(V, B_SSEC, w.cap_structs, ok);
   w.s_len = take<uint32_t>(V, B_SLEN, w.cap_structs + 1, ok);
   w.s_lenscan = take<uint64_t>(V, B_SLENSCAN, w.cap_structs + 1, ok);
@@ -582,7 +631,7 @@ int run_decode(ycrdt_engine* e, ycrdt_batch* b, bool lazy, Decoded& D, bool gene
   w.cl_state = take<uint32_t>(V, B_CLSTATE, w.cap_clients + 1, ok);
   w.cl_base = take<uint64_t>(V, B_CLBASE, w.cap_clients + 2, ok);
   w.cl_start = take<uint32_t>(V, B_CLSTART, w.cap_clients + 1, ok);
-  if (!ok) return fail(YCRDT_E_DEVICE, "hipMalloc failed (struct table)");
+  if (!ok) return fail(YCRDT_E_DEVICE, oom("struct table"));
   launch_struct_scatter(w, s);
   mark(e, "decode.sections");
   {  // the delete sets decode on the side stream (own scratch / scan space) while the client
@@ -592,7 +641,7 @@ int run_decode(ycrdt_engine* e, ycrdt_batch* b, bool lazy, Decoded& D, bool gene
     wd.scratch = take<uint32_t>(V, B_SCRATCH2, (uint64_t)w.nupd + 2, okd);
     wd.tmp = take<uint8_t>(V, B_TMP2, prim_tmp_bytes((uint64_t)w.nupd + 2), okd);
     wd.tmp_bytes = V[B_TMP2].cap;
-    if (!okd) return fail(YCRDT_E_DEVICE, "hipMalloc failed (delete-set scratch)");
+    if (!okd) return fail(YCRDT_E_DEVICE, oom("delete-set scratch"));
     launch_ds_decode(wd, e->side);
     HIPCHK(hipEventRecord(e->side_done, e->side));
   }
@@ -659,7 +708,7 @@ int run_merge(ycrdt_engine* e, ycrdt_batch* b, const std::unordered_map<uint32_t
   w.ncaps = 0;
   if (caps) {
     uint32_t* cb = take<uint32_t>(V, B_CAPS, 2 * caps->size() + 2, ok);
-    if (!ok) return fail(YCRDT_E_DEVICE, "hipMalloc failed (caps)");
+    if (!ok) return fail(YCRDT_E_DEVICE, oom("caps"));
     std::vector<uint32_t> h(2 * caps->size() + 2, 0);
     size_t i = 0;
     for (const auto& kv : *caps) { h[i] = kv.first; h[caps->size() + i] = kv.second; ++i; }
@@ -696,7 +745,7 @@ int run_merge(ycrdt_engine* e, ycrdt_batch* b, const std::unordered_map<uint32_t
     });
     for (uint32_t i = 0; i < nclients; ++i) h[nclients + h[i]] = i;
     uint32_t* eb = take<uint32_t>(V, B_EMIT, h.size(), ok);
-    if (!ok) return fail(YCRDT_E_DEVICE, "hipMalloc failed (client order)");
+    if (!ok) return fail(YCRDT_E_DEVICE, oom("client order"));
     HIPCHK(hipMemcpyAsync(eb, h.data(), sizeof(uint32_t) * h.size(), hipMemcpyHostToDevice, s));
     w.cl_emit = eb;
     w.cl_slot = eb + nclients;
@@ -731,32 +780,6 @@ int run_merge(ycrdt_engine* e, ycrdt_batch* b, const std::unordered_map<uint32_t
   w.g_outid = take<uint32_t>(V, B_GOUTID, U + 2, ok);
   w.g_tmp = take<uint32_t>(V, B_GTMP, U + 2, ok);
   w.g_tmp2 = take<uint32_t>(V, B_GTMP2, U + 2, ok);
-  w.g_right = take<uint32_t>(V, B_GRIGHT, U + 2, ok);
-  w.y_key = take<uint32_t>(V, B_YKEY, U + 2, ok);
-  w.y_keys = take<uint32_t>(V, B_YKEYS, U + 2, ok);
-  w.y_seg = take<uint32_t>(V, B_YSEG, U + 2, ok);
-  w.y_iota = take<uint32_t>(V, B_YIOTA, U + 2, ok);
-  w.y_lstart = take<uint32_t>(V, B_YLSTART, U + 2, ok);
-  w.y_state = take<uint32_t>(V, B_YSTATE, U + 2, ok);
-  w.y_before = take<uint32_t>(V, B_YBEFORE, U + 2, ok);
-  w.y_confl = take<uint32_t>(V, B_YCONFL, U + 2, ok);
-  w.y_stack = take<uint32_t>(V, B_YSTACK, U + 2, ok);
-  w.t_key = take<uint32_t>(V, B_TKEY, U + 2, ok);
-  w.t_keys = take<uint32_t>(V, B_TKEYS, U + 2, ok);
-  w.t_seg = take<uint32_t>(V, B_TSEG, U + 2, ok);
-  w.t_pos = take<uint32_t>(V, B_TPOS, U + 2, ok);
-  w.t_gstart = take<uint32_t>(V, B_TGSTART, U + 2, ok);
-  w.t_next = take<uint32_t>(V, B_TNEXT, U + 2, ok);
-  w.t_done = take<uint32_t>(V, B_TDONE, U + 2, ok);
-  w.t_first = take<uint32_t>(V, B_TFIRST, U + 2, ok);
-  w.t_nsib = take<uint32_t>(V, B_TNSIB, U + 2, ok);
-  w.t_jump = take<uint32_t>(V, B_TJUMP, U + 2, ok);
-  w.t_big = take<uint32_t>(V, B_TBIG, U + 2, ok);
-  w.t_prv = take<uint32_t>(V, B_TPRV, U + 2, ok);
-  w.t_mprv = take<uint32_t>(V, B_TMPRV, U + 2, ok);
-  w.t_mtail = take<uint32_t>(V, B_TMTAIL, U + 2, ok);
-  w.t_trep = take<uint32_t>(V, B_TTREP, U + 2, ok);
-  w.t_otail = take<uint32_t>(V, B_TOTAIL, U + 2, ok);
   w.o_first = take<uint32_t>(V, B_OFIRST, U + 2, ok);
   w.o_cidx = take<uint32_t>(V, B_OCIDX, U + 2, ok);
   w.o_size = take<uint32_t>(V, B_OSIZE, U + 2, ok);
@@ -766,12 +789,13 @@ int run_merge(ycrdt_engine* e, ycrdt_batch* b, const std::unordered_map<uint32_t
   w.r_size = take<uint32_t>(V, B_RSIZE, U + 2, ok);
   w.r_pos = take<uint32_t>(V, B_RPOS, U + 2, ok);
   w.cc = take<uint32_t>(V, B_CC, (size_t)CC_N * (w.cap_clients + 1), ok);
+  w.cc64 = take<uint64_t>(V, B_CC64, (size_t)CC64_N * (w.cap_clients + 1), ok);
   {
     size_t tb = prim_tmp_bytes(std::max<uint64_t>({B, U + 2, 1024}));
     w.tmp = take<uint8_t>(V, B_TMP, tb, ok);
     w.tmp_bytes = V[B_TMP].cap;
   }
-  if (!ok) return fail(YCRDT_E_DEVICE, "hipMalloc failed (unit workspace)");
+  if (!ok) return fail(YCRDT_E_DEVICE, oom("unit workspace"));
   // ---- K2..K5 units
   mark(e, "merge.units");
   // with no units, delete-set ranges still have to be checked: each one is pending (pendingDs)
@@ -793,7 +817,22 @@ int run_merge(ycrdt_engine* e, ycrdt_batch* b, const std::unordered_map<uint32_t
   w.k_winner = take<uint32_t>(V, B_KWIN, w.cap_keys, ok);
   w.k_parent = take<uint32_t>(V, B_KPAR, w.cap_keys, ok);
   w.k_flags = take<uint32_t>(V, B_KFLAG, w.cap_keys, ok);
-  if (!ok) return fail(YCRDT_E_DEVICE, "hipMalloc failed (key table)");
+  if (!ok) return fail(YCRDT_E_DEVICE, oom("key table"));
+  // the YArray arrays (yc_yata.hip, the view's list order) exist only for a merge with YArray
+  // members: a map-only merge (C2) never touches them, and at a billion units they would be
+  // a hundred gigabytes of HBM
+  auto alloc_lists = [&](uint64_t n) -> bool {
+    bool okl = true;
+    w.g_right = take<uint32_t>(V, B_GRIGHT, n + 2, okl);
+    uint32_t** cols[] = {&w.y_key, &w.y_keys, &w.y_seg, &w.y_iota, &w.y_lstart, &w.y_state, &w.y_before, &w.y_confl,
+                         &w.y_stack, &w.t_key, &w.t_keys, &w.t_seg, &w.t_pos, &w.t_gstart, &w.t_next, &w.t_done,
+                         &w.t_first, &w.t_nsib, &w.t_jump, &w.t_big, &w.t_prv, &w.t_mprv, &w.t_mtail, &w.t_trep, &w.t_otail};
+    const int ids[] = {B_YKEY, B_YKEYS, B_YSEG, B_YIOTA, B_YLSTART, B_YSTATE, B_YBEFORE, B_YCONFL, B_YSTACK,
+                       B_TKEY, B_TKEYS, B_TSEG, B_TPOS, B_TGSTART, B_TNEXT, B_TDONE, B_TFIRST, B_TNSIB, B_TJUMP,
+                       B_TBIG, B_TPRV, B_TMPRV, B_TMTAIL, B_TTREP, B_TOTAIL};
+    for (size_t k = 0; k < sizeof(ids) / sizeof(ids[0]); ++k) *cols[k] = take<uint32_t>(V, ids[k], n + 2, okl);
+    return okl;
+  };
   uint32_t nout = 0;
   e->nsegs = nsegs;
   e->nlists = 0;
@@ -807,6 +846,7 @@ int run_merge(ycrdt_engine* e, ycrdt_batch* b, const std::unordered_map<uint32_t
       HIPCHK(hipMemcpyAsync(&narray, &w.ctr->narray, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
       HIPCHK(hipStreamSynchronize(s));
     }
+    if (narray && !alloc_lists(nsegs)) return fail(YCRDT_E_DEVICE, oom("list workspace"));
     // the integrate phases: once, or once per key-hash shard (sh: C4 sharding, §6 of DESIGN.md)
     uint8_t* owner = nullptr;
     uint32_t *gflags0 = nullptr, *acc = nullptr;
@@ -816,7 +856,7 @@ int run_merge(ycrdt_engine* e, ycrdt_batch* b, const std::unordered_map<uint32_t
       owner = take<uint8_t>(V, B_SOWNER, (size_t)nsegs + 16, ok);
       gflags0 = take<uint32_t>(V, B_GFLAGS0, (size_t)nsegs + 1, ok);
       acc = take<uint32_t>(V, B_GFACC, (size_t)nsegs + 1, ok);
-      if (!ok) return fail(YCRDT_E_DEVICE, "hipMalloc failed (shards)");
+      if (!ok) return fail(YCRDT_E_DEVICE, oom("shards"));
       mark(e, "shard.owners");
       launch_key_shards(w, nsegs, sh->nshards, key_shard, owner, s);
       HIPCHK(hipMemcpyAsync(gflags0, w.g_flags, sizeof(uint32_t) * nsegs, hipMemcpyDeviceToDevice, s));
@@ -866,15 +906,25 @@ int run_merge(ycrdt_engine* e, ycrdt_batch* b, const std::unordered_map<uint32_t
   // origin, right origin, parent, length prefix) to content bytes sliced from the input, every
   // delete-set run at most 10, every client block / state-vector entry at most 15 + 10.
   if (!nsegs) HIPCHK(hipMemsetAsync(&w.ctr->nout, 0, sizeof(uint32_t), s));
-  w.cap_out = (uint64_t)b->nbytes + 48ull * nsegs + 32ull * nclients + 64;
+  w.cap_out = (uint64_t)b->in_bytes + 48ull * nsegs + 32ull * nclients + 64;
   w.cap_sv = 16ull + 10ull * nclients;
-  w.out = take<uint8_t>(V, B_OUT, (size_t)w.cap_out + 16, ok);
+  // up to 1 GiB of bound the output is allocated before the sizes are known; past it (a merge of
+  // billions of items: the bound is several times the input) after them, exactly (one more sync)
+  const bool exact_out = w.cap_out > (uint64_t(1) << 30);
+  if (!exact_out) w.out = take<uint8_t>(V, B_OUT, (size_t)w.cap_out + 16, ok);
   w.sv_out = take<uint8_t>(V, B_SVOUT, (size_t)w.cap_sv + 16, ok);
-  if (!ok) return fail(YCRDT_E_DEVICE, "hipMalloc failed (output)");
+  if (!ok) return fail(YCRDT_E_DEVICE, oom("output"));
   uint8_t* tmp2 = take<uint8_t>(V, B_TMP2, prim_tmp_bytes((uint64_t)nsegs + 2), ok);
-  if (!ok) return fail(YCRDT_E_DEVICE, "hipMalloc failed (scan space)");
+  if (!ok) return fail(YCRDT_E_DEVICE, oom("scan space"));
   mark(e, "encode.sizes");
   launch_encode_sizes(w, nsegs, nclients, s, e->side, e->side_fork, e->side_done, tmp2, V[B_TMP2].cap);
+  if (exact_out) {
+    rc = check(e, c, "encode sizes");
+    if (rc) return rc;
+    w.cap_out = c.out_total;
+    w.out = take<uint8_t>(V, B_OUT, (size_t)w.cap_out + 16, ok);
+    if (!ok) return fail(YCRDT_E_DEVICE, oom("output"));
+  }
   mark(e, "encode.write");
   launch_encode_write(w, nsegs, nclients, s);
   mark(e, "end");
@@ -882,7 +932,7 @@ int run_merge(ycrdt_engine* e, ycrdt_batch* b, const std::unordered_map<uint32_t
   rc = check(e, c, "merge / encode");
   if (rc) return rc;
   nout = nsegs ? c.nout : 0;
-  e->out_bytes = c.out_bytes;
+  e->out_bytes = c.out_total;
   e->sv_bytes = c.sv_bytes;
   float ms = 0;
   hipEventElapsedTime(&ms, e->ev0, e->ev1);
@@ -893,7 +943,7 @@ int run_merge(ycrdt_engine* e, ycrdt_batch* b, const std::unordered_map<uint32_t
   st.units = U;
   st.segments = nsegs;
   st.out_structs = nout;
-  st.out_bytes = c.out_bytes;
+  st.out_bytes = c.out_total;
   st.clients = nclients;
   st.device_ms = ms;
   if (e->profiling) {
@@ -909,6 +959,7 @@ int run_merge(ycrdt_engine* e, ycrdt_batch* b, const std::unordered_map<uint32_t
 // K8: materialised view of the doc state just merged into the engine's workspace (yc_view.hip),
 // copied to the host with the state bytes its byte ranges point into.
 int run_view(ycrdt_engine* e, ycrdt_batch* b, HostView& hv) {
+  if (b->nwin > 1) return fail(YCRDT_E_CAPACITY, "a view of a batch over 4 GiB");
   Work& w = e->w;
   auto& V = e->bufs;
   bool ok = true;
@@ -932,7 +983,7 @@ int run_view(ycrdt_engine* e, ycrdt_batch* b, HostView& hv) {
   vb.n1 = take<uint32_t>(V, B_VN1, (size_t)narr + 1, ok);
   vb.order = take<uint32_t>(V, B_VORDER, (size_t)narr + 1, ok);
   vb.segs = take<ViewSeg>(V, B_VSEGS, (size_t)narr + 1, ok);
-  if (!ok) return fail(YCRDT_E_DEVICE, "hipMalloc failed (view)");
+  if (!ok) return fail(YCRDT_E_DEVICE, oom("view"));
   hv.keys.clear();
   hv.segs.clear();
   hv.bytes.assign(b->nbytes, 0);
@@ -1037,6 +1088,7 @@ int split_multi(ycrdt_engine* e, const Decoded& D, uint32_t nr, uint32_t sbytes,
 int run_lazy(ycrdt_engine* e, ycrdt_batch* b, bool merge, const std::vector<std::pair<uint32_t, uint32_t>>& sv,
              ycrdt_out* out, const std::vector<uint32_t>* sv_off = nullptr,
              ycrdt_out* multi = nullptr) {
+  if (b->nwin > 1) return fail(YCRDT_E_CAPACITY, "mergeUpdates / diffUpdate of more than 4 GiB");
   Work& w = e->w;
   w.lz_multi = 0;
   w.capped = 0;
@@ -1098,7 +1150,7 @@ int run_lazy(ycrdt_engine* e, ycrdt_batch* b, bool merge, const std::vector<std:
   }
   const size_t nsvo = sv_off ? sv_off->size() : 0;
   uint32_t* svbuf = take<uint32_t>(V, B_SVC, 2 * sv.size() + nsvo + 2, ok);
-  if (!ok) return fail(YCRDT_E_DEVICE, "hipMalloc failed (lazy merge workspace)");
+  if (!ok) return fail(YCRDT_E_DEVICE, oom("lazy merge workspace"));
   if (merge) {
     mark(e, "lazy.merge");
     if (D.nsections) launch_lazy_merge(w, D.nsections, D.nclients, s);
@@ -1135,7 +1187,7 @@ int run_lazy(ycrdt_engine* e, ycrdt_batch* b, bool merge, const std::vector<std:
   const uint32_t sbytes = vu_size_host(c.pad[0]) + blk_total;
   const uint32_t total = sbytes + dsbytes;
   w.out = take<uint8_t>(V, B_OUT, (size_t)total + 16, ok);
-  if (!ok) return fail(YCRDT_E_DEVICE, "hipMalloc failed (output)");
+  if (!ok) return fail(YCRDT_E_DEVICE, oom("output"));
   mark(e, "lazy.write");
   if (w.lz_nblk) launch_lazy_write(w, nslots, nr, sbytes, s);
   else {
@@ -1171,24 +1223,27 @@ int split_docs(ycrdt_engine* e, uint32_t ndocs, ycrdt_out* outs, ycrdt_out* svs)
   Work& w = e->w;
   const uint32_t nc = (uint32_t)e->last.clients;
   const size_t stride = (size_t)w.cap_clients + 1;
-  std::vector<uint32_t> doc(nc), blk(nc), blkpos(nc), nincl(nc), dsblk(nc), dspos(nc), nruns(nc), sv(nc), svpos(nc);
+  std::vector<uint32_t> doc(nc), blk(nc), nincl(nc), dsblk(nc), nruns(nc), sv(nc);
+  std::vector<uint64_t> blkpos(nc), dspos(nc), svpos(nc);
   std::vector<uint8_t> all(e->out_bytes), svall(e->sv_bytes);
   Counters c;
   hipStream_t s = e->stream;
   HIPCHK(hipMemcpyAsync(&c, w.ctr, sizeof(Counters), hipMemcpyDeviceToHost, s));
   if (nc) {
     HIPCHK(hipMemcpyAsync(doc.data(), w.cl_doc, sizeof(uint32_t) * nc, hipMemcpyDeviceToHost, s));
-    const std::pair<uint32_t, std::vector<uint32_t>*> cols[] = {{CC_BLK, &blk}, {CC_BLKPOS, &blkpos}, {CC_NINCL, &nincl},
-                                                                 {CC_DSBLK, &dsblk}, {CC_DSPOS, &dspos}, {CC_NRUNS, &nruns},
-                                                                 {CC_SV, &sv}, {CC_SVPOS, &svpos}};
+    const std::pair<uint32_t, std::vector<uint32_t>*> cols[] = {{CC_BLK, &blk}, {CC_NINCL, &nincl}, {CC_DSBLK, &dsblk},
+                                                                 {CC_NRUNS, &nruns}, {CC_SV, &sv}};
     for (const auto& col : cols)
       HIPCHK(hipMemcpyAsync(col.second->data(), w.cc + col.first * stride, sizeof(uint32_t) * nc, hipMemcpyDeviceToHost, s));
+    const std::pair<uint32_t, std::vector<uint64_t>*> cols64[] = {{CC64_BLKPOS, &blkpos}, {CC64_DSPOS, &dspos}, {CC64_SVPOS, &svpos}};
+    for (const auto& col : cols64)
+      HIPCHK(hipMemcpyAsync(col.second->data(), w.cc64 + col.first * stride, sizeof(uint64_t) * nc, hipMemcpyDeviceToHost, s));
   }
   if (!all.empty()) HIPCHK(hipMemcpyAsync(all.data(), w.out, all.size(), hipMemcpyDeviceToHost, s));
   if (!svall.empty()) HIPCHK(hipMemcpyAsync(svall.data(), w.sv_out, svall.size(), hipMemcpyDeviceToHost, s));
   HIPCHK(hipStreamSynchronize(s));
-  const uint32_t sbase = c.pad[3], dsbase = c.pad[4] + vu_size_host(c.pad[1]), svbase = vu_size_host(c.pad[2]);
-  struct Rng { uint32_t lo = 0xFFFFFFFFu, hi = 0, n = 0; void add(uint32_t a, uint32_t len, bool in) { if (!in) return; lo = std::min(lo, a); hi = std::max(hi, a + len); ++n; } };
+  const uint64_t sbase = c.pad[3], dsbase = c.ds_base + vu_size_host(c.pad[1]), svbase = vu_size_host(c.pad[2]);
+  struct Rng { uint64_t lo = ~0ull, hi = 0; uint32_t n = 0; void add(uint64_t a, uint32_t len, bool in) { if (!in) return; lo = std::min(lo, a); hi = std::max(hi, a + len); ++n; } };
   std::vector<Rng> rs(ndocs), rd(ndocs), rv(ndocs);
   for (uint32_t i = 0; i < nc; ++i) {
     const uint32_t d = doc[i];
@@ -1308,6 +1363,16 @@ int ycrdt_engine_phase_times(ycrdt_engine* e, const char** names, double* ms, in
   return n;
 }
 
+int ycrdt_engine_device_bytes(ycrdt_engine* e, uint64_t* bytes) {
+  if (!e || !bytes) return fail(YCRDT_E_ARG, "null arg");
+  uint64_t n = 0;
+  for (const auto& b : e->bufs) n += b.cap;
+  n += (uint64_t)e->arena.slabs.size() * Arena::SLAB;
+  if (e->scratch) n += e->scratch->bytes.cap + e->scratch->meta.cap + e->scratch->pieces.cap;
+  *bytes = n;
+  return YCRDT_OK;
+}
+
 int ycrdt_doc_create(ycrdt_engine* e, uint32_t client_id, ycrdt_doc** out) {
   if (!e || !out) return fail(YCRDT_E_ARG, "null arg");
   auto* d = new ycrdt_doc();
@@ -1345,7 +1410,7 @@ int commit_merge(ycrdt_doc* d, const std::vector<ycrdt_buf>& extra, const ClockM
   // source of this merge any more: the batch holds a copy); the doc changes only once it is there
   DevBuf nb = d->state;
   const bool fresh = e->out_bytes + 16 > d->state.cap;
-  if (fresh && !alloc_state(e, nb, e->out_bytes + 16)) return fail(YCRDT_E_DEVICE, "hipMalloc failed (doc state)");
+  if (fresh && !alloc_state(e, nb, e->out_bytes + 16)) return fail(YCRDT_E_DEVICE, oom("doc state"));
   std::vector<uint8_t> sv(e->sv_bytes);
   hipError_t er = hipMemcpyAsync(nb.p, e->w.out, e->out_bytes, hipMemcpyDeviceToDevice, e->stream);
   if (er == hipSuccess && !sv.empty()) er = hipMemcpyAsync(sv.data(), e->w.sv_out, e->sv_bytes, hipMemcpyDeviceToHost, e->stream);
@@ -1466,19 +1531,19 @@ int flush_multi(ycrdt_engine* e, const std::vector<ycrdt_doc*>& docs) {
   Work& w = e->w;
   auto& V = e->bufs;
   bool ok = true;
-  uint32_t* rng = take<uint32_t>(V, B_DOCRNG, 9 * (size_t)nd + 9, ok);
-  if (!ok) return fail(YCRDT_E_DEVICE, "hipMalloc failed (document ranges)");
+  unsigned long long* rng = take<unsigned long long>(V, B_DOCRNG, 9 * (size_t)nd + 9, ok);
+  if (!ok) return fail(YCRDT_E_DEVICE, oom("document ranges"));
   hipStream_t s = e->stream;
   launch_doc_ranges(w, (uint32_t)e->last.clients, nd, rng, s);
-  std::vector<uint32_t> r(9 * (size_t)nd);
+  std::vector<unsigned long long> r(9 * (size_t)nd);
   std::vector<uint8_t> svall(e->sv_bytes);
   Counters c;
-  HIPCHK(hipMemcpyAsync(r.data(), rng, sizeof(uint32_t) * r.size(), hipMemcpyDeviceToHost, s));
+  HIPCHK(hipMemcpyAsync(r.data(), rng, sizeof(unsigned long long) * r.size(), hipMemcpyDeviceToHost, s));
   if (!svall.empty()) HIPCHK(hipMemcpyAsync(svall.data(), w.sv_out, svall.size(), hipMemcpyDeviceToHost, s));
   HIPCHK(hipMemcpyAsync(&c, w.ctr, sizeof(Counters), hipMemcpyDeviceToHost, s));
   HIPCHK(hipStreamSynchronize(s));
   if (c.err) return map_err(c.err, "document split");
-  const uint32_t sbase = c.pad[3], dsbase = c.pad[4] + vu_size_host(c.pad[1]), svbase = vu_size_host(c.pad[2]);
+  const uint64_t sbase = c.pad[3], dsbase = c.ds_base + vu_size_host(c.pad[1]), svbase = vu_size_host(c.pad[2]);
   std::vector<Piece> pc;
   pc.reserve(4 * (size_t)nd);
   std::vector<size_t> len(nd);
@@ -1495,29 +1560,29 @@ int flush_multi(ycrdt_engine* e, const std::vector<ycrdt_doc*>& docs) {
     P.inl[P.len++] = (uint8_t)v;
   };
   for (uint32_t j = 0; j < nd; ++j) {
-    const uint32_t* x = &r[9 * (size_t)j];
-    const uint32_t ns = x[2] ? x[1] - x[0] : 0, ndb = x[5] ? x[4] - x[3] : 0;
-    len[j] = vu_size_host(x[2]) + ns + vu_size_host(x[5]) + ndb;
+    const unsigned long long* x = &r[9 * (size_t)j];
+    const uint32_t ns = x[2] ? (uint32_t)(x[1] - x[0]) : 0, ndb = x[5] ? (uint32_t)(x[4] - x[3]) : 0;
+    len[j] = vu_size_host((uint32_t)x[2]) + ns + vu_size_host((uint32_t)x[5]) + ndb;
     ycrdt_doc* d = fast[j];
     // the batch holds a copy of every document's old state, so a block that fits is rewritten
     // in place (untouched until the copy below), a bigger one is allocated beside the old
     nblk[j] = d->state;
     if (len[j] + 16 > d->state.cap) {
-      if (!alloc_state(e, nblk[j], len[j] + 16)) { drop_fresh(); return fail(YCRDT_E_DEVICE, "hipMalloc failed (doc state)"); }
+      if (!alloc_state(e, nblk[j], len[j] + 16)) { drop_fresh(); return fail(YCRDT_E_DEVICE, oom("doc state")); }
       fresh[j] = 1;
     }
     uint8_t* dst = (uint8_t*)nblk[j].p;
     Piece P{};
-    hdr(P, x[2]); P.dst = dst; dst += P.len; pc.push_back(P);
+    hdr(P, (uint32_t)x[2]); P.dst = dst; dst += P.len; pc.push_back(P);
     if (ns) { pc.push_back(Piece{w.out + sbase + x[0], dst, ns, {0}}); dst += ns; }
-    hdr(P, x[5]); P.dst = dst; dst += P.len; pc.push_back(P);
+    hdr(P, (uint32_t)x[5]); P.dst = dst; dst += P.len; pc.push_back(P);
     if (ndb) pc.push_back(Piece{w.out + dsbase + x[3], dst, ndb, {0}});
     // state vector: its entries (host copy of the encode's state vector section)
     std::vector<uint8_t>& sv = nsv[j];
-    put_vu(sv, x[8]);
+    put_vu(sv, (uint32_t)x[8]);
     if (x[8]) sv.insert(sv.end(), svall.begin() + svbase + x[6], svall.begin() + svbase + x[7]);
   }
-  if (!grow(b.pieces, sizeof(Piece) * (pc.size() + 1))) { drop_fresh(); return fail(YCRDT_E_DEVICE, "hipMalloc failed (pieces)"); }
+  if (!grow(b.pieces, sizeof(Piece) * (pc.size() + 1))) { drop_fresh(); return fail(YCRDT_E_DEVICE, oom("pieces")); }
   hipError_t er = hipMemcpyAsync(b.pieces.p, pc.data(), sizeof(Piece) * pc.size(), hipMemcpyHostToDevice, s);
   if (er == hipSuccess) { copy_pieces((const Piece*)b.pieces.p, (uint32_t)pc.size(), s); er = hipStreamSynchronize(s); }
   if (er != hipSuccess) {

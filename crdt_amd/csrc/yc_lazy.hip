@@ -347,7 +347,7 @@ __global__ __launch_bounds__(256) void k_ev_write(Work w, uint32_t nslots) {
 }
 __global__ void k_blk_write(Work w, uint32_t nblk) {
   const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
-  if (b == 0 && !w.lz_multi) wr_vu(w.out, 0, w.ctr->pad[0]);
+  if (b == 0 && !w.lz_multi) wr_vu(w.out, 0u, w.ctr->pad[0]);
   if (b >= nblk) return;
   const uint32_t n = w.lz_evn[b];
   if (!n) return;

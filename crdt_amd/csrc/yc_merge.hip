@@ -267,7 +267,7 @@ __global__ __launch_bounds__(256) void k_seg_props(Work w, uint32_t nsegs) {
     uint32_t parent = NONE;
     if (pk == 1) {
       if (w.udoc) h = fnv_u32(h ^ 0x3Cu, w.cl_doc[cidx]);  // root types are per document
-      h = fnv_bytes(h, w.bytes + w.s_pa[own], w.s_pb[own]);
+      h = fnv_bytes(h, struct_bytes(w, own) + w.s_pa[own], w.s_pb[own]);
     } else if (pk == 2) {
       const uint32_t pc = w.s_pa[own], pclock = w.s_pb[own];
       if (pc == NONE || pc == UNKNOWN || pclock >= w.cl_state[pc]) { raise_err(&w.ctr->err, ERR_PENDING); gc = true; }
@@ -282,7 +282,7 @@ __global__ __launch_bounds__(256) void k_seg_props(Work w, uint32_t nsegs) {
     }
     if (!gc) {
       const uint32_t ps = w.s_psub[own];
-      if (ps != NONE) { h = fnv_u32(h, 0x5Au); h = fnv_bytes(h, w.bytes + ps, w.s_psublen[own]); }
+      if (ps != NONE) { h = fnv_u32(h, 0x5Au); h = fnv_bytes(h, struct_bytes(w, own) + ps, w.s_psublen[own]); }
       if (h == 0) h = 1;
       key = key_insert(w.k_hash, w.cap_keys, h);
       if (key == NONE) raise_err(&w.ctr->err, ERR_CAPACITY);

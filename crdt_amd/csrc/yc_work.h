@@ -24,7 +24,7 @@ struct Counters {            // device-side counters, read back at the few host 
   uint32_t nsegs;            // NS
   uint32_t nout;             // NO
   uint32_t changed;          // pointer-jumping convergence flag
-  uint32_t out_bytes;        // encoded output size
+  uint32_t out_bytes;        // encoded output size (mergeUpdates / diffUpdate)
   uint32_t sv_bytes;         // encoded state-vector size
   uint32_t nkeys;            // distinct map keys
   uint32_t nruns;            // delete-set runs in the output
@@ -37,6 +37,8 @@ struct Counters {            // device-side counters, read back at the few host 
   uint32_t nroots_sh[NSHARD]; // items with an explicit parent, sharded by workgroup (summed on the host)
   uint32_t nroots;           // items with an explicit parent (bound on the distinct lists: key table size)
   uint32_t pad[12];          // encode scratch (see yc_encode.hip)
+  unsigned long long out_total; // encoded output size (integrate encoder; 64-bit)
+  unsigned long long ds_base;   // integrate encoder: byte position of the delete-set section
   unsigned long long items;  // Σ clock lengths of Skip structs (items = Σ all lengths − this)
   unsigned long long units;  // U = cl_base[NC] (copied on the device before a counter read)
   unsigned long long in_len; // Σ input clock lengths = s_lenscan[S] (same)
@@ -49,11 +51,28 @@ struct DsRange {             // one decoded (client, clock, len) delete-set rang
   uint32_t upd;
 };
 
+// Batches larger than 4 GiB are laid out in WINDOWS of 2^32 bytes: window k holds the bytes
+// [k << 32, (k + 1) << 32) of the batch buffer, an update never straddles two windows, and every
+// byte position a kernel handles (struct / content / section positions, chunk bounds) is a u32
+// relative to its window. A kernel working on one update rebases its byte and bitmap pointers to
+// the update's window once (win_bytes / win_words) and keeps the 32-bit arithmetic; a kernel that
+// reaches a struct's bytes by struct index takes the window from s_win (struct_bytes).
+// (The window size is 2^win_shift with win_shift = 32; tests shrink it through YCRDT_WIN_SHIFT to
+// run every multi-window path on a few megabytes.)
+constexpr uint32_t WIN_SHIFT = 32;
+// bytes of a window updates may fill: the rest is slack for the parsers' reads past an update end
+__host__ __device__ inline uint64_t win_use(uint32_t shift) {
+  return (1ull << shift) - (shift >= 28 ? (1ull << 20) : (1ull << 12));
+}
+
 struct Work {
   // ---- batch input
-  const uint8_t* bytes = nullptr;  // B bytes, every update starts at a 64-byte aligned offset
-  uint32_t nbytes = 0;
-  const uint32_t* uoff = nullptr;  // [nupd+1] update start offsets (aligned)
+  const uint8_t* bytes = nullptr;  // every update starts at a 64-byte aligned offset of its window
+  uint64_t nbytes = 0;             // span of the batch buffer (windows before the last are 2^32 each)
+  uint32_t nwin = 1;               // windows of the batch (1: every position is absolute)
+  uint32_t win_shift = WIN_SHIFT;  // window size 2^win_shift
+  const uint32_t* uwin = nullptr;  // [nupd] window of every update (nullptr: one window)
+  const uint32_t* uoff = nullptr;  // [nupd+1] update start offsets within their windows (aligned)
   const uint32_t* ulen = nullptr;  // [nupd] real update lengths
   const uint32_t* ugroup = nullptr;// [nupd] first decode chunk of each large update
   uint32_t nupd = 0;
@@ -95,7 +114,8 @@ struct Work {
   uint64_t* ds_scan = nullptr;     // [cap_ds+1]
   uint32_t* dsclient_vals = nullptr; // [cap_dsclients] (client values seen in delete sets)
   // ---- per struct (S)
-  uint32_t* s_pos = nullptr;
+  uint32_t* s_pos = nullptr;       // first byte (within the struct's window)
+  uint8_t* s_win = nullptr;        // window of the struct's bytes (written only when nwin > 1)
   uint32_t* s_sec = nullptr;       // index into sections
   uint32_t* s_len = nullptr;
   uint64_t* s_lenscan = nullptr;   // [S+1] exclusive prefix of s_len
@@ -248,6 +268,7 @@ struct Work {
   uint32_t* r_size = nullptr;      // [runs+1] encoded size of (clock,len)
   uint32_t* r_pos = nullptr;       // [runs+1]
   uint32_t* cc = nullptr;          // per-client scratch: CC_N arrays of (cap_clients+1)
+  uint64_t* cc64 = nullptr;        // per-client byte positions (64-bit): CC64_N arrays of (cap_clients+1)
   // compat 135: delete-set / state-vector client order = the doc store's insertion order.
   // cl_emit[slot] = client table index written at that slot, cl_slot = its inverse (null: desc)
   const uint32_t* cl_emit = nullptr;
@@ -291,6 +312,14 @@ __device__ __forceinline__ uint32_t find_client(const Work& w, uint32_t nclients
   return (lo < nclients && w.cl_key[lo] == key) ? lo : NONE;
 }
 __device__ __forceinline__ uint32_t doc_of_update(const Work& w, uint32_t upd) { return w.udoc ? w.udoc[upd] : 0u; }
+// ---- windows (see WIN_SHIFT): the byte and bitmap bases of window k
+__device__ __forceinline__ uint32_t upd_win(const Work& w, uint32_t upd) { return w.uwin ? w.uwin[upd] : 0u; }
+__device__ __forceinline__ const uint8_t* win_bytes(const Work& w, uint32_t win) { return w.bytes + ((uint64_t)win << w.win_shift); }
+#define win_words(bits, win) ((bits) + ((uint64_t)(win) << (w.win_shift - 6)))  // (w: the kernel's Work)
+// the bytes of struct s's window (one window: no load)
+__device__ __forceinline__ const uint8_t* struct_bytes(const Work& w, uint32_t s) {
+  return w.nwin > 1 ? win_bytes(w, w.s_win[s]) : w.bytes;
+}
 
 // Byte range of content elements [e0, e1) of struct `src` (ContentAny: lib0 `any` values,
 // ContentJSON: varStrings, ContentString: UTF-16 code units of the UTF-8 text; every other
@@ -309,7 +338,7 @@ __device__ __forceinline__ bool content_slice(const Work& w, uint32_t src, uint3
     b1 = w.s_cend[src];
     return true;
   }
-  const uint64_t r = content_slice_walk(w.bytes, ref, w.s_celem[src], w.s_cpos[src], w.s_cend[src], e0, e1);
+  const uint64_t r = content_slice_walk(struct_bytes(w, src), ref, w.s_celem[src], w.s_cpos[src], w.s_cend[src], e0, e1);
   if (r == ~0ull) return false;
   b0 = (uint32_t)r;
   b1 = (uint32_t)(r >> 32);
@@ -369,6 +398,10 @@ enum : uint32_t {
   CC_FIRST_OUT = 0, CC_FIRST_INCL, CC_NINCL, CC_HDR, CC_BLK, CC_BLKPOS, CC_NRUNS, CC_FIRST_RUN,
   CC_DSBLK, CC_DSPOS, CC_SV, CC_SVPOS, CC_REV, CC_REVSCAN, CC_RUN_LO, CC_REV2, CC_REVSCAN2, CC_REV3, CC_REVSCAN3, CC_N
 };
+
+// 64-bit per-client columns inside Work::cc64: the block positions of the struct, delete-set and
+// state-vector sections, and the scans they come from
+enum : uint32_t { CC64_BLKPOS = 0, CC64_DSPOS, CC64_SVPOS, CC64_SCAN, CC64_SCAN2, CC64_SCAN3, CC64_N };
 
 // segment flags
 enum : uint32_t {
@@ -462,7 +495,7 @@ struct Piece {
 };
 void copy_pieces(const Piece* pieces, uint32_t n, hipStream_t s);
 // per-document (lo, hi, n) of the struct / delete-set / state-vector sections of a multi-document encode
-void launch_doc_ranges(const Work& w, uint32_t nclients, uint32_t ndocs, uint32_t* rng, hipStream_t s);
+void launch_doc_ranges(const Work& w, uint32_t nclients, uint32_t ndocs, unsigned long long* rng, hipStream_t s);
 // batched u32 fills (n in 32-bit words)
 struct FillDesc { uint32_t* p; uint64_t n; uint32_t v; };
 constexpr uint32_t FILL_MAX = 8;

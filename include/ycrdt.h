@@ -64,6 +64,8 @@ void ycrdt_engine_destroy(ycrdt_engine *e);
 int ycrdt_engine_set_profiling(ycrdt_engine *e, int on);
 /* fills up to `cap` (name, milliseconds) pairs of the last merge; returns the count */
 int ycrdt_engine_phase_times(ycrdt_engine *e, const char **names, double *ms, int cap);
+/* HBM the engine holds: its grow-only merge workspace, the doc-state arena and the staging batch */
+int ycrdt_engine_device_bytes(ycrdt_engine *e, uint64_t *bytes);
 
 /* ---- Y.Doc ------------------------------------------------------------------------------- */
 /* new Y.Doc()  (crdt.js:33,54,56,80,221) */
