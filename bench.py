@@ -717,10 +717,7 @@ def main():
     for _ in range(e2e_steps):
         b2 = crdt_amd.Batch(docs=docs, engine=eng) if ndocs > 1 else crdt_amd.Batch(updates, eng)
         b2.merge()
-        if ndocs > 1:
-            b2.result_docs()
-        else:
-            b2.result()
+        b2.result_docs_packed()  # every document's update + state vector, split on the device
         del b2
     e2e_ms = (time.perf_counter() - e0) * 1e3 / max(1, e2e_steps)
     del batch
@@ -782,8 +779,10 @@ def main():
         "device_ms_per_step": round(dev_ms / args.steps, 4),
         "unique_items_per_step_per_gpu": st.units,
         "end_to_end": {"ms_per_step": round(e2e_ms, 3), "items_per_s": round(steps_items / (e2e_ms * 1e-3), 1),
-                       "includes": "host pack + H2D + merge + D2H of every document's update and state vector "
-                                   "(split per document on the host), 1 GPU"} if e2e_steps else None,
+                       "x_device": round(e2e_ms / (dev_ms / args.steps), 2) if dev_ms else None,
+                       "includes": "host buffers in (no-copy ycrdt_buf packing, pinned pipelined H2D) + merge + "
+                                   "per-document split in HBM + pipelined D2H of every document's update and state "
+                                   "vector into one host array (ycrdt_batch_result_docs_packed), 1 GPU"} if e2e_steps else None,
         "pipeline_roofline": {
             "b_alg_bytes": b_alg,
             "achieved_GBs": round(b_alg / (ms_per_step * 1e-3) / 1e9, 2),

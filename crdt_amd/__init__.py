@@ -84,13 +84,21 @@ EXPORTS = (
     "ycrdt_doc_json", "ycrdt_map_set", "ycrdt_map_set_type", "ycrdt_map_delete", "ycrdt_array_insert",
     "ycrdt_array_delete", "ycrdt_doc_client_id", "ycrdt_map_type_at", "ycrdt_doc_take_local_update",
     "ycrdt_doc_flush", "ycrdt_doc_pending", "ycrdt_doc_track_local", "ycrdt_validate_update", "ycrdt_debug_replay",
-    "ycrdt_batch_stage_docs", "ycrdt_batch_result_docs", "ycrdt_merge_docs",
+    "ycrdt_batch_stage_docs", "ycrdt_batch_result_docs", "ycrdt_batch_result_docs_packed", "ycrdt_merge_docs",
     "ycrdt_map_get", "ycrdt_map_size", "ycrdt_array_length", "ycrdt_array_get", "ycrdt_apply_updates_multi",
     "ycrdt_comm_unique_id", "ycrdt_comm_create", "ycrdt_comm_destroy", "ycrdt_batch_merge_sharded",
-    "ycrdt_comm_sv_allreduce_max", "ycrdt_comm_ds_allgather",
+    "ycrdt_comm_sv_allreduce_max", "ycrdt_comm_ds_allgather", "ycrdt_comm_create_exchange", "ycrdt_route",
+    "ycrdt_comm_fleet_sv_allreduce_max",
 )
 
 MERGE_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p)
+ALLREDUCE_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint32), ctypes.c_size_t, ctypes.c_int)
+ALLGATHER_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint8), ctypes.c_size_t,
+                                ctypes.POINTER(ctypes.c_uint8))
+
+
+class _Exchange(ctypes.Structure):
+    _fields_ = [("ctx", ctypes.c_void_p), ("allreduce_u32", ALLREDUCE_FN), ("allgather", ALLGATHER_FN)]
 
 
 def lib():
@@ -130,6 +138,7 @@ def lib():
     L.ycrdt_validate_update.argtypes = [_Buf, P(i32)]
     L.ycrdt_batch_stage_docs.argtypes = [vp, P(_Buf), P(u32), sz, u32, P(vp)]
     L.ycrdt_batch_result_docs.argtypes = [vp, P(_Out), P(_Out)]
+    L.ycrdt_batch_result_docs_packed.argtypes = [vp, vp, ctypes.c_uint64, P(ctypes.c_uint64), P(ctypes.c_uint64)]
     L.ycrdt_merge_docs.argtypes = [vp, P(_Buf), P(u32), sz, u32, P(_Out), P(_Out)]
     L.ycrdt_debug_replay.argtypes = [P(_Buf), sz, MERGE_FN, vp, P(_Out), P(_Out), P(_Out)]
     L.ycrdt_free.argtypes = [P(_Out)]
@@ -150,6 +159,10 @@ def lib():
     L.ycrdt_batch_merge_sharded.argtypes = [vp, vp, u32, P(MergeStats)]
     L.ycrdt_comm_sv_allreduce_max.argtypes = [vp, vp, _Buf, P(_Out)]
     L.ycrdt_comm_ds_allgather.argtypes = [vp, vp, _Buf, P(_Out)]
+    L.ycrdt_comm_create_exchange.argtypes = [vp, i32, i32, P(_Exchange), P(vp)]
+    L.ycrdt_route.argtypes = [ctypes.c_char_p, sz, u32]
+    L.ycrdt_route.restype = u32
+    L.ycrdt_comm_fleet_sv_allreduce_max.argtypes = [vp, vp, P(u32), P(_Buf), sz, P(_Out), P(_Out), P(_Out)]
     L.ycrdt_map_size.argtypes = [vp, cs, cs, P(u32)]
     L.ycrdt_array_length.argtypes = [vp, cs, cs, P(ctypes.c_uint64)]
     L.ycrdt_array_get.argtypes = [vp, cs, cs, ctypes.c_uint64, P(i32), P(_Out)]
@@ -164,24 +177,23 @@ def _check(rc):
         raise YcrdtError(rc, lib().ycrdt_last_error().decode(errors="replace"))
 
 
-def _bufs(updates):
-    """ycrdt_buf[] over the updates: one joined blob (kept alive on the array) and the pointer /
-    length columns filled with numpy — per-element ctypes assignment costs ~1.5 us per buffer."""
-    import numpy as np
+def _pack():
+    """The in-tree host-glue extension (crdt_amd/_ycpack.c, built with libycrdt.so)."""
+    try:
+        from . import _ycpack
+    except ImportError as e:
+        raise RuntimeError("crdt_amd/_ycpack not built: run `python -c 'import __graft_entry__ as g; g.build()'`") from e
+    return _ycpack
 
-    keep = [bytes(u) for u in updates]
+
+def _bufs(updates):
+    """ycrdt_buf[] over the updates, pointing into the bytes objects themselves (no join / copy;
+    _ycpack.c). The array keeps the objects it points into alive."""
+    keep = updates if isinstance(updates, (list, tuple)) else list(updates)
+    raw, conv = _pack().bufs(keep)
     n = len(keep)
-    arr = (_Buf * max(1, n))()
-    if n:
-        blob = b"".join(keep)
-        arr._blob = blob
-        lens = np.fromiter(map(len, keep), dtype=np.uint64, count=n)
-        offs = np.zeros(n, dtype=np.uint64)
-        np.cumsum(lens[:-1], out=offs[1:])
-        base = ctypes.cast(ctypes.c_char_p(blob), ctypes.c_void_p).value or 0
-        cols = np.frombuffer(arr, dtype=np.uint64).reshape(-1, 2)  # {ptr, len} per ycrdt_buf
-        cols[:n, 0] = offs + np.uint64(base)
-        cols[:n, 1] = lens
+    arr = (_Buf * max(1, n)).from_buffer_copy(raw)
+    arr._keep = (keep, conv)
     return arr, keep
 
 
@@ -361,13 +373,13 @@ class Doc:
 
 
 def _docs_arrays(docs):
-    ups, doc_of = [], []
-    for d, us in enumerate(docs):
-        ups.extend(us)
-        doc_of.extend([d] * len(us))
-    arr, keep = _bufs(ups)
-    do = (ctypes.c_uint32 * max(1, len(doc_of)))(*doc_of)
-    return arr, keep, do
+    docs = docs if isinstance(docs, (list, tuple)) else list(docs)
+    raw, dof, conv = _pack().docs(docs)
+    n = len(raw) // ctypes.sizeof(_Buf) if any(len(d) for d in docs) else 0
+    arr = (_Buf * max(1, n)).from_buffer_copy(raw)
+    do = (ctypes.c_uint32 * max(1, n)).from_buffer_copy(dof)
+    arr._keep = (docs, conv)
+    return arr, range(n), do
 
 
 class Batch:
@@ -419,6 +431,20 @@ class Batch:
         _check(lib().ycrdt_batch_result_docs(self._h, us, ss))
         return [(_take(us[i]), _take(ss[i])) for i in range(self.ndocs)]
 
+    def result_docs_packed(self):
+        """(blob, offs): every document's update and state vector back to back in one numpy uint8
+        array, split on the device — document d's update is blob[offs[2d]:offs[2d+1]], its state
+        vector blob[offs[2d+1]:offs[2d+2]] (ycrdt_batch_result_docs_packed)."""
+        import numpy as np
+
+        offs = np.zeros(2 * self.ndocs + 1, dtype=np.uint64)
+        total = ctypes.c_uint64()
+        op = offs.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64))
+        _check(lib().ycrdt_batch_result_docs_packed(self._h, None, 0, op, ctypes.byref(total)))
+        blob = np.empty(max(1, total.value), dtype=np.uint8)
+        _check(lib().ycrdt_batch_result_docs_packed(self._h, blob.ctypes.data, total.value, op, ctypes.byref(total)))
+        return blob[: total.value], offs
+
 
 def merge_docs(docs, engine=None):
     """Many independent documents' update lists merged in ONE device pass (ycrdt_merge_docs):
@@ -449,8 +475,10 @@ def encode_state_vector(doc: Doc) -> bytes:
 
 
 class Comm:
-    """RCCL communicator inside libycrdt (one rank per GPU): Comm.unique_id() on rank 0, the bytes
-    handed to every rank by any channel, then Comm(engine, nranks, rank, uid) on each."""
+    """Communicator inside libycrdt (one rank per GPU). RCCL: Comm.unique_id() on rank 0, the bytes
+    handed to every rank by any channel, then Comm(engine, nranks, rank, uid) on each. Or
+    Comm.over(engine, nranks, rank, allreduce, allgather): the library's collectives over host
+    callbacks (ycrdt_exchange) — e.g. torch.distributed gloo, see Comm.over_torch."""
 
     @staticmethod
     def unique_id() -> bytes:
@@ -468,6 +496,62 @@ class Comm:
         _check(lib().ycrdt_comm_create(engine._h, nranks, rank, uid, ctypes.byref(h)))
         self._h, self.engine, self.nranks, self.rank = h, engine, nranks, rank
 
+    @classmethod
+    def over(cls, engine, nranks: int, rank: int, allreduce, allgather):
+        """allreduce(numpy u32 array, op) -> None, in place, op 0 = sum / 1 = max, over every rank;
+        allgather(bytes) -> bytes, the ranks' equal-length payloads concatenated in rank order."""
+        import numpy as np
+
+        self = cls.__new__(cls)
+
+        def ar(_ctx, words, n, op):
+            try:
+                a = np.ctypeslib.as_array(words, shape=(n,)) if n else np.zeros(0, np.uint32)
+                allreduce(a, op)
+                return 0
+            except Exception:  # noqa: BLE001 — surfaces as YCRDT_E_DEVICE in the library call
+                return -1
+
+        def ag(_ctx, send, nbytes, recv):
+            try:
+                got = allgather(ctypes.string_at(send, nbytes) if nbytes else b"")
+                if len(got) != nbytes * nranks:
+                    return -1
+                if got:
+                    ctypes.memmove(recv, got, len(got))
+                return 0
+            except Exception:  # noqa: BLE001
+                return -1
+
+        self._cbs = (ALLREDUCE_FN(ar), ALLGATHER_FN(ag))
+        self._x = _Exchange(None, self._cbs[0], self._cbs[1])
+        h = ctypes.c_void_p()
+        _check(lib().ycrdt_comm_create_exchange(engine._h, nranks, rank, ctypes.byref(self._x), ctypes.byref(h)))
+        self._h, self.engine, self.nranks, self.rank = h, engine, nranks, rank
+        return self
+
+    @classmethod
+    def over_torch(cls, engine, group=None):
+        """The host exchange over a torch.distributed process group (gloo: CPU tensors)."""
+        import numpy as np
+        import torch
+        import torch.distributed as dist
+
+        world, rank = dist.get_world_size(group), dist.get_rank(group)
+
+        def allreduce(a, op):
+            t = torch.from_numpy(a.astype(np.int64))
+            dist.all_reduce(t, op=dist.ReduceOp.MAX if op else dist.ReduceOp.SUM, group=group)
+            a[:] = (t.numpy() & 0xFFFFFFFF).astype(np.uint32)
+
+        def allgather(b):
+            t = torch.frombuffer(bytearray(b), dtype=torch.uint8) if b else torch.zeros(0, dtype=torch.uint8)
+            outs = [torch.zeros_like(t) for _ in range(world)]
+            dist.all_gather(outs, t, group=group)
+            return b"".join(o.numpy().tobytes() for o in outs)
+
+        return cls.over(engine, world, rank, allreduce, allgather)
+
     def close(self):
         if getattr(self, "_h", None):
             lib().ycrdt_comm_destroy(self._h)
@@ -478,6 +562,22 @@ class Comm:
             self.close()
         except Exception:
             pass
+
+    def fleet_sv_allreduce_max(self, svs: dict) -> dict:
+        """{doc id (u32): state vector bytes} held by this rank -> {doc id: state vector of the union
+        over the ranks} for every document any rank holds (ycrdt_comm_fleet_sv_allreduce_max)."""
+        import numpy as np
+
+        ids = list(svs)
+        arr, keep = _bufs([svs[i] for i in ids])
+        docs = (ctypes.c_uint32 * max(1, len(ids)))(*ids)
+        d, o, b = _Out(), _Out(), _Out()
+        _check(lib().ycrdt_comm_fleet_sv_allreduce_max(self._h, self.engine._h, docs, arr, len(ids),
+                                                        ctypes.byref(d), ctypes.byref(o), ctypes.byref(b)))
+        dd = np.frombuffer(_take(d), dtype=np.uint32)
+        oo = np.frombuffer(_take(o), dtype=np.uint64)
+        blob = _take(b)
+        return {int(dd[j]): blob[int(oo[j]):int(oo[j + 1])] for j in range(len(dd))}
 
     def sv_allreduce_max(self, sv: bytes) -> bytes:
         out = _Out()
@@ -492,6 +592,12 @@ class Comm:
         return _take(out)
 
 
+def route(doc_id, world: int) -> int:
+    """Owner rank of a document / topic id (ycrdt_route): stable across ranks, processes and runs."""
+    b = doc_id.encode() if isinstance(doc_id, str) else bytes(doc_id)
+    return int(lib().ycrdt_route(b, len(b), world))
+
+
 def apply_updates_multi(docs, updates, engine=None):
     """Y.applyUpdate(docs[i], updates[i]) for every i — a fleet ingest batch — merged in one device
     pass for every document with nothing pending (ycrdt_apply_updates_multi)."""
@@ -499,7 +605,10 @@ def apply_updates_multi(docs, updates, engine=None):
         raise ValueError("one document per update")
     eng = engine or (docs[0].engine if docs else default_engine())
     arr, keep = _bufs(updates)
-    hs = (ctypes.c_void_p * max(1, len(docs)))(*[d._h.value for d in docs])
+    import numpy as np
+
+    hv = np.fromiter((d._h.value for d in docs), dtype=np.uint64, count=len(docs)) if docs else np.zeros(1, np.uint64)
+    hs = hv.ctypes.data_as(ctypes.POINTER(ctypes.c_void_p))
     _check(lib().ycrdt_apply_updates_multi(eng._h, hs, arr, len(keep)))
 
 

@@ -17,6 +17,7 @@
 #include "yc_ingest.h"
 #include "yc_comm.h"
 #include <thread>
+#include <atomic>
 #include "../../include/ycrdt.h"
 
 using namespace yc;
@@ -167,7 +168,7 @@ enum Buf {
   B_TPRV, B_TMPRV, B_TMTAIL, B_TTREP, B_TOTAIL,
   B_OFIRST, B_OCIDX, B_OSIZE, B_OPOS, B_RSEG, B_RLEN, B_RSIZE, B_RPOS, B_OUT, B_SVOUT,
   B_VKMAP, B_VKREP, B_VKEYS, B_VNKEYS, B_VPOS, B_VD0, B_VN0, B_VD1, B_VN1, B_VORDER, B_VSEGS,
-  B_SCRATCH2, B_TMP2, B_CAPS, B_CLKEY, B_CLKEY2, B_CHKEY, B_CHVAL, B_CLDOC, B_DSFA, B_EMIT, B_DOCRNG, B_KSHARD, B_SOWNER, B_GFLAGS0, B_GFACC,
+  B_SCRATCH2, B_TMP2, B_CAPS, B_CLKEY, B_CLKEY2, B_CHKEY, B_CHVAL, B_CLDOC, B_DSFA, B_EMIT, B_DOCRNG, B_PACK, B_PACKPC, B_KSHARD, B_SOWNER, B_GFLAGS0, B_GFACC,
   B_COUNT
 };
 
@@ -188,7 +189,11 @@ struct ycrdt_engine {
   std::vector<hipEvent_t> event_pool;                     // reused across merges (no create per mark)
   std::vector<std::pair<const char*, double>> phase_ms;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
-  std::vector<uint8_t> pinned_stage;
+  // pinned host staging (two halves of PIN_PER chunks: the copy of one wave into a half overlaps
+  // the H2D of the previous wave from the other) and its per-half "H2D done" events
+  uint8_t* pin = nullptr;
+  size_t pin_cap = 0;
+  hipEvent_t pin_ev[2] = {nullptr, nullptr};
   // result of the last merge (e->w.out / e->w.sv_out): ws_owner is the batch that produced it
   // (nullptr after any other call), so ycrdt_batch_result never returns another call's bytes
   const void* ws_owner = nullptr;
@@ -254,6 +259,10 @@ struct ycrdt_batch {
   uint64_t nbytes = 0;          // span of the batch buffer (windows before the last are 2^32 bytes)
   uint64_t in_bytes = 0;
   bool merged = false;
+  // per-document split of a merged multi-document batch (ycrdt_batch_result_docs_packed):
+  // doc d's update = packed[offs[2d], offs[2d+1]), its state vector = [offs[2d+1], offs[2d+2])
+  bool packed = false;
+  std::vector<uint64_t> pack_offs;
 };
 
 namespace {
@@ -378,6 +387,86 @@ void layout(ycrdt_batch* b, const std::vector<Src>& src, std::vector<uint32_t>& 
 // absolute byte offset of staged update u in the batch buffer
 uint64_t uabs(const ycrdt_batch* b, size_t u) { return ((uint64_t)b->uwin[u] << b->win_shift) + b->uoff[u]; }
 
+// Host bytes → HBM through the engine's pinned staging. The span is cut into PIN_CHUNK chunks;
+// a wave of up to PIN_PER chunks is filled by worker threads (each chunk: its pieces copied, the
+// bytes between them — slot padding, window gaps — zeroed) and sent with one async H2D, while the
+// next wave fills the other half of the staging buffer. Small spans: one memcpy on this thread.
+struct HostPiece {
+  uint64_t off;   // within the span
+  uint64_t len;
+  const uint8_t* p;
+};
+constexpr uint32_t PIN_PER = 16;
+// 32 MiB; YCRDT_PIN_CHUNK (tests: e.g. 65536) makes the two-half wave path run on small batches
+uint64_t pin_chunk() {
+  const char* v = getenv("YCRDT_PIN_CHUNK");
+  const uint64_t c = v ? strtoull(v, nullptr, 10) : 0;
+  return c >= 4096 && c <= (uint64_t(1) << 30) ? c : uint64_t(32) << 20;
+}
+// copies the pieces overlapping [lo, hi) of the span to dst (= span byte lo), zero elsewhere
+void fill_range(uint8_t* dst, uint64_t lo, uint64_t hi, const std::vector<HostPiece>& hp) {
+  size_t i = std::upper_bound(hp.begin(), hp.end(), lo, [](uint64_t v, const HostPiece& x) { return v < x.off; }) - hp.begin();
+  if (i > 0) --i;
+  uint64_t cur = lo;
+  for (; i < hp.size() && hp[i].off < hi; ++i) {
+    const uint64_t a = std::max(lo, hp[i].off), z = std::min(hi, hp[i].off + hp[i].len);
+    if (z <= a) continue;
+    if (a > cur) memset(dst + (cur - lo), 0, a - cur);
+    memcpy(dst + (a - lo), hp[i].p + (a - hp[i].off), z - a);
+    cur = z;
+  }
+  if (hi > cur) memset(dst + (cur - lo), 0, hi - cur);
+}
+int ensure_pinned(ycrdt_engine* e, size_t need) {
+  if (need <= e->pin_cap) return YCRDT_OK;
+  HIPCHK(hipStreamSynchronize(e->stream));
+  if (e->pin) hipHostFree(e->pin);
+  e->pin = nullptr;
+  e->pin_cap = 0;
+  const size_t c = std::max<size_t>(need, size_t(1) << 20);
+  if (hipHostMalloc((void**)&e->pin, c, hipHostMallocDefault) != hipSuccess) {
+    (void)hipGetLastError();
+    e->pin = nullptr;
+    return fail(YCRDT_E_DEVICE, "pinned host staging allocation failed");
+  }
+  e->pin_cap = c;
+  return YCRDT_OK;
+}
+int h2d_span(ycrdt_engine* e, uint8_t* dev, uint64_t span, const std::vector<HostPiece>& hp) {
+  if (!span) return YCRDT_OK;
+  const uint64_t PIN_CHUNK = pin_chunk();
+  const uint64_t nch = (span + PIN_CHUNK - 1) / PIN_CHUNK;
+  const bool waves = nch > PIN_PER;
+  if (const int rc = ensure_pinned(e, waves ? 2 * PIN_PER * PIN_CHUNK : (size_t)span)) return rc;
+  const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
+  const uint32_t T = span < (uint64_t(8) << 20) ? 1u : std::min<uint32_t>({16u, hw, (uint32_t)nch});
+  for (uint64_t k0 = 0, wave = 0; k0 < nch; k0 += PIN_PER, ++wave) {
+    const uint64_t k1 = std::min<uint64_t>(nch, k0 + PIN_PER);
+    const uint32_t half = (uint32_t)(wave & 1);
+    uint8_t* base = e->pin + (waves ? half * PIN_PER * PIN_CHUNK : 0);
+    if (wave >= 2) HIPCHK(hipEventSynchronize(e->pin_ev[half]));  // that half's previous H2D is done
+    const uint64_t lo = k0 * PIN_CHUNK, hi = std::min(span, k1 * PIN_CHUNK);
+    if (T == 1) {
+      fill_range(base, lo, hi, hp);
+    } else {
+      std::atomic<uint64_t> next{k0};
+      auto work = [&]() {
+        for (uint64_t k; (k = next.fetch_add(1)) < k1;) {
+          const uint64_t a = k * PIN_CHUNK, z = std::min(span, a + PIN_CHUNK);
+          fill_range(base + (a - lo), a, z, hp);
+        }
+      };
+      std::vector<std::thread> th;
+      for (uint32_t t = 1; t < T; ++t) th.emplace_back(work);
+      work();
+      for (auto& t : th) t.join();
+    }
+    HIPCHK(hipMemcpyAsync(dev + lo, base, hi - lo, hipMemcpyHostToDevice, e->stream));
+    HIPCHK(hipEventRecord(e->pin_ev[half], e->stream));
+  }
+  return YCRDT_OK;
+}
+
 // Stages the sources into the batch buffer: the host region in one H2D copy, device sources by
 // one piece-copy launch. doc_of (one per source) makes it a multi-document batch.
 int stage_srcs(ycrdt_batch* b, const std::vector<Src>& src, const uint32_t* doc_of = nullptr, uint32_t ndocs = 1) {
@@ -391,13 +480,14 @@ int stage_srcs(ycrdt_batch* b, const std::vector<Src>& src, const uint32_t* doc_
   const size_t nu = b->ulen.size();
   size_t ndev = 0;
   while (ndev < nu && src[order[ndev]].dev) ++ndev;
-  // the host updates in one H2D copy of their span (window gaps included)
+  // the host updates: their span (window gaps included) through pinned staging
   const uint64_t host0 = ndev < nu ? uabs(b, ndev) : b->nbytes;
-  e->pinned_stage.assign((size_t)(b->nbytes - host0), 0);
-  for (size_t u = ndev; u < nu; ++u)
-    if (b->ulen[u]) memcpy(e->pinned_stage.data() + (uabs(b, u) - host0), src[order[u]].p, b->ulen[u]);
-  if (!e->pinned_stage.empty())
-    HIPCHK(hipMemcpyAsync((uint8_t*)b->bytes.p + host0, e->pinned_stage.data(), e->pinned_stage.size(), hipMemcpyHostToDevice, e->stream));
+  {
+    std::vector<HostPiece> hp;
+    hp.reserve(nu - ndev);
+    for (size_t u = ndev; u < nu; ++u) hp.push_back(HostPiece{uabs(b, u) - host0, b->ulen[u], src[order[u]].p});
+    if (const int rc = h2d_span(e, (uint8_t*)b->bytes.p + host0, b->nbytes - host0, hp)) return rc;
+  }
   if (ndev == 1) {
     if (b->ulen[0]) HIPCHK(hipMemcpyAsync(b->bytes.p, src[order[0]].p, b->ulen[0], hipMemcpyDeviceToDevice, e->stream));
   } else if (ndev > 1) {
@@ -691,6 +781,7 @@ struct ShardSpec {
   uint32_t nshards = 1;
   int32_t shard = -1;  // -1: every shard in turn (logical shards on one GPU)
   ycrdt_comm* comm = nullptr;
+  mutable bool agreed = false;  // this rank reached the pre-exchange status agreement
 };
 int comm_allreduce_sum_u32(ycrdt_comm* c, uint32_t* buf, size_t n, hipStream_t s) {
   std::string err;
@@ -704,6 +795,7 @@ int run_merge(ycrdt_engine* e, ycrdt_batch* b, const std::unordered_map<uint32_t
   bool ok = true;
   hipStream_t s = e->stream;
   e->ws_owner = nullptr;
+  b->packed = false;
   w.capped = 0;
   w.ncaps = 0;
   if (caps) {
@@ -894,6 +986,13 @@ int run_merge(ycrdt_engine* e, ycrdt_batch* b, const std::unordered_map<uint32_t
     if (sh) {  // combine: every segment's flags come from its owner (RCCL sum across GPUs)
       mark(e, "shard.exchange");
       if (sh->comm) {
+        // every rank reports before the data collective: a rank that failed earlier joins only
+        // this agreement (ycrdt_batch_merge_sharded), so no peer waits in a sum it never enters
+        uint32_t any = 0;
+        std::string err;
+        sh->agreed = true;
+        if (yc::comm_agree(sh->comm, 0u, s, any, err)) return fail(YCRDT_E_DEVICE, err);
+        if (any) return fail(YCRDT_E_DEVICE, "another rank failed the sharded merge before the exchange");
         const int rc2 = comm_allreduce_sum_u32(sh->comm, acc, nsegs, s);
         if (rc2) return rc2;
       }
@@ -1219,61 +1318,134 @@ int run_lazy(ycrdt_engine* e, ycrdt_batch* b, bool merge, const std::vector<std:
 // descending (document, client) order, so every document's struct blocks, delete-set blocks and
 // state-vector entries are contiguous; each document's update is its blocks behind its own
 // varuint counts (writeClientsStructs / writeDeleteSet / writeStateVector headers).
-int split_docs(ycrdt_engine* e, uint32_t ndocs, ycrdt_out* outs, ycrdt_out* svs) {
+// Device-side split of a merged multi-document batch: every document's update ([varuint struct
+// blocks][its blocks][varuint delete-set clients][its delete-set groups]) and state vector laid
+// out back to back in one HBM buffer (B_PACK) by one piece-copy launch, the varuint headers
+// written inline; b->pack_offs holds the boundaries. Clients are encoded in (document, client)
+// descending order, so each document's sections are contiguous ranges (k_doc_ranges).
+constexpr uint32_t PIECE_MAX = 16384;  // large ranges are cut so no wavefront copies megabytes alone
+int pack_docs(ycrdt_engine* e, ycrdt_batch* b) {
+  if (b->packed) return YCRDT_OK;
   Work& w = e->w;
-  const uint32_t nc = (uint32_t)e->last.clients;
-  const size_t stride = (size_t)w.cap_clients + 1;
-  std::vector<uint32_t> doc(nc), blk(nc), nincl(nc), dsblk(nc), nruns(nc), sv(nc);
-  std::vector<uint64_t> blkpos(nc), dspos(nc), svpos(nc);
-  std::vector<uint8_t> all(e->out_bytes), svall(e->sv_bytes);
-  Counters c;
+  auto& V = e->bufs;
+  bool ok = true;
   hipStream_t s = e->stream;
+  const uint32_t nd = b->ndocs;
+  unsigned long long* rng = take<unsigned long long>(V, B_DOCRNG, 9 * (size_t)nd + 9, ok);
+  if (!ok) return fail(YCRDT_E_DEVICE, oom("document ranges"));
+  launch_doc_ranges(w, (uint32_t)e->last.clients, nd, rng, s);
+  std::vector<unsigned long long> r(9 * (size_t)nd);
+  Counters c;
+  HIPCHK(hipMemcpyAsync(r.data(), rng, sizeof(unsigned long long) * r.size(), hipMemcpyDeviceToHost, s));
   HIPCHK(hipMemcpyAsync(&c, w.ctr, sizeof(Counters), hipMemcpyDeviceToHost, s));
-  if (nc) {
-    HIPCHK(hipMemcpyAsync(doc.data(), w.cl_doc, sizeof(uint32_t) * nc, hipMemcpyDeviceToHost, s));
-    const std::pair<uint32_t, std::vector<uint32_t>*> cols[] = {{CC_BLK, &blk}, {CC_NINCL, &nincl}, {CC_DSBLK, &dsblk},
-                                                                 {CC_NRUNS, &nruns}, {CC_SV, &sv}};
-    for (const auto& col : cols)
-      HIPCHK(hipMemcpyAsync(col.second->data(), w.cc + col.first * stride, sizeof(uint32_t) * nc, hipMemcpyDeviceToHost, s));
-    const std::pair<uint32_t, std::vector<uint64_t>*> cols64[] = {{CC64_BLKPOS, &blkpos}, {CC64_DSPOS, &dspos}, {CC64_SVPOS, &svpos}};
-    for (const auto& col : cols64)
-      HIPCHK(hipMemcpyAsync(col.second->data(), w.cc64 + col.first * stride, sizeof(uint64_t) * nc, hipMemcpyDeviceToHost, s));
-  }
-  if (!all.empty()) HIPCHK(hipMemcpyAsync(all.data(), w.out, all.size(), hipMemcpyDeviceToHost, s));
-  if (!svall.empty()) HIPCHK(hipMemcpyAsync(svall.data(), w.sv_out, svall.size(), hipMemcpyDeviceToHost, s));
   HIPCHK(hipStreamSynchronize(s));
+  if (c.err) return map_err(c.err, "document split");
   const uint64_t sbase = c.pad[3], dsbase = c.ds_base + vu_size_host(c.pad[1]), svbase = vu_size_host(c.pad[2]);
-  struct Rng { uint64_t lo = ~0ull, hi = 0; uint32_t n = 0; void add(uint64_t a, uint32_t len, bool in) { if (!in) return; lo = std::min(lo, a); hi = std::max(hi, a + len); ++n; } };
-  std::vector<Rng> rs(ndocs), rd(ndocs), rv(ndocs);
-  for (uint32_t i = 0; i < nc; ++i) {
-    const uint32_t d = doc[i];
-    if (d >= ndocs) return fail(YCRDT_E_DEVICE, "internal: client of an unknown document");
-    rs[d].add(blkpos[i], blk[i], nincl[i] != 0);
-    rd[d].add(dspos[i], dsblk[i], nruns[i] != 0);
-    rv[d].add(svpos[i], sv[i], sv[i] != 0);
+  std::vector<uint64_t>& offs = b->pack_offs;
+  offs.assign(2 * (size_t)nd + 1, 0);
+  uint64_t pos = 0;
+  for (uint32_t d = 0; d < nd; ++d) {
+    const unsigned long long* x = &r[9 * (size_t)d];
+    offs[2 * d] = pos;
+    pos += vu_size_host((uint32_t)x[2]) + (x[2] ? x[1] - x[0] : 0) + vu_size_host((uint32_t)x[5]) + (x[5] ? x[4] - x[3] : 0);
+    offs[2 * d + 1] = pos;
+    pos += vu_size_host((uint32_t)x[8]) + (x[8] ? x[7] - x[6] : 0);
   }
-  auto put = [](std::vector<uint8_t>& o, uint32_t v) {
-    while (v > 127u) { o.push_back((uint8_t)(0x80u | (v & 0x7fu))); v >>= 7; }
-    o.push_back((uint8_t)v);
+  offs[2 * (size_t)nd] = pos;
+  uint8_t* dst0 = take<uint8_t>(V, B_PACK, pos + 16, ok);
+  if (!ok) return fail(YCRDT_E_DEVICE, oom("document split"));
+  std::vector<Piece> pc;
+  pc.reserve(8 * (size_t)nd);
+  auto hdr = [&](uint8_t* dst, uint32_t v) -> uint8_t* {
+    Piece P{};
+    while (v > 127u) { P.inl[P.len++] = (uint8_t)(0x80u | (v & 0x7fu)); v >>= 7; }
+    P.inl[P.len++] = (uint8_t)v;
+    P.dst = dst;
+    pc.push_back(P);
+    return dst + P.len;
   };
-  for (uint32_t d = 0; d < ndocs; ++d) {
-    std::vector<uint8_t> o;
-    put(o, rs[d].n);
-    if (rs[d].n) o.insert(o.end(), all.begin() + sbase + rs[d].lo, all.begin() + sbase + rs[d].hi);
-    put(o, rd[d].n);
-    if (rd[d].n) o.insert(o.end(), all.begin() + dsbase + rd[d].lo, all.begin() + dsbase + rd[d].hi);
-    outs[d].ptr = (uint8_t*)malloc(o.size());
+  auto range = [&](uint8_t* dst, const uint8_t* src, uint64_t n) -> uint8_t* {
+    for (uint64_t k = 0; k < n; k += PIECE_MAX)
+      pc.push_back(Piece{src + k, dst + k, (uint32_t)std::min<uint64_t>(PIECE_MAX, n - k), {0}});
+    return dst + n;
+  };
+  for (uint32_t d = 0; d < nd; ++d) {
+    const unsigned long long* x = &r[9 * (size_t)d];
+    uint8_t* dst = dst0 + offs[2 * d];
+    dst = hdr(dst, (uint32_t)x[2]);
+    if (x[2]) dst = range(dst, w.out + sbase + x[0], x[1] - x[0]);
+    dst = hdr(dst, (uint32_t)x[5]);
+    if (x[5]) dst = range(dst, w.out + dsbase + x[3], x[4] - x[3]);
+    dst = hdr(dst, (uint32_t)x[8]);
+    if (x[8]) range(dst, w.sv_out + svbase + x[6], x[7] - x[6]);
+  }
+  if (pc.size() >= 0xFFFFFFF0ull) return fail(YCRDT_E_CAPACITY, "document split: too many pieces");
+  Piece* dpc = take<Piece>(V, B_PACKPC, pc.size() + 1, ok);
+  if (!ok) return fail(YCRDT_E_DEVICE, oom("document split pieces"));
+  HIPCHK(hipMemcpyAsync(dpc, pc.data(), sizeof(Piece) * pc.size(), hipMemcpyHostToDevice, s));
+  copy_pieces(dpc, (uint32_t)pc.size(), s);
+  HIPCHK(hipStreamSynchronize(s));
+  b->packed = true;
+  return YCRDT_OK;
+}
+
+// HBM → host memory through the engine's pinned staging: a wave of chunks is copied D2H into one
+// half while worker threads move the previous wave out of the other half.
+int d2h_span(ycrdt_engine* e, uint8_t* host, const uint8_t* dev, uint64_t span) {
+  if (!span) return YCRDT_OK;
+  const uint64_t PIN_CHUNK = pin_chunk();
+  const uint64_t nch = (span + PIN_CHUNK - 1) / PIN_CHUNK;
+  const bool waves = nch > PIN_PER;
+  if (const int rc = ensure_pinned(e, waves ? 2 * PIN_PER * PIN_CHUNK : (size_t)span)) return rc;
+  const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
+  const uint32_t T = span < (uint64_t(8) << 20) ? 1u : std::min<uint32_t>({16u, hw, (uint32_t)nch});
+  const uint64_t nw = (nch + PIN_PER - 1) / PIN_PER;
+  auto issue = [&](uint64_t wave) -> int {
+    const uint64_t lo = wave * PIN_PER * PIN_CHUNK, hi = std::min(span, lo + PIN_PER * PIN_CHUNK);
+    uint8_t* base = e->pin + (waves ? (wave & 1) * PIN_PER * PIN_CHUNK : 0);
+    HIPCHK(hipMemcpyAsync(base, dev + lo, hi - lo, hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(hipEventRecord(e->pin_ev[wave & 1], e->stream));
+    return YCRDT_OK;
+  };
+  if (const int rc = issue(0)) return rc;
+  for (uint64_t wave = 0; wave < nw; ++wave) {
+    HIPCHK(hipEventSynchronize(e->pin_ev[wave & 1]));
+    if (wave + 1 < nw)
+      if (const int rc = issue(wave + 1)) return rc;  // into the other half, beside the copy-out below
+    const uint64_t lo = wave * PIN_PER * PIN_CHUNK, hi = std::min(span, lo + PIN_PER * PIN_CHUNK);
+    const uint8_t* base = e->pin + (waves ? (wave & 1) * PIN_PER * PIN_CHUNK : 0);
+    if (T == 1) {
+      memcpy(host + lo, base, hi - lo);
+    } else {
+      std::atomic<uint64_t> next{lo};
+      auto work = [&]() {
+        for (uint64_t a; (a = next.fetch_add(PIN_CHUNK)) < hi;) memcpy(host + a, base + (a - lo), std::min(hi, a + PIN_CHUNK) - a);
+      };
+      std::vector<std::thread> th;
+      for (uint32_t t = 1; t < T; ++t) th.emplace_back(work);
+      work();
+      for (auto& t : th) t.join();
+    }
+  }
+  return YCRDT_OK;
+}
+
+int split_docs(ycrdt_engine* e, ycrdt_batch* b, ycrdt_out* outs, ycrdt_out* svs) {
+  if (const int rc = pack_docs(e, b)) return rc;
+  const std::vector<uint64_t>& offs = b->pack_offs;
+  std::vector<uint8_t> all(offs.back());
+  if (const int rc = d2h_span(e, all.data(), (const uint8_t*)e->bufs[B_PACK].p, all.size())) return rc;
+  for (uint32_t d = 0; d < b->ndocs; ++d) {
+    const uint64_t a = offs[2 * d], m = offs[2 * d + 1], z = offs[2 * d + 2];
+    outs[d].ptr = (uint8_t*)malloc(m - a);
     if (!outs[d].ptr) return fail(YCRDT_E_CAPACITY, "host allocation failed");  // the caller frees the rest
-    outs[d].len = o.size();
-    memcpy(outs[d].ptr, o.data(), o.size());
+    outs[d].len = m - a;
+    memcpy(outs[d].ptr, all.data() + a, m - a);
     if (svs) {
-      std::vector<uint8_t> v;
-      put(v, rv[d].n);
-      if (rv[d].n) v.insert(v.end(), svall.begin() + svbase + rv[d].lo, svall.begin() + svbase + rv[d].hi);
-      svs[d].ptr = (uint8_t*)malloc(v.size());
+      svs[d].ptr = (uint8_t*)malloc(z - m);
       if (!svs[d].ptr) return fail(YCRDT_E_CAPACITY, "host allocation failed");
-      svs[d].len = v.size();
-      memcpy(svs[d].ptr, v.data(), v.size());
+      svs[d].len = z - m;
+      memcpy(svs[d].ptr, all.data() + m, z - m);
     }
   }
   return YCRDT_OK;
@@ -1318,6 +1490,8 @@ int ycrdt_engine_create(int device, int compat, ycrdt_engine** out) {
   hipEventCreateWithFlags(&e->side_fork, hipEventDisableTiming);
   hipEventCreate(&e->ev0);
   hipEventCreate(&e->ev1);
+  hipEventCreateWithFlags(&e->pin_ev[0], hipEventDisableTiming);
+  hipEventCreateWithFlags(&e->pin_ev[1], hipEventDisableTiming);
   e->bufs.resize(B_COUNT);
   *out = e;
   return YCRDT_OK;
@@ -1337,6 +1511,9 @@ void ycrdt_engine_destroy(ycrdt_engine* e) {
   for (auto& ev : e->event_pool) hipEventDestroy(ev);
   hipEventDestroy(e->ev0);
   hipEventDestroy(e->ev1);
+  hipEventDestroy(e->pin_ev[0]);
+  hipEventDestroy(e->pin_ev[1]);
+  if (e->pin) hipHostFree(e->pin);
   hipStreamSynchronize(e->side);
   hipEventDestroy(e->side_done);
   hipEventDestroy(e->side_fork);
@@ -1813,11 +1990,32 @@ int ycrdt_batch_result_docs(ycrdt_batch* b, ycrdt_out* updates, ycrdt_out* svs) 
   HIPCHK(hipSetDevice(e->device));
   for (uint32_t d = 0; d < b->ndocs; ++d) { updates[d] = ycrdt_out{nullptr, 0}; if (svs) svs[d] = ycrdt_out{nullptr, 0}; }
   if (b->ndocs == 1) return ycrdt_batch_result(b, updates, svs);
-  const int rc = split_docs(e, b->ndocs, updates, svs);
+  const int rc = split_docs(e, b, updates, svs);
   if (rc) for (uint32_t d = 0; d < b->ndocs; ++d) { ycrdt_free(&updates[d]); if (svs) ycrdt_free(&svs[d]); }
   return rc;
 }
 
+int ycrdt_batch_result_docs_packed(ycrdt_batch* b, uint8_t* dst, uint64_t cap, uint64_t* offs, uint64_t* total) {
+  if (!b || !b->merged) return fail(YCRDT_E_ARG, "batch not merged");
+  ycrdt_engine* e = b->e;
+  if (e->ws_owner != b) return fail(YCRDT_E_ARG, "batch result no longer available (another engine call ran since ycrdt_batch_merge)");
+  HIPCHK(hipSetDevice(e->device));
+  if (b->ndocs == 1 && !b->packed) {  // one document: the update and the state vector as they are
+    b->pack_offs = {0, e->out_bytes, e->out_bytes + e->sv_bytes};
+  } else if (const int rc = pack_docs(e, b)) {
+    return rc;
+  }
+  const std::vector<uint64_t>& o = b->pack_offs;
+  if (total) *total = o.back();
+  if (offs) memcpy(offs, o.data(), sizeof(uint64_t) * o.size());
+  if (!dst) return YCRDT_OK;
+  if (cap < o.back()) return fail(YCRDT_E_ARG, "destination smaller than the packed result");
+  if (b->ndocs == 1) {
+    if (const int rc = d2h_span(e, dst, e->w.out, e->out_bytes)) return rc;
+    return d2h_span(e, dst + e->out_bytes, e->w.sv_out, e->sv_bytes);
+  }
+  return d2h_span(e, dst, (const uint8_t*)e->bufs[B_PACK].p, o.back());
+}
 int ycrdt_merge_docs(ycrdt_engine* e, const ycrdt_buf* ups, const uint32_t* doc_of, size_t n, uint32_t ndocs,
                      ycrdt_out* updates, ycrdt_out* svs) {
   if (!e || !updates || (n && (!ups || !doc_of)) || !ndocs) return fail(YCRDT_E_ARG, "null arg");
@@ -1864,6 +2062,55 @@ int ycrdt_comm_create(ycrdt_engine* e, int nranks, int rank, const uint8_t id[YC
 
 void ycrdt_comm_destroy(ycrdt_comm* c) { yc::comm_destroy(c); }
 
+int ycrdt_comm_create_exchange(ycrdt_engine* e, int nranks, int rank, const ycrdt_exchange* x, ycrdt_comm** out) {
+  if (!e || !x || !out) return fail(YCRDT_E_ARG, "null arg");
+  std::string err;
+  *out = yc::comm_create_exchange(e->device, nranks, rank, x, err);
+  if (!*out) return fail(YCRDT_E_ARG, err);
+  return YCRDT_OK;
+}
+
+uint32_t ycrdt_route(const uint8_t* id, size_t len, uint32_t world) {
+  if (!world) return 0;
+  uint64_t h = 1469598103934665603ull;
+  for (size_t i = 0; i < len; ++i) { h ^= id[i]; h *= 1099511628211ull; }
+  h ^= h >> 33;
+  h *= 0xff51afd7ed558ccdull;
+  h ^= h >> 33;
+  h *= 0xc4ceb9fe1a85ec53ull;
+  h ^= h >> 33;
+  return (uint32_t)(h % world);
+}
+
+int ycrdt_comm_fleet_sv_allreduce_max(ycrdt_comm* c, ycrdt_engine* e, const uint32_t* docs, const ycrdt_buf* svs, size_t n,
+                                      ycrdt_out* doc_ids, ycrdt_out* offs, ycrdt_out* blob) {
+  if (!c || !e || !doc_ids || !offs || !blob || (n && (!docs || !svs))) return fail(YCRDT_E_ARG, "null arg");
+  *doc_ids = ycrdt_out{nullptr, 0};
+  *offs = ycrdt_out{nullptr, 0};
+  *blob = ycrdt_out{nullptr, 0};
+  HIPCHK(hipSetDevice(e->device));
+  std::string err;
+  std::vector<uint32_t> d;
+  std::vector<uint64_t> o;
+  std::vector<uint8_t> b;
+  const int r = yc::comm_fleet_sv_allreduce_max(c, docs, svs, n, e->stream, d, o, b, err);
+  if (r) return fail(r == -2 ? YCRDT_E_DECODE : r == -3 ? YCRDT_E_ARG : YCRDT_E_DEVICE, err);
+  auto give = [](ycrdt_out* x, const void* p, size_t len) -> bool {
+    x->ptr = (uint8_t*)malloc(len ? len : 1);
+    if (!x->ptr) return false;
+    x->len = len;
+    if (len) memcpy(x->ptr, p, len);
+    return true;
+  };
+  if (!give(doc_ids, d.data(), 4 * d.size()) || !give(offs, o.data(), 8 * o.size()) || !give(blob, b.data(), b.size())) {
+    ycrdt_free(doc_ids);
+    ycrdt_free(offs);
+    ycrdt_free(blob);
+    return fail(YCRDT_E_CAPACITY, "host allocation failed");
+  }
+  return YCRDT_OK;
+}
+
 int ycrdt_batch_merge_sharded(ycrdt_batch* b, ycrdt_comm* comm, uint32_t nshards, ycrdt_merge_stats* st) {
   if (!b || !nshards || nshards > 255) return fail(YCRDT_E_ARG, "bad batch / shard count (1..255)");
   if (b->ndocs > 1) return fail(YCRDT_E_ARG, "sharded merge of a multi-document batch");
@@ -1876,6 +2123,14 @@ int ycrdt_batch_merge_sharded(ycrdt_batch* b, ycrdt_comm* comm, uint32_t nshards
   }
   HIPCHK(hipSetDevice(b->e->device));
   int rc = run_merge(b->e, b, nullptr, nullptr, nullptr, &sh);
+  if (rc != YCRDT_OK && comm && !sh.agreed) {
+    // failed before the exchange: tell the peers (they are waiting in the agreement), keep the error
+    const std::string keep = g_err;
+    uint32_t any = 0;
+    std::string err;
+    if (yc::comm_agree(comm, 1u, b->e->stream, any, err)) yc::comm_abort(comm);
+    g_err = keep;
+  }
   if (rc == YCRDT_OK) {
     b->merged = true;
     b->e->ws_owner = b;

@@ -352,7 +352,7 @@ __global__ __launch_bounds__(256) void k_resolve(Work w, uint32_t nsegs) {
     if (kv == NONE) {  // not a root: climb
       uint32_t x = w.g_link[s];
       bool done = false;
-      for (uint32_t it = 0; it < (1u << 26); ++it) {
+      for (uint32_t it = 0; it <= nsegs; ++it) {  // more hops than segments: a cycle
         const uint32_t fx = w.g_flags[x], k = w.g_tmp[x], y = w.g_link[x];  // one round of loads per hop
         if (!(fx & SEG_ITEM)) {  // the origin chain ends in GC: getMissing drops the parent
           f = (f & ~SEG_ITEM) | SEG_GC | SEG_DEL;
@@ -368,7 +368,7 @@ __global__ __launch_bounds__(256) void k_resolve(Work w, uint32_t nsegs) {
         if (z != y) w.g_link[x] = z;
         x = y;
       }
-      if (!done) raise_err(&w.ctr->err, ERR_CAPACITY);  // a chain longer than any batch can hold
+      if (!done) raise_err(&w.ctr->err, ERR_DECODE);  // an origin cycle
     }
     if (f & SEG_ITEM) {
       if (kv == NONE) raise_err(&w.ctr->err, ERR_DECODE);  // origin chain without a root
@@ -404,17 +404,20 @@ uint32_t run_key_resolution(const Work& w, uint32_t nsegs, hipStream_t s) {
 void launch_map_winner(const Work& w, uint32_t nsegs, hipStream_t s) {}
 // the key's value is the rightmost entry: descend from the max-client root through the max-client
 // child until a leaf (YATA order of an origin-only tree, SURVEY.md §7 hard part 2)
-__global__ void k_winner_walk(Work w) {
+// (a descent visits every segment at most once: more hops than segments is a cycle, an error)
+__global__ void k_winner_walk(Work w, uint32_t nsegs) {
   const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
   if (k >= w.cap_keys) return;
   const uint32_t r = w.k_rootmax[k];
   if (!r) { w.k_winner[k] = NONE; return; }
   uint32_t x = r - 1;
-  for (uint32_t it = 0; it < (1u << 24); ++it) {
+  bool leaf = false;
+  for (uint32_t it = 0; it <= nsegs; ++it) {
     const uint32_t m = w.g_maxchild[x];
-    if (!m) break;
+    if (!m) { leaf = true; break; }
     x = m - 1;
   }
+  if (!leaf) { raise_err(&w.ctr->err, ERR_DECODE); return; }
   w.k_winner[k] = x;
   w.g_flags[x] |= SEG_WIN;  // one winner per key: the only writer of x's flags in this kernel
 }
@@ -429,7 +432,7 @@ __global__ void k_overwrite(Work w, uint32_t nsegs) {
 
 uint32_t run_descent(const Work& w, uint32_t nsegs, hipStream_t s, bool fold) {
   if (!nsegs) return 0;
-  hipLaunchKernelGGL(k_winner_walk, dim3(w.cap_keys / 256 + 1), dim3(256), 0, s, w);
+  hipLaunchKernelGGL(k_winner_walk, dim3(w.cap_keys / 256 + 1), dim3(256), 0, s, w, nsegs);
   if (!fold) hipLaunchKernelGGL(k_overwrite, dim3((nsegs + 255) / 256), dim3(256), 0, s, w, nsegs);
   return 1;
 }
@@ -454,7 +457,7 @@ __global__ void k_dead_climb(Work w) {
   const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
   if (k >= w.cap_keys || w.k_hash[k] == 0 || (w.k_flags[k] & KF_DEAD)) return;
   uint32_t x = k;
-  for (uint32_t depth = 0; depth < (1u << 20); ++depth) {
+  for (uint32_t depth = 0; depth <= w.cap_keys; ++depth) {  // deeper than the key count: a cycle
     const uint32_t pu = w.k_parent[x];
     if (pu == NONE) return;  // a root type: alive
     const uint32_t pk = w.g_key[seg_of(w.u_cutbits, w.u_wpre, pu)];
@@ -462,6 +465,7 @@ __global__ void k_dead_climb(Work w) {
     if (w.k_flags[pk] & KF_DEAD) { atomicOr(&w.k_flags[k], KF_DEAD); return; }
     x = pk;
   }
+  raise_err(&w.ctr->err, ERR_DECODE);
 }
 __global__ void k_dead_apply(Work w, uint32_t nsegs) {
   const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
@@ -546,13 +550,15 @@ __global__ void k_key_shard(Work w, uint32_t nshards, uint32_t* __restrict__ key
   if (k >= w.cap_keys) return;
   if (w.k_hash[k] == 0) { key_shard[k] = 0; return; }
   uint32_t x = k;  // climb to the top-level list: parent item -> the list that holds it
-  for (uint32_t depth = 0; depth < (1u << 20); ++depth) {
+  bool top = false;
+  for (uint32_t depth = 0; depth <= w.cap_keys; ++depth) {  // deeper than the key count: a cycle
     const uint32_t pu = w.k_parent[x];
-    if (pu == NONE) break;
+    if (pu == NONE) { top = true; break; }
     const uint32_t pk = w.g_key[seg_of(w.u_cutbits, w.u_wpre, pu)];
-    if (pk == NONE || pk == x) break;
+    if (pk == NONE || pk == x) { top = true; break; }
     x = pk;
   }
+  if (!top) raise_err(&w.ctr->err, ERR_DECODE);
   key_shard[k] = shard_of_hash(w.k_hash[x], nshards);
 }
 __global__ void k_seg_shard(Work w, uint32_t nsegs, const uint32_t* __restrict__ key_shard, uint8_t* __restrict__ owner) {

@@ -697,17 +697,19 @@ __global__ __launch_bounds__(256) void k_tclimb(Work w, uint32_t nsegs) {
   const uint32_t fc = w.t_first[s];
   if (fc != NONE) { w.g_right[s] = fc; return; }
   uint32_t y = s, res = NONE;
-  for (uint32_t it = 0; it < (1u << 26); ++it) {
+  bool end = false;
+  for (uint32_t it = 0; it <= nsegs; ++it) {  // more hops than segments: an origin cycle
     const uint32_t ns = w.t_nsib[y];
-    if (ns != NONE) { res = ns; break; }
+    if (ns != NONE) { res = ns; end = true; break; }
     const uint32_t z = w.t_jump[y];  // an ancestor whose answer is y's (every node between has no next sibling)
-    if (z == NONE) break;            // a last child of the list's root: the end of the list
+    if (z == NONE) { end = true; break; }  // a last child of the list's root: the end of the list
     if (w.t_nsib[z] == NONE) {       // path halving: y inherits z's link
       const uint32_t zz = w.t_jump[z];
       if (zz != z) w.t_jump[y] = zz;
     }
     y = z;
   }
+  if (!end) raise_err(&w.ctr->err, ERR_DECODE);
   w.g_right[s] = res;
 }
 

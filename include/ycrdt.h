@@ -184,6 +184,13 @@ int ycrdt_batch_stage_docs(ycrdt_engine *e, const ycrdt_buf *ups, const uint32_t
                            ycrdt_batch **out);
 /* updates[ndocs] (and state_vectors[ndocs] unless NULL) receive every document's encoded state */
 int ycrdt_batch_result_docs(ycrdt_batch *b, ycrdt_out *updates, ycrdt_out *state_vectors);
+/* The same results packed back to back in caller memory, split per document on the device (one
+ * HBM buffer, one pipelined D2H through pinned staging; no per-document allocation): document d's
+ * encodeStateAsUpdate is dst[offs[2d] .. offs[2d+1]) and its encodeStateVector dst[offs[2d+1] ..
+ * offs[2d+2]); offs holds 2*ndocs+1 entries, *total = offs[2*ndocs]. dst == NULL only fills offs /
+ * total (size query); cap < total is YCRDT_E_ARG. A sync responder / LevelDB writer hands the
+ * slices on as they are (crdt.js:260,288 send Y.encodeStateAsUpdate bytes; crdt.js:79-98 store). */
+int ycrdt_batch_result_docs_packed(ycrdt_batch *b, uint8_t *dst, uint64_t cap, uint64_t *offs, uint64_t *total);
 /* one-shot form of the two above (host buffers in and out) */
 int ycrdt_merge_docs(ycrdt_engine *e, const ycrdt_buf *ups, const uint32_t *doc_of, size_t n, uint32_t ndocs,
                      ycrdt_out *updates, ycrdt_out *state_vectors);
@@ -207,6 +214,23 @@ int ycrdt_debug_replay(const ycrdt_buf *ups, size_t n, ycrdt_merge_fn merge, voi
 int ycrdt_comm_unique_id(uint8_t id[YCRDT_COMM_ID_BYTES]);
 int ycrdt_comm_create(ycrdt_engine *e, int nranks, int rank, const uint8_t id[YCRDT_COMM_ID_BYTES], ycrdt_comm **out);
 void ycrdt_comm_destroy(ycrdt_comm *c);
+/* A communicator over the caller's own transport: the library's exchanges run their collectives
+ * through these host callbacks instead of RCCL (device buffers are staged through host memory).
+ * Each callback returns 0 on success; every rank must make the same calls in the same order. Used
+ * by hosts without RCCL between their processes (and by the world-size-2 gloo tests, two processes
+ * on one GPU). */
+typedef struct {
+  void *ctx;
+  /* in place over n host words of every rank: op 0 = sum, 1 = max */
+  int (*allreduce_u32)(void *ctx, uint32_t *words, size_t n, int op);
+  /* recv[r * bytes .. (r + 1) * bytes) = rank r's send (bytes is the same on every rank) */
+  int (*allgather)(void *ctx, const uint8_t *send, size_t bytes, uint8_t *recv);
+} ycrdt_exchange;
+int ycrdt_comm_create_exchange(ycrdt_engine *e, int nranks, int rank, const ycrdt_exchange *x, ycrdt_comm **out);
+/* Stable owner rank of a document / topic id (crdt.js:221,235: one Y.Doc per topic): the same on
+ * every rank, process and run (64-bit FNV-1a of the id bytes, mixed, mod world). A fleet routes
+ * every update of a topic to its owner, which merges it alone (weak scaling, no data collective). */
+uint32_t ycrdt_route(const uint8_t *id, size_t len, uint32_t world);
 /* Key-hash sharded merge of ONE document (C4): every rank stages the same updates; the integrate
  * phases (map winner, YATA, dead types, merge adjacency) run for the rank's shard only — lists
  * owned by hash(top-level entry) % nshards — and the per-segment flag words are summed over RCCL;
@@ -217,6 +241,15 @@ int ycrdt_batch_merge_sharded(ycrdt_batch *b, ycrdt_comm *comm, uint32_t nshards
 /* State vector of the union of what the ranks hold of one document (crdt.js:239,289 exchange):
  * all-gather + max per client, descending client order. */
 int ycrdt_comm_sv_allreduce_max(ycrdt_comm *c, ycrdt_engine *e, ycrdt_buf sv, ycrdt_out *out);
+/* Fleet state vectors (C5; crdt.js:239,289 per topic, batched over the fleet): this rank holds n
+ * documents (ids docs[i] < 0xFFFFFFFF, state vectors svs[i]) — any subset of the fleet. Every rank
+ * receives, for each document ANY rank holds, the state vector of the union (max clock per client,
+ * descending client order): *doc_ids = u32[m] ascending, *offs = u64[m + 1], document doc_ids[j]'s
+ * state vector = blob[offs[j] .. offs[j+1]). One dense all-reduce(MAX) over the fleet's sorted
+ * (document, client) key space, built on the device (sort, reduce, all-gather of distinct keys,
+ * unique). Release the three outputs with ycrdt_free. */
+int ycrdt_comm_fleet_sv_allreduce_max(ycrdt_comm *c, ycrdt_engine *e, const uint32_t *docs, const ycrdt_buf *svs, size_t n,
+                                      ycrdt_out *doc_ids, ycrdt_out *offs, ycrdt_out *blob);
 /* Delete sets of all ranks (each a delete-set-only or full update) all-gathered and merged with the
  * engine's HIP mergeUpdates (the delete-set union): every rank receives the same update. */
 int ycrdt_comm_ds_allgather(ycrdt_comm *c, ycrdt_engine *e, ycrdt_buf update, ycrdt_out *out);

@@ -1,4 +1,10 @@
-"""Doc-fleet sharding and the cross-rank exchange steps.
+"""TEST REFERENCE (not product code): a torch restatement of the fleet exchanges that libycrdt
+implements natively (crdt_amd/csrc/yc_comm.hip: ycrdt_comm_fleet_sv_allreduce_max,
+ycrdt_comm_ds_allgather, ycrdt_route). tests/test_fleet.py runs it as world-size-2 gloo groups on
+CPU to pin the exchange rules against the oracle; tests/test_gpu_exchange.py runs the library's own
+exchanges the same way (host exchange over gloo) and compares.
+
+Doc-fleet sharding and the cross-rank exchange steps.
 
 One process per GPU. Documents (crdt.js topics) are independent, so the merge itself needs no
 collective: `shard_of` routes every update of a doc to one rank, which merges its docs on its own

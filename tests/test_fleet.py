@@ -1,5 +1,6 @@
-"""The N>1 path on CPU: doc routing and the two cross-rank exchange steps of crdt_amd/fleet.py,
-run as world_size-2 gloo process groups (the GPU box runs the same code over RCCL).
+"""The N>1 path on CPU: doc routing (the library's ycrdt_route, host-only) and the two cross-rank
+exchange rules, restated in torch (tests/fleet_ref.py), run as world_size-2 gloo process groups;
+tests/test_gpu_exchange.py runs libycrdt's native exchanges over the same kind of group.
 
 * sv_allreduce_max: every doc's updates are split over the ranks (ingest not routed); the
   all-reduced state vectors must equal the oracle's encodeStateVector of a doc that applied ALL
@@ -16,7 +17,7 @@ import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
-from crdt_amd import fleet
+from tests import fleet_ref as fleet
 
 
 def _free_port():
@@ -86,12 +87,20 @@ def _worker(rank, world, port, q):
 
 
 def test_route_is_stable_and_total():
-    items = [(f"topic{i}", b"u") for i in range(1000)]
-    parts = fleet.route(items, 8)
-    assert sum(len(p) for p in parts) == 1000
-    assert all(60 < len(p) < 190 for p in parts)  # roughly balanced
-    assert fleet.shard_of("topic17", 8) == fleet.shard_of(b"topic17", 8)
-    assert [fleet.shard_of(f"topic{i}", 8) for i in range(50)] == [fleet.shard_of(f"topic{i}", 8) for i in range(50)]
+    """libycrdt's ycrdt_route (host-only, no GPU): in range, balanced, stable, str == bytes."""
+    import crdt_amd
+
+    for world in (1, 2, 3, 8):
+        ranks = [crdt_amd.route(f"topic{i}", world) for i in range(4000)]
+        assert all(0 <= r < world for r in ranks)
+        counts = [ranks.count(r) for r in range(world)]
+        assert min(counts) > 0.8 * 4000 / world and max(counts) < 1.2 * 4000 / world, counts
+    assert crdt_amd.route("topic17", 8) == crdt_amd.route(b"topic17", 8)
+    # pinned values: the routing of a topic must not change between releases (a fleet's doc owners)
+    assert [crdt_amd.route(f"topic{i}", 8) for i in range(12)] == ROUTE_PINNED
+
+
+ROUTE_PINNED = [6, 0, 5, 1, 4, 0, 5, 7, 1, 6, 4, 7]  # FNV-1a 64 + fmix64, mod 8
 
 
 def test_sv_codec_roundtrip():
@@ -148,20 +157,3 @@ def test_exchange_world2_gloo():
         want = merge_delete_sets([ds])
         assert union == [[c, k, n] for c in sorted(want) for k, n in want[c]], rank
     assert res[0][1] == res[1][1]
-
-
-@pytest.mark.gpu
-def test_exchange_rccl_world1_on_gpu():
-    """The same exchange on cuda tensors over RCCL (backend "nccl"), world 1 on the one-GPU box."""
-    torch.cuda.set_device(0)
-    dist.init_process_group("nccl", rank=0, world_size=1, init_method=f"tcp://127.0.0.1:{_free_port()}")
-    try:
-        svs = {0: fleet.encode_sv({5: 3, 2 ** 32 - 1: 9}), 3: fleet.encode_sv({1: 1})}
-        got = fleet.sv_allreduce_max(svs)
-        assert got == svs
-        r = torch.tensor([[9, 0, 3], [9, 3, 2], [9, 10, 1], [2 ** 32 - 1, 5, 6]], dtype=torch.int64)
-        u = fleet.ds_allgather(r)
-        assert u.device.type == "cuda"
-        assert u.tolist() == [[9, 0, 5], [9, 10, 1], [2 ** 32 - 1, 5, 6]]
-    finally:
-        dist.destroy_process_group()

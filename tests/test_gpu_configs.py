@@ -4,7 +4,8 @@ from Yjs 13.5.16 itself (tests/golden/configs.json, gen_config_fixtures.js):
 * C3: one YArray edited by 8-16 replicas (push / unshift / insert / cut, gossip rounds) — YATA;
 * C4: YMap keys holding nested YArrays, 10 % of keys overwritten (nested GC), 6-12 replicas;
 * C5: 60 small docs of 2-4 clients with lagging peer state vectors — the delta the sync responder
-  sends (crdt.js:286-291) and the fleet state-vector exchange (crdt_amd/fleet.py).
+  sends (crdt.js:286-291) and the fleet state-vector exchange (libycrdt's
+  ycrdt_comm_fleet_sv_allreduce_max over RCCL).
 """
 import json
 import os
@@ -59,41 +60,32 @@ def test_gpu_config_merge_updates_then_apply():
         _check(d, c)
 
 
-def _fleet_worker(port, q):
-    """torch / RCCL first, then the engine — the order bench.py's ranks use."""
-    import torch
-    import torch.distributed as dist
-
-    from crdt_amd import fleet
-
-    torch.cuda.set_device(0)
-    dist.init_process_group("nccl", rank=0, world_size=1, init_method=f"tcp://127.0.0.1:{port}")
+def _fleet_worker(q):
+    """A fresh process: libycrdt's own RCCL communicator (world 1), the native fleet exchange."""
+    cases = _cases("c5_")
+    eng = crdt_amd.Engine()
+    svs = {}
+    for i, c in enumerate(cases):
+        d = crdt_amd.Doc(client_id=0x7FFFFFF0, engine=eng)
+        d.apply_updates([bytes.fromhex(u) for u in c["updates"]])
+        svs[3 * i + 1] = d.encode_state_vector()
+    comm = crdt_amd.Comm(eng, 1, 0, crdt_amd.Comm.unique_id())
     try:
-        cases = _cases("c5_")
-        svs = {}
-        for i, c in enumerate(cases):
-            d = crdt_amd.Doc(client_id=0x7FFFFFF0)
-            d.apply_updates([bytes.fromhex(u) for u in c["updates"]])
-            svs[i] = d.encode_state_vector()
-        got = fleet.sv_allreduce_max(svs)
-        q.put([(got[i].hex(), c["sv"], c["name"]) for i, c in enumerate(cases)])
+        got = comm.fleet_sv_allreduce_max(svs)
     finally:
-        dist.destroy_process_group()
+        comm.close()
+    q.put([(got.get(3 * i + 1, b"").hex(), c["sv"], c["name"]) for i, c in enumerate(cases)] + [(sorted(got), sorted(svs), "ids")])
 
 
 def test_gpu_config_fleet_state_vectors():
-    """C5 fleet: each doc merged on the GPU, its state vector through the fleet all-reduce (world 1
-    over RCCL, in a fresh process) equals Yjs's."""
+    """C5 fleet: each doc merged on the GPU, its state vector through libycrdt's native fleet
+    all-reduce (ycrdt_comm_fleet_sv_allreduce_max, world 1 over RCCL, in a fresh process) equals
+    Yjs's."""
     import multiprocessing as mp
-    import socket
 
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    port = s.getsockname()[1]
-    s.close()
     ctx = mp.get_context("spawn")
     q = ctx.SimpleQueue()
-    p = ctx.Process(target=_fleet_worker, args=(port, q))
+    p = ctx.Process(target=_fleet_worker, args=(q,))
     p.start()
     p.join(180)
     assert p.exitcode == 0, p.exitcode

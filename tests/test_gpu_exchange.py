@@ -1,0 +1,128 @@
+"""libycrdt's multi-rank exchanges at world size 2: two processes on the one GPU, each with its own
+engine, joined by a torch.distributed gloo group that carries the library's collectives through
+the host exchange (ycrdt_comm_create_exchange; RCCL is the same code with device buffers). The
+library's own code runs on both ranks — shard export, the pre-exchange status agreement, the flag
+sum, the fleet key-space build and MAX all-reduce, the delete-set all-gather — and every result is
+checked against Yjs fixtures / the unsharded merge:
+
+* sharded merge of ONE document (C4 shape): each rank integrates its key-hash shard,
+  the flag words are summed, and both ranks encode bytes equal to the unsharded merge (Yjs state);
+* fleet state vectors (C5): each rank merges a different part of every document's updates; the
+  exchanged state vectors equal Yjs's state vectors of the whole documents;
+* delete-set all-gather: each rank's part of a document; the union equals the delete set of
+  Y.mergeUpdates over all parts;
+* a rank that fails before the exchange makes the other rank's call fail too (no hang).
+"""
+import json
+import os
+import socket
+
+import pytest
+
+crdt_amd = pytest.importorskip("crdt_amd")
+
+pytestmark = pytest.mark.gpu
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _cases(prefix):
+    with open(os.path.join(HERE, "golden", "configs.json")) as f:
+        return [c for c in json.load(f)["cases"] if c["name"].startswith(prefix)]
+
+
+def _worker(rank, world, port, q):
+    import torch.distributed as dist
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    out = {"rank": rank}
+    try:
+        import sys
+
+        sys.path.insert(0, os.path.dirname(HERE))
+        from crdt_amd.workload import gen_nested
+        from tests.v1util import delete_set_of
+
+        eng = crdt_amd.Engine()
+        comm = crdt_amd.Comm.over_torch(eng)
+        # ---- sharded merge of one document: every C4 fixture + a generated C4 history
+        docs = [[bytes.fromhex(u) for u in c["updates"]] for c in _cases("c4_")]
+        docs.append(gen_nested(40, 1500, 200, seed=5)[0])
+        shard_ok = []
+        for ups in docs:
+            b = crdt_amd.Batch(ups, eng)
+            b.merge_sharded(world, comm)
+            got = b.result()
+            b.merge()
+            shard_ok.append(got == b.result())
+            del b
+        out["shard"] = shard_ok
+        # ---- fleet state vectors: rank r holds the updates u[i] with i % world == r of every C5 doc
+        c5 = _cases("c5_")
+        svs = {}
+        for j, c in enumerate(c5):
+            mine = [bytes.fromhex(u) for i, u in enumerate(c["updates"]) if i % world == rank]
+            d = crdt_amd.Doc(client_id=0x7FFFFFF0, engine=eng)
+            d.apply_updates(mine)
+            if mine or j % 3:  # some documents only on some ranks
+                svs[7 * j + 2] = d.encode_state_vector()
+        fleet = comm.fleet_sv_allreduce_max(svs)
+        out["fleet"] = [(fleet.get(7 * j + 2, b"").hex(), c["sv"]) for j, c in enumerate(c5)]
+        # ---- delete-set all-gather: each rank's part of every C3 / C4 fixture (Y.mergeUpdates of its
+        # replicas' states); the union is the delete set of Y.mergeUpdates over all of them
+        ds_ok = []
+        for c in _cases("c3_") + _cases("c4_"):
+            ups = [bytes.fromhex(u) for u in c["updates"]]
+            mine = crdt_amd.merge_updates([u for i, u in enumerate(ups) if i % world == rank], eng)
+            union = comm.ds_allgather(mine)
+            ds_ok.append(delete_set_of(union) == delete_set_of(crdt_amd.merge_updates(ups, eng)))
+        out["ds"] = ds_ok
+        # ---- failure before the exchange on rank 1: both ranks get an error, nobody hangs
+        ups = docs[0]
+        bad = [b"\x01\xff\xff"] if rank == 1 else []
+        try:
+            b = crdt_amd.Batch(ups + bad, eng)
+            b.merge_sharded(world, comm)
+            out["fail"] = "no error"
+        except crdt_amd.YcrdtError as e:
+            out["fail"] = e.kind
+        comm.close()
+    except Exception as e:  # noqa: BLE001 — reported to the parent
+        out["error"] = repr(e)
+    finally:
+        q.put(out)
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(300)
+def test_exchanges_world2_gloo_one_gpu():
+    import multiprocessing as mp
+
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.SimpleQueue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(240)
+    codes = [p.exitcode for p in procs]
+    res = sorted([q.get() for _ in range(world)], key=lambda r: r["rank"])
+    assert codes == [0, 0], (codes, res)
+    for r in res:
+        assert "error" not in r, r
+        assert all(r["shard"]), r["shard"]
+        for got, want in r["fleet"]:
+            assert got == want
+        assert all(r["ds"]), r["ds"]
+        assert r["fail"] != "no error", r
+    assert res[0]["fleet"] == res[1]["fleet"]

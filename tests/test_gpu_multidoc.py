@@ -55,6 +55,43 @@ def test_multidoc_shared_clients_and_batch_api():
         mb.result_docs()
 
 
+def test_multidoc_packed_result_golden_and_large(golden):
+    """ycrdt_batch_result_docs_packed: the device-side split packed back to back in one host array
+    (pipelined D2H) gives every document's Yjs state and state vector; a multi-chunk batch (the
+    112-document C2 shape, reduced) equals the per-document result."""
+    from crdt_amd.workload import gen_map
+
+    cases = [c for s in ("kat", "map", "array", "nested") for c in golden[s]]
+    docs = [[bytes.fromhex(u) for u in c["updates"]] for c in cases]
+    docs.insert(2, [])
+    b = crdt_amd.Batch(docs=docs)
+    b.merge()
+    blob, offs = b.result_docs_packed()
+    assert len(offs) == 2 * len(docs) + 1 and int(offs[-1]) == len(blob)
+    got = [(bytes(blob[offs[2 * d]:offs[2 * d + 1]]), bytes(blob[offs[2 * d + 1]:offs[2 * d + 2]])) for d in range(len(docs))]
+    assert got[2] == (b"\x00\x00", b"\x00")
+    for c, (u, sv) in zip(cases, got[:2] + got[3:]):
+        assert u.hex() == c["state"], c["name"]
+        assert sv.hex() == c["sv"], c["name"]
+    big = [gen_map(n_keys=20000, n_replicas=200, ops_per_replica=400, seed=700 + i)[0] for i in range(6)]
+    os.environ["YCRDT_PIN_CHUNK"] = "65536"  # staging waves in both halves on a few MB
+    try:
+        b = crdt_amd.Batch(docs=big)
+        b.merge()
+        blob, offs = b.result_docs_packed()
+    finally:
+        del os.environ["YCRDT_PIN_CHUNK"]
+    assert len(blob) > 2 * 16 * 65536
+    per = b.result_docs()
+    for d in range(len(big)):
+        assert bytes(blob[offs[2 * d]:offs[2 * d + 1]]) == per[d][0]
+        assert bytes(blob[offs[2 * d + 1]:offs[2 * d + 2]]) == per[d][1]
+    one = crdt_amd.Batch(big[0])
+    one.merge()
+    blob1, offs1 = one.result_docs_packed()
+    assert (bytes(blob1[:offs1[1]]), bytes(blob1[offs1[1]:offs1[2]])) == one.result()
+
+
 # ---------------------------------------------------------------- fleet ingest (apply_updates_multi)
 def _interleaved(cases, rng):
     """(doc index, update) pairs of every case, interleaved across documents, per-doc order kept."""
