@@ -51,7 +51,7 @@ def parse():
     p.add_argument("--port-replicas", type=int, default=1000, help="replicas in the oracle-port timing sample")
     p.add_argument("--profile-phases", action="store_true")
     p.add_argument("--no-per-op", action="store_true", help="skip the crdt.js per-op leg")
-    p.add_argument("--fleet-docs", type=int, default=100_000, help="documents in the C5 fleet-ingest leg (0 = skip)")
+    p.add_argument("--fleet-docs", type=int, default=1_000_000, help="documents in the C5 fleet-ingest leg (0 = skip)")
     p.add_argument("--no-c4", action="store_true", help="skip the single-GPU C4 leg")
     p.add_argument("--c4-sharded", action="store_true",
                    help="with --gpus N > 1: C4 key-hash sharded across the ranks over RCCL (opt-in)")
@@ -381,13 +381,14 @@ def billion_leg(eng, cfg, gen_map, n_docs, reps=3):
 
 
 def c4_leg(eng, reps=3):
-    """C4 (BASELINE configs[3], nested YArrays under YMap keys) on one GPU: the full document
-    (crdt_amd/workload C4: 2 000 replicas x 10 000 ops on 100 k nested arrays, ~47 M items, base
-    snapshot, overwrites that GC whole arrays, deletes) merged in one device pass, and the same
-    merge as 8 logical key-hash shards (each shard's integrate phases run in turn, flag words summed
-    as the RCCL all-reduce would) — byte-identical to the unsharded result."""
+    """C4 (BASELINE configs[3], nested YArrays under YMap keys) on one GPU at BASELINE scale: the
+    whole document (crdt_amd/workload C4_FULL: 1 M keys, 64 replicas, ~100 items per nested array,
+    102 M items, base snapshot, ~10 % of keys overwritten by a fresh array — nested GC —, deletes)
+    merged in one device pass; the merge of the reversed update list and of its own output give the
+    same bytes; and the same merge as 8 logical key-hash shards (each shard's integrate phases run
+    in turn, flag words summed as the RCCL all-reduce would) — byte-identical to the unsharded result."""
     import crdt_amd
-    from crdt_amd.workload import C4, gen_nested
+    from crdt_amd.workload import C4_FULL as C4, gen_nested
 
     t0 = time.perf_counter()
     ups, st = gen_nested(**C4)
@@ -407,8 +408,19 @@ def c4_leg(eng, reps=3):
     b.merge_sharded(8)
     sh_ms = (time.perf_counter() - t0) * 1e3
     same = b.result() == full
-    return {"workload": "C4: YMap 'docs' of 100 000 nested YArrays, 2 000 replicas x 10 000 ops (push 93 %, "
-                        "overwrite with a new array 2 %, delete 5 %), base snapshot",
+    del b
+    rb = crdt_amd.Batch(list(reversed(ups)), eng)
+    rb.merge()
+    rev_ok = rb.result() == full
+    del rb
+    ib = crdt_amd.Batch([full[0]], eng)
+    ib.merge()
+    idem_ok = ib.result() == full
+    del ib
+    return {"workload": f"C4 (BASELINE scale): YMap 'docs' of {C4['n_keys']} nested YArrays, {C4['n_replicas']} replicas x "
+                        f"{C4['pushes']} ops (push of 1-4 values, overwrite with a new array {C4['p_over']:.2%}, delete "
+                        f"{C4['p_del']:.0%}), base snapshot",
+            "order_independent": rev_ok, "idempotent": idem_ok,
             "updates": len(ups), "input_bytes": sum(len(u) for u in ups), "items": s1.items, "structs": s1.structs,
             "segments": s1.segments, "output_bytes": len(full[0]), "ms_per_merge": round(ms, 3),
             "items_per_s": round(s1.items / (ms * 1e-3), 1), "phases_ms": phases,
@@ -465,24 +477,36 @@ def fleet_ingest_leg(eng, n_docs):
             idx.append(d)
             ups.append(u)
     in_bytes = sum(len(u) for u in ups)
+    import numpy as np
+
+    idx_np = np.asarray(idx, dtype=np.int64)
     reps, ms = 2, []
     docs = None
     for _ in range(reps):
         docs = [crdt_amd.Doc(client_id=0x7FFFFFF0, engine=eng) for _ in range(n_docs)]
         t0 = time.perf_counter()
-        crdt_amd.apply_updates_multi([docs[i] for i in idx], ups, engine=eng)
+        crdt_amd.apply_updates_multi(docs, ups, engine=eng, doc_index=idx_np)
         ms.append((time.perf_counter() - t0) * 1e3)
     gpu_ms = min(ms)
+    # every document's state and state vector in one call (ycrdt_docs_states_packed): one gather on
+    # the device, one pipelined D2H
+    r0 = time.perf_counter()
+    blob, offs = crdt_amd.states_packed(docs, eng)
+    read_ms = (time.perf_counter() - r0) * 1e3
+    mv = memoryview(blob)
     parity = True
     h = hashlib.sha256()
     from tests.v1util import canonical_update
     for d in range(n_docs):
         c = cases[d % len(cases)]
-        st = docs[d].encode_state_as_update()
-        h.update(hashlib.sha256(canonical_update(st)).digest())
+        st = mv[int(offs[2 * d]):int(offs[2 * d + 1])]
         if d < len(cases) or d % 4099 == 0:
-            parity = parity and st.hex() == c["state"] and docs[d].encode_state_vector().hex() == c["sv"]
+            # the engine writes the canonical (13.6) order, so the Yjs side's canonical form is the state itself
+            parity = parity and bytes(st).hex() == c["state"] and canonical_update(bytes(st)) == bytes(st)
+            parity = parity and bytes(mv[int(offs[2 * d + 1]):int(offs[2 * d + 2])]).hex() == c["sv"]
+        h.update(hashlib.sha256(st).digest())
     res = {"docs": n_docs, "updates": len(ups), "in_bytes": in_bytes, "ms": round(gpu_ms, 2),
+           "read_all_states_ms": round(read_ms, 2), "out_bytes": int(offs[-1]),
            "docs_per_s": round(n_docs / (gpu_ms * 1e-3), 1), "updates_per_s": round(len(ups) / (gpu_ms * 1e-3), 1),
            "calls": 1, "parity": parity,
            "includes": "ctypes + host validation + H2D + one multi-document merge + per-document split in HBM, 1 GPU"}
@@ -666,22 +690,23 @@ def main():
     value = items_step * args.steps / dt
     phases = [(n, m / args.steps) for n, m in phase_acc.items()]
 
-    # ---- roofline of the dominant kernel: k_children (YMap winner / merge adjacency), the longest
-    # single-kernel phase of the C2 merge ("merge.winner" holds exactly that one launch; its HIP
-    # events are recorded on the engine stream the kernel runs on). Algorithmic bytes per segment
-    # (DESIGN.md §Roofline): flags, origin segment, origin unit and client index read once (16 B)
-    # plus two 4-byte read-modify-write atomics (max child, min child: 8 B) = 24 B. `traffic` is the
-    # HBM bytes per launch from the committed rocprofv3 PMC pass (2 x FETCH_SIZE + WRITE_SIZE,
-    # gfx950 correction; scripts/pmc.sh + scripts/pmc_summary.py).
+    # ---- roofline of the dominant kernel: k_resolve (key resolution + YMap winner settling), the
+    # longest single-kernel phase of the C2 merge ("merge.resolve" holds exactly that one launch; its
+    # HIP events are recorded on the engine stream the kernel runs on). Algorithmic bytes per segment
+    # (DESIGN.md §5.1): its flags, key word, origin link and origin unit read (16 B), its flags and
+    # final key written (8 B), and the winner slot of its origin read-modify-written (4 B) = 28 B.
+    # `traffic` is the HBM bytes per launch from the committed rocprofv3 PMC pass (2 x FETCH_SIZE +
+    # WRITE_SIZE, gfx950 correction; scripts/pmc.sh + scripts/pmc_summary.py).
+    ROOF_KERNEL, ROOF_PHASE, ROOF_B = "yc::k_resolve", "merge.resolve", 28
     ph = dict(phases)
-    k_ms = ph.get("merge.winner", 0.0)
-    alg = 24 * st.segments
+    k_ms = ph.get(ROOF_PHASE, 0.0)
+    alg = ROOF_B * st.segments
     traffic, traffic_src = None, None
     pmc = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_c2_pmc.csv")))
     if pmc:
         with open(pmc[-1]) as f:
             for r in csv.DictReader(f):
-                if r["kernel"] == "yc::k_children":
+                if r["kernel"] == ROOF_KERNEL:
                     traffic = int(float(r["hbm_bytes"]))
                     traffic_src = os.path.basename(pmc[-1])
     # the whole merge's counter traffic from the same PMC pass (sum over its kernels, per merge)
@@ -693,7 +718,7 @@ def main():
     dominant = max(phases, key=lambda p: p[1]) if phases else ("merge", st.device_ms)
     roofline = {
         "bound": "hbm",
-        "kernel": "yc::k_children",
+        "kernel": ROOF_KERNEL,
         "achieved": round(achieved, 2),
         "peak": HBM_PEAK_GBS,
         "unit": "GB/s",
@@ -702,7 +727,7 @@ def main():
         "traffic_unit": "HBM bytes per launch",
         "traffic_source": traffic_src,
         "alg_bytes_per_launch": alg,
-        "alg_bytes_per_unit": "24 B per segment",
+        "alg_bytes_per_unit": f"{ROOF_B} B per segment",
         "avg_launch_ms": round(k_ms, 4),
         "largest_phase": {"name": dominant[0], "ms": round(dominant[1], 4)},
     }

@@ -81,14 +81,14 @@ EXPORTS = (
     "ycrdt_encode_state_as_update", "ycrdt_encode_state_vector", "ycrdt_doc_last_stats",
     "ycrdt_batch_stage", "ycrdt_batch_merge", "ycrdt_batch_result", "ycrdt_batch_destroy",
     "ycrdt_merge_updates", "ycrdt_diff_update", "ycrdt_diff_updates", "ycrdt_free", "ycrdt_last_error", "ycrdt_version",
-    "ycrdt_doc_json", "ycrdt_map_set", "ycrdt_map_set_type", "ycrdt_map_delete", "ycrdt_array_insert",
+    "ycrdt_doc_json", "ycrdt_type_json", "ycrdt_map_entries", "ycrdt_map_set", "ycrdt_map_set_type", "ycrdt_map_delete", "ycrdt_array_insert",
     "ycrdt_array_delete", "ycrdt_doc_client_id", "ycrdt_map_type_at", "ycrdt_doc_take_local_update",
     "ycrdt_doc_flush", "ycrdt_doc_pending", "ycrdt_doc_track_local", "ycrdt_validate_update", "ycrdt_debug_replay",
     "ycrdt_batch_stage_docs", "ycrdt_batch_result_docs", "ycrdt_batch_result_docs_packed", "ycrdt_merge_docs",
     "ycrdt_map_get", "ycrdt_map_size", "ycrdt_array_length", "ycrdt_array_get", "ycrdt_apply_updates_multi",
     "ycrdt_comm_unique_id", "ycrdt_comm_create", "ycrdt_comm_destroy", "ycrdt_batch_merge_sharded",
     "ycrdt_comm_sv_allreduce_max", "ycrdt_comm_ds_allgather", "ycrdt_comm_create_exchange", "ycrdt_route",
-    "ycrdt_comm_fleet_sv_allreduce_max",
+    "ycrdt_comm_fleet_sv_allreduce_max", "ycrdt_docs_states_packed",
 )
 
 MERGE_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p)
@@ -144,6 +144,8 @@ def lib():
     L.ycrdt_free.argtypes = [P(_Out)]
     cs = ctypes.c_char_p
     L.ycrdt_doc_json.argtypes = [vp, cs, i32, P(_Out)]
+    L.ycrdt_type_json.argtypes = [vp, cs, cs, i32, P(_Out)]
+    L.ycrdt_map_entries.argtypes = [vp, cs, cs, P(_Out)]
     L.ycrdt_map_type_at.argtypes = [vp, cs, cs, P(i32)]
     L.ycrdt_map_set.argtypes = [vp, cs, cs, cs, ctypes.c_char_p, sz]
     L.ycrdt_map_set_type.argtypes = [vp, cs, cs, cs, u32]
@@ -160,6 +162,7 @@ def lib():
     L.ycrdt_comm_sv_allreduce_max.argtypes = [vp, vp, _Buf, P(_Out)]
     L.ycrdt_comm_ds_allgather.argtypes = [vp, vp, _Buf, P(_Out)]
     L.ycrdt_comm_create_exchange.argtypes = [vp, i32, i32, P(_Exchange), P(vp)]
+    L.ycrdt_docs_states_packed.argtypes = [vp, P(vp), sz, vp, ctypes.c_uint64, P(ctypes.c_uint64), P(ctypes.c_uint64)]
     L.ycrdt_route.argtypes = [ctypes.c_char_p, sz, u32]
     L.ycrdt_route.restype = u32
     L.ycrdt_comm_fleet_sv_allreduce_max.argtypes = [vp, vp, P(u32), P(_Buf), sz, P(_Out), P(_Out), P(_Out)]
@@ -318,6 +321,13 @@ class Doc:
         """YMap.toJSON / YArray.toJSON of root `name` (kind "map" | "array") as JSON text."""
         out = _Out()
         _check(lib().ycrdt_doc_json(self._h, name.encode(), 0 if kind == "map" else 1, ctypes.byref(out)))
+        return _take(out).decode()
+
+    def type_json(self, root: str, kind: str, parent_key: str = None) -> str:
+        """toJSON of the root type, or of the YMap / YArray stored in root map `root`[parent_key]
+        (only that type's own list is read)."""
+        out = _Out()
+        _check(lib().ycrdt_type_json(self._h, root.encode(), _opt(parent_key), 0 if kind == "map" else 1, ctypes.byref(out)))
         return _take(out).decode()
 
     def map_type_at(self, root: str, key: str) -> int:
@@ -598,18 +608,40 @@ def route(doc_id, world: int) -> int:
     return int(lib().ycrdt_route(b, len(b), world))
 
 
-def apply_updates_multi(docs, updates, engine=None):
+def apply_updates_multi(docs, updates, engine=None, doc_index=None):
     """Y.applyUpdate(docs[i], updates[i]) for every i — a fleet ingest batch — merged in one device
-    pass for every document with nothing pending (ycrdt_apply_updates_multi)."""
-    if len(docs) != len(updates):
-        raise ValueError("one document per update")
-    eng = engine or (docs[0].engine if docs else default_engine())
-    arr, keep = _bufs(updates)
+    pass for every document with nothing pending (ycrdt_apply_updates_multi). With doc_index
+    (integer array, one per update) `docs` lists the documents once and update i goes to
+    docs[doc_index[i]]."""
     import numpy as np
 
     hv = np.fromiter((d._h.value for d in docs), dtype=np.uint64, count=len(docs)) if docs else np.zeros(1, np.uint64)
+    if doc_index is not None:
+        hv = hv[np.asarray(doc_index, dtype=np.int64)] if len(updates) else np.zeros(1, np.uint64)
+    if (len(hv) if len(updates) else 0) != len(updates):
+        raise ValueError("one document per update")
+    eng = engine or (docs[0].engine if docs else default_engine())
+    arr, keep = _bufs(updates)
     hs = hv.ctypes.data_as(ctypes.POINTER(ctypes.c_void_p))
     _check(lib().ycrdt_apply_updates_multi(eng._h, hs, arr, len(keep)))
+
+
+def states_packed(docs, engine=None):
+    """(blob, offs): every document's encodeStateAsUpdate and encodeStateVector back to back in one
+    numpy uint8 array (ycrdt_docs_states_packed) — doc i's update blob[offs[2i]:offs[2i+1]], its
+    state vector blob[offs[2i+1]:offs[2i+2]]."""
+    import numpy as np
+
+    eng = engine or (docs[0].engine if docs else default_engine())
+    hv = np.fromiter((d._h.value for d in docs), dtype=np.uint64, count=len(docs)) if docs else np.zeros(1, np.uint64)
+    hs = hv.ctypes.data_as(ctypes.POINTER(ctypes.c_void_p))
+    offs = np.zeros(2 * len(docs) + 1, dtype=np.uint64)
+    op = offs.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64))
+    total = ctypes.c_uint64()
+    _check(lib().ycrdt_docs_states_packed(eng._h, hs, len(docs), None, 0, op, ctypes.byref(total)))
+    blob = np.empty(max(1, total.value), dtype=np.uint8)
+    _check(lib().ycrdt_docs_states_packed(eng._h, hs, len(docs), blob.ctypes.data, total.value, op, ctypes.byref(total)))
+    return blob[: total.value], offs
 
 
 def merge_updates(updates, engine=None) -> bytes:

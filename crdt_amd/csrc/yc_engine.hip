@@ -866,7 +866,7 @@ int run_merge(ycrdt_engine* e, ycrdt_batch* b, const std::unordered_map<uint32_t
   w.g_flags = take<uint32_t>(V, B_GFLAGS, U + 1, ok);
   w.g_origin = take<uint32_t>(V, B_GORIG, U + 1, ok);
   w.g_rorigin = take<uint32_t>(V, B_GRORIG, U + 1, ok);
-  w.g_link = take<uint32_t>(V, B_GLINK, U + 1, ok);
+  w.g_hop = take<uint4>(V, B_GLINK, U + 1, ok);
   w.g_key = take<uint32_t>(V, B_GKEY, U + 1, ok);
   w.g_maxchild = take<uint32_t>(V, B_GMAXC, U + 1, ok);
   w.g_outid = take<uint32_t>(V, B_GOUTID, U + 2, ok);
@@ -1875,6 +1875,84 @@ int ycrdt_apply_updates_multi(ycrdt_engine* e, ycrdt_doc* const* docs, const ycr
   return frc;
 }
 
+// Every document's Y.encodeStateAsUpdate + Y.encodeStateVector in one call (a fleet's LevelDB
+// storeUpdate / sync snapshot, crdt.js:33-40,260,288): deferred applies flushed as one batched
+// merge, the states gathered from their arena blocks by one piece-copy launch and copied to the
+// host through the pipelined pinned D2H. A document with pending structs takes its own encode.
+int ycrdt_docs_states_packed(ycrdt_engine* e, ycrdt_doc* const* docs, size_t n, uint8_t* dst, uint64_t cap, uint64_t* offs,
+                             uint64_t* total) {
+  if (!e || (n && !docs)) return fail(YCRDT_E_ARG, "null arg");
+  for (size_t i = 0; i < n; ++i)
+    if (!docs[i] || docs[i]->e != e) return fail(YCRDT_E_ARG, "document of another engine (or null) at " + std::to_string(i));
+  HIPCHK(hipSetDevice(e->device));
+  {
+    std::vector<ycrdt_doc*> q;
+    for (size_t i = 0; i < n; ++i) if (!docs[i]->queue.empty()) q.push_back(docs[i]);
+    std::sort(q.begin(), q.end());
+    q.erase(std::unique(q.begin(), q.end()), q.end());
+    if (const int rc = flush_multi(e, q)) return rc;
+  }
+  std::vector<uint64_t> o(2 * n + 1, 0);
+  std::vector<std::vector<uint8_t>> slow(n);  // pending documents: their encode (host)
+  uint64_t pos = 0;
+  for (size_t i = 0; i < n; ++i) {
+    ycrdt_doc* d = docs[i];
+    o[2 * i] = pos;
+    if (d->ing.has_pending || d->ing.has_ds) {
+      ycrdt_out u{nullptr, 0};
+      if (const int rc = ycrdt_encode_state_as_update(d, ycrdt_buf{nullptr, 0}, &u)) return rc;
+      slow[i].assign(u.ptr, u.ptr + u.len);
+      ycrdt_free(&u);
+      pos += slow[i].size();
+    } else {
+      pos += d->state_len ? d->state_len : 2;
+    }
+    o[2 * i + 1] = pos;
+    pos += d->sv.size();
+  }
+  o[2 * n] = pos;
+  if (total) *total = pos;
+  if (offs) memcpy(offs, o.data(), sizeof(uint64_t) * o.size());
+  if (!dst) return YCRDT_OK;
+  if (cap < pos) return fail(YCRDT_E_ARG, "destination smaller than the packed states");
+  // device states: one gather into B_PACK, one pipelined D2H; the rest is written on the host
+  std::vector<Piece> pc;
+  uint64_t dev = 0;
+  std::vector<uint64_t> at(n, ~0ull);
+  for (size_t i = 0; i < n; ++i) {
+    ycrdt_doc* d = docs[i];
+    if (slow[i].empty() && d->state_len) {
+      at[i] = dev;
+      for (uint64_t k = 0; k < d->state_len; k += PIECE_MAX)
+        pc.push_back(Piece{(const uint8_t*)d->state.p + k, nullptr, (uint32_t)std::min<uint64_t>(PIECE_MAX, d->state_len - k), {0}});
+      dev += d->state_len;
+    }
+  }
+  if (dev) {
+    auto& V = e->bufs;
+    bool ok = true;
+    uint8_t* buf = take<uint8_t>(V, B_PACK, dev + 16, ok);
+    Piece* dpc = ok ? take<Piece>(V, B_PACKPC, pc.size() + 1, ok) : nullptr;
+    if (!ok) return fail(YCRDT_E_DEVICE, oom("document states"));
+    uint64_t w = 0;
+    for (Piece& P : pc) { P.dst = buf + w; w += P.len; }
+    HIPCHK(hipMemcpyAsync(dpc, pc.data(), sizeof(Piece) * pc.size(), hipMemcpyHostToDevice, e->stream));
+    copy_pieces(dpc, (uint32_t)pc.size(), e->stream);
+    std::vector<uint8_t> host(dev);
+    if (const int rc = d2h_span(e, host.data(), buf, dev)) return rc;
+    e->ws_owner = nullptr;  // B_PACK held a batch's split
+    for (size_t i = 0; i < n; ++i)
+      if (at[i] != ~0ull) memcpy(dst + o[2 * i], host.data() + at[i], docs[i]->state_len);
+  }
+  for (size_t i = 0; i < n; ++i) {
+    ycrdt_doc* d = docs[i];
+    if (!slow[i].empty()) memcpy(dst + o[2 * i], slow[i].data(), slow[i].size());
+    else if (!d->state_len) { dst[o[2 * i]] = 0; dst[o[2 * i] + 1] = 0; }
+    if (!d->sv.empty()) memcpy(dst + o[2 * i + 1], d->sv.data(), d->sv.size());
+  }
+  return YCRDT_OK;
+}
+
 int ycrdt_doc_flush(ycrdt_doc* d) {
   if (!d) return fail(YCRDT_E_ARG, "null doc");
   return flush(d);
@@ -2343,6 +2421,32 @@ static OpTarget target_of(const char* root, const char* parent_key) {
   return t;
 }
 
+int ycrdt_type_json(ycrdt_doc* d, const char* root, const char* parent_key, int kind, ycrdt_out* out) {
+  if (!d || !root || !out || kind < 0 || kind > 1) return fail(YCRDT_E_ARG, "bad arg");
+  out->ptr = nullptr;
+  out->len = 0;
+  int rc = ensure_view(d);
+  if (rc) return rc;
+  std::string j, err;
+  if (!view_type_json(d->view, target_of(root, parent_key), kind, j, err)) return fail(YCRDT_E_DECODE, err);
+  out->len = j.size();
+  out->ptr = (uint8_t*)malloc(j.size() + 1);
+  if (!out->ptr) { out->len = 0; return fail(YCRDT_E_CAPACITY, "host allocation failed"); }
+  memcpy(out->ptr, j.data(), j.size());
+  out->ptr[j.size()] = 0;
+  return YCRDT_OK;
+}
+static int read_out(const std::string& j, ycrdt_out* out);
+int ycrdt_map_entries(ycrdt_doc* d, const char* root, const char* parent_key, ycrdt_out* out) {
+  if (!d || !root || !out) return fail(YCRDT_E_ARG, "null arg");
+  out->ptr = nullptr;
+  out->len = 0;
+  const int rc = ensure_view(d);
+  if (rc) return rc;
+  std::string j;
+  view_map_entries(d->view, target_of(root, parent_key), j);
+  return read_out(j, out);
+}
 int ycrdt_doc_json(ycrdt_doc* d, const char* root, int kind, ycrdt_out* out) {
   if (!d || !root || !out || kind < 0 || kind > 1) return fail(YCRDT_E_ARG, "bad arg");
   out->ptr = nullptr;

@@ -521,6 +521,60 @@ bool view_root_json(const HostView& v, const std::string& name, int kind, std::s
   return true;
 }
 
+// toJSON of one shared type: a root type (view_root_json), or the YMap / YArray stored in root map
+// `t.root` under `t.key` — only that type's own list is read (a nested YArray's toJSON no longer
+// builds the JSON of the whole root map). A key that holds no type of `kind` gives {} / [].
+bool view_type_json(const HostView& v, const OpTarget& t, int kind, std::string& out, std::string& err) {
+  if (!t.nested) return view_root_json(v, t.root, kind, out, err);
+  out.clear();
+  ParentRef pr;
+  std::string e2;
+  if (resolve_parent(v, t, kind == 0 ? 1u : 0u, pr, e2) != YCRDT_OK) {
+    out = kind == 0 ? "{}" : "[]";
+    return true;
+  }
+  JsonCtx c{v};
+  type_json(c, pr.unit, kind == 0 ? 1u : 0u, nullptr, out);
+  return true;
+}
+
+// The live entries of a YMap with the id of each entry's winning item: {"key": ["client:clock",
+// value], ...}. A key changed in a transaction (YMapEvent.keysChanged, Y@51190) is a key whose
+// winning item changed — the same value set again is a new item — so the facade's map observers
+// compare these ids, not the values (and nested-type contents never count, as in YMap.observe).
+bool view_map_entries(const HostView& v, const OpTarget& t, std::string& out) {
+  out = "{";
+  std::vector<uint32_t> ks;
+  if (!t.nested) {
+    auto it = v.root_entries.find(t.root);
+    if (it != v.root_entries.end()) ks = it->second;
+  } else {
+    ParentRef pr;
+    std::string err;
+    if (resolve_parent(v, t, 1, pr, err) == YCRDT_OK) {
+      auto it = v.by_parent.find(pr.unit);
+      if (it != v.by_parent.end()) ks = it->second;
+    }
+  }
+  JsonCtx c{v};
+  bool first = true;
+  for (uint32_t ki : ks) {
+    const ViewKey& K = v.keys[ki];
+    if (!(K.flags & VK_PSUB) || !(K.win.flags & VS_SET) || (K.win.flags & VS_DELETED) || !(K.win.flags & VS_ITEM)) continue;
+    std::vector<std::pair<bool, std::string>> el;
+    seg_elements(c, K.win, el, true);
+    if (el.empty() || !el.back().first) continue;
+    if (!first) out.push_back(',');
+    first = false;
+    put_json_str(out, v.bytes.data() + K.psub_pos, K.psub_len);
+    out += ":[\"" + std::to_string(K.win.client) + ":" + std::to_string(K.win.clock + K.win.len - 1) + "\",";
+    out += el.back().second;
+    out.push_back(']');
+  }
+  out.push_back('}');
+  return true;
+}
+
 namespace {
 // the list a read addresses (nullptr: it does not exist), `want` = 1 YMap, 0 YArray
 const ViewKey* read_list(const HostView& v, const OpTarget& t, uint32_t want, const std::string* psub) {

@@ -44,6 +44,10 @@ struct OpTarget {
   bool nested = false;
   std::string key;
 };
+// toJSON of a root type or of the type stored in a root map entry (its own list only); kind 0 map, 1 array
+bool view_type_json(const HostView& v, const OpTarget& t, int kind, std::string& out, std::string& err);
+// a YMap's live entries with their winning item ids: {"key": ["client:clock", value], ...}
+bool view_map_entries(const HostView& v, const OpTarget& t, std::string& out);
 
 // Per-key reads of the view (YMap.get / has / size, YArray.length / get) without building the
 // type's JSON: state 0 = absent, 1 = present (`json` holds the value), 2 = present but `undefined`

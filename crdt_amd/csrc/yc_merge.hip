@@ -234,7 +234,7 @@ __device__ __forceinline__ uint64_t fnv_u32(uint64_t h, uint32_t v) {
 // pointer jumping (Item.getMissing, Y@76507). An item whose origin / right origin is GC, or
 // whose parent item is GC, is integrated as GC (getMissing sets parent = null).
 __global__ __launch_bounds__(256) void k_seg_props(Work w, uint32_t nsegs) {
-  const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t s = gidx();
   if (s >= nsegs) return;
   // the source struct's columns in one round of loads (the right-origin clock is unwritten when
   // there is none: read, never used), then the client bases
@@ -314,13 +314,13 @@ __global__ __launch_bounds__(256) void k_seg_props(Work w, uint32_t nsegs) {
   }
   w.g_cidx[s] = cidx;
   w.g_src[s] = own;
-  w.g_flags[s] = sf;
   w.g_origin[s] = gc ? NONE : origin;
   w.g_rorigin[s] = gc ? NONE : rorigin;
-  // a root's key carries its list kind in bit 31 (k_resolve copies it whole down the chains and
-  // writes the final keys, without the bit, to g_key); the chains are climbed over g_tmp
-  w.g_tmp[s] = key != NONE && w.s_psub[own] != NONE ? key | KEY_PSUB : key;
-  w.g_link[s] = link;
+  // the climbing record (k_resolve writes the final flags and keys): a root's key carries its list
+  // kind in bit 31 (k_resolve copies it whole down the chains and writes the final keys, without
+  // the bit, to g_key); the origin's segment is the winner slot of a YMap entry
+  const uint32_t kw = key != NONE && w.s_psub[own] != NONE ? key | KEY_PSUB : key;
+  w.g_hop[s] = make_uint4(sf, kw, link, !gc && origin != NONE ? link : NONE);
 }
 
 void launch_segment_props(const Work& w, uint32_t nsegs, uint32_t nclients, uint64_t nunits, hipStream_t s) {
@@ -343,29 +343,31 @@ void launch_segment_props(const Work& w, uint32_t nsegs, uint32_t nclients, uint
 // second pass of the winner reduction begun in k_seg_props: an atomicMax only where the slot is
 // below itself — segments are numbered in client order, so the max child is the max segment).
 __global__ __launch_bounds__(256) void k_resolve(Work w, uint32_t nsegs) {
-  const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t s = gidx();
   if (s >= nsegs) return;
-  uint32_t f = w.g_flags[s];
-  uint32_t kv = w.g_tmp[s];
+  const uint4 h = w.g_hop[s];  // flags, climbing key, link, origin segment
+  uint32_t f = h.x;
+  uint32_t kv = h.y;
   bool arr = false;
   if (f & SEG_ITEM) {
     if (kv == NONE) {  // not a root: climb
-      uint32_t x = w.g_link[s];
+      uint32_t x = h.z;
       bool done = false;
       for (uint32_t it = 0; it <= nsegs; ++it) {  // more hops than segments: a cycle
-        const uint32_t fx = w.g_flags[x], k = w.g_tmp[x], y = w.g_link[x];  // one round of loads per hop
+        const uint4 hx = w.g_hop[x];  // one 16-B load per hop
+        const uint32_t fx = hx.x, k = hx.y, y = hx.z;
         if (!(fx & SEG_ITEM)) {  // the origin chain ends in GC: getMissing drops the parent
           f = (f & ~SEG_ITEM) | SEG_GC | SEG_DEL;
-          w.g_flags[s] = f;
+          w.g_hop[s].x = f;
           w.g_origin[s] = NONE;
           w.g_rorigin[s] = NONE;
           done = true;
           break;
         }
-        if (k != NONE) { kv = k; w.g_tmp[s] = k; done = true; break; }
+        if (k != NONE) { kv = k; w.g_hop[s].y = k; done = true; break; }
         if (y == x) { done = true; break; }  // a chain without a root: reported below
-        const uint32_t z = w.g_link[y];
-        if (z != y) w.g_link[x] = z;
+        const uint32_t z = w.g_hop[y].z;
+        if (z != y) w.g_hop[x].z = z;
         x = y;
       }
       if (!done) raise_err(&w.ctr->err, ERR_DECODE);  // an origin cycle
@@ -375,17 +377,14 @@ __global__ __launch_bounds__(256) void k_resolve(Work w, uint32_t nsegs) {
       else {
         arr = !(kv & KEY_PSUB);
         f |= arr ? SEG_ARRAY : SEG_PSUB;
-        w.g_flags[s] = f;
         if (!arr) {  // the winner reduction's settling pass (k_seg_props stored one child)
-          // the origin's segment (k_seg_props stored into the same slot: its link)
-          const uint32_t og = w.g_origin[s];
-          uint32_t* slot = og != NONE ? &w.g_maxchild[seg_of(w.u_cutbits, w.u_wpre, og)]
-                           : (f & SEG_ROOT) ? &w.k_rootmax[kv & ~KEY_PSUB] : nullptr;
+          uint32_t* slot = h.w != NONE ? &w.g_maxchild[h.w] : (f & SEG_ROOT) ? &w.k_rootmax[kv & ~KEY_PSUB] : nullptr;
           if (slot && *slot < s + 1) atomicMax(slot, s + 1);
         }
       }
     }
   }
+  w.g_flags[s] = f;
   w.g_key[s] = (f & SEG_ITEM) && kv != NONE ? kv & ~KEY_PSUB : NONE;
   wave_flag(&w.ctr->narray, arr);  // read as zero / non-zero (launch_yata)
 }
@@ -406,7 +405,7 @@ void launch_map_winner(const Work& w, uint32_t nsegs, hipStream_t s) {}
 // child until a leaf (YATA order of an origin-only tree, SURVEY.md §7 hard part 2)
 // (a descent visits every segment at most once: more hops than segments is a cycle, an error)
 __global__ void k_winner_walk(Work w, uint32_t nsegs) {
-  const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t k = gidx();
   if (k >= w.cap_keys) return;
   const uint32_t r = w.k_rootmax[k];
   if (!r) { w.k_winner[k] = NONE; return; }

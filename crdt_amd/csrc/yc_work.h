@@ -165,7 +165,8 @@ struct Work {
   uint32_t* g_flags = nullptr;     // SEG_* flags
   uint32_t* g_origin = nullptr;    // origin unit (global) or NONE
   uint32_t* g_rorigin = nullptr;   // right-origin unit or NONE
-  uint32_t* g_link = nullptr;      // pointer-jumping link (key resolution)
+  uint4* g_hop = nullptr;          // key resolution record {flags, climbing key, link, origin segment}:
+                                   // one 16-B line per climbing hop (k_seg_props -> k_resolve)
   uint32_t* g_key = nullptr;       // resolved key slot or NONE
   uint32_t* g_maxchild = nullptr;  // seg + 1 of the max-client child (segments are in client order), 0 = none
   uint32_t* g_next = nullptr;      // descent pointer / pointer jumping
@@ -286,6 +287,17 @@ struct Work {
 
 // client index of (document, client id); NONE if the batch has no such client. Multi-document
 // batches index clients by (doc, client), so every per-client structure stays per document.
+// XCD-aware block order: workgroups are dealt round-robin over the 8 XCDs (MI355X_MICROARCH.md,
+// speed only, never correctness), so block b and b + 8 share an L2. The logical block below gives
+// XCD x one contiguous 1/8 of the grid: the random gathers of a per-segment / per-struct pass
+// (origins, clients, winner slots) mostly land in the same document's tables, which then stay in
+// that XCD's L2 instead of being pulled into all eight. A bijection on [0, gridDim.x).
+__device__ __forceinline__ uint32_t xcd_block() {
+  const uint32_t b = blockIdx.x, G = gridDim.x, per = G >> 3, rem = G & 7u, x = b & 7u;
+  return x * per + min(x, rem) + (b >> 3);
+}
+__device__ __forceinline__ uint32_t gidx() { return xcd_block() * blockDim.x + threadIdx.x; }
+
 __device__ __forceinline__ uint64_t client_hash(uint64_t k) {  // splitmix64 finaliser
   k ^= k >> 30; k *= 0xBF58476D1CE4E5B9ull;
   k ^= k >> 27; k *= 0x94D049BB133111EBull;

@@ -31,48 +31,80 @@ const TYPE_ARRAY = 0;
 const TYPE_MAP = 1;
 
 // Observers (YMap/YArray.observe, crdt.js:620-656). Yjs calls them once per transaction that
-// changed the type, after the transaction (cleanupTransactions Y@31804). The facade compares
-// the observed type's toJSON before and after each transaction and, when it differs, calls the
-// observer with (event, transaction); event carries target/currentTarget and, for maps,
-// keysChanged + changes.keys ({action, oldValue}) as YMapEvent does. Array deltas are not
-// computed (`changes.delta` is empty): the reference forwards the event untouched.
-function snapshotObserved(doc) {
-  if (!doc._observed.size) return null;
-  const snap = new Map();
-  for (const t of doc._observed) snap.set(t, JSON.stringify(t.toJSON()));
-  return snap;
+// changed the type, synchronously at its end (cleanupTransactions Y@31804). Here Y.applyUpdate
+// stays deferred (one batched merge serves a burst of applies), so events are computed lazily:
+// a mutation only marks the doc; the events fire at the next read of the doc (toJSON, get, has,
+// size, length, encode*) or, if nothing reads it, from setImmediate — whichever comes first — with
+// one read of each observed type, compared with what its previous event delivered (taken when
+// observe() was called). A burst of updates therefore yields one event per type, with the union of
+// their changes (Yjs: one per transaction). Maps compare the winning item id of every entry
+// (ycrdt_map_entries): keysChanged = keys whose winning item changed — a set of the same value is a
+// new item, and changes inside a nested type are not the map's (YMap.observe, not observeDeep);
+// changes.keys carries {action, oldValue}. Arrays carry changes.delta ([{retain}, {delete},
+// {insert}] from the common prefix / suffix of the two arrays, exact for one insert or delete).
+function jsonOf(t) {
+  if (t instanceof YMap) return JSON.parse(binding.mapEntries(t._bound(), t._root, t._pkey));
+  return t.toJSONRaw();
 }
-function fireObservers(doc, before, local) {
-  if (!before) return;
-  const transaction = { doc, local, origin: null };
-  for (const [t, old] of before) {
-    if (!t._observers.length) continue;
-    const nowJson = t.toJSON();
-    const now = JSON.stringify(nowJson);
-    if (now === old) continue;
-    const event = { target: t, currentTarget: t, transaction, changes: { added: new Set(), deleted: new Set(), delta: [], keys: new Map() } };
-    if (t instanceof YMap) {
+function arrayDelta(a, b) {
+  let p = 0;
+  while (p < a.length && p < b.length && JSON.stringify(a[p]) === JSON.stringify(b[p])) ++p;
+  let q = 0;
+  while (q < a.length - p && q < b.length - p && JSON.stringify(a[a.length - 1 - q]) === JSON.stringify(b[b.length - 1 - q])) ++q;
+  const delta = [];
+  if (p) delta.push({ retain: p });
+  if (a.length - p - q) delta.push({ delete: a.length - p - q });
+  if (b.length - p - q) delta.push({ insert: b.slice(p, b.length - q) });
+  return delta;
+}
+function markChanged(doc, local) {
+  if (!doc._observed.size) return;
+  doc._local = doc._dirty ? doc._local && local : local;
+  doc._dirty = true;
+  if (!doc._timer) doc._timer = setImmediate(() => { doc._timer = null; fireObservers(doc); });
+}
+function fireObservers(doc) {
+  if (!doc._dirty || doc._firing) return;
+  doc._dirty = false;
+  doc._firing = true;
+  try {
+    const transaction = { doc, local: doc._local, origin: null };
+    for (const t of Array.from(doc._observed)) {
+      if (!t._observers.length) continue;
+      const nowJson = jsonOf(t);
+      const now = JSON.stringify(nowJson);
+      const old = t._seen;
+      t._seen = now;
+      if (old === undefined || now === old) continue;
+      const event = { target: t, currentTarget: t, transaction, changes: { added: new Set(), deleted: new Set(), delta: [], keys: new Map() } };
       const a = JSON.parse(old), b = nowJson;
-      const keys = new Set([...Object.keys(a), ...Object.keys(b)]);
-      event.keysChanged = new Set();
-      for (const k of keys) {
-        const ina = Object.prototype.hasOwnProperty.call(a, k), inb = Object.prototype.hasOwnProperty.call(b, k);
-        if (ina && inb && JSON.stringify(a[k]) === JSON.stringify(b[k])) continue;
-        event.keysChanged.add(k);
-        event.changes.keys.set(k, { action: !ina ? 'add' : !inb ? 'delete' : 'update', oldValue: ina ? a[k] : undefined });
+      if (t instanceof YMap) {  // a, b: {key: [winning item id, value]}
+        const keys = new Set([...Object.keys(a), ...Object.keys(b)]);
+        event.keysChanged = new Set();
+        for (const k of keys) {
+          const ina = Object.prototype.hasOwnProperty.call(a, k), inb = Object.prototype.hasOwnProperty.call(b, k);
+          if (ina && inb && a[k][0] === b[k][0]) continue;
+          event.keysChanged.add(k);
+          event.changes.keys.set(k, { action: !ina ? 'add' : !inb ? 'delete' : 'update', oldValue: ina ? a[k][1] : undefined });
+        }
+      } else {
+        event.changes.delta = arrayDelta(a, b);
       }
+      event.delta = event.changes.delta;
+      for (const f of t._observers.slice()) f(event, transaction);
     }
-    for (const f of t._observers.slice()) f(event, transaction);
+  } finally {
+    doc._firing = false;
   }
 }
-// runs one mutation of `doc`; observers fire after it unless a transaction is open
-function mutate(doc, fn) {
-  if (doc._txn) return fn();
-  const before = snapshotObserved(doc);
+// runs one mutation of `doc`; its observers fire at the next read (or tick) unless a transaction is open
+function mutate(doc, fn, local = true) {
   const r = fn();
-  fireObservers(doc, before, true);
+  if (!doc._txn) markChanged(doc, local);
   return r;
 }
+// every read of a doc delivers the pending events first (the state it returns is the one they describe)
+function settle(doc) { if (doc && doc._dirty) fireObservers(doc); }
 
 class AbstractType {
   constructor() {
@@ -85,23 +117,28 @@ class AbstractType {
     if (!this.doc) throw new Error('Invalid access: Add Yjs type to a document before reading data.');
     return this.doc._h;
   }
-  observe(f) { this._observers.push(f); if (this.doc) this.doc._observed.add(this); }
+  observe(f) {
+    this._observers.push(f);
+    if (this.doc) {
+      settle(this.doc);
+      if (this._seen === undefined) this._seen = JSON.stringify(jsonOf(this));
+      this.doc._observed.add(this);
+    }
+  }
   unobserve(f) {
     this._observers = this._observers.filter((g) => g !== f);
-    if (this.doc && !this._observers.length) this.doc._observed.delete(this);
+    if (this.doc && !this._observers.length) { this.doc._observed.delete(this); this._seen = undefined; }
   }
 }
 
 class YMap extends AbstractType {
-  toJSON() {
-    const h = this._bound();
-    if (this._pkey === null) return JSON.parse(binding.docJson(h, this._root, 0));
-    const v = JSON.parse(binding.docJson(h, this._root, 0))[this._pkey];
-    return v && typeof v === 'object' && !Array.isArray(v) ? v : {};
-  }
+  // the type's own list only (a nested map does not read its root map's JSON)
+  toJSONRaw() { return JSON.parse(binding.typeJson(this._bound(), this._root, this._pkey, 0)); }
+  toJSON() { settle(this.doc); return this.toJSONRaw(); }
   // per-key reads go to the view's hash index (no toJSON of the whole map per call)
-  has(key) { return binding.mapHas(this._bound(), this._root, this._pkey, key); }
+  has(key) { settle(this.doc); return binding.mapHas(this._bound(), this._root, this._pkey, key); }
   get(key) {
+    settle(this.doc);
     const h = this._bound();
     if (this._pkey === null) {
       const tr = binding.mapTypeAt(h, this._root, key);
@@ -131,21 +168,23 @@ class YMap extends AbstractType {
   delete(key) { const h = this._bound(); mutate(this.doc, () => binding.mapDelete(h, this._root, this._pkey, key)); }
   forEach(f) { const j = this.toJSON(); for (const k of Object.keys(j)) f(j[k], k, this); }
   keys() { return Object.keys(this.toJSON())[Symbol.iterator](); }
-  get size() { return binding.mapSize(this._bound(), this._root, this._pkey); }
+  get size() { settle(this.doc); return binding.mapSize(this._bound(), this._root, this._pkey); }
 }
 
 class YArray extends AbstractType {
   constructor() { super(); this._prelim = []; }
-  toJSON() {
-    const h = this._bound();
-    if (this._pkey === null) return JSON.parse(binding.docJson(h, this._root, 1));
-    const v = JSON.parse(binding.docJson(h, this._root, 0))[this._pkey];
-    return Array.isArray(v) ? v : [];
-  }
+  // the type's own list only (a nested array does not read its root map's JSON)
+  toJSONRaw() { return JSON.parse(binding.typeJson(this._bound(), this._root, this._pkey, 1)); }
+  toJSON() { settle(this.doc); return this.toJSONRaw(); }
   toArray() { return this.toJSON(); }
-  get length() { return this.doc ? binding.arrayLength(this._bound(), this._root, this._pkey) : this._prelim.length; }
+  get length() {
+    if (!this.doc) return this._prelim.length;
+    settle(this.doc);
+    return binding.arrayLength(this._bound(), this._root, this._pkey);
+  }
   get(index) {
     if (!this.doc) return this._prelim[index];
+    settle(this.doc);
     const j = binding.arrayGet(this._bound(), this._root, this._pkey, index);
     return j === undefined ? undefined : JSON.parse(j);
   }
@@ -174,6 +213,9 @@ class Doc {
     this._types = new Map();     // root name / root\0key → the type object handed out
     this._observed = new Set();  // types with observers
     this._txn = 0;
+    this._dirty = false;         // mutated since the observers last saw it
+    this._local = true;
+    this._timer = null;
   }
   _root(name, Cls) {
     let t = this._types.get(name);
@@ -201,37 +243,40 @@ class Doc {
   // the end, as after a Yjs transaction
   transact(f, origin = null) {
     if (this._txn) return f({ doc: this, origin, local: true });
-    const before = snapshotObserved(this);
+    settle(this);
     this._txn = 1;
     try {
       return f({ doc: this, origin, local: true });
     } finally {
       this._txn = 0;
-      fireObservers(this, before, true);
+      markChanged(this, true);
+      settle(this);  // one event per transaction, at its end (Yjs cleanupTransactions)
     }
   }
   destroy() {}
 }
 
+// Y.applyUpdate: validated now, merged at the next read (observers: see above)
 function applyUpdate(doc, update) {
-  mutate(doc, () => binding.applyUpdates(doc._h, update));
+  mutate(doc, () => binding.applyUpdates(doc._h, update), false);
 }
 
 // fleet ingest: Y.applyUpdate(docs[i], updates[i]) for every i, one device pass (not in Yjs)
 function applyUpdatesMulti(docs, updates) {
-  const before = docs.map((d) => snapshotObserved(d));
   binding.applyUpdatesMulti(docs.map((d) => d._h), updates);
-  docs.forEach((d, i) => fireObservers(d, before[i], false));
+  for (const d of new Set(docs)) markChanged(d, false);
 }
 function applyUpdates(doc, updates) {
-  mutate(doc, () => binding.applyUpdates(doc._h, updates));
+  mutate(doc, () => binding.applyUpdates(doc._h, updates), false);
 }
 
 function encodeStateAsUpdate(doc, encodedTargetStateVector) {
+  settle(doc);
   return binding.encodeStateAsUpdate(doc._h, encodedTargetStateVector);
 }
 
 function encodeStateVector(doc) {
+  settle(doc);
   return binding.encodeStateVector(doc._h);
 }
 

@@ -438,6 +438,45 @@ static napi_value js_doc_json(napi_env env, napi_callback_info info) {
   return s;
 }
 
+/* typeJson(doc, root, parentKey, kind) → toJSON of the root type (parentKey null) or of the YMap
+ * (kind 0) / YArray (kind 1) stored under root[parentKey], reading that type's own list only */
+static napi_value js_type_json(napi_env env, napi_callback_info info) {
+  size_t argc = 4;
+  napi_value argv[4], s;
+  CHECK(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+  op_args a;
+  if (!op_target(env, argv, argc, 0, &a)) return NULL;
+  int32_t kind = 0;
+  if (argc < 4 || napi_get_value_int32(env, argv[3], &kind) != napi_ok) {
+    op_free(&a);
+    napi_throw_type_error(env, NULL, "typeJson(doc, root, parentKey, kind)");
+    return NULL;
+  }
+  ycrdt_out o = {NULL, 0};
+  int rc = ycrdt_type_json(a.d, a.root, a.pkey, kind, &o);
+  op_free(&a);
+  if (rc != YCRDT_OK) return throw_rc(env, rc);
+  CHECK(env, napi_create_string_utf8(env, (const char *)o.ptr, o.len, &s));
+  ycrdt_free(&o);
+  return s;
+}
+
+/* mapEntries(doc, root, parentKey) → JSON text {"key": ["client:clock", value]} (map observers) */
+static napi_value js_map_entries(napi_env env, napi_callback_info info) {
+  size_t argc = 3;
+  napi_value argv[3], s;
+  CHECK(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+  op_args a;
+  if (!op_target(env, argv, argc, 0, &a)) return NULL;
+  ycrdt_out o = {NULL, 0};
+  int rc = ycrdt_map_entries(a.d, a.root, a.pkey, &o);
+  op_free(&a);
+  if (rc != YCRDT_OK) return throw_rc(env, rc);
+  CHECK(env, napi_create_string_utf8(env, o.ptr ? (const char *)o.ptr : "{}", o.ptr ? o.len : 2, &s));
+  ycrdt_free(&o);
+  return s;
+}
+
 /* mapSet(doc, root, parentKey, key, anyBytes)   (YMap.set, crdt.js:375,434) */
 static napi_value js_map_set(napi_env env, napi_callback_info info) {
   size_t argc = 5;
@@ -642,6 +681,8 @@ static napi_value init(napi_env env, napi_value exports) {
       {"version", NULL, js_version, NULL, NULL, NULL, napi_default, NULL},
       {"mapTypeAt", NULL, js_map_type_at, NULL, NULL, NULL, napi_default, NULL},
       {"docJson", NULL, js_doc_json, NULL, NULL, NULL, napi_default, NULL},
+      {"typeJson", NULL, js_type_json, NULL, NULL, NULL, napi_default, NULL},
+      {"mapEntries", NULL, js_map_entries, NULL, NULL, NULL, napi_default, NULL},
       {"mapSet", NULL, js_map_set, NULL, NULL, NULL, napi_default, NULL},
       {"mapSetType", NULL, js_map_set_type, NULL, NULL, NULL, napi_default, NULL},
       {"mapDelete", NULL, js_map_delete, NULL, NULL, NULL, napi_default, NULL},

@@ -40,6 +40,9 @@ C3 = dict(n_replicas=256, rounds=16, items=10_000_000, seed=3)
 # C4 (nested YArrays under YMap keys): 100k keys, 2 000 replicas x 10 000 ops ~= 50 M items per
 # document; BASELINE's 100 M items is two such documents' worth per GPU pair, key-hash sharded
 C4 = dict(n_replicas=2000, n_keys=100_000, pushes=10_000, init_len=4, p_over=0.02, p_del=0.05, seed=4)
+# C4 at BASELINE scale: 1 M keys, 64 replicas, ~100 items per nested array (102 M
+# items, 41 M structs, 716 MB of updates), ~10 % of the keys overwritten by a fresh array
+C4_FULL = dict(n_replicas=64, n_keys=1_000_000, pushes=640_000, init_len=4, p_over=0.0025, p_del=0.05, seed=4)
 
 
 def gen_nested(n_replicas, n_keys, pushes, init_len=4, p_over=0.02, p_del=0.05, seed=4):

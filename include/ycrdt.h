@@ -91,6 +91,13 @@ int ycrdt_apply_updates(ycrdt_doc *d, const ycrdt_buf *ups, size_t n);
  * belong to `e`. A malformed update i: updates before it are applied (and merged), then
  * YCRDT_E_DECODE. */
 int ycrdt_apply_updates_multi(ycrdt_engine *e, ycrdt_doc *const *docs, const ycrdt_buf *ups, size_t n);
+/* Y.encodeStateAsUpdate + Y.encodeStateVector of n documents in one call (a fleet's LevelDB
+ * snapshot / sync answers, crdt.js:33-40,260,288): deferred applies are flushed as one batched merge
+ * and the states gathered on the device, then copied with one pipelined D2H. Document i's update
+ * is dst[offs[2i] .. offs[2i+1]), its state vector dst[offs[2i+1] .. offs[2i+2]); offs holds 2n+1
+ * entries. dst == NULL only fills offs / total (size query). */
+int ycrdt_docs_states_packed(ycrdt_engine *e, ycrdt_doc *const *docs, size_t n, uint8_t *dst, uint64_t cap, uint64_t *offs,
+                             uint64_t *total);
 /* Runs the deferred applies now (every read does this implicitly). */
 int ycrdt_doc_flush(ycrdt_doc *d);
 /* Whether Yjs would hold pending structs (store.pendingStructs) / a pending delete set
@@ -127,6 +134,14 @@ int ycrdt_diff_updates(ycrdt_engine *e, const ycrdt_buf *updates, const ycrdt_bu
 /* YMap.toJSON / YArray.toJSON of a root (kind 0 = map, 1 = array) as JSON.stringify text
  * (crdt.js:202,214,304,372,494,528,555,581,607; YMap.toJSON Y@51558, typeListToArray Y@46408) */
 int ycrdt_doc_json(ycrdt_doc *d, const char *root, int kind, ycrdt_out *out);
+/* toJSON of the shared type at a target (parent_key == NULL: root type `root`; else the YMap
+ * (kind 0) / YArray (kind 1) stored in root map `root` under parent_key — crdt.js:423-430 nests one
+ * YArray per key): reads that type's own list only. A key holding no such type gives {} / []. */
+int ycrdt_type_json(ycrdt_doc *d, const char *root, const char *parent_key, int kind, ycrdt_out *out);
+/* The live entries of a YMap target with the id of each entry's winning item, as JSON text
+ * {"key": ["client:clock", value], ...} — what YMap.observe's keysChanged (Y@51190) is computed
+ * from: a key changed iff its winning item changed (crdt.js:620-657 observers). */
+int ycrdt_map_entries(ycrdt_doc *d, const char *root, const char *parent_key, ycrdt_out *out);
 /* YMap.get(key) of root map `root`: *type_ref = the type ref (0 YArray, 1 YMap, ...) when the
  * key holds a live shared type, else -1 (a plain value or nothing)  (crdt.js:423-424) */
 int ycrdt_map_type_at(ycrdt_doc *d, const char *root, const char *key, int32_t *type_ref);

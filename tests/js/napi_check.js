@@ -79,6 +79,54 @@ if (mode === 'cpu') {
   }
   assert.ok(events > 0, 'YMap observers fired');
   console.log('napi ops ok:', n, 'scripts,', events, 'map events');
+} else if (mode === 'observe') {
+  // observer events (tests/golden/observe.json, gen_observe_fixtures.js): the Yjs 13.5.16 events of
+  // every step, replayed through the facade; its events fire at the next read of the doc
+  const cases = JSON.parse(fs.readFileSync(path.join(ROOT, 'tests', 'golden', 'observe.json'))).cases;
+  const norm = (v) => (v === undefined ? null : JSON.parse(JSON.stringify(v)));
+  let nev = 0;
+  for (const c of cases) {
+    const log = [];
+    const rec = (peer, target) => (ev) => {
+      const r = { peer, target, keysChanged: [], keys: {}, delta: [] };
+      if (ev.keysChanged) r.keysChanged = Array.from(ev.keysChanged).sort();
+      for (const [k, ch] of ev.changes.keys) r.keys[k] = [ch.action, norm(ch.oldValue)];
+      if (!ev.keysChanged) r.delta = norm(ev.changes.delta);
+      assert.ok(ev.target && ev.transaction, 'event shape');
+      log.push(r);
+    };
+    const A = new Y.Doc({ clientID: c.clients.A }), B = new Y.Doc({ clientID: c.clients.B });
+    for (const [peer, d] of [['A', A], ['B', B]]) {
+      d.getMap('users').observe(rec(peer, 'users'));
+      d.getArray('messages').observe(rec(peer, 'messages'));
+    }
+    c.steps.forEach((st, i) => {
+      const tag = c.name + ' step ' + i;
+      for (const o of st.ops) {
+        if (o.op === 'map.set') A.getMap('users').set(o.key, o.value);
+        else if (o.op === 'map.delete') A.getMap('users').delete(o.key);
+        else if (o.op === 'map.setArray') A.getMap('users').set(o.key, new Y.Array());
+        else if (o.op === 'nested.insert') A.getMap('users').get(o.key).insert(o.index, o.values);
+        else if (o.op === 'array.insert') A.getArray('messages').insert(o.index, o.values);
+        else if (o.op === 'array.delete') A.getArray('messages').delete(o.index, o.length);
+        else if (o.op === 'c.set') Y.applyUpdate(B, unhex(o.update));
+        else throw new Error(o.op);
+      }
+      Y.applyUpdate(B, unhex(st.sync));
+      const json = { A: norm(A.getMap('users').toJSON()), B: norm(B.getMap('users').toJSON()), Bm: norm(B.getArray('messages').toJSON()) };
+      assert.deepStrictEqual(json, st.json, tag + ' toJSON');
+      if (st.observeNested) {
+        A.getMap('users').get(st.observeNested).observe(rec('A', 'users.' + st.observeNested));
+        B.getMap('users').get(st.observeNested).observe(rec('B', 'users.' + st.observeNested));
+      }
+      const key = (e) => e.peer + ' ' + e.target;
+      const got = log.splice(0).sort((x, y) => (key(x) < key(y) ? -1 : key(x) > key(y) ? 1 : 0));
+      const want = st.events.slice().sort((x, y) => (key(x) < key(y) ? -1 : key(x) > key(y) ? 1 : 0));
+      assert.deepStrictEqual(got, want, tag + ' events');
+      nev += want.length;
+    });
+  }
+  console.log('napi observe ok:', cases.length, 'scripts,', nev, 'events');
 } else if (mode === 'trace') {
   // crdt.js-driven traces (tests/golden/crdtjs_traces.json, gen_crdtjs_traces.js): every Y call
   // crdt.js made on every peer, replayed in order; every wire update / state vector byte-equal

@@ -162,10 +162,25 @@ def test_apply_multi_c5_fleet_large():
         for u in us:
             idx.append(i)
             ups.append(u)
-    crdt_amd.apply_updates_multi([docs[i] for i in idx], ups)
+    crdt_amd.apply_updates_multi(docs, ups, doc_index=idx)
     want = crdt_amd.merge_docs(base)
     for i in range(0, n_docs, 997):
         assert (docs[i].encode_state_as_update(), docs[i].encode_state_vector()) == want[i % len(base)], i
+    # every state at once (ycrdt_docs_states_packed), with a few documents holding deferred applies
+    # (flushed as one batch) and one with a pending struct (its own encode)
+    for i in (3, 4, 5):
+        docs[i].apply_update(base[(i + 1) % len(base)][0])
+    pend = crdt_amd.Doc(client_id=0x7FFFFFF0)
+    pend.apply_update(bytes.fromhex(_PENDING_ONLY))
+    allw = docs + [pend, crdt_amd.Doc(client_id=5)]
+    blob, offs = crdt_amd.states_packed(allw)
+    for i in list(range(0, n_docs, 331)) + [3, 4, 5, n_docs, n_docs + 1]:
+        got = (bytes(blob[offs[2 * i]:offs[2 * i + 1]]), bytes(blob[offs[2 * i + 1]:offs[2 * i + 2]]))
+        assert got == (allw[i].encode_state_as_update(), allw[i].encode_state_vector()), i
+
+
+# one struct of client 7 at clock 1 whose clock-0 predecessor never arrived: Yjs keeps it pending
+_PENDING_ONLY = "010107012801057573657273016201770178" + "00"
 
 
 def test_apply_multi_malformed_applies_prefix(golden):

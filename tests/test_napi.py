@@ -48,3 +48,12 @@ def test_napi_crdtjs_traces_on_gpu():
     raw bytes (compat 135) and every toJSON / get / has the same value (crdt.c, D1 / D7)."""
     out = _run("trace", 600, {"YCRDT_COMPAT": "135"})
     assert "napi trace ok" in out
+
+
+@pytest.mark.gpu
+def test_napi_observer_events_on_gpu():
+    """YMap / YArray observers (crdt.js:620-657) deliver the events Yjs 13.5.16 delivered on the same
+    scripts (tests/golden/observe.json): keysChanged and changes.keys from the entries' winning
+    items, YArray changes.delta, nested arrays observed on their own list; events fire at the next
+    read instead of forcing a merge per Y.applyUpdate."""
+    assert "napi observe ok" in _run("observe", 300)
