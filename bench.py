@@ -199,6 +199,7 @@ def per_op_leg(eng, n_ops_list=(500, 2000)):
         a = crdt_amd.Doc(client_id=1, engine=eng)
         b = crdt_amd.Doc(client_id=2, engine=eng)
         a.track_local(False)
+        dev = 0.0
         t0 = time.perf_counter()
         for i in range(n_ops):
             key = "user%d" % (i % 100)
@@ -207,11 +208,18 @@ def per_op_leg(eng, n_ops_list=(500, 2000)):
             else:
                 a.map_set("users", key, _any_str("v%d" % i))
             u = a.encode_state_as_update()
+            dev += a.last_stats().device_ms
             b.apply_update(u)
             b.root_json("users", "map")
+            dev += b.last_stats().device_ms
         dt = time.perf_counter() - t0
         final = b.encode_state_as_update()
         r = {"ops": n_ops, "ms": round(dt * 1e3, 2), "ops_per_s": round(n_ops / dt, 1),
+             "breakdown": {"merges_per_op": 2, "wall_ms_per_op": round(dt * 1e3 / n_ops, 4),
+                           "device_ms_per_op": round(dev / n_ops, 4),
+                           "host_ms_per_op": round((dt * 1e3 - dev) / n_ops, 4),
+                           "note": "device = the two merges' kernel time (events on the engine stream); host = "
+                                   "launch issue, ~6 host syncs per merge, staging copies, view build, ctypes"},
              "includes": "A: set/delete + full encodeStateAsUpdate; B: applyUpdate + toJSON (crdt.c), ctypes, 1 GPU"}
         y = _yjs_perop(n_ops)
         if y:

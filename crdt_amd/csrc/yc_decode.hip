@@ -898,31 +898,36 @@ __global__ __launch_bounds__(256) void k_scatter_pos(const uint64_t* __restrict_
                                                      uint32_t* __restrict__ out, uint32_t cap, uint32_t* err, uint8_t* __restrict__ swin,
                                                      uint32_t shift) {
   __shared__ uint32_t buf[SCAT_LDS];
-  const uint32_t i0 = blockIdx.x * 256, i = i0 + threadIdx.x;
-  if (i0 >= nwords) return;
-  const uint32_t iend = min(i0 + 256, nwords);
-  const uint32_t base = pre[i0], total = pre[iend] - base;
-  if (base + total > cap) {
-    if (threadIdx.x == 0) raise_err(err, ERR_CAPACITY);
-    return;
+  // a fixed grid walks the 256-word tiles (the per-tile work is small: tens of thousands of
+  // short workgroups were dispatch-bound, 1.2 ms for C2 x 112)
+  const uint32_t ntiles = (nwords + 255) / 256;
+  for (uint32_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    const uint32_t i0 = tile * 256, i = i0 + threadIdx.x;
+    const uint32_t iend = min(i0 + 256, nwords);
+    const uint32_t base = pre[i0], total = pre[iend] - base;
+    if (base + total > cap) {
+      if (threadIdx.x == 0) raise_err(err, ERR_CAPACITY);
+      return;  // (uniform across the workgroup: no barrier left behind)
+    }
+    uint64_t x = i < nwords ? bits[i] : 0ull;
+    uint32_t k = i < nwords ? pre[i] : 0u;
+    // positions within the window; a multi-window batch records the window (a tile's 256 words
+    // never straddle a window: windows are 2^14 words or more)
+    const uint64_t wmask = (1ull << shift) - 1;
+    if (swin) {
+      const uint8_t wn = (uint8_t)(((uint64_t)i0 * 64) >> shift);
+      for (uint32_t t = threadIdx.x; t < total; t += 256) swin[base + t] = wn;
+    }
+    const uint32_t rel = (uint32_t)(((uint64_t)i * 64) & wmask);
+    if (total > SCAT_LDS) {  // a dense stretch: every lane stores its own positions
+      for (; x; x &= x - 1) out[k++] = rel + (uint32_t)__ffsll((long long)x) - 1;
+      continue;
+    }
+    for (k -= base; x; x &= x - 1) buf[k++] = rel + (uint32_t)__ffsll((long long)x) - 1;
+    __syncthreads();
+    for (uint32_t t = threadIdx.x; t < total; t += 256) out[base + t] = buf[t];
+    __syncthreads();  // buf is reused by the next tile
   }
-  uint64_t x = i < nwords ? bits[i] : 0ull;
-  uint32_t k = i < nwords ? pre[i] : 0u;
-  // positions within the window; a multi-window batch records the window (a workgroup's 256
-  // words never straddle a window: windows are 2^14 words or more)
-  const uint64_t wmask = (1ull << shift) - 1;
-  if (swin) {
-    const uint8_t wn = (uint8_t)(((uint64_t)i0 * 64) >> shift);
-    for (uint32_t t = threadIdx.x; t < total; t += 256) swin[base + t] = wn;
-  }
-  const uint32_t rel = (uint32_t)(((uint64_t)i * 64) & wmask);
-  if (total > SCAT_LDS) {  // a dense stretch: every lane stores its own positions
-    for (; x; x &= x - 1) out[k++] = rel + (uint32_t)__ffsll((long long)x) - 1;
-    return;
-  }
-  for (k -= base; x; x &= x - 1) buf[k++] = rel + (uint32_t)__ffsll((long long)x) - 1;
-  __syncthreads();
-  for (uint32_t t = threadIdx.x; t < total; t += 256) out[base + t] = buf[t];
 }
 
 __device__ __forceinline__ uint32_t rank_incl(const uint64_t* __restrict__ bits, const uint32_t* __restrict__ pre, uint32_t p) {
@@ -957,7 +962,7 @@ void launch_struct_count(const Work& w, hipStream_t s) {
 // after it (the struct table is sized from the count): dense struct positions
 void launch_struct_scatter(const Work& w, hipStream_t s) {
   const uint32_t nwords = (w.nbytes + 63) / 64;
-  hipLaunchKernelGGL(k_scatter_pos, dim3(nwords / 256 + 1), dim3(256), 0, s, w.final_bits, w.wcnt, nwords, w.s_pos,
+  hipLaunchKernelGGL(k_scatter_pos, dim3(std::min<uint32_t>(nwords / 256 + 1, 4096)), dim3(256), 0, s, w.final_bits, w.wcnt, nwords, w.s_pos,
                      w.cap_structs, &w.ctr->err, w.nwin > 1 ? w.s_win : nullptr, w.win_shift);
 }
 

@@ -165,10 +165,10 @@ enum Buf {
   B_DWFLAG, B_DWGID, B_DWGSTART, B_DWSIZE, B_DWPOS,
   B_GRIGHT, B_YKEY, B_YKEYS, B_YSEG, B_YIOTA, B_YLSTART, B_YSTATE, B_YBEFORE, B_YCONFL, B_YSTACK,
   B_TKEY, B_TKEYS, B_TSEG, B_TPOS, B_TGSTART, B_TNEXT, B_TDONE, B_TFIRST, B_TNSIB, B_TJUMP, B_TBIG,
-  B_TPRV, B_TMPRV, B_TMTAIL, B_TTREP, B_TOTAIL,
+  B_TPRV, B_TMPRV, B_TMTAIL, B_TTREP, B_TOTAIL, B_THKEY, B_THVAL, B_TFLAG, B_TSCAN,
   B_OFIRST, B_OCIDX, B_OSIZE, B_OPOS, B_RSEG, B_RLEN, B_RSIZE, B_RPOS, B_OUT, B_SVOUT,
   B_VKMAP, B_VKREP, B_VKEYS, B_VNKEYS, B_VPOS, B_VD0, B_VN0, B_VD1, B_VN1, B_VORDER, B_VSEGS,
-  B_SCRATCH2, B_TMP2, B_CAPS, B_CLKEY, B_CLKEY2, B_CHKEY, B_CHVAL, B_CLDOC, B_DSFA, B_EMIT, B_DOCRNG, B_PACK, B_PACKPC, B_KSHARD, B_SOWNER, B_GFLAGS0, B_GFACC,
+  B_SCRATCH2, B_TMP2, B_CAPS, B_CLKEY, B_CLKEY2, B_CHKEY, B_CHVAL, B_CLDOC, B_DSFA, B_EMIT, B_DOCRNG, B_PACK, B_PACKPC, B_SPLITMETA, B_KSHARD, B_SOWNER, B_GFLAGS0, B_GFACC,
   B_COUNT
 };
 
@@ -567,6 +567,27 @@ int check(ycrdt_engine* e, Counters& c, const char* where) {
   return YCRDT_OK;
 }
 
+struct ShardSpec {
+  uint32_t nshards = 1;
+  int32_t shard = -1;  // -1: every shard in turn (logical shards on one GPU)
+  ycrdt_comm* comm = nullptr;
+  // collective bookkeeping: every data exchange is preceded by a status agreement (a max of one
+  // word over the ranks). A rank that fails while its peers head for the next agreement joins that
+  // agreement with a failure status (they all stop there); one that fails inside a data exchange
+  // aborts the communicator (RCCL) instead.
+  mutable bool inside = false;    // between an agreement and the end of its data collectives
+  mutable bool finished = false;  // past the last exchange of the merge
+};
+// the agreement before a data exchange: fails (on every rank) when any rank reports a failure
+int shard_agree(const ShardSpec* sh, hipStream_t s) {
+  uint32_t any = 0;
+  std::string err;
+  if (yc::comm_agree(sh->comm, 0u, s, any, err)) return fail(YCRDT_E_DEVICE, err);
+  if (any) { sh->finished = true; return fail(YCRDT_E_DEVICE, "another rank failed the sharded merge"); }
+  sh->inside = true;
+  return YCRDT_OK;
+}
+
 struct Decoded {
   uint32_t nstructs = 0, nsections = 0, nclients = 0, nds = 0;
   uint64_t nunits = 0, in_len = 0;
@@ -575,9 +596,97 @@ struct Decoded {
   uint32_t nroots = 0;       // items with an explicit parent (key table bound)
 };
 
+// ---- decode split (sharded merge): which updates this rank parses. Updates are dealt to ranks
+// by size (largest first onto the least-loaded rank), identically on every rank; the rank's decode
+// runs over a filtered update list and chunk table (the other updates are staged but not parsed).
+std::vector<uint32_t> split_owners(const ycrdt_batch* b, uint32_t nshards) {
+  const size_t nu = b->ulen.size();
+  std::vector<uint32_t> idx(nu), owner(nu, 0);
+  for (size_t u = 0; u < nu; ++u) idx[u] = (uint32_t)u;
+  std::stable_sort(idx.begin(), idx.end(), [&](uint32_t x, uint32_t y) { return b->ulen[x] > b->ulen[y]; });
+  std::vector<uint64_t> load(nshards, 0);
+  for (const uint32_t u : idx) {
+    const uint32_t r = (uint32_t)(std::min_element(load.begin(), load.end()) - load.begin());
+    owner[u] = r;
+    load[r] += b->ulen[u] + 64;
+  }
+  return owner;
+}
+int split_decode_meta(ycrdt_engine* e, ycrdt_batch* b, const ShardSpec* sh, Work& wd) {
+  const uint32_t me = (uint32_t)sh->shard;
+  const std::vector<uint32_t> owner = split_owners(b, sh->nshards);
+  const size_t nu = b->ulen.size();
+  std::vector<uint32_t> ul, ug(b->ugroup);
+  std::vector<Group> gr;
+  uint32_t nbig = 0;
+  for (uint32_t i = 0; i < b->ulist.size(); ++i) {
+    const uint32_t u = b->ulist[i];
+    if (owner[u] != me) continue;
+    ul.push_back(u);
+    if (i < b->nbig) {  // its chunks, renumbered into this rank's chunk table
+      ++nbig;
+      const uint32_t g0 = b->ugroup[u];
+      ug[u] = (uint32_t)gr.size();
+      for (uint32_t g = g0; g < b->groups.size() && b->groups[g].upd == u; ++g) gr.push_back(b->groups[g]);
+    }
+  }
+  const size_t bytes = sizeof(uint32_t) * (nu + 1) * 2 + sizeof(Group) * (gr.size() + 1) + 64;
+  bool ok = true;
+  uint8_t* m = take<uint8_t>(e->bufs, B_SPLITMETA, bytes, ok);
+  if (!ok) return fail(YCRDT_E_DEVICE, oom("decode split"));
+  std::vector<uint8_t> h(bytes, 0);
+  memcpy(h.data(), ul.data(), sizeof(uint32_t) * ul.size());
+  memcpy(h.data() + sizeof(uint32_t) * (nu + 1), ug.data(), sizeof(uint32_t) * nu);
+  const size_t goff = (sizeof(uint32_t) * (nu + 1) * 2 + 15) & ~size_t(15);
+  if (!gr.empty()) memcpy(h.data() + goff, gr.data(), sizeof(Group) * gr.size());
+  HIPCHK(hipMemcpyAsync(m, h.data(), bytes, hipMemcpyHostToDevice, e->stream));
+  wd.ulist = (const uint32_t*)m;
+  wd.nbig = nbig;
+  wd.nsmall = (uint32_t)ul.size() - nbig;
+  wd.ugroup = (const uint32_t*)(m + sizeof(uint32_t) * (nu + 1));
+  wd.groups = (const Group*)(m + goff);
+  wd.ngroups = (uint32_t)gr.size();
+  // updates parsed elsewhere leave their delete-set start 0 here (combined by a max)
+  HIPCHK(hipMemsetAsync(wd.dsstart, 0, sizeof(uint32_t) * (nu + 1), e->stream));
+  return YCRDT_OK;
+}
+// every rank's parse results combined: struct-start and section-start bitmaps (disjoint words:
+// updates are 64-byte aligned, so a sum is the union), delete-set starts (max), the error word
+// (max), and the section records (all-gathered, rank after rank)
+int split_decode_exchange(ycrdt_engine* e, ycrdt_batch* b, const ShardSpec* sh) {
+  Work& w = e->w;
+  hipStream_t s = e->stream;
+  std::string err;
+  if (const int rc = shard_agree(sh, s)) return rc;
+  const uint64_t nwords = ((uint64_t)b->nbytes + 64) / 64 + 2;
+  const size_t nu = b->ulen.size();
+  if (yc::comm_allreduce_u32(sh->comm, (uint32_t*)w.final_bits, 2 * nwords, false, s, err) ||
+      yc::comm_allreduce_u32(sh->comm, (uint32_t*)w.sec_bits, 2 * nwords, false, s, err) ||
+      yc::comm_allreduce_u32(sh->comm, w.dsstart, nu + 1, true, s, err) ||
+      yc::comm_allreduce_u32(sh->comm, &w.ctr->err, 1, true, s, err))
+    return fail(YCRDT_E_DEVICE, err);
+  uint32_t nsec = 0;
+  HIPCHK(hipMemcpyAsync(&nsec, &w.ctr->nsections, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+  HIPCHK(hipStreamSynchronize(s));
+  std::vector<Section> mine(nsec);
+  if (nsec) HIPCHK(hipMemcpy(mine.data(), w.sections, sizeof(Section) * nsec, hipMemcpyDeviceToHost));
+  std::vector<std::vector<uint8_t>> parts;
+  if (yc::comm_allgather_updates(sh->comm, (const uint8_t*)mine.data(), sizeof(Section) * nsec, s, parts, err))
+    return fail(YCRDT_E_DEVICE, err);
+  std::vector<uint8_t> all;
+  for (const auto& p : parts) all.insert(all.end(), p.begin(), p.end());
+  const uint32_t total = (uint32_t)(all.size() / sizeof(Section));
+  if (total > w.cap_sections) return fail(YCRDT_E_CAPACITY, "decode split: sections past the estimate");
+  if (total) HIPCHK(hipMemcpyAsync(w.sections, all.data(), all.size(), hipMemcpyHostToDevice, s));
+  HIPCHK(hipMemcpyAsync(&w.ctr->nsections, &total, sizeof(uint32_t), hipMemcpyHostToDevice, s));
+  HIPCHK(hipStreamSynchronize(s));
+  sh->inside = false;
+  return YCRDT_OK;
+}
+
 // K1: decode every update of the batch into the struct SoA (+ client table, delete-set ranges).
 // lazy = mergeUpdates / diffUpdate mode: references stay raw client ids, no client states.
-int run_decode(ycrdt_engine* e, ycrdt_batch* b, bool lazy, Decoded& D, bool generous = false) {
+int run_decode(ycrdt_engine* e, ycrdt_batch* b, bool lazy, Decoded& D, bool generous = false, const ShardSpec* sh = nullptr) {
   Work& w = e->w;
   auto& V = e->bufs;
   bool ok = true;
@@ -666,19 +775,36 @@ int run_decode(ycrdt_engine* e, ycrdt_batch* b, bool lazy, Decoded& D, bool gene
   // ---- K1 decode
   // large updates (chunk path, mostly latency-bound) on the side stream, beside k_direct
   mark(e, "decode.direct");
+  // decode split across the ranks of a sharded merge: each rank parses only
+  // its share of the updates (byte-balanced), then the struct / section bitmaps, the delete-set
+  // starts and the section records are combined, and every rank continues on the same tables
+  const bool split = sh && sh->comm && sh->nshards > 1 && !lazy;
+  Work wd = w;
+  if (split) {
+    const int rc0 = split_decode_meta(e, b, sh, wd);
+    if (rc0) return rc0;
+  }
   HIPCHK(hipEventRecord(e->side_fork, s));
   HIPCHK(hipStreamWaitEvent(e->side, e->side_fork, 0));
-  launch_chunks(w, e->side);
+  launch_chunks(wd, e->side);
   HIPCHK(hipEventRecord(e->side_done, e->side));
-  launch_direct(w, s);
+  launch_direct(wd, s);
   HIPCHK(hipStreamWaitEvent(s, e->side_done, 0));
+  if (split) {
+    mark(e, "decode.exchange");
+    // test hook (tests/test_gpu_exchange.py): this rank fails on the host before the exchange
+    const char* fh = getenv("YCRDT_TEST_FAIL_BEFORE_EXCHANGE");
+    if (fh && fh[0] == '1') return fail(YCRDT_E_DEVICE, "test hook: failure before the decode exchange");
+    const int rc0 = split_decode_exchange(e, b, sh);
+    if (rc0) return rc0;
+  }
   mark(e, "decode.bitmap");
   launch_struct_count(w, s);
   launch_ds_bound(w, s);
   if (!w.nupd) HIPCHK(hipMemcpyAsync(&w.ctr->nstructs, w.wcnt + (w.nbytes + 63) / 64, sizeof(uint32_t), hipMemcpyDeviceToDevice, s));
   Counters c;
   int rc = check(e, c, "decode");
-  if (rc == YCRDT_E_CAPACITY && !generous) return run_decode(e, b, lazy, D, true);  // past the estimates
+  if (rc == YCRDT_E_CAPACITY && !generous) return run_decode(e, b, lazy, D, true, sh);  // past the estimates
   if (rc) return rc;
   const uint32_t nstructs = c.nstructs;
   const uint32_t nsections = c.nsections;
@@ -777,12 +903,6 @@ int run_decode(ycrdt_engine* e, ycrdt_batch* b, bool lazy, Decoded& D, bool gene
 // `caps` (optional) integrates every client only up to its cap (Yjs pending structs, yc_ingest.h).
 // `order` (compat 135): the doc store's client insertion order, the delete-set / state-vector order.
 // `sh`: key-hash shards of one document (all of them on this GPU, or this rank's over RCCL).
-struct ShardSpec {
-  uint32_t nshards = 1;
-  int32_t shard = -1;  // -1: every shard in turn (logical shards on one GPU)
-  ycrdt_comm* comm = nullptr;
-  mutable bool agreed = false;  // this rank reached the pre-exchange status agreement
-};
 int comm_allreduce_sum_u32(ycrdt_comm* c, uint32_t* buf, size_t n, hipStream_t s) {
   std::string err;
   if (yc::comm_allreduce_u32(c, buf, n, false, s, err)) return fail(YCRDT_E_DEVICE, err);
@@ -811,7 +931,7 @@ int run_merge(ycrdt_engine* e, ycrdt_batch* b, const std::unordered_map<uint32_t
     w.capped = 1;
   }
   Decoded D;
-  int rc = run_decode(e, b, false, D);
+  int rc = run_decode(e, b, false, D, false, sh);
   if (rc) return rc;
   Counters c;
   const uint32_t nstructs = D.nstructs, nclients = D.nclients, nds = D.nds;
@@ -923,6 +1043,9 @@ int run_merge(ycrdt_engine* e, ycrdt_batch* b, const std::unordered_map<uint32_t
                        B_TKEY, B_TKEYS, B_TSEG, B_TPOS, B_TGSTART, B_TNEXT, B_TDONE, B_TFIRST, B_TNSIB, B_TJUMP,
                        B_TBIG, B_TPRV, B_TMPRV, B_TMTAIL, B_TTREP, B_TOTAIL};
     for (size_t k = 0; k < sizeof(ids) / sizeof(ids[0]); ++k) *cols[k] = take<uint32_t>(V, ids[k], n + 2, okl);
+    w.t_hkey = take<uint32_t>(V, B_THKEY, 2 * n + 4, okl);
+    w.t_hval = take<uint32_t>(V, B_THVAL, 2 * n + 4, okl);
+    w.t_flag = take<uint32_t>(V, B_TFLAG, 2 * n + 4, okl);  // flags, then their scan behind them
     return okl;
   };
   uint32_t nout = 0;
@@ -988,13 +1111,11 @@ int run_merge(ycrdt_engine* e, ycrdt_batch* b, const std::unordered_map<uint32_t
       if (sh->comm) {
         // every rank reports before the data collective: a rank that failed earlier joins only
         // this agreement (ycrdt_batch_merge_sharded), so no peer waits in a sum it never enters
-        uint32_t any = 0;
-        std::string err;
-        sh->agreed = true;
-        if (yc::comm_agree(sh->comm, 0u, s, any, err)) return fail(YCRDT_E_DEVICE, err);
-        if (any) return fail(YCRDT_E_DEVICE, "another rank failed the sharded merge before the exchange");
+        if (const int rc1 = shard_agree(sh, s)) return rc1;
         const int rc2 = comm_allreduce_sum_u32(sh->comm, acc, nsegs, s);
         if (rc2) return rc2;
+        sh->inside = false;
+        sh->finished = true;  // the merge's last exchange
       }
       HIPCHK(hipMemcpyAsync(w.g_flags, acc, sizeof(uint32_t) * nsegs, hipMemcpyDeviceToDevice, s));
       launch_merge_final(w, nsegs, s);
@@ -2201,12 +2322,15 @@ int ycrdt_batch_merge_sharded(ycrdt_batch* b, ycrdt_comm* comm, uint32_t nshards
   }
   HIPCHK(hipSetDevice(b->e->device));
   int rc = run_merge(b->e, b, nullptr, nullptr, nullptr, &sh);
-  if (rc != YCRDT_OK && comm && !sh.agreed) {
-    // failed before the exchange: tell the peers (they are waiting in the agreement), keep the error
+  if (rc != YCRDT_OK && comm && !sh.finished) {
     const std::string keep = g_err;
-    uint32_t any = 0;
-    std::string err;
-    if (yc::comm_agree(comm, 1u, b->e->stream, any, err)) yc::comm_abort(comm);
+    if (sh.inside) {
+      yc::comm_abort(comm);  // inside a data exchange: the peers' collectives return
+    } else {                 // the peers wait in the next agreement: join it with a failure status
+      uint32_t any = 0;
+      std::string err;
+      if (yc::comm_agree(comm, 1u, b->e->stream, any, err)) yc::comm_abort(comm);
+    }
     g_err = keep;
   }
   if (rc == YCRDT_OK) {

@@ -37,6 +37,7 @@ struct Counters {            // device-side counters, read back at the few host 
   uint32_t nroots_sh[NSHARD]; // items with an explicit parent, sharded by workgroup (summed on the host)
   uint32_t nroots;           // items with an explicit parent (bound on the distinct lists: key table size)
   uint32_t pad[12];          // encode scratch (see yc_encode.hip)
+  uint32_t climb_open[40];   // per pointer-jumping round of the YArray climb: pairs still open (yc_yata.hip)
   unsigned long long out_total; // encoded output size (integrate encoder; 64-bit)
   unsigned long long ds_base;   // integrate encoder: byte position of the delete-set section
   unsigned long long items;  // Σ clock lengths of Skip structs (items = Σ all lengths − this)
@@ -207,6 +208,9 @@ struct Work {
   uint32_t* t_mprv = nullptr;      // [NS] previous member of the same right-origin group
   uint32_t* t_mtail = nullptr;     // [NS] last member of the group whose right origin is this sibling
   uint32_t* t_otail = nullptr;     // [NS] last member of the outside-right-origin group anchored here
+  uint32_t* t_hkey = nullptr;      // [2 NS + 4] huge sibling groups: anchor hash keys (right-origin units)
+  uint32_t* t_hval = nullptr;      // [2 NS + 4]   its first member (lowest group position)
+  uint32_t* t_flag = nullptr;      // [NS + 2]   chain starts of a huge group, then their scan
   uint32_t* t_trep = nullptr;      // [NS] anchor of the member's right-origin group
   // ---- lazy merge (mergeUpdates / diffUpdate, yc_lazy.hip)
   uint32_t* usec_start = nullptr;  // [nupd] first section of every update (walker order)

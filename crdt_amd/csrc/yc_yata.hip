@@ -14,6 +14,8 @@
 // per-clock restatement) and the loop can step over segments instead of units.
 #include <cstdlib>
 #include <cstring>
+#include <utility>
+#include <vector>
 
 #include "yc_work.h"
 
@@ -503,7 +505,7 @@ template <uint32_t CAP, uint32_t HS, bool MID>
 __global__ __launch_bounds__(256) void k_tsib_big(Work w, uint32_t nsegs) {
   const uint32_t g = w.t_big[blockIdx.x];
   const uint32_t a = w.t_gstart[g], n = w.t_gstart[g + 1] - a;
-  if (MID ? n > CAP : n <= TMID) return;
+  if (MID ? n > CAP : (n <= TMID || n > CAP)) return;  // n > TLDS: the grid-wide huge-group path
   __shared__ SibRec rec[CAP];
   __shared__ uint8_t st[CAP];
   __shared__ uint32_t hkey[HS], hval[HS];
@@ -690,27 +692,209 @@ __global__ __launch_bounds__(256) void k_tsib_big(Work w, uint32_t nsegs) {
   }
   if (threadIdx.x == 0 && head_s != NONE) sib_publish(w, a, n, nsegs, head_s);
 }
-// pre-order successor: first child, else the next sibling of the nearest ancestor-or-self with one
-__global__ __launch_bounds__(256) void k_tclimb(Work w, uint32_t nsegs) {
+// ---- Huge sibling groups (more members than TLDS): the member passes of k_tsib_big — right-origin
+// anchors, chain marks, chain numbering, the expansion — run grid-wide over the group, and only the
+// loop over the collapsed chains runs on one lane (with the chains in LDS). In one workgroup those
+// passes were latency-bound (C3's list head, 790 k members: ≈9.7 ms, of 16 ms of YATA).
+// Group descriptors: the host reads (start, size) of every big group after k_tsib_small.
+__global__ void k_tbig_desc(Work w, uint32_t nbig, uint32_t* __restrict__ desc) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= nbig) return;
+  const uint32_t g = w.t_big[i], a = w.t_gstart[g];
+  desc[2 * i] = a;
+  desc[2 * i + 1] = w.t_gstart[g + 1] - a;
+}
+// anchors: the first member of every outside right-origin unit (global open addressing, P slots)
+__global__ __launch_bounds__(256) void k_thuge_hash(Work w, uint32_t a, uint32_t n, uint32_t P) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n || w.y_confl[a + i] != NONE) return;
+  const uint32_t r0 = w.y_before[a + i], r = r0 == NONE ? HNONE : r0;
+  uint32_t slot = (r * 2654435761u) & (P - 1);
+  for (uint32_t probe = 0; probe < P; ++probe) {
+    const uint32_t old = atomicCAS(&w.t_hkey[slot], NONE, r);
+    if (old == NONE || old == r) { atomicMin(&w.t_hval[slot], i); return; }
+    slot = (slot + 1) & (P - 1);
+  }
+  raise_err(&w.ctr->err, ERR_CAPACITY);
+}
+// right-origin group anchor of every member (t_trep, as k_tsib_big) and the chain marks: t_mtail[p]
+// = 0 where p is named as right origin by a member other than its chain successor
+__global__ __launch_bounds__(256) void k_thuge_anchor(Work w, uint32_t a, uint32_t n, uint32_t P) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint32_t rp = w.y_confl[a + i];
+  uint32_t t = rp;
+  if (rp == NONE) {
+    const uint32_t r0 = w.y_before[a + i], r = r0 == NONE ? HNONE : r0;
+    uint32_t slot = (r * 2654435761u) & (P - 1);
+    for (uint32_t probe = 0; probe < P && w.t_hkey[slot] != r; ++probe) slot = (slot + 1) & (P - 1);
+    t = (w.t_hkey[slot] == r ? a + w.t_hval[slot] : a + i) | 0x80000000u;
+  } else if (rp + 1 != a + i || w.y_state[a + i] != w.y_state[rp]) {
+    w.t_mtail[rp] = 0;  // (plain stores of the same value)
+  }
+  w.t_trep[a + i] = t;
+}
+// chain starts (a member that does not continue the chain of the member before it)
+__global__ __launch_bounds__(256) void k_thuge_flags(Work w, uint32_t a, uint32_t n) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i > n) return;
+  if (i == n) { w.t_flag[i] = 0; return; }
+  const bool link = i > 0 && w.y_confl[a + i] == a + i - 1 && w.y_state[a + i] == w.y_state[a + i - 1] &&
+                    w.t_mtail[a + i - 1] == NONE;
+  w.t_flag[i] = link ? 0u : 1u;
+}
+// node numbering: t_prv[a + i] = node of position i, t_next[a + k] = first position of node k
+__global__ __launch_bounds__(256) void k_thuge_nodes(Work w, uint32_t a, uint32_t n) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint32_t* pre = w.t_flag + n + 1;  // exclusive scan of the flags
+  const uint32_t k = pre[i] + w.t_flag[i] - 1;
+  w.t_prv[a + i] = k;
+  if (w.t_flag[i]) w.t_next[a + k] = i;
+}
+// the loop over the nn collapsed chains (nn <= TLDS) on one lane, the chains staged in LDS; each
+// chain's successor in the sibling order goes to t_mprv[a + k] (NONE: last), the first to head
+__global__ __launch_bounds__(256) void k_thuge_loop(Work w, uint32_t a, uint32_t n) {
+  __shared__ SibRec rec[TLDS];
+  __shared__ uint8_t st[TLDS];
+  __shared__ uint32_t head_s;
+  const uint32_t nn = w.t_flag[n + 1 + n];
+  if (nn > TLDS) return;  // k_thuge_inplace
+  const uint32_t* node = w.t_prv + a;
+  const uint32_t* nfirst = w.t_next + a;
+  for (uint32_t k = threadIdx.x; k < nn; k += blockDim.x) {
+    const uint32_t f = nfirst[k];
+    const uint32_t rp = w.y_confl[a + f];
+    const uint32_t t = w.t_trep[a + f];
+    const uint32_t tq = node[(t & 0x7FFFFFFFu) - a];
+    rec[k] = SibRec{w.y_state[a + f], (uint16_t)(rp == NONE ? S_NONE : node[rp - a]),
+                    (uint16_t)(tq | ((t >> 31) ? TOUT : 0u)), S_NONE, S_NONE, S_NONE, S_NONE, S_NONE, 0};
+    st[k] = 0;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    SibLds acc{rec, st};
+    head_s = sib_loop(acc, nn, w.y_stack + a, &w.ctr->err);
+    w.t_flag[2 * n + 2] = head_s;  // (read by the expansion)
+  }
+  __syncthreads();
+  for (uint32_t k = threadIdx.x; k < nn; k += blockDim.x) {
+    const uint32_t x = rec[k].nxt;
+    w.t_mprv[a + k] = x == S_NONE ? NONE : x;
+  }
+}
+// expansion: node k spans positions nfirst[k] .. nfirst[k + 1] - 1, listed from the last down
+__global__ __launch_bounds__(256) void k_thuge_expand(Work w, uint32_t a, uint32_t n, uint32_t nsegs) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t nn = w.t_flag[n + 1 + n];
+  if (nn > TLDS || i >= n) return;
+  const uint32_t* node = w.t_prv + a;
+  const uint32_t* nfirst = w.t_next + a;
+  auto leftmost = [&](uint32_t k) { return (k + 1 < nn ? nfirst[k + 1] : n) - 1; };
+  const uint32_t k = node[i], f = nfirst[k];
+  uint32_t nx;
+  if (i > f) nx = i - 1;
+  else {
+    const uint32_t kn = w.t_mprv[a + k];
+    nx = kn == NONE ? NONE : leftmost(kn);
+  }
+  w.t_nsib[w.t_seg[a + i]] = nx == NONE ? NONE : w.t_seg[a + nx];
+  if (i == 0) {
+    const uint32_t head = w.t_flag[2 * n + 2];
+    if (head != NONE) sib_publish(w, a, n, nsegs, leftmost(head));
+  }
+}
+// too many chains for LDS: restore the scratch and run the loop in place over the group (one lane)
+__global__ __launch_bounds__(256) void k_thuge_inplace(Work w, uint32_t a, uint32_t n, uint32_t nsegs) {
+  __shared__ uint32_t head_s;
+  const uint32_t nn = w.t_flag[n + 1 + n];
+  if (nn <= TLDS) return;
+  for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) {
+    w.t_mtail[a + i] = NONE;
+    w.t_prv[a + i] = NONE;
+    w.t_next[a + i] = NONE;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    SibGlobal acc{w, a};
+    head_s = sib_loop(acc, n, w.y_stack + a, &w.ctr->err);
+  }
+  __syncthreads();
+  for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) {
+    const uint32_t x = w.t_next[a + i];
+    w.t_nsib[w.t_seg[a + i]] = x == NONE ? NONE : w.t_seg[x];
+  }
+  if (threadIdx.x == 0 && head_s != NONE) sib_publish(w, a, n, nsegs, head_s);
+}
+void launch_tsib_huge(const Work& w, uint32_t a, uint32_t n, uint32_t nsegs, hipStream_t s) {
+  uint32_t P = 64;  // load < 2/3, within the 2 nsegs + 4 slots of t_hkey / t_hval (P > n always)
+  while (P < n + n / 2 + 1 && 2ull * P <= 2ull * nsegs + 4) P <<= 1;
+  fill_u32_multi({{w.t_hkey, P, NONE}, {w.t_hval, P, NONE}}, s);
+  const uint32_t grid = n / 256 + 1;
+  hipLaunchKernelGGL(k_thuge_hash, dim3(grid), dim3(256), 0, s, w, a, n, P);
+  hipLaunchKernelGGL(k_thuge_anchor, dim3(grid), dim3(256), 0, s, w, a, n, P);
+  hipLaunchKernelGGL(k_thuge_flags, dim3(grid), dim3(256), 0, s, w, a, n);
+  scan_u32(w.tmp, w.tmp_bytes, w.t_flag, w.t_flag + n + 1, n + 1, s);  // [n + 1 + n] = the chain count
+  hipLaunchKernelGGL(k_thuge_nodes, dim3(grid), dim3(256), 0, s, w, a, n);
+  hipLaunchKernelGGL(k_thuge_loop, dim3(1), dim3(256), 0, s, w, a, n);
+  hipLaunchKernelGGL(k_thuge_expand, dim3(grid), dim3(256), 0, s, w, a, n, nsegs);
+  hipLaunchKernelGGL(k_thuge_inplace, dim3(1), dim3(256), 0, s, w, a, n, nsegs);
+}
+
+// Pre-order successor: the first child, else the next sibling of the nearest ancestor-or-self that
+// has one. "The nearest ancestor-or-self with a next sibling" is found by pointer jumping in rounds
+// (Wyllie): every array segment holds (ans, nxt) — ans its answer once known, nxt the next ancestor
+// to look at — and a round replaces an open pair by its nxt's pair: ans = ans[nxt], nxt =
+// nxt[nxt] while that is still open. The distance to the answer halves every round, so a path of
+// d only-children closes in ceil(log2 d) rounds; each round is a coalesced pass (double-buffered,
+// no races), where the lane-serial climb with path halving it replaces walked C3's long push
+// chains at memory latency (4.7 ms). A round launched after the last open pair closed returns at
+// once (its predecessor's "open" word is zero).
+constexpr uint32_t CLIMB_ROUNDS = 34;  // > log2 of any segment count, +1 (<= Counters::climb_open)
+__global__ __launch_bounds__(256) void k_tclimb_init(Work w, uint32_t nsegs, uint32_t* __restrict__ ans, uint32_t* __restrict__ nxt,
+                                                     uint32_t* __restrict__ open) {
   const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
+  if (s < CLIMB_ROUNDS) open[s] = 0;  // the per-round "pairs still open" words
+  if (s >= nsegs) return;
+  const bool arr = (w.g_flags[s] & SEG_ARRAY) != 0;
+  const uint32_t ns = arr ? w.t_nsib[s] : NONE;
+  ans[s] = ns;
+  nxt[s] = arr && ns == NONE ? w.t_jump[s] : NONE;  // the parent (NONE: a child of the list's root)
+}
+__global__ __launch_bounds__(256) void k_tclimb_round(uint32_t nsegs, const uint32_t* __restrict__ ans0, const uint32_t* __restrict__ nxt0,
+                                                      uint32_t* __restrict__ ans1, uint32_t* __restrict__ nxt1, uint32_t* __restrict__ open,
+                                                      uint32_t round) {
+  if (round > 0 && __hip_atomic_load(&open[round - 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) return;
+  const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= nsegs) return;
+  uint32_t a = ans0[s], n = nxt0[s];
+  if (n != NONE) {  // open: a == NONE
+    a = ans0[n];
+    n = a != NONE ? NONE : nxt0[n];
+  }
+  ans1[s] = a;
+  nxt1[s] = n;
+  wave_flag(&open[round], n != NONE);
+}
+__global__ __launch_bounds__(256) void k_tclimb_done(Work w, uint32_t nsegs, const uint32_t* __restrict__ ans, const uint32_t* __restrict__ nxt,
+                                                     const uint32_t* __restrict__ open) {
+  const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
+  if (s == 0 && open[CLIMB_ROUNDS - 1]) raise_err(&w.ctr->err, ERR_DECODE);  // still open: an origin cycle
   if (s >= nsegs || !(w.g_flags[s] & SEG_ARRAY)) return;
   const uint32_t fc = w.t_first[s];
-  if (fc != NONE) { w.g_right[s] = fc; return; }
-  uint32_t y = s, res = NONE;
-  bool end = false;
-  for (uint32_t it = 0; it <= nsegs; ++it) {  // more hops than segments: an origin cycle
-    const uint32_t ns = w.t_nsib[y];
-    if (ns != NONE) { res = ns; end = true; break; }
-    const uint32_t z = w.t_jump[y];  // an ancestor whose answer is y's (every node between has no next sibling)
-    if (z == NONE) { end = true; break; }  // a last child of the list's root: the end of the list
-    if (w.t_nsib[z] == NONE) {       // path halving: y inherits z's link
-      const uint32_t zz = w.t_jump[z];
-      if (zz != z) w.t_jump[y] = zz;
-    }
-    y = z;
+  w.g_right[s] = fc != NONE ? fc : ans[s];
+}
+void launch_tclimb(const Work& w, uint32_t nsegs, hipStream_t s) {
+  const uint32_t grid = nsegs / 256 + 1;
+  // two (ans, nxt) buffers: the sibling-loop scratch is free once the groups are ordered
+  uint32_t *A0 = w.t_prv, *N0 = w.t_mprv, *A1 = w.t_mtail, *N1 = w.t_otail, *open = w.ctr->climb_open;
+  hipLaunchKernelGGL(k_tclimb_init, dim3(grid), dim3(256), 0, s, w, nsegs, A0, N0, open);
+  for (uint32_t r = 0; r < CLIMB_ROUNDS; ++r) {
+    hipLaunchKernelGGL(k_tclimb_round, dim3(grid), dim3(256), 0, s, nsegs, A0, N0, A1, N1, open, r);
+    std::swap(A0, A1);
+    std::swap(N0, N1);
   }
-  if (!end) raise_err(&w.ctr->err, ERR_DECODE);
-  w.g_right[s] = res;
+  hipLaunchKernelGGL(k_tclimb_done, dim3(grid), dim3(256), 0, s, w, nsegs, A0, N0, open);
 }
 
 uint32_t launch_yata_tree(const Work& w, uint32_t nsegs, hipStream_t s) {
@@ -729,8 +913,15 @@ uint32_t launch_yata_tree(const Work& w, uint32_t nsegs, hipStream_t s) {
   if (nbig) {
     hipLaunchKernelGGL((k_tsib_big<TMID, 2048, true>), dim3(nbig), dim3(256), 0, s, w, nsegs);
     hipLaunchKernelGGL((k_tsib_big<TLDS, THASH, false>), dim3(nbig), dim3(256), 0, s, w, nsegs);
+    // the huge groups (> TLDS members): their (start, size) to the host, then the grid-wide path
+    std::vector<uint32_t> desc(2 * (size_t)nbig);
+    hipLaunchKernelGGL(k_tbig_desc, dim3(nbig / 256 + 1), dim3(256), 0, s, w, nbig, w.t_hkey);
+    hipMemcpyAsync(desc.data(), w.t_hkey, sizeof(uint32_t) * desc.size(), hipMemcpyDeviceToHost, s);
+    hipStreamSynchronize(s);
+    for (uint32_t i = 0; i < nbig; ++i)
+      if (desc[2 * i + 1] > TLDS) launch_tsib_huge(w, desc[2 * i], desc[2 * i + 1], nsegs, s);
   }
-  hipLaunchKernelGGL(k_tclimb, dim3(grid), dim3(256), 0, s, w, nsegs);
+  launch_tclimb(w, nsegs, s);
   return nbig;
 }
 

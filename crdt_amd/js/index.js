@@ -87,6 +87,7 @@ function fireObservers(doc) {
           event.keysChanged.add(k);
           event.changes.keys.set(k, { action: !ina ? 'add' : !inb ? 'delete' : 'update', oldValue: ina ? a[k][1] : undefined });
         }
+        if (!event.keysChanged.size) continue;  // only nested contents changed: not this map's event
       } else {
         event.changes.delta = arrayDelta(a, b);
       }

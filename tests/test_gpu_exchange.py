@@ -5,13 +5,17 @@ library's own code runs on both ranks — shard export, the pre-exchange status 
 sum, the fleet key-space build and MAX all-reduce, the delete-set all-gather — and every result is
 checked against Yjs fixtures / the unsharded merge:
 
-* sharded merge of ONE document (C4 shape): each rank integrates its key-hash shard,
-  the flag words are summed, and both ranks encode bytes equal to the unsharded merge (Yjs state);
+* sharded merge of ONE document (C4 shape): each rank parses only its share of the
+  updates (the struct / section bitmaps, delete-set starts and section records are combined), then
+  integrates its key-hash shard; the flag words are summed, and both ranks encode bytes equal to
+  the unsharded merge (Yjs state);
 * fleet state vectors (C5): each rank merges a different part of every document's updates; the
   exchanged state vectors equal Yjs's state vectors of the whole documents;
 * delete-set all-gather: each rank's part of a document; the union equals the delete set of
   Y.mergeUpdates over all parts;
-* a rank that fails before the exchange makes the other rank's call fail too (no hang).
+* a malformed update parsed by one rank fails the merge on every rank; a rank that fails on the
+  host before the exchange makes the other rank's call fail too (no hang), and the communicator
+  keeps working.
 """
 import json
 import os
@@ -85,15 +89,31 @@ def _worker(rank, world, port, q):
             union = comm.ds_allgather(mine)
             ds_ok.append(delete_set_of(union) == delete_set_of(crdt_amd.merge_updates(ups, eng)))
         out["ds"] = ds_ok
-        # ---- failure before the exchange on rank 1: both ranks get an error, nobody hangs
-        ups = docs[0]
-        bad = [b"\x01\xff\xff"] if rank == 1 else []
+        # ---- a malformed update parsed by one rank: the error reaches every rank
+        ups = list(docs[0])
+        ups[3] = b"\x01\xff" + bytes(len(ups[3]) - 2)  # same length: the same layout on every rank
         try:
-            b = crdt_amd.Batch(ups + bad, eng)
+            b = crdt_amd.Batch(ups, eng)
             b.merge_sharded(world, comm)
             out["fail"] = "no error"
         except crdt_amd.YcrdtError as e:
             out["fail"] = e.kind
+        # ---- rank 1 fails on the host before the exchange: rank 0 gets an error too, nobody hangs
+        if rank == 1:
+            os.environ["YCRDT_TEST_FAIL_BEFORE_EXCHANGE"] = "1"
+        try:
+            b = crdt_amd.Batch(docs[0], eng)
+            b.merge_sharded(world, comm)
+            out["fail2"] = "no error"
+        except crdt_amd.YcrdtError as e:
+            out["fail2"] = e.kind
+        os.environ.pop("YCRDT_TEST_FAIL_BEFORE_EXCHANGE", None)
+        # ---- and the communicator still works afterwards
+        b = crdt_amd.Batch(docs[1], eng)
+        b.merge_sharded(world, comm)
+        got = b.result()
+        b.merge()
+        out["after"] = got == b.result()
         comm.close()
     except Exception as e:  # noqa: BLE001 — reported to the parent
         out["error"] = repr(e)
@@ -125,4 +145,6 @@ def test_exchanges_world2_gloo_one_gpu():
             assert got == want
         assert all(r["ds"]), r["ds"]
         assert r["fail"] != "no error", r
+        assert r["fail2"] != "no error", r
+        assert r["after"], r
     assert res[0]["fleet"] == res[1]["fleet"]
