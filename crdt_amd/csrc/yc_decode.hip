@@ -461,7 +461,22 @@ __global__ __launch_bounds__(DL) void k_spec(Work w) {
     }
     m |= 1ull << (p & 63);
     if (__ballot(p - src.s0 + DREFILL > src.wlen)) refill(p);  // the whole wavefront at once: one stall, not one per lane
-    const uint32_t d = chain_len(src, b, p, uend);
+    uint32_t d;
+    if (w.spec_exact) {
+      d = chain_len(src, b, p, uend);
+    } else {  // experiment: a handed-over struct is stepped over byte by byte (the walker re-parses exactly)
+      const uint32_t info = src.u8(p), ref = info & 31u;
+      d = 0;
+      if (ref == REF_GC || ref == REF_SKIP) {
+        uint32_t q = p + 1;
+        bool okv = true;
+        vu_fast(src, q, uend, okv);
+        d = okv ? q - p : 0u;
+      } else if (ref >= 1 && ref <= REF_DOC) {
+        d = spec_len(src, p, uend, (ref - 1) * 8 + (info >> 5));
+        if (d == 1) d = 0;
+      }
+    }
     p += d ? d : 1u;
   }
   const uint32_t wend = (G.end + 63) >> 6;
@@ -639,6 +654,7 @@ __global__ __launch_bounds__(64) void k_walk(Work w) {
   __shared__ uint32_t ent[65], cnt[64], nknown;
   if (blockIdx.x >= w.nbig) return;
   const uint32_t u = w.ulist[blockIdx.x];
+  if (w.ufail[u] == 2u) return;  // k_fastwalk did it
   if (TABLES && !w.ufail[u]) return;
   const uint32_t lane = threadIdx.x;
   const uint32_t uw = upd_win(w, u);  // positions below are relative to the update's window
@@ -826,6 +842,111 @@ __global__ __launch_bounds__(64) void k_walk(Work w) {
   if (L0) w.dsstart[u] = p;
 }
 
+// Fast path of the walk for single-section updates (a snapshot, one replica's own ops): when the
+// synced chunk chains form one chain — every chunk's final chain was entered where its
+// predecessor's final chain leaves (sexit == cexit after the second k_sync round) — and the exact
+// walk from the first struct meets chunk 0's chain inside chunk 0, the chain IS the true struct
+// sequence, so the update needs no serial walk: the n-th struct is found by a popcount scan over
+// the chunks (64 per wavefront round) and the struct-start words are copied in parallel. Anything
+// else (several sections, a chain that never meets, fewer chain positions than structs) is left
+// to k_walk, which also reports malformed input.
+__global__ __launch_bounds__(64) void k_fastwalk(Work w) {
+  __shared__ uint64_t walked[SW + 2];
+  __shared__ uint32_t sh_q, sh_k0, sh_ok;
+  if (blockIdx.x >= w.nbig) return;
+  const uint32_t u = w.ulist[blockIdx.x];
+  const uint32_t lane = threadIdx.x;
+  const uint32_t uw = upd_win(w, u);
+  const uint8_t* __restrict__ b = win_bytes(w, uw);
+  const uint64_t* __restrict__ spec = win_words(w.spec_bits, uw);
+  uint64_t* __restrict__ fbits = win_words(w.final_bits, uw);
+  uint64_t* __restrict__ sbits = win_words(w.sec_bits, uw);
+  const uint32_t ustart = w.uoff[u], uend = ustart + w.ulen[u];
+  const uint32_t CH = w.schunk;
+  const uint32_t c0 = w.ugroup[u], nch = (w.ulen[u] + CH - 1) / CH;
+  if (!w.ulen[u]) return;
+  uint32_t p = ustart;
+  bool ok = true;
+  const uint32_t nsec = rd_vu(b, p, uend, ok);
+  if (!ok || nsec != 1) return;
+  const uint32_t n = rd_vu(b, p, uend, ok);
+  const uint32_t client = rd_vu(b, p, uend, ok);
+  const uint32_t clock = rd_vu(b, p, uend, ok);
+  if (!ok || n == 0 || n > uend - p) return;
+  const uint32_t p1 = p, ce0 = min(ustart + CH, uend);
+  if (p1 >= ce0) return;
+  // one chain through all chunks
+  bool fix = true;
+  for (uint32_t k = lane; k + 1 < nch; k += 64) fix = fix && w.cexit[c0 + k] == w.sexit[c0 + k];
+  if (__ballot(!fix)) return;
+  // chunk 0: the exact walk from the first struct until it meets chunk 0's chain
+  for (uint32_t k = lane; k < SW + 2; k += 64) walked[k] = 0;
+  __syncthreads();
+  if (lane == 0) {
+    uint32_t q = p1, k0 = 0;
+    const uint32_t w0 = ustart >> 6;
+    while (q < ce0 && !((spec[q >> 6] >> (q & 63)) & 1ull)) {
+      walked[(q >> 6) - w0] |= 1ull << (q & 63);
+      q = chain_step(b, q, uend);
+      ++k0;
+    }
+    sh_q = q;
+    sh_k0 = k0;
+    sh_ok = q < ce0 && k0 < n;
+  }
+  __syncthreads();
+  if (!sh_ok) return;
+  const uint32_t q = sh_q, target = n - sh_k0;  // the target-th chain position from q is the last struct
+  // the chunk holding it: per-chunk counts, scanned 64 chunks at a time
+  uint32_t acc = 0, fch = NONE, rem = 0;
+  for (uint32_t base = 0; base < nch && fch == NONE; base += 64) {
+    const uint32_t j = base + lane;
+    uint32_t cnt = 0;
+    if (j < nch) {
+      const uint32_t cs = ustart + j * CH, ce = min(cs + CH, uend), a = j == 0 ? q : cs;
+      cnt = popc_range(spec, a, ce);
+    }
+    uint32_t incl = cnt;
+    for (uint32_t off = 1; off < 64; off <<= 1) {
+      const uint32_t v = __shfl_up(incl, off);
+      if (lane >= off) incl += v;
+    }
+    const uint64_t hit = __ballot(j < nch && acc + incl >= target && acc + incl - cnt < target);
+    if (hit) {
+      const uint32_t L = (uint32_t)__ffsll((long long)hit) - 1;
+      fch = base + L;
+      rem = target - (acc + __shfl(incl, L) - __shfl(cnt, L));
+    } else {
+      acc += __shfl(incl, 63);
+    }
+  }
+  if (fch == NONE) return;  // fewer chain positions than structs
+  const uint32_t fcs = ustart + fch * CH, fa = fch == 0 ? q : fcs;
+  const uint32_t Lp = select_from(spec, fa, rem);
+  const uint32_t dsp = chain_step(b, Lp, uend);
+  if (Lp >= uend || dsp > uend) return;
+  // marks: the walked positions of chunk 0, then every chain position in [q, Lp]
+  const uint32_t wq = q >> 6, wl = Lp >> 6, w0 = ustart >> 6;
+  for (uint32_t wd = w0 + lane; wd <= wl; wd += 64) {
+    uint64_t x = wd >= wq ? range_word(spec, wd, q, Lp + 1) : 0ull;
+    if (wd - w0 < SW + 2) x |= walked[wd - w0];
+    fbits[wd] = x;  // the update's own words (updates and chunks are 64-byte aligned)
+  }
+  if (lane == 0) {
+    const uint32_t sbase = atomicAdd(&w.ctr->nsections, 1u);
+    if (sbase >= w.cap_sections) { raise_err(&w.ctr->err, ERR_CAPACITY); return; }
+    Section sec;
+    sec.upd = u; sec.n = n; sec.client = client; sec.clock = clock;
+    sec.first_pos = p1; sec.cidx = NONE; sec.first_idx = NONE; sec.pad = 0;
+    w.sections[sbase] = sec;
+    atomicOr((unsigned long long*)&sbits[p1 >> 6], 1ull << (p1 & 63));
+    w.usec_start[u] = sbase;
+    w.usec_n[u] = 1;
+    w.dsstart[u] = dsp;
+    w.ufail[u] = 2u;  // done: k_walk leaves the update alone
+  }
+}
+
 // Positions of the chunks the table walk entered without parsing (tentry): one lane per chunk
 // parses exactly from the entry to the chunk end through its LDS window and marks them.
 __global__ __launch_bounds__(DL) void k_xmark(Work w) {
@@ -872,6 +993,8 @@ void launch_chunks(const Work& w, hipStream_t s) {
     hipLaunchKernelGGL(k_sync, dim3((w.ngroups + 255) / 256), dim3(256), 0, s, w, (const uint32_t*)w.sexit, w.cexit);
   }
   if (w.nbig) {
+    static const bool nofast = getenv("YCRDT_NO_FASTWALK") && getenv("YCRDT_NO_FASTWALK")[0] == '1';
+    if (!nofast && !w.force_xtab) hipLaunchKernelGGL(k_fastwalk, dim3(w.nbig), dim3(64), 0, s, w);
     hipLaunchKernelGGL(k_walk<false>, dim3(w.nbig), dim3(64), 0, s, w);
     // the table path, for updates the speculative walk handed over (grid-stride over xlist)
     hipLaunchKernelGGL(k_xtab, dim3(std::min(w.ngroups, 4096u)), dim3(64), 0, s, w);

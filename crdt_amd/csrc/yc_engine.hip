@@ -722,6 +722,8 @@ int run_decode(ycrdt_engine* e, ycrdt_batch* b, bool lazy, Decoded& D, bool gene
   {
     const char* mode = getenv("YCRDT_DECODE");
     w.force_xtab = mode && !strcmp(mode, "xtab") ? 1u : 0u;
+    const char* se = getenv("YCRDT_SPEC_EXACT");
+    w.spec_exact = se && se[0] == '0' ? 0u : 1u;
   }
   const uint64_t B = (uint64_t)b->nbytes + 64;
   const uint64_t nwords = B / 64 + 2;

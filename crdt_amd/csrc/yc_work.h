@@ -83,6 +83,7 @@ struct Work {
   uint32_t nbig = 0, nsmall = 0;
   uint32_t schunk = SCHUNK;        // chunk bytes of this batch's large updates (<= SCHUNK)
   uint32_t force_xtab = 0;         // YCRDT_DECODE=xtab: every large update takes the exit-table walk (tests)
+  uint32_t spec_exact = 1;         // k_spec hands long / deep structs to the exact parser (YCRDT_SPEC_EXACT=0: steps on)
   uint32_t lazy = 0;               // 1: mergeUpdates / diffUpdate decode (references kept raw)
   unsigned long long* dbg = nullptr; // YCRDT_DEBUG_YATA=1: k_yata work counters
   const Group* groups = nullptr;   // [G] chunks of the large updates

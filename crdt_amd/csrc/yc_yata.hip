@@ -864,8 +864,14 @@ __global__ __launch_bounds__(256) void k_tclimb_init(Work w, uint32_t nsegs, uin
 __global__ __launch_bounds__(256) void k_tclimb_round(uint32_t nsegs, const uint32_t* __restrict__ ans0, const uint32_t* __restrict__ nxt0,
                                                       uint32_t* __restrict__ ans1, uint32_t* __restrict__ nxt1, uint32_t* __restrict__ open,
                                                       uint32_t round) {
-  if (round > 0 && __hip_atomic_load(&open[round - 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) return;
   const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
+  if (round > 0 && __hip_atomic_load(&open[round - 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) {
+    // converged: the first round after it copies the final pairs into the other buffer (the
+    // buffers keep alternating), the later ones return at once
+    if (round >= 2 && __hip_atomic_load(&open[round - 2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) return;
+    if (s < nsegs) { ans1[s] = ans0[s]; nxt1[s] = nxt0[s]; }
+    return;
+  }
   if (s >= nsegs) return;
   uint32_t a = ans0[s], n = nxt0[s];
   if (n != NONE) {  // open: a == NONE

@@ -91,7 +91,7 @@ def _worker(rank, world, port, q):
         out["ds"] = ds_ok
         # ---- a malformed update parsed by one rank: the error reaches every rank
         ups = list(docs[0])
-        ups[3] = b"\x01\xff" + bytes(len(ups[3]) - 2)  # same length: the same layout on every rank
+        ups[3] = b"\x01" + b"\xff" * (len(ups[3]) - 1)  # an endless varuint; same length: the same layout
         try:
             b = crdt_amd.Batch(ups, eng)
             b.merge_sharded(world, comm)
