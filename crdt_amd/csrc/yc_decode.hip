@@ -42,12 +42,188 @@ __device__ __forceinline__ uint32_t win4(const uint8_t* __restrict__ b, uint32_t
   const uint32_t* d = (const uint32_t*)(b + (p & ~3u));  // the batch buffer is padded past its end
   return __builtin_amdgcn_alignbyte(d[1], d[0], p & 3u);  // v_alignbyte_b32: the shift counts bytes
 }
+// ---- the register-window sizer (fast path of every struct walk)
+// The 24 bytes from the word holding a struct's start sit in six registers, loaded in one round
+// (from the lane's LDS window, or from the batch buffer); T marks the bytes that end a varuint
+// (high bit clear). A varuint's length is then a count of trailing zeros of T, and the few bytes
+// whose values matter (info byte, element counts, tags, short lengths) come out of the registers
+// through a three-level select: one round of loads per struct instead of one dependent LDS /
+// memory round trip per field. 24 bytes hold the common structs whole (a map set with a 5-byte
+// client id and a short value; a root-map item with its parent name and key).
+struct RegWin {
+  // named words, not an array: an array indexed through the select tree is turned back into a
+  // dynamically indexed (LDS-promoted) alloca by the compiler
+  uint32_t r0, r1, r2, r3, r4, r5;
+  uint32_t T;
+  __device__ __forceinline__ static uint32_t sel(uint32_t m, uint32_t a1, uint32_t a0) { return (a1 & m) | (a0 & ~m); }
+  __device__ __forceinline__ uint32_t word(uint32_t k) const {  // k < 6
+    const uint32_t m0 = 0u - (k & 1u), m1 = 0u - ((k >> 1) & 1u), m2 = 0u - ((k >> 2) & 1u);
+    const uint32_t a0 = sel(m0, r1, r0), a1 = sel(m0, r3, r2), a2 = sel(m0, r5, r4);
+    return sel(m2, a2, sel(m1, a1, a0));
+  }
+  __device__ __forceinline__ uint32_t byte(uint32_t i) const { return (word(i >> 2) >> ((i & 3u) * 8)) & 0xFFu; }
+  // length (1..5) of the varuint at byte i < 24; 0: it does not end inside the window within 5 bytes
+  __device__ __forceinline__ uint32_t vlen(uint32_t i) const {
+    const uint32_t t = T >> i;
+    const uint32_t e = t ? (uint32_t)__builtin_ctz(t) + 1u : 0u;
+    return e <= 5 ? e : 0u;
+  }
+  __device__ __forceinline__ static uint32_t nib(uint32_t x) {  // bit j = byte j of x < 0x80
+    return ((~x & 0x80808080u) * 0x204081u) >> 28;
+  }
+  __device__ __forceinline__ void mask() {
+    T = nib(r0) | nib(r1) << 4 | nib(r2) << 8 | nib(r3) << 12 | nib(r4) << 16 | nib(r5) << 20;
+  }
+  __device__ __forceinline__ void load(const uint32_t* g) {
+    r0 = g[0]; r1 = g[1]; r2 = g[2]; r3 = g[3]; r4 = g[4]; r5 = g[5];
+    mask();
+  }
+};
+constexpr uint32_t WIN_SPAN = 24;
+// one lib0 `any` value with a scalar tag at window byte q (tag already read): q moves past it;
+// false: another tag, or a length byte outside the window
+__device__ __forceinline__ bool win_scalar(const RegWin& x, uint32_t& q, uint32_t tag) {
+  switch (tag) {
+    case 127: case 126: case 121: case 120: return true;
+    case 125: {  // varInt: up to 7 bytes (as the general sizer)
+      if (q >= WIN_SPAN) return false;
+      const uint64_t t = x.T >> q;
+      if (!t) return false;
+      const uint32_t l = (uint32_t)__builtin_ctzll(t) + 1u;
+      q += l;
+      return l <= 7;
+    }
+    case 124: q += 4; return true;
+    case 123: case 122: q += 8; return true;
+    case 119: case 116: {  // string / bytes with a one-byte length
+      if (q >= WIN_SPAN) return false;
+      const uint32_t n = x.byte(q);
+      q += 1 + n;
+      return n < 128;
+    }
+    default: return false;
+  }
+}
+// Exact length of the struct whose info byte is window byte o, for the shapes Yjs documents are
+// made of: an item placed by origin / right origin or under a named parent / parent id (with a
+// key), holding Deleted, String, Binary, Type, or Any with up to 4 scalar values or one-level
+// containers of up to 4 scalar members; GC / Skip. NONE: another shape, a field outside the
+// window, or a struct past `end` — the general sizer decides. A pure function of the bytes at p
+// (the chunk chains, the walker and the direct path all size through it).
+__device__ __forceinline__ uint32_t win_len(const RegWin& x, uint32_t o, uint32_t p, uint32_t end) {
+  const uint32_t info = x.byte(o), ref = info & 31u;
+  uint32_t q = o + 1;
+  if (ref == REF_GC || ref == REF_SKIP) {
+    const uint32_t l = x.vlen(q);
+    if (!l) return NONE;
+    q += l;
+  } else {
+    if (info & 0xC0u) {
+      const uint32_t nid = ((info >> 7) & 1u) * 2u + ((info >> 6) & 1u) * 2u;
+      for (uint32_t k = 0; k < nid; ++k) {
+        const uint32_t l = q < WIN_SPAN ? x.vlen(q) : 0u;
+        if (!l) return NONE;
+        q += l;
+      }
+    } else {
+      const uint32_t l = q < WIN_SPAN ? x.vlen(q) : 0u;
+      if (!l) return NONE;
+      if (l == 1 && x.byte(q) == 1u) {  // parent by name: a string
+        ++q;
+        if (q >= WIN_SPAN) return NONE;
+        const uint32_t n = x.byte(q);
+        if (n >= 128) return NONE;
+        q += 1 + n;
+      } else {  // parent by id: two varuints
+        q += l;
+        for (uint32_t k = 0; k < 2; ++k) {
+          const uint32_t m = q < WIN_SPAN ? x.vlen(q) : 0u;
+          if (!m) return NONE;
+          q += m;
+        }
+      }
+      if (info & 0x20u) {  // parentSub: a string
+        if (q >= WIN_SPAN) return NONE;
+        const uint32_t n = x.byte(q);
+        if (n >= 128) return NONE;
+        q += 1 + n;
+      }
+    }
+    if (q >= WIN_SPAN) return NONE;
+    switch (ref) {
+      case REF_DELETED: {
+        const uint32_t l = x.vlen(q);
+        if (!l) return NONE;
+        q += l;
+        break;
+      }
+      case REF_STRING: case REF_BINARY: {
+        const uint32_t n = x.byte(q);
+        if (n >= 128) return NONE;
+        q += 1 + n;
+        break;
+      }
+      case REF_TYPE: {
+        const uint32_t tr = x.byte(q);
+        if (tr > 6) return NONE;
+        ++q;
+        if (tr == 3 || tr == 5) {
+          if (q >= WIN_SPAN) return NONE;
+          const uint32_t n = x.byte(q);
+          if (n >= 128) return NONE;
+          q += 1 + n;
+        }
+        break;
+      }
+      case REF_ANY: {
+        const uint32_t c = x.byte(q);
+        if (c == 0 || c > 4) return NONE;
+        ++q;
+        for (uint32_t e = 0; e < c; ++e) {
+          if (q >= WIN_SPAN) return NONE;
+          const uint32_t tag = x.byte(q);
+          ++q;
+          if (tag == 118 || tag == 117) {  // object / array of scalars
+            if (q >= WIN_SPAN) return NONE;
+            const uint32_t m = x.byte(q);
+            if (m > 4) return NONE;
+            ++q;
+            for (uint32_t j = 0; j < m; ++j) {
+              if (tag == 118) {
+                if (q >= WIN_SPAN) return NONE;
+                const uint32_t kl = x.byte(q);
+                if (kl >= 128) return NONE;
+                q += 1 + kl;
+              }
+              if (q >= WIN_SPAN) return NONE;
+              const uint32_t t2 = x.byte(q);
+              ++q;
+              if (!win_scalar(x, q, t2)) return NONE;
+            }
+          } else if (!win_scalar(x, q, tag)) {
+            return NONE;
+          }
+        }
+        break;
+      }
+      default: return NONE;
+    }
+  }
+  const uint32_t len = q - o;
+  return p <= end && len <= end - p ? len : NONE;
+}
+
 // Byte sources for the sizer: the slice's bytes staged in LDS (plus a halo past its end), with
 // a fallback to the batch buffer (through the caches) for reads beyond the staged window.
 struct LdsSrc {
   const uint8_t* __restrict__ b;
   const uint32_t* lw;  // staged words of [s0, wend)
   uint32_t s0, wlen;   // wlen = wend - s0
+  // the register window of p: 24 bytes from p & ~3 (staged if the window holds them)
+  __device__ __forceinline__ void load_win(uint32_t p, RegWin& x) const {
+    const uint32_t a = p & ~3u, o = a - s0;
+    x.load((wlen >= WIN_SPAN && o <= wlen - WIN_SPAN) ? lw + (o >> 2) : (const uint32_t*)(b + a));
+  }
   __device__ __forceinline__ uint32_t u8(uint32_t p) const {
     const uint32_t o = p - s0;
     return o < wlen ? (lw[o >> 2] >> ((o & 3u) * 8)) & 0xFFu : (uint32_t)b[p];
@@ -210,34 +386,43 @@ __device__ __forceinline__ uint32_t spec_len(const S& b, uint32_t pos, uint32_t 
       ok = ok && tr <= 6;
       break;
     }
+    // more than SIZER_MAX_ELEMS elements / members: handed over to parse_struct once the first
+    // SIZER_MAX_ELEMS parse (a valid struct always passes; garbage on a chunk chain rarely does,
+    // and the exact parser would crawl through it byte by byte from memory)
     case REF_JSON: {
       const uint32_t n = vu_fast(b, p, end, ok);
-      if (ok && n > SIZER_MAX_ELEMS) return 1;
-      for (uint32_t i = 0; i < n && ok; ++i) {
+      for (uint32_t i = 0; i < n && i < SIZER_MAX_ELEMS && ok; ++i) {
         const uint32_t k = vu_fast(b, p, end, ok);
         ok = ok && k > 0 && p < end && json_start_ok(b.u8(p));
         skip_n(p, k, end, ok);
       }
+      if (ok && n > SIZER_MAX_ELEMS) return 1;
       break;
     }
     case REF_ANY: {
       const uint32_t n = vu_fast(b, p, end, ok);
-      if (ok && n > SIZER_MAX_ELEMS) return 1;
-      for (uint32_t i = 0; i < n && ok; ++i) {
+      for (uint32_t i = 0; i < n && i < SIZER_MAX_ELEMS && ok; ++i) {
         const uint32_t q0 = p;
         if (any_simple(b, p, end, ok)) continue;
         // a container one level deep with simple members; anything deeper goes to parse_struct
         const bool obj = b.u8(q0) == 118;
         const uint32_t m = vu_fast(b, p, end, ok);
-        if (ok && m > SIZER_MAX_ELEMS) return 1;
-        for (uint32_t j = 0; j < m && ok; ++j) {
+        for (uint32_t j = 0; j < m && j < SIZER_MAX_ELEMS && ok; ++j) {
           if (obj) { const uint32_t k = vu_fast(b, p, end, ok); skip_n(p, k, end, ok); }
           if (!any_simple(b, p, end, ok)) return ok ? 1u : 0u;
         }
+        if (ok && m > SIZER_MAX_ELEMS) return 1;
       }
+      if (ok && n > SIZER_MAX_ELEMS) return 1;
       break;
     }
-    default: return 1;  // ContentDoc
+    default: {  // ContentDoc: a guid string, then an `any` (handed over when its tag is one)
+      const uint32_t n = vu_fast(b, p, end, ok);
+      skip_n(p, n, end, ok);
+      if (!ok || p >= end) return 0;
+      const uint32_t tag = b.u8(p);
+      return tag >= 116 && tag <= 127 ? 1u : 0u;
+    }
   }
   if (!ok) return 0;
   return p - pos < 0x10000u ? p - pos : 1u;
@@ -247,22 +432,24 @@ __device__ __forceinline__ uint32_t spec_len(const S& b, uint32_t pos, uint32_t 
 // update's struct-start words of the final bitmap itself (updates are 64-byte aligned, so the
 // words are the lane's own: plain stores, each word once, as the lane moves forward). Each lane
 // reads its update through a private LDS window of DW bytes, refilled with 16-byte loads when
-// fewer than DREFILL bytes are left: the byte-serial parse then waits on LDS, not on L2 / HBM
-// (a wavefront touches 64 different updates, far more lines than L1 keeps). Structs are sized by
-// the speculative sizer (exact on valid structs); what it hands over is parsed by parse_struct.
+// fewer than DREFILL bytes are left (the register window of the struct start then always comes
+// from LDS): the parse waits on LDS, not on L2 / HBM (a wavefront touches 64 different updates,
+// far more lines than L1 keeps). Structs are sized by the register-window sizer, then the
+// speculative sizer (both exact on valid structs); what they hand over is parsed by parse_struct.
 constexpr uint32_t DW = 128;                    // window bytes per lane
 constexpr uint32_t DSTRIDE = DW / 4 + 4;        // words per lane slot (16-byte padded)
-constexpr uint32_t DREFILL = 48;
+constexpr uint32_t DREFILL = WIN_SPAN + 16;
 constexpr uint32_t DL = 256;                    // lanes per direct workgroup
 // A window refill: all DW/16 loads issued before the first LDS store, so a refill costs one
 // memory round trip (a loop bounded by wlen waited on each load in turn). The batch buffer is
 // padded past its end, and bytes past wlen are never taken from the window.
+template <uint32_t W = DW>
 __device__ __forceinline__ void fill_window(uint32_t* slot, const uint4* __restrict__ g) {
-  uint4 v[DW / 16];
+  uint4 v[W / 16];
 #pragma unroll
-  for (uint32_t k = 0; k < DW / 16; ++k) v[k] = g[k];
+  for (uint32_t k = 0; k < W / 16; ++k) v[k] = g[k];
 #pragma unroll
-  for (uint32_t k = 0; k < DW / 16; ++k) ((uint4*)slot)[k] = v[k];
+  for (uint32_t k = 0; k < W / 16; ++k) ((uint4*)slot)[k] = v[k];
 }
 // the exact parser out of line: inlined, its nested-`any` walker multiplies the register demand
 // of the lane loop (one wavefront per SIMD), and it only runs on the few handed-over structs
@@ -319,20 +506,27 @@ __global__ __launch_bounds__(DL) void k_direct(Work w) {
         m = 0;
       }
       m |= 1ull << (p & 63);
-      if (__ballot(p - src.s0 + DREFILL > src.wlen)) refill(p);  // the whole wavefront at once: one stall, not one per lane
-      const uint32_t info = src.u8(p), ref = info & 31u;
-      uint32_t d = 0;
-      if (ref == REF_GC || ref == REF_SKIP) {
-        uint32_t q = p + 1;
-        bool okv = true;
-        vu_fast(src, q, uend, okv);
-        d = okv ? q - p : 0u;
-      } else if (ref >= 1 && ref <= REF_DOC) {
-        d = spec_len(src, p, uend, (ref - 1) * 8 + (info >> 5));
-      }
-      if (d <= 1) {  // handed over (long / deep / Doc), or not sized: the exact parser decides
-        d = exact_len(b, p, uend);
-        if (!d) { raise_err(err, ERR_DECODE); w.ctr->err_info = p; return; }
+      // the whole wavefront at once: one stall, not one per lane (a window that already reaches
+      // the update end is never refilled)
+      if (__ballot(src.wlen == DW && p - src.s0 + DREFILL > DW)) refill(p);
+      RegWin x;
+      src.load_win(p, x);
+      uint32_t d = win_len(x, p & 3u, p, uend);
+      if (d == NONE) {
+        const uint32_t info = src.u8(p), ref = info & 31u;
+        d = 0;
+        if (ref == REF_GC || ref == REF_SKIP) {
+          uint32_t q = p + 1;
+          bool okv = true;
+          vu_fast(src, q, uend, okv);
+          d = okv ? q - p : 0u;
+        } else if (ref >= 1 && ref <= REF_DOC) {
+          d = spec_len(src, p, uend, (ref - 1) * 8 + (info >> 5));
+        }
+        if (d <= 1) {  // handed over (long / deep / Doc), or not sized: the exact parser decides
+          d = exact_len(b, p, uend);
+          if (!d) { raise_err(err, ERR_DECODE); w.ctr->err_info = p; return; }
+        }
       }
       p += d;
     }
@@ -346,7 +540,14 @@ __global__ __launch_bounds__(DL) void k_direct(Work w) {
 // Struct length at p on the all-struct chain, 0 where no struct parses (the chain then steps one
 // byte). The chunk chains and the walker use this one function, so chains that meet stay together.
 template <class S>
-__device__ __forceinline__ uint32_t chain_len(const S& src, const uint8_t* __restrict__ b, uint32_t p, uint32_t uend) {
+__device__ __forceinline__ uint32_t chain_len(const S& src, const uint8_t* __restrict__ b, uint32_t p, uint32_t uend,
+                                              unsigned long long* dbg = nullptr) {
+  {
+    RegWin x;
+    src.load_win(p, x);
+    const uint32_t f = win_len(x, p & 3u, p, uend);
+    if (f != NONE) return f;
+  }
   const uint32_t info = src.u8(p), ref = info & 31u;
   uint32_t d = 0;
   if (ref == REF_GC || ref == REF_SKIP) {
@@ -356,12 +557,16 @@ __device__ __forceinline__ uint32_t chain_len(const S& src, const uint8_t* __res
     d = okv ? q - p : 0u;
   } else if (ref >= 1 && ref <= REF_DOC) {
     d = spec_len(src, p, uend, (ref - 1) * 8 + (info >> 5));
-    if (d == 1) d = exact_len(b, p, uend);  // handed over (long / deep / Doc)
+    if (d == 1) {  // handed over (long / deep / Doc)
+      d = exact_len(b, p, uend);
+      if (dbg) { atomicAdd(&dbg[6], 1ull); atomicAdd(&dbg[7], (unsigned long long)d); }
+    }
   }
   return d;
 }
 struct GlobalSrc {
   const uint8_t* __restrict__ b;
+  __device__ __forceinline__ void load_win(uint32_t p, RegWin& x) const { x.load((const uint32_t*)(b + (p & ~3u))); }
   __device__ __forceinline__ uint32_t u8(uint32_t p) const { return b[p]; }
   __device__ __forceinline__ uint64_t w8(uint32_t p) const { return win8(b, p); }
   __device__ __forceinline__ uint32_t w4(uint32_t p) const { return win4(b, p); }
@@ -429,28 +634,65 @@ __device__ __forceinline__ uint32_t chain_step(const uint8_t* __restrict__ b, ui
   return p + (d ? d : 1u);
 }
 
-// One lane per chunk (SCHUNK bytes of a large update): the chain from the chunk's first byte, every
+// One lane per chunk (SCHUNK bytes of a large update): the chain from the chunk's start (below), every
 // visited position inside the chunk set in spec_bits (the lane owns the chunk's words: chunks and
 // updates are 64-byte aligned) and the first position at / past the chunk end in cexit. The bytes
 // come through the lane's LDS window, as in k_direct.
+// k_spec's window is shorter than the direct path's: a chunk path of many chunks needs more
+// wavefronts resident per CU than the direct path's one lane per update
+constexpr uint32_t SPW = 128, SPSTRIDE = SPW / 4 + 4;
 __global__ __launch_bounds__(DL) void k_spec(Work w) {
-  __shared__ __attribute__((aligned(16))) uint32_t win[DL * DSTRIDE];
+  __shared__ __attribute__((aligned(16))) uint32_t win[DL * SPSTRIDE];
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= w.ngroups) return;
   const Group G = w.groups[i];
   const uint32_t uw = upd_win(w, G.upd);
   const uint8_t* __restrict__ b = win_bytes(w, uw);
   const uint32_t uend = G.uend;
-  uint32_t* slot = win + threadIdx.x * DSTRIDE;
+  uint32_t* slot = win + threadIdx.x * SPSTRIDE;
   LdsSrc src{b, slot, 0, 0};
   auto refill = [&](uint32_t p) {
     src.s0 = p & ~15u;
-    src.wlen = min(DW, (uend + 15u - src.s0) & ~15u);
+    src.wlen = min(SPW, (uend + 15u - src.s0) & ~15u);
     const uint4* g = (const uint4*)(b + src.s0);
-    fill_window(slot, g);
+    fill_window<SPW>(slot, g);
   };
   uint64_t* __restrict__ spec = win_words(w.spec_bits, uw);
-  uint32_t p = G.start, word = G.start >> 6;
+  // Where the chain starts. The first chunk of an update: at its first struct (the headers are
+  // read exactly). Any other chunk of a single-section update (by default; w.spec_hint): at the
+  // first position of its first 96 bytes where three
+  // consecutive chain steps start with the info byte of the update's first struct (a stream of
+  // similar structs: one replica's pushes, a snapshot) — a guess the walker verifies, which keeps a
+  // chunk's chain out of the self-consistent wrong phases such streams lock into (§5.4b); else at
+  // the chunk's first byte.
+  uint32_t start = G.start;
+  {
+    const uint32_t u0 = w.uoff[G.upd];
+    uint32_t h = u0;
+    bool okh = true;
+    const uint32_t nsec = rd_vu(b, h, uend, okh);
+    const uint32_t n0 = nsec ? rd_vu(b, h, uend, okh) : 0u;
+    if (nsec) { rd_vu(b, h, uend, okh); rd_vu(b, h, uend, okh); }
+    if (okh && n0 && h < uend) {
+      if (G.start == u0) {
+        start = min(h, G.end);
+      } else if (w.spec_hint == 1u || (w.spec_hint == 2u && nsec == 1)) {
+        const uint32_t hint = b[h];
+        refill(G.start);
+        const uint32_t lim = min(G.start + 96u, G.end);
+        for (uint32_t q = G.start; q < lim; ++q) {
+          if (src.u8(q) != hint) continue;
+          const uint32_t d1 = chain_len(src, b, q, uend);
+          if (!d1 || q + d1 >= uend || src.u8(q + d1) != hint) continue;
+          const uint32_t d2 = chain_len(src, b, q + d1, uend);
+          if (!d2 || q + d1 + d2 >= uend || src.u8(q + d1 + d2) != hint) continue;
+          start = q;
+          break;
+        }
+      }
+    }
+  }
+  uint32_t p = start, word = G.start >> 6;
   uint64_t m = 0;
   refill(p);
   while (p < G.end) {
@@ -460,23 +702,8 @@ __global__ __launch_bounds__(DL) void k_spec(Work w) {
       while (++word < (p >> 6)) spec[word] = 0;
     }
     m |= 1ull << (p & 63);
-    if (__ballot(p - src.s0 + DREFILL > src.wlen)) refill(p);  // the whole wavefront at once: one stall, not one per lane
-    uint32_t d;
-    if (w.spec_exact) {
-      d = chain_len(src, b, p, uend);
-    } else {  // experiment: a handed-over struct is stepped over byte by byte (the walker re-parses exactly)
-      const uint32_t info = src.u8(p), ref = info & 31u;
-      d = 0;
-      if (ref == REF_GC || ref == REF_SKIP) {
-        uint32_t q = p + 1;
-        bool okv = true;
-        vu_fast(src, q, uend, okv);
-        d = okv ? q - p : 0u;
-      } else if (ref >= 1 && ref <= REF_DOC) {
-        d = spec_len(src, p, uend, (ref - 1) * 8 + (info >> 5));
-        if (d == 1) d = 0;
-      }
-    }
+    if (__ballot(src.wlen == SPW && p - src.s0 + DREFILL > SPW)) refill(p);  // the whole wavefront at once
+    const uint32_t d = chain_len(src, b, p, uend, w.dbg);
     p += d ? d : 1u;
   }
   const uint32_t wend = (G.end + 63) >> 6;
@@ -490,38 +717,58 @@ __global__ __launch_bounds__(DL) void k_spec(Work w) {
 // spec_bits are rewritten to that one chain (walked positions, then the own chain from the meeting
 // point); its exit goes to xout. A chain meets the true struct sequence within ~100 bytes of its
 // start in the median (C2 snapshots: 90 % within 400 bytes), so after one round nearly every
-// chunk's chain is the true sequence from its first struct on; a second round (xin / xout
-// swapped) re-enters the few chunks behind a chunk whose chain had not met it, and the walker
-// finds its entries on the chains. A chunk the chain jumps over entirely (one long struct) gets no
+// chunk's chain is the true sequence from its first struct on; later rounds re-enter the few
+// chunks behind a chunk whose chain had not met it, and the walker finds its entries on the chains. A chunk the chain jumps over entirely (one long struct) gets no
 // positions. The first chunk of an update keeps its chain (the walker enters it after the update /
 // section headers).
-__global__ __launch_bounds__(256) void k_sync(Work w, const uint32_t* __restrict__ xin, uint32_t* __restrict__ xout) {
+// Rounds repeat (SYNC_ROUNDS, xin / xout alternating): a chunk is re-walked only when its entry
+// changed since its last walk (sent), and a round after one that changed no exit only copies. A
+// chunk whose own chain never met the true sequence passes the true exit on one round later, so
+// an isolated such chunk costs one more round, not a hand-over of its update to the walker (an
+// 11 MB C4 state has ~11 k chunks: one of them out of phase used to fail the whole fast walk).
+constexpr uint32_t SYNC_ROUNDS = 6;  // even: the last round writes cexit
+__global__ __launch_bounds__(256) void k_sync(Work w, const uint32_t* __restrict__ xin, uint32_t* __restrict__ xout,
+                                              uint32_t round) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= w.ngroups) return;
-  const Group G = w.groups[i];
   uint32_t X = xin[i];
+  if (round > 0 && !w.ctr->sync_changed[round - 1]) { xout[i] = X; return; }
+  const Group G = w.groups[i];
   if (G.start != w.uoff[G.upd]) {  // chunks of one update are consecutive
-    const uint32_t uw = upd_win(w, G.upd);
-    const uint8_t* __restrict__ b = win_bytes(w, uw);
-    uint64_t* __restrict__ spec = win_words(w.spec_bits, uw);
     const uint32_t E = xin[i - 1];
-    uint32_t q = E, word = G.start >> 6;
-    uint64_t m = 0;
-    while (q < G.end && !((spec[q >> 6] >> (q & 63)) & 1ull)) {
-      while ((q >> 6) != word) { spec[word] = m; m = 0; ++word; }
-      m |= 1ull << (q & 63);
-      q = chain_step(b, q, G.uend);
-    }
-    if (q < G.end) {  // met the own chain at q: keep its positions from q on
-      while ((q >> 6) != word) { spec[word] = m; m = 0; ++word; }
-      spec[word] = m | (spec[word] & (~0ull << (q & 63)));
-    } else {
-      const uint32_t wend = (G.end + 63) >> 6;
-      for (; word < wend; ++word) { spec[word] = m; m = 0; }
-      X = q;
+    uint32_t* jumped = w.sent + w.ngroups + 1;
+    if (E >= G.end) {
+      // the predecessor's chain jumps over the whole chunk: a long struct, or (far more often on
+      // a chunk's own chain) garbage parsed as a long string. Passing such an exit on would cascade
+      // one chunk per round; the chunk keeps its own chain and is flagged, so the update only
+      // reaches the fast walk once a later round enters it from inside the chunk
+      w.sent[i] = E;
+      jumped[i] = 1u;
+    } else if (round == 0 || E != w.sent[i]) {
+      w.sent[i] = E;
+      jumped[i] = 0u;
+      const uint32_t uw = upd_win(w, G.upd);
+      const uint8_t* __restrict__ b = win_bytes(w, uw);
+      uint64_t* __restrict__ spec = win_words(w.spec_bits, uw);
+      uint32_t q = E, word = G.start >> 6;
+      uint64_t m = 0;
+      while (q < G.end && !((spec[q >> 6] >> (q & 63)) & 1ull)) {
+        while ((q >> 6) != word) { spec[word] = m; m = 0; ++word; }
+        m |= 1ull << (q & 63);
+        q = chain_step(b, q, G.uend);
+      }
+      if (q < G.end) {  // met the own chain at q: keep its positions from q on
+        while ((q >> 6) != word) { spec[word] = m; m = 0; ++word; }
+        spec[word] = m | (spec[word] & (~0ull << (q & 63)));
+      } else {
+        const uint32_t wend = (G.end + 63) >> 6;
+        for (; word < wend; ++word) { spec[word] = m; m = 0; }
+        X = q;
+      }
     }
   }
   xout[i] = X;
+  if (X != xin[i]) atomicOr(&w.ctr->sync_changed[round], 1u);
 }
 
 
@@ -761,7 +1008,7 @@ __global__ __launch_bounds__(64) void k_walk(Work w) {
         if (q < ce) refill(q);
         while (q < ce && kk < limit && !((mc[(q - cs) >> 6] >> (q & 63)) & 1ull)) {
           mw[(q - cs) >> 6] |= 1ull << (q & 63);
-          if (q - src.s0 + DREFILL > src.wlen) refill(q);
+          if (src.wlen == DW && q - src.s0 + DREFILL > DW) refill(q);
           const uint32_t d = chain_len(src, b, q, uend);
           q += d ? d : 1u;
           ++kk;
@@ -844,7 +1091,7 @@ __global__ __launch_bounds__(64) void k_walk(Work w) {
 
 // Fast path of the walk for single-section updates (a snapshot, one replica's own ops): when the
 // synced chunk chains form one chain — every chunk's final chain was entered where its
-// predecessor's final chain leaves (sexit == cexit after the second k_sync round) — and the exact
+// predecessor's final chain leaves (sexit == cexit after the last k_sync round) — and the exact
 // walk from the first struct meets chunk 0's chain inside chunk 0, the chain IS the true struct
 // sequence, so the update needs no serial walk: the n-th struct is found by a popcount scan over
 // the chunks (64 per wavefront round) and the struct-start words are copied in parallel. Anything
@@ -868,7 +1115,8 @@ __global__ __launch_bounds__(64) void k_fastwalk(Work w) {
   uint32_t p = ustart;
   bool ok = true;
   const uint32_t nsec = rd_vu(b, p, uend, ok);
-  if (!ok || nsec != 1) return;
+  auto why = [&](uint32_t k) { if (w.dbg && lane == 0) atomicAdd(&w.dbg[k], 1ull); };
+  if (!ok || nsec != 1) { why(1); return; }
   const uint32_t n = rd_vu(b, p, uend, ok);
   const uint32_t client = rd_vu(b, p, uend, ok);
   const uint32_t clock = rd_vu(b, p, uend, ok);
@@ -877,8 +1125,9 @@ __global__ __launch_bounds__(64) void k_fastwalk(Work w) {
   if (p1 >= ce0) return;
   // one chain through all chunks
   bool fix = true;
-  for (uint32_t k = lane; k + 1 < nch; k += 64) fix = fix && w.cexit[c0 + k] == w.sexit[c0 + k];
-  if (__ballot(!fix)) return;
+  for (uint32_t k = lane; k < nch; k += 64)
+    fix = fix && (k + 1 == nch || w.cexit[c0 + k] == w.sexit[c0 + k]) && (k == 0 || !w.sent[w.ngroups + 1 + c0 + k]);
+  if (__ballot(!fix)) { why(2); return; }
   // chunk 0: the exact walk from the first struct until it meets chunk 0's chain
   for (uint32_t k = lane; k < SW + 2; k += 64) walked[k] = 0;
   __syncthreads();
@@ -895,7 +1144,7 @@ __global__ __launch_bounds__(64) void k_fastwalk(Work w) {
     sh_ok = q < ce0 && k0 < n;
   }
   __syncthreads();
-  if (!sh_ok) return;
+  if (!sh_ok) { why(3); return; }
   const uint32_t q = sh_q, target = n - sh_k0;  // the target-th chain position from q is the last struct
   // the chunk holding it: per-chunk counts, scanned 64 chunks at a time
   uint32_t acc = 0, fch = NONE, rem = 0;
@@ -920,11 +1169,11 @@ __global__ __launch_bounds__(64) void k_fastwalk(Work w) {
       acc += __shfl(incl, 63);
     }
   }
-  if (fch == NONE) return;  // fewer chain positions than structs
+  if (fch == NONE) { why(4); return; }  // fewer chain positions than structs
   const uint32_t fcs = ustart + fch * CH, fa = fch == 0 ? q : fcs;
   const uint32_t Lp = select_from(spec, fa, rem);
   const uint32_t dsp = chain_step(b, Lp, uend);
-  if (Lp >= uend || dsp > uend) return;
+  if (Lp >= uend || dsp > uend) { why(5); return; }
   // marks: the walked positions of chunk 0, then every chain position in [q, Lp]
   const uint32_t wq = q >> 6, wl = Lp >> 6, w0 = ustart >> 6;
   for (uint32_t wd = w0 + lane; wd <= wl; wd += 64) {
@@ -944,6 +1193,7 @@ __global__ __launch_bounds__(64) void k_fastwalk(Work w) {
     w.usec_n[u] = 1;
     w.dsstart[u] = dsp;
     w.ufail[u] = 2u;  // done: k_walk leaves the update alone
+    if (w.dbg) atomicAdd(&w.dbg[0], 1ull);
   }
 }
 
@@ -979,7 +1229,7 @@ __global__ __launch_bounds__(DL) void k_xmark(Work w) {
       m = 0;
     }
     m |= 1ull << (p & 63);
-    if (p - src.s0 + DREFILL > src.wlen) refill(p);
+    if (src.wlen == DW && p - src.s0 + DREFILL > DW) refill(p);
     const uint32_t d = chain_len(src, b, p, uend);
     p += d ? d : 1u;
   }
@@ -989,8 +1239,9 @@ __global__ __launch_bounds__(DL) void k_xmark(Work w) {
 void launch_chunks(const Work& w, hipStream_t s) {
   if (w.ngroups) {
     hipLaunchKernelGGL(k_spec, dim3((w.ngroups + DL - 1) / DL), dim3(DL), 0, s, w);
-    hipLaunchKernelGGL(k_sync, dim3((w.ngroups + 255) / 256), dim3(256), 0, s, w, (const uint32_t*)w.cexit, w.sexit);
-    hipLaunchKernelGGL(k_sync, dim3((w.ngroups + 255) / 256), dim3(256), 0, s, w, (const uint32_t*)w.sexit, w.cexit);
+    for (uint32_t r = 0; r < SYNC_ROUNDS; ++r)
+      hipLaunchKernelGGL(k_sync, dim3((w.ngroups + 255) / 256), dim3(256), 0, s, w,
+                         (const uint32_t*)(r & 1 ? w.sexit : w.cexit), r & 1 ? w.cexit : w.sexit, r);
   }
   if (w.nbig) {
     static const bool nofast = getenv("YCRDT_NO_FASTWALK") && getenv("YCRDT_NO_FASTWALK")[0] == '1';
@@ -1257,9 +1508,12 @@ __global__ void k_unique_flags(const uint32_t* __restrict__ v, uint32_t n, uint3
   else if (i == n) flags[i] = 0;
 }
 __global__ void k_unique_scatter(const uint32_t* __restrict__ v, const uint32_t* __restrict__ pre, uint32_t n,
-                                 uint32_t* __restrict__ out, uint32_t* nout) {
+                                 uint32_t* __restrict__ out, uint32_t* nout, uint8_t* __restrict__ single) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < n && (i == 0 || v[i] != v[i - 1])) out[pre[i]] = v[i];
+  if (i < n && (i == 0 || v[i] != v[i - 1])) {
+    out[pre[i]] = v[i];
+    if (single) single[pre[i]] = (i + 1 == n || v[i + 1] != v[i]) ? 1u : 0u;  // a run of one section
+  }
   if (i == n) *nout = pre[n];
 }
 __global__ void k_section_cidx(Section* __restrict__ sec, uint32_t n, const uint32_t* __restrict__ cl, const uint32_t* nc) {
@@ -1284,6 +1538,7 @@ __global__ void k_unique_keys_scatter(Work w, uint32_t n) {
     w.cl_key2[c] = k;
     w.cl_vals[c] = (uint32_t)k;
     w.cl_doc[c] = (uint32_t)(k >> 32);
+    if (w.cl_single) w.cl_single[c] = (i + 1 == n || w.cl_key[i + 1] != k) ? 1u : 0u;  // a run of one section
   }
   if (i == n) w.ctr->nclients = w.cl_tmp[n];
 }
@@ -1310,7 +1565,7 @@ void launch_client_table(Work& w, uint32_t nsections, hipStream_t s) {
   hipLaunchKernelGGL(k_unique_flags, dim3(grid), dim3(256), 0, s, w.cl_vals, nsections, w.scratch);
   scan_u32(w.tmp, w.tmp_bytes, w.scratch, w.cl_tmp, nsections + 1, s);
   // compact in place is unsafe; use cl_state as scratch output, then copy back
-  hipLaunchKernelGGL(k_unique_scatter, dim3(grid), dim3(256), 0, s, w.cl_vals, w.cl_tmp, nsections, w.cl_state, &w.ctr->nclients);
+  hipLaunchKernelGGL(k_unique_scatter, dim3(grid), dim3(256), 0, s, w.cl_vals, w.cl_tmp, nsections, w.cl_state, &w.ctr->nclients, w.cl_single);
   hipMemcpyAsync(w.cl_vals, w.cl_state, sizeof(uint32_t) * nsections, hipMemcpyDeviceToDevice, s);
   hipLaunchKernelGGL(k_section_cidx, dim3(grid), dim3(256), 0, s, w.sections, nsections, w.cl_vals, &w.ctr->nclients);
 }

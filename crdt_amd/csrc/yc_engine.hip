@@ -165,10 +165,10 @@ enum Buf {
   B_DWFLAG, B_DWGID, B_DWGSTART, B_DWSIZE, B_DWPOS,
   B_GRIGHT, B_YKEY, B_YKEYS, B_YSEG, B_YIOTA, B_YLSTART, B_YSTATE, B_YBEFORE, B_YCONFL, B_YSTACK,
   B_TKEY, B_TKEYS, B_TSEG, B_TPOS, B_TGSTART, B_TNEXT, B_TDONE, B_TFIRST, B_TNSIB, B_TJUMP, B_TBIG,
-  B_TPRV, B_TMPRV, B_TMTAIL, B_TTREP, B_TOTAIL, B_THKEY, B_THVAL, B_TFLAG, B_TSCAN,
+  B_TPRV, B_TMPRV, B_TMTAIL, B_TTREP, B_TOTAIL, B_THKEY, B_THVAL, B_TFLAG, B_TSCAN, B_SENT,
   B_OFIRST, B_OCIDX, B_OSIZE, B_OPOS, B_RSEG, B_RLEN, B_RSIZE, B_RPOS, B_OUT, B_SVOUT,
   B_VKMAP, B_VKREP, B_VKEYS, B_VNKEYS, B_VPOS, B_VD0, B_VN0, B_VD1, B_VN1, B_VORDER, B_VSEGS,
-  B_SCRATCH2, B_TMP2, B_CAPS, B_CLKEY, B_CLKEY2, B_CHKEY, B_CHVAL, B_CLDOC, B_DSFA, B_EMIT, B_DOCRNG, B_PACK, B_PACKPC, B_SPLITMETA, B_KSHARD, B_SOWNER, B_GFLAGS0, B_GFACC,
+  B_SCRATCH2, B_TMP2, B_CAPS, B_CLKEY, B_CLKEY2, B_CHKEY, B_CHVAL, B_CLDOC, B_DSFA, B_EMIT, B_DOCRNG, B_PACK, B_PACKPC, B_SPLITMETA, B_CLSINGLE, B_KSHARD, B_SOWNER, B_GFLAGS0, B_GFACC,
   B_COUNT
 };
 
@@ -302,6 +302,7 @@ constexpr size_t DIRECT_TINY_BYTES = 1024;         // always direct (a handful o
 constexpr size_t DIRECT_MIN_COUNT = 1024;          // enough small updates to fill wavefronts
 constexpr size_t SMALL_BATCH_BYTES = size_t(1) << 20;  // chunk-path bytes up to which chunks are short
 constexpr uint32_t SCHUNK_SMALL = 256;
+constexpr size_t MID_BATCH_BYTES = size_t(64) << 20;  // chunk-path bytes up to which chunks are SCHUNK / 2
 
 // One staged input: host bytes, or a device buffer (a doc state already in HBM).
 struct Src {
@@ -333,10 +334,8 @@ void layout(ycrdt_batch* b, const std::vector<Src>& src, std::vector<uint32_t>& 
   b->schunk = SCHUNK;
   if (big_bytes <= SMALL_BATCH_BYTES)
     while (b->schunk > SCHUNK_SMALL && (size_t)(b->schunk / 2) * 64 >= big_max) b->schunk /= 2;
-  if (const char* cs = getenv("YCRDT_SCHUNK")) {  // experiments: a fixed chunk size (64-byte multiple)
-    const uint32_t v = (uint32_t)atoi(cs);
-    if (v >= 64 && v <= SCHUNK && v % 64 == 0) b->schunk = v;
-  }
+  else if (big_bytes <= MID_BATCH_BYTES)
+    b->schunk = SCHUNK / 2;  // a single document's worth: more, shorter chunk chains (the walk is mostly the fast one)
   if (const char* cs = getenv("YCRDT_SCHUNK")) {  // experiments: a fixed chunk size (64-byte multiple)
     const uint32_t v = (uint32_t)atoi(cs);
     if (v >= 64 && v <= SCHUNK && v % 64 == 0) b->schunk = v;
@@ -722,8 +721,11 @@ int run_decode(ycrdt_engine* e, ycrdt_batch* b, bool lazy, Decoded& D, bool gene
   {
     const char* mode = getenv("YCRDT_DECODE");
     w.force_xtab = mode && !strcmp(mode, "xtab") ? 1u : 0u;
-    const char* se = getenv("YCRDT_SPEC_EXACT");
-    w.spec_exact = se && se[0] == '0' ? 0u : 1u;
+    const char* sh = getenv("YCRDT_SPEC_HINT");
+    // chunk-start hints: single-section updates only by default (a C2 snapshot or replica update
+    // syncs with them; multi-section C4 states locked into wrong phases with them, §5.4b);
+    // YCRDT_SPEC_HINT=1 / 0: always / never
+    w.spec_hint = sh && sh[0] == '1' ? 1u : sh && sh[0] == '0' ? 0u : 2u;
   }
   const uint64_t B = (uint64_t)b->nbytes + 64;
   const uint64_t nwords = B / 64 + 2;
@@ -740,6 +742,7 @@ int run_decode(ycrdt_engine* e, ycrdt_batch* b, bool lazy, Decoded& D, bool gene
   w.spec_bits = take<uint64_t>(V, B_SPECB, nwords, ok);
   w.cexit = take<uint32_t>(V, B_CEXIT, (uint64_t)w.ngroups + 1, ok);
   w.sexit = take<uint32_t>(V, B_SEXIT, (uint64_t)w.ngroups + 1, ok);
+  w.sent = take<uint32_t>(V, B_SENT, 2 * ((uint64_t)w.ngroups + 1), ok);  // entries, then jumped flags
   w.xtab = take<uint32_t>(V, B_XTAB, ((uint64_t)w.ngroups + 1) * XK, ok);
   w.tentry = take<uint32_t>(V, B_TENTRY, (uint64_t)w.ngroups + 1, ok);
   w.xlist = take<uint32_t>(V, B_XLIST, (uint64_t)w.ngroups + 1, ok);
@@ -772,7 +775,8 @@ int run_decode(ycrdt_engine* e, ycrdt_batch* b, bool lazy, Decoded& D, bool gene
                   {(uint32_t*)w.final_bits, (uint64_t)nwords * 2, 0u},
                   {(uint32_t*)w.sec_bits, (uint64_t)nwords * 2, 0u}}, s);
   static const bool dbg_yata = getenv("YCRDT_DEBUG_YATA") && getenv("YCRDT_DEBUG_YATA")[0] == '1';
-  w.dbg = dbg_yata ? take<unsigned long long>(V, B_DBG, 8, ok) : nullptr;
+  static const bool dbg_dec = getenv("YCRDT_DEBUG_DECODE") && getenv("YCRDT_DEBUG_DECODE")[0] == '1';
+  w.dbg = dbg_yata || dbg_dec ? take<unsigned long long>(V, B_DBG, 8, ok) : nullptr;
   if (w.dbg) HIPCHK(hipMemsetAsync(w.dbg, 0, 64, s));
   // ---- K1 decode
   // large updates (chunk path, mostly latency-bound) on the side stream, beside k_direct
@@ -806,6 +810,13 @@ int run_decode(ycrdt_engine* e, ycrdt_batch* b, bool lazy, Decoded& D, bool gene
   if (!w.nupd) HIPCHK(hipMemcpyAsync(&w.ctr->nstructs, w.wcnt + (w.nbytes + 63) / 64, sizeof(uint32_t), hipMemcpyDeviceToDevice, s));
   Counters c;
   int rc = check(e, c, "decode");
+  if (dbg_dec && w.dbg) {  // experiments: why k_fastwalk left large updates to k_walk
+    unsigned long long h[8];
+    HIPCHK(hipMemcpy(h, w.dbg, sizeof(h), hipMemcpyDeviceToHost));
+    fprintf(stderr, "[ycrdt decode] fastwalk: done %llu nsec %llu unsynced %llu chunk0 %llu short %llu end %llu; k_spec exact parses %llu (%llu bytes)\n",
+            h[0], h[1], h[2], h[3], h[4], h[5], h[6], h[7]);
+    HIPCHK(hipMemsetAsync(w.dbg, 0, 64, s));
+  }
   if (rc == YCRDT_E_CAPACITY && !generous) return run_decode(e, b, lazy, D, true, sh);  // past the estimates
   if (rc) return rc;
   const uint32_t nstructs = c.nstructs;
@@ -847,6 +858,7 @@ int run_decode(ycrdt_engine* e, ycrdt_batch* b, bool lazy, Decoded& D, bool gene
   w.cl_doc = take<uint32_t>(V, B_CLDOC, w.cap_clients + 1, ok);
   w.cl_tmp = take<uint32_t>(V, B_CLTMP, w.cap_clients + 1, ok);
   w.cl_state = take<uint32_t>(V, B_CLSTATE, w.cap_clients + 1, ok);
+  w.cl_single = lazy ? nullptr : take<uint8_t>(V, B_CLSINGLE, w.cap_clients + 16, ok);
   w.cl_base = take<uint64_t>(V, B_CLBASE, w.cap_clients + 2, ok);
   w.cl_start = take<uint32_t>(V, B_CLSTART, w.cap_clients + 1, ok);
   if (!ok) return fail(YCRDT_E_DEVICE, oom("struct table"));

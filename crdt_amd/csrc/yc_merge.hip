@@ -55,19 +55,33 @@ __global__ __launch_bounds__(256) void k_owner(Work w, uint32_t nstructs) {
       fl = ref == REF_DELETED ? UF_DEL : (ref == REF_GC ? (UF_GC | UF_DEL) : 0u);
     }
   }
+  // a client whose structs all come from one section (one update) owns its units alone: plain
+  // stores (its structs cover disjoint clock ranges); otherwise the earliest struct wins by atomicMin
+  const bool one = n && w.cl_single && w.cl_single[w.s_cidx[s]];
   const bool lng = n > LONG_UNITS;
   if (!lng)
     for (uint32_t k = 0; k < n; ++k) {
-      atomicMin(&w.u_owner[(uint32_t)(gb + k)], s);
-      if (fl) atomicOr(&w.u_flags[(uint32_t)(gb + k)], fl);
+      if (one) {
+        w.u_owner[(uint32_t)(gb + k)] = s;
+        if (fl) w.u_flags[(uint32_t)(gb + k)] = fl;
+      } else {
+        atomicMin(&w.u_owner[(uint32_t)(gb + k)], s);
+        if (fl) atomicOr(&w.u_flags[(uint32_t)(gb + k)], fl);
+      }
     }
   for (uint64_t m = __ballot(lng); m; m &= m - 1) {
     const int L = __ffsll((long long)m) - 1;
     const uint64_t g0 = shfl64(gb, L);
     const uint32_t nl = __shfl(n, L), fll = __shfl(fl, L), sl = __shfl(s, L);
+    const bool onel = __shfl((int)one, L) != 0;
     for (uint32_t k = lane; k < nl; k += 64) {
-      atomicMin(&w.u_owner[(uint32_t)(g0 + k)], sl);
-      if (fll) atomicOr(&w.u_flags[(uint32_t)(g0 + k)], fll);
+      if (onel) {
+        w.u_owner[(uint32_t)(g0 + k)] = sl;
+        if (fll) w.u_flags[(uint32_t)(g0 + k)] = fll;
+      } else {
+        atomicMin(&w.u_owner[(uint32_t)(g0 + k)], sl);
+        if (fll) atomicOr(&w.u_flags[(uint32_t)(g0 + k)], fll);
+      }
     }
   }
 }

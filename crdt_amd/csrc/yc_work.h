@@ -38,6 +38,7 @@ struct Counters {            // device-side counters, read back at the few host 
   uint32_t nroots;           // items with an explicit parent (bound on the distinct lists: key table size)
   uint32_t pad[12];          // encode scratch (see yc_encode.hip)
   uint32_t climb_open[40];   // per pointer-jumping round of the YArray climb: pairs still open (yc_yata.hip)
+  uint32_t sync_changed[8];  // per k_sync round: some chunk's chain exit changed (yc_decode.hip)
   unsigned long long out_total; // encoded output size (integrate encoder; 64-bit)
   unsigned long long ds_base;   // integrate encoder: byte position of the delete-set section
   unsigned long long items;  // Σ clock lengths of Skip structs (items = Σ all lengths − this)
@@ -83,7 +84,7 @@ struct Work {
   uint32_t nbig = 0, nsmall = 0;
   uint32_t schunk = SCHUNK;        // chunk bytes of this batch's large updates (<= SCHUNK)
   uint32_t force_xtab = 0;         // YCRDT_DECODE=xtab: every large update takes the exit-table walk (tests)
-  uint32_t spec_exact = 1;         // k_spec hands long / deep structs to the exact parser (YCRDT_SPEC_EXACT=0: steps on)
+  uint32_t spec_hint = 2;          // k_spec chunk-start hints: 0 never, 1 always, 2 single-section updates
   uint32_t lazy = 0;               // 1: mergeUpdates / diffUpdate decode (references kept raw)
   unsigned long long* dbg = nullptr; // YCRDT_DEBUG_YATA=1: k_yata work counters
   const Group* groups = nullptr;   // [G] chunks of the large updates
@@ -95,7 +96,8 @@ struct Work {
   Counters* ctr = nullptr;
   uint64_t* spec_bits = nullptr;   // [B/64] positions visited by the chunk chains (large updates)
   uint32_t* cexit = nullptr;       // [G] first chain position at / past each chunk's end
-  uint32_t* sexit = nullptr;       // [G] the same after k_sync's first round (the second writes cexit)
+  uint32_t* sexit = nullptr;       // [G] the same after k_sync's odd rounds (the even rounds write cexit)
+  uint32_t* sent = nullptr;        // [2G] k_sync: the entry each chunk was last walked from; then "entered past its end" flags
   uint32_t* xtab = nullptr;        // [G x XK] locked updates only, per entry offset: count << 16 | exit - chunk end
   uint32_t* tentry = nullptr;      // [G] locked updates: true entry of a chunk the table walk did not parse
   uint32_t* xlist = nullptr;       // [G] the chunks of the locked updates (k_xtab / k_xmark work list)
@@ -145,7 +147,8 @@ struct Work {
   uint32_t ch_mask = 0;            // slots - 1 (a power of two >= 2 x the clients)
   uint32_t* cl_doc = nullptr;      // document of every client index (multi-doc)
   uint32_t* cl_tmp = nullptr;      // sort scratch [cap_sections]
-  uint32_t* cl_state = nullptr;    // per client state (max end clock)
+  uint32_t* cl_state = nullptr;
+  uint8_t* cl_single = nullptr;    // [NC] 1: the client's structs come from one section of one update    // per client state (max end clock)
   uint64_t* cl_base = nullptr;     // [NC+1] exclusive prefix of states (unit base)
   uint32_t* cl_start = nullptr;    // per client start clock for diff encodes (sv); 0 = full
   // per-client integration caps (Yjs pending structs, yc_ingest.h): sorted (client, cap) pairs;

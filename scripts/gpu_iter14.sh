@@ -1,0 +1,18 @@
+#!/bin/bash
+set -u
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+timeout -k 10 400 python -u -m pytest tests/test_gpu_chunk_path.py tests/test_gpu_decode_paths.py tests/test_gpu_parity.py tests/test_gpu_edges.py tests/test_gpu_multidoc.py tests/test_gpu_merge.py -x -q --timeout 240 --timeout-method thread -m gpu > gpurun_out/t14.log 2>&1
+rc=$?; echo "tests rc=$rc"; grep -E "passed|failed|FAILED|Error" gpurun_out/t14.log | tail -5
+[ $rc -eq 0 ] || exit $rc
+timeout -k 10 300 python3 bench.py --steps 10 --warmup 2 --only-headline > gpurun_out/b14.log 2>&1 || { echo "bench rc=$?"; tail -5 gpurun_out/b14.log; exit 1; }
+python3 - <<'PY'
+import json
+d = json.loads(open("gpurun_out/b14.log").read().strip().splitlines()[-1])
+print("bench", d["ms_per_step"], d.get("phases_ms"))
+PY
+YCRDT_DEBUG_DECODE=1 timeout -k 10 200 python3 bench.py --steps 1 --warmup 0 --only-headline > gpurun_out/db14.log 2>&1 || { echo "dbg rc=$?"; exit 1; }
+grep "fastwalk" gpurun_out/db14.log | tail -1
+timeout -k 10 120 python3 scripts/probe_single.py 10 > gpurun_out/s14.log 2>&1 || { echo "single rc=$?"; exit 1; }; echo "== single"; grep -E "wall|direct" gpurun_out/s14.log | cut -c1-200
+timeout -k 10 300 python3 scripts/probe_c4full.py 1 > gpurun_out/c14.log 2>&1 || { echo "c4 rc=$?"; tail -3 gpurun_out/c14.log; exit 1; }
+echo "== c4"; grep "merge ms" gpurun_out/c14.log | cut -c1-300
