@@ -718,10 +718,14 @@ def main():
                     traffic = int(float(r["hbm_bytes"]))
                     traffic_src = os.path.basename(pmc[-1])
     # the whole merge's counter traffic from the same PMC pass (sum over its kernels, per merge)
+    # (per-dispatch averages x dispatches / merges when the summary counts dispatches: kernels
+    # launched several times per merge — scans, the k_sync rounds — count every launch)
     pipe_traffic = None
     if pmc:
         with open(pmc[-1]) as f:
-            pipe_traffic = int(sum(float(r["hbm_bytes"]) for r in csv.DictReader(f)))
+            rows = list(csv.DictReader(f))
+        merges = max([int(r.get("dispatches") or 1) for r in rows if r["kernel"] == ROOF_KERNEL] or [1])
+        pipe_traffic = int(sum(float(r["hbm_bytes"]) * int(r.get("dispatches") or merges) for r in rows) / merges)
     achieved = alg / (k_ms * 1e-3) / 1e9 if k_ms > 0 else 0.0
     dominant = max(phases, key=lambda p: p[1]) if phases else ("merge", st.device_ms)
     roofline = {

@@ -29,6 +29,7 @@ def load(pattern):
         for (cn, _), vals in d.items():
             per[cn].append(sum(vals))  # one value per dispatch (summed over dimensions)
         out[name] = {cn: sum(v) / len(v) for cn, v in per.items()}
+        out[name]["DISPATCHES"] = max(len(v) for v in per.values())
     return out
 
 
@@ -44,11 +45,11 @@ def main():
     for k, v in data.items():
         rd = 2 * v.get("FETCH_SIZE", 0.0) * 1024
         wr = v.get("WRITE_SIZE", 0.0) * 1024
-        rows.append([k] + [round(v.get(c, 0.0), 1) for c in cols] + [round(rd), round(wr), round(rd + wr)])
-    rows.sort(key=lambda r: -r[-1])
+        rows.append([k] + [round(v.get(c, 0.0), 1) for c in cols] + [round(rd), round(wr), round(rd + wr), int(v.get("DISPATCHES", 1))])
+    rows.sort(key=lambda r: -r[-2])
     with open(dst, "w", newline="") as f:
         w = csv.writer(f)
-        w.writerow(["kernel"] + [c.lower() for c in cols] + ["hbm_read_bytes", "hbm_write_bytes", "hbm_bytes"])
+        w.writerow(["kernel"] + [c.lower() for c in cols] + ["hbm_read_bytes", "hbm_write_bytes", "hbm_bytes", "dispatches"])
         w.writerows(rows)
     for r in rows[:25]:
         print(r[0][:28].ljust(28), " ".join(str(x) for x in r[1:]))
