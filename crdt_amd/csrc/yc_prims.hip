@@ -2,6 +2,8 @@
 #include <algorithm>
 #include <cstring>
 #include <cstdlib>
+#include <mutex>
+#include <unordered_map>
 #include <rocprim/rocprim.hpp>
 #include "yc_work.h"
 
@@ -62,6 +64,10 @@ size_t prim_tmp_bytes(uint64_t n) {
 // merge runs a dozen scans. Each lane sums a contiguous run, the 1 024 run sums are scanned in LDS,
 // each lane writes its run's prefixes; a lane reads in[i] before it writes out[i] and runs are
 // disjoint, so in == out is safe. Same results as rocprim::exclusive_scan (wrapping plus).
+static bool getenv_flag(const char* name) {  // experiments: YCRDT_ROCPRIM_SCAN=1 takes rocPRIM's scans
+  static const bool v = getenv(name) && getenv(name)[0] == '1';
+  return v;
+}
 constexpr uint32_t SMALL_SCAN_LANES = 1024, SMALL_SCAN_MAX = SMALL_SCAN_LANES * 16;
 template <class T>
 __global__ __launch_bounds__(SMALL_SCAN_LANES) void k_scan_small(const uint32_t* in, T* out, uint32_t n) {
@@ -86,12 +92,161 @@ __global__ __launch_bounds__(SMALL_SCAN_LANES) void k_scan_small(const uint32_t*
   }
 }
 
+// Larger scans: one launch with a decoupled look-back (rocPRIM's is two: the tile-state init and
+// the scan; a merge runs about nine large ones). A tile's state is ONE 64-bit word — epoch (22
+// bits) | status (2: aggregate / inclusive prefix) | value (40 bits) — stored and loaded as a
+// relaxed agent-scope atomic: coherent across the XCDs' L2s without the cache invalidations an
+// acquire costs on gfx950 (an acquire-load spin made every kernel beside it 2-5x slower). Tile
+// states stay valid across launches without an init pass: every scan on a stream gets a new
+// epoch, and a state left by an earlier scan reads as "not yet" (states start zeroed; epoch 0 is
+// never used). The states are per stream (work on one stream is ordered; the merge runs scans on
+// two streams at once). Each tile is 256 lanes x 16 entries; its first wavefront publishes the
+// tile total, then looks back 64 tiles per round (each lane spinning on its own predecessor) until
+// a tile with an inclusive prefix, and publishes its own. Tiles wait only on lower tile ids, which
+// the dispatcher issued earlier. A lane reads all of its entries before it writes any, and tiles
+// are disjoint, so in == out is safe. Values travel mod 2^40: exact for u32 scans (mod 2^32) and
+// for u64 scans whose total is below 2^40 (byte and unit positions of a merge: bounded by HBM).
+constexpr uint32_t LB_LANES = 256, LB_ITEMS = 16, LB_TILE = LB_LANES * LB_ITEMS;
+constexpr uint64_t LB_VAL = (1ull << 40) - 1;
+constexpr uint32_t LB_EPOCHS = 1u << 22;
+template <class T>
+__global__ __launch_bounds__(LB_LANES) void k_scan_lb(const uint32_t* in, T* out, uint64_t n,
+                                                     unsigned long long* __restrict__ state, uint32_t epoch, uint32_t vec) {
+  __shared__ T wtot[LB_LANES / 64];
+  __shared__ T tile_pre;
+  const uint32_t t = threadIdx.x, lane = t & 63, wv = t >> 6, tile = blockIdx.x;
+  const uint64_t base = (uint64_t)tile * LB_TILE + (uint64_t)t * LB_ITEMS;
+  const unsigned long long ep = (unsigned long long)epoch << 42;
+  uint32_t v[LB_ITEMS];
+  if (vec && base + LB_ITEMS <= n) {
+#pragma unroll
+    for (uint32_t k = 0; k < LB_ITEMS / 4; ++k) {
+      const uint4 q = ((const uint4*)(in + base))[k];
+      v[4 * k] = q.x; v[4 * k + 1] = q.y; v[4 * k + 2] = q.z; v[4 * k + 3] = q.w;
+    }
+  } else {
+#pragma unroll
+    for (uint32_t k = 0; k < LB_ITEMS; ++k) v[k] = base + k < n ? in[base + k] : 0u;
+  }
+  T sum = 0;
+#pragma unroll
+  for (uint32_t k = 0; k < LB_ITEMS; ++k) sum += (T)v[k];
+  // tile-exclusive prefix of this lane's run
+  T inc = sum;
+  for (uint32_t off = 1; off < 64; off <<= 1) {
+    const T y = __shfl_up(inc, off);
+    if (lane >= off) inc += y;
+  }
+  if (lane == 63) wtot[wv] = inc;
+  __syncthreads();
+  T wpre = 0, agg = 0;
+#pragma unroll
+  for (uint32_t k = 0; k < LB_LANES / 64; ++k) {
+    wpre += k < wv ? wtot[k] : (T)0;
+    agg += wtot[k];
+  }
+  T run = wpre + inc - sum;
+  if (wv == 0) {
+    uint64_t pre = 0;
+    if (tile == 0) {
+      if (lane == 0)
+        __hip_atomic_store(&state[0], ep | (2ull << 40) | ((uint64_t)agg & LB_VAL), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+      if (lane == 0)
+        __hip_atomic_store(&state[tile], ep | (1ull << 40) | ((uint64_t)agg & LB_VAL), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      int64_t j = (int64_t)tile - 1;
+      for (;;) {
+        const int64_t me = j - (int64_t)lane;
+        uint32_t st = 2;
+        uint64_t val = 0;
+        if (me >= 0) {
+          unsigned long long x;
+          while (((x = __hip_atomic_load(&state[me], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) >> 42) != epoch)
+            __builtin_amdgcn_s_sleep(1);
+          st = (uint32_t)(x >> 40) & 3u;
+          val = x & LB_VAL;
+        }
+        const uint64_t done = __ballot(st == 2);  // lanes past tile 0 count as done with 0
+        const uint32_t stop = (uint32_t)__ffsll((long long)done) - 1;  // nearest inclusive prefix
+        uint64_t part = lane <= stop ? val : 0ull;
+        for (uint32_t off = 32; off > 0; off >>= 1) part += __shfl_xor(part, off);
+        pre += part;
+        if (done) break;
+        j -= 64;
+      }
+      if (lane == 0)
+        __hip_atomic_store(&state[tile], ep | (2ull << 40) | ((pre + (uint64_t)agg) & LB_VAL), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (lane == 0) tile_pre = (T)pre;
+  }
+  __syncthreads();
+  run += tile_pre;
+  T o[LB_ITEMS];
+#pragma unroll
+  for (uint32_t k = 0; k < LB_ITEMS; ++k) { o[k] = run; run += (T)v[k]; }
+  if (vec && base + LB_ITEMS <= n) {
+    if (sizeof(T) == 4) {
+#pragma unroll
+      for (uint32_t k = 0; k < LB_ITEMS / 4; ++k)
+        ((uint4*)(out + base))[k] = make_uint4((uint32_t)o[4 * k], (uint32_t)o[4 * k + 1], (uint32_t)o[4 * k + 2], (uint32_t)o[4 * k + 3]);
+    } else {
+#pragma unroll
+      for (uint32_t k = 0; k < LB_ITEMS / 2; ++k)
+        ((ulonglong2*)(out + base))[k] = make_ulonglong2((unsigned long long)o[2 * k], (unsigned long long)o[2 * k + 1]);
+    }
+  } else {
+#pragma unroll
+    for (uint32_t k = 0; k < LB_ITEMS; ++k)
+      if (base + k < n) out[base + k] = o[k];
+  }
+}
+
+// per-stream look-back states (zeroed at allocation, then only written by k_scan_lb)
+struct LbState {
+  unsigned long long* state = nullptr;
+  uint64_t tiles = 0;
+  uint32_t epoch = 0;
+};
+static std::mutex lb_mu;
+static std::unordered_map<hipStream_t, LbState> lb_states;
+static LbState* lb_state(uint64_t tiles, hipStream_t s) {
+  std::lock_guard<std::mutex> g(lb_mu);
+  LbState& st = lb_states[s];
+  if (st.tiles < tiles || st.epoch + 1 >= LB_EPOCHS) {
+    const uint64_t nt = std::max<uint64_t>(tiles, st.tiles) + 256;
+    if (st.state) {  // the stream's earlier scans may still read the old states
+      if (hipStreamSynchronize(s) != hipSuccess) return nullptr;
+      (void)hipFree(st.state);
+    }
+    st = LbState{};
+    if (hipMalloc((void**)&st.state, nt * 8) != hipSuccess || hipMemsetAsync(st.state, 0, nt * 8, s) != hipSuccess) {
+      (void)hipGetLastError();
+      st = LbState{};
+      return nullptr;
+    }
+    st.tiles = nt;
+  }
+  ++st.epoch;
+  return &st;
+}
+template <class T>
+static bool scan_lb(const uint32_t* in, T* out, uint64_t n, hipStream_t s) {
+  const uint64_t tiles = (n + LB_TILE - 1) / LB_TILE;
+  LbState* st = lb_state(tiles, s);
+  if (!st) return false;
+  const uint32_t vec = (((uintptr_t)in | (uintptr_t)out) & 15u) == 0;
+  hipLaunchKernelGGL(k_scan_lb<T>, dim3((uint32_t)tiles), dim3(LB_LANES), 0, s, in, out, n, st->state, st->epoch, vec);
+  return true;
+}
+
 void scan_u32(void* tmp, size_t tmpb, const uint32_t* in, uint32_t* out, uint64_t n, hipStream_t s) {
   if (!n) return;
   if (n <= SMALL_SCAN_MAX) {
     hipLaunchKernelGGL(k_scan_small<uint32_t>, dim3(1), dim3(SMALL_SCAN_LANES), 0, s, in, out, (uint32_t)n);
     return;
   }
+  if (!getenv_flag("YCRDT_ROCPRIM_SCAN") && scan_lb<uint32_t>(in, out, n, s)) return;
   rocprim::exclusive_scan(tmp, tmpb, in, out, 0u, (size_t)n, rocprim::plus<uint32_t>(), s);
 }
 
@@ -101,6 +256,7 @@ void scan_u32_to_u64(void* tmp, size_t tmpb, const uint32_t* in, uint64_t* out, 
     hipLaunchKernelGGL(k_scan_small<uint64_t>, dim3(1), dim3(SMALL_SCAN_LANES), 0, s, in, out, (uint32_t)n);
     return;
   }
+  if (!getenv_flag("YCRDT_ROCPRIM_SCAN") && scan_lb<uint64_t>(in, out, n, s)) return;
   rocprim::exclusive_scan(tmp, tmpb, in, out, (uint64_t)0, (size_t)n, rocprim::plus<uint64_t>(), s);
 }
 
