@@ -749,14 +749,29 @@ def main():
 
     # ---- end to end (host buffers in, host buffers out): pack + H2D + merge + D2H + per-document
     # split; never `value`
-    e2e_steps = 0 if args.only_headline or args.billion else 2
-    e0 = time.perf_counter()
-    for _ in range(e2e_steps):
-        b2 = crdt_amd.Batch(docs=docs, engine=eng) if ndocs > 1 else crdt_amd.Batch(updates, eng)
-        b2.merge()
-        b2.result_docs_packed()  # every document's update + state vector, split on the device
-        del b2
-    e2e_ms = (time.perf_counter() - e0) * 1e3 / max(1, e2e_steps)
+    # A serving loop: batch k+1 is staged (host pack + pinned H2D on the engine's copy stream) by a
+    # second host thread while batch k merges and its result comes back; one result buffer is
+    # reused. One untimed warm-up batch (pinned areas, first touch of the result buffer).
+    e2e_steps = 0 if args.only_headline or args.billion else 4
+    make = (lambda: crdt_amd.Batch(docs=docs, engine=eng)) if ndocs > 1 else (lambda: crdt_amd.Batch(updates, eng))
+    e2e_ms = 0.0
+    if e2e_steps:
+        from concurrent.futures import ThreadPoolExecutor
+
+        res_buf = None
+        with ThreadPoolExecutor(1) as stager:
+            for i in range(e2e_steps + 1):
+                if i == 1:
+                    e0 = time.perf_counter()
+                nxt = stager.submit(make) if i == 0 else nxt
+                b2 = nxt.result()
+                if i < e2e_steps:
+                    nxt = stager.submit(make)  # staged beside this batch's merge and result
+                b2.merge()
+                blob, _ = b2.result_docs_packed(out=res_buf)  # every document's update + state vector
+                res_buf = blob.base if blob.base is not None else blob
+                del b2, blob
+        e2e_ms = (time.perf_counter() - e0) * 1e3 / e2e_steps
     del batch
     # ---- one C2 document per step (the round-1 headline shape), for continuity
     single = None
@@ -819,7 +834,8 @@ def main():
                        "x_device": round(e2e_ms / (dev_ms / args.steps), 2) if dev_ms else None,
                        "includes": "host buffers in (no-copy ycrdt_buf packing, pinned pipelined H2D) + merge + "
                                    "per-document split in HBM + pipelined D2H of every document's update and state "
-                                   "vector into one host array (ycrdt_batch_result_docs_packed), 1 GPU"} if e2e_steps else None,
+                                   "vector into one reused host array (ycrdt_batch_result_docs_packed); batch k+1 staged by a second host "
+                                   "thread beside batch k's merge and result (the engine's copy stream), 1 GPU"} if e2e_steps else None,
         "pipeline_roofline": {
             "b_alg_bytes": b_alg,
             "achieved_GBs": round(b_alg / (ms_per_step * 1e-3) / 1e9, 2),

@@ -441,17 +441,22 @@ class Batch:
         _check(lib().ycrdt_batch_result_docs(self._h, us, ss))
         return [(_take(us[i]), _take(ss[i])) for i in range(self.ndocs)]
 
-    def result_docs_packed(self):
+    def result_docs_packed(self, out=None):
         """(blob, offs): every document's update and state vector back to back in one numpy uint8
         array, split on the device — document d's update is blob[offs[2d]:offs[2d+1]], its state
-        vector blob[offs[2d+1]:offs[2d+2]] (ycrdt_batch_result_docs_packed)."""
+        vector blob[offs[2d+1]:offs[2d+2]] (ycrdt_batch_result_docs_packed). `out`: a uint8 array to
+        write into when it is large enough (a serving loop reuses one: no page faults of a fresh
+        gigabyte per batch); blob is then a view of it."""
         import numpy as np
 
         offs = np.zeros(2 * self.ndocs + 1, dtype=np.uint64)
         total = ctypes.c_uint64()
         op = offs.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64))
         _check(lib().ycrdt_batch_result_docs_packed(self._h, None, 0, op, ctypes.byref(total)))
-        blob = np.empty(max(1, total.value), dtype=np.uint8)
+        if out is not None and out.dtype == np.uint8 and out.flags.c_contiguous and out.size >= max(1, total.value):
+            blob = out
+        else:
+            blob = np.empty(max(1, total.value), dtype=np.uint8)
         _check(lib().ycrdt_batch_result_docs_packed(self._h, blob.ctypes.data, total.value, op, ctypes.byref(total)))
         return blob[: total.value], offs
 

@@ -174,6 +174,11 @@ enum Buf {
 
 }  // namespace
 
+struct Pinned {
+  uint8_t* p = nullptr;
+  size_t cap = 0;
+  hipEvent_t ev[2] = {nullptr, nullptr};
+};
 struct ycrdt_engine {
   int device = 0;
   int compat = 136;
@@ -190,10 +195,12 @@ struct ycrdt_engine {
   std::vector<std::pair<const char*, double>> phase_ms;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   // pinned host staging (two halves of PIN_PER chunks: the copy of one wave into a half overlaps
-  // the H2D of the previous wave from the other) and its per-half "H2D done" events
-  uint8_t* pin = nullptr;
-  size_t pin_cap = 0;
-  hipEvent_t pin_ev[2] = {nullptr, nullptr};
+  // the copy of the previous wave from the other) and its per-half "copy done" events: one area
+  // for batch staging (H2D, on the copy stream) and one for results (D2H, on the engine stream),
+  // so a batch can be staged by one host thread while another merges the previous batch
+  Pinned pin_in, pin_out;
+  hipStream_t copy = nullptr;  // batch staging (host → HBM)
+  hipEvent_t copy_dep = nullptr;
   // result of the last merge (e->w.out / e->w.sv_out): ws_owner is the batch that produced it
   // (nullptr after any other call), so ycrdt_batch_result never returns another call's bytes
   const void* ws_owner = nullptr;
@@ -395,7 +402,7 @@ struct HostPiece {
   uint64_t len;
   const uint8_t* p;
 };
-constexpr uint32_t PIN_PER = 16;
+constexpr uint32_t PIN_PER = 4;  // 128 MiB waves: the copy of a wave overlaps the transfer of the previous
 // 32 MiB; YCRDT_PIN_CHUNK (tests: e.g. 65536) makes the two-half wave path run on small batches
 uint64_t pin_chunk() {
   const char* v = getenv("YCRDT_PIN_CHUNK");
@@ -416,34 +423,36 @@ void fill_range(uint8_t* dst, uint64_t lo, uint64_t hi, const std::vector<HostPi
   }
   if (hi > cur) memset(dst + (cur - lo), 0, hi - cur);
 }
-int ensure_pinned(ycrdt_engine* e, size_t need) {
-  if (need <= e->pin_cap) return YCRDT_OK;
-  HIPCHK(hipStreamSynchronize(e->stream));
-  if (e->pin) hipHostFree(e->pin);
-  e->pin = nullptr;
-  e->pin_cap = 0;
+int ensure_pinned(Pinned& pin, size_t need, hipStream_t s) {
+  if (need <= pin.cap) return YCRDT_OK;
+  HIPCHK(hipStreamSynchronize(s));
+  if (pin.p) hipHostFree(pin.p);
+  pin.p = nullptr;
+  pin.cap = 0;
   const size_t c = std::max<size_t>(need, size_t(1) << 20);
-  if (hipHostMalloc((void**)&e->pin, c, hipHostMallocDefault) != hipSuccess) {
+  if (hipHostMalloc((void**)&pin.p, c, hipHostMallocDefault) != hipSuccess) {
     (void)hipGetLastError();
-    e->pin = nullptr;
+    pin.p = nullptr;
     return fail(YCRDT_E_DEVICE, "pinned host staging allocation failed");
   }
-  e->pin_cap = c;
+  pin.cap = c;
   return YCRDT_OK;
 }
 int h2d_span(ycrdt_engine* e, uint8_t* dev, uint64_t span, const std::vector<HostPiece>& hp) {
   if (!span) return YCRDT_OK;
+  Pinned& pin = e->pin_in;
+  const hipStream_t s = e->copy;
   const uint64_t PIN_CHUNK = pin_chunk();
   const uint64_t nch = (span + PIN_CHUNK - 1) / PIN_CHUNK;
   const bool waves = nch > PIN_PER;
-  if (const int rc = ensure_pinned(e, waves ? 2 * PIN_PER * PIN_CHUNK : (size_t)span)) return rc;
+  if (const int rc = ensure_pinned(pin, waves ? 2 * PIN_PER * PIN_CHUNK : (size_t)span, s)) return rc;
   const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
   const uint32_t T = span < (uint64_t(8) << 20) ? 1u : std::min<uint32_t>({16u, hw, (uint32_t)nch});
   for (uint64_t k0 = 0, wave = 0; k0 < nch; k0 += PIN_PER, ++wave) {
     const uint64_t k1 = std::min<uint64_t>(nch, k0 + PIN_PER);
     const uint32_t half = (uint32_t)(wave & 1);
-    uint8_t* base = e->pin + (waves ? half * PIN_PER * PIN_CHUNK : 0);
-    if (wave >= 2) HIPCHK(hipEventSynchronize(e->pin_ev[half]));  // that half's previous H2D is done
+    uint8_t* base = pin.p + (waves ? half * PIN_PER * PIN_CHUNK : 0);
+    if (wave >= 2) HIPCHK(hipEventSynchronize(pin.ev[half]));  // that half's previous H2D is done
     const uint64_t lo = k0 * PIN_CHUNK, hi = std::min(span, k1 * PIN_CHUNK);
     if (T == 1) {
       fill_range(base, lo, hi, hp);
@@ -460,8 +469,8 @@ int h2d_span(ycrdt_engine* e, uint8_t* dev, uint64_t span, const std::vector<Hos
       work();
       for (auto& t : th) t.join();
     }
-    HIPCHK(hipMemcpyAsync(dev + lo, base, hi - lo, hipMemcpyHostToDevice, e->stream));
-    HIPCHK(hipEventRecord(e->pin_ev[half], e->stream));
+    HIPCHK(hipMemcpyAsync(dev + lo, base, hi - lo, hipMemcpyHostToDevice, s));
+    HIPCHK(hipEventRecord(pin.ev[half], s));
   }
   return YCRDT_OK;
 }
@@ -479,6 +488,14 @@ int stage_srcs(ycrdt_batch* b, const std::vector<Src>& src, const uint32_t* doc_
   const size_t nu = b->ulen.size();
   size_t ndev = 0;
   while (ndev < nu && src[order[ndev]].dev) ++ndev;
+  // staging runs on the copy stream (a host thread may stage the next batch while another merges
+  // on the engine stream); device sources (doc states in HBM) are read after the engine stream's
+  // work so far, which may still be writing them
+  const hipStream_t cs = e->copy;
+  if (ndev) {
+    HIPCHK(hipEventRecord(e->copy_dep, e->stream));
+    HIPCHK(hipStreamWaitEvent(cs, e->copy_dep, 0));
+  }
   // the host updates: their span (window gaps included) through pinned staging
   const uint64_t host0 = ndev < nu ? uabs(b, ndev) : b->nbytes;
   {
@@ -488,15 +505,15 @@ int stage_srcs(ycrdt_batch* b, const std::vector<Src>& src, const uint32_t* doc_
     if (const int rc = h2d_span(e, (uint8_t*)b->bytes.p + host0, b->nbytes - host0, hp)) return rc;
   }
   if (ndev == 1) {
-    if (b->ulen[0]) HIPCHK(hipMemcpyAsync(b->bytes.p, src[order[0]].p, b->ulen[0], hipMemcpyDeviceToDevice, e->stream));
+    if (b->ulen[0]) HIPCHK(hipMemcpyAsync(b->bytes.p, src[order[0]].p, b->ulen[0], hipMemcpyDeviceToDevice, cs));
   } else if (ndev > 1) {
     std::vector<Piece> pc;
     pc.reserve(ndev);
     for (size_t u = 0; u < ndev; ++u)
       if (b->ulen[u]) pc.push_back(Piece{src[order[u]].p, (uint8_t*)b->bytes.p + uabs(b, u), b->ulen[u], {0}});
     if (!grow(b->pieces, sizeof(Piece) * (pc.size() + 1))) return fail(YCRDT_E_DEVICE, oom("pieces"));
-    HIPCHK(hipMemcpyAsync(b->pieces.p, pc.data(), sizeof(Piece) * pc.size(), hipMemcpyHostToDevice, e->stream));
-    copy_pieces((const Piece*)b->pieces.p, (uint32_t)pc.size(), e->stream);
+    HIPCHK(hipMemcpyAsync(b->pieces.p, pc.data(), sizeof(Piece) * pc.size(), hipMemcpyHostToDevice, cs));
+    copy_pieces((const Piece*)b->pieces.p, (uint32_t)pc.size(), cs);
   }
   // meta: uoff | ulen | ugroup | groups | udoc | ulist
   b->ndocs = doc_of && ndocs > 1 ? ndocs : 1;
@@ -531,8 +548,8 @@ int stage_srcs(ycrdt_batch* b, const std::vector<Src>& src, const uint32_t* doc_
   o = (o + 15) & ~size_t(15);
   b->uwin_off = o;
   if (!b->uwin.empty()) memcpy(meta.data() + o, b->uwin.data(), sizeof(uint32_t) * b->uwin.size());
-  HIPCHK(hipMemcpyAsync(b->meta.p, meta.data(), meta_bytes, hipMemcpyHostToDevice, e->stream));
-  HIPCHK(hipStreamSynchronize(e->stream));
+  HIPCHK(hipMemcpyAsync(b->meta.p, meta.data(), meta_bytes, hipMemcpyHostToDevice, cs));
+  HIPCHK(hipStreamSynchronize(cs));
   b->merged = false;
   return YCRDT_OK;
 }
@@ -1531,24 +1548,25 @@ int d2h_span(ycrdt_engine* e, uint8_t* host, const uint8_t* dev, uint64_t span) 
   const uint64_t PIN_CHUNK = pin_chunk();
   const uint64_t nch = (span + PIN_CHUNK - 1) / PIN_CHUNK;
   const bool waves = nch > PIN_PER;
-  if (const int rc = ensure_pinned(e, waves ? 2 * PIN_PER * PIN_CHUNK : (size_t)span)) return rc;
+  Pinned& pin = e->pin_out;
+  if (const int rc = ensure_pinned(pin, waves ? 2 * PIN_PER * PIN_CHUNK : (size_t)span, e->stream)) return rc;
   const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
   const uint32_t T = span < (uint64_t(8) << 20) ? 1u : std::min<uint32_t>({16u, hw, (uint32_t)nch});
   const uint64_t nw = (nch + PIN_PER - 1) / PIN_PER;
   auto issue = [&](uint64_t wave) -> int {
     const uint64_t lo = wave * PIN_PER * PIN_CHUNK, hi = std::min(span, lo + PIN_PER * PIN_CHUNK);
-    uint8_t* base = e->pin + (waves ? (wave & 1) * PIN_PER * PIN_CHUNK : 0);
+    uint8_t* base = pin.p + (waves ? (wave & 1) * PIN_PER * PIN_CHUNK : 0);
     HIPCHK(hipMemcpyAsync(base, dev + lo, hi - lo, hipMemcpyDeviceToHost, e->stream));
-    HIPCHK(hipEventRecord(e->pin_ev[wave & 1], e->stream));
+    HIPCHK(hipEventRecord(pin.ev[wave & 1], e->stream));
     return YCRDT_OK;
   };
   if (const int rc = issue(0)) return rc;
   for (uint64_t wave = 0; wave < nw; ++wave) {
-    HIPCHK(hipEventSynchronize(e->pin_ev[wave & 1]));
+    HIPCHK(hipEventSynchronize(pin.ev[wave & 1]));
     if (wave + 1 < nw)
       if (const int rc = issue(wave + 1)) return rc;  // into the other half, beside the copy-out below
     const uint64_t lo = wave * PIN_PER * PIN_CHUNK, hi = std::min(span, lo + PIN_PER * PIN_CHUNK);
-    const uint8_t* base = e->pin + (waves ? (wave & 1) * PIN_PER * PIN_CHUNK : 0);
+    const uint8_t* base = pin.p + (waves ? (wave & 1) * PIN_PER * PIN_CHUNK : 0);
     if (T == 1) {
       memcpy(host + lo, base, hi - lo);
     } else {
@@ -1625,8 +1643,12 @@ int ycrdt_engine_create(int device, int compat, ycrdt_engine** out) {
   hipEventCreateWithFlags(&e->side_fork, hipEventDisableTiming);
   hipEventCreate(&e->ev0);
   hipEventCreate(&e->ev1);
-  hipEventCreateWithFlags(&e->pin_ev[0], hipEventDisableTiming);
-  hipEventCreateWithFlags(&e->pin_ev[1], hipEventDisableTiming);
+  if (hipStreamCreateWithFlags(&e->copy, hipStreamNonBlocking) != hipSuccess) { delete e; return fail(YCRDT_E_DEVICE, "stream"); }
+  hipEventCreateWithFlags(&e->copy_dep, hipEventDisableTiming);
+  for (Pinned* pin : {&e->pin_in, &e->pin_out}) {
+    hipEventCreateWithFlags(&pin->ev[0], hipEventDisableTiming);
+    hipEventCreateWithFlags(&pin->ev[1], hipEventDisableTiming);
+  }
   e->bufs.resize(B_COUNT);
   *out = e;
   return YCRDT_OK;
@@ -1646,9 +1668,14 @@ void ycrdt_engine_destroy(ycrdt_engine* e) {
   for (auto& ev : e->event_pool) hipEventDestroy(ev);
   hipEventDestroy(e->ev0);
   hipEventDestroy(e->ev1);
-  hipEventDestroy(e->pin_ev[0]);
-  hipEventDestroy(e->pin_ev[1]);
-  if (e->pin) hipHostFree(e->pin);
+  hipStreamSynchronize(e->copy);
+  for (Pinned* pin : {&e->pin_in, &e->pin_out}) {
+    hipEventDestroy(pin->ev[0]);
+    hipEventDestroy(pin->ev[1]);
+    if (pin->p) hipHostFree(pin->p);
+  }
+  hipEventDestroy(e->copy_dep);
+  hipStreamDestroy(e->copy);
   hipStreamSynchronize(e->side);
   hipEventDestroy(e->side_done);
   hipEventDestroy(e->side_fork);
