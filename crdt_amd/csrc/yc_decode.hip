@@ -541,7 +541,8 @@ __global__ __launch_bounds__(DL) void k_direct(Work w) {
 // byte). The chunk chains and the walker use this one function, so chains that meet stay together.
 template <class S>
 __device__ __forceinline__ uint32_t chain_len(const S& src, const uint8_t* __restrict__ b, uint32_t p, uint32_t uend,
-                                              unsigned long long* dbg = nullptr) {
+                                              unsigned long long* dbg = nullptr, const uint8_t* xb = nullptr,
+                                              uint32_t xoff = 0) {
   {
     RegWin x;
     src.load_win(p, x);
@@ -558,7 +559,8 @@ __device__ __forceinline__ uint32_t chain_len(const S& src, const uint8_t* __res
   } else if (ref >= 1 && ref <= REF_DOC) {
     d = spec_len(src, p, uend, (ref - 1) * 8 + (info >> 5));
     if (d == 1) {  // handed over (long / deep / Doc)
-      d = exact_len(b, p, uend);
+      // (xb: the update staged in LDS, xoff its first position: the exact parser reads LDS)
+      d = xb ? exact_len(xb, p - xoff, uend - xoff) : exact_len(b, p, uend);
       if (dbg) { atomicAdd(&dbg[6], 1ull); atomicAdd(&dbg[7], (unsigned long long)d); }
     }
   }
@@ -1197,6 +1199,233 @@ __global__ __launch_bounds__(64) void k_fastwalk(Work w) {
   }
 }
 
+// Small updates, one wavefront each (k_direct: one lane each). The update (<= DIRECT 16 KiB) is
+// staged in LDS with one round of loads; for a single-section update each lane follows the chunk
+// chain of 1/64 of it (lane 0 from the first struct, exactly), the lanes re-enter their chunks
+// where the previous lane's chain leaves until no exit changes (a wavefront-local k_sync), and the
+// n-th chain position from the first struct — a popcount scan across the lanes — is the section's
+// last struct. A struct step waits on LDS only, and 64 lanes share an update: an update costs
+// ~1/64 of the lane-serial walk's latency, so few updates (one C2 document's 1 000 replicas) no
+// longer leave the GPU idle, and many pack 64 x more parallel work. Several sections, a chain that
+// does not settle in WD_ROUNDS, or fewer chain positions than structs: lane 0 walks the update
+// exactly (as k_direct, from LDS), which also reports malformed input.
+// k_wdecode's struct step out of line: inlined at each of its call sites, the sizer made the kernel
+// ~150 KB of code, far past the instruction cache (every step then waited on instruction fetch)
+__device__ __attribute__((noinline)) uint32_t wd_len(const uint32_t* ub, uint32_t ustart, uint32_t wlen,
+                                                     const uint8_t* __restrict__ b, uint32_t q, uint32_t uend) {
+  const LdsSrc src{b, ub, ustart, wlen};
+  return chain_len(src, b, q, uend, nullptr, (const uint8_t*)ub, ustart);
+}
+constexpr uint32_t WD_MAX = 16384, WD_WORDS = WD_MAX / 64, WD_ROUNDS = 64;
+__global__ __launch_bounds__(64) void k_wdecode(Work w) {
+  __shared__ __attribute__((aligned(16))) uint32_t ub[(WD_MAX + 64) / 4];
+  __shared__ uint64_t bits[WD_WORDS + 1];
+  __shared__ uint64_t walkbuf[64][WD_WORDS / 64];  // a lane's walked positions, before it commits them
+  const uint32_t lane = threadIdx.x;
+  if (blockIdx.x >= w.nsmall) return;
+  const uint32_t u = w.ulist[w.nbig + blockIdx.x];
+  const uint32_t uw = upd_win(w, u);
+  const uint8_t* __restrict__ b = win_bytes(w, uw);
+  uint64_t* __restrict__ fbits = win_words(w.final_bits, uw);
+  uint64_t* __restrict__ sbits = win_words(w.sec_bits, uw);
+  const uint32_t ustart = w.uoff[u], L = w.ulen[u], uend = ustart + L;
+  uint32_t* err = &w.ctr->err;
+  if (L > WD_MAX) { if (lane == 0) raise_err(err, ERR_CAPACITY); return; }  // (the layout never sends one)
+  // stage: the update's 16-byte lines (updates are 64-byte aligned; the buffer is padded)
+  const uint32_t nq = (L + 15) / 16;
+  for (uint32_t k = lane; k < nq; k += 64) ((uint4*)ub)[k] = ((const uint4*)(b + ustart))[k];
+  const uint32_t nw = (L + 63) / 64;
+  for (uint32_t k = lane; k < nw; k += 64) bits[k] = 0;
+  __syncthreads();
+  const LdsSrc src{b, ub, ustart, nq * 16};
+  const uint8_t* ubb = (const uint8_t*)ub;  // the staged bytes (update position ustart + k at ubb[k])
+  bool ok = true;
+  uint32_t p = ustart;
+  const uint32_t nsec = rd_vu(b, p, uend, ok);
+  if (!ok || nsec > (uend - p) / 3 + 1) { if (lane == 0) { raise_err(err, ERR_DECODE); w.dsstart[u] = NONE; } return; }
+  uint32_t sbase = 0;
+  if (lane == 0) sbase = atomicAdd(&w.ctr->nsections, nsec);
+  sbase = __shfl(sbase, 0);
+  if (sbase + nsec > w.cap_sections) { if (lane == 0) { raise_err(err, ERR_CAPACITY); w.dsstart[u] = NONE; } return; }
+  auto setbit = [&](uint32_t q) { bits[(q - ustart) >> 6] |= 1ull << (q & 63); };
+  uint32_t dsp = NONE;
+  bool done = false;
+  uint32_t why = 5;  // debug: 4 = not settled / jumped, 5 = several sections or short
+  if (nsec == 1) {
+    uint32_t q1 = p;
+    const uint32_t n = rd_vu(b, q1, uend, ok), client = rd_vu(b, q1, uend, ok), clock = rd_vu(b, q1, uend, ok);
+    if (ok && n > 0 && n <= uend - q1) {
+      // chunks: CW bytes per lane, 64-byte multiples from the update start (each lane owns words)
+      const uint32_t CW = ((L + 63) / 64 + 63) & ~63u;
+      const uint32_t cs = ustart + lane * CW, ce = min(cs + CW, uend);
+      const bool live = ce > q1 && cs < uend;
+      uint32_t x = NONE;  // this lane's chain exit
+      if (live) {
+        uint32_t q = max(cs, q1);
+        if (cs > q1) {
+          // a hinted start (as k_spec): the first position of the chunk's first 96 bytes where
+          // three consecutive chain steps begin with the info byte of the first struct
+          const uint32_t hint = src.u8(q1), lim = min(cs + 96u, ce);
+          for (uint32_t h = cs; h < lim; ++h) {
+            if (src.u8(h) != hint) continue;
+            const uint32_t d1 = wd_len(ub, ustart, nq * 16, b, h, uend);
+            if (!d1 || h + d1 >= uend || src.u8(h + d1) != hint) continue;
+            const uint32_t d2 = wd_len(ub, ustart, nq * 16, b, h + d1, uend);
+            if (!d2 || h + d1 + d2 >= uend || src.u8(h + d1 + d2) != hint) continue;
+            q = h;
+            break;
+          }
+        }
+        while (q < ce) {
+          setbit(q);
+          const uint32_t d = wd_len(ub, ustart, nq * 16, b, q, uend);
+          q += d ? d : 1u;
+        }
+        x = q;
+      }
+      // Settling. A lane re-walks its chunk from its entry E (the previous lane's exit) when E
+      // changed, collecting the walked positions aside; meeting its own chain, it keeps the own
+      // positions from there (they are the walk's continuation). A walk that does not meet means
+      // one of the two chains is out of phase: only the lowest such lane — whose entry is right,
+      // every lane before it being consistent — overwrites its chunk with the walk; the others
+      // keep their own chains (the next lane's chain is usually the right one: overwriting it
+      // with a walk from a wrong entry cascaded one chunk per round to the update's end) and stay
+      // "unsettled" until they are the lowest. Settled: no exit changed and every lane consistent.
+      bool settled = false;
+      bool okc = !(live && lane > 0 && cs >= q1);  // lanes that never re-walk are consistent
+      uint32_t sent = NONE;
+      uint64_t* wk = walkbuf[lane];
+      const uint32_t w0 = (cs - ustart) >> 6, wend = live ? (ce - ustart + 63) >> 6 : w0;
+      for (uint32_t r = 0; r < WD_ROUNDS; ++r) {
+        const uint32_t E = __shfl_up(x, 1);
+        const uint64_t bad = __ballot(!okc);
+        const uint32_t first_bad = bad ? (uint32_t)__ffsll((long long)bad) - 1 : 64u;
+        uint32_t nx = x;
+        bool walked = false, met = false;
+        uint32_t q = E;
+        if (!okc || (live && lane > 0 && cs >= q1 && E != sent)) {
+          if (E != sent || lane == first_bad) {
+            sent = E;
+            walked = true;
+            if (E >= ce) {  // the previous chain jumps over this chunk: no struct starts in it
+              for (uint32_t k = w0; k < wend; ++k) bits[k] = 0;
+              nx = E;
+              met = true;
+            } else {
+              for (uint32_t k = 0; k < wend - w0; ++k) wk[k] = 0;
+              while (q < ce && !((bits[(q - ustart) >> 6] >> (q & 63)) & 1ull)) {
+                wk[((q - ustart) >> 6) - w0] |= 1ull << (q & 63);
+                const uint32_t d = wd_len(ub, ustart, nq * 16, b, q, uend);
+                q += d ? d : 1u;
+              }
+              met = q < ce;
+              if (met) {  // met the own chain at q: walked positions, then the own chain
+                const uint32_t qw = (q - ustart) >> 6;
+                for (uint32_t k = w0; k < qw; ++k) bits[k] = wk[k - w0];
+                bits[qw] = wk[qw - w0] | (bits[qw] & (~0ull << (q & 63)));
+              }
+            }
+          }
+        }
+        const uint64_t nm = __ballot(walked && !met);
+        const uint32_t first_nm = nm ? (uint32_t)__ffsll((long long)nm) - 1 : 64u;
+        if (walked && met) okc = true;
+        if (walked && !met) {
+          if (lane == first_nm) {  // the lowest: its entry is right, its own chain is not
+            for (uint32_t k = w0; k < wend; ++k) bits[k] = wk[k - w0];
+            nx = q;
+            okc = true;
+          } else {
+            okc = false;
+          }
+        }
+        const bool changed = __ballot(nx != x) != 0;
+        x = nx;
+        if (!changed && !__ballot(!okc)) { settled = true; break; }
+      }
+      const bool jumped = false;
+      __syncthreads();
+      if (!settled || jumped) why = 4;
+      if (settled && !jumped) {
+        // the n-th chain position from q1: per-lane counts over the lane's words, a wave scan
+        const uint32_t w0 = (cs - ustart) >> 6, w1 = live ? (ce - ustart + 63) >> 6 : w0;
+        uint32_t cnt = 0;
+        for (uint32_t k = w0; k < w1; ++k) cnt += (uint32_t)__popcll(bits[k]);
+        uint32_t inc = cnt;
+        for (uint32_t off = 1; off < 64; off <<= 1) {
+          const uint32_t y = __shfl_up(inc, off);
+          if (lane >= off) inc += y;
+        }
+        const uint64_t hit = __ballot(inc >= n && inc - cnt < n);
+        if (hit) {
+          const uint32_t owner = (uint32_t)__ffsll((long long)hit) - 1;
+          uint32_t lp = NONE;
+          if (lane == owner) {
+            uint32_t rem = n - (inc - cnt), k = w0;
+            for (;; ++k) { const uint32_t c = (uint32_t)__popcll(bits[k]); if (c >= rem) break; rem -= c; }
+            uint64_t m = bits[k];
+            for (uint32_t t = 1; t < rem; ++t) m &= m - 1;
+            lp = ustart + k * 64 + (uint32_t)__ffsll((long long)m) - 1;
+            const uint32_t d = wd_len(ub, ustart, nq * 16, b, lp, uend);
+            dsp = d ? lp + d : NONE;
+            // drop the chain positions past the last struct (delete-set bytes)
+            bits[k] &= ~0ull >> (63 - (lp & 63));
+            for (++k; k < w1; ++k) bits[k] = 0;
+          }
+          dsp = __shfl(dsp, owner);
+          if (lane > owner) for (uint32_t k = w0; k < w1; ++k) bits[k] = 0;
+          if (dsp != NONE && dsp <= uend) {
+            done = true;
+            if (lane == 0) {
+              Section sec;
+              sec.upd = u; sec.n = n; sec.client = client; sec.clock = clock;
+              sec.first_pos = q1; sec.cidx = NONE; sec.first_idx = NONE; sec.pad = 0;
+              w.sections[sbase] = sec;
+              atomicOr((unsigned long long*)&sbits[q1 >> 6], 1ull << (q1 & 63));
+            }
+          }
+        }
+      }
+      __syncthreads();
+      if (!done) for (uint32_t k = lane; k < nw; k += 64) bits[k] = 0;
+      __syncthreads();
+    }
+  }
+  if (lane == 0 && w.dbg) atomicAdd(&w.dbg[done ? 3 : why], 1ull);  // (YCRDT_DEBUG_DECODE)
+  if (!done && lane == 0) {
+    // exact walk of every section (as k_direct), from LDS
+    dsp = NONE;
+    bool fail = false;
+    uint32_t q = p;
+    for (uint32_t sct = 0; sct < nsec && !fail; ++sct) {
+      const uint32_t n = rd_vu(b, q, uend, ok), client = rd_vu(b, q, uend, ok), clock = rd_vu(b, q, uend, ok);
+      if (!ok || n > uend - q) { raise_err(err, ERR_DECODE); fail = true; break; }
+      Section sec;
+      sec.upd = u; sec.n = n; sec.client = client; sec.clock = clock;
+      sec.first_pos = n ? q : NONE; sec.cidx = NONE; sec.first_idx = NONE; sec.pad = 0;
+      w.sections[sbase + sct] = sec;
+      if (n) atomicOr((unsigned long long*)&sbits[q >> 6], 1ull << (q & 63));
+      for (uint32_t k = 0; k < n; ++k) {
+        if (q >= uend) { raise_err(err, ERR_DECODE); w.ctr->err_info = q; fail = true; break; }
+        setbit(q);
+        const uint32_t d = wd_len(ub, ustart, nq * 16, b, q, uend);  // exact on valid structs; 0: none parses
+        if (!d) { raise_err(err, ERR_DECODE); w.ctr->err_info = q; fail = true; break; }
+        q += d;
+      }
+    }
+    if (!fail) dsp = q;
+  }
+  __syncthreads();
+  if (lane == 0) {
+    w.usec_start[u] = sbase;
+    w.usec_n[u] = nsec;
+  }
+  dsp = __shfl(dsp, 0);
+  if (lane == 0) w.dsstart[u] = dsp;
+  // the update's words of the final bitmap (its own: updates are 64-byte aligned)
+  for (uint32_t k = lane; k < nw; k += 64) fbits[(ustart >> 6) + k] = bits[k];
+}
+
 // Positions of the chunks the table walk entered without parsing (tentry): one lane per chunk
 // parses exactly from the entry to the chunk end through its LDS window and marks them.
 __global__ __launch_bounds__(DL) void k_xmark(Work w) {
@@ -1254,7 +1483,10 @@ void launch_chunks(const Work& w, hipStream_t s) {
   }
 }
 void launch_direct(const Work& w, hipStream_t s) {
-  if (w.nsmall) hipLaunchKernelGGL(k_direct, dim3((w.nsmall + DL - 1) / DL), dim3(DL), 0, s, w);
+  const char* wd = getenv("YCRDT_DIRECT_WAVE");  // read per merge (tests switch it)
+  const bool lane_direct = !(wd && wd[0] == '1');
+  if (w.nsmall && !lane_direct) hipLaunchKernelGGL(k_wdecode, dim3(w.nsmall), dim3(64), 0, s, w);
+  else if (w.nsmall) hipLaunchKernelGGL(k_direct, dim3((w.nsmall + DL - 1) / DL), dim3(DL), 0, s, w);
 }
 
 // --------------------------------------------------------------------------- 3. struct positions

@@ -328,9 +328,14 @@ void layout(ycrdt_batch* b, const std::vector<Src>& src, std::vector<uint32_t>& 
                     : mode && !strcmp(mode, "direct") ? 2 : 0;
   size_t nsmall = 0;
   for (const Src& x : src) nsmall += x.len <= DIRECT_MAX_BYTES;
+  // (with the lane-per-update k_direct, small updates take the direct path only when there are
+  // enough to fill wavefronts; with k_wdecode — one wavefront each, YCRDT_DIRECT_WAVE=1, an
+  // experiment — however few there are)
+  const char* wd = getenv("YCRDT_DIRECT_WAVE");
+  const bool lane_direct = !(wd && wd[0] == '1');
   auto direct = [&](size_t len) {
     if (len > DIRECT_MAX_BYTES || force == 1) return false;
-    return force == 2 || nsmall >= DIRECT_MIN_COUNT || len <= DIRECT_TINY_BYTES;
+    return force == 2 || !lane_direct || nsmall >= DIRECT_MIN_COUNT || len <= DIRECT_TINY_BYTES;
   };
   // chunk size: a lane walks its chunk serially, so a batch with little chunk-path input (a doc
   // state and a few updates: the per-op path) takes short chunks; big ones the full SCHUNK
@@ -830,7 +835,7 @@ int run_decode(ycrdt_engine* e, ycrdt_batch* b, bool lazy, Decoded& D, bool gene
   if (dbg_dec && w.dbg) {  // experiments: why k_fastwalk left large updates to k_walk
     unsigned long long h[8];
     HIPCHK(hipMemcpy(h, w.dbg, sizeof(h), hipMemcpyDeviceToHost));
-    fprintf(stderr, "[ycrdt decode] fastwalk: done %llu nsec %llu unsynced %llu chunk0 %llu short %llu end %llu; k_spec exact parses %llu (%llu bytes)\n",
+    fprintf(stderr, "[ycrdt decode] fastwalk: done %llu nsec %llu unsynced %llu | wave: done %llu unsettled %llu other %llu | k_spec exact parses %llu (%llu bytes)\n",
             h[0], h[1], h[2], h[3], h[4], h[5], h[6], h[7]);
     HIPCHK(hipMemsetAsync(w.dbg, 0, 64, s));
   }

@@ -344,16 +344,18 @@ __device__ uint32_t sib_loop(A& a, uint32_t n, uint32_t* __restrict__ stack, uin
   uint32_t head = NONE, tail = NONE;
   for (uint32_t i0 = 0; i0 < n; ++i0) {
     if (a.done(i0) == 2) continue;
-    uint32_t sp = 0;
+    // the stack's top stays in a register (the stack is in global memory: reading back the
+    // element just pushed cost a memory round trip per member); it is read only after a pop
+    uint32_t sp = 0, c = i0;
     stack[sp++] = i0;
     a.set_done(i0, 1);
     while (sp > 0) {
-      const uint32_t c = stack[sp - 1];
       const uint32_t rp = a.rpos(c);
       if (rp != NONE && a.done(rp) != 2) {  // the right origin is a sibling: place it first
         if (a.done(rp) == 1 || sp >= n) { raise_err(err, ERR_DECODE); return NONE; }
         a.set_done(rp, 1);
         stack[sp++] = rp;
+        c = rp;
         continue;
       }
       bool out = false;
@@ -376,7 +378,7 @@ __device__ uint32_t sib_loop(A& a, uint32_t n, uint32_t* __restrict__ stack, uin
       if (left != NONE) a.set_next(left, c); else head = c;
       if (nx != NONE) a.set_prv(nx, c); else tail = c;
       a.set_done(c, 2);
-      --sp;
+      if (--sp > 0) c = stack[sp - 1];
     }
   }
   return head;
@@ -498,6 +500,55 @@ __device__ __forceinline__ uint32_t block_excl_scan256(uint32_t v, uint32_t* sh,
   return off + x - v;
 }
 
+// Groups of TSMALL+1 .. TWAVE members: one wavefront each, four per workgroup (C4's list heads:
+// the pushes of up to 64 replicas after one element, ~10^5 groups). Lane i stages member i in LDS
+// and finds its anchor with a shuffle scan (the lowest member with the same outside right origin);
+// lane 0 runs the loop. k_tsib_big's MID variant took them one workgroup (and a 2 048-slot hash
+// table to clear) each.
+constexpr uint32_t TWAVE = 64;
+__global__ __launch_bounds__(256) void k_tsib_wave(Work w, uint32_t nsegs, uint32_t nbig) {
+  __shared__ SibRec rec[4][TWAVE];
+  __shared__ uint8_t st[4][TWAVE];
+  const uint32_t wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const uint32_t bi = blockIdx.x * 4 + wv;
+  if (bi >= nbig) return;  // whole wavefronts only: no workgroup barrier below
+  const uint32_t g = w.t_big[bi];
+  const uint32_t a = w.t_gstart[g], n = w.t_gstart[g + 1] - a;
+  if (n > TWAVE) return;
+  const bool in = lane < n;
+  const uint32_t rp = in ? w.y_confl[a + lane] : NONE;
+  const uint32_t cid = in ? w.y_state[a + lane] : 0u;
+  const uint32_t r0 = in && rp == NONE ? w.y_before[a + lane] : NONE;
+  const uint32_t rk = !in || rp != NONE ? NONE : r0 == NONE ? HNONE : r0;  // (units < HNONE)
+  uint32_t anc = NONE;
+  for (uint32_t j = 0; j < n; ++j) {
+    const uint32_t rj = __shfl(rk, j);
+    if (anc == NONE && rk != NONE && rj == rk) anc = j;
+  }
+  if (in) {
+    w.t_trep[a + lane] = rp != NONE ? rp : (a + anc) | 0x80000000u;
+    rec[wv][lane] = SibRec{cid, (uint16_t)(rp == NONE ? S_NONE : rp - a),
+                           (uint16_t)(rp != NONE ? rp - a : anc | TOUT), S_NONE, S_NONE, S_NONE, S_NONE, S_NONE, 0};
+    st[wv][lane] = 0;
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  uint32_t head = NONE;
+  if (lane == 0) {
+    SibLds acc{rec[wv], st[wv]};
+    head = sib_loop(acc, n, w.y_stack + a, &w.ctr->err);
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  if (in) {
+    const uint32_t x = rec[wv][lane].nxt;
+    w.t_nsib[w.t_seg[a + lane]] = x == S_NONE ? NONE : w.t_seg[a + x];
+  }
+  if (lane == 0 && head != NONE) sib_publish(w, a, n, nsegs, head);
+}
+
 // CAP: LDS capacity in members, HS: anchor hash slots. MID = the variant for groups of at most
 // CAP members (a small LDS footprint, several workgroups per CU); the other takes the rest.
 constexpr uint32_t TMID = 1024;
@@ -505,7 +556,7 @@ template <uint32_t CAP, uint32_t HS, bool MID>
 __global__ __launch_bounds__(256) void k_tsib_big(Work w, uint32_t nsegs) {
   const uint32_t g = w.t_big[blockIdx.x];
   const uint32_t a = w.t_gstart[g], n = w.t_gstart[g + 1] - a;
-  if (MID ? n > CAP : (n <= TMID || n > CAP)) return;  // n > TLDS: the grid-wide huge-group path
+  if (MID ? (n > CAP || n <= TWAVE) : (n <= TMID || n > CAP)) return;  // n > TLDS: the grid-wide huge-group path
   __shared__ SibRec rec[CAP];
   __shared__ uint8_t st[CAP];
   __shared__ uint32_t hkey[HS], hval[HS];
@@ -917,6 +968,7 @@ uint32_t launch_yata_tree(const Work& w, uint32_t nsegs, hipStream_t s) {
   hipMemcpyAsync(&nbig, &w.ctr->tbig, sizeof(uint32_t), hipMemcpyDeviceToHost, s);
   hipStreamSynchronize(s);
   if (nbig) {
+    hipLaunchKernelGGL(k_tsib_wave, dim3((nbig + 3) / 4), dim3(256), 0, s, w, nsegs, nbig);
     hipLaunchKernelGGL((k_tsib_big<TMID, 2048, true>), dim3(nbig), dim3(256), 0, s, w, nsegs);
     hipLaunchKernelGGL((k_tsib_big<TLDS, THASH, false>), dim3(nbig), dim3(256), 0, s, w, nsegs);
     // the huge groups (> TLDS members): their (start, size) to the host, then the grid-wide path

@@ -1,21 +1,28 @@
-"""Both decode paths for small updates give the same bytes.
+"""Every decode path for small updates gives the same bytes.
 
-A batch with many small updates is parsed directly (one lane per update walks its structs,
-k_direct); few small updates and every large one take the chunk path (k_spec / k_walk).
-YCRDT_DECODE forces one path for every update of at most 16 KiB; both must
-match the Yjs fixtures and the oracle byte for byte, and report the same malformed input.
+Many small updates (<= 16 KiB) are parsed one lane per update (k_direct); few small updates and
+every large one take the chunk path (k_spec / k_sync / k_walk). YCRDT_DECODE=direct|chunks forces
+one path for the small ones, and "wave" (YCRDT_DIRECT_WAVE=1) the one-wavefront-per-update
+k_wdecode (chunk chains per lane settled inside the wavefront, an exact lane-0 walk otherwise).
+All must match the Yjs fixtures and the oracle byte for byte, and report the same malformed input.
 """
 import pytest
 
 crdt_amd = pytest.importorskip("crdt_amd")
 
 pytestmark = pytest.mark.gpu
-MODES = ("chunks", "direct")
+MODES = ("chunks", "direct", "wave")
+
+
+def _mode(monkeypatch, mode):
+    monkeypatch.setenv("YCRDT_DECODE", "direct" if mode == "wave" else mode)
+    if mode == "wave":
+        monkeypatch.setenv("YCRDT_DIRECT_WAVE", "1")
 
 
 @pytest.mark.parametrize("mode", MODES)
 def test_paths_golden(golden, mode, monkeypatch):
-    monkeypatch.setenv("YCRDT_DECODE", mode)
+    _mode(monkeypatch, mode)
     for setname in ("kat", "map", "array", "nested"):
         for c in golden[setname]:
             d = crdt_amd.Doc(client_id=0x7FFFFFF0)
@@ -32,7 +39,7 @@ def test_paths_generated_vs_oracle(mode, monkeypatch):
     from crdt_amd.workload import C2, gen_map
     from oracle.yref import Doc as ODoc
 
-    monkeypatch.setenv("YCRDT_DECODE", mode)
+    _mode(monkeypatch, mode)
     cfg = dict(C2)
     cfg.update(n_keys=2000, n_replicas=300, ops_per_replica=200)
     ups, _ = gen_map(**cfg)
@@ -49,7 +56,7 @@ def test_paths_array_vs_oracle(mode, monkeypatch):
     from tests.histories import array_history
     from oracle.yref import Doc as ODoc
 
-    monkeypatch.setenv("YCRDT_DECODE", mode)
+    _mode(monkeypatch, mode)
     states, wire = array_history(77, n_replicas=6, rounds=4, ops=10, with_map=True)
     ups = states + wire
     o = ODoc(0x7FFFFFF0)
@@ -63,7 +70,7 @@ def test_paths_array_vs_oracle(mode, monkeypatch):
 @pytest.mark.parametrize("mode", MODES)
 def test_paths_malformed(golden, mode, monkeypatch):
     """A truncated update in a batch fails the merge on both paths (Yjs throws on it)."""
-    monkeypatch.setenv("YCRDT_DECODE", mode)
+    _mode(monkeypatch, mode)
     good = [bytes.fromhex(u) for u in golden["map"][0]["updates"]]
     bad = good[0][: max(3, len(good[0]) // 2)]
     b = crdt_amd.Batch(good + [bad])

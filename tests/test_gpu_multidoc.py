@@ -92,6 +92,43 @@ def test_multidoc_packed_result_golden_and_large(golden):
     assert (bytes(blob1[:offs1[1]]), bytes(blob1[offs1[1]:offs1[2]])) == one.result()
 
 
+def test_staging_beside_merges_serving_loop():
+    """The serving loop of bench.py end_to_end: a second host thread stages batch k+1 (copy stream,
+    its own pinned area) while batch k merges and returns its packed result into a reused buffer;
+    every batch equals its sequential merge. Multi-wave staging (YCRDT_PIN_CHUNK) on a few MB."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    from crdt_amd.workload import gen_map
+
+    sets = [[gen_map(n_keys=3000, n_replicas=40, ops_per_replica=200, seed=900 + 7 * k + i)[0] for i in range(5)]
+            for k in range(4)]
+    eng = crdt_amd.Engine()
+    want = []
+    for docs in sets:
+        b = crdt_amd.Batch(docs=docs, engine=eng)
+        b.merge()
+        want.append(b.result_docs())
+        del b
+    os.environ["YCRDT_PIN_CHUNK"] = "65536"
+    try:
+        got, buf = [], None
+        with ThreadPoolExecutor(1) as stager:
+            nxt = stager.submit(lambda: crdt_amd.Batch(docs=sets[0], engine=eng))
+            for k in range(len(sets)):
+                b = nxt.result()
+                if k + 1 < len(sets):
+                    nxt = stager.submit(lambda d=sets[k + 1]: crdt_amd.Batch(docs=d, engine=eng))
+                b.merge()
+                blob, offs = b.result_docs_packed(out=buf)
+                got.append([(bytes(blob[offs[2 * d]:offs[2 * d + 1]]), bytes(blob[offs[2 * d + 1]:offs[2 * d + 2]]))
+                            for d in range(len(sets[k]))])
+                buf = blob.base if blob.base is not None else blob
+                del b
+    finally:
+        del os.environ["YCRDT_PIN_CHUNK"]
+    assert got == want
+
+
 # ---------------------------------------------------------------- fleet ingest (apply_updates_multi)
 def _interleaved(cases, rng):
     """(doc index, update) pairs of every case, interleaved across documents, per-doc order kept."""
