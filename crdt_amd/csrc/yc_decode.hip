@@ -1217,10 +1217,12 @@ __device__ __attribute__((noinline)) uint32_t wd_len(const uint32_t* ub, uint32_
   return chain_len(src, b, q, uend, nullptr, (const uint8_t*)ub, ustart);
 }
 constexpr uint32_t WD_MAX = 16384, WD_WORDS = WD_MAX / 64, WD_ROUNDS = 64;
+constexpr uint32_t WD_LANE_MIN = 1024;  // small updates from which k_direct (a lane each) takes over
 __global__ __launch_bounds__(64) void k_wdecode(Work w) {
   __shared__ __attribute__((aligned(16))) uint32_t ub[(WD_MAX + 64) / 4];
   __shared__ uint64_t bits[WD_WORDS + 1];
   __shared__ uint64_t walkbuf[64][WD_WORDS / 64];  // a lane's walked positions, before it commits them
+  __shared__ uint32_t infoset[8];                   // info bytes on lane 0's exact chain
   const uint32_t lane = threadIdx.x;
   if (blockIdx.x >= w.nsmall) return;
   const uint32_t u = w.ulist[w.nbig + blockIdx.x];
@@ -1260,18 +1262,36 @@ __global__ __launch_bounds__(64) void k_wdecode(Work w) {
       const uint32_t cs = ustart + lane * CW, ce = min(cs + CW, uend);
       const bool live = ce > q1 && cs < uend;
       uint32_t x = NONE;  // this lane's chain exit
-      if (live) {
+      // lane 0's chain is exact (from the first struct): the info bytes it meets are the stream's
+      // struct kinds; the other lanes start their chains at a run of three chain steps on such
+      // bytes (a hint the settling verifies) — a single first-struct byte missed streams whose
+      // first struct is of a rarer kind, and their chains locked out of phase
+      if (lane == 0) {
+        for (uint32_t k = 0; k < 8; ++k) infoset[k] = 0;
+        if (live) {
+          uint32_t q = q1;
+          while (q < ce) {
+            setbit(q);
+            const uint32_t c = src.u8(q);
+            infoset[c >> 5] |= 1u << (c & 31);
+            const uint32_t d = wd_len(ub, ustart, nq * 16, b, q, uend);
+            q += d ? d : 1u;
+          }
+          x = q;
+        }
+      }
+      __syncthreads();
+      auto kind = [&](uint32_t h) { const uint32_t c = src.u8(h); return (infoset[c >> 5] >> (c & 31)) & 1u; };
+      if (live && lane > 0) {
         uint32_t q = max(cs, q1);
         if (cs > q1) {
-          // a hinted start (as k_spec): the first position of the chunk's first 96 bytes where
-          // three consecutive chain steps begin with the info byte of the first struct
-          const uint32_t hint = src.u8(q1), lim = min(cs + 96u, ce);
+          const uint32_t lim = min(cs + 96u, ce);
           for (uint32_t h = cs; h < lim; ++h) {
-            if (src.u8(h) != hint) continue;
+            if (!kind(h)) continue;
             const uint32_t d1 = wd_len(ub, ustart, nq * 16, b, h, uend);
-            if (!d1 || h + d1 >= uend || src.u8(h + d1) != hint) continue;
+            if (!d1 || h + d1 >= uend || !kind(h + d1)) continue;
             const uint32_t d2 = wd_len(ub, ustart, nq * 16, b, h + d1, uend);
-            if (!d2 || h + d1 + d2 >= uend || src.u8(h + d1 + d2) != hint) continue;
+            if (!d2 || h + d1 + d2 >= uend || !kind(h + d1 + d2)) continue;
             q = h;
             break;
           }
@@ -1341,7 +1361,7 @@ __global__ __launch_bounds__(64) void k_wdecode(Work w) {
         }
         const bool changed = __ballot(nx != x) != 0;
         x = nx;
-        if (!changed && !__ballot(!okc)) { settled = true; break; }
+        if (!changed && !__ballot(!okc)) { settled = true; if (lane == 0 && w.dbg) atomicAdd(&w.dbg[6], (unsigned long long)r + 1); break; }
       }
       const bool jumped = false;
       __syncthreads();
@@ -1483,8 +1503,10 @@ void launch_chunks(const Work& w, hipStream_t s) {
   }
 }
 void launch_direct(const Work& w, hipStream_t s) {
-  const char* wd = getenv("YCRDT_DIRECT_WAVE");  // read per merge (tests switch it)
-  const bool lane_direct = !(wd && wd[0] == '1');
+  // one lane per update when there are enough updates to fill wavefronts, else one wavefront per
+  // update; YCRDT_DIRECT_WAVE=1 / 0 forces one (read per merge: tests switch it)
+  const char* wd = getenv("YCRDT_DIRECT_WAVE");
+  const bool lane_direct = wd && (wd[0] == '1' || wd[0] == '0') ? wd[0] == '0' : w.nsmall >= WD_LANE_MIN;
   if (w.nsmall && !lane_direct) hipLaunchKernelGGL(k_wdecode, dim3(w.nsmall), dim3(64), 0, s, w);
   else if (w.nsmall) hipLaunchKernelGGL(k_direct, dim3((w.nsmall + DL - 1) / DL), dim3(DL), 0, s, w);
 }

@@ -328,14 +328,14 @@ void layout(ycrdt_batch* b, const std::vector<Src>& src, std::vector<uint32_t>& 
                     : mode && !strcmp(mode, "direct") ? 2 : 0;
   size_t nsmall = 0;
   for (const Src& x : src) nsmall += x.len <= DIRECT_MAX_BYTES;
-  // (with the lane-per-update k_direct, small updates take the direct path only when there are
-  // enough to fill wavefronts; with k_wdecode — one wavefront each, YCRDT_DIRECT_WAVE=1, an
-  // experiment — however few there are)
+  // small updates are parsed directly however few there are: one lane each (k_direct) when they
+  // fill wavefronts, else one wavefront each (k_wdecode); YCRDT_DIRECT_WAVE=0 keeps the lane
+  // kernel, and then few small updates take the chunk path as before
   const char* wd = getenv("YCRDT_DIRECT_WAVE");
-  const bool lane_direct = !(wd && wd[0] == '1');
+  const bool lane_only = wd && wd[0] == '0';
   auto direct = [&](size_t len) {
     if (len > DIRECT_MAX_BYTES || force == 1) return false;
-    return force == 2 || !lane_direct || nsmall >= DIRECT_MIN_COUNT || len <= DIRECT_TINY_BYTES;
+    return force == 2 || !lane_only || nsmall >= DIRECT_MIN_COUNT || len <= DIRECT_TINY_BYTES;
   };
   // chunk size: a lane walks its chunk serially, so a batch with little chunk-path input (a doc
   // state and a few updates: the per-op path) takes short chunks; big ones the full SCHUNK

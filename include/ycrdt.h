@@ -15,6 +15,10 @@
  *    descending); see DESIGN.md §Compat for the 13.5.16 insertion-order difference.
  *  - There is no CPU fallback: without a usable HIP device every compute entry point fails
  *    with YCRDT_E_DEVICE.
+ *  - Threads: calls on one engine are serialised by the caller, with one exception — a batch may
+ *    be created (ycrdt_batch_stage*: host packing + H2D on the engine's copy stream) by one thread
+ *    while another thread merges a different batch or reads its result (the serving loop:
+ *    batch k+1 staged beside batch k's merge).
  */
 #ifndef YCRDT_H
 #define YCRDT_H

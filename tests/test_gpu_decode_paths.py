@@ -1,9 +1,9 @@
 """Every decode path for small updates gives the same bytes.
 
-Many small updates (<= 16 KiB) are parsed one lane per update (k_direct); few small updates and
-every large one take the chunk path (k_spec / k_sync / k_walk). YCRDT_DECODE=direct|chunks forces
-one path for the small ones, and "wave" (YCRDT_DIRECT_WAVE=1) the one-wavefront-per-update
-k_wdecode (chunk chains per lane settled inside the wavefront, an exact lane-0 walk otherwise).
+Small updates (<= 16 KiB) are parsed one lane per update (k_direct) when there are many, one
+wavefront per update (k_wdecode: chunk chains per lane settled inside the wavefront, an exact
+lane-0 walk otherwise) when there are few; large ones take the chunk path (k_spec / k_sync /
+k_walk). The modes force one: "direct" = k_direct, "wave" = k_wdecode, "chunks" = the chunk path.
 All must match the Yjs fixtures and the oracle byte for byte, and report the same malformed input.
 """
 import pytest
@@ -16,8 +16,8 @@ MODES = ("chunks", "direct", "wave")
 
 def _mode(monkeypatch, mode):
     monkeypatch.setenv("YCRDT_DECODE", "direct" if mode == "wave" else mode)
-    if mode == "wave":
-        monkeypatch.setenv("YCRDT_DIRECT_WAVE", "1")
+    if mode in ("wave", "direct"):
+        monkeypatch.setenv("YCRDT_DIRECT_WAVE", "1" if mode == "wave" else "0")
 
 
 @pytest.mark.parametrize("mode", MODES)
