@@ -1209,15 +1209,16 @@ __global__ __launch_bounds__(64) void k_fastwalk(Work w) {
 // longer leave the GPU idle, and many pack 64 x more parallel work. Several sections, a chain that
 // does not settle in WD_ROUNDS, or fewer chain positions than structs: lane 0 walks the update
 // exactly (as k_direct, from LDS), which also reports malformed input.
-// k_wdecode's struct step out of line: inlined at each of its call sites, the sizer made the kernel
-// ~150 KB of code, far past the instruction cache (every step then waited on instruction fetch)
-__device__ __attribute__((noinline)) uint32_t wd_len(const uint32_t* ub, uint32_t ustart, uint32_t wlen,
-                                                     const uint8_t* __restrict__ b, uint32_t q, uint32_t uend) {
+// k_wdecode's struct step (inline: an out-of-line step, or only its slow part out of line, was
+// slower — the garbage the chunk chains parse takes the slow part often)
+__device__ __forceinline__ uint32_t wd_len(const uint32_t* ub, uint32_t ustart, uint32_t wlen,
+                                           const uint8_t* __restrict__ b, uint32_t q, uint32_t uend) {
   const LdsSrc src{b, ub, ustart, wlen};
   return chain_len(src, b, q, uend, nullptr, (const uint8_t*)ub, ustart);
 }
 constexpr uint32_t WD_MAX = 16384, WD_WORDS = WD_MAX / 64, WD_ROUNDS = 64;
 constexpr uint32_t WD_LANE_MIN = 1024;  // small updates from which k_direct (a lane each) takes over
+constexpr uint32_t WD_HINT = 5;
 __global__ __launch_bounds__(64) void k_wdecode(Work w) {
   __shared__ __attribute__((aligned(16))) uint32_t ub[(WD_MAX + 64) / 4];
   __shared__ uint64_t bits[WD_WORDS + 1];
@@ -1288,10 +1289,13 @@ __global__ __launch_bounds__(64) void k_wdecode(Work w) {
           const uint32_t lim = min(cs + 96u, ce);
           for (uint32_t h = cs; h < lim; ++h) {
             if (!kind(h)) continue;
-            const uint32_t d1 = wd_len(ub, ustart, nq * 16, b, h, uend);
-            if (!d1 || h + d1 >= uend || !kind(h + d1)) continue;
-            const uint32_t d2 = wd_len(ub, ustart, nq * 16, b, h + d1, uend);
-            if (!d2 || h + d1 + d2 >= uend || !kind(h + d1 + d2)) continue;
+            uint32_t t = h, k = 0;  // WD_HINT consecutive chain steps on struct-kind bytes
+            for (; k < WD_HINT; ++k) {
+              const uint32_t d = wd_len(ub, ustart, nq * 16, b, t, uend);
+              if (!d || t + d >= uend || !kind(t + d)) break;
+              t += d;
+            }
+            if (k < WD_HINT && t + 1 < uend) continue;
             q = h;
             break;
           }
@@ -1316,14 +1320,30 @@ __global__ __launch_bounds__(64) void k_wdecode(Work w) {
       uint32_t sent = NONE;
       uint64_t* wk = walkbuf[lane];
       const uint32_t w0 = (cs - ustart) >> 6, wend = live ? (ce - ustart + 63) >> 6 : w0;
+      bool beyond = false;  // this chunk lies past the section's last struct: nothing to settle
       for (uint32_t r = 0; r < WD_ROUNDS; ++r) {
         const uint32_t E = __shfl_up(x, 1);
+        {
+          // lanes whose predecessors are all consistent and already hold n chain positions are past
+          // the last struct (their chunks hold the delete set): they leave the settling, which
+          // otherwise cascaded through the delete set's garbage chains a chunk per round
+          uint32_t cnt = 0;
+          for (uint32_t k = w0; k < wend; ++k) cnt += (uint32_t)__popcll(bits[k]);
+          uint32_t inc = cnt;
+          for (uint32_t off = 1; off < 64; off <<= 1) {
+            const uint32_t y = __shfl_up(inc, off);
+            if (lane >= off) inc += y;
+          }
+          const uint64_t b0 = __ballot(!okc);
+          const uint32_t fb = b0 ? (uint32_t)__ffsll((long long)b0) - 1 : 64u;
+          if (lane > 0 && lane <= fb && inc - cnt >= n) { beyond = true; okc = true; }
+        }
         const uint64_t bad = __ballot(!okc);
         const uint32_t first_bad = bad ? (uint32_t)__ffsll((long long)bad) - 1 : 64u;
         uint32_t nx = x;
         bool walked = false, met = false;
         uint32_t q = E;
-        if (!okc || (live && lane > 0 && cs >= q1 && E != sent)) {
+        if (!beyond && (!okc || (live && lane > 0 && cs >= q1 && E != sent))) {
           if (E != sent || lane == first_bad) {
             sent = E;
             walked = true;
@@ -1359,7 +1379,7 @@ __global__ __launch_bounds__(64) void k_wdecode(Work w) {
             okc = false;
           }
         }
-        const bool changed = __ballot(nx != x) != 0;
+        const bool changed = __ballot(nx != x && !beyond) != 0;
         x = nx;
         if (!changed && !__ballot(!okc)) { settled = true; if (lane == 0 && w.dbg) atomicAdd(&w.dbg[6], (unsigned long long)r + 1); break; }
       }
