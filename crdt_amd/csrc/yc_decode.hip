@@ -1334,7 +1334,9 @@ __global__ __launch_bounds__(64) void k_wdecode(Work w) {
             const uint32_t y = __shfl_up(inc, off);
             if (lane >= off) inc += y;
           }
-          const uint64_t b0 = __ballot(!okc);
+          // (a lane whose entry changed since its walk is not consistent yet, whatever okc says)
+          const bool stale = !beyond && live && lane > 0 && cs >= q1 && E != sent;
+          const uint64_t b0 = __ballot(!okc || stale);
           const uint32_t fb = b0 ? (uint32_t)__ffsll((long long)b0) - 1 : 64u;
           if (lane > 0 && lane <= fb && inc - cnt >= n) { beyond = true; okc = true; }
         }
