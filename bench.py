@@ -350,20 +350,33 @@ def billion_leg(eng, cfg, gen_map, n_docs, reps=3):
 
     import crdt_amd
 
+    def log(msg):  # progress on stderr: a multi-minute leg must not look hung
+        print(f"[billion {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
+
+    log(f"engine holds {eng.device_bytes() / 2**30:.1f} GiB after the headline; trimming")
+    eng.trim()
     seeds = [cfg["seed"] + 7_000_003 + i * 1_009 for i in range(n_docs)]
     g0 = time.perf_counter()
+    docs = []
     with ThreadPoolExecutor(16) as ex:
-        docs = list(ex.map(lambda sd: gen_map(**dict(cfg, seed=sd))[0], seeds))
+        for i, d in enumerate(ex.map(lambda sd: gen_map(**dict(cfg, seed=sd))[0], seeds)):
+            docs.append(d)
+            if i % 100 == 99:
+                log(f"generated {i + 1}/{n_docs} documents")
     gen_s = time.perf_counter() - g0
     in_bytes = sum(len(u) for d in docs for u in d)
+    log(f"{in_bytes / 1e9:.2f} GB of updates in {gen_s:.1f} s; staging")
     s0 = time.perf_counter()
     b = crdt_amd.Batch(docs=docs, engine=eng)
     stage_s = time.perf_counter() - s0
+    log(f"staged in {stage_s:.1f} s; first merge")
     st = b.merge()  # first merge: workspace allocation
+    log(f"first merge: {st.items} items, device {st.device_ms:.1f} ms, HBM {eng.device_bytes() / 2**30:.1f} GiB")
     t0 = time.perf_counter()
     for _ in range(reps):
         st = b.merge()
     ms = (time.perf_counter() - t0) * 1e3 / reps
+    log(f"{reps} merges: {ms:.1f} ms each")
     hbm = eng.device_bytes()
     outs = [u for u, _ in b.result_docs()]
     out_bytes = sum(map(len, outs))

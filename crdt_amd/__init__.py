@@ -76,7 +76,7 @@ def library_path():
 
 EXPORTS = (
     "ycrdt_engine_create", "ycrdt_engine_destroy", "ycrdt_engine_set_profiling", "ycrdt_engine_phase_times",
-    "ycrdt_engine_device_bytes",
+    "ycrdt_engine_device_bytes", "ycrdt_engine_trim",
     "ycrdt_doc_create", "ycrdt_doc_destroy", "ycrdt_apply_update", "ycrdt_apply_updates",
     "ycrdt_encode_state_as_update", "ycrdt_encode_state_vector", "ycrdt_doc_last_stats",
     "ycrdt_batch_stage", "ycrdt_batch_merge", "ycrdt_batch_result", "ycrdt_batch_destroy",
@@ -117,6 +117,7 @@ def lib():
     L.ycrdt_engine_set_profiling.argtypes = [vp, i32]
     L.ycrdt_engine_phase_times.argtypes = [vp, P(ctypes.c_char_p), P(ctypes.c_double), i32]
     L.ycrdt_engine_device_bytes.argtypes = [vp, P(ctypes.c_uint64)]
+    L.ycrdt_engine_trim.argtypes = [vp]
     L.ycrdt_doc_create.argtypes = [vp, u32, P(vp)]
     L.ycrdt_doc_destroy.argtypes = [vp]
     L.ycrdt_apply_update.argtypes = [vp, _Buf]
@@ -238,6 +239,10 @@ class Engine:
         v = ctypes.c_uint64()
         _check(lib().ycrdt_engine_device_bytes(self._h, ctypes.byref(v)))
         return v.value
+
+    def trim(self):
+        """Releases the merge workspace (ycrdt_engine_trim): HBM back after a giant merge."""
+        _check(lib().ycrdt_engine_trim(self._h))
 
     def phase_times(self):
         names = (ctypes.c_char_p * 64)()

@@ -100,14 +100,32 @@ bool grow(DevBuf& b, size_t bytes) {
   b.cap = c;
   return true;
 }
-// "hipMalloc failed (what)" with the request and the device's free / total memory
+thread_local const std::vector<DevBuf>* g_bufs = nullptr;  // the workspace of the merge in progress (oom reports)
+// "hipMalloc failed (what)" with the request, the device's free / total memory and the largest
+// workspace buffers held at that point (buffer index: the Buf enum below)
 std::string oom(const char* what) {
   size_t fr = 0, tot = 0;
   (void)hipMemGetInfo(&fr, &tot);
   char buf[256];
   snprintf(buf, sizeof buf, "hipMalloc failed (%s): request %.2f GB, device free %.2f of %.2f GB", what,
            g_failed_alloc / 1e9, fr / 1e9, tot / 1e9);
-  return buf;
+  std::string r = buf;
+  if (g_bufs) {
+    std::vector<std::pair<size_t, size_t>> big;
+    size_t sum = 0;
+    for (size_t i = 0; i < g_bufs->size(); ++i) {
+      sum += (*g_bufs)[i].cap;
+      big.emplace_back((*g_bufs)[i].cap, i);
+    }
+    std::sort(big.rbegin(), big.rend());
+    snprintf(buf, sizeof buf, "; workspace %.2f GB, largest (buffer:GB)", sum / 1e9);
+    r += buf;
+    for (size_t k = 0; k < big.size() && k < 8; ++k) {
+      snprintf(buf, sizeof buf, " %zu:%.2f", big[k].second, big[k].first / 1e9);
+      r += buf;
+    }
+  }
+  return r;
 }
 
 template <class T>
@@ -710,6 +728,7 @@ int split_decode_exchange(ycrdt_engine* e, ycrdt_batch* b, const ShardSpec* sh) 
 int run_decode(ycrdt_engine* e, ycrdt_batch* b, bool lazy, Decoded& D, bool generous = false, const ShardSpec* sh = nullptr) {
   Work& w = e->w;
   auto& V = e->bufs;
+  g_bufs = &V;
   bool ok = true;
   hipStream_t s = e->stream;
   e->marks.clear();
@@ -948,6 +967,7 @@ int run_merge(ycrdt_engine* e, ycrdt_batch* b, const std::unordered_map<uint32_t
               const ClockMap* caps = nullptr, const std::vector<uint32_t>* order = nullptr, const ShardSpec* sh = nullptr) {
   Work& w = e->w;
   auto& V = e->bufs;
+  g_bufs = &V;
   bool ok = true;
   hipStream_t s = e->stream;
   e->ws_owner = nullptr;
@@ -1060,6 +1080,10 @@ int run_merge(ycrdt_engine* e, ycrdt_batch* b, const std::unordered_map<uint32_t
   // every list is rooted by an explicit-parent item (a key per root struct at most): the table is
   // sized from those, not from every segment
   w.cap_keys = next_pow2(std::max<uint64_t>(2ull * std::min<uint64_t>(D.nroots, nsegs), 64));
+  {  // test hook: keep only the low YCRDT_KEY_HASH_BITS bits of every list hash (collisions certain)
+    const int kb = getenv("YCRDT_KEY_HASH_BITS") ? atoi(getenv("YCRDT_KEY_HASH_BITS")) : 64;
+    w.key_mask = kb >= 1 && kb < 64 ? (1ull << kb) - 1 : ~0ull;
+  }
   w.k_hash = take<uint64_t>(V, B_KHASH, w.cap_keys, ok);
   w.k_rootmax = take<uint32_t>(V, B_KROOT, w.cap_keys, ok);
   w.k_winner = take<uint32_t>(V, B_KWIN, w.cap_keys, ok);
@@ -1218,6 +1242,7 @@ int run_view(ycrdt_engine* e, ycrdt_batch* b, HostView& hv) {
   if (b->nwin > 1) return fail(YCRDT_E_CAPACITY, "a view of a batch over 4 GiB");
   Work& w = e->w;
   auto& V = e->bufs;
+  g_bufs = &V;
   bool ok = true;
   hipStream_t s = e->stream;
   const uint32_t nsegs = e->nsegs, nlists = e->nlists;
@@ -1351,6 +1376,7 @@ int run_lazy(ycrdt_engine* e, ycrdt_batch* b, bool merge, const std::vector<std:
   w.ds_first = e->compat == 135 ? 1u : 0u;
   e->ws_owner = nullptr;
   auto& V = e->bufs;
+  g_bufs = &V;
   bool ok = true;
   hipStream_t s = e->stream;
   Decoded D;
@@ -1485,6 +1511,7 @@ int pack_docs(ycrdt_engine* e, ycrdt_batch* b) {
   if (b->packed) return YCRDT_OK;
   Work& w = e->w;
   auto& V = e->bufs;
+  g_bufs = &V;
   bool ok = true;
   hipStream_t s = e->stream;
   const uint32_t nd = b->ndocs;
@@ -1717,6 +1744,19 @@ int ycrdt_engine_device_bytes(ycrdt_engine* e, uint64_t* bytes) {
   return YCRDT_OK;
 }
 
+int ycrdt_engine_trim(ycrdt_engine* e) {
+  if (!e) return fail(YCRDT_E_ARG, "null arg");
+  hipSetDevice(e->device);
+  HIPCHK(hipStreamSynchronize(e->stream));
+  HIPCHK(hipStreamSynchronize(e->side));
+  for (auto& b : e->bufs)
+    if (b.p && !b.arena) { hipFree(b.p); b = DevBuf{}; }
+  e->ws_owner = nullptr;  // no doc's merge results are held any more: its next read merges again
+  e->nsegs = 0;
+  e->nlists = 0;
+  return YCRDT_OK;
+}
+
 int ycrdt_doc_create(ycrdt_engine* e, uint32_t client_id, ycrdt_doc** out) {
   if (!e || !out) return fail(YCRDT_E_ARG, "null arg");
   auto* d = new ycrdt_doc();
@@ -1874,6 +1914,7 @@ int flush_multi(ycrdt_engine* e, const std::vector<ycrdt_doc*>& docs) {
   // per-document ranges of the encode, then every document's state assembled on the device
   Work& w = e->w;
   auto& V = e->bufs;
+  g_bufs = &V;
   bool ok = true;
   unsigned long long* rng = take<unsigned long long>(V, B_DOCRNG, 9 * (size_t)nd + 9, ok);
   if (!ok) return fail(YCRDT_E_DEVICE, oom("document ranges"));
@@ -2097,6 +2138,7 @@ int ycrdt_docs_states_packed(ycrdt_engine* e, ycrdt_doc* const* docs, size_t n, 
   }
   if (dev) {
     auto& V = e->bufs;
+  g_bufs = &V;
     bool ok = true;
     uint8_t* buf = take<uint8_t>(V, B_PACK, dev + 16, ok);
     Piece* dpc = ok ? take<Piece>(V, B_PACKPC, pc.size() + 1, ok) : nullptr;

@@ -227,11 +227,46 @@ __device__ __forceinline__ uint64_t fnv_bytes(uint64_t h, const uint8_t* __restr
   for (uint32_t i = 0; i < n; ++i) { h ^= p[i]; h *= 1099511628211ull; }
   return h;
 }
-__device__ __forceinline__ uint32_t key_insert(uint64_t* __restrict__ tab, uint32_t cap, uint64_t h) {
+__device__ __forceinline__ bool bytes_eq(const uint8_t* __restrict__ a, const uint8_t* __restrict__ b, uint32_t n) {
+  for (uint32_t i = 0; i < n; ++i)
+    if (a[i] != b[i]) return false;
+  return true;
+}
+// Do root structs a and b name the same list? A list is (document, root type name | parent item,
+// parentSub) (Item.integrate's parent / parentSub after Item.getMissing, Y@76507; typeMapSet keys,
+// crdt.js:434). Names and parentSubs are compared as whole varStrings (length prefix included).
+__device__ __attribute__((noinline)) bool same_list(const Work& w, uint32_t a, uint32_t b) {
+  if (a == b) return true;
+  const uint32_t pk = w.s_pk[a];
+  if (pk != w.s_pk[b]) return false;
+  if (pk == 1) {
+    const uint32_t n = w.s_pb[a];
+    if (n != w.s_pb[b]) return false;
+    if (w.udoc && w.cl_doc[w.s_cidx[a]] != w.cl_doc[w.s_cidx[b]]) return false;
+    if (!bytes_eq(struct_bytes(w, a) + w.s_pa[a], struct_bytes(w, b) + w.s_pa[b], n)) return false;
+  } else if (w.s_pa[a] != w.s_pa[b] || w.s_pb[a] != w.s_pb[b]) {  // parent item id (client index, clock)
+    return false;
+  }
+  const uint32_t pa = w.s_psub[a], pb = w.s_psub[b];
+  if ((pa == NONE) != (pb == NONE)) return false;
+  if (pa == NONE) return true;
+  const uint32_t n = w.s_psublen[a];
+  return n == w.s_psublen[b] && bytes_eq(struct_bytes(w, a) + pa, struct_bytes(w, b) + pb, n);
+}
+// Open-addressing insert of the list rooted by struct `own` with hash h. A slot's word is
+// (claiming struct + 1) << 32 | low half of h, written by one CAS, so whoever meets a taken slot
+// with the same low hash reads the claimer from the same word and compares the two lists' names
+// exactly (same_list): equal hashes of different lists keep probing (no hash-only identity).
+// Every struct of one list walks the same probe sequence, so the list gets exactly one slot.
+__device__ __forceinline__ uint32_t key_insert(const Work& w, uint64_t h, uint32_t own) {
+  uint64_t* __restrict__ tab = w.k_hash;
+  const uint32_t cap = w.cap_keys;
+  const uint64_t mine = ((uint64_t)(own + 1) << 32) | (uint32_t)h;
   uint32_t slot = (uint32_t)(h ^ (h >> 29)) & (cap - 1);
   for (uint32_t probe = 0; probe < cap; ++probe) {
-    const unsigned long long old = atomicCAS((unsigned long long*)&tab[slot], 0ull, (unsigned long long)h);
-    if (old == 0ull || old == h) return slot;
+    const unsigned long long old = atomicCAS((unsigned long long*)&tab[slot], 0ull, (unsigned long long)mine);
+    if (old == 0ull || old == mine) return slot;
+    if ((uint32_t)old == (uint32_t)h && same_list(w, (uint32_t)(old >> 32) - 1u, own)) return slot;
     slot = (slot + 1) & (cap - 1);
   }
   return NONE;
@@ -297,8 +332,8 @@ __global__ __launch_bounds__(256) void k_seg_props(Work w, uint32_t nsegs) {
     if (!gc) {
       const uint32_t ps = w.s_psub[own];
       if (ps != NONE) { h = fnv_u32(h, 0x5Au); h = fnv_bytes(h, struct_bytes(w, own) + ps, w.s_psublen[own]); }
-      if (h == 0) h = 1;
-      key = key_insert(w.k_hash, w.cap_keys, h);
+      h &= w.key_mask;  // tests: YCRDT_KEY_HASH_BITS truncates the hash so distinct lists collide
+      key = key_insert(w, h, own);
       if (key == NONE) raise_err(&w.ctr->err, ERR_CAPACITY);
       else {
         sf |= SEG_ROOT;
@@ -572,7 +607,7 @@ __global__ void k_key_shard(Work w, uint32_t nshards, uint32_t* __restrict__ key
     x = pk;
   }
   if (!top) raise_err(&w.ctr->err, ERR_DECODE);
-  key_shard[k] = shard_of_hash(w.k_hash[x], nshards);
+  key_shard[k] = shard_of_hash((uint32_t)w.k_hash[x], nshards);  // the list's low hash half (slot words, key_insert)
 }
 __global__ void k_seg_shard(Work w, uint32_t nsegs, const uint32_t* __restrict__ key_shard, uint8_t* __restrict__ owner) {
   const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;

@@ -179,7 +179,9 @@ struct Work {
   uint32_t* g_tmp = nullptr;       // scratch per segment
   uint32_t* g_tmp2 = nullptr;
   // ---- keys (hash table)
-  uint64_t* k_hash = nullptr;      // [cap_keys] open addressing table of 64-bit key hashes (0 = empty)
+  uint64_t* k_hash = nullptr;      // [cap_keys] open addressing table: (claiming root struct + 1) << 32 | low
+                                   // half of the list hash (0 = empty); lists compared by name (key_insert)
+  uint64_t key_mask = ~0ull;       // list-hash bits kept (YCRDT_KEY_HASH_BITS: tests force collisions)
   uint32_t* k_rootmax = nullptr;   // [cap_keys] seg + 1 of the max-client root, 0 = none
   uint32_t* k_winner = nullptr;    // [cap_keys] winning (rightmost) segment
   uint32_t* k_parent = nullptr;    // [cap_keys] parent type item unit (NONE = root type)
