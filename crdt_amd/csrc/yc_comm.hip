@@ -335,12 +335,27 @@ int comm_fleet_sv_allreduce_max(ycrdt_comm* c, const uint32_t* docs, const ycrdt
   if (K && (hipMemcpyAsync(hk.data(), space.p, 8 * K, hipMemcpyDeviceToHost, s) != hipSuccess ||
             hipMemcpyAsync(hc.data(), dense.p, 4 * K, hipMemcpyDeviceToHost, s) != hipSuccess)) { err = "copy"; return -1; }
   if (hipStreamSynchronize(s) != hipSuccess) { err = "copy"; return -1; }
+  // ---- the documents any rank holds (a document whose state vector is empty on every rank has
+  // no key above, yet it is held: its result is the empty state vector, encodeStateVector = [0])
+  std::vector<uint32_t> held(docs, docs + n);
+  std::sort(held.begin(), held.end());
+  held.erase(std::unique(held.begin(), held.end()), held.end());
+  std::vector<std::vector<uint8_t>> hparts;
+  if (allgather_bytes(c, (const uint8_t*)held.data(), 4 * held.size(), s, hparts, err)) return -1;
+  std::vector<uint32_t> all_docs;
+  for (const auto& p : hparts) {
+    const size_t k0 = all_docs.size();
+    all_docs.resize(k0 + p.size() / 4);
+    if (!p.empty()) memcpy(all_docs.data() + k0, p.data(), p.size() / 4 * 4);
+  }
+  std::sort(all_docs.begin(), all_docs.end());
+  all_docs.erase(std::unique(all_docs.begin(), all_docs.end()), all_docs.end());
   // ---- per document: writeStateVector, clients descending (the keys of one document are a run)
   out_docs.clear();
   out_offs.clear();
   out.clear();
-  for (uint64_t a = 0; a < K;) {
-    const uint32_t d = (uint32_t)(hk[a] >> 32);
+  uint64_t a = 0;
+  for (const uint32_t d : all_docs) {
     uint64_t z = a;
     while (z < K && (uint32_t)(hk[z] >> 32) == d) ++z;
     out_docs.push_back(d);
@@ -349,6 +364,7 @@ int comm_fleet_sv_allreduce_max(ycrdt_comm* c, const uint32_t* docs, const ycrdt
     for (uint64_t i = z; i-- > a;) { put_vu(out, (uint32_t)hk[i]); put_vu(out, hc[i]); }
     a = z;
   }
+  if (a != K) { err = "fleet exchange: a key of a document no rank holds"; return -1; }
   out_offs.push_back(out.size());
   return 0;
 }

@@ -704,9 +704,13 @@ int split_decode_exchange(ycrdt_engine* e, ycrdt_batch* b, const ShardSpec* sh) 
       yc::comm_allreduce_u32(sh->comm, w.dsstart, nu + 1, true, s, err) ||
       yc::comm_allreduce_u32(sh->comm, &w.ctr->err, 1, true, s, err))
     return fail(YCRDT_E_DEVICE, err);
-  uint32_t nsec = 0;
-  HIPCHK(hipMemcpyAsync(&nsec, &w.ctr->nsections, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+  uint32_t cw[2] = {0, 0};  // the reduced error word, this rank's section count
+  HIPCHK(hipMemcpyAsync(&cw[0], &w.ctr->err, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+  HIPCHK(hipMemcpyAsync(&cw[1], &w.ctr->nsections, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
   HIPCHK(hipStreamSynchronize(s));
+  // the walkers bump the count before their capacity test: past the estimate only the first
+  // cap_sections records exist (the error word then says ERR_CAPACITY on every rank)
+  const uint32_t nsec = std::min(cw[1], w.cap_sections);
   std::vector<Section> mine(nsec);
   if (nsec) HIPCHK(hipMemcpy(mine.data(), w.sections, sizeof(Section) * nsec, hipMemcpyDeviceToHost));
   std::vector<std::vector<uint8_t>> parts;
@@ -714,12 +718,15 @@ int split_decode_exchange(ycrdt_engine* e, ycrdt_batch* b, const ShardSpec* sh) 
     return fail(YCRDT_E_DEVICE, err);
   std::vector<uint8_t> all;
   for (const auto& p : parts) all.insert(all.end(), p.begin(), p.end());
-  const uint32_t total = (uint32_t)(all.size() / sizeof(Section));
-  if (total > w.cap_sections) return fail(YCRDT_E_CAPACITY, "decode split: sections past the estimate");
+  const uint64_t total = all.size() / sizeof(Section);
+  sh->inside = false;  // the exchange is complete on every rank
+  // a capacity overflow on any rank (reduced error word) or of the gathered table: the same on
+  // every rank, so all of them re-run the decode with the worst-case bound (run_decode)
+  if (cw[0] == ERR_CAPACITY || total > w.cap_sections) return fail(YCRDT_E_CAPACITY, "decode split: sections past the estimate");
   if (total) HIPCHK(hipMemcpyAsync(w.sections, all.data(), all.size(), hipMemcpyHostToDevice, s));
-  HIPCHK(hipMemcpyAsync(&w.ctr->nsections, &total, sizeof(uint32_t), hipMemcpyHostToDevice, s));
+  const uint32_t t32 = (uint32_t)total;
+  HIPCHK(hipMemcpyAsync(&w.ctr->nsections, &t32, sizeof(uint32_t), hipMemcpyHostToDevice, s));
   HIPCHK(hipStreamSynchronize(s));
-  sh->inside = false;
   return YCRDT_OK;
 }
 
@@ -776,6 +783,8 @@ int run_decode(ycrdt_engine* e, ycrdt_batch* b, bool lazy, Decoded& D, bool gene
   const uint64_t est_sec = std::min<uint64_t>(generous ? B / 3 + 64 : std::min<uint64_t>(B / 3 + 64, (uint64_t)nu * 16 + B / 256 + 4096),
                                               0x7FFFFFFFull);
   w.cap_sections = (uint32_t)est_sec;
+  if (const char* tc = getenv("YCRDT_TEST_SECTION_CAP"))  // tests: a tiny estimate forces the overflow re-run
+    if (!generous && atoi(tc) > 0) w.cap_sections = std::min<uint32_t>(w.cap_sections, (uint32_t)atoi(tc));
   w.cap_structs = 0;
   w.cap_ds = 0;
   // ---- decode buffers
@@ -805,7 +814,9 @@ int run_decode(ycrdt_engine* e, ycrdt_batch* b, bool lazy, Decoded& D, bool gene
   if (!ok) return fail(YCRDT_E_DEVICE, oom("decode workspace"));
   // rocPRIM scratch sized for the largest scan of this batch (units may grow it later)
   {
-    size_t tb = prim_tmp_bytes(std::max<uint64_t>(B, 1024));
+    // scans: the bitmap words, per-update and per-struct columns; sorts: the client table (sections)
+    size_t tb = prim_tmp_bytes(std::max<uint64_t>({B / 64 + 4, (uint64_t)nu + 2, (uint64_t)w.cap_sections + 2, 1024}),
+                               (uint64_t)w.cap_sections + 2);
     w.tmp = take<uint8_t>(V, B_TMP, tb, ok);
     w.tmp_bytes = V[B_TMP].cap;
   }
@@ -843,6 +854,7 @@ int run_decode(ycrdt_engine* e, ycrdt_batch* b, bool lazy, Decoded& D, bool gene
     const char* fh = getenv("YCRDT_TEST_FAIL_BEFORE_EXCHANGE");
     if (fh && fh[0] == '1') return fail(YCRDT_E_DEVICE, "test hook: failure before the decode exchange");
     const int rc0 = split_decode_exchange(e, b, sh);
+    if (rc0 == YCRDT_E_CAPACITY && !generous) return run_decode(e, b, lazy, D, true, sh);  // every rank alike
     if (rc0) return rc0;
   }
   mark(e, "decode.bitmap");
@@ -910,7 +922,7 @@ int run_decode(ycrdt_engine* e, ycrdt_batch* b, bool lazy, Decoded& D, bool gene
     Work wd = w;
     bool okd = true;
     wd.scratch = take<uint32_t>(V, B_SCRATCH2, (uint64_t)w.nupd + 2, okd);
-    wd.tmp = take<uint8_t>(V, B_TMP2, prim_tmp_bytes((uint64_t)w.nupd + 2), okd);
+    wd.tmp = take<uint8_t>(V, B_TMP2, prim_tmp_bytes((uint64_t)w.nupd + 2, 0), okd);
     wd.tmp_bytes = V[B_TMP2].cap;
     if (!okd) return fail(YCRDT_E_DEVICE, oom("delete-set scratch"));
     launch_ds_decode(wd, e->side);
@@ -1059,7 +1071,8 @@ int run_merge(ycrdt_engine* e, ycrdt_batch* b, const std::unordered_map<uint32_t
   w.cc = take<uint32_t>(V, B_CC, (size_t)CC_N * (w.cap_clients + 1), ok);
   w.cc64 = take<uint64_t>(V, B_CC64, (size_t)CC64_N * (w.cap_clients + 1), ok);
   {
-    size_t tb = prim_tmp_bytes(std::max<uint64_t>({B, U + 2, 1024}));
+    // scans up to the units; sorts: the client table (YATA's sorts over segments grow it, alloc_lists)
+    size_t tb = prim_tmp_bytes(std::max<uint64_t>({B / 64 + 4, U + 2, (uint64_t)nstructs + 2, 1024}), (uint64_t)D.nsections + 2);
     w.tmp = take<uint8_t>(V, B_TMP, tb, ok);
     w.tmp_bytes = V[B_TMP].cap;
   }
@@ -1106,6 +1119,9 @@ int run_merge(ycrdt_engine* e, ycrdt_batch* b, const std::unordered_map<uint32_t
     w.t_hkey = take<uint32_t>(V, B_THKEY, 2 * n + 4, okl);
     w.t_hval = take<uint32_t>(V, B_THVAL, 2 * n + 4, okl);
     w.t_flag = take<uint32_t>(V, B_TFLAG, 2 * n + 4, okl);  // flags, then their scan behind them
+    // YATA sorts the segments (sibling groups, list members)
+    w.tmp = take<uint8_t>(V, B_TMP, prim_tmp_bytes(std::max<uint64_t>({B / 64 + 4, U + 2, (uint64_t)nstructs + 2, 1024}), n + 2), okl);
+    w.tmp_bytes = V[B_TMP].cap;
     return okl;
   };
   uint32_t nout = 0;
@@ -1194,7 +1210,7 @@ int run_merge(ycrdt_engine* e, ycrdt_batch* b, const std::unordered_map<uint32_t
   if (!exact_out) w.out = take<uint8_t>(V, B_OUT, (size_t)w.cap_out + 16, ok);
   w.sv_out = take<uint8_t>(V, B_SVOUT, (size_t)w.cap_sv + 16, ok);
   if (!ok) return fail(YCRDT_E_DEVICE, oom("output"));
-  uint8_t* tmp2 = take<uint8_t>(V, B_TMP2, prim_tmp_bytes((uint64_t)nsegs + 2), ok);
+  uint8_t* tmp2 = take<uint8_t>(V, B_TMP2, prim_tmp_bytes((uint64_t)nsegs + 2, 0), ok);
   if (!ok) return fail(YCRDT_E_DEVICE, oom("scan space"));
   mark(e, "encode.sizes");
   launch_encode_sizes(w, nsegs, nclients, s, e->side, e->side_fork, e->side_done, tmp2, V[B_TMP2].cap);
@@ -1426,7 +1442,8 @@ int run_lazy(ycrdt_engine* e, ycrdt_batch* b, bool merge, const std::vector<std:
   w.dw_pos = take<uint32_t>(V, B_DWPOS, NDS, ok);
   w.ds_fa = w.ds_first ? take<uint32_t>(V, B_DSFA, NDS, ok) : nullptr;
   {
-    size_t tb = prim_tmp_bytes(std::max<uint64_t>({(uint64_t)b->nbytes + 64, SLOTS, NDS, 1024}));
+    size_t tb = prim_tmp_bytes(std::max<uint64_t>({((uint64_t)b->nbytes + 64) / 64 + 4, SLOTS, NDS, NSEC, 1024}),
+                               std::max<uint64_t>(NSEC, NDS));
     w.tmp = take<uint8_t>(V, B_TMP, tb, ok);
     w.tmp_bytes = V[B_TMP].cap;
   }

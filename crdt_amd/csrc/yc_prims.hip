@@ -40,23 +40,26 @@ void fill_u32_multi(std::initializer_list<FillDesc> fills, hipStream_t s) {
     hipLaunchKernelGGL(k_fill_multi, dim3((uint32_t)std::min<uint64_t>(nmax / 256 + 1, 2048), b.count), dim3(256), 0, s, b);
 }
 
-size_t prim_tmp_bytes(uint64_t n) {
-  size_t a = 0, b = 0, c = 0;
-  rocprim::exclusive_scan(nullptr, a, (const uint32_t*)nullptr, (uint32_t*)nullptr, 0u, (size_t)n, rocprim::plus<uint32_t>());
-  rocprim::exclusive_scan(nullptr, b, (const uint32_t*)nullptr, (uint64_t*)nullptr, (uint64_t)0, (size_t)n, rocprim::plus<uint64_t>());
-  rocprim::radix_sort_keys(nullptr, c, (const uint32_t*)nullptr, (uint32_t*)nullptr, (size_t)n, 0, 32);
-  size_t d = 0;
-  rocprim::radix_sort_pairs(nullptr, d, (const uint32_t*)nullptr, (uint32_t*)nullptr, (const uint32_t*)nullptr,
-                            (uint32_t*)nullptr, (size_t)n, 0, 32);
-  size_t e = 0, f = 0;
-  rocprim::radix_sort_pairs(nullptr, e, (const uint64_t*)nullptr, (uint64_t*)nullptr, (const uint32_t*)nullptr,
-                            (uint32_t*)nullptr, (size_t)n, 0, 64);
-  rocprim::inclusive_scan(nullptr, f, (const uint64_t*)nullptr, (uint64_t*)nullptr, (size_t)n, SegMax64());
-  size_t m = a > b ? a : b;
-  m = m > c ? m : c;
-  m = m > d ? m : d;
-  m = m > e ? m : e;
-  return (m > f ? m : f) + 256;
+// rocPRIM scratch for scans of up to scan_n items and radix sorts of up to sort_n items. The two
+// are sized apart: a sort needs double buffers of its keys and values (12 B per item for the
+// 64-bit keys), a scan only its tile states — sized together from the batch bytes, a 15 GB batch
+// asked for 187 GB of scratch.
+size_t prim_tmp_bytes(uint64_t scan_n, uint64_t sort_n) {
+  size_t a = 0, b = 0, f = 0;
+  rocprim::exclusive_scan(nullptr, a, (const uint32_t*)nullptr, (uint32_t*)nullptr, 0u, (size_t)scan_n, rocprim::plus<uint32_t>());
+  rocprim::exclusive_scan(nullptr, b, (const uint32_t*)nullptr, (uint64_t*)nullptr, (uint64_t)0, (size_t)scan_n, rocprim::plus<uint64_t>());
+  rocprim::inclusive_scan(nullptr, f, (const uint64_t*)nullptr, (uint64_t*)nullptr, (size_t)scan_n, SegMax64());
+  size_t m = std::max({a, b, f});
+  if (sort_n) {
+    size_t c = 0, d = 0, e = 0;
+    rocprim::radix_sort_keys(nullptr, c, (const uint32_t*)nullptr, (uint32_t*)nullptr, (size_t)sort_n, 0, 32);
+    rocprim::radix_sort_pairs(nullptr, d, (const uint32_t*)nullptr, (uint32_t*)nullptr, (const uint32_t*)nullptr,
+                              (uint32_t*)nullptr, (size_t)sort_n, 0, 32);
+    rocprim::radix_sort_pairs(nullptr, e, (const uint64_t*)nullptr, (uint64_t*)nullptr, (const uint32_t*)nullptr,
+                              (uint32_t*)nullptr, (size_t)sort_n, 0, 64);
+    m = std::max({m, c, d, e});
+  }
+  return m + 256;
 }
 
 // A small exclusive scan in one workgroup and one launch (rocPRIM's look-back scan is two: state

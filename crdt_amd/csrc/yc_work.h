@@ -504,7 +504,7 @@ void launch_encode_sizes(const Work& w, uint32_t nsegs, uint32_t nclients, hipSt
 void launch_encode_write(const Work& w, uint32_t nsegs, uint32_t nclients, hipStream_t s);
 
 // rocPRIM wrappers (yc_prims.hip)
-size_t prim_tmp_bytes(uint64_t max_items);
+size_t prim_tmp_bytes(uint64_t scan_n, uint64_t sort_n);  // scratch for scans of scan_n / sorts of sort_n items
 void scan_u32(void* tmp, size_t tmpb, const uint32_t* in, uint32_t* out, uint64_t n, hipStream_t s);          // exclusive
 void scan_u32_to_u64(void* tmp, size_t tmpb, const uint32_t* in, uint64_t* out, uint64_t n, hipStream_t s);   // exclusive
 void sort_u32(void* tmp, size_t tmpb, const uint32_t* in, uint32_t* out, uint64_t n, hipStream_t s);

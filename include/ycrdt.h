@@ -241,7 +241,12 @@ void ycrdt_comm_destroy(ycrdt_comm *c);
  * through these host callbacks instead of RCCL (device buffers are staged through host memory).
  * Each callback returns 0 on success; every rank must make the same calls in the same order. Used
  * by hosts without RCCL between their processes (and by the world-size-2 gloo tests, two processes
- * on one GPU). */
+ * on one GPU). Failure inside an exchange: a rank that fails between two collectives of one
+ * exchange cannot abort a host transport the way it aborts an RCCL communicator (ncclCommAbort),
+ * so its peers stay in the callback they are in until the TRANSPORT gives up: host transports must
+ * carry their own timeout (gloo's process-group timeout does) and return nonzero from the callback,
+ * which then fails the merge on that rank. Failures before an exchange never block: every exchange
+ * starts with a one-word status agreement. */
 typedef struct {
   void *ctx;
   /* in place over n host words of every rank: op 0 = sum, 1 = max */

@@ -13,6 +13,8 @@ checked against Yjs fixtures / the unsharded merge:
   exchanged state vectors equal Yjs's state vectors of the whole documents;
 * delete-set all-gather: each rank's part of a document; the union equals the delete set of
   Y.mergeUpdates over all parts;
+* an empty document held by the ranks is in the fleet result (state vector [0]);
+* a section table past its estimate on one rank makes every rank re-run the decode alike;
 * a malformed update parsed by one rank fails the merge on every rank; a rank that fails on the
   host before the exchange makes the other rank's call fail too (no hang), and the communicator
   keeps working.
@@ -78,8 +80,12 @@ def _worker(rank, world, port, q):
             d.apply_updates(mine)
             if mine or j % 3:  # some documents only on some ranks
                 svs[7 * j + 2] = d.encode_state_vector()
+        svs[999_999] = b"\x00"  # a document every rank holds with an empty state vector
+        if rank == 1:
+            svs[999_998] = b"\x00"  # ... and one only rank 1 holds
         fleet = comm.fleet_sv_allreduce_max(svs)
         out["fleet"] = [(fleet.get(7 * j + 2, b"").hex(), c["sv"]) for j, c in enumerate(c5)]
+        out["fleet_empty"] = [fleet.get(999_999), fleet.get(999_998)]
         # ---- delete-set all-gather: each rank's part of every C3 / C4 fixture (Y.mergeUpdates of its
         # replicas' states); the union is the delete set of Y.mergeUpdates over all of them
         ds_ok = []
@@ -108,6 +114,16 @@ def _worker(rank, world, port, q):
         except crdt_amd.YcrdtError as e:
             out["fail2"] = e.kind
         os.environ.pop("YCRDT_TEST_FAIL_BEFORE_EXCHANGE", None)
+        # ---- rank 0's section table overflows its (test-shrunk) estimate: both ranks re-run the
+        # decode with the worst-case bound and still give the unsharded bytes
+        if rank == 0:
+            os.environ["YCRDT_TEST_SECTION_CAP"] = "2"
+        b = crdt_amd.Batch(docs[-1], eng)
+        b.merge_sharded(world, comm)
+        got = b.result()
+        os.environ.pop("YCRDT_TEST_SECTION_CAP", None)
+        b.merge()
+        out["overflow"] = got == b.result()
         # ---- and the communicator still works afterwards
         b = crdt_amd.Batch(docs[1], eng)
         b.merge_sharded(world, comm)
@@ -147,4 +163,6 @@ def test_exchanges_world2_gloo_one_gpu():
         assert r["fail"] != "no error", r
         assert r["fail2"] != "no error", r
         assert r["after"], r
+        assert r["overflow"], r
+        assert r["fleet_empty"] == [b"\x00", b"\x00"], r
     assert res[0]["fleet"] == res[1]["fleet"]
