@@ -15,10 +15,14 @@ tests/test_gpu_parity.py, tests/test_gpu_multidoc.py). Items = Σ struct clock l
 inputs (Item + GC, Skip excluded), the SURVEY §8(d) unit. `single_doc` keeps the one-document
 step of round 1 for continuity.
 
-Multi-GPU: one process per GPU; the path shards by document (north_star: "partitioned ... by
-document/topic"), so every rank merges its own independent documents (seeds offset per rank) with
-no data-path collective ⇒ "scaling": "weak". torch.distributed (RCCL) is used only for the barrier
-and the max-over-ranks of the step time.
+Multi-GPU: one process per GPU — under torch.distributed.run, or `bench.py --gpus N` spawns the N
+ranks itself (rank r on device r % devices). The headline shards by document (north_star:
+"partitioned ... by document/topic"): every rank merges its own independent documents (seeds
+offset per rank) with no data-path collective ⇒ "scaling": "weak". Barriers, the max-over-ranks
+step time and the per-rank reports go through libycrdt's own communicator (RCCL; a host exchange
+over gloo when ranks share a device). With N > 1 two more legs run by default: C4 key-hash sharded
+across the ranks (one 102 M-item document) and the C5 fleet (routed ingest + the fleet
+state-vector all-reduce).
 """
 import argparse
 import csv
@@ -52,9 +56,7 @@ def parse():
     p.add_argument("--profile-phases", action="store_true")
     p.add_argument("--no-per-op", action="store_true", help="skip the crdt.js per-op leg")
     p.add_argument("--fleet-docs", type=int, default=1_000_000, help="documents in the C5 fleet-ingest leg (0 = skip)")
-    p.add_argument("--no-c4", action="store_true", help="skip the single-GPU C4 leg")
-    p.add_argument("--c4-sharded", action="store_true",
-                   help="with --gpus N > 1: C4 key-hash sharded across the ranks over RCCL (opt-in)")
+    p.add_argument("--no-c4", action="store_true", help="skip the C4 leg (N = 1: one GPU; N > 1: key-hash sharded over the ranks)")
     p.add_argument("--only-headline", action="store_true",
                    help="time the headline merge only (no side legs): rocprof averages then match the bench line")
     p.add_argument("--c3-items", type=int, default=10_000_000,
@@ -451,30 +453,110 @@ def c4_leg(eng, reps=3):
             "generate_s": round(gen_s, 2)}
 
 
-def c4_sharded_leg(eng, world, rank, dist, reps=3):
-    """C4 key-hash sharded across the ranks (one GPU each): every rank stages the same C4 updates,
-    runs its shard's integrate phases, and the flag words are summed over RCCL inside libycrdt."""
+def c4_sharded_leg(eng, comm, world, rank, reps=2):
+    """C4 (BASELINE configs[3]) at BASELINE scale, key-hash sharded across the ranks: every rank
+    stages the same C4_FULL updates (102 M items), parses its share of them and integrates its
+    shard; the parse results and the flag words are combined inside libycrdt over its own
+    communicator (RCCL between GPUs, the host exchange when ranks share a device). Checked against
+    the unsharded merge of the same batch on every rank."""
     import crdt_amd
-    from crdt_amd.workload import C4, gen_nested
+    from crdt_amd.workload import C4_FULL, gen_nested
 
-    ups, st = gen_nested(**C4)
-    uid = [crdt_amd.Comm.unique_id() if rank == 0 else None]
-    dist.broadcast_object_list(uid, src=0)
-    comm = crdt_amd.Comm(eng, world, rank, uid[0])
-    try:
-        b = crdt_amd.Batch(ups, eng)
-        b.merge_sharded(world, comm)
-        t0 = time.perf_counter()
-        for _ in range(reps):
-            s1 = b.merge_sharded(world, comm)
-        ms = (time.perf_counter() - t0) * 1e3 / reps
-        full = b.result()
-        b.merge()
-        same = b.result() == full
-    finally:
-        comm.close()
-    return {"ranks": world, "ms_per_merge": round(ms, 3), "items": s1.items,
-            "items_per_s": round(s1.items / (ms * 1e-3), 1), "identical_to_unsharded": same}
+    ups, _ = gen_nested(**C4_FULL)
+    b = crdt_amd.Batch(ups, eng)
+    eng.set_profiling(True)
+    b.merge_sharded(world, comm)  # warm-up (workspace)
+    comm.barrier()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        s1 = b.merge_sharded(world, comm)
+    ms = (time.perf_counter() - t0) * 1e3 / reps
+    phases = {n: round(m, 3) for n, m in eng.phase_times()}
+    eng.set_profiling(False)
+    full = b.result()
+    b.merge()
+    same = b.result() == full
+    del b
+    ms_all = [struct_unpack_d(x) for x in comm.allgather(struct_pack_d(ms))]
+    return {"ranks": world, "ms_per_merge": round(max(ms_all), 3), "ms_per_rank": [round(x, 3) for x in ms_all],
+            "items": s1.items, "items_per_s": round(s1.items / (max(ms_all) * 1e-3), 1),
+            "identical_to_unsharded": same, "phases_ms_rank": phases,
+            "transport": comm.transport}
+
+
+def struct_pack_d(x):
+    import struct
+
+    return struct.pack("<d", float(x))
+
+
+def struct_unpack_d(b):
+    import struct
+
+    return struct.unpack("<d", b)[0]
+
+
+def fleet_ranks_leg(eng, comm, world, rank, n_docs):
+    """C5 (BASELINE configs[4]) across the ranks: a fleet of n_docs topics (one Y.Doc each,
+    crdt.js:221,235; the updates of the 60 Yjs-generated C5 fixture documents, cycled).
+    (1) routed ingest: every rank applies, in ONE ycrdt_apply_updates_multi call, the updates of
+    the topics ycrdt_route assigns to it (no data collective; fleet documents/s = all topics over
+    the slowest rank's time). (2) gossip without routing: every rank holds every topic, but only the
+    updates u_i with i % world == rank; ycrdt_comm_fleet_sv_allreduce_max gives every rank the state
+    vector of the union for every topic (sampled topics compared with Yjs's state vectors)."""
+    import numpy as np
+
+    import crdt_amd
+
+    with open(os.path.join(ROOT, "tests", "golden", "configs.json")) as f:
+        cases = [c for c in json.load(f)["cases"] if c["name"].startswith("c5_")]
+    base = [[bytes.fromhex(u) for u in c["updates"]] for c in cases]
+    # (1) routed ingest
+    mine = [d for d in range(n_docs) if crdt_amd.route(str(d).encode(), world) == rank]
+    idx, ups = [], []
+    for j, d in enumerate(mine):
+        for u in base[d % len(base)]:
+            idx.append(j)
+            ups.append(u)
+    docs = [crdt_amd.Doc(client_id=0x7FFFFFF0, engine=eng) for _ in mine]
+    comm.barrier()
+    t0 = time.perf_counter()
+    crdt_amd.apply_updates_multi(docs, ups, engine=eng, doc_index=np.asarray(idx, dtype=np.int64))
+    ingest_ms = (time.perf_counter() - t0) * 1e3
+    ok = True
+    for j, d in enumerate(mine[:50]):
+        ok = ok and docs[j].encode_state_vector().hex() == cases[d % len(cases)]["sv"]
+    del docs
+    ing = [struct_unpack_d(x) for x in comm.allgather(struct_pack_d(ingest_ms))]
+    # (2) un-routed gossip: the fleet's state vectors over the ranks (a sample of the topics: every
+    # rank holds a part of each)
+    n_sv = min(n_docs, 100_000)
+    svs = {}
+    idx, ups, held = [], [], []
+    for d in range(n_sv):
+        part = [u for i, u in enumerate(base[d % len(base)]) if i % world == rank]
+        if part:
+            held.append(d)
+            for u in part:
+                idx.append(len(held) - 1)
+                ups.append(u)
+    docs = [crdt_amd.Doc(client_id=0x7FFFFFF0, engine=eng) for _ in held]
+    crdt_amd.apply_updates_multi(docs, ups, engine=eng, doc_index=np.asarray(idx, dtype=np.int64))
+    blob, offs = crdt_amd.states_packed(docs, eng)
+    for j, d in enumerate(held):
+        svs[d] = bytes(blob[int(offs[2 * j + 1]):int(offs[2 * j + 2])])
+    del docs
+    comm.barrier()
+    t0 = time.perf_counter()
+    fleet = comm.fleet_sv_allreduce_max(svs)
+    sv_ms = (time.perf_counter() - t0) * 1e3
+    sv_ok = len(fleet) == n_sv and all(fleet[d].hex() == cases[d % len(cases)]["sv"] for d in range(0, n_sv, 97))
+    svm = [struct_unpack_d(x) for x in comm.allgather(struct_pack_d(sv_ms))]
+    return {"docs": n_docs, "routed_ingest": {"ms": round(max(ing), 2), "ms_per_rank": [round(x, 2) for x in ing],
+                                             "docs_per_s": round(n_docs / (max(ing) * 1e-3), 1), "parity": ok,
+                                             "docs_this_rank": len(mine)},
+            "sv_allreduce": {"docs": n_sv, "ms": round(max(svm), 2), "parity": sv_ok,
+                             "includes": "host pack + device sort/reduce + key-space all-gather + one MAX all-reduce"}}
 
 
 def fleet_ingest_leg(eng, n_docs):
@@ -629,17 +711,99 @@ def fleet_sync_leg(eng, n_pairs):
 
 def main():
     args = parse()
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(spawn_ranks(args))  # no GPU call in this process before the ranks exist
+    sys.exit(run_rank(args))
+
+
+def _free_port():
+    import socket
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _rank_entry(rank, world, port, q):
+    os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank), LOCAL_WORLD_SIZE=str(world),
+                      MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    sys.exit(run_rank(parse(), report=q))
+
+
+def spawn_ranks(args):
+    """`bench.py --gpus N` without a launcher: N fresh processes (multiprocessing spawn), rank r on
+    device r % devices, the same code path as under torch.distributed.run. Fails unless exactly N
+    ranks came up and all of them finished cleanly."""
+    import multiprocessing as mp
+
+    ctx = mp.get_context("spawn")
+    q = ctx.SimpleQueue()
+    port = _free_port()
+    procs = [ctx.Process(target=_rank_entry, args=(r, args.gpus, port, q)) for r in range(args.gpus)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join()
+    seen = set()
+    while not q.empty():
+        seen.add(q.get())
+    codes = [p.exitcode for p in procs]
+    if any(codes):
+        print(f"bench: rank exit codes {codes}", file=sys.stderr, flush=True)
+        return 1
+    if seen != set(range(args.gpus)):
+        print(f"bench: {len(seen)} of {args.gpus} ranks reported ({sorted(seen)})", file=sys.stderr, flush=True)
+        return 1
+    return 0
+
+
+def setup_ranks(rank, world, local, report):
+    """The engine on this rank's device and libycrdt's communicator. torch.distributed (gloo: host
+    TCP, no GPU) only bootstraps — it carries the RCCL unique id — and is the host transport when
+    ranks share a device (RCCL takes one rank per GPU). Barriers, the max-over-ranks step time and
+    every data exchange go through libycrdt's Comm."""
+    import crdt_amd
+
+    ndev = crdt_amd.device_count()
+    if ndev < 1:
+        raise RuntimeError("no HIP device")
+    dev = int(os.environ.get("YCRDT_DEVICE", "0")) if world == 1 else local % ndev
+    eng = crdt_amd.Engine(device=dev)
+    if world == 1:
+        return eng, None, ndev
+    import torch.distributed as tdist
+
+    # gloo prints its connection lines on stdout: keep stdout for the one JSON line
+    saved = os.dup(1)
+    os.dup2(2, 1)
+    try:
+        tdist.init_process_group("gloo", rank=rank, world_size=world)
+    finally:
+        sys.stdout.flush()
+        os.dup2(saved, 1)
+        os.close(saved)
+    local_world = int(os.environ.get("LOCAL_WORLD_SIZE", str(world)))
+    if local_world > ndev:  # ranks share a device: the library's collectives over gloo
+        comm = crdt_amd.Comm.over_torch(eng)
+        comm.transport = f"host exchange over gloo ({local_world} ranks on {ndev} device(s))"
+    else:
+        uid = [crdt_amd.Comm.unique_id() if rank == 0 else None]
+        tdist.broadcast_object_list(uid, src=0)
+        comm = crdt_amd.Comm(eng, world, rank, uid[0])
+        comm.transport = "rccl"
+    comm.barrier()
+    if report is not None:
+        report.put(rank)
+    return eng, comm, ndev
+
+
+def run_rank(args, report=None):
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    dist = None
-    if world > 1:
-        import torch
-        import torch.distributed as tdist
-
-        torch.cuda.set_device(local)
-        tdist.init_process_group("nccl")
-        dist = tdist
+    eng, comm, ndev = setup_ranks(rank, world, local, report)
 
     import crdt_amd
     from crdt_amd.workload import C1, C2, gen_map
@@ -658,7 +822,6 @@ def main():
     ndocs = len(docs)
     in_bytes = sum(len(u) for d in docs for u in d)
 
-    eng = crdt_amd.Engine(device=local if world > 1 else int(os.environ.get("YCRDT_DEVICE", "0")))
     batch = crdt_amd.Batch(docs=docs, engine=eng) if ndocs > 1 else crdt_amd.Batch(updates, eng)
     st = None
     for _ in range(max(1, args.warmup)):
@@ -673,12 +836,8 @@ def main():
         out_bytes = len(out_update) + len(out_sv)
 
     def barrier():
-        if dist is not None:
-            import torch
-
-            t = torch.zeros(1, device="cuda")
-            dist.all_reduce(t)
-            torch.cuda.synchronize()
+        if comm is not None:
+            comm.barrier()  # libycrdt's own transport (RCCL / host exchange)
 
     # ---- timed region: K merges, inputs resident in HBM. The engine's phase events stay on: they
     # time the dominant kernel live, on the engine stream it runs on (roofline below).
@@ -696,15 +855,17 @@ def main():
     t1 = time.perf_counter()
     eng.set_profiling(False)
     dt = t1 - t0
-    if dist is not None:
-        import torch
-
-        t = torch.tensor([dt], device="cuda", dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dt = float(t.item())
-        items_all = torch.tensor([float(st.items)], device="cuda", dtype=torch.float64)
-        dist.all_reduce(items_all)
-        items_step = float(items_all.item())
+    rank_reports = None
+    if comm is not None:
+        # the max over the ranks of the step time, the items of all ranks, and each rank's report
+        mine = {"rank": rank, "device": local % ndev, "dt_s": dt, "items": int(st.items),
+                "ms_per_step": round(dt * 1e3 / args.steps, 4),
+                "phases_ms": {n: round(m / args.steps, 4) for n, m in phase_acc.items()}}
+        rank_reports = [json.loads(x) for x in comm.allgather(json.dumps(mine).encode())]
+        if len(rank_reports) != world:
+            raise RuntimeError(f"{len(rank_reports)} rank reports for world {world}")
+        dt = max(r["dt_s"] for r in rank_reports)
+        items_step = float(sum(r["items"] for r in rank_reports))
     else:
         items_step = float(st.items)
     ms_per_step = dt * 1e3 / args.steps
@@ -765,7 +926,7 @@ def main():
     # A serving loop: batch k+1 is staged (host pack + pinned H2D on the engine's copy stream) by a
     # second host thread while batch k merges and its result comes back; one result buffer is
     # reused. One untimed warm-up batch (pinned areas, first touch of the result buffer).
-    e2e_steps = 0 if args.only_headline or args.billion else 4
+    e2e_steps = 0 if args.only_headline or args.billion or world > 1 else 4
     make = (lambda: crdt_amd.Batch(docs=docs, engine=eng)) if ndocs > 1 else (lambda: crdt_amd.Batch(updates, eng))
     e2e_ms = 0.0
     if e2e_steps:
@@ -812,7 +973,10 @@ def main():
     per_op = per_op_leg(eng) if side and not args.no_per_op else None
     c3 = c3_leg(eng, args.c3_items) if side and args.c3_items > 0 else None
     c4 = c4_leg(eng) if side and not args.no_c4 else None
-    c4s = c4_sharded_leg(eng, world, rank, dist) if dist is not None and args.c4_sharded else None
+    # N > 1: the multi-GPU legs (on by default): C4 key-hash sharded over the ranks, the C5 fleet
+    multi = comm is not None and not args.only_headline and not args.billion
+    c4s = c4_sharded_leg(eng, comm, world, rank) if multi and not args.no_c4 else None
+    fleet_ranks = fleet_ranks_leg(eng, comm, world, rank, args.fleet_docs) if multi and args.fleet_docs > 0 else None
     billion = billion_leg(eng, cfg, gen_map, args.billion) if args.billion and rank == 0 else None
     line = {
         "metric": "CRDT items merged/sec at 1/2/4/8 MI355X + % of HBM roofline",
@@ -839,7 +1003,9 @@ def main():
             "segments": st.segments,
             "output_bytes": out_bytes,
             "parallelism": f"doc-sharded x{world}",
+            "transport": comm.transport if comm is not None else None,
         },
+        "ranks": rank_reports,
         "single_doc": single,
         "device_ms_per_step": round(dev_ms / args.steps, 4),
         "unique_items_per_step_per_gpu": st.units,
@@ -869,13 +1035,19 @@ def main():
         "c3": c3,
         "c4": c4,
         "c4_sharded": c4s,
+        "fleet_ranks": fleet_ranks,
         "billion": billion,
         "phases_ms": {n: round(m, 4) for n, m in phases},
     }
     if rank == 0:
         print(json.dumps(line), flush=True)
-    if dist is not None:
-        dist.destroy_process_group()
+    if comm is not None:
+        comm.barrier()
+        comm.close()
+        import torch.distributed as tdist
+
+        tdist.destroy_process_group()
+    return 0
 
 
 if __name__ == "__main__":

@@ -88,7 +88,7 @@ EXPORTS = (
     "ycrdt_map_get", "ycrdt_map_size", "ycrdt_array_length", "ycrdt_array_get", "ycrdt_apply_updates_multi",
     "ycrdt_comm_unique_id", "ycrdt_comm_create", "ycrdt_comm_destroy", "ycrdt_batch_merge_sharded",
     "ycrdt_comm_sv_allreduce_max", "ycrdt_comm_ds_allgather", "ycrdt_comm_create_exchange", "ycrdt_route",
-    "ycrdt_comm_fleet_sv_allreduce_max", "ycrdt_docs_states_packed",
+    "ycrdt_comm_fleet_sv_allreduce_max", "ycrdt_docs_states_packed", "ycrdt_comm_allgather", "ycrdt_device_count",
 )
 
 MERGE_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p)
@@ -162,6 +162,8 @@ def lib():
     L.ycrdt_batch_merge_sharded.argtypes = [vp, vp, u32, P(MergeStats)]
     L.ycrdt_comm_sv_allreduce_max.argtypes = [vp, vp, _Buf, P(_Out)]
     L.ycrdt_comm_ds_allgather.argtypes = [vp, vp, _Buf, P(_Out)]
+    L.ycrdt_comm_allgather.argtypes = [vp, vp, _Buf, P(_Out), P(_Out)]
+    L.ycrdt_device_count.argtypes = [P(i32)]
     L.ycrdt_comm_create_exchange.argtypes = [vp, i32, i32, P(_Exchange), P(vp)]
     L.ycrdt_docs_states_packed.argtypes = [vp, P(vp), sz, vp, ctypes.c_uint64, P(ctypes.c_uint64), P(ctypes.c_uint64)]
     L.ycrdt_route.argtypes = [ctypes.c_char_p, sz, u32]
@@ -605,11 +607,33 @@ class Comm:
         _check(lib().ycrdt_comm_sv_allreduce_max(self._h, self.engine._h, _Buf(ctypes.cast(ctypes.c_char_p(b), ctypes.c_void_p), len(b)), ctypes.byref(out)))
         return _take(out)
 
+    def allgather(self, payload: bytes) -> list:
+        """Every rank's bytes, in rank order (ycrdt_comm_allgather, the library's own transport)."""
+        import numpy as np
+
+        b, o = _Out(), _Out()
+        p = bytes(payload)
+        _check(lib().ycrdt_comm_allgather(self._h, self.engine._h, _Buf(ctypes.cast(ctypes.c_char_p(p), ctypes.c_void_p), len(p)),
+                                          ctypes.byref(b), ctypes.byref(o)))
+        blob = _take(b)
+        offs = np.frombuffer(_take(o), dtype=np.uint64)
+        return [blob[int(offs[r]):int(offs[r + 1])] for r in range(len(offs) - 1)]
+
+    def barrier(self):
+        self.allgather(b"")
+
     def ds_allgather(self, update: bytes) -> bytes:
         out = _Out()
         b = bytes(update)
         _check(lib().ycrdt_comm_ds_allgather(self._h, self.engine._h, _Buf(ctypes.cast(ctypes.c_char_p(b), ctypes.c_void_p), len(b)), ctypes.byref(out)))
         return _take(out)
+
+
+def device_count() -> int:
+    """HIP devices visible to this process (ycrdt_device_count); 0 without a GPU."""
+    n = ctypes.c_int32()
+    rc = lib().ycrdt_device_count(ctypes.byref(n))
+    return n.value if rc == 0 else 0
 
 
 def route(doc_id, world: int) -> int:

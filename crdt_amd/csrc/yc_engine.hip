@@ -2462,6 +2462,43 @@ int ycrdt_comm_sv_allreduce_max(ycrdt_comm* c, ycrdt_engine* e, ycrdt_buf sv, yc
   return YCRDT_OK;
 }
 
+int ycrdt_comm_allgather(ycrdt_comm* c, ycrdt_engine* e, ycrdt_buf mine, ycrdt_out* blob, ycrdt_out* offs) {
+  if (!c || !e || !blob || !offs || (mine.len && !mine.ptr)) return fail(YCRDT_E_ARG, "null arg");
+  blob->ptr = offs->ptr = nullptr;
+  blob->len = offs->len = 0;
+  HIPCHK(hipSetDevice(e->device));
+  std::string err;
+  std::vector<std::vector<uint8_t>> parts;
+  if (yc::comm_allgather_updates(c, mine.ptr, mine.len, e->stream, parts, err)) return fail(YCRDT_E_DEVICE, err);
+  std::vector<uint64_t> o(1, 0);
+  for (const auto& p : parts) o.push_back(o.back() + p.size());
+  blob->ptr = (uint8_t*)malloc(o.back() ? o.back() : 1);
+  offs->ptr = (uint8_t*)malloc(sizeof(uint64_t) * o.size());
+  if (!blob->ptr || !offs->ptr) {
+    free(blob->ptr);
+    free(offs->ptr);
+    blob->ptr = offs->ptr = nullptr;
+    return fail(YCRDT_E_CAPACITY, "host allocation failed");
+  }
+  for (size_t r = 0; r < parts.size(); ++r)
+    if (!parts[r].empty()) memcpy(blob->ptr + o[r], parts[r].data(), parts[r].size());
+  memcpy(offs->ptr, o.data(), sizeof(uint64_t) * o.size());
+  blob->len = o.back();
+  offs->len = sizeof(uint64_t) * o.size();
+  return YCRDT_OK;
+}
+
+int ycrdt_device_count(int* count) {
+  if (!count) return fail(YCRDT_E_ARG, "null arg");
+  *count = 0;
+  if (hipGetDeviceCount(count) != hipSuccess) {
+    (void)hipGetLastError();
+    *count = 0;
+    return fail(YCRDT_E_DEVICE, "no HIP device");
+  }
+  return YCRDT_OK;
+}
+
 int ycrdt_comm_ds_allgather(ycrdt_comm* c, ycrdt_engine* e, ycrdt_buf update, ycrdt_out* out) {
   if (!c || !e || !out || (update.len && !update.ptr)) return fail(YCRDT_E_ARG, "null arg");
   out->ptr = nullptr;

@@ -83,9 +83,11 @@ struct Cur {
   uint32_t len;
 };
 
-__global__ __launch_bounds__(64) void k_lz_merge(Work w, uint32_t nclients) {
+__global__ __launch_bounds__(64) void k_lz_merge(Work w, uint32_t nclients, unsigned long long* ord, unsigned long long ord_base) {
   __shared__ uint32_t rcur[LZ_KMAX], rend[LZ_KMAX], rhi[LZ_KMAX], rlo[LZ_KMAX];
-  const uint32_t r = blockIdx.x;  // client rank (descending client order)
+  // client rank (descending client order) in workgroup start order: the stamps it waits for come
+  // from lower ranks, i.e. from workgroups already running (ordered_block_id, yc_work.h)
+  const uint32_t r = ordered_block_id(ord, ord_base);
   const uint32_t lane = threadIdx.x;
   const uint32_t a = w.lz_rstart[r], K = w.lz_rstart[r + 1] - a;
   const uint32_t base = w.lz_evbase[r];
@@ -490,7 +492,9 @@ void launch_lazy_merge(Work& w, uint32_t nsections, uint32_t nclients, hipStream
   hipLaunchKernelGGL(k_lz_cap, dim3(G(nclients + 1)), dim3(256), 0, s, w, nclients);
   scan_u32(w.tmp, w.tmp_bytes, w.lz_cap, w.lz_evbase, nclients + 1, s);
   hipMemsetAsync(w.lz_flag, 0, sizeof(uint32_t) * (nsections + 1), s);
-  hipLaunchKernelGGL(k_lz_merge, dim3(nclients), dim3(64), 0, s, w, nclients);
+  OrderedIds o;
+  if (!ordered_ids(nclients, s, o)) { hipMemsetAsync(&w.ctr->err, ERR_CAPACITY, 1, s); return; }
+  hipLaunchKernelGGL(k_lz_merge, dim3(nclients), dim3(64), 0, s, w, nclients, o.ctr, o.base);
 }
 
 // diffUpdate: one block per section of the single input update

@@ -235,7 +235,7 @@ __device__ __forceinline__ bool bytes_eq(const uint8_t* __restrict__ a, const ui
 // Do root structs a and b name the same list? A list is (document, root type name | parent item,
 // parentSub) (Item.integrate's parent / parentSub after Item.getMissing, Y@76507; typeMapSet keys,
 // crdt.js:434). Names and parentSubs are compared as whole varStrings (length prefix included).
-__device__ __attribute__((noinline)) bool same_list(const Work& w, uint32_t a, uint32_t b) {
+__device__ __forceinline__ bool same_list(const Work& w, uint32_t a, uint32_t b) {  // inline: a Work reference into an out-of-line call copies the whole Work to scratch
   if (a == b) return true;
   const uint32_t pk = w.s_pk[a];
   if (pk != w.s_pk[b]) return false;

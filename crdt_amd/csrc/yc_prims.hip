@@ -114,10 +114,16 @@ constexpr uint64_t LB_VAL = (1ull << 40) - 1;
 constexpr uint32_t LB_EPOCHS = 1u << 22;
 template <class T>
 __global__ __launch_bounds__(LB_LANES) void k_scan_lb(const uint32_t* in, T* out, uint64_t n,
-                                                     unsigned long long* __restrict__ state, uint32_t epoch, uint32_t vec) {
+                                                     unsigned long long* __restrict__ state, uint32_t epoch, uint32_t vec,
+                                                     unsigned long long* ord, unsigned long long ord_base) {
   __shared__ T wtot[LB_LANES / 64];
   __shared__ T tile_pre;
-  const uint32_t t = threadIdx.x, lane = t & 63, wv = t >> 6, tile = blockIdx.x;
+  // the tile is the order the workgroup STARTED in, not its block id: every tile it waits on has
+  // started, so it is resident and finishes (block ids are dealt to the XCDs' dispatchers
+  // independently: with another kernel filling one XCD — a second stream, another process — a
+  // tile could wait on a lower block id that cannot be dispatched until the waiting tiles leave)
+  const uint32_t tile = ordered_block_id(ord, ord_base);
+  const uint32_t t = threadIdx.x, lane = t & 63, wv = t >> 6;
   const uint64_t base = (uint64_t)tile * LB_TILE + (uint64_t)t * LB_ITEMS;
   const unsigned long long ep = (unsigned long long)epoch << 42;
   uint32_t v[LB_ITEMS];
@@ -207,14 +213,14 @@ __global__ __launch_bounds__(LB_LANES) void k_scan_lb(const uint32_t* in, T* out
 
 // per-stream look-back states (zeroed at allocation, then only written by k_scan_lb)
 struct LbState {
-  unsigned long long* state = nullptr;
+  unsigned long long* state = nullptr;  // [tiles] tile states, then the ordered-id counter
   uint64_t tiles = 0;
   uint32_t epoch = 0;
+  unsigned long long issued = 0;        // ordered ids handed out on this stream (= the counter once they ran)
 };
 static std::mutex lb_mu;
 static std::unordered_map<hipStream_t, LbState> lb_states;
-static LbState* lb_state(uint64_t tiles, hipStream_t s) {
-  std::lock_guard<std::mutex> g(lb_mu);
+static LbState* lb_state(uint64_t tiles, hipStream_t s) {  // (lb_mu held)
   LbState& st = lb_states[s];
   if (st.tiles < tiles || st.epoch + 1 >= LB_EPOCHS) {
     const uint64_t nt = std::max<uint64_t>(tiles, st.tiles) + 256;
@@ -223,7 +229,7 @@ static LbState* lb_state(uint64_t tiles, hipStream_t s) {
       (void)hipFree(st.state);
     }
     st = LbState{};
-    if (hipMalloc((void**)&st.state, nt * 8) != hipSuccess || hipMemsetAsync(st.state, 0, nt * 8, s) != hipSuccess) {
+    if (hipMalloc((void**)&st.state, (nt + 1) * 8) != hipSuccess || hipMemsetAsync(st.state, 0, (nt + 1) * 8, s) != hipSuccess) {
       (void)hipGetLastError();
       st = LbState{};
       return nullptr;
@@ -236,10 +242,23 @@ static LbState* lb_state(uint64_t tiles, hipStream_t s) {
 template <class T>
 static bool scan_lb(const uint32_t* in, T* out, uint64_t n, hipStream_t s) {
   const uint64_t tiles = (n + LB_TILE - 1) / LB_TILE;
+  std::lock_guard<std::mutex> g(lb_mu);
   LbState* st = lb_state(tiles, s);
   if (!st) return false;
   const uint32_t vec = (((uintptr_t)in | (uintptr_t)out) & 15u) == 0;
-  hipLaunchKernelGGL(k_scan_lb<T>, dim3((uint32_t)tiles), dim3(LB_LANES), 0, s, in, out, n, st->state, st->epoch, vec);
+  hipLaunchKernelGGL(k_scan_lb<T>, dim3((uint32_t)tiles), dim3(LB_LANES), 0, s, in, out, n, st->state, st->epoch, vec,
+                     st->state + st->tiles, st->issued);
+  st->issued += tiles;
+  return true;
+}
+
+bool ordered_ids(uint64_t nblocks, hipStream_t s, OrderedIds& out) {
+  std::lock_guard<std::mutex> g(lb_mu);
+  LbState* st = lb_state(1, s);
+  if (!st) return false;
+  out.ctr = st->state + st->tiles;
+  out.base = st->issued;
+  st->issued += nblocks;
   return true;
 }
 

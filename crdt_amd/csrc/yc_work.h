@@ -308,6 +308,24 @@ __device__ __forceinline__ uint32_t xcd_block() {
 }
 __device__ __forceinline__ uint32_t gidx() { return xcd_block() * blockDim.x + threadIdx.x; }
 
+// Workgroups that wait on other workgroups of the same launch (decoupled look-back, the lazy
+// merge's stamps) take their index in START order: ordered_block_id hands out base, base + 1, ...
+// as the workgroups begin, so every index a workgroup waits on belongs to one that is already
+// running. Block ids give no such guarantee: each XCD dispatches its share independently, and a
+// concurrent kernel (another stream or process) filling one XCD can leave a lower block id
+// undispatched behind workgroups spinning on it. Counter and base per stream (yc_prims.hip).
+struct OrderedIds {
+  unsigned long long* ctr = nullptr;
+  unsigned long long base = 0;
+};
+bool ordered_ids(uint64_t nblocks, hipStream_t s, OrderedIds& out);  // one per launch, in launch order
+__device__ __forceinline__ uint32_t ordered_block_id(unsigned long long* ctr, unsigned long long base) {
+  __shared__ uint32_t id;
+  if (threadIdx.x == 0) id = (uint32_t)(atomicAdd(ctr, 1ull) - base);
+  __syncthreads();
+  return id;
+}
+
 __device__ __forceinline__ uint64_t client_hash(uint64_t k) {  // splitmix64 finaliser
   k ^= k >> 30; k *= 0xBF58476D1CE4E5B9ull;
   k ^= k >> 27; k *= 0x94D049BB133111EBull;

@@ -282,6 +282,13 @@ int ycrdt_comm_fleet_sv_allreduce_max(ycrdt_comm *c, ycrdt_engine *e, const uint
  * engine's HIP mergeUpdates (the delete-set union): every rank receives the same update. */
 int ycrdt_comm_ds_allgather(ycrdt_comm *c, ycrdt_engine *e, ycrdt_buf update, ycrdt_out *out);
 
+/* Every rank's byte string, in rank order (variable lengths): blob = the concatenation, offs =
+ * (nranks + 1) u64 offsets into it. The host-side control exchange of a multi-rank job (barrier,
+ * the max of the ranks' step times, per-rank reports) over the library's own transport. */
+int ycrdt_comm_allgather(ycrdt_comm *c, ycrdt_engine *e, ycrdt_buf mine, ycrdt_out *blob, ycrdt_out *offs);
+/* HIP devices visible to this process (a launcher assigns rank r to device r % count) */
+int ycrdt_device_count(int *count);
+
 void ycrdt_free(ycrdt_out *o);
 const char *ycrdt_last_error(void);
 const char *ycrdt_version(void);
