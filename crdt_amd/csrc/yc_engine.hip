@@ -186,7 +186,7 @@ enum Buf {
   B_TPRV, B_TMPRV, B_TMTAIL, B_TTREP, B_TOTAIL, B_THKEY, B_THVAL, B_TFLAG, B_TSCAN, B_SENT,
   B_OFIRST, B_OCIDX, B_OSIZE, B_OPOS, B_RSEG, B_RLEN, B_RSIZE, B_RPOS, B_OUT, B_SVOUT,
   B_VKMAP, B_VKREP, B_VKEYS, B_VNKEYS, B_VPOS, B_VD0, B_VN0, B_VD1, B_VN1, B_VORDER, B_VSEGS,
-  B_SCRATCH2, B_TMP2, B_CAPS, B_CLKEY, B_CLKEY2, B_CHKEY, B_CHVAL, B_CLDOC, B_DSFA, B_EMIT, B_DOCRNG, B_PACK, B_PACKPC, B_SPLITMETA, B_CLSINGLE, B_KSHARD, B_SOWNER, B_GFLAGS0, B_GFACC,
+  B_SCRATCH2, B_TMP2, B_CAPS, B_CLKEY, B_CLKEY2, B_CHKEY, B_CHVAL, B_CLDOC, B_DSFA, B_EMIT, B_DOCRNG, B_PACK, B_PACKPC, B_SPLITMETA, B_CLSINGLE, B_KSHARD, B_SOWNER, B_GFLAGS0, B_GFACC, B_LZBCLIENT,
   B_COUNT
 };
 
@@ -633,6 +633,7 @@ struct Decoded {
   uint32_t array_roots = 0;  // 1: some item names a parent without a parentSub (a YArray may exist)
   uint32_t nested = 0;       // 1: some item names a parent item (nested types: dead-type pass needed)
   uint32_t nroots = 0;       // items with an explicit parent (key table bound)
+  uint32_t noncanon = 0;     // lazy: some update's sections are not in strictly descending client order
 };
 
 // ---- decode split (sharded merge): which updates this rank parses. Updates are dealt to ranks
@@ -826,8 +827,8 @@ int run_decode(ycrdt_engine* e, ycrdt_batch* b, bool lazy, Decoded& D, bool gene
                   {w.ufail, (uint64_t)nu + 1, 0u},
                   {(uint32_t*)w.final_bits, (uint64_t)nwords * 2, 0u},
                   {(uint32_t*)w.sec_bits, (uint64_t)nwords * 2, 0u}}, s);
-  static const bool dbg_yata = getenv("YCRDT_DEBUG_YATA") && getenv("YCRDT_DEBUG_YATA")[0] == '1';
-  static const bool dbg_dec = getenv("YCRDT_DEBUG_DECODE") && getenv("YCRDT_DEBUG_DECODE")[0] == '1';
+  const bool dbg_yata = getenv("YCRDT_DEBUG_YATA") && getenv("YCRDT_DEBUG_YATA")[0] == '1';
+  const bool dbg_dec = getenv("YCRDT_DEBUG_DECODE") && getenv("YCRDT_DEBUG_DECODE")[0] == '1';
   w.dbg = dbg_yata || dbg_dec ? take<unsigned long long>(V, B_DBG, 8, ok) : nullptr;
   if (w.dbg) HIPCHK(hipMemsetAsync(w.dbg, 0, 64, s));
   // ---- K1 decode
@@ -946,8 +947,10 @@ int run_decode(ycrdt_engine* e, ycrdt_batch* b, bool lazy, Decoded& D, bool gene
     HIPCHK(hipMemsetAsync(w.cl_start, 0, sizeof(uint32_t) * (nsections + 1), s));
   }
   HIPCHK(hipStreamWaitEvent(s, e->side_done, 0));
+  if (lazy) launch_lazy_canon(w, s);  // sections out of the descending client order (yc_lazy.hip)
   rc = check(e, c, "struct decode");
   if (rc) return rc;
+  D.noncanon = c.noncanon;
   const uint32_t nclients = c.nclients;
   const uint64_t nunits = lazy ? 0 : c.units;
   D.in_len = c.in_len;
@@ -1400,8 +1403,10 @@ int run_lazy(ycrdt_engine* e, ycrdt_batch* b, bool merge, const std::vector<std:
   if (rc) return rc;
   Counters c;
   const uint64_t NSEC = D.nsections + 2, NC = D.nclients + 2;
-  const uint64_t NBLK = (merge ? D.nclients : D.nsections) + 2;
-  const uint64_t SLOTS = 2ull * D.nstructs + 2ull * NBLK + 4;
+  const bool seq = merge && D.noncanon;  // the serial mergeUpdates loop: output sections follow the events
+  const uint64_t NBLK0 = (merge ? D.nclients : D.nsections) + 2;
+  const uint64_t SLOTS = 2ull * D.nstructs + 2ull * NBLK0 + 4;
+  const uint64_t NBLK = seq ? SLOTS + 2 : NBLK0;
   const uint64_t NDS = D.nds + 2;
   w.lz_key = take<uint64_t>(V, B_LZKEY, NSEC, ok);
   w.lz_keys = take<uint64_t>(V, B_LZKEYS, NSEC, ok);
@@ -1413,6 +1418,7 @@ int run_lazy(ycrdt_engine* e, ycrdt_batch* b, bool merge, const std::vector<std:
   w.lz_cap = take<uint32_t>(V, B_LZCAP, NBLK, ok);
   w.lz_evbase = take<uint32_t>(V, B_LZEVBASE, NBLK, ok);
   w.lz_evn = take<uint32_t>(V, B_LZEVN, NBLK, ok);
+  w.lz_bclient = seq ? take<uint32_t>(V, B_LZBCLIENT, NBLK, ok) : nullptr;
   w.lz_flag = take<uint32_t>(V, B_LZFLAG, NSEC, ok);
   w.lz_leave_hi = take<uint32_t>(V, B_LZLHI, NSEC, ok);
   w.lz_leave_lo = take<uint32_t>(V, B_LZLLO, NSEC, ok);
@@ -1452,7 +1458,8 @@ int run_lazy(ycrdt_engine* e, ycrdt_batch* b, bool merge, const std::vector<std:
   if (!ok) return fail(YCRDT_E_DEVICE, oom("lazy merge workspace"));
   if (merge) {
     mark(e, "lazy.merge");
-    if (D.nsections) launch_lazy_merge(w, D.nsections, D.nclients, s);
+    if (seq) launch_lazy_merge_seq(w, (uint32_t)SLOTS, (uint32_t)(NBLK - 1), s);
+    else if (D.nsections) launch_lazy_merge(w, D.nsections, D.nclients, s);
     else { w.lz_nblk = 0; w.lz_diff = 0; HIPCHK(hipMemsetAsync(w.lz_evbase, 0, sizeof(uint32_t) * 2, s)); }
   } else {
     std::vector<uint32_t> h(2 * sv.size() + nsvo + 2, 0);
@@ -1470,6 +1477,7 @@ int run_lazy(ycrdt_engine* e, ycrdt_batch* b, bool merge, const std::vector<std:
   }
   rc = check(e, c, merge ? "mergeUpdates" : "diffUpdate");
   if (rc) return rc;
+  if (seq) w.lz_nblk = c.lz_blocks;
   mark(e, "lazy.sizes");
   uint32_t nslots = 0;
   if (w.lz_nblk) launch_event_sizes(w, s, &nslots);

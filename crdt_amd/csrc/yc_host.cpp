@@ -132,7 +132,7 @@ void put_uint8array(std::string& o, const uint8_t* p, size_t n) {  // JSON.strin
 
 // lib0 readAny -> JSON text; returns false for `undefined` (the caller omits / nulls it)
 bool any_json(Rd& r, std::string& o, int depth) {
-  if (depth > 256) { r.ok = false; return false; }
+  if (depth > 4000) { r.ok = false; return false; }  // lib0 readAny recurses without a limit (V8 overflows its stack near here)
   const uint32_t tag = r.u8();
   switch (tag) {
     case 127: return false;  // undefined
@@ -187,7 +187,7 @@ bool any_json(Rd& r, std::string& o, int depth) {
 }
 
 bool skip_any(Rd& r, int depth) {
-  if (depth > 256) { r.ok = false; return false; }
+  if (depth > 4000) { r.ok = false; return false; }  // lib0 readAny recurses without a limit (V8 overflows its stack near here)
   const uint32_t tag = r.u8();
   switch (tag) {
     case 127: case 126: case 121: case 120: return r.ok;

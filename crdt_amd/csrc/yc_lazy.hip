@@ -42,7 +42,6 @@ __global__ void k_lz_runs(Work w, uint32_t nsections, uint32_t nclients) {
   const uint64_t k = w.lz_keys[i];
   const uint32_t r = (uint32_t)(k >> 32);
   if (i == 0 || (uint32_t)(w.lz_keys[i - 1] >> 32) != r) w.lz_rstart[r] = i;
-  if (i > 0 && w.lz_keys[i - 1] == k) raise_err(&w.ctr->err, ERR_UNSUPPORTED);  // two sections of one client in one update
   if (i == nsections - 1) w.lz_rstart[nclients] = nsections;
 }
 // one lane per update: previous non-empty section (arrival source), client-desc check
@@ -58,7 +57,6 @@ __global__ void k_lz_prev(Work w, uint32_t nupd) {
   uint32_t prev = NONE;
   for (uint32_t i = a; i < b; ++i) {
     const Section s = w.sections[i];
-    if (i > a && s.client >= w.sections[i - 1].client && s.n > 0) raise_err(&w.ctr->err, ERR_UNSUPPORTED);
     w.lz_prev[i] = prev;
     const uint32_t f = s.n ? first_nonskip(w, s.first_idx, s.n) : END;
     w.lz_first[i] = f;
@@ -211,13 +209,177 @@ __global__ __launch_bounds__(64) void k_lz_merge(Work w, uint32_t nclients, unsi
   }
 }
 
+// ---------------------------------------------------------------- non-canonical input: one loop
+// An update whose struct section holds two sections of one client, or sections out of the
+// descending client order Yjs writes, breaks the per-client split above (a reader may come back to
+// a higher client). Such input is valid for Yjs's readers, so it runs mergeUpdatesV2's loop
+// (Y@39011) as written, over all readers in one workgroup: each step picks the front reader
+// (client desc, clock asc, ties to the latest arrival — the stable re-sort), and the output
+// sections follow the lazy writer (a new section whenever the client changes, Y@38735).
+// k_lz_canon (run_decode) flags such input; it is rare, and the loop is serial.
+__global__ void k_lz_canon(Work w, uint32_t nupd) {
+  const uint32_t u = blockIdx.x * blockDim.x + threadIdx.x;
+  if (u >= nupd) return;
+  const uint32_t a = w.usec_start[u], b = a + w.usec_n[u];
+  uint32_t prev = NONE;
+  for (uint32_t i = a; i < b; ++i) {
+    const Section s = w.sections[i];
+    if (!s.n) continue;
+    if (prev != NONE && s.client >= prev) { w.ctr->noncanon = 1; return; }
+    prev = s.client;
+  }
+}
+__global__ __launch_bounds__(64) void k_lz_merge_seq(Work w, uint32_t nupd, uint32_t cap_ev, uint32_t cap_blk) {
+  __shared__ uint32_t rcur[LZ_KMAX], rend[LZ_KMAX], rhi[LZ_KMAX], rlo[LZ_KMAX];
+  const uint32_t lane = threadIdx.x;
+  const uint32_t K = nupd;
+  if (K > LZ_KMAX) { if (lane == 0) raise_err(&w.ctr->err, ERR_CAPACITY); return; }
+  auto skip_of = [&](uint32_t s) { return (w.s_info[s] & 31u) == REF_SKIP; };
+  for (uint32_t k = lane; k < K; k += 64) {  // reader k: the structs of update k, Skips filtered
+    const uint32_t a = w.usec_start[k], b = a + w.usec_n[k];
+    uint32_t first = END, tot = 0;
+    for (uint32_t t = a; t < b; ++t) {
+      const Section S = w.sections[t];
+      if (!S.n) continue;
+      if (first == END) first = S.first_idx;
+      tot += S.n;
+    }
+    uint32_t c = first, e = first == END ? END : first + tot;
+    if (first != END) while (c < e && skip_of(c)) ++c;
+    rcur[k] = (first == END || c >= e) ? END : c;
+    rend[k] = e;
+    rhi[k] = 0;
+    rlo[k] = 0xFFFFFFFFu - k;  // never moved: update order
+  }
+  __syncthreads();
+  auto client_of = [&](uint32_t s) { return w.sections[w.s_sec[s]].client; };
+  auto kind_of = [&](uint32_t s) -> uint32_t {
+    const uint32_t ref = w.s_info[s] & 31u;
+    return ref == REF_GC ? (uint32_t)REF_GC : ref == REF_SKIP ? (uint32_t)REF_SKIP : 1u;
+  };
+  uint32_t step = 0, evn = 0, nb = 0, last_client = 0;
+  bool fail = false;
+  auto emit = [&](const Cur& c, uint32_t client) {
+    if (evn >= cap_ev || nb >= cap_blk) { fail = true; return; }
+    if (evn == 0 || client != last_client) {
+      if (lane == 0) { w.lz_evbase[nb] = evn; w.lz_bclient[nb] = client; w.lz_evn[nb] = 0; }
+      ++nb;
+      last_client = client;
+    }
+    if (lane == 0) {
+      w.ev_kind[evn] = c.kind;
+      w.ev_src[evn] = c.src;
+      w.ev_clock[evn] = c.clock;
+      w.ev_len[evn] = c.len;
+      w.lz_evn[nb - 1] += 1;
+    }
+    ++evn;
+  };
+  auto advance = [&](uint32_t t) {
+    uint32_t c = rcur[t] + 1;
+    const uint32_t e = rend[t];
+    while (c < e && skip_of(c)) ++c;
+    ++step;
+    __syncthreads();
+    if (lane == 0) {
+      rcur[t] = c < e ? c : END;
+      rhi[t] = 1;
+      rlo[t] = step;
+    }
+    __syncthreads();
+  };
+  Cur cur{0, NONE, 0, 0};
+  uint32_t cur_client = 0;
+  bool have = false;
+  uint64_t guard = 0;
+  const uint64_t max_iter = 8ull * cap_ev + 64;
+  for (;;) {
+    if (++guard > max_iter || fail) { fail = true; break; }
+    // front reader: max client, then min clock, then the latest arrival (max stamp)
+    uint32_t bk = NONE, bcl = 0, bc = 0, bh = 0, bl = 0;
+    for (uint32_t k = lane; k < K; k += 64) {
+      const uint32_t s = rcur[k];
+      if (s == END) continue;
+      const uint32_t cl = client_of(s), c = w.s_clock[s], h = rhi[k], l = rlo[k];
+      if (bk == NONE || cl > bcl || (cl == bcl && (c < bc || (c == bc && (h > bh || (h == bh && l > bl)))))) {
+        bk = k; bcl = cl; bc = c; bh = h; bl = l;
+      }
+    }
+    for (int off = 32; off > 0; off >>= 1) {
+      const uint32_t ok = __shfl_xor(bk, off), ocl = __shfl_xor(bcl, off), oc = __shfl_xor(bc, off), oh = __shfl_xor(bh, off),
+                     ol = __shfl_xor(bl, off);
+      if (ok != NONE && (bk == NONE || ocl > bcl || (ocl == bcl && (oc < bc || (oc == bc && (oh > bh || (oh == bh && ol > bl))))))) {
+        bk = ok; bcl = ocl; bc = oc; bh = oh; bl = ol;
+      }
+    }
+    if (bk == NONE) break;  // every reader is exhausted
+    const uint32_t t = bk, first_client = bcl;
+    uint32_t n = rcur[t];
+    if (have) {
+      bool iterated = false;
+      const uint32_t cend = cur.clock + cur.len;
+      while (n != END && w.s_clock[n] + w.s_len[n] <= cend && client_of(n) >= cur_client) { advance(t); n = rcur[t]; iterated = true; }
+      if (n == END || client_of(n) != first_client || (iterated && w.s_clock[n] > cend)) continue;
+      if (first_client != cur_client) {
+        emit(cur, cur_client);
+        cur = Cur{kind_of(n), n, w.s_clock[n], w.s_len[n]};
+        cur_client = first_client;
+        advance(t);
+      } else {
+        const uint32_t nclock = w.s_clock[n], nlen = w.s_len[n];
+        if (cend < nclock) {  // gap
+          if (cur.kind == REF_SKIP) cur.len = nclock + nlen - cur.clock;
+          else { emit(cur, cur_client); cur = Cur{REF_SKIP, NONE, cend, nclock - cend}; }
+        } else {
+          const uint32_t diff = cend - nclock;
+          Cur nn{kind_of(n), n, nclock, nlen};
+          if (diff > 0) {
+            if (cur.kind == REF_SKIP) cur.len -= diff;
+            else { nn.clock += diff; nn.len -= diff; }  // sliceStruct
+          }
+          if (cur.kind == nn.kind && cur.kind != 1u) cur.len += nn.len;  // GC / Skip mergeWith (the reader stays)
+          else { emit(cur, cur_client); cur = nn; advance(t); }
+        }
+      }
+    } else {
+      cur = Cur{kind_of(n), n, w.s_clock[n], w.s_len[n]};
+      cur_client = first_client;
+      have = true;
+      advance(t);
+    }
+    // consecutive structs of the front reader are written without re-sorting
+    n = rcur[t];
+    while (n != END && client_of(n) == first_client && w.s_clock[n] == cur.clock + cur.len && kind_of(n) != REF_SKIP) {
+      emit(cur, cur_client);
+      cur = Cur{kind_of(n), n, w.s_clock[n], w.s_len[n]};
+      advance(t);
+      n = rcur[t];
+    }
+  }
+  if (have && !fail) emit(cur, cur_client);
+  if (lane == 0) {
+    if (fail) raise_err(&w.ctr->err, ERR_CAPACITY);
+    w.lz_evbase[nb] = evn;
+    w.ctr->lz_blocks = nb;
+  }
+}
+
 // ---------------------------------------------------------------- diffUpdate events
-// one lane per section: the section's events live at lz_evbase[section]
+// One lane per section: the section's events live at lz_evbase[section]. Yjs's reader runs on
+// while the client stays the same (diffUpdateV2, Y@40711: `while (reader.curr.id.client ===
+// currClient)`), so adjacent sections of one client (a layout Yjs never writes, but reads) are one
+// run: its first section's lane handles all of them and the others stay empty.
+__device__ __forceinline__ bool lz_run_start(const Work& w, uint32_t i) {
+  return i == 0 || w.sections[i - 1].upd != w.sections[i].upd || w.sections[i - 1].client != w.sections[i].client;
+}
 __global__ void k_lz_diff(Work w, uint32_t nsections) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= nsections) return;
   const Section S = w.sections[i];
   const uint32_t base = w.lz_evbase[i];
+  if (!lz_run_start(w, i)) { w.lz_evn[i] = 0; return; }
+  uint32_t j = i + 1, nrun = S.n;  // the run: sections [i, j)
+  while (j < nsections && !lz_run_start(w, j)) nrun += w.sections[j++].n;
   uint32_t svc = 0;  // target state of this client (lz_multi: in this update's own state vector)
   {
     const uint32_t sv0 = w.lz_multi ? w.sv_off[S.upd] : 0u, sv1 = w.lz_multi ? w.sv_off[S.upd + 1] : w.sv_n;
@@ -226,25 +388,47 @@ __global__ void k_lz_diff(Work w, uint32_t nsections) {
     if (lo < sv1 && w.sv_client[lo] == S.client) svc = w.sv_clock[lo];
   }
   uint32_t evn = 0;
-  // first struct (non-Skip) that ends past the target state: binary search on the clocks
-  uint32_t lo = S.first_idx, hi = S.first_idx + S.n;
-  while (lo < hi) { const uint32_t m = (lo + hi) >> 1; if (w.s_clock[m] + w.s_len[m] <= svc) lo = m + 1; else hi = m; }
-  while (lo < S.first_idx + S.n && (w.s_info[lo] & 31u) == REF_SKIP) ++lo;
-  for (uint32_t j = lo; j < S.first_idx + S.n; ++j) {
-    const uint32_t ref = w.s_info[j] & 31u;
-    const uint32_t off = (j == lo && svc > w.s_clock[j]) ? svc - w.s_clock[j] : 0u;
+  auto put = [&](uint32_t j2, uint32_t off) {
+    const uint32_t ref = w.s_info[j2] & 31u;
     w.ev_kind[base + evn] = ref == REF_GC ? (uint32_t)REF_GC : ref == REF_SKIP ? (uint32_t)REF_SKIP : 1u;
-    w.ev_src[base + evn] = j;
-    w.ev_clock[base + evn] = w.s_clock[j] + off;
-    w.ev_len[base + evn] = w.s_len[j] - off;
+    w.ev_src[base + evn] = j2;
+    w.ev_clock[base + evn] = w.s_clock[j2] + off;
+    w.ev_len[base + evn] = w.s_len[j2] - off;
     ++evn;
+  };
+  if (j == i + 1) {
+    // one section (clocks ascending): the first struct (non-Skip) that ends past the target state by
+    // a binary search, then everything after it
+    uint32_t lo = S.first_idx, hi = S.first_idx + S.n;
+    while (lo < hi) { const uint32_t m = (lo + hi) >> 1; if (w.s_clock[m] + w.s_len[m] <= svc) lo = m + 1; else hi = m; }
+    while (lo < S.first_idx + S.n && (w.s_info[lo] & 31u) == REF_SKIP) ++lo;
+    for (uint32_t k = lo; k < S.first_idx + S.n; ++k) put(k, (k == lo && svc > w.s_clock[k]) ? svc - w.s_clock[k] : 0u);
+  } else {
+    // several sections: Yjs's loop struct by struct (clocks need not ascend across sections)
+    uint32_t k = 0;
+    for (uint32_t t = i; t < j; ++t)
+      if (w.sections[t].n) { k = w.sections[t].first_idx; break; }  // (empty sections have no first struct)
+    const uint32_t kend = k + nrun;
+    bool writing = false;
+    while (k < kend) {
+      if (writing) { put(k++, 0); continue; }
+      const uint32_t c = w.s_clock[k], l = w.s_len[k];
+      if ((w.s_info[k] & 31u) == REF_SKIP) { ++k; continue; }
+      if (c + l > svc) { put(k++, svc > c ? svc - c : 0u); writing = true; }
+      else while (k < kend && w.s_clock[k] + w.s_len[k] <= svc) ++k;
+    }
   }
   w.lz_evn[i] = evn;
 }
 __global__ void k_lz_diff_cap(Work w, uint32_t nsections) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i > nsections) return;
-  w.lz_cap[i] = i < nsections ? w.sections[i].n : 0u;
+  uint32_t n = 0;
+  if (i < nsections && lz_run_start(w, i)) {
+    n = w.sections[i].n;
+    for (uint32_t j = i + 1; j < nsections && !lz_run_start(w, j); ++j) n += w.sections[j].n;
+  }
+  w.lz_cap[i] = n;
 }
 
 // ---------------------------------------------------------------- event encoding
@@ -312,6 +496,7 @@ __device__ uint32_t encode_event(const Work& w, uint32_t client, uint32_t e, uin
 
 // block b (client rank for merge, section for diff): its client id
 __device__ __forceinline__ uint32_t blk_client(const Work& w, uint32_t b) {
+  if (w.lz_bclient) return w.lz_bclient[b];  // the serial merge's output sections
   return w.lz_diff ? w.sections[b].client : w.cl_vals[w.lz_nblk - 1 - b];
 }
 // event slots [evbase[b], evbase[b] + cap[b]); slots past evn[b] are empty
@@ -495,6 +680,14 @@ void launch_lazy_merge(Work& w, uint32_t nsections, uint32_t nclients, hipStream
   OrderedIds o;
   if (!ordered_ids(nclients, s, o)) { hipMemsetAsync(&w.ctr->err, ERR_CAPACITY, 1, s); return; }
   hipLaunchKernelGGL(k_lz_merge, dim3(nclients), dim3(64), 0, s, w, nclients, o.ctr, o.base);
+}
+// non-canonical input (k_lz_canon): the serial loop; the block count comes back in ctr->lz_blocks
+void launch_lazy_merge_seq(Work& w, uint32_t cap_ev, uint32_t cap_blk, hipStream_t s) {
+  w.lz_diff = 0;
+  hipLaunchKernelGGL(k_lz_merge_seq, dim3(1), dim3(64), 0, s, w, w.nupd, cap_ev, cap_blk);
+}
+void launch_lazy_canon(Work& w, hipStream_t s) {
+  if (w.nupd) hipLaunchKernelGGL(k_lz_canon, dim3(G(w.nupd)), dim3(256), 0, s, w, w.nupd);
 }
 
 // diffUpdate: one block per section of the single input update

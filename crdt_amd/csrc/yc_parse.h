@@ -71,6 +71,10 @@ YC_HDI void skip_bytes(uint32_t& p, uint32_t n, uint32_t end, bool& ok) {
 // nesting fails the parse: speculative callers use a shallow stack, exact callers a deep one).
 template <int DEPTH>
 YC_HD inline bool skip_any(const uint8_t* __restrict__ b, uint32_t& p, uint32_t end, uint32_t& steps) {
+  // A level is kept only while members FOLLOW the one being read (rem[d] >= 1): the last member of
+  // a container is read in the container's place (a tail position), so nesting along last members
+  // — [[[..]]], {a: {b: ..}}, however deep — takes no stack, and DEPTH bounds only containers
+  // nested inside members that are not their container's last.
   uint32_t rem[DEPTH];
   uint32_t objmask = 0;  // bit d set: level d is an object (key before each member)
   int d = 0;
@@ -91,10 +95,12 @@ YC_HD inline bool skip_any(const uint8_t* __restrict__ b, uint32_t& p, uint32_t 
         uint32_t n = rd_vu(b, p, end, ok);
         if (!ok) return false;
         if (n > 0) {
-          if (d == DEPTH) { steps = 0; return false; }  // too deep: "unknown" (-1), never "malformed"
-          rem[d] = n;
-          if (tag == 118) objmask |= 1u << d; else objmask &= ~(1u << d);
-          ++d;
+          if (n > 1) {  // members follow this one: keep the level
+            if (d == DEPTH) { steps = 0; return false; }  // too deep: "unknown" (-1), never "malformed"
+            rem[d] = n - 1;
+            if (tag == 118) objmask |= 1u << d; else objmask &= ~(1u << d);
+            ++d;
+          }
           if (tag == 118) { uint32_t k = rd_vu(b, p, end, ok); if (ok) skip_bytes(p, k, end, ok); }
           if (!ok) return false;
           continue;  // read the first member value
@@ -104,16 +110,12 @@ YC_HD inline bool skip_any(const uint8_t* __restrict__ b, uint32_t& p, uint32_t 
       default: return false;
     }
     if (!ok) return false;
-    // a value completed: pop finished containers
-#pragma unroll 1
-    for (;;) {
-      if (d == 0) return true;
-      if (--rem[d - 1] > 0) {
-        if ((objmask >> (d - 1)) & 1u) { uint32_t k = rd_vu(b, p, end, ok); if (ok) skip_bytes(p, k, end, ok); if (!ok) return false; }
-        break;  // next member value
-      }
-      --d;
-    }
+    // a value completed: the innermost kept level moves to its next member (the last one is read
+    // in the level's place)
+    if (d == 0) return true;
+    const uint32_t lvl = (uint32_t)d - 1;
+    if ((objmask >> lvl) & 1u) { uint32_t k = rd_vu(b, p, end, ok); if (ok) skip_bytes(p, k, end, ok); if (!ok) return false; }
+    if (--rem[lvl] == 0) --d;
   }
 }
 

@@ -39,6 +39,8 @@ struct Counters {            // device-side counters, read back at the few host 
   uint32_t pad[12];          // encode scratch (see yc_encode.hip)
   uint32_t climb_open[40];   // per pointer-jumping round of the YArray climb: pairs still open (yc_yata.hip)
   uint32_t sync_changed[8];  // per k_sync round: some chunk's chain exit changed (yc_decode.hip)
+  uint32_t noncanon;          // lazy decode: an update's sections are not in strictly descending client order
+  uint32_t lz_blocks;         // serial lazy merge: output sections
   unsigned long long out_total; // encoded output size (integrate encoder; 64-bit)
   unsigned long long ds_base;   // integrate encoder: byte position of the delete-set section
   unsigned long long items;  // Σ clock lengths of Skip structs (items = Σ all lengths − this)
@@ -236,6 +238,7 @@ struct Work {
   uint32_t* lz_leave_lo = nullptr;
   uint32_t lz_nblk = 0, lz_diff = 0;
   uint32_t lz_multi = 0;            // 1: one diffUpdate per input update (sync responder batch); no global headers
+  uint32_t* lz_bclient = nullptr;   // serial lazy merge: client of every output section (null: per-client blocks)
   uint32_t* ev_kind = nullptr;     // [slots] REF_GC | REF_SKIP | 1 (item)
   uint32_t* ev_src = nullptr;
   uint32_t* ev_clock = nullptr;
@@ -550,6 +553,8 @@ void scan_segmax_u64(void* tmp, size_t tmpb, const uint64_t* in, uint64_t* out, 
 
 // lazy merge (yc_lazy.hip)
 void launch_lazy_merge(Work& w, uint32_t nsections, uint32_t nclients, hipStream_t s);
+void launch_lazy_merge_seq(Work& w, uint32_t cap_ev, uint32_t cap_blk, hipStream_t s);
+void launch_lazy_canon(Work& w, hipStream_t s);
 void launch_lazy_diff(Work& w, uint32_t nsections, hipStream_t s);
 uint32_t launch_event_sizes(Work& w, hipStream_t s, uint32_t* nslots_out);
 uint32_t launch_ds_runs(Work& w, uint32_t nds, bool merge, hipStream_t s);

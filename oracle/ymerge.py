@@ -72,26 +72,39 @@ class Dec:
         return self.b[st:self.p]
 
     def _any(self):
-        t = self.u8()
-        if t in (127, 126, 121, 120):
-            return
-        if t == 125:
-            self.vi()
-        elif t == 124:
-            self.raw(4)
-        elif t in (123, 122):
-            self.raw(8)
-        elif t in (119, 116):
-            self.raw(self.vu())
-        elif t == 118:
-            for _ in range(self.vu()):
-                self.vstr_raw()
-                self._any()
-        elif t == 117:
-            for _ in range(self.vu()):
-                self._any()
-        else:
-            raise ValueError("Unexpected case")
+        # readAny (L0@1937) recurses without a limit: an explicit stack of [members left, is object]
+        stack = []
+        while True:
+            t = self.u8()
+            if t in (127, 126, 121, 120):
+                pass
+            elif t == 125:
+                self.vi()
+            elif t == 124:
+                self.raw(4)
+            elif t in (123, 122):
+                self.raw(8)
+            elif t in (119, 116):
+                self.raw(self.vu())
+            elif t in (117, 118):
+                n = self.vu()
+                if n:
+                    stack.append([n, t == 118])
+                    if t == 118:
+                        self.vstr_raw()
+                    continue
+            else:
+                raise ValueError("Unexpected case")
+            while stack:  # a value completed: the next member of the innermost open container
+                top = stack[-1]
+                top[0] -= 1
+                if top[0]:
+                    if top[1]:
+                        self.vstr_raw()
+                    break
+                stack.pop()
+            if not stack:
+                return
 
 
 def wvu(out, v):

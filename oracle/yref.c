@@ -118,7 +118,7 @@ static const uint8_t *dbytes(dec_t *d, uint32_t n) {
 }
 /* skips one lib0 `any` (readAny B) */
 static void dskip_any(dec_t *d, int depth) {
-  if (depth > 512) { d->err = 1; return; }
+  if (depth > 20000) { d->err = 1; return; }  /* lib0 readAny recurses without a limit */
   uint8_t t = du8(d);
   if (d->err) return;
   switch (t) {

@@ -132,3 +132,56 @@ def test_oracle_config_fixtures():
         for root, val in c["json"].items():
             kind = "array" if isinstance(val, list) else "map"
             assert _json.loads(d.root_json(root, kind)) == val, (c["name"], root)
+
+
+def _edges():
+    import json as _json
+    import os as _os
+    import sys as _sys
+
+    _sys.setrecursionlimit(max(_sys.getrecursionlimit(), 20000))  # 2 000-level JSON values
+    with open(_os.path.join(_os.path.dirname(__file__), "golden", "edges.json")) as f:
+        return _json.load(f)["cases"]
+
+
+def test_oracle_edge_fixtures_apply():
+    """Deep `any` values and non-canonical section layouts (tests/golden/edges.json, Yjs 13.5.16):
+    Y.applyUpdate results."""
+    import json as _json
+
+    checked = 0
+    for c in _edges():
+        groups = [(c["updates"], "")] if c["kind"] == "deep" else [([c["update"]], ""), ([c["update"]] + c["others"], "_with_others")]
+        for ups, sfx in groups:
+            d = Doc(0x7FFFFFF0)
+            try:
+                for u in ups:
+                    d.apply_update(bytes.fromhex(u))
+            except OracleError as e:  # the oracle has no pending store: those are pinned on the GPU
+                assert e.code == -2, (c["name"], sfx)  # side against the fixture (test_gpu_edges_fixtures)
+                continue
+            checked += 1
+            assert d.encode_state_as_update().hex() == c["state" + sfx], (c["name"], sfx)
+            assert d.encode_state_vector().hex() == c["sv" + sfx], (c["name"], sfx)
+            for root, kind in c["roots"].items():
+                assert _json.loads(d.root_json(root, kind)) == c["json" + sfx][root], (c["name"], root)
+    assert checked >= 10
+
+
+def test_oracle_edge_fixtures_lazy():
+    """The same inputs through mergeUpdates / diffUpdate (oracle/ymerge.py), Yjs's raw bytes."""
+    from oracle.ymerge import diff_update, merge_updates
+
+    for c in _edges():
+        if c["kind"] == "deep":
+            ups = [bytes.fromhex(u) for u in c["updates"]]
+            assert merge_updates(ups).hex() == c["merged_raw"], c["name"]
+            continue
+        x = bytes.fromhex(c["update"])
+        others = [bytes.fromhex(u) for u in c["others"]]
+        assert merge_updates([x] + others).hex() == c["merged_with_others_raw"], c["name"]
+        assert merge_updates(others + [x]).hex() == c["merged_others_first_raw"], c["name"]
+        assert merge_updates([x, x]).hex() == c["merged_pair_raw"], c["name"]
+        assert diff_update(x, b"\x00").hex() == c["diff_empty_raw"], c["name"]
+        assert diff_update(x, bytes.fromhex(c["diff_sv_of"])).hex() == c["diff_sv_raw"], c["name"]
+        assert diff_update(x, bytes.fromhex(c["diff_hi1_of"])).hex() == c["diff_hi1_raw"], c["name"]
