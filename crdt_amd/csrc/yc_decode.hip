@@ -1746,6 +1746,19 @@ __global__ void k_ds_bound(Work w) {  // region size per update: (delete-set byt
   const uint32_t st = w.dsstart[u];
   w.scratch[u] = st == NONE ? 0 : (w.uoff[u] + w.ulen[u] - st + 1) / 2;
   w.ds_count[u] = 0;
+  // Sections out of strictly descending client order (Yjs never writes them; its readers accept
+  // them): mergeUpdates / diffUpdate take the serial loop (ctr->noncanon, yc_lazy.hip), and
+  // applyUpdate keeps only the LAST section of a client (readClientsStructRefs' Map.set, Y@19286):
+  // an earlier one is marked superseded (pad = 1) and its structs decode as Skips
+  const uint32_t a = w.usec_start[u], b = a + w.usec_n[u];
+  bool canon = true;
+  for (uint32_t i = a + 1; i < b && canon; ++i) canon = w.sections[i].client < w.sections[i - 1].client;
+  if (canon) return;
+  w.ctr->noncanon = 1;
+  if (w.lazy) return;
+  for (uint32_t i = a; i < b; ++i)
+    for (uint32_t j = i + 1; j < b; ++j)
+      if (w.sections[j].client == w.sections[i].client) { w.sections[i].pad = 1; break; }
 }
 __global__ void k_ds_compact(Work w) {  // one wave per update: region -> dense ds[]
   const uint32_t lane = threadIdx.x & 63;
@@ -1886,6 +1899,10 @@ __global__ __launch_bounds__(256) void k_struct_decode(Work w, uint32_t nstructs
   uint32_t p = p0;
   const int pr = parse_struct<true, 32, WinSrc>(WinSrc{bw, slot, s0}, p, uend, 0xFFFFFFFFu, &v);
   if (pr <= 0) { raise_err(err, pr == -1 ? ERR_UNSUPPORTED : ERR_DECODE); return; }  // -1: any nested > 32 deep
+  if (sec.pad && !w.lazy) {  // a superseded section (k_ds_bound): its structs are not integrated
+    v.info = (uint8_t)((v.info & 0xE0u) | REF_SKIP);
+    v.ref = REF_SKIP;
+  }
   w.s_len[i] = v.len;
   w.s_info[i] = v.info;
   w.s_cidx[i] = sec.cidx;

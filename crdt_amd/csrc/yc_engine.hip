@@ -947,7 +947,6 @@ int run_decode(ycrdt_engine* e, ycrdt_batch* b, bool lazy, Decoded& D, bool gene
     HIPCHK(hipMemsetAsync(w.cl_start, 0, sizeof(uint32_t) * (nsections + 1), s));
   }
   HIPCHK(hipStreamWaitEvent(s, e->side_done, 0));
-  if (lazy) launch_lazy_canon(w, s);  // sections out of the descending client order (yc_lazy.hip)
   rc = check(e, c, "struct decode");
   if (rc) return rc;
   D.noncanon = c.noncanon;

@@ -216,19 +216,7 @@ __global__ __launch_bounds__(64) void k_lz_merge(Work w, uint32_t nclients, unsi
 // (Y@39011) as written, over all readers in one workgroup: each step picks the front reader
 // (client desc, clock asc, ties to the latest arrival — the stable re-sort), and the output
 // sections follow the lazy writer (a new section whenever the client changes, Y@38735).
-// k_lz_canon (run_decode) flags such input; it is rare, and the loop is serial.
-__global__ void k_lz_canon(Work w, uint32_t nupd) {
-  const uint32_t u = blockIdx.x * blockDim.x + threadIdx.x;
-  if (u >= nupd) return;
-  const uint32_t a = w.usec_start[u], b = a + w.usec_n[u];
-  uint32_t prev = NONE;
-  for (uint32_t i = a; i < b; ++i) {
-    const Section s = w.sections[i];
-    if (!s.n) continue;
-    if (prev != NONE && s.client >= prev) { w.ctr->noncanon = 1; return; }
-    prev = s.client;
-  }
-}
+// k_ds_bound (yc_decode.hip) flags such input; it is rare, and the loop is serial.
 __global__ __launch_bounds__(64) void k_lz_merge_seq(Work w, uint32_t nupd, uint32_t cap_ev, uint32_t cap_blk) {
   __shared__ uint32_t rcur[LZ_KMAX], rend[LZ_KMAX], rhi[LZ_KMAX], rlo[LZ_KMAX];
   const uint32_t lane = threadIdx.x;
@@ -686,9 +674,7 @@ void launch_lazy_merge_seq(Work& w, uint32_t cap_ev, uint32_t cap_blk, hipStream
   w.lz_diff = 0;
   hipLaunchKernelGGL(k_lz_merge_seq, dim3(1), dim3(64), 0, s, w, w.nupd, cap_ev, cap_blk);
 }
-void launch_lazy_canon(Work& w, hipStream_t s) {
-  if (w.nupd) hipLaunchKernelGGL(k_lz_canon, dim3(G(w.nupd)), dim3(256), 0, s, w, w.nupd);
-}
+
 
 // diffUpdate: one block per section of the single input update
 void launch_lazy_diff(Work& w, uint32_t nsections, hipStream_t s) {

@@ -554,7 +554,6 @@ void scan_segmax_u64(void* tmp, size_t tmpb, const uint64_t* in, uint64_t* out, 
 // lazy merge (yc_lazy.hip)
 void launch_lazy_merge(Work& w, uint32_t nsections, uint32_t nclients, hipStream_t s);
 void launch_lazy_merge_seq(Work& w, uint32_t cap_ev, uint32_t cap_blk, hipStream_t s);
-void launch_lazy_canon(Work& w, hipStream_t s);
 void launch_lazy_diff(Work& w, uint32_t nsections, hipStream_t s);
 uint32_t launch_event_sizes(Work& w, hipStream_t s, uint32_t* nslots_out);
 uint32_t launch_ds_runs(Work& w, uint32_t nds, bool merge, hipStream_t s);
