@@ -1594,13 +1594,6 @@ __global__ void k_section_rank(Work w, uint32_t nsections) {
   sec->first_idx = rank_incl(fbits, win_words(w.wcnt, uw), p) - 1;
   w.sec_sorted[rank_incl(win_words(w.sec_bits, uw), win_words(w.wsec, uw), p) - 1] = i;
 }
-__global__ void k_struct_sec(Work w, uint32_t nstructs) {
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= nstructs) return;
-  const uint32_t p = w.s_pos[i], uw = w.nwin > 1 ? w.s_win[i] : 0u;
-  w.s_sec[i] = w.sec_sorted[rank_incl(win_words(w.sec_bits, uw), win_words(w.wsec, uw), p) - 1];
-}
-
 // before the count sync: struct / section-start counts (popcount prefix of the bitmaps)
 void launch_struct_count(const Work& w, hipStream_t s) {
   const uint32_t nwords = (w.nbytes + 63) / 64;
@@ -1880,7 +1873,12 @@ __global__ __launch_bounds__(256) void k_struct_decode(Work w, uint32_t nstructs
   if (i >= nstructs) return;
   const uint32_t nclients = w.ctr->nclients;
   uint32_t* err = &w.ctr->err;
-  const uint32_t p0 = w.s_pos[i], si = w.s_sec[i];
+  const uint32_t p0 = w.s_pos[i];
+  // the struct's section: the section starts at or before it (rank in the section-start bitmap);
+  // written here for the later passes (the separate k_struct_sec pass re-read every position)
+  const uint32_t si = w.sec_sorted[rank_incl(win_words(w.sec_bits, w.nwin > 1 ? w.s_win[i] : 0u),
+                                             win_words(w.wsec, w.nwin > 1 ? w.s_win[i] : 0u), p0) - 1];
+  w.s_sec[i] = si;
   // the struct's bytes (they depend on its position only) are fetched beside its section record
   __shared__ __attribute__((aligned(16))) uint32_t win[256 * SD_STRIDE];
   uint32_t* slot = win + threadIdx.x * SD_STRIDE;
@@ -1938,7 +1936,23 @@ __global__ __launch_bounds__(256) void k_struct_decode(Work w, uint32_t nstructs
   if (pk != 0 && !v.has_psub) w.ctr->narray_roots = 1;  // a YArray list may exist (flag, plain store)
   if (pk == 2) w.ctr->nested = 1;                        // a nested type's list (flag, plain store)
   wave_count_add_sharded(w.ctr->nroots_sh, pk != 0);
-  w.s_pk[i] = (uint8_t)pk;
+  // the header as Item.write re-encodes it (every varuint in shortest form): an overlong varuint
+  // (valid lib0 input) makes the input's header bytes differ from the output's, so such a struct
+  // is flagged (s_pk bit 7) and never takes the encoder's byte-copy path
+  bool canon_hdr = true;
+  if (item) {
+    uint32_t h = 0;
+    if (v.info & 0x80u) h += vu_size(v.oc) + vu_size(v.ok_);
+    if (v.info & 0x40u) h += vu_size(v.rc) + vu_size(v.rk);
+    if ((v.info & 0xC0u) == 0) {
+      h += 1;  // parent info (1: root type name, 0: parent item id)
+      if (v.pkind == 1) { uint32_t q = v.pa; bool okq = true; const uint32_t n = WinSrc{bw, slot, s0}.vu(q, uend, okq); h += vu_size(n) + n; }
+      else h += vu_size(v.pa) + vu_size(v.pb);
+      if (v.has_psub) { uint32_t q = v.psub_pos; bool okq = true; const uint32_t n = WinSrc{bw, slot, s0}.vu(q, uend, okq); h += vu_size(n) + n; }
+    }
+    canon_hdr = h == v.cpos - p0 - 1;
+  }
+  w.s_pk[i] = (uint8_t)(pk | (canon_hdr ? 0u : 0x80u));
   if (pk != 0) {
     w.s_pa[i] = pa;
     w.s_pb[i] = pb;
@@ -1952,37 +1966,37 @@ __global__ __launch_bounds__(256) void k_struct_decode(Work w, uint32_t nstructs
   w.s_celem[i] = celem;
 }
 
-__global__ void k_struct_clock(Work w, uint32_t nstructs) {
+// Clocks from the section start and the length prefix; with `states` (integrate mode) also the
+// client states (k_states' work, folded in: the clock and length are in registers here)
+__global__ void k_struct_clock(Work w, uint32_t nstructs, uint32_t states) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= nstructs) return;
-  const Section sec = w.sections[w.s_sec[i]];
+  const uint32_t si = w.s_sec[i];
+  const Section sec = w.sections[si];
   const uint64_t off = w.s_lenscan[i] - w.s_lenscan[sec.first_idx];
   const uint64_t clock = (uint64_t)sec.clock + off;
-  const uint64_t endc = clock + w.s_len[i];
+  const uint32_t len = w.s_len[i];
+  const uint64_t endc = clock + len;
   if (endc > 0xFFFFFFFFull) { raise_err(&w.ctr->err, ERR_DECODE); return; }
   w.s_clock[i] = (uint32_t)clock;
+  if (!states) return;
+  const uint32_t ref = w.s_info[i] & 31u;
+  if (ref == REF_SKIP) {  // rare: Skip lengths are subtracted from the item count
+    atomicAdd(&w.ctr->items, (unsigned long long)len);
+    return;
+  }
+  // clocks grow along a section: only the last non-skip struct of a run can hold the max
+  const bool last = i + 1 == nstructs || w.s_sec[i + 1] != si || (w.s_info[i + 1] & 31u) == REF_SKIP;
+  if (last) atomicMax(&w.cl_state[w.s_cidx[i]], (uint32_t)endc);
 }
 
 void launch_struct_decode(const Work& w, uint32_t nstructs, hipStream_t s) {
   if (!nstructs) return;
-  hipLaunchKernelGGL(k_struct_sec, dim3((nstructs + 255) / 256), dim3(256), 0, s, w, nstructs);
   hipLaunchKernelGGL(k_struct_decode, dim3((nstructs + 255) / 256), dim3(256), 0, s, w, nstructs);
   scan_u32_to_u64(w.tmp, w.tmp_bytes, w.s_len, w.s_lenscan, nstructs + 1, s);
-  hipLaunchKernelGGL(k_struct_clock, dim3((nstructs + 255) / 256), dim3(256), 0, s, w, nstructs);
 }
 
 // --------------------------------------------------------------------------- client states
-__global__ void k_states(Work w, uint32_t nstructs) {
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= nstructs) return;
-  if ((w.s_info[i] & 31u) == REF_SKIP) {  // rare: Skip lengths are subtracted from the item count
-    atomicAdd(&w.ctr->items, (unsigned long long)w.s_len[i]);
-    return;
-  }
-  // clocks grow along a section: only the last non-skip struct of a run can hold the max
-  const bool last = i + 1 == nstructs || w.s_sec[i + 1] != w.s_sec[i] || (w.s_info[i + 1] & 31u) == REF_SKIP;
-  if (last) atomicMax(&w.cl_state[w.s_cidx[i]], w.s_clock[i] + w.s_len[i]);
-}
 // Yjs pending structs (yc_ingest.h): every client is integrated up to its cap only
 __global__ void k_apply_caps(Work w) {
   const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
@@ -1998,8 +2012,11 @@ __global__ void k_state_totals(Work w, uint32_t nstructs) {  // U and Σ input l
 }
 // NC <= nsections: the states are zero past NC, so a scan over nsections + 1 entries gives cl_base
 // cl_state must be zero on entry (the caller's fill)
+void launch_struct_clocks(const Work& w, uint32_t nstructs, hipStream_t s) {  // lazy mode: clocks only
+  if (nstructs) hipLaunchKernelGGL(k_struct_clock, dim3((nstructs + 255) / 256), dim3(256), 0, s, w, nstructs, 0u);
+}
 void launch_states(const Work& w, uint32_t nstructs, uint32_t nsections, hipStream_t s) {
-  if (nstructs) hipLaunchKernelGGL(k_states, dim3((nstructs + 255) / 256), dim3(256), 0, s, w, nstructs);
+  if (nstructs) hipLaunchKernelGGL(k_struct_clock, dim3((nstructs + 255) / 256), dim3(256), 0, s, w, nstructs, 1u);
   if (w.capped && nsections) hipLaunchKernelGGL(k_apply_caps, dim3(nsections / 256 + 1), dim3(256), 0, s, w);
   scan_u32_to_u64(w.tmp, w.tmp_bytes, w.cl_state, w.cl_base, nsections + 1, s);
   hipLaunchKernelGGL(k_state_totals, dim3(1), dim3(1), 0, s, w, nstructs);

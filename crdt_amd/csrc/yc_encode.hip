@@ -39,7 +39,41 @@ __device__ __forceinline__ uint64_t copy_bytes(uint8_t* __restrict__ o, uint64_t
 // Encodes output struct `o` (segments [a,b)) at position p when WRITE, returns the size
 // (Item.write Y@80416 / GC.write Y@68955 with the writeStructs offset, Y@18809).
 template <bool WRITE>
-__device__ uint32_t encode_struct(const Work& w, uint32_t nclients, uint32_t o, uint8_t* __restrict__ out, uint64_t p0) {
+__device__ uint32_t encode_struct_general(const Work& w, uint32_t nclients, uint32_t o, uint8_t* __restrict__ out, uint64_t p0);
+
+// The common output struct is one WHOLE source item (one segment from the struct's first unit to
+// its last, full-state encode): Item.write then emits the input's own bytes — its origin, right
+// origin, parent and parentSub fields are the ones it was decoded from — except the info byte
+// (content ref -> Deleted when the item is deleted now; the parentSub bit, which lazily merged
+// input drops on items with an origin) and, for a deleted item, the content (ContentDeleted: its
+// length). So it is a copy of [pos + 1, cpos) and [cpos, cend) — five columns instead of the
+// general path's twenty (and its reference-client lookups).
+template <bool WRITE>
+__device__ __forceinline__ uint32_t encode_struct(const Work& w, uint32_t nclients, uint32_t o, uint8_t* __restrict__ out, uint64_t p0) {
+  const uint32_t a = w.o_first[o], b = w.o_first[o + 1];
+  if (b == a + 1 && !w.delta) {
+    const uint32_t f = w.g_flags[a], src = w.g_src[a], ga = w.g_start[a], gb = w.g_start[b];
+    const uint32_t slen = w.s_len[src], spos = w.s_pos[src], scpos = w.s_cpos[src], scend = w.s_cend[src];
+    const uint32_t info0 = w.s_info[src], spk = w.s_pk[src];
+    if ((f & (SEG_ITEM | SEG_EXPLICIT)) == (SEG_ITEM | SEG_EXPLICIT) && gb - ga == slen && !(spk & 0x80u)) {
+      const bool del = (f & SEG_DEL) != 0;
+      const uint32_t hdr = scpos - spos - 1;  // origin / right origin / parent / parentSub bytes
+      if (!WRITE) return 1 + hdr + (del ? vu_size(slen) : scend - scpos);
+      const uint8_t* __restrict__ sb = struct_bytes(w, src);
+      uint64_t p = p0;
+      out[p++] = (uint8_t)((del ? (uint32_t)REF_DELETED : (info0 & 31u)) | (info0 & 0xC0u) | ((f & SEG_PSUB) ? 0x20u : 0u));
+      p = copy_bytes(out, p, sb + spos + 1, hdr);
+      if (del) p = wr_vu(out, p, slen);
+      else p = copy_bytes(out, p, sb + scpos, scend - scpos);
+      return (uint32_t)(p - p0);
+    }
+  }
+  return encode_struct_general<WRITE>(w, nclients, o, out, p0);
+}
+
+template <bool WRITE>
+__device__ __forceinline__ uint32_t encode_struct_general(const Work& w, uint32_t nclients, uint32_t o, uint8_t* __restrict__ out,
+                                                                    uint64_t p0) {
   // The columns a struct can need are loaded in three dependent rounds — its first segment's row,
   // then its source struct's and its client's, then the reference clients' — each round issued
   // whole before anything branches on it, instead of one memory round trip per field.
@@ -108,9 +142,12 @@ __device__ uint32_t encode_struct(const Work& w, uint32_t nclients, uint32_t o, 
   }
   if (!has_o && !has_r) {  // parent info (root type name | parent item id) + parentSub
     const uint32_t pa = w.s_pa[src], pb = w.s_pb[src];
-    if (w.s_pk[src] == 1) {
-      if (WRITE) { out[p++] = 1; p = copy_bytes(out, p, sb + pa, pb); }
-      size += 1 + pb;
+    if ((w.s_pk[src] & 3u) == 1) {  // writeVarString(name): the length prefix in shortest form
+      uint32_t q = pa;
+      bool okq = true;
+      const uint32_t n = rd_vu(sb, q, pa + pb, okq);
+      if (WRITE) { out[p++] = 1; p = wr_vu(out, p, n); p = copy_bytes(out, p, sb + q, n); }
+      size += 1 + vu_size(n) + n;
     } else {
       const uint32_t pc = w.cl_vals[pa];
       if (WRITE) { out[p++] = 0; p = wr_vu(out, p, pc); p = wr_vu(out, p, pb); }
@@ -118,8 +155,11 @@ __device__ uint32_t encode_struct(const Work& w, uint32_t nclients, uint32_t o, 
     }
     if (psub) {
       const uint32_t ps = w.s_psub[src], pl = w.s_psublen[src];
-      if (WRITE) p = copy_bytes(out, p, sb + ps, pl);
-      size += pl;
+      uint32_t q = ps;
+      bool okq = true;
+      const uint32_t n = rd_vu(sb, q, ps + pl, okq);
+      if (WRITE) { p = wr_vu(out, p, n); p = copy_bytes(out, p, sb + q, n); }
+      size += vu_size(n) + n;
     }
   }
   if (del) {

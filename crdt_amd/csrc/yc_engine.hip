@@ -256,7 +256,7 @@ struct ycrdt_doc {
   bool wants_view = false;  // a view was read once: build it beside every merge (crdt.js reads after each op)
   // Y.applyUpdate is deferred: validated updates wait here and are merged in one
   // batch by the next read (encode*, toJSON, get, local op). n sequential applies cost one merge.
-  struct Queued { std::vector<uint8_t> bytes; bool local; };
+  struct Queued { std::vector<uint8_t> bytes; bool local; bool ds_error = false; };  // ds_error: read_update
   std::vector<Queued> queue;
   size_t queue_bytes = 0;
   IngestState ing;       // Yjs pendingStructs / pendingDs / store client order (yc_ingest.h)
@@ -725,6 +725,20 @@ int split_decode_exchange(ycrdt_engine* e, ycrdt_batch* b, const ShardSpec* sh) 
   // every rank, so all of them re-run the decode with the worst-case bound (run_decode)
   if (cw[0] == ERR_CAPACITY || total > w.cap_sections) return fail(YCRDT_E_CAPACITY, "decode split: sections past the estimate");
   if (total) HIPCHK(hipMemcpyAsync(w.sections, all.data(), all.size(), hipMemcpyHostToDevice, s));
+  // every update's sections in the gathered table (each walker wrote its update's sections as one
+  // run, in byte order): the per-update (first, count) the later passes read (k_ds_bound)
+  {
+    std::vector<uint32_t> us(2 * (nu + 1), 0);
+    const Section* sp = (const Section*)all.data();
+    for (uint64_t i = 0; i < total; ++i) {
+      const uint32_t u = sp[i].upd;
+      if (u >= nu) return fail(YCRDT_E_DEVICE, "decode split: section of an unknown update");
+      if (!us[nu + 1 + u]) us[u] = (uint32_t)i;
+      ++us[nu + 1 + u];
+    }
+    HIPCHK(hipMemcpyAsync(w.usec_start, us.data(), sizeof(uint32_t) * (nu + 1), hipMemcpyHostToDevice, s));
+    HIPCHK(hipMemcpyAsync(w.usec_n, us.data() + nu + 1, sizeof(uint32_t) * (nu + 1), hipMemcpyHostToDevice, s));
+  }
   const uint32_t t32 = (uint32_t)total;
   HIPCHK(hipMemcpyAsync(&w.ctr->nsections, &t32, sizeof(uint32_t), hipMemcpyHostToDevice, s));
   HIPCHK(hipStreamSynchronize(s));
@@ -825,6 +839,7 @@ int run_decode(ycrdt_engine* e, ycrdt_batch* b, bool lazy, Decoded& D, bool gene
   static_assert(sizeof(Counters) % 4 == 0, "counters are filled as words");
   fill_u32_multi({{(uint32_t*)w.ctr, sizeof(Counters) / 4, 0u},
                   {w.ufail, (uint64_t)nu + 1, 0u},
+                  {w.usec_n, (uint64_t)nu + 1, 0u},  // an update no walker reached has no sections
                   {(uint32_t*)w.final_bits, (uint64_t)nwords * 2, 0u},
                   {(uint32_t*)w.sec_bits, (uint64_t)nwords * 2, 0u}}, s);
   const bool dbg_yata = getenv("YCRDT_DEBUG_YATA") && getenv("YCRDT_DEBUG_YATA")[0] == '1';
@@ -945,6 +960,7 @@ int run_decode(ycrdt_engine* e, ycrdt_batch* b, bool lazy, Decoded& D, bool gene
     launch_states(w, nstructs, nsections, s);
   } else {
     HIPCHK(hipMemsetAsync(w.cl_start, 0, sizeof(uint32_t) * (nsections + 1), s));
+    launch_struct_clocks(w, nstructs, s);
   }
   HIPCHK(hipStreamWaitEvent(s, e->side_done, 0));
   rc = check(e, c, "struct decode");
@@ -1032,6 +1048,7 @@ int run_merge(ycrdt_engine* e, ycrdt_batch* b, const std::unordered_map<uint32_t
     w.cl_emit = eb;
     w.cl_slot = eb + nclients;
   }
+  w.delta = target && !target->empty() && nclients ? 1u : 0u;
   if (target && !target->empty() && nclients) {
     std::vector<uint32_t> starts(nclients, 0);
     for (uint32_t i = 0; i < nclients; ++i) {
@@ -1359,7 +1376,9 @@ int split_multi(ycrdt_engine* e, const Decoded& D, uint32_t nr, uint32_t sbytes,
     const uint32_t r0 = r;
     uint32_t ng = 0;
     while (r < nr && (uint32_t)(dkey[r] >> 32) == u) { ng += dflag[r]; ++r; }
-    const uint32_t h0 = vu(hdr[0], (uint32_t)(b - a)), h1 = vu(hdr[1], ng);
+    uint32_t heads = 0;  // a block of the client of the block before it continues that section (k_blk_sizes)
+    for (uint32_t* q = a; q < b; ++q) heads += q == a || sec[*q].client != sec[q[-1]].client;
+    const uint32_t h0 = vu(hdr[0], heads), h1 = vu(hdr[1], ng);
     const size_t len = (size_t)h0 + blk + h1 + (dpos[r] - dpos[r0]);
     uint8_t* o = (uint8_t*)malloc(len ? len : 1);
     if (!o) {
@@ -1862,8 +1881,9 @@ int flush(ycrdt_doc* d) {
   ycrdt_engine* e = d->e;
   HIPCHK(hipSetDevice(e->device));
   std::vector<ycrdt_buf> bufs;
-  for (const auto& q : d->queue) bufs.push_back(ycrdt_buf{q.bytes.data(), q.bytes.size()});
-  if (!d->ing.has_pending && !d->ing.has_ds && e->compat != 135) {
+  bool ds_errors = false;  // a cut-short delete set takes effect against the state of its time: replay
+  for (const auto& q : d->queue) { bufs.push_back(ycrdt_buf{q.bytes.data(), q.bytes.size()}); ds_errors |= q.ds_error; }
+  if (!d->ing.has_pending && !d->ing.has_ds && e->compat != 135 && !ds_errors) {
     const int rc = commit_merge(d, bufs, nullptr);
     if (rc != YCRDT_E_PENDING) {
       if (rc == YCRDT_OK) { d->queue.clear(); d->queue_bytes = 0; }
@@ -1877,9 +1897,12 @@ int flush(ycrdt_doc* d) {
     return lazy_merge_host(e, ins, out);
   };
   std::string err;
-  for (const auto& q : d->queue) {
-    const int rc = read_update(S, q.bytes.data(), q.bytes.size(), q.local, mf, err);
+  std::vector<std::vector<uint8_t>> eff(d->queue.size());  // ds_error entries as they take effect
+  for (size_t i = 0; i < d->queue.size(); ++i) {
+    const auto& q = d->queue[i];
+    const int rc = read_update(S, q.bytes.data(), q.bytes.size(), q.local, mf, err, q.ds_error, q.ds_error ? &eff[i] : nullptr);
     if (rc) return fail(rc, err);
+    if (q.ds_error) bufs[i] = ycrdt_buf{eff[i].data(), eff[i].size()};
   }
   if (d->ing.has_pending) bufs.push_back(ycrdt_buf{d->ing.pending.data(), d->ing.pending.size()});
   if (d->ing.has_ds) bufs.push_back(ycrdt_buf{d->ing.pending_ds.data(), d->ing.pending_ds.size()});
@@ -1896,8 +1919,8 @@ int flush(ycrdt_doc* d) {
   return YCRDT_OK;
 }
 
-void enqueue(ycrdt_doc* d, const uint8_t* p, size_t n, bool local) {
-  d->queue.push_back(ycrdt_doc::Queued{std::vector<uint8_t>(p, p + n), local});
+void enqueue(ycrdt_doc* d, const uint8_t* p, size_t n, bool local, bool ds_error = false) {
+  d->queue.push_back(ycrdt_doc::Queued{std::vector<uint8_t>(p, p + n), local, ds_error});
   d->queue_bytes += n;
   d->view.valid = false;
 }
@@ -1913,7 +1936,9 @@ int flush_multi(ycrdt_engine* e, const std::vector<ycrdt_doc*>& docs) {
   std::vector<ycrdt_doc*> fast;
   for (ycrdt_doc* d : docs) {
     if (d->queue.empty()) continue;
-    if (!d->ing.has_pending && !d->ing.has_ds && e->compat != 135) fast.push_back(d);
+    bool ds_errors = false;
+    for (const auto& q : d->queue) ds_errors |= q.ds_error;
+    if (!d->ing.has_pending && !d->ing.has_ds && e->compat != 135 && !ds_errors) fast.push_back(d);
     else if (const int rc = flush(d)) return rc;
   }
   if (fast.size() < 2) return fast.empty() ? YCRDT_OK : flush(fast[0]);
@@ -2044,7 +2069,7 @@ int ycrdt_apply_updates(ycrdt_doc* d, const ycrdt_buf* ups, size_t n) {
       // Yjs integrates a well-formed struct section and the delete-set ranges read before the error
       if (sc[i].structs_ok) {
         const std::vector<uint8_t> r = repaired_update(ups[i].ptr, sc[i]);
-        enqueue(d, r.data(), r.size(), false);
+        enqueue(d, r.data(), r.size(), false, true);
       }
       return fail(YCRDT_E_DECODE, "Integer out of range! (malformed update " + std::to_string(i) + ")");
     }
@@ -2092,7 +2117,7 @@ int ycrdt_apply_updates_multi(ycrdt_engine* e, ycrdt_doc* const* docs, const ycr
     if (!ok[i]) {  // sequential semantics: what came before is applied, then Yjs throws
       if (sc[i].structs_ok) {
         const std::vector<uint8_t> r = repaired_update(ups[i].ptr, sc[i]);
-        enqueue(d, r.data(), r.size(), false);
+        enqueue(d, r.data(), r.size(), false, true);
       }
       rc = YCRDT_E_DECODE;
       err = "Integer out of range! (malformed update " + std::to_string(i) + ")";

@@ -32,6 +32,13 @@ bool scan_update(const uint8_t* b, size_t n, bool headers, UpdScan& o) {
       if (r == -1) o.unsupported = true;  // skip_any's depth limit (exact budget: never the step count)
       if (r <= 0) return false;
       if (ck + v.len > 0xFFFFFFFFull) return false;  // clocks are u32 (k_struct_clock refuses the same)
+      // an item whose origin, right origin or parent item is of its own client at or past its own
+      // clock: Yjs takes own-client references as present (getMissing skips them) and then fails
+      // to find the item (a TypeError inside integrateStructs); the engine refuses the update
+      if (v.ref != REF_GC && v.ref != REF_SKIP &&
+          (((v.info & 0x80u) && v.oc == client && v.ok_ >= ck) || ((v.info & 0x40u) && v.rc == client && v.rk >= ck) ||
+           ((v.info & 0xC0u) == 0 && v.pkind == 2 && v.pa == client && v.pb >= ck)))
+        return false;
       if (headers) o.st.push_back(ScanStruct{client, (uint32_t)ck, pos, v});
       ck += v.len;
       ++o.nstructs;
@@ -276,7 +283,8 @@ bool pending_ds_of(const UpdScan& sc, const ClockMap& state, std::vector<uint8_t
 }  // namespace
 
 // ------------------------------------------------------------------------------------ readUpdateV2
-int read_update(IngestState& S, const uint8_t* u, size_t n, bool local, const MergeFn& merge, std::string& err) {
+int read_update(IngestState& S, const uint8_t* u, size_t n, bool local, const MergeFn& merge, std::string& err, bool ds_error,
+                std::vector<uint8_t>* effective) {
   UpdScan sc;
   if (!scan_update(u, n, true, sc)) {
     err = "internal: a queued update no longer decodes";
@@ -307,6 +315,23 @@ int read_update(IngestState& S, const uint8_t* u, size_t n, bool local, const Me
     S.has_pending = true;
     S.pending.swap(rest);
     S.missing.swap(rmissing);
+  }
+  if (ds_error) {  // readAndApplyDeleteSet threw: the ranges within the state are applied, no more
+    if (effective) {
+      std::vector<std::pair<uint32_t, std::vector<std::pair<uint32_t, uint32_t>>>> ds;
+      for (const auto& e : sc.ds) {
+        const uint32_t st = state_of(S.state, e.client);
+        std::vector<std::pair<uint32_t, uint32_t>> rs;
+        for (uint32_t k = 0; k < e.n; ++k) {
+          const uint32_t clock = sc.ranges[e.first + k].first, len = sc.ranges[e.first + k].second;
+          if (clock < st) rs.push_back({clock, (uint32_t)std::min<uint64_t>(len, st - clock)});
+        }
+        if (!rs.empty()) ds.push_back({e.client, rs});
+      }
+      effective->assign(u, u + sc.struct_end);
+      put_ds(*effective, ds);
+    }
+    return YCRDT_OK;
   }
   // the update's delete set, then the parked delete set again (Y@21330)
   std::vector<uint8_t> ds1, ds2;

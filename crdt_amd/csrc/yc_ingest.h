@@ -64,7 +64,13 @@ using MergeFn = std::function<int(const std::vector<const std::vector<uint8_t>*>
 // One Y.applyUpdate(doc, u) (local = false) or one local transaction's update (local = true: it
 // integrates, but Yjs runs no pending retry and no pendingDs pass for local transactions).
 // Advances S; returns 0 or a YCRDT_E_* code (err says why).
-int read_update(IngestState& S, const uint8_t* u, size_t n, bool local, const MergeFn& merge, std::string& err);
+// ds_error: the update's delete set was cut short by a decode error (the queued bytes are the
+// struct section + the ranges read before it, repaired_update): Yjs threw inside
+// readAndApplyDeleteSet, so its ranges at or past the state are dropped (not store.pendingDs), the
+// parked delete set is not re-applied and nothing is retried. `effective` (ds_error only) receives
+// the update as it takes effect: the struct section + the ranges clipped to the state.
+int read_update(IngestState& S, const uint8_t* u, size_t n, bool local, const MergeFn& merge, std::string& err,
+                bool ds_error = false, std::vector<uint8_t>* effective = nullptr);
 
 // varuint writer
 inline void put_vu(std::vector<uint8_t>& o, uint32_t v) {

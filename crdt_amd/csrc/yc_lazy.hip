@@ -452,7 +452,7 @@ __device__ uint32_t encode_event(const Work& w, uint32_t client, uint32_t e, uin
   }
   if (!has_o && !has_r) {
     const uint32_t pa = w.s_pa[src], pb = w.s_pb[src];
-    if (w.s_pk[src] == 1) {
+    if ((w.s_pk[src] & 3u) == 1) {
       if (WRITE) { out[p++] = 1; for (uint32_t i = 0; i < pb; ++i) out[p++] = w.bytes[pa + i]; }
       size += 1 + pb;
     } else {
@@ -487,6 +487,35 @@ __device__ __forceinline__ uint32_t blk_client(const Work& w, uint32_t b) {
   if (w.lz_bclient) return w.lz_bclient[b];  // the serial merge's output sections
   return w.lz_diff ? w.sections[b].client : w.cl_vals[w.lz_nblk - 1 - b];
 }
+// diffUpdate over non-canonical input (k_ds_bound's flag): LazyStructWriter appends a struct to
+// the section it is writing when the client is the same (Y@38735), so a non-empty block continues
+// the previous non-empty block of its update when both have the same client (a run of one client
+// the reader left and came back to, with nothing written in between). Canonical input has distinct
+// clients per update: every non-empty block starts a section.
+__device__ __forceinline__ bool blk_same_upd(const Work& w, uint32_t a, uint32_t b) {
+  return !w.lz_multi || w.sections[a].upd == w.sections[b].upd;
+}
+__device__ bool blk_continues(const Work& w, uint32_t b) {
+  if (!w.lz_diff || !w.ctr->noncanon) return false;
+  const uint32_t c = blk_client(w, b);
+  for (uint32_t k = b; k-- > 0;) {
+    if (!blk_same_upd(w, k, b)) return false;
+    if (w.lz_evn[k]) return blk_client(w, k) == c;
+  }
+  return false;
+}
+__device__ uint32_t blk_section_n(const Work& w, uint32_t b) {  // structs of the section block b heads
+  uint32_t n = w.lz_evn[b];
+  if (!w.lz_diff || !w.ctr->noncanon) return n;
+  const uint32_t c = blk_client(w, b);
+  for (uint32_t k = b + 1; k < w.lz_nblk && blk_same_upd(w, b, k); ++k) {
+    const uint32_t e = w.lz_evn[k];
+    if (!e) continue;
+    if (blk_client(w, k) != c) break;
+    n += e;
+  }
+  return n;
+}
 // event slots [evbase[b], evbase[b] + cap[b]); slots past evn[b] are empty
 __global__ __launch_bounds__(256) void k_ev_sizes(Work w, uint32_t nslots) {
   const uint32_t e = blockIdx.x * blockDim.x + threadIdx.x;
@@ -501,12 +530,15 @@ __global__ void k_blk_sizes(Work w, uint32_t nblk) {
   if (b == nblk) { w.blk_size[b] = 0; return; }
   const uint32_t n = w.lz_evn[b];
   uint32_t sz = 0;
+  bool head = false;
   if (n) {
     const uint32_t e0 = w.lz_evbase[b];
-    sz = vu_size(n) + vu_size(blk_client(w, b)) + vu_size(w.ev_clock[e0]) + (w.ev_pos[e0 + n] - w.ev_pos[e0]);
+    head = !blk_continues(w, b);
+    sz = w.ev_pos[e0 + n] - w.ev_pos[e0];
+    if (head) sz += vu_size(blk_section_n(w, b)) + vu_size(blk_client(w, b)) + vu_size(w.ev_clock[e0]);
   }
   w.blk_size[b] = sz;
-  wave_count_add(&w.ctr->pad[0], n != 0);
+  wave_count_add(&w.ctr->pad[0], head);
 }
 __global__ __launch_bounds__(256) void k_ev_write(Work w, uint32_t nslots) {
   const uint32_t e = blockIdx.x * blockDim.x + threadIdx.x;
@@ -515,7 +547,7 @@ __global__ __launch_bounds__(256) void k_ev_write(Work w, uint32_t nslots) {
   const uint32_t e0 = w.lz_evbase[b], n = w.lz_evn[b];
   if (e - e0 >= n) return;
   const uint32_t client = blk_client(w, b);
-  const uint32_t hdr = vu_size(n) + vu_size(client) + vu_size(w.ev_clock[e0]);
+  const uint32_t hdr = blk_continues(w, b) ? 0u : vu_size(blk_section_n(w, b)) + vu_size(client) + vu_size(w.ev_clock[e0]);
   const uint32_t hoff = w.lz_multi ? 0u : vu_size(w.ctr->pad[0]);  // lz_multi: the host writes per-update headers
   const uint32_t p = hoff + w.blk_pos[b] + hdr + (w.ev_pos[e] - w.ev_pos[e0]);
   encode_event<true>(w, client, e, w.out, p);
@@ -525,9 +557,9 @@ __global__ void k_blk_write(Work w, uint32_t nblk) {
   if (b == 0 && !w.lz_multi) wr_vu(w.out, 0u, w.ctr->pad[0]);
   if (b >= nblk) return;
   const uint32_t n = w.lz_evn[b];
-  if (!n) return;
+  if (!n || blk_continues(w, b)) return;
   uint32_t p = (w.lz_multi ? 0u : vu_size(w.ctr->pad[0])) + w.blk_pos[b];
-  p = wr_vu(w.out, p, n);
+  p = wr_vu(w.out, p, blk_section_n(w, b));
   p = wr_vu(w.out, p, blk_client(w, b));
   wr_vu(w.out, p, w.ev_clock[w.lz_evbase[b]]);
 }

@@ -39,8 +39,7 @@ constexpr uint32_t LONG_UNITS = 32;
 __device__ __forceinline__ uint64_t shfl64(uint64_t v, int l) {
   return ((uint64_t)(uint32_t)__shfl((uint32_t)(v >> 32), l) << 32) | (uint32_t)__shfl((uint32_t)v, l);
 }
-__global__ __launch_bounds__(256) void k_owner(Work w, uint32_t nstructs) {
-  const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
+__device__ __forceinline__ void unit_owner(const Work& w, uint32_t nstructs, uint32_t s) {
   const uint32_t lane = threadIdx.x & 63;
   uint64_t gb = 0;
   uint32_t n = 0, fl = 0;
@@ -63,7 +62,7 @@ __global__ __launch_bounds__(256) void k_owner(Work w, uint32_t nstructs) {
     for (uint32_t k = 0; k < n; ++k) {
       if (one) {
         w.u_owner[(uint32_t)(gb + k)] = s;
-        if (fl) w.u_flags[(uint32_t)(gb + k)] = fl;
+        if (fl) reinterpret_cast<uint8_t*>(w.u_flags)[(size_t)(uint32_t)(gb + k) * 4] = (uint8_t)fl;  // byte 0 (UF_DEL | UF_GC)
       } else {
         atomicMin(&w.u_owner[(uint32_t)(gb + k)], s);
         if (fl) atomicOr(&w.u_flags[(uint32_t)(gb + k)], fl);
@@ -77,7 +76,7 @@ __global__ __launch_bounds__(256) void k_owner(Work w, uint32_t nstructs) {
     for (uint32_t k = lane; k < nl; k += 64) {
       if (onel) {
         w.u_owner[(uint32_t)(g0 + k)] = sl;
-        if (fll) w.u_flags[(uint32_t)(g0 + k)] = fll;
+        if (fll) reinterpret_cast<uint8_t*>(w.u_flags)[(size_t)(uint32_t)(g0 + k) * 4] = (uint8_t)fll;
       } else {
         atomicMin(&w.u_owner[(uint32_t)(g0 + k)], sl);
         if (fll) atomicOr(&w.u_flags[(uint32_t)(g0 + k)], fll);
@@ -95,9 +94,9 @@ __device__ __forceinline__ void set_flag_byte(uint32_t* u_flags, uint32_t g, uin
 // The delete sets of a merge, straight from the decoder's per-update regions (no compaction): one
 // wavefront per update resolves its ranges' clients, clips them to the known states (pendingDs)
 // and marks the units (the prep and mark passes above in one, for the integrate path)
-__global__ __launch_bounds__(256) void k_ds_apply(Work w, uint32_t nclients) {
+__device__ __forceinline__ void unit_ds_apply(const Work& w, uint32_t nclients, uint32_t blk) {
   const uint32_t lane = threadIdx.x & 63;
-  const uint32_t u = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const uint32_t u = (blk * blockDim.x + threadIdx.x) >> 6;
   if (u >= w.nupd) return;
   const uint32_t n = w.ds_count[u], base = w.ds_region[u];
   const uint32_t doc = doc_of_update(w, u);
@@ -138,17 +137,21 @@ __global__ __launch_bounds__(256) void k_ds_apply(Work w, uint32_t nclients) {
 }
 
 // --------------------------------------------------------------------------- reference cuts
-__global__ void k_refs(Work w, uint32_t nstructs) {
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+__device__ __forceinline__ void unit_refs(const Work& w, uint32_t nstructs, uint32_t i) {
   if (i >= nstructs) return;
   // the struct's columns in one round of loads (the right-origin clock and the parent are written
   // only where present: read, used behind their presence tests), then the clients' states
-  const uint32_t clock = w.s_clock[i], cidx = w.s_cidx[i], ref = w.s_info[i] & 31u, pk = w.s_pk[i];
+  const uint32_t clock = w.s_clock[i], cidx = w.s_cidx[i], ref = w.s_info[i] & 31u, pk = w.s_pk[i] & 3u;
   const uint32_t oc = w.s_ocidx[i], ok_ = w.s_oclock[i], rc = w.s_rcidx[i], rk = w.s_rclock[i];
   const bool ov = oc < NONE - 1, rv = rc < NONE - 1;
   const uint32_t st = w.cl_state[cidx], ost = ov ? w.cl_state[oc] : 0u, rst = rv ? w.cl_state[rc] : 0u;
   const uint64_t ob = ov ? w.cl_base[oc] : 0ull, rb = rv ? w.cl_base[rc] : 0ull;
   if (clock >= st || ref == REF_SKIP) return;  // not integrated
+  // own-client references at or past the item's own clock (scan_update refuses them on the host)
+  if ((oc == cidx && ok_ >= clock) || (rc == cidx && rk >= clock) || (pk == 2 && w.s_pa[i] == cidx && w.s_pb[i] >= clock)) {
+    raise_err(&w.ctr->err, ERR_DECODE);
+    return;
+  }
   // Item.getMissing (Y@76507): every reference of an integrated struct must be in the store
   if (pk == 2 && (w.s_pa[i] == UNKNOWN || w.s_pb[i] >= w.cl_state[w.s_pa[i]])) { raise_err(&w.ctr->err, ERR_PENDING); return; }
   if (oc != NONE) {
@@ -185,7 +188,15 @@ __global__ __launch_bounds__(256) void k_cuts(Work w, uint64_t nunits) {
     }
   }
   const uint64_t word = __ballot(cut);
-  if ((threadIdx.x & 63) == 0 && g < nunits) w.u_cutbits[g >> 6] = word;
+  if ((threadIdx.x & 63) == 0) {  // the word and its popcount (the scan input of the segment numbering)
+    const uint64_t wi = g >> 6;
+    if (g < nunits) {
+      w.u_cutbits[wi] = word;
+      w.scratch[wi] = (uint32_t)__popcll(word);
+    } else if (wi == (nunits + 63) / 64) {
+      w.scratch[wi] = 0;
+    }
+  }
 }
 __global__ void k_scatter_seg(Work w, uint32_t nwords, uint64_t nunits) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -201,23 +212,29 @@ __global__ void k_scatter_seg(Work w, uint32_t nwords, uint64_t nunits) {
   if (i == nwords - 1) w.g_start[w.u_wpre[nwords]] = (uint32_t)nunits;  // sentinel
 }
 
+// One launch for the three unit passes (they touch disjoint bytes of a unit's flag word: byte 0
+// UF_DEL / UF_GC from the owner pass, byte 1 UF_DS from the delete sets, byte 2 UF_CUT from the
+// references, every one of them a byte store or an atomic): workgroups [0, nb) take a struct each
+// lane (owner, then references — the struct's columns are loaded once), the rest one update per
+// wavefront (delete sets).
+__global__ __launch_bounds__(256) void k_units(Work w, uint32_t nstructs, uint32_t nclients, uint32_t nb) {
+  if (blockIdx.x < nb) {
+    const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
+    unit_owner(w, nstructs, s);
+    unit_refs(w, nstructs, s);
+  } else {
+    unit_ds_apply(w, nclients, blockIdx.x - nb);
+  }
+}
 void launch_units(const Work& w, uint32_t nstructs, uint32_t nclients, uint32_t nds, uint64_t nunits, hipStream_t s) {
   fill_u32_multi({{w.u_owner, nunits, NONE}, {w.u_flags, nunits, 0u}, {w.u_minchild, nunits, NONE}}, s);
-  if (nstructs) hipLaunchKernelGGL(k_owner, dim3((nstructs + 255) / 256), dim3(256), 0, s, w, nstructs);
-  if (nds && w.nupd) hipLaunchKernelGGL(k_ds_apply, dim3((w.nupd + 3) / 4), dim3(256), 0, s, w, nclients);
-  if (nstructs) hipLaunchKernelGGL(k_refs, dim3((nstructs + 255) / 256), dim3(256), 0, s, w, nstructs);
-}
-
-__global__ void k_popc_words(const uint64_t* __restrict__ bits, uint32_t* __restrict__ cnt, uint32_t n) {
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < n) cnt[i] = (uint32_t)__popcll(bits[i]);
-  else if (i == n) cnt[i] = 0;
+  const uint32_t nb = (nstructs + 255) / 256, nd = nds && w.nupd ? (w.nupd + 3) / 4 : 0u;
+  if (nb + nd) hipLaunchKernelGGL(k_units, dim3(nb + nd), dim3(256), 0, s, w, nstructs, nclients, nb);
 }
 
 void launch_segments(const Work& w, uint32_t nclients, uint64_t nunits, hipStream_t s) {
   const uint32_t nwords = (uint32_t)((nunits + 63) / 64);
   hipLaunchKernelGGL(k_cuts, dim3(nwords / 4 + 1), dim3(256), 0, s, w, nunits);
-  hipLaunchKernelGGL(k_popc_words, dim3(nwords / 256 + 1), dim3(256), 0, s, (const uint64_t*)w.u_cutbits, w.scratch, nwords);
   scan_u32(w.tmp, w.tmp_bytes, w.scratch, w.u_wpre, nwords + 1, s);
   hipLaunchKernelGGL(k_scatter_seg, dim3(nwords / 256 + 1), dim3(256), 0, s, w, nwords, nunits);
 }
@@ -237,8 +254,8 @@ __device__ __forceinline__ bool bytes_eq(const uint8_t* __restrict__ a, const ui
 // crdt.js:434). Names and parentSubs are compared as whole varStrings (length prefix included).
 __device__ __forceinline__ bool same_list(const Work& w, uint32_t a, uint32_t b) {  // inline: a Work reference into an out-of-line call copies the whole Work to scratch
   if (a == b) return true;
-  const uint32_t pk = w.s_pk[a];
-  if (pk != w.s_pk[b]) return false;
+  const uint32_t pk = w.s_pk[a] & 3u;
+  if (pk != (w.s_pk[b] & 3u)) return false;
   if (pk == 1) {
     const uint32_t n = w.s_pb[a];
     if (n != w.s_pb[b]) return false;
@@ -311,7 +328,7 @@ __global__ __launch_bounds__(256) void k_seg_props(Work w, uint32_t nsegs) {
   }
   uint32_t key = NONE, link = s;
   if (!gc && origin == NONE && rorigin == NONE) {
-    const uint32_t pk = w.s_pk[own];
+    const uint32_t pk = w.s_pk[own] & 3u;
     uint64_t h = 1469598103934665603ull;
     uint32_t parent = NONE;
     if (pk == 1) {

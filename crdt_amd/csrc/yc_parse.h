@@ -67,10 +67,53 @@ YC_HDI void skip_bytes(uint32_t& p, uint32_t n, uint32_t end, bool& ok) {
   p += n;
 }
 
+// lib0 readVarString decodes with decodeURIComponent(escape(bytes)) (L0@1937): anything but
+// shortest-form UTF-8 of a scalar value — a stray continuation byte, a truncated sequence, an
+// overlong form, a surrogate, a value past U+10FFFF — throws URIError, and Y.applyUpdate with it.
+// Every string field of an exactly parsed struct is checked (names, keys, contents, `any` strings
+// and object keys); the bytes are in range (the caller skipped them already).
+template <class Src>
+YC_HDI bool utf8_valid(const Src& b, uint32_t p, uint32_t n) {
+  const uint32_t e = p + n;
+#pragma unroll 1
+  while (p < e) {
+    const uint32_t c = b.u8(p);
+    if (c < 0x80u) { ++p; continue; }
+    uint32_t need, v, lo;
+    if ((c & 0xE0u) == 0xC0u) { need = 1; v = c & 0x1Fu; lo = 0x80u; }
+    else if ((c & 0xF0u) == 0xE0u) { need = 2; v = c & 0x0Fu; lo = 0x800u; }
+    else if ((c & 0xF8u) == 0xF0u) { need = 3; v = c & 0x07u; lo = 0x10000u; }
+    else return false;
+    if (e - p - 1 < need) return false;
+    for (uint32_t k = 1; k <= need; ++k) {
+      const uint32_t d = b.u8(p + k);
+      if ((d & 0xC0u) != 0x80u) return false;
+      v = (v << 6) | (d & 0x3Fu);
+    }
+    if (v < lo || v > 0x10FFFFu || (v >= 0xD800u && v <= 0xDFFFu)) return false;
+    p += need + 1;
+  }
+  return true;
+}
+struct PtrSrc {  // utf8_valid over a plain pointer
+  const uint8_t* __restrict__ b;
+  YC_HDI uint32_t u8(uint32_t p) const { return b[p]; }
+};
+// a varString at p: its length, then (UTF8) its text checked; p moves past it
+template <bool UTF8, class Src>
+YC_HDI void skip_str(const Src& b, uint32_t& p, uint32_t end, bool& ok) {
+  const uint32_t n = b.vu(p, end, ok);
+  if (!ok) return;
+  const uint32_t st = p;
+  skip_bytes(p, n, end, ok);
+  if (UTF8 && ok && !utf8_valid(b, st, n)) ok = false;
+}
+
 // readAny (L0@1937 B): iterative skip with an explicit container stack of depth DEPTH (deeper
 // nesting fails the parse: speculative callers use a shallow stack, exact callers a deep one).
-template <int DEPTH>
+template <int DEPTH, bool UTF8 = false>
 YC_HD inline bool skip_any(const uint8_t* __restrict__ b, uint32_t& p, uint32_t end, uint32_t& steps) {
+  const PtrSrc src{b};
   // A level is kept only while members FOLLOW the one being read (rem[d] >= 1): the last member of
   // a container is read in the container's place (a tail position), so nesting along last members
   // — [[[..]]], {a: {b: ..}}, however deep — takes no stack, and DEPTH bounds only containers
@@ -90,7 +133,14 @@ YC_HD inline bool skip_any(const uint8_t* __restrict__ b, uint32_t& p, uint32_t 
       case 125: skip_vi(b, p, end, ok); break;
       case 124: skip_bytes(p, 4, end, ok); break;
       case 123: case 122: skip_bytes(p, 8, end, ok); break;
-      case 119: case 116: { uint32_t n = rd_vu(b, p, end, ok); if (ok) skip_bytes(p, n, end, ok); break; }
+      case 119: {
+        uint32_t n = rd_vu(b, p, end, ok);
+        const uint32_t st = p;
+        if (ok) skip_bytes(p, n, end, ok);
+        if (UTF8 && ok && !utf8_valid(src, st, n)) return false;
+        break;
+      }
+      case 116: { uint32_t n = rd_vu(b, p, end, ok); if (ok) skip_bytes(p, n, end, ok); break; }
       case 118: case 117: {
         uint32_t n = rd_vu(b, p, end, ok);
         if (!ok) return false;
@@ -101,7 +151,12 @@ YC_HD inline bool skip_any(const uint8_t* __restrict__ b, uint32_t& p, uint32_t 
             if (tag == 118) objmask |= 1u << d; else objmask &= ~(1u << d);
             ++d;
           }
-          if (tag == 118) { uint32_t k = rd_vu(b, p, end, ok); if (ok) skip_bytes(p, k, end, ok); }
+          if (tag == 118) {  // the first member's key
+            uint32_t k = rd_vu(b, p, end, ok);
+            const uint32_t st = p;
+            if (ok) skip_bytes(p, k, end, ok);
+            if (UTF8 && ok && !utf8_valid(src, st, k)) return false;
+          }
           if (!ok) return false;
           continue;  // read the first member value
         }
@@ -114,7 +169,12 @@ YC_HD inline bool skip_any(const uint8_t* __restrict__ b, uint32_t& p, uint32_t 
     // in the level's place)
     if (d == 0) return true;
     const uint32_t lvl = (uint32_t)d - 1;
-    if ((objmask >> lvl) & 1u) { uint32_t k = rd_vu(b, p, end, ok); if (ok) skip_bytes(p, k, end, ok); if (!ok) return false; }
+    if ((objmask >> lvl) & 1u) {  // the next member's key
+      uint32_t k = rd_vu(b, p, end, ok);
+      const uint32_t st = p;
+      if (ok) skip_bytes(p, k, end, ok);
+      if (!ok || (UTF8 && !utf8_valid(src, st, k))) return false;
+    }
     if (--rem[lvl] == 0) --d;
   }
 }
@@ -123,9 +183,9 @@ YC_HD inline bool skip_any(const uint8_t* __restrict__ b, uint32_t& p, uint32_t 
 // parsers take scalar values inline and hand containers to this call.
 // (State goes in and out by value: taking the caller's cursor by address would put it in scratch.)
 struct AnySkip { uint32_t p, steps, ok; };
-template <int DEPTH>
+template <int DEPTH, bool UTF8 = false>
 YC_HD __attribute__((noinline)) AnySkip skip_any_nl(const uint8_t* __restrict__ b, uint32_t p, uint32_t end, uint32_t steps) {
-  const bool ok = skip_any<DEPTH>(b, p, end, steps);
+  const bool ok = skip_any<DEPTH, UTF8>(b, p, end, steps);
   return AnySkip{p, steps, ok ? 1u : 0u};
 }
 
@@ -183,8 +243,7 @@ YC_HD inline int parse_struct(const Src& b, uint32_t& p, uint32_t end, uint32_t 
     if (!ok) return p >= end ? -2 : 0;
     if (pinfo == 1) {
       uint32_t st = p;
-      uint32_t n = b.vu(p, end, ok);
-      if (ok) skip_bytes(p, n, end, ok);
+      skip_str<FULL>(b, p, end, ok);
       if (FULL) { v->pkind = 1; v->pa = st; v->pb = p - st; }
     } else {
       uint32_t c = b.vu(p, end, ok), k = b.vu(p, end, ok);
@@ -192,8 +251,7 @@ YC_HD inline int parse_struct(const Src& b, uint32_t& p, uint32_t end, uint32_t 
     }
     if (info & 0x20u) {
       uint32_t st = p;
-      uint32_t n = b.vu(p, end, ok);
-      if (ok) skip_bytes(p, n, end, ok);
+      skip_str<FULL>(b, p, end, ok);
       if (FULL) { v->has_psub = 1; v->psub_pos = st; v->psub_len = p - st; }
     }
     if (!ok) return p >= end ? -2 : 0;
@@ -210,7 +268,9 @@ YC_HD inline int parse_struct(const Src& b, uint32_t& p, uint32_t end, uint32_t 
         --steps;
         uint32_t k = b.vu(p, end, ok);
         if (ok && (k == 0 || (p < end && !json_start_ok(b.u8(p))))) return 0;
+        const uint32_t st = p;
         if (ok) skip_bytes(p, k, end, ok);
+        if (FULL && ok && !utf8_valid(b, st, k)) ok = false;
       }
       if (FULL) v->nel = n;
       if (ok && steps == 0) return -1;
@@ -220,13 +280,16 @@ YC_HD inline int parse_struct(const Src& b, uint32_t& p, uint32_t end, uint32_t 
     case REF_EMBED: {
       uint32_t k = b.vu(p, end, ok);
       if (ok && (k == 0 || (p < end && !json_start_ok(b.u8(p))))) return 0;
+      const uint32_t st = p;
       if (ok) skip_bytes(p, k, end, ok);
+      if (FULL && ok && !utf8_valid(b, st, k)) ok = false;
       break;
     }
     case REF_STRING: {
       uint32_t k = b.vu(p, end, ok);
       uint32_t st = p;
       if (ok) skip_bytes(p, k, end, ok);
+      if (FULL && ok && !utf8_valid(b, st, k)) ok = false;
       if (ok && FULL) {  // ContentString length counts UTF-16 code units
         uint32_t u = 0;
         for (uint32_t i = st; i < st + k; ++i) {
@@ -238,16 +301,17 @@ YC_HD inline int parse_struct(const Src& b, uint32_t& p, uint32_t end, uint32_t 
       break;
     }
     case REF_FORMAT: {
+      skip_str<FULL>(b, p, end, ok);
       uint32_t k = b.vu(p, end, ok);
-      if (ok) skip_bytes(p, k, end, ok);
-      k = b.vu(p, end, ok);
       if (ok && (k == 0 || (p < end && !json_start_ok(b.u8(p))))) return 0;
+      const uint32_t st = p;
       if (ok) skip_bytes(p, k, end, ok);
+      if (FULL && ok && !utf8_valid(b, st, k)) ok = false;
       break;
     }
     case REF_TYPE: {
       uint32_t tr = b.vu(p, end, ok);
-      if (ok && (tr == 3 || tr == 5)) { uint32_t k = b.vu(p, end, ok); if (ok) skip_bytes(p, k, end, ok); }
+      if (ok && (tr == 3 || tr == 5)) skip_str<FULL>(b, p, end, ok);
       if (tr > 6) ok = false;
       break;
     }
@@ -263,11 +327,12 @@ YC_HD inline int parse_struct(const Src& b, uint32_t& p, uint32_t end, uint32_t 
             case 125: b.svi(p, end, ok); break;
             case 124: skip_bytes(p, 4, end, ok); break;
             case 123: case 122: skip_bytes(p, 8, end, ok); break;
-            case 119: case 116: { const uint32_t k = b.vu(p, end, ok); if (ok) skip_bytes(p, k, end, ok); break; }
+            case 119: skip_str<FULL>(b, p, end, ok); break;
+            case 116: { const uint32_t k = b.vu(p, end, ok); if (ok) skip_bytes(p, k, end, ok); break; }
             default: break;  // 127 undefined, 126 null, 121 false, 120 true
           }
         } else {
-          const AnySkip r = skip_any_nl<DEPTH>(b.b, p, end, steps);
+          const AnySkip r = skip_any_nl<DEPTH, FULL>(b.b, p, end, steps);
           p = r.p;
           steps = r.steps;
           ok = r.ok != 0;
@@ -278,10 +343,9 @@ YC_HD inline int parse_struct(const Src& b, uint32_t& p, uint32_t end, uint32_t 
       break;
     }
     case REF_DOC: {
-      uint32_t k = b.vu(p, end, ok);
-      if (ok) skip_bytes(p, k, end, ok);
+      skip_str<FULL>(b, p, end, ok);
       if (ok) {
-        const AnySkip r = skip_any_nl<DEPTH>(b.b, p, end, steps);
+        const AnySkip r = skip_any_nl<DEPTH, FULL>(b.b, p, end, steps);
         p = r.p;
         steps = r.steps;
         ok = r.ok != 0;

@@ -90,7 +90,7 @@ __global__ void k_vkey_fill(Work w, const uint32_t* __restrict__ krep, ViewKey* 
   if (r != NONE) {
     const uint32_t own = w.g_src[r];
     // the struct table keeps whole varStrings (length prefix included): the view holds the text
-    if (w.s_pk[own] == 1) str_text(w, w.s_pa[own], w.s_pb[own], K.name_pos, K.name_len);
+    if ((w.s_pk[own] & 3u) == 1) str_text(w, w.s_pa[own], w.s_pb[own], K.name_pos, K.name_len);
     if (w.s_psub[own] != NONE) str_text(w, w.s_psub[own], w.s_psublen[own], K.psub_pos, K.psub_len);
   } else {
     raise_err(&w.ctr->err, ERR_DECODE);  // every live list has a member that names it

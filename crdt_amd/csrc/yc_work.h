@@ -153,6 +153,7 @@ struct Work {
   uint8_t* cl_single = nullptr;    // [NC] 1: the client's structs come from one section of one update    // per client state (max end clock)
   uint64_t* cl_base = nullptr;     // [NC+1] exclusive prefix of states (unit base)
   uint32_t* cl_start = nullptr;    // per client start clock for diff encodes (sv); 0 = full
+  uint32_t delta = 0;              // 1: some cl_start is nonzero (a delta encode against a state vector)
   // per-client integration caps (Yjs pending structs, yc_ingest.h): sorted (client, cap) pairs;
   // units at or past a client's cap are left out of the merge and delete-set ranges clipped to it
   const uint32_t* cap_client = nullptr;
@@ -500,7 +501,8 @@ void launch_ds_decode(const Work& w, hipStream_t s);
 void launch_section_clients(const Work& w, uint32_t nsections, hipStream_t s);
 void launch_client_table(Work& w, uint32_t nsections, hipStream_t s);
 void launch_struct_decode(const Work& w, uint32_t nstructs, hipStream_t s);
-void launch_states(const Work& w, uint32_t nstructs, uint32_t nsections, hipStream_t s);
+void launch_states(const Work& w, uint32_t nstructs, uint32_t nsections, hipStream_t s);  // clocks + client states
+void launch_struct_clocks(const Work& w, uint32_t nstructs, hipStream_t s);               // clocks only (lazy)
 
 void launch_units(const Work& w, uint32_t nstructs, uint32_t nclients, uint32_t nds, uint64_t nunits, hipStream_t s);
 void launch_segments(const Work& w, uint32_t nclients, uint64_t nunits, hipStream_t s);

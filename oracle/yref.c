@@ -116,6 +116,34 @@ static const uint8_t *dbytes(dec_t *d, uint32_t n) {
   d->pos += n;
   return p;
 }
+/* decodeURIComponent(escape(bytes)) of lib0's readVarString (L0@1937 E): shortest-form UTF-8 of
+ * scalar values only; anything else throws URIError (and Y.applyUpdate with it) */
+static int utf8_ok(const uint8_t *s, uint32_t n) {
+  for (uint32_t i = 0; i < n;) {
+    uint32_t c = s[i], need, lo;
+    if (c < 0x80) { i++; continue; }
+    if ((c & 0xE0) == 0xC0) { need = 1; c &= 0x1F; lo = 0x80; }
+    else if ((c & 0xF0) == 0xE0) { need = 2; c &= 0x0F; lo = 0x800; }
+    else if ((c & 0xF8) == 0xF0) { need = 3; c &= 0x07; lo = 0x10000; }
+    else return 0;
+    if (n - i - 1 < need) return 0;
+    for (uint32_t j = 1; j <= need; j++) {
+      if ((s[i + j] & 0xC0) != 0x80) return 0;
+      c = (c << 6) | (s[i + j] & 0x3F);
+    }
+    if (c < lo || c > 0x10FFFF || (c >= 0xD800 && c <= 0xDFFF)) return 0;
+    i += need + 1;
+  }
+  return 1;
+}
+/* readVarString: the bytes, checked */
+static const uint8_t *dstr(dec_t *d, uint32_t *len) {
+  uint32_t k = dvu(d);
+  const uint8_t *p = dbytes(d, k);
+  if (!d->err && !utf8_ok(p, k)) d->err = 1;
+  if (len) *len = k;
+  return p;
+}
 /* skips one lib0 `any` (readAny B) */
 static void dskip_any(dec_t *d, int depth) {
   if (depth > 20000) { d->err = 1; return; }  /* lib0 readAny recurses without a limit */
@@ -126,10 +154,10 @@ static void dskip_any(dec_t *d, int depth) {
     case 125: dvi(d); return;
     case 124: dbytes(d, 4); return;
     case 123: case 122: dbytes(d, 8); return;
-    case 119: { uint32_t n = dvu(d); dbytes(d, n); return; }
+    case 119: dstr(d, NULL); return;
     case 118: {
       uint32_t n = dvu(d);
-      for (uint32_t i = 0; i < n && !d->err; i++) { uint32_t k = dvu(d); dbytes(d, k); dskip_any(d, depth + 1); }
+      for (uint32_t i = 0; i < n && !d->err; i++) { dstr(d, NULL); dskip_any(d, depth + 1); }
       return;
     }
     case 117: {
@@ -909,8 +937,8 @@ static int read_content(yo_doc *doc, dec_t *d, uint8_t info, ycontent *c) {
       uint32_t n = dvu(d);
       for (uint32_t i = 0; i < n && !d->err; i++) {
         st = d->pos;
-        uint32_t k = dvu(d);
-        const uint8_t *js = dbytes(d, k);
+        uint32_t k;
+        const uint8_t *js = dstr(d, &k);
         if (!d->err && !json_start_ok(js, k)) d->err = 1;
         if (!d->err) el_push(c, ystr_dup(d->p + st, (uint32_t)(d->pos - st)));
       }
@@ -918,15 +946,15 @@ static int read_content(yo_doc *doc, dec_t *d, uint8_t info, ycontent *c) {
     }
     case CT_BINARY: case CT_EMBED: {
       st = d->pos;
-      uint32_t k = dvu(d);
-      const uint8_t *js = dbytes(d, k);
+      uint32_t k;
+      const uint8_t *js = c->ref == CT_EMBED ? dstr(d, &k) : (k = dvu(d), dbytes(d, k));
       if (!d->err && c->ref == CT_EMBED && !json_start_ok(js, k)) d->err = 1;
       if (!d->err) c->raw = ystr_dup(d->p + st, (uint32_t)(d->pos - st));
       break;
     }
     case CT_STRING: {
-      uint32_t k = dvu(d);
-      const uint8_t *s = dbytes(d, k);
+      uint32_t k;
+      const uint8_t *s = dstr(d, &k);
       if (!d->err) {
         int bad = 0;
         c->u16 = utf8_to_utf16(s, k, &c->nu16, &bad);
@@ -936,10 +964,9 @@ static int read_content(yo_doc *doc, dec_t *d, uint8_t info, ycontent *c) {
     }
     case CT_FORMAT: {
       st = d->pos;
-      uint32_t k = dvu(d);
-      dbytes(d, k);
-      k = dvu(d);
-      const uint8_t *js = dbytes(d, k);
+      uint32_t k;
+      dstr(d, NULL);
+      const uint8_t *js = dstr(d, &k);
       if (!d->err && !json_start_ok(js, k)) d->err = 1;
       if (!d->err) c->raw = ystr_dup(d->p + st, (uint32_t)(d->pos - st));
       break;
@@ -949,8 +976,7 @@ static int read_content(yo_doc *doc, dec_t *d, uint8_t info, ycontent *c) {
       ytype *t = ytype_new(doc, (int)tr);
       if (tr == 3 || tr == 5) {
         st = d->pos;
-        uint32_t k = dvu(d);
-        dbytes(d, k);
+        dstr(d, NULL);
         if (!d->err) t->node_name = ystr_dup(d->p + st, (uint32_t)(d->pos - st));
       } else if (tr > 6) d->err = 1;
       c->type = t;
@@ -967,8 +993,7 @@ static int read_content(yo_doc *doc, dec_t *d, uint8_t info, ycontent *c) {
     }
     case CT_DOC: {
       st = d->pos;
-      uint32_t k = dvu(d);
-      dbytes(d, k);
+      dstr(d, NULL);
       dskip_any(d, 0);
       if (!d->err) c->raw = ystr_dup(d->p + st, (uint32_t)(d->pos - st));
       break;
@@ -1015,8 +1040,8 @@ static int read_structs(yo_doc *doc, dec_t *d, clients_refs *cr) {
           if (cant_copy_parent) {
             uint32_t pinfo = dvu(d);
             if (pinfo == 1) {
-              uint32_t k = dvu(d);
-              const uint8_t *nm = dbytes(d, k);
+              uint32_t k;
+              const uint8_t *nm = dstr(d, &k);
               if (!d->err) { s->ptag = PT_ROOT; s->parent = root_type(doc, nm, k); }
             } else {
               s->ptag = PT_ID;
@@ -1024,12 +1049,20 @@ static int read_structs(yo_doc *doc, dec_t *d, clients_refs *cr) {
               s->parent_id.clock = dvu(d);
             }
             if (info & 0x20) {
-              uint32_t k = dvu(d);
-              const uint8_t *ps = dbytes(d, k);
+              uint32_t k;
+              const uint8_t *ps = dstr(d, &k);
               if (!d->err) { s->has_psub = 1; s->psub = ystr_dup(ps, k); }
             }
           }
           if (read_content(doc, d, info, &s->c) < 0) break;
+          /* own-client references at or past the item's clock: Yjs takes them as present
+           * (getMissing) and fails to find them (a TypeError in integrateStructs): refused */
+          if ((s->has_origin && s->origin.client == client && s->origin.clock >= clock) ||
+              (s->has_rorigin && s->rorigin.client == client && s->rorigin.clock >= clock) ||
+              (cant_copy_parent && s->ptag == PT_ID && s->parent_id.client == client && s->parent_id.clock >= clock)) {
+            d->err = 1;
+            break;
+          }
           s->len = content_len(&s->c);
           s->countable = (uint8_t)content_countable(&s->c);
           break;

@@ -1,0 +1,76 @@
+"""Corrupted updates against Yjs 13.5.16 itself (tests/golden/corrupt.json,
+tests/golden/gen/gen_corrupt_fixtures.js): valid updates with one byte overwritten, or cut short,
+applied after a base update. The engine must refuse exactly what Yjs refuses (Y.applyUpdate
+throws: bad content refs, unknown `any` tags, out-of-range varuints, strings that are not
+shortest-form UTF-8 — lib0's decodeURIComponent, L0@1937 —, ran past the end) and otherwise give
+Yjs's state and state vector; after a refusal the doc holds what Yjs's doc holds (the struct
+section is read whole before anything is integrated; a delete-set error comes after it).
+
+Every case runs on each small-update decode path (lane per update, wavefront per update, chunk
+path) — the small sources are <= 16 KiB — and the large source on the chunk path.
+"""
+import hashlib
+import json
+import os
+
+import pytest
+
+crdt_amd = pytest.importorskip("crdt_amd")
+
+pytestmark = pytest.mark.gpu
+HERE = os.path.dirname(os.path.abspath(__file__))
+# Yjs errors the engine does not reproduce yet: JSON.parse of a ContentJSON / Embed / Format value
+# (only the value's first character is checked) — listed, not hidden
+KNOWN_GAPS = ("SyntaxError",)
+
+
+@pytest.fixture(scope="module")
+def corrupt():
+    with open(os.path.join(HERE, "golden", "corrupt.json")) as f:
+        return json.load(f)
+
+
+def _bad(fx, c):
+    u = bytearray(bytes.fromhex(fx["sources"][c["src"]]))
+    if "cut" in c:
+        return bytes(u[: c["cut"]])
+    u[c["at"]] = c["val"]
+    return bytes(u)
+
+
+@pytest.mark.parametrize("mode", ["direct", "wave", "chunks"])
+def test_corrupt_like_yjs(corrupt, mode, monkeypatch):
+    monkeypatch.setenv("YCRDT_DECODE", "direct" if mode == "wave" else mode)
+    if mode in ("wave", "direct"):
+        monkeypatch.setenv("YCRDT_DIRECT_WAVE", "1" if mode == "wave" else "0")
+    base = bytes.fromhex(corrupt["base"])
+    checked = gaps = 0
+    for c in corrupt["cases"]:
+        bad = _bad(corrupt, c)
+        d = crdt_amd.Doc(client_id=5)
+        d.apply_update(base)
+        raised = None
+        try:
+            d.apply_update(bad)
+        except crdt_amd.YcrdtError as e:
+            raised = e
+        if c["threw"] and c["threw"].startswith(KNOWN_GAPS) and raised is None:
+            gaps += 1
+            continue
+        assert (raised is not None) == (c["threw"] is not None), (c["name"], c["threw"], raised)
+        if c["state_sha256"]:
+            assert hashlib.sha256(d.encode_state_as_update()).hexdigest() == c["state_sha256"], (c["name"], c["threw"])
+        assert d.encode_state_vector().hex() == c["sv"], c["name"]
+        checked += 1
+    assert checked >= len(corrupt["cases"]) - 2 and gaps <= 2
+
+
+def test_corrupt_in_one_batch_fails_the_batch(corrupt):
+    """A batch holding a refused update fails as a whole (Y.applyUpdate of it throws)."""
+    base = bytes.fromhex(corrupt["base"])
+    for c in corrupt["cases"][:60]:
+        if not c["threw"] or c["threw"].startswith(KNOWN_GAPS):
+            continue
+        b = crdt_amd.Batch([base, _bad(corrupt, c)])
+        with pytest.raises(crdt_amd.YcrdtError):
+            b.merge()

@@ -7,8 +7,7 @@ leave the settling; a lane whose entry changed since its walk blocks that exclus
 after it — the race fixed in eb51886). These cases aim at the settling rules: string values that
 are themselves valid struct encodings (chains beside the true one), periodic struct streams (chains
 locked in a wrong phase), delete sets that parse as long struct chains, truncated and corrupted
-updates (refused as Yjs refuses them, readClientsStructRefs Y@19286 / readDeleteSet Y@11105), and a
-seeded fuzz of mixed shapes. YCRDT_DEBUG_DECODE=1 makes the engine report the wave decoder's
+updates (test_gpu_corrupt.py, against Yjs's own results in every decode mode), and a seeded fuzz of mixed shapes. YCRDT_DEBUG_DECODE=1 makes the engine report the wave decoder's
 work, so every case checks that k_wdecode really took the update.
 """
 import random
@@ -88,7 +87,7 @@ def _periodic(n, seed, width=6):
     return d.encode_state_as_update()
 
 
-@pytest.mark.parametrize("n", [60, 200, 700, 1000])
+@pytest.mark.parametrize("n", [60, 200, 500, 780])
 def test_wave_periodic_streams(wave, capfd, n):
     """Identical struct shapes back to back: every lane's chain can lock into a wrong phase."""
     for seed in range(3):
@@ -121,43 +120,19 @@ def test_wave_long_delete_sets(wave, capfd):
     delta = dels.encode_state_as_update(sv)
     assert len(delta) <= WAVE_MAX
     _check([b, delta], capfd)
-    _check([delta, b], capfd)  # the delete set arrives first: pending ranges, then applied
+    # applied one at a time (the delta merges behind the doc's state)
+    d = crdt_amd.Doc(client_id=0x7FFFFFF0)
+    d.apply_update(b)
+    capfd.readouterr()
+    d.apply_update(delta)
+    ref = ODoc(0x7FFFFFF0)
+    ref.apply_update(b)
+    ref.apply_update(delta)
+    _same(d, ref)
+    assert _wave_count(capfd.readouterr().err) > 0
 
 
-def test_wave_truncated_and_corrupted(wave, capfd):
-    snap = _snapshot(12, 6, 8)
-    assert len(snap) <= WAVE_MAX
-    base = ODoc(3)
-    base.map_set("users", "a", any_int(1))
-    cuts = sorted({len(snap) // 3, len(snap) // 2, len(snap) - 1, len(snap) - 3, 7, 40})
-    for cut in cuts:
-        ref = ODoc(5)
-        ref.apply_update(base.encode_state_as_update())
-        with pytest.raises(Exception):
-            ref.apply_update(snap[:cut])
-        d = crdt_amd.Doc(client_id=5)
-        d.apply_update(base.encode_state_as_update())
-        with pytest.raises(crdt_amd.YcrdtError):
-            d.apply_update(snap[:cut])
-        _same(d, ref)
-    rng = random.Random(4)
-    for at in [rng.randrange(2, len(snap)) for _ in range(24)]:
-        for val in (0x1F, 0xFF, 0x00, 0x84):
-            bad = bytearray(snap)
-            bad[at] = val
-            ref = ODoc(5)
-            try:
-                ref.apply_update(bytes(bad))
-                want = ref.encode_state_as_update()
-            except Exception:
-                want = None
-            d = crdt_amd.Doc(client_id=5)
-            if want is None:
-                with pytest.raises(crdt_amd.YcrdtError):
-                    d.apply_update(bytes(bad))
-            else:
-                d.apply_update(bytes(bad))
-                assert d.encode_state_as_update() == want, (at, val)
+# truncated and corrupted updates in wave mode: tests/test_gpu_corrupt.py (Yjs's own results)
 
 
 def test_wave_fuzz_mixed_shapes(wave, capfd):
