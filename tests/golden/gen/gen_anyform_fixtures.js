@@ -1,0 +1,75 @@
+#!/usr/bin/env node
+// `any` encodings lib0's writeAny never produces, but readAny accepts (TEST INFRASTRUCTURE ONLY;
+// runs in the build container against the in-image Yjs 13.5.16 + lib0 0.2.42). Yjs keeps `any`
+// content as JS values and writes them back with writeAny, so its bytes come out in writeAny's
+// form: integer-valued floats become varints, float64s that float32 holds become float32, NaN
+// becomes 0x7FF8000000000000, overlong varuints / varints shrink, positive varints past
+// 0x7FFFFFFF become floats. Object keys follow Object.keys order (array indices first) — the
+// engine refuses those (listed with `refused: true`).
+//
+// Every update is one YMap set on root 'users' by client 77, hand-written:
+//   [1 section][1 struct][client 77][clock 0] info=0x28 (Any, parentSub) parentInfo=1 'users'
+//   key count=1 <value bytes> [empty delete set]
+// Usage: node gen_anyform_fixtures.js <out_dir>  ->  <out_dir>/anyform.json
+'use strict';
+const fs = require('fs');
+const path = require('path');
+const { loadYjs } = require('./load_yjs.js');
+const { canonicalUpdate, canonicalSv, hex } = require('./v1.js');
+
+const Y = loadYjs();
+
+const vs = (s) => { const b = Buffer.from(s, 'utf8'); return [b.length, ...b]; };
+const f64 = (x) => { const b = Buffer.alloc(8); b.writeDoubleBE(x); return [...b]; };
+const f32 = (x) => { const b = Buffer.alloc(4); b.writeFloatBE(x); return [...b]; };
+const update = (key, value, client = 77) => Uint8Array.from([1, 1, client, 0, 0x28, 1, ...vs('users'), ...vs(key), 1, ...value, 0]);
+
+const values = {
+  f64_int: [123, ...f64(7)],
+  f64_neg_int: [123, ...f64(-5)],
+  f64_int_max: [123, ...f64(2147483647)],
+  f64_2p31: [123, ...f64(2147483648)],
+  f64_1e10: [123, ...f64(1e10)],
+  f64_half: [123, ...f64(0.5)],
+  f64_inf: [123, ...f64(Infinity)],
+  f64_ninf: [123, ...f64(-Infinity)],
+  f64_tenth: [123, ...f64(0.1)],
+  f64_nan_payload: [123, 0x7f, 0xf8, 0, 0, 0, 0, 0, 1],
+  f64_neg_zero: [123, ...f64(-0)],
+  f32_int: [124, ...f32(3)],
+  f32_nan: [124, 0x7f, 0xc0, 0, 0],
+  f32_frac: [124, ...f32(1.25)],
+  vi_overlong: [125, 0x87, 0x00],
+  vi_overlong_neg: [125, 0xc7, 0x80, 0x00],
+  vi_neg_zero: [125, 0x40],
+  vi_big_pos: [125, 0x80, 0x80, 0x80, 0x80, 0x0b],          // magnitude past 0x7FFFFFFF
+  vi_wrap: [125, 0x81, 0x80, 0x80, 0x80, 0x80, 0x01],       // a group shifted past bit 31 (lib0 wraps)
+  str_overlong_len: [119, 0x83, 0x00, 0x61, 0x62, 0x63],
+  bytes_overlong_len: [116, 0x82, 0x00, 1, 2],
+  arr_overlong_count: [117, 0x82, 0x00, 125, 1, 123, ...f64(2)],
+  obj_overlong_key: [118, 1, 0x81, 0x00, 0x6b, 123, ...f64(4)],
+  obj_nested_floats: [118, 2, ...vs('a'), 117, 2, 123, ...f64(1), 124, ...f32(0.5), ...vs('b'), 118, 1, ...vs('c'), 123, ...f64(0.1)],
+  bigint: [122, 0, 0, 0, 0, 0, 0, 0, 9],
+  obj_index_keys_out_of_order: [118, 2, ...vs('b'), 125, 1, ...vs('2'), 125, 2],
+  obj_proto_key: [118, 1, ...vs('__proto__'), 125, 1],
+};
+const refused = new Set(['obj_index_keys_out_of_order', 'obj_proto_key']);
+
+const cases = [];
+for (const [name, v] of Object.entries(values)) {
+  const u = update('k_' + name, v);
+  const d = new Y.Doc(); d.clientID = 5;
+  Y.applyUpdate(d, u);
+  const other = new Y.Doc(); other.clientID = 33; other.getMap('users').set('x', 1.5);
+  const o = Y.encodeStateAsUpdate(other);
+  const merged = Y.mergeUpdates([u, o]);
+  const diff = Y.diffUpdate(u, new Uint8Array([0]));
+  cases.push({ name, update: hex(u), other: hex(o), refused: refused.has(name),
+               state: hex(canonicalUpdate(Y.encodeStateAsUpdate(d))), sv: hex(canonicalSv(Y.encodeStateVector(d))),
+               json: name === 'bigint' ? null : JSON.parse(JSON.stringify(d.getMap('users').toJSON())),
+               merged: hex(canonicalUpdate(merged)), diff: hex(canonicalUpdate(diff)) });
+}
+const outDir = process.argv[2] || path.join(__dirname, '..');
+fs.writeFileSync(path.join(outDir, 'anyform.json'), JSON.stringify({ yjs: '13.5.16', cases }, null, 0));
+console.log(`anyform.json: ${cases.length} cases`);
+for (const c of cases) console.log(c.name, c.state.length / 2, JSON.stringify(c.json).slice(0, 60));
