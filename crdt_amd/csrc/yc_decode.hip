@@ -1952,7 +1952,8 @@ __global__ __launch_bounds__(256) void k_struct_decode(Work w, uint32_t nstructs
     }
     canon_hdr = h == v.cpos - p0 - 1;
   }
-  w.s_pk[i] = (uint8_t)(pk | (canon_hdr ? 0u : 0x80u));
+  // bit 6: the content's `any` values are not in writeAny's form (the encoders re-encode them)
+  w.s_pk[i] = (uint8_t)(pk | (canon_hdr ? 0u : 0x80u) | ((v.anyf & ANY_REENCODE) ? 0x40u : 0u));
   if (pk != 0) {
     w.s_pa[i] = pa;
     w.s_pb[i] = pb;

@@ -55,7 +55,7 @@ __device__ __forceinline__ uint32_t encode_struct(const Work& w, uint32_t nclien
     const uint32_t f = w.g_flags[a], src = w.g_src[a], ga = w.g_start[a], gb = w.g_start[b];
     const uint32_t slen = w.s_len[src], spos = w.s_pos[src], scpos = w.s_cpos[src], scend = w.s_cend[src];
     const uint32_t info0 = w.s_info[src], spk = w.s_pk[src];
-    if ((f & (SEG_ITEM | SEG_EXPLICIT)) == (SEG_ITEM | SEG_EXPLICIT) && gb - ga == slen && !(spk & 0x80u)) {
+    if ((f & (SEG_ITEM | SEG_EXPLICIT)) == (SEG_ITEM | SEG_EXPLICIT) && gb - ga == slen && !(spk & 0xC0u)) {
       const bool del = (f & SEG_DEL) != 0;
       const uint32_t hdr = scpos - spos - 1;  // origin / right origin / parent / parentSub bytes
       if (!WRITE) return 1 + hdr + (del ? vu_size(slen) : scend - scpos);
@@ -166,10 +166,18 @@ __device__ __forceinline__ uint32_t encode_struct_general(const Work& w, uint32_
     if (WRITE) p = wr_vu(out, p, len - off);
     size += vu_size(len - off);
   } else if ((ref == REF_ANY || ref == REF_JSON) && b == a + 1 && off == 0 && k0 == sclk && len == slen) {
-    // the whole content of one source struct (the common case): its element bytes verbatim
-    const uint32_t nbytes = scend - scel;
-    if (WRITE) { p = wr_vu(out, p, len); p = copy_bytes(out, p, sb + scel, nbytes); }
-    size += vu_size(len) + nbytes;
+    // the whole content of one source struct (the common case): its element bytes verbatim (in
+    // writeAny's form when the input's were not, s_pk bit 6)
+    if (ref == REF_ANY && (w.s_pk[src] & 0x40u)) {
+      if (WRITE) p = wr_vu(out, p, len);
+      const uint32_t nb = any_canon<WRITE>(sb, scel, scend, 0, len, out, p);
+      if (WRITE) p += nb;
+      size += vu_size(len) + nb;
+    } else {
+      const uint32_t nbytes = scend - scel;
+      if (WRITE) { p = wr_vu(out, p, len); p = copy_bytes(out, p, sb + scel, nbytes); }
+      size += vu_size(len) + nbytes;
+    }
   } else if (ref == REF_ANY || ref == REF_JSON || ref == REF_STRING) {
     // elements of every segment from unit k0 + off on, sliced out of their source structs
     uint32_t nbytes = 0;
@@ -180,6 +188,12 @@ __device__ __forceinline__ uint32_t encode_struct_general(const Work& w, uint32_
         const uint32_t sb = w.s_clock[sr];  // source struct's first clock
         const uint32_t u0 = max((uint32_t)(w.g_start[s] - base), k0 + off), u1 = (uint32_t)(w.g_start[s + 1] - base);
         if (u1 <= u0) continue;
+        if (ref == REF_ANY && (w.s_pk[sr] & 0x40u)) {  // flagged content: writeAny's form
+          const uint32_t nb = any_canon<WRITE>(struct_bytes(w, sr), w.s_celem[sr], w.s_cend[sr], u0 - sb, u1 - sb, out, p);
+          if (pass == 1) p += nb;
+          else nbytes += nb;
+          continue;
+        }
         uint32_t b0 = 0, b1 = 0;
         if (!content_slice(w, sr, u0 - sb, u1 - sb, b0, b1)) { raise_err(&w.ctr->err, ERR_UNSUPPORTED); return size; }
         if (pass == 1) p = copy_bytes(out, p, struct_bytes(w, sr) + b0, b1 - b0);

@@ -468,6 +468,10 @@ __device__ uint32_t encode_event(const Work& w, uint32_t client, uint32_t e, uin
   if (ref == REF_DELETED) {
     if (WRITE) p = wr_vu(out, p, len);
     size += vu_size(len);
+  } else if (ref == REF_ANY && (w.s_pk[src] & 0x40u)) {  // `any` values not in writeAny's form
+    if (WRITE) p = wr_vu(out, p, len);
+    const uint32_t nb = any_canon<WRITE>(w.bytes, w.s_celem[src], w.s_cend[src], off, off + len, out, p);
+    size += vu_size(len) + nb;
   } else if (ref == REF_ANY || ref == REF_JSON || ref == REF_STRING) {
     uint32_t b0 = 0, b1 = 0;
     if (!content_slice(w, src, off, off + len, b0, b1)) { raise_err(&w.ctr->err, ERR_UNSUPPORTED); return size; }

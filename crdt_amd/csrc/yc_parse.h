@@ -109,11 +109,86 @@ YC_HDI void skip_str(const Src& b, uint32_t& p, uint32_t end, bool& ok) {
   if (UTF8 && ok && !utf8_valid(b, st, n)) ok = false;
 }
 
+// ---- lib0 writeAny canonical forms (L0@1937: readAny -> JS value -> writeAny). Yjs stores
+// `any` content as JS values and writes them back, so an input encoding that is not what writeAny
+// produces comes out different: an overlong varuint / varint, an integer-valued float (-> varint
+// when <= 0x7FFFFFFF), a float64 that float32 holds exactly (-> float32), a NaN (-> float64
+// 0x7FF8000000000000), a positive varint past 0x7FFFFFFF (-> float32 / float64). Such values are
+// flagged ANY_REENCODE and the encoders write them canonically (any_canon below). What needs JS
+// object semantics — array-index keys after others or out of order (Object.keys order), the key
+// "__proto__", a negative integer past 2^32 (writeVarInt's 32-bit shifts) — is ANY_UNSUP: refused.
+enum : uint32_t { ANY_REENCODE = 1u, ANY_UNSUP = 2u };
+YC_HDI uint32_t vu_overlong(const uint8_t* __restrict__ b, uint32_t p0, uint32_t p1) {  // [p0, p1) one varuint
+  return (p1 - p0 > 1 && b[p1 - 1] == 0u) ? ANY_REENCODE : 0u;
+}
+// readVarInt (lib0 0.2.42: 32-bit shifts, so group k lands at bit (6 + 7k) & 31): sign, magnitude
+YC_HDI uint32_t vi_decode(const uint8_t* __restrict__ b, uint32_t p0, uint32_t p1, bool& neg) {
+  uint32_t r = b[p0], n = r & 0x3Fu, e = 6;
+  neg = (r & 0x40u) != 0;
+  for (uint32_t q = p0 + 1; q < p1; ++q) { n |= (uint32_t)(b[q] & 0x7Fu) << (e & 31u); e += 7; }
+  return n;
+}
+YC_HDI uint32_t vi_size(uint32_t m) { uint32_t s = 1; m >>= 6; while (m) { ++s; m >>= 7; } return s; }
+YC_HDI uint32_t vi_flag(const uint8_t* __restrict__ b, uint32_t p0, uint32_t p1) {
+  bool neg;
+  const uint32_t m = vi_decode(b, p0, p1, neg);
+  if (!neg && m > 0x7FFFFFFFu) return ANY_REENCODE;  // writeAny: a float
+  return vi_size(m) == p1 - p0 ? 0u : ANY_REENCODE;  // (a wrapped overlong form is longer too)
+}
+YC_HDI uint32_t be32(const uint8_t* __restrict__ b, uint32_t p) {
+  return ((uint32_t)b[p] << 24) | ((uint32_t)b[p + 1] << 16) | ((uint32_t)b[p + 2] << 8) | b[p + 3];
+}
+YC_HDI uint64_t be64(const uint8_t* __restrict__ b, uint32_t p) { return ((uint64_t)be32(b, p) << 32) | be32(b, p + 4); }
+// writeAny(number) of a double: 0 varint, 1 float32, 2 float64, 3 refused (a negative integer
+// past 2^32, which writeVarInt's 32-bit arithmetic garbles)
+YC_HDI uint32_t num_form(double x) {
+  if (x == x && x == (double)(long long)x && x >= -9.2e18 && x <= 9.2e18) {  // an integer (finite)
+    if (x <= 2147483647.0) return x > -4294967296.0 ? 0u : 3u;
+  }
+  if (x != x) return 2u;  // NaN: float32 does not compare equal
+  const float f = (float)x;
+  return (double)f == x ? 1u : 2u;
+}
+YC_HDI double f32_of(uint32_t bits) { union { uint32_t u; float f; } c; c.u = bits; return (double)c.f; }
+YC_HDI double f64_of(uint64_t bits) { union { uint64_t u; double d; } c; c.u = bits; return c.d; }
+YC_HDI uint32_t f32_flag(uint32_t bits) {
+  const double x = f32_of(bits);
+  const uint32_t k = num_form(x);
+  return k == 3 ? ANY_UNSUP : k == 1 ? 0u : ANY_REENCODE;
+}
+YC_HDI uint32_t f64_flag(uint64_t bits) {
+  const double x = f64_of(bits);
+  const uint32_t k = num_form(x);
+  if (k == 3) return ANY_UNSUP;
+  if (k != 2) return ANY_REENCODE;
+  return (x != x && bits != 0x7FF8000000000000ull) ? ANY_REENCODE : 0u;
+}
+// an object key that JS orders first (an array index: "0" or [1-9][0-9]* below 2^32 - 1), or "__proto__"
+YC_HDI int64_t key_index(const uint8_t* __restrict__ b, uint32_t p, uint32_t n) {
+  if (n == 0 || n > 10 || (n > 1 && b[p] == '0')) return -1;
+  uint64_t v = 0;
+  for (uint32_t i = 0; i < n; ++i) {
+    const uint32_t c = b[p + i];
+    if (c < '0' || c > '9') return -1;
+    v = v * 10 + (c - '0');
+  }
+  return v < 0xFFFFFFFFull ? (int64_t)v : -1;
+}
+YC_HDI bool key_proto(const uint8_t* __restrict__ b, uint32_t p, uint32_t n) {
+  const char* k = "__proto__";
+  if (n != 9) return false;
+  for (uint32_t i = 0; i < 9; ++i)
+    if (b[p + i] != (uint8_t)k[i]) return false;
+  return true;
+}
+
 // readAny (L0@1937 B): iterative skip with an explicit container stack of depth DEPTH (deeper
 // nesting fails the parse: speculative callers use a shallow stack, exact callers a deep one).
 template <int DEPTH, bool UTF8 = false>
-YC_HD inline bool skip_any(const uint8_t* __restrict__ b, uint32_t& p, uint32_t end, uint32_t& steps) {
+YC_HD inline bool skip_any(const uint8_t* __restrict__ b, uint32_t& p, uint32_t end, uint32_t& steps, uint32_t* cflags = nullptr) {
   const PtrSrc src{b};
+  uint32_t cf = 0;                  // ANY_* flags (UTF8 mode: the exact parse checks the encoding)
+  int64_t lastkey[UTF8 ? DEPTH + 1 : 1];  // per object level: the last array-index key, or -2 after a string key
   // A level is kept only while members FOLLOW the one being read (rem[d] >= 1): the last member of
   // a container is read in the container's place (a tail position), so nesting along last members
   // — [[[..]]], {a: {b: ..}}, however deep — takes no stack, and DEPTH bounds only containers
@@ -130,32 +205,51 @@ YC_HD inline bool skip_any(const uint8_t* __restrict__ b, uint32_t& p, uint32_t 
     uint32_t tag = b[p++];
     switch (tag) {
       case 127: case 126: case 121: case 120: break;
-      case 125: skip_vi(b, p, end, ok); break;
-      case 124: skip_bytes(p, 4, end, ok); break;
-      case 123: case 122: skip_bytes(p, 8, end, ok); break;
+      case 125: { const uint32_t q0 = p; skip_vi(b, p, end, ok); if (UTF8 && ok) cf |= vi_flag(b, q0, p); break; }
+      case 124: { const uint32_t q0 = p; skip_bytes(p, 4, end, ok); if (UTF8 && ok) cf |= f32_flag(be32(b, q0)); break; }
+      case 123: { const uint32_t q0 = p; skip_bytes(p, 8, end, ok); if (UTF8 && ok) cf |= f64_flag(be64(b, q0)); break; }
+      case 122: skip_bytes(p, 8, end, ok); break;
       case 119: {
+        const uint32_t q0 = p;
         uint32_t n = rd_vu(b, p, end, ok);
         const uint32_t st = p;
         if (ok) skip_bytes(p, n, end, ok);
         if (UTF8 && ok && !utf8_valid(src, st, n)) return false;
+        if (UTF8 && ok) cf |= vu_overlong(b, q0, st);
         break;
       }
-      case 116: { uint32_t n = rd_vu(b, p, end, ok); if (ok) skip_bytes(p, n, end, ok); break; }
+      case 116: {
+        const uint32_t q0 = p;
+        uint32_t n = rd_vu(b, p, end, ok);
+        if (UTF8 && ok) cf |= vu_overlong(b, q0, p);
+        if (ok) skip_bytes(p, n, end, ok);
+        break;
+      }
       case 118: case 117: {
+        const uint32_t q0 = p;
         uint32_t n = rd_vu(b, p, end, ok);
         if (!ok) return false;
+        if (UTF8) cf |= vu_overlong(b, q0, p);
         if (n > 0) {
           if (n > 1) {  // members follow this one: keep the level
             if (d == DEPTH) { steps = 0; return false; }  // too deep: "unknown" (-1), never "malformed"
             rem[d] = n - 1;
             if (tag == 118) objmask |= 1u << d; else objmask &= ~(1u << d);
+            if (UTF8) lastkey[d] = -1;
             ++d;
           }
           if (tag == 118) {  // the first member's key
+            const uint32_t q0 = p;
             uint32_t k = rd_vu(b, p, end, ok);
             const uint32_t st = p;
             if (ok) skip_bytes(p, k, end, ok);
             if (UTF8 && ok && !utf8_valid(src, st, k)) return false;
+            if (UTF8 && ok) {
+              cf |= vu_overlong(b, q0, st);
+              if (key_proto(b, st, k)) cf |= ANY_UNSUP;
+              const int64_t ki = key_index(b, st, k);
+              if (n > 1) lastkey[d - 1] = ki >= 0 ? ki : -2;
+            }
           }
           if (!ok) return false;
           continue;  // read the first member value
@@ -167,13 +261,26 @@ YC_HD inline bool skip_any(const uint8_t* __restrict__ b, uint32_t& p, uint32_t 
     if (!ok) return false;
     // a value completed: the innermost kept level moves to its next member (the last one is read
     // in the level's place)
-    if (d == 0) return true;
+    if (d == 0) {
+      if (UTF8 && cflags) *cflags |= cf;
+      return true;
+    }
     const uint32_t lvl = (uint32_t)d - 1;
     if ((objmask >> lvl) & 1u) {  // the next member's key
+      const uint32_t q0 = p;
       uint32_t k = rd_vu(b, p, end, ok);
       const uint32_t st = p;
       if (ok) skip_bytes(p, k, end, ok);
       if (!ok || (UTF8 && !utf8_valid(src, st, k))) return false;
+      if (UTF8) {
+        cf |= vu_overlong(b, q0, st);
+        if (key_proto(b, st, k)) cf |= ANY_UNSUP;
+        // Object.keys order: array-index keys first, ascending; then the others in insertion order
+        // (a repeated string key keeps its first place; not detected here)
+        const int64_t ki = key_index(b, st, k), prev = lastkey[lvl];
+        if (ki >= 0 && (prev == -2 || (prev >= 0 && ki <= prev))) cf |= ANY_UNSUP;
+        lastkey[lvl] = ki >= 0 ? ki : -2;
+      }
     }
     if (--rem[lvl] == 0) --d;
   }
@@ -182,11 +289,12 @@ YC_HD inline bool skip_any(const uint8_t* __restrict__ b, uint32_t& p, uint32_t 
 // Out of line: the container stack costs DEPTH registers wherever skip_any is inlined, so struct
 // parsers take scalar values inline and hand containers to this call.
 // (State goes in and out by value: taking the caller's cursor by address would put it in scratch.)
-struct AnySkip { uint32_t p, steps, ok; };
+struct AnySkip { uint32_t p, steps, ok, cf; };
 template <int DEPTH, bool UTF8 = false>
 YC_HD __attribute__((noinline)) AnySkip skip_any_nl(const uint8_t* __restrict__ b, uint32_t p, uint32_t end, uint32_t steps) {
-  const bool ok = skip_any<DEPTH, UTF8>(b, p, end, steps);
-  return AnySkip{p, steps, ok ? 1u : 0u};
+  uint32_t cf = 0;
+  const bool ok = skip_any<DEPTH, UTF8>(b, p, end, steps, &cf);
+  return AnySkip{p, steps, ok ? 1u : 0u, cf};
 }
 
 // Decoded view of one struct (Y@19286 readClientsStructRefs + readItemContent).
@@ -202,6 +310,7 @@ struct StructView {
   uint32_t psub_pos, psub_len;  // varString (incl. length prefix)
   uint32_t cpos, cend; // content bytes [cpos, cend)
   uint32_t nel;        // Any/JSON element count
+  uint32_t anyf;       // ANY_* flags of the content's `any` values (FULL parses)
 };
 
 // Byte sources for parse_struct: the lib0 readers over a plain pointer (host and device); the
@@ -222,7 +331,7 @@ YC_HD inline int parse_struct(const Src& b, uint32_t& p, uint32_t end, uint32_t 
   if (p >= end) return -2;
   uint32_t info = b.u8(p++);
   uint32_t ref = info & 31u;
-  if (FULL) { v->info = (uint8_t)info; v->ref = (uint8_t)ref; v->pkind = 0; v->has_psub = 0; v->nel = 0; }
+  if (FULL) { v->info = (uint8_t)info; v->ref = (uint8_t)ref; v->pkind = 0; v->has_psub = 0; v->nel = 0; v->anyf = 0; }
   if (ref == REF_GC || ref == REF_SKIP) {
     uint32_t len = b.vu(p, end, ok);
     if (FULL) { v->len = len; v->cpos = v->cend = p; }
@@ -316,19 +425,27 @@ YC_HD inline int parse_struct(const Src& b, uint32_t& p, uint32_t end, uint32_t 
       break;
     }
     case REF_ANY: {
+      const uint32_t q0 = p;
       uint32_t n = b.vu(p, end, ok);
+      uint32_t cf = FULL && ok ? vu_overlong(b.b, q0, p) : 0u;
       len = n;
       for (uint32_t i = 0; i < n && ok; ++i) {
         const uint32_t tag = p < end ? b.u8(p) : 0u;
         if (p < end && steps > 0 && tag >= 116u && tag <= 127u && tag != 117u && tag != 118u) {  // a scalar: skip_any's one step
           --steps;
           ++p;
+          const uint32_t s0 = p;
           switch (tag) {
-            case 125: b.svi(p, end, ok); break;
-            case 124: skip_bytes(p, 4, end, ok); break;
-            case 123: case 122: skip_bytes(p, 8, end, ok); break;
-            case 119: skip_str<FULL>(b, p, end, ok); break;
-            case 116: { const uint32_t k = b.vu(p, end, ok); if (ok) skip_bytes(p, k, end, ok); break; }
+            case 125: b.svi(p, end, ok); if (FULL && ok) cf |= vi_flag(b.b, s0, p); break;
+            case 124: skip_bytes(p, 4, end, ok); if (FULL && ok) cf |= f32_flag(be32(b.b, s0)); break;
+            case 123: skip_bytes(p, 8, end, ok); if (FULL && ok) cf |= f64_flag(be64(b.b, s0)); break;
+            case 122: skip_bytes(p, 8, end, ok); break;
+            case 119: {
+              skip_str<FULL>(b, p, end, ok);
+              if (FULL && ok) { uint32_t q = s0; bool o2 = true; rd_vu(b.b, q, end, o2); cf |= vu_overlong(b.b, s0, q); }
+              break;
+            }
+            case 116: { const uint32_t k = b.vu(p, end, ok); if (FULL && ok) cf |= vu_overlong(b.b, s0, p); if (ok) skip_bytes(p, k, end, ok); break; }
             default: break;  // 127 undefined, 126 null, 121 false, 120 true
           }
         } else {
@@ -336,10 +453,12 @@ YC_HD inline int parse_struct(const Src& b, uint32_t& p, uint32_t end, uint32_t 
           p = r.p;
           steps = r.steps;
           ok = r.ok != 0;
+          cf |= r.cf;
         }
       }
       if (!ok && steps == 0) return -1;
-      if (FULL) v->nel = n;
+      if (FULL) { v->nel = n; v->anyf = cf; }
+      if (FULL && ok && (cf & ANY_UNSUP)) return -1;  // valid Yjs input the engine refuses (YCRDT_E_UNSUPPORTED)
       break;
     }
     case REF_DOC: {
@@ -349,6 +468,7 @@ YC_HD inline int parse_struct(const Src& b, uint32_t& p, uint32_t end, uint32_t 
         p = r.p;
         steps = r.steps;
         ok = r.ok != 0;
+        if (FULL && ok && r.cf) return -1;  // a ContentDoc's options not in writeAny's form: refused
       }
       if (!ok && steps == 0) return -1;
       break;

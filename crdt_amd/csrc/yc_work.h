@@ -437,6 +437,90 @@ static __device__ __attribute__((noinline)) uint64_t content_slice_walk(const ui
   return got ? ((uint64_t)b1 << 32) | b0 : ~0ull;
 }
 
+// writeAny (L0@1937) of the `any` values [e0, e1) of a struct whose content is flagged
+// ANY_REENCODE (yc_parse.h): containers, keys and strings with shortest-form lengths, numbers in the
+// form writeAny picks for the JS number they decode to. Returns the bytes; writes them when WRITE.
+// Out of line (rare): a Work reference is never taken (the callers pass plain values).
+template <bool WRITE>
+__device__ __attribute__((noinline)) uint32_t any_canon(const uint8_t* __restrict__ by, uint32_t p, uint32_t end, uint32_t e0,
+                                                        uint32_t e1, uint8_t* __restrict__ out, uint64_t q0) {
+  uint64_t q = q0;
+  auto put = [&](uint32_t x) { if (WRITE) out[q] = (uint8_t)x; ++q; };
+  auto put_vu = [&](uint32_t v) { while (v > 0x7Fu) { put(0x80u | (v & 0x7Fu)); v >>= 7; } put(v); };
+  auto put_vi = [&](bool neg, uint32_t m) {
+    put((m > 63u ? 0x80u : 0u) | (neg ? 0x40u : 0u) | (m & 63u));
+    m >>= 6;
+    while (m) { put((m > 127u ? 0x80u : 0u) | (m & 127u)); m >>= 7; }
+  };
+  auto put_num = [&](double x) {
+    const uint32_t k = num_form(x);
+    if (k == 0) { put(125); put_vi(x < 0 || (x == 0 && signbit(x)), (uint32_t)fabs(x)); return; }
+    if (k == 1) { union { float f; uint32_t u; } c; c.f = (float)x; put(124); for (int s = 24; s >= 0; s -= 8) put((c.u >> s) & 0xFFu); return; }
+    union { double d; uint64_t u; } c; c.d = x;
+    if (x != x) c.u = 0x7FF8000000000000ull;
+    put(123);
+    for (int s = 56; s >= 0; s -= 8) put((uint32_t)(c.u >> s) & 0xFFu);
+  };
+  bool ok = true;
+  // members left per open container level (the elements of the content are one implicit level)
+  uint32_t rem[33];
+  uint32_t objm = 0;  // bit d: level d is an object
+  int d = 0;
+  rem[0] = e1;
+  uint32_t idx = 0;  // content element index at level 0
+  for (;;) {
+    // one value at p
+    if (d == 0 && idx >= e1) break;
+    const bool emit = idx >= e0;  // (constant while inside one content element)
+    const uint32_t tag = by[p++];
+    const uint32_t s0 = p;
+    switch (tag) {
+      case 127: case 126: case 121: case 120: if (emit) put(tag); break;
+      case 125: {
+        skip_vi(by, p, end, ok);
+        bool neg;
+        const uint32_t m = vi_decode(by, s0, p, neg);
+        if (emit) { if (!neg && m > 0x7FFFFFFFu) put_num((double)m); else { put(125); put_vi(neg, m); } }
+        break;
+      }
+      case 124: p += 4; if (emit) put_num(f32_of(be32(by, s0))); break;
+      case 123: p += 8; if (emit) put_num(f64_of(be64(by, s0))); break;
+      case 122: p += 8; if (emit) { put(122); for (uint32_t i = s0; i < p; ++i) put(by[i]); } break;
+      case 119: case 116: {
+        const uint32_t n = rd_vu(by, p, end, ok);
+        if (emit) { put(tag); put_vu(n); for (uint32_t i = 0; i < n; ++i) put(by[p + i]); }
+        p += n;
+        break;
+      }
+      default: {  // 117 array / 118 object
+        const uint32_t n = rd_vu(by, p, end, ok);
+        if (emit) { put(tag); put_vu(n); }
+        if (n > 0) {
+          if (d >= 32) return 0;  // (the decoder's stack bound: never reached for flagged content)
+          ++d;
+          rem[d] = n;
+          if (tag == 118) objm |= 1u << d; else objm &= ~(1u << d);
+          if (tag == 118) { const uint32_t k = rd_vu(by, p, end, ok); if (emit) { put_vu(k); for (uint32_t i = 0; i < k; ++i) put(by[p + i]); } p += k; }
+          continue;
+        }
+        break;
+      }
+    }
+    // a value completed: pop finished levels, read the next key of an object
+    for (;;) {
+      if (d == 0) { ++idx; break; }
+      if (--rem[d] == 0) { --d; continue; }
+      if ((objm >> d) & 1u) {
+        const uint32_t k = rd_vu(by, p, end, ok);
+        if (idx >= e0) { put_vu(k); for (uint32_t i = 0; i < k; ++i) put(by[p + i]); }
+        p += k;
+      }
+      break;
+    }
+  }
+  return (uint32_t)(q - q0);
+}
+
 // per-client scratch arrays inside Work::cc
 enum : uint32_t {
   CC_FIRST_OUT = 0, CC_FIRST_INCL, CC_NINCL, CC_HDR, CC_BLK, CC_BLKPOS, CC_NRUNS, CC_FIRST_RUN,
