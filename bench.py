@@ -872,50 +872,76 @@ def run_rank(args, report=None):
     value = items_step * args.steps / dt
     phases = [(n, m / args.steps) for n, m in phase_acc.items()]
 
-    # ---- roofline of the dominant kernel: k_resolve (key resolution + YMap winner settling), the
-    # longest single-kernel phase of the C2 merge ("merge.resolve" holds exactly that one launch; its
-    # HIP events are recorded on the engine stream the kernel runs on). Algorithmic bytes per segment
-    # (DESIGN.md §5.1): its flags, key word, origin link and origin unit read (16 B), its flags and
-    # final key written (8 B), and the winner slot of its origin read-modify-written (4 B) = 28 B.
-    # `traffic` is the HBM bytes per launch from the committed rocprofv3 PMC pass (2 x FETCH_SIZE +
-    # WRITE_SIZE, gfx950 correction; scripts/pmc.sh + scripts/pmc_summary.py).
-    ROOF_KERNEL, ROOF_PHASE, ROOF_B = "yc::k_resolve", "merge.resolve", 28
+    # ---- roofline of the dominant kernel. Every single-kernel phase of the merge (one launch,
+    # timed by the engine's HIP events on the stream it runs on) with its algorithmic bytes per
+    # unit: `roofline` is the one with the longest average launch, `kernels` lists
+    # them all. `traffic` is the HBM bytes per launch from the committed rocprofv3 PMC pass
+    # (2 x FETCH_SIZE + WRITE_SIZE, gfx950 correction; scripts/pmc.sh + scripts/pmc_summary.py).
+    S, G, OS = st.structs, st.segments, st.out_structs
+    roof_models = [
+        # phase, kernel, algorithmic bytes per launch, per-unit statement
+        ("decode.direct", "yc::k_direct", in_bytes + in_bytes * 3 // 8,
+         "every input byte read once + spec / final / section-start bitmaps (3 bits per input byte)"),
+        ("decode.structs", "yc::k_struct_decode", 42 * S + in_bytes,
+         "42 B per struct (position + section read, 34 B of struct columns written) + the struct's own bytes"),
+        ("merge.units", "yc::k_units", 37 * S + 5 * st.units,
+         "37 B of struct columns per struct + owner (4 B) and flag byte per unit"),
+        ("merge.segment_props", "yc::k_seg_props", 85 * G,
+         "85 B per segment (unit owner / flags + 7 source-struct columns + origin segment lookup read; "
+         "hop record, cidx / src / origin / right origin, winner slot written)"),
+        ("merge.resolve", "yc::k_resolve", 28 * G,
+         "28 B per segment (hop record read, flags / key written, winner slot read-modify-write)"),
+        ("encode.sizes", "yc::k_out_sizes", 46 * OS,
+         "46 B per output struct (segment bounds, flags, source + 6 struct columns read; size + client written)"),
+        ("encode.write", "yc::k_write_structs", 46 * OS + 2 * st.out_bytes,
+         "46 B of columns per output struct + every output byte copied (read from the input, written)"),
+    ]
     ph = dict(phases)
-    k_ms = ph.get(ROOF_PHASE, 0.0)
-    alg = ROOF_B * st.segments
+    kernels = []
+    for phase, kname, alg_b, per in roof_models:
+        k_ms = ph.get(phase, 0.0)
+        if k_ms <= 0:
+            continue
+        gbs = alg_b / (k_ms * 1e-3) / 1e9
+        kernels.append({"kernel": kname, "phase": phase, "avg_launch_ms": round(k_ms, 4), "alg_bytes_per_launch": int(alg_b),
+                        "alg_bytes_per_unit": per, "achieved_GBs": round(gbs, 2), "frac": round(gbs / HBM_PEAK_GBS, 5)})
+    dom = max(kernels, key=lambda k: k["avg_launch_ms"]) if kernels else None
+    ROOF_KERNEL = dom["kernel"] if dom else "yc::k_resolve"
     traffic, traffic_src = None, None
     pmc = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_c2_pmc.csv")))
-    if pmc:
-        with open(pmc[-1]) as f:
-            for r in csv.DictReader(f):
-                if r["kernel"] == ROOF_KERNEL:
-                    traffic = int(float(r["hbm_bytes"]))
-                    traffic_src = os.path.basename(pmc[-1])
-    # the whole merge's counter traffic from the same PMC pass (sum over its kernels, per merge)
-    # (per-dispatch averages x dispatches / merges when the summary counts dispatches: kernels
-    # launched several times per merge — scans, the k_sync rounds — count every launch)
-    pipe_traffic = None
+    rows = []
     if pmc:
         with open(pmc[-1]) as f:
             rows = list(csv.DictReader(f))
-        merges = max([int(r.get("dispatches") or 1) for r in rows if r["kernel"] == ROOF_KERNEL] or [1])
+        traffic_src = os.path.basename(pmc[-1])
+    for k in kernels:
+        for r in rows:
+            if r["kernel"] == k["kernel"]:
+                k["traffic"] = int(float(r["hbm_bytes"]))
+    traffic = dom.get("traffic") if dom else None
+    # the whole merge's counter traffic from the same PMC pass (sum over its kernels, per merge)
+    # (per-dispatch averages x dispatches / merges when the summary counts dispatches: kernels
+    # launched several times per merge — scans — count every launch)
+    pipe_traffic = None
+    if rows:
+        merges = max([int(r.get("dispatches") or 1) for r in rows if r["kernel"] == "yc::k_resolve"] or [1])
         pipe_traffic = int(sum(float(r["hbm_bytes"]) * int(r.get("dispatches") or merges) for r in rows) / merges)
-    achieved = alg / (k_ms * 1e-3) / 1e9 if k_ms > 0 else 0.0
     dominant = max(phases, key=lambda p: p[1]) if phases else ("merge", st.device_ms)
     roofline = {
         "bound": "hbm",
         "kernel": ROOF_KERNEL,
-        "achieved": round(achieved, 2),
+        "achieved": dom["achieved_GBs"] if dom else 0.0,
         "peak": HBM_PEAK_GBS,
         "unit": "GB/s",
-        "frac": round(achieved / HBM_PEAK_GBS, 5),
+        "frac": dom["frac"] if dom else 0.0,
         "traffic": traffic,
         "traffic_unit": "HBM bytes per launch",
         "traffic_source": traffic_src,
-        "alg_bytes_per_launch": alg,
-        "alg_bytes_per_unit": f"{ROOF_B} B per segment",
-        "avg_launch_ms": round(k_ms, 4),
+        "alg_bytes_per_launch": dom["alg_bytes_per_launch"] if dom else 0,
+        "alg_bytes_per_unit": dom["alg_bytes_per_unit"] if dom else None,
+        "avg_launch_ms": dom["avg_launch_ms"] if dom else 0.0,
         "largest_phase": {"name": dominant[0], "ms": round(dominant[1], 4)},
+        "kernels": kernels,
     }
     # algorithmic bytes of the whole merge: B_in + B_out + 64·S
     b_alg = in_bytes + out_bytes + 64 * st.structs

@@ -430,7 +430,13 @@ void launch_encode_sizes(const Work& w, uint32_t nsegs, uint32_t nclients, hipSt
   hipLaunchKernelGGL(k_run_sizes, dim3(grid), dim3(256), 0, side, w, nsegs);
   scan_u32(tmp2, tmp2_bytes, w.r_size, w.r_pos, nsegs + 1, side);
   hipEventRecord(ev_join, side);
-  hipLaunchKernelGGL(k_out_sizes, dim3(grid), dim3(256), 0, s, w, nsegs, nclients);
+}
+// the output struct sizes (its own phase: the bench times it live when it is the longest kernel)
+void launch_out_sizes(const Work& w, uint32_t nsegs, uint32_t nclients, hipStream_t s) {
+  hipLaunchKernelGGL(k_out_sizes, dim3(nsegs / 256 + 1), dim3(256), 0, s, w, nsegs, nclients);
+}
+void launch_encode_layout(const Work& w, uint32_t nsegs, uint32_t nclients, hipStream_t s, hipEvent_t ev_join) {
+  const uint32_t grid = nsegs / 256 + 1;
   scan_u32(w.tmp, w.tmp_bytes, w.o_size, w.o_pos, nsegs + 1, s);
   hipStreamWaitEvent(s, ev_join, 0);
   hipLaunchKernelGGL(k_client_bounds, dim3(grid), dim3(256), 0, s, w, nclients, nsegs);
@@ -442,10 +448,10 @@ void launch_encode_sizes(const Work& w, uint32_t nsegs, uint32_t nclients, hipSt
 // Phase 2: write bytes (buffers sized from a bound, checked in k_totals)
 void launch_encode_write(const Work& w, uint32_t nsegs, uint32_t nclients, hipStream_t s) {
   hipLaunchKernelGGL(k_write_clients, dim3(nclients / 256 + 1), dim3(256), 0, s, w, nclients);
-  if (nsegs) {
-    hipLaunchKernelGGL(k_write_structs, dim3((nsegs + 255) / 256), dim3(256), 0, s, w, nsegs, nclients);
-    hipLaunchKernelGGL(k_write_runs, dim3((nsegs + 255) / 256), dim3(256), 0, s, w, nsegs);
-  }
+  if (nsegs) hipLaunchKernelGGL(k_write_runs, dim3((nsegs + 255) / 256), dim3(256), 0, s, w, nsegs);
+}
+void launch_write_structs(const Work& w, uint32_t nsegs, uint32_t nclients, hipStream_t s) {
+  if (nsegs) hipLaunchKernelGGL(k_write_structs, dim3((nsegs + 255) / 256), dim3(256), 0, s, w, nsegs, nclients);
 }
 
 // Per-document byte ranges of a multi-document encode. Clients are laid out in (document, client)

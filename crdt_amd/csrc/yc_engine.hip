@@ -863,6 +863,7 @@ int run_decode(ycrdt_engine* e, ycrdt_batch* b, bool lazy, Decoded& D, bool gene
   launch_chunks(wd, e->side);
   HIPCHK(hipEventRecord(e->side_done, e->side));
   launch_direct(wd, s);
+  mark(e, "decode.chunk_wait");  // decode.direct: k_direct alone (the chunk path runs beside it)
   HIPCHK(hipStreamWaitEvent(s, e->side_done, 0));
   if (split) {
     mark(e, "decode.exchange");
@@ -931,6 +932,7 @@ int run_decode(ycrdt_engine* e, ycrdt_batch* b, bool lazy, Decoded& D, bool gene
   w.cl_base = take<uint64_t>(V, B_CLBASE, w.cap_clients + 2, ok);
   w.cl_start = take<uint32_t>(V, B_CLSTART, w.cap_clients + 1, ok);
   if (!ok) return fail(YCRDT_E_DEVICE, oom("struct table"));
+  launch_section_clients(w, nsections, s);  // section ranks first: the scatter writes every struct's section
   launch_struct_scatter(w, s);
   mark(e, "decode.sections");
   {  // the delete sets decode on the side stream (own scratch / scan space) while the client
@@ -944,7 +946,6 @@ int run_decode(ycrdt_engine* e, ycrdt_batch* b, bool lazy, Decoded& D, bool gene
     launch_ds_decode(wd, e->side);
     HIPCHK(hipEventRecord(e->side_done, e->side));
   }
-  launch_section_clients(w, nsections, s);
   if (nsections) {
     launch_client_table(w, nsections, s);
     fill_u32_multi({{(uint32_t*)ch_key, 2ull * ch_slots, 0xFFFFFFFFu}}, s);
@@ -953,8 +954,10 @@ int run_decode(ycrdt_engine* e, ycrdt_batch* b, bool lazy, Decoded& D, bool gene
     w.ch_val = ch_val;
     w.ch_mask = ch_slots - 1;
   }
-  mark(e, "decode.structs");
+  mark(e, "decode.structs");  // k_struct_decode alone
   launch_struct_decode(w, nstructs, s);
+  mark(e, "decode.clocks");
+  launch_struct_lenscan(w, nstructs, s);
   if (!lazy) {
     fill_u32_multi({{w.cl_start, (uint64_t)nsections + 1, 0u}, {w.cl_state, (uint64_t)nsections + 1, 0u}}, s);
     launch_states(w, nstructs, nsections, s);
@@ -1097,7 +1100,9 @@ int run_merge(ycrdt_engine* e, ycrdt_batch* b, const std::unordered_map<uint32_t
   }
   if (!ok) return fail(YCRDT_E_DEVICE, oom("unit workspace"));
   // ---- K2..K5 units
-  mark(e, "merge.units");
+  mark(e, "merge.units_fill");
+  if (U || nds) launch_units_fill(w, U, s);
+  mark(e, "merge.units");  // k_units alone
   // with no units, delete-set ranges still have to be checked: each one is pending (pendingDs)
   if (U || nds) launch_units(w, nstructs, nclients, nds, U, s);
   mark(e, "merge.segments");
@@ -1147,7 +1152,9 @@ int run_merge(ycrdt_engine* e, ycrdt_batch* b, const std::unordered_map<uint32_t
   e->nsegs = nsegs;
   e->nlists = 0;
   if (nsegs) {
-    mark(e, "merge.segment_props");
+    mark(e, "merge.segment_fill");
+    launch_segment_props_fill(w, nsegs, s);
+    mark(e, "merge.segment_props");  // k_seg_props alone
     launch_segment_props(w, nsegs, nclients, U, s);
     mark(e, "merge.resolve");  // k_resolve alone
     run_key_resolution(w, nsegs, s);
@@ -1231,8 +1238,12 @@ int run_merge(ycrdt_engine* e, ycrdt_batch* b, const std::unordered_map<uint32_t
   if (!ok) return fail(YCRDT_E_DEVICE, oom("output"));
   uint8_t* tmp2 = take<uint8_t>(V, B_TMP2, prim_tmp_bytes((uint64_t)nsegs + 2, 0), ok);
   if (!ok) return fail(YCRDT_E_DEVICE, oom("scan space"));
-  mark(e, "encode.sizes");
+  mark(e, "encode.runs");
   launch_encode_sizes(w, nsegs, nclients, s, e->side, e->side_fork, e->side_done, tmp2, V[B_TMP2].cap);
+  mark(e, "encode.sizes");  // k_out_sizes alone
+  launch_out_sizes(w, nsegs, nclients, s);
+  mark(e, "encode.layout");
+  launch_encode_layout(w, nsegs, nclients, s, e->side_done);
   if (exact_out) {
     rc = check(e, c, "encode sizes");
     if (rc) return rc;
@@ -1240,7 +1251,9 @@ int run_merge(ycrdt_engine* e, ycrdt_batch* b, const std::unordered_map<uint32_t
     w.out = take<uint8_t>(V, B_OUT, (size_t)w.cap_out + 16, ok);
     if (!ok) return fail(YCRDT_E_DEVICE, oom("output"));
   }
-  mark(e, "encode.write");
+  mark(e, "encode.write");  // k_write_structs alone
+  launch_write_structs(w, nsegs, nclients, s);
+  mark(e, "encode.write_tail");
   launch_encode_write(w, nsegs, nclients, s);
   mark(e, "end");
   HIPCHK(hipEventRecord(e->ev1, s));

@@ -226,8 +226,10 @@ __global__ __launch_bounds__(256) void k_units(Work w, uint32_t nstructs, uint32
     unit_ds_apply(w, nclients, blockIdx.x - nb);
   }
 }
-void launch_units(const Work& w, uint32_t nstructs, uint32_t nclients, uint32_t nds, uint64_t nunits, hipStream_t s) {
+void launch_units_fill(const Work& w, uint64_t nunits, hipStream_t s) {
   fill_u32_multi({{w.u_owner, nunits, NONE}, {w.u_flags, nunits, 0u}, {w.u_minchild, nunits, NONE}}, s);
+}
+void launch_units(const Work& w, uint32_t nstructs, uint32_t nclients, uint32_t nds, uint64_t nunits, hipStream_t s) {
   const uint32_t nb = (nstructs + 255) / 256, nd = nds && w.nupd ? (w.nupd + 3) / 4 : 0u;
   if (nb + nd) hipLaunchKernelGGL(k_units, dim3(nb + nd), dim3(256), 0, s, w, nstructs, nclients, nb);
 }
@@ -389,12 +391,14 @@ __global__ __launch_bounds__(256) void k_seg_props(Work w, uint32_t nsegs) {
   w.g_hop[s] = make_uint4(sf, kw, link, !gc && origin != NONE ? link : NONE);
 }
 
-void launch_segment_props(const Work& w, uint32_t nsegs, uint32_t nclients, uint64_t nunits, hipStream_t s) {
+void launch_segment_props_fill(const Work& w, uint32_t nsegs, hipStream_t s) {
   fill_u32_multi({{(uint32_t*)w.k_hash, (uint64_t)w.cap_keys * 2, 0u},
                   {w.k_rootmax, (uint64_t)w.cap_keys, 0u},
                   {w.k_flags, w.cap_keys, 0u},
                   {w.k_parent, w.cap_keys, NONE},
                   {w.g_maxchild, (uint64_t)nsegs, 0u}}, s);
+}
+void launch_segment_props(const Work& w, uint32_t nsegs, uint32_t nclients, uint64_t nunits, hipStream_t s) {
   if (nsegs) hipLaunchKernelGGL(k_seg_props, dim3((nsegs + 255) / 256), dim3(256), 0, s, w, nsegs);
 }
 
@@ -463,10 +467,9 @@ uint32_t run_key_resolution(const Work& w, uint32_t nsegs, hipStream_t s) {
 
 // --------------------------------------------------------------------------- map winner
 // Per YMap entry: the max-client child of its origin (the winner descent: YATA orders siblings by
-// client, Item.integrate Y@77594) — computed by k_seg_props + k_resolve above — and whether its
+// client, Item.integrate Y@77594) is computed by k_seg_props + k_resolve above, and whether its
 // origin unit has a child of a lower client than the unit's own (then the origin's own-client
-// successor is not adjacent to it: no merge; marked in k_seg_props).
-void launch_map_winner(const Work& w, uint32_t nsegs, hipStream_t s) {}
+// successor is not adjacent to it: no merge) is marked in k_seg_props.
 // the key's value is the rightmost entry: descend from the max-client root through the max-client
 // child until a leaf (YATA order of an origin-only tree, SURVEY.md §7 hard part 2)
 // (a descent visits every segment at most once: more hops than segments is a cycle, an error)

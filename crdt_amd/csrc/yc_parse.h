@@ -112,8 +112,8 @@ YC_HDI void skip_str(const Src& b, uint32_t& p, uint32_t end, bool& ok) {
 // ---- lib0 writeAny canonical forms (L0@1937: readAny -> JS value -> writeAny). Yjs stores
 // `any` content as JS values and writes them back, so an input encoding that is not what writeAny
 // produces comes out different: an overlong varuint / varint, an integer-valued float (-> varint
-// when <= 0x7FFFFFFF), a float64 that float32 holds exactly (-> float32), a NaN (-> float64
-// 0x7FF8000000000000), a positive varint past 0x7FFFFFFF (-> float32 / float64). Such values are
+// when <= 0x7FFFFFFF), a float64 that float32 holds exactly (-> float32), a float32 NaN (-> the
+// float64 it widens to), a positive varint past 0x7FFFFFFF (-> float32 / float64). Such values are
 // flagged ANY_REENCODE and the encoders write them canonically (any_canon below). What needs JS
 // object semantics — array-index keys after others or out of order (Object.keys order), the key
 // "__proto__", a negative integer past 2^32 (writeVarInt's 32-bit shifts) — is ANY_UNSUP: refused.
@@ -134,6 +134,25 @@ YC_HDI uint32_t vi_flag(const uint8_t* __restrict__ b, uint32_t p0, uint32_t p1)
   const uint32_t m = vi_decode(b, p0, p1, neg);
   if (!neg && m > 0x7FFFFFFFu) return ANY_REENCODE;  // writeAny: a float
   return vi_size(m) == p1 - p0 ? 0u : ANY_REENCODE;  // (a wrapped overlong form is longer too)
+}
+// the same checks through parse_struct's byte source (the device decoder's LDS window)
+template <class S>
+YC_HDI uint32_t vu_overlong_at(const S& b, uint32_t p0, uint32_t p1) {
+  return (p1 - p0 > 1 && b.u8(p1 - 1) == 0u) ? ANY_REENCODE : 0u;
+}
+template <class S>
+YC_HDI uint32_t vi_flag_at(const S& b, uint32_t p0, uint32_t p1) {
+  const uint32_t r = b.u8(p0);
+  uint32_t m = r & 0x3Fu, e = 6;
+  for (uint32_t q = p0 + 1; q < p1; ++q) { m |= (b.u8(q) & 0x7Fu) << (e & 31u); e += 7; }
+  if (!(r & 0x40u) && m > 0x7FFFFFFFu) return ANY_REENCODE;
+  return vi_size(m) == p1 - p0 ? 0u : ANY_REENCODE;
+}
+template <class S>
+YC_HDI uint64_t be_at(const S& b, uint32_t p, uint32_t n) {
+  uint64_t x = 0;
+  for (uint32_t i = 0; i < n; ++i) x = (x << 8) | b.u8(p + i);
+  return x;
 }
 YC_HDI uint32_t be32(const uint8_t* __restrict__ b, uint32_t p) {
   return ((uint32_t)b[p] << 24) | ((uint32_t)b[p + 1] << 16) | ((uint32_t)b[p + 2] << 8) | b[p + 3];
@@ -160,8 +179,7 @@ YC_HDI uint32_t f64_flag(uint64_t bits) {
   const double x = f64_of(bits);
   const uint32_t k = num_form(x);
   if (k == 3) return ANY_UNSUP;
-  if (k != 2) return ANY_REENCODE;
-  return (x != x && bits != 0x7FF8000000000000ull) ? ANY_REENCODE : 0u;
+  return k != 2 ? ANY_REENCODE : 0u;  // (a NaN keeps its bits: V8 writes the double it read)
 }
 // an object key that JS orders first (an array index: "0" or [1-9][0-9]* below 2^32 - 1), or "__proto__"
 YC_HDI int64_t key_index(const uint8_t* __restrict__ b, uint32_t p, uint32_t n) {
@@ -427,7 +445,7 @@ YC_HD inline int parse_struct(const Src& b, uint32_t& p, uint32_t end, uint32_t 
     case REF_ANY: {
       const uint32_t q0 = p;
       uint32_t n = b.vu(p, end, ok);
-      uint32_t cf = FULL && ok ? vu_overlong(b.b, q0, p) : 0u;
+      uint32_t cf = FULL && ok ? vu_overlong_at(b, q0, p) : 0u;
       len = n;
       for (uint32_t i = 0; i < n && ok; ++i) {
         const uint32_t tag = p < end ? b.u8(p) : 0u;
@@ -436,16 +454,16 @@ YC_HD inline int parse_struct(const Src& b, uint32_t& p, uint32_t end, uint32_t 
           ++p;
           const uint32_t s0 = p;
           switch (tag) {
-            case 125: b.svi(p, end, ok); if (FULL && ok) cf |= vi_flag(b.b, s0, p); break;
-            case 124: skip_bytes(p, 4, end, ok); if (FULL && ok) cf |= f32_flag(be32(b.b, s0)); break;
-            case 123: skip_bytes(p, 8, end, ok); if (FULL && ok) cf |= f64_flag(be64(b.b, s0)); break;
+            case 125: b.svi(p, end, ok); if (FULL && ok) cf |= vi_flag_at(b, s0, p); break;
+            case 124: skip_bytes(p, 4, end, ok); if (FULL && ok) cf |= f32_flag((uint32_t)be_at(b, s0, 4)); break;
+            case 123: skip_bytes(p, 8, end, ok); if (FULL && ok) cf |= f64_flag(be_at(b, s0, 8)); break;
             case 122: skip_bytes(p, 8, end, ok); break;
             case 119: {
               skip_str<FULL>(b, p, end, ok);
-              if (FULL && ok) { uint32_t q = s0; bool o2 = true; rd_vu(b.b, q, end, o2); cf |= vu_overlong(b.b, s0, q); }
+              if (FULL && ok) { uint32_t q = s0; bool o2 = true; b.vu(q, end, o2); cf |= vu_overlong_at(b, s0, q); }
               break;
             }
-            case 116: { const uint32_t k = b.vu(p, end, ok); if (FULL && ok) cf |= vu_overlong(b.b, s0, p); if (ok) skip_bytes(p, k, end, ok); break; }
+            case 116: { const uint32_t k = b.vu(p, end, ok); if (FULL && ok) cf |= vu_overlong_at(b, s0, p); if (ok) skip_bytes(p, k, end, ok); break; }
             default: break;  // 127 undefined, 126 null, 121 false, 120 true
           }
         } else {

@@ -456,8 +456,7 @@ __device__ __attribute__((noinline)) uint32_t any_canon(const uint8_t* __restric
     const uint32_t k = num_form(x);
     if (k == 0) { put(125); put_vi(x < 0 || (x == 0 && signbit(x)), (uint32_t)fabs(x)); return; }
     if (k == 1) { union { float f; uint32_t u; } c; c.f = (float)x; put(124); for (int s = 24; s >= 0; s -= 8) put((c.u >> s) & 0xFFu); return; }
-    union { double d; uint64_t u; } c; c.d = x;
-    if (x != x) c.u = 0x7FF8000000000000ull;
+    union { double d; uint64_t u; } c; c.d = x;  // (a NaN: the bits it has, as V8 writes them)
     put(123);
     for (int s = 56; s >= 0; s -= 8) put((uint32_t)(c.u >> s) & 0xFFu);
   };
@@ -585,14 +584,16 @@ void launch_ds_decode(const Work& w, hipStream_t s);
 void launch_section_clients(const Work& w, uint32_t nsections, hipStream_t s);
 void launch_client_table(Work& w, uint32_t nsections, hipStream_t s);
 void launch_struct_decode(const Work& w, uint32_t nstructs, hipStream_t s);
+void launch_struct_lenscan(const Work& w, uint32_t nstructs, hipStream_t s);
 void launch_states(const Work& w, uint32_t nstructs, uint32_t nsections, hipStream_t s);  // clocks + client states
 void launch_struct_clocks(const Work& w, uint32_t nstructs, hipStream_t s);               // clocks only (lazy)
 
+void launch_units_fill(const Work& w, uint64_t nunits, hipStream_t s);
 void launch_units(const Work& w, uint32_t nstructs, uint32_t nclients, uint32_t nds, uint64_t nunits, hipStream_t s);
 void launch_segments(const Work& w, uint32_t nclients, uint64_t nunits, hipStream_t s);
+void launch_segment_props_fill(const Work& w, uint32_t nsegs, hipStream_t s);
 void launch_segment_props(const Work& w, uint32_t nsegs, uint32_t nclients, uint64_t nunits, hipStream_t s);
 uint32_t run_key_resolution(const Work& w, uint32_t nsegs, hipStream_t s);
-void launch_map_winner(const Work& w, uint32_t nsegs, hipStream_t s);
 uint32_t run_descent(const Work& w, uint32_t nsegs, hipStream_t s, bool fold_overwrite);
 void launch_merge_flags(const Work& w, uint32_t nsegs, hipStream_t s, bool fold_overwrite);
 void launch_merge_flags_only(const Work& w, uint32_t nsegs, hipStream_t s, bool fold_overwrite);
@@ -608,7 +609,10 @@ uint32_t launch_yata(const Work& w, uint32_t nsegs, uint32_t narray, uint32_t nc
 // side / ev_fork / ev_join / tmp2: the delete-set run chain runs on `side` with its own scan space
 void launch_encode_sizes(const Work& w, uint32_t nsegs, uint32_t nclients, hipStream_t s, hipStream_t side,
                          hipEvent_t ev_fork, hipEvent_t ev_join, void* tmp2, size_t tmp2_bytes);
+void launch_out_sizes(const Work& w, uint32_t nsegs, uint32_t nclients, hipStream_t s);
+void launch_encode_layout(const Work& w, uint32_t nsegs, uint32_t nclients, hipStream_t s, hipEvent_t ev_join);
 void launch_encode_write(const Work& w, uint32_t nsegs, uint32_t nclients, hipStream_t s);
+void launch_write_structs(const Work& w, uint32_t nsegs, uint32_t nclients, hipStream_t s);
 
 // rocPRIM wrappers (yc_prims.hip)
 size_t prim_tmp_bytes(uint64_t scan_n, uint64_t sort_n);  // scratch for scans of scan_n / sorts of sort_n items

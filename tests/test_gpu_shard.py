@@ -129,8 +129,9 @@ def test_c4_generated_vs_oracle_and_shards():
 
 
 def test_c4_full_size_shards_properties():
-    """Full-size C4 (≈47 M items, 2 000 replicas, 100 k nested arrays): 4 key-hash shards give the
-    unsharded bytes; the merge is order-independent and idempotent."""
+    """The generator's C4 (≈47 M items, 2 000 replicas, 100 k nested arrays): 4 key-hash shards give
+    the unsharded bytes; the merge is order-independent and idempotent. (BASELINE's C4 scale,
+    C4_FULL at 102 M items, runs in bench.py's c4 / c4_sharded legs through the same properties.)"""
     from crdt_amd.workload import C4, gen_nested
 
     ups, st = gen_nested(**C4)
