@@ -891,8 +891,9 @@ def run_rank(args, report=None):
          "hop record, cidx / src / origin / right origin, winner slot written)"),
         ("merge.resolve", "yc::k_resolve", 28 * G,
          "28 B per segment (hop record read, flags / key written, winner slot read-modify-write)"),
-        ("encode.sizes", "yc::k_out_sizes", 46 * OS,
-         "46 B per output struct (segment bounds, flags, source + 6 struct columns read; size + client written)"),
+        ("encode.sizes", "yc::k_out_sizes", 8 * G + 46 * OS,
+         "8 B per segment (output number, flags) + 46 B per output struct (segment bounds, source + 6 struct "
+         "columns read; first segment, client, size written)"),
         ("encode.write", "yc::k_write_structs", 46 * OS + 2 * st.out_bytes,
          "46 B of columns per output struct + every output byte copied (read from the input, written)"),
     ]

@@ -1544,15 +1544,10 @@ __global__ void k_popc(const uint64_t* __restrict__ bits, uint32_t* __restrict__
 // contiguous run: coalesced stores instead of every lane storing its ~5 positions at its own
 // offset, one divergent store per bit of the word with the most.
 constexpr uint32_t SCAT_LDS = 4096;
-// With sbits (the section-start bitmap) each struct also gets its section: the last section start
-// at or before it (rank in sbits), mapped through sec_sorted (k_section_rank) — written here, where
-// the words are in registers, instead of a dependent lookup chain at the head of k_struct_decode.
 __global__ __launch_bounds__(256) void k_scatter_pos(const uint64_t* __restrict__ bits, const uint32_t* __restrict__ pre, uint32_t nwords,
                                                      uint32_t* __restrict__ out, uint32_t cap, uint32_t* err, uint8_t* __restrict__ swin,
-                                                     uint32_t shift, const uint64_t* __restrict__ sbits, const uint32_t* __restrict__ spre,
-                                                     const uint32_t* __restrict__ sec_sorted, uint32_t* __restrict__ s_sec) {
+                                                     uint32_t shift) {
   __shared__ uint32_t buf[SCAT_LDS];
-  __shared__ uint32_t sbuf[SCAT_LDS];
   // a fixed grid walks the 256-word tiles (the per-tile work is small: tens of thousands of
   // short workgroups were dispatch-bound, 1.2 ms for C2 x 112)
   const uint32_t ntiles = (nwords + 255) / 256;
@@ -1574,28 +1569,13 @@ __global__ __launch_bounds__(256) void k_scatter_pos(const uint64_t* __restrict_
       for (uint32_t t = threadIdx.x; t < total; t += 256) swin[base + t] = wn;
     }
     const uint32_t rel = (uint32_t)(((uint64_t)i * 64) & wmask);
-    const uint64_t sx = sbits && i < nwords ? sbits[i] : 0ull;
-    const uint32_t sp = sbits && i < nwords ? spre[i] : 0u;
-    auto sec_of = [&](uint32_t j) { return sec_sorted[sp + (uint32_t)__popcll(sx & ((2ull << j) - 1)) - 1]; };
     if (total > SCAT_LDS) {  // a dense stretch: every lane stores its own positions
-      for (; x; x &= x - 1) {
-        const uint32_t j = (uint32_t)__ffsll((long long)x) - 1;
-        if (sbits) s_sec[k] = sec_of(j);
-        out[k++] = rel + j;
-      }
+      for (; x; x &= x - 1) out[k++] = rel + (uint32_t)__ffsll((long long)x) - 1;
       continue;
     }
-    for (k -= base; x; x &= x - 1) {
-      const uint32_t j = (uint32_t)__ffsll((long long)x) - 1;
-      buf[k] = rel + j;
-      if (sbits) sbuf[k] = sec_of(j);
-      ++k;
-    }
+    for (k -= base; x; x &= x - 1) buf[k++] = rel + (uint32_t)__ffsll((long long)x) - 1;
     __syncthreads();
-    for (uint32_t t = threadIdx.x; t < total; t += 256) {
-      out[base + t] = buf[t];
-      if (sbits) s_sec[base + t] = sbuf[t];
-    }
+    for (uint32_t t = threadIdx.x; t < total; t += 256) out[base + t] = buf[t];
     __syncthreads();  // buf is reused by the next tile
   }
 }
@@ -1625,9 +1605,8 @@ void launch_struct_count(const Work& w, hipStream_t s) {
 // after it (the struct table is sized from the count): dense struct positions
 void launch_struct_scatter(const Work& w, hipStream_t s) {
   const uint32_t nwords = (w.nbytes + 63) / 64;
-  // (k_section_rank ran first: sec_sorted maps section-start ranks to sections)
   hipLaunchKernelGGL(k_scatter_pos, dim3(std::min<uint32_t>(nwords / 256 + 1, 4096)), dim3(256), 0, s, w.final_bits, w.wcnt, nwords, w.s_pos,
-                     w.cap_structs, &w.ctr->err, w.nwin > 1 ? w.s_win : nullptr, w.win_shift, w.sec_bits, w.wsec, w.sec_sorted, w.s_sec);
+                     w.cap_structs, &w.ctr->err, w.nwin > 1 ? w.s_win : nullptr, w.win_shift);
 }
 
 // called once the section count is known on the host
@@ -1894,7 +1873,13 @@ __global__ __launch_bounds__(256) void k_struct_decode(Work w, uint32_t nstructs
   if (i >= nstructs) return;
   const uint32_t nclients = w.ctr->nclients;
   uint32_t* err = &w.ctr->err;
-  const uint32_t p0 = w.s_pos[i], si = w.s_sec[i];  // (s_sec: k_scatter_pos)
+  const uint32_t p0 = w.s_pos[i];
+  // the struct's section: the section starts at or before it (rank in the section-start bitmap);
+  // written here for the later passes (computing it in k_scatter_pos doubled that kernel's LDS
+  // and time: 0.32 -> 1.36 ms on the C2 batch)
+  const uint32_t si = w.sec_sorted[rank_incl(win_words(w.sec_bits, w.nwin > 1 ? w.s_win[i] : 0u),
+                                             win_words(w.wsec, w.nwin > 1 ? w.s_win[i] : 0u), p0) - 1];
+  w.s_sec[i] = si;
   // the struct's bytes (they depend on its position only) are fetched beside its section record
   __shared__ __attribute__((aligned(16))) uint32_t win[256 * SD_STRIDE];
   uint32_t* slot = win + threadIdx.x * SD_STRIDE;
@@ -1962,9 +1947,9 @@ __global__ __launch_bounds__(256) void k_struct_decode(Work w, uint32_t nstructs
     if (v.info & 0x40u) h += vu_size(v.rc) + vu_size(v.rk);
     if ((v.info & 0xC0u) == 0) {
       h += 1;  // parent info (1: root type name, 0: parent item id)
-      if (v.pkind == 1) { uint32_t q = v.pa; bool okq = true; const uint32_t n = WinSrc{bw, slot, s0}.vu(q, uend, okq); h += vu_size(n) + n; }
+      if (v.pkind == 1) h += vu_size(v.pn) + v.pn;
       else h += vu_size(v.pa) + vu_size(v.pb);
-      if (v.has_psub) { uint32_t q = v.psub_pos; bool okq = true; const uint32_t n = WinSrc{bw, slot, s0}.vu(q, uend, okq); h += vu_size(n) + n; }
+      if (v.has_psub) h += vu_size(v.psn) + v.psn;
     }
     canon_hdr = h == v.cpos - p0 - 1;
   }

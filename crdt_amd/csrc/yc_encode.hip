@@ -39,7 +39,7 @@ __device__ __forceinline__ uint64_t copy_bytes(uint8_t* __restrict__ o, uint64_t
 // Encodes output struct `o` (segments [a,b)) at position p when WRITE, returns the size
 // (Item.write Y@80416 / GC.write Y@68955 with the writeStructs offset, Y@18809).
 template <bool WRITE>
-__device__ uint32_t encode_struct_general(const Work& w, uint32_t nclients, uint32_t o, uint8_t* __restrict__ out, uint64_t p0);
+__device__ uint32_t encode_struct_general(const Work& w, uint32_t nclients, uint32_t a, uint32_t b, uint8_t* __restrict__ out, uint64_t p0);
 
 // The common output struct is one WHOLE source item (one segment from the struct's first unit to
 // its last, full-state encode): Item.write then emits the input's own bytes — its origin, right
@@ -48,9 +48,9 @@ __device__ uint32_t encode_struct_general(const Work& w, uint32_t nclients, uint
 // input drops on items with an origin) and, for a deleted item, the content (ContentDeleted: its
 // length). So it is a copy of [pos + 1, cpos) and [cpos, cend) — five columns instead of the
 // general path's twenty (and its reference-client lookups).
+// (output struct = segments [a, b))
 template <bool WRITE>
-__device__ __forceinline__ uint32_t encode_struct(const Work& w, uint32_t nclients, uint32_t o, uint8_t* __restrict__ out, uint64_t p0) {
-  const uint32_t a = w.o_first[o], b = w.o_first[o + 1];
+__device__ __forceinline__ uint32_t encode_struct(const Work& w, uint32_t nclients, uint32_t a, uint32_t b, uint8_t* __restrict__ out, uint64_t p0) {
   if (b == a + 1 && !w.delta) {
     const uint32_t f = w.g_flags[a], src = w.g_src[a], ga = w.g_start[a], gb = w.g_start[b];
     const uint32_t slen = w.s_len[src], spos = w.s_pos[src], scpos = w.s_cpos[src], scend = w.s_cend[src];
@@ -68,16 +68,15 @@ __device__ __forceinline__ uint32_t encode_struct(const Work& w, uint32_t nclien
       return (uint32_t)(p - p0);
     }
   }
-  return encode_struct_general<WRITE>(w, nclients, o, out, p0);
+  return encode_struct_general<WRITE>(w, nclients, a, b, out, p0);
 }
 
 template <bool WRITE>
-__device__ __forceinline__ uint32_t encode_struct_general(const Work& w, uint32_t nclients, uint32_t o, uint8_t* __restrict__ out,
+__device__ __forceinline__ uint32_t encode_struct_general(const Work& w, uint32_t nclients, uint32_t a, uint32_t b, uint8_t* __restrict__ out,
                                                                     uint64_t p0) {
   // The columns a struct can need are loaded in three dependent rounds — its first segment's row,
   // then its source struct's and its client's, then the reference clients' — each round issued
   // whole before anything branches on it, instead of one memory round trip per field.
-  const uint32_t a = w.o_first[o], b = w.o_first[o + 1];
   const uint32_t cidx = w.g_cidx[a], ga = w.g_start[a], gb = w.g_start[b], f = w.g_flags[a], src = w.g_src[a];
   const uint32_t go = w.g_origin[a], gr = w.g_rorigin[a];
   const uint64_t base = w.cl_base[cidx], base1 = w.cl_base[cidx + 1];
@@ -209,25 +208,33 @@ __device__ __forceinline__ uint32_t encode_struct_general(const Work& w, uint32_
   return size;
 }
 
-// NO (ctr->nout) and the run count (g_tmp2[NS]) stay on the device: grids and scans cover NS + 1
+// NO (ctr->nout) and the run count (g_tmp2[NS]) stay on the device: grids and scans cover NS + 1.
+// One lane per segment: a segment that starts output struct o = g_outid[s] (the exclusive scan of
+// the merge flags) records it (o_first, o_cidx) and sizes it, finding the struct's end by stepping
+// over the segments merged into it (usually none); the others zero the size slots past NO, so the
+// scan over NS + 1 entries sees exactly the NO sizes.
 __global__ __launch_bounds__(256) void k_out_sizes(Work w, uint32_t nsegs, uint32_t nclients) {
-  const uint32_t o = blockIdx.x * blockDim.x + threadIdx.x;
-  if (o > nsegs) return;
-  if (o >= w.ctr->nout) { w.o_size[o] = 0; return; }
-  w.o_cidx[o] = w.g_cidx[w.o_first[o]];
-  w.o_size[o] = encode_struct<false>(w, nclients, o, nullptr, 0);
-}
-
-// runs of consecutive deleted segments (createDeleteSetFromStructStore)
-__device__ __forceinline__ bool seg_deleted(uint32_t f) { return (f & SEG_DEL) || !(f & SEG_ITEM); }
-__global__ void k_run_flags(Work w, uint32_t nsegs) {
   const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
   if (s > nsegs) return;
-  if (s == nsegs) { w.g_tmp[s] = 0; return; }
-  const bool d = seg_deleted(w.g_flags[s]);
-  const bool start = d && (s == 0 || w.g_cidx[s - 1] != w.g_cidx[s] || !seg_deleted(w.g_flags[s - 1]));
-  w.g_tmp[s] = start ? 1u : 0u;
+  const uint32_t nout = nsegs ? w.g_outid[nsegs] : 0u;
+  if (s == nsegs) {
+    w.o_first[nout] = nsegs;  // sentinel
+    w.o_size[nsegs] = 0;
+    w.ctr->nout = nout;
+    return;
+  }
+  const uint32_t o = w.g_outid[s];
+  if (w.g_flags[s] & SEG_MERGE) { w.o_size[nout + (s - o)] = 0; return; }  // (s - o: its rank among the non-starts)
+  uint32_t b = s + 1;
+  while (b < nsegs && (w.g_flags[b] & SEG_MERGE)) ++b;
+  w.o_first[o] = s;
+  w.o_cidx[o] = w.g_cidx[s];
+  w.o_size[o] = encode_struct<false>(w, nclients, s, b, nullptr, 0);
 }
+
+// runs of consecutive deleted segments (createDeleteSetFromStructStore): their starts were flagged
+// in r_size by k_merge_flags / k_merge_final
+__device__ __forceinline__ bool seg_deleted(uint32_t f) { return (f & SEG_DEL) || !(f & SEG_ITEM); }
 __global__ void k_run_fill(Work w, uint32_t nsegs) {
   const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
   if (s >= nsegs) return;
@@ -362,7 +369,7 @@ __global__ __launch_bounds__(256) void k_write_structs(Work w, uint32_t nsegs, u
   const uint32_t fi = ccol(w, CC_FIRST_INCL)[c];
   // (o_pos wraps at 2^32: differences within one client's block are exact)
   const uint64_t p = w.ctr->pad[3] + ccol64(w, CC64_BLKPOS)[c] + ccol(w, CC_HDR)[c] + (uint32_t)(w.o_pos[o] - w.o_pos[fi]);
-  encode_struct<true>(w, nclients, o, w.out, p);
+  encode_struct<true>(w, nclients, w.o_first[o], w.o_first[o + 1], w.out, p);
 }
 __global__ void k_write_clients(Work w, uint32_t nclients) {
   const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
@@ -424,8 +431,8 @@ void launch_encode_sizes(const Work& w, uint32_t nsegs, uint32_t nclients, hipSt
   // delete-set runs (side stream) || output struct sizes (main stream)
   hipEventRecord(ev_fork, s);
   hipStreamWaitEvent(side, ev_fork, 0);
-  hipLaunchKernelGGL(k_run_flags, dim3(grid), dim3(256), 0, side, w, nsegs);
-  scan_u32(tmp2, tmp2_bytes, w.g_tmp, w.g_tmp2, nsegs + 1, side);
+  if (!nsegs) fill_u32_multi({{w.r_size, 1, 0u}}, side);  // (no merge-flag pass wrote the run starts)
+  scan_u32(tmp2, tmp2_bytes, w.r_size, w.g_tmp2, nsegs + 1, side);
   if (nsegs) hipLaunchKernelGGL(k_run_fill, dim3((nsegs + 255) / 256), dim3(256), 0, side, w, nsegs);
   hipLaunchKernelGGL(k_run_sizes, dim3(grid), dim3(256), 0, side, w, nsegs);
   scan_u32(tmp2, tmp2_bytes, w.r_size, w.r_pos, nsegs + 1, side);

@@ -932,8 +932,8 @@ int run_decode(ycrdt_engine* e, ycrdt_batch* b, bool lazy, Decoded& D, bool gene
   w.cl_base = take<uint64_t>(V, B_CLBASE, w.cap_clients + 2, ok);
   w.cl_start = take<uint32_t>(V, B_CLSTART, w.cap_clients + 1, ok);
   if (!ok) return fail(YCRDT_E_DEVICE, oom("struct table"));
-  launch_section_clients(w, nsections, s);  // section ranks first: the scatter writes every struct's section
   launch_struct_scatter(w, s);
+  launch_section_clients(w, nsections, s);
   mark(e, "decode.sections");
   {  // the delete sets decode on the side stream (own scratch / scan space) while the client
      // table and the struct table are built; both streams only read what the sync above published

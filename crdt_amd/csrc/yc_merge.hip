@@ -554,6 +554,7 @@ void run_dead_keys(const Work& w, uint32_t nsegs, hipStream_t s) {
 }
 
 // --------------------------------------------------------------------------- merge flags
+__device__ __forceinline__ bool seg_deleted(uint32_t f) { return (f & SEG_DEL) || !(f & SEG_ITEM); }  // in a delete set
 __device__ __forceinline__ bool content_mergeable(uint32_t ref) {  // ContentX.mergeWith
   return ref == REF_ANY || ref == REF_JSON || ref == REF_STRING || ref == REF_DELETED;
 }
@@ -565,7 +566,7 @@ __device__ __forceinline__ uint32_t overwritten(uint32_t f, uint32_t fold) {
 __global__ __launch_bounds__(256) void k_merge_flags(Work w, uint32_t nsegs, uint32_t fold) {
   const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
   if (s > nsegs) return;
-  if (s == nsegs) { w.g_tmp[s] = 0; return; }
+  if (s == nsegs) { w.g_tmp[s] = 0; w.r_size[s] = 0; return; }
   bool merge = false;
   const uint32_t f0 = w.g_flags[s], fr = overwritten(f0, fold);
   if (s > 0 && w.g_cidx[s - 1] == w.g_cidx[s]) {
@@ -587,18 +588,12 @@ __global__ __launch_bounds__(256) void k_merge_flags(Work w, uint32_t nsegs, uin
   const uint32_t f1 = merge ? fr | SEG_MERGE : fr;
   if (f1 != f0) w.g_flags[s] = f1;
   w.g_tmp[s] = merge ? 0u : 1u;
+  // the encode's delete-set runs (createDeleteSetFromStructStore): s starts a run of deleted
+  // segments of one client — flagged here, where both final flags are in registers
+  const bool del = seg_deleted(fr);
+  const bool pdel = s > 0 && w.g_cidx[s - 1] == w.g_cidx[s] && seg_deleted(overwritten(w.g_flags[s - 1], fold));
+  w.r_size[s] = del && !pdel ? 1u : 0u;
 }
-__global__ void k_out_first(Work w, uint32_t nsegs) {
-  const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
-  if (s >= nsegs) return;
-  if (!(w.g_flags[s] & SEG_MERGE)) w.o_first[w.g_outid[s]] = s;
-  if (s == nsegs - 1) {
-    const uint32_t nout = w.g_outid[nsegs];
-    w.o_first[nout] = nsegs;  // sentinel
-    w.ctr->nout = nout;
-  }
-}
-
 // ---- key-hash sharding of one document (C4). Every list — a YMap entry, a
 // YArray — and every mergeWith adjacency lives inside ONE top-level entry of a root type (nested
 // lists hang below their parent item's entry), so the integrate phases (map winner, dead types,
@@ -648,15 +643,18 @@ __global__ void k_shard_export(Work w, uint32_t nsegs, const uint8_t* __restrict
 __global__ void k_merge_final(Work w, uint32_t nsegs) {
   const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
   if (s > nsegs) return;
-  if (s == nsegs) { w.g_tmp[s] = 0; return; }
+  if (s == nsegs) { w.g_tmp[s] = 0; w.r_size[s] = 0; return; }
   uint32_t f = w.g_flags[s];
+  const bool same = s > 0 && w.g_cidx[s - 1] == w.g_cidx[s];
+  const uint32_t fp = same ? w.g_flags[s - 1] : 0u;
   if (!(f & SEG_ITEM)) {  // GC + GC merge (only the MERGE bit changes, so neighbours read ITEM safely)
-    const bool m = s > 0 && w.g_cidx[s - 1] == w.g_cidx[s] && !(w.g_flags[s - 1] & SEG_ITEM);
+    const bool m = same && !(fp & SEG_ITEM);
     const uint32_t g = m ? (f | SEG_MERGE) : (f & ~SEG_MERGE);
     if (g != f) w.g_flags[s] = g;
     f = g;
   }
   w.g_tmp[s] = (f & SEG_MERGE) ? 0u : 1u;
+  w.r_size[s] = seg_deleted(f) && !(same && seg_deleted(fp)) ? 1u : 0u;  // delete-set run starts (k_merge_flags)
 }
 void launch_key_shards(const Work& w, uint32_t nsegs, uint32_t nshards, uint32_t* key_shard, uint8_t* owner, hipStream_t s) {
   hipLaunchKernelGGL(k_key_shard, dim3(w.cap_keys / 256 + 1), dim3(256), 0, s, w, nshards, key_shard);
@@ -679,17 +677,16 @@ void launch_merge_final(const Work& w, uint32_t nsegs, hipStream_t s) {
 void launch_merge_flags_only(const Work& w, uint32_t nsegs, hipStream_t s, bool fold) {
   if (nsegs) hipLaunchKernelGGL(k_merge_flags, dim3(nsegs / 256 + 1), dim3(256), 0, s, w, nsegs, fold ? 1u : 0u);
 }
+// (the output structs are numbered by the scan; k_out_sizes records their first segments)
 void launch_merge_tail(const Work& w, uint32_t nsegs, hipStream_t s) {
   if (!nsegs) return;
   scan_u32(w.tmp, w.tmp_bytes, w.g_tmp, w.g_outid, nsegs + 1, s);
-  hipLaunchKernelGGL(k_out_first, dim3((nsegs + 255) / 256), dim3(256), 0, s, w, nsegs);
 }
 
 void launch_merge_flags(const Work& w, uint32_t nsegs, hipStream_t s, bool fold) {
   if (!nsegs) return;
   hipLaunchKernelGGL(k_merge_flags, dim3(nsegs / 256 + 1), dim3(256), 0, s, w, nsegs, fold ? 1u : 0u);
   scan_u32(w.tmp, w.tmp_bytes, w.g_tmp, w.g_outid, nsegs + 1, s);
-  hipLaunchKernelGGL(k_out_first, dim3((nsegs + 255) / 256), dim3(256), 0, s, w, nsegs);
 }
 
 }  // namespace yc

@@ -73,40 +73,54 @@ YC_HDI void skip_bytes(uint32_t& p, uint32_t n, uint32_t end, bool& ok) {
 // Every string field of an exactly parsed struct is checked (names, keys, contents, `any` strings
 // and object keys); the bytes are in range (the caller skipped them already).
 template <class Src>
-YC_HDI bool utf8_valid(const Src& b, uint32_t p, uint32_t n) {
+YC_HDI uint32_t utf8_units(const Src& b, uint32_t p, uint32_t n, bool& ok) {  // UTF-16 code units of valid UTF-8
   const uint32_t e = p + n;
+  uint32_t u = 0;
 #pragma unroll 1
   while (p < e) {
+    if (e - p >= 4 && !(b.w4(p) & 0x80808080u)) { p += 4; u += 4; continue; }  // four ASCII bytes
     const uint32_t c = b.u8(p);
-    if (c < 0x80u) { ++p; continue; }
+    if (c < 0x80u) { ++p; ++u; continue; }
     uint32_t need, v, lo;
     if ((c & 0xE0u) == 0xC0u) { need = 1; v = c & 0x1Fu; lo = 0x80u; }
     else if ((c & 0xF0u) == 0xE0u) { need = 2; v = c & 0x0Fu; lo = 0x800u; }
     else if ((c & 0xF8u) == 0xF0u) { need = 3; v = c & 0x07u; lo = 0x10000u; }
-    else return false;
-    if (e - p - 1 < need) return false;
+    else { ok = false; return u; }
+    if (e - p - 1 < need) { ok = false; return u; }
     for (uint32_t k = 1; k <= need; ++k) {
       const uint32_t d = b.u8(p + k);
-      if ((d & 0xC0u) != 0x80u) return false;
+      if ((d & 0xC0u) != 0x80u) { ok = false; return u; }
       v = (v << 6) | (d & 0x3Fu);
     }
-    if (v < lo || v > 0x10FFFFu || (v >= 0xD800u && v <= 0xDFFFu)) return false;
+    if (v < lo || v > 0x10FFFFu || (v >= 0xD800u && v <= 0xDFFFu)) { ok = false; return u; }
     p += need + 1;
+    u += need == 3 ? 2u : 1u;  // a 4-byte sequence is a surrogate pair
   }
-  return true;
+  return u;
+}
+template <class Src>
+YC_HDI bool utf8_valid(const Src& b, uint32_t p, uint32_t n) {
+  bool ok = true;
+  utf8_units(b, p, n, ok);
+  return ok;
+}
+YC_HDI uint32_t le32(const uint8_t* __restrict__ b, uint32_t p) {
+  return (uint32_t)b[p] | ((uint32_t)b[p + 1] << 8) | ((uint32_t)b[p + 2] << 16) | ((uint32_t)b[p + 3] << 24);
 }
 struct PtrSrc {  // utf8_valid over a plain pointer
   const uint8_t* __restrict__ b;
   YC_HDI uint32_t u8(uint32_t p) const { return b[p]; }
+  YC_HDI uint32_t w4(uint32_t p) const { return le32(b, p); }
 };
 // a varString at p: its length, then (UTF8) its text checked; p moves past it
 template <bool UTF8, class Src>
-YC_HDI void skip_str(const Src& b, uint32_t& p, uint32_t end, bool& ok) {
+YC_HDI uint32_t skip_str(const Src& b, uint32_t& p, uint32_t end, bool& ok) {  // returns the byte length
   const uint32_t n = b.vu(p, end, ok);
-  if (!ok) return;
+  if (!ok) return 0;
   const uint32_t st = p;
   skip_bytes(p, n, end, ok);
   if (UTF8 && ok && !utf8_valid(b, st, n)) ok = false;
+  return n;
 }
 
 // ---- lib0 writeAny canonical forms (L0@1937: readAny -> JS value -> writeAny). Yjs stores
@@ -304,8 +318,96 @@ YC_HD inline bool skip_any(const uint8_t* __restrict__ b, uint32_t& p, uint32_t 
   }
 }
 
+// An object key's flags through a byte source: ANY_UNSUP for "__proto__"; ki = its array index
+// (key_index), else -1
+template <class S>
+YC_HDI uint32_t key_flags_at(const S& b, uint32_t p, uint32_t n, int64_t& ki) {
+  ki = -1;
+  const uint32_t c0 = n ? b.u8(p) : 0u;
+  if (n == 9 && c0 == '_') {
+    const char* k = "__proto__";
+    uint32_t i = 0;
+    while (i < 9 && b.u8(p + i) == (uint8_t)k[i]) ++i;
+    return i == 9 ? ANY_UNSUP : 0u;
+  }
+  if (n == 0 || n > 10 || c0 < '0' || c0 > '9' || (n > 1 && c0 == '0')) return 0u;
+  uint64_t v = 0;
+  for (uint32_t i = 0; i < n; ++i) {
+    const uint32_t c = b.u8(p + i);
+    if (c < '0' || c > '9') return 0u;
+    v = v * 10 + (c - '0');
+  }
+  if (v < 0xFFFFFFFFull) ki = (int64_t)v;
+  return 0u;
+}
+// One scalar `any` value after its tag (at p), flags in cf (FULL): 127 undefined, 126 null,
+// 121 / 120 false / true, 125 varint, 124 float32, 123 float64, 122 bigint, 119 string, 116 bytes.
+template <bool FULL, class S>
+YC_HDI void any_scalar(const S& b, uint32_t tag, uint32_t& p, uint32_t end, bool& ok, uint32_t& cf) {
+  const uint32_t s0 = p;
+  switch (tag) {
+    case 125: b.svi(p, end, ok); if (FULL && ok) cf |= vi_flag_at(b, s0, p); break;
+    case 124: skip_bytes(p, 4, end, ok); if (FULL && ok) cf |= f32_flag((uint32_t)be_at(b, s0, 4)); break;
+    case 123: skip_bytes(p, 8, end, ok); if (FULL && ok) cf |= f64_flag(be_at(b, s0, 8)); break;
+    case 122: skip_bytes(p, 8, end, ok); break;
+    case 119: {
+      const uint32_t n = b.vu(p, end, ok);
+      if (FULL && ok) cf |= vu_overlong_at(b, s0, p);
+      const uint32_t st = p;
+      if (ok) skip_bytes(p, n, end, ok);
+      if (FULL && ok && !utf8_valid(b, st, n)) ok = false;
+      break;
+    }
+    case 116: { const uint32_t k = b.vu(p, end, ok); if (FULL && ok) cf |= vu_overlong_at(b, s0, p); if (ok) skip_bytes(p, k, end, ok); break; }
+    default: break;  // 127, 126, 121, 120
+  }
+}
+YC_HDI bool any_scalar_tag(uint32_t tag) { return tag >= 116u && tag <= 127u && tag != 117u && tag != 118u; }
+// A one-level array / object of at most 8 scalar members (C1's {name, v}, C2's {name}), inline:
+// true when it was one (p past it; ok false if malformed), false otherwise (p unchanged: the
+// container goes to skip_any_nl).
+template <bool FULL, class S>
+YC_HDI bool any_flat(const S& b, uint32_t& p, uint32_t end, uint32_t& steps, bool& ok, uint32_t& cf) {
+  const uint32_t p0 = p, tag = b.u8(p);
+  uint32_t q = p + 1, c = 0, st = steps;
+  bool o = true;
+  const uint32_t m = b.vu(q, end, o);
+  if (!o || m > 8 || st < m + 1) return false;
+  if (FULL) c |= vu_overlong_at(b, p0 + 1, q);
+  int64_t prev = -1;
+  for (uint32_t i = 0; i < m; ++i) {
+    if (tag == 118) {  // the member's key
+      const uint32_t k0 = q, k = b.vu(q, end, o);
+      if (!o) { ok = false; p = q; return true; }
+      const uint32_t ks = q;
+      skip_bytes(q, k, end, o);
+      if (FULL && o) {
+        if (!utf8_valid(b, ks, k)) o = false;
+        c |= vu_overlong_at(b, k0, ks);
+        int64_t ki;
+        c |= key_flags_at(b, ks, k, ki);
+        // Object.keys order: array-index keys first, ascending, then the others (skip_any)
+        if (ki >= 0 && (prev == -2 || (prev >= 0 && ki <= prev))) c |= ANY_UNSUP;
+        prev = ki >= 0 ? ki : -2;
+      }
+      if (!o) { ok = false; p = q; return true; }
+    }
+    if (q >= end) { ok = false; p = q; return true; }
+    const uint32_t t = b.u8(q);
+    if (!any_scalar_tag(t)) return false;  // a nested container: the general reader
+    ++q;
+    any_scalar<FULL>(b, t, q, end, o, c);
+    if (!o) { ok = false; p = q; return true; }
+  }
+  p = q;
+  steps = st - (m + 1);
+  cf |= c;
+  return true;
+}
+
 // Out of line: the container stack costs DEPTH registers wherever skip_any is inlined, so struct
-// parsers take scalar values inline and hand containers to this call.
+// parsers take scalar values (and one-level containers of scalars) inline and hand the other
+// containers to this call.
 // (State goes in and out by value: taking the caller's cursor by address would put it in scratch.)
 struct AnySkip { uint32_t p, steps, ok, cf; };
 template <int DEPTH, bool UTF8 = false>
@@ -326,6 +428,7 @@ struct StructView {
   uint32_t rc, rk;     // right origin valid if info&0x40
   uint32_t pa, pb;     // root name: (pos of varString, byte length incl. prefix) | parent id (client, clock)
   uint32_t psub_pos, psub_len;  // varString (incl. length prefix)
+  uint32_t pn, psn;    // byte lengths of the root name / parentSub strings (FULL parses)
   uint32_t cpos, cend; // content bytes [cpos, cend)
   uint32_t nel;        // Any/JSON element count
   uint32_t anyf;       // ANY_* flags of the content's `any` values (FULL parses)
@@ -336,6 +439,7 @@ struct StructView {
 struct RawSrc {
   const uint8_t* __restrict__ b;
   YC_HDI uint32_t u8(uint32_t p) const { return b[p]; }
+  YC_HDI uint32_t w4(uint32_t p) const { return le32(b, p); }
   YC_HDI uint32_t vu(uint32_t& p, uint32_t end, bool& ok) const { return rd_vu(b, p, end, ok); }
   YC_HDI void svi(uint32_t& p, uint32_t end, bool& ok) const { skip_vi(b, p, end, ok); }
 };
@@ -370,16 +474,16 @@ YC_HD inline int parse_struct(const Src& b, uint32_t& p, uint32_t end, uint32_t 
     if (!ok) return p >= end ? -2 : 0;
     if (pinfo == 1) {
       uint32_t st = p;
-      skip_str<FULL>(b, p, end, ok);
-      if (FULL) { v->pkind = 1; v->pa = st; v->pb = p - st; }
+      const uint32_t n = skip_str<FULL>(b, p, end, ok);
+      if (FULL) { v->pkind = 1; v->pa = st; v->pb = p - st; v->pn = n; }
     } else {
       uint32_t c = b.vu(p, end, ok), k = b.vu(p, end, ok);
       if (FULL) { v->pkind = 2; v->pa = c; v->pb = k; }
     }
     if (info & 0x20u) {
       uint32_t st = p;
-      skip_str<FULL>(b, p, end, ok);
-      if (FULL) { v->has_psub = 1; v->psub_pos = st; v->psub_len = p - st; }
+      const uint32_t n = skip_str<FULL>(b, p, end, ok);
+      if (FULL) { v->has_psub = 1; v->psub_pos = st; v->psub_len = p - st; v->psn = n; }
     }
     if (!ok) return p >= end ? -2 : 0;
   }
@@ -416,15 +520,7 @@ YC_HD inline int parse_struct(const Src& b, uint32_t& p, uint32_t end, uint32_t 
       uint32_t k = b.vu(p, end, ok);
       uint32_t st = p;
       if (ok) skip_bytes(p, k, end, ok);
-      if (FULL && ok && !utf8_valid(b, st, k)) ok = false;
-      if (ok && FULL) {  // ContentString length counts UTF-16 code units
-        uint32_t u = 0;
-        for (uint32_t i = st; i < st + k; ++i) {
-          uint32_t c = b.u8(i);
-          if ((c & 0xC0u) != 0x80u) u += (c >= 0xF0u) ? 2u : 1u;
-        }
-        len = u;
-      }
+      if (FULL && ok) len = utf8_units(b, st, k, ok);  // ContentString length counts UTF-16 code units
       break;
     }
     case REF_FORMAT: {
@@ -449,23 +545,12 @@ YC_HD inline int parse_struct(const Src& b, uint32_t& p, uint32_t end, uint32_t 
       len = n;
       for (uint32_t i = 0; i < n && ok; ++i) {
         const uint32_t tag = p < end ? b.u8(p) : 0u;
-        if (p < end && steps > 0 && tag >= 116u && tag <= 127u && tag != 117u && tag != 118u) {  // a scalar: skip_any's one step
+        if (p < end && steps > 0 && any_scalar_tag(tag)) {  // a scalar: skip_any's one step
           --steps;
           ++p;
-          const uint32_t s0 = p;
-          switch (tag) {
-            case 125: b.svi(p, end, ok); if (FULL && ok) cf |= vi_flag_at(b, s0, p); break;
-            case 124: skip_bytes(p, 4, end, ok); if (FULL && ok) cf |= f32_flag((uint32_t)be_at(b, s0, 4)); break;
-            case 123: skip_bytes(p, 8, end, ok); if (FULL && ok) cf |= f64_flag(be_at(b, s0, 8)); break;
-            case 122: skip_bytes(p, 8, end, ok); break;
-            case 119: {
-              skip_str<FULL>(b, p, end, ok);
-              if (FULL && ok) { uint32_t q = s0; bool o2 = true; b.vu(q, end, o2); cf |= vu_overlong_at(b, s0, q); }
-              break;
-            }
-            case 116: { const uint32_t k = b.vu(p, end, ok); if (FULL && ok) cf |= vu_overlong_at(b, s0, p); if (ok) skip_bytes(p, k, end, ok); break; }
-            default: break;  // 127 undefined, 126 null, 121 false, 120 true
-          }
+          any_scalar<FULL>(b, tag, p, end, ok, cf);
+        } else if (p < end && steps > 0 && (tag == 117u || tag == 118u) && any_flat<FULL>(b, p, end, steps, ok, cf)) {
+          // (a one-level container of scalars, inline)
         } else {
           const AnySkip r = skip_any_nl<DEPTH, FULL>(b.b, p, end, steps);
           p = r.p;

@@ -501,14 +501,79 @@ __device__ __forceinline__ uint32_t block_excl_scan256(uint32_t v, uint32_t* sh,
 }
 
 // Groups of TSMALL+1 .. TWAVE members: one wavefront each, four per workgroup (C4's list heads:
-// the pushes of up to 64 replicas after one element, ~10^5 groups). Lane i stages member i in LDS
-// and finds its anchor with a shuffle scan (the lowest member with the same outside right origin);
-// lane 0 runs the loop. k_tsib_big's MID variant took them one workgroup (and a 2 048-slot hash
-// table to clear) each.
+// the pushes of up to 64 replicas after one element, ~10^5 groups). Lane i holds member i and
+// finds its anchor with a shuffle scan (the lowest member with the same outside right origin).
+// The loop runs on the whole wavefront in position form (sib_wave).
 constexpr uint32_t TWAVE = 64;
+__device__ __forceinline__ int wave_max_i32(int v) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) v = max(v, __shfl_xor(v, o, 64));
+  return v;
+}
+__device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) v = min(v, (uint32_t)__shfl_xor((int)v, o, 64));
+  return v;
+}
+// The B.1 loop of sib_loop, evaluated by the whole wavefront (lane = member, n <= 64) over list
+// POSITIONS instead of lane 0 walking linked lists (scripts/sib_wave_proto.py checks the two forms
+// equal, ties and right-origin cycles included). The members are placed in sib_loop's order (by
+// index, each right-origin sibling first); every lane keeps its position in the list built so far
+// and when it was placed. Placing c:
+//   succ = the placed member of c's right-origin group (gk) with the smallest client above c's —
+//          lanes are in client order, so the lowest such lane (ties: the one placed first);
+//   stop = succ, else c's right-origin sibling, else the end;
+//   left = the largest position before stop held by a placed member of a lower client;
+//   c takes the position after left, every position at or past it moves up by one.
+// Each step is a few ballots, shuffles and one max reduction: no dependent LDS walks. Returns the
+// first member (NONE on a right-origin cycle, reported as ERR_DECODE); pos is the lane's final
+// position.
+__device__ uint32_t sib_wave(uint32_t n, uint32_t lane, uint32_t cid, uint32_t rp, uint32_t gk, int& pos, uint32_t* err) {
+  uint32_t done = 0, seq = 0, stk = 0, placed = 0;
+  pos = -1;
+  for (uint32_t i0 = 0; i0 < n; ++i0) {
+    if ((uint32_t)__shfl((int)done, (int)i0, 64) == 2u) continue;
+    if (lane == i0) done = 1;
+    if (lane == 0) stk = i0;
+    uint32_t sp = 1, c = i0;
+    while (sp > 0) {
+      const uint32_t r = (uint32_t)__shfl((int)rp, (int)c, 64);
+      if (r != NONE) {
+        const uint32_t dr = (uint32_t)__shfl((int)done, (int)r, 64);
+        if (dr != 2u) {  // the right origin is a sibling: place it first
+          if (dr == 1u || sp >= n) { if (lane == 0) raise_err(err, ERR_DECODE); return NONE; }
+          if (lane == r) done = 1;
+          if (lane == sp) stk = r;
+          ++sp;
+          c = r;
+          continue;
+        }
+      }
+      const uint32_t cc = (uint32_t)__shfl((int)cid, (int)c, 64), g = (uint32_t)__shfl((int)gk, (int)c, 64);
+      const bool pl = done == 2u;
+      const uint64_t cand = __ballot(pl && gk == g && cid > cc);
+      uint32_t stop = r;
+      if (cand) {
+        stop = (uint32_t)__ffsll((long long)cand) - 1;
+        const uint32_t cs = (uint32_t)__shfl((int)cid, (int)stop, 64);
+        const uint64_t ties = cand & __ballot(cid == cs);
+        if (ties & (ties - 1)) {  // one client twice in one group (never from Yjs): the first placed
+          const uint32_t m = wave_min_u32(((ties >> lane) & 1ull) ? seq : 0xFFFFFFFFu);
+          stop = (uint32_t)__ffsll((long long)(ties & __ballot(seq == m))) - 1;
+        }
+      }
+      const int pstop = stop != NONE ? __shfl(pos, (int)stop, 64) : (int)placed;
+      const int p = wave_max_i32(pl && pos < pstop && cid < cc ? pos : -1) + 1;
+      if (pl && pos >= p) ++pos;
+      if (lane == c) { pos = p; seq = placed; done = 2; }
+      ++placed;
+      if (--sp > 0) c = (uint32_t)__shfl((int)stk, (int)(sp - 1), 64);
+    }
+  }
+  return (uint32_t)__ffsll((long long)__ballot(pos == 0)) - 1;
+}
 __global__ __launch_bounds__(256) void k_tsib_wave(Work w, uint32_t nsegs, uint32_t nbig) {
-  __shared__ SibRec rec[4][TWAVE];
-  __shared__ uint8_t st[4][TWAVE];
+  __shared__ uint8_t ord[4][TWAVE];
   const uint32_t wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const uint32_t bi = blockIdx.x * 4 + wv;
   if (bi >= nbig) return;  // whole wavefronts only: no workgroup barrier below
@@ -525,28 +590,22 @@ __global__ __launch_bounds__(256) void k_tsib_wave(Work w, uint32_t nsegs, uint3
     const uint32_t rj = __shfl(rk, j);
     if (anc == NONE && rk != NONE && rj == rk) anc = j;
   }
-  if (in) {
-    w.t_trep[a + lane] = rp != NONE ? rp : (a + anc) | 0x80000000u;
-    rec[wv][lane] = SibRec{cid, (uint16_t)(rp == NONE ? S_NONE : rp - a),
-                           (uint16_t)(rp != NONE ? rp - a : anc | TOUT), S_NONE, S_NONE, S_NONE, S_NONE, S_NONE, 0};
-    st[wv][lane] = 0;
-  }
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-  uint32_t head = NONE;
-  if (lane == 0) {
-    SibLds acc{rec[wv], st[wv]};
-    head = sib_loop(acc, n, w.y_stack + a, &w.ctr->err);
-  }
+  if (in) w.t_trep[a + lane] = rp != NONE ? rp : (a + anc) | 0x80000000u;
+  // right-origin group: the sibling (local index), or 64 + the anchor of an outside right origin
+  const uint32_t lrp = rp != NONE ? rp - a : NONE;
+  const uint32_t gk = !in ? 0xFFFFu : lrp != NONE ? lrp : TWAVE + anc;
+  int pos;
+  const uint32_t head = sib_wave(n, lane, in ? cid : 0xFFFFFFFFu, in ? lrp : NONE, gk, pos, &w.ctr->err);
+  if (head == NONE) return;
+  if (in) ord[wv][pos] = (uint8_t)lane;
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   if (in) {
-    const uint32_t x = rec[wv][lane].nxt;
-    w.t_nsib[w.t_seg[a + lane]] = x == S_NONE ? NONE : w.t_seg[a + x];
+    const uint32_t x = pos + 1 < (int)n ? ord[wv][pos + 1] : NONE;
+    w.t_nsib[w.t_seg[a + lane]] = x == NONE ? NONE : w.t_seg[a + x];
   }
-  if (lane == 0 && head != NONE) sib_publish(w, a, n, nsegs, head);
+  if (lane == 0) sib_publish(w, a, n, nsegs, head);
 }
 
 // CAP: LDS capacity in members, HS: anchor hash slots. MID = the variant for groups of at most

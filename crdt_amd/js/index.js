@@ -31,13 +31,17 @@ const TYPE_ARRAY = 0;
 const TYPE_MAP = 1;
 
 // Observers (YMap/YArray.observe, crdt.js:620-656). Yjs calls them once per transaction that
-// changed the type, synchronously at its end (cleanupTransactions Y@31804). Here Y.applyUpdate
-// stays deferred (one batched merge serves a burst of applies), so events are computed lazily:
-// a mutation only marks the doc; the events fire at the next read of the doc (toJSON, get, has,
-// size, length, encode*) or, if nothing reads it, from setImmediate — whichever comes first — with
-// one read of each observed type, compared with what its previous event delivered (taken when
-// observe() was called). A burst of updates therefore yields one event per type, with the union of
-// their changes (Yjs: one per transaction). Maps compare the winning item id of every entry
+// changed the type, synchronously at its end (cleanupTransactions Y@31804). Two modes:
+//  - 'sync' (the default, Yjs's timing): a doc with observers settles at the end of every mutation
+//    (Y.applyUpdate, set, insert, delete; a transaction at its end), so each event fires inside the
+//    call that caused it — the applied update is merged right away instead of at the next read;
+//  - 'deferred' (opt-in: Y.setObserverMode('deferred') or new Y.Doc({observers: 'deferred'})): a
+//    mutation only marks the doc; the events fire at the next read of the doc (toJSON, get, has,
+//    size, length, encode*) or, if nothing reads it, from setImmediate — whichever comes first — so
+//    one batched merge serves a burst of applies, which then yields one event per type with the
+//    union of their changes (Yjs: one per transaction).
+// Either way an event is computed from one read of each observed type, compared with what its
+// previous event delivered (taken when observe() was called). Maps compare the winning item id of every entry
 // (ycrdt_map_entries): keysChanged = keys whose winning item changed — a set of the same value is a
 // new item, and changes inside a nested type are not the map's (YMap.observe, not observeDeep);
 // changes.keys carries {action, oldValue}. Arrays carry changes.delta ([{retain}, {delete},
@@ -57,48 +61,64 @@ function arrayDelta(a, b) {
   if (b.length - p - q) delta.push({ insert: b.slice(p, b.length - q) });
   return delta;
 }
+let observerMode = 'sync';
+function setObserverMode(mode) {
+  if (mode !== 'sync' && mode !== 'deferred') throw new Error("observer mode is 'sync' or 'deferred'");
+  observerMode = mode;
+}
+const syncObservers = (doc) => (doc._obsMode || observerMode) === 'sync';
 function markChanged(doc, local) {
   if (!doc._observed.size) return;
   doc._local = doc._dirty ? doc._local && local : local;
   doc._dirty = true;
+  if (syncObservers(doc)) { if (!doc._firing) fireObservers(doc); return; }  // (inside a callback: after it)
   if (!doc._timer) doc._timer = setImmediate(() => { doc._timer = null; fireObservers(doc); });
 }
 function fireObservers(doc) {
   if (!doc._dirty || doc._firing) return;
-  doc._dirty = false;
   doc._firing = true;
   try {
-    const transaction = { doc, local: doc._local, origin: null };
-    for (const t of Array.from(doc._observed)) {
-      if (!t._observers.length) continue;
-      const nowJson = jsonOf(t);
-      const now = JSON.stringify(nowJson);
-      const old = t._seen;
-      t._seen = now;
-      if (old === undefined || now === old) continue;
-      const event = { target: t, currentTarget: t, transaction, changes: { added: new Set(), deleted: new Set(), delta: [], keys: new Map() } };
-      const a = JSON.parse(old), b = nowJson;
-      if (t instanceof YMap) {  // a, b: {key: [winning item id, value]}
-        const keys = new Set([...Object.keys(a), ...Object.keys(b)]);
-        event.keysChanged = new Set();
-        for (const k of keys) {
-          const ina = Object.prototype.hasOwnProperty.call(a, k), inb = Object.prototype.hasOwnProperty.call(b, k);
-          if (ina && inb && a[k][0] === b[k][0]) continue;
-          event.keysChanged.add(k);
-          event.changes.keys.set(k, { action: !ina ? 'add' : !inb ? 'delete' : 'update', oldValue: ina ? a[k][1] : undefined });
-        }
-        if (!event.keysChanged.size) continue;  // only nested contents changed: not this map's event
-      } else {
-        event.changes.delta = arrayDelta(a, b);
-      }
-      event.delta = event.changes.delta;
-      for (const f of t._observers.slice()) f(event, transaction);
+    // sync mode: a callback's own mutations are a transaction of their own, delivered after it
+    // (bounded: callbacks that keep mutating end after 100 rounds, the rest at the next read)
+    for (let round = 0; doc._dirty && round < 100; ++round) {
+      doc._dirty = false;
+      fireRound(doc);
+      if (!syncObservers(doc)) break;
     }
   } finally {
     doc._firing = false;
   }
 }
-// runs one mutation of `doc`; its observers fire at the next read (or tick) unless a transaction is open
+function fireRound(doc) {
+  const transaction = { doc, local: doc._local, origin: null };
+  for (const t of Array.from(doc._observed)) {
+    if (!t._observers.length) continue;
+    const nowJson = jsonOf(t);
+    const now = JSON.stringify(nowJson);
+    const old = t._seen;
+    t._seen = now;
+    if (old === undefined || now === old) continue;
+    const event = { target: t, currentTarget: t, transaction, changes: { added: new Set(), deleted: new Set(), delta: [], keys: new Map() } };
+    const a = JSON.parse(old), b = nowJson;
+    if (t instanceof YMap) {  // a, b: {key: [winning item id, value]}
+      const keys = new Set([...Object.keys(a), ...Object.keys(b)]);
+      event.keysChanged = new Set();
+      for (const k of keys) {
+        const ina = Object.prototype.hasOwnProperty.call(a, k), inb = Object.prototype.hasOwnProperty.call(b, k);
+        if (ina && inb && a[k][0] === b[k][0]) continue;
+        event.keysChanged.add(k);
+        event.changes.keys.set(k, { action: !ina ? 'add' : !inb ? 'delete' : 'update', oldValue: ina ? a[k][1] : undefined });
+      }
+      if (!event.keysChanged.size) continue;  // only nested contents changed: not this map's event
+    } else {
+      event.changes.delta = arrayDelta(a, b);
+    }
+    event.delta = event.changes.delta;
+    for (const f of t._observers.slice()) f(event, transaction);
+  }
+}
+// runs one mutation of `doc`; its observers fire at its end (sync) or at the next read / tick
+// (deferred), unless a transaction is open
 function mutate(doc, fn, local = true) {
   const r = fn();
   if (!doc._txn) markChanged(doc, local);
@@ -217,6 +237,8 @@ class Doc {
     this._dirty = false;         // mutated since the observers last saw it
     this._local = true;
     this._timer = null;
+    this._obsMode = opts.observers;  // 'sync' | 'deferred' | undefined (the module's mode)
+    if (this._obsMode !== undefined && this._obsMode !== 'sync' && this._obsMode !== 'deferred') throw new Error("observers: 'sync' or 'deferred'");
   }
   _root(name, Cls) {
     let t = this._types.get(name);
@@ -301,6 +323,7 @@ module.exports = {
   takeLocalUpdate: (doc) => binding.takeLocalUpdate(doc._h),
   trackLocalUpdates: (doc, on = true) => binding.trackLocalUpdates(doc._h, on),
   lastStats: (doc) => binding.lastStats(doc._h),
+  setObserverMode,
   version: binding.version,
   setDevice: binding.setDevice,
   _setNextClientId: (c) => { nextClient = c; },

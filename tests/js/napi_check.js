@@ -81,10 +81,14 @@ if (mode === 'cpu') {
   console.log('napi ops ok:', n, 'scripts,', events, 'map events');
 } else if (mode === 'observe') {
   // observer events (tests/golden/observe.json, gen_observe_fixtures.js): the Yjs 13.5.16 events of
-  // every step, replayed through the facade; its events fire at the next read of the doc
+  // every step, replayed through the facade in both observer modes: 'sync' (the default: every
+  // event inside the call that caused it, checked before anything reads the docs) and 'deferred'
+  // (events at the next read)
   const cases = JSON.parse(fs.readFileSync(path.join(ROOT, 'tests', 'golden', 'observe.json'))).cases;
   const norm = (v) => (v === undefined ? null : JSON.parse(JSON.stringify(v)));
   let nev = 0;
+  for (const om of ['sync', 'deferred']) {
+  Y.setObserverMode(om);
   for (const c of cases) {
     const log = [];
     const rec = (peer, target) => (ev) => {
@@ -113,6 +117,7 @@ if (mode === 'cpu') {
         else throw new Error(o.op);
       }
       Y.applyUpdate(B, unhex(st.sync));
+      const early = om === 'sync' ? log.splice(0) : [];  // delivered before anything read the docs
       const json = { A: norm(A.getMap('users').toJSON()), B: norm(B.getMap('users').toJSON()), Bm: norm(B.getArray('messages').toJSON()) };
       assert.deepStrictEqual(json, st.json, tag + ' toJSON');
       if (st.observeNested) {
@@ -120,13 +125,15 @@ if (mode === 'cpu') {
         B.getMap('users').get(st.observeNested).observe(rec('B', 'users.' + st.observeNested));
       }
       const key = (e) => e.peer + ' ' + e.target;
-      const got = log.splice(0).sort((x, y) => (key(x) < key(y) ? -1 : key(x) > key(y) ? 1 : 0));
+      if (om === 'sync') assert.strictEqual(log.length, 0, tag + ' sync events after a read');
+      const got = early.concat(log.splice(0)).sort((x, y) => (key(x) < key(y) ? -1 : key(x) > key(y) ? 1 : 0));
       const want = st.events.slice().sort((x, y) => (key(x) < key(y) ? -1 : key(x) > key(y) ? 1 : 0));
       assert.deepStrictEqual(got, want, tag + ' events');
       nev += want.length;
     });
   }
-  console.log('napi observe ok:', cases.length, 'scripts,', nev, 'events');
+  }
+  console.log('napi observe ok:', cases.length, 'scripts x 2 modes,', nev, 'events');
 } else if (mode === 'trace') {
   // crdt.js-driven traces (tests/golden/crdtjs_traces.json, gen_crdtjs_traces.js): every Y call
   // crdt.js made on every peer, replayed in order; every wire update / state vector byte-equal

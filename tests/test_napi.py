@@ -54,6 +54,7 @@ def test_napi_crdtjs_traces_on_gpu():
 def test_napi_observer_events_on_gpu():
     """YMap / YArray observers (crdt.js:620-657) deliver the events Yjs 13.5.16 delivered on the same
     scripts (tests/golden/observe.json): keysChanged and changes.keys from the entries' winning
-    items, YArray changes.delta, nested arrays observed on their own list; events fire at the next
-    read instead of forcing a merge per Y.applyUpdate."""
+    items, YArray changes.delta, nested arrays observed on their own list. Both observer modes:
+    'sync' (Yjs's timing: every event inside the call that caused it, before any read) and
+    'deferred' (events at the next read, one merge per burst of Y.applyUpdate)."""
     assert "napi observe ok" in _run("observe", 300)
