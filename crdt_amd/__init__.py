@@ -71,7 +71,8 @@ class MergeStats(ctypes.Structure):
 
 
 def library_path():
-    return os.path.join(_HERE, "libycrdt.so")
+    # YCRDT_LIB: another build of the library (A/B experiments); the in-tree one by default
+    return os.environ.get("YCRDT_LIB") or os.path.join(_HERE, "libycrdt.so")
 
 
 EXPORTS = (

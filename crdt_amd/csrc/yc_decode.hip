@@ -1176,8 +1176,10 @@ __global__ __launch_bounds__(64) void k_fastwalk(Work w) {
   const uint32_t Lp = select_from(spec, fa, rem);
   const uint32_t dsp = chain_step(b, Lp, uend);
   if (Lp >= uend || dsp > uend) { why(5); return; }
-  // marks: the walked positions of chunk 0, then every chain position in [q, Lp]
-  const uint32_t wq = q >> 6, wl = Lp >> 6, w0 = ustart >> 6;
+  // marks: the walked positions of chunk 0, then every chain position in [q, Lp] — here the words
+  // that can hold walked positions, the rest grid-wide (k_fastmark: one wavefront copying a 15 MB
+  // update's words took 4 ms of C4's decode)
+  const uint32_t wq = q >> 6, wl = min(Lp >> 6, (ustart >> 6) + SW + 1), w0 = ustart >> 6;
   for (uint32_t wd = w0 + lane; wd <= wl; wd += 64) {
     uint64_t x = wd >= wq ? range_word(spec, wd, q, Lp + 1) : 0ull;
     if (wd - w0 < SW + 2) x |= walked[wd - w0];
@@ -1194,8 +1196,27 @@ __global__ __launch_bounds__(64) void k_fastwalk(Work w) {
     w.usec_start[u] = sbase;
     w.usec_n[u] = 1;
     w.dsstart[u] = dsp;
+    w.fw[2 * u] = q;
+    w.fw[2 * u + 1] = Lp + 1;
     w.ufail[u] = 2u;  // done: k_walk leaves the update alone
     if (w.dbg) atomicAdd(&w.dbg[0], 1ull);
+  }
+}
+
+// The chain-position words of the fast-walked updates past their first chunk, one lane per word
+// of every chunk (grid-stride).
+__global__ __launch_bounds__(256) void k_fastmark(Work w) {
+  const uint32_t wpc = w.schunk / 64;  // words per chunk (chunks are 64-byte aligned)
+  const uint64_t total = (uint64_t)w.ngroups * wpc;
+  for (uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total; t += (uint64_t)gridDim.x * blockDim.x) {
+    const Group gr = w.groups[t / wpc];
+    const uint32_t u = gr.upd;
+    if (w.ufail[u] != 2u) continue;
+    const uint32_t wd = (gr.start >> 6) + (uint32_t)(t % wpc);
+    const uint32_t q = w.fw[2 * u], e = w.fw[2 * u + 1];
+    if (wd <= (w.uoff[u] >> 6) + SW + 1 || wd > ((e - 1) >> 6)) continue;  // (k_fastwalk's words; past the last struct)
+    const uint32_t uw = upd_win(w, u);
+    win_words(w.final_bits, uw)[wd] = range_word(win_words(w.spec_bits, uw), wd, q, e);
   }
 }
 
@@ -1516,7 +1537,10 @@ void launch_chunks(const Work& w, hipStream_t s) {
   }
   if (w.nbig) {
     static const bool nofast = getenv("YCRDT_NO_FASTWALK") && getenv("YCRDT_NO_FASTWALK")[0] == '1';
-    if (!nofast && !w.force_xtab) hipLaunchKernelGGL(k_fastwalk, dim3(w.nbig), dim3(64), 0, s, w);
+    if (!nofast && !w.force_xtab) {
+      hipLaunchKernelGGL(k_fastwalk, dim3(w.nbig), dim3(64), 0, s, w);
+      hipLaunchKernelGGL(k_fastmark, dim3(std::min<uint64_t>((uint64_t)w.ngroups * (w.schunk / 64) / 256 + 1, 8192)), dim3(256), 0, s, w);
+    }
     hipLaunchKernelGGL(k_walk<false>, dim3(w.nbig), dim3(64), 0, s, w);
     // the table path, for updates the speculative walk handed over (grid-stride over xlist)
     hipLaunchKernelGGL(k_xtab, dim3(std::min(w.ngroups, 4096u)), dim3(64), 0, s, w);

@@ -176,7 +176,7 @@ enum Buf {
   B_UOWN, B_UFLAG, B_UMIN, B_UCUT, B_UWPRE,
   B_GSTART, B_GCIDX, B_GSRC, B_GFLAGS, B_GORIG, B_GRORIG, B_GLINK, B_GOSEG, B_GKEY, B_GMAXC, B_GNEXT, B_GOUTID, B_GTMP, B_GTMP2,
   B_KHASH, B_KROOT, B_KWIN, B_KPAR, B_KFLAG, B_SPK,
-  B_USEC, B_USECN, B_DBG, B_XTAB, B_UFAIL, B_TENTRY, B_XLIST,
+  B_USEC, B_USECN, B_DBG, B_XTAB, B_UFAIL, B_FW, B_TENTRY, B_XLIST,
   B_LZKEY, B_LZKEYS, B_LZIOTA, B_LZSEC, B_LZRSTART, B_LZPREV, B_LZFIRST, B_LZCAP, B_LZEVBASE, B_LZEVN, B_LZFLAG,
   B_LZLHI, B_LZLLO, B_EVKIND, B_EVSRC, B_EVCLOCK, B_EVLEN, B_EVSIZE, B_EVPOS, B_BLKSIZE, B_BLKPOS, B_SVC, B_SVK,
   B_DSMKEY, B_DSMKEYS, B_DSMLEN, B_DSMLENS, B_DSMEND, B_DSMMAX, B_DSMFLAG, B_DSMRID, B_DRCLIENT, B_DRCLOCK, B_DREND,
@@ -812,6 +812,7 @@ int run_decode(ycrdt_engine* e, ycrdt_batch* b, bool lazy, Decoded& D, bool gene
   w.tentry = take<uint32_t>(V, B_TENTRY, (uint64_t)w.ngroups + 1, ok);
   w.xlist = take<uint32_t>(V, B_XLIST, (uint64_t)w.ngroups + 1, ok);
   w.ufail = take<uint32_t>(V, B_UFAIL, nu + 1, ok);
+  w.fw = take<uint32_t>(V, B_FW, 2ull * nu + 2, ok);
   w.final_bits = take<uint64_t>(V, B_FINAL, nwords, ok);
   w.sec_bits = take<uint64_t>(V, B_SECB, nwords, ok);
   w.dsstart = take<uint32_t>(V, B_DSSTART, nu + 1, ok);
@@ -1194,7 +1195,7 @@ int run_merge(ycrdt_engine* e, ycrdt_batch* b, const std::unordered_map<uint32_t
       if (D.nested) run_dead_keys(w, nsegs, s);  // only lists under a parent item can die with it
       mark(e, "merge.yata");
       e->nlists = launch_yata(w, nsegs, narray, nclients, s);
-      if (w.dbg && e->nlists) {
+      if (w.dbg && e->nlists && e->nlists != LISTS_UNNUMBERED) {
         unsigned long long h[3];
         HIPCHK(hipStreamSynchronize(s));
         HIPCHK(hipMemcpy(h, w.dbg, sizeof(h), hipMemcpyDeviceToHost));
@@ -1293,6 +1294,7 @@ int run_view(ycrdt_engine* e, ycrdt_batch* b, HostView& hv) {
   g_bufs = &V;
   bool ok = true;
   hipStream_t s = e->stream;
+  if (e->nlists == LISTS_UNNUMBERED) e->nlists = launch_ylists(w, e->nsegs, s);  // (the merge's tree path skipped it)
   const uint32_t nsegs = e->nsegs, nlists = e->nlists;
   uint32_t narr = 0;
   if (nlists) {
@@ -1318,17 +1320,36 @@ int run_view(ycrdt_engine* e, ycrdt_batch* b, HostView& hv) {
   hv.bytes.assign(b->nbytes, 0);
   if (nsegs) {
     launch_view(w, vb, nsegs, nlists, narr, s);
+    // a small view (the per-op path's doc) comes back in ONE synchronisation: counters, key count,
+    // the key table up to its capacity, the list segments and the state bytes, queued together
+    // (each synchronous copy cost a ~25 us round trip); a large one sizes the key copy first
+    static const bool big_only = getenv("YCRDT_VIEW_SYNC") && getenv("YCRDT_VIEW_SYNC")[0] == '1';
+    const bool small = !big_only && (uint64_t)ck * sizeof(ViewKey) <= (256u << 10);
     Counters c;
-    int rc = check(e, c, "view");
-    if (rc) return rc;
     uint32_t nkeys = 0;
-    HIPCHK(hipMemcpy(&nkeys, vb.nkeys, sizeof(uint32_t), hipMemcpyDeviceToHost));
-    hv.keys.resize(nkeys);
+    HIPCHK(hipMemcpyAsync(&c, w.ctr, sizeof(Counters), hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(&nkeys, vb.nkeys, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
     hv.segs.resize(narr);
-    if (nkeys) HIPCHK(hipMemcpy(hv.keys.data(), vb.keys, sizeof(ViewKey) * nkeys, hipMemcpyDeviceToHost));
-    if (narr) HIPCHK(hipMemcpy(hv.segs.data(), vb.segs, sizeof(ViewSeg) * narr, hipMemcpyDeviceToHost));
+    if (small) {
+      hv.keys.resize(ck);
+      HIPCHK(hipMemcpyAsync(hv.keys.data(), vb.keys, sizeof(ViewKey) * ck, hipMemcpyDeviceToHost, s));
+      if (narr) HIPCHK(hipMemcpyAsync(hv.segs.data(), vb.segs, sizeof(ViewSeg) * narr, hipMemcpyDeviceToHost, s));
+      if (b->nbytes) HIPCHK(hipMemcpyAsync(hv.bytes.data(), b->bytes.p, b->nbytes, hipMemcpyDeviceToHost, s));
+    }
+    HIPCHK(hipStreamSynchronize(s));
+    if (c.err) return map_err(c.err, "view");
+    if (nkeys > ck) return fail(YCRDT_E_DEVICE, "view: key count past the key table");
+    if (small) {
+      hv.keys.resize(nkeys);
+    } else {
+      hv.keys.resize(nkeys);
+      if (nkeys) HIPCHK(hipMemcpy(hv.keys.data(), vb.keys, sizeof(ViewKey) * nkeys, hipMemcpyDeviceToHost));
+      if (narr) HIPCHK(hipMemcpy(hv.segs.data(), vb.segs, sizeof(ViewSeg) * narr, hipMemcpyDeviceToHost));
+      if (b->nbytes) HIPCHK(hipMemcpy(hv.bytes.data(), b->bytes.p, b->nbytes, hipMemcpyDeviceToHost));
+    }
+  } else if (b->nbytes) {
+    HIPCHK(hipMemcpy(hv.bytes.data(), b->bytes.p, b->nbytes, hipMemcpyDeviceToHost));
   }
-  if (b->nbytes) HIPCHK(hipMemcpy(hv.bytes.data(), b->bytes.p, b->nbytes, hipMemcpyDeviceToHost));
   hv.index();
   hv.valid = true;
   return YCRDT_OK;

@@ -103,6 +103,7 @@ struct Work {
   uint32_t* xtab = nullptr;        // [G x XK] locked updates only, per entry offset: count << 16 | exit - chunk end
   uint32_t* tentry = nullptr;      // [G] locked updates: true entry of a chunk the table walk did not parse
   uint32_t* xlist = nullptr;       // [G] the chunks of the locked updates (k_xtab / k_xmark work list)
+  uint32_t* fw = nullptr;          // [2 nupd] fast-walked updates: first chain position past the exact walk, end of the last struct
   uint32_t* ufail = nullptr;       // [nupd] 1: the speculative walk gave up (locked chain phases), tables next
   uint64_t* final_bits = nullptr;  // [B/64] verified struct starts
   uint64_t* sec_bits = nullptr;    // [B/64] first struct of every non-empty section
@@ -604,7 +605,9 @@ void launch_shard_mask(const Work& w, uint32_t nsegs, const uint8_t* owner, uint
 void launch_shard_export(const Work& w, uint32_t nsegs, const uint8_t* owner, uint32_t shard, uint32_t* acc, hipStream_t s);
 void launch_merge_final(const Work& w, uint32_t nsegs, hipStream_t s);
 void run_dead_keys(const Work& w, uint32_t nsegs, hipStream_t s);
+constexpr uint32_t LISTS_UNNUMBERED = 0xFFFFFFFFu;  // launch_yata: lists exist, launch_ylists numbers them
 uint32_t launch_yata(const Work& w, uint32_t nsegs, uint32_t narray, uint32_t nclients, hipStream_t s);
+uint32_t launch_ylists(const Work& w, uint32_t nsegs, hipStream_t s);
 
 // side / ev_fork / ev_join / tmp2: the delete-set run chain runs on `side` with its own scan space
 void launch_encode_sizes(const Work& w, uint32_t nsegs, uint32_t nclients, hipStream_t s, hipStream_t side,

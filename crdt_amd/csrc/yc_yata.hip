@@ -25,13 +25,19 @@ __device__ __forceinline__ uint32_t seg_of_unit(const Work& w, uint32_t g) {
   return w.u_wpre[g >> 6] + (uint32_t)__popcll(w.u_cutbits[g >> 6] & ((2ull << (g & 63)) - 1)) - 1;
 }
 
+// YATA's per-segment state: the sort values, the final right neighbours, the sequential kernels' stamps
+__global__ void k_yinit(Work w, uint32_t nsegs) {
+  const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= nsegs) return;
+  w.y_iota[s] = s;
+  w.g_right[s] = NONE;
+  w.y_state[s] = 0;
+}
 __global__ void k_ykey(Work w, uint32_t nsegs) {
   const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
   if (s >= nsegs) return;
   w.y_key[s] = (w.g_flags[s] & SEG_ARRAY) ? w.g_key[s] : NONE;
   w.y_iota[s] = s;
-  w.g_right[s] = NONE;
-  w.y_state[s] = 0;
 }
 
 // flag list starts; y_before doubles as the flag array, y_confl receives the scan
@@ -267,7 +273,7 @@ constexpr uint32_t TSMALL = 16, TLDS = 6144;  // 20 B per member in LDS
 __global__ void k_tkey(Work w, uint32_t nsegs) {
   const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
   if (s >= nsegs) return;
-  uint32_t key = NONE, p = NONE;
+  uint32_t key = NONE, p = NONE, rs = NONE;
   if (w.g_flags[s] & SEG_ARRAY) {
     const uint32_t list = w.g_key[s];
     const uint32_t o = w.g_origin[s], r = w.g_rorigin[s];
@@ -276,12 +282,13 @@ __global__ void k_tkey(Work w, uint32_t nsegs) {
       if (!(w.g_flags[p] & SEG_ARRAY) || w.g_key[p] != list) raise_err(&w.ctr->err, ERR_DECODE);  // outside the list
     }
     if (r != NONE) {
-      const uint32_t rs = seg_of_unit(w, r);
+      rs = seg_of_unit(w, r);
       if (!(w.g_flags[rs] & SEG_ARRAY) || w.g_key[rs] != list) raise_err(&w.ctr->err, ERR_DECODE);
     }
     key = p != NONE ? p : nsegs + list;
   }
   w.t_key[s] = key;
+  w.y_key[s] = rs;  // the right-origin segment, for k_tprep (y_key is free until launch_ylists)
   w.t_first[s] = NONE;
   w.t_nsib[s] = NONE;
   w.t_jump[s] = p;
@@ -303,7 +310,7 @@ __global__ void k_tgroup_starts(Work w, uint32_t nsegs) {
   if (w.t_done[i]) w.t_gstart[w.t_next[i]] = i;
   if (i + 1 == nsegs || w.t_keys[i + 1] == NONE) w.t_gstart[w.t_next[nsegs]] = i + 1;  // sentinel
 }
-// per sorted position: client index, right-origin unit, sorted position of a sibling right origin
+// per sorted position: client index, right-origin segment, sorted position of a sibling right origin
 // (y_state / y_before / y_confl are free once the list table is built)
 __global__ void k_tprep(Work w, uint32_t nsegs) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -317,14 +324,11 @@ __global__ void k_tprep(Work w, uint32_t nsegs) {
   const uint32_t k = w.t_keys[i];
   if (k == NONE) return;
   const uint32_t s = w.t_seg[i];
-  const uint32_t r = w.g_rorigin[s];
+  const uint32_t rs = w.y_key[s];  // (k_tkey)
   uint32_t rp = NONE;
-  if (r != NONE) {
-    const uint32_t rs = seg_of_unit(w, r);
-    if (w.t_key[rs] == k) rp = w.t_pos[rs];
-  }
+  if (rs != NONE && w.t_key[rs] == k) rp = w.t_pos[rs];
   w.y_state[i] = w.g_cidx[s];
-  w.y_before[i] = r;
+  w.y_before[i] = rs;  // the anchor key: a right-origin unit starts its segment (k_refs), so unit and segment name it alike
   w.y_confl[i] = rp;
 }
 
@@ -449,7 +453,37 @@ __device__ __forceinline__ void sib_anchors_small(const Work& w, uint32_t a, uin
   }
 }
 
-__global__ void k_tsib_small(Work w, uint32_t nsegs) {
+// Groups of at most TSMALL members: one lane each, the group staged in the lane's slice of LDS
+// (8-bit links) so the loop's dependent steps wait on LDS, not on memory (it walked the group in
+// global memory: C4's 1.4 ms).
+struct __attribute__((aligned(4))) SibRec8 { uint32_t cid; uint8_t rpos, trep, nxt, prv, mprv, mtail, otail, pad; };
+struct SibLds8 {
+  SibRec8* rec;
+  uint8_t* st;
+  static constexpr uint8_t N8 = 0xFFu, OUT8 = 0x80u;
+  __device__ static uint32_t w32(uint8_t x) { return x == N8 ? NONE : x; }
+  __device__ static uint8_t w8(uint32_t x) { return x == NONE ? N8 : (uint8_t)x; }
+  __device__ uint32_t done(uint32_t i) const { return st[i]; }
+  __device__ void set_done(uint32_t i, uint32_t v) { st[i] = (uint8_t)v; }
+  __device__ uint32_t rpos(uint32_t i) const { return w32(rec[i].rpos); }
+  __device__ uint32_t trep(uint32_t i, bool& out) const { out = (rec[i].trep & OUT8) != 0; return rec[i].trep & ~OUT8; }
+  __device__ uint32_t cid(uint32_t i) const { return rec[i].cid; }
+  __device__ uint32_t next(uint32_t i) const { return w32(rec[i].nxt); }
+  __device__ void set_next(uint32_t i, uint32_t v) { rec[i].nxt = w8(v); }
+  __device__ uint32_t prv(uint32_t i) const { return w32(rec[i].prv); }
+  __device__ void set_prv(uint32_t i, uint32_t v) { rec[i].prv = w8(v); }
+  __device__ uint32_t mprv(uint32_t i) const { return w32(rec[i].mprv); }
+  __device__ void set_mprv(uint32_t i, uint32_t v) { rec[i].mprv = w8(v); }
+  __device__ uint32_t mtail(uint32_t i) const { return w32(rec[i].mtail); }
+  __device__ void set_mtail(uint32_t i, uint32_t v) { rec[i].mtail = w8(v); }
+  __device__ uint32_t otail(uint32_t i) const { return w32(rec[i].otail); }
+  __device__ void set_otail(uint32_t i, uint32_t v) { rec[i].otail = w8(v); }
+};
+constexpr uint32_t TS_BLOCK = 64;
+__global__ __launch_bounds__(TS_BLOCK) void k_tsib_small(Work w, uint32_t nsegs) {
+  __shared__ SibRec8 rec[TS_BLOCK][TSMALL];
+  __shared__ uint32_t rr[TS_BLOCK][TSMALL];   // right-origin units (anchors), then the loop's stack
+  __shared__ uint8_t st[TS_BLOCK][TSMALL];
   const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
   if (g >= w.ctr->tgroups) return;
   const uint32_t a = w.t_gstart[g], n = w.t_gstart[g + 1] - a;
@@ -457,16 +491,31 @@ __global__ void k_tsib_small(Work w, uint32_t nsegs) {
     w.t_big[atomicAdd(&w.ctr->tbig, 1u)] = g;
     return;
   }
+  const uint32_t t = threadIdx.x;
   uint32_t head = 0;
   if (n > 1) {
-    sib_anchors_small(w, a, n);
-    SibGlobal acc{w, a};
-    head = sib_loop(acc, n, w.y_stack + a, &w.ctr->err);
+    for (uint32_t i = 0; i < n; ++i) {  // independent loads, issued together
+      const uint32_t rp = w.y_confl[a + i];
+      rec[t][i] = SibRec8{w.y_state[a + i], rp == NONE ? SibLds8::N8 : (uint8_t)(rp - a), 0, SibLds8::N8, SibLds8::N8,
+                          SibLds8::N8, SibLds8::N8, SibLds8::N8, 0};
+      rr[t][i] = rp == NONE ? w.y_before[a + i] : NONE;
+      st[t][i] = 0;
+    }
+    // right-origin group anchors (sib_anchors_small): the sibling itself, else the first member
+    // with the same outside right origin
+    for (uint32_t i = 0; i < n; ++i) {
+      if (rec[t][i].rpos != SibLds8::N8) { rec[t][i].trep = rec[t][i].rpos; continue; }
+      uint32_t j = 0;
+      while (j < i && !(rec[t][j].rpos == SibLds8::N8 && rr[t][j] == rr[t][i])) ++j;
+      rec[t][i].trep = (uint8_t)(j | SibLds8::OUT8);
+    }
+    SibLds8 acc{rec[t], st[t]};
+    head = sib_loop(acc, n, rr[t], &w.ctr->err);  // (the anchors are set: rr is the stack now)
   }
   sib_publish(w, a, n, nsegs, head);
   for (uint32_t i = 0; i < n; ++i) {
-    const uint32_t x = n == 1 ? NONE : w.t_next[a + i];
-    w.t_nsib[w.t_seg[a + i]] = x == NONE ? NONE : w.t_seg[x];
+    const uint32_t x = n == 1 ? SibLds8::N8 : rec[t][i].nxt;
+    w.t_nsib[w.t_seg[a + i]] = x == SibLds8::N8 ? NONE : w.t_seg[a + x];
   }
 }
 // one workgroup per large group: anchors of outside right origins through an LDS hash table,
@@ -505,41 +554,35 @@ __device__ __forceinline__ uint32_t block_excl_scan256(uint32_t v, uint32_t* sh,
 // finds its anchor with a shuffle scan (the lowest member with the same outside right origin).
 // The loop runs on the whole wavefront in position form (sib_wave).
 constexpr uint32_t TWAVE = 64;
-__device__ __forceinline__ int wave_max_i32(int v) {
-#pragma unroll
-  for (int o = 32; o >= 1; o >>= 1) v = max(v, __shfl_xor(v, o, 64));
-  return v;
-}
-__device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) {
-#pragma unroll
-  for (int o = 32; o >= 1; o >>= 1) v = min(v, (uint32_t)__shfl_xor((int)v, o, 64));
-  return v;
-}
-// The B.1 loop of sib_loop, evaluated by the whole wavefront (lane = member, n <= 64) over list
-// POSITIONS instead of lane 0 walking linked lists (scripts/sib_wave_proto.py checks the two forms
-// equal, ties and right-origin cycles included). The members are placed in sib_loop's order (by
-// index, each right-origin sibling first); every lane keeps its position in the list built so far
-// and when it was placed. Placing c:
-//   succ = the placed member of c's right-origin group (gk) with the smallest client above c's —
-//          lanes are in client order, so the lowest such lane (ties: the one placed first);
+// The B.1 loop of sib_loop, evaluated by the whole wavefront (lane = member, n <= 64) with the
+// list kept in POSITION space instead of lane 0 walking linked lists (scripts/sib_wave_proto.py
+// checks the forms equal, ties and right-origin cycles included). Member-space registers (lane =
+// member): done, pos, the stack; position-space registers (lane = list position x): the client,
+// right-origin group and member at x. Members are placed in sib_loop's order (by index, each
+// right-origin sibling first). Placing c:
+//   succ = the first position holding a member of c's right-origin group with a client above c's
+//          (a group's members stand in ascending client order, equal clients in placement order);
 //   stop = succ, else c's right-origin sibling, else the end;
-//   left = the largest position before stop held by a placed member of a lower client;
-//   c takes the position after left, every position at or past it moves up by one.
-// Each step is a few ballots, shuffles and one max reduction: no dependent LDS walks. Returns the
-// first member (NONE on a right-origin cycle, reported as ERR_DECODE); pos is the lane's final
-// position.
-__device__ uint32_t sib_wave(uint32_t n, uint32_t lane, uint32_t cid, uint32_t rp, uint32_t gk, int& pos, uint32_t* err) {
-  uint32_t done = 0, seq = 0, stk = 0, placed = 0;
+//   left = the last position before stop holding a client below c's;
+//   c goes after left: the position-space entries at or past it shift up one lane.
+// A step is two ballots, three lane shifts and readlanes of wave-uniform indices. Returns the
+// first member (NONE on a right-origin cycle, reported as ERR_DECODE); pos = the lane's member's
+// final position, pm = the member at the lane's position.
+__device__ __forceinline__ uint32_t rdlane(uint32_t v, uint32_t i) { return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)i); }
+__device__ uint32_t sib_wave(uint32_t n, uint32_t lane, uint32_t cid, uint32_t rp, uint32_t gk, int& pos, uint32_t& pm, uint32_t* err) {
+  uint32_t done = 0, stk = 0, placed = 0;
+  uint32_t pc = 0, pg = 0xFFFFFFFFu;
   pos = -1;
+  pm = NONE;
   for (uint32_t i0 = 0; i0 < n; ++i0) {
-    if ((uint32_t)__shfl((int)done, (int)i0, 64) == 2u) continue;
+    if (rdlane(done, i0) == 2u) continue;
     if (lane == i0) done = 1;
     if (lane == 0) stk = i0;
     uint32_t sp = 1, c = i0;
     while (sp > 0) {
-      const uint32_t r = (uint32_t)__shfl((int)rp, (int)c, 64);
+      const uint32_t r = rdlane(rp, c);
       if (r != NONE) {
-        const uint32_t dr = (uint32_t)__shfl((int)done, (int)r, 64);
+        const uint32_t dr = rdlane(done, r);
         if (dr != 2u) {  // the right origin is a sibling: place it first
           if (dr == 1u || sp >= n) { if (lane == 0) raise_err(err, ERR_DECODE); return NONE; }
           if (lane == r) done = 1;
@@ -549,31 +592,25 @@ __device__ uint32_t sib_wave(uint32_t n, uint32_t lane, uint32_t cid, uint32_t r
           continue;
         }
       }
-      const uint32_t cc = (uint32_t)__shfl((int)cid, (int)c, 64), g = (uint32_t)__shfl((int)gk, (int)c, 64);
-      const bool pl = done == 2u;
-      const uint64_t cand = __ballot(pl && gk == g && cid > cc);
-      uint32_t stop = r;
-      if (cand) {
-        stop = (uint32_t)__ffsll((long long)cand) - 1;
-        const uint32_t cs = (uint32_t)__shfl((int)cid, (int)stop, 64);
-        const uint64_t ties = cand & __ballot(cid == cs);
-        if (ties & (ties - 1)) {  // one client twice in one group (never from Yjs): the first placed
-          const uint32_t m = wave_min_u32(((ties >> lane) & 1ull) ? seq : 0xFFFFFFFFu);
-          stop = (uint32_t)__ffsll((long long)(ties & __ballot(seq == m))) - 1;
-        }
-      }
-      const int pstop = stop != NONE ? __shfl(pos, (int)stop, 64) : (int)placed;
-      const int p = wave_max_i32(pl && pos < pstop && cid < cc ? pos : -1) + 1;
-      if (pl && pos >= p) ++pos;
-      if (lane == c) { pos = p; seq = placed; done = 2; }
+      const uint32_t cc = rdlane(cid, c), g = rdlane(gk, c);
+      const bool live = lane < placed;
+      const uint64_t sm = __ballot(live && pg == g && pc > cc);
+      const uint32_t pstop = sm ? (uint32_t)__ffsll((long long)sm) - 1 : r != NONE ? (uint32_t)rdlane((uint32_t)pos, r) : placed;
+      const uint64_t lm = __ballot(live && lane < pstop && pc < cc);
+      const uint32_t p = lm ? 64u - (uint32_t)__clzll((long long)lm) : 0u;  // past the last such position
+      if (done == 2u && pos >= (int)p) ++pos;
+      const uint32_t upc = (uint32_t)__shfl_up((int)pc, 1, 64), upg = (uint32_t)__shfl_up((int)pg, 1, 64),
+                     upm = (uint32_t)__shfl_up((int)pm, 1, 64);
+      if (lane > p) { pc = upc; pg = upg; pm = upm; }
+      else if (lane == p) { pc = cc; pg = g; pm = c; }
+      if (lane == c) { pos = (int)p; done = 2; }
       ++placed;
-      if (--sp > 0) c = (uint32_t)__shfl((int)stk, (int)(sp - 1), 64);
+      if (--sp > 0) c = rdlane(stk, sp - 1);
     }
   }
-  return (uint32_t)__ffsll((long long)__ballot(pos == 0)) - 1;
+  return n ? rdlane(pm, 0) : NONE;
 }
 __global__ __launch_bounds__(256) void k_tsib_wave(Work w, uint32_t nsegs, uint32_t nbig) {
-  __shared__ uint8_t ord[4][TWAVE];
   const uint32_t wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const uint32_t bi = blockIdx.x * 4 + wv;
   if (bi >= nbig) return;  // whole wavefronts only: no workgroup barrier below
@@ -587,24 +624,19 @@ __global__ __launch_bounds__(256) void k_tsib_wave(Work w, uint32_t nsegs, uint3
   const uint32_t rk = !in || rp != NONE ? NONE : r0 == NONE ? HNONE : r0;  // (units < HNONE)
   uint32_t anc = NONE;
   for (uint32_t j = 0; j < n; ++j) {
-    const uint32_t rj = __shfl(rk, j);
+    const uint32_t rj = rdlane(rk, j);
     if (anc == NONE && rk != NONE && rj == rk) anc = j;
   }
-  if (in) w.t_trep[a + lane] = rp != NONE ? rp : (a + anc) | 0x80000000u;
   // right-origin group: the sibling (local index), or 64 + the anchor of an outside right origin
   const uint32_t lrp = rp != NONE ? rp - a : NONE;
   const uint32_t gk = !in ? 0xFFFFu : lrp != NONE ? lrp : TWAVE + anc;
   int pos;
-  const uint32_t head = sib_wave(n, lane, in ? cid : 0xFFFFFFFFu, in ? lrp : NONE, gk, pos, &w.ctr->err);
+  uint32_t pm;
+  const uint32_t head = sib_wave(n, lane, in ? cid : 0xFFFFFFFFu, in ? lrp : NONE, gk, pos, pm, &w.ctr->err);
   if (head == NONE) return;
-  if (in) ord[wv][pos] = (uint8_t)lane;
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-  if (in) {
-    const uint32_t x = pos + 1 < (int)n ? ord[wv][pos + 1] : NONE;
-    w.t_nsib[w.t_seg[a + lane]] = x == NONE ? NONE : w.t_seg[a + x];
-  }
+  const uint32_t x = (uint32_t)__shfl((int)pm, (pos + 1) & 63, 64);  // the member after this one
+  const uint32_t sx = in && pos + 1 < (int)n ? w.t_seg[a + x] : NONE;
+  if (in) w.t_nsib[w.t_seg[a + lane]] = sx;
   if (lane == 0) sib_publish(w, a, n, nsegs, head);
 }
 
@@ -956,61 +988,63 @@ void launch_tsib_huge(const Work& w, uint32_t a, uint32_t n, uint32_t nsegs, hip
 // (Wyllie): every array segment holds (ans, nxt) — ans its answer once known, nxt the next ancestor
 // to look at — and a round replaces an open pair by its nxt's pair: ans = ans[nxt], nxt =
 // nxt[nxt] while that is still open. The distance to the answer halves every round, so a path of
-// d only-children closes in ceil(log2 d) rounds; each round is a coalesced pass (double-buffered,
-// no races), where the lane-serial climb with path halving it replaces walked C3's long push
-// chains at memory latency (4.7 ms). A round launched after the last open pair closed returns at
-// once (its predecessor's "open" word is zero).
+// d only-children closes in at most ceil(log2 d) rounds; each round is a coalesced pass, where the
+// lane-serial climb with path halving it replaces walked C3's long push chains at memory latency
+// (4.7 ms). A round launched after the last open pair closed returns at once (its predecessor's
+// "open" word is zero).
 constexpr uint32_t CLIMB_ROUNDS = 34;  // > log2 of any segment count, +1 (<= Counters::climb_open)
-__global__ __launch_bounds__(256) void k_tclimb_init(Work w, uint32_t nsegs, uint32_t* __restrict__ ans, uint32_t* __restrict__ nxt,
-                                                     uint32_t* __restrict__ open) {
+// The (answer, next) pair of a segment is one 64-bit word, jumped IN PLACE: a segment's word is
+// written only by its own lane, with one 8-byte store, and a lane reading its next's word (one
+// 8-byte load) sees either its old or its new pair — both states of the same climb — so a round
+// only ever moves a pair further up its chain and no second buffer (nor a copy round) is needed.
+// Closed pairs are read and skipped. A fixed grid strides over the segments: a round launched
+// after convergence is a few thousand workgroups that read one word and return (one workgroup per
+// 256 segments, C4's 27 such rounds cost 70 us each in dispatch alone).
+__global__ __launch_bounds__(256) void k_tclimb_init(Work w, uint32_t nsegs, uint2* __restrict__ cl, uint32_t* __restrict__ open) {
   const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
   if (s < CLIMB_ROUNDS) open[s] = 0;  // the per-round "pairs still open" words
   if (s >= nsegs) return;
   const bool arr = (w.g_flags[s] & SEG_ARRAY) != 0;
   const uint32_t ns = arr ? w.t_nsib[s] : NONE;
-  ans[s] = ns;
-  nxt[s] = arr && ns == NONE ? w.t_jump[s] : NONE;  // the parent (NONE: a child of the list's root)
+  cl[s] = make_uint2(ns, arr && ns == NONE ? w.t_jump[s] : NONE);  // next: the parent (NONE: a child of the list's root)
 }
-__global__ __launch_bounds__(256) void k_tclimb_round(uint32_t nsegs, const uint32_t* __restrict__ ans0, const uint32_t* __restrict__ nxt0,
-                                                      uint32_t* __restrict__ ans1, uint32_t* __restrict__ nxt1, uint32_t* __restrict__ open,
-                                                      uint32_t round) {
-  const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
-  if (round > 0 && __hip_atomic_load(&open[round - 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) {
-    // converged: the first round after it copies the final pairs into the other buffer (the
-    // buffers keep alternating), the later ones return at once
-    if (round >= 2 && __hip_atomic_load(&open[round - 2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) return;
-    if (s < nsegs) { ans1[s] = ans0[s]; nxt1[s] = nxt0[s]; }
-    return;
+constexpr uint32_t CLIMB_GRID = 4096;
+__global__ __launch_bounds__(256) void k_tclimb_round(uint32_t nsegs, uint2* __restrict__ cl, uint32_t* __restrict__ open, uint32_t round) {
+  if (round > 0 && __hip_atomic_load(&open[round - 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) return;  // converged
+  const uint32_t stride = gridDim.x * blockDim.x;
+  // (the pair is read and written as ONE 64-bit atomic: as a uint2 the compiler split the read of
+  // the next's pair into two 32-bit loads, and a torn (old answer, new next) pair closed a climb
+  // with no answer)
+  unsigned long long* w64 = (unsigned long long*)cl;
+  bool any_open = false;
+  for (uint32_t s = blockIdx.x * blockDim.x + threadIdx.x; s < nsegs; s += stride) {
+    const unsigned long long v = __hip_atomic_load(&w64[s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint32_t vn = (uint32_t)(v >> 32);
+    if (vn == NONE) continue;  // closed (ans == the answer)
+    const unsigned long long u = __hip_atomic_load(&w64[vn], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint32_t ua = (uint32_t)u, un = (uint32_t)(u >> 32);
+    const unsigned long long nv = ua != NONE ? ((unsigned long long)NONE << 32) | ua : ((unsigned long long)un << 32) | NONE;
+    __hip_atomic_store(&w64[s], nv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    any_open |= ua == NONE && un != NONE;
   }
-  if (s >= nsegs) return;
-  uint32_t a = ans0[s], n = nxt0[s];
-  if (n != NONE) {  // open: a == NONE
-    a = ans0[n];
-    n = a != NONE ? NONE : nxt0[n];
-  }
-  ans1[s] = a;
-  nxt1[s] = n;
-  wave_flag(&open[round], n != NONE);
+  wave_flag(&open[round], any_open);
 }
-__global__ __launch_bounds__(256) void k_tclimb_done(Work w, uint32_t nsegs, const uint32_t* __restrict__ ans, const uint32_t* __restrict__ nxt,
-                                                     const uint32_t* __restrict__ open) {
+__global__ __launch_bounds__(256) void k_tclimb_done(Work w, uint32_t nsegs, const uint2* __restrict__ cl, const uint32_t* __restrict__ open) {
   const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
   if (s == 0 && open[CLIMB_ROUNDS - 1]) raise_err(&w.ctr->err, ERR_DECODE);  // still open: an origin cycle
   if (s >= nsegs || !(w.g_flags[s] & SEG_ARRAY)) return;
   const uint32_t fc = w.t_first[s];
-  w.g_right[s] = fc != NONE ? fc : ans[s];
+  w.g_right[s] = fc != NONE ? fc : cl[s].x;
 }
 void launch_tclimb(const Work& w, uint32_t nsegs, hipStream_t s) {
   const uint32_t grid = nsegs / 256 + 1;
-  // two (ans, nxt) buffers: the sibling-loop scratch is free once the groups are ordered
-  uint32_t *A0 = w.t_prv, *N0 = w.t_mprv, *A1 = w.t_mtail, *N1 = w.t_otail, *open = w.ctr->climb_open;
-  hipLaunchKernelGGL(k_tclimb_init, dim3(grid), dim3(256), 0, s, w, nsegs, A0, N0, open);
-  for (uint32_t r = 0; r < CLIMB_ROUNDS; ++r) {
-    hipLaunchKernelGGL(k_tclimb_round, dim3(grid), dim3(256), 0, s, nsegs, A0, N0, A1, N1, open, r);
-    std::swap(A0, A1);
-    std::swap(N0, N1);
-  }
-  hipLaunchKernelGGL(k_tclimb_done, dim3(grid), dim3(256), 0, s, w, nsegs, A0, N0, open);
+  // the pairs live in the anchor-hash scratch (2 NS + 4 words), free once the groups are ordered
+  uint2* cl = (uint2*)w.t_hkey;
+  uint32_t* open = w.ctr->climb_open;
+  hipLaunchKernelGGL(k_tclimb_init, dim3(grid), dim3(256), 0, s, w, nsegs, cl, open);
+  const uint32_t rgrid = std::min<uint32_t>(grid, CLIMB_GRID);
+  for (uint32_t r = 0; r < CLIMB_ROUNDS; ++r) hipLaunchKernelGGL(k_tclimb_round, dim3(rgrid), dim3(256), 0, s, nsegs, cl, open, r);
+  hipLaunchKernelGGL(k_tclimb_done, dim3(grid), dim3(256), 0, s, w, nsegs, cl, open);
 }
 
 uint32_t launch_yata_tree(const Work& w, uint32_t nsegs, hipStream_t s) {
@@ -1022,7 +1056,7 @@ uint32_t launch_yata_tree(const Work& w, uint32_t nsegs, hipStream_t s) {
   hipMemsetAsync(&w.ctr->tbig, 0, sizeof(uint32_t), s);
   hipLaunchKernelGGL(k_tgroup_starts, dim3(grid), dim3(256), 0, s, w, nsegs);
   hipLaunchKernelGGL(k_tprep, dim3(grid), dim3(256), 0, s, w, nsegs);
-  hipLaunchKernelGGL(k_tsib_small, dim3(grid), dim3(256), 0, s, w, nsegs);
+  hipLaunchKernelGGL(k_tsib_small, dim3(nsegs / TS_BLOCK + 1), dim3(TS_BLOCK), 0, s, w, nsegs);
   uint32_t nbig = 0;
   hipMemcpyAsync(&nbig, &w.ctr->tbig, sizeof(uint32_t), hipMemcpyDeviceToHost, s);
   hipStreamSynchronize(s);
@@ -1042,10 +1076,12 @@ uint32_t launch_yata_tree(const Work& w, uint32_t nsegs, hipStream_t s) {
   return nbig;
 }
 
-uint32_t launch_yata(const Work& w, uint32_t nsegs, uint32_t narray, uint32_t nclients, hipStream_t s) {
+// The YArray lists numbered (members sorted by (list, segment), y_lstart): the view's list table
+// and the sequential kernels' work list. The parallel tree path does not need it, so a merge
+// without a view skips it (one sort and a host sync: 1.4 ms of C4's merge).
+uint32_t launch_ylists(const Work& w, uint32_t nsegs, hipStream_t s) {
   if (!nsegs) return 0;
   const uint32_t grid = nsegs / 256 + 1;
-  if (!narray) return 0;  // g_right is only read for YArray members (merge predicate, view)
   hipLaunchKernelGGL(k_ykey, dim3(grid), dim3(256), 0, s, w, nsegs);
   sort_pairs_u32(w.tmp, w.tmp_bytes, w.y_key, w.y_keys, w.y_iota, w.y_seg, nsegs, s);
   hipLaunchKernelGGL(k_ylist_flags, dim3(grid), dim3(256), 0, s, w, nsegs);
@@ -1053,13 +1089,25 @@ uint32_t launch_yata(const Work& w, uint32_t nsegs, uint32_t narray, uint32_t nc
   uint32_t nlists = 0;
   hipMemcpyAsync(&nlists, w.y_confl + nsegs, sizeof(uint32_t), hipMemcpyDeviceToHost, s);
   hipStreamSynchronize(s);
-  if (!nlists) return 0;
-  hipLaunchKernelGGL(k_ylist_starts, dim3(grid), dim3(256), 0, s, w, nsegs);
+  if (nlists) hipLaunchKernelGGL(k_ylist_starts, dim3(grid), dim3(256), 0, s, w, nsegs);
+  return nlists;
+}
+
+// Returns the list count, or LISTS_UNNUMBERED when the tree path ran without numbering them
+// (launch_ylists, when a view asks).
+uint32_t launch_yata(const Work& w, uint32_t nsegs, uint32_t narray, uint32_t nclients, hipStream_t s) {
+  if (!nsegs) return 0;
+  if (!narray) return 0;  // g_right is only read for YArray members (merge predicate, view)
+  hipLaunchKernelGGL(k_yinit, dim3(nsegs / 256 + 1), dim3(256), 0, s, w, nsegs);
   static const bool seq = getenv("YCRDT_YATA") && !strcmp(getenv("YCRDT_YATA"), "seq");
   if (!seq && (uint64_t)nsegs * 5 < 0xFFFFFFF0ull) {  // sibling keys NS + list slot stay below NONE
+    static const bool eager = getenv("YCRDT_YLISTS_EAGER") && getenv("YCRDT_YLISTS_EAGER")[0] == '1';
+    const uint32_t nl = eager ? launch_ylists(w, nsegs, s) : LISTS_UNNUMBERED;
     launch_yata_tree(w, nsegs, s);
-    return nlists;
+    return nl;
   }
+  const uint32_t nlists = launch_ylists(w, nsegs, s);
+  if (!nlists) return 0;
   hipMemsetAsync(w.y_before, 0, sizeof(uint32_t) * (nsegs + 1), s);  // stamps: 0 is never issued
   hipMemsetAsync(w.y_confl, 0, sizeof(uint32_t) * (nsegs + 1), s);
   if (nclients < 16384 && !getenv("YCRDT_YATA_GLOBAL")) {  // client index in 14 bits

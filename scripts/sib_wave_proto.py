@@ -136,6 +136,58 @@ def sib_positions(cid, rp, anc):
     return order
 
 
+def sib_positions_space(cid, rp, anc):
+    """The same loop with the list held in POSITION space (what k_tsib_wave keeps in its lanes):
+    P_cid / P_gk / P_mem at list position x. succ = the first position of c's group whose client is
+    above c's (a group's members stand in ascending client order, equal clients in placement
+    order); left = the last position before stop whose client is below c's; inserting shifts the
+    positions at or past it up by one."""
+    n = len(cid)
+    done = [0] * n
+    pos = [None] * n
+    P_cid, P_gk, P_mem = [], [], []
+    for i0 in range(n):
+        if done[i0] == 2:
+            continue
+        stack = [i0]
+        done[i0] = 1
+        c = i0
+        while stack:
+            r = rp[c]
+            if r is not NONE and done[r] != 2:
+                if done[r] == 1 or len(stack) >= n:
+                    return "error"
+                done[r] = 1
+                stack.append(r)
+                c = r
+                continue
+            cc = cid[c]
+            succ = NONE
+            for x in range(len(P_cid)):
+                if P_gk[x] == anc[c] and P_cid[x] > cc:
+                    succ = P_mem[x]
+                    break
+            stop = succ if succ is not NONE else r
+            pstop = pos[stop] if stop is not NONE else len(P_cid)
+            p = 0
+            for x in range(pstop - 1, -1, -1):
+                if P_cid[x] < cc:
+                    p = x + 1
+                    break
+            for j in range(n):
+                if done[j] == 2 and pos[j] >= p:
+                    pos[j] += 1
+            P_cid.insert(p, cc)
+            P_gk.insert(p, anc[c])
+            P_mem.insert(p, c)
+            pos[c] = p
+            done[c] = 2
+            stack.pop()
+            if stack:
+                c = stack[-1]
+    return P_mem
+
+
 def random_group(rng, n):
     nclients = rng.randint(1, n)
     cid = sorted(rng.randrange(nclients) for _ in range(n))
@@ -171,8 +223,9 @@ def main():
         cid, rp, anc = random_group(rng, n)
         a = sib_loop(cid, rp, anc)
         b = sib_positions(cid, rp, anc)
-        if a != b:
-            print("MISMATCH", t, n, cid, rp, anc, a, b)
+        c = sib_positions_space(cid, rp, anc)
+        if a != b or a != c:
+            print("MISMATCH", t, n, cid, rp, anc, a, b, c)
             return 1
         errs += a == "error"
     print(f"ok: {trials} groups, {errs} with right-origin cycles (both report them)")
