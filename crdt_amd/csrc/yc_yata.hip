@@ -289,11 +289,10 @@ __global__ void k_tkey(Work w, uint32_t nsegs) {
   }
   w.t_key[s] = key;
   w.y_key[s] = rs;  // the right-origin segment, for k_tprep (y_key is free until launch_ylists)
-  w.t_first[s] = NONE;
-  w.t_nsib[s] = NONE;
+  w.t_first[s] = NONE;  // (t_nsib: every member's group writes it)
   w.t_jump[s] = p;
 }
-// group starts: t_done = flags, t_next = their exclusive scan (both re-initialised afterwards)
+// group starts: t_done = flags, t_next = their exclusive scan (re-initialised by the groups that use them: sib_state_init)
 __global__ void k_tgroup_flags(Work w, uint32_t nsegs) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i > nsegs) return;
@@ -315,12 +314,6 @@ __global__ void k_tgroup_starts(Work w, uint32_t nsegs) {
 __global__ void k_tprep(Work w, uint32_t nsegs) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= nsegs) return;
-  w.t_done[i] = 0;
-  w.t_next[i] = NONE;
-  w.t_prv[i] = NONE;
-  w.t_mprv[i] = NONE;
-  w.t_mtail[i] = NONE;
-  w.t_otail[i] = NONE;
   const uint32_t k = w.t_keys[i];
   if (k == NONE) return;
   const uint32_t s = w.t_seg[i];
@@ -330,6 +323,22 @@ __global__ void k_tprep(Work w, uint32_t nsegs) {
   w.y_state[i] = w.g_cidx[s];
   w.y_before[i] = rs;  // the anchor key: a right-origin unit starts its segment (k_refs), so unit and segment name it alike
   w.y_confl[i] = rp;
+}
+
+// The global loop state of a group's members (t_done, t_next, t_prv, t_mprv, t_mtail, t_otail:
+// the in-place loop and the chain scratch of the big / huge groups): set by the group's own kernel
+// (the small and wavefront groups keep theirs in LDS / registers)
+__device__ __forceinline__ void sib_state_init(const Work& w, uint32_t i) {
+  w.t_done[i] = 0;
+  w.t_next[i] = NONE;
+  w.t_prv[i] = NONE;
+  w.t_mprv[i] = NONE;
+  w.t_mtail[i] = NONE;
+  w.t_otail[i] = NONE;
+}
+__global__ void k_thuge_init(Work w, uint32_t a, uint32_t n) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) sib_state_init(w, a + i);
 }
 
 // One sibling group (local indices 0..n-1 in ascending client order). The forward B.1 scan
@@ -648,6 +657,8 @@ __global__ __launch_bounds__(256) void k_tsib_big(Work w, uint32_t nsegs) {
   const uint32_t g = w.t_big[blockIdx.x];
   const uint32_t a = w.t_gstart[g], n = w.t_gstart[g + 1] - a;
   if (MID ? (n > CAP || n <= TWAVE) : (n <= TMID || n > CAP)) return;  // n > TLDS: the grid-wide huge-group path
+  for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) sib_state_init(w, a + i);
+  __syncthreads();  // (workgroup-scope: the stores are visible to the block's later reads)
   __shared__ SibRec rec[CAP];
   __shared__ uint8_t st[CAP];
   __shared__ uint32_t hkey[HS], hval[HS];
@@ -973,6 +984,7 @@ void launch_tsib_huge(const Work& w, uint32_t a, uint32_t n, uint32_t nsegs, hip
   while (P < n + n / 2 + 1 && 2ull * P <= 2ull * nsegs + 4) P <<= 1;
   fill_u32_multi({{w.t_hkey, P, NONE}, {w.t_hval, P, NONE}}, s);
   const uint32_t grid = n / 256 + 1;
+  hipLaunchKernelGGL(k_thuge_init, dim3(grid), dim3(256), 0, s, w, a, n);
   hipLaunchKernelGGL(k_thuge_hash, dim3(grid), dim3(256), 0, s, w, a, n, P);
   hipLaunchKernelGGL(k_thuge_anchor, dim3(grid), dim3(256), 0, s, w, a, n, P);
   hipLaunchKernelGGL(k_thuge_flags, dim3(grid), dim3(256), 0, s, w, a, n);
