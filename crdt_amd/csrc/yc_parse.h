@@ -552,15 +552,11 @@ YC_HD inline int parse_struct(const Src& b, uint32_t& p, uint32_t end, uint32_t 
         } else if (p < end && steps > 0 && (tag == 117u || tag == 118u) && any_flat<FULL>(b, p, end, steps, ok, cf)) {
           // (a one-level container of scalars, inline)
         } else {
-#ifdef YC_AB_NO_DEEP  // (A/B experiment builds only: no out-of-line reader)
-          ok = false; steps = 0;
-#else
           const AnySkip r = skip_any_nl<DEPTH, FULL>(b.b, p, end, steps);
           p = r.p;
           steps = r.steps;
           ok = r.ok != 0;
           cf |= r.cf;
-#endif
         }
       }
       if (!ok && steps == 0) return -1;
@@ -571,15 +567,11 @@ YC_HD inline int parse_struct(const Src& b, uint32_t& p, uint32_t end, uint32_t 
     case REF_DOC: {
       skip_str<FULL>(b, p, end, ok);
       if (ok) {
-#ifdef YC_AB_NO_DEEP
-        ok = false; steps = 0;
-#else
         const AnySkip r = skip_any_nl<DEPTH, FULL>(b.b, p, end, steps);
         p = r.p;
         steps = r.steps;
         ok = r.ok != 0;
         if (FULL && ok && r.cf) return -1;  // a ContentDoc's options not in writeAny's form: refused
-#endif
       }
       if (!ok && steps == 0) return -1;
       break;
