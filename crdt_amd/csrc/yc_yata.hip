@@ -277,10 +277,9 @@ __global__ void k_tkey(Work w, uint32_t nsegs) {
   if (w.g_flags[s] & SEG_ARRAY) {
     const uint32_t list = w.g_key[s];
     const uint32_t o = w.g_origin[s], r = w.g_rorigin[s];
-    if (o != NONE) {
-      p = seg_of_unit(w, o);
-      if (!(w.g_flags[p] & SEG_ARRAY) || w.g_key[p] != list) raise_err(&w.ctr->err, ERR_DECODE);  // outside the list
-    }
+    // (an origin is in the item's list by construction: k_resolve gave the item its origin's key;
+    // a right origin is only checked here)
+    if (o != NONE) p = seg_of_unit(w, o);
     if (r != NONE) {
       rs = seg_of_unit(w, r);
       if (!(w.g_flags[rs] & SEG_ARRAY) || w.g_key[rs] != list) raise_err(&w.ctr->err, ERR_DECODE);
@@ -502,29 +501,45 @@ __global__ __launch_bounds__(TS_BLOCK) void k_tsib_small(Work w, uint32_t nsegs)
   }
   const uint32_t t = threadIdx.x;
   uint32_t head = 0;
-  if (n > 1) {
+  const uint32_t gkey = w.t_keys[a];
+  if (n == 1) {  // (most groups: one child)
+    const uint32_t s0 = w.t_seg[a];
+    if (gkey < nsegs) w.t_first[gkey] = s0;
+    w.t_nsib[s0] = NONE;
+    return;
+  }
+  {
+    bool plain = true;  // (as in k_tsib_wave: one outside right origin, clients strictly ascending)
     for (uint32_t i = 0; i < n; ++i) {  // independent loads, issued together
       const uint32_t rp = w.y_confl[a + i];
       rec[t][i] = SibRec8{w.y_state[a + i], rp == NONE ? SibLds8::N8 : (uint8_t)(rp - a), 0, SibLds8::N8, SibLds8::N8,
                           SibLds8::N8, SibLds8::N8, SibLds8::N8, 0};
       rr[t][i] = rp == NONE ? w.y_before[a + i] : NONE;
       st[t][i] = 0;
+      plain = plain && rp == NONE && rr[t][i] == rr[t][0] && (i == 0 || rec[t][i].cid > rec[t][i - 1].cid);
     }
-    // right-origin group anchors (sib_anchors_small): the sibling itself, else the first member
-    // with the same outside right origin
-    for (uint32_t i = 0; i < n; ++i) {
-      if (rec[t][i].rpos != SibLds8::N8) { rec[t][i].trep = rec[t][i].rpos; continue; }
-      uint32_t j = 0;
-      while (j < i && !(rec[t][j].rpos == SibLds8::N8 && rr[t][j] == rr[t][i])) ++j;
-      rec[t][i].trep = (uint8_t)(j | SibLds8::OUT8);
+    if (plain) {
+      for (uint32_t i = 0; i < n; ++i) rec[t][i].nxt = i + 1 < n ? (uint8_t)(i + 1) : SibLds8::N8;
+      head = 0;
+    } else {
+      // right-origin group anchors (sib_anchors_small): the sibling itself, else the first member
+      // with the same outside right origin
+      for (uint32_t i = 0; i < n; ++i) {
+        if (rec[t][i].rpos != SibLds8::N8) { rec[t][i].trep = rec[t][i].rpos; continue; }
+        uint32_t j = 0;
+        while (j < i && !(rec[t][j].rpos == SibLds8::N8 && rr[t][j] == rr[t][i])) ++j;
+        rec[t][i].trep = (uint8_t)(j | SibLds8::OUT8);
+      }
+      SibLds8 acc{rec[t], st[t]};
+      head = sib_loop(acc, n, rr[t], &w.ctr->err);  // (the anchors are set: rr is the stack now)
     }
-    SibLds8 acc{rec[t], st[t]};
-    head = sib_loop(acc, n, rr[t], &w.ctr->err);  // (the anchors are set: rr is the stack now)
   }
-  sib_publish(w, a, n, nsegs, head);
+  if (head == NONE) return;  // (a right-origin cycle: reported)
+  for (uint32_t i = 0; i < n; ++i) rec[t][i].cid = w.t_seg[a + i];  // the members' segments (cid is done with)
+  if (gkey < nsegs) w.t_first[gkey] = rec[t][head].cid;  // (sib_publish)
   for (uint32_t i = 0; i < n; ++i) {
-    const uint32_t x = n == 1 ? SibLds8::N8 : rec[t][i].nxt;
-    w.t_nsib[w.t_seg[a + i]] = x == SibLds8::N8 ? NONE : w.t_seg[a + x];
+    const uint32_t x = rec[t][i].nxt;
+    w.t_nsib[rec[t][i].cid] = x == SibLds8::N8 ? NONE : rec[t][x].cid;
   }
 }
 // one workgroup per large group: anchors of outside right origins through an LDS hash table,
@@ -627,10 +642,13 @@ __global__ __launch_bounds__(256) void k_tsib_wave(Work w, uint32_t nsegs, uint3
   const uint32_t a = w.t_gstart[g], n = w.t_gstart[g + 1] - a;
   if (n > TWAVE) return;
   const bool in = lane < n;
+  // every load the group needs, in one round: the member's columns, its segment, the group key
   const uint32_t rp = in ? w.y_confl[a + lane] : NONE;
   const uint32_t cid = in ? w.y_state[a + lane] : 0u;
-  const uint32_t r0 = in && rp == NONE ? w.y_before[a + lane] : NONE;
-  const uint32_t rk = !in || rp != NONE ? NONE : r0 == NONE ? HNONE : r0;  // (units < HNONE)
+  const uint32_t r0 = in ? w.y_before[a + lane] : NONE;
+  const uint32_t segl = in ? w.t_seg[a + lane] : NONE;
+  const uint32_t gkey = w.t_keys[a];
+  const uint32_t rk = !in || rp != NONE ? NONE : r0 == NONE ? HNONE : r0;  // (segments < HNONE)
   uint32_t anc = NONE;
   for (uint32_t j = 0; j < n; ++j) {
     const uint32_t rj = rdlane(rk, j);
@@ -641,12 +659,25 @@ __global__ __launch_bounds__(256) void k_tsib_wave(Work w, uint32_t nsegs, uint3
   const uint32_t gk = !in ? 0xFFFFu : lrp != NONE ? lrp : TWAVE + anc;
   int pos;
   uint32_t pm;
-  const uint32_t head = sib_wave(n, lane, in ? cid : 0xFFFFFFFFu, in ? lrp : NONE, gk, pos, pm, &w.ctr->err);
-  if (head == NONE) return;
+  uint32_t head;
+  // the common group — every member's right origin the same outside unit (or none), clients
+  // strictly ascending (C4's list heads: concurrent pushes after one element) — is ordered by
+  // client: each newcomer goes to the end (no higher client is placed yet, no stop before it)
+  const uint32_t cprev = (uint32_t)__shfl_up((int)cid, 1, 64);
+  const bool plain = !__ballot(in && (rp != NONE || rk != rdlane(rk, 0) || (lane > 0 && cid <= cprev)));
+  if (plain) {
+    pos = in ? (int)lane : -1;
+    pm = lane;
+    head = 0;
+  } else {
+    head = sib_wave(n, lane, in ? cid : 0xFFFFFFFFu, in ? lrp : NONE, gk, pos, pm, &w.ctr->err);
+    if (head == NONE) return;
+  }
   const uint32_t x = (uint32_t)__shfl((int)pm, (pos + 1) & 63, 64);  // the member after this one
-  const uint32_t sx = in && pos + 1 < (int)n ? w.t_seg[a + x] : NONE;
-  if (in) w.t_nsib[w.t_seg[a + lane]] = sx;
-  if (lane == 0) sib_publish(w, a, n, nsegs, head);
+  const uint32_t sx = (uint32_t)__shfl((int)segl, (int)(x & 63), 64);  // ... and its segment
+  if (in) w.t_nsib[segl] = pos + 1 < (int)n ? sx : NONE;
+  const uint32_t hseg = rdlane(segl, head);
+  if (lane == 0 && gkey < nsegs) w.t_first[gkey] = hseg;  // (sib_publish, from registers)
 }
 
 // CAP: LDS capacity in members, HS: anchor hash slots. MID = the variant for groups of at most
@@ -1012,13 +1043,27 @@ constexpr uint32_t CLIMB_ROUNDS = 34;  // > log2 of any segment count, +1 (<= Co
 // Closed pairs are read and skipped. A fixed grid strides over the segments: a round launched
 // after convergence is a few thousand workgroups that read one word and return (one workgroup per
 // 256 segments, C4's 27 such rounds cost 70 us each in dispatch alone).
-__global__ __launch_bounds__(256) void k_tclimb_init(Work w, uint32_t nsegs, uint2* __restrict__ cl, uint32_t* __restrict__ open) {
-  const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
-  if (s < CLIMB_ROUNDS) open[s] = 0;  // the per-round "pairs still open" words
-  if (s >= nsegs) return;
+// The first round builds the pairs from the sibling links and jumps once: a segment's initial pair
+// is (next sibling, NONE), or (NONE, parent) without one (parent NONE: a child of the list's root);
+// its parent's initial pair comes from the same links (no separate init pass).
+__device__ __forceinline__ uint2 climb_pair0(const Work& w, uint32_t s) {
   const bool arr = (w.g_flags[s] & SEG_ARRAY) != 0;
   const uint32_t ns = arr ? w.t_nsib[s] : NONE;
-  cl[s] = make_uint2(ns, arr && ns == NONE ? w.t_jump[s] : NONE);  // next: the parent (NONE: a child of the list's root)
+  return make_uint2(ns, arr && ns == NONE ? w.t_jump[s] : NONE);
+}
+__global__ __launch_bounds__(256) void k_tclimb_first(Work w, uint32_t nsegs, uint2* __restrict__ cl, uint32_t* __restrict__ open) {
+  const uint32_t stride = gridDim.x * blockDim.x;
+  bool any_open = false;
+  for (uint32_t s = blockIdx.x * blockDim.x + threadIdx.x; s < nsegs; s += stride) {
+    uint2 v = climb_pair0(w, s);
+    if (v.y != NONE) {
+      const uint2 u = climb_pair0(w, v.y);
+      v = u.x != NONE ? make_uint2(u.x, NONE) : make_uint2(NONE, u.y);
+    }
+    cl[s] = v;
+    any_open |= v.y != NONE;
+  }
+  wave_flag(&open[0], any_open);
 }
 constexpr uint32_t CLIMB_GRID = 4096;
 __global__ __launch_bounds__(256) void k_tclimb_round(uint32_t nsegs, uint2* __restrict__ cl, uint32_t* __restrict__ open, uint32_t round) {
@@ -1053,9 +1098,10 @@ void launch_tclimb(const Work& w, uint32_t nsegs, hipStream_t s) {
   // the pairs live in the anchor-hash scratch (2 NS + 4 words), free once the groups are ordered
   uint2* cl = (uint2*)w.t_hkey;
   uint32_t* open = w.ctr->climb_open;
-  hipLaunchKernelGGL(k_tclimb_init, dim3(grid), dim3(256), 0, s, w, nsegs, cl, open);
   const uint32_t rgrid = std::min<uint32_t>(grid, CLIMB_GRID);
-  for (uint32_t r = 0; r < CLIMB_ROUNDS; ++r) hipLaunchKernelGGL(k_tclimb_round, dim3(rgrid), dim3(256), 0, s, nsegs, cl, open, r);
+  hipMemsetAsync(open, 0, sizeof(uint32_t) * CLIMB_ROUNDS, s);  // the per-round "pairs still open" words
+  hipLaunchKernelGGL(k_tclimb_first, dim3(rgrid), dim3(256), 0, s, w, nsegs, cl, open);
+  for (uint32_t r = 1; r < CLIMB_ROUNDS; ++r) hipLaunchKernelGGL(k_tclimb_round, dim3(rgrid), dim3(256), 0, s, nsegs, cl, open, r);
   hipLaunchKernelGGL(k_tclimb_done, dim3(grid), dim3(256), 0, s, w, nsegs, cl, open);
 }
 

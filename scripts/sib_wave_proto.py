@@ -228,7 +228,13 @@ def main():
             print("MISMATCH", t, n, cid, rp, anc, a, b, c)
             return 1
         errs += a == "error"
-    print(f"ok: {trials} groups, {errs} with right-origin cycles (both report them)")
+    # the kernels' shortcut: one outside right origin for every member and strictly ascending
+    # clients give the ascending order (no newcomer ever finds a higher client placed, or a stop)
+    for t in range(trials // 4):
+        n = rng.randint(1, 64)
+        cid = sorted(rng.sample(range(4 * n + 4), n))
+        assert sib_loop(cid, [NONE] * n, [("out", 0)] * n) == list(range(n))
+    print(f"ok: {trials} groups, {errs} with right-origin cycles (both report them); plain groups ascending")
     return 0
 
 
