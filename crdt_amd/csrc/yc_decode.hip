@@ -1154,8 +1154,10 @@ __global__ __launch_bounds__(64) void k_fastwalk(Work w) {
     const uint32_t j = base + lane;
     uint32_t cnt = 0;
     if (j < nch) {
-      const uint32_t cs = ustart + j * CH, ce = min(cs + CH, uend), a = j == 0 ? q : cs;
-      cnt = popc_range(spec, a, ce);
+      // (the chain positions of every chunk were counted grid-wide by k_chunk_counts; chunk 0
+      // from q on here)
+      if (j == 0) cnt = popc_range(spec, q, min(ustart + CH, uend));
+      else cnt = w.ccnt[c0 + j];
     }
     uint32_t incl = cnt;
     for (uint32_t off = 1; off < 64; off <<= 1) {
@@ -1201,6 +1203,16 @@ __global__ __launch_bounds__(64) void k_fastwalk(Work w) {
     w.ufail[u] = 2u;  // done: k_walk leaves the update alone
     if (w.dbg) atomicAdd(&w.dbg[0], 1ull);
   }
+}
+
+// Chain positions per chunk of the large updates (one lane per chunk, after the sync rounds): the
+// fast walk's search for the n-th position reads one count per chunk instead of popcounting the
+// chunk's words from one wavefront (C4: 15 K chunks per update, 16 words each)
+__global__ __launch_bounds__(256) void k_chunk_counts(Work w) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= w.ngroups) return;
+  const Group G = w.groups[i];
+  w.ccnt[i] = popc_range(win_words(w.spec_bits, upd_win(w, G.upd)), G.start, G.end);
 }
 
 // The chain-position words of the fast-walked updates past their first chunk, one lane per word
@@ -1538,6 +1550,7 @@ void launch_chunks(const Work& w, hipStream_t s) {
   if (w.nbig) {
     static const bool nofast = getenv("YCRDT_NO_FASTWALK") && getenv("YCRDT_NO_FASTWALK")[0] == '1';
     if (!nofast && !w.force_xtab) {
+      hipLaunchKernelGGL(k_chunk_counts, dim3(w.ngroups / 256 + 1), dim3(256), 0, s, w);
       hipLaunchKernelGGL(k_fastwalk, dim3(w.nbig), dim3(64), 0, s, w);
       hipLaunchKernelGGL(k_fastmark, dim3(std::min<uint64_t>((uint64_t)w.ngroups * (w.schunk / 64) / 256 + 1, 8192)), dim3(256), 0, s, w);
     }
@@ -1618,9 +1631,41 @@ __global__ void k_section_rank(Work w, uint32_t nsections) {
   sec->first_idx = rank_incl(fbits, win_words(w.wcnt, uw), p) - 1;
   w.sec_sorted[rank_incl(win_words(w.sec_bits, uw), win_words(w.wsec, uw), p) - 1] = i;
 }
+// Small batches: both popcount prefixes in one workgroup and one launch (four launches otherwise):
+// a lane sums the popcounts of a contiguous run of words, the run sums are scanned in LDS, each
+// lane writes its run's prefixes (n = nwords + 1 entries; the last is the total).
+constexpr uint32_t COUNT_LANES = 1024, COUNT_SMALL = COUNT_LANES * 16;
+__global__ __launch_bounds__(COUNT_LANES) void k_count_small(const uint64_t* __restrict__ b0, uint32_t* __restrict__ o0,
+                                                             const uint64_t* __restrict__ b1, uint32_t* __restrict__ o1, uint32_t nwords) {
+  __shared__ uint32_t part[COUNT_LANES];
+  const uint32_t t = threadIdx.x, n = nwords + 1, per = (n + COUNT_LANES - 1) / COUNT_LANES;
+  const uint32_t a = min(n, t * per), e = min(n, a + per);
+  for (int k = 0; k < 2; ++k) {
+    const uint64_t* bits = k ? b1 : b0;
+    uint32_t* out = k ? o1 : o0;
+    uint32_t sum = 0;
+    for (uint32_t i = a; i < e; ++i) sum += i < nwords ? (uint32_t)__popcll(bits[i]) : 0u;
+    part[t] = sum;
+    __syncthreads();
+    for (uint32_t off = 1; off < COUNT_LANES; off <<= 1) {
+      const uint32_t v = t >= off ? part[t - off] : 0u;
+      __syncthreads();
+      part[t] += v;
+      __syncthreads();
+    }
+    uint32_t run = part[t] - sum;
+    for (uint32_t i = a; i < e; ++i) { out[i] = run; run += i < nwords ? (uint32_t)__popcll(bits[i]) : 0u; }
+    __syncthreads();
+  }
+}
+
 // before the count sync: struct / section-start counts (popcount prefix of the bitmaps)
 void launch_struct_count(const Work& w, hipStream_t s) {
   const uint32_t nwords = (w.nbytes + 63) / 64;
+  if (nwords + 1 <= COUNT_SMALL) {
+    hipLaunchKernelGGL(k_count_small, dim3(1), dim3(COUNT_LANES), 0, s, w.final_bits, w.wcnt, w.sec_bits, w.wsec, nwords);
+    return;
+  }
   hipLaunchKernelGGL(k_popc, dim3(nwords / 256 + 1), dim3(256), 0, s, w.final_bits, w.scratch, nwords);
   scan_u32(w.tmp, w.tmp_bytes, w.scratch, w.wcnt, nwords + 1, s);
   hipLaunchKernelGGL(k_popc, dim3(nwords / 256 + 1), dim3(256), 0, s, w.sec_bits, w.scratch, nwords);

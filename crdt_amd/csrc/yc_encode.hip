@@ -348,7 +348,7 @@ __global__ void k_unreverse3(Work w, uint32_t nclients) {
   }
 }
 
-__global__ void k_totals(Work w, uint32_t nclients) {
+__device__ __forceinline__ void totals_body(const Work& w, uint32_t nclients) {
   const uint32_t nincl = w.ctr->pad[0], nds = w.ctr->pad[1], nsv = w.ctr->pad[2];
   const uint64_t sblk = ccol64(w, CC64_BLKPOS)[nclients];
   const uint64_t sds = ccol64(w, CC64_DSPOS)[nclients];
@@ -360,6 +360,7 @@ __global__ void k_totals(Work w, uint32_t nclients) {
   // the output buffers were sized from a bound before the sizes were known; never write past them
   if (w.ctr->out_total > w.cap_out || vu_size(nsv) + ssv > w.cap_sv) { w.ctr->pad[5] = 1; raise_err(&w.ctr->err, ERR_CAPACITY); }
 }
+__global__ void k_totals(Work w, uint32_t nclients) { totals_body(w, nclients); }
 
 __global__ __launch_bounds__(256) void k_write_structs(Work w, uint32_t nsegs, uint32_t nclients) {
   const uint32_t o = blockIdx.x * blockDim.x + threadIdx.x;
@@ -412,7 +413,48 @@ __global__ void k_write_runs(Work w, uint32_t nsegs) {
   wr_vu(w.out, p, w.r_len[r]);
 }
 
+// Small client tables (the per-op path, one document): the reverse, the three scans, the
+// unreverse and the totals in ONE workgroup and one launch (six launches otherwise). Each scan:
+// a lane sums a contiguous run of the emit-order sizes, the run sums are scanned in LDS, each lane
+// writes its run's prefixes into the scan column; then every client reads its slot's prefix.
+constexpr uint32_t LAYOUT_LANES = 1024, LAYOUT_SMALL = LAYOUT_LANES * 16;
+__global__ __launch_bounds__(LAYOUT_LANES) void k_layout_small(Work w, uint32_t nclients) {
+  __shared__ uint64_t part[LAYOUT_LANES];
+  const uint32_t t = threadIdx.x, n = nclients + 1, per = (n + LAYOUT_LANES - 1) / LAYOUT_LANES;
+  const uint32_t a = min(n, t * per), b = min(n, a + per);
+  const uint32_t src[3] = {CC_BLK, CC_DSBLK, CC_SV}, scol[3] = {CC64_SCAN, CC64_SCAN2, CC64_SCAN3};
+  for (int k = 0; k < 3; ++k) {
+    auto val = [&](uint32_t i) -> uint64_t { return i < nclients ? ccol(w, src[k])[emit_slot_client(w, nclients, k, i)] : 0u; };
+    uint64_t sum = 0;
+    for (uint32_t i = a; i < b; ++i) sum += val(i);
+    part[t] = sum;
+    __syncthreads();
+    for (uint32_t off = 1; off < LAYOUT_LANES; off <<= 1) {
+      const uint64_t v = t >= off ? part[t - off] : 0ull;
+      __syncthreads();
+      part[t] += v;
+      __syncthreads();
+    }
+    uint64_t run = part[t] - sum;
+    for (uint32_t i = a; i < b; ++i) { ccol64(w, scol[k])[i] = run; run += val(i); }
+    __syncthreads();
+  }
+  __threadfence_block();
+  const uint32_t dst[3] = {CC64_BLKPOS, CC64_DSPOS, CC64_SVPOS};
+  for (uint32_t c = t; c <= nclients; c += LAYOUT_LANES)
+    for (int k = 0; k < 3; ++k) {
+      const uint32_t slot = c == nclients ? nclients : (k > 0 && w.cl_emit) ? w.cl_slot[c] : nclients - 1 - c;
+      ccol64(w, dst[k])[c] = ccol64(w, scol[k])[slot];
+    }
+  __syncthreads();
+  if (t == 0) totals_body(w, nclients);  // (k_totals)
+}
+
 static void rev_scans(const Work& w, uint32_t nclients, hipStream_t s) {
+  if (nclients + 1 <= LAYOUT_SMALL) {  // (k_totals included)
+    hipLaunchKernelGGL(k_layout_small, dim3(1), dim3(LAYOUT_LANES), 0, s, w, nclients);
+    return;
+  }
   const uint32_t grid = nclients / 256 + 1;
   hipLaunchKernelGGL(k_reverse3, dim3(grid), dim3(256), 0, s, w, nclients);
   const uint32_t cols[3][2] = {{CC_REV, CC64_SCAN}, {CC_REV2, CC64_SCAN2}, {CC_REV3, CC64_SCAN3}};
@@ -448,8 +490,12 @@ void launch_encode_layout(const Work& w, uint32_t nsegs, uint32_t nclients, hipS
   hipStreamWaitEvent(s, ev_join, 0);
   hipLaunchKernelGGL(k_client_bounds, dim3(grid), dim3(256), 0, s, w, nclients, nsegs);
   hipLaunchKernelGGL(k_client_sizes, dim3(nclients / 256 + 1), dim3(256), 0, s, w, nclients, nsegs);
-  rev_scans(w, nclients, s);
-  hipLaunchKernelGGL(k_totals, dim3(1), dim3(1), 0, s, w, nclients);
+  if (nclients + 1 <= LAYOUT_SMALL) {
+    rev_scans(w, nclients, s);  // (with the totals)
+  } else {
+    rev_scans(w, nclients, s);
+    hipLaunchKernelGGL(k_totals, dim3(1), dim3(1), 0, s, w, nclients);
+  }
 }
 
 // Phase 2: write bytes (buffers sized from a bound, checked in k_totals)

@@ -176,7 +176,7 @@ enum Buf {
   B_UOWN, B_UFLAG, B_UMIN, B_UCUT, B_UWPRE,
   B_GSTART, B_GCIDX, B_GSRC, B_GFLAGS, B_GORIG, B_GRORIG, B_GLINK, B_GOSEG, B_GKEY, B_GMAXC, B_GNEXT, B_GOUTID, B_GTMP, B_GTMP2,
   B_KHASH, B_KROOT, B_KWIN, B_KPAR, B_KFLAG, B_SPK,
-  B_USEC, B_USECN, B_DBG, B_XTAB, B_UFAIL, B_FW, B_TENTRY, B_XLIST,
+  B_USEC, B_USECN, B_DBG, B_XTAB, B_UFAIL, B_FW, B_CCNT, B_TENTRY, B_XLIST,
   B_LZKEY, B_LZKEYS, B_LZIOTA, B_LZSEC, B_LZRSTART, B_LZPREV, B_LZFIRST, B_LZCAP, B_LZEVBASE, B_LZEVN, B_LZFLAG,
   B_LZLHI, B_LZLLO, B_EVKIND, B_EVSRC, B_EVCLOCK, B_EVLEN, B_EVSIZE, B_EVPOS, B_BLKSIZE, B_BLKPOS, B_SVC, B_SVK,
   B_DSMKEY, B_DSMKEYS, B_DSMLEN, B_DSMLENS, B_DSMEND, B_DSMMAX, B_DSMFLAG, B_DSMRID, B_DRCLIENT, B_DRCLOCK, B_DREND,
@@ -813,6 +813,7 @@ int run_decode(ycrdt_engine* e, ycrdt_batch* b, bool lazy, Decoded& D, bool gene
   w.xlist = take<uint32_t>(V, B_XLIST, (uint64_t)w.ngroups + 1, ok);
   w.ufail = take<uint32_t>(V, B_UFAIL, nu + 1, ok);
   w.fw = take<uint32_t>(V, B_FW, 2ull * nu + 2, ok);
+  w.ccnt = take<uint32_t>(V, B_CCNT, (uint64_t)w.ngroups + 1, ok);
   w.final_bits = take<uint64_t>(V, B_FINAL, nwords, ok);
   w.sec_bits = take<uint64_t>(V, B_SECB, nwords, ok);
   w.dsstart = take<uint32_t>(V, B_DSSTART, nu + 1, ok);

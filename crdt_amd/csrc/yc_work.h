@@ -103,6 +103,7 @@ struct Work {
   uint32_t* xtab = nullptr;        // [G x XK] locked updates only, per entry offset: count << 16 | exit - chunk end
   uint32_t* tentry = nullptr;      // [G] locked updates: true entry of a chunk the table walk did not parse
   uint32_t* xlist = nullptr;       // [G] the chunks of the locked updates (k_xtab / k_xmark work list)
+  uint32_t* ccnt = nullptr;        // [G] chain positions per chunk (k_chunk_counts, for the fast walk)
   uint32_t* fw = nullptr;          // [2 nupd] fast-walked updates: first chain position past the exact walk, end of the last struct
   uint32_t* ufail = nullptr;       // [nupd] 1: the speculative walk gave up (locked chain phases), tables next
   uint64_t* final_bits = nullptr;  // [B/64] verified struct starts

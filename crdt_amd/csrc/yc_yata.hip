@@ -315,6 +315,8 @@ __global__ void k_tprep(Work w, uint32_t nsegs) {
   if (i >= nsegs) return;
   const uint32_t k = w.t_keys[i];
   if (k == NONE) return;
+  // a one-member group (most of them) needs no loop state (t_done: k_tgroup_flags' start flags)
+  if (w.t_done[i] && (i + 1 == nsegs || w.t_keys[i + 1] != k)) return;
   const uint32_t s = w.t_seg[i];
   const uint32_t rs = w.y_key[s];  // (k_tkey)
   uint32_t rp = NONE;
@@ -351,8 +353,11 @@ __global__ void k_thuge_init(Work w, uint32_t a, uint32_t n) {
 // walks O(1) in practice (scripts/yata_tree_proto.py: 49 backward steps where the forward scans
 // take 151 k on the same groups, identical orders).
 constexpr uint32_t TOUT = 0x8000u;  // LDS trep flag (bit 31 in global memory): the anchor is the first member of an outside right origin
-template <class A>
-__device__ uint32_t sib_loop(A& a, uint32_t n, uint32_t* __restrict__ stack, uint32_t* err) {
+// (stack: global memory for the in-place groups, LDS for the staged ones — a pop reads the new
+// top back, and from global memory that read was a memory round trip per pop: C3's list-head loop
+// spent 2.6 ms on them)
+template <class A, class S>
+__device__ uint32_t sib_loop(A& a, uint32_t n, S* __restrict__ stack, uint32_t* err) {
   uint32_t head = NONE, tail = NONE;
   for (uint32_t i0 = 0; i0 < n; ++i0) {
     if (a.done(i0) == 2) continue;
@@ -688,10 +693,32 @@ __global__ __launch_bounds__(256) void k_tsib_big(Work w, uint32_t nsegs) {
   const uint32_t g = w.t_big[blockIdx.x];
   const uint32_t a = w.t_gstart[g], n = w.t_gstart[g + 1] - a;
   if (MID ? (n > CAP || n <= TWAVE) : (n <= TMID || n > CAP)) return;  // n > TLDS: the grid-wide huge-group path
+  // a plain group (k_tsib_wave: one outside right origin, strictly ascending clients) is in
+  // ascending order: no staging, no loop
+  __shared__ uint32_t notplain;
+  if (threadIdx.x == 0) notplain = 0;
+  __syncthreads();
+  {
+    const uint32_t r00 = w.y_before[a];
+    bool bad = false;
+    for (uint32_t i = threadIdx.x; i < n; i += blockDim.x)
+      bad |= w.y_confl[a + i] != NONE || w.y_before[a + i] != r00 || (i > 0 && w.y_state[a + i] <= w.y_state[a + i - 1]);
+    if (bad) notplain = 1;  // (plain stores of one value)
+  }
+  __syncthreads();
+  if (!notplain) {
+    for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) w.t_nsib[w.t_seg[a + i]] = i + 1 < n ? w.t_seg[a + i + 1] : NONE;
+    if (threadIdx.x == 0) {
+      const uint32_t key = w.t_keys[a];
+      if (key < nsegs) w.t_first[key] = w.t_seg[a];
+    }
+    return;
+  }
   for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) sib_state_init(w, a + i);
   __syncthreads();  // (workgroup-scope: the stores are visible to the block's later reads)
   __shared__ SibRec rec[CAP];
   __shared__ uint8_t st[CAP];
+  __shared__ uint16_t stk[CAP];  // the loop's stack (staged groups)
   __shared__ uint32_t hkey[HS], hval[HS];
   __shared__ uint32_t head_s, scan_sh[4];
   for (uint32_t i = threadIdx.x; i < HS; i += blockDim.x) { hkey[i] = NONE; hval[i] = NONE; }
@@ -812,7 +839,7 @@ __global__ __launch_bounds__(256) void k_tsib_big(Work w, uint32_t nsegs) {
     __syncthreads();
     if (threadIdx.x == 0) {
       SibLds acc{rec, st};
-      head_s = sib_loop(acc, nn, w.y_stack + a, &w.ctr->err);
+      head_s = sib_loop(acc, nn, stk, &w.ctr->err);
     }
     __syncthreads();
     // expand: node k spans positions nfirst[k] .. nfirst[k + 1] - 1, listed from the last down
@@ -856,7 +883,7 @@ __global__ __launch_bounds__(256) void k_tsib_big(Work w, uint32_t nsegs) {
     __syncthreads();
     if (threadIdx.x == 0) {
       SibLds acc{rec, st};
-      head_s = sib_loop(acc, n, w.y_stack + a, &w.ctr->err);
+      head_s = sib_loop(acc, n, stk, &w.ctr->err);
     }
     __syncthreads();
     for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) {
@@ -880,13 +907,18 @@ __global__ __launch_bounds__(256) void k_tsib_big(Work w, uint32_t nsegs) {
 // anchors, chain marks, chain numbering, the expansion — run grid-wide over the group, and only the
 // loop over the collapsed chains runs on one lane (with the chains in LDS). In one workgroup those
 // passes were latency-bound (C3's list head, 790 k members: ≈9.7 ms, of 16 ms of YATA).
-// Group descriptors: the host reads (start, size) of every big group after k_tsib_small.
+// Group descriptors: the host reads (start, size) of the huge groups (> TLDS members) — a count
+// and a short compacted list (copying a descriptor for every big group, 800 KB pageable on C4, took
+// 0.4 ms of host time between two kernels)
+constexpr uint32_t HUGE_DESC_MAX = 62;  // descriptors read with the count in one copy (more: a second copy)
 __global__ void k_tbig_desc(Work w, uint32_t nbig, uint32_t* __restrict__ desc) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= nbig) return;
-  const uint32_t g = w.t_big[i], a = w.t_gstart[g];
-  desc[2 * i] = a;
-  desc[2 * i + 1] = w.t_gstart[g + 1] - a;
+  const uint32_t g = w.t_big[i], a = w.t_gstart[g], n = w.t_gstart[g + 1] - a;
+  if (n <= TLDS) return;
+  const uint32_t k = atomicAdd(&desc[0], 1u);
+  desc[2 + 2 * k] = a;
+  desc[3 + 2 * k] = n;
 }
 // anchors: the first member of every outside right-origin unit (global open addressing, P slots)
 __global__ __launch_bounds__(256) void k_thuge_hash(Work w, uint32_t a, uint32_t n, uint32_t P) {
@@ -941,6 +973,7 @@ __global__ __launch_bounds__(256) void k_thuge_nodes(Work w, uint32_t a, uint32_
 __global__ __launch_bounds__(256) void k_thuge_loop(Work w, uint32_t a, uint32_t n) {
   __shared__ SibRec rec[TLDS];
   __shared__ uint8_t st[TLDS];
+  __shared__ uint16_t stk[TLDS];  // the loop's stack
   __shared__ uint32_t head_s;
   const uint32_t nn = w.t_flag[n + 1 + n];
   if (nn > TLDS) return;  // k_thuge_inplace
@@ -958,7 +991,7 @@ __global__ __launch_bounds__(256) void k_thuge_loop(Work w, uint32_t a, uint32_t
   __syncthreads();
   if (threadIdx.x == 0) {
     SibLds acc{rec, st};
-    head_s = sib_loop(acc, nn, w.y_stack + a, &w.ctr->err);
+    head_s = sib_loop(acc, nn, stk, &w.ctr->err);
     w.t_flag[2 * n + 2] = head_s;  // (read by the expansion)
   }
   __syncthreads();
@@ -1101,7 +1134,19 @@ void launch_tclimb(const Work& w, uint32_t nsegs, hipStream_t s) {
   const uint32_t rgrid = std::min<uint32_t>(grid, CLIMB_GRID);
   hipMemsetAsync(open, 0, sizeof(uint32_t) * CLIMB_ROUNDS, s);  // the per-round "pairs still open" words
   hipLaunchKernelGGL(k_tclimb_first, dim3(rgrid), dim3(256), 0, s, w, nsegs, cl, open);
-  for (uint32_t r = 1; r < CLIMB_ROUNDS; ++r) hipLaunchKernelGGL(k_tclimb_round, dim3(rgrid), dim3(256), 0, s, nsegs, cl, open, r);
+  // rounds in batches of CLIMB_BATCH, with a look at the last round's word between batches: the
+  // converged rounds of one long batch were launched faster than they ran (15 us of dispatch gap
+  // each, 0.4 ms per C4 merge), a look costs one synchronisation
+  constexpr uint32_t CLIMB_BATCH = 8;
+  for (uint32_t r = 1; r < CLIMB_ROUNDS;) {
+    const uint32_t r1 = std::min(r + CLIMB_BATCH, CLIMB_ROUNDS);
+    for (; r < r1; ++r) hipLaunchKernelGGL(k_tclimb_round, dim3(rgrid), dim3(256), 0, s, nsegs, cl, open, r);
+    if (r >= CLIMB_ROUNDS) break;
+    uint32_t still = 1;
+    hipMemcpyAsync(&still, &open[r - 1], sizeof(uint32_t), hipMemcpyDeviceToHost, s);
+    hipStreamSynchronize(s);
+    if (!still) break;
+  }
   hipLaunchKernelGGL(k_tclimb_done, dim3(grid), dim3(256), 0, s, w, nsegs, cl, open);
 }
 
@@ -1123,12 +1168,18 @@ uint32_t launch_yata_tree(const Work& w, uint32_t nsegs, hipStream_t s) {
     hipLaunchKernelGGL((k_tsib_big<TMID, 2048, true>), dim3(nbig), dim3(256), 0, s, w, nsegs);
     hipLaunchKernelGGL((k_tsib_big<TLDS, THASH, false>), dim3(nbig), dim3(256), 0, s, w, nsegs);
     // the huge groups (> TLDS members): their (start, size) to the host, then the grid-wide path
-    std::vector<uint32_t> desc(2 * (size_t)nbig);
+    std::vector<uint32_t> desc(2 + 2 * (size_t)HUGE_DESC_MAX);
+    hipMemsetAsync(w.t_hkey, 0, sizeof(uint32_t), s);
     hipLaunchKernelGGL(k_tbig_desc, dim3(nbig / 256 + 1), dim3(256), 0, s, w, nbig, w.t_hkey);
     hipMemcpyAsync(desc.data(), w.t_hkey, sizeof(uint32_t) * desc.size(), hipMemcpyDeviceToHost, s);
     hipStreamSynchronize(s);
-    for (uint32_t i = 0; i < nbig; ++i)
-      if (desc[2 * i + 1] > TLDS) launch_tsib_huge(w, desc[2 * i], desc[2 * i + 1], nsegs, s);
+    const uint32_t nhuge = desc[0];
+    if (nhuge > HUGE_DESC_MAX) {
+      desc.resize(2 + 2 * (size_t)nhuge);
+      hipMemcpy(desc.data(), w.t_hkey, sizeof(uint32_t) * desc.size(), hipMemcpyDeviceToHost);
+    }
+    // (t_hkey is the huge path's hash table: the descriptors are read before it runs)
+    for (uint32_t k = 0; k < nhuge; ++k) launch_tsib_huge(w, desc[2 + 2 * k], desc[3 + 2 * k], nsegs, s);
   }
   launch_tclimb(w, nsegs, s);
   return nbig;
