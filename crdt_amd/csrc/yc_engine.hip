@@ -1195,7 +1195,7 @@ int run_merge(ycrdt_engine* e, ycrdt_batch* b, const std::unordered_map<uint32_t
       mark(e, "merge.dead_types");
       if (D.nested) run_dead_keys(w, nsegs, s);  // only lists under a parent item can die with it
       mark(e, "merge.yata");
-      e->nlists = launch_yata(w, nsegs, narray, nclients, s);
+      e->nlists = launch_yata(w, nsegs, narray, nclients, s, e->side, e->side_fork, e->side_done);
       if (w.dbg && e->nlists && e->nlists != LISTS_UNNUMBERED) {
         unsigned long long h[3];
         HIPCHK(hipStreamSynchronize(s));

@@ -607,7 +607,8 @@ void launch_shard_export(const Work& w, uint32_t nsegs, const uint8_t* owner, ui
 void launch_merge_final(const Work& w, uint32_t nsegs, hipStream_t s);
 void run_dead_keys(const Work& w, uint32_t nsegs, hipStream_t s);
 constexpr uint32_t LISTS_UNNUMBERED = 0xFFFFFFFFu;  // launch_yata: lists exist, launch_ylists numbers them
-uint32_t launch_yata(const Work& w, uint32_t nsegs, uint32_t narray, uint32_t nclients, hipStream_t s);
+uint32_t launch_yata(const Work& w, uint32_t nsegs, uint32_t narray, uint32_t nclients, hipStream_t s, hipStream_t side,
+                     hipEvent_t ev_fork, hipEvent_t ev_join);
 uint32_t launch_ylists(const Work& w, uint32_t nsegs, hipStream_t s);
 
 // side / ev_fork / ev_join / tmp2: the delete-set run chain runs on `side` with its own scan space

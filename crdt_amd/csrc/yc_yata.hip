@@ -911,14 +911,15 @@ __global__ __launch_bounds__(256) void k_tsib_big(Work w, uint32_t nsegs) {
 // and a short compacted list (copying a descriptor for every big group, 800 KB pageable on C4, took
 // 0.4 ms of host time between two kernels)
 constexpr uint32_t HUGE_DESC_MAX = 62;  // descriptors read with the count in one copy (more: a second copy)
-__global__ void k_tbig_desc(Work w, uint32_t nbig, uint32_t* __restrict__ desc) {
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= nbig) return;
-  const uint32_t g = w.t_big[i], a = w.t_gstart[g], n = w.t_gstart[g + 1] - a;
-  if (n <= TLDS) return;
-  const uint32_t k = atomicAdd(&desc[0], 1u);
-  desc[2 + 2 * k] = a;
-  desc[3 + 2 * k] = n;
+__global__ void k_tbig_desc(Work w, uint32_t* __restrict__ desc) {  // (grid-stride over the big groups: no count on the host)
+  const uint32_t nbig = w.ctr->tbig;
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < nbig; i += gridDim.x * blockDim.x) {
+    const uint32_t g = w.t_big[i], a = w.t_gstart[g], n = w.t_gstart[g + 1] - a;
+    if (n <= TLDS) continue;
+    const uint32_t k = atomicAdd(&desc[0], 1u);
+    desc[2 + 2 * k] = a;
+    desc[3 + 2 * k] = n;
+  }
 }
 // anchors: the first member of every outside right-origin unit (global open addressing, P slots)
 __global__ __launch_bounds__(256) void k_thuge_hash(Work w, uint32_t a, uint32_t n, uint32_t P) {
@@ -1150,7 +1151,7 @@ void launch_tclimb(const Work& w, uint32_t nsegs, hipStream_t s) {
   hipLaunchKernelGGL(k_tclimb_done, dim3(grid), dim3(256), 0, s, w, nsegs, cl, open);
 }
 
-uint32_t launch_yata_tree(const Work& w, uint32_t nsegs, hipStream_t s) {
+uint32_t launch_yata_tree(const Work& w, uint32_t nsegs, hipStream_t s, hipStream_t side, hipEvent_t ev_fork, hipEvent_t ev_join) {
   const uint32_t grid = nsegs / 256 + 1;
   hipLaunchKernelGGL(k_tkey, dim3(grid), dim3(256), 0, s, w, nsegs);
   sort_pairs_u32(w.tmp, w.tmp_bytes, w.t_key, w.t_keys, w.y_iota, w.t_seg, nsegs, s);
@@ -1160,27 +1161,34 @@ uint32_t launch_yata_tree(const Work& w, uint32_t nsegs, hipStream_t s) {
   hipLaunchKernelGGL(k_tgroup_starts, dim3(grid), dim3(256), 0, s, w, nsegs);
   hipLaunchKernelGGL(k_tprep, dim3(grid), dim3(256), 0, s, w, nsegs);
   hipLaunchKernelGGL(k_tsib_small, dim3(nsegs / TS_BLOCK + 1), dim3(TS_BLOCK), 0, s, w, nsegs);
+  // the big-group count and the huge groups' (start, size) in ONE synchronisation
+  std::vector<uint32_t> desc(2 + 2 * (size_t)HUGE_DESC_MAX);
   uint32_t nbig = 0;
+  hipMemsetAsync(w.t_hkey, 0, sizeof(uint32_t), s);
+  hipLaunchKernelGGL(k_tbig_desc, dim3(std::min<uint32_t>(grid, 256)), dim3(256), 0, s, w, w.t_hkey);
   hipMemcpyAsync(&nbig, &w.ctr->tbig, sizeof(uint32_t), hipMemcpyDeviceToHost, s);
+  hipMemcpyAsync(desc.data(), w.t_hkey, sizeof(uint32_t) * desc.size(), hipMemcpyDeviceToHost, s);
   hipStreamSynchronize(s);
+  const uint32_t nhuge = desc[0];
+  if (nhuge > HUGE_DESC_MAX) {
+    desc.resize(2 + 2 * (size_t)nhuge);
+    hipMemcpy(desc.data(), w.t_hkey, sizeof(uint32_t) * desc.size(), hipMemcpyDeviceToHost);
+  }
+  // The huge groups (> TLDS members; t_hkey turns into their hash table now that the descriptors
+  // are read) on the side stream, BESIDE the wavefront / workgroup groups: their loop is one
+  // workgroup on one CU (C3's list head: 2.7 ms) and the groups are independent.
+  if (nhuge) {
+    hipEventRecord(ev_fork, s);
+    hipStreamWaitEvent(side, ev_fork, 0);
+    for (uint32_t k = 0; k < nhuge; ++k) launch_tsib_huge(w, desc[2 + 2 * k], desc[3 + 2 * k], nsegs, side);
+    hipEventRecord(ev_join, side);
+  }
   if (nbig) {
     hipLaunchKernelGGL(k_tsib_wave, dim3((nbig + 3) / 4), dim3(256), 0, s, w, nsegs, nbig);
     hipLaunchKernelGGL((k_tsib_big<TMID, 2048, true>), dim3(nbig), dim3(256), 0, s, w, nsegs);
     hipLaunchKernelGGL((k_tsib_big<TLDS, THASH, false>), dim3(nbig), dim3(256), 0, s, w, nsegs);
-    // the huge groups (> TLDS members): their (start, size) to the host, then the grid-wide path
-    std::vector<uint32_t> desc(2 + 2 * (size_t)HUGE_DESC_MAX);
-    hipMemsetAsync(w.t_hkey, 0, sizeof(uint32_t), s);
-    hipLaunchKernelGGL(k_tbig_desc, dim3(nbig / 256 + 1), dim3(256), 0, s, w, nbig, w.t_hkey);
-    hipMemcpyAsync(desc.data(), w.t_hkey, sizeof(uint32_t) * desc.size(), hipMemcpyDeviceToHost, s);
-    hipStreamSynchronize(s);
-    const uint32_t nhuge = desc[0];
-    if (nhuge > HUGE_DESC_MAX) {
-      desc.resize(2 + 2 * (size_t)nhuge);
-      hipMemcpy(desc.data(), w.t_hkey, sizeof(uint32_t) * desc.size(), hipMemcpyDeviceToHost);
-    }
-    // (t_hkey is the huge path's hash table: the descriptors are read before it runs)
-    for (uint32_t k = 0; k < nhuge; ++k) launch_tsib_huge(w, desc[2 + 2 * k], desc[3 + 2 * k], nsegs, s);
   }
+  if (nhuge) hipStreamWaitEvent(s, ev_join, 0);
   launch_tclimb(w, nsegs, s);
   return nbig;
 }
@@ -1204,7 +1212,8 @@ uint32_t launch_ylists(const Work& w, uint32_t nsegs, hipStream_t s) {
 
 // Returns the list count, or LISTS_UNNUMBERED when the tree path ran without numbering them
 // (launch_ylists, when a view asks).
-uint32_t launch_yata(const Work& w, uint32_t nsegs, uint32_t narray, uint32_t nclients, hipStream_t s) {
+uint32_t launch_yata(const Work& w, uint32_t nsegs, uint32_t narray, uint32_t nclients, hipStream_t s, hipStream_t side,
+                     hipEvent_t ev_fork, hipEvent_t ev_join) {
   if (!nsegs) return 0;
   if (!narray) return 0;  // g_right is only read for YArray members (merge predicate, view)
   hipLaunchKernelGGL(k_yinit, dim3(nsegs / 256 + 1), dim3(256), 0, s, w, nsegs);
@@ -1212,7 +1221,7 @@ uint32_t launch_yata(const Work& w, uint32_t nsegs, uint32_t narray, uint32_t nc
   if (!seq && (uint64_t)nsegs * 5 < 0xFFFFFFF0ull) {  // sibling keys NS + list slot stay below NONE
     static const bool eager = getenv("YCRDT_YLISTS_EAGER") && getenv("YCRDT_YLISTS_EAGER")[0] == '1';
     const uint32_t nl = eager ? launch_ylists(w, nsegs, s) : LISTS_UNNUMBERED;
-    launch_yata_tree(w, nsegs, s);
+    launch_yata_tree(w, nsegs, s, side, ev_fork, ev_join);
     return nl;
   }
   const uint32_t nlists = launch_ylists(w, nsegs, s);
