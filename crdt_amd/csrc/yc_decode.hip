@@ -1898,9 +1898,69 @@ __global__ void k_section_cidx_multi(Work w, uint32_t n) {
   if (i < n) w.sections[i].cidx = find_client(w, w.ctr->nclients, w.udoc[w.sections[i].upd], w.sections[i].client);
 }
 
+// Small single-document batches (the per-op path): the client table in ONE workgroup launch
+// (seven otherwise): the sections' clients sorted in LDS (bitonic), the distinct ones numbered by a
+// scan of the run-start flags, then every section's client index by binary search in LDS.
+constexpr uint32_t CT_LANES = 1024, CT_SMALL = 2048;
+__global__ __launch_bounds__(CT_LANES) void k_client_table_small(Work w, uint32_t n) {
+  __shared__ uint32_t v[CT_SMALL], pre[CT_SMALL + 1], u[CT_SMALL];
+  __shared__ uint32_t part[CT_LANES];
+  const uint32_t t = threadIdx.x;
+  uint32_t N = 1;
+  while (N < n) N <<= 1;
+  for (uint32_t i = t; i < N; i += CT_LANES) v[i] = i < n ? w.sections[i].client : 0xFFFFFFFFu;
+  __syncthreads();
+  for (uint32_t k = 2; k <= N; k <<= 1)
+    for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+      for (uint32_t i = t; i < N; i += CT_LANES) {
+        const uint32_t l = i ^ j;
+        if (l > i) {
+          const uint32_t x = v[i], y = v[l];
+          if (((i & k) == 0) ? (x > y) : (x < y)) { v[i] = y; v[l] = x; }
+        }
+      }
+      __syncthreads();
+    }
+  // run starts, scanned: two entries per lane
+  const uint32_t i0 = 2 * t, i1 = 2 * t + 1;
+  const uint32_t f0 = i0 < n && (i0 == 0 || v[i0] != v[i0 - 1]) ? 1u : 0u;
+  const uint32_t f1 = i1 < n && v[i1] != v[i1 - 1] ? 1u : 0u;
+  part[t] = f0 + f1;
+  __syncthreads();
+  for (uint32_t off = 1; off < CT_LANES; off <<= 1) {
+    const uint32_t x = t >= off ? part[t - off] : 0u;
+    __syncthreads();
+    part[t] += x;
+    __syncthreads();
+  }
+  const uint32_t base = part[t] - f0 - f1;
+  if (i0 < n) pre[i0] = base;
+  if (i1 < n) pre[i1] = base + f0;
+  const uint32_t nc = part[CT_LANES - 1];
+  __syncthreads();
+  for (uint32_t i = t; i < n; i += CT_LANES)
+    if (i == 0 || v[i] != v[i - 1]) {
+      u[pre[i]] = v[i];
+      w.cl_vals[pre[i]] = v[i];
+      if (w.cl_single) w.cl_single[pre[i]] = (i + 1 == n || v[i + 1] != v[i]) ? 1u : 0u;  // a run of one section
+    }
+  if (t == 0) w.ctr->nclients = nc;
+  __syncthreads();
+  for (uint32_t i = t; i < n; i += CT_LANES) {
+    const uint32_t c = w.sections[i].client;
+    uint32_t lo = 0, hi = nc;
+    while (lo < hi) { const uint32_t m = (lo + hi) >> 1; if (u[m] < c) lo = m + 1; else hi = m; }
+    w.sections[i].cidx = lo;
+  }
+}
+
 // NC stays on the device (ctr->nclients) until the struct-decode counter read
 void launch_client_table(Work& w, uint32_t nsections, hipStream_t s) {
   const uint32_t grid = nsections / 256 + 1;
+  if (!w.udoc && nsections <= CT_SMALL) {
+    hipLaunchKernelGGL(k_client_table_small, dim3(1), dim3(CT_LANES), 0, s, w, nsections);
+    return;
+  }
   if (w.udoc) {
     hipLaunchKernelGGL(k_gather_sec_keys, dim3(grid), dim3(256), 0, s, w, nsections);
     sort_pairs_u64_u32(w.tmp, w.tmp_bytes, w.cl_key2, w.cl_key, w.cl_tmp, w.cl_state, nsections, s);
