@@ -67,6 +67,28 @@ __device__ __forceinline__ void wave_flag(uint32_t* flag, bool pred) {
   if (__ballot(pred) && (threadIdx.x & 63u) == 0) *flag = 1u;
 }
 
+// Exclusive scan of n (<= LANES * 16) u32 values in ONE workgroup of LANES threads: a lane sums a
+// contiguous run, the run sums are scanned in LDS (part[LANES]), each lane writes its run's prefixes
+// (out[i] may alias in[i]: a lane reads its run before writing it). The small-batch kernels use it.
+template <uint32_t LANES>
+__device__ __forceinline__ void block_scan_u32(const uint32_t* in, uint32_t* out, uint32_t n, uint32_t* part) {
+  const uint32_t t = threadIdx.x, per = (n + LANES - 1) / LANES;
+  const uint32_t a = min(n, t * per), b = min(n, a + per);
+  uint32_t sum = 0;
+  for (uint32_t i = a; i < b; ++i) sum += in[i];
+  part[t] = sum;
+  __syncthreads();
+  for (uint32_t off = 1; off < LANES; off <<= 1) {
+    const uint32_t v = t >= off ? part[t - off] : 0u;
+    __syncthreads();
+    part[t] += v;
+    __syncthreads();
+  }
+  uint32_t run = part[t] - sum;
+  for (uint32_t i = a; i < b; ++i) { const uint32_t x = in[i]; out[i] = run; run += x; }
+  __syncthreads();
+}
+
 __device__ __forceinline__ void raise_err(uint32_t* err, uint32_t code) {
   atomicCAS(err, 0u, code);
 }

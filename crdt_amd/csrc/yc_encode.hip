@@ -235,9 +235,7 @@ __global__ __launch_bounds__(256) void k_out_sizes(Work w, uint32_t nsegs, uint3
 // runs of consecutive deleted segments (createDeleteSetFromStructStore): their starts were flagged
 // in r_size by k_merge_flags / k_merge_final
 __device__ __forceinline__ bool seg_deleted(uint32_t f) { return (f & SEG_DEL) || !(f & SEG_ITEM); }
-__global__ void k_run_fill(Work w, uint32_t nsegs) {
-  const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
-  if (s >= nsegs) return;
+__device__ __forceinline__ void run_fill_at(const Work& w, uint32_t s, uint32_t nsegs) {
   const uint32_t f = w.g_flags[s];
   if (!seg_deleted(f)) return;
   const uint32_t rid = w.g_tmp2[s + 1] - 1;  // inclusive count of run starts up to s
@@ -246,15 +244,33 @@ __global__ void k_run_fill(Work w, uint32_t nsegs) {
   const bool last = s + 1 == nsegs || w.g_cidx[s + 1] != w.g_cidx[s] || !seg_deleted(w.g_flags[s + 1]);
   if (last) w.r_len[rid] = w.g_start[s + 1];  // end unit; the start is subtracted in k_run_sizes
 }
-__global__ void k_run_sizes(Work w, uint32_t nsegs) {
-  const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
-  if (r > nsegs) return;
+__global__ void k_run_fill(Work w, uint32_t nsegs) {
+  const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
+  if (s < nsegs) run_fill_at(w, s, nsegs);
+}
+__device__ __forceinline__ void run_sizes_at(const Work& w, uint32_t r, uint32_t nsegs) {
   if (r >= w.g_tmp2[nsegs]) { w.r_size[r] = 0; return; }
   const uint32_t s = w.r_seg[r];
   const uint32_t len = w.r_len[r] - w.g_start[s];
   w.r_len[r] = len;
   const uint32_t clock = (uint32_t)(w.g_start[s] - w.cl_base[w.g_cidx[s]]);
   w.r_size[r] = vu_size(clock) + vu_size(len);
+}
+__global__ void k_run_sizes(Work w, uint32_t nsegs) {
+  const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r <= nsegs) run_sizes_at(w, r, nsegs);
+}
+// Small batches: the delete-set runs (scan of the run starts, fill, sizes, scan of the sizes) in
+// ONE workgroup launch on the main stream (four launches on the side stream and its fork / join)
+constexpr uint32_t RUNS_LANES = 1024, RUNS_SMALL = RUNS_LANES * 16;
+__global__ __launch_bounds__(RUNS_LANES) void k_runs_small(Work w, uint32_t nsegs) {
+  __shared__ uint32_t part[RUNS_LANES];
+  block_scan_u32<RUNS_LANES>(w.r_size, w.g_tmp2, nsegs + 1, part);  // (r_size: k_merge_flags' run starts)
+  for (uint32_t s = threadIdx.x; s < nsegs; s += RUNS_LANES) run_fill_at(w, s, nsegs);
+  __syncthreads();
+  for (uint32_t r = threadIdx.x; r <= nsegs; r += RUNS_LANES) run_sizes_at(w, r, nsegs);
+  __syncthreads();
+  block_scan_u32<RUNS_LANES>(w.r_size, w.r_pos, nsegs + 1, part);
 }
 
 // per client: first output struct and first delete-set run, from the boundaries of the (client-
@@ -470,6 +486,12 @@ void launch_encode_sizes(const Work& w, uint32_t nsegs, uint32_t nclients, hipSt
                          hipEvent_t ev_fork, hipEvent_t ev_join, void* tmp2, size_t tmp2_bytes) {
   fill_u32_multi({{w.ctr->pad, 8, 0u}, {w.cc + (size_t)CC_NRUNS * (w.cap_clients + 1), (uint64_t)w.cap_clients + 1, 0u}}, s);
   const uint32_t grid = nsegs / 256 + 1;
+  if (nsegs + 1 <= RUNS_SMALL) {  // (a small batch: one launch, main stream)
+    if (!nsegs) fill_u32_multi({{w.r_size, 1, 0u}}, s);
+    hipLaunchKernelGGL(k_runs_small, dim3(1), dim3(RUNS_LANES), 0, s, w, nsegs);
+    hipEventRecord(ev_join, s);  // (the layout waits on it)
+    return;
+  }
   // delete-set runs (side stream) || output struct sizes (main stream)
   hipEventRecord(ev_fork, s);
   hipStreamWaitEvent(side, ev_fork, 0);

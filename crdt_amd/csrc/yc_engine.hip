@@ -1196,11 +1196,12 @@ int run_merge(ycrdt_engine* e, ycrdt_batch* b, const std::unordered_map<uint32_t
       if (D.nested) run_dead_keys(w, nsegs, s);  // only lists under a parent item can die with it
       mark(e, "merge.yata");
       e->nlists = launch_yata(w, nsegs, narray, nclients, s, e->side, e->side_fork, e->side_done);
-      if (w.dbg && e->nlists && e->nlists != LISTS_UNNUMBERED) {
-        unsigned long long h[3];
+      if (w.dbg && e->nlists) {
+        unsigned long long h[7];
         HIPCHK(hipStreamSynchronize(s));
         HIPCHK(hipMemcpy(h, w.dbg, sizeof(h), hipMemcpyDeviceToHost));
-        fprintf(stderr, "[ycrdt] k_yata: %u lists, %llu integrations, %llu conflict-scan steps, %llu stack dives\n", e->nlists, h[0], h[1], h[2]);
+        fprintf(stderr, "[ycrdt] k_yata: %llu integrations, %llu conflict-scan steps, %llu stack dives | huge sibling loop: %llu placements, %llu group-list steps, %llu left steps, %llu dives\n",
+                h[0], h[1], h[2], h[3], h[4], h[5], h[6]);
       }
       mark(e, "merge.merge_flags");
       if (!sh) {

@@ -165,8 +165,7 @@ __device__ __forceinline__ void unit_refs(const Work& w, uint32_t nstructs, uint
     set_flag_byte(w.u_flags, g, 2);                          // getItemCleanStart(rightOrigin)
   }
 }
-__global__ __launch_bounds__(256) void k_cuts(Work w, uint64_t nunits) {
-  const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+__device__ __forceinline__ bool cut_at(const Work& w, uint64_t g, uint64_t nunits) {
   bool cut = false;
   if (g < nunits) {
     const uint32_t own = w.u_owner[g];
@@ -187,6 +186,11 @@ __global__ __launch_bounds__(256) void k_cuts(Work w, uint64_t nunits) {
       }
     }
   }
+  return cut;
+}
+__global__ __launch_bounds__(256) void k_cuts(Work w, uint64_t nunits) {
+  const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const bool cut = cut_at(w, g, nunits);
   const uint64_t word = __ballot(cut);
   if ((threadIdx.x & 63) == 0) {  // the word and its popcount (the scan input of the segment numbering)
     const uint64_t wi = g >> 6;
@@ -198,8 +202,7 @@ __global__ __launch_bounds__(256) void k_cuts(Work w, uint64_t nunits) {
     }
   }
 }
-__global__ void k_scatter_seg(Work w, uint32_t nwords, uint64_t nunits) {
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+__device__ __forceinline__ void scatter_seg_at(const Work& w, uint32_t i, uint32_t nwords, uint64_t nunits) {
   if (i == 0) w.ctr->nsegs = w.u_wpre[nwords];  // the scan's total (no copy launch)
   if (i >= nwords) return;
   uint64_t x = w.u_cutbits[i];
@@ -210,6 +213,28 @@ __global__ void k_scatter_seg(Work w, uint32_t nwords, uint64_t nunits) {
     w.g_start[k++] = i * 64 + bit;
   }
   if (i == nwords - 1) w.g_start[w.u_wpre[nwords]] = (uint32_t)nunits;  // sentinel
+}
+__global__ void k_scatter_seg(Work w, uint32_t nwords, uint64_t nunits) {
+  scatter_seg_at(w, blockIdx.x * blockDim.x + threadIdx.x, nwords, nunits);
+}
+// Small batches: the cut words, their popcount prefix and the segment starts in ONE workgroup launch
+// (three otherwise); a wavefront takes 64 consecutive units at a time, as in k_cuts
+constexpr uint32_t SEG_LANES = 1024, SEG_SMALL_WORDS = SEG_LANES * 16 - 1;
+__global__ __launch_bounds__(SEG_LANES) void k_segments_small(Work w, uint64_t nunits) {
+  __shared__ uint32_t part[SEG_LANES];
+  const uint32_t nwords = (uint32_t)((nunits + 63) / 64);
+  for (uint32_t base = 0; base < nwords * 64; base += SEG_LANES) {
+    const uint32_t g = base + threadIdx.x;
+    const uint64_t word = __ballot(cut_at(w, g, nunits));
+    if ((threadIdx.x & 63) == 0 && g < nunits) {
+      w.u_cutbits[g >> 6] = word;
+      w.scratch[g >> 6] = (uint32_t)__popcll(word);
+    }
+  }
+  if (threadIdx.x == 0) w.scratch[nwords] = 0;
+  __syncthreads();
+  block_scan_u32<SEG_LANES>(w.scratch, w.u_wpre, nwords + 1, part);
+  for (uint32_t i = threadIdx.x; i < nwords; i += SEG_LANES) scatter_seg_at(w, i, nwords, nunits);
 }
 
 // One launch for the three unit passes (they touch disjoint bytes of a unit's flag word: byte 0
@@ -236,6 +261,10 @@ void launch_units(const Work& w, uint32_t nstructs, uint32_t nclients, uint32_t 
 
 void launch_segments(const Work& w, uint32_t nclients, uint64_t nunits, hipStream_t s) {
   const uint32_t nwords = (uint32_t)((nunits + 63) / 64);
+  if (nwords <= SEG_SMALL_WORDS) {
+    hipLaunchKernelGGL(k_segments_small, dim3(1), dim3(SEG_LANES), 0, s, w, nunits);
+    return;
+  }
   hipLaunchKernelGGL(k_cuts, dim3(nwords / 4 + 1), dim3(256), 0, s, w, nunits);
   scan_u32(w.tmp, w.tmp_bytes, w.scratch, w.u_wpre, nwords + 1, s);
   hipLaunchKernelGGL(k_scatter_seg, dim3(nwords / 256 + 1), dim3(256), 0, s, w, nwords, nunits);

@@ -357,8 +357,9 @@ constexpr uint32_t TOUT = 0x8000u;  // LDS trep flag (bit 31 in global memory): 
 // top back, and from global memory that read was a memory round trip per pop: C3's list-head loop
 // spent 2.6 ms on them)
 template <class A, class S>
-__device__ uint32_t sib_loop(A& a, uint32_t n, S* __restrict__ stack, uint32_t* err) {
+__device__ uint32_t sib_loop(A& a, uint32_t n, S* __restrict__ stack, uint32_t* err, unsigned long long* dbg = nullptr) {
   uint32_t head = NONE, tail = NONE;
+  unsigned long long st_place = 0, st_m = 0, st_left = 0, st_dive = 0;  // (YCRDT_DEBUG_YATA=1: loop statistics)
   for (uint32_t i0 = 0; i0 < n; ++i0) {
     if (a.done(i0) == 2) continue;
     // the stack's top stays in a register (the stack is in global memory: reading back the
@@ -373,6 +374,7 @@ __device__ uint32_t sib_loop(A& a, uint32_t n, S* __restrict__ stack, uint32_t* 
         a.set_done(rp, 1);
         stack[sp++] = rp;
         c = rp;
+        ++st_dive;
         continue;
       }
       bool out = false;
@@ -381,14 +383,15 @@ __device__ uint32_t sib_loop(A& a, uint32_t n, S* __restrict__ stack, uint32_t* 
       // is anchored at its right-origin sibling (mtail) or, for a right origin outside the group,
       // at its first member (otail: a member can anchor both kinds)
       uint32_t m = out ? a.otail(ta) : a.mtail(ta), succ = NONE;
-      while (m != NONE && a.cid(m) > cc) { succ = m; m = a.mprv(m); }
+      while (m != NONE && a.cid(m) > cc) { succ = m; m = a.mprv(m); ++st_m; }
       a.set_mprv(c, m);
       if (succ != NONE) a.set_mprv(succ, c);
       else if (out) a.set_otail(ta, c);
       else a.set_mtail(ta, c);
       const uint32_t stop = succ != NONE ? succ : rp;
       uint32_t left = stop != NONE ? a.prv(stop) : tail;
-      while (left != NONE && a.cid(left) >= cc) left = a.prv(left);
+      while (left != NONE && a.cid(left) >= cc) { left = a.prv(left); ++st_left; }
+      ++st_place;
       const uint32_t nx = left != NONE ? a.next(left) : head;
       a.set_prv(c, left);
       a.set_next(c, nx);
@@ -398,6 +401,7 @@ __device__ uint32_t sib_loop(A& a, uint32_t n, S* __restrict__ stack, uint32_t* 
       if (--sp > 0) c = stack[sp - 1];
     }
   }
+  if (dbg) { atomicAdd(&dbg[3], st_place); atomicAdd(&dbg[4], st_m); atomicAdd(&dbg[5], st_left); atomicAdd(&dbg[6], st_dive); }
   return head;
 }
 struct SibGlobal {  // a group read in place (sorted positions base..base+n); links hold positions
@@ -992,7 +996,7 @@ __global__ __launch_bounds__(256) void k_thuge_loop(Work w, uint32_t a, uint32_t
   __syncthreads();
   if (threadIdx.x == 0) {
     SibLds acc{rec, st};
-    head_s = sib_loop(acc, nn, stk, &w.ctr->err);
+    head_s = sib_loop(acc, nn, stk, &w.ctr->err, w.dbg);
     w.t_flag[2 * n + 2] = head_s;  // (read by the expansion)
   }
   __syncthreads();
