@@ -1561,13 +1561,141 @@ void launch_chunks(const Work& w, hipStream_t s) {
     hipLaunchKernelGGL(k_xmark, dim3((w.ngroups + DL - 1) / DL), dim3(DL), 0, s, w);
   }
 }
-void launch_direct(const Work& w, hipStream_t s) {
-  // one lane per update when there are enough updates to fill wavefronts, else one wavefront per
-  // update; YCRDT_DIRECT_WAVE=1 / 0 forces one (read per merge: tests switch it)
+// ---- Few small updates, ranked: every position's chain step in parallel (k_wlen: one lane per
+// byte over the whole chip), then in one workgroup per update the first n positions of each
+// section's chain from its first struct are found by pointer doubling in LDS (k_wrank). The result
+// is the exact walk's (the same step function from the same start), without its latency: a
+// wavefront walking a 9 KB per-op doc state struct by struct (k_wdecode's chains and their
+// settling) took 0.5-0.8 ms, one struct step being ~1 000 dependent instructions on one SIMD.
+__global__ __launch_bounds__(256) void k_wlen(Work w) {
+  const uint32_t j = blockIdx.y;
+  const uint32_t u = w.ulist[w.nbig + j];
+  const uint32_t ustart = w.uoff[u], L = w.ulen[u];
+  const uint32_t k = blockIdx.x * 256 + threadIdx.x;
+  if (k >= L || L > WD_MAX) return;
+  const uint8_t* __restrict__ b = win_bytes(w, upd_win(w, u));
+  w.wlen[(size_t)j * WD_MAX + k] = (uint16_t)chain_len(GlobalSrc{b}, b, ustart + k, ustart + L);
+}
+constexpr uint32_t WR_LANES = 1024;
+constexpr uint16_t WR_INF = 0xFFFFu;
+__global__ __launch_bounds__(WR_LANES) void k_wrank(Work w) {
+  __shared__ uint16_t ja[WD_MAX + 2], jb[WD_MAX + 2], dist[WD_MAX + 2];  // [L]: the update end, [L + 1]: no struct parses
+  __shared__ uint64_t bits[WD_WORDS];
+  __shared__ uint32_t sh_base, sh_last;
+  const uint32_t t = threadIdx.x, j = blockIdx.x;
+  const uint32_t u = w.ulist[w.nbig + j];
+  const uint32_t uw = upd_win(w, u);
+  const uint8_t* __restrict__ b = win_bytes(w, uw);
+  uint64_t* __restrict__ fbits = win_words(w.final_bits, uw);
+  uint64_t* __restrict__ sbits = win_words(w.sec_bits, uw);
+  const uint32_t ustart = w.uoff[u], L = w.ulen[u], uend = ustart + L;
+  const uint16_t* __restrict__ dl = w.wlen + (size_t)j * WD_MAX;
+  uint32_t* err = &w.ctr->err;
+  if (L > WD_MAX) { if (t == 0) raise_err(err, ERR_CAPACITY); return; }  // (the layout never sends one)
+  bool ok = true;
+  uint32_t q = ustart;
+  const uint32_t nsec = rd_vu(b, q, uend, ok);
+  if (!ok || nsec > (uend - q) / 3 + 1) { if (t == 0) { raise_err(err, ERR_DECODE); w.dsstart[u] = NONE; } return; }
+  if (t == 0) sh_base = atomicAdd(&w.ctr->nsections, nsec);
+  const uint32_t nw = (L + 63) / 64;
+  for (uint32_t k = t; k < nw; k += WR_LANES) bits[k] = 0;
+  __syncthreads();
+  const uint32_t sbase = sh_base;
+  if (sbase + nsec > w.cap_sections) { if (t == 0) { raise_err(err, ERR_CAPACITY); w.dsstart[u] = NONE; } return; }
+  bool fail = false;
+  for (uint32_t sct = 0; sct < nsec; ++sct) {  // (q, n, fail: the same in every lane)
+    const uint32_t n = rd_vu(b, q, uend, ok), client = rd_vu(b, q, uend, ok), clock = rd_vu(b, q, uend, ok);
+    if (!ok || n > uend - q) { if (t == 0) raise_err(err, ERR_DECODE); fail = true; break; }
+    if (t == 0) {
+      Section sec;
+      sec.upd = u; sec.n = n; sec.client = client; sec.clock = clock;
+      sec.first_pos = n ? q : NONE; sec.cidx = NONE; sec.first_idx = NONE; sec.pad = 0;
+      w.sections[sbase + sct] = sec;
+      if (n) atomicOr((unsigned long long*)&sbits[q >> 6], 1ull << (q & 63));
+    }
+    if (!n) continue;
+    // jump tables: ja = one chain step (the end and "no struct" are sinks), distances unknown
+    const uint32_t q1 = q - ustart;
+    for (uint32_t i = t; i < L + 2; i += WR_LANES) {
+      uint32_t x = i;
+      if (i < L) { const uint32_t d = dl[i]; x = !d ? L + 1 : min(i + d, L); }
+      ja[i] = (uint16_t)x;
+      dist[i] = i == q1 ? 0 : WR_INF;
+    }
+    __syncthreads();
+    // doubling: in the round of step 2^k every position at distance < 2^k marks the one 2^k steps
+    // on (distances below n only), then the table advances to 2^(k+1) steps. The chain's positions
+    // increase, so each distance names one position; a sink reached below n is a struct missing.
+    uint16_t *A = ja, *B = jb;
+    for (uint32_t step = 1; step < n; step <<= 1) {
+      for (uint32_t i = t; i < L; i += WR_LANES) {
+        const uint32_t dv = dist[i];
+        if (dv < step && dv + step < n) dist[A[i]] = (uint16_t)(dv + step);
+      }
+      __syncthreads();
+      if (2 * step < n) {
+        for (uint32_t i = t; i < L + 2; i += WR_LANES) B[i] = A[A[i]];
+        __syncthreads();
+        uint16_t* x = A; A = B; B = x;
+      }
+    }
+    // the section's structs: the positions at distance < n; the last one's end starts the next
+    if (t == 0) sh_last = NONE;
+    __syncthreads();
+    for (uint32_t i = t; i < L; i += WR_LANES)
+      if (dist[i] == n - 1) sh_last = i;
+    for (uint32_t k = t; k < nw; k += WR_LANES) {
+      uint64_t m = 0;
+      for (uint32_t x = 0; x < 64 && k * 64 + x < L; ++x) m |= (uint64_t)(dist[k * 64 + x] < n) << x;
+      bits[k] |= m;
+    }
+    __syncthreads();
+    const uint32_t last = sh_last;
+    const bool sunk = dist[L] != WR_INF || dist[L + 1] != WR_INF;
+    if (!sunk && last != NONE && dl[last]) {
+      q = ustart + last + dl[last];
+    } else {
+      // a struct missing (malformed input): the exact walk, which reports where
+      if (t == 0) {
+        uint32_t x = q;
+        for (uint32_t k = 0; k < n; ++k) {
+          if (x >= uend) { raise_err(err, ERR_DECODE); w.ctr->err_info = x; break; }
+          const uint32_t d = dl[x - ustart];
+          if (!d) { raise_err(err, ERR_DECODE); w.ctr->err_info = x; break; }
+          x += d;
+        }
+      }
+      fail = true;
+      break;
+    }
+    __syncthreads();  // (the tables are rebuilt for the next section)
+  }
+  __syncthreads();
+  if (t == 0) {
+    w.usec_start[u] = sbase;
+    w.usec_n[u] = nsec;
+    w.dsstart[u] = fail ? NONE : q;
+    if (w.dbg) atomicAdd(&w.dbg[fail ? 5 : 3], 1ull);  // (YCRDT_DEBUG_DECODE: counted as the wave path's)
+  }
+  for (uint32_t k = t; k < nw; k += WR_LANES) fbits[(ustart >> 6) + k] = bits[k];
+}
+
+bool wave_decode(const Work& w) {
+  // one lane per update when there are enough updates to fill wavefronts, else the ranked path;
+  // YCRDT_DIRECT_WAVE=1 / 0 forces one (read per merge: tests switch it)
   const char* wd = getenv("YCRDT_DIRECT_WAVE");
   const bool lane_direct = wd && (wd[0] == '1' || wd[0] == '0') ? wd[0] == '0' : w.nsmall >= WD_LANE_MIN;
-  if (w.nsmall && !lane_direct) hipLaunchKernelGGL(k_wdecode, dim3(w.nsmall), dim3(64), 0, s, w);
-  else if (w.nsmall) hipLaunchKernelGGL(k_direct, dim3((w.nsmall + DL - 1) / DL), dim3(DL), 0, s, w);
+  return w.nsmall && !lane_direct;
+}
+void launch_direct(const Work& w, hipStream_t s) {
+  // YCRDT_WDECODE=settle: the wavefront-per-update chains of k_wdecode instead of the ranking
+  const char* wm = getenv("YCRDT_WDECODE");
+  // (a split decode's share may take this path where the whole batch did not: no rank tables)
+  if (wave_decode(w) && ((wm && !strcmp(wm, "settle")) || !w.wlen)) hipLaunchKernelGGL(k_wdecode, dim3(w.nsmall), dim3(64), 0, s, w);
+  else if (wave_decode(w)) {
+    hipLaunchKernelGGL(k_wlen, dim3(WD_MAX / 256, w.nsmall), dim3(256), 0, s, w);
+    hipLaunchKernelGGL(k_wrank, dim3(w.nsmall), dim3(WR_LANES), 0, s, w);
+  } else if (w.nsmall) hipLaunchKernelGGL(k_direct, dim3((w.nsmall + DL - 1) / DL), dim3(DL), 0, s, w);
 }
 
 // --------------------------------------------------------------------------- 3. struct positions

@@ -176,7 +176,7 @@ enum Buf {
   B_UOWN, B_UFLAG, B_UMIN, B_UCUT, B_UWPRE,
   B_GSTART, B_GCIDX, B_GSRC, B_GFLAGS, B_GORIG, B_GRORIG, B_GLINK, B_GOSEG, B_GKEY, B_GMAXC, B_GNEXT, B_GOUTID, B_GTMP, B_GTMP2,
   B_KHASH, B_KROOT, B_KWIN, B_KPAR, B_KFLAG, B_SPK,
-  B_USEC, B_USECN, B_DBG, B_XTAB, B_UFAIL, B_FW, B_CCNT, B_TENTRY, B_XLIST,
+  B_USEC, B_USECN, B_DBG, B_XTAB, B_UFAIL, B_FW, B_CCNT, B_TENTRY, B_XLIST, B_WLEN,
   B_LZKEY, B_LZKEYS, B_LZIOTA, B_LZSEC, B_LZRSTART, B_LZPREV, B_LZFIRST, B_LZCAP, B_LZEVBASE, B_LZEVN, B_LZFLAG,
   B_LZLHI, B_LZLLO, B_EVKIND, B_EVSRC, B_EVCLOCK, B_EVLEN, B_EVSIZE, B_EVPOS, B_BLKSIZE, B_BLKPOS, B_SVC, B_SVK,
   B_DSMKEY, B_DSMKEYS, B_DSMLEN, B_DSMLENS, B_DSMEND, B_DSMMAX, B_DSMFLAG, B_DSMRID, B_DRCLIENT, B_DRCLOCK, B_DREND,
@@ -217,6 +217,11 @@ struct ycrdt_engine {
   // for batch staging (H2D, on the copy stream) and one for results (D2H, on the engine stream),
   // so a batch can be staged by one host thread while another merges the previous batch
   Pinned pin_in, pin_out;
+  // pinned read-back areas of the sync points (a copy into pageable memory goes through the
+  // runtime's staging: ~20-30 us per copy on the per-op path): the counters, and a small view
+  Counters* ctr_pin = nullptr;
+  uint8_t* rb = nullptr;
+  size_t rb_cap = 0;
   hipStream_t copy = nullptr;  // batch staging (host → HBM)
   hipEvent_t copy_dep = nullptr;
   // result of the last merge (e->w.out / e->w.sv_out): ws_owner is the batch that produced it
@@ -600,8 +605,14 @@ int map_err(uint32_t code, const char* where) {
 
 // Reads the counters (sync) and returns an error if the device raised one.
 int check(ycrdt_engine* e, Counters& c, const char* where) {
-  HIPCHK(hipMemcpyAsync(&c, e->w.ctr, sizeof(Counters), hipMemcpyDeviceToHost, e->stream));
+  if (!e->ctr_pin && hipHostMalloc((void**)&e->ctr_pin, sizeof(Counters), hipHostMallocDefault) != hipSuccess) {
+    (void)hipGetLastError();
+    e->ctr_pin = nullptr;
+    return fail(YCRDT_E_DEVICE, "pinned counter read-back allocation failed");
+  }
+  HIPCHK(hipMemcpyAsync(e->ctr_pin, e->w.ctr, sizeof(Counters), hipMemcpyDeviceToHost, e->stream));
   HIPCHK(hipStreamSynchronize(e->stream));
+  c = *e->ctr_pin;
   if (c.err) return map_err(c.err, where);
   return YCRDT_OK;
 }
@@ -828,6 +839,7 @@ int run_decode(ycrdt_engine* e, ycrdt_batch* b, bool lazy, Decoded& D, bool gene
   w.scratch = take<uint32_t>(V, B_SCRATCH, std::max<uint64_t>({nwords + 2, (uint64_t)w.cap_sections + 66, (uint64_t)nu + 2}), ok);
   w.usec_start = take<uint32_t>(V, B_USEC, nu + 1, ok);
   w.usec_n = take<uint32_t>(V, B_USECN, nu + 1, ok);
+  w.wlen = wave_decode(w) ? take<uint16_t>(V, B_WLEN, (uint64_t)w.nsmall * 16384, ok) : nullptr;
   if (!ok) return fail(YCRDT_E_DEVICE, oom("decode workspace"));
   // rocPRIM scratch sized for the largest scan of this batch (units may grow it later)
   {
@@ -1329,20 +1341,42 @@ int run_view(ycrdt_engine* e, ycrdt_batch* b, HostView& hv) {
     const bool small = !big_only && (uint64_t)ck * sizeof(ViewKey) <= (256u << 10);
     Counters c;
     uint32_t nkeys = 0;
-    HIPCHK(hipMemcpyAsync(&c, w.ctr, sizeof(Counters), hipMemcpyDeviceToHost, s));
-    HIPCHK(hipMemcpyAsync(&nkeys, vb.nkeys, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
     hv.segs.resize(narr);
-    if (small) {
-      hv.keys.resize(ck);
-      HIPCHK(hipMemcpyAsync(hv.keys.data(), vb.keys, sizeof(ViewKey) * ck, hipMemcpyDeviceToHost, s));
-      if (narr) HIPCHK(hipMemcpyAsync(hv.segs.data(), vb.segs, sizeof(ViewSeg) * narr, hipMemcpyDeviceToHost, s));
-      if (b->nbytes) HIPCHK(hipMemcpyAsync(hv.bytes.data(), b->bytes.p, b->nbytes, hipMemcpyDeviceToHost, s));
+    // (the small view's pieces land in the pinned read-back area, 256-byte aligned)
+    auto al = [](size_t x) { return (x + 255) & ~size_t(255); };
+    const size_t o_keys = al(sizeof(Counters) + 4), o_segs = o_keys + al(sizeof(ViewKey) * ck),
+                 o_bytes = o_segs + al(sizeof(ViewSeg) * narr), rb_need = o_bytes + b->nbytes;
+    if (small && rb_need > e->rb_cap) {
+      if (e->rb) hipHostFree(e->rb);
+      e->rb_cap = 0;
+      if (hipHostMalloc((void**)&e->rb, std::max<size_t>(rb_need, size_t(1) << 20), hipHostMallocDefault) != hipSuccess) {
+        (void)hipGetLastError();
+        e->rb = nullptr;
+        return fail(YCRDT_E_DEVICE, "pinned view read-back allocation failed");
+      }
+      e->rb_cap = std::max<size_t>(rb_need, size_t(1) << 20);
     }
-    HIPCHK(hipStreamSynchronize(s));
+    if (small) {
+      HIPCHK(hipMemcpyAsync(e->rb, w.ctr, sizeof(Counters), hipMemcpyDeviceToHost, s));
+      HIPCHK(hipMemcpyAsync(e->rb + sizeof(Counters), vb.nkeys, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+      HIPCHK(hipMemcpyAsync(e->rb + o_keys, vb.keys, sizeof(ViewKey) * ck, hipMemcpyDeviceToHost, s));
+      if (narr) HIPCHK(hipMemcpyAsync(e->rb + o_segs, vb.segs, sizeof(ViewSeg) * narr, hipMemcpyDeviceToHost, s));
+      if (b->nbytes) HIPCHK(hipMemcpyAsync(e->rb + o_bytes, b->bytes.p, b->nbytes, hipMemcpyDeviceToHost, s));
+      HIPCHK(hipStreamSynchronize(s));
+      memcpy(&c, e->rb, sizeof(Counters));
+      memcpy(&nkeys, e->rb + sizeof(Counters), sizeof(uint32_t));
+    } else {
+      HIPCHK(hipMemcpyAsync(&c, w.ctr, sizeof(Counters), hipMemcpyDeviceToHost, s));
+      HIPCHK(hipMemcpyAsync(&nkeys, vb.nkeys, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+      HIPCHK(hipStreamSynchronize(s));
+    }
     if (c.err) return map_err(c.err, "view");
     if (nkeys > ck) return fail(YCRDT_E_DEVICE, "view: key count past the key table");
     if (small) {
       hv.keys.resize(nkeys);
+      if (nkeys) memcpy(hv.keys.data(), e->rb + o_keys, sizeof(ViewKey) * nkeys);
+      if (narr) memcpy(hv.segs.data(), e->rb + o_segs, sizeof(ViewSeg) * narr);
+      if (b->nbytes) memcpy(hv.bytes.data(), e->rb + o_bytes, b->nbytes);
     } else {
       hv.keys.resize(nkeys);
       if (nkeys) HIPCHK(hipMemcpy(hv.keys.data(), vb.keys, sizeof(ViewKey) * nkeys, hipMemcpyDeviceToHost));
@@ -1785,6 +1819,8 @@ void ycrdt_engine_destroy(ycrdt_engine* e) {
     hipEventDestroy(pin->ev[1]);
     if (pin->p) hipHostFree(pin->p);
   }
+  if (e->ctr_pin) hipHostFree(e->ctr_pin);
+  if (e->rb) hipHostFree(e->rb);
   hipEventDestroy(e->copy_dep);
   hipStreamDestroy(e->copy);
   hipStreamSynchronize(e->side);

@@ -84,6 +84,7 @@ struct Work {
   uint32_t ndocs = 1;
   const uint32_t* ulist = nullptr; // [nbig] updates on the chunk path, then [nsmall] parsed directly
   uint32_t nbig = 0, nsmall = 0;
+  uint16_t* wlen = nullptr;        // [nsmall * 16384] few small updates: the chain step at every position (k_wlen)
   uint32_t schunk = SCHUNK;        // chunk bytes of this batch's large updates (<= SCHUNK)
   uint32_t force_xtab = 0;         // YCRDT_DECODE=xtab: every large update takes the exit-table walk (tests)
   uint32_t spec_hint = 2;          // k_spec chunk-start hints: 0 never, 1 always, 2 single-section updates
@@ -578,6 +579,7 @@ void launch_view(const Work& w, const ViewBufs& v, uint32_t nsegs, uint32_t nlis
 // ---- launch entry points (yc_decode.hip / yc_merge.hip / yc_encode.hip / yc_prims.hip)
 void launch_chunks(const Work& w, hipStream_t s);  // k_spec + k_walk: large updates
 void launch_direct(const Work& w, hipStream_t s);  // k_direct: small updates
+bool wave_decode(const Work& w);                  // few small updates: k_wlen + k_wrank (else k_direct)
 void launch_client_hash(const Work& w, uint64_t* key, uint32_t* val, uint32_t mask, hipStream_t s);
 void launch_struct_count(const Work& w, hipStream_t s);
 void launch_struct_scatter(const Work& w, hipStream_t s);

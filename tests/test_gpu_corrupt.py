@@ -50,11 +50,13 @@ def _bad(fx, c):
     return bytes(u)
 
 
-@pytest.mark.parametrize("mode", ["direct", "wave", "chunks"])
+@pytest.mark.parametrize("mode", ["direct", "wave", "settle", "chunks"])
 def test_corrupt_like_yjs(corrupt, mode, monkeypatch):
-    monkeypatch.setenv("YCRDT_DECODE", "direct" if mode == "wave" else mode)
-    if mode in ("wave", "direct"):
-        monkeypatch.setenv("YCRDT_DIRECT_WAVE", "1" if mode == "wave" else "0")
+    wave = mode in ("wave", "settle")  # few small updates: ranked / k_wdecode's settled chains
+    monkeypatch.setenv("YCRDT_DECODE", "direct" if wave else mode)
+    if mode != "chunks":
+        monkeypatch.setenv("YCRDT_DIRECT_WAVE", "1" if wave else "0")
+    monkeypatch.setenv("YCRDT_WDECODE", "settle" if mode == "settle" else "rank")
     base = bytes.fromhex(corrupt["base"])
     checked = gaps = 0
     for c in corrupt["cases"]:

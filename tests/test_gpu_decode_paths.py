@@ -1,9 +1,10 @@
 """Every decode path for small updates gives the same bytes.
 
 Small updates (<= 16 KiB) are parsed one lane per update (k_direct) when there are many, one
-wavefront per update (k_wdecode: chunk chains per lane settled inside the wavefront, an exact
-lane-0 walk otherwise) when there are few; large ones take the chunk path (k_spec / k_sync /
-k_walk). The modes force one: "direct" = k_direct, "wave" = k_wdecode, "chunks" = the chunk path.
+workgroup per update when there are few (k_wlen steps every position, k_wrank ranks each section's
+chain by pointer doubling; or, YCRDT_WDECODE=settle, k_wdecode: chunk chains per lane settled
+inside a wavefront); large ones take the chunk path (k_spec / k_sync / k_walk). The modes force
+one: "direct" = k_direct, "wave" = k_wlen + k_wrank, "settle" = k_wdecode, "chunks" = the chunk path.
 All must match the Yjs fixtures and the oracle byte for byte, and report the same malformed input.
 """
 import pytest
@@ -11,13 +12,16 @@ import pytest
 crdt_amd = pytest.importorskip("crdt_amd")
 
 pytestmark = pytest.mark.gpu
-MODES = ("chunks", "direct", "wave")
+MODES = ("chunks", "direct", "wave", "settle")
 
 
 def _mode(monkeypatch, mode):
-    monkeypatch.setenv("YCRDT_DECODE", "direct" if mode == "wave" else mode)
-    if mode in ("wave", "direct"):
-        monkeypatch.setenv("YCRDT_DIRECT_WAVE", "1" if mode == "wave" else "0")
+    # wave: few small updates ranked (k_wlen + k_wrank); settle: k_wdecode's settled chains
+    wave = mode in ("wave", "settle")
+    monkeypatch.setenv("YCRDT_DECODE", "direct" if wave else mode)
+    if mode != "chunks":
+        monkeypatch.setenv("YCRDT_DIRECT_WAVE", "1" if wave else "0")
+    monkeypatch.setenv("YCRDT_WDECODE", "settle" if mode == "settle" else "rank")
 
 
 @pytest.mark.parametrize("mode", MODES)

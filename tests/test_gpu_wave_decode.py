@@ -24,10 +24,12 @@ pytestmark = pytest.mark.gpu
 WAVE_MAX = 16384  # DIRECT_MAX_BYTES: larger updates take the chunk path
 
 
-@pytest.fixture
-def wave(monkeypatch):
+@pytest.fixture(params=["rank", "settle"])
+def wave(monkeypatch, request):
+    """Few small updates: ranked (k_wlen + k_wrank, the default) or k_wdecode's settled chains."""
     monkeypatch.setenv("YCRDT_DECODE", "direct")
     monkeypatch.setenv("YCRDT_DIRECT_WAVE", "1")
+    monkeypatch.setenv("YCRDT_WDECODE", request.param)
     monkeypatch.setenv("YCRDT_DEBUG_DECODE", "1")
     yield
 
