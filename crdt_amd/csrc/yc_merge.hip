@@ -219,7 +219,9 @@ __global__ void k_scatter_seg(Work w, uint32_t nwords, uint64_t nunits) {
 }
 // Small batches: the cut words, their popcount prefix and the segment starts in ONE workgroup launch
 // (three otherwise); a wavefront takes 64 consecutive units at a time, as in k_cuts
-constexpr uint32_t SEG_LANES = 1024, SEG_SMALL_WORDS = SEG_LANES * 16 - 1;
+// (up to 16 K units: a unit's cut test gathers several columns, so one workgroup is only worth it
+// while each lane takes a few units — a 900 K-unit C2 document spent 1 ms in it)
+constexpr uint32_t SEG_LANES = 1024, SEG_SMALL_WORDS = 256;
 __global__ __launch_bounds__(SEG_LANES) void k_segments_small(Work w, uint64_t nunits) {
   __shared__ uint32_t part[SEG_LANES];
   const uint32_t nwords = (uint32_t)((nunits + 63) / 64);
