@@ -1567,14 +1567,33 @@ void launch_chunks(const Work& w, hipStream_t s) {
 // is the exact walk's (the same step function from the same start), without its latency: a
 // wavefront walking a 9 KB per-op doc state struct by struct (k_wdecode's chains and their
 // settling) took 0.5-0.8 ms, one struct step being ~1 000 dependent instructions on one SIMD.
+// A workgroup takes WL_SPAN positions: those whose info byte names no struct kind (ref > 10: no
+// struct parses there, chain_len's 0) are settled by one byte test, the rest are gathered in LDS
+// and sized by full wavefronts (the sizer is VALU-bound, ~1 500 instructions a position: a
+// wavefront with a few live lanes costs as much as a full one).
+constexpr uint32_t WL_SPAN = 1024;
 __global__ __launch_bounds__(256) void k_wlen(Work w) {
+  __shared__ uint16_t cand[WL_SPAN];
+  __shared__ uint32_t ncand;
   const uint32_t j = blockIdx.y;
   const uint32_t u = w.ulist[w.nbig + j];
   const uint32_t ustart = w.uoff[u], L = w.ulen[u];
-  const uint32_t k = blockIdx.x * 256 + threadIdx.x;
-  if (k >= L || L > WD_MAX) return;
+  const uint32_t k0 = blockIdx.x * WL_SPAN;
+  if (k0 >= L || L > WD_MAX) return;
   const uint8_t* __restrict__ b = win_bytes(w, upd_win(w, u));
-  w.wlen[(size_t)j * WD_MAX + k] = (uint16_t)chain_len(GlobalSrc{b}, b, ustart + k, ustart + L);
+  uint16_t* __restrict__ out = w.wlen + (size_t)j * WD_MAX;
+  if (threadIdx.x == 0) ncand = 0;
+  __syncthreads();
+  for (uint32_t k = k0 + threadIdx.x; k < min(L, k0 + WL_SPAN); k += 256) {
+    if ((b[ustart + k] & 31u) <= REF_SKIP) cand[atomicAdd(&ncand, 1u)] = (uint16_t)(k - k0);
+    else out[k] = 0;
+  }
+  __syncthreads();
+  const uint32_t nc = ncand;
+  for (uint32_t i = threadIdx.x; i < nc; i += 256) {
+    const uint32_t k = k0 + cand[i];
+    out[k] = (uint16_t)chain_len(GlobalSrc{b}, b, ustart + k, ustart + L);
+  }
 }
 constexpr uint32_t WR_LANES = 1024;
 constexpr uint16_t WR_INF = 0xFFFFu;
@@ -1693,7 +1712,7 @@ void launch_direct(const Work& w, hipStream_t s) {
   // (a split decode's share may take this path where the whole batch did not: no rank tables)
   if (wave_decode(w) && ((wm && !strcmp(wm, "settle")) || !w.wlen)) hipLaunchKernelGGL(k_wdecode, dim3(w.nsmall), dim3(64), 0, s, w);
   else if (wave_decode(w)) {
-    hipLaunchKernelGGL(k_wlen, dim3(WD_MAX / 256, w.nsmall), dim3(256), 0, s, w);
+    hipLaunchKernelGGL(k_wlen, dim3(WD_MAX / WL_SPAN, w.nsmall), dim3(256), 0, s, w);
     hipLaunchKernelGGL(k_wrank, dim3(w.nsmall), dim3(WR_LANES), 0, s, w);
   } else if (w.nsmall) hipLaunchKernelGGL(k_direct, dim3((w.nsmall + DL - 1) / DL), dim3(DL), 0, s, w);
 }
