@@ -1568,10 +1568,19 @@ void launch_chunks(const Work& w, hipStream_t s) {
 // wavefront walking a 9 KB per-op doc state struct by struct (k_wdecode's chains and their
 // settling) took 0.5-0.8 ms, one struct step being ~1 000 dependent instructions on one SIMD.
 // A workgroup takes WL_SPAN positions: those whose info byte names no struct kind (ref > 10: no
-// struct parses there, chain_len's 0) are settled by one byte test, the rest are gathered in LDS
-// and sized by full wavefronts (the sizer is VALU-bound, ~1 500 instructions a position: a
-// wavefront with a few live lanes costs as much as a full one).
+// struct parses there, chain_len's 0) are settled by one byte test; those naming a rare kind
+// (JSON, Binary, Embed, Format, Doc) are left unevaluated (WL_LATER: k_wrank sizes them all when a
+// chain reaches one); the rest are gathered in LDS and sized by full wavefronts (the sizer is
+// VALU-bound, ~1 500 instructions a position: a wavefront with a few live lanes costs as much as a
+// full one). The common kinds — GC, Deleted, String, Type, Any, Skip — are 34 of the 256 byte
+// values (ref <= 10: 88).
 constexpr uint32_t WL_SPAN = 1024;
+constexpr uint16_t WL_LATER = 0xFFFFu;  // (a length is at most 16 384)
+__device__ __forceinline__ uint32_t wl_class(uint32_t info) {  // 0: no struct, 1: common kind, 2: rare kind
+  const uint32_t ref = info & 31u;
+  if (ref > REF_SKIP) return 0u;
+  return ((1u << REF_GC) | (1u << REF_DELETED) | (1u << REF_STRING) | (1u << REF_TYPE) | (1u << REF_ANY) | (1u << REF_SKIP)) >> ref & 1u ? 1u : 2u;
+}
 __global__ __launch_bounds__(256) void k_wlen(Work w) {
   __shared__ uint16_t cand[WL_SPAN];
   __shared__ uint32_t ncand;
@@ -1585,8 +1594,9 @@ __global__ __launch_bounds__(256) void k_wlen(Work w) {
   if (threadIdx.x == 0) ncand = 0;
   __syncthreads();
   for (uint32_t k = k0 + threadIdx.x; k < min(L, k0 + WL_SPAN); k += 256) {
-    if ((b[ustart + k] & 31u) <= REF_SKIP) cand[atomicAdd(&ncand, 1u)] = (uint16_t)(k - k0);
-    else out[k] = 0;
+    const uint32_t c = wl_class(b[ustart + k]);
+    if (c == 1u) cand[atomicAdd(&ncand, 1u)] = (uint16_t)(k - k0);
+    else out[k] = c ? WL_LATER : 0;
   }
   __syncthreads();
   const uint32_t nc = ncand;
@@ -1598,7 +1608,9 @@ __global__ __launch_bounds__(256) void k_wlen(Work w) {
 constexpr uint32_t WR_LANES = 1024;
 constexpr uint16_t WR_INF = 0xFFFFu;
 __global__ __launch_bounds__(WR_LANES) void k_wrank(Work w) {
-  __shared__ uint16_t ja[WD_MAX + 2], jb[WD_MAX + 2], dist[WD_MAX + 2];  // [L]: the update end, [L + 1]: no struct parses
+  // [L]: the update end, [L + 1]: no struct parses, [L + 2]: a position k_wlen left unevaluated
+  __shared__ uint16_t ja[WD_MAX + 3], jb[WD_MAX + 3], dist[WD_MAX + 3];
+  __shared__ uint32_t sh_later;
   __shared__ uint64_t bits[WD_WORDS];
   __shared__ uint32_t sh_base, sh_last;
   const uint32_t t = threadIdx.x, j = blockIdx.x;
@@ -1608,7 +1620,8 @@ __global__ __launch_bounds__(WR_LANES) void k_wrank(Work w) {
   uint64_t* __restrict__ fbits = win_words(w.final_bits, uw);
   uint64_t* __restrict__ sbits = win_words(w.sec_bits, uw);
   const uint32_t ustart = w.uoff[u], L = w.ulen[u], uend = ustart + L;
-  const uint16_t* __restrict__ dl = w.wlen + (size_t)j * WD_MAX;
+  uint16_t* __restrict__ dl = w.wlen + (size_t)j * WD_MAX;
+  bool sized = false;  // every position sized (the rare kinds too)
   uint32_t* err = &w.ctr->err;
   if (L > WD_MAX) { if (t == 0) raise_err(err, ERR_CAPACITY); return; }  // (the layout never sends one)
   bool ok = true;
@@ -1633,11 +1646,12 @@ __global__ __launch_bounds__(WR_LANES) void k_wrank(Work w) {
       if (n) atomicOr((unsigned long long*)&sbits[q >> 6], 1ull << (q & 63));
     }
     if (!n) continue;
-    // jump tables: ja = one chain step (the end and "no struct" are sinks), distances unknown
+  rank:
+    // jump tables: ja = one chain step (the end, "no struct" and "not sized" are sinks)
     const uint32_t q1 = q - ustart;
-    for (uint32_t i = t; i < L + 2; i += WR_LANES) {
+    for (uint32_t i = t; i < L + 3; i += WR_LANES) {
       uint32_t x = i;
-      if (i < L) { const uint32_t d = dl[i]; x = !d ? L + 1 : min(i + d, L); }
+      if (i < L) { const uint32_t d = dl[i]; x = d == WL_LATER ? L + 2 : !d ? L + 1 : min(i + d, L); }
       ja[i] = (uint16_t)x;
       dist[i] = i == q1 ? 0 : WR_INF;
     }
@@ -1653,7 +1667,7 @@ __global__ __launch_bounds__(WR_LANES) void k_wrank(Work w) {
       }
       __syncthreads();
       if (2 * step < n) {
-        for (uint32_t i = t; i < L + 2; i += WR_LANES) B[i] = A[A[i]];
+        for (uint32_t i = t; i < L + 3; i += WR_LANES) B[i] = A[A[i]];
         __syncthreads();
         uint16_t* x = A; A = B; B = x;
       }
@@ -1663,13 +1677,22 @@ __global__ __launch_bounds__(WR_LANES) void k_wrank(Work w) {
     __syncthreads();
     for (uint32_t i = t; i < L; i += WR_LANES)
       if (dist[i] == n - 1) sh_last = i;
+    __syncthreads();
+    const uint32_t last = sh_last;
+    if (!sized && (dist[L + 2] != WR_INF || (last != NONE && dl[last] == WL_LATER))) {
+      // the chain reaches a rare struct kind: size every position left unevaluated, rank again
+      for (uint32_t i = t; i < L; i += WR_LANES)
+        if (dl[i] == WL_LATER) dl[i] = (uint16_t)chain_len(GlobalSrc{b}, b, ustart + i, uend);
+      sized = true;
+      __syncthreads();
+      goto rank;
+    }
     for (uint32_t k = t; k < nw; k += WR_LANES) {
       uint64_t m = 0;
       for (uint32_t x = 0; x < 64 && k * 64 + x < L; ++x) m |= (uint64_t)(dist[k * 64 + x] < n) << x;
       bits[k] |= m;
     }
     __syncthreads();
-    const uint32_t last = sh_last;
     const bool sunk = dist[L] != WR_INF || dist[L + 1] != WR_INF;
     if (!sunk && last != NONE && dl[last]) {
       q = ustart + last + dl[last];

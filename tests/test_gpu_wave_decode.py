@@ -176,3 +176,43 @@ def test_wave_fuzz_mixed_shapes(wave, capfd):
         _check(ups, capfd)
         total += len(ups)
     assert total > 100
+
+
+def _vs(s):
+    b = s.encode()
+    return bytes([len(b)]) + b
+
+
+def _rare_kinds_update(reps):
+    """One section of client 5: runs of Format / String / Embed / JSON / Binary items (the content
+    kinds k_wlen leaves unsized until a chain reaches one) behind a common Any item, reps times."""
+    out, clock, prev = [], 0, None
+
+    def item(ref, content, length):
+        nonlocal clock, prev
+        if prev is None:
+            s = bytes([ref]) + b"\x01" + _vs("t") + content  # under the root type "t"
+        else:
+            s = bytes([0x80 | ref, 5, prev]) + content         # origin: (5, prev)
+        out.append(s)
+        clock += length
+        prev = clock - 1
+
+    for r in range(reps):
+        item(8, b"\x01\x7d" + bytes([r % 60]), 1)            # Any: one varInt
+        item(6, _vs("bold") + _vs("true"), 1)                # Format
+        item(4, _vs("hello"), 5)                             # String
+        item(5, _vs('{"x":1}'), 1)                           # Embed
+        item(2, b"\x01" + _vs('"j"'), 1)                     # JSON, one value
+        item(3, b"\x03abc", 1)                               # Binary
+    assert clock < 128  # (one-byte clocks above)
+    return bytes([1, len(out), 5, 0]) + b"".join(out) + b"\x00"
+
+
+def test_wave_rare_content_kinds(wave, capfd):
+    """Rare content kinds on the chain: the ranked path sizes the positions it skipped, ranks again."""
+    for reps in (1, 3, 8):
+        _check([_rare_kinds_update(reps)], capfd)
+        extra = ODoc(9)
+        extra.map_set("users", "k1", any_int(reps))
+        _check([_rare_kinds_update(reps), extra.encode_state_as_update()], capfd)
