@@ -11,6 +11,7 @@
 #include <unordered_map>
 #include <algorithm>
 #include <memory>
+#include <functional>
 
 #include "yc_work.h"
 #include "yc_host.h"
@@ -197,6 +198,7 @@ struct Pinned {
   size_t cap = 0;
   hipEvent_t ev[2] = {nullptr, nullptr};
 };
+constexpr uint64_t PIN_SV = uint64_t(1) << 20;  // pinned state-vector read-back of a small merge
 struct ycrdt_engine {
   int device = 0;
   int compat = 136;
@@ -220,8 +222,13 @@ struct ycrdt_engine {
   // pinned read-back areas of the sync points (a copy into pageable memory goes through the
   // runtime's staging: ~20-30 us per copy on the per-op path): the counters, and a small view
   Counters* ctr_pin = nullptr;
+  uint8_t* sv_pin = nullptr;  // [PIN_SV] a small merge's state vector
   uint8_t* rb = nullptr;
   size_t rb_cap = 0;
+  // commit_merge's copies (the merged state into the doc's block, the state vector out), queued by
+  // run_merge before its last synchronisation so that one wait covers the merge and the copies
+  // (cap_out, cap_sv: the bounds the outputs were sized by)
+  const std::function<int(uint64_t cap_out, uint64_t cap_sv)>* before_final = nullptr;
   hipStream_t copy = nullptr;  // batch staging (host → HBM)
   hipEvent_t copy_dep = nullptr;
   // result of the last merge (e->w.out / e->w.sv_out): ws_owner is the batch that produced it
@@ -254,6 +261,7 @@ struct ycrdt_doc {
   ycrdt_engine* e = nullptr;
   uint32_t client_id = 0;
   DevBuf state;          // canonical encoded state (Yjs v1 update) in HBM
+  DevBuf spare;          // the previous state's block, reused by the next folded merge (commit_merge)
   size_t state_len = 0;  // 0 = empty doc
   std::vector<uint8_t> sv;
   ycrdt_merge_stats last{};
@@ -1272,6 +1280,8 @@ int run_merge(ycrdt_engine* e, ycrdt_batch* b, const std::unordered_map<uint32_t
   launch_encode_write(w, nsegs, nclients, s);
   mark(e, "end");
   HIPCHK(hipEventRecord(e->ev1, s));
+  if (e->before_final)
+    if (const int r = (*e->before_final)(w.cap_out, w.cap_sv)) return r;
   rc = check(e, c, "merge / encode");
   if (rc) return rc;
   nout = nsegs ? c.nout : 0;
@@ -1820,6 +1830,7 @@ void ycrdt_engine_destroy(ycrdt_engine* e) {
     if (pin->p) hipHostFree(pin->p);
   }
   if (e->ctr_pin) hipHostFree(e->ctr_pin);
+  if (e->sv_pin) hipHostFree(e->sv_pin);
   if (e->rb) hipHostFree(e->rb);
   hipEventDestroy(e->copy_dep);
   hipStreamDestroy(e->copy);
@@ -1887,6 +1898,7 @@ void ycrdt_doc_destroy(ycrdt_doc* d) {
   hipSetDevice(d->e->device);
   if (d->e->ws_owner == d) d->e->ws_owner = nullptr;
   if (d->state.p) { if (d->state.arena) d->e->arena.release(d->state.p, d->state.cap); else hipFree(d->state.p); }
+  if (d->spare.p) { if (d->spare.arena) d->e->arena.release(d->spare.p, d->spare.cap); else hipFree(d->spare.p); }
   delete d;
 }
 
@@ -1903,22 +1915,63 @@ int commit_merge(ycrdt_doc* d, const std::vector<ycrdt_buf>& extra, const ClockM
   ycrdt_engine* e = d->e;
   ycrdt_batch& b = scratch_batch(e);  // engine-owned: no hipMalloc / hipFree per call
   int rc = stage(&b, extra.data(), extra.size(), d->state_len ? &d->state : nullptr, d->state_len);
-  if (rc == YCRDT_OK) rc = run_merge(e, &b, nullptr, caps, order);
-  if (rc) return rc;
-  // the merged state goes to a block of its own (or the doc's, when it fits and is not the
-  // source of this merge any more: the batch holds a copy); the doc changes only once it is there
+  // The merged state goes to a block of its own (or the doc's, when it fits and is not the source
+  // of this merge any more: the batch holds a copy once staged); the doc changes only once it is
+  // there. A small merge queues the copies before its last synchronisation (run_merge's
+  // before_final) — its output bound, not yet its size, is known then: the bound is copied.
+  constexpr uint64_t FOLD_MAX = uint64_t(4) << 20;
   DevBuf nb = d->state;
-  const bool fresh = e->out_bytes + 16 > d->state.cap;
-  if (fresh && !alloc_state(e, nb, e->out_bytes + 16)) return fail(YCRDT_E_DEVICE, oom("doc state"));
-  std::vector<uint8_t> sv(e->sv_bytes);
-  hipError_t er = hipMemcpyAsync(nb.p, e->w.out, e->out_bytes, hipMemcpyDeviceToDevice, e->stream);
-  if (er == hipSuccess && !sv.empty()) er = hipMemcpyAsync(sv.data(), e->w.sv_out, e->sv_bytes, hipMemcpyDeviceToHost, e->stream);
-  if (er == hipSuccess) er = hipStreamSynchronize(e->stream);
-  if (er != hipSuccess) {
-    if (fresh) release_state(e, nb);
-    return fail(YCRDT_E_DEVICE, std::string("HIP error: ") + hipGetErrorString(er) + " (doc state copy)");
+  bool fresh = false, folded = false;
+  const std::function<int(uint64_t, uint64_t)> fold = [&](uint64_t cap_out, uint64_t cap_sv) -> int {
+    if (cap_out > FOLD_MAX || cap_sv > PIN_SV) return YCRDT_OK;
+    if (!e->sv_pin && hipHostMalloc((void**)&e->sv_pin, PIN_SV, hipHostMallocDefault) != hipSuccess) {
+      (void)hipGetLastError();
+      e->sv_pin = nullptr;
+      return YCRDT_OK;  // (the copies after the merge)
+    }
+    // never the doc's own block (the merge may still fail at its last check, and the doc's state
+    // must then be what it was): the spare block when it is large enough, else a new one
+    fresh = true;
+    if (d->spare.p && d->spare.cap >= cap_out + 16) { nb = d->spare; d->spare = DevBuf(); }
+    else if (!alloc_state(e, nb, cap_out + 16)) return fail(YCRDT_E_DEVICE, oom("doc state"));
+    HIPCHK(hipMemcpyAsync(nb.p, e->w.out, cap_out, hipMemcpyDeviceToDevice, e->stream));
+    HIPCHK(hipMemcpyAsync(e->sv_pin, e->w.sv_out, cap_sv, hipMemcpyDeviceToHost, e->stream));
+    folded = true;
+    return YCRDT_OK;
+  };
+  static const bool nofold = getenv("YCRDT_NO_FOLD") && getenv("YCRDT_NO_FOLD")[0] == '1';  // (A/B)
+  if (rc == YCRDT_OK) {
+    e->before_final = nofold ? nullptr : &fold;
+    rc = run_merge(e, &b, nullptr, caps, order);
+    e->before_final = nullptr;
   }
-  if (fresh) { release_state(e, d->state); d->state = nb; }
+  if (rc) {
+    if (fresh && !d->spare.p) d->spare = nb;  // (kept for the next merge)
+    else if (fresh) release_state(e, nb);
+    return rc;
+  }
+  std::vector<uint8_t> sv(e->sv_bytes);
+  if (folded) {
+    if (!sv.empty()) memcpy(sv.data(), e->sv_pin, e->sv_bytes);
+  } else {
+    fresh = e->out_bytes + 16 > d->state.cap;
+    if (fresh && !alloc_state(e, nb, e->out_bytes + 16)) return fail(YCRDT_E_DEVICE, oom("doc state"));
+    hipError_t er = hipMemcpyAsync(nb.p, e->w.out, e->out_bytes, hipMemcpyDeviceToDevice, e->stream);
+    if (er == hipSuccess && !sv.empty()) er = hipMemcpyAsync(sv.data(), e->w.sv_out, e->sv_bytes, hipMemcpyDeviceToHost, e->stream);
+    if (er == hipSuccess) er = hipStreamSynchronize(e->stream);
+    if (er != hipSuccess) {
+      if (fresh) release_state(e, nb);
+      return fail(YCRDT_E_DEVICE, std::string("HIP error: ") + hipGetErrorString(er) + " (doc state copy)");
+    }
+  }
+  if (fresh && folded) {  // the old block becomes the spare
+    release_state(e, d->spare);
+    d->spare = d->state;
+    d->state = nb;
+  } else if (fresh) {
+    release_state(e, d->state);
+    d->state = nb;
+  }
   d->state_len = e->out_bytes;
   d->sv.swap(sv);
   d->last = e->last;
