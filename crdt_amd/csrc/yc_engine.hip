@@ -177,7 +177,7 @@ enum Buf {
   B_UOWN, B_UFLAG, B_UMIN, B_UCUT, B_UWPRE,
   B_GSTART, B_GCIDX, B_GSRC, B_GFLAGS, B_GORIG, B_GRORIG, B_GLINK, B_GOSEG, B_GKEY, B_GMAXC, B_GNEXT, B_GOUTID, B_GTMP, B_GTMP2,
   B_KHASH, B_KROOT, B_KWIN, B_KPAR, B_KFLAG, B_SPK,
-  B_USEC, B_USECN, B_DBG, B_XTAB, B_UFAIL, B_FW, B_CCNT, B_TENTRY, B_XLIST, B_WLEN,
+  B_USEC, B_USECN, B_DBG, B_XTAB, B_UFAIL, B_FW, B_CCNT, B_TENTRY, B_XLIST, B_WLEN, B_FWSEC, B_UNSYNC,
   B_LZKEY, B_LZKEYS, B_LZIOTA, B_LZSEC, B_LZRSTART, B_LZPREV, B_LZFIRST, B_LZCAP, B_LZEVBASE, B_LZEVN, B_LZFLAG,
   B_LZLHI, B_LZLLO, B_EVKIND, B_EVSRC, B_EVCLOCK, B_EVLEN, B_EVSIZE, B_EVPOS, B_BLKSIZE, B_BLKPOS, B_SVC, B_SVK,
   B_DSMKEY, B_DSMKEYS, B_DSMLEN, B_DSMLENS, B_DSMEND, B_DSMMAX, B_DSMFLAG, B_DSMRID, B_DRCLIENT, B_DRCLOCK, B_DREND,
@@ -831,6 +831,7 @@ int run_decode(ycrdt_engine* e, ycrdt_batch* b, bool lazy, Decoded& D, bool gene
   w.tentry = take<uint32_t>(V, B_TENTRY, (uint64_t)w.ngroups + 1, ok);
   w.xlist = take<uint32_t>(V, B_XLIST, (uint64_t)w.ngroups + 1, ok);
   w.ufail = take<uint32_t>(V, B_UFAIL, nu + 1, ok);
+  w.unsync = take<uint32_t>(V, B_UNSYNC, nu + 1, ok);
   w.fw = take<uint32_t>(V, B_FW, 2ull * nu + 2, ok);
   w.ccnt = take<uint32_t>(V, B_CCNT, (uint64_t)w.ngroups + 1, ok);
   w.final_bits = take<uint64_t>(V, B_FINAL, nwords, ok);
@@ -848,6 +849,7 @@ int run_decode(ycrdt_engine* e, ycrdt_batch* b, bool lazy, Decoded& D, bool gene
   w.usec_start = take<uint32_t>(V, B_USEC, nu + 1, ok);
   w.usec_n = take<uint32_t>(V, B_USECN, nu + 1, ok);
   w.wlen = wave_decode(w) ? take<uint16_t>(V, B_WLEN, (uint64_t)w.nsmall * 16384, ok) : nullptr;
+  w.fwsec = w.nbig ? take<uint32_t>(V, B_FWSEC, 2ull * w.cap_sections + 2, ok) : nullptr;
   if (!ok) return fail(YCRDT_E_DEVICE, oom("decode workspace"));
   // rocPRIM scratch sized for the largest scan of this batch (units may grow it later)
   {
@@ -861,6 +863,7 @@ int run_decode(ycrdt_engine* e, ycrdt_batch* b, bool lazy, Decoded& D, bool gene
   static_assert(sizeof(Counters) % 4 == 0, "counters are filled as words");
   fill_u32_multi({{(uint32_t*)w.ctr, sizeof(Counters) / 4, 0u},
                   {w.ufail, (uint64_t)nu + 1, 0u},
+                  {w.unsync, (uint64_t)nu + 1, 0u},
                   {w.usec_n, (uint64_t)nu + 1, 0u},  // an update no walker reached has no sections
                   {(uint32_t*)w.final_bits, (uint64_t)nwords * 2, 0u},
                   {(uint32_t*)w.sec_bits, (uint64_t)nwords * 2, 0u}}, s);

@@ -3,7 +3,7 @@
 set -u
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-timeout -s KILL 300 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/c3trace -o c4 -- python3 scripts/probe_c3.py 10000000 256 16 > gpurun_out/c3trace.log 2>&1 || exit 1
+YCRDT_DEBUG_DECODE=1 timeout -s KILL 300 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/c3trace -o c4 -- python3 scripts/probe_c3.py 10000000 256 16 > gpurun_out/c3trace.log 2>&1 || exit 1
 python3 - <<'PY'
 import csv, glob
 f = glob.glob("gpurun_out/c3trace/**/*kernel_trace.csv", recursive=True)[0]
@@ -18,3 +18,4 @@ out.close()
 PY
 grep -E "k_spec|k_sync|k_walk|k_fastwalk|k_fastmark|k_chunk_counts|k_xtab|k_xmark|k_ds_decode|k_direct|k_wlen|k_wrank" gpurun_out/c3trace_last.txt | head -30
 rm -rf gpurun_out/c3trace
+grep "ycrdt decode" gpurun_out/c3trace.log | sort | uniq -c | head
