@@ -1125,8 +1125,10 @@ __global__ __launch_bounds__(64) void k_fastwalk(Work w) {
   if (!ok || n == 0 || n > uend - p) return;
   const uint32_t p1 = p, ce0 = min(ustart + CH, uend);
   if (p1 >= ce0) return;
-  // one chain through all chunks (k_chunk_counts)
-  if (w.unsync[u]) { why(2); return; }
+  // one chain through every chunk up to the one holding the last struct (k_chunk_counts: the first
+  // chunk whose entry may be off it — C4's replica updates each have one, past their structs)
+  const uint32_t bad = w.unsync[u];
+  if (bad == 0) { why(2); return; }
   // chunk 0: the exact walk from the first struct until it meets chunk 0's chain
   for (uint32_t k = lane; k < SW + 2; k += 64) walked[k] = 0;
   __syncthreads();
@@ -1171,6 +1173,7 @@ __global__ __launch_bounds__(64) void k_fastwalk(Work w) {
     }
   }
   if (fch == NONE) { why(4); return; }  // fewer chain positions than structs
+  if (fch >= bad) { why(2); return; }
   const uint32_t fcs = ustart + fch * CH, fa = fch == 0 ? q : fcs;
   const uint32_t Lp = select_from(spec, fa, rem);
   const uint32_t dsp = chain_step(b, Lp, uend);
@@ -1223,7 +1226,7 @@ __global__ __launch_bounds__(64) void k_fastwalk_multi(Work w) {
   const uint32_t u = w.ulist[blockIdx.x];
   const uint32_t lane = threadIdx.x;
   // (YCRDT_DEBUG_DECODE: updates left to k_walk, and why — bit r of the mask: reason r)
-  auto why = [&](uint32_t r) { if (w.dbg && lane == 0) { atomicAdd(&w.dbg[4], 1ull); atomicOr(&w.dbg[5], 1ull << r); } };
+  auto why = [&](uint32_t r) { if (w.dbg && lane == 0 && r != 2u) atomicAdd(&w.dbg[1], 1ull); };
   if (w.ufail[u] || !w.fwsec) return;
   const uint32_t uw = upd_win(w, u);
   const uint8_t* __restrict__ b = win_bytes(w, uw);
@@ -1239,7 +1242,7 @@ __global__ __launch_bounds__(64) void k_fastwalk_multi(Work w) {
   const uint32_t nsec = rd_vu(b, p, uend, ok);
   if (!ok || nsec < 2) return;
   if (nsec > FWM_MAX) { why(1); return; }
-  if (w.unsync[u]) { why(2); return; }  // (k_chunk_counts)
+  const uint32_t bad = w.unsync[u];  // (k_chunk_counts: chunks from here on may be off the chain)
   auto spec_bit = [&](uint32_t q) { return (spec[q >> 6] >> (q & 63)) & 1ull; };
   // pass 1 (every value below is the same in every lane)
   for (uint32_t s = 0; s < nsec; ++s) {
@@ -1292,6 +1295,7 @@ __global__ __launch_bounds__(64) void k_fastwalk_multi(Work w) {
           }
         }
         if (fch == NONE) { why(6); return; }  // fewer chain positions than structs
+        if (fch >= bad) { why(2); return; }
         const uint32_t fa = fch == jq ? q : ustart + fch * CH;
         const uint32_t Lp = select_from(spec, fa, rem);
         const uint32_t dl = Lp < uend ? chain_len(GlobalSrc{b}, b, Lp, uend) : 0u;
@@ -1344,8 +1348,17 @@ __global__ __launch_bounds__(256) void k_chunk_counts(Work w) {
   if (i >= w.ngroups) return;
   const Group G = w.groups[i];
   w.ccnt[i] = popc_range(win_words(w.spec_bits, upd_win(w, G.upd)), G.start, G.end);
-  const bool fixed = (G.end >= G.uend || w.cexit[i] == w.sexit[i]) && (G.start == w.uoff[G.upd] || !w.sent[w.ngroups + 1 + i]);
-  if (!fixed) w.unsync[G.upd] = 1u;  // (plain stores of one value)
+  // (the first chunk, counted from the update's first, whose entry may not be on the one chain)
+  const uint32_t k = i - w.ugroup[G.upd];
+  const bool jumped = G.start != w.uoff[G.upd] && w.sent[w.ngroups + 1 + i];
+  const bool moved = G.end < G.uend && w.cexit[i] != w.sexit[i];
+  const bool fixed = !jumped && !moved;
+  if (jumped) atomicMin(&w.unsync[G.upd], k);
+  if (moved) atomicMin(&w.unsync[G.upd], k + 1);
+  if (!fixed && w.dbg) {  // (YCRDT_DEBUG_DECODE, printed as the wave path's "unsettled" / "other")
+    if (G.end < G.uend && w.cexit[i] != w.sexit[i]) atomicAdd(&w.dbg[4], 1ull);
+    if (G.start != w.uoff[G.upd] && w.sent[w.ngroups + 1 + i]) atomicAdd(&w.dbg[5], 1ull);
+  }
 }
 
 // The chain-position words of the fast-walked updates past their first chunk, one lane per word

@@ -863,7 +863,7 @@ int run_decode(ycrdt_engine* e, ycrdt_batch* b, bool lazy, Decoded& D, bool gene
   static_assert(sizeof(Counters) % 4 == 0, "counters are filled as words");
   fill_u32_multi({{(uint32_t*)w.ctr, sizeof(Counters) / 4, 0u},
                   {w.ufail, (uint64_t)nu + 1, 0u},
-                  {w.unsync, (uint64_t)nu + 1, 0u},
+                  {w.unsync, (uint64_t)nu + 1, NONE},
                   {w.usec_n, (uint64_t)nu + 1, 0u},  // an update no walker reached has no sections
                   {(uint32_t*)w.final_bits, (uint64_t)nwords * 2, 0u},
                   {(uint32_t*)w.sec_bits, (uint64_t)nwords * 2, 0u}}, s);

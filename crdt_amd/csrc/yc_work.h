@@ -84,7 +84,7 @@ struct Work {
   uint32_t ndocs = 1;
   const uint32_t* ulist = nullptr; // [nbig] updates on the chunk path, then [nsmall] parsed directly
   uint32_t nbig = 0, nsmall = 0;
-  uint32_t* unsync = nullptr;      // [nupd] the update's synced chunk chains still disagree (k_chunk_counts)
+  uint32_t* unsync = nullptr;      // [nupd] first chunk (of the update's) whose entry may be off the one chain, NONE: none
   uint32_t* fwsec = nullptr;       // [2 cap_sections] k_fastwalk_multi: each section's chain range [q, e)
   uint16_t* wlen = nullptr;        // [nsmall * 16384] few small updates: the chain step at every position (k_wlen)
   uint32_t schunk = SCHUNK;        // chunk bytes of this batch's large updates (<= SCHUNK)
