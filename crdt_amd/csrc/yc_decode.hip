@@ -1099,6 +1099,7 @@ __global__ __launch_bounds__(64) void k_walk(Work w) {
 // the chunks (64 per wavefront round) and the struct-start words are copied in parallel. Anything
 // else (several sections, a chain that never meets, fewer chain positions than structs) is left
 // to k_walk, which also reports malformed input.
+constexpr uint32_t CC_OFF = 0x80000000u;  // ccnt: the chunk's entry may be off the one chain (k_chunk_counts)
 __global__ __launch_bounds__(64) void k_fastwalk(Work w) {
   __shared__ uint64_t walked[SW + 2];
   __shared__ uint32_t sh_q, sh_k0, sh_ok;
@@ -1125,10 +1126,8 @@ __global__ __launch_bounds__(64) void k_fastwalk(Work w) {
   if (!ok || n == 0 || n > uend - p) return;
   const uint32_t p1 = p, ce0 = min(ustart + CH, uend);
   if (p1 >= ce0) return;
-  // one chain through every chunk up to the one holding the last struct (k_chunk_counts: the first
-  // chunk whose entry may be off it — C4's replica updates each have one, past their structs)
-  const uint32_t bad = w.unsync[u];
-  if (bad == 0) { why(2); return; }
+  // one chain through every chunk up to the one holding the last struct (k_chunk_counts flags the
+  // chunks whose entry may be off it — C4's replica updates each have one, past their structs)
   // chunk 0: the exact walk from the first struct until it meets chunk 0's chain
   for (uint32_t k = lane; k < SW + 2; k += 64) walked[k] = 0;
   __syncthreads();
@@ -1149,14 +1148,16 @@ __global__ __launch_bounds__(64) void k_fastwalk(Work w) {
   const uint32_t q = sh_q, target = n - sh_k0;  // the target-th chain position from q is the last struct
   // the chunk holding it: per-chunk counts, scanned 64 chunks at a time
   uint32_t acc = 0, fch = NONE, rem = 0;
+  bool off_seen = false;  // an off-chain chunk after chunk 0, up to the last struct's
   for (uint32_t base = 0; base < nch && fch == NONE; base += 64) {
     const uint32_t j = base + lane;
     uint32_t cnt = 0;
+    bool offj = false;
     if (j < nch) {
       // (the chain positions of every chunk were counted grid-wide by k_chunk_counts; chunk 0
       // from q on here)
       if (j == 0) cnt = popc_range(spec, q, min(ustart + CH, uend));
-      else cnt = w.ccnt[c0 + j];
+      else { cnt = w.ccnt[c0 + j]; offj = (cnt & CC_OFF) != 0; cnt &= ~CC_OFF; }
     }
     uint32_t incl = cnt;
     for (uint32_t off = 1; off < 64; off <<= 1) {
@@ -1164,16 +1165,19 @@ __global__ __launch_bounds__(64) void k_fastwalk(Work w) {
       if (lane >= off) incl += v;
     }
     const uint64_t hit = __ballot(j < nch && acc + incl >= target && acc + incl - cnt < target);
+    const uint64_t offm = __ballot(offj);
     if (hit) {
       const uint32_t L = (uint32_t)__ffsll((long long)hit) - 1;
       fch = base + L;
       rem = target - (acc + __shfl(incl, L) - __shfl(cnt, L));
+      off_seen |= (offm & ((2ull << L) - 1)) != 0;
     } else {
       acc += __shfl(incl, 63);
+      off_seen |= offm != 0;
     }
   }
   if (fch == NONE) { why(4); return; }  // fewer chain positions than structs
-  if (fch >= bad) { why(2); return; }
+  if (off_seen) { why(2); return; }
   const uint32_t fcs = ustart + fch * CH, fa = fch == 0 ? q : fcs;
   const uint32_t Lp = select_from(spec, fa, rem);
   const uint32_t dsp = chain_step(b, Lp, uend);
@@ -1219,6 +1223,7 @@ __global__ __launch_bounds__(64) void k_fastwalk(Work w) {
 // ranges stay clear). C4's base snapshot (65 sections, 11 MB) took k_walk 2.3 ms; C3's merged
 // output (256 sections, 156 MB) 35 ms.
 constexpr uint32_t FWM_MAX = 1024;  // sections checked in LDS
+constexpr uint32_t FWM_WALK = 256;  // exact steps from a section's first struct to the chain, at most
 __global__ __launch_bounds__(64) void k_fastwalk_multi(Work w) {
   __shared__ uint32_t sp1[FWM_MAX], sn[FWM_MAX], scl[FWM_MAX], sck[FWM_MAX], sq[FWM_MAX], se[FWM_MAX], sk0[FWM_MAX];
   __shared__ uint32_t sh_sbase;
@@ -1226,7 +1231,7 @@ __global__ __launch_bounds__(64) void k_fastwalk_multi(Work w) {
   const uint32_t u = w.ulist[blockIdx.x];
   const uint32_t lane = threadIdx.x;
   // (YCRDT_DEBUG_DECODE: updates left to k_walk, and why — bit r of the mask: reason r)
-  auto why = [&](uint32_t r) { if (w.dbg && lane == 0 && r != 2u) atomicAdd(&w.dbg[1], 1ull); };
+  auto why = [&](uint32_t r) { if (w.dbg && lane == 0) { atomicAdd(&w.dbg[1], 1ull); atomicAdd(&w.dbg[8 + r], 1ull); } };
   if (w.ufail[u] || !w.fwsec) return;
   const uint32_t uw = upd_win(w, u);
   const uint8_t* __restrict__ b = win_bytes(w, uw);
@@ -1242,7 +1247,6 @@ __global__ __launch_bounds__(64) void k_fastwalk_multi(Work w) {
   const uint32_t nsec = rd_vu(b, p, uend, ok);
   if (!ok || nsec < 2) return;
   if (nsec > FWM_MAX) { why(1); return; }
-  const uint32_t bad = w.unsync[u];  // (k_chunk_counts: chunks from here on may be off the chain)
   auto spec_bit = [&](uint32_t q) { return (spec[q >> 6] >> (q & 63)) & 1ull; };
   // pass 1 (every value below is the same in every lane)
   for (uint32_t s = 0; s < nsec; ++s) {
@@ -1252,18 +1256,20 @@ __global__ __launch_bounds__(64) void k_fastwalk_multi(Work w) {
     uint32_t q = p1, k0 = 0, e = p1;
     if (n) {
       if (p1 >= uend) return;
-      // the exact walk (lane 0) until the chain, within the first struct's chunk
-      const uint32_t j1 = (p1 - ustart) / CH, ce1 = min(ustart + (j1 + 1) * CH, uend);
-      uint32_t bad = 0;
+      // the exact walk (lane 0) until it meets the chain: a section header breaks the chain's
+      // phase, and a section starting near a chunk's end meets it only in a later chunk (the true
+      // sequence and the chain take the same steps from any common position on)
+      uint32_t walk_bad = 0;
       if (lane == 0) {
-        while (q < ce1 && k0 < n && !spec_bit(q)) {
+        for (uint32_t steps = 0; q < uend && k0 < n && !spec_bit(q); ++steps) {
+          if (steps == FWM_WALK) { q = uend; break; }  // no meeting: left to k_walk (why 5)
           const uint32_t dq = chain_len(GlobalSrc{b}, b, q, uend);
-          if (!dq) { bad = 1; break; }  // no struct parses: k_walk reports it
+          if (!dq) { walk_bad = 1; break; }  // no struct parses: k_walk reports it
           q += dq;
           ++k0;
         }
       }
-      if (__shfl(bad, 0)) { why(4); return; }
+      if (__shfl(walk_bad, 0)) { why(4); return; }
       q = __shfl(q, 0);
       k0 = __shfl(k0, 0);
       if (k0 == n) {  // every struct walked: the section ends where the walk stopped
@@ -1272,30 +1278,38 @@ __global__ __launch_bounds__(64) void k_fastwalk_multi(Work w) {
         p = q;
         sq[s] = q;
       } else {
-        if (q >= ce1) { why(5); return; }  // no meeting inside the chunk
+        if (q >= uend) { why(5); return; }  // no meeting within FWM_WALK structs
         const uint32_t target = n - k0;
         const uint32_t jq = (q - ustart) / CH;
         uint32_t acc = 0, fch = NONE, rem = 0;
+        bool off_seen = false;  // an off-chain chunk after the meeting chunk, up to the last struct's
         for (uint32_t base = jq; base < nch && fch == NONE; base += 64) {
           const uint32_t j = base + lane;
           uint32_t cnt = 0;
-          if (j < nch) cnt = j == jq ? popc_range(spec, q, min(ustart + (jq + 1) * CH, uend)) : w.ccnt[c0 + j];
+          bool offj = false;
+          if (j < nch) {
+            if (j == jq) cnt = popc_range(spec, q, min(ustart + (jq + 1) * CH, uend));
+            else { cnt = w.ccnt[c0 + j]; offj = (cnt & CC_OFF) != 0; cnt &= ~CC_OFF; }
+          }
           uint32_t incl = cnt;
           for (uint32_t off = 1; off < 64; off <<= 1) {
             const uint32_t v = __shfl_up(incl, off);
             if (lane >= off) incl += v;
           }
           const uint64_t hit = __ballot(j < nch && acc + incl >= target && acc + incl - cnt < target);
+          const uint64_t offm = __ballot(offj);
           if (hit) {
             const uint32_t L = (uint32_t)__ffsll((long long)hit) - 1;
             fch = base + L;
             rem = target - (acc + __shfl(incl, L) - __shfl(cnt, L));
+            off_seen |= (offm & ((2ull << L) - 1)) != 0;
           } else {
             acc += __shfl(incl, 63);
+            off_seen |= offm != 0;
           }
         }
         if (fch == NONE) { why(6); return; }  // fewer chain positions than structs
-        if (fch >= bad) { why(2); return; }
+        if (off_seen) { why(2); return; }
         const uint32_t fa = fch == jq ? q : ustart + fch * CH;
         const uint32_t Lp = select_from(spec, fa, rem);
         const uint32_t dl = Lp < uend ? chain_len(GlobalSrc{b}, b, Lp, uend) : 0u;
@@ -1339,25 +1353,28 @@ __global__ __launch_bounds__(64) void k_fastwalk_multi(Work w) {
     if (w.dbg) atomicAdd(&w.dbg[0], 1ull);
   }
 }
-// per chunk: its chain positions, and whether the synced chains still disagree here (its exit was
-// not passed on unchanged, or its predecessor's chain jumped over it): then the update's chunk
-// chains are not one chain, and the fast walks leave it to k_walk (checked here grid-wide, not
-// chunk by chunk in the fast walk's wavefront: 0.7 ms on C4, 1.3 ms on a 150 MB state)
+// per chunk: its chain positions, and whether its entry may be off the one chain (CC_OFF): it was
+// entered past its end (its predecessor's chain jumped over it: it keeps a chain of its own), or
+// its predecessor's exit moved in the last sync round (it was walked from an older entry). A fast
+// walk trusts the chunk chains from its meeting point to its last struct only when no chunk after
+// the meeting chunk is off (checked per section, not per update: a multi-section snapshot's
+// headers, parsed as garbage, jump chunks in other sections)
+__device__ __forceinline__ bool chunk_moved(const Work& w, uint32_t i) {
+  const Group G = w.groups[i];
+  return G.end < G.uend && w.cexit[i] != w.sexit[i];
+}
 __global__ __launch_bounds__(256) void k_chunk_counts(Work w) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= w.ngroups) return;
   const Group G = w.groups[i];
-  w.ccnt[i] = popc_range(win_words(w.spec_bits, upd_win(w, G.upd)), G.start, G.end);
-  // (the first chunk, counted from the update's first, whose entry may not be on the one chain)
-  const uint32_t k = i - w.ugroup[G.upd];
-  const bool jumped = G.start != w.uoff[G.upd] && w.sent[w.ngroups + 1 + i];
-  const bool moved = G.end < G.uend && w.cexit[i] != w.sexit[i];
-  const bool fixed = !jumped && !moved;
-  if (jumped) atomicMin(&w.unsync[G.upd], k);
-  if (moved) atomicMin(&w.unsync[G.upd], k + 1);
-  if (!fixed && w.dbg) {  // (YCRDT_DEBUG_DECODE, printed as the wave path's "unsettled" / "other")
-    if (G.end < G.uend && w.cexit[i] != w.sexit[i]) atomicAdd(&w.dbg[4], 1ull);
-    if (G.start != w.uoff[G.upd] && w.sent[w.ngroups + 1 + i]) atomicAdd(&w.dbg[5], 1ull);
+  const uint32_t cnt = popc_range(win_words(w.spec_bits, upd_win(w, G.upd)), G.start, G.end);
+  const bool first = i == w.ugroup[G.upd];
+  const bool jumped = !first && w.sent[w.ngroups + 1 + i];
+  const bool moved = !first && chunk_moved(w, i - 1);
+  w.ccnt[i] = cnt | (jumped || moved ? CC_OFF : 0u);
+  if (w.dbg) {  // (YCRDT_DEBUG_DECODE, printed as the wave path's "unsettled" / "other")
+    if (moved) atomicAdd(&w.dbg[4], 1ull);
+    if (jumped) atomicAdd(&w.dbg[5], 1ull);
   }
 }
 
@@ -1711,7 +1728,8 @@ void launch_chunks(const Work& w, hipStream_t s) {
                          (const uint32_t*)(r & 1 ? w.sexit : w.cexit), r & 1 ? w.cexit : w.sexit, r);
   }
   if (w.nbig) {
-    static const bool nofast = getenv("YCRDT_NO_FASTWALK") && getenv("YCRDT_NO_FASTWALK")[0] == '1';
+    // (read per merge: tests compare the fast walks with k_walk alone)
+    const bool nofast = getenv("YCRDT_NO_FASTWALK") && getenv("YCRDT_NO_FASTWALK")[0] == '1';
     if (!nofast && !w.force_xtab) {
       hipLaunchKernelGGL(k_chunk_counts, dim3(w.ngroups / 256 + 1), dim3(256), 0, s, w);
       hipLaunchKernelGGL(k_fastwalk, dim3(w.nbig), dim3(64), 0, s, w);

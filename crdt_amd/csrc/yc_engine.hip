@@ -9,6 +9,7 @@
 #include <string>
 #include <vector>
 #include <unordered_map>
+#include <unordered_set>
 #include <algorithm>
 #include <memory>
 #include <functional>
@@ -239,6 +240,7 @@ struct ycrdt_engine {
   uint32_t nsegs = 0, nlists = 0;  // segments / YArray lists of the last merge (the view reads them)
   ycrdt_merge_stats last{};
   Arena arena;                      // doc states (alloc_state / release_state)
+  std::unordered_set<ycrdt_doc*> docs;  // live docs (ycrdt_engine_trim releases their spare blocks)
 };
 
 // a fresh doc state block of at least `bytes` (arena block, or its own hipMalloc when large)
@@ -831,7 +833,6 @@ int run_decode(ycrdt_engine* e, ycrdt_batch* b, bool lazy, Decoded& D, bool gene
   w.tentry = take<uint32_t>(V, B_TENTRY, (uint64_t)w.ngroups + 1, ok);
   w.xlist = take<uint32_t>(V, B_XLIST, (uint64_t)w.ngroups + 1, ok);
   w.ufail = take<uint32_t>(V, B_UFAIL, nu + 1, ok);
-  w.unsync = take<uint32_t>(V, B_UNSYNC, nu + 1, ok);
   w.fw = take<uint32_t>(V, B_FW, 2ull * nu + 2, ok);
   w.ccnt = take<uint32_t>(V, B_CCNT, (uint64_t)w.ngroups + 1, ok);
   w.final_bits = take<uint64_t>(V, B_FINAL, nwords, ok);
@@ -863,14 +864,13 @@ int run_decode(ycrdt_engine* e, ycrdt_batch* b, bool lazy, Decoded& D, bool gene
   static_assert(sizeof(Counters) % 4 == 0, "counters are filled as words");
   fill_u32_multi({{(uint32_t*)w.ctr, sizeof(Counters) / 4, 0u},
                   {w.ufail, (uint64_t)nu + 1, 0u},
-                  {w.unsync, (uint64_t)nu + 1, NONE},
                   {w.usec_n, (uint64_t)nu + 1, 0u},  // an update no walker reached has no sections
                   {(uint32_t*)w.final_bits, (uint64_t)nwords * 2, 0u},
                   {(uint32_t*)w.sec_bits, (uint64_t)nwords * 2, 0u}}, s);
   const bool dbg_yata = getenv("YCRDT_DEBUG_YATA") && getenv("YCRDT_DEBUG_YATA")[0] == '1';
   const bool dbg_dec = getenv("YCRDT_DEBUG_DECODE") && getenv("YCRDT_DEBUG_DECODE")[0] == '1';
-  w.dbg = dbg_yata || dbg_dec ? take<unsigned long long>(V, B_DBG, 8, ok) : nullptr;
-  if (w.dbg) HIPCHK(hipMemsetAsync(w.dbg, 0, 64, s));
+  w.dbg = dbg_yata || dbg_dec ? take<unsigned long long>(V, B_DBG, 16, ok) : nullptr;
+  if (w.dbg) HIPCHK(hipMemsetAsync(w.dbg, 0, 128, s));
   // ---- K1 decode
   // large updates (chunk path, mostly latency-bound) on the side stream, beside k_direct
   mark(e, "decode.direct");
@@ -906,11 +906,11 @@ int run_decode(ycrdt_engine* e, ycrdt_batch* b, bool lazy, Decoded& D, bool gene
   Counters c;
   int rc = check(e, c, "decode");
   if (dbg_dec && w.dbg) {  // experiments: why k_fastwalk left large updates to k_walk
-    unsigned long long h[8];
+    unsigned long long h[16];
     HIPCHK(hipMemcpy(h, w.dbg, sizeof(h), hipMemcpyDeviceToHost));
-    fprintf(stderr, "[ycrdt decode] fastwalk: done %llu nsec %llu unsynced %llu | wave: done %llu unsettled %llu other %llu | k_spec exact parses %llu (%llu bytes)\n",
-            h[0], h[1], h[2], h[3], h[4], h[5], h[6], h[7]);
-    HIPCHK(hipMemsetAsync(w.dbg, 0, 64, s));
+    fprintf(stderr, "[ycrdt decode] fastwalk: done %llu nsec %llu unsynced %llu | wave: done %llu unsettled %llu other %llu (chunk path: moved / jumped chunk entries) | k_spec exact parses %llu (%llu bytes) | multi-section left to k_walk, by reason 1-7: %llu %llu %llu %llu %llu %llu %llu\n",
+            h[0], h[1], h[2], h[3], h[4], h[5], h[6], h[7], h[9], h[10], h[11], h[12], h[13], h[14], h[15]);
+    HIPCHK(hipMemsetAsync(w.dbg, 0, 128, s));
   }
   if (rc == YCRDT_E_CAPACITY && !generous) return run_decode(e, b, lazy, D, true, sh);  // past the estimates
   if (rc) return rc;
@@ -1880,6 +1880,9 @@ int ycrdt_engine_trim(ycrdt_engine* e) {
   HIPCHK(hipStreamSynchronize(e->side));
   for (auto& b : e->bufs)
     if (b.p && !b.arena) { hipFree(b.p); b = DevBuf{}; }
+  // the docs' spare blocks (a folded merge keeps the previous state block, up to FOLD_MAX, for the
+  // next one: about twice the state bytes of every small doc until trimmed)
+  for (ycrdt_doc* d : e->docs) release_state(e, d->spare);
   e->ws_owner = nullptr;  // no doc's merge results are held any more: its next read merges again
   e->nsegs = 0;
   e->nlists = 0;
@@ -1892,6 +1895,7 @@ int ycrdt_doc_create(ycrdt_engine* e, uint32_t client_id, ycrdt_doc** out) {
   d->e = e;
   d->client_id = client_id;
   d->sv = {0};
+  e->docs.insert(d);
   *out = d;
   return YCRDT_OK;
 }
@@ -1902,6 +1906,7 @@ void ycrdt_doc_destroy(ycrdt_doc* d) {
   if (d->e->ws_owner == d) d->e->ws_owner = nullptr;
   if (d->state.p) { if (d->state.arena) d->e->arena.release(d->state.p, d->state.cap); else hipFree(d->state.p); }
   if (d->spare.p) { if (d->spare.arena) d->e->arena.release(d->spare.p, d->spare.cap); else hipFree(d->spare.p); }
+  d->e->docs.erase(d);
   delete d;
 }
 

@@ -175,7 +175,10 @@ YC_HDI uint64_t be64(const uint8_t* __restrict__ b, uint32_t p) { return ((uint6
 // writeAny(number) of a double: 0 varint, 1 float32, 2 float64, 3 refused (a negative integer
 // past 2^32, which writeVarInt's 32-bit arithmetic garbles)
 YC_HDI uint32_t num_form(double x) {
-  if (x == x && x == (double)(long long)x && x >= -9.2e18 && x <= 9.2e18) {  // an integer (finite)
+  // an integer (finite); the range test comes first: the cast of a NaN, an infinity or a magnitude
+  // past 2^63 is undefined (writeAny checks `data <= BITS31`, not |data|: tests/golden/anyform.json
+  // pins -2^31 - 1, -3e9 and -2^32 + 1 as varints)
+  if (x >= -9.2e18 && x <= 9.2e18 && x == (double)(long long)x) {
     if (x <= 2147483647.0) return x > -4294967296.0 ? 0u : 3u;
   }
   if (x != x) return 2u;  // NaN: float32 does not compare equal

@@ -84,7 +84,6 @@ struct Work {
   uint32_t ndocs = 1;
   const uint32_t* ulist = nullptr; // [nbig] updates on the chunk path, then [nsmall] parsed directly
   uint32_t nbig = 0, nsmall = 0;
-  uint32_t* unsync = nullptr;      // [nupd] first chunk (of the update's) whose entry may be off the one chain, NONE: none
   uint32_t* fwsec = nullptr;       // [2 cap_sections] k_fastwalk_multi: each section's chain range [q, e)
   uint16_t* wlen = nullptr;        // [nsmall * 16384] few small updates: the chain step at every position (k_wlen)
   uint32_t schunk = SCHUNK;        // chunk bytes of this batch's large updates (<= SCHUNK)
@@ -106,7 +105,7 @@ struct Work {
   uint32_t* xtab = nullptr;        // [G x XK] locked updates only, per entry offset: count << 16 | exit - chunk end
   uint32_t* tentry = nullptr;      // [G] locked updates: true entry of a chunk the table walk did not parse
   uint32_t* xlist = nullptr;       // [G] the chunks of the locked updates (k_xtab / k_xmark work list)
-  uint32_t* ccnt = nullptr;        // [G] chain positions per chunk (k_chunk_counts, for the fast walk)
+  uint32_t* ccnt = nullptr;        // [G] chain positions per chunk | CC_OFF: its entry may be off the one chain (k_chunk_counts)
   uint32_t* fw = nullptr;          // [2 nupd] fast-walked updates: first chain position past the exact walk, end of the last struct
   uint32_t* ufail = nullptr;       // [nupd] 1: the speculative walk gave up (locked chain phases), tables next
   uint64_t* final_bits = nullptr;  // [B/64] verified struct starts

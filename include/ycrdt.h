@@ -70,7 +70,8 @@ int ycrdt_engine_set_profiling(ycrdt_engine *e, int on);
 int ycrdt_engine_phase_times(ycrdt_engine *e, const char **names, double *ms, int cap);
 /* HBM the engine holds: its grow-only merge workspace, the doc-state arena and the staging batch */
 int ycrdt_engine_device_bytes(ycrdt_engine *e, uint64_t *bytes);
-/* Releases the engine's merge workspace (grow-only HBM buffers; doc states and batches stay):
+/* Releases the engine's merge workspace (grow-only HBM buffers) and every doc's spare state block
+ * (a folded merge keeps the previous state's block for the next one; doc states and batches stay):
  * after a giant merge, e.g. the >= 1 B-item replay of crdt.js:79-98, a server gets its HBM back.
  * The next merge allocates what it needs again. */
 int ycrdt_engine_trim(ycrdt_engine *e);

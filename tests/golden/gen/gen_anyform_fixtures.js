@@ -30,6 +30,13 @@ const values = {
   f64_int_max: [123, ...f64(2147483647)],
   f64_2p31: [123, ...f64(2147483648)],
   f64_1e10: [123, ...f64(1e10)],
+  // negative integers between -2^32 and -2^31: writeAny checks `data <= BITS31` (not |data|), so
+  // they go out as varints; below -2^32 the engine refuses (writeVarInt's 32-bit shifts)
+  f64_neg_2p31: [123, ...f64(-2147483648)],
+  f64_neg_2p31m1: [123, ...f64(-2147483649)],
+  f64_neg_3e9: [123, ...f64(-3e9)],
+  f64_neg_2p32p1: [123, ...f64(-4294967295)],
+  f64_1e300: [123, ...f64(1e300)],
   f64_half: [123, ...f64(0.5)],
   f64_inf: [123, ...f64(Infinity)],
   f64_ninf: [123, ...f64(-Infinity)],
