@@ -307,12 +307,13 @@ def c3_leg(eng, n_items, steps=3):
     ib.merge()
     idem_ok = ib.result()[0] == out
     del ib
-    res = {"workload": "C3: YArray 'messages', 256 replicas x 16 rounds, push 40% / unshift 15% / insert 30% / cut 15%",
+    res = {"full_state_ingest": full_state_leg(eng, "C3 merged state (256 clients) as one update", ups, out)}
+    res.update({"workload": "C3: YArray 'messages', 256 replicas x 16 rounds, push 40% / unshift 15% / insert 30% / cut 15%",
            "updates": len(ups), "input_bytes": sum(map(len, ups)), "items": st.items, "structs": st.structs,
            "segments": st.segments, "output_bytes": len(out), "ms_per_merge": round(wall * 1e3, 3),
            "device_ms": round(st.device_ms, 3), "items_per_s": round(st.items / wall, 1),
            "phases_ms": {n: round(m / steps, 3) for n, m in acc.items()},
-           "order_independent": rev_ok, "idempotent": idem_ok, "generate_s": round(gen_s, 2)}
+           "order_independent": rev_ok, "idempotent": idem_ok, "generate_s": round(gen_s, 2)})
     # the oracle port and Yjs on bounded samples of the same generator
     for key, n, runner in (("port", 1_000_000, "port"), ("yjs", 200_000, "yjs")):
         sups, sst = gen_array(256, 16, n, 3)
@@ -335,10 +336,53 @@ def c3_leg(eng, n_items, steps=3):
                         "parity": ref == gout, "sample": f"{n} values, oracle/yref.c sequential Yjs restatement"}
         else:
             y = _yjs_time(sups)
+            yf = _yjs_time([gout])  # the sample's merged state applied as one update (full-state ingest)
+            if yf:
+                res["full_state_ingest"]["yjs_sample"] = {
+                    "items": gst2.items, "cpu_ms": round(yf["ms"], 1), "cores": 1, "kind": "reference",
+                    "parity": yf["out_sha256"] == hashlib.sha256(gout).hexdigest(),
+                    "sample": f"the {n}-value sample's merged state ({len(gout)} B) as one update, Yjs {yf['yjs']} in Node {yf['node']}"}
             if y:
                 res[key] = {"items": gst2.items, "cpu_ms": round(y["ms"], 1), "gpu_ms": round(gms, 2), "cores": 1,
                             "kind": "reference", "parity": y["out_sha256"] == hashlib.sha256(gout).hexdigest(),
                             "sample": f"{n} values, Yjs {y['yjs']} in Node {y['node']}"}
+    return res
+
+
+def full_state_leg(eng, name, ups, full, reps=3):
+    """crdt.js's wire shape (crdt.js:288 sync step 2, :443 every local op, :79-98 LevelDB replay):
+    a peer's FULL state arrives as ONE multi-client update. Timed with the update resident in HBM
+    (ycrdt_batch_merge): merged alone (an empty doc applying it) and behind the state of a doc
+    that holds the first half of the history (the merge of ups[:n/2]). Both must give the full
+    state's bytes back (it is canonical and covers the half). Beside it, the same through the doc
+    path (Y.applyUpdate into a fresh doc + encodeStateAsUpdate: host staging included)."""
+    import crdt_amd
+
+    half_b = crdt_amd.Batch(ups[: len(ups) // 2], eng)
+    half_b.merge()
+    half = half_b.result()[0]
+    del half_b
+    res = {"what": name, "full_bytes": len(full), "half_bytes": len(half)}
+    for key, batch in (("into_empty", [full]), ("into_half", [half, full])):
+        b = crdt_amd.Batch(batch, eng)
+        st = b.merge()
+        t0 = time.perf_counter()
+        dev = 0.0
+        for _ in range(reps):
+            st = b.merge()
+            dev += st.device_ms
+        ms = (time.perf_counter() - t0) * 1e3 / reps
+        ok = b.result()[0] == full
+        del b
+        res[key] = {"ms_per_merge": round(ms, 3), "device_ms": round(dev / reps, 3), "items": st.items,
+                    "items_per_s": round(st.items / (ms * 1e-3), 1), "equal_to_full_state": ok}
+    d = crdt_amd.Doc(client_id=0x7FFFFFF0, engine=eng)
+    t0 = time.perf_counter()
+    d.apply_update(full)
+    got = d.encode_state_as_update()
+    res["doc_apply_ms"] = round((time.perf_counter() - t0) * 1e3, 3)
+    res["doc_equal"] = got == full
+    del d
     return res
 
 
@@ -997,6 +1041,7 @@ def run_rank(args, report=None):
         ingest = fleet_ingest_leg(eng, args.fleet_docs)
     side = rank == 0 and world == 1 and not args.only_headline and not args.billion
     loop = apply_loop_leg(eng, updates, out_update) if side else None
+    full_c2 = full_state_leg(eng, "one C2 document's merged state (1 001 clients) as one update", updates, out_update) if side else None
     per_op = per_op_leg(eng) if side and not args.no_per_op else None
     c3 = c3_leg(eng, args.c3_items) if side and args.c3_items > 0 else None
     c4 = c4_leg(eng) if side and not args.no_c4 else None
@@ -1058,6 +1103,7 @@ def run_rank(args, report=None):
         "fleet_sync": fleet,
         "fleet_ingest": ingest,
         "apply_loop": loop,
+        "full_state_ingest": full_c2,
         "per_op": per_op,
         "c3": c3,
         "c4": c4,

@@ -1099,7 +1099,45 @@ __global__ __launch_bounds__(64) void k_walk(Work w) {
 // the chunks (64 per wavefront round) and the struct-start words are copied in parallel. Anything
 // else (several sections, a chain that never meets, fewer chain positions than structs) is left
 // to k_walk, which also reports malformed input.
-constexpr uint32_t CC_OFF = 0x80000000u;  // ccnt: the chunk's entry may be off the one chain (k_chunk_counts)
+// The chain positions of the chunks, scanned (cpre, 64-bit), and the chunks whose entry may be off
+// the one chain, scanned (opre): k_chunk_counts + two scans. A fast walk's search for the chunk
+// holding a section's last struct is then a 64-way search over the scan (two or three rounds of one
+// load per lane), not a walk over every chunk's count (C4's 15 MB replica updates: 235 rounds).
+// The smallest j in [j0, nch) with cpre[c0 + j + 1] - cpre[c0 + j0] >= need; nch when none.
+__device__ __forceinline__ uint32_t chunk_search(const Work& w, uint32_t c0, uint32_t j0, uint32_t nch, uint64_t need, uint32_t lane) {
+  const uint64_t base = w.cpre[c0 + j0];
+  uint32_t lo = j0, hi = nch;  // the answer is in [lo, hi]; hi == nch: none, else known to hold
+  while (lo < hi) {
+    const uint32_t step = (hi - lo + 63) / 64;
+    const uint32_t pv = lo + lane * step;
+    const uint64_t m = __ballot(pv < hi && w.cpre[c0 + pv + 1] - base >= need);
+    if (!m) {
+      lo += min(63u, (hi - 1 - lo) / step) * step + 1;  // past the last pivot
+    } else {
+      const uint32_t L = (uint32_t)__ffsll((long long)m) - 1;
+      if (L == 0) { hi = lo; break; }
+      hi = lo + L * step;
+      lo += (L - 1) * step + 1;
+    }
+  }
+  return lo;
+}
+// The chunk fch holding the target-th (>= 1) chain position counted from q (in chunk jq) and the
+// rank rem (>= 1) of that position inside it (counted from q when fch == jq). No chunk after jq up
+// to fch may be off the one chain. false: fewer positions (why = 0) or an off chunk (why = 1).
+__device__ __forceinline__ bool chain_target(const Work& w, const uint64_t* __restrict__ spec, uint32_t ustart, uint32_t uend, uint32_t c0,
+                                             uint32_t nch, uint32_t jq, uint32_t q, uint32_t target, uint32_t lane, uint32_t& fch,
+                                             uint32_t& rem, uint32_t& why) {
+  const uint32_t cq = popc_range(spec, q, min(ustart + (jq + 1) * w.schunk, uend));
+  if (target <= cq) { fch = jq; rem = target; return true; }
+  const uint64_t need = target - cq;
+  const uint32_t j = jq + 1 < nch ? chunk_search(w, c0, jq + 1, nch, need, lane) : nch;
+  if (j >= nch) { why = 0; return false; }
+  if (w.opre[c0 + j + 1] != w.opre[c0 + jq + 1]) { why = 1; return false; }
+  fch = j;
+  rem = (uint32_t)(need - (w.cpre[c0 + j] - w.cpre[c0 + jq + 1]));
+  return true;
+}
 __global__ __launch_bounds__(64) void k_fastwalk(Work w) {
   __shared__ uint64_t walked[SW + 2];
   __shared__ uint32_t sh_q, sh_k0, sh_ok;
@@ -1146,38 +1184,8 @@ __global__ __launch_bounds__(64) void k_fastwalk(Work w) {
   __syncthreads();
   if (!sh_ok) { why(3); return; }
   const uint32_t q = sh_q, target = n - sh_k0;  // the target-th chain position from q is the last struct
-  // the chunk holding it: per-chunk counts, scanned 64 chunks at a time
-  uint32_t acc = 0, fch = NONE, rem = 0;
-  bool off_seen = false;  // an off-chain chunk after chunk 0, up to the last struct's
-  for (uint32_t base = 0; base < nch && fch == NONE; base += 64) {
-    const uint32_t j = base + lane;
-    uint32_t cnt = 0;
-    bool offj = false;
-    if (j < nch) {
-      // (the chain positions of every chunk were counted grid-wide by k_chunk_counts; chunk 0
-      // from q on here)
-      if (j == 0) cnt = popc_range(spec, q, min(ustart + CH, uend));
-      else { cnt = w.ccnt[c0 + j]; offj = (cnt & CC_OFF) != 0; cnt &= ~CC_OFF; }
-    }
-    uint32_t incl = cnt;
-    for (uint32_t off = 1; off < 64; off <<= 1) {
-      const uint32_t v = __shfl_up(incl, off);
-      if (lane >= off) incl += v;
-    }
-    const uint64_t hit = __ballot(j < nch && acc + incl >= target && acc + incl - cnt < target);
-    const uint64_t offm = __ballot(offj);
-    if (hit) {
-      const uint32_t L = (uint32_t)__ffsll((long long)hit) - 1;
-      fch = base + L;
-      rem = target - (acc + __shfl(incl, L) - __shfl(cnt, L));
-      off_seen |= (offm & ((2ull << L) - 1)) != 0;
-    } else {
-      acc += __shfl(incl, 63);
-      off_seen |= offm != 0;
-    }
-  }
-  if (fch == NONE) { why(4); return; }  // fewer chain positions than structs
-  if (off_seen) { why(2); return; }
+  uint32_t fch = 0, rem = 0, wy = 0;
+  if (!chain_target(w, spec, ustart, uend, c0, nch, 0, q, target, lane, fch, rem, wy)) { why(wy ? 2 : 4); return; }
   const uint32_t fcs = ustart + fch * CH, fa = fch == 0 ? q : fcs;
   const uint32_t Lp = select_from(spec, fa, rem);
   const uint32_t dsp = chain_step(b, Lp, uend);
@@ -1281,35 +1289,8 @@ __global__ __launch_bounds__(64) void k_fastwalk_multi(Work w) {
         if (q >= uend) { why(5); return; }  // no meeting within FWM_WALK structs
         const uint32_t target = n - k0;
         const uint32_t jq = (q - ustart) / CH;
-        uint32_t acc = 0, fch = NONE, rem = 0;
-        bool off_seen = false;  // an off-chain chunk after the meeting chunk, up to the last struct's
-        for (uint32_t base = jq; base < nch && fch == NONE; base += 64) {
-          const uint32_t j = base + lane;
-          uint32_t cnt = 0;
-          bool offj = false;
-          if (j < nch) {
-            if (j == jq) cnt = popc_range(spec, q, min(ustart + (jq + 1) * CH, uend));
-            else { cnt = w.ccnt[c0 + j]; offj = (cnt & CC_OFF) != 0; cnt &= ~CC_OFF; }
-          }
-          uint32_t incl = cnt;
-          for (uint32_t off = 1; off < 64; off <<= 1) {
-            const uint32_t v = __shfl_up(incl, off);
-            if (lane >= off) incl += v;
-          }
-          const uint64_t hit = __ballot(j < nch && acc + incl >= target && acc + incl - cnt < target);
-          const uint64_t offm = __ballot(offj);
-          if (hit) {
-            const uint32_t L = (uint32_t)__ffsll((long long)hit) - 1;
-            fch = base + L;
-            rem = target - (acc + __shfl(incl, L) - __shfl(cnt, L));
-            off_seen |= (offm & ((2ull << L) - 1)) != 0;
-          } else {
-            acc += __shfl(incl, 63);
-            off_seen |= offm != 0;
-          }
-        }
-        if (fch == NONE) { why(6); return; }  // fewer chain positions than structs
-        if (off_seen) { why(2); return; }
+        uint32_t fch = 0, rem = 0, wy = 0;
+        if (!chain_target(w, spec, ustart, uend, c0, nch, jq, q, target, lane, fch, rem, wy)) { why(wy ? 2 : 6); return; }
         const uint32_t fa = fch == jq ? q : ustart + fch * CH;
         const uint32_t Lp = select_from(spec, fa, rem);
         const uint32_t dl = Lp < uend ? chain_len(GlobalSrc{b}, b, Lp, uend) : 0u;
@@ -1353,7 +1334,7 @@ __global__ __launch_bounds__(64) void k_fastwalk_multi(Work w) {
     if (w.dbg) atomicAdd(&w.dbg[0], 1ull);
   }
 }
-// per chunk: its chain positions, and whether its entry may be off the one chain (CC_OFF): it was
+// per chunk: its chain positions, and whether its entry may be off the one chain (coff): it was
 // entered past its end (its predecessor's chain jumped over it: it keeps a chain of its own), or
 // its predecessor's exit moved in the last sync round (it was walked from an older entry). A fast
 // walk trusts the chunk chains from its meeting point to its last struct only when no chunk after
@@ -1365,13 +1346,14 @@ __device__ __forceinline__ bool chunk_moved(const Work& w, uint32_t i) {
 }
 __global__ __launch_bounds__(256) void k_chunk_counts(Work w) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= w.ngroups) return;
+  if (i > w.ngroups) return;
+  if (i == w.ngroups) { w.ccnt[i] = 0; w.coff[i] = 0; return; }  // (the scans' last entries)
   const Group G = w.groups[i];
-  const uint32_t cnt = popc_range(win_words(w.spec_bits, upd_win(w, G.upd)), G.start, G.end);
   const bool first = i == w.ugroup[G.upd];
   const bool jumped = !first && w.sent[w.ngroups + 1 + i];
   const bool moved = !first && chunk_moved(w, i - 1);
-  w.ccnt[i] = cnt | (jumped || moved ? CC_OFF : 0u);
+  w.ccnt[i] = popc_range(win_words(w.spec_bits, upd_win(w, G.upd)), G.start, G.end);
+  w.coff[i] = jumped || moved ? 1u : 0u;
   if (w.dbg) {  // (YCRDT_DEBUG_DECODE, printed as the wave path's "unsettled" / "other")
     if (moved) atomicAdd(&w.dbg[4], 1ull);
     if (jumped) atomicAdd(&w.dbg[5], 1ull);
@@ -1732,6 +1714,8 @@ void launch_chunks(const Work& w, hipStream_t s) {
     const bool nofast = getenv("YCRDT_NO_FASTWALK") && getenv("YCRDT_NO_FASTWALK")[0] == '1';
     if (!nofast && !w.force_xtab) {
       hipLaunchKernelGGL(k_chunk_counts, dim3(w.ngroups / 256 + 1), dim3(256), 0, s, w);
+      scan_u32_to_u64(w.tmp, w.tmp_bytes, w.ccnt, w.cpre, (uint64_t)w.ngroups + 1, s);
+      scan_u32(w.tmp, w.tmp_bytes, w.coff, w.opre, (uint64_t)w.ngroups + 1, s);
       hipLaunchKernelGGL(k_fastwalk, dim3(w.nbig), dim3(64), 0, s, w);
       hipLaunchKernelGGL(k_fastwalk_multi, dim3(w.nbig), dim3(64), 0, s, w);
       hipLaunchKernelGGL(k_fastmark, dim3(std::min<uint64_t>((uint64_t)w.ngroups * (w.schunk / 64) / 256 + 1, 8192)), dim3(256), 0, s, w);
@@ -2048,6 +2032,7 @@ __global__ __launch_bounds__(256) void k_ds_decode(Work w) {
   if (u >= w.nupd) return;
   const uint32_t p0 = w.dsstart[u];
   if (p0 == NONE) return;
+  if (w.dsp_b && w.dsp_b[u] != NONE) return;  // decoded grid-wide (k_dsp_*)
   const uint8_t* __restrict__ b = win_bytes(w, upd_win(w, u));
   const uint32_t end = w.uoff[u] + w.ulen[u];
   uint32_t* err = &w.ctr->err;
@@ -2149,6 +2134,162 @@ __global__ __launch_bounds__(256) void k_ds_decode(Work w) {
   if (lane == 0) w.ds_count[u] = obase - obase0;
 }
 
+// ---- Large delete sets, grid-wide. A delete set is a flat varuint stream (readDeleteSet, Y@11105:
+// client blocks of {client, n, (clock, len) x n} behind a client count), so its k-th value ends at
+// its k-th terminal byte (high bit clear). k_dsp_count counts the terminal bytes of every chunk's
+// delete-set part (one wavefront per chunk, 16 bytes a lane), a scan numbers them, k_dsp_vals
+// decodes every value where it ends (back to the previous terminal), k_dsp_headers walks the client
+// blocks over the decoded values (one lane per update: a block costs two reads), and k_dsp_ranges
+// writes every (clock, len) pair into the update's range region. One wavefront stepping 64 bytes at
+// a time took 55 ms for the 156 MB C3 state as one update (crdt.js's full-state wire shape).
+// Anything irregular — a varuint of more than 6 bytes, a truncated stream, a range count past
+// 2^31, more than DSP_MAXBLK client blocks — leaves the update to the wavefront (k_ds_decode),
+// which decodes and reports it exactly as before.
+constexpr uint32_t DSP_MIN = 4096;  // delete sets of at least this many bytes (to the update end)
+__device__ __forceinline__ bool dsp_applies(const Work& w, uint32_t u) {
+  const uint32_t ds = w.dsstart[u];
+  return ds != NONE && w.uoff[u] + w.ulen[u] - ds >= DSP_MIN;
+}
+// this lane's 16 bytes of chunk i: the terminal bytes inside the update's delete set (bit k: byte
+// p + k), or 0 when the update is not on the grid path
+__device__ __forceinline__ uint32_t dsp_terms(const Work& w, const Group& G, uint32_t lane, uint32_t& p) {
+  const uint32_t u = G.upd;
+  p = G.start + lane * 16;
+  if (!dsp_applies(w, u)) return 0u;
+  const uint32_t ds = w.dsstart[u];
+  if (p >= G.end || p + 16 <= ds) return 0u;
+  const uint4 v = *(const uint4*)(win_bytes(w, upd_win(w, u)) + p);  // (chunks are 64-byte aligned; the buffer is padded)
+  const uint32_t x[4] = {v.x, v.y, v.z, v.w};
+  uint32_t m = 0;
+  for (int j = 0; j < 4; ++j)
+    for (int k = 0; k < 4; ++k) m |= ((~x[j] >> (8 * k + 7)) & 1u) << (4 * j + k);
+  if (ds > p) m &= ~0u << (ds - p);
+  if (G.end < p + 16) m &= (1u << (G.end - p)) - 1u;
+  return m;
+}
+__device__ __forceinline__ uint32_t wave_excl_scan(uint32_t x, uint32_t lane, uint32_t& total) {
+  uint32_t incl = x;
+  for (uint32_t off = 1; off < 64; off <<= 1) {
+    const uint32_t v = __shfl_up(incl, off);
+    if (lane >= off) incl += v;
+  }
+  total = __shfl(incl, 63);
+  return incl - x;
+}
+__global__ __launch_bounds__(256) void k_dsp_count(Work w) {
+  const uint32_t i = (blockIdx.x * blockDim.x + threadIdx.x) >> 6, lane = threadIdx.x & 63;
+  if (i > w.ngroups) return;  // (whole wavefronts)
+  if (i == w.ngroups) { if (lane == 0) w.dsp_cnt[i] = 0; return; }
+  const Group G = w.groups[i];
+  uint32_t p;
+  const uint32_t m = dsp_terms(w, G, lane, p);
+  uint32_t total;
+  wave_excl_scan((uint32_t)__popc(m), lane, total);
+  if (lane == 0) w.dsp_cnt[i] = total;
+}
+// the value index of this lane's first terminal: terminals before its chunk in the update's delete
+// set, then before its lane
+__device__ __forceinline__ uint32_t dsp_first_index(const Work& w, const Group& G, uint32_t i, uint32_t m, uint32_t lane) {
+  const uint32_t u = G.upd;
+  const uint32_t g0 = w.ugroup[u] + (w.dsstart[u] - w.uoff[u]) / w.schunk;
+  uint32_t total;
+  const uint32_t ex = wave_excl_scan((uint32_t)__popc(m), lane, total);
+  return w.dsp_pre[i] - w.dsp_pre[g0] + ex;
+}
+__global__ __launch_bounds__(256) void k_dsp_vals(Work w) {
+  const uint32_t i = (blockIdx.x * blockDim.x + threadIdx.x) >> 6, lane = threadIdx.x & 63;
+  if (i >= w.ngroups) return;
+  const Group G = w.groups[i];
+  uint32_t p;
+  uint32_t m = dsp_terms(w, G, lane, p);
+  if (!__ballot(m != 0)) return;
+  const uint32_t u = G.upd, ds = w.dsstart[u];
+  uint32_t v = dsp_first_index(w, G, i, m, lane);
+  const uint8_t* __restrict__ b = win_bytes(w, upd_win(w, u));
+  uint32_t* __restrict__ vals = w.dsp_val + 2ull * w.ds_region[u];
+  for (; m; m &= m - 1, ++v) {
+    const uint32_t e = p + (uint32_t)__ffs(m) - 1;  // the value's last byte
+    uint32_t q = e, n = 1;
+    while (q > ds && b[q - 1] >= 0x80u && n <= 6) { --q; ++n; }
+    if (n > 6) { w.dsp_fail[u] = 1u; return; }  // a varuint of more than 6 bytes (the wavefront reports it)
+    uint32_t x = 0;
+    for (uint32_t k = 0; k < n && 7 * k < 32; ++k) x |= (uint32_t)(b[q + k] & 0x7Fu) << (7 * k);
+    vals[v] = x;
+  }
+}
+__global__ void k_dsp_headers(Work w) {
+  const uint32_t bi = blockIdx.x * blockDim.x + threadIdx.x;
+  if (bi >= w.nbig) return;
+  const uint32_t u = w.ulist[bi];
+  if (!dsp_applies(w, u) || w.dsp_fail[u]) return;
+  const uint32_t CH = w.schunk;
+  const uint32_t g0 = w.ugroup[u] + (w.dsstart[u] - w.uoff[u]) / CH, gl = w.ugroup[u] + (w.ulen[u] + CH - 1) / CH;
+  const uint64_t total = w.dsp_pre[gl] - w.dsp_pre[g0];
+  const uint32_t* __restrict__ vals = w.dsp_val + 2ull * w.ds_region[u];
+  uint4* __restrict__ blk = w.dsp_blk + (size_t)bi * DSP_MAXBLK;
+  if (total < 1) return;
+  const uint32_t ncl = vals[0];
+  uint64_t k = 1;
+  uint32_t off = 0, c = 0;
+  for (; c < ncl; ++c) {
+    if (c >= DSP_MAXBLK || k + 2 > total) return;  // (truncated: the wavefront reports it)
+    const uint32_t client = vals[k], nr = vals[k + 1];
+    if (nr > 0x7FFFFFFFu || k + 2 + 2ull * nr > total) return;
+    blk[c] = make_uint4((uint32_t)k, client, nr, off);
+    off += nr;
+    k += 2 + 2ull * nr;
+  }
+  w.dsp_nb[bi] = c;
+  w.ds_count[u] = off;
+  w.dsp_b[u] = bi;
+}
+__global__ __launch_bounds__(256) void k_dsp_ranges(Work w) {
+  const uint32_t i = (blockIdx.x * blockDim.x + threadIdx.x) >> 6, lane = threadIdx.x & 63;
+  if (i >= w.ngroups) return;
+  const Group G = w.groups[i];
+  const uint32_t u = G.upd;
+  const uint32_t bi = w.dsp_b[u];
+  if (bi == NONE) return;
+  uint32_t p;
+  uint32_t m = dsp_terms(w, G, lane, p);
+  uint32_t v = dsp_first_index(w, G, i, m, lane);
+  if (!m) return;
+  const uint32_t nb = w.dsp_nb[bi];
+  const uint4* __restrict__ blk = w.dsp_blk + (size_t)bi * DSP_MAXBLK;
+  const uint32_t* __restrict__ vals = w.dsp_val + 2ull * w.ds_region[u];
+  DsRange* __restrict__ out = w.ds_tmp + w.ds_region[u];
+  // the block of the lane's first value (the last block starting at or before it), then onwards
+  uint32_t lo = 0, hi = nb;
+  while (lo < hi) { const uint32_t mid = (lo + hi) >> 1; if (blk[mid].x <= v) lo = mid + 1; else hi = mid; }
+  if (lo == 0) { if (nb == 0) return; lo = 1; }  // (value 0, the client count: no block)
+  uint32_t c = lo - 1;
+  uint4 B = blk[c];
+  for (; m; m &= m - 1, ++v) {
+    while (c + 1 < nb && blk[c + 1].x <= v) B = blk[++c];
+    if (v < B.x + 2) continue;  // the block's client / count
+    const uint32_t rel = v - B.x - 2;
+    if (rel >= 2 * B.z) continue;  // past the last block: bytes Yjs never reads
+    if (!(rel & 1u)) continue;  // a clock: written with its length
+    DsRange r;
+    r.client = B.y;
+    r.clock = vals[v - 1];
+    r.len = vals[v];
+    r.upd = u;
+    out[B.w + (rel >> 1)] = r;
+  }
+}
+void launch_ds_grid(const Work& w, hipStream_t s) {
+  if (!w.nbig || !w.dsp_cnt) return;
+  // YCRDT_DS_GRID=0: every delete set on the wavefront (read per merge: tests compare the two)
+  if (const char* g = getenv("YCRDT_DS_GRID")) if (g[0] == '0') return;
+  const uint32_t nb = (uint32_t)(((uint64_t)w.ngroups + 1) * 64 / 256 + 1);
+  hipLaunchKernelGGL(k_dsp_count, dim3(nb), dim3(256), 0, s, w);
+  scan_u32(w.tmp, w.tmp_bytes, w.dsp_cnt, w.dsp_pre, (uint64_t)w.ngroups + 1, s);
+  hipLaunchKernelGGL(k_dsp_vals, dim3(nb), dim3(256), 0, s, w);
+  hipLaunchKernelGGL(k_dsp_headers, dim3(w.nbig / 64 + 1), dim3(64), 0, s, w);
+  hipLaunchKernelGGL(k_dsp_ranges, dim3(nb), dim3(256), 0, s, w);
+}
+
 __global__ void k_ds_bound(Work w) {  // region size per update: (delete-set bytes + 1) / 2
   const uint32_t u = blockIdx.x * blockDim.x + threadIdx.x;
   if (u > w.nupd) return;
@@ -2194,6 +2335,7 @@ void launch_ds_bound(const Work& w, hipStream_t s) {
 // diffUpdate (lazy) sort them, so there they are compacted into the dense table
 void launch_ds_decode(const Work& w, hipStream_t s) {
   if (w.nupd == 0) return;
+  launch_ds_grid(w, s);
   hipLaunchKernelGGL(k_ds_decode, dim3((w.nupd + 3) / 4), dim3(256), 0, s, w);
   if (!w.lazy) return;
   scan_u32(w.tmp, w.tmp_bytes, w.ds_count, w.ds_dense_off, w.nupd + 1, s);

@@ -178,7 +178,7 @@ enum Buf {
   B_UOWN, B_UFLAG, B_UMIN, B_UCUT, B_UWPRE,
   B_GSTART, B_GCIDX, B_GSRC, B_GFLAGS, B_GORIG, B_GRORIG, B_GLINK, B_GOSEG, B_GKEY, B_GMAXC, B_GNEXT, B_GOUTID, B_GTMP, B_GTMP2,
   B_KHASH, B_KROOT, B_KWIN, B_KPAR, B_KFLAG, B_SPK,
-  B_USEC, B_USECN, B_DBG, B_XTAB, B_UFAIL, B_FW, B_CCNT, B_TENTRY, B_XLIST, B_WLEN, B_FWSEC, B_UNSYNC,
+  B_USEC, B_USECN, B_DBG, B_XTAB, B_UFAIL, B_FW, B_CCNT, B_TENTRY, B_XLIST, B_WLEN, B_FWSEC, B_DSPCNT, B_DSPPRE, B_DSPVAL, B_DSPBLK, B_DSPB, B_DSPNB, B_DSPFAIL, B_COFF, B_CPRE, B_OPRE,
   B_LZKEY, B_LZKEYS, B_LZIOTA, B_LZSEC, B_LZRSTART, B_LZPREV, B_LZFIRST, B_LZCAP, B_LZEVBASE, B_LZEVN, B_LZFLAG,
   B_LZLHI, B_LZLLO, B_EVKIND, B_EVSRC, B_EVCLOCK, B_EVLEN, B_EVSIZE, B_EVPOS, B_BLKSIZE, B_BLKPOS, B_SVC, B_SVK,
   B_DSMKEY, B_DSMKEYS, B_DSMLEN, B_DSMLENS, B_DSMEND, B_DSMMAX, B_DSMFLAG, B_DSMRID, B_DRCLIENT, B_DRCLOCK, B_DREND,
@@ -835,6 +835,9 @@ int run_decode(ycrdt_engine* e, ycrdt_batch* b, bool lazy, Decoded& D, bool gene
   w.ufail = take<uint32_t>(V, B_UFAIL, nu + 1, ok);
   w.fw = take<uint32_t>(V, B_FW, 2ull * nu + 2, ok);
   w.ccnt = take<uint32_t>(V, B_CCNT, (uint64_t)w.ngroups + 1, ok);
+  w.coff = take<uint32_t>(V, B_COFF, (uint64_t)w.ngroups + 1, ok);
+  w.cpre = take<uint64_t>(V, B_CPRE, (uint64_t)w.ngroups + 1, ok);
+  w.opre = take<uint32_t>(V, B_OPRE, (uint64_t)w.ngroups + 1, ok);
   w.final_bits = take<uint64_t>(V, B_FINAL, nwords, ok);
   w.sec_bits = take<uint64_t>(V, B_SECB, nwords, ok);
   w.dsstart = take<uint32_t>(V, B_DSSTART, nu + 1, ok);
@@ -965,9 +968,23 @@ int run_decode(ycrdt_engine* e, ycrdt_batch* b, bool lazy, Decoded& D, bool gene
     Work wd = w;
     bool okd = true;
     wd.scratch = take<uint32_t>(V, B_SCRATCH2, (uint64_t)w.nupd + 2, okd);
-    wd.tmp = take<uint8_t>(V, B_TMP2, prim_tmp_bytes((uint64_t)w.nupd + 2, 0), okd);
+    wd.tmp = take<uint8_t>(V, B_TMP2, prim_tmp_bytes(std::max<uint64_t>((uint64_t)w.nupd + 2, (uint64_t)w.ngroups + 2), 0), okd);
     wd.tmp_bytes = V[B_TMP2].cap;
+    if (w.nbig) {  // large delete sets decode grid-wide (yc_decode.hip k_dsp_*)
+      wd.dsp_cnt = take<uint32_t>(V, B_DSPCNT, (uint64_t)w.ngroups + 1, okd);
+      wd.dsp_pre = take<uint32_t>(V, B_DSPPRE, (uint64_t)w.ngroups + 1, okd);
+      wd.dsp_val = take<uint32_t>(V, B_DSPVAL, 2ull * w.cap_ds, okd);
+      wd.dsp_blk = take<uint4>(V, B_DSPBLK, (uint64_t)w.nbig * DSP_MAXBLK, okd);
+      wd.dsp_nb = take<uint32_t>(V, B_DSPNB, w.nbig, okd);
+      wd.dsp_b = take<uint32_t>(V, B_DSPB, (uint64_t)w.nupd + 1, okd);
+      wd.dsp_fail = take<uint32_t>(V, B_DSPFAIL, (uint64_t)w.nupd + 1, okd);
+      if (okd) fill_u32_multi({{wd.dsp_b, (uint64_t)w.nupd + 1, NONE}, {wd.dsp_fail, (uint64_t)w.nupd + 1, 0u}}, e->side);
+    } else {
+      wd.dsp_cnt = wd.dsp_pre = wd.dsp_val = wd.dsp_nb = wd.dsp_b = wd.dsp_fail = nullptr;
+      wd.dsp_blk = nullptr;
+    }
     if (!okd) return fail(YCRDT_E_DEVICE, oom("delete-set scratch"));
+    w.dsp_b = wd.dsp_b;  // (the range apply reads which updates took the grid path)
     launch_ds_decode(wd, e->side);
     HIPCHK(hipEventRecord(e->side_done, e->side));
   }

@@ -94,36 +94,41 @@ __device__ __forceinline__ void set_flag_byte(uint32_t* u_flags, uint32_t g, uin
 // The delete sets of a merge, straight from the decoder's per-update regions (no compaction): one
 // wavefront per update resolves its ranges' clients, clips them to the known states (pendingDs)
 // and marks the units (the prep and mark passes above in one, for the integrate path)
+// one range: its units' first index and length, clipped to the client's known state (a range
+// past it is Yjs's pendingDs: an error here — the host then takes the pending path —, clipped
+// silently when the host already computed the caps)
+__device__ __forceinline__ uint32_t ds_range_units(const Work& w, uint32_t nclients, uint32_t doc, const DsRange& r, uint64_t& gb) {
+  uint32_t len = r.len;
+  gb = 0;
+  if (!len) return 0;
+  const uint32_t c = find_client(w, nclients, doc, r.client);
+  if (c == NONE) {
+    if (!w.capped) raise_err(&w.ctr->err, ERR_PENDING);
+    return 0;
+  }
+  const uint32_t st = w.cl_state[c];
+  if ((uint64_t)r.clock + len > st) {
+    if (!w.capped) raise_err(&w.ctr->err, ERR_PENDING);
+    len = r.clock < st ? st - r.clock : 0;
+  }
+  gb = w.cl_base[c] + r.clock;
+  return len;
+}
+// a wavefront applies the first DSA_WAVE ranges of its update; a large update's delete set (a
+// full state as one update: C3's 156 MB state holds a million ranges) is spread over the extra
+// workgroups of k_units (unit_ds_apply_big)
+constexpr uint32_t DSA_WAVE = 4096;
 __device__ __forceinline__ void unit_ds_apply(const Work& w, uint32_t nclients, uint32_t blk) {
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t u = (blk * blockDim.x + threadIdx.x) >> 6;
   if (u >= w.nupd) return;
-  const uint32_t n = w.ds_count[u], base = w.ds_region[u];
+  const uint32_t n = min(w.ds_count[u], DSA_WAVE), base = w.ds_region[u];
   const uint32_t doc = doc_of_update(w, u);
   for (uint32_t i0 = 0; i0 < n; i0 += 64) {
     const uint32_t i = i0 + lane;
     uint64_t gb = 0;
     uint32_t len = 0;
-    if (i < n) {
-      const DsRange r = w.ds_tmp[base + i];
-      len = r.len;
-      if (len) {
-        const uint32_t c = find_client(w, nclients, doc, r.client);
-        // a range past the known state is Yjs's pendingDs: an error here (the host then takes the
-        // pending path), clipped silently when the host already computed the caps
-        if (c == NONE) {
-          if (!w.capped) raise_err(&w.ctr->err, ERR_PENDING);
-          len = 0;
-        } else {
-          const uint32_t st = w.cl_state[c];
-          if ((uint64_t)r.clock + len > st) {
-            if (!w.capped) raise_err(&w.ctr->err, ERR_PENDING);
-            len = r.clock < st ? st - r.clock : 0;
-          }
-          gb = w.cl_base[c] + r.clock;
-        }
-      }
-    }
+    if (i < n) len = ds_range_units(w, nclients, doc, w.ds_tmp[base + i], gb);
     const bool lng = len > LONG_UNITS;
     if (!lng)
       for (uint32_t k = 0; k < len; ++k) set_flag_byte(w.u_flags, (uint32_t)(gb + k), 1);
@@ -244,13 +249,31 @@ __global__ __launch_bounds__(SEG_LANES) void k_segments_small(Work w, uint64_t n
 // references, every one of them a byte store or an atomic): workgroups [0, nb) take a struct each
 // lane (owner, then references — the struct's columns are loaded once), the rest one update per
 // wavefront (delete sets).
-__global__ __launch_bounds__(256) void k_units(Work w, uint32_t nstructs, uint32_t nclients, uint32_t nb) {
+// ranges DSA_WAVE.. of the large updates' delete sets, one lane per range (grid-stride over the
+// extra workgroups; only the chunk-path updates can hold that many)
+__device__ __forceinline__ void unit_ds_apply_big(const Work& w, uint32_t nclients, uint32_t blk, uint32_t nx) {
+  const uint32_t t = blk * blockDim.x + threadIdx.x, stride = nx * blockDim.x;
+  for (uint32_t bi = 0; bi < w.nbig; ++bi) {
+    const uint32_t u = w.ulist[bi];
+    const uint32_t n = w.ds_count[u];
+    if (n <= DSA_WAVE) continue;
+    const uint32_t base = w.ds_region[u], doc = doc_of_update(w, u);
+    for (uint32_t i = DSA_WAVE + t; i < n; i += stride) {
+      uint64_t gb;
+      const uint32_t len = ds_range_units(w, nclients, doc, w.ds_tmp[base + i], gb);
+      for (uint32_t k = 0; k < len; ++k) set_flag_byte(w.u_flags, (uint32_t)(gb + k), 1);
+    }
+  }
+}
+__global__ __launch_bounds__(256) void k_units(Work w, uint32_t nstructs, uint32_t nclients, uint32_t nb, uint32_t nd, uint32_t nx) {
   if (blockIdx.x < nb) {
     const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
     unit_owner(w, nstructs, s);
     unit_refs(w, nstructs, s);
-  } else {
+  } else if (blockIdx.x < nb + nd) {
     unit_ds_apply(w, nclients, blockIdx.x - nb);
+  } else {
+    unit_ds_apply_big(w, nclients, blockIdx.x - nb - nd, nx);
   }
 }
 void launch_units_fill(const Work& w, uint64_t nunits, hipStream_t s) {
@@ -258,7 +281,8 @@ void launch_units_fill(const Work& w, uint64_t nunits, hipStream_t s) {
 }
 void launch_units(const Work& w, uint32_t nstructs, uint32_t nclients, uint32_t nds, uint64_t nunits, hipStream_t s) {
   const uint32_t nb = (nstructs + 255) / 256, nd = nds && w.nupd ? (w.nupd + 3) / 4 : 0u;
-  if (nb + nd) hipLaunchKernelGGL(k_units, dim3(nb + nd), dim3(256), 0, s, w, nstructs, nclients, nb);
+  const uint32_t nx = nd && w.nbig ? 256u : 0u;  // (they return at once unless a large delete set has > DSA_WAVE ranges)
+  if (nb + nd) hipLaunchKernelGGL(k_units, dim3(nb + nd + nx), dim3(256), 0, s, w, nstructs, nclients, nb, nd, nx);
 }
 
 void launch_segments(const Work& w, uint32_t nclients, uint64_t nunits, hipStream_t s) {

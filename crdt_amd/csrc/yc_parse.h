@@ -420,6 +420,256 @@ YC_HD __attribute__((noinline)) AnySkip skip_any_nl(const uint8_t* __restrict__ 
   return AnySkip{p, steps, ok ? 1u : 0u, cf};
 }
 
+// JSON.parse of a ContentJSON / ContentEmbed / ContentFormat value (Y@72137 readContentJSON,
+// Y@14715 readJSON), and whether JSON.stringify gives the same text back: Yjs keeps the parsed
+// value and writes it with JSON.stringify (Y@71991), while the engine copies the bytes.
+//   JSON_OK        valid, in JSON.stringify's form: copied as is;
+//   JSON_BAD       JSON.parse throws (SyntaxError): the update is refused, as Yjs refuses it;
+//   JSON_NONCANON  valid, but not what JSON.stringify writes (whitespace, an escape it does not
+//                  write, a number not in Number::toString's form, a duplicate or array-index
+//                  object key, more than 64 levels, more than 15 significant digits, which the
+//                  engine does not verify): valid Yjs input refused (YCRDT_E_UNSUPPORTED) instead
+//                  of written back differently.
+// The text is valid UTF-8 already (lib0's readVarString, checked by the caller). Out of line:
+// called only for these rare contents (Yjs itself writes ContentAny for JS values).
+enum : uint32_t { JSON_OK = 0, JSON_BAD = 1, JSON_NONCANON = 2 };
+YC_HDI bool json_ws(uint32_t c) { return c == ' ' || c == '\t' || c == '\n' || c == '\r'; }
+YC_HDI int json_hex(uint32_t c) {
+  return c >= '0' && c <= '9' ? (int)(c - '0') : c >= 'a' && c <= 'f' ? (int)(c - 'a' + 10) : c >= 'A' && c <= 'F' ? (int)(c - 'A' + 10) : -1;
+}
+// a string at p (b[p] == '"'): p past its closing quote; res |= NONCANON for escapes stringify
+// does not write; h = FNV-1a of its raw bytes, idx = its array-index value (key_index) or -1
+YC_HD inline uint32_t json_string(const uint8_t* __restrict__ b, uint32_t& p, uint32_t e, uint32_t& res, uint64_t& h, int64_t& idx) {
+  ++p;
+  const uint32_t s0 = p;
+  h = 1469598103934665603ull;
+  for (;;) {
+    if (p >= e) return JSON_BAD;
+    const uint32_t c = b[p];
+    if (c == '"') break;
+    if (c < 0x20u) return JSON_BAD;
+    h = (h ^ c) * 1099511628211ull;
+    ++p;
+    if (c != '\\') continue;
+    if (p >= e) return JSON_BAD;
+    const uint32_t x = b[p++];
+    h = (h ^ x) * 1099511628211ull;
+    if (x == '"' || x == '\\' || x == 'b' || x == 'f' || x == 'n' || x == 'r' || x == 't') continue;
+    if (x == '/') { res = JSON_NONCANON; continue; }
+    if (x != 'u') return JSON_BAD;
+    uint32_t v = 0;
+    bool lower = true;
+    for (int k = 0; k < 4; ++k) {
+      if (p >= e) return JSON_BAD;
+      const uint32_t d = b[p++];
+      const int hv = json_hex(d);
+      if (hv < 0) return JSON_BAD;
+      if (d >= 'A' && d <= 'F') lower = false;
+      h = (h ^ d) * 1099511628211ull;
+      v = (v << 4) | (uint32_t)hv;
+    }
+    // stringify writes \u only for controls without a short escape and for lone surrogates (lowercase)
+    const bool ctl = v < 0x20u && v != 8 && v != 9 && v != 10 && v != 12 && v != 13;
+    bool lone = false;
+    if (v >= 0xD800u && v <= 0xDBFFu) {  // a high surrogate: lone unless a \uDC00-\uDFFF follows
+      lone = true;
+      if (p + 6 <= e && b[p] == '\\' && b[p + 1] == 'u') {
+        uint32_t w2 = 0;
+        bool hexok = true;
+        for (int k = 0; k < 4; ++k) { const int hv = json_hex(b[p + 2 + k]); if (hv < 0) hexok = false; else w2 = (w2 << 4) | (uint32_t)hv; }
+        if (hexok && w2 >= 0xDC00u && w2 <= 0xDFFFu) lone = false;  // a pair: stringify writes the character
+      }
+    } else if (v >= 0xDC00u && v <= 0xDFFFu) {
+      lone = true;  // (a low surrogate after a high one was judged with it: the pair is non-canonical already)
+    }
+    if (!(ctl || lone) || !lower) res = JSON_NONCANON;
+  }
+  // array-index keys (JSON.parse keeps them, Object.keys moves them first): key_index's rule
+  const uint32_t n = p - s0;
+  idx = key_index(b, s0, n);
+  ++p;
+  return JSON_OK;
+}
+// a number at p: p past it; res |= NONCANON unless it is Number::toString's form of its value
+YC_HD inline uint32_t json_number(const uint8_t* __restrict__ b, uint32_t& p, uint32_t e, uint32_t& res) {
+  const uint32_t s0 = p;
+  const bool neg = b[p] == '-';
+  if (neg) ++p;
+  if (p >= e) return JSON_BAD;
+  // digits: the integer part, then the fraction
+  const uint32_t i0 = p;
+  if (b[p] == '0') ++p;
+  else if (b[p] >= '1' && b[p] <= '9') { while (p < e && b[p] >= '0' && b[p] <= '9') ++p; }
+  else return JSON_BAD;
+  const uint32_t i1 = p;
+  uint32_t f0 = p, f1 = p;
+  if (p < e && b[p] == '.') {
+    ++p;
+    f0 = p;
+    while (p < e && b[p] >= '0' && b[p] <= '9') ++p;
+    f1 = p;
+    if (f1 == f0) return JSON_BAD;
+  }
+  int32_t ex = 0;
+  if (p < e && (b[p] == 'e' || b[p] == 'E')) {
+    ++p;
+    bool eneg = false;
+    if (p < e && (b[p] == '+' || b[p] == '-')) { eneg = b[p] == '-'; ++p; }
+    const uint32_t x0 = p;
+    while (p < e && b[p] >= '0' && b[p] <= '9') { if (ex < 100000) ex = ex * 10 + (int32_t)(b[p] - '0'); ++p; }
+    if (p == x0) return JSON_BAD;
+    if (eneg) ex = -ex;
+  }
+  if (res == JSON_NONCANON) return JSON_OK;  // (already refused: the form needs no check)
+  // significant digits d[0..k) and the decimal exponent n: value = 0.d1..dk x 10^n
+  char d[24];
+  uint32_t k = 0;
+  int32_t n = (int32_t)(i1 - i0) + ex;  // position of the decimal point in int ++ frac, shifted by the exponent
+  bool lead = true;
+  uint32_t zeros = 0;  // zeros after the last nonzero digit (trailing ones are not significant)
+  for (uint32_t q = i0; q < f1; ++q) {
+    if (q == i1) { q = f0; if (q >= f1) break; }
+    const char c = (char)b[q];
+    if (lead && c == '0') { --n; continue; }
+    lead = false;
+    if (c == '0') { ++zeros; continue; }
+    if (k + zeros >= 15) { res = JSON_NONCANON; return JSON_OK; }  // more than 15 significant digits: not verified
+    for (; zeros; --zeros) d[k++] = '0';
+    d[k++] = c;
+  }
+  // the text Number::toString writes for it (ECMA-262 Number::toString, radix 10)
+  char t[40];
+  uint32_t m = 0;
+  if (k == 0) {
+    t[m++] = '0';  // (-0 is written "0")
+  } else {
+    if (n > 308 || n < -306) { res = JSON_NONCANON; return JSON_OK; }  // Infinity / subnormal digits: not verified
+    if (neg) t[m++] = '-';
+    if ((int32_t)k <= n && n <= 21) {
+      for (uint32_t i = 0; i < k; ++i) t[m++] = d[i];
+      for (int32_t i = (int32_t)k; i < n; ++i) t[m++] = '0';
+    } else if (0 < n && n <= 21) {
+      for (int32_t i = 0; i < n; ++i) t[m++] = d[i];
+      t[m++] = '.';
+      for (uint32_t i = (uint32_t)n; i < k; ++i) t[m++] = d[i];
+    } else if (-6 < n && n <= 0) {
+      t[m++] = '0';
+      t[m++] = '.';
+      for (int32_t i = 0; i < -n; ++i) t[m++] = '0';
+      for (uint32_t i = 0; i < k; ++i) t[m++] = d[i];
+    } else {
+      t[m++] = d[0];
+      if (k > 1) { t[m++] = '.'; for (uint32_t i = 1; i < k; ++i) t[m++] = d[i]; }
+      t[m++] = 'e';
+      int32_t x = n - 1;
+      t[m++] = x < 0 ? '-' : '+';
+      if (x < 0) x = -x;
+      char r[4];
+      uint32_t nr = 0;
+      do { r[nr++] = (char)('0' + x % 10); x /= 10; } while (x);
+      while (nr) t[m++] = r[--nr];
+    }
+  }
+  if (p - s0 != m) { res = JSON_NONCANON; return JSON_OK; }
+  for (uint32_t i = 0; i < m; ++i)
+    if (b[s0 + i] != (uint8_t)t[i]) { res = JSON_NONCANON; return JSON_OK; }
+  return JSON_OK;
+}
+YC_HD inline __attribute__((noinline)) uint32_t json_check(const uint8_t* __restrict__ b, uint32_t p, uint32_t n) {
+  const uint32_t e = p + n;
+  uint32_t res = JSON_OK;
+  uint64_t objbits = 0;  // bit d: level d is an object
+  int d = 0;
+  uint64_t kh[32];       // the keys of the open objects (hash, level, array index or -1): a repeated
+  uint8_t kl[32];        // key, or an array-index key after another key that is not a smaller
+  int64_t ki[32];        // index, is not what JSON.stringify writes (Object.keys order)
+  uint32_t nk = 0;
+  auto skip_ws = [&]() { while (p < e && json_ws(b[p])) { ++p; res = JSON_NONCANON; } };
+  // an object member's key and colon (p at the key)
+  auto key = [&]() -> uint32_t {
+    if (p >= e || b[p] != '"') return JSON_BAD;
+    uint64_t h;
+    int64_t idx;
+    if (json_string(b, p, e, res, h, idx) != JSON_OK) return JSON_BAD;
+    const bool first = nk == 0 || kl[nk - 1] != (uint8_t)(d - 1);
+    if (idx >= 0 && !first && (ki[nk - 1] < 0 || ki[nk - 1] >= idx)) res = JSON_NONCANON;  // (JSON.parse moves index keys first)
+    for (uint32_t i = nk; i > 0 && kl[i - 1] == (uint8_t)(d - 1); --i)
+      if (kh[i - 1] == h) res = JSON_NONCANON;  // a repeated key (or a hash collision: refused either way)
+    if (nk == 32) res = JSON_NONCANON;
+    else { kh[nk] = h; kl[nk] = (uint8_t)(d - 1); ki[nk] = idx; ++nk; }
+    skip_ws();
+    if (p >= e || b[p] != ':') return JSON_BAD;
+    ++p;
+    skip_ws();
+    return JSON_OK;
+  };
+  skip_ws();
+  for (;;) {
+    // a value at p
+    if (p >= e) return JSON_BAD;
+    const uint32_t c = b[p];
+    if (c == '{' || c == '[') {
+      ++p;
+      skip_ws();
+      if (p >= e) return JSON_BAD;
+      if (b[p] == (c == '{' ? '}' : ']')) {
+        ++p;
+      } else {
+        if (d == 64) return JSON_NONCANON;  // deeper than the level mask (valid or not: refused)
+        if (c == '{') objbits |= 1ull << d; else objbits &= ~(1ull << d);
+        ++d;
+        if (c == '{' && key() != JSON_OK) return JSON_BAD;
+        continue;
+      }
+    } else if (c == '"') {
+      uint64_t h;
+      int64_t idx;
+      if (json_string(b, p, e, res, h, idx) != JSON_OK) return JSON_BAD;
+    } else if (c == '-' || (c >= '0' && c <= '9')) {
+      if (json_number(b, p, e, res) != JSON_OK) return JSON_BAD;
+    } else if (c == 't' || c == 'f' || c == 'n') {
+      const char* lit = c == 't' ? "true" : c == 'f' ? "false" : "null";
+      uint32_t i = 0;
+      while (lit[i] && p + i < e && b[p + i] == (uint8_t)lit[i]) ++i;
+      if (lit[i]) return JSON_BAD;
+      p += i;
+    } else {
+      return JSON_BAD;
+    }
+    // a value completed: close containers, or the next member
+    for (;;) {
+      skip_ws();
+      if (d == 0) return p == e ? res : JSON_BAD;
+      if (p >= e) return JSON_BAD;
+      const bool obj = (objbits >> (d - 1)) & 1ull;
+      const uint32_t x = b[p];
+      if (x == (obj ? '}' : ']')) {
+        ++p;
+        --d;
+        while (nk > 0 && kl[nk - 1] >= (uint8_t)d) --nk;  // the closed object's keys
+        continue;
+      }
+      if (x != ',') return JSON_BAD;
+      ++p;
+      skip_ws();
+      if (obj && key() != JSON_OK) return JSON_BAD;
+      break;
+    }
+  }
+}
+// a JSON value inside parse_struct (FULL): 0 ok, otherwise parse_struct's result (0 malformed,
+// -1 valid input the engine refuses); ContentJSON also takes the text "undefined"
+YC_HDI int json_value(const uint8_t* __restrict__ b, uint32_t st, uint32_t k, bool undef_ok) {
+  if (undef_ok && k == 9) {
+    const char* u = "undefined";
+    uint32_t i = 0;
+    while (i < 9 && b[st + i] == (uint8_t)u[i]) ++i;
+    if (i == 9) return 0;
+  }
+  const uint32_t r = json_check(b, st, k);
+  return r == JSON_OK ? 0 : r == JSON_BAD ? 0x100 : -1;
+}
+
 // Decoded view of one struct (Y@19286 readClientsStructRefs + readItemContent).
 struct StructView {
   uint8_t info;
@@ -505,6 +755,7 @@ YC_HD inline int parse_struct(const Src& b, uint32_t& p, uint32_t end, uint32_t 
         const uint32_t st = p;
         if (ok) skip_bytes(p, k, end, ok);
         if (FULL && ok && !utf8_valid(b, st, k)) ok = false;
+        if (FULL && ok) { const int jr = json_value(b.b, st, k, true); if (jr) return jr < 0 ? -1 : 0; }
       }
       if (FULL) v->nel = n;
       if (ok && steps == 0) return -1;
@@ -517,6 +768,7 @@ YC_HD inline int parse_struct(const Src& b, uint32_t& p, uint32_t end, uint32_t 
       const uint32_t st = p;
       if (ok) skip_bytes(p, k, end, ok);
       if (FULL && ok && !utf8_valid(b, st, k)) ok = false;
+      if (FULL && ok) { const int jr = json_value(b.b, st, k, false); if (jr) return jr < 0 ? -1 : 0; }
       break;
     }
     case REF_STRING: {
@@ -533,6 +785,7 @@ YC_HD inline int parse_struct(const Src& b, uint32_t& p, uint32_t end, uint32_t 
       const uint32_t st = p;
       if (ok) skip_bytes(p, k, end, ok);
       if (FULL && ok && !utf8_valid(b, st, k)) ok = false;
+      if (FULL && ok) { const int jr = json_value(b.b, st, k, false); if (jr) return jr < 0 ? -1 : 0; }
       break;
     }
     case REF_TYPE: {

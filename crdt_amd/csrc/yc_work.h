@@ -105,7 +105,10 @@ struct Work {
   uint32_t* xtab = nullptr;        // [G x XK] locked updates only, per entry offset: count << 16 | exit - chunk end
   uint32_t* tentry = nullptr;      // [G] locked updates: true entry of a chunk the table walk did not parse
   uint32_t* xlist = nullptr;       // [G] the chunks of the locked updates (k_xtab / k_xmark work list)
-  uint32_t* ccnt = nullptr;        // [G] chain positions per chunk | CC_OFF: its entry may be off the one chain (k_chunk_counts)
+  uint32_t* ccnt = nullptr;        // [G+1] chain positions per chunk (k_chunk_counts)
+  uint32_t* coff = nullptr;        // [G+1] 1: the chunk's entry may be off the one chain
+  uint64_t* cpre = nullptr;        // [G+1] exclusive scan of ccnt (the fast walks' chunk search)
+  uint32_t* opre = nullptr;        // [G+1] exclusive scan of coff
   uint32_t* fw = nullptr;          // [2 nupd] fast-walked updates: first chain position past the exact walk, end of the last struct
   uint32_t* ufail = nullptr;       // [nupd] 1: the speculative walk gave up (locked chain phases), tables next
   uint64_t* final_bits = nullptr;  // [B/64] verified struct starts
@@ -121,6 +124,16 @@ struct Work {
   uint32_t* ds_count = nullptr;    // [nupd+1] ranges decoded per update
   uint32_t* ds_dense_off = nullptr;// [nupd+1] scan of ds_count
   uint32_t* ds_len = nullptr;      // [cap_ds+1] clipped lengths (scan input)
+  // large delete sets decoded grid-wide (yc_decode.hip k_dsp_*): per chunk of the large updates
+  // the terminal bytes (varuint ends) of its delete-set part and their scan; every varuint's value;
+  // the client blocks (value index of the client, client, ranges, first range) of each update
+  uint32_t* dsp_cnt = nullptr;     // [G+1] terminal bytes of the chunk's delete-set part
+  uint32_t* dsp_pre = nullptr;     // [G+1] exclusive scan of dsp_cnt
+  uint32_t* dsp_val = nullptr;     // [2 cap_ds] varuint values, update u's at 2 ds_region[u]
+  uint4* dsp_blk = nullptr;        // [nbig x DSP_MAXBLK] client blocks of big update b
+  uint32_t* dsp_b = nullptr;       // [nupd] big index of an update whose delete set took the grid path, NONE: the wavefront's
+  uint32_t* dsp_nb = nullptr;      // [nbig] its client blocks
+  uint32_t* dsp_fail = nullptr;    // [nupd] a varuint longer than 6 bytes: the wavefront decodes (and reports) it
   uint64_t* ds_scan = nullptr;     // [cap_ds+1]
   uint32_t* dsclient_vals = nullptr; // [cap_dsclients] (client values seen in delete sets)
   // ---- per struct (S)
@@ -609,6 +622,7 @@ void launch_shard_mask(const Work& w, uint32_t nsegs, const uint8_t* owner, uint
 void launch_shard_export(const Work& w, uint32_t nsegs, const uint8_t* owner, uint32_t shard, uint32_t* acc, hipStream_t s);
 void launch_merge_final(const Work& w, uint32_t nsegs, hipStream_t s);
 void run_dead_keys(const Work& w, uint32_t nsegs, hipStream_t s);
+constexpr uint32_t DSP_MAXBLK = 8192;  // client blocks of one delete set decoded grid-wide (yc_decode.hip)
 constexpr uint32_t LISTS_UNNUMBERED = 0xFFFFFFFFu;  // launch_yata: lists exist, launch_ylists numbers them
 uint32_t launch_yata(const Work& w, uint32_t nsegs, uint32_t narray, uint32_t nclients, hipStream_t s, hipStream_t side,
                      hipEvent_t ev_fork, hipEvent_t ev_join);
