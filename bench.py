@@ -772,7 +772,7 @@ def _free_port():
 
 def _rank_entry(rank, world, port, q):
     os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank), LOCAL_WORLD_SIZE=str(world),
-                      MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+                      MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), YCRDT_HUB_PORT=str(port))
     sys.exit(run_rank(parse(), report=q))
 
 
@@ -804,11 +804,13 @@ def spawn_ranks(args):
 
 
 def setup_ranks(rank, world, local, report):
-    """The engine on this rank's device and libycrdt's communicator. torch.distributed (gloo: host
-    TCP, no GPU) only bootstraps — it carries the RCCL unique id — and is the host transport when
-    ranks share a device (RCCL takes one rank per GPU). Barriers, the max-over-ranks step time and
-    every data exchange go through libycrdt's Comm."""
+    """The engine on this rank's device and libycrdt's communicator. The package's TCP hub
+    (crdt_amd/hosthub.py: rank 0 listens on MASTER_PORT + 1, or YCRDT_HUB_PORT; no torch) only
+    bootstraps — it carries the RCCL unique id — and is the host transport when ranks share a device
+    (RCCL takes one rank per GPU). Barriers, the max-over-ranks step time and every data exchange go
+    through libycrdt's Comm."""
     import crdt_amd
+    from crdt_amd.hosthub import HostHub
 
     ndev = crdt_amd.device_count()
     if ndev < 1:
@@ -817,26 +819,17 @@ def setup_ranks(rank, world, local, report):
     eng = crdt_amd.Engine(device=dev)
     if world == 1:
         return eng, None, ndev
-    import torch.distributed as tdist
-
-    # gloo prints its connection lines on stdout: keep stdout for the one JSON line
-    saved = os.dup(1)
-    os.dup2(2, 1)
-    try:
-        tdist.init_process_group("gloo", rank=rank, world_size=world)
-    finally:
-        sys.stdout.flush()
-        os.dup2(saved, 1)
-        os.close(saved)
+    port = int(os.environ.get("YCRDT_HUB_PORT") or int(os.environ["MASTER_PORT"]) + 1)
+    hub = HostHub(world, rank, os.environ.get("MASTER_ADDR", "127.0.0.1"), port)
     local_world = int(os.environ.get("LOCAL_WORLD_SIZE", str(world)))
-    if local_world > ndev:  # ranks share a device: the library's collectives over gloo
-        comm = crdt_amd.Comm.over_torch(eng)
-        comm.transport = f"host exchange over gloo ({local_world} ranks on {ndev} device(s))"
+    if local_world > ndev:  # ranks share a device: the library's collectives over the hub
+        comm = crdt_amd.Comm.over_hub(eng, hub)
+        comm.transport = f"host exchange over the TCP hub ({local_world} ranks on {ndev} device(s))"
     else:
-        uid = [crdt_amd.Comm.unique_id() if rank == 0 else None]
-        tdist.broadcast_object_list(uid, src=0)
-        comm = crdt_amd.Comm(eng, world, rank, uid[0])
+        uid = hub.bcast(crdt_amd.Comm.unique_id() if rank == 0 else None)
+        comm = crdt_amd.Comm(eng, world, rank, uid)
         comm.transport = "rccl"
+    comm.hub = hub
     comm.barrier()
     if report is not None:
         report.put(rank)
@@ -1112,14 +1105,15 @@ def run_rank(args, report=None):
         "billion": billion,
         "phases_ms": {n: round(m, 4) for n, m in phases},
     }
+    # no PyTorch anywhere in a rank (north_star: the host side is libycrdt + its C ABI)
+    assert "torch" not in sys.modules, "torch was imported"
+    line["torch_loaded"] = False
     if rank == 0:
         print(json.dumps(line), flush=True)
     if comm is not None:
         comm.barrier()
         comm.close()
-        import torch.distributed as tdist
-
-        tdist.destroy_process_group()
+        comm.hub.close()
     return 0
 
 

@@ -501,7 +501,7 @@ class Comm:
     """Communicator inside libycrdt (one rank per GPU). RCCL: Comm.unique_id() on rank 0, the bytes
     handed to every rank by any channel, then Comm(engine, nranks, rank, uid) on each. Or
     Comm.over(engine, nranks, rank, allreduce, allgather): the library's collectives over host
-    callbacks (ycrdt_exchange) — e.g. torch.distributed gloo, see Comm.over_torch."""
+    callbacks (ycrdt_exchange) — e.g. the package's TCP hub, Comm.over_hub (crdt_amd/hosthub.py)."""
 
     @staticmethod
     def unique_id() -> bytes:
@@ -554,26 +554,9 @@ class Comm:
         return self
 
     @classmethod
-    def over_torch(cls, engine, group=None):
-        """The host exchange over a torch.distributed process group (gloo: CPU tensors)."""
-        import numpy as np
-        import torch
-        import torch.distributed as dist
-
-        world, rank = dist.get_world_size(group), dist.get_rank(group)
-
-        def allreduce(a, op):
-            t = torch.from_numpy(a.astype(np.int64))
-            dist.all_reduce(t, op=dist.ReduceOp.MAX if op else dist.ReduceOp.SUM, group=group)
-            a[:] = (t.numpy() & 0xFFFFFFFF).astype(np.uint32)
-
-        def allgather(b):
-            t = torch.frombuffer(bytearray(b), dtype=torch.uint8) if b else torch.zeros(0, dtype=torch.uint8)
-            outs = [torch.zeros_like(t) for _ in range(world)]
-            dist.all_gather(outs, t, group=group)
-            return b"".join(o.numpy().tobytes() for o in outs)
-
-        return cls.over(engine, world, rank, allreduce, allgather)
+    def over_hub(cls, engine, hub):
+        """The host exchange over a crdt_amd.hosthub.HostHub (TCP through rank 0, no torch)."""
+        return cls.over(engine, hub.world, hub.rank, hub.allreduce_u32, lambda b: b"".join(hub.allgather(b)))
 
     def close(self):
         if getattr(self, "_h", None):

@@ -2559,6 +2559,7 @@ __global__ __launch_bounds__(256) void k_struct_decode(Work w, uint32_t nstructs
   }
   if (pk != 0 && !v.has_psub) w.ctr->narray_roots = 1;  // a YArray list may exist (flag, plain store)
   if (pk == 2) w.ctr->nested = 1;                        // a nested type's list (flag, plain store)
+  wave_flag(&w.ctr->any_rorigin, item && (v.info & 0x40u));  // (a YMap entry may need full YATA)
   wave_count_add_sharded(w.ctr->nroots_sh, pk != 0);
   // the header as Item.write re-encodes it (every varuint in shortest form): an overlong varuint
   // (valid lib0 input) makes the input's header bytes differ from the output's, so such a struct

@@ -4,6 +4,7 @@
 // decode → dedupe → delete-set → segmentation → map-winner → encode kernels back to back on the
 // engine stream; the host only reads a handful of counters at the sync points where the next
 // phase's size depends on data (struct count, unit count, segment count, output bytes).
+#include <cstddef>
 #include <cstdio>
 #include <cstring>
 #include <string>
@@ -652,6 +653,7 @@ struct Decoded {
   uint32_t nstructs = 0, nsections = 0, nclients = 0, nds = 0;
   uint64_t nunits = 0, in_len = 0;
   uint32_t array_roots = 0;  // 1: some item names a parent without a parentSub (a YArray may exist)
+  uint32_t any_rorigin = 0;  // 1: some item has a right origin (a YMap entry may need full YATA)
   uint32_t nested = 0;       // 1: some item names a parent item (nested types: dead-type pass needed)
   uint32_t nroots = 0;       // items with an explicit parent (key table bound)
   uint32_t noncanon = 0;     // lazy: some update's sections are not in strictly descending client order
@@ -1015,6 +1017,7 @@ int run_decode(ycrdt_engine* e, ycrdt_batch* b, bool lazy, Decoded& D, bool gene
   const uint64_t nunits = lazy ? 0 : c.units;
   D.in_len = c.in_len;
   D.array_roots = c.narray_roots;
+  D.any_rorigin = c.any_rorigin;
   D.nested = c.nested;
   D.nroots = 0;
   for (uint32_t k = 0; k < NSHARD; ++k) D.nroots += c.nroots_sh[k];
@@ -1201,9 +1204,18 @@ int run_merge(ycrdt_engine* e, ycrdt_batch* b, const std::unordered_map<uint32_t
     mark(e, "merge.resolve");  // k_resolve alone
     run_key_resolution(w, nsegs, s);
     uint32_t narray = 0;  // YArray members; only read when the decode saw a possible array root
-    if (D.array_roots) {
-      HIPCHK(hipMemcpyAsync(&narray, &w.ctr->narray, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+    uint32_t nmapx = 0;   // a YMap entry that needs full YATA (only with a right origin somewhere)
+    if (D.array_roots || D.any_rorigin) {
+      uint32_t h2[2];
+      static_assert(offsetof(Counters, nmapx) == offsetof(Counters, narray) + 4, "read together");
+      HIPCHK(hipMemcpyAsync(h2, &w.ctr->narray, sizeof(h2), hipMemcpyDeviceToHost, s));
       HIPCHK(hipStreamSynchronize(s));
+      narray = h2[0];
+      nmapx = h2[1];
+    }
+    if (nmapx) {
+      launch_mapx_flip(w, nsegs, s);
+      narray = 1;
     }
     if (narray && !alloc_lists(nsegs)) return fail(YCRDT_E_DEVICE, oom("list workspace"));
     // the integrate phases: once, or once per key-hash shard (sh: C4 sharding, §6 of DESIGN.md)
@@ -1236,6 +1248,7 @@ int run_merge(ycrdt_engine* e, ycrdt_batch* b, const std::unordered_map<uint32_t
       if (D.nested) run_dead_keys(w, nsegs, s);  // only lists under a parent item can die with it
       mark(e, "merge.yata");
       e->nlists = launch_yata(w, nsegs, narray, nclients, s, e->side, e->side_fork, e->side_done);
+      if (nmapx) launch_mapx_fix(w, nsegs, s);
       if (w.dbg && e->nlists) {
         unsigned long long h[7];
         HIPCHK(hipStreamSynchronize(s));

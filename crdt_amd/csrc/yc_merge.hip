@@ -420,6 +420,7 @@ __global__ __launch_bounds__(256) void k_seg_props(Work w, uint32_t nsegs) {
   }
   if (gc) sf |= SEG_GC | SEG_DEL;
   else sf |= SEG_ITEM;
+  if (!gc && rorigin != NONE) sf |= SEG_HASRO;  // (a YMap entry item with one needs full YATA: k_resolve)
   const bool olow = !gc && expl && origin != NONE && socx < NONE - 1 && cidx < socx;
   if (olow) sf |= SEG_OLOW;
   // The YMap winner's max-client child / max-client root, first pass: a plain store of s + 1 into
@@ -502,6 +503,10 @@ __global__ __launch_bounds__(256) void k_resolve(Work w, uint32_t nsegs) {
       else {
         arr = !(kv & KEY_PSUB);
         f |= arr ? SEG_ARRAY : SEG_PSUB;
+        // a YMap entry item with a right origin (never written by typeMapSet: crafted input) — or
+        // placed by one alone — is not ordered by the max-client descent: the whole entry takes the
+        // YATA kernels (launch_mapx_flip / launch_mapx_fix)
+        if (!arr && (f & SEG_HASRO)) { atomicOr(&w.k_flags[kv & ~KEY_PSUB], KF_YATA); w.ctr->nmapx = 1u; }
         if (!arr) {  // the winner reduction's settling pass (k_seg_props stored one child)
           uint32_t* slot = h.w != NONE ? &w.g_maxchild[h.w] : (f & SEG_ROOT) ? &w.k_rootmax[kv & ~KEY_PSUB] : nullptr;
           if (slot && *slot < s + 1) atomicMax(slot, s + 1);
@@ -509,9 +514,54 @@ __global__ __launch_bounds__(256) void k_resolve(Work w, uint32_t nsegs) {
       }
     }
   }
-  w.g_flags[s] = f;
+  w.g_flags[s] = f & ~SEG_HASRO;
   w.g_key[s] = (f & SEG_ITEM) && kv != NONE ? kv & ~KEY_PSUB : NONE;
   wave_flag(&w.ctr->narray, arr);  // read as zero / non-zero (launch_yata)
+}
+
+// ---- YMap entries ordered by full YATA (KF_YATA keys). Yjs integrates a map entry's items by the
+// same YATA loop as a YArray's (Item.integrate, Y@77594: the list starts at the entry's leftmost
+// item), keeps the LAST one as the value (_map.set when right is null) and deletes every other
+// (this.delete() when right is not null, left.delete() of the new last one). The descent over
+// max-client children orders the origin-only shape typeMapSet writes; an entry with a right origin
+// goes through the YArray kernels instead: flipped to SEG_ARRAY before the descent, back to
+// SEG_PSUB after YATA with the last member as the winner (g_right == NONE) and every other deleted.
+// The origin-tree order (yc_yata.hip) holds for the shapes Yjs's own histories have. One it does
+// not: a right origin that is a split piece of another item (a segment starting inside its struct)
+// while the item's origin is not the unit before it — the piece's origin. Yjs integrated the item
+// before that split existed and may place it inside the split item; no replica can create that
+// shape (it would have to see the piece without the item), and for a map entry — whose items never
+// carry a right origin from typeMapSet — it only comes from corrupted or crafted bytes: refused
+// (YCRDT_E_UNSUPPORTED) rather than merged into a state Yjs would not reach.
+__global__ void k_mapx_flip(Work w, uint32_t nsegs) {
+  const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= nsegs) return;
+  const uint32_t f = w.g_flags[s];
+  if (!(f & SEG_PSUB) || !(w.k_flags[w.g_key[s]] & KF_YATA)) return;
+  const uint32_t r = w.g_rorigin[s];
+  if (r != NONE && !(w.g_flags[seg_of(w.u_cutbits, w.u_wpre, r)] & SEG_EXPLICIT) && w.g_origin[s] != r - 1)
+    raise_err(&w.ctr->err, ERR_UNSUPPORTED);
+  w.g_flags[s] = (f & ~(SEG_PSUB | SEG_WIN)) | SEG_ARRAY | SEG_YMAPX;
+}
+__global__ void k_mapx_fix(Work w, uint32_t nsegs) {
+  const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= nsegs) return;
+  uint32_t f = w.g_flags[s];
+  if ((f & (SEG_YMAPX | SEG_ITEM | SEG_ARRAY)) != (SEG_YMAPX | SEG_ITEM | SEG_ARRAY)) return;  // (GC / dead / another shard's)
+  f = (f & ~(SEG_ARRAY | SEG_WIN)) | SEG_PSUB;
+  if (w.g_right[s] == NONE) {
+    f |= SEG_WIN;
+    w.k_winner[w.g_key[s]] = s;
+  } else {
+    f |= SEG_DEL;
+  }
+  w.g_flags[s] = f;
+}
+void launch_mapx_flip(const Work& w, uint32_t nsegs, hipStream_t s) {
+  if (nsegs) hipLaunchKernelGGL(k_mapx_flip, dim3(nsegs / 256 + 1), dim3(256), 0, s, w, nsegs);
+}
+void launch_mapx_fix(const Work& w, uint32_t nsegs, hipStream_t s) {
+  if (nsegs) hipLaunchKernelGGL(k_mapx_fix, dim3(nsegs / 256 + 1), dim3(256), 0, s, w, nsegs);
 }
 
 uint32_t run_key_resolution(const Work& w, uint32_t nsegs, hipStream_t s) {
@@ -533,6 +583,7 @@ __global__ void k_winner_walk(Work w, uint32_t nsegs) {
   if (k >= w.cap_keys) return;
   const uint32_t r = w.k_rootmax[k];
   if (!r) { w.k_winner[k] = NONE; return; }
+  if (w.k_flags[k] & KF_YATA) { w.k_winner[k] = NONE; return; }  // ordered by the YATA kernels (k_mapx_fix writes the winner)
   uint32_t x = r - 1;
   bool leaf = false;
   for (uint32_t it = 0; it <= nsegs; ++it) {
@@ -631,7 +682,7 @@ __global__ __launch_bounds__(256) void k_merge_flags(Work w, uint32_t nsegs, uin
       if (!(fr & SEG_ITEM)) merge = true;  // GC + GC
       else if ((fl & SEG_DEL) == (fr & SEG_DEL) && w.g_origin[s] == gs - 1 && w.g_rorigin[s - 1] == w.g_rorigin[s] &&
                (fl & (SEG_ARRAY | SEG_PSUB)) == (fr & (SEG_ARRAY | SEG_PSUB)) &&
-               ((fr & SEG_ARRAY) ? w.g_right[s - 1] == s : w.u_minchild[gs - 1] != 0u)) {
+               ((fr & (SEG_ARRAY | SEG_YMAPX)) ? w.g_right[s - 1] == s : w.u_minchild[gs - 1] != 0u)) {
         if (fr & SEG_DEL) merge = true;  // both become ContentDeleted after GC
         else {
           const uint32_t rl = w.s_info[w.g_src[s - 1]] & 31u, rr = w.s_info[w.g_src[s]] & 31u;

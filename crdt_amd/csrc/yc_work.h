@@ -29,6 +29,8 @@ struct Counters {            // device-side counters, read back at the few host 
   uint32_t nkeys;            // distinct map keys
   uint32_t nruns;            // delete-set runs in the output
   uint32_t narray;           // YArray list members (segments)
+  uint32_t nmapx;            // 1: a YMap entry needs full YATA (an entry item with a right origin, k_resolve)
+  uint32_t any_rorigin;      // 1: a decoded item has a right origin (only then can nmapx be set)
   uint32_t narray_roots;     // 1: a decoded item may root a YArray list (parent given, no parentSub)
   uint32_t tgroups;          // sibling groups of the YArray origin trees (yc_yata.hip)
   uint32_t tbig;             // groups too large for one lane
@@ -560,6 +562,9 @@ enum : uint32_t {
   SEG_OLOW = 256u,     // its client index is below its origin's (a YATA sibling placed before the
                        // origin's own-client successor: that successor cannot merge, k_seg_props)
   SEG_WIN = 512u,      // the value of its YMap entry (k_winner_walk); every other entry item is deleted
+  SEG_YMAPX = 1024u,   // a YMap entry ordered by full YATA (its key has an entry item with a right
+                       // origin: the max-client descent does not apply): adjacency from g_right
+  SEG_HASRO = 2048u,   // (hop record only, k_seg_props -> k_resolve) the item has a right origin
 };
 // bit 31 of the climbing keys (g_tmp) between k_seg_props and k_resolve: the list is a YMap entry
 // (key slots < 2^31); g_key holds the final slots without it
@@ -568,6 +573,7 @@ constexpr uint32_t KEY_PSUB = 0x80000000u;
 enum : uint32_t {
   KF_PSUB = 1u,        // the list is a YMap entry (items carry a parentSub)
   KF_DEAD = 2u,        // the parent type item is deleted: every member becomes GC
+  KF_YATA = 4u,        // a YMap entry with an item carrying a right origin: ordered by full YATA
 };
 // unit flags
 enum : uint32_t {
@@ -613,6 +619,8 @@ void launch_segment_props_fill(const Work& w, uint32_t nsegs, hipStream_t s);
 void launch_segment_props(const Work& w, uint32_t nsegs, uint32_t nclients, uint64_t nunits, hipStream_t s);
 uint32_t run_key_resolution(const Work& w, uint32_t nsegs, hipStream_t s);
 uint32_t run_descent(const Work& w, uint32_t nsegs, hipStream_t s, bool fold_overwrite);
+void launch_mapx_flip(const Work& w, uint32_t nsegs, hipStream_t s);  // full-YATA map entries -> the YATA kernels
+void launch_mapx_fix(const Work& w, uint32_t nsegs, hipStream_t s);   // ... and back: the last one wins
 void launch_merge_flags(const Work& w, uint32_t nsegs, hipStream_t s, bool fold_overwrite);
 void launch_merge_flags_only(const Work& w, uint32_t nsegs, hipStream_t s, bool fold_overwrite);
 void launch_merge_tail(const Work& w, uint32_t nsegs, hipStream_t s);

@@ -282,7 +282,11 @@ __global__ void k_tkey(Work w, uint32_t nsegs) {
     if (o != NONE) p = seg_of_unit(w, o);
     if (r != NONE) {
       rs = seg_of_unit(w, r);
-      if (!(w.g_flags[rs] & SEG_ARRAY) || w.g_key[rs] != list) raise_err(&w.ctr->err, ERR_DECODE);
+      // a right origin in another list than the origin's: Yjs takes the RIGHT one's parent
+      // (Item.getMissing, Y@76507) but links the item next to its origin in the origin's list —
+      // an item in one list's chain that belongs to another. No replica writes that (only corrupted
+      // or crafted bytes): refused, as valid Yjs input the engine does not model
+      if (!(w.g_flags[rs] & SEG_ARRAY) || w.g_key[rs] != list) raise_err(&w.ctr->err, ERR_UNSUPPORTED);
     }
     key = p != NONE ? p : nsegs + list;
   }

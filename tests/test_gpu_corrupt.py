@@ -19,20 +19,24 @@ crdt_amd = pytest.importorskip("crdt_amd")
 
 pytestmark = pytest.mark.gpu
 HERE = os.path.dirname(os.path.abspath(__file__))
-# Yjs errors the engine does not reproduce yet: JSON.parse of a ContentJSON / Embed / Format value
-# (only the value's first character is checked) — listed, not hidden
-KNOWN_GAPS = ("SyntaxError",)
+# Yjs errors the engine does not reproduce (none since round 5: ContentJSON / Embed / Format values
+# go through JSON.parse's grammar on the device, yc_parse.h json_check)
+KNOWN_GAPS = ()
 # Cases whose refusal matches Yjs but whose resulting state does not, or whose state differs:
 # listed by name with the reason (DESIGN.md §3 "Corrupted input"), never skipped silently.
+# Cases Yjs accepts and the engine refuses (YCRDT_E_UNSUPPORTED) instead of writing a state Yjs
+# would not reach: a corrupted length makes later items of a map entry name an origin INSIDE a
+# deleted item and a right origin elsewhere — a split piece of that item placed before the split
+# existed (k_mapx_flip), or an item whose origin and right origin lie in different lists (k_tkey).
+# Map entries with right origins otherwise go through full YATA (yc_merge.hip k_mapx_*).
+KNOWN_REFUSED = {
+    "small2_b1340_127": "right origin = split piece of another item, origin elsewhere",
+    "large_b2846_31": "origin and right origin in different lists",
+}
 KNOWN_STATE = {
     # Yjs crashes inside integrateStructs (a TypeError: an own-client origin past the item's clock)
     # after integrating part of the update; the engine refuses the whole update
     "small2_b1315_31": "Yjs internal TypeError mid-integration",
-    # a corrupted length makes later items of a map entry name an origin INSIDE a deleted item and
-    # carry a right origin: full YATA for that map entry (the engine's map-entry order assumes the
-    # origin / right-origin shape Yjs's typeMapSet writes)
-    "small2_b1340_127": "crafted map-entry YATA shape",
-    "large_b2846_31": "crafted map-entry YATA shape",
 }
 
 
@@ -68,7 +72,15 @@ def test_corrupt_like_yjs(corrupt, mode, monkeypatch):
             d.apply_update(bad)
         except crdt_amd.YcrdtError as e:
             raised = e
-        if c["threw"] and c["threw"].startswith(KNOWN_GAPS) and raised is None:
+        if c["name"] in KNOWN_REFUSED:
+            try:
+                d.encode_state_as_update()  # (the merge is deferred to the next read)
+            except crdt_amd.YcrdtError as e:
+                raised = raised or e
+            assert c["threw"] is None and raised is not None and raised.kind == "UNSUPPORTED", (c["name"], raised)
+            gaps += 1
+            continue
+        if KNOWN_GAPS and c["threw"] and c["threw"].startswith(KNOWN_GAPS) and raised is None:
             gaps += 1
             continue
         assert (raised is not None) == (c["threw"] is not None), (c["name"], c["threw"], raised)
@@ -86,7 +98,7 @@ def test_corrupt_in_one_batch_fails_the_batch(corrupt):
     """A batch holding a refused update fails as a whole (Y.applyUpdate of it throws)."""
     base = bytes.fromhex(corrupt["base"])
     for c in corrupt["cases"][:60]:
-        if not c["threw"] or c["threw"].startswith(KNOWN_GAPS):
+        if not c["threw"] or (KNOWN_GAPS and c["threw"].startswith(KNOWN_GAPS)):
             continue
         b = crdt_amd.Batch([base, _bad(corrupt, c)])
         with pytest.raises(crdt_amd.YcrdtError):

@@ -1,6 +1,8 @@
 """libycrdt's multi-rank exchanges at world size 2: two processes on the one GPU, each with its own
-engine, joined by a torch.distributed gloo group that carries the library's collectives through
-the host exchange (ycrdt_comm_create_exchange; RCCL is the same code with device buffers). The
+engine, joined by the package's torch-free TCP hub (crdt_amd/hosthub.py) — and, as a second
+independent transport, a torch.distributed gloo group (tests/torch_comm.py) — that carries the
+library's collectives through the host exchange (ycrdt_comm_create_exchange; RCCL is the same code
+with device buffers). The
 library's own code runs on both ranks — shard export, the pre-exchange status agreement, the flag
 sum, the fleet key-space build and MAX all-reduce, the delete-set all-gather — and every result is
 checked against Yjs fixtures / the unsharded merge:
@@ -44,21 +46,32 @@ def _cases(prefix):
         return [c for c in json.load(f)["cases"] if c["name"].startswith(prefix)]
 
 
-def _worker(rank, world, port, q):
-    import torch.distributed as dist
+def _worker(rank, world, port, q, transport):
+    import sys
 
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    dist.init_process_group("gloo", rank=rank, world_size=world)
-    out = {"rank": rank}
+    sys.path.insert(0, os.path.dirname(HERE))
+    hub = None
+    if transport == "gloo":
+        import torch.distributed as dist
+
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+    else:
+        from crdt_amd.hosthub import HostHub
+
+        hub = HostHub(world, rank, "127.0.0.1", port)
+    out = {"rank": rank, "torch_loaded": "torch" in sys.modules}
     try:
-        import sys
-
-        sys.path.insert(0, os.path.dirname(HERE))
         from crdt_amd.workload import gen_nested
         from tests.v1util import delete_set_of
 
         eng = crdt_amd.Engine()
-        comm = crdt_amd.Comm.over_torch(eng)
+        if transport == "gloo":
+            from tests.torch_comm import comm_over_torch
+
+            comm = comm_over_torch(crdt_amd, eng)
+        else:
+            comm = crdt_amd.Comm.over_hub(eng, hub)
         # ---- sharded merge of one document: every C4 fixture + a generated C4 history
         docs = [[bytes.fromhex(u) for u in c["updates"]] for c in _cases("c4_")]
         docs.append(gen_nested(40, 1500, 200, seed=5)[0])
@@ -135,18 +148,24 @@ def _worker(rank, world, port, q):
         out["error"] = repr(e)
     finally:
         q.put(out)
-        dist.destroy_process_group()
+        if hub is not None:
+            hub.close()
+        else:
+            import torch.distributed as dist
+
+            dist.destroy_process_group()
 
 
 @pytest.mark.timeout(300)
-def test_exchanges_world2_gloo_one_gpu():
+@pytest.mark.parametrize("transport", ["hub", "gloo"])
+def test_exchanges_world2_one_gpu(transport):
     import multiprocessing as mp
 
     world = 2
     ctx = mp.get_context("spawn")
     q = ctx.SimpleQueue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q, transport)) for r in range(world)]
     for p in procs:
         p.start()
     for p in procs:
@@ -156,6 +175,7 @@ def test_exchanges_world2_gloo_one_gpu():
     assert codes == [0, 0], (codes, res)
     for r in res:
         assert "error" not in r, r
+        assert r["torch_loaded"] == (transport == "gloo"), r  # the package's own transport needs no torch
         assert all(r["shard"]), r["shard"]
         for got, want in r["fleet"]:
             assert got == want
