@@ -528,18 +528,27 @@ __global__ __launch_bounds__(256) void k_resolve(Work w, uint32_t nsegs) {
 // SEG_PSUB after YATA with the last member as the winner (g_right == NONE) and every other deleted.
 // The origin-tree order (yc_yata.hip) holds for the shapes Yjs's own histories have. One it does
 // not: a right origin that is a split piece of another item (a segment starting inside its struct)
-// while the item's origin is not the unit before it — the piece's origin. Yjs integrated the item
-// before that split existed and may place it inside the split item; no replica can create that
-// shape (it would have to see the piece without the item), and for a map entry — whose items never
-// carry a right origin from typeMapSet — it only comes from corrupted or crafted bytes: refused
-// (YCRDT_E_UNSUPPORTED) rather than merged into a state Yjs would not reach.
+// while the item's origin is neither the unit before it — the piece's origin — nor a descendant of
+// that unit (an item inserted between the two halves). Yjs integrated such an item before that split
+// existed and may place it inside the split item; no replica can create that shape (it would have
+// to see the piece without the item), and for a map entry — whose items never carry a right origin
+// from typeMapSet — it only comes from corrupted or crafted bytes: refused (YCRDT_E_UNSUPPORTED)
+// rather than merged into a state Yjs would not reach.
+__device__ __forceinline__ bool origin_below(const Work& w, uint32_t o, uint32_t target, uint32_t nsegs) {
+  for (uint32_t it = 0; it <= nsegs && o != NONE; ++it) {  // o: a unit; climb segment by segment
+    const uint32_t so = seg_of(w.u_cutbits, w.u_wpre, o);
+    if (target >= w.g_start[so] && target <= o) return true;  // (the units before o in its segment are its ancestors)
+    o = w.g_origin[so];
+  }
+  return false;
+}
 __global__ void k_mapx_flip(Work w, uint32_t nsegs) {
   const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
   if (s >= nsegs) return;
   const uint32_t f = w.g_flags[s];
   if (!(f & SEG_PSUB) || !(w.k_flags[w.g_key[s]] & KF_YATA)) return;
   const uint32_t r = w.g_rorigin[s];
-  if (r != NONE && !(w.g_flags[seg_of(w.u_cutbits, w.u_wpre, r)] & SEG_EXPLICIT) && w.g_origin[s] != r - 1)
+  if (r != NONE && !(w.g_flags[seg_of(w.u_cutbits, w.u_wpre, r)] & SEG_EXPLICIT) && !origin_below(w, w.g_origin[s], r - 1, nsegs))
     raise_err(&w.ctr->err, ERR_UNSUPPORTED);
   w.g_flags[s] = (f & ~(SEG_PSUB | SEG_WIN)) | SEG_ARRAY | SEG_YMAPX;
 }
