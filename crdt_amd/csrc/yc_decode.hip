@@ -691,6 +691,31 @@ __global__ __launch_bounds__(DL) void k_spec(Work w) {
           start = q;
           break;
         }
+      } else if (w.spec_hint == 2u) {
+        // several sections (a full state: one section per client): the chunk's own struct kind is
+        // unknown, so the hint is SELF-similar — the first of the first 96 bytes where three
+        // consecutive chain steps start with the same struct-kind byte. A snapshot section of one
+        // client's similar structs (C2's base: 15-byte root map entries; its replicas' 4-byte
+        // deleted entries) otherwise locks every chain into a wrong phase for its whole length
+        // (else the first position whose chain parses four structs in a row: wrong phases of a
+        // stream of text keys run into bytes no struct starts with)
+        refill(G.start);
+        const uint32_t lim = min(G.start + 96u, G.end);
+        uint32_t valid4 = NONE;
+        for (uint32_t q = G.start; q < lim; ++q) {
+          const uint32_t c = src.u8(q);
+          if ((c & 31u) > REF_SKIP) continue;
+          const uint32_t d1 = chain_len(src, b, q, uend);
+          if (!d1 || q + d1 >= uend) continue;
+          const uint32_t d2 = chain_len(src, b, q + d1, uend);
+          if (!d2 || q + d1 + d2 >= uend) continue;
+          if (src.u8(q + d1) == c && src.u8(q + d1 + d2) == c) { start = q; valid4 = NONE; break; }
+          if (valid4 == NONE) {
+            const uint32_t q3 = q + d1 + d2, d3 = chain_len(src, b, q3, uend);
+            if (d3 && q3 + d3 < uend && chain_len(src, b, q3 + d3, uend)) valid4 = q;
+          }
+        }
+        if (valid4 != NONE && start == G.start) start = valid4;
       }
     }
   }
@@ -1286,7 +1311,11 @@ __global__ __launch_bounds__(64) void k_fastwalk_multi(Work w) {
         p = q;
         sq[s] = q;
       } else {
-        if (q >= uend) { why(5); return; }  // no meeting within FWM_WALK structs
+        if (q >= uend) {  // no meeting within FWM_WALK structs
+          if (w.dbg && lane == 0) { w.dbg[14] = s; w.dbg[15] = n; w.dbg[13] = popc_range(spec, p1, min(p1 + 4096, uend)); w.dbg[12] = p1 - ustart; w.dbg[11] = uend - ustart; }
+          why(5);
+          return;
+        }
         const uint32_t target = n - k0;
         const uint32_t jq = (q - ustart) / CH;
         uint32_t fch = 0, rem = 0, wy = 0;
@@ -2131,7 +2160,10 @@ __global__ __launch_bounds__(256) void k_ds_decode(Work w) {
     }
   }
   if (phase != PH_DONE) raise_err(err, ERR_DECODE);  // truncated delete set
-  if (lane == 0) w.ds_count[u] = obase - obase0;
+  if (lane == 0) {
+    w.ds_count[u] = obase - obase0;
+    if (obase - obase0 > DSA_WAVE) w.ctr->ds_big = 1u;  // (k_units spreads the rest)
+  }
 }
 
 // ---- Large delete sets, grid-wide. A delete set is a flat varuint stream (readDeleteSet, Y@11105:
@@ -2176,16 +2208,47 @@ __device__ __forceinline__ uint32_t wave_excl_scan(uint32_t x, uint32_t lane, ui
   total = __shfl(incl, 63);
   return incl - x;
 }
+// The chunks the grid path visits: those of the large delete sets only, numbered by one
+// workgroup (per big update: its delete set's chunks, scanned). The three grid kernels stride over
+// them with a fixed grid: launched over every chunk of every large update, the passes cost a C2
+// batch (112 base snapshots, no large delete set) a millisecond beside its struct decode.
+constexpr uint32_t DSP_PLAN_LANES = 1024, DSP_GRID = 1024;
+__global__ __launch_bounds__(DSP_PLAN_LANES) void k_dsp_plan(Work w) {
+  __shared__ uint32_t part[DSP_PLAN_LANES];
+  for (uint32_t bi = threadIdx.x; bi <= w.nbig; bi += DSP_PLAN_LANES) {
+    uint32_t c = 0;
+    if (bi < w.nbig) {
+      const uint32_t u = w.ulist[bi];
+      if (dsp_applies(w, u)) {
+        const uint32_t CH = w.schunk;
+        c = (w.ulen[u] + CH - 1) / CH - (w.dsstart[u] - w.uoff[u]) / CH;
+      }
+    }
+    w.dsp_gb[bi] = c;
+  }
+  __syncthreads();
+  block_scan_u32<DSP_PLAN_LANES>(w.dsp_gb, w.dsp_gb, w.nbig + 1, part);
+}
+// the t-th chunk of the plan: its group index (NONE past the end)
+__device__ __forceinline__ uint32_t dsp_group(const Work& w, uint32_t t) {
+  if (t >= w.dsp_gb[w.nbig]) return NONE;
+  uint32_t lo = 0, hi = w.nbig;  // the last big update whose first planned chunk is <= t
+  while (hi - lo > 1) { const uint32_t m = (lo + hi) >> 1; if (w.dsp_gb[m] <= t) lo = m; else hi = m; }
+  const uint32_t u = w.ulist[lo];
+  return w.ugroup[u] + (w.dsstart[u] - w.uoff[u]) / w.schunk + (t - w.dsp_gb[lo]);
+}
 __global__ __launch_bounds__(256) void k_dsp_count(Work w) {
-  const uint32_t i = (blockIdx.x * blockDim.x + threadIdx.x) >> 6, lane = threadIdx.x & 63;
-  if (i > w.ngroups) return;  // (whole wavefronts)
-  if (i == w.ngroups) { if (lane == 0) w.dsp_cnt[i] = 0; return; }
-  const Group G = w.groups[i];
-  uint32_t p;
-  const uint32_t m = dsp_terms(w, G, lane, p);
-  uint32_t total;
-  wave_excl_scan((uint32_t)__popc(m), lane, total);
-  if (lane == 0) w.dsp_cnt[i] = total;
+  const uint32_t lane = threadIdx.x & 63;
+  for (uint32_t t = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;; t += gridDim.x * (blockDim.x >> 6)) {
+    const uint32_t i = dsp_group(w, t);
+    if (i == NONE) return;  // (whole wavefronts)
+    const Group G = w.groups[i];
+    uint32_t p;
+    const uint32_t m = dsp_terms(w, G, lane, p);
+    uint32_t total;
+    wave_excl_scan((uint32_t)__popc(m), lane, total);
+    if (lane == 0) w.dsp_cnt[i] = total;
+  }
 }
 // the value index of this lane's first terminal: terminals before its chunk in the update's delete
 // set, then before its lane
@@ -2196,9 +2259,7 @@ __device__ __forceinline__ uint32_t dsp_first_index(const Work& w, const Group& 
   const uint32_t ex = wave_excl_scan((uint32_t)__popc(m), lane, total);
   return w.dsp_pre[i] - w.dsp_pre[g0] + ex;
 }
-__global__ __launch_bounds__(256) void k_dsp_vals(Work w) {
-  const uint32_t i = (blockIdx.x * blockDim.x + threadIdx.x) >> 6, lane = threadIdx.x & 63;
-  if (i >= w.ngroups) return;
+__device__ __forceinline__ void dsp_vals_group(const Work& w, uint32_t i, uint32_t lane) {
   const Group G = w.groups[i];
   uint32_t p;
   uint32_t m = dsp_terms(w, G, lane, p);
@@ -2215,6 +2276,14 @@ __global__ __launch_bounds__(256) void k_dsp_vals(Work w) {
     uint32_t x = 0;
     for (uint32_t k = 0; k < n && 7 * k < 32; ++k) x |= (uint32_t)(b[q + k] & 0x7Fu) << (7 * k);
     vals[v] = x;
+  }
+}
+__global__ __launch_bounds__(256) void k_dsp_vals(Work w) {
+  const uint32_t lane = threadIdx.x & 63;
+  for (uint32_t t = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;; t += gridDim.x * (blockDim.x >> 6)) {
+    const uint32_t i = dsp_group(w, t);
+    if (i == NONE) return;
+    dsp_vals_group(w, i, lane);
   }
 }
 __global__ void k_dsp_headers(Work w) {
@@ -2241,11 +2310,10 @@ __global__ void k_dsp_headers(Work w) {
   }
   w.dsp_nb[bi] = c;
   w.ds_count[u] = off;
+  if (off > DSA_WAVE) w.ctr->ds_big = 1u;
   w.dsp_b[u] = bi;
 }
-__global__ __launch_bounds__(256) void k_dsp_ranges(Work w) {
-  const uint32_t i = (blockIdx.x * blockDim.x + threadIdx.x) >> 6, lane = threadIdx.x & 63;
-  if (i >= w.ngroups) return;
+__device__ __forceinline__ void dsp_ranges_group(const Work& w, uint32_t i, uint32_t lane) {
   const Group G = w.groups[i];
   const uint32_t u = G.upd;
   const uint32_t bi = w.dsp_b[u];
@@ -2278,16 +2346,25 @@ __global__ __launch_bounds__(256) void k_dsp_ranges(Work w) {
     out[B.w + (rel >> 1)] = r;
   }
 }
+__global__ __launch_bounds__(256) void k_dsp_ranges(Work w) {
+  const uint32_t lane = threadIdx.x & 63;
+  for (uint32_t t = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;; t += gridDim.x * (blockDim.x >> 6)) {
+    const uint32_t i = dsp_group(w, t);
+    if (i == NONE) return;
+    dsp_ranges_group(w, i, lane);
+  }
+}
 void launch_ds_grid(const Work& w, hipStream_t s) {
-  if (!w.nbig || !w.dsp_cnt) return;
+  if (!w.nbig || !w.dsp_cnt || w.nbig + 1 > DSP_PLAN_LANES * 16) return;
   // YCRDT_DS_GRID=0: every delete set on the wavefront (read per merge: tests compare the two)
   if (const char* g = getenv("YCRDT_DS_GRID")) if (g[0] == '0') return;
-  const uint32_t nb = (uint32_t)(((uint64_t)w.ngroups + 1) * 64 / 256 + 1);
-  hipLaunchKernelGGL(k_dsp_count, dim3(nb), dim3(256), 0, s, w);
+  hipMemsetAsync(w.dsp_cnt, 0, sizeof(uint32_t) * ((size_t)w.ngroups + 1), s);
+  hipLaunchKernelGGL(k_dsp_plan, dim3(1), dim3(DSP_PLAN_LANES), 0, s, w);
+  hipLaunchKernelGGL(k_dsp_count, dim3(DSP_GRID), dim3(256), 0, s, w);
   scan_u32(w.tmp, w.tmp_bytes, w.dsp_cnt, w.dsp_pre, (uint64_t)w.ngroups + 1, s);
-  hipLaunchKernelGGL(k_dsp_vals, dim3(nb), dim3(256), 0, s, w);
+  hipLaunchKernelGGL(k_dsp_vals, dim3(DSP_GRID), dim3(256), 0, s, w);
   hipLaunchKernelGGL(k_dsp_headers, dim3(w.nbig / 64 + 1), dim3(64), 0, s, w);
-  hipLaunchKernelGGL(k_dsp_ranges, dim3(nb), dim3(256), 0, s, w);
+  hipLaunchKernelGGL(k_dsp_ranges, dim3(DSP_GRID), dim3(256), 0, s, w);
 }
 
 __global__ void k_ds_bound(Work w) {  // region size per update: (delete-set bytes + 1) / 2
@@ -2521,6 +2598,7 @@ __global__ __launch_bounds__(256) void k_struct_decode(Work w, uint32_t nstructs
   uint32_t p = p0;
   const int pr = parse_struct<true, 32, WinSrc>(WinSrc{bw, slot, s0}, p, uend, 0xFFFFFFFFu, &v);
   if (pr <= 0) { raise_err(err, pr == -1 ? ERR_UNSUPPORTED : ERR_DECODE); return; }  // -1: any nested > 32 deep
+  const uint32_t ref0 = v.ref;  // (a superseded section's structs are still read: JSON.parse runs on them)
   if (sec.pad && !w.lazy) {  // a superseded section (k_ds_bound): its structs are not integrated
     v.info = (uint8_t)((v.info & 0xE0u) | REF_SKIP);
     v.ref = REF_SKIP;
@@ -2590,6 +2668,23 @@ __global__ __launch_bounds__(256) void k_struct_decode(Work w, uint32_t nstructs
   uint32_t celem = v.cpos;
   if (v.ref == REF_ANY || v.ref == REF_JSON) celem += vu_size(v.nel);
   w.s_celem[i] = celem;
+  // a JSON / Embed / Format content: JSON.parse runs in k_json_structs (a call from here, however
+  // rare, cost every struct one wave per SIMD: the kernel's registers cover the callee's)
+  wave_flag(&w.ctr->any_json, ref0 == REF_JSON || ref0 == REF_EMBED || ref0 == REF_FORMAT);
+}
+// JSON.parse of the JSON / Embed / Format contents (yc_parse.h json_content), one lane per struct,
+// launched only when k_struct_decode saw such a content (Yjs writes ContentAny for JS values)
+__global__ __launch_bounds__(256) void k_json_structs(Work w, uint32_t nstructs) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= nstructs) return;
+  const uint8_t* __restrict__ bw = struct_bytes(w, i);
+  const uint32_t ref = bw[w.s_pos[i]] & 31u;  // (the input's info byte: superseded sections' structs too)
+  if (ref != REF_JSON && ref != REF_EMBED && ref != REF_FORMAT) return;
+  const int jr = json_content(bw, w.s_cpos[i], w.s_cend[i], ref);
+  if (jr) raise_err(&w.ctr->err, jr < 0 ? ERR_UNSUPPORTED : ERR_DECODE);
+}
+void launch_json_structs(const Work& w, uint32_t nstructs, hipStream_t s) {
+  if (nstructs) hipLaunchKernelGGL(k_json_structs, dim3(nstructs / 256 + 1), dim3(256), 0, s, w, nstructs);
 }
 
 // Clocks from the section start and the length prefix; with `states` (integrate mode) also the

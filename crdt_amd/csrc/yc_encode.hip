@@ -49,8 +49,12 @@ __device__ uint32_t encode_struct_general(const Work& w, uint32_t nclients, uint
 // length). So it is a copy of [pos + 1, cpos) and [cpos, cend) — five columns instead of the
 // general path's twenty (and its reference-client lookups).
 // (output struct = segments [a, b))
+// ENC_DEFER: not the whole-item case; the general encoder takes it in a kernel of its own
+// (k_out_sizes_general / k_write_general): inlined, the general path's registers — 74 / 94 VGPRs —
+// cost the one-pass kernels two to three waves per SIMD for every output struct
+constexpr uint32_t ENC_DEFER = 0xFFFFFFFFu;
 template <bool WRITE>
-__device__ __forceinline__ uint32_t encode_struct(const Work& w, uint32_t nclients, uint32_t a, uint32_t b, uint8_t* __restrict__ out, uint64_t p0) {
+__device__ __forceinline__ uint32_t encode_struct_fast(const Work& w, uint32_t a, uint32_t b, uint8_t* __restrict__ out, uint64_t p0) {
   if (b == a + 1 && !w.delta) {
     const uint32_t f = w.g_flags[a], src = w.g_src[a], ga = w.g_start[a], gb = w.g_start[b];
     const uint32_t slen = w.s_len[src], spos = w.s_pos[src], scpos = w.s_cpos[src], scend = w.s_cend[src];
@@ -68,7 +72,7 @@ __device__ __forceinline__ uint32_t encode_struct(const Work& w, uint32_t nclien
       return (uint32_t)(p - p0);
     }
   }
-  return encode_struct_general<WRITE>(w, nclients, a, b, out, p0);
+  return ENC_DEFER;
 }
 
 template <bool WRITE>
@@ -224,12 +228,36 @@ __global__ __launch_bounds__(256) void k_out_sizes(Work w, uint32_t nsegs, uint3
     return;
   }
   const uint32_t o = w.g_outid[s];
-  if (w.g_flags[s] & SEG_MERGE) { w.o_size[nout + (s - o)] = 0; return; }  // (s - o: its rank among the non-starts)
-  uint32_t b = s + 1;
-  while (b < nsegs && (w.g_flags[b] & SEG_MERGE)) ++b;
-  w.o_first[o] = s;
-  w.o_cidx[o] = w.g_cidx[s];
-  w.o_size[o] = encode_struct<false>(w, nclients, s, b, nullptr, 0);
+  const bool start = !(w.g_flags[s] & SEG_MERGE);
+  uint32_t sz = 0;
+  if (!start) {
+    w.o_size[nout + (s - o)] = 0;  // (s - o: its rank among the non-starts)
+  } else {
+    uint32_t b = s + 1;
+    while (b < nsegs && (w.g_flags[b] & SEG_MERGE)) ++b;
+    w.o_first[o] = s;
+    w.o_cidx[o] = w.g_cidx[s];
+    sz = encode_struct_fast<false>(w, s, b, nullptr, 0);
+    w.o_size[o] = sz == ENC_DEFER ? 0u : sz;  // (a deferred one: k_out_sizes_general)
+  }
+  // the deferred output structs, appended to a list (one atomic per wavefront)
+  const bool defer = start && sz == ENC_DEFER;
+  const uint64_t m = __ballot(defer);
+  if (m) {
+    const uint32_t lane = threadIdx.x & 63u, leader = (uint32_t)__ffsll((long long)m) - 1;
+    uint32_t base = 0;
+    if (lane == leader) base = atomicAdd(&w.ctr->pad[6], (uint32_t)__popcll(m));
+    base = __shfl(base, leader);
+    if (defer) w.o_gen[base + (uint32_t)__popcll(m & ((1ull << lane) - 1))] = o;
+  }
+}
+// the deferred output structs (split, merged or delta-cut ones), sized by the general encoder
+__global__ __launch_bounds__(256) void k_out_sizes_general(Work w, uint32_t nclients) {
+  const uint32_t n = w.ctr->pad[6];
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    const uint32_t o = w.o_gen[i];
+    w.o_size[o] = encode_struct_general<false>(w, nclients, w.o_first[o], w.o_first[o + 1], nullptr, 0);
+  }
 }
 
 // runs of consecutive deleted segments (createDeleteSetFromStructStore): their starts were flagged
@@ -378,15 +406,27 @@ __device__ __forceinline__ void totals_body(const Work& w, uint32_t nclients) {
 }
 __global__ void k_totals(Work w, uint32_t nclients) { totals_body(w, nclients); }
 
+__device__ __forceinline__ uint64_t out_pos(const Work& w, uint32_t o) {
+  const uint32_t c = w.o_cidx[o];
+  const uint32_t fi = ccol(w, CC_FIRST_INCL)[c];
+  // (o_pos wraps at 2^32: differences within one client's block are exact)
+  return w.ctr->pad[3] + ccol64(w, CC64_BLKPOS)[c] + ccol(w, CC_HDR)[c] + (uint32_t)(w.o_pos[o] - w.o_pos[fi]);
+}
 __global__ __launch_bounds__(256) void k_write_structs(Work w, uint32_t nsegs, uint32_t nclients) {
   const uint32_t o = blockIdx.x * blockDim.x + threadIdx.x;
   if (o >= w.ctr->nout || w.ctr->pad[5]) return;
   if (w.o_size[o] == 0) return;
-  const uint32_t c = w.o_cidx[o];
-  const uint32_t fi = ccol(w, CC_FIRST_INCL)[c];
-  // (o_pos wraps at 2^32: differences within one client's block are exact)
-  const uint64_t p = w.ctr->pad[3] + ccol64(w, CC64_BLKPOS)[c] + ccol(w, CC_HDR)[c] + (uint32_t)(w.o_pos[o] - w.o_pos[fi]);
-  encode_struct<true>(w, nclients, w.o_first[o], w.o_first[o + 1], w.out, p);
+  // (the deferred ones decline here, k_write_general writes them)
+  encode_struct_fast<true>(w, w.o_first[o], w.o_first[o + 1], w.out, out_pos(w, o));
+}
+__global__ __launch_bounds__(256) void k_write_general(Work w, uint32_t nclients) {
+  if (w.ctr->pad[5]) return;
+  const uint32_t n = w.ctr->pad[6];
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    const uint32_t o = w.o_gen[i];
+    if (w.o_size[o] == 0) continue;
+    encode_struct_general<true>(w, nclients, w.o_first[o], w.o_first[o + 1], w.out, out_pos(w, o));
+  }
 }
 __global__ void k_write_clients(Work w, uint32_t nclients) {
   const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
@@ -503,8 +543,10 @@ void launch_encode_sizes(const Work& w, uint32_t nsegs, uint32_t nclients, hipSt
   hipEventRecord(ev_join, side);
 }
 // the output struct sizes (its own phase: the bench times it live when it is the longest kernel)
+constexpr uint32_t GEN_GRID = 2048;  // grid-stride over the deferred list (its length stays on the device)
 void launch_out_sizes(const Work& w, uint32_t nsegs, uint32_t nclients, hipStream_t s) {
   hipLaunchKernelGGL(k_out_sizes, dim3(nsegs / 256 + 1), dim3(256), 0, s, w, nsegs, nclients);
+  hipLaunchKernelGGL(k_out_sizes_general, dim3(std::min<uint32_t>(nsegs / 256 + 1, GEN_GRID)), dim3(256), 0, s, w, nclients);
 }
 void launch_encode_layout(const Work& w, uint32_t nsegs, uint32_t nclients, hipStream_t s, hipEvent_t ev_join) {
   const uint32_t grid = nsegs / 256 + 1;
@@ -526,7 +568,9 @@ void launch_encode_write(const Work& w, uint32_t nsegs, uint32_t nclients, hipSt
   if (nsegs) hipLaunchKernelGGL(k_write_runs, dim3((nsegs + 255) / 256), dim3(256), 0, s, w, nsegs);
 }
 void launch_write_structs(const Work& w, uint32_t nsegs, uint32_t nclients, hipStream_t s) {
-  if (nsegs) hipLaunchKernelGGL(k_write_structs, dim3((nsegs + 255) / 256), dim3(256), 0, s, w, nsegs, nclients);
+  if (!nsegs) return;
+  hipLaunchKernelGGL(k_write_structs, dim3((nsegs + 255) / 256), dim3(256), 0, s, w, nsegs, nclients);
+  hipLaunchKernelGGL(k_write_general, dim3(std::min<uint32_t>(nsegs / 256 + 1, GEN_GRID)), dim3(256), 0, s, w, nclients);
 }
 
 // Per-document byte ranges of a multi-document encode. Clients are laid out in (document, client)

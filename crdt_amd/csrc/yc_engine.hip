@@ -179,7 +179,7 @@ enum Buf {
   B_UOWN, B_UFLAG, B_UMIN, B_UCUT, B_UWPRE,
   B_GSTART, B_GCIDX, B_GSRC, B_GFLAGS, B_GORIG, B_GRORIG, B_GLINK, B_GOSEG, B_GKEY, B_GMAXC, B_GNEXT, B_GOUTID, B_GTMP, B_GTMP2,
   B_KHASH, B_KROOT, B_KWIN, B_KPAR, B_KFLAG, B_SPK,
-  B_USEC, B_USECN, B_DBG, B_XTAB, B_UFAIL, B_FW, B_CCNT, B_TENTRY, B_XLIST, B_WLEN, B_FWSEC, B_DSPCNT, B_DSPPRE, B_DSPVAL, B_DSPBLK, B_DSPB, B_DSPNB, B_DSPFAIL, B_COFF, B_CPRE, B_OPRE,
+  B_USEC, B_USECN, B_DBG, B_XTAB, B_UFAIL, B_FW, B_CCNT, B_TENTRY, B_XLIST, B_WLEN, B_FWSEC, B_DSPCNT, B_DSPPRE, B_DSPVAL, B_DSPBLK, B_DSPB, B_DSPNB, B_DSPFAIL, B_DSPGB, B_OGEN, B_COFF, B_CPRE, B_OPRE,
   B_LZKEY, B_LZKEYS, B_LZIOTA, B_LZSEC, B_LZRSTART, B_LZPREV, B_LZFIRST, B_LZCAP, B_LZEVBASE, B_LZEVN, B_LZFLAG,
   B_LZLHI, B_LZLLO, B_EVKIND, B_EVSRC, B_EVCLOCK, B_EVLEN, B_EVSIZE, B_EVPOS, B_BLKSIZE, B_BLKPOS, B_SVC, B_SVK,
   B_DSMKEY, B_DSMKEYS, B_DSMLEN, B_DSMLENS, B_DSMEND, B_DSMMAX, B_DSMFLAG, B_DSMRID, B_DRCLIENT, B_DRCLOCK, B_DREND,
@@ -654,6 +654,7 @@ struct Decoded {
   uint64_t nunits = 0, in_len = 0;
   uint32_t array_roots = 0;  // 1: some item names a parent without a parentSub (a YArray may exist)
   uint32_t any_rorigin = 0;  // 1: some item has a right origin (a YMap entry may need full YATA)
+  bool ds_big = false;       // a delete set with more ranges than one wavefront applies
   uint32_t nested = 0;       // 1: some item names a parent item (nested types: dead-type pass needed)
   uint32_t nroots = 0;       // items with an explicit parent (key table bound)
   uint32_t noncanon = 0;     // lazy: some update's sections are not in strictly descending client order
@@ -913,8 +914,8 @@ int run_decode(ycrdt_engine* e, ycrdt_batch* b, bool lazy, Decoded& D, bool gene
   if (dbg_dec && w.dbg) {  // experiments: why k_fastwalk left large updates to k_walk
     unsigned long long h[16];
     HIPCHK(hipMemcpy(h, w.dbg, sizeof(h), hipMemcpyDeviceToHost));
-    fprintf(stderr, "[ycrdt decode] fastwalk: done %llu nsec %llu unsynced %llu | wave: done %llu unsettled %llu other %llu (chunk path: moved / jumped chunk entries) | k_spec exact parses %llu (%llu bytes) | multi-section left to k_walk, by reason 1-7: %llu %llu %llu %llu %llu %llu %llu\n",
-            h[0], h[1], h[2], h[3], h[4], h[5], h[6], h[7], h[9], h[10], h[11], h[12], h[13], h[14], h[15]);
+    fprintf(stderr, "[ycrdt decode] fastwalk: done %llu nsec %llu unsynced %llu | wave: done %llu unsettled %llu other %llu (chunk path: moved / jumped chunk entries) | k_spec exact parses %llu (%llu bytes) | multi-section left to k_walk, by reason 1-5: %llu %llu %llu %llu %llu (section %llu of %llu structs) | %llu %llu %llu\n",
+            h[0], h[1], h[2], h[3], h[4], h[5], h[6], h[7], h[9], h[10], h[11], h[12], h[13], h[14], h[15], h[11], h[12], h[13]);
     HIPCHK(hipMemsetAsync(w.dbg, 0, 128, s));
   }
   if (rc == YCRDT_E_CAPACITY && !generous) return run_decode(e, b, lazy, D, true, sh);  // past the estimates
@@ -978,6 +979,7 @@ int run_decode(ycrdt_engine* e, ycrdt_batch* b, bool lazy, Decoded& D, bool gene
       wd.dsp_val = take<uint32_t>(V, B_DSPVAL, 2ull * w.cap_ds, okd);
       wd.dsp_blk = take<uint4>(V, B_DSPBLK, (uint64_t)w.nbig * DSP_MAXBLK, okd);
       wd.dsp_nb = take<uint32_t>(V, B_DSPNB, w.nbig, okd);
+      wd.dsp_gb = take<uint32_t>(V, B_DSPGB, (uint64_t)w.nbig + 1, okd);
       wd.dsp_b = take<uint32_t>(V, B_DSPB, (uint64_t)w.nupd + 1, okd);
       wd.dsp_fail = take<uint32_t>(V, B_DSPFAIL, (uint64_t)w.nupd + 1, okd);
       if (okd) fill_u32_multi({{wd.dsp_b, (uint64_t)w.nupd + 1, NONE}, {wd.dsp_fail, (uint64_t)w.nupd + 1, 0u}}, e->side);
@@ -1012,12 +1014,18 @@ int run_decode(ycrdt_engine* e, ycrdt_batch* b, bool lazy, Decoded& D, bool gene
   HIPCHK(hipStreamWaitEvent(s, e->side_done, 0));
   rc = check(e, c, "struct decode");
   if (rc) return rc;
+  if (c.any_json) {  // ContentJSON / Embed / Format values: JSON.parse (rare: one more pass and sync)
+    launch_json_structs(w, nstructs, s);
+    rc = check(e, c, "JSON values");
+    if (rc) return rc;
+  }
   D.noncanon = c.noncanon;
   const uint32_t nclients = c.nclients;
   const uint64_t nunits = lazy ? 0 : c.units;
   D.in_len = c.in_len;
   D.array_roots = c.narray_roots;
   D.any_rorigin = c.any_rorigin;
+  D.ds_big = c.ds_big != 0;
   D.nested = c.nested;
   D.nroots = 0;
   for (uint32_t k = 0; k < NSHARD; ++k) D.nroots += c.nroots_sh[k];
@@ -1131,6 +1139,7 @@ int run_merge(ycrdt_engine* e, ycrdt_batch* b, const std::unordered_map<uint32_t
   w.o_cidx = take<uint32_t>(V, B_OCIDX, U + 2, ok);
   w.o_size = take<uint32_t>(V, B_OSIZE, U + 2, ok);
   w.o_pos = take<uint32_t>(V, B_OPOS, U + 2, ok);
+  w.o_gen = take<uint32_t>(V, B_OGEN, U + 2, ok);
   w.r_seg = take<uint32_t>(V, B_RSEG, U + 2, ok);
   w.r_len = take<uint32_t>(V, B_RLEN, U + 2, ok);
   w.r_size = take<uint32_t>(V, B_RSIZE, U + 2, ok);
@@ -1149,7 +1158,7 @@ int run_merge(ycrdt_engine* e, ycrdt_batch* b, const std::unordered_map<uint32_t
   if (U || nds) launch_units_fill(w, U, s);
   mark(e, "merge.units");  // k_units alone
   // with no units, delete-set ranges still have to be checked: each one is pending (pendingDs)
-  if (U || nds) launch_units(w, nstructs, nclients, nds, U, s);
+  if (U || nds) launch_units(w, nstructs, nclients, nds, U, D.ds_big, s);
   mark(e, "merge.segments");
   uint32_t nsegs = 0;
   if (U) {

@@ -28,7 +28,11 @@ bool scan_update(const uint8_t* b, size_t n, bool headers, UpdScan& o) {
     for (uint32_t k = 0; k < ns; ++k) {
       StructView v;
       const uint32_t pos = p;
-      const int r = parse_struct<true>(b, p, end, 0xFFFFFFFFu, &v);
+      int r = parse_struct<true>(b, p, end, 0xFFFFFFFFu, &v);
+      if (r > 0 && (v.ref == REF_JSON || v.ref == REF_EMBED || v.ref == REF_FORMAT)) {  // JSON.parse (k_struct_decode alike)
+        const int jr = json_content(b, v.cpos, v.cend, v.ref);
+        if (jr) r = jr < 0 ? -1 : 0;
+      }
       if (r == -1) o.unsupported = true;  // skip_any's depth limit (exact budget: never the step count)
       if (r <= 0) return false;
       if (ck + v.len > 0xFFFFFFFFull) return false;  // clocks are u32 (k_struct_clock refuses the same)

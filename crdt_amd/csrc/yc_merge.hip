@@ -117,7 +117,6 @@ __device__ __forceinline__ uint32_t ds_range_units(const Work& w, uint32_t nclie
 // a wavefront applies the first DSA_WAVE ranges of its update; a large update's delete set (a
 // full state as one update: C3's 156 MB state holds a million ranges) is spread over the extra
 // workgroups of k_units (unit_ds_apply_big)
-constexpr uint32_t DSA_WAVE = 4096;
 __device__ __forceinline__ void unit_ds_apply(const Work& w, uint32_t nclients, uint32_t blk) {
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t u = (blk * blockDim.x + threadIdx.x) >> 6;
@@ -279,9 +278,9 @@ __global__ __launch_bounds__(256) void k_units(Work w, uint32_t nstructs, uint32
 void launch_units_fill(const Work& w, uint64_t nunits, hipStream_t s) {
   fill_u32_multi({{w.u_owner, nunits, NONE}, {w.u_flags, nunits, 0u}, {w.u_minchild, nunits, NONE}}, s);
 }
-void launch_units(const Work& w, uint32_t nstructs, uint32_t nclients, uint32_t nds, uint64_t nunits, hipStream_t s) {
+void launch_units(const Work& w, uint32_t nstructs, uint32_t nclients, uint32_t nds, uint64_t nunits, bool ds_big, hipStream_t s) {
   const uint32_t nb = (nstructs + 255) / 256, nd = nds && w.nupd ? (w.nupd + 3) / 4 : 0u;
-  const uint32_t nx = nd && w.nbig ? 256u : 0u;  // (they return at once unless a large delete set has > DSA_WAVE ranges)
+  const uint32_t nx = nd && ds_big ? 256u : 0u;  // a delete set of more than DSA_WAVE ranges (k_dsp_headers says)
   if (nb + nd) hipLaunchKernelGGL(k_units, dim3(nb + nd + nx), dim3(256), 0, s, w, nstructs, nclients, nb, nd, nx);
 }
 

@@ -580,9 +580,9 @@ YC_HD inline __attribute__((noinline)) uint32_t json_check(const uint8_t* __rest
   uint32_t res = JSON_OK;
   uint64_t objbits = 0;  // bit d: level d is an object
   int d = 0;
-  uint64_t kh[32];       // the keys of the open objects (hash, level, array index or -1): a repeated
-  uint8_t kl[32];        // key, or an array-index key after another key that is not a smaller
-  int64_t ki[32];        // index, is not what JSON.stringify writes (Object.keys order)
+  uint32_t kh[32];       // the keys of the open objects (hash, level, array index or NONE): a repeated
+  uint8_t kl[32];        // key (or a hash collision: refused either way), or an array-index key after
+  uint32_t ki[32];       // another key that is not a smaller index, is not what JSON.stringify writes
   uint32_t nk = 0;
   auto skip_ws = [&]() { while (p < e && json_ws(b[p])) { ++p; res = JSON_NONCANON; } };
   // an object member's key and colon (p at the key)
@@ -592,11 +592,12 @@ YC_HD inline __attribute__((noinline)) uint32_t json_check(const uint8_t* __rest
     int64_t idx;
     if (json_string(b, p, e, res, h, idx) != JSON_OK) return JSON_BAD;
     const bool first = nk == 0 || kl[nk - 1] != (uint8_t)(d - 1);
-    if (idx >= 0 && !first && (ki[nk - 1] < 0 || ki[nk - 1] >= idx)) res = JSON_NONCANON;  // (JSON.parse moves index keys first)
+    const uint32_t ix = idx >= 0 ? (uint32_t)idx : 0xFFFFFFFFu, h32 = (uint32_t)(h ^ (h >> 32));
+    if (idx >= 0 && !first && (ki[nk - 1] == 0xFFFFFFFFu || ki[nk - 1] >= ix)) res = JSON_NONCANON;  // (JSON.parse moves index keys first)
     for (uint32_t i = nk; i > 0 && kl[i - 1] == (uint8_t)(d - 1); --i)
-      if (kh[i - 1] == h) res = JSON_NONCANON;  // a repeated key (or a hash collision: refused either way)
+      if (kh[i - 1] == h32) res = JSON_NONCANON;
     if (nk == 32) res = JSON_NONCANON;
-    else { kh[nk] = h; kl[nk] = (uint8_t)(d - 1); ki[nk] = idx; ++nk; }
+    else { kh[nk] = h32; kl[nk] = (uint8_t)(d - 1); ki[nk] = ix; ++nk; }
     skip_ws();
     if (p >= e || b[p] != ':') return JSON_BAD;
     ++p;
@@ -657,17 +658,31 @@ YC_HD inline __attribute__((noinline)) uint32_t json_check(const uint8_t* __rest
     }
   }
 }
-// a JSON value inside parse_struct (FULL): 0 ok, otherwise parse_struct's result (0 malformed,
-// -1 valid input the engine refuses); ContentJSON also takes the text "undefined"
-YC_HDI int json_value(const uint8_t* __restrict__ b, uint32_t st, uint32_t k, bool undef_ok) {
-  if (undef_ok && k == 9) {
-    const char* u = "undefined";
-    uint32_t i = 0;
-    while (i < 9 && b[st + i] == (uint8_t)u[i]) ++i;
-    if (i == 9) return 0;
+// The JSON values of one ContentJSON / ContentEmbed / ContentFormat content [p, end) (Y@72137
+// readContentJSON: n varStrings, "undefined" allowed; readContentEmbed: one; readContentFormat: a
+// key, then one): 0 ok, 0x100 malformed (JSON.parse throws), -1 valid input the engine refuses.
+// Called by the exact decoders once a struct's columns are out (k_struct_decode, the host scanner
+// scan_update): inside parse_struct the call kept the whole struct view live across it (+24 VGPRs,
+// one wave per SIMD less for every struct).
+YC_HD inline __attribute__((noinline)) int json_content(const uint8_t* __restrict__ b, uint32_t p, uint32_t end, uint32_t ref) {
+  bool ok = true;
+  uint32_t n = 1;
+  if (ref == REF_JSON) n = rd_vu(b, p, end, ok);
+  else if (ref == REF_FORMAT) { const uint32_t k = rd_vu(b, p, end, ok); p += k; }
+  for (uint32_t i = 0; i < n && ok; ++i) {
+    const uint32_t k = rd_vu(b, p, end, ok);
+    if (!ok) break;
+    const uint8_t* u = b + p;
+    const bool undef = ref == REF_JSON && k == 9 && u[0] == 'u' && u[1] == 'n' && u[2] == 'd' && u[3] == 'e' && u[4] == 'f' &&
+                       u[5] == 'i' && u[6] == 'n' && u[7] == 'e' && u[8] == 'd';
+    if (!undef) {
+      const uint32_t r = json_check(b, p, k);
+      if (r == JSON_BAD) return 0x100;
+      if (r == JSON_NONCANON) return -1;
+    }
+    p += k;
   }
-  const uint32_t r = json_check(b, st, k);
-  return r == JSON_OK ? 0 : r == JSON_BAD ? 0x100 : -1;
+  return ok ? 0 : 0x100;
 }
 
 // Decoded view of one struct (Y@19286 readClientsStructRefs + readItemContent).
@@ -755,7 +770,6 @@ YC_HD inline int parse_struct(const Src& b, uint32_t& p, uint32_t end, uint32_t 
         const uint32_t st = p;
         if (ok) skip_bytes(p, k, end, ok);
         if (FULL && ok && !utf8_valid(b, st, k)) ok = false;
-        if (FULL && ok) { const int jr = json_value(b.b, st, k, true); if (jr) return jr < 0 ? -1 : 0; }
       }
       if (FULL) v->nel = n;
       if (ok && steps == 0) return -1;
@@ -768,7 +782,6 @@ YC_HD inline int parse_struct(const Src& b, uint32_t& p, uint32_t end, uint32_t 
       const uint32_t st = p;
       if (ok) skip_bytes(p, k, end, ok);
       if (FULL && ok && !utf8_valid(b, st, k)) ok = false;
-      if (FULL && ok) { const int jr = json_value(b.b, st, k, false); if (jr) return jr < 0 ? -1 : 0; }
       break;
     }
     case REF_STRING: {
@@ -785,7 +798,6 @@ YC_HD inline int parse_struct(const Src& b, uint32_t& p, uint32_t end, uint32_t 
       const uint32_t st = p;
       if (ok) skip_bytes(p, k, end, ok);
       if (FULL && ok && !utf8_valid(b, st, k)) ok = false;
-      if (FULL && ok) { const int jr = json_value(b.b, st, k, false); if (jr) return jr < 0 ? -1 : 0; }
       break;
     }
     case REF_TYPE: {

@@ -31,6 +31,8 @@ struct Counters {            // device-side counters, read back at the few host 
   uint32_t narray;           // YArray list members (segments)
   uint32_t nmapx;            // 1: a YMap entry needs full YATA (an entry item with a right origin, k_resolve)
   uint32_t any_rorigin;      // 1: a decoded item has a right origin (only then can nmapx be set)
+  uint32_t ds_big;           // 1: a delete set decoded grid-wide has more ranges than one wavefront applies (DSA_WAVE)
+  uint32_t any_json;         // 1: a decoded struct holds ContentJSON / Embed / Format (k_json_structs checks them)
   uint32_t narray_roots;     // 1: a decoded item may root a YArray list (parent given, no parentSub)
   uint32_t tgroups;          // sibling groups of the YArray origin trees (yc_yata.hip)
   uint32_t tbig;             // groups too large for one lane
@@ -135,6 +137,7 @@ struct Work {
   uint4* dsp_blk = nullptr;        // [nbig x DSP_MAXBLK] client blocks of big update b
   uint32_t* dsp_b = nullptr;       // [nupd] big index of an update whose delete set took the grid path, NONE: the wavefront's
   uint32_t* dsp_nb = nullptr;      // [nbig] its client blocks
+  uint32_t* dsp_gb = nullptr;      // [nbig+1] scan of the delete-set chunks of each big update (the grid's work list)
   uint32_t* dsp_fail = nullptr;    // [nupd] a varuint longer than 6 bytes: the wavefront decodes (and reports) it
   uint64_t* ds_scan = nullptr;     // [cap_ds+1]
   uint32_t* dsclient_vals = nullptr; // [cap_dsclients] (client values seen in delete sets)
@@ -297,6 +300,7 @@ struct Work {
   uint32_t* o_cidx = nullptr;      // client of output struct
   uint32_t* o_size = nullptr;      // encoded size (0 = below the target state vector)
   uint32_t* o_pos = nullptr;       // [NO+1] exclusive prefix of o_size
+  uint32_t* o_gen = nullptr;       // [NO] output structs the general encoder takes (count: ctr->pad[6])
   uint32_t* r_seg = nullptr;       // [runs] first segment of delete-set run
   uint32_t* r_len = nullptr;       // [runs] run length in units
   uint32_t* r_size = nullptr;      // [runs+1] encoded size of (clock,len)
@@ -609,11 +613,13 @@ void launch_section_clients(const Work& w, uint32_t nsections, hipStream_t s);
 void launch_client_table(Work& w, uint32_t nsections, hipStream_t s);
 void launch_struct_decode(const Work& w, uint32_t nstructs, hipStream_t s);
 void launch_struct_lenscan(const Work& w, uint32_t nstructs, hipStream_t s);
+void launch_json_structs(const Work& w, uint32_t nstructs, hipStream_t s);  // JSON.parse of JSON-like contents
 void launch_states(const Work& w, uint32_t nstructs, uint32_t nsections, hipStream_t s);  // clocks + client states
 void launch_struct_clocks(const Work& w, uint32_t nstructs, hipStream_t s);               // clocks only (lazy)
 
 void launch_units_fill(const Work& w, uint64_t nunits, hipStream_t s);
-void launch_units(const Work& w, uint32_t nstructs, uint32_t nclients, uint32_t nds, uint64_t nunits, hipStream_t s);
+void launch_units(const Work& w, uint32_t nstructs, uint32_t nclients, uint32_t nds, uint64_t nunits, bool ds_big, hipStream_t s);
+constexpr uint32_t DSA_WAVE = 4096;  // delete-set ranges one wavefront applies per update (k_units); the rest spread
 void launch_segments(const Work& w, uint32_t nclients, uint64_t nunits, hipStream_t s);
 void launch_segment_props_fill(const Work& w, uint32_t nsegs, hipStream_t s);
 void launch_segment_props(const Work& w, uint32_t nsegs, uint32_t nclients, uint64_t nunits, hipStream_t s);
