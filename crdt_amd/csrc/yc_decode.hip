@@ -2568,9 +2568,10 @@ void launch_client_hash(const Work& w, uint64_t* key, uint32_t* val, uint32_t ma
 
 // --------------------------------------------------------------------------- 6. struct decode
 
-__global__ __launch_bounds__(256) void k_struct_decode(Work w, uint32_t nstructs) {
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= nstructs) return;
+// One struct's columns (DEFER: a struct whose content needs the out-of-line `any` reader is
+// appended to the deferred list and left to k_struct_decode_deferred). win: the workgroup's LDS.
+template <bool DEFER>
+__device__ __forceinline__ void struct_decode_one(const Work& w, uint32_t i, uint32_t* win) {
   const uint32_t nclients = w.ctr->nclients;
   uint32_t* err = &w.ctr->err;
   const uint32_t p0 = w.s_pos[i];
@@ -2581,7 +2582,6 @@ __global__ __launch_bounds__(256) void k_struct_decode(Work w, uint32_t nstructs
                                              win_words(w.wsec, w.nwin > 1 ? w.s_win[i] : 0u), p0) - 1];
   w.s_sec[i] = si;
   // the struct's bytes (they depend on its position only) are fetched beside its section record
-  __shared__ __attribute__((aligned(16))) uint32_t win[256 * SD_STRIDE];
   uint32_t* slot = win + threadIdx.x * SD_STRIDE;
   const uint32_t s0 = p0 & ~15u;
   const uint8_t* __restrict__ bw = struct_bytes(w, i);  // the struct's window
@@ -2596,7 +2596,11 @@ __global__ __launch_bounds__(256) void k_struct_decode(Work w, uint32_t nstructs
   const uint32_t doc = doc_of_update(w, sec.upd);
   StructView v;
   uint32_t p = p0;
-  const int pr = parse_struct<true, 32, WinSrc>(WinSrc{bw, slot, s0}, p, uend, 0xFFFFFFFFu, &v);
+  const int pr = parse_struct<true, 32, WinSrc, DEFER>(WinSrc{bw, slot, s0}, p, uend, 0xFFFFFFFFu, &v);
+  if (DEFER && pr == PARSE_DEFER) {
+    w.sd_defer[atomicAdd(&w.ctr->nsd_defer, 1u)] = i;  // (rare: nested `any` containers, ContentDoc)
+    return;
+  }
   if (pr <= 0) { raise_err(err, pr == -1 ? ERR_UNSUPPORTED : ERR_DECODE); return; }  // -1: any nested > 32 deep
   const uint32_t ref0 = v.ref;  // (a superseded section's structs are still read: JSON.parse runs on them)
   if (sec.pad && !w.lazy) {  // a superseded section (k_ds_bound): its structs are not integrated
@@ -2672,6 +2676,19 @@ __global__ __launch_bounds__(256) void k_struct_decode(Work w, uint32_t nstructs
   // rare, cost every struct one wave per SIMD: the kernel's registers cover the callee's)
   wave_flag(&w.ctr->any_json, ref0 == REF_JSON || ref0 == REF_EMBED || ref0 == REF_FORMAT);
 }
+__global__ __launch_bounds__(256) void k_struct_decode(Work w, uint32_t nstructs) {
+  __shared__ __attribute__((aligned(16))) uint32_t win[256 * SD_STRIDE];
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < nstructs) struct_decode_one<true>(w, i, win);
+}
+// the structs k_struct_decode deferred (their contents need the out-of-line `any` reader)
+constexpr uint32_t SD_DEFER_GRID = 1024;
+__global__ __launch_bounds__(256) void k_struct_decode_deferred(Work w) {
+  __shared__ __attribute__((aligned(16))) uint32_t win[256 * SD_STRIDE];
+  const uint32_t n = w.ctr->nsd_defer;
+  for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < n; k += gridDim.x * blockDim.x)
+    struct_decode_one<false>(w, w.sd_defer[k], win);
+}
 // JSON.parse of the JSON / Embed / Format contents (yc_parse.h json_content), one lane per struct,
 // launched only when k_struct_decode saw such a content (Yjs writes ContentAny for JS values)
 __global__ __launch_bounds__(256) void k_json_structs(Work w, uint32_t nstructs) {
@@ -2714,6 +2731,7 @@ __global__ void k_struct_clock(Work w, uint32_t nstructs, uint32_t states) {
 void launch_struct_decode(const Work& w, uint32_t nstructs, hipStream_t s) {
   if (!nstructs) return;
   hipLaunchKernelGGL(k_struct_decode, dim3((nstructs + 255) / 256), dim3(256), 0, s, w, nstructs);
+  hipLaunchKernelGGL(k_struct_decode_deferred, dim3(std::min<uint32_t>(nstructs / 256 + 1, SD_DEFER_GRID)), dim3(256), 0, s, w);
 }
 void launch_struct_lenscan(const Work& w, uint32_t nstructs, hipStream_t s) {
   if (nstructs) scan_u32_to_u64(w.tmp, w.tmp_bytes, w.s_len, w.s_lenscan, nstructs + 1, s);

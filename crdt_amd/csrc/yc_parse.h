@@ -715,7 +715,12 @@ struct RawSrc {
 // Parses one struct starting at p. FULL fills `v`. Speculative callers pass a finite
 // step budget; exact callers pass 0xFFFFFFFF. Returns 1 = ok, 0 = malformed, -1 = budget hit,
 // -2 = ran past `end` (only distinguishable from 0 when `end` is not the update end).
-template <bool FULL, int DEPTH = 32, class Src = RawSrc>
+// DEFER: a content that needs the out-of-line `any` reader (containers nested past one level, a
+// ContentDoc's options) returns PARSE_DEFER instead of calling it — the caller hands the struct to
+// a kernel of its own (a call site in a kernel sizes its registers for the callee's: k_struct_decode
+// ran one wave per SIMD short for every struct).
+constexpr int PARSE_DEFER = -3;
+template <bool FULL, int DEPTH = 32, class Src = RawSrc, bool DEFER = false>
 YC_HD inline int parse_struct(const Src& b, uint32_t& p, uint32_t end, uint32_t steps, StructView* v) {
   bool ok = true;
   if (p >= end) return -2;
@@ -820,6 +825,7 @@ YC_HD inline int parse_struct(const Src& b, uint32_t& p, uint32_t end, uint32_t 
         } else if (p < end && steps > 0 && (tag == 117u || tag == 118u) && any_flat<FULL>(b, p, end, steps, ok, cf)) {
           // (a one-level container of scalars, inline)
         } else {
+          if (DEFER) return PARSE_DEFER;
           const AnySkip r = skip_any_nl<DEPTH, FULL>(b.b, p, end, steps);
           p = r.p;
           steps = r.steps;
@@ -835,6 +841,7 @@ YC_HD inline int parse_struct(const Src& b, uint32_t& p, uint32_t end, uint32_t 
     case REF_DOC: {
       skip_str<FULL>(b, p, end, ok);
       if (ok) {
+        if (DEFER) return PARSE_DEFER;
         const AnySkip r = skip_any_nl<DEPTH, FULL>(b.b, p, end, steps);
         p = r.p;
         steps = r.steps;

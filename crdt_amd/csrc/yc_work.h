@@ -32,6 +32,7 @@ struct Counters {            // device-side counters, read back at the few host 
   uint32_t nmapx;            // 1: a YMap entry needs full YATA (an entry item with a right origin, k_resolve)
   uint32_t any_rorigin;      // 1: a decoded item has a right origin (only then can nmapx be set)
   uint32_t ds_big;           // 1: a delete set decoded grid-wide has more ranges than one wavefront applies (DSA_WAVE)
+  uint32_t nsd_defer;        // structs k_struct_decode deferred to k_struct_decode_deferred
   uint32_t any_json;         // 1: a decoded struct holds ContentJSON / Embed / Format (k_json_structs checks them)
   uint32_t narray_roots;     // 1: a decoded item may root a YArray list (parent given, no parentSub)
   uint32_t tgroups;          // sibling groups of the YArray origin trees (yc_yata.hip)
@@ -162,6 +163,7 @@ struct Work {
   uint32_t* s_cpos = nullptr;      // content byte range
   uint32_t* s_cend = nullptr;
   uint32_t* s_celem = nullptr;     // position of first Any/JSON element (after the count varuint)
+  uint32_t* sd_defer = nullptr;    // [S] structs whose decode k_struct_decode deferred (nested `any`, ContentDoc)
   // ---- clients (NC)
   uint32_t* cl_vals = nullptr;     // sorted distinct client ids [cap_sections]
   uint64_t* cl_key = nullptr;      // multi-doc: sorted distinct (doc << 32 | client) keys; cl_vals = their low words
