@@ -1140,7 +1140,7 @@ int run_merge(ycrdt_engine* e, ycrdt_batch* b, const std::unordered_map<uint32_t
   w.o_cidx = take<uint32_t>(V, B_OCIDX, U + 2, ok);
   w.o_size = take<uint32_t>(V, B_OSIZE, U + 2, ok);
   w.o_pos = take<uint32_t>(V, B_OPOS, U + 2, ok);
-  w.o_gen = take<uint32_t>(V, B_OGEN, U + 2, ok);
+  w.o_gen = take<uint8_t>(V, B_OGEN, U + 2, ok);
   w.r_seg = take<uint32_t>(V, B_RSEG, U + 2, ok);
   w.r_len = take<uint32_t>(V, B_RLEN, U + 2, ok);
   w.r_size = take<uint32_t>(V, B_RSIZE, U + 2, ok);

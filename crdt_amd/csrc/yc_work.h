@@ -302,7 +302,7 @@ struct Work {
   uint32_t* o_cidx = nullptr;      // client of output struct
   uint32_t* o_size = nullptr;      // encoded size (0 = below the target state vector)
   uint32_t* o_pos = nullptr;       // [NO+1] exclusive prefix of o_size
-  uint32_t* o_gen = nullptr;       // [NO] output structs the general encoder takes (count: ctr->pad[6])
+  uint8_t* o_gen = nullptr;        // [NO] 1: the general encoder takes the output struct (k_out_sizes_general)
   uint32_t* r_seg = nullptr;       // [runs] first segment of delete-set run
   uint32_t* r_len = nullptr;       // [runs] run length in units
   uint32_t* r_size = nullptr;      // [runs+1] encoded size of (clock,len)
