@@ -457,8 +457,10 @@ __device__ __attribute__((noinline)) uint32_t exact_len(const uint8_t* __restric
   uint32_t q = p;
   return parse_struct<false>(b, q, end, 0xFFFFFFFFu, nullptr) > 0 ? q - p : 0u;
 }
+template <uint32_t DWT>
 __global__ __launch_bounds__(DL) void k_direct(Work w) {
-  __shared__ __attribute__((aligned(16))) uint32_t win[DL * DSTRIDE];
+  constexpr uint32_t DSTR = DWT / 4 + 4;
+  __shared__ __attribute__((aligned(16))) uint32_t win[DL * DSTR];
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= w.nsmall) return;
   const uint32_t u = w.ulist[w.nbig + i];
@@ -468,13 +470,13 @@ __global__ __launch_bounds__(DL) void k_direct(Work w) {
   uint64_t* __restrict__ sbits = win_words(w.sec_bits, uw);
   const uint32_t ustart = w.uoff[u], uend = ustart + w.ulen[u];
   uint32_t* err = &w.ctr->err;
-  uint32_t* slot = win + threadIdx.x * DSTRIDE;
+  uint32_t* slot = win + threadIdx.x * DSTR;
   LdsSrc src{b, slot, 0, 0};
   auto refill = [&](uint32_t p) {
     src.s0 = p & ~15u;
-    src.wlen = min(DW, (uend + 15u - src.s0) & ~15u);
+    src.wlen = min(DWT, (uend + 15u - src.s0) & ~15u);
     const uint4* g = (const uint4*)(b + src.s0);
-    fill_window(slot, g);
+    fill_window<DWT>(slot, g);
   };
   w.dsstart[u] = NONE;
   bool ok = true;
@@ -508,7 +510,7 @@ __global__ __launch_bounds__(DL) void k_direct(Work w) {
       m |= 1ull << (p & 63);
       // the whole wavefront at once: one stall, not one per lane (a window that already reaches
       // the update end is never refilled)
-      if (__ballot(src.wlen == DW && p - src.s0 + DREFILL > DW)) refill(p);
+      if (__ballot(src.wlen == DWT && p - src.s0 + DREFILL > DWT)) refill(p);
       RegWin x;
       src.load_win(p, x);
       uint32_t d = win_len(x, p & 3u, p, uend);
@@ -1932,7 +1934,9 @@ void launch_direct(const Work& w, hipStream_t s) {
   else if (wave_decode(w)) {
     hipLaunchKernelGGL(k_wlen, dim3(WD_MAX / WL_SPAN, w.nsmall), dim3(256), 0, s, w);
     hipLaunchKernelGGL(k_wrank, dim3(w.nsmall), dim3(WR_LANES), 0, s, w);
-  } else if (w.nsmall) hipLaunchKernelGGL(k_direct, dim3((w.nsmall + DL - 1) / DL), dim3(DL), 0, s, w);
+  } else if (w.nsmall) {
+    hipLaunchKernelGGL(k_direct<DW>, dim3((w.nsmall + DL - 1) / DL), dim3(DL), 0, s, w);  // (64 / 96 / 256 B windows: slower on C2)
+  }
 }
 
 // --------------------------------------------------------------------------- 3. struct positions
@@ -2538,7 +2542,9 @@ void launch_client_table(Work& w, uint32_t nsections, hipStream_t s) {
     hipLaunchKernelGGL(k_unique_keys, dim3(grid), dim3(256), 0, s, w, nsections);
     scan_u32(w.tmp, w.tmp_bytes, w.scratch, w.cl_tmp, nsections + 1, s);
     hipLaunchKernelGGL(k_unique_keys_scatter, dim3(grid), dim3(256), 0, s, w, nsections);
-    hipMemcpyAsync(w.cl_key, w.cl_key2, sizeof(uint64_t) * nsections, hipMemcpyDeviceToDevice, s);
+    // the distinct keys are in cl_key2: the two buffers trade places (a copy back waited ~0.6 ms
+    // for compute units beside the delete-set decode on the side stream)
+    std::swap(w.cl_key, w.cl_key2);
     hipLaunchKernelGGL(k_section_cidx_multi, dim3(grid), dim3(256), 0, s, w, nsections);
     return;
   }
@@ -2546,9 +2552,9 @@ void launch_client_table(Work& w, uint32_t nsections, hipStream_t s) {
   sort_u32(w.tmp, w.tmp_bytes, w.cl_tmp, w.cl_vals, nsections, s);
   hipLaunchKernelGGL(k_unique_flags, dim3(grid), dim3(256), 0, s, w.cl_vals, nsections, w.scratch);
   scan_u32(w.tmp, w.tmp_bytes, w.scratch, w.cl_tmp, nsections + 1, s);
-  // compact in place is unsafe; use cl_state as scratch output, then copy back
+  // compact in place is unsafe: into cl_state's buffer, and the two trade places (same size)
   hipLaunchKernelGGL(k_unique_scatter, dim3(grid), dim3(256), 0, s, w.cl_vals, w.cl_tmp, nsections, w.cl_state, &w.ctr->nclients, w.cl_single);
-  hipMemcpyAsync(w.cl_vals, w.cl_state, sizeof(uint32_t) * nsections, hipMemcpyDeviceToDevice, s);
+  std::swap(w.cl_vals, w.cl_state);
   hipLaunchKernelGGL(k_section_cidx, dim3(grid), dim3(256), 0, s, w.sections, nsections, w.cl_vals, &w.ctr->nclients);
 }
 
@@ -2676,7 +2682,7 @@ __device__ __forceinline__ void struct_decode_one(const Work& w, uint32_t i, uin
   // rare, cost every struct one wave per SIMD: the kernel's registers cover the callee's)
   wave_flag(&w.ctr->any_json, ref0 == REF_JSON || ref0 == REF_EMBED || ref0 == REF_FORMAT);
 }
-__global__ __launch_bounds__(256) void k_struct_decode(Work w, uint32_t nstructs) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_struct_decode(Work w, uint32_t nstructs) {
   __shared__ __attribute__((aligned(16))) uint32_t win[256 * SD_STRIDE];
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i < nstructs) struct_decode_one<true>(w, i, win);

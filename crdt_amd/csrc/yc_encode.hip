@@ -56,7 +56,7 @@ constexpr uint32_t ENC_DEFER = 0xFFFFFFFFu;
 template <bool WRITE>
 __device__ __forceinline__ uint32_t encode_struct_fast(const Work& w, uint32_t a, uint32_t b, uint8_t* __restrict__ out, uint64_t p0) {
   if (b == a + 1 && !w.delta) {
-    const uint32_t f = w.g_flags[a], src = w.g_src[a], ga = w.g_start[a], gb = w.g_start[b];
+    const uint32_t f = w.g_flags[a], src = w.g_src[a], ga = seg_start(w, a), gb = seg_start(w, b);
     const uint32_t slen = w.s_len[src], spos = w.s_pos[src], scpos = w.s_cpos[src], scend = w.s_cend[src];
     const uint32_t info0 = w.s_info[src], spk = w.s_pk[src];
     if ((f & (SEG_ITEM | SEG_EXPLICIT)) == (SEG_ITEM | SEG_EXPLICIT) && gb - ga == slen && !(spk & 0xC0u)) {
@@ -81,7 +81,7 @@ __device__ __forceinline__ uint32_t encode_struct_general(const Work& w, uint32_
   // The columns a struct can need are loaded in three dependent rounds — its first segment's row,
   // then its source struct's and its client's, then the reference clients' — each round issued
   // whole before anything branches on it, instead of one memory round trip per field.
-  const uint32_t cidx = w.g_cidx[a], ga = w.g_start[a], gb = w.g_start[b], f = w.g_flags[a], src = w.g_src[a];
+  const uint32_t cidx = w.g_cidx[a], ga = seg_start(w, a), gb = seg_start(w, b), f = w.g_flags[a], src = w.g_src[a];
   const uint32_t go = w.g_origin[a], gr = w.g_rorigin[a];
   const uint64_t base = w.cl_base[cidx], base1 = w.cl_base[cidx + 1];
   const uint32_t cs = w.cl_start[cidx], cval = w.cl_vals[cidx];
@@ -189,7 +189,7 @@ __device__ __forceinline__ uint32_t encode_struct_general(const Work& w, uint32_
       for (uint32_t s = a; s < b; ++s) {
         const uint32_t sr = w.g_src[s];
         const uint32_t sb = w.s_clock[sr];  // source struct's first clock
-        const uint32_t u0 = max((uint32_t)(w.g_start[s] - base), k0 + off), u1 = (uint32_t)(w.g_start[s + 1] - base);
+        const uint32_t u0 = max((uint32_t)(seg_start(w, s) - base), k0 + off), u1 = (uint32_t)(seg_start(w, s + 1) - base);
         if (u1 <= u0) continue;
         if (ref == REF_ANY && (w.s_pk[sr] & 0x40u)) {  // flagged content: writeAny's form
           const uint32_t nb = any_canon<WRITE>(struct_bytes(w, sr), w.s_celem[sr], w.s_cend[sr], u0 - sb, u1 - sb, out, p);
@@ -243,12 +243,30 @@ __global__ __launch_bounds__(256) void k_out_sizes(Work w, uint32_t nsegs, uint3
     w.o_size[o] = sz == ENC_DEFER ? 0u : sz;
     w.o_gen[o] = sz == ENC_DEFER ? 1u : 0u;
   }
+  wave_flag(&w.ctr->pad[6], sz == ENC_DEFER);  // (the general kernels run only when some struct is deferred)
 }
 // the deferred output structs (split, merged or delta-cut ones), sized by the general encoder
+// (the flags are read 16 at a time: a quad of zeros — nearly all of them — is skipped whole; the
+// buffer is padded to whole quads, and flags past NO are never taken)
+template <class F>
+__device__ __forceinline__ void for_deferred(const Work& w, uint32_t n, F f) {
+  const uint32_t nq = (n + 15) / 16;
+  for (uint32_t q = blockIdx.x * blockDim.x + threadIdx.x; q < nq; q += gridDim.x * blockDim.x) {
+    const uint4 v = ((const uint4*)w.o_gen)[q];
+    if (!(v.x | v.y | v.z | v.w)) continue;
+    const uint32_t m[4] = {v.x, v.y, v.z, v.w};
+    for (uint32_t k = 0; k < 16; ++k)
+      if ((m[k >> 2] >> ((k & 3u) * 8)) & 0xFFu) {
+        const uint32_t o = q * 16 + k;
+        if (o < n) f(o);
+      }
+  }
+}
 __global__ __launch_bounds__(256) void k_out_sizes_general(Work w, uint32_t nclients) {
-  const uint32_t n = w.ctr->nout;
-  for (uint32_t o = blockIdx.x * blockDim.x + threadIdx.x; o < n; o += gridDim.x * blockDim.x)
-    if (w.o_gen[o]) w.o_size[o] = encode_struct_general<false>(w, nclients, w.o_first[o], w.o_first[o + 1], nullptr, 0);
+  if (!w.ctr->pad[6]) return;
+  for_deferred(w, w.ctr->nout, [&](uint32_t o) {
+    w.o_size[o] = encode_struct_general<false>(w, nclients, w.o_first[o], w.o_first[o + 1], nullptr, 0);
+  });
 }
 
 // runs of consecutive deleted segments (createDeleteSetFromStructStore): their starts were flagged
@@ -261,7 +279,7 @@ __device__ __forceinline__ void run_fill_at(const Work& w, uint32_t s, uint32_t 
   if (w.g_tmp2[s + 1] != w.g_tmp2[s]) w.r_seg[rid] = s;  // s starts run rid
   // s ends run rid: the next segment is live or belongs to another client
   const bool last = s + 1 == nsegs || w.g_cidx[s + 1] != w.g_cidx[s] || !seg_deleted(w.g_flags[s + 1]);
-  if (last) w.r_len[rid] = w.g_start[s + 1];  // end unit; the start is subtracted in k_run_sizes
+  if (last) w.r_len[rid] = seg_start(w, s + 1);  // end unit; the start is subtracted in k_run_sizes
 }
 __global__ void k_run_fill(Work w, uint32_t nsegs) {
   const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
@@ -270,9 +288,9 @@ __global__ void k_run_fill(Work w, uint32_t nsegs) {
 __device__ __forceinline__ void run_sizes_at(const Work& w, uint32_t r, uint32_t nsegs) {
   if (r >= w.g_tmp2[nsegs]) { w.r_size[r] = 0; return; }
   const uint32_t s = w.r_seg[r];
-  const uint32_t len = w.r_len[r] - w.g_start[s];
+  const uint32_t len = w.r_len[r] - seg_start(w, s);
   w.r_len[r] = len;
-  const uint32_t clock = (uint32_t)(w.g_start[s] - w.cl_base[w.g_cidx[s]]);
+  const uint32_t clock = (uint32_t)(seg_start(w, s) - w.cl_base[w.g_cidx[s]]);
   w.r_size[r] = vu_size(clock) + vu_size(len);
 }
 __global__ void k_run_sizes(Work w, uint32_t nsegs) {
@@ -332,7 +350,7 @@ __global__ void k_client_sizes(Work w, uint32_t nclients, uint32_t nsegs) {
     uint32_t lo = fo, hi = cs == 0 ? fo : eo;  // a full-state encode starts at the first output
     while (lo < hi) {
       const uint32_t mid = (lo + hi) >> 1;
-      const uint32_t k1 = (uint32_t)(w.g_start[w.o_first[mid + 1]] - w.cl_base[c]);
+      const uint32_t k1 = (uint32_t)(seg_start(w, w.o_first[mid + 1]) - w.cl_base[c]);
       if (k1 <= cs) lo = mid + 1; else hi = mid;
     }
     fi = lo;
@@ -411,10 +429,10 @@ __global__ __launch_bounds__(256) void k_write_structs(Work w, uint32_t nsegs, u
   encode_struct_fast<true>(w, w.o_first[o], w.o_first[o + 1], w.out, out_pos(w, o));
 }
 __global__ __launch_bounds__(256) void k_write_general(Work w, uint32_t nclients) {
-  if (w.ctr->pad[5]) return;
-  const uint32_t n = w.ctr->nout;
-  for (uint32_t o = blockIdx.x * blockDim.x + threadIdx.x; o < n; o += gridDim.x * blockDim.x)
-    if (w.o_gen[o] && w.o_size[o]) encode_struct_general<true>(w, nclients, w.o_first[o], w.o_first[o + 1], w.out, out_pos(w, o));
+  if (w.ctr->pad[5] || !w.ctr->pad[6]) return;
+  for_deferred(w, w.ctr->nout, [&](uint32_t o) {
+    if (w.o_size[o]) encode_struct_general<true>(w, nclients, w.o_first[o], w.o_first[o + 1], w.out, out_pos(w, o));
+  });
 }
 __global__ void k_write_clients(Work w, uint32_t nclients) {
   const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
@@ -453,7 +471,7 @@ __global__ void k_write_runs(Work w, uint32_t nsegs) {
   const uint32_t nr = ccol(w, CC_NRUNS)[c];
   const uint64_t dsbase = w.ctr->ds_base + vu_size(w.ctr->pad[1]);
   uint64_t p = dsbase + ccol64(w, CC64_DSPOS)[c] + vu_size(w.cl_vals[c]) + vu_size(nr) + (uint32_t)(w.r_pos[r] - w.r_pos[first]);
-  p = wr_vu(w.out, p, (uint32_t)(w.g_start[s] - w.cl_base[c]));
+  p = wr_vu(w.out, p, (uint32_t)(seg_start(w, s) - w.cl_base[c]));
   wr_vu(w.out, p, w.r_len[r]);
 }
 
@@ -510,8 +528,10 @@ static void rev_scans(const Work& w, uint32_t nclients, hipStream_t s) {
 
 // Phase 1: sizes + layout (ends with out_bytes / sv_bytes in the counters). No host sync: the
 // output / run counts are read on the device, grids and scans are sized for NS + 1 entries.
+bool encode_runs_small(uint32_t nsegs) { return nsegs + 1 <= RUNS_SMALL; }
+// runs_scanned: k_merge_flags already made the run ids (g_tmp2)
 void launch_encode_sizes(const Work& w, uint32_t nsegs, uint32_t nclients, hipStream_t s, hipStream_t side,
-                         hipEvent_t ev_fork, hipEvent_t ev_join, void* tmp2, size_t tmp2_bytes) {
+                         hipEvent_t ev_fork, hipEvent_t ev_join, void* tmp2, size_t tmp2_bytes, bool runs_scanned) {
   fill_u32_multi({{w.ctr->pad, 8, 0u}, {w.cc + (size_t)CC_NRUNS * (w.cap_clients + 1), (uint64_t)w.cap_clients + 1, 0u}}, s);
   const uint32_t grid = nsegs / 256 + 1;
   if (nsegs + 1 <= RUNS_SMALL) {  // (a small batch: one launch, main stream)
@@ -524,14 +544,16 @@ void launch_encode_sizes(const Work& w, uint32_t nsegs, uint32_t nclients, hipSt
   hipEventRecord(ev_fork, s);
   hipStreamWaitEvent(side, ev_fork, 0);
   if (!nsegs) fill_u32_multi({{w.r_size, 1, 0u}}, side);  // (no merge-flag pass wrote the run starts)
-  scan_u32(tmp2, tmp2_bytes, w.r_size, w.g_tmp2, nsegs + 1, side);
+  if (!runs_scanned) scan_u32(tmp2, tmp2_bytes, w.r_size, w.g_tmp2, nsegs + 1, side);
   if (nsegs) hipLaunchKernelGGL(k_run_fill, dim3((nsegs + 255) / 256), dim3(256), 0, side, w, nsegs);
+  // (a look-back fused into k_run_sizes ran 2x slower beside k_out_sizes_general: its waiting
+  // wavefronts held the CUs the main stream's kernel needed)
   hipLaunchKernelGGL(k_run_sizes, dim3(grid), dim3(256), 0, side, w, nsegs);
   scan_u32(tmp2, tmp2_bytes, w.r_size, w.r_pos, nsegs + 1, side);
   hipEventRecord(ev_join, side);
 }
 // the output struct sizes (its own phase: the bench times it live when it is the longest kernel)
-constexpr uint32_t GEN_GRID = 2048;  // grid-stride over the deferred list (its length stays on the device)
+constexpr uint32_t GEN_GRID = 2048;  // grid-stride over the deferral flags (NO stays on the device)
 void launch_out_sizes(const Work& w, uint32_t nsegs, uint32_t nclients, hipStream_t s) {
   hipLaunchKernelGGL(k_out_sizes, dim3(nsegs / 256 + 1), dim3(256), 0, s, w, nsegs, nclients);
   hipLaunchKernelGGL(k_out_sizes_general, dim3(std::min<uint32_t>(nsegs / 256 + 1, GEN_GRID)), dim3(256), 0, s, w, nclients);

@@ -176,7 +176,7 @@ enum Buf {
   B_SPOS, B_SSEC, B_SLEN, B_SLENSCAN, B_SCLOCK, B_SCIDX, B_SINFO, B_SOC, B_SOK, B_SRC, B_SRK, B_SPA, B_SPB, B_SPS, B_SPL,
   B_SCPOS, B_SCEND, B_SCELEM,
   B_CLVALS, B_CLTMP, B_CLSTATE, B_CLBASE, B_CLSTART, B_CC, B_CC64, B_SWIN,
-  B_UOWN, B_UFLAG, B_UMIN, B_UCUT, B_UWPRE,
+  B_UOWN, B_UFLAG, B_UCUT, B_UWPRE,
   B_GSTART, B_GCIDX, B_GSRC, B_GFLAGS, B_GORIG, B_GRORIG, B_GLINK, B_GOSEG, B_GKEY, B_GMAXC, B_GNEXT, B_GOUTID, B_GTMP, B_GTMP2,
   B_KHASH, B_KROOT, B_KWIN, B_KPAR, B_KFLAG, B_SPK,
   B_USEC, B_USECN, B_DBG, B_XTAB, B_UFAIL, B_FW, B_CCNT, B_TENTRY, B_XLIST, B_WLEN, B_FWSEC, B_DSPCNT, B_DSPPRE, B_DSPVAL, B_DSPBLK, B_DSPB, B_DSPNB, B_DSPFAIL, B_DSPGB, B_OGEN, B_SDDEFER, B_COFF, B_CPRE, B_OPRE,
@@ -1120,7 +1120,6 @@ int run_merge(ycrdt_engine* e, ycrdt_batch* b, const std::unordered_map<uint32_t
   w.cap_units = U + 1;
   w.u_owner = take<uint32_t>(V, B_UOWN, U + 1, ok);
   w.u_flags = take<uint32_t>(V, B_UFLAG, U + 1, ok);
-  w.u_minchild = take<uint32_t>(V, B_UMIN, U + 1, ok);
   w.u_cutbits = take<uint64_t>(V, B_UCUT, uw, ok);
   w.u_wpre = take<uint32_t>(V, B_UWPRE, uw + 1, ok);
   w.scratch = take<uint32_t>(V, B_SCRATCH, std::max<uint64_t>({nwords + 2, (uint64_t)w.cap_sections + 66, uw + 2, U + 2}), ok);
@@ -1140,7 +1139,7 @@ int run_merge(ycrdt_engine* e, ycrdt_batch* b, const std::unordered_map<uint32_t
   w.o_cidx = take<uint32_t>(V, B_OCIDX, U + 2, ok);
   w.o_size = take<uint32_t>(V, B_OSIZE, U + 2, ok);
   w.o_pos = take<uint32_t>(V, B_OPOS, U + 2, ok);
-  w.o_gen = take<uint8_t>(V, B_OGEN, U + 2, ok);
+  w.o_gen = take<uint8_t>(V, B_OGEN, U + 32, ok);  // (whole 16-byte quads: for_deferred)
   w.r_seg = take<uint32_t>(V, B_RSEG, U + 2, ok);
   w.r_len = take<uint32_t>(V, B_RLEN, U + 2, ok);
   w.r_size = take<uint32_t>(V, B_RSIZE, U + 2, ok);
@@ -1204,6 +1203,7 @@ int run_merge(ycrdt_engine* e, ycrdt_batch* b, const std::unordered_map<uint32_t
     return okl;
   };
   uint32_t nout = 0;
+  bool runs_scanned = false;  // (k_merge_flags made the delete-set run ids)
   e->nsegs = nsegs;
   e->nlists = 0;
   if (nsegs) {
@@ -1268,7 +1268,7 @@ int run_merge(ycrdt_engine* e, ycrdt_batch* b, const std::unordered_map<uint32_t
       }
       mark(e, "merge.merge_flags");
       if (!sh) {
-        launch_merge_flags(w, nsegs, s, !D.nested);
+        runs_scanned = launch_merge_flags(w, nsegs, s, !D.nested);
       } else {
         launch_merge_flags_only(w, nsegs, s, !D.nested);
         launch_shard_export(w, nsegs, owner, shard, acc, s);
@@ -1305,7 +1305,7 @@ int run_merge(ycrdt_engine* e, ycrdt_batch* b, const std::unordered_map<uint32_t
   uint8_t* tmp2 = take<uint8_t>(V, B_TMP2, prim_tmp_bytes((uint64_t)nsegs + 2, 0), ok);
   if (!ok) return fail(YCRDT_E_DEVICE, oom("scan space"));
   mark(e, "encode.runs");
-  launch_encode_sizes(w, nsegs, nclients, s, e->side, e->side_fork, e->side_done, tmp2, V[B_TMP2].cap);
+  launch_encode_sizes(w, nsegs, nclients, s, e->side, e->side_fork, e->side_done, tmp2, V[B_TMP2].cap, runs_scanned);
   mark(e, "encode.sizes");  // k_out_sizes alone
   launch_out_sizes(w, nsegs, nclients, s);
   mark(e, "encode.layout");

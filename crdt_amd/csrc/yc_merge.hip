@@ -26,9 +26,6 @@
 namespace yc {
 
 
-__device__ __forceinline__ uint32_t seg_of(const uint64_t* __restrict__ cut, const uint32_t* __restrict__ wpre, uint32_t g) {
-  return wpre[g >> 6] + (uint32_t)__popcll(cut[g >> 6] & ((2ull << (g & 63)) - 1)) - 1;
-}
 
 // --------------------------------------------------------------------------- owner / dedupe
 // One lane per struct (one per delete-set range below): a struct's units are consecutive in the
@@ -276,7 +273,7 @@ __global__ __launch_bounds__(256) void k_units(Work w, uint32_t nstructs, uint32
   }
 }
 void launch_units_fill(const Work& w, uint64_t nunits, hipStream_t s) {
-  fill_u32_multi({{w.u_owner, nunits, NONE}, {w.u_flags, nunits, 0u}, {w.u_minchild, nunits, NONE}}, s);
+  fill_u32_multi({{w.u_owner, nunits, NONE}, {w.u_flags, nunits, 0u}}, s);
 }
 void launch_units(const Work& w, uint32_t nstructs, uint32_t nclients, uint32_t nds, uint64_t nunits, bool ds_big, hipStream_t s) {
   const uint32_t nb = (nstructs + 255) / 256, nd = nds && w.nupd ? (w.nupd + 3) / 4 : 0u;
@@ -360,7 +357,7 @@ __global__ __launch_bounds__(256) void k_seg_props(Work w, uint32_t nsegs) {
   if (s >= nsegs) return;
   // the source struct's columns in one round of loads (the right-origin clock is unwritten when
   // there is none: read, never used), then the client bases
-  const uint32_t g0 = w.g_start[s];
+  const uint32_t g0 = seg_start(w, s);
   const uint32_t own = w.u_owner[g0];
   const uint32_t f = w.u_flags[g0];
   const uint32_t cidx = w.s_cidx[own], ref = w.s_info[own] & 31u, sclk = w.s_clock[own];
@@ -415,7 +412,7 @@ __global__ __launch_bounds__(256) void k_seg_props(Work w, uint32_t nsegs) {
       }
     }
   } else if (!gc) {
-    link = seg_of(w.u_cutbits, w.u_wpre, origin != NONE ? origin : rorigin);
+    link = seg_of_unit(w, origin != NONE ? origin : rorigin);
   }
   if (gc) sf |= SEG_GC | SEG_DEL;
   else sf |= SEG_ITEM;
@@ -428,10 +425,11 @@ __global__ __launch_bounds__(256) void k_seg_props(Work w, uint32_t nsegs) {
   // in L2 where the one-atomic-per-segment form (98 M memory-side atomics on the C2 batch, 4.9 ms)
   // was bound by the chip's atomic rate. Every item stores: its kind (YMap entry / YArray member)
   // is only known after k_resolve, and a YArray origin's slot is never read. A lower-client child
-  // marks its origin unit (no merge with the origin's own-client successor; read for entries only).
+  // marks its origin unit (UF_LOWCHILD: no merge with the origin's own-client successor; read for
+  // entries only).
   if (!gc && origin != NONE) {
     w.g_maxchild[link] = s + 1;
-    if (olow) w.u_minchild[origin] = 0u;
+    if (olow) set_flag_byte(w.u_flags, origin, 3);  // (UF_LOWCHILD)
   } else if (key != NONE) {
     w.k_rootmax[key] = s + 1;
   }
@@ -535,8 +533,8 @@ __global__ __launch_bounds__(256) void k_resolve(Work w, uint32_t nsegs) {
 // rather than merged into a state Yjs would not reach.
 __device__ __forceinline__ bool origin_below(const Work& w, uint32_t o, uint32_t target, uint32_t nsegs) {
   for (uint32_t it = 0; it <= nsegs && o != NONE; ++it) {  // o: a unit; climb segment by segment
-    const uint32_t so = seg_of(w.u_cutbits, w.u_wpre, o);
-    if (target >= w.g_start[so] && target <= o) return true;  // (the units before o in its segment are its ancestors)
+    const uint32_t so = seg_of_unit(w, o);
+    if (target >= seg_start(w, so) && target <= o) return true;  // (the units before o in its segment are its ancestors)
     o = w.g_origin[so];
   }
   return false;
@@ -547,7 +545,7 @@ __global__ void k_mapx_flip(Work w, uint32_t nsegs) {
   const uint32_t f = w.g_flags[s];
   if (!(f & SEG_PSUB) || !(w.k_flags[w.g_key[s]] & KF_YATA)) return;
   const uint32_t r = w.g_rorigin[s];
-  if (r != NONE && !(w.g_flags[seg_of(w.u_cutbits, w.u_wpre, r)] & SEG_EXPLICIT) && !origin_below(w, w.g_origin[s], r - 1, nsegs))
+  if (r != NONE && !(w.g_flags[seg_of_unit(w, r)] & SEG_EXPLICIT) && !origin_below(w, w.g_origin[s], r - 1, nsegs))
     raise_err(&w.ctr->err, ERR_UNSUPPORTED);
   w.g_flags[s] = (f & ~(SEG_PSUB | SEG_WIN)) | SEG_ARRAY | SEG_YMAPX;
 }
@@ -628,7 +626,7 @@ __global__ void k_dead_init(Work w) {
   if (k >= w.cap_keys || w.k_hash[k] == 0) return;
   const uint32_t pu = w.k_parent[k];
   if (pu == NONE) return;
-  const uint32_t p = seg_of(w.u_cutbits, w.u_wpre, pu);
+  const uint32_t p = seg_of_unit(w, pu);
   const uint32_t pf = w.g_flags[p];
   const bool is_type = (w.s_info[w.g_src[p]] & 31u) == REF_TYPE;
   if ((pf & SEG_DEL) || !(pf & SEG_ITEM) || !is_type) w.k_flags[k] |= KF_DEAD;
@@ -642,7 +640,7 @@ __global__ void k_dead_climb(Work w) {
   for (uint32_t depth = 0; depth <= w.cap_keys; ++depth) {  // deeper than the key count: a cycle
     const uint32_t pu = w.k_parent[x];
     if (pu == NONE) return;  // a root type: alive
-    const uint32_t pk = w.g_key[seg_of(w.u_cutbits, w.u_wpre, pu)];
+    const uint32_t pk = w.g_key[seg_of_unit(w, pu)];
     if (pk == NONE) return;
     if (w.k_flags[pk] & KF_DEAD) { atomicOr(&w.k_flags[k], KF_DEAD); return; }
     x = pk;
@@ -677,20 +675,21 @@ __device__ __forceinline__ bool content_mergeable(uint32_t ref) {  // ContentX.m
 __device__ __forceinline__ uint32_t overwritten(uint32_t f, uint32_t fold) {
   return (fold && (f & (SEG_PSUB | SEG_WIN)) == SEG_PSUB) ? f | SEG_DEL : f;
 }
-__global__ __launch_bounds__(256) void k_merge_flags(Work w, uint32_t nsegs, uint32_t fold) {
-  const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
-  if (s > nsegs) return;
-  if (s == nsegs) { w.g_tmp[s] = 0; w.r_size[s] = 0; return; }
+// One lane per segment: the merge flag (s merges into its left neighbour) and the delete-set run
+// starts. Either the flags go to g_tmp / r_size and launch_merge_tail / the encoder scan them, or
+// (merge_flags_at's caller k_merge_flags_scan, the unsharded merge) their exclusive counts are made
+// in the same pass.
+__device__ __forceinline__ void merge_flags_at(const Work& w, uint32_t s, uint32_t fold, bool& start, bool& rstart) {
   bool merge = false;
   const uint32_t f0 = w.g_flags[s], fr = overwritten(f0, fold);
   if (s > 0 && w.g_cidx[s - 1] == w.g_cidx[s]) {
     const uint32_t fl = overwritten(w.g_flags[s - 1], fold);
-    const uint32_t gs = w.g_start[s];
+    const uint32_t gs = seg_start(w, s);
     if ((fl & SEG_ITEM) == (fr & SEG_ITEM)) {
       if (!(fr & SEG_ITEM)) merge = true;  // GC + GC
       else if ((fl & SEG_DEL) == (fr & SEG_DEL) && w.g_origin[s] == gs - 1 && w.g_rorigin[s - 1] == w.g_rorigin[s] &&
                (fl & (SEG_ARRAY | SEG_PSUB)) == (fr & (SEG_ARRAY | SEG_PSUB)) &&
-               ((fr & (SEG_ARRAY | SEG_YMAPX)) ? w.g_right[s - 1] == s : w.u_minchild[gs - 1] != 0u)) {
+               ((fr & (SEG_ARRAY | SEG_YMAPX)) ? w.g_right[s - 1] == s : !(w.u_flags[gs - 1] & UF_LOWCHILD))) {
         if (fr & SEG_DEL) merge = true;  // both become ContentDeleted after GC
         else {
           const uint32_t rl = w.s_info[w.g_src[s - 1]] & 31u, rr = w.s_info[w.g_src[s]] & 31u;
@@ -701,12 +700,67 @@ __global__ __launch_bounds__(256) void k_merge_flags(Work w, uint32_t nsegs, uin
   }
   const uint32_t f1 = merge ? fr | SEG_MERGE : fr;
   if (f1 != f0) w.g_flags[s] = f1;
-  w.g_tmp[s] = merge ? 0u : 1u;
   // the encode's delete-set runs (createDeleteSetFromStructStore): s starts a run of deleted
   // segments of one client — flagged here, where both final flags are in registers
   const bool del = seg_deleted(fr);
   const bool pdel = s > 0 && w.g_cidx[s - 1] == w.g_cidx[s] && seg_deleted(overwritten(w.g_flags[s - 1], fold));
-  w.r_size[s] = del && !pdel ? 1u : 0u;
+  start = !merge;
+  rstart = del && !pdel;
+}
+__global__ __launch_bounds__(256) void k_merge_flags(Work w, uint32_t nsegs, uint32_t fold) {
+  const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
+  if (s > nsegs) return;
+  if (s == nsegs) { w.g_tmp[s] = 0; w.r_size[s] = 0; return; }
+  bool start, rstart;
+  merge_flags_at(w, s, fold, start, rstart);
+  w.g_tmp[s] = start ? 1u : 0u;
+  w.r_size[s] = rstart ? 1u : 0u;
+}
+// The same flags, and their exclusive counts — output struct ids (g_outid) and delete-set run ids
+// (g_tmp2), entries [0, NS] (the last: the totals) — by a decoupled look-back per tile of MF_ITEMS
+// x 256 segments (two chains), instead of two scan passes over flag columns. Segment
+// tile * MF_TILE + k * 256 + t is lane t's k-th: coalesced, and the counts come from ballots.
+constexpr uint32_t MF_ITEMS = 16, MF_TILE = 256 * MF_ITEMS;
+__global__ __launch_bounds__(256) void k_merge_flags_scan(Work w, uint32_t nsegs, uint32_t fold, LbChains lb) {
+  __shared__ uint32_t ca[MF_ITEMS][4], cb[MF_ITEMS][4];
+  __shared__ uint32_t pa, pb;
+  const uint32_t tile = ordered_block_id(lb.ord, lb.ord_base);
+  const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const uint64_t lt = (1ull << lane) - 1ull;
+  uint32_t bits_a = 0, bits_b = 0;
+#pragma unroll 4
+  for (uint32_t k = 0; k < MF_ITEMS; ++k) {
+    const uint32_t s = tile * MF_TILE + k * 256 + threadIdx.x;
+    bool start = false, rstart = false;
+    if (s < nsegs) merge_flags_at(w, s, fold, start, rstart);
+    bits_a |= (start ? 1u : 0u) << k;
+    bits_b |= (rstart ? 1u : 0u) << k;
+    const uint64_t ba = __ballot(start), bb = __ballot(rstart);
+    if (lane == 0) { ca[k][wv] = (uint32_t)__popcll(ba); cb[k][wv] = (uint32_t)__popcll(bb); }
+  }
+  __syncthreads();
+  if (wv < 2) {
+    uint32_t tot = 0;
+    for (uint32_t i = lane; i < MF_ITEMS * 4; i += 64) tot += wv == 0 ? (&ca[0][0])[i] : (&cb[0][0])[i];
+    for (uint32_t off = 32; off > 0; off >>= 1) tot += __shfl_xor(tot, off);
+    const uint32_t p = (uint32_t)lb_wave_lookback(lb.state + (wv ? lb.stride : 0), tile, lb.epoch, tot);
+    if (lane == 0) { if (wv == 0) pa = p; else pb = p; }
+  }
+  __syncthreads();
+  uint32_t ra = pa, rb = pb;  // counts before lane t's k-th segment
+  for (uint32_t k = 0; k < MF_ITEMS; ++k) {
+    const uint64_t ba = __ballot((bits_a >> k) & 1u), bb = __ballot((bits_b >> k) & 1u);
+    uint32_t oa = (uint32_t)__popcll(ba & lt), ob = (uint32_t)__popcll(bb & lt);
+    for (uint32_t x = 0; x < 4; ++x) {
+      if (x < wv) { oa += ca[k][x]; ob += cb[k][x]; }
+    }
+    const uint32_t s = tile * MF_TILE + k * 256 + threadIdx.x;
+    if (s <= nsegs) {
+      w.g_outid[s] = ra + oa;
+      w.g_tmp2[s] = rb + ob;
+    }
+    for (uint32_t x = 0; x < 4; ++x) { ra += ca[k][x]; rb += cb[k][x]; }
+  }
 }
 // ---- key-hash sharding of one document (C4). Every list — a YMap entry, a
 // YArray — and every mergeWith adjacency lives inside ONE top-level entry of a root type (nested
@@ -731,7 +785,7 @@ __global__ void k_key_shard(Work w, uint32_t nshards, uint32_t* __restrict__ key
   for (uint32_t depth = 0; depth <= w.cap_keys; ++depth) {  // deeper than the key count: a cycle
     const uint32_t pu = w.k_parent[x];
     if (pu == NONE) { top = true; break; }
-    const uint32_t pk = w.g_key[seg_of(w.u_cutbits, w.u_wpre, pu)];
+    const uint32_t pk = w.g_key[seg_of_unit(w, pu)];
     if (pk == NONE || pk == x) { top = true; break; }
     x = pk;
   }
@@ -797,10 +851,18 @@ void launch_merge_tail(const Work& w, uint32_t nsegs, hipStream_t s) {
   scan_u32(w.tmp, w.tmp_bytes, w.g_tmp, w.g_outid, nsegs + 1, s);
 }
 
-void launch_merge_flags(const Work& w, uint32_t nsegs, hipStream_t s, bool fold) {
-  if (!nsegs) return;
+// true: the run ids are scanned too (g_tmp2; the encoder skips that scan)
+bool launch_merge_flags(const Work& w, uint32_t nsegs, hipStream_t s, bool fold) {
+  if (!nsegs) return false;
+  const uint32_t tiles = (nsegs + 1 + MF_TILE - 1) / MF_TILE;
+  LbChains lb;
+  if (!encode_runs_small(nsegs) && lb_launch(tiles, 2, s, lb)) {
+    hipLaunchKernelGGL(k_merge_flags_scan, dim3(tiles), dim3(256), 0, s, w, nsegs, fold ? 1u : 0u, lb);
+    return true;
+  }
   hipLaunchKernelGGL(k_merge_flags, dim3(nsegs / 256 + 1), dim3(256), 0, s, w, nsegs, fold ? 1u : 0u);
   scan_u32(w.tmp, w.tmp_bytes, w.g_tmp, w.g_outid, nsegs + 1, s);
+  return false;
 }
 
 }  // namespace yc

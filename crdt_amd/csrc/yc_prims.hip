@@ -110,7 +110,6 @@ __global__ __launch_bounds__(SMALL_SCAN_LANES) void k_scan_small(const uint32_t*
 // are disjoint, so in == out is safe. Values travel mod 2^40: exact for u32 scans (mod 2^32) and
 // for u64 scans whose total is below 2^40 (byte and unit positions of a merge: bounded by HBM).
 constexpr uint32_t LB_LANES = 256, LB_ITEMS = 16, LB_TILE = LB_LANES * LB_ITEMS;
-constexpr uint64_t LB_VAL = (1ull << 40) - 1;
 constexpr uint32_t LB_EPOCHS = 1u << 22;
 template <class T>
 __global__ __launch_bounds__(LB_LANES) void k_scan_lb(const uint32_t* in, T* out, uint64_t n,
@@ -125,7 +124,6 @@ __global__ __launch_bounds__(LB_LANES) void k_scan_lb(const uint32_t* in, T* out
   const uint32_t tile = ordered_block_id(ord, ord_base);
   const uint32_t t = threadIdx.x, lane = t & 63, wv = t >> 6;
   const uint64_t base = (uint64_t)tile * LB_TILE + (uint64_t)t * LB_ITEMS;
-  const unsigned long long ep = (unsigned long long)epoch << 42;
   uint32_t v[LB_ITEMS];
   if (vec && base + LB_ITEMS <= n) {
 #pragma unroll
@@ -156,37 +154,7 @@ __global__ __launch_bounds__(LB_LANES) void k_scan_lb(const uint32_t* in, T* out
   }
   T run = wpre + inc - sum;
   if (wv == 0) {
-    uint64_t pre = 0;
-    if (tile == 0) {
-      if (lane == 0)
-        __hip_atomic_store(&state[0], ep | (2ull << 40) | ((uint64_t)agg & LB_VAL), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    } else {
-      if (lane == 0)
-        __hip_atomic_store(&state[tile], ep | (1ull << 40) | ((uint64_t)agg & LB_VAL), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      int64_t j = (int64_t)tile - 1;
-      for (;;) {
-        const int64_t me = j - (int64_t)lane;
-        uint32_t st = 2;
-        uint64_t val = 0;
-        if (me >= 0) {
-          unsigned long long x;
-          while (((x = __hip_atomic_load(&state[me], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) >> 42) != epoch)
-            __builtin_amdgcn_s_sleep(1);
-          st = (uint32_t)(x >> 40) & 3u;
-          val = x & LB_VAL;
-        }
-        const uint64_t done = __ballot(st == 2);  // lanes past tile 0 count as done with 0
-        const uint32_t stop = (uint32_t)__ffsll((long long)done) - 1;  // nearest inclusive prefix
-        uint64_t part = lane <= stop ? val : 0ull;
-        for (uint32_t off = 32; off > 0; off >>= 1) part += __shfl_xor(part, off);
-        pre += part;
-        if (done) break;
-        j -= 64;
-      }
-      if (lane == 0)
-        __hip_atomic_store(&state[tile], ep | (2ull << 40) | ((pre + (uint64_t)agg) & LB_VAL), __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
-    }
+    const uint64_t pre = lb_wave_lookback(state, tile, epoch, (uint64_t)agg);
     if (lane == 0) tile_pre = (T)pre;
   }
   __syncthreads();
@@ -248,6 +216,19 @@ static bool scan_lb(const uint32_t* in, T* out, uint64_t n, hipStream_t s) {
   const uint32_t vec = (((uintptr_t)in | (uintptr_t)out) & 15u) == 0;
   hipLaunchKernelGGL(k_scan_lb<T>, dim3((uint32_t)tiles), dim3(LB_LANES), 0, s, in, out, n, st->state, st->epoch, vec,
                      st->state + st->tiles, st->issued);
+  st->issued += tiles;
+  return true;
+}
+
+bool lb_launch(uint64_t tiles, uint32_t chains, hipStream_t s, LbChains& out) {
+  std::lock_guard<std::mutex> g(lb_mu);
+  LbState* st = lb_state(tiles * chains, s);
+  if (!st) return false;
+  out.state = st->state;
+  out.stride = tiles;
+  out.epoch = st->epoch;
+  out.ord = st->state + st->tiles;
+  out.ord_base = st->issued;
   st->issued += tiles;
   return true;
 }

@@ -24,7 +24,7 @@ __device__ __forceinline__ bool countable_ref(uint32_t ref) { return ref != REF_
 
 // ViewSeg of segment s: every element, or only the last one (a YMap entry's value)
 __device__ void fill_seg(const Work& w, uint32_t s, bool last_only, ViewSeg& v) {
-  const uint32_t g0 = w.g_start[s], g1 = w.g_start[s + 1];
+  const uint32_t g0 = seg_start(w, s), g1 = seg_start(w, s + 1);
   const uint32_t cidx = w.g_cidx[s], own = w.g_src[s];
   const uint32_t clock = (uint32_t)(g0 - w.cl_base[cidx]);
   const uint32_t f = w.g_flags[s];

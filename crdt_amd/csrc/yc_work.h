@@ -187,7 +187,6 @@ struct Work {
   // ---- per unit (U)
   uint32_t* u_owner = nullptr;
   uint32_t* u_flags = nullptr;
-  uint32_t* u_minchild = nullptr;  // 0 = some YMap child of this unit has a lower client than the unit (merge blocked)
   uint64_t* u_cutbits = nullptr;   // [U/64+1]
   uint32_t* u_wpre = nullptr;      // [U/64+2] popcount prefix of u_cutbits words
   // ---- per segment (NS <= U)
@@ -355,6 +354,55 @@ __device__ __forceinline__ uint32_t ordered_block_id(unsigned long long* ctr, un
   return id;
 }
 
+// Decoupled look-back (yc_prims.hip k_scan_lb; also inside producer kernels, whose scan then needs
+// no pass of its own). A tile's state on a chain is ONE 64-bit word — epoch (22 bits) | status (2:
+// aggregate / inclusive prefix) | value (40 bits) — stored and loaded as a relaxed agent-scope
+// atomic (coherent across the XCDs' L2s without the invalidations an acquire costs on gfx950).
+// Every launch takes a new epoch, so states left by earlier launches read as "not yet".
+constexpr uint64_t LB_VAL = (1ull << 40) - 1;
+struct LbChains {                       // one launch's look-back chains (lb_launch, yc_prims.hip)
+  unsigned long long* state = nullptr;  // chain c's tile states at state + c * stride
+  uint64_t stride = 0;
+  uint32_t epoch = 0;
+  unsigned long long* ord = nullptr;    // ordered tile ids (ordered_block_id)
+  unsigned long long ord_base = 0;
+};
+bool lb_launch(uint64_t tiles, uint32_t chains, hipStream_t s, LbChains& out);
+// One full wavefront: publishes `tile`'s aggregate, looks back 64 tiles per round (each lane
+// spinning on its own predecessor) to the nearest inclusive prefix, publishes its own inclusive
+// prefix, and returns the tile-exclusive prefix (mod 2^40) in every lane. Tiles wait only on
+// lower ordered ids, which are running.
+__device__ __forceinline__ uint64_t lb_wave_lookback(unsigned long long* __restrict__ state, uint32_t tile, uint32_t epoch, uint64_t agg) {
+  const uint32_t lane = threadIdx.x & 63;
+  const unsigned long long ep = (unsigned long long)epoch << 42;
+  if (tile == 0) {
+    if (lane == 0) __hip_atomic_store(&state[0], ep | (2ull << 40) | (agg & LB_VAL), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return 0;
+  }
+  if (lane == 0) __hip_atomic_store(&state[tile], ep | (1ull << 40) | (agg & LB_VAL), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  uint64_t pre = 0;
+  for (int64_t j = (int64_t)tile - 1;; j -= 64) {
+    const int64_t me = j - (int64_t)lane;
+    uint32_t st = 2;
+    uint64_t val = 0;
+    if (me >= 0) {
+      unsigned long long x;
+      while (((x = __hip_atomic_load(&state[me], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) >> 42) != epoch)
+        __builtin_amdgcn_s_sleep(1);
+      st = (uint32_t)(x >> 40) & 3u;
+      val = x & LB_VAL;
+    }
+    const uint64_t done = __ballot(st == 2);  // lanes past tile 0 count as done with 0
+    const uint32_t stop = (uint32_t)__ffsll((long long)done) - 1;  // nearest inclusive prefix
+    uint64_t part = lane <= stop ? val : 0ull;
+    for (uint32_t off = 32; off > 0; off >>= 1) part += __shfl_xor(part, off);
+    pre += part;
+    if (done) break;
+  }
+  if (lane == 0) __hip_atomic_store(&state[tile], ep | (2ull << 40) | ((pre + agg) & LB_VAL), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return pre;
+}
+
 __device__ __forceinline__ uint64_t client_hash(uint64_t k) {  // splitmix64 finaliser
   k ^= k >> 30; k *= 0xBF58476D1CE4E5B9ull;
   k ^= k >> 27; k *= 0x94D049BB133111EBull;
@@ -381,6 +429,11 @@ __device__ __forceinline__ uint32_t find_client(const Work& w, uint32_t nclients
   return (lo < nclients && w.cl_key[lo] == key) ? lo : NONE;
 }
 __device__ __forceinline__ uint32_t doc_of_update(const Work& w, uint32_t upd) { return w.udoc ? w.udoc[upd] : 0u; }
+// first unit of segment s (s = NS: the sentinel U) and the segment of unit g
+__device__ __forceinline__ uint32_t seg_start(const Work& w, uint32_t s) { return w.g_start[s]; }
+__device__ __forceinline__ uint32_t seg_of_unit(const Work& w, uint32_t g) {
+  return w.u_wpre[g >> 6] + (uint32_t)__popcll(w.u_cutbits[g >> 6] & ((2ull << (g & 63)) - 1)) - 1;
+}
 // ---- windows (see WIN_SHIFT): the byte and bitmap bases of window k
 __device__ __forceinline__ uint32_t upd_win(const Work& w, uint32_t upd) { return w.uwin ? w.uwin[upd] : 0u; }
 __device__ __forceinline__ const uint8_t* win_bytes(const Work& w, uint32_t win) { return w.bytes + ((uint64_t)win << w.win_shift); }
@@ -587,6 +640,8 @@ enum : uint32_t {
   UF_GC = 2u,          // a GC struct covers the unit
   UF_DS = 0x100u,      // a delete-set range covers the unit (byte 1: set by a plain byte store)
   UF_CUT = 0x10000u,   // a struct boundary is required before this unit (byte 2: plain byte store)
+  UF_LOWCHILD = 0x1000000u,  // some YMap child of this unit has a lower client than the unit: no merge
+                             // with its own-client successor (byte 3: plain byte store, k_seg_props)
 };
 
 // ---- materialised view (yc_view.hip), copied to the host as is
@@ -629,7 +684,8 @@ uint32_t run_key_resolution(const Work& w, uint32_t nsegs, hipStream_t s);
 uint32_t run_descent(const Work& w, uint32_t nsegs, hipStream_t s, bool fold_overwrite);
 void launch_mapx_flip(const Work& w, uint32_t nsegs, hipStream_t s);  // full-YATA map entries -> the YATA kernels
 void launch_mapx_fix(const Work& w, uint32_t nsegs, hipStream_t s);   // ... and back: the last one wins
-void launch_merge_flags(const Work& w, uint32_t nsegs, hipStream_t s, bool fold_overwrite);
+bool launch_merge_flags(const Work& w, uint32_t nsegs, hipStream_t s, bool fold_overwrite);  // true: run ids scanned too
+bool encode_runs_small(uint32_t nsegs);  // the one-workgroup delete-set runs (k_runs_small)
 void launch_merge_flags_only(const Work& w, uint32_t nsegs, hipStream_t s, bool fold_overwrite);
 void launch_merge_tail(const Work& w, uint32_t nsegs, hipStream_t s);
 // key-hash shards of one document (yc_merge.hip)
@@ -646,7 +702,7 @@ uint32_t launch_ylists(const Work& w, uint32_t nsegs, hipStream_t s);
 
 // side / ev_fork / ev_join / tmp2: the delete-set run chain runs on `side` with its own scan space
 void launch_encode_sizes(const Work& w, uint32_t nsegs, uint32_t nclients, hipStream_t s, hipStream_t side,
-                         hipEvent_t ev_fork, hipEvent_t ev_join, void* tmp2, size_t tmp2_bytes);
+                         hipEvent_t ev_fork, hipEvent_t ev_join, void* tmp2, size_t tmp2_bytes, bool runs_scanned);
 void launch_out_sizes(const Work& w, uint32_t nsegs, uint32_t nclients, hipStream_t s);
 void launch_encode_layout(const Work& w, uint32_t nsegs, uint32_t nclients, hipStream_t s, hipEvent_t ev_join);
 void launch_encode_write(const Work& w, uint32_t nsegs, uint32_t nclients, hipStream_t s);

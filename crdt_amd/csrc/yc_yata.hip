@@ -21,9 +21,6 @@
 
 namespace yc {
 
-__device__ __forceinline__ uint32_t seg_of_unit(const Work& w, uint32_t g) {
-  return w.u_wpre[g >> 6] + (uint32_t)__popcll(w.u_cutbits[g >> 6] & ((2ull << (g & 63)) - 1)) - 1;
-}
 
 // YATA's per-segment state: the sort values, the final right neighbours, the sequential kernels' stamps
 __global__ void k_yinit(Work w, uint32_t nsegs) {

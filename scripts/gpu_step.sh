@@ -1,8 +1,11 @@
 #!/bin/bash
-# the per-call GPU step (edited per experiment): every -m gpu test, then the C2 PMC / stats passes
+# the per-call GPU step (edited per experiment)
 set -u
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 timeout -k 10 900 python -u -m pytest tests -x -q --timeout 300 --timeout-method thread -m gpu > gpurun_out/step_tests.log 2>&1 || { grep -E "^E |FAIL|Error" gpurun_out/step_tests.log | head -30; tail -5 gpurun_out/step_tests.log; exit 1; }
 tail -1 gpurun_out/step_tests.log
-bash scripts/pmc.sh r05a && python3 scripts/pmc_summary.py gpurun_out/pmc_r05a gpurun_out/pmc_r05a/c2_pmc.csv > gpurun_out/pmc_r05a/summary.txt 2>&1; tail -30 gpurun_out/pmc_r05a/summary.txt; python3 scripts/prof_summary.py gpurun_out/pmc_r05a/stats 2>/dev/null | head -5 || true
+timeout -k 10 300 python bench.py --only-headline --profile-phases --steps 10 --warmup 3 > gpurun_out/s_h.json 2> gpurun_out/s_h.err || { tail -20 gpurun_out/s_h.err; exit 1; }
+python3 scripts/bench_summary.py gpurun_out/s_h.json || true
+rm -rf gpurun_out/pmc_r05b
+bash scripts/pmc.sh r05b && python3 scripts/pmc_summary.py gpurun_out/pmc_r05b gpurun_out/pmc_r05b/c2_pmc.csv > gpurun_out/pmc_r05b/summary.txt 2>&1; tail -12 gpurun_out/pmc_r05b/summary.txt
