@@ -457,20 +457,15 @@ __device__ __attribute__((noinline)) uint32_t exact_len(const uint8_t* __restric
   uint32_t q = p;
   return parse_struct<false>(b, q, end, 0xFFFFFFFFu, nullptr) > 0 ? q - p : 0u;
 }
+// (one update's exact walk through the lane's LDS window `slot`; k_direct_split's fallback too)
 template <uint32_t DWT>
-__global__ __launch_bounds__(DL) void k_direct(Work w) {
-  constexpr uint32_t DSTR = DWT / 4 + 4;
-  __shared__ __attribute__((aligned(16))) uint32_t win[DL * DSTR];
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= w.nsmall) return;
-  const uint32_t u = w.ulist[w.nbig + i];
+__device__ __forceinline__ void direct_walk(const Work& w, uint32_t u, uint32_t* slot) {
   const uint32_t uw = upd_win(w, u);  // positions below are relative to the update's window
   const uint8_t* __restrict__ b = win_bytes(w, uw);
   uint64_t* __restrict__ fbits = win_words(w.final_bits, uw);
   uint64_t* __restrict__ sbits = win_words(w.sec_bits, uw);
   const uint32_t ustart = w.uoff[u], uend = ustart + w.ulen[u];
   uint32_t* err = &w.ctr->err;
-  uint32_t* slot = win + threadIdx.x * DSTR;
   LdsSrc src{b, slot, 0, 0};
   auto refill = [&](uint32_t p) {
     src.s0 = p & ~15u;
@@ -535,6 +530,13 @@ __global__ __launch_bounds__(DL) void k_direct(Work w) {
   }
   if (word != NONE) fbits[word] = m;
   w.dsstart[u] = p;
+}
+template <uint32_t DWT>
+__global__ __launch_bounds__(DL) void k_direct(Work w) {
+  constexpr uint32_t DSTR = DWT / 4 + 4;
+  __shared__ __attribute__((aligned(16))) uint32_t win[DL * DSTR];
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < w.nsmall) direct_walk<DWT>(w, w.ulist[w.nbig + i], win + threadIdx.x * DSTR);
 }
 
 
@@ -930,8 +932,11 @@ __global__ __launch_bounds__(64) void k_walk(Work w) {
   __shared__ uint32_t ent[65], cnt[64], nknown;
   if (blockIdx.x >= w.nbig) return;
   const uint32_t u = w.ulist[blockIdx.x];
-  if (w.ufail[u] >= 2u) return;  // k_fastwalk / k_fastwalk_multi did it
-  if (TABLES && !w.ufail[u]) return;
+  if (w.ufail[u] == 2u || w.ufail[u] == 3u) return;  // k_fastwalk / k_fastwalk_multi did it
+  if (TABLES && w.ufail[u] != 1u && w.ufail[u] != 5u) return;
+  // k_fastwalk_multi vouched for the first sections (ufail 4; 5 once handed to the tables): the
+  // walk resumes at the next one
+  const bool resume = TABLES ? w.ufail[u] == 5u : w.ufail[u] == 4u;
   const uint32_t lane = threadIdx.x;
   const uint32_t uw = upd_win(w, u);  // positions below are relative to the update's window
   const uint8_t* __restrict__ b = win_bytes(w, uw);
@@ -960,20 +965,23 @@ __global__ __launch_bounds__(64) void k_walk(Work w) {
   const uint32_t nsec = rd_vu(b, p, uend, ok);
   if (!ok || nsec > (uend - p) / 3 + 1) { if (L0) raise_err(err, ERR_DECODE); return; }
   uint32_t sbase = 0;
-  if (TABLES) sbase = w.usec_start[u];  // the speculative walk gave up on this update: same sections
+  if (TABLES || resume) sbase = w.usec_start[u];  // (the sections were allocated by the first walk)
   else if (L0) sbase = atomicAdd(&w.ctr->nsections, nsec);
   sbase = __shfl(sbase, 0);
   if (sbase + nsec > w.cap_sections) { if (L0) raise_err(err, ERR_CAPACITY); return; }
-  if (L0 && !TABLES) { w.usec_start[u] = sbase; w.usec_n[u] = nsec; }
-  auto hand_over = [&]() {  // to the exit tables: flag the update, list its chunks
+  if (L0 && !TABLES && !resume) { w.usec_start[u] = sbase; w.usec_n[u] = nsec; }
+  uint32_t sfirst = 0;
+  if (resume) { sfirst = w.fw[2 * u]; p = w.fw[2 * u + 1]; }
+  auto hand_over = [&]() {  // to the exit tables: flag the update, list its chunks (from the resume point's)
+    const uint32_t j0 = resume ? (w.fw[2 * u + 1] - ustart) / CH : 0u;
     uint32_t base = 0;
-    if (L0) { w.ufail[u] = 1u; base = atomicAdd(&w.ctr->xchunks, nch); }
+    if (L0) { w.ufail[u] = resume ? 5u : 1u; base = atomicAdd(&w.ctr->xchunks, nch - j0); }
     base = __shfl(base, 0);
-    for (uint32_t k = lane; k < nch; k += 64) w.xlist[base + k] = c0 + k;
+    for (uint32_t k = j0 + lane; k < nch; k += 64) w.xlist[base + k - j0] = c0 + k;
   };
   if (!TABLES && w.force_xtab) { hand_over(); return; }
   uint32_t steps = 0, fails = 0;
-  for (uint32_t sct = 0; sct < nsec; ++sct) {
+  for (uint32_t sct = sfirst; sct < nsec; ++sct) {
     const uint32_t n = rd_vu(b, p, uend, ok);
     const uint32_t client = rd_vu(b, p, uend, ok);
     const uint32_t clock = rd_vu(b, p, uend, ok);
@@ -1251,21 +1259,52 @@ __global__ __launch_bounds__(64) void k_fastwalk(Work w) {
 // chains form one chain through the whole update (section headers included, parsed as garbage),
 // so for each section in turn: the exact walk from its first struct until it meets the chain
 // (inside that struct's chunk), then the section's last struct is the (n - walked)-th chain
-// position from the meeting point (chunk counts, 64 chunks per round), and the next header starts
-// where that struct ends. Pass 1 checks every section without writing anything (any doubt: the
-// update is left to k_walk, as before); pass 2 writes the section records, the walked positions
-// and each section's chain range, which k_fastmark copies grid-wide (the header gaps between the
-// ranges stay clear). C4's base snapshot (65 sections, 11 MB) took k_walk 2.3 ms; C3's merged
-// output (256 sections, 156 MB) 35 ms.
-constexpr uint32_t FWM_MAX = 1024;  // sections checked in LDS
-constexpr uint32_t FWM_WALK = 256;  // exact steps from a section's first struct to the chain, at most
+// position from the meeting point, and the next header starts where that struct ends. Pass 1
+// checks the sections in order without writing anything; pass 2 writes the records of the sections
+// it vouched for, their walked positions and chain ranges (k_fastmark copies the ranges grid-wide;
+// the header gaps stay clear). A section it cannot vouch for (a chain that never meets, an off
+// chunk, more than FWM_MAX sections) ends pass 1: the sections before it are committed and k_walk
+// resumes at its header (ufail 4) — one phase-locked section no longer sends a snapshot of a
+// thousand clients (a C2 document's state, crdt.js's wire shape) back through the serial walk.
+// The sections are a serial chain (a header's position is the end of the section before it), so
+// each step is cut to a few rounds of wavefront-wide loads: the bytes from the section's header
+// (and the previous section's last struct) and their struct-start words staged in LDS, the exact
+// walk from LDS, the meeting chunk's words and the next 64 chunks' count / off prefixes in one
+// round, the last struct's chunk words in one more (64-way searches past 64 chunks).
+// (C4's base snapshot: 65 sections, 11 MB; C3's merged output: 256 sections, 156 MB.)
+constexpr uint32_t FWM_MAX = 1024;    // sections checked per update (LDS records); k_walk resumes past them
+constexpr uint32_t FWM_WALK = 256;    // exact steps from a section's first struct to the chain, at most
+constexpr uint32_t FWM_STAGE = 512;   // bytes staged per step
+template <class S>
+__device__ __forceinline__ uint32_t rd_vu_src(const S& b, uint32_t& p, uint32_t end, bool& ok) {  // rd_vu over a source
+  uint32_t v = 0, shift = 0;
+#pragma unroll 1
+  for (;;) {
+    if (p >= end) { ok = false; return 0; }
+    const uint32_t r = b.u8(p++);
+    if (shift < 32) v |= (r & 0x7fu) << shift;
+    shift += 7;
+    if (r < 0x80u) return v;
+    if (shift > 35) { ok = false; return 0; }
+  }
+}
+__device__ __forceinline__ uint32_t wave_sum_u32(uint32_t v) {
+  for (uint32_t off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+  return v;
+}
+__device__ __forceinline__ uint32_t nth_set1(uint64_t x, uint32_t k) {  // position of the k-th (>= 1) set bit
+  for (uint32_t i = 1; i < k; ++i) x &= x - 1;
+  return (uint32_t)__ffsll((long long)x) - 1;
+}
 __global__ __launch_bounds__(64) void k_fastwalk_multi(Work w) {
-  __shared__ uint32_t sp1[FWM_MAX], sn[FWM_MAX], scl[FWM_MAX], sck[FWM_MAX], sq[FWM_MAX], se[FWM_MAX], sk0[FWM_MAX];
+  __shared__ uint32_t sp1[FWM_MAX], sn[FWM_MAX], scl[FWM_MAX], sck[FWM_MAX], sq[FWM_MAX], se[FWM_MAX], sk0[FWM_MAX], shp[FWM_MAX];
+  __shared__ __attribute__((aligned(16))) uint32_t stg[FWM_STAGE / 4 + 4];
+  __shared__ uint64_t sspec[FWM_STAGE / 64 + 2];
   __shared__ uint32_t sh_sbase;
   if (blockIdx.x >= w.nbig) return;
   const uint32_t u = w.ulist[blockIdx.x];
   const uint32_t lane = threadIdx.x;
-  // (YCRDT_DEBUG_DECODE: updates left to k_walk, and why — bit r of the mask: reason r)
+  // (YCRDT_DEBUG_DECODE: updates (partly) left to k_walk, and why — dbg[8 + r]: reason r)
   auto why = [&](uint32_t r) { if (w.dbg && lane == 0) { atomicAdd(&w.dbg[1], 1ull); atomicAdd(&w.dbg[8 + r], 1ull); } };
   if (w.ufail[u] || !w.fwsec) return;
   const uint32_t uw = upd_win(w, u);
@@ -1274,74 +1313,179 @@ __global__ __launch_bounds__(64) void k_fastwalk_multi(Work w) {
   uint64_t* __restrict__ fbits = win_words(w.final_bits, uw);
   uint64_t* __restrict__ sbits = win_words(w.sec_bits, uw);
   const uint32_t ustart = w.uoff[u], uend = ustart + w.ulen[u];
-  const uint32_t CH = w.schunk;
+  const uint32_t CH = w.schunk, SWC = CH / 64;
   const uint32_t c0 = w.ugroup[u], nch = (w.ulen[u] + CH - 1) / CH;
-  if (!w.ulen[u]) return;
+  if (!w.ulen[u] || SWC > 64) return;
   uint32_t p = ustart;
   bool ok = true;
   const uint32_t nsec = rd_vu(b, p, uend, ok);
   if (!ok || nsec < 2) return;
-  if (nsec > FWM_MAX) { why(1); return; }
-  auto spec_bit = [&](uint32_t q) { return (spec[q >> 6] >> (q & 63)) & 1ull; };
   // pass 1 (every value below is the same in every lane)
-  for (uint32_t s = 0; s < nsec; ++s) {
-    const uint32_t n = rd_vu(b, p, uend, ok), client = rd_vu(b, p, uend, ok), clock = rd_vu(b, p, uend, ok);
-    if (!ok || n > uend - p) { why(3); return; }
+  const uint32_t nchk = min(nsec, w.fwm_max ? min(w.fwm_max, FWM_MAX) : FWM_MAX);
+  uint32_t done = 0;          // sections vouched for
+  uint32_t hdr = p;           // section done's header (unless from_last: then past cur's struct)
+  uint32_t cur = p;           // the previous section's last struct when from_last
+  bool from_last = false;
+  bool broke = false;
+  for (uint32_t s = 0; s < nchk; ++s) {
+    // ONE round of loads: the bytes from the header (or the previous section's last struct) and
+    // their struct-start words staged in LDS; the struct-start words of the two chunks from the
+    // stage's start (held in lanes 0 .. 2 SWC - 1); the count and off prefixes of the 64 chunks from
+    // there (lane l: through the end of chunk jb + l)
+    const uint32_t s0 = (from_last ? cur : hdr) & ~15u;
+    const uint32_t wlen = min(FWM_STAGE, (uend + 15u - min(s0, uend)) & ~15u);  // (never past the update)
+    const uint32_t jb = (min(s0, uend - 1) - ustart) / CH;
+    const uint32_t wb = (ustart + jb * CH) >> 6, wlast = (uend - 1) >> 6;
+    __syncthreads();  // (the previous step's reads of the stage are done)
+    if (lane * 8 < wlen) ((uint2*)stg)[lane] = ((const uint2*)(b + s0))[lane];
+    if (lane < FWM_STAGE / 64 + 2) sspec[lane] = (s0 >> 6) + lane <= wlast ? spec[(s0 >> 6) + lane] : 0ull;
+    const uint64_t cw = lane < 2 * SWC && wb + lane <= wlast ? spec[wb + lane] : 0ull;
+    const bool pv = jb + lane < nch;
+    const uint64_t P = pv ? w.cpre[c0 + jb + lane + 1] : ~0ull;
+    const uint32_t O = pv ? w.opre[c0 + jb + lane + 1] : 0u;
+    __syncthreads();
+    const LdsSrc src{b, stg, s0, wlen};
+    auto spec_bit = [&](uint32_t q) {
+      const uint32_t k = (q >> 6) - (s0 >> 6);
+      return ((k < FWM_STAGE / 64 + 2 ? sspec[k] : spec[q >> 6]) >> (q & 63)) & 1ull;
+    };
+    // the chain positions in [a, e) of chunk j's words (lanes' registers when j is jb or jb + 1)
+    auto chunk_words = [&](uint32_t jc, uint32_t a, uint32_t e) -> uint64_t {
+      const uint32_t cs = ustart + jc * CH;
+      uint64_t x = 0;
+      if (jc == jb || (jc == jb + 1 && 2 * SWC <= 64)) {
+        const uint32_t k = lane - (jc - jb) * SWC;
+        if (k < SWC) {
+          const uint32_t wd = (cs >> 6) + k;
+          if (wd * 64 + 63 >= a && wd * 64 < e) {
+            x = cw;
+            if (wd == (a >> 6)) x &= ~0ull << (a & 63);
+            if (wd == ((e - 1) >> 6)) x &= ~0ull >> (63 - ((e - 1) & 63));
+          }
+        }
+      } else if (lane < SWC) {
+        const uint32_t wd = (cs >> 6) + lane;
+        if (wd * 64 + 63 >= a && wd * 64 < e) x = range_word(spec, wd, a, e);
+      }
+      return x;
+    };
+    if (from_last) {  // the header follows the previous section's last struct
+      const uint32_t dl = cur < uend ? chain_len(src, b, cur, uend) : 0u;
+      if (!dl || cur + dl > uend) {  // (the previous section's end is unknown: it is not vouched for)
+        why(7);
+        done = s - 1;
+        hdr = shp[s - 1];
+        broke = true;
+        break;
+      }
+      hdr = cur + dl;
+    }
+    if (lane == 0) shp[s] = hdr;
+    p = hdr;
+    const uint32_t n = rd_vu_src(src, p, uend, ok), client = rd_vu_src(src, p, uend, ok), clock = rd_vu_src(src, p, uend, ok);
+    if (!ok || n > uend - p) { why(3); broke = true; break; }
     const uint32_t p1 = p;
     uint32_t q = p1, k0 = 0, e = p1;
+    from_last = false;
     if (n) {
-      if (p1 >= uend) return;
-      // the exact walk (lane 0) until it meets the chain: a section header breaks the chain's
-      // phase, and a section starting near a chunk's end meets it only in a later chunk (the true
-      // sequence and the chain take the same steps from any common position on)
+      if (p1 >= uend) { why(3); broke = true; break; }
+      // the exact walk (lane 0, from the stage) until it meets the chain: a section header breaks
+      // the chain's phase, and a section starting near a chunk's end meets it only in a later chunk
       uint32_t walk_bad = 0;
       if (lane == 0) {
         for (uint32_t steps = 0; q < uend && k0 < n && !spec_bit(q); ++steps) {
-          if (steps == FWM_WALK) { q = uend; break; }  // no meeting: left to k_walk (why 5)
-          const uint32_t dq = chain_len(GlobalSrc{b}, b, q, uend);
+          if (steps == FWM_WALK) { q = uend; break; }
+          const uint32_t dq = chain_len(src, b, q, uend);
           if (!dq) { walk_bad = 1; break; }  // no struct parses: k_walk reports it
           q += dq;
           ++k0;
         }
       }
-      if (__shfl(walk_bad, 0)) { why(4); return; }
+      if (__shfl(walk_bad, 0)) { why(4); broke = true; break; }
       q = __shfl(q, 0);
       k0 = __shfl(k0, 0);
-      if (k0 == n) {  // every struct walked: the section ends where the walk stopped
+      if (k0 == n) {  // every struct walked: the next header is where the walk stopped
+        if (q > uend) { why(3); broke = true; break; }
         e = q;  // (an empty chain range [q, q))
-        if (q > uend) return;
         p = q;
-        sq[s] = q;
       } else {
         if (q >= uend) {  // no meeting within FWM_WALK structs
-          if (w.dbg && lane == 0) { w.dbg[14] = s; w.dbg[15] = n; w.dbg[13] = popc_range(spec, p1, min(p1 + 4096, uend)); w.dbg[12] = p1 - ustart; w.dbg[11] = uend - ustart; }
+          if (w.dbg && lane == 0) { w.dbg[14] = s; w.dbg[15] = n; w.dbg[12] = p1 - ustart; w.dbg[11] = uend - ustart; }
           why(5);
-          return;
+          broke = true;
+          break;
         }
+        // the target-th chain position from q (q the first) is the section's last struct
         const uint32_t target = n - k0;
-        const uint32_t jq = (q - ustart) / CH;
-        uint32_t fch = 0, rem = 0, wy = 0;
-        if (!chain_target(w, spec, ustart, uend, c0, nch, jq, q, target, lane, fch, rem, wy)) { why(wy ? 2 : 6); return; }
-        const uint32_t fa = fch == jq ? q : ustart + fch * CH;
-        const uint32_t Lp = select_from(spec, fa, rem);
-        const uint32_t dl = Lp < uend ? chain_len(GlobalSrc{b}, b, Lp, uend) : 0u;
-        const uint32_t dsp = Lp + dl;
-        if (!dl || dsp > uend) { why(7); return; }
+        const uint32_t jq = (q - ustart) / CH, ceq = min(ustart + jq * CH + CH, uend);
+        const uint32_t cq = wave_sum_u32((uint32_t)__popcll(chunk_words(jq, q, ceq)));
+        uint32_t fch = jq, rem = target, fa = q;
+        if (target > cq) {
+          const uint64_t need = target - cq;
+          bool found = false;
+          if (jq - jb < 2u) {  // the prefixes from the stage's chunk: chunks jq + 1 .. jb + 63
+            const uint32_t jr = jq - jb;
+            const uint64_t base = __shfl((unsigned long long)P, jr);
+            const uint32_t obase = __shfl(O, jr);
+            const uint64_t m = __ballot(lane > jr && pv && P - base >= need);
+            if (m) {
+              const uint32_t L = (uint32_t)__ffsll((long long)m) - 1;
+              if (__shfl((uint32_t)(O != obase), L)) { why(2); broke = true; break; }
+              const uint64_t before = L > jr + 1 ? (uint64_t)__shfl((unsigned long long)P, L - 1) - base : 0ull;
+              fch = jb + L;
+              rem = (uint32_t)(need - before);
+              found = true;
+            }
+          }
+          if (!found) {  // further on: the 64-way search over the prefixes
+            uint32_t wy = 0;
+            if (!chain_target(w, spec, ustart, uend, c0, nch, jq, q, target, lane, fch, rem, wy)) { why(wy ? 2 : 6); broke = true; break; }
+          }
+          fa = ustart + fch * CH;
+        }
+        // the rem-th chain position at or after fa in chunk fch
+        const uint32_t fcs = ustart + fch * CH, fce = min(fcs + CH, uend);
+        const uint64_t yw = chunk_words(fch, fa, fce);
+        const uint32_t yc = (uint32_t)__popcll(yw);
+        uint32_t incl = yc;
+        for (uint32_t off = 1; off < 64; off <<= 1) {
+          const uint32_t v = __shfl_up(incl, off);
+          if (lane >= off) incl += v;
+        }
+        const uint64_t hit = __ballot(yc && incl >= rem);
+        if (!hit) { why(6); broke = true; break; }  // (the counts said the chunk holds it)
+        const uint32_t L = (uint32_t)__ffsll((long long)hit) - 1;
+        // (the lane's word: from the registers' chunk layout, or lane = word offset in chunk fch)
+        const uint32_t kword = (fch == jb || (fch == jb + 1 && 2 * SWC <= 64)) ? L - (fch - jb) * SWC : L;
+        const uint32_t Lp = __shfl(lane == L ? ((fcs >> 6) + kword) * 64 + nth_set1(yw, rem - (incl - yc)) : 0u, L);
         e = Lp + 1;
-        sq[s] = q;
-        p = dsp;
+        cur = Lp;
+        from_last = true;
       }
-    } else {
-      sq[s] = p1;
     }
-    if (lane == 0) { sp1[s] = p1; sn[s] = n; scl[s] = client; sck[s] = clock; se[s] = e; sk0[s] = k0; }
+    if (lane == 0) { sp1[s] = p1; sn[s] = n; scl[s] = client; sck[s] = clock; se[s] = e; sk0[s] = k0; sq[s] = n ? q : p1; }
+    done = s + 1;
+    if (!from_last) hdr = p;  // the next header (the section ends where its header or walk ended)
   }
-  // pass 2: commit
+  if (!broke && from_last) {  // the last section checked ends at its last struct (cur)
+    const uint32_t dl = cur < uend ? chain_len(GlobalSrc{b}, b, cur, uend) : 0u;
+    if (!dl || cur + dl > uend) {
+      why(7);
+      done -= 1;
+      hdr = shp[done];
+    } else {
+      hdr = cur + dl;
+    }
+  }
+  if (done == 0) return;  // nothing vouched for: k_walk takes the update from its start
+  if (!broke && done < nsec) why(1);  // more sections than FWM_MAX
+  // pass 2: commit the vouched sections (records for all nsec; k_walk writes the rest)
+  __syncthreads();
   if (lane == 0) sh_sbase = atomicAdd(&w.ctr->nsections, nsec);
   __syncthreads();
   const uint32_t sbase = sh_sbase;
   if (sbase + nsec > w.cap_sections) { if (lane == 0) raise_err(&w.ctr->err, ERR_CAPACITY); return; }
-  for (uint32_t s = lane; s < nsec; s += 64) {
+  for (uint32_t s = lane; s < done; s += 64) {
     const uint32_t n = sn[s], p1 = sp1[s];
     Section sec;
     sec.upd = u; sec.n = n; sec.client = scl[s]; sec.clock = sck[s];
@@ -1360,9 +1504,15 @@ __global__ __launch_bounds__(64) void k_fastwalk_multi(Work w) {
   if (lane == 0) {
     w.usec_start[u] = sbase;
     w.usec_n[u] = nsec;
-    w.dsstart[u] = p;
-    w.ufail[u] = 3u;  // done: k_walk leaves it alone, k_fastmark copies the chain ranges
-    if (w.dbg) atomicAdd(&w.dbg[0], 1ull);
+    if (done == nsec) {
+      w.dsstart[u] = hdr;  // (past the last section: the delete set)
+      w.ufail[u] = 3u;     // done: k_walk leaves it alone, k_fastmark copies the chain ranges
+      if (w.dbg) atomicAdd(&w.dbg[0], 1ull);
+    } else {
+      w.fw[2 * u] = done;  // k_walk resumes at section `done`, whose header is at hdr
+      w.fw[2 * u + 1] = hdr;
+      w.ufail[u] = 4u;
+    }
   }
 }
 // per chunk: its chain positions, and whether its entry may be off the one chain (coff): it was
@@ -1402,9 +1552,10 @@ __global__ __launch_bounds__(256) void k_fastmark(Work w) {
     const uint32_t uf = w.ufail[u];
     if (uf < 2u) continue;
     const uint32_t wd = (gr.start >> 6) + (uint32_t)(t % wpc);
-    if (uf == 3u) {  // several sections (k_fastwalk_multi): the chain ranges meeting this word
+    if (uf >= 3u) {  // several sections (k_fastwalk_multi): the chain ranges meeting this word
+      // (ufail 4: only its first fw[2u] sections; k_walk resumes past them)
       if ((uint64_t)wd * 64 >= gr.end) continue;
-      const uint32_t s0 = w.usec_start[u], ns = w.usec_n[u], a = wd * 64;
+      const uint32_t s0 = w.usec_start[u], ns = uf == 4u ? w.fw[2 * u] : w.usec_n[u], a = wd * 64;
       uint32_t lo = 0, hi = ns;
       while (lo < hi) { const uint32_t m = (lo + hi) >> 1; if (w.fwsec[2 * (s0 + m) + 1] <= a) lo = m + 1; else hi = m; }
       const uint32_t uw = upd_win(w, u);
@@ -1919,6 +2070,231 @@ __global__ __launch_bounds__(WR_LANES) void k_wrank(Work w) {
   for (uint32_t k = t; k < nw; k += WR_LANES) fbits[(ustart >> 6) + k] = bits[k];
 }
 
+// Direct path, split: P lanes per small single-section update (k_direct's one lane per update
+// leaves a C2 batch at 1.7 wavefronts per SIMD, each struct step a chain of dependent instructions
+// and LDS reads: more chains in flight is the lever). The update's struct bytes are cut at 64-byte
+// boundaries into P parts; lane 0 of the group walks its part exactly from the first struct, lane
+// j > 0 follows the all-struct chain of its part from a hinted start (the first of its first 96
+// bytes where three chain steps start with the first struct's info byte), each writing its own
+// words of the final bitmap. Then P - 1 rounds re-enter each part where the previous part's chain
+// leaves (as k_sync: walk until meeting the part's own chain; a part whose own chain never meets is
+// replaced by the re-walk and passes its exit on), the struct counts are scanned across the group,
+// the n-th position is the section's last struct, and the bits past it are cleared. Any doubt — a
+// position on the final chain where no struct parses, fewer positions than structs — and lane 0
+// walks the update exactly as k_direct does (clearing the parts first), which reports the error.
+// Several sections, or an update too short to split: lane 0 walks it exactly.
+constexpr uint32_t DSPLIT = 4;  // lanes per update
+template <uint32_t DWT, uint32_t P>
+__global__ __launch_bounds__(DL) void k_direct_split(Work w) {
+  constexpr uint32_t DSTR = DWT / 4 + 4;
+  __shared__ __attribute__((aligned(16))) uint32_t win[DL * DSTR];
+  const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t i = gid / P, j = gid % P, lane = threadIdx.x & 63, g0 = lane - j;  // g0: the group's lane 0
+  const bool live = i < w.nsmall;
+  const uint32_t u = live ? w.ulist[w.nbig + i] : 0u;
+  const uint32_t uw = live ? upd_win(w, u) : 0u;
+  const uint8_t* __restrict__ b = win_bytes(w, uw);
+  uint64_t* __restrict__ fbits = win_words(w.final_bits, uw);
+  uint64_t* __restrict__ sbits = win_words(w.sec_bits, uw);
+  const uint32_t ustart = live ? w.uoff[u] : 0u, uend = live ? ustart + w.ulen[u] : 0u;
+  uint32_t* err = &w.ctr->err;
+  uint32_t* slot = win + threadIdx.x * DSTR;
+  LdsSrc src{b, slot, 0, 0};
+  auto refill = [&](uint32_t q) {
+    src.s0 = q & ~15u;
+    src.wlen = min(DWT, (uend + 15u - src.s0) & ~15u);
+    fill_window<DWT>(slot, (const uint4*)(b + src.s0));
+  };
+  // wave-uniform call: every lane's window holds q (act: the lane's step is real)
+  auto size_at = [&](bool act, uint32_t q) -> uint32_t {
+    const bool need = act && (q < src.s0 || (src.wlen == DWT && q - src.s0 + DREFILL > DWT) || q - src.s0 >= src.wlen);
+    if (__ballot(need)) { if (need) refill(q); }
+    return act ? chain_len(src, b, q, uend) : 0u;
+  };
+  // ---- headers (every lane of the group reads them; lane 0 of the group records them)
+  bool ok = live;
+  uint32_t p = ustart, nsec = 0, n = 0, client = 0, clock = 0;
+  if (live) {
+    nsec = rd_vu(b, p, uend, ok);
+    if (ok && nsec == 1) {
+      n = rd_vu(b, p, uend, ok);
+      client = rd_vu(b, p, uend, ok);
+      clock = rd_vu(b, p, uend, ok);
+    }
+  }
+  const uint32_t p0 = p;  // (nsec == 1: the first struct)
+  const uint32_t L = uend - p0;
+  // split only a well-formed single section long enough for P parts of >= 256 bytes
+  const bool split = live && ok && nsec == 1 && n > 0 && n <= L && L >= P * 256u;
+  uint32_t a0 = 0, a1 = 0;  // this lane's part [a0, a1)
+  if (split) {
+    a0 = j == 0 ? p0 : ((p0 + j * (L / P)) & ~63u);
+    a1 = j == P - 1 ? uend : ((p0 + (j + 1) * (L / P)) & ~63u);
+  }
+  uint32_t X = 0, C = 0, bad = NONE, entered = NONE;
+  if (__ballot(split)) {
+    // ---- phase 1: each part's chain
+    uint32_t q = a0;
+    if (split) refill(a0);
+    if (split && j > 0) {  // the hinted start (from the window)
+      const uint32_t hint = b[p0], lim = min(a0 + 96u, a1);
+      bool found = false;
+      for (uint32_t c = a0; c < lim && !found; ++c) {
+        if (src.u8(c) != hint) continue;
+        const uint32_t d1 = chain_len(src, b, c, uend);
+        if (!d1 || c + d1 >= uend || src.u8(c + d1) != hint) continue;
+        const uint32_t d2 = chain_len(src, b, c + d1, uend);
+        if (!d2 || c + d1 + d2 >= uend || src.u8(c + d1 + d2) != hint) continue;
+        q = c;
+        found = true;
+      }
+    }
+    uint32_t word = NONE;
+    uint64_t m = 0;
+    for (;;) {
+      const bool act = split && q < a1;
+      if (!__ballot(act)) break;
+      if (act) {
+        if ((q >> 6) != word) {
+          if (word != NONE) fbits[word] = m;
+          word = q >> 6;
+          m = 0;
+        }
+        m |= 1ull << (q & 63);
+        ++C;
+      }
+      const uint32_t d = size_at(act, q);
+      if (act) {
+        if (!d && bad == NONE) bad = q;
+        q += d ? d : 1u;
+      }
+    }
+    if (split && word != NONE) fbits[word] = m;
+    X = q;
+    entered = j == 0 ? p0 : NONE;
+    // ---- phase 2: P - 1 rounds of re-entry at the previous part's exit
+    for (uint32_t r = 0; r + 1 < P; ++r) {
+      const uint32_t E = __shfl(X, (lane + 63) & 63);  // the previous lane's exit (lane j - 1 of the group for j > 0)
+      const bool redo = split && j > 0 && E != entered;
+      if (!__ballot(redo)) continue;
+      bool jumped = false;
+      uint32_t meet = NONE, qa = E, bada = NONE;
+      if (redo) {
+        entered = E;
+        jumped = E >= a1;
+      }
+      // pass A: from E until a position of the own chain (its bit) or the part's end
+      for (;;) {
+        const bool act = redo && !jumped && qa < a1 && !((fbits[qa >> 6] >> (qa & 63)) & 1ull);
+        if (!__ballot(act)) break;
+        const uint32_t d = size_at(act, qa);
+        if (act) {
+          if (!d && bada == NONE) bada = qa;
+          qa += d ? d : 1u;
+        }
+      }
+      if (redo && !jumped && qa < a1) meet = qa;
+      // the own chain's positions below the meeting point (a few words from the part's start)
+      const uint32_t below = redo && meet != NONE ? popc_range(fbits, a0, meet) : 0u;
+      // pass B: the own chain below the meeting point is not the true one: clear it, and mark the
+      // re-walked positions (none when the entry jumped the part)
+      if (redo) {
+        const uint32_t cend = jumped ? a1 : meet != NONE ? meet : a1;
+        for (uint32_t wd = a0 >> 6; wd * 64 < cend; ++wd) {
+          const uint64_t keep = wd == (cend >> 6) ? (~0ull << (cend & 63)) : 0ull;
+          fbits[wd] &= keep;
+        }
+      }
+      uint32_t qb = E, kb = 0;
+      for (;;) {
+        const bool act = redo && !jumped && qb < a1 && (meet == NONE || qb < meet);
+        if (!__ballot(act)) break;
+        if (act) { fbits[qb >> 6] |= 1ull << (qb & 63); ++kb; }
+        const uint32_t d = size_at(act, qb);
+        if (act) qb += d ? d : 1u;
+      }
+      if (redo) {
+        if (jumped) { C = 0; X = E; bad = NONE; }
+        else if (meet != NONE) {
+          C = kb + C - below;
+          bad = bada != NONE ? bada : (bad != NONE && bad >= meet ? bad : NONE);
+        } else {
+          C = kb;
+          X = qb;
+          bad = bada;
+        }
+      }
+    }
+  }
+  // ---- phase 3: the n-th chain position across the group
+  uint32_t incl = split ? C : 0u;
+  for (uint32_t off = 1; off < P; off <<= 1) {
+    const uint32_t v = __shfl_up(incl, off);
+    if (j >= off) incl += v;
+  }
+  const uint32_t total = __shfl(incl, g0 + P - 1);
+  const bool mine = split && incl >= n && incl - C < n;  // the part holding the n-th position
+  uint32_t Lp = NONE;
+  if (mine) {  // the rem-th of the part's C positions: from the part's end when nearer (the last
+               // struct is usually a few positions before the end: the delete set's garbage chain)
+    const uint32_t rem = n - (incl - C), back = C - rem + 1;
+    if (back < rem) {
+      uint32_t wd = (a1 - 1) >> 6, k = back;
+      uint64_t x = fbits[wd] & (~0ull >> (63 - ((a1 - 1) & 63)));
+      for (;;) {
+        const uint32_t c = (uint32_t)__popcll(x);
+        if (c >= k) break;
+        k -= c;
+        x = fbits[--wd];
+      }
+      for (uint32_t t = 1; t < k; ++t) x &= ~(1ull << (63 - __clzll(x)));  // drop the highest k - 1
+      Lp = wd * 64 + 63 - (uint32_t)__clzll(x);
+    } else {
+      Lp = select_from(fbits, a0, rem);
+    }
+  }
+  // the lanes up to the last struct's: no position on the final chain where no struct parses
+  const uint64_t grp = (P == 64 ? ~0ull : ((1ull << P) - 1ull)) << g0;
+  const uint32_t lastj = __ffsll((long long)(__ballot(mine) & grp)) - 1 - g0;  // (garbage when total < n)
+  const uint32_t LpG = __shfl(Lp, g0 + (lastj < P ? lastj : 0u));
+  const bool badj = split && j <= lastj && bad != NONE && (j < lastj || bad <= LpG);
+  const bool gfail = split && (total < n || (__ballot(badj) & grp) != 0);
+  uint32_t dsp = NONE;
+  if (split && !gfail) {
+    if (j == lastj) {
+      const uint32_t d = chain_len(GlobalSrc{b}, b, Lp, uend);
+      dsp = d ? Lp + d : NONE;
+      // the chain past the last struct (the delete set parsed as structs): cleared
+      for (uint32_t wd = Lp >> 6; wd * 64 < a1; ++wd) fbits[wd] &= wd == (Lp >> 6) ? (~0ull >> (63 - (Lp & 63))) : 0ull;
+    } else if (j > lastj) {
+      for (uint32_t wd = a0 >> 6; wd * 64 < a1; ++wd) fbits[wd] = 0;
+    }
+  }
+  dsp = __shfl(dsp, g0 + (lastj < P ? lastj : 0u));
+  const bool exact = live && (!split || gfail || dsp == NONE || dsp > uend);
+  if (split && exact) {  // clear the parts before the exact walk rewrites the update's words
+    for (uint32_t wd = a0 >> 6; wd * 64 < a1; ++wd) fbits[wd] = 0;
+  }
+  __threadfence_block();  // (the clears land before the group's lane 0 walks)
+  if (j != 0 || !live) return;
+  if (w.dbg) atomicAdd(&w.dbg[!exact ? 16 : split ? 17 : 18], 1ull);  // (YCRDT_DEBUG_DECODE)
+  // ---- the group's lane 0: the exact walk when the split could not vouch, else the records
+  if (exact) {
+    direct_walk<DWT>(w, u, slot);
+    return;
+  }
+  w.dsstart[u] = dsp;
+  const uint32_t sbase = atomicAdd(&w.ctr->nsections, 1u);
+  if (sbase + 1 > w.cap_sections) { raise_err(err, ERR_CAPACITY); return; }
+  w.usec_start[u] = sbase;
+  w.usec_n[u] = 1;
+  Section sec;
+  sec.upd = u; sec.n = n; sec.client = client; sec.clock = clock;
+  sec.first_pos = p0; sec.cidx = NONE; sec.first_idx = NONE; sec.pad = 0;
+  w.sections[sbase] = sec;
+  atomicOr((unsigned long long*)&sbits[p0 >> 6], 1ull << (p0 & 63));
+}
+
 bool wave_decode(const Work& w) {
   // one lane per update when there are enough updates to fill wavefronts, else the ranked path;
   // YCRDT_DIRECT_WAVE=1 / 0 forces one (read per merge: tests switch it)
@@ -1935,7 +2311,10 @@ void launch_direct(const Work& w, hipStream_t s) {
     hipLaunchKernelGGL(k_wlen, dim3(WD_MAX / WL_SPAN, w.nsmall), dim3(256), 0, s, w);
     hipLaunchKernelGGL(k_wrank, dim3(w.nsmall), dim3(WR_LANES), 0, s, w);
   } else if (w.nsmall) {
-    hipLaunchKernelGGL(k_direct<DW>, dim3((w.nsmall + DL - 1) / DL), dim3(DL), 0, s, w);  // (64 / 96 / 256 B windows: slower on C2)
+    // YCRDT_DIRECT_SPLIT=1: DSPLIT lanes per update (k_direct_split) instead of one (read per merge: tests)
+    const char* ds = getenv("YCRDT_DIRECT_SPLIT");
+    if (!(ds && ds[0] == '1')) hipLaunchKernelGGL(k_direct<DW>, dim3((w.nsmall + DL - 1) / DL), dim3(DL), 0, s, w);  // (64 / 96 / 256 B windows: slower on C2)
+    else hipLaunchKernelGGL((k_direct_split<DW, DSPLIT>), dim3((w.nsmall * DSPLIT + DL - 1) / DL), dim3(DL), 0, s, w);
   }
 }
 

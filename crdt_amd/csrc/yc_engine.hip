@@ -808,6 +808,7 @@ int run_decode(ycrdt_engine* e, ycrdt_batch* b, bool lazy, Decoded& D, bool gene
   {
     const char* mode = getenv("YCRDT_DECODE");
     w.force_xtab = mode && !strcmp(mode, "xtab") ? 1u : 0u;
+    w.fwm_max = getenv("YCRDT_FWM_MAX") ? (uint32_t)atoi(getenv("YCRDT_FWM_MAX")) : 0u;
     const char* sh = getenv("YCRDT_SPEC_HINT");
     // chunk-start hints: single-section updates only by default (a C2 snapshot or replica update
     // syncs with them; multi-section C4 states locked into wrong phases with them, §5.4b);
@@ -875,8 +876,8 @@ int run_decode(ycrdt_engine* e, ycrdt_batch* b, bool lazy, Decoded& D, bool gene
                   {(uint32_t*)w.sec_bits, (uint64_t)nwords * 2, 0u}}, s);
   const bool dbg_yata = getenv("YCRDT_DEBUG_YATA") && getenv("YCRDT_DEBUG_YATA")[0] == '1';
   const bool dbg_dec = getenv("YCRDT_DEBUG_DECODE") && getenv("YCRDT_DEBUG_DECODE")[0] == '1';
-  w.dbg = dbg_yata || dbg_dec ? take<unsigned long long>(V, B_DBG, 16, ok) : nullptr;
-  if (w.dbg) HIPCHK(hipMemsetAsync(w.dbg, 0, 128, s));
+  w.dbg = dbg_yata || dbg_dec ? take<unsigned long long>(V, B_DBG, 24, ok) : nullptr;
+  if (w.dbg) HIPCHK(hipMemsetAsync(w.dbg, 0, 192, s));
   // ---- K1 decode
   // large updates (chunk path, mostly latency-bound) on the side stream, beside k_direct
   mark(e, "decode.direct");
@@ -912,11 +913,12 @@ int run_decode(ycrdt_engine* e, ycrdt_batch* b, bool lazy, Decoded& D, bool gene
   Counters c;
   int rc = check(e, c, "decode");
   if (dbg_dec && w.dbg) {  // experiments: why k_fastwalk left large updates to k_walk
-    unsigned long long h[16];
+    unsigned long long h[24];
     HIPCHK(hipMemcpy(h, w.dbg, sizeof(h), hipMemcpyDeviceToHost));
+    fprintf(stderr, "[ycrdt decode] direct split: vouched %llu, exact after a split %llu, exact (several sections / short) %llu\n", h[16], h[17], h[18]);
     fprintf(stderr, "[ycrdt decode] fastwalk: done %llu nsec %llu unsynced %llu | wave: done %llu unsettled %llu other %llu (chunk path: moved / jumped chunk entries) | k_spec exact parses %llu (%llu bytes) | multi-section left to k_walk, by reason 1-5: %llu %llu %llu %llu %llu (section %llu of %llu structs) | %llu %llu %llu\n",
             h[0], h[1], h[2], h[3], h[4], h[5], h[6], h[7], h[9], h[10], h[11], h[12], h[13], h[14], h[15], h[11], h[12], h[13]);
-    HIPCHK(hipMemsetAsync(w.dbg, 0, 128, s));
+    HIPCHK(hipMemsetAsync(w.dbg, 0, 192, s));
   }
   if (rc == YCRDT_E_CAPACITY && !generous) return run_decode(e, b, lazy, D, true, sh);  // past the estimates
   if (rc) return rc;

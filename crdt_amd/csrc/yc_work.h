@@ -93,6 +93,7 @@ struct Work {
   uint16_t* wlen = nullptr;        // [nsmall * 16384] few small updates: the chain step at every position (k_wlen)
   uint32_t schunk = SCHUNK;        // chunk bytes of this batch's large updates (<= SCHUNK)
   uint32_t force_xtab = 0;         // YCRDT_DECODE=xtab: every large update takes the exit-table walk (tests)
+  uint32_t fwm_max = 0;            // YCRDT_FWM_MAX=n: k_fastwalk_multi vouches for at most n sections per update (tests: k_walk resumes)
   uint32_t spec_hint = 2;          // k_spec chunk-start hints: 0 never, 1 always, 2 single-section updates
   uint32_t lazy = 0;               // 1: mergeUpdates / diffUpdate decode (references kept raw)
   unsigned long long* dbg = nullptr; // YCRDT_DEBUG_YATA=1: k_yata work counters

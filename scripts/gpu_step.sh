@@ -3,9 +3,11 @@
 set -u
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-timeout -k 10 900 python -u -m pytest tests -x -q --timeout 300 --timeout-method thread -m gpu > gpurun_out/step_tests.log 2>&1 || { grep -E "^E |FAIL|Error" gpurun_out/step_tests.log | head -30; tail -5 gpurun_out/step_tests.log; exit 1; }
-tail -1 gpurun_out/step_tests.log
-timeout -k 10 300 python bench.py --only-headline --profile-phases --steps 10 --warmup 3 > gpurun_out/s_h.json 2> gpurun_out/s_h.err || { tail -20 gpurun_out/s_h.err; exit 1; }
-python3 scripts/bench_summary.py gpurun_out/s_h.json || true
-rm -rf gpurun_out/pmc_r05b
-bash scripts/pmc.sh r05b && python3 scripts/pmc_summary.py gpurun_out/pmc_r05b gpurun_out/pmc_r05b/c2_pmc.csv > gpurun_out/pmc_r05b/summary.txt 2>&1; tail -12 gpurun_out/pmc_r05b/summary.txt
+YCRDT_DEBUG_DECODE=1 timeout -k 10 300 python3 scripts/probe_trace.py c2x112 > gpurun_out/dbg_c2.log 2>&1 || { tail -20 gpurun_out/dbg_c2.log; exit 1; }
+grep "direct split" gpurun_out/dbg_c2.log | tail -2; tail -1 gpurun_out/dbg_c2.log
+rm -rf gpurun_out/tr_c2full
+timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/tr_c2full -o tr -- python3 scripts/probe_trace.py c2full > gpurun_out/tr_c2full.log 2>&1 || { tail -20 gpurun_out/tr_c2full.log; exit 1; }
+python3 scripts/trace_last.py gpurun_out/tr_c2full 100 > gpurun_out/tr_c2full.txt; head -30 gpurun_out/tr_c2full.txt
+rm -rf gpurun_out/tr_c2
+timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/tr_c2 -o tr -- python3 scripts/probe_trace.py c2x112 > gpurun_out/tr_c2.log 2>&1 || { tail -20 gpurun_out/tr_c2.log; exit 1; }
+python3 scripts/trace_last.py gpurun_out/tr_c2 300 > gpurun_out/tr_c2.txt; head -8 gpurun_out/tr_c2.txt

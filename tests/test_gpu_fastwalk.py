@@ -121,3 +121,18 @@ def test_multi_section_walk_is_taken(monkeypatch, capfd):
     snap = _snapshot(40, 200, 5, arrays=False)
     assert len(snap) > 16384
     assert _check([snap], monkeypatch, capfd) >= 1
+
+
+@pytest.mark.parametrize("fwm_max", [1, 2, 7])
+@pytest.mark.parametrize("n_clients,per_client,arrays", [(40, 200, False), (64, 60, True), (600, 4, True)])
+def test_multi_section_walk_resumes(fwm_max, n_clients, per_client, arrays, monkeypatch, capfd):
+    """k_fastwalk_multi vouches for a prefix of the sections and k_walk resumes at the next header
+    (YCRDT_FWM_MAX caps the prefix: the resume path on every snapshot here); the state must be
+    k_walk's alone and the oracle's."""
+    snap = _snapshot(n_clients, per_client, n_clients * 17 + per_client + fwm_max, arrays=arrays)
+    assert len(snap) > 16384
+    monkeypatch.setenv("YCRDT_FWM_MAX", str(fwm_max))
+    _check([snap], monkeypatch, capfd)
+    extra = ODoc(9)
+    extra.map_set("users", "k2", any_int(6))
+    _check([extra.encode_state_as_update(), snap], monkeypatch, capfd)
