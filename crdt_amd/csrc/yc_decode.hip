@@ -457,7 +457,7 @@ __device__ __attribute__((noinline)) uint32_t exact_len(const uint8_t* __restric
   uint32_t q = p;
   return parse_struct<false>(b, q, end, 0xFFFFFFFFu, nullptr) > 0 ? q - p : 0u;
 }
-// (one update's exact walk through the lane's LDS window `slot`; k_direct_split's fallback too)
+// (one update's exact walk through the lane's LDS window `slot`)
 template <uint32_t DWT>
 __device__ __forceinline__ void direct_walk(const Work& w, uint32_t u, uint32_t* slot) {
   const uint32_t uw = upd_win(w, u);  // positions below are relative to the update's window
@@ -1327,7 +1327,9 @@ __global__ __launch_bounds__(64) void k_fastwalk_multi(Work w) {
   uint32_t cur = p;           // the previous section's last struct when from_last
   bool from_last = false;
   bool broke = false;
+  unsigned long long t_stage = 0, t_walk = 0, t_search = 0, n_walk = 0;  // (YCRDT_DEBUG_DECODE: cycles per part)
   for (uint32_t s = 0; s < nchk; ++s) {
+    const unsigned long long tc0 = w.dbg ? clock64() : 0ull;
     // ONE round of loads: the bytes from the header (or the previous section's last struct) and
     // their struct-start words staged in LDS; the struct-start words of the two chunks from the
     // stage's start (held in lanes 0 .. 2 SWC - 1); the count and off prefixes of the 64 chunks from
@@ -1344,6 +1346,7 @@ __global__ __launch_bounds__(64) void k_fastwalk_multi(Work w) {
     const uint64_t P = pv ? w.cpre[c0 + jb + lane + 1] : ~0ull;
     const uint32_t O = pv ? w.opre[c0 + jb + lane + 1] : 0u;
     __syncthreads();
+    const unsigned long long tc1 = w.dbg ? clock64() : 0ull;
     const LdsSrc src{b, stg, s0, wlen};
     auto spec_bit = [&](uint32_t q) {
       const uint32_t k = (q >> 6) - (s0 >> 6);
@@ -1404,6 +1407,8 @@ __global__ __launch_bounds__(64) void k_fastwalk_multi(Work w) {
       if (__shfl(walk_bad, 0)) { why(4); broke = true; break; }
       q = __shfl(q, 0);
       k0 = __shfl(k0, 0);
+      const unsigned long long tc2 = w.dbg ? clock64() : 0ull;
+      if (w.dbg) { t_stage += tc1 - tc0; t_walk += tc2 - tc1; n_walk += k0; }
       if (k0 == n) {  // every struct walked: the next header is where the walk stopped
         if (q > uend) { why(3); broke = true; break; }
         e = q;  // (an empty chain range [q, q))
@@ -1461,6 +1466,7 @@ __global__ __launch_bounds__(64) void k_fastwalk_multi(Work w) {
         e = Lp + 1;
         cur = Lp;
         from_last = true;
+        if (w.dbg) t_search += clock64() - tc2;
       }
     }
     if (lane == 0) { sp1[s] = p1; sn[s] = n; scl[s] = client; sck[s] = clock; se[s] = e; sk0[s] = k0; sq[s] = n ? q : p1; }
@@ -1476,6 +1482,10 @@ __global__ __launch_bounds__(64) void k_fastwalk_multi(Work w) {
     } else {
       hdr = cur + dl;
     }
+  }
+  if (w.dbg && lane == 0) {
+    atomicAdd(&w.dbg[19], t_stage); atomicAdd(&w.dbg[20], t_walk); atomicAdd(&w.dbg[21], t_search);
+    atomicAdd(&w.dbg[22], n_walk); atomicAdd(&w.dbg[23], (unsigned long long)done);
   }
   if (done == 0) return;  // nothing vouched for: k_walk takes the update from its start
   if (!broke && done < nsec) why(1);  // more sections than FWM_MAX
@@ -2070,231 +2080,6 @@ __global__ __launch_bounds__(WR_LANES) void k_wrank(Work w) {
   for (uint32_t k = t; k < nw; k += WR_LANES) fbits[(ustart >> 6) + k] = bits[k];
 }
 
-// Direct path, split: P lanes per small single-section update (k_direct's one lane per update
-// leaves a C2 batch at 1.7 wavefronts per SIMD, each struct step a chain of dependent instructions
-// and LDS reads: more chains in flight is the lever). The update's struct bytes are cut at 64-byte
-// boundaries into P parts; lane 0 of the group walks its part exactly from the first struct, lane
-// j > 0 follows the all-struct chain of its part from a hinted start (the first of its first 96
-// bytes where three chain steps start with the first struct's info byte), each writing its own
-// words of the final bitmap. Then P - 1 rounds re-enter each part where the previous part's chain
-// leaves (as k_sync: walk until meeting the part's own chain; a part whose own chain never meets is
-// replaced by the re-walk and passes its exit on), the struct counts are scanned across the group,
-// the n-th position is the section's last struct, and the bits past it are cleared. Any doubt — a
-// position on the final chain where no struct parses, fewer positions than structs — and lane 0
-// walks the update exactly as k_direct does (clearing the parts first), which reports the error.
-// Several sections, or an update too short to split: lane 0 walks it exactly.
-constexpr uint32_t DSPLIT = 4;  // lanes per update
-template <uint32_t DWT, uint32_t P>
-__global__ __launch_bounds__(DL) void k_direct_split(Work w) {
-  constexpr uint32_t DSTR = DWT / 4 + 4;
-  __shared__ __attribute__((aligned(16))) uint32_t win[DL * DSTR];
-  const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
-  const uint32_t i = gid / P, j = gid % P, lane = threadIdx.x & 63, g0 = lane - j;  // g0: the group's lane 0
-  const bool live = i < w.nsmall;
-  const uint32_t u = live ? w.ulist[w.nbig + i] : 0u;
-  const uint32_t uw = live ? upd_win(w, u) : 0u;
-  const uint8_t* __restrict__ b = win_bytes(w, uw);
-  uint64_t* __restrict__ fbits = win_words(w.final_bits, uw);
-  uint64_t* __restrict__ sbits = win_words(w.sec_bits, uw);
-  const uint32_t ustart = live ? w.uoff[u] : 0u, uend = live ? ustart + w.ulen[u] : 0u;
-  uint32_t* err = &w.ctr->err;
-  uint32_t* slot = win + threadIdx.x * DSTR;
-  LdsSrc src{b, slot, 0, 0};
-  auto refill = [&](uint32_t q) {
-    src.s0 = q & ~15u;
-    src.wlen = min(DWT, (uend + 15u - src.s0) & ~15u);
-    fill_window<DWT>(slot, (const uint4*)(b + src.s0));
-  };
-  // wave-uniform call: every lane's window holds q (act: the lane's step is real)
-  auto size_at = [&](bool act, uint32_t q) -> uint32_t {
-    const bool need = act && (q < src.s0 || (src.wlen == DWT && q - src.s0 + DREFILL > DWT) || q - src.s0 >= src.wlen);
-    if (__ballot(need)) { if (need) refill(q); }
-    return act ? chain_len(src, b, q, uend) : 0u;
-  };
-  // ---- headers (every lane of the group reads them; lane 0 of the group records them)
-  bool ok = live;
-  uint32_t p = ustart, nsec = 0, n = 0, client = 0, clock = 0;
-  if (live) {
-    nsec = rd_vu(b, p, uend, ok);
-    if (ok && nsec == 1) {
-      n = rd_vu(b, p, uend, ok);
-      client = rd_vu(b, p, uend, ok);
-      clock = rd_vu(b, p, uend, ok);
-    }
-  }
-  const uint32_t p0 = p;  // (nsec == 1: the first struct)
-  const uint32_t L = uend - p0;
-  // split only a well-formed single section long enough for P parts of >= 256 bytes
-  const bool split = live && ok && nsec == 1 && n > 0 && n <= L && L >= P * 256u;
-  uint32_t a0 = 0, a1 = 0;  // this lane's part [a0, a1)
-  if (split) {
-    a0 = j == 0 ? p0 : ((p0 + j * (L / P)) & ~63u);
-    a1 = j == P - 1 ? uend : ((p0 + (j + 1) * (L / P)) & ~63u);
-  }
-  uint32_t X = 0, C = 0, bad = NONE, entered = NONE;
-  if (__ballot(split)) {
-    // ---- phase 1: each part's chain
-    uint32_t q = a0;
-    if (split) refill(a0);
-    if (split && j > 0) {  // the hinted start (from the window)
-      const uint32_t hint = b[p0], lim = min(a0 + 96u, a1);
-      bool found = false;
-      for (uint32_t c = a0; c < lim && !found; ++c) {
-        if (src.u8(c) != hint) continue;
-        const uint32_t d1 = chain_len(src, b, c, uend);
-        if (!d1 || c + d1 >= uend || src.u8(c + d1) != hint) continue;
-        const uint32_t d2 = chain_len(src, b, c + d1, uend);
-        if (!d2 || c + d1 + d2 >= uend || src.u8(c + d1 + d2) != hint) continue;
-        q = c;
-        found = true;
-      }
-    }
-    uint32_t word = NONE;
-    uint64_t m = 0;
-    for (;;) {
-      const bool act = split && q < a1;
-      if (!__ballot(act)) break;
-      if (act) {
-        if ((q >> 6) != word) {
-          if (word != NONE) fbits[word] = m;
-          word = q >> 6;
-          m = 0;
-        }
-        m |= 1ull << (q & 63);
-        ++C;
-      }
-      const uint32_t d = size_at(act, q);
-      if (act) {
-        if (!d && bad == NONE) bad = q;
-        q += d ? d : 1u;
-      }
-    }
-    if (split && word != NONE) fbits[word] = m;
-    X = q;
-    entered = j == 0 ? p0 : NONE;
-    // ---- phase 2: P - 1 rounds of re-entry at the previous part's exit
-    for (uint32_t r = 0; r + 1 < P; ++r) {
-      const uint32_t E = __shfl(X, (lane + 63) & 63);  // the previous lane's exit (lane j - 1 of the group for j > 0)
-      const bool redo = split && j > 0 && E != entered;
-      if (!__ballot(redo)) continue;
-      bool jumped = false;
-      uint32_t meet = NONE, qa = E, bada = NONE;
-      if (redo) {
-        entered = E;
-        jumped = E >= a1;
-      }
-      // pass A: from E until a position of the own chain (its bit) or the part's end
-      for (;;) {
-        const bool act = redo && !jumped && qa < a1 && !((fbits[qa >> 6] >> (qa & 63)) & 1ull);
-        if (!__ballot(act)) break;
-        const uint32_t d = size_at(act, qa);
-        if (act) {
-          if (!d && bada == NONE) bada = qa;
-          qa += d ? d : 1u;
-        }
-      }
-      if (redo && !jumped && qa < a1) meet = qa;
-      // the own chain's positions below the meeting point (a few words from the part's start)
-      const uint32_t below = redo && meet != NONE ? popc_range(fbits, a0, meet) : 0u;
-      // pass B: the own chain below the meeting point is not the true one: clear it, and mark the
-      // re-walked positions (none when the entry jumped the part)
-      if (redo) {
-        const uint32_t cend = jumped ? a1 : meet != NONE ? meet : a1;
-        for (uint32_t wd = a0 >> 6; wd * 64 < cend; ++wd) {
-          const uint64_t keep = wd == (cend >> 6) ? (~0ull << (cend & 63)) : 0ull;
-          fbits[wd] &= keep;
-        }
-      }
-      uint32_t qb = E, kb = 0;
-      for (;;) {
-        const bool act = redo && !jumped && qb < a1 && (meet == NONE || qb < meet);
-        if (!__ballot(act)) break;
-        if (act) { fbits[qb >> 6] |= 1ull << (qb & 63); ++kb; }
-        const uint32_t d = size_at(act, qb);
-        if (act) qb += d ? d : 1u;
-      }
-      if (redo) {
-        if (jumped) { C = 0; X = E; bad = NONE; }
-        else if (meet != NONE) {
-          C = kb + C - below;
-          bad = bada != NONE ? bada : (bad != NONE && bad >= meet ? bad : NONE);
-        } else {
-          C = kb;
-          X = qb;
-          bad = bada;
-        }
-      }
-    }
-  }
-  // ---- phase 3: the n-th chain position across the group
-  uint32_t incl = split ? C : 0u;
-  for (uint32_t off = 1; off < P; off <<= 1) {
-    const uint32_t v = __shfl_up(incl, off);
-    if (j >= off) incl += v;
-  }
-  const uint32_t total = __shfl(incl, g0 + P - 1);
-  const bool mine = split && incl >= n && incl - C < n;  // the part holding the n-th position
-  uint32_t Lp = NONE;
-  if (mine) {  // the rem-th of the part's C positions: from the part's end when nearer (the last
-               // struct is usually a few positions before the end: the delete set's garbage chain)
-    const uint32_t rem = n - (incl - C), back = C - rem + 1;
-    if (back < rem) {
-      uint32_t wd = (a1 - 1) >> 6, k = back;
-      uint64_t x = fbits[wd] & (~0ull >> (63 - ((a1 - 1) & 63)));
-      for (;;) {
-        const uint32_t c = (uint32_t)__popcll(x);
-        if (c >= k) break;
-        k -= c;
-        x = fbits[--wd];
-      }
-      for (uint32_t t = 1; t < k; ++t) x &= ~(1ull << (63 - __clzll(x)));  // drop the highest k - 1
-      Lp = wd * 64 + 63 - (uint32_t)__clzll(x);
-    } else {
-      Lp = select_from(fbits, a0, rem);
-    }
-  }
-  // the lanes up to the last struct's: no position on the final chain where no struct parses
-  const uint64_t grp = (P == 64 ? ~0ull : ((1ull << P) - 1ull)) << g0;
-  const uint32_t lastj = __ffsll((long long)(__ballot(mine) & grp)) - 1 - g0;  // (garbage when total < n)
-  const uint32_t LpG = __shfl(Lp, g0 + (lastj < P ? lastj : 0u));
-  const bool badj = split && j <= lastj && bad != NONE && (j < lastj || bad <= LpG);
-  const bool gfail = split && (total < n || (__ballot(badj) & grp) != 0);
-  uint32_t dsp = NONE;
-  if (split && !gfail) {
-    if (j == lastj) {
-      const uint32_t d = chain_len(GlobalSrc{b}, b, Lp, uend);
-      dsp = d ? Lp + d : NONE;
-      // the chain past the last struct (the delete set parsed as structs): cleared
-      for (uint32_t wd = Lp >> 6; wd * 64 < a1; ++wd) fbits[wd] &= wd == (Lp >> 6) ? (~0ull >> (63 - (Lp & 63))) : 0ull;
-    } else if (j > lastj) {
-      for (uint32_t wd = a0 >> 6; wd * 64 < a1; ++wd) fbits[wd] = 0;
-    }
-  }
-  dsp = __shfl(dsp, g0 + (lastj < P ? lastj : 0u));
-  const bool exact = live && (!split || gfail || dsp == NONE || dsp > uend);
-  if (split && exact) {  // clear the parts before the exact walk rewrites the update's words
-    for (uint32_t wd = a0 >> 6; wd * 64 < a1; ++wd) fbits[wd] = 0;
-  }
-  __threadfence_block();  // (the clears land before the group's lane 0 walks)
-  if (j != 0 || !live) return;
-  if (w.dbg) atomicAdd(&w.dbg[!exact ? 16 : split ? 17 : 18], 1ull);  // (YCRDT_DEBUG_DECODE)
-  // ---- the group's lane 0: the exact walk when the split could not vouch, else the records
-  if (exact) {
-    direct_walk<DWT>(w, u, slot);
-    return;
-  }
-  w.dsstart[u] = dsp;
-  const uint32_t sbase = atomicAdd(&w.ctr->nsections, 1u);
-  if (sbase + 1 > w.cap_sections) { raise_err(err, ERR_CAPACITY); return; }
-  w.usec_start[u] = sbase;
-  w.usec_n[u] = 1;
-  Section sec;
-  sec.upd = u; sec.n = n; sec.client = client; sec.clock = clock;
-  sec.first_pos = p0; sec.cidx = NONE; sec.first_idx = NONE; sec.pad = 0;
-  w.sections[sbase] = sec;
-  atomicOr((unsigned long long*)&sbits[p0 >> 6], 1ull << (p0 & 63));
-}
-
 bool wave_decode(const Work& w) {
   // one lane per update when there are enough updates to fill wavefronts, else the ranked path;
   // YCRDT_DIRECT_WAVE=1 / 0 forces one (read per merge: tests switch it)
@@ -2311,10 +2096,9 @@ void launch_direct(const Work& w, hipStream_t s) {
     hipLaunchKernelGGL(k_wlen, dim3(WD_MAX / WL_SPAN, w.nsmall), dim3(256), 0, s, w);
     hipLaunchKernelGGL(k_wrank, dim3(w.nsmall), dim3(WR_LANES), 0, s, w);
   } else if (w.nsmall) {
-    // YCRDT_DIRECT_SPLIT=1: DSPLIT lanes per update (k_direct_split) instead of one (read per merge: tests)
-    const char* ds = getenv("YCRDT_DIRECT_SPLIT");
-    if (!(ds && ds[0] == '1')) hipLaunchKernelGGL(k_direct<DW>, dim3((w.nsmall + DL - 1) / DL), dim3(DL), 0, s, w);  // (64 / 96 / 256 B windows: slower on C2)
-    else hipLaunchKernelGGL((k_direct_split<DW, DSPLIT>), dim3((w.nsmall * DSPLIT + DL - 1) / DL), dim3(DL), 0, s, w);
+    // (one lane per update; 64 / 96 / 256 B windows and 2 / 4 / 8 lanes per update with a
+    // wavefront-local chain sync were slower on C2: DESIGN.md §5.1)
+    hipLaunchKernelGGL(k_direct<DW>, dim3((w.nsmall + DL - 1) / DL), dim3(DL), 0, s, w);
   }
 }
 

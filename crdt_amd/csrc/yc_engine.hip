@@ -915,7 +915,8 @@ int run_decode(ycrdt_engine* e, ycrdt_batch* b, bool lazy, Decoded& D, bool gene
   if (dbg_dec && w.dbg) {  // experiments: why k_fastwalk left large updates to k_walk
     unsigned long long h[24];
     HIPCHK(hipMemcpy(h, w.dbg, sizeof(h), hipMemcpyDeviceToHost));
-    fprintf(stderr, "[ycrdt decode] direct split: vouched %llu, exact after a split %llu, exact (several sections / short) %llu\n", h[16], h[17], h[18]);
+    fprintf(stderr, "[ycrdt decode] multi-section fast walk cycles: stage %llu walk %llu search %llu, walked structs %llu, sections vouched %llu\n",
+            h[19], h[20], h[21], h[22], h[23]);
     fprintf(stderr, "[ycrdt decode] fastwalk: done %llu nsec %llu unsynced %llu | wave: done %llu unsettled %llu other %llu (chunk path: moved / jumped chunk entries) | k_spec exact parses %llu (%llu bytes) | multi-section left to k_walk, by reason 1-5: %llu %llu %llu %llu %llu (section %llu of %llu structs) | %llu %llu %llu\n",
             h[0], h[1], h[2], h[3], h[4], h[5], h[6], h[7], h[9], h[10], h[11], h[12], h[13], h[14], h[15], h[11], h[12], h[13]);
     HIPCHK(hipMemsetAsync(w.dbg, 0, 192, s));

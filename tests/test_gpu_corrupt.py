@@ -6,8 +6,8 @@ shortest-form UTF-8 — lib0's decodeURIComponent, L0@1937 —, ran past the end
 Yjs's state and state vector; after a refusal the doc holds what Yjs's doc holds (the struct
 section is read whole before anything is integrated; a delete-set error comes after it).
 
-Every case runs on each small-update decode path (lanes per update — split and one —, wavefront per
-update, chunk path) — the small sources are <= 16 KiB — and the large source on the chunk path.
+Every case runs on each small-update decode path (lane per update, wavefront per update, chunk
+path) — the small sources are <= 16 KiB — and the large source on the chunk path.
 """
 import hashlib
 import json
@@ -54,15 +54,13 @@ def _bad(fx, c):
     return bytes(u)
 
 
-@pytest.mark.parametrize("mode", ["direct", "direct1", "wave", "settle", "chunks"])
+@pytest.mark.parametrize("mode", ["direct", "wave", "settle", "chunks"])
 def test_corrupt_like_yjs(corrupt, mode, monkeypatch):
     wave = mode in ("wave", "settle")  # few small updates: ranked / k_wdecode's settled chains
     monkeypatch.setenv("YCRDT_DECODE", "chunks" if mode == "chunks" else "direct")
     if mode != "chunks":
         monkeypatch.setenv("YCRDT_DIRECT_WAVE", "1" if wave else "0")
     monkeypatch.setenv("YCRDT_WDECODE", "settle" if mode == "settle" else "rank")
-    # direct: DSPLIT lanes per update (k_direct_split); direct1: one lane per update (k_direct)
-    monkeypatch.setenv("YCRDT_DIRECT_SPLIT", "0" if mode == "direct1" else "1")
     base = bytes.fromhex(corrupt["base"])
     checked = gaps = 0
     for c in corrupt["cases"]:

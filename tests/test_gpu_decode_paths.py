@@ -4,8 +4,7 @@ Small updates (<= 16 KiB) are parsed one lane per update (k_direct) when there a
 workgroup per update when there are few (k_wlen steps every position, k_wrank ranks each section's
 chain by pointer doubling; or, YCRDT_WDECODE=settle, k_wdecode: chunk chains per lane settled
 inside a wavefront); large ones take the chunk path (k_spec / k_sync / k_walk). The modes force
-one: "direct" = k_direct_split (DSPLIT lanes per single-section update), "direct1" = k_direct (one
-lane per update), "wave" = k_wlen + k_wrank, "settle" = k_wdecode, "chunks" = the chunk path.
+one: "direct" = k_direct, "wave" = k_wlen + k_wrank, "settle" = k_wdecode, "chunks" = the chunk path.
 All must match the Yjs fixtures and the oracle byte for byte, and report the same malformed input.
 """
 import pytest
@@ -13,7 +12,7 @@ import pytest
 crdt_amd = pytest.importorskip("crdt_amd")
 
 pytestmark = pytest.mark.gpu
-MODES = ("chunks", "direct", "direct1", "wave", "settle")
+MODES = ("chunks", "direct", "wave", "settle")
 
 
 def _mode(monkeypatch, mode):
@@ -23,7 +22,6 @@ def _mode(monkeypatch, mode):
     if mode != "chunks":
         monkeypatch.setenv("YCRDT_DIRECT_WAVE", "1" if wave else "0")
     monkeypatch.setenv("YCRDT_WDECODE", "settle" if mode == "settle" else "rank")
-    monkeypatch.setenv("YCRDT_DIRECT_SPLIT", "0" if mode == "direct1" else "1")
 
 
 @pytest.mark.parametrize("mode", MODES)
