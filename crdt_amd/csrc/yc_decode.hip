@@ -2162,6 +2162,10 @@ __global__ void k_section_rank(Work w, uint32_t nsections) {
   if (!((fbits[p >> 6] >> (p & 63)) & 1ull)) { raise_err(&w.ctr->err, ERR_DECODE); return; }
   sec->first_idx = rank_incl(fbits, win_words(w.wcnt, uw), p) - 1;
   w.sec_sorted[rank_incl(win_words(w.sec_bits, uw), win_words(w.wsec, uw), p) - 1] = i;
+  // the struct decode's bound and document, beside the section record (one dependent load fewer
+  // per struct than update -> offsets)
+  w.sec_uend[i] = w.uoff[sec->upd] + w.ulen[sec->upd];
+  w.sec_doc[i] = doc_of_update(w, sec->upd);
 }
 // Small batches: both popcount prefixes in one workgroup and one launch (four launches otherwise):
 // a lane sums the popcounts of a contiguous run of words, the run sums are scanned in LDS, each
@@ -2759,10 +2763,10 @@ __device__ __forceinline__ void struct_decode_one(const Work& w, uint32_t i, uin
 #pragma unroll
   for (uint32_t k = 0; k < SD_WIN / 16; ++k) v4[k] = g[k];
   const Section sec = w.sections[si];
+  const uint32_t uend = w.sec_uend[si];
+  const uint32_t doc = w.sec_doc[si];
 #pragma unroll
   for (uint32_t k = 0; k < SD_WIN / 16; ++k) ((uint4*)slot)[k] = v4[k];
-  const uint32_t uend = w.uoff[sec.upd] + w.ulen[sec.upd];
-  const uint32_t doc = doc_of_update(w, sec.upd);
   StructView v;
   uint32_t p = p0;
   const int pr = parse_struct<true, 32, WinSrc, DEFER>(WinSrc{bw, slot, s0}, p, uend, 0xFFFFFFFFu, &v);

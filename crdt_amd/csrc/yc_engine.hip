@@ -179,7 +179,7 @@ enum Buf {
   B_UOWN, B_UFLAG, B_UCUT, B_UWPRE,
   B_GSTART, B_GCIDX, B_GSRC, B_GFLAGS, B_GORIG, B_GRORIG, B_GLINK, B_GOSEG, B_GKEY, B_GMAXC, B_GNEXT, B_GOUTID, B_GTMP, B_GTMP2,
   B_KHASH, B_KROOT, B_KWIN, B_KPAR, B_KFLAG, B_SPK,
-  B_USEC, B_USECN, B_DBG, B_XTAB, B_UFAIL, B_FW, B_CCNT, B_TENTRY, B_XLIST, B_WLEN, B_FWSEC, B_DSPCNT, B_DSPPRE, B_DSPVAL, B_DSPBLK, B_DSPB, B_DSPNB, B_DSPFAIL, B_DSPGB, B_OGEN, B_SDDEFER, B_COFF, B_CPRE, B_OPRE,
+  B_USEC, B_USECN, B_DBG, B_XTAB, B_UFAIL, B_FW, B_CCNT, B_TENTRY, B_XLIST, B_WLEN, B_FWSEC, B_DSPCNT, B_DSPPRE, B_DSPVAL, B_DSPBLK, B_DSPB, B_DSPNB, B_DSPFAIL, B_DSPGB, B_OGEN, B_SDDEFER, B_COFF, B_CPRE, B_OPRE, B_SECUEND, B_SECDOC,
   B_LZKEY, B_LZKEYS, B_LZIOTA, B_LZSEC, B_LZRSTART, B_LZPREV, B_LZFIRST, B_LZCAP, B_LZEVBASE, B_LZEVN, B_LZFLAG,
   B_LZLHI, B_LZLLO, B_EVKIND, B_EVSRC, B_EVCLOCK, B_EVLEN, B_EVSIZE, B_EVPOS, B_BLKSIZE, B_BLKPOS, B_SVC, B_SVK,
   B_DSMKEY, B_DSMKEYS, B_DSMLEN, B_DSMLENS, B_DSMEND, B_DSMMAX, B_DSMFLAG, B_DSMRID, B_DRCLIENT, B_DRCLOCK, B_DREND,
@@ -847,6 +847,8 @@ int run_decode(ycrdt_engine* e, ycrdt_batch* b, bool lazy, Decoded& D, bool gene
   w.dsstart = take<uint32_t>(V, B_DSSTART, nu + 1, ok);
   w.sections = take<Section>(V, B_SECT, w.cap_sections, ok);
   w.sec_sorted = take<uint32_t>(V, B_SECSORT, w.cap_sections, ok);
+  w.sec_uend = take<uint32_t>(V, B_SECUEND, w.cap_sections, ok);
+  w.sec_doc = take<uint32_t>(V, B_SECDOC, w.cap_sections, ok);
   w.wcnt = take<uint32_t>(V, B_WCNT, nwords + 1, ok);
   w.wsec = take<uint32_t>(V, B_WSEC, nwords + 1, ok);
   w.ds_region = take<uint32_t>(V, B_DSREG, nu + 2, ok);

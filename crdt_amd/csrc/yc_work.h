@@ -122,6 +122,8 @@ struct Work {
   uint32_t* dsstart = nullptr;     // [nupd] byte position of the delete set
   Section* sections = nullptr;     // [cap_sections] (walker order)
   uint32_t* sec_sorted = nullptr;  // [cap_sections] section index by position rank
+  uint32_t* sec_uend = nullptr;    // [cap_sections] the section's update end (k_section_rank; the struct decode's bound)
+  uint32_t* sec_doc = nullptr;     // [cap_sections] the section's document (multi-document batches)
   uint32_t* wcnt = nullptr;        // [B/64 + 1] popcount prefix of final_bits words
   uint32_t* wsec = nullptr;        // [B/64 + 1] popcount prefix of sec_bits words
   DsRange* ds = nullptr;           // [cap_ds] dense delete-set ranges

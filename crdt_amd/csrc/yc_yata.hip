@@ -369,31 +369,45 @@ __device__ uint32_t sib_loop(A& a, uint32_t n, S* __restrict__ stack, uint32_t* 
     stack[sp++] = i0;
     a.set_done(i0, 1);
     while (sp > 0) {
+      // (the reads of a step are issued in rounds of independent loads — c's fields; then its
+      // right origin's state and its group's top; each walk step's fields together — since one
+      // lane runs the loop and every dependent LDS / memory read is a wait: C3's list head)
       const uint32_t rp = a.rpos(c);
-      if (rp != NONE && a.done(rp) != 2) {  // the right origin is a sibling: place it first
-        if (a.done(rp) == 1 || sp >= n) { raise_err(err, ERR_DECODE); return NONE; }
+      bool out = false;
+      const uint32_t cc = a.cid(c), ta = a.trep(c, out);
+      const uint32_t drp = rp != NONE ? a.done(rp) : 2u;
+      // member list of c's right-origin group, walked from its top (highest client) down; a group
+      // is anchored at its right-origin sibling (mtail) or, for a right origin outside the group,
+      // at its first member (otail: a member can anchor both kinds)
+      uint32_t m = out ? a.otail(ta) : a.mtail(ta), succ = NONE;
+      if (drp != 2) {  // the right origin is a sibling: place it first
+        if (drp == 1 || sp >= n) { raise_err(err, ERR_DECODE); return NONE; }
         a.set_done(rp, 1);
         stack[sp++] = rp;
         c = rp;
         ++st_dive;
         continue;
       }
-      bool out = false;
-      const uint32_t cc = a.cid(c), ta = a.trep(c, out);
-      // member list of c's right-origin group, walked from its top (highest client) down; a group
-      // is anchored at its right-origin sibling (mtail) or, for a right origin outside the group,
-      // at its first member (otail: a member can anchor both kinds)
-      uint32_t m = out ? a.otail(ta) : a.mtail(ta), succ = NONE;
-      while (m != NONE && a.cid(m) > cc) { succ = m; m = a.mprv(m); ++st_m; }
+      while (m != NONE) {
+        const uint32_t cm = a.cid(m), pm = a.mprv(m);
+        if (cm <= cc) break;
+        succ = m;
+        m = pm;
+        ++st_m;
+      }
       a.set_mprv(c, m);
       if (succ != NONE) a.set_mprv(succ, c);
       else if (out) a.set_otail(ta, c);
       else a.set_mtail(ta, c);
       const uint32_t stop = succ != NONE ? succ : rp;
-      uint32_t left = stop != NONE ? a.prv(stop) : tail;
-      while (left != NONE && a.cid(left) >= cc) { left = a.prv(left); ++st_left; }
+      uint32_t left = stop != NONE ? a.prv(stop) : tail, nx = head;
+      while (left != NONE) {
+        const uint32_t cl = a.cid(left), pl = a.prv(left), nl = a.next(left);
+        if (cl < cc) { nx = nl; break; }
+        left = pl;
+        ++st_left;
+      }
       ++st_place;
-      const uint32_t nx = left != NONE ? a.next(left) : head;
       a.set_prv(c, left);
       a.set_next(c, nx);
       if (left != NONE) a.set_next(left, c); else head = c;
