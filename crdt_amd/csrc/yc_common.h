@@ -89,6 +89,40 @@ __device__ __forceinline__ void block_scan_u32(const uint32_t* in, uint32_t* out
   __syncthreads();
 }
 
+// the same with 64-bit prefixes (the clock-length and client-state scans)
+template <uint32_t LANES>
+__device__ __forceinline__ void block_scan_u32_u64(const uint32_t* in, uint64_t* out, uint32_t n, uint64_t* part) {
+  const uint32_t t = threadIdx.x, per = (n + LANES - 1) / LANES;
+  const uint32_t a = min(n, t * per), b = min(n, a + per);
+  uint64_t sum = 0;
+  for (uint32_t i = a; i < b; ++i) sum += in[i];
+  part[t] = sum;
+  __syncthreads();
+  for (uint32_t off = 1; off < LANES; off <<= 1) {
+    const uint64_t v = t >= off ? part[t - off] : 0ull;
+    __syncthreads();
+    part[t] += v;
+    __syncthreads();
+  }
+  uint64_t run = part[t] - sum;
+  for (uint32_t i = a; i < b; ++i) { const uint32_t x = in[i]; out[i] = run; run += x; }
+  __syncthreads();
+}
+// a phase boundary inside one workgroup where the phase before handed data over through memory-side
+// (L2) atomics as well as plain stores: agent-scope fences on both sides of the barrier, so no
+// wavefront reads an L1 line older than an atomic of the phase before
+__device__ __forceinline__ void phase_sync() {
+  __threadfence();
+  __syncthreads();
+  __threadfence();
+}
+
+// a host switch set to 0 (the small-batch kernels' A/B toggles)
+inline bool env_off(const char* name) {
+  const char* v = getenv(name);
+  return v && v[0] == '0';
+}
+
 __device__ __forceinline__ void raise_err(uint32_t* err, uint32_t code) {
   atomicCAS(err, 0u, code);
 }

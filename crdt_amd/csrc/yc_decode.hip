@@ -2879,9 +2879,7 @@ void launch_json_structs(const Work& w, uint32_t nstructs, hipStream_t s) {
 
 // Clocks from the section start and the length prefix; with `states` (integrate mode) also the
 // client states (k_states' work, folded in: the clock and length are in registers here)
-__global__ void k_struct_clock(Work w, uint32_t nstructs, uint32_t states) {
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= nstructs) return;
+__device__ __forceinline__ void struct_clock_at(const Work& w, uint32_t i, uint32_t nstructs, uint32_t states) {
   const uint32_t si = w.s_sec[i];
   const Section sec = w.sections[si];
   const uint64_t off = w.s_lenscan[i] - w.s_lenscan[sec.first_idx];
@@ -2900,6 +2898,10 @@ __global__ void k_struct_clock(Work w, uint32_t nstructs, uint32_t states) {
   const bool last = i + 1 == nstructs || w.s_sec[i + 1] != si || (w.s_info[i + 1] & 31u) == REF_SKIP;
   if (last) atomicMax(&w.cl_state[w.s_cidx[i]], (uint32_t)endc);
 }
+__global__ void k_struct_clock(Work w, uint32_t nstructs, uint32_t states) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < nstructs) struct_clock_at(w, i, nstructs, states);
+}
 
 void launch_struct_decode(const Work& w, uint32_t nstructs, hipStream_t s) {
   if (!nstructs) return;
@@ -2912,13 +2914,15 @@ void launch_struct_lenscan(const Work& w, uint32_t nstructs, hipStream_t s) {
 
 // --------------------------------------------------------------------------- client states
 // Yjs pending structs (yc_ingest.h): every client is integrated up to its cap only
-__global__ void k_apply_caps(Work w) {
-  const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= w.ctr->nclients) return;
+__device__ __forceinline__ void apply_caps_at(const Work& w, uint32_t c) {
   const uint32_t v = w.cl_vals[c];
   const uint32_t i = lower_bound_u32(w.cap_client, w.ncaps, v);
   const uint32_t cap = (i < w.ncaps && w.cap_client[i] == v) ? w.cap_clock[i] : 0u;
   if (w.cl_state[c] > cap) w.cl_state[c] = cap;
+}
+__global__ void k_apply_caps(Work w) {
+  const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c < w.ctr->nclients) apply_caps_at(w, c);
 }
 __global__ void k_state_totals(Work w, uint32_t nstructs) {  // U and Σ input lengths into the counters
   w.ctr->units = w.cl_base[w.ctr->nclients];
@@ -2934,6 +2938,38 @@ void launch_states(const Work& w, uint32_t nstructs, uint32_t nsections, hipStre
   if (w.capped && nsections) hipLaunchKernelGGL(k_apply_caps, dim3(nsections / 256 + 1), dim3(256), 0, s, w);
   scan_u32_to_u64(w.tmp, w.tmp_bytes, w.cl_state, w.cl_base, nsections + 1, s);
   hipLaunchKernelGGL(k_state_totals, dim3(1), dim3(1), 0, s, w, nstructs);
+}
+
+// Small batches (integrate mode): the struct decode (rare contents inline, no deferred pass), the
+// clock-length scan, the clocks and client states, the caps, the state scan and the totals as
+// phases of ONE workgroup — one launch for six.
+constexpr uint32_t DT_LANES = 256, DT_SMALL = 4096;
+__global__ __launch_bounds__(DT_LANES) void k_decode_tail_small(Work w, uint32_t nstructs, uint32_t nsections) {
+  __shared__ __attribute__((aligned(16))) uint32_t win[DT_LANES * SD_STRIDE];
+  __shared__ uint64_t part[DT_LANES];
+  const uint32_t t = threadIdx.x;
+  for (uint32_t i = t; i <= nsections; i += DT_LANES) { w.cl_start[i] = 0; w.cl_state[i] = 0; }
+  for (uint32_t i = t; i < nstructs; i += DT_LANES) struct_decode_one<false>(w, i, win);
+  __syncthreads();
+  block_scan_u32_u64<DT_LANES>(w.s_len, w.s_lenscan, nstructs + 1, part);
+  for (uint32_t i = t; i < nstructs; i += DT_LANES) struct_clock_at(w, i, nstructs, 1u);
+  phase_sync();  // (client states: atomicMax)
+  const uint32_t nclients = w.ctr->nclients;
+  if (w.capped) {
+    for (uint32_t c = t; c < nclients; c += DT_LANES) apply_caps_at(w, c);
+    __syncthreads();
+  }
+  block_scan_u32_u64<DT_LANES>(w.cl_state, w.cl_base, nsections + 1, part);
+  if (t == 0) {  // (k_state_totals)
+    w.ctr->units = w.cl_base[nclients];
+    w.ctr->in_len = w.s_lenscan[nstructs];
+  }
+}
+bool decode_tail_small(const Work& w, uint32_t nstructs, uint32_t nsections, hipStream_t s) {
+  const bool off = env_off("YCRDT_DECODE_SMALL");  // (read per merge: A/B in one process)
+  if (off || !nstructs || nstructs > DT_SMALL || nsections + 1 > DT_LANES * 16) return false;
+  hipLaunchKernelGGL(k_decode_tail_small, dim3(1), dim3(DT_LANES), 0, s, w, nstructs, nsections);
+  return true;
 }
 
 }  // namespace yc

@@ -217,15 +217,12 @@ __device__ __forceinline__ uint32_t encode_struct_general(const Work& w, uint32_
 // the merge flags) records it (o_first, o_cidx) and sizes it, finding the struct's end by stepping
 // over the segments merged into it (usually none); the others zero the size slots past NO, so the
 // scan over NS + 1 entries sees exactly the NO sizes.
-__global__ __launch_bounds__(256) void k_out_sizes(Work w, uint32_t nsegs, uint32_t nclients) {
-  const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
-  if (s > nsegs) return;
-  const uint32_t nout = nsegs ? w.g_outid[nsegs] : 0u;
+__device__ __forceinline__ bool out_sizes_at(const Work& w, uint32_t s, uint32_t nsegs, uint32_t nout) {
   if (s == nsegs) {
     w.o_first[nout] = nsegs;  // sentinel
     w.o_size[nsegs] = 0;
     w.ctr->nout = nout;
-    return;
+    return false;
   }
   const uint32_t o = w.g_outid[s];
   const bool start = !(w.g_flags[s] & SEG_MERGE);
@@ -243,7 +240,13 @@ __global__ __launch_bounds__(256) void k_out_sizes(Work w, uint32_t nsegs, uint3
     w.o_size[o] = sz == ENC_DEFER ? 0u : sz;
     w.o_gen[o] = sz == ENC_DEFER ? 1u : 0u;
   }
-  wave_flag(&w.ctr->pad[6], sz == ENC_DEFER);  // (the general kernels run only when some struct is deferred)
+  return sz == ENC_DEFER;
+}
+__global__ __launch_bounds__(256) void k_out_sizes(Work w, uint32_t nsegs, uint32_t nclients) {
+  const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
+  if (s > nsegs) return;
+  const bool defer = out_sizes_at(w, s, nsegs, nsegs ? w.g_outid[nsegs] : 0u);
+  wave_flag(&w.ctr->pad[6], defer);  // (the general kernels run only when some struct is deferred)
 }
 // the deferred output structs (split, merged or delta-cut ones), sized by the general encoder
 // (a wavefront reads the flags of 1 024 consecutive output structs as 64 quads and skips the whole
@@ -318,10 +321,7 @@ __global__ __launch_bounds__(RUNS_LANES) void k_runs_small(Work w, uint32_t nseg
 // per client: first output struct and first delete-set run, from the boundaries of the (client-
 // sorted) output and run arrays — one parallel pass instead of per-client binary searches, whose
 // ~80 dependent loads per lane made the per-client pass latency-bound
-__global__ void k_client_bounds(Work w, uint32_t nclients, uint32_t nsegs) {
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i > nsegs) return;
-  const uint32_t nout = w.ctr->nout, nruns = w.g_tmp2[nsegs];
+__device__ __forceinline__ void client_bounds_at(const Work& w, uint32_t i, uint32_t nclients, uint32_t nout, uint32_t nruns) {
   if (i <= nout) {
     const int64_t a = i == 0 ? -1 : (int64_t)w.o_cidx[i - 1];
     const int64_t b = i == nout ? (int64_t)nclients : (int64_t)w.o_cidx[i];
@@ -333,16 +333,18 @@ __global__ void k_client_bounds(Work w, uint32_t nclients, uint32_t nsegs) {
     for (int64_t c = a + 1; c <= b; ++c) ccol(w, CC_RUN_LO)[c] = i;
   }
 }
+__global__ void k_client_bounds(Work w, uint32_t nclients, uint32_t nsegs) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i <= nsegs) client_bounds_at(w, i, nclients, w.ctr->nout, w.g_tmp2[nsegs]);
+}
 
-// per client: struct block + delete-set block + state-vector entry sizes
-__global__ void k_client_sizes(Work w, uint32_t nclients, uint32_t nsegs) {
-  const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c > nclients) return;
-  const uint32_t nout = w.ctr->nout, nruns = w.g_tmp2[nsegs];
+// per client: struct block + delete-set block + state-vector entry sizes; returns bit 0: the
+// client's structs are included, 1: it has delete-set runs, 2: a state-vector entry
+__device__ __forceinline__ uint32_t client_sizes_at(const Work& w, uint32_t c, uint32_t nclients) {
   uint32_t* first_out = ccol(w, CC_FIRST_OUT);
   if (c == nclients) {
     ccol(w, CC_BLK)[c] = 0; ccol(w, CC_DSBLK)[c] = 0; ccol(w, CC_SV)[c] = 0;
-    return;
+    return 0u;
   }
   // first output struct of client c and of the next client (outputs are sorted by client)
   const uint32_t fo = first_out[c], eo = first_out[c + 1];
@@ -377,9 +379,15 @@ __global__ void k_client_sizes(Work w, uint32_t nclients, uint32_t nsegs) {
   }
   ccol(w, CC_DSBLK)[c] = dsblk;
   ccol(w, CC_SV)[c] = state ? vu_size(w.cl_vals[c]) + vu_size(state) : 0;
-  wave_count_add(&w.ctr->pad[0], incl);        // included clients
-  wave_count_add(&w.ctr->pad[1], nr != 0);     // ds clients
-  wave_count_add(&w.ctr->pad[2], state != 0);  // sv entries
+  return (incl ? 1u : 0u) | (nr ? 2u : 0u) | (state ? 4u : 0u);
+}
+__global__ void k_client_sizes(Work w, uint32_t nclients, uint32_t nsegs) {
+  const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c > nclients) return;
+  const uint32_t m = client_sizes_at(w, c, nclients);
+  wave_count_add(&w.ctr->pad[0], m & 1u);  // included clients
+  wave_count_add(&w.ctr->pad[1], m & 2u);  // ds clients
+  wave_count_add(&w.ctr->pad[2], m & 4u);  // sv entries
 }
 
 // reverse the three per-client size columns (structs, delete set, state vector) so that ascending
@@ -439,9 +447,7 @@ __global__ __launch_bounds__(256) void k_write_general(Work w, uint32_t nclients
     if (w.o_size[o]) encode_struct_general<true>(w, nclients, w.o_first[o], w.o_first[o + 1], w.out, out_pos(w, o));
   });
 }
-__global__ void k_write_clients(Work w, uint32_t nclients) {
-  const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (w.ctr->pad[5]) return;
+__device__ __forceinline__ void write_clients_at(const Work& w, uint32_t c, uint32_t nclients) {
   if (c == 0) {
     wr_vu(w.out, (uint64_t)0, w.ctr->pad[0]);
     wr_vu(w.out, (uint64_t)w.ctr->ds_base, w.ctr->pad[1]);
@@ -467,9 +473,11 @@ __global__ void k_write_clients(Work w, uint32_t nclients) {
     wr_vu(w.sv_out, p, w.cl_state[c]);
   }
 }
-__global__ void k_write_runs(Work w, uint32_t nsegs) {
-  const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
-  if (r >= w.g_tmp2[nsegs] || w.ctr->pad[5]) return;
+__global__ void k_write_clients(Work w, uint32_t nclients) {
+  const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (!w.ctr->pad[5]) write_clients_at(w, c, nclients);
+}
+__device__ __forceinline__ void write_runs_at(const Work& w, uint32_t r) {
   const uint32_t s = w.r_seg[r];
   const uint32_t c = w.g_cidx[s];
   const uint32_t first = ccol(w, CC_FIRST_RUN)[c];
@@ -479,14 +487,18 @@ __global__ void k_write_runs(Work w, uint32_t nsegs) {
   p = wr_vu(w.out, p, (uint32_t)(seg_start(w, s) - w.cl_base[c]));
   wr_vu(w.out, p, w.r_len[r]);
 }
+__global__ void k_write_runs(Work w, uint32_t nsegs) {
+  const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r < w.g_tmp2[nsegs] && !w.ctr->pad[5]) write_runs_at(w, r);
+}
 
 // Small client tables (the per-op path, one document): the reverse, the three scans, the
 // unreverse and the totals in ONE workgroup and one launch (six launches otherwise). Each scan:
 // a lane sums a contiguous run of the emit-order sizes, the run sums are scanned in LDS, each lane
 // writes its run's prefixes into the scan column; then every client reads its slot's prefix.
 constexpr uint32_t LAYOUT_LANES = 1024, LAYOUT_SMALL = LAYOUT_LANES * 16;
-__global__ __launch_bounds__(LAYOUT_LANES) void k_layout_small(Work w, uint32_t nclients) {
-  __shared__ uint64_t part[LAYOUT_LANES];
+template <uint32_t LAYOUT_LANES>
+__device__ __forceinline__ void layout_small_body(const Work& w, uint32_t nclients, uint64_t* part) {
   const uint32_t t = threadIdx.x, n = nclients + 1, per = (n + LAYOUT_LANES - 1) / LAYOUT_LANES;
   const uint32_t a = min(n, t * per), b = min(n, a + per);
   const uint32_t src[3] = {CC_BLK, CC_DSBLK, CC_SV}, scol[3] = {CC64_SCAN, CC64_SCAN2, CC64_SCAN3};
@@ -516,6 +528,10 @@ __global__ __launch_bounds__(LAYOUT_LANES) void k_layout_small(Work w, uint32_t 
   __syncthreads();
   if (t == 0) totals_body(w, nclients);  // (k_totals)
 }
+__global__ __launch_bounds__(LAYOUT_LANES) void k_layout_small(Work w, uint32_t nclients) {
+  __shared__ uint64_t part[LAYOUT_LANES];
+  layout_small_body<LAYOUT_LANES>(w, nclients, part);
+}
 
 static void rev_scans(const Work& w, uint32_t nclients, hipStream_t s) {
   if (nclients + 1 <= LAYOUT_SMALL) {  // (k_totals included)
@@ -529,6 +545,78 @@ static void rev_scans(const Work& w, uint32_t nclients, hipStream_t s) {
     scan_u32_to_u64(w.tmp, w.tmp_bytes, w.cc + (size_t)c[0] * (w.cap_clients + 1), w.cc64 + (size_t)c[1] * (w.cap_clients + 1),
                     nclients + 1, s);
   hipLaunchKernelGGL(k_unreverse3, dim3(grid), dim3(256), 0, s, w, nclients);
+}
+
+// Small batches (the per-op path): the whole encode — run starts, fill, sizes and scans, output
+// struct sizes (general ones inline), their scan, client bounds and sizes, layout, totals and every
+// write — as barrier-separated phases of ONE workgroup: one launch where the phases above take
+// twelve (≈4-5 us each at this size). Counters other lanes feed are gathered in LDS, not in the
+// counter words (a relaxed L2 atomic is not seen through another wavefront's L1 line).
+constexpr uint32_t ENC_SMALL_LANES = 512, ENC_SMALL = ENC_SMALL_LANES * 16;
+__global__ __launch_bounds__(ENC_SMALL_LANES) void k_encode_small(Work w, uint32_t nsegs, uint32_t nclients) {
+  __shared__ uint64_t part64[ENC_SMALL_LANES];
+  __shared__ uint32_t cnt[3];
+  if (nsegs == NONE) {  // (a small merge left the count on the device)
+    if (w.ctr->err) return;  // (k_merge_small stopped at an earlier error: nothing to encode)
+    nsegs = w.ctr->nsegs;
+  }
+  uint32_t* part = (uint32_t*)part64;
+  const uint32_t t = threadIdx.x;
+  for (uint32_t i = t; i < 8; i += ENC_SMALL_LANES) w.ctr->pad[i] = 0;
+  for (uint32_t c = t; c <= w.cap_clients; c += ENC_SMALL_LANES) ccol(w, CC_NRUNS)[c] = 0;
+  if (t < 3) cnt[t] = 0;
+  if (!nsegs && t == 0) w.r_size[0] = 0;
+  __syncthreads();
+  // delete-set runs (k_runs_small)
+  block_scan_u32<ENC_SMALL_LANES>(w.r_size, w.g_tmp2, nsegs + 1, part);
+  for (uint32_t s = t; s < nsegs; s += ENC_SMALL_LANES) run_fill_at(w, s, nsegs);
+  __syncthreads();
+  for (uint32_t r = t; r <= nsegs; r += ENC_SMALL_LANES) run_sizes_at(w, r, nsegs);
+  __syncthreads();
+  block_scan_u32<ENC_SMALL_LANES>(w.r_size, w.r_pos, nsegs + 1, part);
+  // output struct sizes (k_out_sizes, k_out_sizes_general)
+  const uint32_t nout = nsegs ? w.g_outid[nsegs] : 0u;
+  for (uint32_t s = t; s <= nsegs; s += ENC_SMALL_LANES) out_sizes_at(w, s, nsegs, nout);
+  __syncthreads();
+  for (uint32_t o = t; o < nout; o += ENC_SMALL_LANES)
+    if (w.o_gen[o]) w.o_size[o] = encode_struct_general<false>(w, nclients, w.o_first[o], w.o_first[o + 1], nullptr, 0);
+  __syncthreads();
+  block_scan_u32<ENC_SMALL_LANES>(w.o_size, w.o_pos, nsegs + 1, part);
+  // per-client bounds and sizes (k_client_bounds, k_client_sizes)
+  const uint32_t nruns = w.g_tmp2[nsegs];
+  for (uint32_t i = t; i <= nsegs; i += ENC_SMALL_LANES) client_bounds_at(w, i, nclients, nout, nruns);
+  __syncthreads();
+  uint32_t m = 0;
+  for (uint32_t c = t; c <= nclients; c += ENC_SMALL_LANES) {
+    const uint32_t x = client_sizes_at(w, c, nclients);
+    m += (x & 1u) | (x & 2u) << 15;
+    if (x & 4u) atomicAdd(&cnt[2], 1u);
+  }
+  if (m & 0xFFFFu) atomicAdd(&cnt[0], m & 0xFFFFu);
+  if (m >> 16) atomicAdd(&cnt[1], m >> 16);
+  __syncthreads();
+  if (t == 0) { w.ctr->pad[0] = cnt[0]; w.ctr->pad[1] = cnt[1]; w.ctr->pad[2] = cnt[2]; }
+  __syncthreads();
+  // layout and totals (k_layout_small)
+  layout_small_body<ENC_SMALL_LANES>(w, nclients, part64);
+  __syncthreads();
+  if (w.ctr->pad[5]) return;  // (past the output bound: k_totals raised the error)
+  // every write (k_write_structs, k_write_general, k_write_clients, k_write_runs)
+  for (uint32_t o = t; o < nout; o += ENC_SMALL_LANES) {
+    if (!w.o_size[o]) continue;
+    if (w.o_gen[o]) encode_struct_general<true>(w, nclients, w.o_first[o], w.o_first[o + 1], w.out, out_pos(w, o));
+    else encode_struct_fast<true>(w, w.o_first[o], w.o_first[o + 1], w.out, out_pos(w, o));
+  }
+  for (uint32_t c = t; c < max(nclients, 1u); c += ENC_SMALL_LANES) write_clients_at(w, c, nclients);
+  for (uint32_t r = t; r < nruns; r += ENC_SMALL_LANES) write_runs_at(w, r);
+}
+bool encode_small_fits(uint64_t nsegs_bound, uint32_t nclients) {
+  const bool off = env_off("YCRDT_ENCODE_SMALL");  // (read per merge: A/B in one process)
+  return !off && nsegs_bound + 1 <= ENC_SMALL && nclients + 1 <= ENC_SMALL;
+}
+// (nsegs: NONE = read on the device)
+void launch_encode_small(const Work& w, uint32_t nsegs, uint32_t nclients, hipStream_t s) {
+  hipLaunchKernelGGL(k_encode_small, dim3(1), dim3(ENC_SMALL_LANES), 0, s, w, nsegs, nclients);
 }
 
 // Phase 1: sizes + layout (ends with out_bytes / sv_bytes in the counters). No host sync: the

@@ -1007,6 +1007,9 @@ int run_decode(ycrdt_engine* e, ycrdt_batch* b, bool lazy, Decoded& D, bool gene
     w.ch_mask = ch_slots - 1;
   }
   mark(e, "decode.structs");  // k_struct_decode alone
+  if (!lazy && decode_tail_small(w, nstructs, nsections, s)) {
+    mark(e, "decode.clocks");  // (one workgroup: structs, clocks, client states, totals)
+  } else {
   launch_struct_decode(w, nstructs, s);
   mark(e, "decode.clocks");
   launch_struct_lenscan(w, nstructs, s);
@@ -1016,6 +1019,7 @@ int run_decode(ycrdt_engine* e, ycrdt_batch* b, bool lazy, Decoded& D, bool gene
   } else {
     HIPCHK(hipMemsetAsync(w.cl_start, 0, sizeof(uint32_t) * (nsections + 1), s));
     launch_struct_clocks(w, nstructs, s);
+  }
   }
   HIPCHK(hipStreamWaitEvent(s, e->side_done, 0));
   rc = check(e, c, "struct decode");
@@ -1166,16 +1170,25 @@ int run_merge(ycrdt_engine* e, ycrdt_batch* b, const std::unordered_map<uint32_t
   if (U || nds) launch_units(w, nstructs, nclients, nds, U, D.ds_big, s);
   mark(e, "merge.segments");
   uint32_t nsegs = 0;
+  // A small map-only merge (the per-op path: no YArray, no right origin, no nested type, one GPU)
+  // runs the integrate phases and the encode as two single-workgroup launches that read the
+  // segment count on the device: no count synchronisation (a ~25 us round trip per merge), the
+  // key table and output sized from the unit count (segments <= units)
+  const bool small = U && !sh && !D.array_roots && !D.any_rorigin && !D.nested && merge_small_fits(U) &&
+                     encode_small_fits(U, nclients) && (uint64_t)b->in_bytes + 48ull * U + 32ull * nclients + 64 <= (uint64_t(1) << 30);
   if (U) {
     launch_segments(w, nclients, U, s);
-    rc = check(e, c, "segments");
-    if (rc) return rc;
-    nsegs = c.nsegs;
+    if (!small) {
+      rc = check(e, c, "segments");
+      if (rc) return rc;
+      nsegs = c.nsegs;
+    }
   }
+  const uint64_t nseg_bound = small ? U : nsegs;
   // keys
   // every list is rooted by an explicit-parent item (a key per root struct at most): the table is
   // sized from those, not from every segment
-  w.cap_keys = next_pow2(std::max<uint64_t>(2ull * std::min<uint64_t>(D.nroots, nsegs), 64));
+  w.cap_keys = next_pow2(std::max<uint64_t>(2ull * std::min<uint64_t>(D.nroots, nseg_bound), 64));
   {  // test hook: keep only the low YCRDT_KEY_HASH_BITS bits of every list hash (collisions certain)
     const int kb = getenv("YCRDT_KEY_HASH_BITS") ? atoi(getenv("YCRDT_KEY_HASH_BITS")) : 64;
     w.key_mask = kb >= 1 && kb < 64 ? (1ull << kb) - 1 : ~0ull;
@@ -1211,7 +1224,11 @@ int run_merge(ycrdt_engine* e, ycrdt_batch* b, const std::unordered_map<uint32_t
   bool runs_scanned = false;  // (k_merge_flags made the delete-set run ids)
   e->nsegs = nsegs;
   e->nlists = 0;
-  if (nsegs) {
+  if (small) {
+    // key table, segment properties, resolution, winners and merge flags (yc_merge.hip k_merge_small)
+    mark(e, "merge.small");
+    launch_merge_small(w, NONE, s);
+  } else if (nsegs) {
     mark(e, "merge.segment_fill");
     launch_segment_props_fill(w, nsegs, s);
     mark(e, "merge.segment_props");  // k_seg_props alone
@@ -1298,8 +1315,8 @@ int run_merge(ycrdt_engine* e, ycrdt_batch* b, const std::unordered_map<uint32_t
   // ---- K7 encode. Output bound: every output struct adds at most 37 bytes of header (info,
   // origin, right origin, parent, length prefix) to content bytes sliced from the input, every
   // delete-set run at most 10, every client block / state-vector entry at most 15 + 10.
-  if (!nsegs) HIPCHK(hipMemsetAsync(&w.ctr->nout, 0, sizeof(uint32_t), s));
-  w.cap_out = (uint64_t)b->in_bytes + 48ull * nsegs + 32ull * nclients + 64;
+  if (!nsegs && !small) HIPCHK(hipMemsetAsync(&w.ctr->nout, 0, sizeof(uint32_t), s));
+  w.cap_out = (uint64_t)b->in_bytes + 48ull * nseg_bound + 32ull * nclients + 64;
   w.cap_sv = 16ull + 10ull * nclients;
   // up to 1 GiB of bound the output is allocated before the sizes are known; past it (a merge of
   // billions of items: the bound is several times the input) after them, exactly (one more sync)
@@ -1307,9 +1324,13 @@ int run_merge(ycrdt_engine* e, ycrdt_batch* b, const std::unordered_map<uint32_t
   if (!exact_out) w.out = take<uint8_t>(V, B_OUT, (size_t)w.cap_out + 16, ok);
   w.sv_out = take<uint8_t>(V, B_SVOUT, (size_t)w.cap_sv + 16, ok);
   if (!ok) return fail(YCRDT_E_DEVICE, oom("output"));
-  uint8_t* tmp2 = take<uint8_t>(V, B_TMP2, prim_tmp_bytes((uint64_t)nsegs + 2, 0), ok);
+  uint8_t* tmp2 = take<uint8_t>(V, B_TMP2, prim_tmp_bytes(nseg_bound + 2, 0), ok);
   if (!ok) return fail(YCRDT_E_DEVICE, oom("scan space"));
   mark(e, "encode.runs");
+  if (small || (!exact_out && encode_small_fits(nsegs, nclients))) {
+    launch_encode_small(w, small ? NONE : nsegs, nclients, s);  // (the whole encode, one workgroup)
+    mark(e, "end");
+  } else {
   launch_encode_sizes(w, nsegs, nclients, s, e->side, e->side_fork, e->side_done, tmp2, V[B_TMP2].cap, runs_scanned);
   mark(e, "encode.sizes");  // k_out_sizes alone
   launch_out_sizes(w, nsegs, nclients, s);
@@ -1327,11 +1348,16 @@ int run_merge(ycrdt_engine* e, ycrdt_batch* b, const std::unordered_map<uint32_t
   mark(e, "encode.write_tail");
   launch_encode_write(w, nsegs, nclients, s);
   mark(e, "end");
+  }
   HIPCHK(hipEventRecord(e->ev1, s));
   if (e->before_final)
     if (const int r = (*e->before_final)(w.cap_out, w.cap_sv)) return r;
   rc = check(e, c, "merge / encode");
   if (rc) return rc;
+  if (small) {
+    nsegs = c.nsegs;
+    e->nsegs = nsegs;
+  }
   nout = nsegs ? c.nout : 0;
   e->out_bytes = c.out_total;
   e->sv_bytes = c.sv_bytes;

@@ -352,9 +352,7 @@ __device__ __forceinline__ uint64_t fnv_u32(uint64_t h, uint32_t v) {
 // YMap entries; every other item inherits the list from its origin (else right origin) by
 // pointer jumping (Item.getMissing, Y@76507). An item whose origin / right origin is GC, or
 // whose parent item is GC, is integrated as GC (getMissing sets parent = null).
-__global__ __launch_bounds__(256) void k_seg_props(Work w, uint32_t nsegs) {
-  const uint32_t s = gidx();
-  if (s >= nsegs) return;
+__device__ __forceinline__ void seg_props_at(const Work& w, uint32_t s) {
   // the source struct's columns in one round of loads (the right-origin clock is unwritten when
   // there is none: read, never used), then the client bases
   const uint32_t g0 = seg_start(w, s);
@@ -443,6 +441,10 @@ __global__ __launch_bounds__(256) void k_seg_props(Work w, uint32_t nsegs) {
   const uint32_t kw = key != NONE && w.s_psub[own] != NONE ? key | KEY_PSUB : key;
   w.g_hop[s] = make_uint4(sf, kw, link, !gc && origin != NONE ? link : NONE);
 }
+__global__ __launch_bounds__(256) void k_seg_props(Work w, uint32_t nsegs) {
+  const uint32_t s = gidx();
+  if (s < nsegs) seg_props_at(w, s);
+}
 
 void launch_segment_props_fill(const Work& w, uint32_t nsegs, hipStream_t s) {
   fill_u32_multi({{(uint32_t*)w.k_hash, (uint64_t)w.cap_keys * 2, 0u},
@@ -465,9 +467,7 @@ void launch_segment_props(const Work& w, uint32_t nsegs, uint32_t nclients, uint
 // (parentSub) or YArray member, and a YMap entry settles its origin's max-client child slot (the
 // second pass of the winner reduction begun in k_seg_props: an atomicMax only where the slot is
 // below itself — segments are numbered in client order, so the max child is the max segment).
-__global__ __launch_bounds__(256) void k_resolve(Work w, uint32_t nsegs) {
-  const uint32_t s = gidx();
-  if (s >= nsegs) return;
+__device__ __forceinline__ bool resolve_at(const Work& w, uint32_t s, uint32_t nsegs) {
   const uint4 h = w.g_hop[s];  // flags, climbing key, link, origin segment
   uint32_t f = h.x;
   uint32_t kv = h.y;
@@ -513,7 +513,12 @@ __global__ __launch_bounds__(256) void k_resolve(Work w, uint32_t nsegs) {
   }
   w.g_flags[s] = f & ~SEG_HASRO;
   w.g_key[s] = (f & SEG_ITEM) && kv != NONE ? kv & ~KEY_PSUB : NONE;
-  wave_flag(&w.ctr->narray, arr);  // read as zero / non-zero (launch_yata)
+  return arr;
+}
+__global__ __launch_bounds__(256) void k_resolve(Work w, uint32_t nsegs) {
+  const uint32_t s = gidx();
+  if (s >= nsegs) return;
+  wave_flag(&w.ctr->narray, resolve_at(w, s, nsegs));  // read as zero / non-zero (launch_yata)
 }
 
 // ---- YMap entries ordered by full YATA (KF_YATA keys). Yjs integrates a map entry's items by the
@@ -584,9 +589,7 @@ uint32_t run_key_resolution(const Work& w, uint32_t nsegs, hipStream_t s) {
 // the key's value is the rightmost entry: descend from the max-client root through the max-client
 // child until a leaf (YATA order of an origin-only tree, SURVEY.md §7 hard part 2)
 // (a descent visits every segment at most once: more hops than segments is a cycle, an error)
-__global__ void k_winner_walk(Work w, uint32_t nsegs) {
-  const uint32_t k = gidx();
-  if (k >= w.cap_keys) return;
+__device__ __forceinline__ void winner_at(const Work& w, uint32_t k, uint32_t nsegs) {
   const uint32_t r = w.k_rootmax[k];
   if (!r) { w.k_winner[k] = NONE; return; }
   if (w.k_flags[k] & KF_YATA) { w.k_winner[k] = NONE; return; }  // ordered by the YATA kernels (k_mapx_fix writes the winner)
@@ -600,6 +603,10 @@ __global__ void k_winner_walk(Work w, uint32_t nsegs) {
   if (!leaf) { raise_err(&w.ctr->err, ERR_DECODE); return; }
   w.k_winner[k] = x;
   w.g_flags[x] |= SEG_WIN;  // one winner per key: the only writer of x's flags in this kernel
+}
+__global__ void k_winner_walk(Work w, uint32_t nsegs) {
+  const uint32_t k = gidx();
+  if (k < w.cap_keys) winner_at(w, k, nsegs);
 }
 // every entry item but the winner is deleted (overwritten): a flag test, no gather of the key's winner
 __global__ void k_overwrite(Work w, uint32_t nsegs) {
@@ -852,6 +859,57 @@ void launch_merge_tail(const Work& w, uint32_t nsegs, hipStream_t s) {
 }
 
 // true: the run ids are scanned too (g_tmp2; the encoder skips that scan)
+// Small map-only merges (the per-op path: no YArray, no right origin, no nested type, unsharded):
+// the key table fill, segment properties, key resolution, winner descent and merge flags with
+// their scans as barrier-separated phases of ONE workgroup — one launch for six. The phases hand
+// over through atomics (the key table, the winner slots) as well as plain stores (phase_sync).
+constexpr uint32_t MS_LANES = 512, MS_SMALL = MS_LANES * 8;
+// nsegs == NONE: the segment count is read on the device (k_segments_small wrote it; the host
+// skipped the count synchronisation)
+__global__ __launch_bounds__(MS_LANES) void k_merge_small(Work w, uint32_t nsegs) {
+  __shared__ uint32_t part[MS_LANES];
+  __shared__ uint32_t sarr;
+  // an error raised before (the unit passes: a missing dependency, a malformed reference) ends the
+  // merge here, as the count synchronisation's check does on the other path: past it the unit
+  // references are not bounded
+  if (w.ctr->err) return;
+  if (nsegs == NONE) nsegs = w.ctr->nsegs;
+  const uint32_t t = threadIdx.x, ck = w.cap_keys;
+  if (t == 0) sarr = 0;
+  for (uint32_t i = t; i < 2 * ck; i += MS_LANES) ((uint32_t*)w.k_hash)[i] = 0;
+  for (uint32_t i = t; i < ck; i += MS_LANES) { w.k_rootmax[i] = 0; w.k_flags[i] = 0; w.k_parent[i] = NONE; }
+  for (uint32_t i = t; i < nsegs; i += MS_LANES) w.g_maxchild[i] = 0;
+  phase_sync();
+  for (uint32_t i = t; i < nsegs; i += MS_LANES) seg_props_at(w, i);
+  phase_sync();
+  bool arr = false;
+  for (uint32_t i = t; i < nsegs; i += MS_LANES) arr |= resolve_at(w, i, nsegs);
+  if (arr) sarr = 1u;
+  phase_sync();
+  if (t == 0 && sarr) w.ctr->narray = 1u;
+  for (uint32_t k = t; k < ck; k += MS_LANES) winner_at(w, k, nsegs);
+  phase_sync();
+  // merge flags (fold: no dead-type pass), then the output struct ids and the run starts' scan
+  // input, as k_merge_flags + its scan
+  for (uint32_t i = t; i <= nsegs; i += MS_LANES) {
+    if (i == nsegs) { w.g_tmp[i] = 0; w.r_size[i] = 0; continue; }
+    bool start, rstart;
+    merge_flags_at(w, i, 1u, start, rstart);
+    w.g_tmp[i] = start ? 1u : 0u;
+    w.r_size[i] = rstart ? 1u : 0u;
+  }
+  __syncthreads();
+  block_scan_u32<MS_LANES>(w.g_tmp, w.g_outid, nsegs + 1, part);
+}
+bool merge_small_fits(uint64_t nsegs_bound) {
+  const bool off = env_off("YCRDT_MERGE_SMALL");  // (read per merge: A/B in one process)
+  return !off && nsegs_bound && nsegs_bound <= MS_SMALL && encode_runs_small((uint32_t)nsegs_bound);
+}
+// (nsegs: NONE = read on the device, at most nsegs_bound)
+void launch_merge_small(const Work& w, uint32_t nsegs, hipStream_t s) {
+  hipLaunchKernelGGL(k_merge_small, dim3(1), dim3(MS_LANES), 0, s, w, nsegs);
+}
+
 bool launch_merge_flags(const Work& w, uint32_t nsegs, hipStream_t s, bool fold) {
   if (!nsegs) return false;
   const uint32_t tiles = (nsegs + 1 + MF_TILE - 1) / MF_TILE;

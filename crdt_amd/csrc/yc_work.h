@@ -673,6 +673,7 @@ void launch_section_clients(const Work& w, uint32_t nsections, hipStream_t s);
 void launch_client_table(Work& w, uint32_t nsections, hipStream_t s);
 void launch_struct_decode(const Work& w, uint32_t nstructs, hipStream_t s);
 void launch_struct_lenscan(const Work& w, uint32_t nstructs, hipStream_t s);
+bool decode_tail_small(const Work& w, uint32_t nstructs, uint32_t nsections, hipStream_t s);  // one workgroup: structs .. client states (small, integrate)
 void launch_json_structs(const Work& w, uint32_t nstructs, hipStream_t s);  // JSON.parse of JSON-like contents
 void launch_states(const Work& w, uint32_t nstructs, uint32_t nsections, hipStream_t s);  // clocks + client states
 void launch_struct_clocks(const Work& w, uint32_t nstructs, hipStream_t s);               // clocks only (lazy)
@@ -687,6 +688,8 @@ uint32_t run_key_resolution(const Work& w, uint32_t nsegs, hipStream_t s);
 uint32_t run_descent(const Work& w, uint32_t nsegs, hipStream_t s, bool fold_overwrite);
 void launch_mapx_flip(const Work& w, uint32_t nsegs, hipStream_t s);  // full-YATA map entries -> the YATA kernels
 void launch_mapx_fix(const Work& w, uint32_t nsegs, hipStream_t s);   // ... and back: the last one wins
+bool merge_small_fits(uint64_t nsegs_bound);  // map-only small merges: one workgroup (k_merge_small)
+void launch_merge_small(const Work& w, uint32_t nsegs, hipStream_t s);  // nsegs NONE: read on the device
 bool launch_merge_flags(const Work& w, uint32_t nsegs, hipStream_t s, bool fold_overwrite);  // true: run ids scanned too
 bool encode_runs_small(uint32_t nsegs);  // the one-workgroup delete-set runs (k_runs_small)
 void launch_merge_flags_only(const Work& w, uint32_t nsegs, hipStream_t s, bool fold_overwrite);
@@ -710,6 +713,8 @@ void launch_out_sizes(const Work& w, uint32_t nsegs, uint32_t nclients, hipStrea
 void launch_encode_layout(const Work& w, uint32_t nsegs, uint32_t nclients, hipStream_t s, hipEvent_t ev_join);
 void launch_encode_write(const Work& w, uint32_t nsegs, uint32_t nclients, hipStream_t s);
 void launch_write_structs(const Work& w, uint32_t nsegs, uint32_t nclients, hipStream_t s);
+bool encode_small_fits(uint64_t nsegs_bound, uint32_t nclients);  // the whole encode, one workgroup (small batches)
+void launch_encode_small(const Work& w, uint32_t nsegs, uint32_t nclients, hipStream_t s);  // nsegs NONE: read on the device
 
 // rocPRIM wrappers (yc_prims.hip)
 size_t prim_tmp_bytes(uint64_t scan_n, uint64_t sort_n);  // scratch for scans of scan_n / sorts of sort_n items
