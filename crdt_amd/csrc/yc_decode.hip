@@ -2538,9 +2538,7 @@ void launch_ds_grid(const Work& w, hipStream_t s) {
   hipLaunchKernelGGL(k_dsp_ranges, dim3(DSP_GRID), dim3(256), 0, s, w);
 }
 
-__global__ void k_ds_bound(Work w) {  // region size per update: (delete-set bytes + 1) / 2
-  const uint32_t u = blockIdx.x * blockDim.x + threadIdx.x;
-  if (u > w.nupd) return;
+__device__ __forceinline__ void ds_bound_at(const Work& w, uint32_t u) {  // region size per update: (delete-set bytes + 1) / 2
   if (u == w.nupd) {
     w.scratch[u] = 0; w.ds_count[u] = 0;
     w.ctr->nstructs = w.wcnt[(w.nbytes + 63) / 64];  // launch_struct_count's total (no copy launch)
@@ -2563,6 +2561,10 @@ __global__ void k_ds_bound(Work w) {  // region size per update: (delete-set byt
     for (uint32_t j = i + 1; j < b; ++j)
       if (w.sections[j].client == w.sections[i].client) { w.sections[i].pad = 1; break; }
 }
+__global__ void k_ds_bound(Work w) {
+  const uint32_t u = blockIdx.x * blockDim.x + threadIdx.x;
+  if (u <= w.nupd) ds_bound_at(w, u);
+}
 __global__ void k_ds_compact(Work w) {  // one wave per update: region -> dense ds[]
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t u = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
@@ -2578,6 +2580,40 @@ void launch_ds_bound(const Work& w, hipStream_t s) {
   hipLaunchKernelGGL(k_ds_bound, dim3(w.nupd / 256 + 1), dim3(256), 0, s, w);
   scan_u32(w.tmp, w.tmp_bytes, w.scratch, w.ds_region, w.nupd + 1, s);
   hipMemcpyAsync(&w.ctr->ds_region, w.ds_region + w.nupd, sizeof(uint32_t), hipMemcpyDeviceToDevice, s);
+}
+// Small batches: the struct / section-start counts (k_count_small), the delete-set region bounds
+// and their scan, and the region total, in ONE workgroup launch (four launches otherwise)
+__global__ __launch_bounds__(COUNT_LANES) void k_count_ds_small(Work w, uint32_t nwords) {
+  __shared__ uint32_t part[COUNT_LANES];
+  const uint32_t t = threadIdx.x, n = nwords + 1, per = (n + COUNT_LANES - 1) / COUNT_LANES;
+  const uint32_t a = min(n, t * per), e = min(n, a + per);
+  for (int k = 0; k < 2; ++k) {
+    const uint64_t* bits = k ? w.sec_bits : w.final_bits;
+    uint32_t* out = k ? w.wsec : w.wcnt;
+    uint32_t sum = 0;
+    for (uint32_t i = a; i < e; ++i) sum += i < nwords ? (uint32_t)__popcll(bits[i]) : 0u;
+    part[t] = sum;
+    __syncthreads();
+    for (uint32_t off = 1; off < COUNT_LANES; off <<= 1) {
+      const uint32_t v = t >= off ? part[t - off] : 0u;
+      __syncthreads();
+      part[t] += v;
+      __syncthreads();
+    }
+    uint32_t run = part[t] - sum;
+    for (uint32_t i = a; i < e; ++i) { out[i] = run; run += i < nwords ? (uint32_t)__popcll(bits[i]) : 0u; }
+    __syncthreads();
+  }
+  for (uint32_t u = t; u <= w.nupd; u += COUNT_LANES) ds_bound_at(w, u);
+  __syncthreads();
+  block_scan_u32<COUNT_LANES>(w.scratch, w.ds_region, w.nupd + 1, part);
+  if (t == 0) w.ctr->ds_region = w.ds_region[w.nupd];
+}
+bool count_ds_small(const Work& w, hipStream_t s) {
+  const uint32_t nwords = (w.nbytes + 63) / 64;
+  if (env_off("YCRDT_DECODE_SMALL") || !w.nupd || nwords + 1 > COUNT_SMALL || w.nupd + 1 > COUNT_SMALL) return false;
+  hipLaunchKernelGGL(k_count_ds_small, dim3(1), dim3(COUNT_LANES), 0, s, w, nwords);
+  return true;
 }
 // the integrate path reads the ranges in their per-update regions (k_ds_apply); mergeUpdates /
 // diffUpdate (lazy) sort them, so there they are compacted into the dense table

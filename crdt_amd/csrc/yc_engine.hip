@@ -909,8 +909,10 @@ int run_decode(ycrdt_engine* e, ycrdt_batch* b, bool lazy, Decoded& D, bool gene
     if (rc0) return rc0;
   }
   mark(e, "decode.bitmap");
-  launch_struct_count(w, s);
-  launch_ds_bound(w, s);
+  if (!count_ds_small(w, s)) {  // (small batches: one workgroup)
+    launch_struct_count(w, s);
+    launch_ds_bound(w, s);
+  }
   if (!w.nupd) HIPCHK(hipMemcpyAsync(&w.ctr->nstructs, w.wcnt + (w.nbytes + 63) / 64, sizeof(uint32_t), hipMemcpyDeviceToDevice, s));
   Counters c;
   int rc = check(e, c, "decode");

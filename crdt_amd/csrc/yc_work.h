@@ -668,6 +668,7 @@ void launch_client_hash(const Work& w, uint64_t* key, uint32_t* val, uint32_t ma
 void launch_struct_count(const Work& w, hipStream_t s);
 void launch_struct_scatter(const Work& w, hipStream_t s);
 void launch_ds_bound(const Work& w, hipStream_t s);
+bool count_ds_small(const Work& w, hipStream_t s);  // counts + delete-set bounds in one workgroup (small batches)
 void launch_ds_decode(const Work& w, hipStream_t s);
 void launch_section_clients(const Work& w, uint32_t nsections, hipStream_t s);
 void launch_client_table(Work& w, uint32_t nsections, hipStream_t s);
