@@ -2152,9 +2152,7 @@ __global__ __launch_bounds__(256) void k_scatter_pos(const uint64_t* __restrict_
 __device__ __forceinline__ uint32_t rank_incl(const uint64_t* __restrict__ bits, const uint32_t* __restrict__ pre, uint32_t p) {
   return pre[p >> 6] + (uint32_t)__popcll(bits[p >> 6] & (((2ull << (p & 63)) - 1)));  // bits <= p
 }
-__global__ void k_section_rank(Work w, uint32_t nsections) {
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= nsections) return;
+__device__ __forceinline__ void section_rank_at(const Work& w, uint32_t i) {
   Section* sec = &w.sections[i];
   if (sec->n == 0) return;
   const uint32_t p = sec->first_pos, uw = upd_win(w, sec->upd);  // (bitmap words and prefixes of its window)
@@ -2166,6 +2164,10 @@ __global__ void k_section_rank(Work w, uint32_t nsections) {
   // per struct than update -> offsets)
   w.sec_uend[i] = w.uoff[sec->upd] + w.ulen[sec->upd];
   w.sec_doc[i] = doc_of_update(w, sec->upd);
+}
+__global__ void k_section_rank(Work w, uint32_t nsections) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < nsections) section_rank_at(w, i);
 }
 // Small batches: both popcount prefixes in one workgroup and one launch (four launches otherwise):
 // a lane sums the popcounts of a contiguous run of words, the run sums are scanned in LDS, each
@@ -2680,9 +2682,7 @@ __global__ void k_section_cidx_multi(Work w, uint32_t n) {
 // (seven otherwise): the sections' clients sorted in LDS (bitonic), the distinct ones numbered by a
 // scan of the run-start flags, then every section's client index by binary search in LDS.
 constexpr uint32_t CT_LANES = 1024, CT_SMALL = 2048;
-__global__ __launch_bounds__(CT_LANES) void k_client_table_small(Work w, uint32_t n) {
-  __shared__ uint32_t v[CT_SMALL], pre[CT_SMALL + 1], u[CT_SMALL];
-  __shared__ uint32_t part[CT_LANES];
+__device__ __forceinline__ void client_table_small_body(const Work& w, uint32_t n, uint32_t* v, uint32_t* pre, uint32_t* u, uint32_t* part) {
   const uint32_t t = threadIdx.x;
   uint32_t N = 1;
   while (N < n) N <<= 1;
@@ -2731,6 +2731,11 @@ __global__ __launch_bounds__(CT_LANES) void k_client_table_small(Work w, uint32_
     w.sections[i].cidx = lo;
   }
 }
+__global__ __launch_bounds__(CT_LANES) void k_client_table_small(Work w, uint32_t n) {
+  __shared__ uint32_t v[CT_SMALL], pre[CT_SMALL + 1], u[CT_SMALL];
+  __shared__ uint32_t part[CT_LANES];
+  client_table_small_body(w, n, v, pre, u, part);
+}
 
 // NC stays on the device (ctr->nclients) until the struct-decode counter read
 void launch_client_table(Work& w, uint32_t nsections, hipStream_t s) {
@@ -2773,6 +2778,31 @@ __global__ void k_client_hash(Work w, uint64_t* __restrict__ key, uint32_t* __re
 }
 void launch_client_hash(const Work& w, uint64_t* key, uint32_t* val, uint32_t mask, hipStream_t s) {
   hipLaunchKernelGGL(k_client_hash, dim3((mask + 1) / 512 + 1), dim3(256), 0, s, w, key, val, mask);
+}
+// Small single-document batches: the section ranks, the client table and the client hash (its
+// fill included) as phases of ONE workgroup (four launches otherwise)
+__global__ __launch_bounds__(CT_LANES) void k_sections_small(Work w, uint32_t n, uint64_t* __restrict__ key, uint32_t* __restrict__ val,
+                                                             uint32_t mask) {
+  __shared__ uint32_t v[CT_SMALL], pre[CT_SMALL + 1], u[CT_SMALL];
+  __shared__ uint32_t part[CT_LANES];
+  const uint32_t t = threadIdx.x;
+  for (uint32_t i = t; i < n; i += CT_LANES) section_rank_at(w, i);
+  for (uint32_t i = t; i <= mask; i += CT_LANES) key[i] = ~0ull;
+  client_table_small_body(w, n, v, pre, u, part);  // (ends with the sections' client indexes)
+  phase_sync();  // (the key fill, plain stores, before the atomics below)
+  const uint32_t nc = w.ctr->nclients;
+  for (uint32_t i = t; i < nc; i += CT_LANES) {
+    const uint64_t k = (uint64_t)w.cl_vals[i];
+    for (uint32_t slot = (uint32_t)client_hash(k) & mask;; slot = (slot + 1) & mask) {
+      const unsigned long long old = atomicCAS((unsigned long long*)&key[slot], ~0ull, (unsigned long long)k);
+      if (old == ~0ull || old == k) { val[slot] = i; break; }  // keys are distinct
+    }
+  }
+}
+bool sections_small(const Work& w, uint32_t nsections, uint64_t* key, uint32_t* val, uint32_t mask, hipStream_t s) {
+  if (env_off("YCRDT_DECODE_SMALL") || w.udoc || !nsections || nsections > CT_SMALL || mask + 1 > 4 * CT_SMALL) return false;
+  hipLaunchKernelGGL(k_sections_small, dim3(1), dim3(CT_LANES), 0, s, w, nsections, key, val, mask);
+  return true;
 }
 
 // --------------------------------------------------------------------------- 6. struct decode

@@ -972,7 +972,9 @@ int run_decode(ycrdt_engine* e, ycrdt_batch* b, bool lazy, Decoded& D, bool gene
   w.cl_start = take<uint32_t>(V, B_CLSTART, w.cap_clients + 1, ok);
   if (!ok) return fail(YCRDT_E_DEVICE, oom("struct table"));
   launch_struct_scatter(w, s);
-  launch_section_clients(w, nsections, s);
+  // small single-document batches: section ranks, client table and client hash in one launch
+  const bool sec_small = !w.udoc && nsections && nsections <= 2048 && ch_slots <= 8192 && !env_off("YCRDT_DECODE_SMALL");
+  if (!sec_small) launch_section_clients(w, nsections, s);
   mark(e, "decode.sections");
   {  // the delete sets decode on the side stream (own scratch / scan space) while the client
      // table and the struct table are built; both streams only read what the sync above published
@@ -1000,7 +1002,12 @@ int run_decode(ycrdt_engine* e, ycrdt_batch* b, bool lazy, Decoded& D, bool gene
     launch_ds_decode(wd, e->side);
     HIPCHK(hipEventRecord(e->side_done, e->side));
   }
-  if (nsections) {
+  if (sec_small) {
+    if (!sections_small(w, nsections, ch_key, ch_val, ch_slots - 1, s)) return fail(YCRDT_E_DEVICE, "small section pass refused");
+    w.ch_key = ch_key;
+    w.ch_val = ch_val;
+    w.ch_mask = ch_slots - 1;
+  } else if (nsections) {
     launch_client_table(w, nsections, s);
     fill_u32_multi({{(uint32_t*)ch_key, 2ull * ch_slots, 0xFFFFFFFFu}}, s);
     launch_client_hash(w, ch_key, ch_val, ch_slots - 1, s);

@@ -75,10 +75,7 @@ __global__ void k_vrep(Work w, uint32_t nsegs, const uint32_t* __restrict__ kmap
   if (k != NONE && kmap[k] != NONE) atomicMin(&krep[k], s);
 }
 
-__global__ void k_vkey_fill(Work w, const uint32_t* __restrict__ krep, ViewKey* __restrict__ keys,
-                            const uint32_t* __restrict__ nkeys) {
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= *nkeys) return;
+__device__ __forceinline__ void vkey_fill_at(const Work& w, const uint32_t* __restrict__ krep, ViewKey* __restrict__ keys, uint32_t i) {
   ViewKey& K = keys[i];
   const uint32_t k = K.slot;
   K.flags = (w.k_flags[k] & KF_PSUB) ? VK_PSUB : 0u;
@@ -101,6 +98,40 @@ __global__ void k_vkey_fill(Work w, const uint32_t* __restrict__ krep, ViewKey* 
     const uint32_t s = w.k_winner[k];
     if (s != NONE) fill_seg(w, s, true, K.win);
   }
+}
+__global__ void k_vkey_fill(Work w, const uint32_t* __restrict__ krep, ViewKey* __restrict__ keys,
+                            const uint32_t* __restrict__ nkeys) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < *nkeys) vkey_fill_at(w, krep, keys, i);
+}
+// A small view with no YArray list (the per-op path's map doc): the key compaction, the root
+// members and the key records as phases of ONE workgroup (a fill and three launches otherwise)
+constexpr uint32_t VS_LANES = 512, VS_SMALL = VS_LANES * 16;
+__global__ __launch_bounds__(VS_LANES) void k_view_small(Work w, uint32_t nsegs, uint32_t* __restrict__ kmap, uint32_t* __restrict__ krep,
+                                                         ViewKey* __restrict__ keys, uint32_t* __restrict__ nkeys) {
+  __shared__ uint32_t n;
+  const uint32_t t = threadIdx.x;
+  if (t == 0) n = 0;
+  __syncthreads();
+  for (uint32_t k = t; k < w.cap_keys; k += VS_LANES) {
+    krep[k] = NONE;
+    kmap[k] = NONE;
+    if (w.k_hash[k] == 0 || (w.k_flags[k] & KF_DEAD)) continue;
+    const uint32_t i = atomicAdd(&n, 1u);
+    kmap[k] = i;
+    keys[i].slot = k;
+  }
+  __syncthreads();
+  for (uint32_t s = t; s < nsegs; s += VS_LANES) {
+    const uint32_t f = w.g_flags[s];
+    if (!(f & SEG_ROOT) || !(f & SEG_ITEM)) continue;
+    const uint32_t k = w.g_key[s];
+    if (k != NONE && kmap[k] != NONE) atomicMin(&krep[k], s);
+  }
+  phase_sync();  // (krep: atomicMin)
+  const uint32_t nk = n;
+  if (t == 0) *nkeys = nk;
+  for (uint32_t i = t; i < nk; i += VS_LANES) vkey_fill_at(w, krep, keys, i);
 }
 
 // ---- YArray list ranking. Positions i index the (list, segment)-sorted member array y_seg.
@@ -153,6 +184,10 @@ __global__ void k_vseg_fill(Work w, uint32_t narr, const uint32_t* __restrict__ 
 }
 
 void launch_view(const Work& w, const ViewBufs& v, uint32_t nsegs, uint32_t nlists, uint32_t narr, hipStream_t s) {
+  if ((!nlists || !narr) && w.cap_keys <= VS_SMALL && nsegs <= VS_SMALL && !env_off("YCRDT_VIEW_SMALL")) {
+    hipLaunchKernelGGL(k_view_small, dim3(1), dim3(VS_LANES), 0, s, w, nsegs, v.kmap, v.krep, v.keys, v.nkeys);
+    return;
+  }
   hipMemsetAsync(v.nkeys, 0, sizeof(uint32_t), s);
   hipLaunchKernelGGL(k_vkeys, dim3(w.cap_keys / 256 + 1), dim3(256), 0, s, w, v.kmap, v.krep, v.keys, v.nkeys);
   if (nsegs) hipLaunchKernelGGL(k_vrep, dim3(nsegs / 256 + 1), dim3(256), 0, s, w, nsegs, v.kmap, v.krep);

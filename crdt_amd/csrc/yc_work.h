@@ -665,6 +665,7 @@ void launch_chunks(const Work& w, hipStream_t s);  // k_spec + k_walk: large upd
 void launch_direct(const Work& w, hipStream_t s);  // k_direct: small updates
 bool wave_decode(const Work& w);                  // few small updates: k_wlen + k_wrank (else k_direct)
 void launch_client_hash(const Work& w, uint64_t* key, uint32_t* val, uint32_t mask, hipStream_t s);
+bool sections_small(const Work& w, uint32_t nsections, uint64_t* key, uint32_t* val, uint32_t mask, hipStream_t s);  // ranks + client table + hash, one workgroup
 void launch_struct_count(const Work& w, hipStream_t s);
 void launch_struct_scatter(const Work& w, hipStream_t s);
 void launch_ds_bound(const Work& w, hipStream_t s);

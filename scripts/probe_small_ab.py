@@ -10,7 +10,7 @@ import crdt_amd  # noqa: E402
 MODES = {
     "all_on": {},
     "merge_off": {"YCRDT_MERGE_SMALL": "0"},
-    "all_off": {"YCRDT_MERGE_SMALL": "0", "YCRDT_ENCODE_SMALL": "0", "YCRDT_DECODE_SMALL": "0"},
+    "all_off": {"YCRDT_MERGE_SMALL": "0", "YCRDT_ENCODE_SMALL": "0", "YCRDT_DECODE_SMALL": "0", "YCRDT_VIEW_SMALL": "0"},
 }
 bench._yjs_perop = lambda n: None  # (the Yjs leg is not compared here)
 eng = crdt_amd.Engine()
@@ -18,7 +18,7 @@ bench.per_op_leg(eng, (100,))  # warm-up
 res = {m: [] for m in MODES}
 for rnd in range(int(sys.argv[1]) if len(sys.argv) > 1 else 3):
     for m, env in MODES.items():
-        for k in ("YCRDT_MERGE_SMALL", "YCRDT_ENCODE_SMALL", "YCRDT_DECODE_SMALL"):
+        for k in ("YCRDT_MERGE_SMALL", "YCRDT_ENCODE_SMALL", "YCRDT_DECODE_SMALL", "YCRDT_VIEW_SMALL"):
             os.environ.pop(k, None)
         os.environ.update(env)
         r = bench.per_op_leg(eng, (500,))["500"]
