@@ -1185,13 +1185,11 @@ int run_merge(ycrdt_engine* e, ycrdt_batch* b, const std::unordered_map<uint32_t
   // key table and output sized from the unit count (segments <= units)
   const bool small = U && !sh && !D.array_roots && !D.any_rorigin && !D.nested && merge_small_fits(U) &&
                      encode_small_fits(U, nclients) && (uint64_t)b->in_bytes + 48ull * U + 32ull * nclients + 64 <= (uint64_t(1) << 30);
-  if (U) {
+  if (U && !small) {  // (a small merge cuts its segments in k_merge_small)
     launch_segments(w, nclients, U, s);
-    if (!small) {
-      rc = check(e, c, "segments");
-      if (rc) return rc;
-      nsegs = c.nsegs;
-    }
+    rc = check(e, c, "segments");
+    if (rc) return rc;
+    nsegs = c.nsegs;
   }
   const uint64_t nseg_bound = small ? U : nsegs;
   // keys
@@ -1236,7 +1234,7 @@ int run_merge(ycrdt_engine* e, ycrdt_batch* b, const std::unordered_map<uint32_t
   if (small) {
     // key table, segment properties, resolution, winners and merge flags (yc_merge.hip k_merge_small)
     mark(e, "merge.small");
-    launch_merge_small(w, NONE, s);
+    launch_merge_small(w, NONE, U, s);
   } else if (nsegs) {
     mark(e, "merge.segment_fill");
     launch_segment_props_fill(w, nsegs, s);

@@ -223,8 +223,8 @@ __global__ void k_scatter_seg(Work w, uint32_t nwords, uint64_t nunits) {
 // (up to 16 K units: a unit's cut test gathers several columns, so one workgroup is only worth it
 // while each lane takes a few units — a 900 K-unit C2 document spent 1 ms in it)
 constexpr uint32_t SEG_LANES = 1024, SEG_SMALL_WORDS = 256;
-__global__ __launch_bounds__(SEG_LANES) void k_segments_small(Work w, uint64_t nunits) {
-  __shared__ uint32_t part[SEG_LANES];
+template <uint32_t SEG_LANES>
+__device__ __forceinline__ void segments_small_body(const Work& w, uint64_t nunits, uint32_t* part) {
   const uint32_t nwords = (uint32_t)((nunits + 63) / 64);
   for (uint32_t base = 0; base < nwords * 64; base += SEG_LANES) {
     const uint32_t g = base + threadIdx.x;
@@ -238,6 +238,10 @@ __global__ __launch_bounds__(SEG_LANES) void k_segments_small(Work w, uint64_t n
   __syncthreads();
   block_scan_u32<SEG_LANES>(w.scratch, w.u_wpre, nwords + 1, part);
   for (uint32_t i = threadIdx.x; i < nwords; i += SEG_LANES) scatter_seg_at(w, i, nwords, nunits);
+}
+__global__ __launch_bounds__(SEG_LANES) void k_segments_small(Work w, uint64_t nunits) {
+  __shared__ uint32_t part[SEG_LANES];
+  segments_small_body<SEG_LANES>(w, nunits, part);
 }
 
 // One launch for the three unit passes (they touch disjoint bytes of a unit's flag word: byte 0
@@ -864,16 +868,21 @@ void launch_merge_tail(const Work& w, uint32_t nsegs, hipStream_t s) {
 // their scans as barrier-separated phases of ONE workgroup — one launch for six. The phases hand
 // over through atomics (the key table, the winner slots) as well as plain stores (phase_sync).
 constexpr uint32_t MS_LANES = 512, MS_SMALL = MS_LANES * 8;
-// nsegs == NONE: the segment count is read on the device (k_segments_small wrote it; the host
-// skipped the count synchronisation)
-__global__ __launch_bounds__(MS_LANES) void k_merge_small(Work w, uint32_t nsegs) {
+// nunits != 0: the segment cuts and starts (k_segments_small's work) run here first, and the
+// segment count is read on the device (the host skipped the count synchronisation)
+__global__ __launch_bounds__(MS_LANES) void k_merge_small(Work w, uint32_t nsegs, uint64_t nunits) {
   __shared__ uint32_t part[MS_LANES];
   __shared__ uint32_t sarr;
   // an error raised before (the unit passes: a missing dependency, a malformed reference) ends the
   // merge here, as the count synchronisation's check does on the other path: past it the unit
   // references are not bounded
   if (w.ctr->err) return;
-  if (nsegs == NONE) nsegs = w.ctr->nsegs;
+  if (nunits) {
+    segments_small_body<MS_LANES>(w, nunits, part);
+    phase_sync();  // (ERR_PENDING: an atomic)
+    if (w.ctr->err) return;
+    nsegs = w.ctr->nsegs;
+  }
   const uint32_t t = threadIdx.x, ck = w.cap_keys;
   if (t == 0) sarr = 0;
   for (uint32_t i = t; i < 2 * ck; i += MS_LANES) ((uint32_t*)w.k_hash)[i] = 0;
@@ -903,11 +912,11 @@ __global__ __launch_bounds__(MS_LANES) void k_merge_small(Work w, uint32_t nsegs
 }
 bool merge_small_fits(uint64_t nsegs_bound) {
   const bool off = env_off("YCRDT_MERGE_SMALL");  // (read per merge: A/B in one process)
-  return !off && nsegs_bound && nsegs_bound <= MS_SMALL && encode_runs_small((uint32_t)nsegs_bound);
+  return !off && nsegs_bound && nsegs_bound <= MS_SMALL && (nsegs_bound + 63) / 64 <= SEG_SMALL_WORDS && encode_runs_small((uint32_t)nsegs_bound);
 }
-// (nsegs: NONE = read on the device, at most nsegs_bound)
-void launch_merge_small(const Work& w, uint32_t nsegs, hipStream_t s) {
-  hipLaunchKernelGGL(k_merge_small, dim3(1), dim3(MS_LANES), 0, s, w, nsegs);
+// (nunits != 0: the segments too, nsegs read on the device)
+void launch_merge_small(const Work& w, uint32_t nsegs, uint64_t nunits, hipStream_t s) {
+  hipLaunchKernelGGL(k_merge_small, dim3(1), dim3(MS_LANES), 0, s, w, nsegs, nunits);
 }
 
 bool launch_merge_flags(const Work& w, uint32_t nsegs, hipStream_t s, bool fold) {

@@ -691,7 +691,7 @@ uint32_t run_descent(const Work& w, uint32_t nsegs, hipStream_t s, bool fold_ove
 void launch_mapx_flip(const Work& w, uint32_t nsegs, hipStream_t s);  // full-YATA map entries -> the YATA kernels
 void launch_mapx_fix(const Work& w, uint32_t nsegs, hipStream_t s);   // ... and back: the last one wins
 bool merge_small_fits(uint64_t nsegs_bound);  // map-only small merges: one workgroup (k_merge_small)
-void launch_merge_small(const Work& w, uint32_t nsegs, hipStream_t s);  // nsegs NONE: read on the device
+void launch_merge_small(const Work& w, uint32_t nsegs, uint64_t nunits, hipStream_t s);  // nunits != 0: segments too, nsegs on the device
 bool launch_merge_flags(const Work& w, uint32_t nsegs, hipStream_t s, bool fold_overwrite);  // true: run ids scanned too
 bool encode_runs_small(uint32_t nsegs);  // the one-workgroup delete-set runs (k_runs_small)
 void launch_merge_flags_only(const Work& w, uint32_t nsegs, hipStream_t s, bool fold_overwrite);
