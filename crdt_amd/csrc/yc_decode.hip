@@ -2786,6 +2786,12 @@ __global__ __launch_bounds__(CT_LANES) void k_sections_small(Work w, uint32_t n,
   __shared__ uint32_t v[CT_SMALL], pre[CT_SMALL + 1], u[CT_SMALL];
   __shared__ uint32_t part[CT_LANES];
   const uint32_t t = threadIdx.x;
+  if (n == NONE) {  // (the quick decode: no count synchronisation ran, the count is on the device)
+    if (w.ctr->err) return;  // (the walk failed: the sections are not to be read)
+    n = w.ctr->nsections;
+    if (n > CT_SMALL) { if (t == 0) raise_err(&w.ctr->err, ERR_CAPACITY); return; }  // (rerun, counted)
+    if (!n) return;
+  }
   for (uint32_t i = t; i < n; i += CT_LANES) section_rank_at(w, i);
   for (uint32_t i = t; i <= mask; i += CT_LANES) key[i] = ~0ull;
   client_table_small_body(w, n, v, pre, u, part);  // (ends with the sections' client indexes)
@@ -2800,7 +2806,7 @@ __global__ __launch_bounds__(CT_LANES) void k_sections_small(Work w, uint32_t n,
   }
 }
 bool sections_small(const Work& w, uint32_t nsections, uint64_t* key, uint32_t* val, uint32_t mask, hipStream_t s) {
-  if (env_off("YCRDT_DECODE_SMALL") || w.udoc || !nsections || nsections > CT_SMALL || mask + 1 > 4 * CT_SMALL) return false;
+  if (env_off("YCRDT_DECODE_SMALL") || w.udoc || !nsections || (nsections != NONE && nsections > CT_SMALL) || mask + 1 > 16 * CT_SMALL) return false;
   hipLaunchKernelGGL(k_sections_small, dim3(1), dim3(CT_LANES), 0, s, w, nsections, key, val, mask);
   return true;
 }
@@ -3014,6 +3020,12 @@ __global__ __launch_bounds__(DT_LANES) void k_decode_tail_small(Work w, uint32_t
   __shared__ __attribute__((aligned(16))) uint32_t win[DT_LANES * SD_STRIDE];
   __shared__ uint64_t part[DT_LANES];
   const uint32_t t = threadIdx.x;
+  if (nstructs == NONE) {  // (the quick decode: the counts are on the device)
+    if (w.ctr->err) return;
+    nstructs = w.ctr->nstructs;
+    nsections = w.ctr->nsections;
+    if (nstructs > DT_SMALL || nsections + 1 > DT_LANES * 16) { if (t == 0) raise_err(&w.ctr->err, ERR_CAPACITY); return; }
+  }
   for (uint32_t i = t; i <= nsections; i += DT_LANES) { w.cl_start[i] = 0; w.cl_state[i] = 0; }
   for (uint32_t i = t; i < nstructs; i += DT_LANES) struct_decode_one<false>(w, i, win);
   __syncthreads();
@@ -3030,6 +3042,9 @@ __global__ __launch_bounds__(DT_LANES) void k_decode_tail_small(Work w, uint32_t
     w.ctr->units = w.cl_base[nclients];
     w.ctr->in_len = w.s_lenscan[nstructs];
   }
+}
+void launch_decode_tail_small(const Work& w, uint32_t nstructs, uint32_t nsections, hipStream_t s) {
+  hipLaunchKernelGGL(k_decode_tail_small, dim3(1), dim3(DT_LANES), 0, s, w, nstructs, nsections);
 }
 bool decode_tail_small(const Work& w, uint32_t nstructs, uint32_t nsections, hipStream_t s) {
   const bool off = env_off("YCRDT_DECODE_SMALL");  // (read per merge: A/B in one process)

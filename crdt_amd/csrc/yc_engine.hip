@@ -915,7 +915,20 @@ int run_decode(ycrdt_engine* e, ycrdt_batch* b, bool lazy, Decoded& D, bool gene
   }
   if (!w.nupd) HIPCHK(hipMemcpyAsync(&w.ctr->nstructs, w.wcnt + (w.nbytes + 63) / 64, sizeof(uint32_t), hipMemcpyDeviceToDevice, s));
   Counters c;
-  int rc = check(e, c, "decode");
+  // A small single-document integrate batch skips the count synchronisation: the struct, delete-
+  // set and client tables are sized from bounds (a struct starts at a distinct byte; a delete-set
+  // region is at most half its bytes; the sections fit the section table), the single-workgroup
+  // passes read the counts on the device, and one past their sizes raises a capacity error that
+  // reruns the decode the counted way (generous)
+  const bool quick = !lazy && !split && !generous && !w.dbg && !w.udoc && w.nupd && b->nwin <= 1 && w.nbytes <= (64u << 10) && w.cap_sections <= 16000 &&
+                     !env_off("YCRDT_DECODE_SMALL") && !env_off("YCRDT_DECODE_QUICK");
+  int rc = quick ? YCRDT_OK : check(e, c, "decode");
+  if (quick) {
+    c = Counters();
+    c.nstructs = (uint32_t)w.nbytes + 1;
+    c.nsections = w.cap_sections;
+    c.ds_region = (uint32_t)w.nbytes + w.nupd + 1;
+  }
   if (dbg_dec && w.dbg) {  // experiments: why k_fastwalk left large updates to k_walk
     unsigned long long h[24];
     HIPCHK(hipMemcpy(h, w.dbg, sizeof(h), hipMemcpyDeviceToHost));
@@ -930,7 +943,7 @@ int run_decode(ycrdt_engine* e, ycrdt_batch* b, bool lazy, Decoded& D, bool gene
   const uint32_t nstructs = c.nstructs;
   const uint32_t nsections = c.nsections;
   // ---- tables sized from the counts
-  w.cap_structs = nstructs + 64;
+  w.cap_structs = nstructs + 64;  // (quick: the bounds)
   w.cap_ds = c.ds_region + 64;
   w.cap_clients = nsections + 64;
   w.ds = lazy ? take<DsRange>(V, B_DS, w.cap_ds, ok) : nullptr;  // dense ranges: mergeUpdates / diffUpdate only
@@ -973,13 +986,17 @@ int run_decode(ycrdt_engine* e, ycrdt_batch* b, bool lazy, Decoded& D, bool gene
   if (!ok) return fail(YCRDT_E_DEVICE, oom("struct table"));
   launch_struct_scatter(w, s);
   // small single-document batches: section ranks, client table and client hash in one launch
-  const bool sec_small = !w.udoc && nsections && nsections <= 2048 && ch_slots <= 8192 && !env_off("YCRDT_DECODE_SMALL");
+  const bool sec_small = quick || (!w.udoc && nsections && nsections <= 2048 && ch_slots <= 8192 && !env_off("YCRDT_DECODE_SMALL"));
   if (!sec_small) launch_section_clients(w, nsections, s);
   mark(e, "decode.sections");
   {  // the delete sets decode on the side stream (own scratch / scan space) while the client
      // table and the struct table are built; both streams only read what the sync above published
     Work wd = w;
     bool okd = true;
+    if (quick) {  // (no host synchronisation ordered the walk and the bounds before this stream's work)
+      HIPCHK(hipEventRecord(e->side_fork, s));
+      HIPCHK(hipStreamWaitEvent(e->side, e->side_fork, 0));
+    }
     wd.scratch = take<uint32_t>(V, B_SCRATCH2, (uint64_t)w.nupd + 2, okd);
     wd.tmp = take<uint8_t>(V, B_TMP2, prim_tmp_bytes(std::max<uint64_t>((uint64_t)w.nupd + 2, (uint64_t)w.ngroups + 2), 0), okd);
     wd.tmp_bytes = V[B_TMP2].cap;
@@ -1003,7 +1020,7 @@ int run_decode(ycrdt_engine* e, ycrdt_batch* b, bool lazy, Decoded& D, bool gene
     HIPCHK(hipEventRecord(e->side_done, e->side));
   }
   if (sec_small) {
-    if (!sections_small(w, nsections, ch_key, ch_val, ch_slots - 1, s)) return fail(YCRDT_E_DEVICE, "small section pass refused");
+    if (!sections_small(w, quick ? NONE : nsections, ch_key, ch_val, ch_slots - 1, s)) return fail(YCRDT_E_DEVICE, "small section pass refused");
     w.ch_key = ch_key;
     w.ch_val = ch_val;
     w.ch_mask = ch_slots - 1;
@@ -1016,7 +1033,10 @@ int run_decode(ycrdt_engine* e, ycrdt_batch* b, bool lazy, Decoded& D, bool gene
     w.ch_mask = ch_slots - 1;
   }
   mark(e, "decode.structs");  // k_struct_decode alone
-  if (!lazy && decode_tail_small(w, nstructs, nsections, s)) {
+  if (quick) {
+    launch_decode_tail_small(w, NONE, NONE, s);  // (the counts on the device)
+    mark(e, "decode.clocks");
+  } else if (!lazy && decode_tail_small(w, nstructs, nsections, s)) {
     mark(e, "decode.clocks");  // (one workgroup: structs, clocks, client states, totals)
   } else {
   launch_struct_decode(w, nstructs, s);
@@ -1032,9 +1052,11 @@ int run_decode(ycrdt_engine* e, ycrdt_batch* b, bool lazy, Decoded& D, bool gene
   }
   HIPCHK(hipStreamWaitEvent(s, e->side_done, 0));
   rc = check(e, c, "struct decode");
+  if (quick && rc == YCRDT_E_CAPACITY) return run_decode(e, b, lazy, D, true, sh);  // past a small pass's size
   if (rc) return rc;
+  const uint32_t nstructs_q = quick ? c.nstructs : nstructs, nsections_q = quick ? c.nsections : nsections;
   if (c.any_json) {  // ContentJSON / Embed / Format values: JSON.parse (rare: one more pass and sync)
-    launch_json_structs(w, nstructs, s);
+    launch_json_structs(w, nstructs_q, s);
     rc = check(e, c, "JSON values");
     if (rc) return rc;
   }
@@ -1049,8 +1071,8 @@ int run_decode(ycrdt_engine* e, ycrdt_batch* b, bool lazy, Decoded& D, bool gene
   D.nroots = 0;
   for (uint32_t k = 0; k < NSHARD; ++k) D.nroots += c.nroots_sh[k];
   if (nunits >= 0xF0000000ull) return fail(YCRDT_E_CAPACITY, "more than 2^32 units in one batch");
-  D.nstructs = nstructs;
-  D.nsections = nsections;
+  D.nstructs = nstructs_q;
+  D.nsections = nsections_q;
   D.nclients = nclients;
   // lazy: the compacted range count; integrate: the ranges stay in their regions (a nonzero
   // region total says there may be some, k_ds_apply reads each update's count)

@@ -675,7 +675,8 @@ void launch_section_clients(const Work& w, uint32_t nsections, hipStream_t s);
 void launch_client_table(Work& w, uint32_t nsections, hipStream_t s);
 void launch_struct_decode(const Work& w, uint32_t nstructs, hipStream_t s);
 void launch_struct_lenscan(const Work& w, uint32_t nstructs, hipStream_t s);
-bool decode_tail_small(const Work& w, uint32_t nstructs, uint32_t nsections, hipStream_t s);  // one workgroup: structs .. client states (small, integrate)
+bool decode_tail_small(const Work& w, uint32_t nstructs, uint32_t nsections, hipStream_t s);
+void launch_decode_tail_small(const Work& w, uint32_t nstructs, uint32_t nsections, hipStream_t s);  // NONE: counts on the device  // one workgroup: structs .. client states (small, integrate)
 void launch_json_structs(const Work& w, uint32_t nstructs, hipStream_t s);  // JSON.parse of JSON-like contents
 void launch_states(const Work& w, uint32_t nstructs, uint32_t nsections, hipStream_t s);  // clocks + client states
 void launch_struct_clocks(const Work& w, uint32_t nstructs, hipStream_t s);               // clocks only (lazy)

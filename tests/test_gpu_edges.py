@@ -204,3 +204,20 @@ def test_local_ops_by_max_client_id():
             doc.map_delete("users", "a")
         _same(d, ref)
         assert d.root_json("messages", "array") == ref.root_json("messages", "array")
+
+
+@pytest.mark.parametrize("nclients", [1500, 2500])
+def test_small_update_many_clients(nclients):
+    """One small update holding many clients' sections (crdt.js's full-state wire shape): the
+    count-free small decode takes it; past its one-workgroup client table (2 048 sections) it
+    raises a capacity error and the decode reruns counted. Both against the oracle."""
+    src = ODoc(0x7FFFFFF0)
+    for c in range(1, nclients + 1):
+        p = ODoc(c)
+        p.map_set("users", "k%d" % (c % 97), any_int(c))
+        src.apply_update(p.encode_state_as_update())
+    state = src.encode_state_as_update()
+    assert len(state) <= 64 << 10
+    d, ref = _merge_both([state])
+    _same(d, ref)
+    assert json.loads(d.root_json("users", "map")) == json.loads(ref.root_json("users", "map"))
