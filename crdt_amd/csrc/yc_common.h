@@ -108,6 +108,11 @@ __device__ __forceinline__ void block_scan_u32_u64(const uint32_t* in, uint64_t*
   for (uint32_t i = a; i < b; ++i) { const uint32_t x = in[i]; out[i] = run; run += x; }
   __syncthreads();
 }
+// a load that never hits a vector-L1 line older than a memory-side atomic (a relaxed agent-scope
+// atomic load: served by L2) — the single-workgroup kernels read what other lanes' atomics wrote
+__device__ __forceinline__ uint32_t ld_fresh(const uint32_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
 // a phase boundary inside one workgroup where the phase before handed data over through memory-side
 // (L2) atomics as well as plain stores: agent-scope fences on both sides of the barrier, so no
 // wavefront reads an L1 line older than an atomic of the phase before

@@ -593,14 +593,16 @@ uint32_t run_key_resolution(const Work& w, uint32_t nsegs, hipStream_t s) {
 // the key's value is the rightmost entry: descend from the max-client root through the max-client
 // child until a leaf (YATA order of an origin-only tree, SURVEY.md §7 hard part 2)
 // (a descent visits every segment at most once: more hops than segments is a cycle, an error)
+// (k_rootmax / k_flags / g_maxchild were last written by atomics: ld_fresh, for k_merge_small's
+// barrier-separated phases)
 __device__ __forceinline__ void winner_at(const Work& w, uint32_t k, uint32_t nsegs) {
-  const uint32_t r = w.k_rootmax[k];
+  const uint32_t r = ld_fresh(&w.k_rootmax[k]);
   if (!r) { w.k_winner[k] = NONE; return; }
-  if (w.k_flags[k] & KF_YATA) { w.k_winner[k] = NONE; return; }  // ordered by the YATA kernels (k_mapx_fix writes the winner)
+  if (ld_fresh(&w.k_flags[k]) & KF_YATA) { w.k_winner[k] = NONE; return; }  // ordered by the YATA kernels (k_mapx_fix writes the winner)
   uint32_t x = r - 1;
   bool leaf = false;
   for (uint32_t it = 0; it <= nsegs; ++it) {
-    const uint32_t m = w.g_maxchild[x];
+    const uint32_t m = ld_fresh(&w.g_maxchild[x]);
     if (!m) { leaf = true; break; }
     x = m - 1;
   }
@@ -870,6 +872,12 @@ void launch_merge_tail(const Work& w, uint32_t nsegs, hipStream_t s) {
 constexpr uint32_t MS_LANES = 512, MS_SMALL = MS_LANES * 8;
 // nunits != 0: the segment cuts and starts (k_segments_small's work) run here first, and the
 // segment count is read on the device (the host skipped the count synchronisation)
+template <bool FENCE>
+__device__ __forceinline__ void ms_sync() {  // FENCE: agent-scope fences around the barrier (A/B)
+  if (FENCE) phase_sync();
+  else __syncthreads();
+}
+template <bool FENCE>
 __global__ __launch_bounds__(MS_LANES) void k_merge_small(Work w, uint32_t nsegs, uint64_t nunits) {
   __shared__ uint32_t part[MS_LANES];
   __shared__ uint32_t sarr;
@@ -879,8 +887,8 @@ __global__ __launch_bounds__(MS_LANES) void k_merge_small(Work w, uint32_t nsegs
   if (w.ctr->err) return;
   if (nunits) {
     segments_small_body<MS_LANES>(w, nunits, part);
-    phase_sync();  // (ERR_PENDING: an atomic)
-    if (w.ctr->err) return;
+    ms_sync<FENCE>();
+    if (ld_fresh(&w.ctr->err)) return;  // (ERR_PENDING: an atomic)
     nsegs = w.ctr->nsegs;
   }
   const uint32_t t = threadIdx.x, ck = w.cap_keys;
@@ -888,16 +896,16 @@ __global__ __launch_bounds__(MS_LANES) void k_merge_small(Work w, uint32_t nsegs
   for (uint32_t i = t; i < 2 * ck; i += MS_LANES) ((uint32_t*)w.k_hash)[i] = 0;
   for (uint32_t i = t; i < ck; i += MS_LANES) { w.k_rootmax[i] = 0; w.k_flags[i] = 0; w.k_parent[i] = NONE; }
   for (uint32_t i = t; i < nsegs; i += MS_LANES) w.g_maxchild[i] = 0;
-  phase_sync();
+  ms_sync<FENCE>();
   for (uint32_t i = t; i < nsegs; i += MS_LANES) seg_props_at(w, i);
-  phase_sync();
+  ms_sync<FENCE>();
   bool arr = false;
   for (uint32_t i = t; i < nsegs; i += MS_LANES) arr |= resolve_at(w, i, nsegs);
   if (arr) sarr = 1u;
-  phase_sync();
+  ms_sync<FENCE>();
   if (t == 0 && sarr) w.ctr->narray = 1u;
   for (uint32_t k = t; k < ck; k += MS_LANES) winner_at(w, k, nsegs);
-  phase_sync();
+  ms_sync<FENCE>();
   // merge flags (fold: no dead-type pass), then the output struct ids and the run starts' scan
   // input, as k_merge_flags + its scan
   for (uint32_t i = t; i <= nsegs; i += MS_LANES) {
@@ -916,7 +924,10 @@ bool merge_small_fits(uint64_t nsegs_bound) {
 }
 // (nunits != 0: the segments too, nsegs read on the device)
 void launch_merge_small(const Work& w, uint32_t nsegs, uint64_t nunits, hipStream_t s) {
-  hipLaunchKernelGGL(k_merge_small, dim3(1), dim3(MS_LANES), 0, s, w, nsegs, nunits);
+  if (getenv("YCRDT_PHASE_FENCE") && getenv("YCRDT_PHASE_FENCE")[0] == '1')
+    hipLaunchKernelGGL(k_merge_small<true>, dim3(1), dim3(MS_LANES), 0, s, w, nsegs, nunits);
+  else
+    hipLaunchKernelGGL(k_merge_small<false>, dim3(1), dim3(MS_LANES), 0, s, w, nsegs, nunits);
 }
 
 bool launch_merge_flags(const Work& w, uint32_t nsegs, hipStream_t s, bool fold) {

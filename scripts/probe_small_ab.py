@@ -10,6 +10,7 @@ import crdt_amd  # noqa: E402
 MODES = {
     "all_on": {},
     "quick_off": {"YCRDT_DECODE_QUICK": "0"},
+    "fence": {"YCRDT_PHASE_FENCE": "1"},
     "merge_off": {"YCRDT_MERGE_SMALL": "0"},
     "all_off": {"YCRDT_MERGE_SMALL": "0", "YCRDT_ENCODE_SMALL": "0", "YCRDT_DECODE_SMALL": "0", "YCRDT_VIEW_SMALL": "0"},
 }
@@ -19,7 +20,7 @@ bench.per_op_leg(eng, (100,))  # warm-up
 res = {m: [] for m in MODES}
 for rnd in range(int(sys.argv[1]) if len(sys.argv) > 1 else 3):
     for m, env in MODES.items():
-        for k in ("YCRDT_MERGE_SMALL", "YCRDT_ENCODE_SMALL", "YCRDT_DECODE_SMALL", "YCRDT_VIEW_SMALL", "YCRDT_DECODE_QUICK"):
+        for k in ("YCRDT_MERGE_SMALL", "YCRDT_ENCODE_SMALL", "YCRDT_DECODE_SMALL", "YCRDT_VIEW_SMALL", "YCRDT_DECODE_QUICK", "YCRDT_PHASE_FENCE"):
             os.environ.pop(k, None)
         os.environ.update(env)
         r = bench.per_op_leg(eng, (500,))["500"]
