@@ -89,13 +89,19 @@ __device__ __forceinline__ void block_scan_u32(const uint32_t* in, uint32_t* out
   __syncthreads();
 }
 
+// a load that never hits a vector-L1 line older than a memory-side atomic (a relaxed agent-scope
+// atomic load: served by L2) — the single-workgroup kernels read what other lanes' atomics wrote
+__device__ __forceinline__ uint32_t ld_fresh(const uint32_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
 // the same with 64-bit prefixes (the clock-length and client-state scans)
-template <uint32_t LANES>
+// (FRESH: the input was written by atomics in the same kernel — read through L2)
+template <uint32_t LANES, bool FRESH = false>
 __device__ __forceinline__ void block_scan_u32_u64(const uint32_t* in, uint64_t* out, uint32_t n, uint64_t* part) {
   const uint32_t t = threadIdx.x, per = (n + LANES - 1) / LANES;
   const uint32_t a = min(n, t * per), b = min(n, a + per);
   uint64_t sum = 0;
-  for (uint32_t i = a; i < b; ++i) sum += in[i];
+  for (uint32_t i = a; i < b; ++i) sum += FRESH ? ld_fresh(&in[i]) : in[i];
   part[t] = sum;
   __syncthreads();
   for (uint32_t off = 1; off < LANES; off <<= 1) {
@@ -105,13 +111,8 @@ __device__ __forceinline__ void block_scan_u32_u64(const uint32_t* in, uint64_t*
     __syncthreads();
   }
   uint64_t run = part[t] - sum;
-  for (uint32_t i = a; i < b; ++i) { const uint32_t x = in[i]; out[i] = run; run += x; }
+  for (uint32_t i = a; i < b; ++i) { const uint32_t x = FRESH ? ld_fresh(&in[i]) : in[i]; out[i] = run; run += x; }
   __syncthreads();
-}
-// a load that never hits a vector-L1 line older than a memory-side atomic (a relaxed agent-scope
-// atomic load: served by L2) — the single-workgroup kernels read what other lanes' atomics wrote
-__device__ __forceinline__ uint32_t ld_fresh(const uint32_t* p) {
-  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 // a phase boundary inside one workgroup where the phase before handed data over through memory-side
 // (L2) atomics as well as plain stores: agent-scope fences on both sides of the barrier, so no

@@ -2795,7 +2795,7 @@ __global__ __launch_bounds__(CT_LANES) void k_sections_small(Work w, uint32_t n,
   for (uint32_t i = t; i < n; i += CT_LANES) section_rank_at(w, i);
   for (uint32_t i = t; i <= mask; i += CT_LANES) key[i] = ~0ull;
   client_table_small_body(w, n, v, pre, u, part);  // (ends with the sections' client indexes)
-  phase_sync();  // (the key fill, plain stores, before the atomics below)
+  __syncthreads();  // (the key fill's stores reach L2 before the later atomics: one CU's vector L1 forwards in order)
   const uint32_t nc = w.ctr->nclients;
   for (uint32_t i = t; i < nc; i += CT_LANES) {
     const uint64_t k = (uint64_t)w.cl_vals[i];
@@ -2990,7 +2990,7 @@ __device__ __forceinline__ void apply_caps_at(const Work& w, uint32_t c) {
   const uint32_t v = w.cl_vals[c];
   const uint32_t i = lower_bound_u32(w.cap_client, w.ncaps, v);
   const uint32_t cap = (i < w.ncaps && w.cap_client[i] == v) ? w.cap_clock[i] : 0u;
-  if (w.cl_state[c] > cap) w.cl_state[c] = cap;
+  if (ld_fresh(&w.cl_state[c]) > cap) w.cl_state[c] = cap;
 }
 __global__ void k_apply_caps(Work w) {
   const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
@@ -3031,13 +3031,13 @@ __global__ __launch_bounds__(DT_LANES) void k_decode_tail_small(Work w, uint32_t
   __syncthreads();
   block_scan_u32_u64<DT_LANES>(w.s_len, w.s_lenscan, nstructs + 1, part);
   for (uint32_t i = t; i < nstructs; i += DT_LANES) struct_clock_at(w, i, nstructs, 1u);
-  phase_sync();  // (client states: atomicMax)
+  __syncthreads();
   const uint32_t nclients = w.ctr->nclients;
   if (w.capped) {
-    for (uint32_t c = t; c < nclients; c += DT_LANES) apply_caps_at(w, c);
+    for (uint32_t c = t; c < nclients; c += DT_LANES) apply_caps_at(w, c);  // (reads cl_state through L2)
     __syncthreads();
   }
-  block_scan_u32_u64<DT_LANES>(w.cl_state, w.cl_base, nsections + 1, part);
+  block_scan_u32_u64<DT_LANES, true>(w.cl_state, w.cl_base, nsections + 1, part);  // (client states: atomicMax)
   if (t == 0) {  // (k_state_totals)
     w.ctr->units = w.cl_base[nclients];
     w.ctr->in_len = w.s_lenscan[nstructs];

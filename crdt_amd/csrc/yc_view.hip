@@ -83,7 +83,7 @@ __device__ __forceinline__ void vkey_fill_at(const Work& w, const uint32_t* __re
   K.name_pos = K.name_len = 0;
   K.psub_pos = K.psub_len = 0;
   K.seg0 = K.nseg = 0;
-  const uint32_t r = krep[k];
+  const uint32_t r = ld_fresh(&krep[k]);  // (atomicMin: read through L2, k_view_small's phases)
   if (r != NONE) {
     const uint32_t own = w.g_src[r];
     // the struct table keeps whole varStrings (length prefix included): the view holds the text
@@ -128,7 +128,7 @@ __global__ __launch_bounds__(VS_LANES) void k_view_small(Work w, uint32_t nsegs,
     const uint32_t k = w.g_key[s];
     if (k != NONE && kmap[k] != NONE) atomicMin(&krep[k], s);
   }
-  phase_sync();  // (krep: atomicMin)
+  __syncthreads();  // (krep, written by atomicMin, is read with ld_fresh)
   const uint32_t nk = n;
   if (t == 0) *nkeys = nk;
   for (uint32_t i = t; i < nk; i += VS_LANES) vkey_fill_at(w, krep, keys, i);
