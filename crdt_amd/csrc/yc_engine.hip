@@ -892,13 +892,17 @@ int run_decode(ycrdt_engine* e, ycrdt_batch* b, bool lazy, Decoded& D, bool gene
     const int rc0 = split_decode_meta(e, b, sh, wd);
     if (rc0) return rc0;
   }
-  HIPCHK(hipEventRecord(e->side_fork, s));
-  HIPCHK(hipStreamWaitEvent(e->side, e->side_fork, 0));
-  launch_chunks(wd, e->side);
-  HIPCHK(hipEventRecord(e->side_done, e->side));
+  // (no large update: no chunk path, no fork / join — four runtime calls fewer per small merge)
+  const bool chunks = wd.ngroups || wd.nbig;
+  if (chunks) {
+    HIPCHK(hipEventRecord(e->side_fork, s));
+    HIPCHK(hipStreamWaitEvent(e->side, e->side_fork, 0));
+    launch_chunks(wd, e->side);
+    HIPCHK(hipEventRecord(e->side_done, e->side));
+  }
   launch_direct(wd, s);
   mark(e, "decode.chunk_wait");  // decode.direct: k_direct alone (the chunk path runs beside it)
-  HIPCHK(hipStreamWaitEvent(s, e->side_done, 0));
+  if (chunks) HIPCHK(hipStreamWaitEvent(s, e->side_done, 0));
   if (split) {
     mark(e, "decode.exchange");
     // test hook (tests/test_gpu_exchange.py): this rank fails on the host before the exchange

@@ -1,11 +1,17 @@
 #!/bin/bash
-# the per-call GPU step: the round-end rehearsal (tests, smoke, bench), the small-batch A/B and a
-# per-op kernel trace
+# the per-call GPU step: GPU tests, the small-batch A/B, a per-op kernel trace
 set -u
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-bash scripts/gpu_final.sh || exit 1
-timeout -k 10 300 python3 scripts/probe_small_ab.py 2 > gpurun_out/ab_small5.log 2>&1 || exit 1
-tail -5 gpurun_out/ab_small5.log
-timeout -s KILL 200 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/trp -- python3 scripts/probe_trace.py perop > gpurun_out/trp.log 2>&1 || exit 1
-python3 scripts/trace_last.py gpurun_out/trp 0 > gpurun_out/tr_perop7.txt; rm -rf gpurun_out/trp
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/t_nf.log 2>&1; rc=$?
+tail -3 gpurun_out/t_nf.log; [ $rc = 0 ] || exit 1
+timeout -k 10 300 python3 scripts/probe_small_ab.py 2 > gpurun_out/ab_small6.log 2>&1 || exit 1
+tail -5 gpurun_out/ab_small6.log
+timeout -k 10 200 python3 -c "
+import sys; sys.path.insert(0, '.')
+import bench, crdt_amd
+bench._yjs_perop = lambda n: None
+r = bench.per_op_leg(crdt_amd.Engine(), (500, 2000))
+print({k: (v['ops_per_s'], v['breakdown']['device_ms_per_op'], v['breakdown']['host_ms_per_op']) for k, v in r.items()})
+" > gpurun_out/perop_nf.log 2>&1 || exit 1
+cat gpurun_out/perop_nf.log
