@@ -2335,7 +2335,7 @@ __global__ __launch_bounds__(256) void k_ds_decode(Work w) {
   if (phase != PH_DONE) raise_err(err, ERR_DECODE);  // truncated delete set
   if (lane == 0) {
     w.ds_count[u] = obase - obase0;
-    if (obase - obase0 > DSA_WAVE) w.ctr->ds_big = 1u;  // (k_units spreads the rest)
+    if (obase - obase0 > DSA_WAVE) w.ds_biglist[atomicAdd(&w.ctr->ds_big, 1u)] = u;  // (k_units spreads the rest)
   }
 }
 
@@ -2483,7 +2483,7 @@ __global__ void k_dsp_headers(Work w) {
   }
   w.dsp_nb[bi] = c;
   w.ds_count[u] = off;
-  if (off > DSA_WAVE) w.ctr->ds_big = 1u;
+  if (off > DSA_WAVE) w.ds_biglist[atomicAdd(&w.ctr->ds_big, 1u)] = u;
   w.dsp_b[u] = bi;
 }
 __device__ __forceinline__ void dsp_ranges_group(const Work& w, uint32_t i, uint32_t lane) {
@@ -2787,10 +2787,15 @@ __global__ __launch_bounds__(CT_LANES) void k_sections_small(Work w, uint32_t n,
   __shared__ uint32_t part[CT_LANES];
   const uint32_t t = threadIdx.x;
   if (n == NONE) {  // (the quick decode: no count synchronisation ran, the count is on the device)
-    if (w.ctr->err) return;  // (the walk failed: the sections are not to be read)
-    n = w.ctr->nsections;
-    if (n > CT_SMALL) { if (t == 0) raise_err(&w.ctr->err, ERR_CAPACITY); return; }  // (rerun, counted)
-    if (!n) return;
+    n = w.ctr->err ? 0u : w.ctr->nsections;  // (the walk failed: the sections are not to be read)
+    if (n > CT_SMALL) { if (t == 0) raise_err(&w.ctr->err, ERR_CAPACITY); n = 0; }  // (rerun, counted)
+    if (!n) {
+      // no client table: the host still hands the hash to find_client (k_units clips a delete-only
+      // update's ranges against it), so it must be EMPTY here, not the previous merge's slots
+      for (uint32_t i = t; i <= mask; i += CT_LANES) key[i] = ~0ull;
+      if (t == 0) w.ctr->nclients = 0;
+      return;
+    }
   }
   for (uint32_t i = t; i < n; i += CT_LANES) section_rank_at(w, i);
   for (uint32_t i = t; i <= mask; i += CT_LANES) key[i] = ~0ull;

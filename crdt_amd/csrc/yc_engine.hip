@@ -179,7 +179,7 @@ enum Buf {
   B_UOWN, B_UFLAG, B_UCUT, B_UWPRE,
   B_GSTART, B_GCIDX, B_GSRC, B_GFLAGS, B_GORIG, B_GRORIG, B_GLINK, B_GOSEG, B_GKEY, B_GMAXC, B_GNEXT, B_GOUTID, B_GTMP, B_GTMP2,
   B_KHASH, B_KROOT, B_KWIN, B_KPAR, B_KFLAG, B_SPK,
-  B_USEC, B_USECN, B_DBG, B_XTAB, B_UFAIL, B_FW, B_CCNT, B_TENTRY, B_XLIST, B_WLEN, B_FWSEC, B_DSPCNT, B_DSPPRE, B_DSPVAL, B_DSPBLK, B_DSPB, B_DSPNB, B_DSPFAIL, B_DSPGB, B_OGEN, B_SDDEFER, B_COFF, B_CPRE, B_OPRE, B_SECUEND, B_SECDOC,
+  B_USEC, B_USECN, B_DBG, B_XTAB, B_UFAIL, B_FW, B_CCNT, B_TENTRY, B_XLIST, B_WLEN, B_FWSEC, B_DSPCNT, B_DSPPRE, B_DSPVAL, B_DSPBLK, B_DSPB, B_DSPNB, B_DSPFAIL, B_DSPGB, B_OGEN, B_SDDEFER, B_COFF, B_CPRE, B_OPRE, B_SECUEND, B_SECDOC, B_DSBIGL,
   B_LZKEY, B_LZKEYS, B_LZIOTA, B_LZSEC, B_LZRSTART, B_LZPREV, B_LZFIRST, B_LZCAP, B_LZEVBASE, B_LZEVN, B_LZFLAG,
   B_LZLHI, B_LZLLO, B_EVKIND, B_EVSRC, B_EVCLOCK, B_EVLEN, B_EVSIZE, B_EVPOS, B_BLKSIZE, B_BLKPOS, B_SVC, B_SVK,
   B_DSMKEY, B_DSMKEYS, B_DSMLEN, B_DSMLENS, B_DSMEND, B_DSMMAX, B_DSMFLAG, B_DSMRID, B_DRCLIENT, B_DRCLOCK, B_DREND,
@@ -854,6 +854,7 @@ int run_decode(ycrdt_engine* e, ycrdt_batch* b, bool lazy, Decoded& D, bool gene
   w.ds_region = take<uint32_t>(V, B_DSREG, nu + 2, ok);
   w.ds_count = take<uint32_t>(V, B_DSCNT, nu + 2, ok);
   w.ds_dense_off = take<uint32_t>(V, B_DSOFF, nu + 2, ok);
+  w.ds_biglist = take<uint32_t>(V, B_DSBIGL, nu + 1, ok);
   w.cap_clients = w.cap_sections;
   w.scratch = take<uint32_t>(V, B_SCRATCH, std::max<uint64_t>({nwords + 2, (uint64_t)w.cap_sections + 66, (uint64_t)nu + 2}), ok);
   w.usec_start = take<uint32_t>(V, B_USEC, nu + 1, ok);

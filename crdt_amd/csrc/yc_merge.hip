@@ -249,12 +249,15 @@ __global__ __launch_bounds__(SEG_LANES) void k_segments_small(Work w, uint64_t n
 // references, every one of them a byte store or an atomic): workgroups [0, nb) take a struct each
 // lane (owner, then references — the struct's columns are loaded once), the rest one update per
 // wavefront (delete sets).
-// ranges DSA_WAVE.. of the large updates' delete sets, one lane per range (grid-stride over the
-// extra workgroups; only the chunk-path updates can hold that many)
+// ranges DSA_WAVE.. of the delete sets that hold more, one lane per range (grid-stride over the
+// extra workgroups). Any update can: a 16 KiB direct-path update of one transaction that deleted
+// ~8 000 scattered items carries that many 2-byte ranges, so the list is every such update the
+// decoders met (k_ds_decode, k_dsp_headers), not the chunk-path updates
 __device__ __forceinline__ void unit_ds_apply_big(const Work& w, uint32_t nclients, uint32_t blk, uint32_t nx) {
   const uint32_t t = blk * blockDim.x + threadIdx.x, stride = nx * blockDim.x;
-  for (uint32_t bi = 0; bi < w.nbig; ++bi) {
-    const uint32_t u = w.ulist[bi];
+  const uint32_t nlist = min(w.ctr->ds_big, w.nupd);
+  for (uint32_t bi = 0; bi < nlist; ++bi) {
+    const uint32_t u = w.ds_biglist[bi];
     const uint32_t n = w.ds_count[u];
     if (n <= DSA_WAVE) continue;
     const uint32_t base = w.ds_region[u], doc = doc_of_update(w, u);

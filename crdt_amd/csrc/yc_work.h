@@ -31,7 +31,7 @@ struct Counters {            // device-side counters, read back at the few host 
   uint32_t narray;           // YArray list members (segments)
   uint32_t nmapx;            // 1: a YMap entry needs full YATA (an entry item with a right origin, k_resolve)
   uint32_t any_rorigin;      // 1: a decoded item has a right origin (only then can nmapx be set)
-  uint32_t ds_big;           // 1: a delete set decoded grid-wide has more ranges than one wavefront applies (DSA_WAVE)
+  uint32_t ds_big;           // updates whose delete set has more ranges than one wavefront applies (DSA_WAVE), listed in ds_biglist
   uint32_t nsd_defer;        // structs k_struct_decode deferred to k_struct_decode_deferred
   uint32_t any_json;         // 1: a decoded struct holds ContentJSON / Embed / Format (k_json_structs checks them)
   uint32_t narray_roots;     // 1: a decoded item may root a YArray list (parent given, no parentSub)
@@ -132,6 +132,8 @@ struct Work {
   uint32_t* ds_count = nullptr;    // [nupd+1] ranges decoded per update
   uint32_t* ds_dense_off = nullptr;// [nupd+1] scan of ds_count
   uint32_t* ds_len = nullptr;      // [cap_ds+1] clipped lengths (scan input)
+  uint32_t* ds_biglist = nullptr;  // [nupd] updates with more than DSA_WAVE ranges (ctr->ds_big of them): k_units spreads
+                                   // their ranges past the first DSA_WAVE over extra workgroups, whichever decoder read them
   // large delete sets decoded grid-wide (yc_decode.hip k_dsp_*): per chunk of the large updates
   // the terminal bytes (varuint ends) of its delete-set part and their scan; every varuint's value;
   // the client blocks (value index of the client, client, ranges, first range) of each update
