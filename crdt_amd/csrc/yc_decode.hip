@@ -1296,6 +1296,175 @@ __device__ __forceinline__ uint32_t nth_set1(uint64_t x, uint32_t k) {  // posit
   for (uint32_t i = 1; i < k; ++i) x &= x - 1;
   return (uint32_t)__ffsll((long long)x) - 1;
 }
+// ---- Record mode of the multi-section fast walk (a full state as ONE update: crdt.js's wire shape,
+// crdt.js:288,443; a thousand client sections). A section's step — header, exact walk from its
+// first struct to the chain, count search, the last struct's end = the next header — depends only
+// on the header's position, and every header after the first lies on the synced chain (the chain
+// runs through the previous section's last struct and on into the header bytes). So the step is
+// evaluated for EVERY chain position of the update at once (k_fwc: one lane per chain position,
+// whole chip), and the serial part shrinks to following the records from header to header: one
+// memory round trip per section instead of ~20 dependent parse steps (C2 document state, 1 001
+// sections: the walk took ~22 ms). A header off the chain (the update's first; the end of a
+// section walked whole) or a record that gave up early is evaluated by the walker itself with the
+// same function. The records never vouch for anything the exact walk would not: fwc_eval IS the
+// section step (the walk, the off-chunk test, the count search and the select of the old pass).
+struct FwcRes { uint32_t next, e, k0, why; };  // next header (NONE: not vouched), chain range end, walked structs, reason
+__device__ __forceinline__ bool spec_at(const uint64_t* __restrict__ spec, uint32_t q) { return (spec[q >> 6] >> (q & 63)) & 1ull; }
+__device__ __forceinline__ FwcRes fwc_eval(const Work& w, const uint8_t* __restrict__ b, const uint64_t* __restrict__ spec, uint32_t ustart,
+                                           uint32_t uend, uint32_t c0, uint32_t nch, uint32_t hdr, uint32_t walk_max) {
+  FwcRes r{NONE, NONE, 0u, 0u};
+  uint32_t p = hdr;
+  bool ok = hdr < uend;
+  const uint32_t n = rd_vu(b, p, uend, ok);
+  rd_vu(b, p, uend, ok);  // client
+  rd_vu(b, p, uend, ok);  // clock
+  if (!ok || n > uend - p) { r.why = 3; return r; }
+  const uint32_t p1 = p;
+  if (n == 0) { r.next = p1; r.e = p1; return r; }
+  if (p1 >= uend) { r.why = 3; return r; }
+  // the exact walk until it meets the chain (or walks the whole section)
+  uint32_t q = p1, k0 = 0;
+  for (uint32_t steps = 0; q < uend && k0 < n && !spec_at(spec, q); ++steps) {
+    if (steps == walk_max) { r.why = walk_max < FWM_WALK ? 8u : 5u; return r; }
+    const uint32_t dq = chain_len(GlobalSrc{b}, b, q, uend);
+    if (!dq) { r.why = 4; return r; }  // no struct parses: k_walk reports it
+    q += dq;
+    ++k0;
+  }
+  r.k0 = k0;
+  if (k0 == n) {  // every struct walked: the next header is where the walk stopped
+    if (q > uend) { r.why = 3; return r; }
+    r.next = q;
+    r.e = q;
+    return r;
+  }
+  if (q >= uend) { r.why = 5; return r; }
+  // the target-th chain position from q (q the first) is the section's last struct
+  const uint32_t target = n - k0, CH = w.schunk;
+  const uint32_t jq = (q - ustart) / CH, ceq = min(ustart + jq * CH + CH, uend);
+  const uint32_t cq = popc_range(spec, q, ceq);
+  uint32_t fa = q, rem = target;
+  if (target > cq) {
+    const uint64_t need = target - cq, base = w.cpre[c0 + jq + 1];
+    uint32_t lo = jq + 1, hi = nch;  // the first chunk j with cpre[c0 + j + 1] - base >= need
+    while (lo < hi) { const uint32_t m = (lo + hi) >> 1; if (w.cpre[c0 + m + 1] - base >= need) hi = m; else lo = m + 1; }
+    if (lo >= nch) { r.why = 6; return r; }
+    if (w.opre[c0 + lo + 1] != w.opre[c0 + jq + 1]) { r.why = 2; return r; }  // an off chunk between
+    rem = (uint32_t)(need - (w.cpre[c0 + lo] - base));
+    fa = ustart + lo * CH;
+  }
+  const uint32_t Lp = select_from(spec, fa, rem);
+  const uint32_t dl = Lp < uend ? chain_len(GlobalSrc{b}, b, Lp, uend) : 0u;
+  if (!dl || Lp + dl > uend) { r.why = 7; return r; }  // the last struct's end is unknown
+  r.next = Lp + dl;
+  r.e = Lp + 1;
+  return r;
+}
+// every chain position of the record-mode updates: its section step as if a header started there
+// (one lane per bitmap word of their chunks, grid-stride)
+__global__ __launch_bounds__(256) void k_fwc(Work w) {
+  const uint32_t wpc = w.schunk / 64;
+  const uint64_t total = (uint64_t)w.ngroups * wpc;
+  for (uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total; t += (uint64_t)gridDim.x * blockDim.x) {
+    const Group G = w.groups[t / wpc];
+    const uint32_t u = G.upd, off = w.fwc_off[u];
+    if (off == NONE) continue;
+    const uint32_t wd = (G.start >> 6) + (uint32_t)(t % wpc);
+    if ((uint64_t)wd * 64 >= G.end) continue;
+    const uint32_t uw = upd_win(w, u);
+    const uint8_t* __restrict__ b = win_bytes(w, uw);
+    const uint64_t* __restrict__ spec = win_words(w.spec_bits, uw);
+    const uint32_t ustart = w.uoff[u], uend = ustart + w.ulen[u], c0 = w.ugroup[u], nch = (w.ulen[u] + w.schunk - 1) / w.schunk;
+    for (uint64_t x = range_word(spec, wd, G.start, G.end); x; x &= x - 1) {
+      const uint32_t c = wd * 64 + (uint32_t)__ffsll((long long)x) - 1;
+      const FwcRes r = fwc_eval(w, b, spec, ustart, uend, c0, nch, c, w.fwc_walk);
+      w.fwc[off + (c - ustart)] = make_uint4(r.next, r.e, r.k0, r.why);
+    }
+  }
+}
+// the walker's record-mode pass: lane 0 follows the records from header to header; every section
+// it vouches for gets (header, chain range end) in fwsec, k_fwc_commit writes the rest
+__device__ __forceinline__ void fwm_records(const Work& w, uint32_t u, uint32_t nsec, uint32_t hdr0) {
+  const uint32_t uw = upd_win(w, u);
+  const uint8_t* __restrict__ b = win_bytes(w, uw);
+  const uint64_t* __restrict__ spec = win_words(w.spec_bits, uw);
+  const uint32_t ustart = w.uoff[u], uend = ustart + w.ulen[u], c0 = w.ugroup[u], nch = (w.ulen[u] + w.schunk - 1) / w.schunk;
+  const uint32_t off = w.fwc_off[u];
+  const uint32_t sbase = atomicAdd(&w.ctr->nsections, nsec);
+  if (sbase + nsec > w.cap_sections) { raise_err(&w.ctr->err, ERR_CAPACITY); return; }
+  uint32_t h = hdr0, done = 0;
+  const uint32_t lim = w.fwm_max ? min(nsec, w.fwm_max) : nsec;  // (YCRDT_FWM_MAX: tests cap the vouched prefix)
+  for (; done < lim; ++done) {
+    FwcRes r{NONE, NONE, 0u, 8u};
+    if (h > ustart && h < uend && spec_at(spec, h)) {  // a chain position: k_fwc evaluated it
+      const uint4 x = w.fwc[off + (h - ustart)];
+      r = FwcRes{x.x, x.y, x.z, x.w};
+    }
+    if (r.next == NONE && r.why == 8u) {  // off the chain, or walked past k_fwc's bound
+      r = fwc_eval(w, b, spec, ustart, uend, c0, nch, h, FWM_WALK);
+      if (w.dbg) atomicAdd(&w.dbg[16], 1ull);
+    }
+    if (r.next == NONE) {
+      if (w.dbg) {
+        atomicAdd(&w.dbg[1], 1ull);
+        atomicAdd(&w.dbg[8 + min(r.why, 7u)], 1ull);
+        w.dbg[14] = done; w.dbg[15] = nsec; w.dbg[17] = h - ustart; w.dbg[18] = uend - ustart;
+      }
+      break;
+    }
+    w.fwsec[2 * (sbase + done)] = h;
+    w.fwsec[2 * (sbase + done) + 1] = r.e;
+    h = r.next;
+  }
+  w.usec_start[u] = sbase;
+  w.usec_n[u] = nsec;
+  if (done == nsec) {
+    w.dsstart[u] = h;  // (past the last section: the delete set)
+    w.ufail[u] = 3u;   // done: k_walk leaves it alone, k_fwc_commit + k_fastmark write it
+    if (w.dbg) { atomicAdd(&w.dbg[0], 1ull); atomicAdd(&w.dbg[23], (unsigned long long)done); }
+  } else {
+    w.fw[2 * u] = done;  // k_walk resumes at section `done`, whose header is at h (section 0: the whole update)
+    w.fw[2 * u + 1] = h;
+    w.ufail[u] = 4u;
+  }
+}
+// the vouched sections of the record-mode updates, one lane per section (grid-stride): the section
+// record, its first-struct mark, the walked positions before the chain, the chain range for k_fastmark
+__global__ __launch_bounds__(256) void k_fwc_commit(Work w) {
+  const uint32_t gt = blockIdx.x * blockDim.x + threadIdx.x, gs = gridDim.x * blockDim.x;
+  for (uint32_t bi = 0; bi < w.nbig; ++bi) {
+    const uint32_t u = w.ulist[bi];
+    if (w.fwc_off[u] == NONE) continue;
+    const uint32_t uf = w.ufail[u];
+    if (uf != 3u && uf != 4u) continue;
+    const uint32_t sbase = w.usec_start[u], ndone = uf == 3u ? w.usec_n[u] : w.fw[2 * u];
+    const uint32_t uw = upd_win(w, u);
+    const uint8_t* __restrict__ b = win_bytes(w, uw);
+    const uint64_t* __restrict__ spec = win_words(w.spec_bits, uw);
+    uint64_t* __restrict__ fbits = win_words(w.final_bits, uw);
+    uint64_t* __restrict__ sbits = win_words(w.sec_bits, uw);
+    const uint32_t uend = w.uoff[u] + w.ulen[u];
+    for (uint32_t s = gt; s < ndone; s += gs) {
+      uint32_t p = w.fwsec[2 * (sbase + s)];
+      bool ok = true;
+      const uint32_t n = rd_vu(b, p, uend, ok), client = rd_vu(b, p, uend, ok), clock = rd_vu(b, p, uend, ok);
+      const uint32_t p1 = p;
+      Section sec;
+      sec.upd = u; sec.n = n; sec.client = client; sec.clock = clock;
+      sec.first_pos = n ? p1 : NONE; sec.cidx = NONE; sec.first_idx = NONE; sec.pad = 0;
+      w.sections[sbase + s] = sec;
+      if (n) atomicOr((unsigned long long*)&sbits[p1 >> 6], 1ull << (p1 & 63));
+      // the walked positions (not on the chain): the record's walk again, to where it met the chain
+      uint32_t x = p1, k0 = 0;
+      while (n && k0 < n && x < uend && !spec_at(spec, x)) {
+        atomicOr((unsigned long long*)&fbits[x >> 6], 1ull << (x & 63));
+        x = chain_step(b, x, uend);
+        ++k0;
+      }
+      w.fwsec[2 * (sbase + s)] = n ? x : p1;  // the chain range [q, e) (k_fastmark)
+    }
+  }
+}
 __global__ __launch_bounds__(64) void k_fastwalk_multi(Work w) {
   __shared__ uint32_t sp1[FWM_MAX], sn[FWM_MAX], scl[FWM_MAX], sck[FWM_MAX], sq[FWM_MAX], se[FWM_MAX], sk0[FWM_MAX], shp[FWM_MAX];
   __shared__ __attribute__((aligned(16))) uint32_t stg[FWM_STAGE / 4 + 4];
@@ -1320,6 +1489,10 @@ __global__ __launch_bounds__(64) void k_fastwalk_multi(Work w) {
   bool ok = true;
   const uint32_t nsec = rd_vu(b, p, uend, ok);
   if (!ok || nsec < 2) return;
+  if (w.fwc_off && w.fwc_off[u] != NONE) {  // record mode (k_fwc ran over the update's chain)
+    if (lane == 0) fwm_records(w, u, nsec, p);
+    return;
+  }
   // pass 1 (every value below is the same in every lane)
   const uint32_t nchk = min(nsec, w.fwm_max ? min(w.fwm_max, FWM_MAX) : FWM_MAX);
   uint32_t done = 0;          // sections vouched for
@@ -1909,7 +2082,10 @@ void launch_chunks(const Work& w, hipStream_t s) {
       scan_u32_to_u64(w.tmp, w.tmp_bytes, w.ccnt, w.cpre, (uint64_t)w.ngroups + 1, s);
       scan_u32(w.tmp, w.tmp_bytes, w.coff, w.opre, (uint64_t)w.ngroups + 1, s);
       hipLaunchKernelGGL(k_fastwalk, dim3(w.nbig), dim3(64), 0, s, w);
+      const uint32_t wgrid = (uint32_t)std::min<uint64_t>((uint64_t)w.ngroups * (w.schunk / 64) / 256 + 1, 8192);
+      if (w.fwc) hipLaunchKernelGGL(k_fwc, dim3(wgrid), dim3(256), 0, s, w);  // (record-mode updates only)
       hipLaunchKernelGGL(k_fastwalk_multi, dim3(w.nbig), dim3(64), 0, s, w);
+      if (w.fwc) hipLaunchKernelGGL(k_fwc_commit, dim3(64), dim3(256), 0, s, w);
       hipLaunchKernelGGL(k_fastmark, dim3(std::min<uint64_t>((uint64_t)w.ngroups * (w.schunk / 64) / 256 + 1, 8192)), dim3(256), 0, s, w);
     }
     hipLaunchKernelGGL(k_walk<false>, dim3(w.nbig), dim3(64), 0, s, w);

@@ -179,7 +179,7 @@ enum Buf {
   B_UOWN, B_UFLAG, B_UCUT, B_UWPRE,
   B_GSTART, B_GCIDX, B_GSRC, B_GFLAGS, B_GORIG, B_GRORIG, B_GLINK, B_GOSEG, B_GKEY, B_GMAXC, B_GNEXT, B_GOUTID, B_GTMP, B_GTMP2,
   B_KHASH, B_KROOT, B_KWIN, B_KPAR, B_KFLAG, B_SPK,
-  B_USEC, B_USECN, B_DBG, B_XTAB, B_UFAIL, B_FW, B_CCNT, B_TENTRY, B_XLIST, B_WLEN, B_FWSEC, B_DSPCNT, B_DSPPRE, B_DSPVAL, B_DSPBLK, B_DSPB, B_DSPNB, B_DSPFAIL, B_DSPGB, B_OGEN, B_SDDEFER, B_COFF, B_CPRE, B_OPRE, B_SECUEND, B_SECDOC, B_DSBIGL,
+  B_USEC, B_USECN, B_DBG, B_XTAB, B_UFAIL, B_FW, B_CCNT, B_TENTRY, B_XLIST, B_WLEN, B_FWSEC, B_DSPCNT, B_DSPPRE, B_DSPVAL, B_DSPBLK, B_DSPB, B_DSPNB, B_DSPFAIL, B_DSPGB, B_OGEN, B_SDDEFER, B_COFF, B_CPRE, B_OPRE, B_SECUEND, B_SECDOC, B_DSBIGL, B_FWC, B_FWCOFF,
   B_LZKEY, B_LZKEYS, B_LZIOTA, B_LZSEC, B_LZRSTART, B_LZPREV, B_LZFIRST, B_LZCAP, B_LZEVBASE, B_LZEVN, B_LZFLAG,
   B_LZLHI, B_LZLLO, B_EVKIND, B_EVSRC, B_EVCLOCK, B_EVLEN, B_EVSIZE, B_EVPOS, B_BLKSIZE, B_BLKPOS, B_SVC, B_SVK,
   B_DSMKEY, B_DSMKEYS, B_DSMLEN, B_DSMLENS, B_DSMEND, B_DSMMAX, B_DSMFLAG, B_DSMRID, B_DRCLIENT, B_DRCLOCK, B_DREND,
@@ -297,6 +297,10 @@ struct ycrdt_batch {
   uint32_t schunk = SCHUNK;     // chunk bytes of the large updates (layout)
   size_t ulist_off = 0;
   std::vector<Group> groups;
+  // record mode of the multi-section fast walk (yc_decode.hip k_fwc): per staged update, the base of
+  // its records (one per byte) or NONE; fwc_recs records in all
+  std::vector<uint32_t> fwc_off;
+  uint64_t fwc_recs = 0;
   uint64_t nbytes = 0;          // span of the batch buffer (windows before the last are 2^32 bytes)
   uint64_t in_bytes = 0;
   bool merged = false;
@@ -356,7 +360,27 @@ struct Src {
 // first, then the host ones in one contiguous region) + decode group table.
 void layout(ycrdt_batch* b, const std::vector<Src>& src, std::vector<uint32_t>& order) {
   b->uoff.clear(); b->ulen.clear(); b->ugroup.clear(); b->groups.clear(); b->ulist.clear(); b->uwin.clear();
+  b->fwc_off.clear();
+  b->fwc_recs = 0;
   b->in_bytes = 0;
+  // A large update of many client sections (a full state sent as one update, crdt.js:288,443) gets
+  // the record mode of the multi-section fast walk: 16 bytes of records per update byte, so only
+  // updates of >= FWC_MIN_SECTIONS sections (read from the host bytes; a doc state in HBM of
+  // >= FWC_MIN_BYTES is taken as one) and at most FWC_MAX_RECS records per batch. YCRDT_FWC=0: off.
+  constexpr size_t FWC_MIN_BYTES = size_t(64) << 10;
+  constexpr uint32_t FWC_MIN_SECTIONS = 16;
+  constexpr uint64_t FWC_MAX_RECS = uint64_t(128) << 20;
+  // (YCRDT_FWC=force, tests: every large update of two or more sections, however small)
+  const char* fwc_env = getenv("YCRDT_FWC");
+  const bool fwc_on = !env_off("YCRDT_FWC"), fwc_force = fwc_env && !strcmp(fwc_env, "force");
+  auto fwc_wants = [&](const Src& x) {
+    if (!fwc_on || (x.len < FWC_MIN_BYTES && !fwc_force)) return false;
+    if (x.dev) return true;
+    uint32_t q = 0;
+    bool okq = true;
+    const uint32_t nsec = rd_vu(x.p, q, (uint32_t)std::min<size_t>(x.len, 16), okq);
+    return okq && nsec >= (fwc_force ? 2u : FWC_MIN_SECTIONS);
+  };
   const char* mode = getenv("YCRDT_DECODE");
   const int force = mode && (!strcmp(mode, "chunks") || !strcmp(mode, "tables") || !strcmp(mode, "xtab")) ? 1
                     : mode && !strcmp(mode, "direct") ? 2 : 0;
@@ -405,10 +429,15 @@ void layout(ycrdt_batch* b, const std::vector<Src>& src, std::vector<uint32_t>& 
     b->uoff.push_back((uint32_t)off);
     b->uwin.push_back((uint32_t)win);
     b->ulen.push_back((uint32_t)len);
+    b->fwc_off.push_back(NONE);
     if (len && direct(len)) {
       b->ugroup.push_back(NONE);
       small.push_back(u);
     } else {
+      if (fwc_wants(src[i]) && b->fwc_recs + len <= FWC_MAX_RECS) {
+        b->fwc_off.back() = (uint32_t)b->fwc_recs;
+        b->fwc_recs += (len + 63) & ~size_t(63);
+      }
       b->ugroup.push_back((uint32_t)b->groups.size());
       b->ulist.push_back(u);
       for (size_t g = 0; g < len; g += b->schunk) {
@@ -861,6 +890,16 @@ int run_decode(ycrdt_engine* e, ycrdt_batch* b, bool lazy, Decoded& D, bool gene
   w.usec_n = take<uint32_t>(V, B_USECN, nu + 1, ok);
   w.wlen = wave_decode(w) ? take<uint16_t>(V, B_WLEN, (uint64_t)w.nsmall * 16384, ok) : nullptr;
   w.fwsec = w.nbig ? take<uint32_t>(V, B_FWSEC, 2ull * w.cap_sections + 2, ok) : nullptr;
+  w.fwc = nullptr;
+  w.fwc_off = nullptr;
+  if (b->fwc_recs && w.fwsec) {  // record mode: the records and each update's base
+    w.fwc = take<uint4>(V, B_FWC, b->fwc_recs + 1, ok);
+    uint32_t* fo = take<uint32_t>(V, B_FWCOFF, nu + 1, ok);
+    if (ok) HIPCHK(hipMemcpyAsync(fo, b->fwc_off.data(), sizeof(uint32_t) * nu, hipMemcpyHostToDevice, e->stream));
+    w.fwc_off = fo;
+    const char* fw = getenv("YCRDT_FWC_WALK");  // (experiments)
+    w.fwc_walk = fw && atoi(fw) > 0 ? (uint32_t)atoi(fw) : 256u;
+  }
   if (!ok) return fail(YCRDT_E_DEVICE, oom("decode workspace"));
   // rocPRIM scratch sized for the largest scan of this batch (units may grow it later)
   {
@@ -939,8 +978,8 @@ int run_decode(ycrdt_engine* e, ycrdt_batch* b, bool lazy, Decoded& D, bool gene
     HIPCHK(hipMemcpy(h, w.dbg, sizeof(h), hipMemcpyDeviceToHost));
     fprintf(stderr, "[ycrdt decode] multi-section fast walk cycles: stage %llu walk %llu search %llu, walked structs %llu, sections vouched %llu\n",
             h[19], h[20], h[21], h[22], h[23]);
-    fprintf(stderr, "[ycrdt decode] fastwalk: done %llu nsec %llu unsynced %llu | wave: done %llu unsettled %llu other %llu (chunk path: moved / jumped chunk entries) | k_spec exact parses %llu (%llu bytes) | multi-section left to k_walk, by reason 1-5: %llu %llu %llu %llu %llu (section %llu of %llu structs) | %llu %llu %llu\n",
-            h[0], h[1], h[2], h[3], h[4], h[5], h[6], h[7], h[9], h[10], h[11], h[12], h[13], h[14], h[15], h[11], h[12], h[13]);
+    fprintf(stderr, "[ycrdt decode] fastwalk: done %llu nsec %llu unsynced %llu | wave: done %llu unsettled %llu other %llu (chunk path: moved / jumped chunk entries) | k_spec exact parses %llu (%llu bytes) | multi-section left to k_walk, by reason 1-5: %llu %llu %llu %llu %llu (section %llu of %llu structs) | record mode: %llu sections evaluated by the walker, stopped at byte %llu of %llu\n",
+            h[0], h[1], h[2], h[3], h[4], h[5], h[6], h[7], h[9], h[10], h[11], h[12], h[13], h[14], h[15], h[16], h[17], h[18]);
     HIPCHK(hipMemsetAsync(w.dbg, 0, 192, s));
   }
   if (rc == YCRDT_E_CAPACITY && !generous) return run_decode(e, b, lazy, D, true, sh);  // past the estimates

@@ -90,6 +90,10 @@ struct Work {
   const uint32_t* ulist = nullptr; // [nbig] updates on the chunk path, then [nsmall] parsed directly
   uint32_t nbig = 0, nsmall = 0;
   uint32_t* fwsec = nullptr;       // [2 cap_sections] k_fastwalk_multi: each section's chain range [q, e)
+  uint4* fwc = nullptr;            // record mode (k_fwc): per byte of a multi-section large update, the section
+                                   // step from a header there {next header, chain range end, walked, why}
+  const uint32_t* fwc_off = nullptr; // [nupd] record base of each record-mode update, NONE otherwise (null: none)
+  uint32_t fwc_walk = 256;         // k_fwc's walk bound (YCRDT_FWC_WALK; at FWM_WALK the walker never re-evaluates a chain-position header)
   uint16_t* wlen = nullptr;        // [nsmall * 16384] few small updates: the chain step at every position (k_wlen)
   uint32_t schunk = SCHUNK;        // chunk bytes of this batch's large updates (<= SCHUNK)
   uint32_t force_xtab = 0;         // YCRDT_DECODE=xtab: every large update takes the exit-table walk (tests)

@@ -16,13 +16,26 @@ b.merge()
 full = b.result()[0]
 del b
 print("full state", len(full), flush=True)
-os.environ["YCRDT_DEBUG_DECODE"] = "1"
-fb = crdt_amd.Batch([full], eng)
-fb.merge()
-os.environ.pop("YCRDT_DEBUG_DECODE")
 eng.set_profiling(True)
-for _ in range(3):
-    t0 = time.perf_counter()
-    st = fb.merge()
-    print(f"merge {1e3 * (time.perf_counter() - t0):.2f} ms, device {st.device_ms:.2f}", flush=True)
-print(", ".join(f"{n} {m:.3f}" for n, m in eng.phase_times() if m > 0.05), flush=True)
+res = {}
+CONFIGS = {"1": {}, "0": {}}  # record mode on (the default) and off; more from argv: name:VAR=v,VAR=v
+for a in sys.argv[1:]:
+    name, kv = a.split(":", 1)
+    CONFIGS[name] = dict(x.split("=", 1) for x in kv.split(","))
+for fwc, env in CONFIGS.items():
+    for k in ("YCRDT_FWC_WALK", "YCRDT_SPEC_HINT", "YCRDT_SCHUNK"):
+        os.environ.pop(k, None)
+    os.environ.update(env)
+    os.environ["YCRDT_FWC"] = fwc if fwc in ("0", "1") else env.get("YCRDT_FWC", "1")
+    fb = crdt_amd.Batch([full], eng)
+    os.environ["YCRDT_DEBUG_DECODE"] = "1"
+    print(fwc, env, flush=True)
+    fb.merge()
+    os.environ.pop("YCRDT_DEBUG_DECODE")
+    for _ in range(3):
+        t0 = time.perf_counter()
+        st = fb.merge()
+        print(f"YCRDT_FWC={fwc}: merge {1e3 * (time.perf_counter() - t0):.2f} ms, device {st.device_ms:.2f}", flush=True)
+    res[fwc] = fb.result()
+    print(", ".join(f"{n} {m:.3f}" for n, m in eng.phase_times() if m > 0.05), flush=True)
+print("all configs equal:", all(r == res["0"] for r in res.values()), "state equal:", res["1"][0] == full, flush=True)

@@ -24,9 +24,10 @@ pytestmark = pytest.mark.gpu
 CHUNK = 1024
 
 
-def _merge(batch, monkeypatch, capfd, fast):
+def _merge(batch, monkeypatch, capfd, fast, fwc="1"):
     monkeypatch.setenv("YCRDT_DECODE", "chunks")
     monkeypatch.setenv("YCRDT_DEBUG_DECODE", "1")
+    monkeypatch.setenv("YCRDT_FWC", fwc)  # record mode: "force" takes every multi-section large update
     if fast:
         monkeypatch.delenv("YCRDT_NO_FASTWALK", raising=False)
     else:
@@ -47,11 +48,13 @@ def _check(batch, monkeypatch, capfd):
         ref.apply_update(u)
     want = (ref.encode_state_as_update(), ref.encode_state_vector())
     fast, n_fast = _merge(batch, monkeypatch, capfd, True)
+    rec, n_rec = _merge(batch, monkeypatch, capfd, True, fwc="force")
     slow, n_slow = _merge(batch, monkeypatch, capfd, False)
     assert slow == want
     assert fast == want
+    assert rec == want
     assert n_slow == 0
-    return n_fast
+    return n_fast + n_rec
 
 
 def _replica(client, n_sets, n_keys, seed, value_len=3):
@@ -136,3 +139,38 @@ def test_multi_section_walk_resumes(fwm_max, n_clients, per_client, arrays, monk
     extra = ODoc(9)
     extra.map_set("users", "k2", any_int(6))
     _check([extra.encode_state_as_update(), snap], monkeypatch, capfd)
+
+
+def test_document_state_as_one_update_record_mode(monkeypatch, capfd):
+    """A C2-shaped document's merged state (hundreds of client sections, > 64 KiB) applied as ONE
+    update — crdt.js's full-state message — takes the record mode by default (k_fwc evaluates the
+    section step at every chain position; the walker follows the records): equal to the oracle,
+    to record mode off and to k_walk alone, and really taken."""
+    from crdt_amd.workload import C2, gen_map
+
+    cfg = dict(C2)
+    cfg.update(n_keys=2000, n_replicas=300, ops_per_replica=200)
+    ups, _ = gen_map(**cfg)
+    o = ODoc(0x7FFFFFF0)
+    for u in ups:
+        o.apply_update(u)
+    state = o.encode_state_as_update()
+    assert len(state) > 64 * 1024
+    want = (state, o.encode_state_vector())
+    outs = {}
+    for fwc in ("1", "0"):
+        outs[fwc] = _merge([state], monkeypatch, capfd, True, fwc=fwc)
+    slow, n_slow = _merge([state], monkeypatch, capfd, False)
+    assert outs["1"][0] == want and outs["0"][0] == want and slow == want
+    assert outs["1"][1] >= 0 and n_slow == 0  # (the base section may be left to the table walk)
+    # into a doc holding part of it (a device-resident state beside the update)
+    half = ODoc(0x7FFFFFF0)
+    for u in ups[: len(ups) // 2]:
+        half.apply_update(u)
+    for fwc in ("1", "0"):
+        monkeypatch.setenv("YCRDT_FWC", fwc)
+        d = crdt_amd.Doc(client_id=0x7FFFFFF0)
+        d.apply_update(half.encode_state_as_update())
+        d.encode_state_vector()
+        d.apply_update(state)
+        assert (d.encode_state_as_update(), d.encode_state_vector()) == want
