@@ -116,7 +116,16 @@ __device__ __forceinline__ void block_scan_u32_u64(const uint32_t* in, uint64_t*
 }
 // a phase boundary inside one workgroup where the phase before handed data over through memory-side
 // (L2) atomics as well as plain stores: agent-scope fences on both sides of the barrier, so no
-// wavefront reads an L1 line older than an atomic of the phase before
+// wavefront reads an L1 line older than an atomic of the phase before.
+// THE INVARIANT of the single-workgroup kernels (k_merge_small, k_view_small, k_decode_tail_small,
+// k_sections_small, k_encode_small), which separate their phases with a plain __syncthreads
+// (k_merge_small: by default; YCRDT_PHASE_FENCE=1 puts phase_sync back, A/B): a column written by ATOMICS in one
+// phase is read in a later phase only through ld_fresh (or block_scan_*<.., true>), never by a plain
+// load — plain stores reach the CU's vector L1 in order, atomics execute in L2 and leave a stale L1
+// line behind. The atomically written columns are: the key table's k_hash (CAS) and k_flags (Or),
+// the winner slots k_rootmax / g_maxchild (atomicMax settling pass), the client states cl_state
+// (atomicMax), the view representatives krep (atomicMin), the counters ctr->* (err, nsegs, ...).
+// tests/test_gpu_phase_fence.py runs the small-merge suites under both settings.
 __device__ __forceinline__ void phase_sync() {
   __threadfence();
   __syncthreads();

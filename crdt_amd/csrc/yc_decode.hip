@@ -639,6 +639,40 @@ __device__ __forceinline__ uint32_t chain_step(const uint8_t* __restrict__ b, ui
   const uint32_t d = chain_len(GlobalSrc{b}, b, p, uend);
   return p + (d ? d : 1u);
 }
+// Step table of a record-mode update (k_rtab): chain_len at every byte, computed once on the whole
+// chip, so the chunk chains, the sync rounds, the section-step records and the walkers of that update
+// follow the chain by one load per step instead of ~1 500 dependent instructions (k_spec held one
+// lane per 512-byte chunk: 16 K lanes, a wavefront per SIMD, 2.5 ms on a C2 document state).
+// tab: the update's table (indexed by p - ustart), nullptr for the other updates.
+__device__ __forceinline__ const uint32_t* rtab_of(const Work& w, uint32_t u) {
+  return w.rtab && w.fwc_off[u] != NONE ? w.rtab + w.fwc_off[u] : nullptr;
+}
+template <class S>
+__device__ __forceinline__ uint32_t tab_len(const uint32_t* __restrict__ tab, uint32_t ustart, const S& src, const uint8_t* __restrict__ b,
+                                            uint32_t p, uint32_t uend) {
+  return tab && p < uend ? tab[p - ustart] : chain_len(src, b, p, uend);
+}
+__device__ __forceinline__ uint32_t tab_step(const uint32_t* __restrict__ tab, uint32_t ustart, const uint8_t* __restrict__ b, uint32_t p,
+                                             uint32_t uend) {
+  const uint32_t d = tab_len(tab, ustart, GlobalSrc{b}, b, p, uend);
+  return p + (d ? d : 1u);
+}
+// one lane per byte of the record-mode updates (grid-stride over the chunk table); a byte whose
+// struct-kind bits name no struct (ref > Skip) is chain_len's 0 without a parse
+__global__ __launch_bounds__(256) void k_rtab(Work w) {
+  const uint32_t CH = w.schunk;
+  const uint64_t total = (uint64_t)w.ngroups * CH;
+  for (uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total; t += (uint64_t)gridDim.x * blockDim.x) {
+    const Group G = w.groups[t / CH];
+    const uint32_t p = G.start + (uint32_t)(t % CH);
+    if (p >= G.end) continue;
+    const uint32_t off = w.fwc_off[G.upd];
+    if (off == NONE) continue;
+    const uint8_t* __restrict__ b = win_bytes(w, upd_win(w, G.upd));
+    const uint32_t ustart = w.uoff[G.upd];
+    w.rtab[off + (p - ustart)] = (b[p] & 31u) > REF_SKIP ? 0u : chain_len(GlobalSrc{b}, b, p, G.uend);
+  }
+}
 
 // One lane per chunk (SCHUNK bytes of a large update): the chain from the chunk's start (below), every
 // visited position inside the chunk set in spec_bits (the lane owns the chunk's words: chunks and
@@ -655,6 +689,8 @@ __global__ __launch_bounds__(DL) void k_spec(Work w) {
   const uint32_t uw = upd_win(w, G.upd);
   const uint8_t* __restrict__ b = win_bytes(w, uw);
   const uint32_t uend = G.uend;
+  const uint32_t* __restrict__ tab = rtab_of(w, G.upd);
+  const uint32_t ustart = w.uoff[G.upd];
   uint32_t* slot = win + threadIdx.x * SPSTRIDE;
   LdsSrc src{b, slot, 0, 0};
   auto refill = [&](uint32_t p) {
@@ -688,9 +724,9 @@ __global__ __launch_bounds__(DL) void k_spec(Work w) {
         const uint32_t lim = min(G.start + 96u, G.end);
         for (uint32_t q = G.start; q < lim; ++q) {
           if (src.u8(q) != hint) continue;
-          const uint32_t d1 = chain_len(src, b, q, uend);
+          const uint32_t d1 = tab_len(tab, ustart, src, b, q, uend);
           if (!d1 || q + d1 >= uend || src.u8(q + d1) != hint) continue;
-          const uint32_t d2 = chain_len(src, b, q + d1, uend);
+          const uint32_t d2 = tab_len(tab, ustart, src, b, q + d1, uend);
           if (!d2 || q + d1 + d2 >= uend || src.u8(q + d1 + d2) != hint) continue;
           start = q;
           break;
@@ -709,14 +745,14 @@ __global__ __launch_bounds__(DL) void k_spec(Work w) {
         for (uint32_t q = G.start; q < lim; ++q) {
           const uint32_t c = src.u8(q);
           if ((c & 31u) > REF_SKIP) continue;
-          const uint32_t d1 = chain_len(src, b, q, uend);
+          const uint32_t d1 = tab_len(tab, ustart, src, b, q, uend);
           if (!d1 || q + d1 >= uend) continue;
-          const uint32_t d2 = chain_len(src, b, q + d1, uend);
+          const uint32_t d2 = tab_len(tab, ustart, src, b, q + d1, uend);
           if (!d2 || q + d1 + d2 >= uend) continue;
           if (src.u8(q + d1) == c && src.u8(q + d1 + d2) == c) { start = q; valid4 = NONE; break; }
           if (valid4 == NONE) {
-            const uint32_t q3 = q + d1 + d2, d3 = chain_len(src, b, q3, uend);
-            if (d3 && q3 + d3 < uend && chain_len(src, b, q3 + d3, uend)) valid4 = q;
+            const uint32_t q3 = q + d1 + d2, d3 = tab_len(tab, ustart, src, b, q3, uend);
+            if (d3 && q3 + d3 < uend && tab_len(tab, ustart, src, b, q3 + d3, uend)) valid4 = q;
           }
         }
         if (valid4 != NONE && start == G.start) start = valid4;
@@ -734,7 +770,7 @@ __global__ __launch_bounds__(DL) void k_spec(Work w) {
     }
     m |= 1ull << (p & 63);
     if (__ballot(src.wlen == SPW && p - src.s0 + DREFILL > SPW)) refill(p);  // the whole wavefront at once
-    const uint32_t d = chain_len(src, b, p, uend, w.dbg);
+    const uint32_t d = tab_len(tab, ustart, src, b, p, uend);
     p += d ? d : 1u;
   }
   const uint32_t wend = (G.end + 63) >> 6;
@@ -781,12 +817,14 @@ __global__ __launch_bounds__(256) void k_sync(Work w, const uint32_t* __restrict
       const uint32_t uw = upd_win(w, G.upd);
       const uint8_t* __restrict__ b = win_bytes(w, uw);
       uint64_t* __restrict__ spec = win_words(w.spec_bits, uw);
+      const uint32_t* __restrict__ tab = rtab_of(w, G.upd);
+      const uint32_t ustart = w.uoff[G.upd];
       uint32_t q = E, word = G.start >> 6;
       uint64_t m = 0;
       while (q < G.end && !((spec[q >> 6] >> (q & 63)) & 1ull)) {
         while ((q >> 6) != word) { spec[word] = m; m = 0; ++word; }
         m |= 1ull << (q & 63);
-        q = chain_step(b, q, G.uend);
+        q = tab_step(tab, ustart, b, q, G.uend);
       }
       if (q < G.end) {  // met the own chain at q: keep its positions from q on
         while ((q >> 6) != word) { spec[word] = m; m = 0; ++word; }
@@ -831,6 +869,8 @@ __global__ __launch_bounds__(64) void k_xtab(Work w) {
   if (e == 0) w.tentry[i] = NONE;
   __syncthreads();
   const LdsSrc src{b, cb, cs, wlen};
+  const uint32_t* __restrict__ tab = rtab_of(w, G.upd);
+  const uint32_t ustart = w.uoff[G.upd];
   uint32_t q = cs + e, k = 0, tgt = NONE, tidx = 0;
   bool active = true;
   for (;;) {
@@ -848,7 +888,7 @@ __global__ __launch_bounds__(64) void k_xtab(Work w) {
       const uint32_t v = rec[q - cs];
       if ((v >> 16) != e) { tgt = v >> 16; tidx = v & 0xFFFFu; active = false; }
       else {
-        const uint32_t d = chain_len(src, b, q, uend);
+        const uint32_t d = tab_len(tab, ustart, src, b, q, uend);
         q += d ? d : 1u;
         ++k;
       }
@@ -944,6 +984,7 @@ __global__ __launch_bounds__(64) void k_walk(Work w) {
   uint64_t* __restrict__ fbits = win_words(w.final_bits, uw);
   uint64_t* __restrict__ sbits = win_words(w.sec_bits, uw);
   const uint32_t ustart = w.uoff[u], uend = ustart + w.ulen[u];
+  const uint32_t* __restrict__ stab = rtab_of(w, u);  // (step table; `tab` is the exit tables)
   const uint32_t CH = w.schunk;
   const uint32_t c0 = w.ugroup[u], nch = (w.ulen[u] + CH - 1) / CH;
   uint32_t* err = &w.ctr->err;
@@ -1046,7 +1087,7 @@ __global__ __launch_bounds__(64) void k_walk(Work w) {
         while (q < ce && kk < limit && !((mc[(q - cs) >> 6] >> (q & 63)) & 1ull)) {
           mw[(q - cs) >> 6] |= 1ull << (q & 63);
           if (src.wlen == DW && q - src.s0 + DREFILL > DW) refill(q);
-          const uint32_t d = chain_len(src, b, q, uend);
+          const uint32_t d = tab_len(stab, ustart, src, b, q, uend);
           q += d ? d : 1u;
           ++kk;
         }
@@ -1111,7 +1152,7 @@ __global__ __launch_bounds__(64) void k_walk(Work w) {
             Lp = select_from(spec, q, rr - k);
             or_range(fbits, spec, q, Lp + 1);
           }
-          np = chain_step(b, Lp, uend);
+          np = tab_step(stab, ustart, b, Lp, uend);
         }
         p = __shfl(np, jl);
         r = 0;
@@ -1311,7 +1352,8 @@ __device__ __forceinline__ uint32_t nth_set1(uint64_t x, uint32_t k) {  // posit
 struct FwcRes { uint32_t next, e, k0, why; };  // next header (NONE: not vouched), chain range end, walked structs, reason
 __device__ __forceinline__ bool spec_at(const uint64_t* __restrict__ spec, uint32_t q) { return (spec[q >> 6] >> (q & 63)) & 1ull; }
 __device__ __forceinline__ FwcRes fwc_eval(const Work& w, const uint8_t* __restrict__ b, const uint64_t* __restrict__ spec, uint32_t ustart,
-                                           uint32_t uend, uint32_t c0, uint32_t nch, uint32_t hdr, uint32_t walk_max) {
+                                           uint32_t uend, uint32_t c0, uint32_t nch, uint32_t hdr, uint32_t walk_max,
+                                           const uint32_t* __restrict__ tab) {
   FwcRes r{NONE, NONE, 0u, 0u};
   uint32_t p = hdr;
   bool ok = hdr < uend;
@@ -1326,7 +1368,7 @@ __device__ __forceinline__ FwcRes fwc_eval(const Work& w, const uint8_t* __restr
   uint32_t q = p1, k0 = 0;
   for (uint32_t steps = 0; q < uend && k0 < n && !spec_at(spec, q); ++steps) {
     if (steps == walk_max) { r.why = walk_max < FWM_WALK ? 8u : 5u; return r; }
-    const uint32_t dq = chain_len(GlobalSrc{b}, b, q, uend);
+    const uint32_t dq = tab_len(tab, ustart, GlobalSrc{b}, b, q, uend);
     if (!dq) { r.why = 4; return r; }  // no struct parses: k_walk reports it
     q += dq;
     ++k0;
@@ -1354,7 +1396,7 @@ __device__ __forceinline__ FwcRes fwc_eval(const Work& w, const uint8_t* __restr
     fa = ustart + lo * CH;
   }
   const uint32_t Lp = select_from(spec, fa, rem);
-  const uint32_t dl = Lp < uend ? chain_len(GlobalSrc{b}, b, Lp, uend) : 0u;
+  const uint32_t dl = Lp < uend ? tab_len(tab, ustart, GlobalSrc{b}, b, Lp, uend) : 0u;
   if (!dl || Lp + dl > uend) { r.why = 7; return r; }  // the last struct's end is unknown
   r.next = Lp + dl;
   r.e = Lp + 1;
@@ -1377,7 +1419,7 @@ __global__ __launch_bounds__(256) void k_fwc(Work w) {
     const uint32_t ustart = w.uoff[u], uend = ustart + w.ulen[u], c0 = w.ugroup[u], nch = (w.ulen[u] + w.schunk - 1) / w.schunk;
     for (uint64_t x = range_word(spec, wd, G.start, G.end); x; x &= x - 1) {
       const uint32_t c = wd * 64 + (uint32_t)__ffsll((long long)x) - 1;
-      const FwcRes r = fwc_eval(w, b, spec, ustart, uend, c0, nch, c, w.fwc_walk);
+      const FwcRes r = fwc_eval(w, b, spec, ustart, uend, c0, nch, c, w.fwc_walk, rtab_of(w, u));
       w.fwc[off + (c - ustart)] = make_uint4(r.next, r.e, r.k0, r.why);
     }
   }
@@ -1401,7 +1443,7 @@ __device__ __forceinline__ void fwm_records(const Work& w, uint32_t u, uint32_t 
       r = FwcRes{x.x, x.y, x.z, x.w};
     }
     if (r.next == NONE && r.why == 8u) {  // off the chain, or walked past k_fwc's bound
-      r = fwc_eval(w, b, spec, ustart, uend, c0, nch, h, FWM_WALK);
+      r = fwc_eval(w, b, spec, ustart, uend, c0, nch, h, FWM_WALK, rtab_of(w, u));
       if (w.dbg) atomicAdd(&w.dbg[16], 1ull);
     }
     if (r.next == NONE) {
@@ -1458,7 +1500,7 @@ __global__ __launch_bounds__(256) void k_fwc_commit(Work w) {
       uint32_t x = p1, k0 = 0;
       while (n && k0 < n && x < uend && !spec_at(spec, x)) {
         atomicOr((unsigned long long*)&fbits[x >> 6], 1ull << (x & 63));
-        x = chain_step(b, x, uend);
+        x = tab_step(rtab_of(w, u), w.uoff[u], b, x, uend);
         ++k0;
       }
       w.fwsec[2 * (sbase + s)] = n ? x : p1;  // the chain range [q, e) (k_fastmark)
@@ -2061,7 +2103,7 @@ __global__ __launch_bounds__(DL) void k_xmark(Work w) {
     }
     m |= 1ull << (p & 63);
     if (src.wlen == DW && p - src.s0 + DREFILL > DW) refill(p);
-    const uint32_t d = chain_len(src, b, p, uend);
+    const uint32_t d = tab_len(rtab_of(w, G.upd), w.uoff[G.upd], src, b, p, uend);
     p += d ? d : 1u;
   }
   if (m) atomicOr((unsigned long long*)&fbits[word], (unsigned long long)m);
@@ -2069,6 +2111,7 @@ __global__ __launch_bounds__(DL) void k_xmark(Work w) {
 
 void launch_chunks(const Work& w, hipStream_t s) {
   if (w.ngroups) {
+    if (w.rtab) hipLaunchKernelGGL(k_rtab, dim3((uint32_t)std::min<uint64_t>((uint64_t)w.ngroups * w.schunk / 256 + 1, 16384)), dim3(256), 0, s, w);
     hipLaunchKernelGGL(k_spec, dim3((w.ngroups + DL - 1) / DL), dim3(DL), 0, s, w);
     for (uint32_t r = 0; r < SYNC_ROUNDS; ++r)
       hipLaunchKernelGGL(k_sync, dim3((w.ngroups + 255) / 256), dim3(256), 0, s, w,

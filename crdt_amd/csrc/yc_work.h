@@ -93,6 +93,7 @@ struct Work {
   uint4* fwc = nullptr;            // record mode (k_fwc): per byte of a multi-section large update, the section
                                    // step from a header there {next header, chain range end, walked, why}
   const uint32_t* fwc_off = nullptr; // [nupd] record base of each record-mode update, NONE otherwise (null: none)
+  uint32_t* rtab = nullptr;        // record mode: chain_len at every byte of those updates (k_rtab), indexed as fwc
   uint32_t fwc_walk = 256;         // k_fwc's walk bound (YCRDT_FWC_WALK; at FWM_WALK the walker never re-evaluates a chain-position header)
   uint16_t* wlen = nullptr;        // [nsmall * 16384] few small updates: the chain step at every position (k_wlen)
   uint32_t schunk = SCHUNK;        // chunk bytes of this batch's large updates (<= SCHUNK)

@@ -10,7 +10,14 @@ router's own peer sockets, and nothing here imports torch.
     uid = hub.bcast(Comm.unique_id() if rank == 0 else None)
     comm = Comm(engine, world, rank, uid)            # RCCL, one rank per GPU
     comm = Comm.over_hub(engine, hub)                # or the library's collectives over the hub
+
+Trust model: the hub is a job-internal channel. Bind it to loopback or a trusted interface. Every
+rank sends a job token in its handshake (YCRDT_HUB_TOKEN, else a token derived from the launcher's
+MASTER_ADDR / MASTER_PORT), and rank 0 drops a connection whose token or rank is wrong. Frames are
+capped at YCRDT_HUB_MAX_FRAME bytes (default 4 GiB), so a peer cannot make a rank allocate more.
 """
+import hashlib
+import os
 import socket
 import struct
 import time
@@ -18,6 +25,14 @@ import time
 import numpy as np
 
 _HDR = struct.Struct("<Q")
+_MAX_FRAME = int(os.environ.get("YCRDT_HUB_MAX_FRAME", str(4 << 30)))
+
+
+def _job_token(addr: str, port: int) -> bytes:
+    tok = os.environ.get("YCRDT_HUB_TOKEN")
+    if tok is None:
+        tok = f"ycrdt-hub:{os.environ.get('MASTER_ADDR', addr)}:{os.environ.get('MASTER_PORT', port)}"
+    return hashlib.sha256(tok.encode()).digest()
 
 
 def _send(sock, payload: bytes):
@@ -38,6 +53,8 @@ def _recv_exact(sock, n: int) -> bytes:
 
 def _recv(sock) -> bytes:
     (n,) = _HDR.unpack(_recv_exact(sock, _HDR.size))
+    if n > _MAX_FRAME:
+        raise ConnectionError(f"host hub: a {n}-byte frame exceeds the {_MAX_FRAME}-byte cap")
     return _recv_exact(sock, n)
 
 
@@ -50,6 +67,7 @@ class HostHub:
         self._sock = None
         if world == 1:
             return
+        token = _job_token(addr, port)
         if rank == 0:
             srv = socket.socket(socket.AF_INET, socket.SOCK_STREAM)
             srv.setsockopt(socket.SOL_SOCKET, socket.SO_REUSEADDR, 1)
@@ -61,9 +79,15 @@ class HostHub:
                     c, _ = srv.accept()
                     c.setsockopt(socket.IPPROTO_TCP, socket.TCP_NODELAY, 1)
                     c.settimeout(timeout)
-                    (r,) = struct.unpack("<I", _recv_exact(c, 4))
-                    if not 0 < r < world or r in self._peers:
-                        raise ConnectionError(f"host hub: unexpected rank {r}")
+                    try:
+                        hello = _recv_exact(c, 4 + len(token))
+                    except (OSError, ConnectionError):
+                        c.close()
+                        continue
+                    (r,) = struct.unpack("<I", hello[:4])
+                    if hello[4:] != token or not 0 < r < world or r in self._peers:
+                        c.close()  # not a rank of this job: dropped, the hub keeps waiting
+                        continue
                     self._peers[r] = c
             finally:
                 srv.close()
@@ -78,7 +102,7 @@ class HostHub:
                         raise
                     time.sleep(0.05)
             s.setsockopt(socket.IPPROTO_TCP, socket.TCP_NODELAY, 1)
-            s.sendall(struct.pack("<I", rank))
+            s.sendall(struct.pack("<I", rank) + token)
             self._sock = s
 
     def allgather(self, payload: bytes) -> list:

@@ -57,3 +57,60 @@ def test_hosthub(world):
         assert r["sum"] == [sum(range(world)), (0xFFFFFFFF * world) & 0xFFFFFFFF, sum(7 * k + 1 for k in range(world))]
         assert r["max"] == [world - 1, 0xFFFFFFFF, 7 * (world - 1) + 1]
         assert not r["torch"]
+
+
+def _rogue(port, kind):
+    """A connection that is no rank of the job: a wrong token, or a length header past the cap."""
+    import struct
+    import time
+
+    for _ in range(200):
+        try:
+            s = socket.create_connection(("127.0.0.1", port), timeout=10)
+            break
+        except OSError:
+            time.sleep(0.05)
+    if kind == "token":
+        s.sendall(struct.pack("<I", 1) + b"\0" * 32)
+    else:
+        s.sendall(b"\xff" * 64)
+    time.sleep(0.5)
+    s.close()
+
+
+def test_hosthub_drops_connections_without_the_job_token():
+    """Rank 0 drops a connection whose handshake carries a wrong token (the hub
+    accepted any peer that sent a rank number) and still forms the job with the real ranks."""
+    import threading
+
+    ctx = mp.get_context("spawn")
+    q = ctx.SimpleQueue()
+    port = _free_port()
+    p0 = ctx.Process(target=_worker, args=(2, 0, port, q))
+    p0.start()
+    for kind in ("token", "junk"):
+        t = threading.Thread(target=_rogue, args=(port, kind))
+        t.start()
+        t.join(30)
+    p1 = ctx.Process(target=_worker, args=(2, 1, port, q))
+    p1.start()
+    p0.join(120)
+    p1.join(120)
+    assert [p0.exitcode, p1.exitcode] == [0, 0]
+    res = sorted([q.get() for _ in range(2)], key=lambda r: r["rank"])
+    assert res[1]["bcast"] == b"unique-id-from-rank-0"
+
+
+def test_hosthub_frame_cap():
+    import struct
+
+    from crdt_amd import hosthub
+
+    a, b = socket.socketpair()
+    try:
+        a.sendall(struct.pack("<Q", hosthub._MAX_FRAME + 1))
+        with pytest.raises(ConnectionError):
+            hosthub._recv(b)
+    finally:
+        a.close()
+        b.close()
