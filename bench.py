@@ -349,7 +349,7 @@ def c3_leg(eng, n_items, steps=3):
     return res
 
 
-def full_state_leg(eng, name, ups, full, reps=3):
+def full_state_leg(eng, name, ups, full, reps=3, small_ops=0):
     """crdt.js's wire shape (crdt.js:288 sync step 2, :443 every local op, :79-98 LevelDB replay):
     a peer's FULL state arrives as ONE multi-client update. Timed with the update resident in HBM
     (ycrdt_batch_merge): merged alone (an empty doc applying it) and behind the state of a doc
@@ -382,8 +382,45 @@ def full_state_leg(eng, name, ups, full, reps=3):
     got = d.encode_state_as_update()
     res["doc_apply_ms"] = round((time.perf_counter() - t0) * 1e3, 3)
     res["doc_equal"] = got == full
+    if small_ops:
+        res["small_into_large"] = small_into_large(eng, d, full, small_ops)
     del d
     return res
+
+
+def small_into_large(eng, d, full, n_ops, root="users"):
+    """crdt.js's steady state on a large document (crdt.js:294 then :297-305): ONE small remote
+    update (a peer's map set, sent as a delta) applied to a doc holding the full state, then the
+    read that merges it. Per apply: Y.applyUpdate + Y.encodeStateVector (the merge), and separately
+    the crdt.c rebuild (toJSON of the root map). The peer's deltas come from the oracle port holding
+    the same state; the doc's final state is compared with the oracle's."""
+    from oracle.yref import Doc as ODoc
+
+    peer = ODoc(0x5EED0001)
+    peer.apply_update(full)
+    deltas = []
+    for i in range(n_ops):
+        sv = peer.encode_state_vector()
+        peer.map_set(root, "k%d" % (i * 7919 % 100_000), _any_str("w%d" % i))
+        deltas.append(peer.encode_state_as_update(sv))
+    d.encode_state_vector()
+    merge_ms, json_ms = [], []
+    for u in deltas:
+        t0 = time.perf_counter()
+        d.apply_update(u)
+        d.encode_state_vector()
+        t1 = time.perf_counter()
+        merge_ms.append((t1 - t0) * 1e3)
+    for u in deltas[:3]:  # (toJSON of a 100 k-key map: timed on a few applies)
+        t1 = time.perf_counter()
+        d.root_json(root, "map")
+        json_ms.append((time.perf_counter() - t1) * 1e3)
+    merge_ms.sort()
+    same = d.encode_state_as_update() == peer.encode_state_as_update()
+    return {"applies": n_ops, "delta_bytes": len(deltas[-1]), "apply_merge_ms_median": round(merge_ms[len(merge_ms) // 2], 3),
+            "apply_merge_ms_min": round(merge_ms[0], 3), "tojson_ms": round(min(json_ms), 3), "parity": same,
+            "includes": "per apply: host validation + queue, the merge of (doc state + delta) on the device (the state is "
+                        "re-decoded: record mode + step table), the state-vector read-back"}
 
 
 def billion_leg(eng, cfg, gen_map, n_docs, reps=3):
@@ -1034,7 +1071,7 @@ def run_rank(args, report=None):
         ingest = fleet_ingest_leg(eng, args.fleet_docs)
     side = rank == 0 and world == 1 and not args.only_headline and not args.billion
     loop = apply_loop_leg(eng, updates, out_update) if side else None
-    full_c2 = full_state_leg(eng, "one C2 document's merged state (1 001 clients) as one update", updates, out_update) if side else None
+    full_c2 = full_state_leg(eng, "one C2 document's merged state (1 001 clients) as one update", updates, out_update, small_ops=30) if side else None
     per_op = per_op_leg(eng) if side and not args.no_per_op else None
     c3 = c3_leg(eng, args.c3_items) if side and args.c3_items > 0 else None
     c4 = c4_leg(eng) if side and not args.no_c4 else None

@@ -686,6 +686,7 @@ __global__ __launch_bounds__(DL) void k_spec(Work w) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= w.ngroups) return;
   const Group G = w.groups[i];
+  if (w.ufail[G.upd] >= UF_PRE) { w.cexit[i] = G.end; return; }  // (decoded already — by its marks, or whole by k_prewalk: its chunks serve the grid delete-set decode only)
   const uint32_t uw = upd_win(w, G.upd);
   const uint8_t* __restrict__ b = win_bytes(w, uw);
   const uint32_t uend = G.uend;
@@ -801,7 +802,7 @@ __global__ __launch_bounds__(256) void k_sync(Work w, const uint32_t* __restrict
   uint32_t X = xin[i];
   if (round > 0 && !w.ctr->sync_changed[round - 1]) { xout[i] = X; return; }
   const Group G = w.groups[i];
-  if (G.start != w.uoff[G.upd]) {  // chunks of one update are consecutive
+  if (G.start != w.uoff[G.upd] && w.ufail[G.upd] < UF_PRE) {  // chunks of one update are consecutive
     const uint32_t E = xin[i - 1];
     uint32_t* jumped = w.sent + w.ngroups + 1;
     if (E >= G.end) {
@@ -972,7 +973,7 @@ __global__ __launch_bounds__(64) void k_walk(Work w) {
   __shared__ uint32_t ent[65], cnt[64], nknown;
   if (blockIdx.x >= w.nbig) return;
   const uint32_t u = w.ulist[blockIdx.x];
-  if (w.ufail[u] == 2u || w.ufail[u] == 3u) return;  // k_fastwalk / k_fastwalk_multi did it
+  if (w.ufail[u] == 2u || w.ufail[u] == 3u || w.ufail[u] >= UF_PRE) return;  // k_fastwalk / k_fastwalk_multi / k_predecoded / k_prewalk did it
   if (TABLES && w.ufail[u] != 1u && w.ufail[u] != 5u) return;
   // k_fastwalk_multi vouched for the first sections (ufail 4; 5 once handed to the tables): the
   // walk resumes at the next one
@@ -1228,7 +1229,7 @@ __global__ __launch_bounds__(64) void k_fastwalk(Work w) {
   const uint32_t ustart = w.uoff[u], uend = ustart + w.ulen[u];
   const uint32_t CH = w.schunk;
   const uint32_t c0 = w.ugroup[u], nch = (w.ulen[u] + CH - 1) / CH;
-  if (!w.ulen[u]) return;
+  if (!w.ulen[u] || w.ufail[u] >= UF_PRE) return;
   uint32_t p = ustart;
   bool ok = true;
   const uint32_t nsec = rd_vu(b, p, uend, ok);
@@ -1775,7 +1776,7 @@ __global__ __launch_bounds__(256) void k_fastmark(Work w) {
     const Group gr = w.groups[t / wpc];
     const uint32_t u = gr.upd;
     const uint32_t uf = w.ufail[u];
-    if (uf < 2u) continue;
+    if (uf < 2u || uf >= UF_PRE) continue;
     const uint32_t wd = (gr.start >> 6) + (uint32_t)(t % wpc);
     if (uf >= 3u) {  // several sections (k_fastwalk_multi): the chain ranges meeting this word
       // (ufail 4: only its first fw[2u] sections; k_walk resumes past them)
@@ -2109,7 +2110,133 @@ __global__ __launch_bounds__(DL) void k_xmark(Work w) {
   if (m) atomicOr((unsigned long long*)&fbits[word], (unsigned long long)m);
 }
 
+// A doc state decoded by the encode that produced it (PreMarks, k_state_marks): its bitmap words
+// copied into the batch's (the state is 64-byte aligned: word for word), its section records
+// appended, its delete-set start set. check: the state was decoded the usual way as well — every
+// word and the delete-set start must agree (YCRDT_PREDECODE=check, tests).
+__global__ void k_predecoded(Work w, uint32_t u, PreMarks m, uint32_t check) {
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x, gs = gridDim.x * blockDim.x;
+  const uint32_t uw = upd_win(w, u), w0 = w.uoff[u] >> 6;
+  uint64_t* __restrict__ fb = win_words(w.final_bits, uw);
+  uint64_t* __restrict__ sb = win_words(w.sec_bits, uw);
+  const uint32_t nsec = min(m.meta[0], m.cap_secs);
+  if (check) {
+    for (uint32_t k = t; k < m.nw; k += gs)
+      if (fb[w0 + k] != m.fbits[k] || sb[w0 + k] != m.sbits[k]) {
+        raise_err(&w.ctr->err, ERR_DECODE);
+        const bool f = fb[w0 + k] != m.fbits[k];
+        w.ctr->err_info = 0xC0DE0000u | (f ? 0u : 0x8000u) | min(k, 0x7FFFu);  // (for the message: check() in yc_engine.hip)
+        const uint64_t a = f ? fb[w0 + k] : sb[w0 + k], z = f ? m.fbits[k] : m.sbits[k];
+        w.ctr->pad[8] = (uint32_t)a; w.ctr->pad[9] = (uint32_t)(a >> 32); w.ctr->pad[10] = (uint32_t)z; w.ctr->pad[11] = (uint32_t)(z >> 32) | (f ? 0u : 0u);
+      }
+    if (t == 0 && w.dsstart[u] != w.uoff[u] + m.meta[1]) {
+      raise_err(&w.ctr->err, ERR_DECODE);
+      w.ctr->err_info = 0xC0DF0000u;
+      w.ctr->pad[8] = w.dsstart[u]; w.ctr->pad[9] = w.uoff[u] + m.meta[1]; w.ctr->pad[10] = m.meta[0]; w.ctr->pad[11] = m.nw;
+    }
+    return;
+  }
+  for (uint32_t k = t; k < m.nw; k += gs) { fb[w0 + k] = m.fbits[k]; sb[w0 + k] = m.sbits[k]; }
+  __shared__ uint32_t sbase, part[256];
+  if (blockIdx.x == 0) {
+    if (threadIdx.x == 0) sbase = atomicAdd(&w.ctr->nsections, nsec);
+    __syncthreads();
+    if (sbase + nsec > w.cap_sections) { if (threadIdx.x == 0) raise_err(&w.ctr->err, ERR_CAPACITY); return; }
+    // the records in the update's byte order (descending client slot), compacted 256 at a time
+    const uint32_t nslots = m.meta[2];
+    uint32_t out = 0;
+    for (uint32_t r0 = 0; r0 < nslots; r0 += 256) {
+      const uint32_t r = r0 + threadIdx.x;
+      Section sec;
+      const bool has = r < nslots && (sec = m.secs[nslots - 1 - r]).n != 0;
+      part[threadIdx.x] = has ? 1u : 0u;
+      __syncthreads();
+      for (uint32_t off = 1; off < 256; off <<= 1) {
+        const uint32_t x = threadIdx.x >= off ? part[threadIdx.x - off] : 0u;
+        __syncthreads();
+        part[threadIdx.x] += x;
+        __syncthreads();
+      }
+      if (has && out + part[threadIdx.x] - 1 < nsec) {
+        sec.upd = u;
+        sec.first_pos += w.uoff[u];
+        w.sections[sbase + out + part[threadIdx.x] - 1] = sec;
+      }
+      out += part[255];
+      __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+      w.usec_start[u] = sbase;
+      w.usec_n[u] = nsec;
+      w.ufail[u] = UF_PRE;  // (every walker leaves it alone; its chunks serve the grid delete-set decode)
+      w.dsstart[u] = w.uoff[u] + m.meta[1];
+    }
+  }
+}
+void launch_predecoded(const Work& w, uint32_t u, const PreMarks& m, bool check, hipStream_t s) {
+  hipLaunchKernelGGL(k_predecoded, dim3(std::min<uint32_t>(m.nw / 256 + 1, 1024)), dim3(256), 0, s, w, u, m, check ? 1u : 0u);
+}
+
+// Large updates with a short struct section — a delta carrying the doc's whole delete set (the sync
+// reply, crdt.js:288, Y.encodeStateAsUpdate(doc, sv) always writes the full delete set), a few
+// structs in front of hundreds of KB of ranges: one lane per large update walks the struct section
+// exactly for up to PREWALK_STEPS structs. When it reaches the end, the update is decoded (sections,
+// struct starts, delete-set start; ufail UF_WALKED) and the chunk chains skip its chunks, whose
+// speculative walks over the delete set's bytes were all garbage (a 228 KB delta: k_spec + k_sync
+// 2.4 ms at 14 wavefronts). Otherwise it leaves the update to the chunk path untouched.
+constexpr uint32_t PREWALK_STEPS = 64;
+__global__ void k_prewalk(Work w) {
+  const uint32_t bi = blockIdx.x * blockDim.x + threadIdx.x;
+  if (bi >= w.nbig) return;
+  const uint32_t u = w.ulist[bi];
+  if (w.ufail[u] || !w.ulen[u]) return;
+  const uint32_t uw = upd_win(w, u);
+  const uint8_t* __restrict__ b = win_bytes(w, uw);
+  const uint32_t ustart = w.uoff[u], uend = ustart + w.ulen[u];
+  uint32_t p = ustart, steps = 0;
+  bool ok = true;
+  const uint32_t nsec = rd_vu(b, p, uend, ok);
+  if (!ok || nsec > 8) return;
+  uint32_t hp[8];  // the section headers
+  for (uint32_t s = 0; s < nsec; ++s) {
+    hp[s] = p;
+    const uint32_t n = rd_vu(b, p, uend, ok);
+    rd_vu(b, p, uend, ok);
+    rd_vu(b, p, uend, ok);
+    if (!ok || n > PREWALK_STEPS - steps) return;
+    for (uint32_t k = 0; k < n; ++k) {
+      const uint32_t d = p < uend ? chain_len(GlobalSrc{b}, b, p, uend) : 0u;
+      if (!d || p + d > uend) return;  // (malformed: the walkers report it)
+      p += d;
+    }
+    steps += n;
+  }
+  // decoded: the records, the marks, the delete-set start
+  const uint32_t sbase = atomicAdd(&w.ctr->nsections, nsec);
+  if (sbase + nsec > w.cap_sections) { raise_err(&w.ctr->err, ERR_CAPACITY); return; }
+  uint64_t* __restrict__ fbits = win_words(w.final_bits, uw);
+  uint64_t* __restrict__ sbits = win_words(w.sec_bits, uw);
+  for (uint32_t s = 0; s < nsec; ++s) {
+    uint32_t q = hp[s];
+    const uint32_t n = rd_vu(b, q, uend, ok), client = rd_vu(b, q, uend, ok), clock = rd_vu(b, q, uend, ok);
+    Section sec;
+    sec.upd = u; sec.n = n; sec.client = client; sec.clock = clock;
+    sec.first_pos = n ? q : NONE; sec.cidx = NONE; sec.first_idx = NONE; sec.pad = 0;
+    w.sections[sbase + s] = sec;
+    if (n) atomicOr((unsigned long long*)&sbits[q >> 6], 1ull << (q & 63));
+    for (uint32_t k = 0; k < n; ++k) {
+      atomicOr((unsigned long long*)&fbits[q >> 6], 1ull << (q & 63));
+      q += chain_len(GlobalSrc{b}, b, q, uend);
+    }
+  }
+  w.usec_start[u] = sbase;
+  w.usec_n[u] = nsec;
+  w.dsstart[u] = p;
+  w.ufail[u] = UF_WALKED;
+}
+
 void launch_chunks(const Work& w, hipStream_t s) {
+  if (w.nbig && !w.force_xtab && !env_off("YCRDT_PREWALK")) hipLaunchKernelGGL(k_prewalk, dim3(w.nbig / 64 + 1), dim3(64), 0, s, w);
   if (w.ngroups) {
     if (w.rtab) hipLaunchKernelGGL(k_rtab, dim3((uint32_t)std::min<uint64_t>((uint64_t)w.ngroups * w.schunk / 256 + 1, 16384)), dim3(256), 0, s, w);
     hipLaunchKernelGGL(k_spec, dim3((w.ngroups + DL - 1) / DL), dim3(DL), 0, s, w);

@@ -676,6 +676,39 @@ void launch_write_structs(const Work& w, uint32_t nsegs, uint32_t nclients, hipS
   hipLaunchKernelGGL(k_write_general, dim3(std::min<uint32_t>(nsegs / 256 + 1, GEN_GRID)), dim3(256), 0, s, w, nclients);
 }
 
+// The decode of the update just encoded, from the encoder's own layout (a doc's merged state: the
+// doc's next merge reads it instead of parsing the state, yc_engine.hip commit_merge): every output
+// struct's start (out_pos), every client block's section record and first struct, the delete set's
+// start. The bitmaps were zeroed by the caller; the count of sections is meta[0] (atomic).
+__global__ void k_state_marks(Work w, uint32_t nout, uint32_t nclients, PreMarks m) {
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t < nout && w.o_size[t]) {
+    const uint32_t p = (uint32_t)out_pos(w, t);
+    atomicOr((unsigned long long*)&m.fbits[p >> 6], 1ull << (p & 63));
+  }
+  // the client blocks: slot c holds client c's record (n = 0: no block); struct blocks are written
+  // in descending client order (both compat modes), which k_predecoded restores when it compacts
+  if (t < nclients && t < m.cap_secs) {
+    const uint32_t n = ccol(w, CC_NINCL)[t];
+    Section sec;
+    sec.upd = 0; sec.n = n; sec.client = w.cl_vals[t]; sec.clock = w.cl_start[t];
+    sec.first_pos = NONE; sec.cidx = NONE; sec.first_idx = NONE; sec.pad = 0;
+    if (n) {
+      const uint32_t first = (uint32_t)(w.ctr->pad[3] + ccol64(w, CC64_BLKPOS)[t] + ccol(w, CC_HDR)[t]);
+      sec.first_pos = first;
+      atomicOr((unsigned long long*)&m.sbits[first >> 6], 1ull << (first & 63));
+      atomicAdd(&m.meta[0], 1u);
+    }
+    m.secs[t] = sec;
+  }
+  if (t == 0) { m.meta[1] = (uint32_t)w.ctr->ds_base; m.meta[2] = min(nclients, m.cap_secs); }
+}
+void launch_state_marks(const Work& w, uint32_t nout, uint32_t nclients, const PreMarks& m, hipStream_t s) {
+  fill_u32_multi({{(uint32_t*)m.fbits, 2ull * m.nw, 0u}, {(uint32_t*)m.sbits, 2ull * m.nw, 0u}, {m.meta, 3, 0u}}, s);
+  const uint32_t n = std::max(nout, nclients) + 1;
+  hipLaunchKernelGGL(k_state_marks, dim3(n / 256 + 1), dim3(256), 0, s, w, nout, nclients, m);
+}
+
 // Per-document byte ranges of a multi-document encode. Clients are laid out in (document, client)
 // descending order, so each document's struct blocks, delete-set blocks and state-vector entries
 // are contiguous: rng[9d + 0..8] = struct (lo, hi, clients), delete set (lo, hi, clients),

@@ -276,6 +276,13 @@ struct ycrdt_doc {
   std::vector<Queued> queue;
   size_t queue_bytes = 0;
   IngestState ing;       // Yjs pendingStructs / pendingDs / store client order (yc_ingest.h)
+  // the decode of `state`, written by the encode that produced it (k_state_marks): the next merge of
+  // the doc reads its state's struct / section starts from here instead of parsing it (k_predecoded;
+  // YCRDT_PREDECODE=0: off, =check: decoded both ways and compared). marks_len: the state length the
+  // marks describe (0: none)
+  DevBuf marks;
+  size_t marks_len = 0;
+  uint32_t marks_nw = 0, marks_cap = 0;
   bool track_local = false;                 // ycrdt_doc_track_local: record local-op updates
   std::vector<std::vector<uint8_t>> local;  // local-op updates since the last ycrdt_doc_take_local_update
   size_t local_bytes = 0;
@@ -301,6 +308,12 @@ struct ycrdt_batch {
   // its records (one per byte) or NONE; fwc_recs records in all
   std::vector<uint32_t> fwc_off;
   uint64_t fwc_recs = 0;
+  // a source decoded by its own encode (a doc state with PreMarks): its index among the sources
+  // (-1: none), the marks, whether to check them against a real decode instead, its update index
+  int pre_src = -1;
+  PreMarks pre;
+  bool pre_check = false;
+  uint32_t pre_u = 0;
   uint64_t nbytes = 0;          // span of the batch buffer (windows before the last are 2^32 bytes)
   uint64_t in_bytes = 0;
   bool merged = false;
@@ -384,8 +397,9 @@ void layout(ycrdt_batch* b, const std::vector<Src>& src, std::vector<uint32_t>& 
   const char* mode = getenv("YCRDT_DECODE");
   const int force = mode && (!strcmp(mode, "chunks") || !strcmp(mode, "tables") || !strcmp(mode, "xtab")) ? 1
                     : mode && !strcmp(mode, "direct") ? 2 : 0;
+  const int pre = b->pre_check ? -1 : b->pre_src;  // (decoded by k_predecoded: in the big list for its delete set only)
   size_t nsmall = 0;
-  for (const Src& x : src) nsmall += x.len <= DIRECT_MAX_BYTES;
+  for (size_t i = 0; i < src.size(); ++i) nsmall += src[i].len <= DIRECT_MAX_BYTES && (int)i != pre;
   // small updates are parsed directly however few there are: one lane each (k_direct) when they
   // fill wavefronts, else one wavefront each (k_wdecode); YCRDT_DIRECT_WAVE=0 keeps the lane
   // kernel, and then few small updates take the chunk path as before
@@ -399,8 +413,8 @@ void layout(ycrdt_batch* b, const std::vector<Src>& src, std::vector<uint32_t>& 
   // state and a few updates: the per-op path) takes short chunks; big ones the full SCHUNK
   // (short enough that the walker's 64 lanes still span the largest update in one step)
   size_t big_bytes = 0, big_max = 0;
-  for (const Src& x : src)
-    if (x.len && !direct(x.len)) { big_bytes += x.len; big_max = std::max(big_max, x.len); }
+  for (size_t i = 0; i < src.size(); ++i)
+    if (src[i].len && (!direct(src[i].len) || (int)i == pre)) { big_bytes += src[i].len; big_max = std::max(big_max, src[i].len); }
   b->schunk = SCHUNK;
   if (big_bytes <= SMALL_BATCH_BYTES)
     while (b->schunk > SCHUNK_SMALL && (size_t)(b->schunk / 2) * 64 >= big_max) b->schunk /= 2;
@@ -430,11 +444,13 @@ void layout(ycrdt_batch* b, const std::vector<Src>& src, std::vector<uint32_t>& 
     b->uwin.push_back((uint32_t)win);
     b->ulen.push_back((uint32_t)len);
     b->fwc_off.push_back(NONE);
-    if (len && direct(len)) {
+    if ((int)i == pre) b->pre_u = u;
+    if (len && direct(len) && (int)i != pre) {
       b->ugroup.push_back(NONE);
       small.push_back(u);
     } else {
-      if (fwc_wants(src[i]) && b->fwc_recs + len <= FWC_MAX_RECS) {
+      // (a doc state decoded by its marks keeps its chunks for the grid delete-set decode only)
+      if ((int)i != pre && fwc_wants(src[i]) && b->fwc_recs + len <= FWC_MAX_RECS) {
         b->fwc_off.back() = (uint32_t)b->fwc_recs;
         b->fwc_recs += (len + 63) & ~size_t(63);
       }
@@ -653,6 +669,13 @@ int check(ycrdt_engine* e, Counters& c, const char* where) {
   HIPCHK(hipMemcpyAsync(e->ctr_pin, e->w.ctr, sizeof(Counters), hipMemcpyDeviceToHost, e->stream));
   HIPCHK(hipStreamSynchronize(e->stream));
   c = *e->ctr_pin;
+  if (c.err && (c.err_info >> 16) >= 0xC0DEu && (c.err_info >> 16) <= 0xC0DFu) {  // YCRDT_PREDECODE=check: marks != decode
+    char m[200];
+    snprintf(m, sizeof(m), "doc state marks differ from its decode (%s word %u: decode %08x%08x, marks %08x%08x)",
+             (c.err_info >> 16) == 0xC0DFu ? "delete-set start" : (c.err_info & 0x8000u) ? "section bitmap" : "struct bitmap",
+             c.err_info & 0x7FFFu, c.pad[9], c.pad[8], c.pad[11], c.pad[10]);
+    return fail(YCRDT_E_DECODE, m);
+  }
   if (c.err) return map_err(c.err, where);
   return YCRDT_OK;
 }
@@ -918,6 +941,8 @@ int run_decode(ycrdt_engine* e, ycrdt_batch* b, bool lazy, Decoded& D, bool gene
                   {w.usec_n, (uint64_t)nu + 1, 0u},  // an update no walker reached has no sections
                   {(uint32_t*)w.final_bits, (uint64_t)nwords * 2, 0u},
                   {(uint32_t*)w.sec_bits, (uint64_t)nwords * 2, 0u}}, s);
+  w.upre = b->pre_src >= 0 && !b->pre_check ? b->pre_u : NONE;
+  if (w.upre != NONE) launch_predecoded(w, b->pre_u, b->pre, false, s);  // (a doc state: its own encode's decode)
   const bool dbg_yata = getenv("YCRDT_DEBUG_YATA") && getenv("YCRDT_DEBUG_YATA")[0] == '1';
   const bool dbg_dec = getenv("YCRDT_DEBUG_DECODE") && getenv("YCRDT_DEBUG_DECODE")[0] == '1';
   w.dbg = dbg_yata || dbg_dec ? take<unsigned long long>(V, B_DBG, 24, ok) : nullptr;
@@ -968,6 +993,7 @@ int run_decode(ycrdt_engine* e, ycrdt_batch* b, bool lazy, Decoded& D, bool gene
   // reruns the decode the counted way (generous)
   const bool quick = !lazy && !split && !generous && !w.dbg && !w.udoc && w.nupd && b->nwin <= 1 && w.nbytes <= (64u << 10) && w.cap_sections <= 16000 &&
                      !env_off("YCRDT_DECODE_SMALL") && !env_off("YCRDT_DECODE_QUICK");
+  if (b->pre_src >= 0 && b->pre_check) launch_predecoded(w, b->pre_u, b->pre, true, s);  // (reported at the next check)
   int rc = quick ? YCRDT_OK : check(e, c, "decode");
   if (quick) {
     c = Counters();
@@ -2051,6 +2077,7 @@ void ycrdt_doc_destroy(ycrdt_doc* d) {
   hipSetDevice(d->e->device);
   if (d->e->ws_owner == d) d->e->ws_owner = nullptr;
   if (d->state.p) { if (d->state.arena) d->e->arena.release(d->state.p, d->state.cap); else hipFree(d->state.p); }
+  if (d->marks.p) { if (d->marks.arena) d->e->arena.release(d->marks.p, d->marks.cap); else hipFree(d->marks.p); }
   if (d->spare.p) { if (d->spare.arena) d->e->arena.release(d->spare.p, d->spare.cap); else hipFree(d->spare.p); }
   d->e->docs.erase(d);
   delete d;
@@ -2062,12 +2089,62 @@ namespace {
 
 constexpr size_t QUEUE_FLUSH_BYTES = size_t(1) << 30;  // deferred updates past this are merged at once
 
+// YCRDT_PREDECODE: 0 off, "check" decode the state the usual way and compare with its marks
+int predecode_mode() {
+  const char* v = getenv("YCRDT_PREDECODE");
+  return v && v[0] == '0' ? 0 : v && !strcmp(v, "check") ? 2 : 1;
+}
+// the doc's state goes into the next batch as source 0: decoded from its marks when they describe it
+void doc_pre(ycrdt_doc* d, ycrdt_batch& b) {
+  b.pre_src = -1;
+  b.pre_check = false;
+  const int mode = predecode_mode();
+  if (!mode || !d->state_len || d->marks_len != d->state_len || !d->marks.p) return;
+  uint8_t* m = (uint8_t*)d->marks.p;
+  b.pre.fbits = (uint64_t*)m;
+  b.pre.sbits = (uint64_t*)(m + 8ull * d->marks_nw);
+  b.pre.secs = (Section*)(m + 16ull * d->marks_nw);
+  b.pre.meta = (uint32_t*)(m + 16ull * d->marks_nw + sizeof(Section) * d->marks_cap);
+  b.pre.nw = d->marks_nw;
+  b.pre.cap_secs = d->marks_cap;
+  b.pre_src = 0;
+  b.pre_check = mode == 2;
+}
+// after a successful merge of the doc (the workspace holds its encode): the marks of the new state
+void doc_marks(ycrdt_doc* d) {
+  ycrdt_engine* e = d->e;
+  d->marks_len = 0;
+  if (!predecode_mode() || !e->out_bytes || e->out_bytes >= (uint64_t(1) << 31)) return;
+  // (exactly the state's own 64-byte slot: the next staged update's words follow it)
+  const uint32_t nw = (uint32_t)((e->out_bytes + 63) / 64), cap = (uint32_t)e->last.clients + 1;
+  const size_t bytes = 16ull * nw + sizeof(Section) * cap + 16;
+  if (d->marks.cap < bytes) {
+    release_state(e, d->marks);
+    if (!alloc_state(e, d->marks, bytes)) { (void)hipGetLastError(); d->marks = DevBuf(); return; }
+  }
+  d->marks_nw = nw;
+  d->marks_cap = cap;
+  {
+    uint8_t* m = (uint8_t*)d->marks.p;
+    PreMarks pm;
+    pm.fbits = (uint64_t*)m;
+    pm.sbits = (uint64_t*)(m + 8ull * nw);
+    pm.secs = (Section*)(m + 16ull * nw);
+    pm.meta = (uint32_t*)(m + 16ull * nw + sizeof(Section) * cap);
+    pm.nw = nw;
+    pm.cap_secs = cap;
+    launch_state_marks(e->w, (uint32_t)e->last.out_structs, (uint32_t)e->last.clients, pm, e->stream);
+  }
+  d->marks_len = e->out_bytes;
+}
+
 // Merges `extra` (host updates) behind the doc's state in one device pass and makes the result the
 // doc's state. caps: integrate only below the per-client caps (the pending path).
 int commit_merge(ycrdt_doc* d, const std::vector<ycrdt_buf>& extra, const ClockMap* caps,
                  const std::vector<uint32_t>* order = nullptr) {
   ycrdt_engine* e = d->e;
   ycrdt_batch& b = scratch_batch(e);  // engine-owned: no hipMalloc / hipFree per call
+  doc_pre(d, b);
   int rc = stage(&b, extra.data(), extra.size(), d->state_len ? &d->state : nullptr, d->state_len);
   // The merged state goes to a block of its own (or the doc's, when it fits and is not the source
   // of this merge any more: the batch holds a copy once staged); the doc changes only once it is
@@ -2099,6 +2176,8 @@ int commit_merge(ycrdt_doc* d, const std::vector<ycrdt_buf>& extra, const ClockM
     rc = run_merge(e, &b, nullptr, caps, order);
     e->before_final = nullptr;
   }
+  b.pre_src = -1;
+  if (rc == YCRDT_OK) doc_marks(d);  // (the new state's decode, from this encode: queued on the stream)
   if (rc) {
     if (fresh && !d->spare.p) d->spare = nb;  // (kept for the next merge)
     else if (fresh) release_state(e, nb);
@@ -2308,6 +2387,7 @@ int flush_multi(ycrdt_engine* e, const std::vector<ycrdt_doc*>& docs) {
     if (fresh[j]) { release_state(e, d->state); d->state = nblk[j]; }
     d->sv.swap(nsv[j]);
     d->state_len = len[j];
+    d->marks_len = 0;  // (assembled from a multi-document encode: no marks)
     d->last = e->last;  // the whole pass
     d->view.valid = false;
     d->queue.clear();
@@ -2523,8 +2603,10 @@ int ycrdt_encode_state_as_update(ycrdt_doc* d, ycrdt_buf sv, ycrdt_out* out) {
     HIPCHK(hipMemcpy(main.data(), d->state.p, d->state_len, hipMemcpyDeviceToHost));
   } else {  // delta: re-run the (idempotent) merge of the canonical state with per-client start clocks
     ycrdt_batch& b = scratch_batch(e);
+    doc_pre(d, b);  // (the state's own decode: crdt.js's sync reply, crdt.js:288)
     rc = stage(&b, nullptr, 0, &d->state, d->state_len);
     if (rc == YCRDT_OK) rc = run_merge(e, &b, &target, nullptr, e->compat == 135 ? &d->ing.order : nullptr);
+    b.pre_src = -1;
     if (rc) return rc;
     main.resize(e->out_bytes);
     HIPCHK(hipMemcpy(main.data(), e->w.out, e->out_bytes, hipMemcpyDeviceToHost));
@@ -2926,8 +3008,10 @@ static int ensure_view(ycrdt_doc* d) {
   HIPCHK(hipSetDevice(e->device));
   ycrdt_batch& b = scratch_batch(e);  // engine-owned: no hipMalloc / hipFree per call
   if (e->ws_owner != d) {  // the workspace no longer holds this doc's merge: redo it (idempotent)
+    doc_pre(d, b);
     rc = stage(&b, nullptr, 0, &d->state, d->state_len);
     if (rc == YCRDT_OK) rc = run_merge(e, &b, nullptr);
+    b.pre_src = -1;
     if (rc) return rc;
     e->ws_owner = d;
   }

@@ -121,7 +121,10 @@ struct Work {
   uint64_t* cpre = nullptr;        // [G+1] exclusive scan of ccnt (the fast walks' chunk search)
   uint32_t* opre = nullptr;        // [G+1] exclusive scan of coff
   uint32_t* fw = nullptr;          // [2 nupd] fast-walked updates: first chain position past the exact walk, end of the last struct
-  uint32_t* ufail = nullptr;       // [nupd] 1: the speculative walk gave up (locked chain phases), tables next
+  uint32_t* ufail = nullptr;       // [nupd] 1: the speculative walk gave up (locked chain phases), tables next;
+                                   // 2 / 3 fast-walked, 4 / 5 resumed by k_walk, UF_PRE decoded by its marks,
+                                   // UF_WALKED walked whole by k_prewalk
+  uint32_t upre = 0xFFFFFFFFu;     // the update decoded by its marks (k_predecoded), NONE: none
   uint64_t* final_bits = nullptr;  // [B/64] verified struct starts
   uint64_t* sec_bits = nullptr;    // [B/64] first struct of every non-empty section
   uint32_t* dsstart = nullptr;     // [nupd] byte position of the delete set
@@ -666,6 +669,23 @@ struct ViewBufs {
   ViewSeg* segs = nullptr;   // [narr]
 };
 void launch_view(const Work& w, const ViewBufs& v, uint32_t nsegs, uint32_t nlists, uint32_t narr, hipStream_t s);
+
+// ---- a doc state's decode, written by the encode that produced it (k_state_marks): the next merge
+// of the doc takes its state's struct / section starts, section records and delete-set start from
+// here instead of parsing the state again (k_predecoded). Positions are the state's own.
+constexpr uint32_t UF_PRE = 6;   // ufail of the update k_predecoded decoded
+constexpr uint32_t UF_WALKED = 7;  // ufail of a large update k_prewalk decoded whole (a short struct section)
+struct PreMarks {
+  uint64_t* fbits = nullptr;   // [nw] struct starts
+  uint64_t* sbits = nullptr;   // [nw] first struct of every non-empty section
+  Section* secs = nullptr;     // [cap_secs] section record of every client slot (n = 0: no block; upd 0)
+  uint32_t* meta = nullptr;    // [3] sections (non-empty blocks), delete-set start, client slots
+  uint32_t nw = 0, cap_secs = 0;
+};
+void launch_state_marks(const Work& w, uint32_t nout, uint32_t nclients, const PreMarks& m, hipStream_t s);
+// update u of the batch is the state the marks describe: its decode (check: compare, the state was
+// decoded the usual way too)
+void launch_predecoded(const Work& w, uint32_t u, const PreMarks& m, bool check, hipStream_t s);
 
 // ---- launch entry points (yc_decode.hip / yc_merge.hip / yc_encode.hip / yc_prims.hip)
 void launch_chunks(const Work& w, hipStream_t s);  // k_spec + k_walk: large updates

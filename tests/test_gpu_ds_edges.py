@@ -119,3 +119,32 @@ def test_delete_only_into_empty_doc_after_other_merges(mode, monkeypatch):
     d = crdt_amd.Doc(client_id=0x7FFFFFF0)
     d.apply_updates([b"\x00\x00", delta])
     assert (d.encode_state_as_update(), d.encode_state_vector()) == (pending_state, b"\x00")
+
+
+@pytest.mark.parametrize("prewalk", ("1", "0"))
+@pytest.mark.parametrize("extra", (0, 3, 70))
+def test_large_delta_short_struct_section(prewalk, extra, monkeypatch):
+    """A LARGE update whose struct section is a few structs in front of a big delete set — the sync
+    reply's shape (Y.encodeStateAsUpdate(doc, sv) writes the whole delete set, crdt.js:288). k_prewalk
+    decodes it whole (<= 64 structs) and the chunk chains skip it; with 70 structs (past its budget)
+    or YCRDT_PREWALK=0 the chunk path takes it: the same bytes as the oracle either way."""
+    monkeypatch.setenv("YCRDT_PREWALK", prewalk)
+    d0 = ODoc(77)
+    d0.array_insert("messages", 0, [any_int(i % 50) for i in range(30_000)])
+    base = d0.encode_state_as_update()
+    sv = d0.encode_state_vector()
+    for i in range(29_999, -1, -2):
+        d0.array_delete("messages", i, 1)
+    for k in range(extra):
+        d0.map_set("users", f"x{k}", any_int(k))
+    delta = d0.encode_state_as_update(sv)
+    assert len(delta) > 16 * 1024
+    want = _oracle([base, delta])
+    d = crdt_amd.Doc(client_id=0x7FFFFFF0)
+    d.apply_update(base)
+    d.encode_state_vector()
+    d.apply_update(delta)
+    assert (d.encode_state_as_update(), d.encode_state_vector()) == want
+    b = crdt_amd.Batch([delta, base])  # (one batch merge is order-independent)
+    b.merge()
+    assert b.result() == want
