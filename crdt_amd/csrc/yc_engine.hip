@@ -397,7 +397,10 @@ void layout(ycrdt_batch* b, const std::vector<Src>& src, std::vector<uint32_t>& 
   const char* mode = getenv("YCRDT_DECODE");
   const int force = mode && (!strcmp(mode, "chunks") || !strcmp(mode, "tables") || !strcmp(mode, "xtab")) ? 1
                     : mode && !strcmp(mode, "direct") ? 2 : 0;
-  const int pre = b->pre_check ? -1 : b->pre_src;  // (decoded by k_predecoded: in the big list for its delete set only)
+  // (decoded by k_predecoded; a large one stays in the big list, its chunks serving the grid
+  // delete-set decode only; a small one is in neither list)
+  constexpr size_t PRE_GROUPS_MIN = size_t(64) << 10;
+  const int pre = b->pre_check ? -1 : b->pre_src;
   size_t nsmall = 0;
   for (size_t i = 0; i < src.size(); ++i) nsmall += src[i].len <= DIRECT_MAX_BYTES && (int)i != pre;
   // small updates are parsed directly however few there are: one lane each (k_direct) when they
@@ -414,7 +417,7 @@ void layout(ycrdt_batch* b, const std::vector<Src>& src, std::vector<uint32_t>& 
   // (short enough that the walker's 64 lanes still span the largest update in one step)
   size_t big_bytes = 0, big_max = 0;
   for (size_t i = 0; i < src.size(); ++i)
-    if (src[i].len && (!direct(src[i].len) || (int)i == pre)) { big_bytes += src[i].len; big_max = std::max(big_max, src[i].len); }
+    if (src[i].len && ((int)i == pre ? src[i].len > PRE_GROUPS_MIN : !direct(src[i].len))) { big_bytes += src[i].len; big_max = std::max(big_max, src[i].len); }
   b->schunk = SCHUNK;
   if (big_bytes <= SMALL_BATCH_BYTES)
     while (b->schunk > SCHUNK_SMALL && (size_t)(b->schunk / 2) * 64 >= big_max) b->schunk /= 2;
@@ -445,7 +448,10 @@ void layout(ycrdt_batch* b, const std::vector<Src>& src, std::vector<uint32_t>& 
     b->ulen.push_back((uint32_t)len);
     b->fwc_off.push_back(NONE);
     if ((int)i == pre) b->pre_u = u;
-    if (len && direct(len) && (int)i != pre) {
+    if ((int)i == pre && len <= PRE_GROUPS_MIN) {
+      // (a small doc state: no chunks at all — its delete set is short, the wavefront decodes it)
+      b->ugroup.push_back(NONE);
+    } else if (len && direct(len) && (int)i != pre) {
       b->ugroup.push_back(NONE);
       small.push_back(u);
     } else {
