@@ -3143,6 +3143,10 @@ __global__ __launch_bounds__(CT_LANES) void k_sections_small(Work w, uint32_t n,
       return;
     }
   }
+  if (w.dbg_bounds && (n > w.cap_sections || n + 1 > w.cap_clients + 1 || 2 * (n + 1) > mask + 1)) {
+    if (t == 0) bounds_fail(w, "k_sections_small sections / client hash", n, w.cap_sections);
+    return;
+  }
   for (uint32_t i = t; i < n; i += CT_LANES) section_rank_at(w, i);
   for (uint32_t i = t; i <= mask; i += CT_LANES) key[i] = ~0ull;
   client_table_small_body(w, n, v, pre, u, part);  // (ends with the sections' client indexes)
@@ -3376,6 +3380,10 @@ __global__ __launch_bounds__(DT_LANES) void k_decode_tail_small(Work w, uint32_t
     nstructs = w.ctr->nstructs;
     nsections = w.ctr->nsections;
     if (nstructs > DT_SMALL || nsections + 1 > DT_LANES * 16) { if (t == 0) raise_err(&w.ctr->err, ERR_CAPACITY); return; }
+  }
+  if (w.dbg_bounds && (nstructs > w.cap_structs || nsections + 1 > w.cap_clients + 1)) {
+    if (t == 0) bounds_fail(w, "k_decode_tail_small structs / sections", nstructs, w.cap_structs);
+    return;
   }
   for (uint32_t i = t; i <= nsections; i += DT_LANES) { w.cl_start[i] = 0; w.cl_state[i] = 0; }
   for (uint32_t i = t; i < nstructs; i += DT_LANES) struct_decode_one<false>(w, i, win);

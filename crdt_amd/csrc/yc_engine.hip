@@ -947,6 +947,7 @@ int run_decode(ycrdt_engine* e, ycrdt_batch* b, bool lazy, Decoded& D, bool gene
                   {w.usec_n, (uint64_t)nu + 1, 0u},  // an update no walker reached has no sections
                   {(uint32_t*)w.final_bits, (uint64_t)nwords * 2, 0u},
                   {(uint32_t*)w.sec_bits, (uint64_t)nwords * 2, 0u}}, s);
+  w.dbg_bounds = getenv("YCRDT_DEBUG_BOUNDS") && getenv("YCRDT_DEBUG_BOUNDS")[0] == '1' ? 1u : 0u;
   w.upre = b->pre_src >= 0 && !b->pre_check ? b->pre_u : NONE;
   if (w.upre != NONE) launch_predecoded(w, b->pre_u, b->pre, false, s);  // (a doc state: its own encode's decode)
   const bool dbg_yata = getenv("YCRDT_DEBUG_YATA") && getenv("YCRDT_DEBUG_YATA")[0] == '1';

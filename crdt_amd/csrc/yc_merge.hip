@@ -88,6 +88,11 @@ __device__ __forceinline__ void unit_owner(const Work& w, uint32_t nstructs, uin
 __device__ __forceinline__ void set_flag_byte(uint32_t* u_flags, uint32_t g, uint32_t byte) {
   reinterpret_cast<uint8_t*>(u_flags)[(size_t)g * 4 + byte] = 1;
 }
+// a unit's flag byte (YCRDT_DEBUG_BOUNDS: the unit checked against the unit table first)
+__device__ __forceinline__ void unit_flag(const Work& w, uint64_t g, uint32_t byte) {
+  if (w.dbg_bounds && g >= w.cap_units) { bounds_fail(w, "unit flag", g, w.cap_units); return; }
+  set_flag_byte(w.u_flags, (uint32_t)g, byte);
+}
 // The delete sets of a merge, straight from the decoder's per-update regions (no compaction): one
 // wavefront per update resolves its ranges' clients, clips them to the known states (pendingDs)
 // and marks the units (the prep and mark passes above in one, for the integrate path)
@@ -127,12 +132,12 @@ __device__ __forceinline__ void unit_ds_apply(const Work& w, uint32_t nclients, 
     if (i < n) len = ds_range_units(w, nclients, doc, w.ds_tmp[base + i], gb);
     const bool lng = len > LONG_UNITS;
     if (!lng)
-      for (uint32_t k = 0; k < len; ++k) set_flag_byte(w.u_flags, (uint32_t)(gb + k), 1);
+      for (uint32_t k = 0; k < len; ++k) unit_flag(w, (uint32_t)(gb + k), 1);
     for (uint64_t m = __ballot(lng); m; m &= m - 1) {
       const int L = __ffsll((long long)m) - 1;
       const uint64_t g0 = shfl64(gb, L);
       const uint32_t nl = __shfl(len, L);
-      for (uint32_t k = lane; k < nl; k += 64) set_flag_byte(w.u_flags, (uint32_t)(g0 + k), 1);
+      for (uint32_t k = lane; k < nl; k += 64) unit_flag(w, (uint32_t)(g0 + k), 1);
     }
   }
 }
@@ -158,12 +163,12 @@ __device__ __forceinline__ void unit_refs(const Work& w, uint32_t nstructs, uint
   if (oc != NONE) {
     if (oc == UNKNOWN || ok_ >= ost) { raise_err(&w.ctr->err, ERR_PENDING); return; }
     const uint32_t g = (uint32_t)(ob + ok_);
-    if (ok_ + 1 < ost) set_flag_byte(w.u_flags, g + 1, 2);  // getItemCleanEnd(origin)
+    if (ok_ + 1 < ost) unit_flag(w, g + 1, 2);  // getItemCleanEnd(origin)
   }
   if (rc != NONE) {
     if (rc == UNKNOWN || rk >= rst) { raise_err(&w.ctr->err, ERR_PENDING); return; }
     const uint32_t g = (uint32_t)(rb + rk);
-    set_flag_byte(w.u_flags, g, 2);                          // getItemCleanStart(rightOrigin)
+    unit_flag(w, g, 2);                          // getItemCleanStart(rightOrigin)
   }
 }
 __device__ __forceinline__ bool cut_at(const Work& w, uint64_t g, uint64_t nunits) {
@@ -264,7 +269,7 @@ __device__ __forceinline__ void unit_ds_apply_big(const Work& w, uint32_t nclien
     for (uint32_t i = DSA_WAVE + t; i < n; i += stride) {
       uint64_t gb;
       const uint32_t len = ds_range_units(w, nclients, doc, w.ds_tmp[base + i], gb);
-      for (uint32_t k = 0; k < len; ++k) set_flag_byte(w.u_flags, (uint32_t)(gb + k), 1);
+      for (uint32_t k = 0; k < len; ++k) unit_flag(w, (uint32_t)(gb + k), 1);
     }
   }
 }
@@ -409,6 +414,7 @@ __device__ __forceinline__ void seg_props_at(const Work& w, uint32_t s) {
       if (ps != NONE) { h = fnv_u32(h, 0x5Au); h = fnv_bytes(h, struct_bytes(w, own) + ps, w.s_psublen[own]); }
       h &= w.key_mask;  // tests: YCRDT_KEY_HASH_BITS truncates the hash so distinct lists collide
       key = key_insert(w, h, own);
+      if (key != NONE) YC_BOUND(w, key, w.cap_keys, "key slot");
       if (key == NONE) raise_err(&w.ctr->err, ERR_CAPACITY);
       else {
         sf |= SEG_ROOT;
@@ -434,7 +440,7 @@ __device__ __forceinline__ void seg_props_at(const Work& w, uint32_t s) {
   // entries only).
   if (!gc && origin != NONE) {
     w.g_maxchild[link] = s + 1;
-    if (olow) set_flag_byte(w.u_flags, origin, 3);  // (UF_LOWCHILD)
+    if (olow) unit_flag(w, origin, 3);  // (UF_LOWCHILD)
   } else if (key != NONE) {
     w.k_rootmax[key] = s + 1;
   }
@@ -893,6 +899,10 @@ __global__ __launch_bounds__(MS_LANES) void k_merge_small(Work w, uint32_t nsegs
     ms_sync<FENCE>();
     if (ld_fresh(&w.ctr->err)) return;  // (ERR_PENDING: an atomic)
     nsegs = w.ctr->nsegs;
+  }
+  if (w.dbg_bounds && nsegs + 2 > w.cap_units + 1) {  // (the segment columns hold U + 2 entries)
+    if (threadIdx.x == 0) bounds_fail(w, "k_merge_small segments", nsegs, w.cap_units);
+    return;
   }
   const uint32_t t = threadIdx.x, ck = w.cap_keys;
   if (t == 0) sarr = 0;

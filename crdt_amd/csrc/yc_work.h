@@ -94,6 +94,8 @@ struct Work {
                                    // step from a header there {next header, chain range end, walked, why}
   const uint32_t* fwc_off = nullptr; // [nupd] record base of each record-mode update, NONE otherwise (null: none)
   uint32_t* rtab = nullptr;        // record mode: chain_len at every byte of those updates (k_rtab), indexed as fwc
+  uint32_t dbg_bounds = 0;         // YCRDT_DEBUG_BOUNDS=1: table indexes of the unit passes and the single-workgroup
+                                   // kernels checked against their tables' sizes (bounds_fail: a message + ERR_CAPACITY)
   uint32_t fwc_walk = 256;         // k_fwc's walk bound (YCRDT_FWC_WALK; at FWM_WALK the walker never re-evaluates a chain-position header)
   uint16_t* wlen = nullptr;        // [nsmall * 16384] few small updates: the chain step at every position (k_wlen)
   uint32_t schunk = SCHUNK;        // chunk bytes of this batch's large updates (<= SCHUNK)
@@ -610,6 +612,15 @@ __device__ __attribute__((noinline)) uint32_t any_canon(const uint8_t* __restric
   }
   return (uint32_t)(q - q0);
 }
+
+// YCRDT_DEBUG_BOUNDS: an index past its table (never on a correct merge: the bound every small pass
+// and every unit pass sizes from) is reported and stops the merge instead of writing past the table
+__device__ __noinline__ inline void bounds_fail(const Work& w, const char* what, uint64_t idx, uint64_t cap) {
+  printf("[ycrdt bounds] %s: index %llu past its table of %llu\n", what, (unsigned long long)idx, (unsigned long long)cap);
+  raise_err(&w.ctr->err, ERR_CAPACITY);
+}
+#define YC_BOUND(w, idx, cap, what) \
+  do { if ((w).dbg_bounds && (uint64_t)(idx) >= (uint64_t)(cap)) bounds_fail((w), (what), (idx), (cap)); } while (0)
 
 // per-client scratch arrays inside Work::cc
 enum : uint32_t {
