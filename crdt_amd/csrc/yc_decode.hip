@@ -3144,7 +3144,7 @@ __global__ __launch_bounds__(CT_LANES) void k_sections_small(Work w, uint32_t n,
     }
   }
   if (w.dbg_bounds && (n > w.cap_sections || n + 1 > w.cap_clients + 1 || 2 * (n + 1) > mask + 1)) {
-    if (t == 0) bounds_fail(w, "k_sections_small sections / client hash", n, w.cap_sections);
+    if (t == 0) bounds_fail(w.ctr, BOUNDS_SECTIONS);
     return;
   }
   for (uint32_t i = t; i < n; i += CT_LANES) section_rank_at(w, i);
@@ -3382,7 +3382,7 @@ __global__ __launch_bounds__(DT_LANES) void k_decode_tail_small(Work w, uint32_t
     if (nstructs > DT_SMALL || nsections + 1 > DT_LANES * 16) { if (t == 0) raise_err(&w.ctr->err, ERR_CAPACITY); return; }
   }
   if (w.dbg_bounds && (nstructs > w.cap_structs || nsections + 1 > w.cap_clients + 1)) {
-    if (t == 0) bounds_fail(w, "k_decode_tail_small structs / sections", nstructs, w.cap_structs);
+    if (t == 0) bounds_fail(w.ctr, BOUNDS_DECODE_TAIL);
     return;
   }
   for (uint32_t i = t; i <= nsections; i += DT_LANES) { w.cl_start[i] = 0; w.cl_state[i] = 0; }

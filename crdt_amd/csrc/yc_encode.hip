@@ -561,7 +561,7 @@ __global__ __launch_bounds__(ENC_SMALL_LANES) void k_encode_small(Work w, uint32
     nsegs = w.ctr->nsegs;
   }
   if (w.dbg_bounds && (nsegs + 2 > w.cap_units + 1 || nclients + 1 > w.cap_clients + 1)) {
-    if (threadIdx.x == 0) bounds_fail(w, "k_encode_small segments / clients", nsegs, w.cap_units);
+    if (threadIdx.x == 0) bounds_fail(w.ctr, BOUNDS_ENCODE_SMALL);
     return;
   }
   uint32_t* part = (uint32_t*)part64;
@@ -608,7 +608,7 @@ __global__ __launch_bounds__(ENC_SMALL_LANES) void k_encode_small(Work w, uint32
   // every write (k_write_structs, k_write_general, k_write_clients, k_write_runs)
   for (uint32_t o = t; o < nout; o += ENC_SMALL_LANES) {
     if (!w.o_size[o]) continue;
-    YC_BOUND(w, out_pos(w, o) + w.o_size[o], w.cap_out + 1, "k_encode_small output struct");
+    YC_BOUND(w, out_pos(w, o) + w.o_size[o], w.cap_out + 1, BOUNDS_OUTPUT);
     if (w.o_gen[o]) encode_struct_general<true>(w, nclients, w.o_first[o], w.o_first[o + 1], w.out, out_pos(w, o));
     else encode_struct_fast<true>(w, w.o_first[o], w.o_first[o + 1], w.out, out_pos(w, o));
   }

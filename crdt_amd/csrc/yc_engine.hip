@@ -682,6 +682,12 @@ int check(ycrdt_engine* e, Counters& c, const char* where) {
              c.err_info & 0x7FFFu, c.pad[9], c.pad[8], c.pad[11], c.pad[10]);
     return fail(YCRDT_E_DECODE, m);
   }
+  if (c.err == ERR_CAPACITY && (c.err_info >> 16) == 0xB0DEu) {  // YCRDT_DEBUG_BOUNDS
+    static const char* what[] = {"?", "unit flag", "key slot", "k_merge_small segments", "k_encode_small segments / clients",
+                                 "k_encode_small output struct", "k_decode_tail_small structs / sections", "k_sections_small sections / client hash"};
+    const uint32_t k = c.err_info & 0xFFFFu;
+    return fail(YCRDT_E_CAPACITY, std::string("bounds check (YCRDT_DEBUG_BOUNDS): an index past its table: ") + what[k < 8 ? k : 0] + " at " + where);
+  }
   if (c.err) return map_err(c.err, where);
   return YCRDT_OK;
 }

@@ -90,7 +90,7 @@ __device__ __forceinline__ void set_flag_byte(uint32_t* u_flags, uint32_t g, uin
 }
 // a unit's flag byte (YCRDT_DEBUG_BOUNDS: the unit checked against the unit table first)
 __device__ __forceinline__ void unit_flag(const Work& w, uint64_t g, uint32_t byte) {
-  if (w.dbg_bounds && g >= w.cap_units) { bounds_fail(w, "unit flag", g, w.cap_units); return; }
+  if (w.dbg_bounds && g >= w.cap_units) { bounds_fail(w.ctr, BOUNDS_UNIT); return; }
   set_flag_byte(w.u_flags, (uint32_t)g, byte);
 }
 // The delete sets of a merge, straight from the decoder's per-update regions (no compaction): one
@@ -414,7 +414,7 @@ __device__ __forceinline__ void seg_props_at(const Work& w, uint32_t s) {
       if (ps != NONE) { h = fnv_u32(h, 0x5Au); h = fnv_bytes(h, struct_bytes(w, own) + ps, w.s_psublen[own]); }
       h &= w.key_mask;  // tests: YCRDT_KEY_HASH_BITS truncates the hash so distinct lists collide
       key = key_insert(w, h, own);
-      if (key != NONE) YC_BOUND(w, key, w.cap_keys, "key slot");
+      if (key != NONE) YC_BOUND(w, key, w.cap_keys, BOUNDS_KEY);
       if (key == NONE) raise_err(&w.ctr->err, ERR_CAPACITY);
       else {
         sf |= SEG_ROOT;
@@ -901,7 +901,7 @@ __global__ __launch_bounds__(MS_LANES) void k_merge_small(Work w, uint32_t nsegs
     nsegs = w.ctr->nsegs;
   }
   if (w.dbg_bounds && nsegs + 2 > w.cap_units + 1) {  // (the segment columns hold U + 2 entries)
-    if (threadIdx.x == 0) bounds_fail(w, "k_merge_small segments", nsegs, w.cap_units);
+    if (threadIdx.x == 0) bounds_fail(w.ctr, BOUNDS_MERGE_SMALL);
     return;
   }
   const uint32_t t = threadIdx.x, ck = w.cap_keys;

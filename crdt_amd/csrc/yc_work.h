@@ -614,13 +614,18 @@ __device__ __attribute__((noinline)) uint32_t any_canon(const uint8_t* __restric
 }
 
 // YCRDT_DEBUG_BOUNDS: an index past its table (never on a correct merge: the bound every small pass
-// and every unit pass sizes from) is reported and stops the merge instead of writing past the table
-__device__ __noinline__ inline void bounds_fail(const Work& w, const char* what, uint64_t idx, uint64_t cap) {
-  printf("[ycrdt bounds] %s: index %llu past its table of %llu\n", what, (unsigned long long)idx, (unsigned long long)cap);
-  raise_err(&w.ctr->err, ERR_CAPACITY);
+// and every unit pass sizes from) stops the merge with a capacity error instead of writing past the
+// table; err_info names the check (BOUNDS_* below), the host reports it (yc_engine.hip check()).
+// Inline and without printf: a call in a kernel (even one never taken) makes it keep registers
+// across the call — k_units 38 -> 60 VGPRs — and a Work reference passed out of line copies the
+// whole Work to scratch in every lane (k_units / k_seg_props 20 x slower; tests/test_kernel_resources.py)
+enum : uint32_t { BOUNDS_UNIT = 1, BOUNDS_KEY, BOUNDS_MERGE_SMALL, BOUNDS_ENCODE_SMALL, BOUNDS_OUTPUT, BOUNDS_DECODE_TAIL, BOUNDS_SECTIONS };
+__device__ __forceinline__ void bounds_fail(Counters* ctr, uint32_t what) {
+  raise_err(&ctr->err, ERR_CAPACITY);
+  ctr->err_info = 0xB0DE0000u | what;
 }
 #define YC_BOUND(w, idx, cap, what) \
-  do { if ((w).dbg_bounds && (uint64_t)(idx) >= (uint64_t)(cap)) bounds_fail((w), (what), (idx), (cap)); } while (0)
+  do { if ((w).dbg_bounds && (uint64_t)(idx) >= (uint64_t)(cap)) bounds_fail((w).ctr, (what)); } while (0)
 
 // per-client scratch arrays inside Work::cc
 enum : uint32_t {

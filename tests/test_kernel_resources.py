@@ -1,0 +1,84 @@
+"""Scratch budgets of the hot kernels, read from the built library's gfx950 code object (CPU only).
+
+A reference to the whole Work struct passed into an out-of-line call makes the compiler copy the
+Work to scratch memory in every lane of the calling kernel: a debug-only bounds helper written that
+way gave k_units and k_seg_props 1 824 bytes of scratch per lane and ran the C2 headline merge at
+112 ms instead of 26 ms (round 6, caught by the headline profile). The kernels of the headline merge
+keep the scratch and registers they were measured with; this test fails the build check when one grows.
+"""
+import os
+import re
+import struct
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LLVM = "/opt/rocm/lib/llvm/bin"
+LIB = os.path.join(ROOT, "crdt_amd", "libycrdt.so")
+
+# kernel (mangled-name fragment) -> scratch bytes per lane it may use
+BUDGET = {
+    "7k_units": 0, "11k_seg_props": 0, "9k_resolve": 0, "13k_winner_walk": 0, "18k_merge_flags_scan": 0,
+    "11k_out_sizes": 0, "15k_write_structs": 0, "6k_cuts": 0, "14k_struct_clock": 0, "13k_scatter_seg": 0,
+    "15k_struct_decode": 16, "8k_direct": 160, "6k_spec": 160,
+}
+
+
+def _kernels(tmp_path):
+    for tool in ("llvm-objcopy", "llvm-readelf"):
+        if not os.path.exists(os.path.join(LLVM, tool)):
+            pytest.skip(f"{tool} not in this image")
+    if not os.path.exists(LIB):
+        pytest.skip("libycrdt.so not built")
+    fat = tmp_path / "fatbin"
+    subprocess.check_call([os.path.join(LLVM, "llvm-objcopy"), f"--dump-section=.hip_fatbin={fat}", LIB, str(tmp_path / "lib.copy")])
+    blob = fat.read_bytes()
+    # one clang offload bundle per source file: magic, entry count, (offset, size, triple) entries
+    magic = b"__CLANG_OFFLOAD_BUNDLE__"
+    out = {}
+    at = blob.find(magic)
+    k = 0
+    while at >= 0:
+        n = struct.unpack_from("<Q", blob, at + 24)[0]
+        q = at + 32
+        for _ in range(n):
+            off, size, tl = struct.unpack_from("<QQQ", blob, q)
+            triple = blob[q + 24:q + 24 + tl].decode()
+            q += 24 + tl
+            if "gfx950" in triple:
+                co = tmp_path / f"co{k}.o"
+                k += 1
+                co.write_bytes(blob[at + off:at + off + size])
+                notes = subprocess.check_output([os.path.join(LLVM, "llvm-readelf"), "--notes", str(co)], text=True)
+                for m in re.finditer(r"\.name:\s+(\S+)\n(.*?)(?=\n\s+- \.|\n\s+\.name:|\Z)", notes, re.S):
+                    ps = re.search(r"\.private_segment_fixed_size:\s+(\d+)", m.group(2))
+                    vg = re.search(r"\.vgpr_count:\s+(\d+)", m.group(2))
+                    if ps:
+                        out[m.group(1)] = (int(ps.group(1)), int(vg.group(1)) if vg else 0)
+        at = blob.find(magic, at + 1)
+    return out
+
+
+def test_hot_kernels_scratch(tmp_path):
+    k = _kernels(tmp_path)
+    assert k, "no kernel metadata found"
+    for frag, budget in BUDGET.items():
+        hits = {n: v for n, v in k.items() if f"_ZN2yc{frag}" in n}
+        assert hits, frag
+        for n, (v, _) in hits.items():
+            assert v <= budget, f"{n}: {v} bytes of scratch per lane (budget {budget})"
+
+
+# VGPR ceilings of the unit / segment passes (a call site, even an untaken debug one, raised k_units
+# from 26 to 60) and of the struct decode (forced to 8 wavefronts per SIMD: <= 64)
+VGPRS = {"7k_units": 40, "11k_seg_props": 48, "9k_resolve": 32, "15k_struct_decode": 64}
+
+
+def test_hot_kernels_vgprs(tmp_path):
+    k = _kernels(tmp_path)
+    for frag, cap in VGPRS.items():
+        hits = {n: v for n, v in k.items() if f"_ZN2yc{frag}" in n}
+        assert hits, frag
+        for n, (_, vg) in hits.items():
+            assert vg <= cap, f"{n}: {vg} VGPRs (ceiling {cap})"
