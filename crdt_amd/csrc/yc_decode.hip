@@ -3092,7 +3092,10 @@ void launch_client_table(Work& w, uint32_t nsections, hipStream_t s) {
   }
   if (w.udoc) {
     hipLaunchKernelGGL(k_gather_sec_keys, dim3(grid), dim3(256), 0, s, w, nsections);
-    sort_pairs_u64_u32(w.tmp, w.tmp_bytes, w.cl_key2, w.cl_key, w.cl_tmp, w.cl_state, nsections, s);
+    // (doc << 32 | client keys: the radix passes stop past the document bits)
+    uint32_t dbits = 0;
+    while (dbits < 32 && (w.ndocs - 1) >> dbits) ++dbits;
+    sort_pairs_u64_u32(w.tmp, w.tmp_bytes, w.cl_key2, w.cl_key, w.cl_tmp, w.cl_state, nsections, s, 32 + dbits);
     hipLaunchKernelGGL(k_unique_keys, dim3(grid), dim3(256), 0, s, w, nsections);
     scan_u32(w.tmp, w.tmp_bytes, w.scratch, w.cl_tmp, nsections + 1, s);
     hipLaunchKernelGGL(k_unique_keys_scatter, dim3(grid), dim3(256), 0, s, w, nsections);

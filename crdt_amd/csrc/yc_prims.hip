@@ -275,9 +275,9 @@ void sort_pairs_u32(void* tmp, size_t tmpb, const uint32_t* kin, uint32_t* kout,
 }
 
 void sort_pairs_u64_u32(void* tmp, size_t tmpb, const uint64_t* kin, uint64_t* kout, const uint32_t* vin, uint32_t* vout,
-                        uint64_t n, hipStream_t s) {
+                        uint64_t n, hipStream_t s, uint32_t end_bit) {
   if (!n) return;
-  rocprim::radix_sort_pairs(tmp, tmpb, kin, kout, vin, vout, (size_t)n, 0, 64, s);
+  rocprim::radix_sort_pairs(tmp, tmpb, kin, kout, vin, vout, (size_t)n, 0, end_bit, s);
 }
 
 void scan_segmax_u64(void* tmp, size_t tmpb, const uint64_t* in, uint64_t* out, uint64_t n, hipStream_t s) {

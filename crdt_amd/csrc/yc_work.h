@@ -785,7 +785,7 @@ void fill_u32_multi(std::initializer_list<FillDesc> fills, hipStream_t s);
 void sort_pairs_u32(void* tmp, size_t tmpb, const uint32_t* kin, uint32_t* kout, const uint32_t* vin, uint32_t* vout,
                     uint64_t n, hipStream_t s);
 void sort_pairs_u64_u32(void* tmp, size_t tmpb, const uint64_t* kin, uint64_t* kout, const uint32_t* vin, uint32_t* vout,
-                        uint64_t n, hipStream_t s);
+                        uint64_t n, hipStream_t s, uint32_t end_bit = 64);  // (keys below 2^end_bit: fewer radix passes)
 // inclusive scan with "max within equal high words" (segmented running max of packed values)
 void scan_segmax_u64(void* tmp, size_t tmpb, const uint64_t* in, uint64_t* out, uint64_t n, hipStream_t s);
 
