@@ -1425,6 +1425,133 @@ __global__ __launch_bounds__(256) void k_fwc(Work w) {
     }
   }
 }
+// ---- The last section of a record-mode update, ranked. A section the records cannot vouch for is
+// one whose chunk chains never settle into the true phase (a long snapshot of similar structs: C2's
+// 100 k-struct base section, the LAST of a document state's sections); k_walk then resumed at its
+// header and composed exit tables, 64 chunks a step (1.5 ms on the C2 state). With the step table
+// the section's structs are the first n positions of the chain from its first struct, found by
+// pointer doubling over the section's bytes (k_wrank's method on the whole chip): in round k every
+// position at distance d < 2^k from the first struct marks the one 2^k steps on (d + 2^k <= n), and
+// the jump table advances from 2^k to 2^(k+1) steps (two buffers). Positions at distance < n are the
+// structs, the one at distance n starts the delete set. The jump tables and distances live in the
+// update's records (free once the walker has followed them). Only the update's last section, and only
+// n < 2^RK_ROUNDS; anything else — or a chain that ends short — stays with k_walk.
+constexpr uint32_t RK_ROUNDS = 24;
+__device__ __forceinline__ uint32_t* rk_base(const Work& w, uint32_t u) { return (uint32_t*)(w.fwc + w.fwc_off[u]); }
+// one lane per large update: the ranked section of a record-mode update, if any (rk[u]: first struct,
+// n, section index, 1 = ranked)
+__global__ void k_rk_setup(Work w) {
+  const uint32_t bi = blockIdx.x * blockDim.x + threadIdx.x;
+  if (bi >= w.nbig) return;
+  const uint32_t u = w.ulist[bi];
+  w.rk[u] = make_uint4(0u, 0u, 0u, 0u);
+  if (w.fwc_off[u] == NONE || !w.rtab || w.ufail[u] != 4u) return;  // (YCRDT_FWM_MAX = sections - 1: tests take this path)
+  const uint32_t done = w.fw[2 * u];
+  if (done + 1 != w.usec_n[u]) return;  // (not the last section)
+  const uint8_t* __restrict__ b = win_bytes(w, upd_win(w, u));
+  const uint32_t uend = w.uoff[u] + w.ulen[u];
+  uint32_t p = w.fw[2 * u + 1];
+  bool ok = true;
+  const uint32_t n = rd_vu(b, p, uend, ok);
+  rd_vu(b, p, uend, ok);
+  rd_vu(b, p, uend, ok);
+  if (!ok || n == 0 || n >= (1u << RK_ROUNDS) || p >= uend) return;
+  w.rk[u] = make_uint4(p, n, w.usec_start[u] + done, 1u);
+  w.dsstart[u] = NONE;  // (set by the marks only if the chain reaches distance n)
+}
+// the positions of the record-mode updates (grid-stride over their chunks): (update, position) or false
+__device__ __forceinline__ bool rk_pos(const Work& w, uint64_t t, uint32_t& u, uint32_t& p) {
+  const Group G = w.groups[t / w.schunk];
+  u = G.upd;
+  p = G.start + (uint32_t)(t % w.schunk);
+  return p < G.end && w.fwc_off[u] != NONE;
+}
+__global__ __launch_bounds__(256) void k_rk_init(Work w) {
+  const uint64_t total = (uint64_t)w.ngroups * w.schunk;
+  for (uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total; t += (uint64_t)gridDim.x * blockDim.x) {
+    uint32_t u, p;
+    if (!rk_pos(w, t, u, p)) continue;
+    const uint4 d = w.rk[u];
+    if (!d.w) continue;
+    const uint32_t ustart = w.uoff[u], L = w.ulen[u], uend = ustart + L, i = p - ustart;
+    uint32_t* __restrict__ A = rk_base(w, u);
+    const uint32_t st = p >= d.x ? rtab_of(w, u)[i] : 0u;
+    A[i] = st && p + st < uend ? p + st : (st && p + st == uend ? uend : NONE);  // J_1 (the update end: a sink that counts)
+    A[2 * L + i] = p == d.x ? 0u : NONE;                                         // distance from the first struct
+  }
+}
+__global__ __launch_bounds__(256) void k_rk_round(Work w, uint32_t k) {
+  const uint64_t total = (uint64_t)w.ngroups * w.schunk;
+  for (uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total; t += (uint64_t)gridDim.x * blockDim.x) {
+    uint32_t u, p;
+    if (!rk_pos(w, t, u, p)) continue;
+    const uint4 d = w.rk[u];
+    if (!d.w || (1u << k) > d.y || p < d.x) continue;  // (no round needed past n)
+    const uint32_t ustart = w.uoff[u], L = w.ulen[u], uend = ustart + L, i = p - ustart;
+    uint32_t* __restrict__ A = rk_base(w, u);
+    const uint32_t* __restrict__ J = A + (k & 1u) * L;
+    uint32_t* __restrict__ J2 = A + ((k + 1) & 1u) * L;
+    uint32_t* __restrict__ dist = A + 2 * L;
+    const uint32_t j = J[i], di = dist[i];
+    if (di != NONE && di < (1u << k) && j != NONE && di + (1u << k) <= d.y) {
+      if (j < uend) dist[j - ustart] = di + (1u << k);
+      else if (j == uend && di + (1u << k) == d.y) w.dsstart[u] = uend;  // (the section ends the update: no delete set)
+    }
+    J2[i] = j == NONE || j >= uend ? (j == uend ? uend : NONE) : J[j - ustart];
+  }
+}
+// the marks: structs at distance < n, the delete set at n (one lane per bitmap word); the section
+// record, its first-struct mark and an empty chain range (k_fastmark), ufail 3
+__global__ __launch_bounds__(256) void k_rk_final(Work w) {
+  const uint32_t wpc = w.schunk / 64;
+  const uint64_t total = (uint64_t)w.ngroups * wpc;
+  for (uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total; t += (uint64_t)gridDim.x * blockDim.x) {
+    const Group G = w.groups[t / wpc];
+    const uint32_t u = G.upd;
+    if (w.fwc_off[u] == NONE) continue;
+    const uint4 d = w.rk[u];
+    if (!d.w) continue;
+    const uint32_t wd = (G.start >> 6) + (uint32_t)(t % wpc);
+    if ((uint64_t)wd * 64 >= G.end) continue;
+    const uint32_t ustart = w.uoff[u], L = w.ulen[u];
+    const uint32_t* __restrict__ dist = rk_base(w, u) + 2 * L;
+    uint64_t m = 0;
+    for (uint32_t bb = 0; bb < 64; ++bb) {
+      const uint32_t p = wd * 64 + bb;
+      if (p < max(G.start, d.x) || p >= G.end) continue;
+      const uint32_t di = dist[p - ustart];
+      if (di < d.y) m |= 1ull << bb;
+      else if (di == d.y) w.dsstart[u] = p;
+    }
+    uint64_t* __restrict__ fbits = win_words(w.final_bits, upd_win(w, u));
+    if (m) atomicOr((unsigned long long*)&fbits[wd], (unsigned long long)m);
+  }
+}
+// the section's record once the marks are in (one lane per large update); a chain that ends short
+// (no position at distance n) leaves the section to k_walk, which reports it
+__global__ void k_rk_commit(Work w) {
+  const uint32_t bi = blockIdx.x * blockDim.x + threadIdx.x;
+  if (bi >= w.nbig) return;
+  const uint32_t u = w.ulist[bi];
+  const uint4 d = w.rk[u];
+  if (!d.w || w.dsstart[u] == NONE) return;
+  const uint8_t* __restrict__ b = win_bytes(w, upd_win(w, u));
+  const uint32_t uend = w.uoff[u] + w.ulen[u];
+  uint32_t p = w.fw[2 * u + 1];
+  bool ok = true;
+  const uint32_t n = rd_vu(b, p, uend, ok), client = rd_vu(b, p, uend, ok), clock = rd_vu(b, p, uend, ok);
+  Section sec;
+  sec.upd = u; sec.n = n; sec.client = client; sec.clock = clock;
+  sec.first_pos = d.x; sec.cidx = NONE; sec.first_idx = NONE; sec.pad = 0;
+  w.sections[d.z] = sec;
+  uint64_t* __restrict__ sbits = win_words(w.sec_bits, upd_win(w, u));
+  atomicOr((unsigned long long*)&sbits[d.x >> 6], 1ull << (d.x & 63));
+  w.fwsec[2 * d.z] = d.x;  // (an empty chain range: the marks are in)
+  w.fwsec[2 * d.z + 1] = d.x;
+  w.ufail[u] = 3u;
+  if (w.dbg) atomicAdd(&w.dbg[0], 1ull);
+}
+
 // the walker's record-mode pass: lane 0 follows the records from header to header; every section
 // it vouches for gets (header, chain range end) in fwsec, k_fwc_commit writes the rest
 __device__ __forceinline__ void fwm_records(const Work& w, uint32_t u, uint32_t nsec, uint32_t hdr0) {
@@ -2256,6 +2383,14 @@ void launch_chunks(const Work& w, hipStream_t s) {
       if (w.fwc) hipLaunchKernelGGL(k_fwc, dim3(wgrid), dim3(256), 0, s, w);  // (record-mode updates only)
       hipLaunchKernelGGL(k_fastwalk_multi, dim3(w.nbig), dim3(64), 0, s, w);
       if (w.fwc) hipLaunchKernelGGL(k_fwc_commit, dim3(64), dim3(256), 0, s, w);
+      if (w.rk) {  // the last section the records left, ranked (YCRDT_RANK_LAST=0: k_walk takes it)
+        const uint32_t pgrid = (uint32_t)std::min<uint64_t>((uint64_t)w.ngroups * w.schunk / 256 + 1, 16384);
+        hipLaunchKernelGGL(k_rk_setup, dim3(w.nbig / 64 + 1), dim3(64), 0, s, w);
+        hipLaunchKernelGGL(k_rk_init, dim3(pgrid), dim3(256), 0, s, w);
+        for (uint32_t k = 0; k < RK_ROUNDS; ++k) hipLaunchKernelGGL(k_rk_round, dim3(pgrid), dim3(256), 0, s, w, k);
+        hipLaunchKernelGGL(k_rk_final, dim3(wgrid), dim3(256), 0, s, w);
+        hipLaunchKernelGGL(k_rk_commit, dim3(w.nbig / 64 + 1), dim3(64), 0, s, w);
+      }
       hipLaunchKernelGGL(k_fastmark, dim3(std::min<uint64_t>((uint64_t)w.ngroups * (w.schunk / 64) / 256 + 1, 8192)), dim3(256), 0, s, w);
     }
     hipLaunchKernelGGL(k_walk<false>, dim3(w.nbig), dim3(64), 0, s, w);

@@ -179,7 +179,7 @@ enum Buf {
   B_UOWN, B_UFLAG, B_UCUT, B_UWPRE,
   B_GSTART, B_GCIDX, B_GSRC, B_GFLAGS, B_GORIG, B_GRORIG, B_GLINK, B_GOSEG, B_GKEY, B_GMAXC, B_GNEXT, B_GOUTID, B_GTMP, B_GTMP2,
   B_KHASH, B_KROOT, B_KWIN, B_KPAR, B_KFLAG, B_SPK,
-  B_USEC, B_USECN, B_DBG, B_XTAB, B_UFAIL, B_FW, B_CCNT, B_TENTRY, B_XLIST, B_WLEN, B_FWSEC, B_DSPCNT, B_DSPPRE, B_DSPVAL, B_DSPBLK, B_DSPB, B_DSPNB, B_DSPFAIL, B_DSPGB, B_OGEN, B_SDDEFER, B_COFF, B_CPRE, B_OPRE, B_SECUEND, B_SECDOC, B_DSBIGL, B_FWC, B_FWCOFF, B_RTAB,
+  B_USEC, B_USECN, B_DBG, B_XTAB, B_UFAIL, B_FW, B_CCNT, B_TENTRY, B_XLIST, B_WLEN, B_FWSEC, B_DSPCNT, B_DSPPRE, B_DSPVAL, B_DSPBLK, B_DSPB, B_DSPNB, B_DSPFAIL, B_DSPGB, B_OGEN, B_SDDEFER, B_COFF, B_CPRE, B_OPRE, B_SECUEND, B_SECDOC, B_DSBIGL, B_FWC, B_FWCOFF, B_RTAB, B_RK,
   B_LZKEY, B_LZKEYS, B_LZIOTA, B_LZSEC, B_LZRSTART, B_LZPREV, B_LZFIRST, B_LZCAP, B_LZEVBASE, B_LZEVN, B_LZFLAG,
   B_LZLHI, B_LZLLO, B_EVKIND, B_EVSRC, B_EVCLOCK, B_EVLEN, B_EVSIZE, B_EVPOS, B_BLKSIZE, B_BLKPOS, B_SVC, B_SVK,
   B_DSMKEY, B_DSMKEYS, B_DSMLEN, B_DSMLENS, B_DSMEND, B_DSMMAX, B_DSMFLAG, B_DSMRID, B_DRCLIENT, B_DRCLOCK, B_DREND,
@@ -928,12 +928,14 @@ int run_decode(ycrdt_engine* e, ycrdt_batch* b, bool lazy, Decoded& D, bool gene
   w.fwc = nullptr;
   w.fwc_off = nullptr;
   w.rtab = nullptr;
+  w.rk = nullptr;
   if (b->fwc_recs && w.fwsec) {  // record mode: the records and each update's base
     w.fwc = take<uint4>(V, B_FWC, b->fwc_recs + 1, ok);
     uint32_t* fo = take<uint32_t>(V, B_FWCOFF, nu + 1, ok);
     if (ok) HIPCHK(hipMemcpyAsync(fo, b->fwc_off.data(), sizeof(uint32_t) * nu, hipMemcpyHostToDevice, e->stream));
     w.fwc_off = fo;
     if (!env_off("YCRDT_RTAB")) w.rtab = take<uint32_t>(V, B_RTAB, b->fwc_recs + 1, ok);  // (YCRDT_RTAB=0: parse every step, A/B)
+    if (w.rtab && !env_off("YCRDT_RANK_LAST")) w.rk = take<uint4>(V, B_RK, nu + 1, ok);
     const char* fw = getenv("YCRDT_FWC_WALK");  // (experiments)
     w.fwc_walk = fw && atoi(fw) > 0 ? (uint32_t)atoi(fw) : 256u;
   }

@@ -94,6 +94,7 @@ struct Work {
                                    // step from a header there {next header, chain range end, walked, why}
   const uint32_t* fwc_off = nullptr; // [nupd] record base of each record-mode update, NONE otherwise (null: none)
   uint32_t* rtab = nullptr;        // record mode: chain_len at every byte of those updates (k_rtab), indexed as fwc
+  uint4* rk = nullptr;             // [nupd] record mode: the ranked last section (first struct, n, section, 1)
   uint32_t dbg_bounds = 0;         // YCRDT_DEBUG_BOUNDS=1: table indexes of the unit passes and the single-workgroup
                                    // kernels checked against their tables' sizes (bounds_fail: a message + ERR_CAPACITY)
   uint32_t fwc_walk = 256;         // k_fwc's walk bound (YCRDT_FWC_WALK; at FWM_WALK the walker never re-evaluates a chain-position header)

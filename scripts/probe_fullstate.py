@@ -23,7 +23,7 @@ for a in sys.argv[1:]:
     name, kv = a.split(":", 1)
     CONFIGS[name] = dict(x.split("=", 1) for x in kv.split(","))
 for fwc, env in CONFIGS.items():
-    for k in ("YCRDT_FWC_WALK", "YCRDT_SPEC_HINT", "YCRDT_SCHUNK", "YCRDT_RTAB"):
+    for k in ("YCRDT_FWC_WALK", "YCRDT_SPEC_HINT", "YCRDT_SCHUNK", "YCRDT_RTAB", "YCRDT_RANK_LAST"):
         os.environ.pop(k, None)
     os.environ.update(env)
     os.environ["YCRDT_FWC"] = fwc if fwc in ("0", "1") else env.get("YCRDT_FWC", "1")

@@ -174,3 +174,39 @@ def test_document_state_as_one_update_record_mode(monkeypatch, capfd):
         d.encode_state_vector()
         d.apply_update(state)
         assert (d.encode_state_as_update(), d.encode_state_vector()) == want
+
+
+@pytest.mark.parametrize("rank", ("1", "0"))
+def test_last_section_ranked(rank, monkeypatch, capfd):
+    """Record mode stops before the last section (YCRDT_FWM_MAX = sections - 1, the place a
+    phase-locked snapshot section stops it); the last section is then ranked by pointer doubling over
+    the step table (YCRDT_RANK_LAST=0: k_walk resumes instead). Equal to the oracle either way, and
+    the ranked path really taken."""
+    from crdt_amd.workload import C2, gen_map
+
+    cfg = dict(C2)
+    cfg.update(n_keys=4000, n_replicas=120, ops_per_replica=150)
+    ups, _ = gen_map(**cfg)
+    o = ODoc(0x7FFFFFF0)
+    for u in ups:
+        o.apply_update(u)
+    state = o.encode_state_as_update()
+    nsec, k = 0, 0
+    while True:  # the section count (first varuint)
+        nsec |= (state[k] & 0x7F) << (7 * k)
+        if state[k] < 0x80:
+            break
+        k += 1
+    monkeypatch.setenv("YCRDT_FWM_MAX", str(nsec - 1))
+    monkeypatch.setenv("YCRDT_RANK_LAST", rank)
+    got, done = _merge([state], monkeypatch, capfd, True, fwc="force")
+    assert got == (state, o.encode_state_vector())
+    assert done >= (1 if rank == "1" else 0)
+    other = ODoc(9)
+    other.map_set("users", "k7", any_int(70))
+    batch = [other.encode_state_as_update(), state]
+    ref = ODoc(0x7FFFFFF0)
+    for u in batch:
+        ref.apply_update(u)
+    got, _ = _merge(batch, monkeypatch, capfd, True, fwc="force")
+    assert got == (ref.encode_state_as_update(), ref.encode_state_vector())
