@@ -9,13 +9,23 @@ sys.path.insert(0, ROOT)
 import crdt_amd  # noqa: E402
 from crdt_amd.workload import C2, gen_map  # noqa: E402
 
-ups = gen_map(**C2)[0]
+if os.environ.get("PROBE_WL") == "c3":  # (a C3 state: 256 sections of ~600 KB; with PROBE_HALF=1 behind half of it)
+    from crdt_amd.workload import gen_array
+    ups = gen_array(256, 16, 10_000_000, 3)[0]
+else:
+    ups = gen_map(**C2)[0]
 eng = crdt_amd.Engine()
 b = crdt_amd.Batch(ups, eng)
 b.merge()
 full = b.result()[0]
 del b
 print("full state", len(full), flush=True)
+src = [full]
+if os.environ.get("PROBE_HALF") == "1":
+    hb = crdt_amd.Batch(ups[: len(ups) // 2], eng)
+    hb.merge()
+    src = [hb.result()[0], full]
+    del hb
 eng.set_profiling(True)
 res = {}
 CONFIGS = {"1": {}, "0": {}}  # record mode on (the default) and off; more from argv: name:VAR=v,VAR=v
@@ -27,7 +37,7 @@ for fwc, env in CONFIGS.items():
         os.environ.pop(k, None)
     os.environ.update(env)
     os.environ["YCRDT_FWC"] = fwc if fwc in ("0", "1") else env.get("YCRDT_FWC", "1")
-    fb = crdt_amd.Batch([full], eng)
+    fb = crdt_amd.Batch(src, eng)
     os.environ["YCRDT_DEBUG_DECODE"] = "1"
     print(fwc, env, flush=True)
     fb.merge()
