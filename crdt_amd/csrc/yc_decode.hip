@@ -3436,10 +3436,42 @@ __global__ __launch_bounds__(256) void k_json_structs(Work w, uint32_t nstructs)
   const uint32_t ref = bw[w.s_pos[i]] & 31u;  // (the input's info byte: superseded sections' structs too)
   if (ref != REF_JSON && ref != REF_EMBED && ref != REF_FORMAT) return;
   const int jr = json_content(bw, w.s_cpos[i], w.s_cend[i], ref);
-  if (jr) raise_err(&w.ctr->err, jr < 0 ? ERR_UNSUPPORTED : ERR_DECODE);
+  if (jr > 0) raise_err(&w.ctr->err, ERR_DECODE);
+  if (jr < 0) {  // not in the form Yjs writes back: listed for k_json_canon (run_decode rewrites the update)
+    const uint32_t k = atomicAdd(&w.ctr->njson, 1u);
+    if (k < w.jcap) w.jlist[k] = i;
+  }
 }
 void launch_json_structs(const Work& w, uint32_t nstructs, hipStream_t s) {
   if (nstructs) hipLaunchKernelGGL(k_json_structs, dim3(nstructs / 256 + 1), dim3(256), 0, s, w, nstructs);
+}
+// The canonical contents of the listed structs (yc_parse.h json_content_canon): pass 0 (out null)
+// records each one's position, input length, canonical length and verdict; pass 1 writes it at
+// out + offs[j]. One lane per struct over a lane-private arena: these are the rare values a Yjs
+// peer of an old version (or a hand-made update) sent outside JSON.stringify's form.
+__global__ __launch_bounds__(64) void k_json_canon(Work w, const uint32_t* __restrict__ list, uint32_t n, JItem* __restrict__ items,
+                                                   uint32_t* __restrict__ arena, uint32_t acap, uint32_t lanes,
+                                                   const unsigned long long* __restrict__ offs, uint8_t* __restrict__ out) {
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= lanes) return;
+  uint32_t* a = arena + (uint64_t)t * acap;
+  for (uint32_t j = t; j < n; j += lanes) {
+    const uint32_t i = list[j];
+    const uint8_t* __restrict__ bw = struct_bytes(w, i);
+    const uint32_t ref = bw[w.s_pos[i]] & 31u, cp = w.s_cpos[i], ce = w.s_cend[i];
+    uint32_t len = 0;
+    if (!out) {
+      const uint32_t r = json_content_canon(bw, cp, ce, ref, nullptr, a, acap, len);
+      const unsigned long long base = w.nwin > 1 ? ((unsigned long long)w.s_win[i] << w.win_shift) : 0ull;
+      items[j] = JItem{base + cp, ce - cp, len, r, 0u};
+    } else if (items[j].res == JSON_OK) {
+      json_content_canon(bw, cp, ce, ref, out + offs[j], a, acap, len);
+    }
+  }
+}
+void launch_json_canon(const Work& w, const uint32_t* list, uint32_t n, JItem* items, uint32_t* arena, uint32_t acap,
+                       uint32_t lanes, const unsigned long long* offs, uint8_t* out, hipStream_t s) {
+  if (n) hipLaunchKernelGGL(k_json_canon, dim3((lanes + 63) / 64), dim3(64), 0, s, w, list, n, items, arena, acap, lanes, offs, out);
 }
 
 // Clocks from the section start and the length prefix; with `states` (integrate mode) also the

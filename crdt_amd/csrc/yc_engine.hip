@@ -179,7 +179,7 @@ enum Buf {
   B_UOWN, B_UFLAG, B_UCUT, B_UWPRE,
   B_GSTART, B_GCIDX, B_GSRC, B_GFLAGS, B_GORIG, B_GRORIG, B_GLINK, B_GOSEG, B_GKEY, B_GMAXC, B_GNEXT, B_GOUTID, B_GTMP, B_GTMP2,
   B_KHASH, B_KROOT, B_KWIN, B_KPAR, B_KFLAG, B_SPK,
-  B_USEC, B_USECN, B_DBG, B_XTAB, B_UFAIL, B_FW, B_CCNT, B_TENTRY, B_XLIST, B_WLEN, B_FWSEC, B_DSPCNT, B_DSPPRE, B_DSPVAL, B_DSPBLK, B_DSPB, B_DSPNB, B_DSPFAIL, B_DSPGB, B_OGEN, B_SDDEFER, B_COFF, B_CPRE, B_OPRE, B_SECUEND, B_SECDOC, B_DSBIGL, B_FWC, B_FWCOFF, B_RTAB, B_RK,
+  B_USEC, B_USECN, B_DBG, B_XTAB, B_UFAIL, B_FW, B_CCNT, B_TENTRY, B_XLIST, B_WLEN, B_FWSEC, B_DSPCNT, B_DSPPRE, B_DSPVAL, B_DSPBLK, B_DSPB, B_DSPNB, B_DSPFAIL, B_DSPGB, B_OGEN, B_SDDEFER, B_COFF, B_CPRE, B_OPRE, B_SECUEND, B_SECDOC, B_DSBIGL, B_FWC, B_FWCOFF, B_RTAB, B_RK, B_JLIST, B_JITEM, B_JARENA, B_JOFF, B_JOUT,
   B_LZKEY, B_LZKEYS, B_LZIOTA, B_LZSEC, B_LZRSTART, B_LZPREV, B_LZFIRST, B_LZCAP, B_LZEVBASE, B_LZEVN, B_LZFLAG,
   B_LZLHI, B_LZLLO, B_EVKIND, B_EVSRC, B_EVCLOCK, B_EVLEN, B_EVSIZE, B_EVPOS, B_BLKSIZE, B_BLKPOS, B_SVC, B_SVK,
   B_DSMKEY, B_DSMKEYS, B_DSMLEN, B_DSMLENS, B_DSMEND, B_DSMMAX, B_DSMFLAG, B_DSMRID, B_DRCLIENT, B_DRCLOCK, B_DREND,
@@ -314,6 +314,10 @@ struct ycrdt_batch {
   PreMarks pre;
   bool pre_check = false;
   uint32_t pre_u = 0;
+  // updates rewritten with their JSON-like contents in JSON.stringify's form (json_rewrite): the
+  // host copies the batch was re-staged from, and the rewrite passes so far
+  std::vector<std::vector<uint8_t>> jstore;
+  uint32_t jpasses = 0;
   uint64_t nbytes = 0;          // span of the batch buffer (windows before the last are 2^32 bytes)
   uint64_t in_bytes = 0;
   bool merged = false;
@@ -653,6 +657,8 @@ int stage_srcs(ycrdt_batch* b, const std::vector<Src>& src, const uint32_t* doc_
 int stage(ycrdt_batch* b, const ycrdt_buf* ups, size_t n, const DevBuf* prefix, size_t prefix_len,
           const uint32_t* doc_of = nullptr, uint32_t ndocs = 1) {
   if (prefix_len && doc_of && ndocs > 1) return fail(YCRDT_E_ARG, "internal: multi-document batch with a state prefix");
+  b->jpasses = 0;
+  b->jstore.clear();
   std::vector<Src> src;
   src.reserve(n + 1);
   if (prefix_len) src.push_back(Src{(const uint8_t*)prefix->p, prefix_len, true});
@@ -838,6 +844,98 @@ int split_decode_exchange(ycrdt_engine* e, ycrdt_batch* b, const ShardSpec* sh) 
   return YCRDT_OK;
 }
 
+// ---- ContentJSON / Embed / Format values outside JSON.stringify's form (Y@72137 readContentJSON
+// parses them, Y@71991 writes JSON.stringify of the parsed value back): the decode lists their
+// structs (k_json_structs), k_json_canon computes the canonical contents on the device, and the
+// batch is staged again with those contents spliced into their updates (host copies of the staged
+// updates: byte moves only), so that every later pass sees what Yjs would hold. A pass whose
+// canonical contents all equal the input (a text json_check could not judge: nesting past its
+// level mask) keeps the batch as it is. Rare by construction: Yjs itself writes ContentAny.
+constexpr uint32_t JLIST_CAP = 1u << 16;     // structs per rewrite pass (more: another pass)
+constexpr uint32_t JARENA_WORDS = JSON_ARENA_WORDS;  // arena per lane (yc_parse.h json_canon): 256 KiB
+constexpr uint32_t JLANES = 256;
+int json_rewrite(ycrdt_engine* e, ycrdt_batch* b, uint32_t n, const ShardSpec* sh, bool& restaged) {
+  restaged = false;
+  if (sh) return fail(YCRDT_E_UNSUPPORTED, "a ContentJSON / Embed / Format value outside JSON.stringify's form in a sharded merge");
+  if (++b->jpasses > 8) return fail(YCRDT_E_DEVICE, "internal: the JSON rewrite did not settle");
+  Work& w = e->w;
+  auto& V = e->bufs;
+  hipStream_t s = e->stream;
+  bool ok = true;
+  const uint32_t lanes = std::min(n, JLANES);
+  JItem* items = take<JItem>(V, B_JITEM, n, ok);
+  uint32_t* arena = take<uint32_t>(V, B_JARENA, (size_t)lanes * JARENA_WORDS, ok);
+  unsigned long long* offs = take<unsigned long long>(V, B_JOFF, n, ok);
+  if (!ok) return fail(YCRDT_E_DEVICE, oom("JSON rewrite"));
+  launch_json_canon(w, w.jlist, n, items, arena, JARENA_WORDS, lanes, nullptr, nullptr, s);
+  std::vector<JItem> it(n);
+  HIPCHK(hipMemcpyAsync(it.data(), items, sizeof(JItem) * n, hipMemcpyDeviceToHost, s));
+  HIPCHK(hipStreamSynchronize(s));
+  std::vector<unsigned long long> off(n);
+  unsigned long long total = 0;
+  for (uint32_t j = 0; j < n; ++j) {
+    if (it[j].res == JSON_BAD) return fail(YCRDT_E_DECODE, "JSON.parse: a ContentJSON / Embed / Format value is not JSON");
+    if (it[j].res != JSON_OK) return fail(YCRDT_E_UNSUPPORTED, "a ContentJSON / Embed / Format value past the rewrite arena (nesting or object size)");
+    off[j] = total;
+    total += it[j].len;
+  }
+  uint8_t* cout = take<uint8_t>(V, B_JOUT, total + 1, ok);
+  if (!ok) return fail(YCRDT_E_DEVICE, oom("JSON rewrite"));
+  HIPCHK(hipMemcpyAsync(offs, off.data(), sizeof(unsigned long long) * n, hipMemcpyHostToDevice, s));
+  launch_json_canon(w, w.jlist, n, items, arena, JARENA_WORDS, lanes, offs, cout, s);
+  std::vector<uint8_t> canon(total);
+  if (total) HIPCHK(hipMemcpyAsync(canon.data(), cout, total, hipMemcpyDeviceToHost, s));
+  // the updates as staged (layout order), and which of them a content lies in
+  const size_t nu = b->ulen.size();
+  std::vector<std::vector<uint8_t>> ups(nu);
+  for (size_t u = 0; u < nu; ++u) {
+    ups[u].resize(b->ulen[u]);
+    if (b->ulen[u]) HIPCHK(hipMemcpyAsync(ups[u].data(), (const uint8_t*)b->bytes.p + uabs(b, u), b->ulen[u], hipMemcpyDeviceToHost, s));
+  }
+  HIPCHK(hipStreamSynchronize(s));
+  std::vector<std::vector<uint32_t>> per(nu);  // items of each update
+  bool changed = false;
+  for (uint32_t j = 0; j < n; ++j) {
+    size_t u = nu;
+    for (size_t v = 0; v < nu; ++v)
+      if (it[j].cpos >= uabs(b, v) && it[j].cpos + it[j].clen <= uabs(b, v) + b->ulen[v]) { u = v; break; }
+    if (u == nu) return fail(YCRDT_E_DEVICE, "internal: a JSON content outside every staged update");
+    const uint64_t rel = it[j].cpos - uabs(b, u);
+    if (it[j].len != it[j].clen || memcmp(ups[u].data() + rel, canon.data() + off[j], it[j].len) != 0) {
+      per[u].push_back(j);
+      changed = true;
+    }
+  }
+  if (!changed) return YCRDT_OK;  // already in JSON.stringify's form (a text json_check could not judge)
+  std::vector<std::vector<uint8_t>> store(nu);
+  std::vector<Src> src(nu);
+  for (size_t u = 0; u < nu; ++u) {
+    if (per[u].empty()) {
+      store[u] = std::move(ups[u]);
+    } else {
+      std::sort(per[u].begin(), per[u].end(), [&](uint32_t x, uint32_t y) { return it[x].cpos < it[y].cpos; });
+      std::vector<uint8_t>& o = store[u];
+      uint64_t at = 0;
+      for (const uint32_t j : per[u]) {
+        const uint64_t rel = it[j].cpos - uabs(b, u);
+        o.insert(o.end(), ups[u].begin() + at, ups[u].begin() + rel);
+        o.insert(o.end(), canon.begin() + off[j], canon.begin() + off[j] + it[j].len);
+        at = rel + it[j].clen;
+      }
+      o.insert(o.end(), ups[u].begin() + at, ups[u].end());
+    }
+    src[u] = Src{store[u].data(), store[u].size(), false};
+  }
+  const std::vector<uint32_t> udoc = b->udoc;
+  const uint32_t ndocs = b->ndocs;
+  b->pre_src = -1;  // (a doc state's marks no longer name a source: it is decoded like the others)
+  b->pre_check = false;
+  if (const int rc = stage_srcs(b, src, udoc.empty() ? nullptr : udoc.data(), ndocs)) return rc;
+  b->jstore = std::move(store);
+  restaged = true;
+  return YCRDT_OK;
+}
+
 // K1: decode every update of the batch into the struct SoA (+ client table, delete-set ranges).
 // lazy = mergeUpdates / diffUpdate mode: references stay raw client ids, no client states.
 int run_decode(ycrdt_engine* e, ycrdt_batch* b, bool lazy, Decoded& D, bool generous = false, const ShardSpec* sh = nullptr) {
@@ -924,6 +1022,8 @@ int run_decode(ycrdt_engine* e, ycrdt_batch* b, bool lazy, Decoded& D, bool gene
   w.ds_count = take<uint32_t>(V, B_DSCNT, nu + 2, ok);
   w.ds_dense_off = take<uint32_t>(V, B_DSOFF, nu + 2, ok);
   w.ds_biglist = take<uint32_t>(V, B_DSBIGL, nu + 1, ok);
+  w.jcap = JLIST_CAP;
+  w.jlist = take<uint32_t>(V, B_JLIST, JLIST_CAP, ok);
   w.cap_clients = w.cap_sections;
   w.scratch = take<uint32_t>(V, B_SCRATCH, std::max<uint64_t>({nwords + 2, (uint64_t)w.cap_sections + 66, (uint64_t)nu + 2}), ok);
   w.usec_start = take<uint32_t>(V, B_USEC, nu + 1, ok);
@@ -1151,6 +1251,11 @@ int run_decode(ycrdt_engine* e, ycrdt_batch* b, bool lazy, Decoded& D, bool gene
     launch_json_structs(w, nstructs_q, s);
     rc = check(e, c, "JSON values");
     if (rc) return rc;
+    if (c.njson) {  // values Yjs would write back differently: the updates rewritten, then decoded again
+      bool restaged = false;
+      if ((rc = json_rewrite(e, b, std::min(c.njson, w.jcap), sh, restaged))) return rc;
+      if (restaged) return run_decode(e, b, lazy, D, generous, sh);
+    }
   }
   D.noncanon = c.noncanon;
   const uint32_t nclients = c.nclients;

@@ -268,8 +268,11 @@ void seg_elements(JsonCtx& c, const ViewSeg& s, std::vector<std::pair<bool, std:
       out.push_back({true, r.ok ? std::string((const char*)q, k) : std::string("null")});
       return;
     }
+    case R_FORMAT:  // ContentFormat.getContent() is [] (Y@72137 area): a map entry's value is undefined
+      out.push_back({false, std::string()});
+      return;
     default:
-      out.push_back({true, "null"});  // ContentDoc / ContentFormat are outside crdt.c
+      out.push_back({true, "null"});  // ContentDoc is outside crdt.c
   }
 }
 

@@ -4,6 +4,7 @@
 
 #include <algorithm>
 #include <cstring>
+#include <vector>
 
 #include "../../include/ycrdt.h"
 
@@ -31,7 +32,14 @@ bool scan_update(const uint8_t* b, size_t n, bool headers, UpdScan& o) {
       int r = parse_struct<true>(b, p, end, 0xFFFFFFFFu, &v);
       if (r > 0 && (v.ref == REF_JSON || v.ref == REF_EMBED || v.ref == REF_FORMAT)) {  // JSON.parse (k_struct_decode alike)
         const int jr = json_content(b, v.cpos, v.cend, v.ref);
-        if (jr) r = jr < 0 ? -1 : 0;
+        if (jr > 0) r = 0;
+        if (jr < 0) {  // not in JSON.stringify's form: valid if JSON.parse takes it (the merge rewrites it, k_json_canon)
+          thread_local std::vector<uint32_t> arena(JSON_ARENA_WORDS);
+          uint32_t len = 0;
+          const uint32_t cr = json_content_canon(b, v.cpos, v.cend, v.ref, nullptr, arena.data(), JSON_ARENA_WORDS, len);
+          if (cr == JSON_BAD) r = 0;
+          else if (cr != JSON_OK) r = -1;  // past the rewrite arena: refused
+        }
       }
       if (r == -1) o.unsupported = true;  // skip_any's depth limit (exact budget: never the step count)
       if (r <= 0) return false;

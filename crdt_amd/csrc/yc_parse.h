@@ -13,6 +13,8 @@
 #define YC_HDI inline __attribute__((always_inline))
 #endif
 
+#include "yc_num.h"
+
 namespace yc {
 
 // content refs (low 5 bits of the info byte)
@@ -533,42 +535,20 @@ YC_HD inline uint32_t json_number(const uint8_t* __restrict__ b, uint32_t& p, ui
     if (lead && c == '0') { --n; continue; }
     lead = false;
     if (c == '0') { ++zeros; continue; }
-    if (k + zeros >= 15) { res = JSON_NONCANON; return JSON_OK; }  // more than 15 significant digits: not verified
+    if (k + zeros >= 15) { k = 99; break; }  // more than 15 significant digits: the exact test below
     for (; zeros; --zeros) d[k++] = '0';
     d[k++] = c;
   }
   // the text Number::toString writes for it (ECMA-262 Number::toString, radix 10)
   char t[40];
   uint32_t m = 0;
-  if (k == 0) {
-    t[m++] = '0';  // (-0 is written "0")
+  if (k == 99 || (k != 0 && (n > 308 || n < -306))) {
+    // past what a double holds exactly as 15 digits, or at the ends of its range: JSON.parse's
+    // double and its shortest form, in big-integer arithmetic (yc_num.h)
+    m = json_number_canon(b, s0, p, t);
+    if (m == 0) { res = JSON_NONCANON; return JSON_OK; }
   } else {
-    if (n > 308 || n < -306) { res = JSON_NONCANON; return JSON_OK; }  // Infinity / subnormal digits: not verified
-    if (neg) t[m++] = '-';
-    if ((int32_t)k <= n && n <= 21) {
-      for (uint32_t i = 0; i < k; ++i) t[m++] = d[i];
-      for (int32_t i = (int32_t)k; i < n; ++i) t[m++] = '0';
-    } else if (0 < n && n <= 21) {
-      for (int32_t i = 0; i < n; ++i) t[m++] = d[i];
-      t[m++] = '.';
-      for (uint32_t i = (uint32_t)n; i < k; ++i) t[m++] = d[i];
-    } else if (-6 < n && n <= 0) {
-      t[m++] = '0';
-      t[m++] = '.';
-      for (int32_t i = 0; i < -n; ++i) t[m++] = '0';
-      for (uint32_t i = 0; i < k; ++i) t[m++] = d[i];
-    } else {
-      t[m++] = d[0];
-      if (k > 1) { t[m++] = '.'; for (uint32_t i = 1; i < k; ++i) t[m++] = d[i]; }
-      t[m++] = 'e';
-      int32_t x = n - 1;
-      t[m++] = x < 0 ? '-' : '+';
-      if (x < 0) x = -x;
-      char r[4];
-      uint32_t nr = 0;
-      do { r[nr++] = (char)('0' + x % 10); x /= 10; } while (x);
-      while (nr) t[m++] = r[--nr];
-    }
+    m = num_text(neg, d, k, n, t);
   }
   if (p - s0 != m) { res = JSON_NONCANON; return JSON_OK; }
   for (uint32_t i = 0; i < m; ++i)
@@ -660,29 +640,461 @@ YC_HD inline __attribute__((noinline)) uint32_t json_check(const uint8_t* __rest
 }
 // The JSON values of one ContentJSON / ContentEmbed / ContentFormat content [p, end) (Y@72137
 // readContentJSON: n varStrings, "undefined" allowed; readContentEmbed: one; readContentFormat: a
-// key, then one): 0 ok, 0x100 malformed (JSON.parse throws), -1 valid input the engine refuses.
+// key, then one): 0 ok, 0x100 malformed (JSON.parse throws), -1 not (or not surely) in the form Yjs
+// writes back (json_content_canon rewrites it; a value json_check could not judge — nesting past
+// its level mask — is validated there).
 // Called by the exact decoders once a struct's columns are out (k_struct_decode, the host scanner
 // scan_update): inside parse_struct the call kept the whole struct view live across it (+24 VGPRs,
 // one wave per SIMD less for every struct).
 YC_HD inline __attribute__((noinline)) int json_content(const uint8_t* __restrict__ b, uint32_t p, uint32_t end, uint32_t ref) {
   bool ok = true;
   uint32_t n = 1;
-  if (ref == REF_JSON) n = rd_vu(b, p, end, ok);
-  else if (ref == REF_FORMAT) { const uint32_t k = rd_vu(b, p, end, ok); p += k; }
+  bool over = false;  // an overlong length prefix: valid, but not writeVarUint's form
+  uint32_t q0 = p;
+  if (ref == REF_JSON) { n = rd_vu(b, p, end, ok); over |= vu_overlong(b, q0, p) != 0; }
+  else if (ref == REF_FORMAT) { const uint32_t k = rd_vu(b, p, end, ok); over |= vu_overlong(b, q0, p) != 0; p += k; }
+  int res = 0;
   for (uint32_t i = 0; i < n && ok; ++i) {
+    q0 = p;
     const uint32_t k = rd_vu(b, p, end, ok);
     if (!ok) break;
+    over |= vu_overlong(b, q0, p) != 0;
     const uint8_t* u = b + p;
     const bool undef = ref == REF_JSON && k == 9 && u[0] == 'u' && u[1] == 'n' && u[2] == 'd' && u[3] == 'e' && u[4] == 'f' &&
                        u[5] == 'i' && u[6] == 'n' && u[7] == 'e' && u[8] == 'd';
     if (!undef) {
       const uint32_t r = json_check(b, p, k);
       if (r == JSON_BAD) return 0x100;
-      if (r == JSON_NONCANON) return -1;
+      if (r == JSON_NONCANON) res = -1;  // (the later values may still be malformed)
     }
     p += k;
   }
-  return ok ? 0 : 0x100;
+  if (!ok) return 0x100;
+  return over ? -1 : res;
+}
+
+// ---- JSON.stringify(JSON.parse(text)): the canonical form of a ContentJSON / Embed / Format value
+// that json_check found not in it (whitespace, escapes stringify does not write, numbers not in
+// Number::toString's form, duplicate or array-index keys, nesting past its level mask). Yjs keeps
+// the parsed value (Y@72137) and writes it with JSON.stringify (Y@71991), so the engine rewrites
+// such a value once, on the device (yc_decode.hip k_json_canon), before the update is merged:
+//   - strings: the UTF-16 code units JSON.parse makes of the text, written back with
+//     stringify's escapes (\" \\ \b \f \n \r \t, \u00xx for other controls, \udxxx for lone
+//     surrogates, everything else as UTF-8; a surrogate pair as its 4-byte character);
+//   - numbers: yc_num.h json_number_canon (an infinity comes out "null");
+//   - objects: one member per distinct key (the last value, at the first key's place), array-index
+//     keys first in ascending order (Object.keys order), keys compared by their code units;
+//   - no whitespace; any depth (explicit stacks in a caller-provided word arena).
+constexpr uint32_t JSON_ARENA = 3;  // the arena is too small for the value's nesting / object sizes
+constexpr uint32_t JSON_ARENA_WORDS = 1u << 16;  // the arena the engine gives a value (device lane and host scanner alike)
+// the code units of a JSON string's text, escapes decoded (the text is valid: json_valid)
+struct JStr {
+  uint32_t p;    // next byte
+  uint32_t low;  // pending low surrogate of a 4-byte UTF-8 character (0: none)
+};
+YC_HDI int32_t jstr_next(const uint8_t* __restrict__ b, JStr& s) {
+  if (s.low) { const uint32_t u = s.low; s.low = 0; return (int32_t)u; }
+  const uint32_t c = b[s.p];
+  if (c == '"') return -1;
+  if (c == '\\') {
+    const uint32_t x = b[s.p + 1];
+    s.p += 2;
+    switch (x) {
+      case 'b': return 8;
+      case 'f': return 12;
+      case 'n': return 10;
+      case 'r': return 13;
+      case 't': return 9;
+      case 'u': {
+        uint32_t v = 0;
+        for (int k = 0; k < 4; ++k) v = (v << 4) | (uint32_t)json_hex(b[s.p + k]);
+        s.p += 4;
+        return (int32_t)v;
+      }
+      default: return (int32_t)x;  // " \ /
+    }
+  }
+  if (c < 0x80u) { ++s.p; return (int32_t)c; }
+  if ((c & 0xE0u) == 0xC0u) { const uint32_t v = ((c & 0x1Fu) << 6) | (b[s.p + 1] & 0x3Fu); s.p += 2; return (int32_t)v; }
+  if ((c & 0xF0u) == 0xE0u) {
+    const uint32_t v = ((c & 0x0Fu) << 12) | ((b[s.p + 1] & 0x3Fu) << 6) | (b[s.p + 2] & 0x3Fu);
+    s.p += 3;
+    return (int32_t)v;
+  }
+  const uint32_t v = ((c & 0x07u) << 18) | ((b[s.p + 1] & 0x3Fu) << 12) | ((b[s.p + 2] & 0x3Fu) << 6) | (b[s.p + 3] & 0x3Fu);
+  s.p += 4;
+  s.low = 0xDC00u + ((v - 0x10000u) & 0x3FFu);
+  return (int32_t)(0xD800u + ((v - 0x10000u) >> 10));
+}
+struct JOut {
+  uint8_t* o;  // null: size only
+  uint32_t n;
+  YC_HDI void put(uint32_t c) { if (o) o[n] = (uint8_t)c; ++n; }
+};
+// the string at p (b[p] == '"') in stringify's form; p moves past it. h: FNV-1a of its code units,
+// idx: its array-index value (key_index's rule on the code units) or -1
+YC_HD inline void jstr_emit(const uint8_t* __restrict__ b, uint32_t& p, JOut* out, uint64_t& h, int64_t& idx) {
+  JStr s{p + 1, 0};
+  h = 1469598103934665603ull;
+  uint64_t v = 0;
+  uint32_t nu = 0;
+  bool digits = true;
+  const char* hex = "0123456789abcdef";
+  if (out) out->put('"');
+  for (;;) {
+    int32_t u = jstr_next(b, s);
+    if (u < 0) break;
+    h = (h ^ (uint32_t)u) * 1099511628211ull;
+    if (u < '0' || u > '9' || (nu == 1 && v == 0) || nu >= 10) digits = false;
+    else v = v * 10 + (uint32_t)(u - '0');
+    ++nu;
+    if (!out) continue;
+    if (u >= 0xD800 && u <= 0xDBFF) {  // a pair with the next unit, or a lone surrogate
+      JStr t = s;
+      const int32_t w = jstr_next(b, t);
+      if (w >= 0xDC00 && w <= 0xDFFF) {
+        s = t;
+        h = (h ^ (uint32_t)w) * 1099511628211ull;
+        ++nu;
+        const uint32_t cp = 0x10000u + (((uint32_t)u - 0xD800u) << 10) + ((uint32_t)w - 0xDC00u);
+        out->put(0xF0u | (cp >> 18));
+        out->put(0x80u | ((cp >> 12) & 0x3Fu));
+        out->put(0x80u | ((cp >> 6) & 0x3Fu));
+        out->put(0x80u | (cp & 0x3Fu));
+        continue;
+      }
+    }
+    if (u >= 0xD800 && u <= 0xDFFF) {
+      out->put('\\'); out->put('u');
+      for (int k = 3; k >= 0; --k) out->put((uint8_t)hex[(u >> (4 * k)) & 15]);
+    } else if (u == '"' || u == '\\') {
+      out->put('\\'); out->put((uint32_t)u);
+    } else if (u < 0x20) {
+      out->put('\\');
+      if (u == 8) out->put('b');
+      else if (u == 9) out->put('t');
+      else if (u == 10) out->put('n');
+      else if (u == 12) out->put('f');
+      else if (u == 13) out->put('r');
+      else { out->put('u'); out->put('0'); out->put('0'); out->put(hex[u >> 4]); out->put(hex[u & 15]); }
+    } else if (u < 0x80) {
+      out->put((uint32_t)u);
+    } else if (u < 0x800) {
+      out->put(0xC0u | ((uint32_t)u >> 6)); out->put(0x80u | ((uint32_t)u & 0x3Fu));
+    } else {
+      out->put(0xE0u | ((uint32_t)u >> 12)); out->put(0x80u | (((uint32_t)u >> 6) & 0x3Fu)); out->put(0x80u | ((uint32_t)u & 0x3Fu));
+    }
+  }
+  if (out) out->put('"');
+  p = s.p + 1;
+  idx = (digits && nu > 0 && v < 0xFFFFFFFFull) ? (int64_t)v : -1;
+}
+// two strings' code units equal (keys whose hashes matched)
+YC_HD inline bool jstr_eq(const uint8_t* __restrict__ b, uint32_t p, uint32_t q) {
+  JStr s{p + 1, 0}, t{q + 1, 0};
+  for (;;) {
+    const int32_t x = jstr_next(b, s), y = jstr_next(b, t);
+    if (x != y) return false;
+    if (x < 0) return true;
+  }
+}
+// past one (valid) value at p: strings and brackets only
+YC_HD inline uint32_t json_skip_value(const uint8_t* __restrict__ b, uint32_t p, uint32_t e) {
+  uint32_t depth = 0;
+  do {
+    const uint32_t c = b[p];
+    if (c == '"') {
+      ++p;
+      while (b[p] != '"') p += b[p] == '\\' ? 2u : 1u;
+      ++p;
+    } else if (c == '[' || c == '{') {
+      ++depth; ++p;
+    } else if (c == ']' || c == '}') {
+      --depth; ++p;
+    } else if (depth == 0) {  // a number or a literal
+      while (p < e && b[p] != ',' && b[p] != ']' && b[p] != '}' && !json_ws(b[p])) ++p;
+    } else {
+      ++p;
+    }
+  } while (depth > 0);
+  return p;
+}
+// JSON.parse's grammar at any depth (the container kinds of the open levels as bits in the arena):
+// JSON_OK, JSON_BAD, or JSON_ARENA
+YC_HD inline uint32_t json_valid(const uint8_t* __restrict__ b, uint32_t p, uint32_t n, uint32_t* arena, uint32_t acap) {
+  const uint32_t e = p + n;
+  uint32_t d = 0, res = 0;
+  auto ws = [&]() { while (p < e && json_ws(b[p])) ++p; };
+  auto key = [&]() -> bool {
+    if (p >= e || b[p] != '"') return false;
+    uint64_t h;
+    int64_t idx;
+    if (json_string(b, p, e, res, h, idx) != JSON_OK) return false;
+    ws();
+    if (p >= e || b[p] != ':') return false;
+    ++p;
+    ws();
+    return true;
+  };
+  ws();
+  for (;;) {
+    if (p >= e) return JSON_BAD;
+    const uint32_t c = b[p];
+    if (c == '{' || c == '[') {
+      ++p;
+      ws();
+      if (p >= e) return JSON_BAD;
+      if (b[p] == (c == '{' ? '}' : ']')) {
+        ++p;
+      } else {
+        if ((d >> 5) >= acap) return JSON_ARENA;
+        if (c == '{') arena[d >> 5] |= 1u << (d & 31); else arena[d >> 5] &= ~(1u << (d & 31));
+        ++d;
+        if (c == '{' && !key()) return JSON_BAD;
+        continue;
+      }
+    } else if (c == '"') {
+      uint64_t h;
+      int64_t idx;
+      if (json_string(b, p, e, res, h, idx) != JSON_OK) return JSON_BAD;
+    } else if (c == '-' || (c >= '0' && c <= '9')) {
+      res = JSON_NONCANON;  // (the grammar only: no form test)
+      if (json_number(b, p, e, res) != JSON_OK) return JSON_BAD;
+    } else if (c == 't' || c == 'f' || c == 'n') {
+      const char* lit = c == 't' ? "true" : c == 'f' ? "false" : "null";
+      uint32_t i = 0;
+      while (lit[i] && p + i < e && b[p + i] == (uint8_t)lit[i]) ++i;
+      if (lit[i]) return JSON_BAD;
+      p += i;
+    } else {
+      return JSON_BAD;
+    }
+    for (;;) {
+      ws();
+      if (d == 0) return p == e ? JSON_OK : JSON_BAD;
+      if (p >= e) return JSON_BAD;
+      const bool obj = (arena[(d - 1) >> 5] >> ((d - 1) & 31)) & 1u;
+      const uint32_t x = b[p];
+      if (x == (obj ? '}' : ']')) { ++p; --d; continue; }
+      if (x != ',') return JSON_BAD;
+      ++p;
+      ws();
+      if (obj && !key()) return JSON_BAD;
+      break;
+    }
+  }
+}
+// The canonical text of the JSON value [p, p + n) into out (null: size only), its length in olen.
+// The arena holds per open container a frame of 5 words (previous frame, kind 0 array / 1 object,
+// member count, next member, position past the object) and per open object its members, 5 words
+// each (key position, value position, key hash lo / hi, array index or ~0).
+YC_HD inline __attribute__((noinline)) uint32_t json_canon(const uint8_t* __restrict__ b, uint32_t p, uint32_t n, uint8_t* out,
+                                                          uint32_t* arena, uint32_t acap, uint32_t& olen) {
+  olen = 0;
+  const uint32_t vr = json_valid(b, p, n, arena, acap);
+  if (vr != JSON_OK) return vr;
+  const uint32_t e = p + n;
+  JOut o{out, 0};
+  constexpr uint32_t NOF = 0xFFFFFFFFu;
+  uint32_t top = NOF, used = 0;
+  auto ws = [&]() { while (p < e && json_ws(b[p])) ++p; };
+  auto mem = [&](uint32_t f, uint32_t i) -> uint32_t* { return arena + f + 5 + 5 * i; };
+  auto emit_key = [&](uint32_t f, uint32_t i) {
+    uint32_t kp = mem(f, i)[0];
+    uint64_t h;
+    int64_t idx;
+    jstr_emit(b, kp, &o, h, idx);
+    o.put(':');
+  };
+  ws();
+  for (;;) {
+    // a value at p
+    const uint32_t c = b[p];
+    bool done = true;
+    if (c == '[') {
+      ++p;
+      ws();
+      o.put('[');
+      if (b[p] == ']') { ++p; o.put(']'); }
+      else {
+        if (used + 5 > acap) return JSON_ARENA;
+        arena[used] = top; arena[used + 1] = 0; arena[used + 2] = 0; arena[used + 3] = 0; arena[used + 4] = 0;
+        top = used;
+        used += 5;
+        done = false;
+      }
+    } else if (c == '{') {
+      // the members: key, value position, key hash and index, in text order
+      const uint32_t f = used;
+      if (f + 5 > acap) return JSON_ARENA;
+      uint32_t m = 0;
+      ++p;
+      ws();
+      if (b[p] == '}') {
+        ++p;
+      } else {
+        for (;;) {
+          ws();
+          if (f + 5 + 5 * (m + 1) > acap) return JSON_ARENA;
+          uint32_t* r = mem(f, m);
+          r[0] = p;
+          uint64_t h;
+          int64_t idx;
+          jstr_emit(b, p, nullptr, h, idx);
+          ws();
+          ++p;  // ':'
+          ws();
+          r[1] = p;
+          r[2] = (uint32_t)h;
+          r[3] = (uint32_t)(h >> 32);
+          r[4] = idx >= 0 ? (uint32_t)idx : NOF;
+          p = json_skip_value(b, p, e);
+          ++m;
+          ws();
+          if (b[p++] == '}') break;  // else ','
+        }
+      }
+      // one member per key: the last value at the first key's place
+      uint32_t k = 0;
+      for (uint32_t j = 0; j < m; ++j) {
+        uint32_t* rj = mem(f, j);
+        bool dup = false;
+        for (uint32_t i = 0; i < k; ++i) {
+          uint32_t* ri = mem(f, i);
+          if (ri[2] == rj[2] && ri[3] == rj[3] && jstr_eq(b, ri[0], rj[0])) { ri[1] = rj[1]; dup = true; break; }
+        }
+        if (dup) continue;
+        if (k != j) { uint32_t* rk = mem(f, k); for (int w = 0; w < 5; ++w) rk[w] = rj[w]; }
+        ++k;
+      }
+      // array-index keys first, ascending (stable: the others keep their order)
+      uint32_t ni = 0;
+      for (uint32_t j = 0; j < k; ++j) {
+        uint32_t* rj = mem(f, j);
+        if (rj[4] == NOF) continue;
+        uint32_t t[5];
+        for (int w = 0; w < 5; ++w) t[w] = rj[w];
+        uint32_t i = j;
+        // shift the non-index members and larger index members right
+        while (i > 0) {
+          uint32_t* rp = mem(f, i - 1);
+          if (i - 1 < ni && rp[4] <= t[4]) break;
+          uint32_t* rc = mem(f, i);
+          for (int w = 0; w < 5; ++w) rc[w] = rp[w];
+          --i;
+        }
+        uint32_t* ri = mem(f, i);
+        for (int w = 0; w < 5; ++w) ri[w] = t[w];
+        ++ni;
+      }
+      o.put('{');
+      if (k == 0) {
+        o.put('}');
+      } else {
+        arena[f] = top; arena[f + 1] = 1; arena[f + 2] = k; arena[f + 3] = 0; arena[f + 4] = p;
+        top = f;
+        used = f + 5 + 5 * k;
+        emit_key(f, 0);
+        p = mem(f, 0)[1];
+        done = false;
+      }
+    } else if (c == '"') {
+      uint64_t h;
+      int64_t idx;
+      jstr_emit(b, p, &o, h, idx);
+    } else if (c == '-' || (c >= '0' && c <= '9')) {
+      uint32_t q = p, res = JSON_OK;
+      json_number(b, q, e, res);
+      if (res == JSON_OK) {
+        for (uint32_t i = p; i < q; ++i) o.put(b[i]);
+      } else {
+        char t[40];
+        const uint32_t m = json_number_canon(b, p, q, t);
+        if (m == 0) return JSON_ARENA;
+        for (uint32_t i = 0; i < m; ++i) o.put((uint8_t)t[i]);
+      }
+      p = q;
+    } else {  // true / false / null
+      const uint32_t len = c == 'f' ? 5u : 4u;
+      for (uint32_t i = 0; i < len; ++i) o.put(b[p + i]);
+      p += len;
+    }
+    if (!done) { if (arena[top + 1] == 0) ws(); continue; }
+    // a value completed: the enclosing containers move on
+    for (;;) {
+      if (top == NOF) { olen = o.n; return JSON_OK; }
+      if (arena[top + 1] == 0) {  // array: the next element, or its end
+        ws();
+        if (b[p] == ',') { ++p; ws(); o.put(','); break; }
+        ++p;  // ']'
+        o.put(']');
+        used = top;
+        top = arena[top];
+        continue;
+      }
+      const uint32_t k = arena[top + 2], next = arena[top + 3] + 1;  // object: the next member
+      if (next < k) {
+        arena[top + 3] = next;
+        o.put(',');
+        emit_key(top, next);
+        p = mem(top, next)[1];
+        break;
+      }
+      o.put('}');
+      p = arena[top + 4];
+      used = top;
+      top = arena[top];
+    }
+  }
+}
+
+// The canonical bytes of a whole ContentJSON / Embed / Format content [p, end) — what Yjs writes
+// for it (Y@71991 ContentJSON.write: the count, then each value's JSON.stringify, "undefined" as
+// is; ContentEmbed / ContentFormat: writeJSON, after Format's key) — into out (null: size only),
+// every length prefix in writeVarUint's shortest form. JSON_OK, JSON_BAD or JSON_ARENA.
+YC_HD inline uint32_t json_content_canon(const uint8_t* __restrict__ b, uint32_t p, uint32_t end, uint32_t ref, uint8_t* out,
+                                         uint32_t* arena, uint32_t acap, uint32_t& olen) {
+  bool ok = true;
+  uint32_t o = 0;
+  auto put_vu = [&](uint32_t v) {
+    while (v > 127u) { if (out) out[o] = (uint8_t)(0x80u | (v & 0x7Fu)); ++o; v >>= 7; }
+    if (out) out[o] = (uint8_t)v;
+    ++o;
+  };
+  uint32_t n = 1;
+  if (ref == REF_JSON) { n = rd_vu(b, p, end, ok); put_vu(n); }
+  else if (ref == REF_FORMAT) {
+    const uint32_t k = rd_vu(b, p, end, ok);
+    if (!ok || end - p < k) return JSON_BAD;
+    put_vu(k);
+    for (uint32_t i = 0; i < k; ++i) { if (out) out[o] = b[p + i]; ++o; }
+    p += k;
+  }
+  for (uint32_t i = 0; i < n && ok; ++i) {
+    const uint32_t k = rd_vu(b, p, end, ok);
+    if (!ok || end - p < k) return JSON_BAD;
+    const uint8_t* u = b + p;
+    const bool undef = ref == REF_JSON && k == 9 && u[0] == 'u' && u[1] == 'n' && u[2] == 'd' && u[3] == 'e' && u[4] == 'f' &&
+                       u[5] == 'i' && u[6] == 'n' && u[7] == 'e' && u[8] == 'd';
+    if (undef) {
+      put_vu(9);
+      for (uint32_t j = 0; j < 9; ++j) { if (out) out[o] = u[j]; ++o; }
+    } else {
+      uint32_t len = 0;
+      const uint32_t r = json_canon(b, p, k, nullptr, arena, acap, len);
+      if (r != JSON_OK) return r;
+      put_vu(len);
+      if (out) {
+        uint32_t len2 = 0;
+        json_canon(b, p, k, out + o, arena, acap, len2);
+      }
+      o += len;
+    }
+    p += k;
+  }
+  if (!ok || p != end) return JSON_BAD;
+  olen = o;
+  return JSON_OK;
 }
 
 // Decoded view of one struct (Y@19286 readClientsStructRefs + readItemContent).

@@ -46,6 +46,8 @@ struct Counters {            // device-side counters, read back at the few host 
   uint32_t sync_changed[8];  // per k_sync round: some chunk's chain exit changed (yc_decode.hip)
   uint32_t noncanon;          // lazy decode: an update's sections are not in strictly descending client order
   uint32_t lz_blocks;         // serial lazy merge: output sections
+  uint32_t njson;             // JSON-like contents not in JSON.stringify's form (k_json_structs: listed in jlist)
+  uint32_t njson_pad;
   unsigned long long out_total; // encoded output size (integrate encoder; 64-bit)
   unsigned long long ds_base;   // integrate encoder: byte position of the delete-set section
   unsigned long long items;  // Σ clock lengths of Skip structs (items = Σ all lengths − this)
@@ -143,6 +145,8 @@ struct Work {
   uint32_t* ds_count = nullptr;    // [nupd+1] ranges decoded per update
   uint32_t* ds_dense_off = nullptr;// [nupd+1] scan of ds_count
   uint32_t* ds_len = nullptr;      // [cap_ds+1] clipped lengths (scan input)
+  uint32_t* jlist = nullptr;       // [jcap] structs whose JSON-like content Yjs would write back differently (k_json_structs)
+  uint32_t jcap = 0;
   uint32_t* ds_biglist = nullptr;  // [nupd] updates with more than DSA_WAVE ranges (ctr->ds_big of them): k_units spreads
                                    // their ranges past the first DSA_WAVE over extra workgroups, whichever decoder read them
   // large delete sets decoded grid-wide (yc_decode.hip k_dsp_*): per chunk of the large updates
@@ -722,6 +726,17 @@ void launch_struct_lenscan(const Work& w, uint32_t nstructs, hipStream_t s);
 bool decode_tail_small(const Work& w, uint32_t nstructs, uint32_t nsections, hipStream_t s);
 void launch_decode_tail_small(const Work& w, uint32_t nstructs, uint32_t nsections, hipStream_t s);  // NONE: counts on the device  // one workgroup: structs .. client states (small, integrate)
 void launch_json_structs(const Work& w, uint32_t nstructs, hipStream_t s);  // JSON.parse of JSON-like contents
+// JSON.stringify(JSON.parse(.)) of the listed structs' contents (k_json_canon): one lane per struct,
+// an arena of `acap` words per lane. pass 0 sizes them (items), pass 1 writes them at out + offs[j].
+struct JItem {
+  unsigned long long cpos;  // the content's first byte, as a batch-buffer position (window included)
+  uint32_t clen;            // its bytes in the update
+  uint32_t len;             // its canonical bytes
+  uint32_t res;             // JSON_OK / JSON_BAD / JSON_ARENA
+  uint32_t pad;
+};
+void launch_json_canon(const Work& w, const uint32_t* list, uint32_t n, JItem* items, uint32_t* arena, uint32_t acap,
+                       uint32_t lanes, const unsigned long long* offs, uint8_t* out, hipStream_t s);
 void launch_states(const Work& w, uint32_t nstructs, uint32_t nsections, hipStream_t s);  // clocks + client states
 void launch_struct_clocks(const Work& w, uint32_t nstructs, hipStream_t s);               // clocks only (lazy)
 

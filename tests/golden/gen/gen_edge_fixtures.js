@@ -147,6 +147,70 @@ function assemble(secs, ds) {
   }
 }
 
+// ---- ContentJSON / ContentEmbed / ContentFormat values outside JSON.stringify's form (round 6:
+// rewritten, no longer refused). Yjs 13.5 itself writes ContentAny for JS values; these updates are
+// hand-assembled the way an older Yjs peer (ContentJSON) or a rich-text peer (Embed / Format) sends
+// them, with texts JSON.parse takes but JSON.stringify writes differently. Yjs keeps the parsed
+// values (Y@72137) and writes them with JSON.stringify (Y@71991).
+{
+  const vs = (out, str) => { const b = Buffer.from(str, 'utf8'); writeVu(out, b.length); for (const x of b) out.push(x); };
+  // one section of `client` from clock 0: items [{root, sub?, ref, vals | key+val}], chained by origin
+  function handUpdate(client, items, overlong) {
+    const out = [];
+    writeVu(out, 1); writeVu(out, items.length); writeVu(out, client); writeVu(out, 0);
+    let clock = 0; let prev = null;
+    for (const it of items) {
+      const chain = prev && prev.root === it.root && !it.sub && !prev.sub;
+      out.push(it.ref | (chain ? 0x80 : 0) | (!chain && it.sub ? 0x20 : 0));
+      if (chain) { writeVu(out, client); writeVu(out, clock - 1); }
+      else { writeVu(out, 1); vs(out, it.root); if (it.sub) vs(out, it.sub); }
+      let len = 1;
+      if (it.ref === 2) {
+        writeVu(out, it.vals.length);
+        for (const v of it.vals) {
+          if (overlong) { const b = Buffer.from(v, 'utf8'); out.push(0x80 | (b.length & 0x7f), b.length >> 7); for (const x of b) out.push(x); }
+          else vs(out, v);
+        }
+        len = it.vals.length;
+      } else if (it.ref === 5) {
+        vs(out, it.val);
+      } else {
+        vs(out, it.key); vs(out, it.val);
+      }
+      clock += len; prev = it;
+    }
+    out.push(0);  // no delete set
+    return new Uint8Array(out);
+  }
+  const deep = '['.repeat(90) + ' 1.0 ' + ']'.repeat(90);
+  const sets = {
+    array_values: [{ root: 'messages', ref: 2, vals: ['0.30000000000000004', ' 1 ', '1.50', '{"b":1,"a":2,"b":3}', '"\\u0041\\/"', '1e400', 'undefined',
+      '{"2":1,"1":2,"a":3,"0":[]}', '[1.0, 2.50, -0.0]', '"\\ud83d\\ude00\\ud800"', '123456789012345678901234567890', deep, '1e-7', '{"__proto__":{"x" :1}}'] }],
+    map_values: [{ root: 'users', sub: 'k1', ref: 2, vals: [' {"x" : 1e2} '] }, { root: 'users', sub: 'k2', ref: 2, vals: ['-0'] },
+      { root: 'users', sub: 'k3', ref: 2, vals: ['{"a":1,"\\u0061":2}'] }, { root: 'users', sub: 'k4', ref: 2, vals: ['0.1', ' "x" '] }],
+    embed_format: [{ root: 'messages', ref: 5, val: ' {"insert" : "x", "n": 1.0} ' }, { root: 'messages', ref: 2, vals: ['[ ]'] },
+      { root: 'users', sub: 'f', ref: 6, key: 'bold', val: ' true ' }],
+    canonical_long: [{ root: 'messages', ref: 2, vals: ['0.30000000000000004', '1.7976931348623157e+308', '5e-324', '123456789012345680000', '"\\u001f"'] }],
+  };
+  const base = new Y.Doc(); base.clientID = 303;
+  base.getMap('users').set('k1', 'base'); base.getArray('messages').push(['m0', 1]);
+  const baseU = Y.encodeStateAsUpdate(base);
+  Object.entries(sets).forEach(([name, items], i) => {
+    for (const overlong of [false, true]) {
+      if (overlong && name !== 'array_values' && name !== 'map_values') continue;
+      const u = handUpdate(1000 + i, items, overlong);
+      const roots = { users: 'map', messages: 'array' };
+      const rec = { name: `json_${name}${overlong ? '_overlong' : ''}`, kind: 'json', update: hex(u), base: hex(baseU), roots };
+      Object.assign(rec, result([u], roots));
+      const both = result([baseU, u], roots);
+      rec.state_with_base = both.state; rec.sv_with_base = both.sv; rec.json_with_base = both.json;
+      const outs = { merged_with_base: Y.mergeUpdates([baseU, u]), merged_pair: Y.mergeUpdates([u, u]), diff_empty: Y.diffUpdate(u, new Uint8Array([0])) };
+      for (const [k, v] of Object.entries(outs)) { rec[k] = hexc(v); rec[k + '_raw'] = hex(v); }
+      cases.push(rec);
+    }
+  });
+}
+
 const outDir = process.argv[2] || path.join(__dirname, '..');
 fs.writeFileSync(path.join(outDir, 'edges.json'), JSON.stringify({ yjs: '13.5.16', cases }, null, 0));
 console.log(`edges.json: ${cases.length} cases`);

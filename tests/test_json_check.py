@@ -1,12 +1,14 @@
-"""ContentJSON / ContentEmbed / ContentFormat values (yc_parse.h json_check) against Node's own
-JSON: tests/golden/json_forms.json (tests/golden/gen/gen_json_fixtures.js) records, for 2 566
-seeded strings, whether JSON.parse throws (the engine must refuse the update: Yjs throws
-SyntaxError in readContentJSON / readJSON, Y@72137 / Y@14715) and whether JSON.stringify gives the
-text back (Yjs writes the parsed value with JSON.stringify, Y@71991; the engine copies the bytes,
-so it refuses — YCRDT_E_UNSUPPORTED — what it would write differently). The host build of the
-function the decoder runs: no case may be accepted that Node refuses or writes differently; some
-canonical texts are refused conservatively (more than 15 significant digits, subnormal numbers),
-counted here."""
+"""ContentJSON / ContentEmbed / ContentFormat values (yc_parse.h json_check, json_canon) against Node's
+own JSON: tests/golden/json_forms.json (tests/golden/gen/gen_json_fixtures.js) records, for 5 399
+seeded strings, whether JSON.parse throws (the engine must refuse the update: Yjs throws SyntaxError
+in readContentJSON / readJSON, Y@72137 / Y@14715), whether JSON.stringify gives the text back, and
+JSON.stringify(JSON.parse(s)). Yjs keeps the parsed value and writes it with JSON.stringify
+(Y@71991), so the engine rewrites every value not in that form (yc_decode.hip k_json_canon) instead
+of refusing it. The host build of the functions the decoder runs: json_check's verdict must match
+Node's (a canonical text nested past its level mask may be left unjudged: it is rewritten to
+itself), and json_canon's text must equal Node's for every valid case and refuse every malformed
+one — long numbers (0.30000000000000004, 800-digit and halfway forms, subnormals, overflow to
+null), deep nesting, duplicate / array-index / escaped keys, escapes of every kind."""
 import json
 import os
 import subprocess
@@ -21,10 +23,12 @@ def test_json_check_matches_node(tmp_path):
                            os.path.join(HERE, "csrc", "json_check_main.cpp"), "-o", str(exe)])
     with open(os.path.join(HERE, "golden", "json_forms.json")) as f:
         cases = json.load(f)["cases"]
-    inp = "".join(f"{w} {h}\n" for w, h in cases)
+    inp = "".join(f"{w} {h} {c}\n" for w, h, c in cases)
     r = subprocess.run([str(exe)], input=inp, capture_output=True, text=True)
     assert r.returncode == 0, r.stdout[-2000:]
     last = r.stdout.strip().splitlines()[-1].split()
-    assert int(last[1]) == len(cases) and int(last[3]) == 0
-    assert int(last[5]) < len(cases) // 8  # conservative refusals stay a small minority
-    assert {w for w, _ in cases} == {0, 1, 2}
+    assert int(last[1]) == len(cases) and int(last[3]) == 0 and int(last[9]) == 0
+    assert int(last[5]) <= 8  # canonical texts json_check leaves to json_canon (nesting past 64 levels)
+    assert int(last[7]) == sum(1 for w, _, _ in cases if w != 1)
+    assert {w for w, _, _ in cases} == {0, 1, 2}
+    assert any(bytes.fromhex(h) == b"0.30000000000000004" and w == 0 for w, h, _ in cases)

@@ -141,7 +141,9 @@ def _edges():
 
     _sys.setrecursionlimit(max(_sys.getrecursionlimit(), 20000))  # 2 000-level JSON values
     with open(_os.path.join(_os.path.dirname(__file__), "golden", "edges.json")) as f:
-        return _json.load(f)["cases"]
+        # (the "json" cases — ContentJSON texts Yjs rewrites with JSON.stringify — are pinned on the
+        # GPU side against the fixture itself, test_gpu_json_rewrite.py; the oracle copies such texts)
+        return [c for c in _json.load(f)["cases"] if c["kind"] != "json"]
 
 
 def test_oracle_edge_fixtures_apply():
