@@ -3398,7 +3398,9 @@ __device__ __forceinline__ void struct_decode_one(const Work& w, uint32_t i, uin
     canon_hdr = h == v.cpos - p0 - 1;
   }
   // bit 6: the content's `any` values are not in writeAny's form (the encoders re-encode them)
-  w.s_pk[i] = (uint8_t)(pk | (canon_hdr ? 0u : 0x80u) | ((v.anyf & ANY_REENCODE) ? 0x40u : 0u));
+  // bit 5: object keys JS treats specially (ANY_KEYS): the struct is rewritten before the merge
+  // (k_json_structs lists it, k_json_canon writes writeAny(readAny(.)) of its content)
+  w.s_pk[i] = (uint8_t)(pk | (canon_hdr ? 0u : 0x80u) | ((v.anyf & ANY_REENCODE) ? 0x40u : 0u) | ((v.anyf & ANY_KEYS) ? 0x20u : 0u));
   if (pk != 0) {
     w.s_pa[i] = pa;
     w.s_pb[i] = pb;
@@ -3412,7 +3414,7 @@ __device__ __forceinline__ void struct_decode_one(const Work& w, uint32_t i, uin
   w.s_celem[i] = celem;
   // a JSON / Embed / Format content: JSON.parse runs in k_json_structs (a call from here, however
   // rare, cost every struct one wave per SIMD: the kernel's registers cover the callee's)
-  wave_flag(&w.ctr->any_json, ref0 == REF_JSON || ref0 == REF_EMBED || ref0 == REF_FORMAT);
+  wave_flag(&w.ctr->any_json, ref0 == REF_JSON || ref0 == REF_EMBED || ref0 == REF_FORMAT || (v.anyf & ANY_KEYS) != 0);
 }
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_struct_decode(Work w, uint32_t nstructs) {
   __shared__ __attribute__((aligned(16))) uint32_t win[256 * SD_STRIDE];
@@ -3434,6 +3436,11 @@ __global__ __launch_bounds__(256) void k_json_structs(Work w, uint32_t nstructs)
   if (i >= nstructs) return;
   const uint8_t* __restrict__ bw = struct_bytes(w, i);
   const uint32_t ref = bw[w.s_pos[i]] & 31u;  // (the input's info byte: superseded sections' structs too)
+  if (ref == REF_ANY && (w.s_pk[i] & 0x20u)) {  // `any` objects with keys JS treats specially: rewritten
+    const uint32_t k = atomicAdd(&w.ctr->njson, 1u);
+    if (k < w.jcap) w.jlist[k] = i;
+    return;
+  }
   if (ref != REF_JSON && ref != REF_EMBED && ref != REF_FORMAT) return;
   const int jr = json_content(bw, w.s_cpos[i], w.s_cend[i], ref);
   if (jr > 0) raise_err(&w.ctr->err, ERR_DECODE);

@@ -132,8 +132,16 @@ YC_HDI uint32_t skip_str(const Src& b, uint32_t& p, uint32_t end, bool& ok) {  /
 // float64 it widens to), a positive varint past 0x7FFFFFFF (-> float32 / float64). Such values are
 // flagged ANY_REENCODE and the encoders write them canonically (any_canon below). What needs JS
 // object semantics — array-index keys after others or out of order (Object.keys order), the key
-// "__proto__", a negative integer past 2^32 (writeVarInt's 32-bit shifts) — is ANY_UNSUP: refused.
-enum : uint32_t { ANY_REENCODE = 1u, ANY_UNSUP = 2u };
+// "__proto__" (readAny's obj[key] = v: the prototype setter, no own member), a key that may repeat
+// (the last value at the first key's place) — is ANY_KEYS: the struct is rewritten on the device
+// before the merge (any_content_canon, yc_decode.hip k_json_canon), as Yjs's decode + writeAny would.
+// A repeat is judged by a 64-bit mask of key hashes per object: a false alarm costs a rewrite pass
+// that changes nothing. ANY_UNSUP — refused — is left for a negative integer past 2^32 (writeVarInt's
+// 32-bit shifts write bytes no reader gets the number back from) and a "__proto__" member holding an
+// array or bytes (the object then passes `instanceof Array / Uint8Array` in writeAny).
+enum : uint32_t { ANY_REENCODE = 1u, ANY_UNSUP = 2u, ANY_KEYS = 4u };
+// the bit of a key in an object's repeat mask (its length and first and last bytes)
+YC_HDI uint64_t key_bit(uint32_t n, uint32_t c0, uint32_t c1) { return 1ull << ((n * 7u + c0 * 3u + c1) & 63u); }
 YC_HDI uint32_t vu_overlong(const uint8_t* __restrict__ b, uint32_t p0, uint32_t p1) {  // [p0, p1) one varuint
   return (p1 - p0 > 1 && b[p1 - 1] == 0u) ? ANY_REENCODE : 0u;
 }
@@ -226,6 +234,7 @@ YC_HD inline bool skip_any(const uint8_t* __restrict__ b, uint32_t& p, uint32_t 
   const PtrSrc src{b};
   uint32_t cf = 0;                  // ANY_* flags (UTF8 mode: the exact parse checks the encoding)
   int64_t lastkey[UTF8 ? DEPTH + 1 : 1];  // per object level: the last array-index key, or -2 after a string key
+  uint64_t keym[UTF8 ? DEPTH + 1 : 1];    // per object level: the repeat mask of its keys (key_bit)
   // A level is kept only while members FOLLOW the one being read (rem[d] >= 1): the last member of
   // a container is read in the container's place (a tail position), so nesting along last members
   // — [[[..]]], {a: {b: ..}}, however deep — takes no stack, and DEPTH bounds only containers
@@ -283,9 +292,12 @@ YC_HD inline bool skip_any(const uint8_t* __restrict__ b, uint32_t& p, uint32_t 
             if (UTF8 && ok && !utf8_valid(src, st, k)) return false;
             if (UTF8 && ok) {
               cf |= vu_overlong(b, q0, st);
-              if (key_proto(b, st, k)) cf |= ANY_UNSUP;
+              if (key_proto(b, st, k)) cf |= (p < end && (b[p] == 116 || b[p] == 117)) ? ANY_UNSUP : ANY_KEYS;
               const int64_t ki = key_index(b, st, k);
-              if (n > 1) lastkey[d - 1] = ki >= 0 ? ki : -2;
+              if (n > 1) {
+                lastkey[d - 1] = ki >= 0 ? ki : -2;
+                keym[d - 1] = key_bit(k, k ? b[st] : 0u, k ? b[st + k - 1] : 0u);
+              }
             }
           }
           if (!ok) return false;
@@ -311,29 +323,34 @@ YC_HD inline bool skip_any(const uint8_t* __restrict__ b, uint32_t& p, uint32_t 
       if (!ok || (UTF8 && !utf8_valid(src, st, k))) return false;
       if (UTF8) {
         cf |= vu_overlong(b, q0, st);
-        if (key_proto(b, st, k)) cf |= ANY_UNSUP;
+        if (key_proto(b, st, k)) cf |= (p < end && (b[p] == 116 || b[p] == 117)) ? ANY_UNSUP : ANY_KEYS;
         // Object.keys order: array-index keys first, ascending; then the others in insertion order
-        // (a repeated string key keeps its first place; not detected here)
+        // (a repeated key keeps its first place: a possible repeat is flagged by the key mask)
         const int64_t ki = key_index(b, st, k), prev = lastkey[lvl];
-        if (ki >= 0 && (prev == -2 || (prev >= 0 && ki <= prev))) cf |= ANY_UNSUP;
+        if (ki >= 0 && (prev == -2 || (prev >= 0 && ki <= prev))) cf |= ANY_KEYS;
         lastkey[lvl] = ki >= 0 ? ki : -2;
+        const uint64_t kb = key_bit(k, k ? b[st] : 0u, k ? b[st + k - 1] : 0u);
+        if (keym[lvl] & kb) cf |= ANY_KEYS;
+        keym[lvl] |= kb;
       }
     }
     if (--rem[lvl] == 0) --d;
   }
 }
 
-// An object key's flags through a byte source: ANY_UNSUP for "__proto__"; ki = its array index
-// (key_index), else -1
+// An object key's flags through a byte source: ANY_KEYS for "__proto__" (ANY_UNSUP when its value,
+// the byte after the key, is bytes or an array); ki = its array index (key_index), else -1
 template <class S>
-YC_HDI uint32_t key_flags_at(const S& b, uint32_t p, uint32_t n, int64_t& ki) {
+YC_HDI uint32_t key_flags_at(const S& b, uint32_t p, uint32_t n, uint32_t end, int64_t& ki) {
   ki = -1;
   const uint32_t c0 = n ? b.u8(p) : 0u;
   if (n == 9 && c0 == '_') {
     const char* k = "__proto__";
     uint32_t i = 0;
     while (i < 9 && b.u8(p + i) == (uint8_t)k[i]) ++i;
-    return i == 9 ? ANY_UNSUP : 0u;
+    if (i != 9) return 0u;
+    const uint32_t t = p + 9 < end ? b.u8(p + 9) : 0u;
+    return (t == 116u || t == 117u) ? ANY_UNSUP : ANY_KEYS;
   }
   if (n == 0 || n > 10 || c0 < '0' || c0 > '9' || (n > 1 && c0 == '0')) return 0u;
   uint64_t v = 0;
@@ -380,6 +397,7 @@ YC_HDI bool any_flat(const S& b, uint32_t& p, uint32_t end, uint32_t& steps, boo
   if (!o || m > 8 || st < m + 1) return false;
   if (FULL) c |= vu_overlong_at(b, p0 + 1, q);
   int64_t prev = -1;
+  uint64_t km = 0;  // the keys' repeat mask
   for (uint32_t i = 0; i < m; ++i) {
     if (tag == 118) {  // the member's key
       const uint32_t k0 = q, k = b.vu(q, end, o);
@@ -390,10 +408,13 @@ YC_HDI bool any_flat(const S& b, uint32_t& p, uint32_t end, uint32_t& steps, boo
         if (!utf8_valid(b, ks, k)) o = false;
         c |= vu_overlong_at(b, k0, ks);
         int64_t ki;
-        c |= key_flags_at(b, ks, k, ki);
+        c |= key_flags_at(b, ks, k, end, ki);
         // Object.keys order: array-index keys first, ascending, then the others (skip_any)
-        if (ki >= 0 && (prev == -2 || (prev >= 0 && ki <= prev))) c |= ANY_UNSUP;
+        if (ki >= 0 && (prev == -2 || (prev >= 0 && ki <= prev))) c |= ANY_KEYS;
         prev = ki >= 0 ? ki : -2;
+        const uint64_t kb = key_bit(k, k ? b.u8(ks) : 0u, k ? b.u8(ks + k - 1) : 0u);
+        if (km & kb) c |= ANY_KEYS;
+        km |= kb;
       }
       if (!o) { ok = false; p = q; return true; }
     }
@@ -1052,8 +1073,11 @@ YC_HD inline __attribute__((noinline)) uint32_t json_canon(const uint8_t* __rest
 // for it (Y@71991 ContentJSON.write: the count, then each value's JSON.stringify, "undefined" as
 // is; ContentEmbed / ContentFormat: writeJSON, after Format's key) — into out (null: size only),
 // every length prefix in writeVarUint's shortest form. JSON_OK, JSON_BAD or JSON_ARENA.
+YC_HD inline uint32_t any_content_canon(const uint8_t* __restrict__ b, uint32_t p, uint32_t end, uint8_t* out,
+                                        uint32_t* arena, uint32_t acap, uint32_t& olen);
 YC_HD inline uint32_t json_content_canon(const uint8_t* __restrict__ b, uint32_t p, uint32_t end, uint32_t ref, uint8_t* out,
                                          uint32_t* arena, uint32_t acap, uint32_t& olen) {
+  if (ref == REF_ANY) return any_content_canon(b, p, end, out, arena, acap, olen);  // (object key semantics, ANY_KEYS)
   bool ok = true;
   uint32_t o = 0;
   auto put_vu = [&](uint32_t v) {
@@ -1094,6 +1118,237 @@ YC_HD inline uint32_t json_content_canon(const uint8_t* __restrict__ b, uint32_t
   }
   if (!ok || p != end) return JSON_BAD;
   olen = o;
+  return JSON_OK;
+}
+
+// ---- writeAny(readAny(bytes)) for the `any` values whose object keys JS treats specially (ANY_KEYS):
+// readAny builds each object with obj[key] = value (L0@1937), so a "__proto__" member sets the
+// prototype instead of a member, a repeated key keeps its first place with its last value, and
+// Object.keys — the order writeAny writes (L0 writeAny) — lists array-index keys first, ascending.
+// Every scalar comes out in writeAny's form too (any_canon's rules). Iterative over arena frames
+// like json_canon: per open container 5 words (previous frame, kind 0 array / 1 object, count,
+// next member, position past the object) and per open object 5 words a member (key bytes, key
+// length, value position, array index or ~0, key hash).
+// past one `any` value at p (any depth; the level counts in arena[base, acap)): false if malformed
+// or past the arena
+YC_HD inline bool any_skip_deep(const uint8_t* __restrict__ b, uint32_t& p, uint32_t end, uint32_t* arena, uint32_t base, uint32_t acap) {
+  bool ok = true;
+  uint32_t d = 0;
+  for (;;) {
+    if (p >= end) return false;
+    const uint32_t tag = b[p++];
+    switch (tag) {
+      case 127: case 126: case 121: case 120: break;
+      case 125: skip_vi(b, p, end, ok); break;
+      case 124: skip_bytes(p, 4, end, ok); break;
+      case 123: case 122: skip_bytes(p, 8, end, ok); break;
+      case 119: case 116: { const uint32_t n = rd_vu(b, p, end, ok); if (ok) skip_bytes(p, n, end, ok); break; }
+      case 117: case 118: {
+        const uint32_t n = rd_vu(b, p, end, ok);
+        if (!ok) return false;
+        if (n > 0) {
+          if (base + d >= acap || n > 0x7FFFFFFFu) return false;
+          arena[base + d++] = n | (tag == 118 ? 0x80000000u : 0u);
+          if (tag == 118) { const uint32_t k = rd_vu(b, p, end, ok); if (ok) skip_bytes(p, k, end, ok); }
+          if (!ok) return false;
+          continue;
+        }
+        break;
+      }
+      default: return false;
+    }
+    if (!ok) return false;
+    for (;;) {
+      if (d == 0) return true;
+      uint32_t& top = arena[base + d - 1];
+      if (((top & 0x7FFFFFFFu) - 1) == 0) { --d; continue; }
+      --top;
+      if (top & 0x80000000u) { const uint32_t k = rd_vu(b, p, end, ok); if (ok) skip_bytes(p, k, end, ok); if (!ok) return false; }
+      break;
+    }
+  }
+}
+YC_HD inline __attribute__((noinline)) uint32_t any_content_canon(const uint8_t* __restrict__ b, uint32_t p, uint32_t end, uint8_t* out,
+                                                                 uint32_t* arena, uint32_t acap, uint32_t& olen) {
+  olen = 0;
+  bool ok = true;
+  JOut o{out, 0};
+  auto put_vu = [&](uint32_t v) { while (v > 0x7Fu) { o.put(0x80u | (v & 0x7Fu)); v >>= 7; } o.put(v); };
+  auto put_vi = [&](bool neg, uint32_t m) {
+    o.put((m > 63u ? 0x80u : 0u) | (neg ? 0x40u : 0u) | (m & 63u));
+    m >>= 6;
+    while (m) { o.put((m > 127u ? 0x80u : 0u) | (m & 127u)); m >>= 7; }
+  };
+  auto put_num = [&](double x) -> bool {  // writeAny(number)
+    const uint32_t k = num_form(x);
+    if (k == 3) return false;
+    if (k == 0) {
+      const bool neg = x < 0 || (x == 0 && (f64_bits(x) >> 63));
+      put_vi(neg, (uint32_t)(x < 0 ? -x : x));
+      return true;
+    }
+    if (k == 1) {
+      union { float f; uint32_t u; } c;
+      c.f = (float)x;
+      for (int sh = 24; sh >= 0; sh -= 8) o.put((c.u >> sh) & 0xFFu);
+      return true;
+    }
+    const uint64_t u = f64_bits(x);
+    for (int sh = 56; sh >= 0; sh -= 8) o.put((uint32_t)(u >> sh) & 0xFFu);
+    return true;
+  };
+  auto num_tag = [&](double x) -> uint32_t { const uint32_t k = num_form(x); return k == 0 ? 125u : k == 1 ? 124u : 123u; };
+  constexpr uint32_t NOF = 0xFFFFFFFFu;
+  auto mem = [&](uint32_t f, uint32_t i) -> uint32_t* { return arena + f + 5 + 5 * i; };
+  const uint32_t n = rd_vu(b, p, end, ok);
+  if (!ok) return JSON_BAD;
+  put_vu(n);
+  for (uint32_t e = 0; e < n; ++e) {
+    uint32_t top = NOF, used = 0;
+    for (;;) {
+      // one value at p
+      if (p >= end) return JSON_BAD;
+      const uint32_t tag = b[p++], s0 = p;
+      bool done = true;
+      switch (tag) {
+        case 127: case 126: case 121: case 120: o.put(tag); break;
+        case 125: {
+          skip_vi(b, p, end, ok);
+          if (!ok) return JSON_BAD;
+          bool neg;
+          const uint32_t m = vi_decode(b, s0, p, neg);
+          if (!neg && m > 0x7FFFFFFFu) { o.put(num_tag((double)m)); put_num((double)m); }
+          else { o.put(125); put_vi(neg, m); }
+          break;
+        }
+        case 124: case 123: {
+          skip_bytes(p, tag == 124 ? 4u : 8u, end, ok);
+          if (!ok) return JSON_BAD;
+          const double x = tag == 124 ? f32_of(be32(b, s0)) : f64_of(be64(b, s0));
+          o.put(num_tag(x));
+          if (!put_num(x)) return JSON_ARENA;  // (a negative integer past 2^32: refused)
+          break;
+        }
+        case 122: skip_bytes(p, 8, end, ok); if (!ok) return JSON_BAD; o.put(122); for (uint32_t i = s0; i < p; ++i) o.put(b[i]); break;
+        case 119: case 116: {
+          const uint32_t k = rd_vu(b, p, end, ok);
+          if (!ok || end - p < k) return JSON_BAD;
+          o.put(tag);
+          put_vu(k);
+          for (uint32_t i = 0; i < k; ++i) o.put(b[p + i]);
+          p += k;
+          break;
+        }
+        case 117: {
+          const uint32_t m = rd_vu(b, p, end, ok);
+          if (!ok) return JSON_BAD;
+          o.put(117);
+          put_vu(m);
+          if (m > 0) {
+            if (used + 5 > acap) return JSON_ARENA;
+            arena[used] = top; arena[used + 1] = 0; arena[used + 2] = m; arena[used + 3] = 0; arena[used + 4] = 0;
+            top = used;
+            used += 5;
+            done = false;
+          }
+          break;
+        }
+        case 118: {
+          const uint32_t m = rd_vu(b, p, end, ok);
+          if (!ok) return JSON_BAD;
+          const uint32_t f = used;
+          if ((uint64_t)f + 5 + 5ull * m > acap) return JSON_ARENA;
+          uint32_t k = 0;
+          for (uint32_t j = 0; j < m; ++j) {
+            const uint32_t kl = rd_vu(b, p, end, ok);
+            if (!ok || end - p < kl) return JSON_BAD;
+            const uint32_t ks = p;
+            p += kl;
+            const uint32_t vp = p;
+            if (!any_skip_deep(b, p, end, arena, f + 5 + 5 * m, acap)) return JSON_ARENA;
+            if (key_proto(b, ks, kl)) {  // the prototype setter: no own member
+              if (b[vp] == 116 || b[vp] == 117) return JSON_ARENA;  // (instanceof Uint8Array / Array: refused)
+              continue;
+            }
+            uint32_t h = 2166136261u;
+            for (uint32_t i = 0; i < kl; ++i) h = (h ^ b[ks + i]) * 16777619u;
+            bool dup = false;
+            for (uint32_t i = 0; i < k && !dup; ++i) {
+              uint32_t* r = mem(f, i);
+              if (r[4] != h || r[1] != kl) continue;
+              uint32_t q = 0;
+              while (q < kl && b[r[0] + q] == b[ks + q]) ++q;
+              if (q == kl) { r[2] = vp; dup = true; }  // the last value, at the first key's place
+            }
+            if (dup) continue;
+            uint32_t* r = mem(f, k++);
+            const int64_t ki = key_index(b, ks, kl);
+            r[0] = ks; r[1] = kl; r[2] = vp; r[3] = ki >= 0 ? (uint32_t)ki : NOF; r[4] = h;
+          }
+          // array-index keys first, ascending (the others keep their order)
+          uint32_t ni = 0;
+          for (uint32_t j = 0; j < k; ++j) {
+            uint32_t* rj = mem(f, j);
+            if (rj[3] == NOF) continue;
+            uint32_t t[5];
+            for (int w = 0; w < 5; ++w) t[w] = rj[w];
+            uint32_t i = j;
+            while (i > 0) {
+              uint32_t* rp = mem(f, i - 1);
+              if (i - 1 < ni && rp[3] <= t[3]) break;
+              uint32_t* rc = mem(f, i);
+              for (int w = 0; w < 5; ++w) rc[w] = rp[w];
+              --i;
+            }
+            uint32_t* ri = mem(f, i);
+            for (int w = 0; w < 5; ++w) ri[w] = t[w];
+            ++ni;
+          }
+          o.put(118);
+          put_vu(k);
+          if (k > 0) {
+            arena[f] = top; arena[f + 1] = 1; arena[f + 2] = k; arena[f + 3] = 0; arena[f + 4] = p;
+            top = f;
+            used = f + 5 + 5 * k;
+            const uint32_t* r = mem(f, 0);
+            put_vu(r[1]);
+            for (uint32_t i = 0; i < r[1]; ++i) o.put(b[r[0] + i]);
+            p = r[2];
+            done = false;
+          }
+          break;
+        }
+        default: return JSON_BAD;
+      }
+      if (!done) continue;
+      // a value completed: the open containers move on
+      bool fin = false;
+      for (;;) {
+        if (top == NOF) { fin = true; break; }
+        if (arena[top + 1] == 0) {  // array: its next element follows in the text
+          if (--arena[top + 2] > 0) break;
+          used = top;
+          top = arena[top];
+          continue;
+        }
+        const uint32_t k = arena[top + 2], next = arena[top + 3] + 1;
+        if (next < k) {
+          arena[top + 3] = next;
+          const uint32_t* r = mem(top, next);
+          put_vu(r[1]);
+          for (uint32_t i = 0; i < r[1]; ++i) o.put(b[r[0] + i]);
+          p = r[2];
+          break;
+        }
+        p = arena[top + 4];
+        used = top;
+        top = arena[top];
+      }
+      if (fin) break;
+    }
+  }
+  if (p != end) return JSON_BAD;
+  olen = o.n;
   return JSON_OK;
 }
 
