@@ -155,14 +155,16 @@ function assemble(secs, ds) {
 {
   const vs = (out, str) => { const b = Buffer.from(str, 'utf8'); writeVu(out, b.length); for (const x of b) out.push(x); };
   // one section of `client` from clock 0: items [{root, sub?, ref, vals | key+val}], chained by origin
-  function handUpdate(client, items, overlong) {
+  function handUpdate(client, items, overlong, after) {  // after: [client, clock] the first item's origin
     const out = [];
     writeVu(out, 1); writeVu(out, items.length); writeVu(out, client); writeVu(out, 0);
     let clock = 0; let prev = null;
     for (const it of items) {
       const chain = prev && prev.root === it.root && !it.sub && !prev.sub;
-      out.push(it.ref | (chain ? 0x80 : 0) | (!chain && it.sub ? 0x20 : 0));
+      const ext = !prev && after;
+      out.push(it.ref | (chain || ext ? 0x80 : 0) | (!chain && !ext && it.sub ? 0x20 : 0));
       if (chain) { writeVu(out, client); writeVu(out, clock - 1); }
+      else if (ext) { writeVu(out, after[0]); writeVu(out, after[1]); }
       else { writeVu(out, 1); vs(out, it.root); if (it.sub) vs(out, it.sub); }
       let len = 1;
       if (it.ref === 2) {
@@ -209,6 +211,25 @@ function assemble(secs, ds) {
       cases.push(rec);
     }
   });
+  // pending: the texts arrive in an update whose first item follows another client's item not yet
+  // seen (Yjs parks it: pendingStructs, written back by encodeStateAsUpdate), then the dependency
+  {
+    const dep = new Y.Doc(); dep.clientID = 1999;
+    dep.getArray('messages').push(['d0', 'd1']);
+    const depU = Y.encodeStateAsUpdate(dep);
+    const u = handUpdate(2000, [{ root: 'messages', ref: 2, vals: [' 1.50 ', '{"b":1,"a":[ 1e2 ],"b":2}', '"\\u00e9"'] }], false, [1999, 1]);
+    const roots = { users: 'map', messages: 'array' };
+    const rec = { name: 'json_pending', kind: 'json_pending', update: hex(u), dep: hex(depU), roots };
+    const d = new Y.Doc(); d.clientID = 0x7ffffff0;
+    Y.applyUpdate(d, u);
+    rec.state_pending = hex(canonicalUpdate(Y.encodeStateAsUpdate(d)));
+    rec.sv_pending = hex(canonicalSv(Y.encodeStateVector(d)));
+    Y.applyUpdate(d, depU);
+    rec.state = hex(canonicalUpdate(Y.encodeStateAsUpdate(d)));
+    rec.sv = hex(canonicalSv(Y.encodeStateVector(d)));
+    rec.json = JSON.parse(JSON.stringify({ users: d.getMap('users').toJSON(), messages: d.getArray('messages').toJSON() }));
+    cases.push(rec);
+  }
 }
 
 const outDir = process.argv[2] || path.join(__dirname, '..');

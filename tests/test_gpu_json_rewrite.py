@@ -34,6 +34,12 @@ def cases():
 
 
 @pytest.fixture(scope="module")
+def pending_case():
+    with open(os.path.join(HERE, "golden", "edges.json")) as f:
+        return [c for c in json.load(f)["cases"] if c["kind"] == "json_pending"][0]
+
+
+@pytest.fixture(scope="module")
 def e135():
     e = crdt_amd.Engine(int(os.environ.get("YCRDT_DEVICE", "0")), compat=135)
     yield e
@@ -72,6 +78,23 @@ def test_json_apply(cases, mode, monkeypatch):
         d3.encode_state_vector()
         d3.apply_update(u)
         _check_doc(d3, c, "_with_base")
+
+
+@pytest.mark.gpu
+def test_json_pending(pending_case):
+    """The texts in an update Yjs parks (its first item follows an item of a client not seen yet):
+    Yjs writes the parked structs back re-encoded (pendingStructs, Y@21330), then integrates them
+    when the dependency arrives."""
+    c = pending_case
+    d = crdt_amd.Doc(client_id=0x7FFFFFF0)
+    d.apply_update(bytes.fromhex(c["update"]))
+    assert d.encode_state_as_update().hex() == c["state_pending"]
+    assert d.encode_state_vector().hex() == c["sv_pending"]
+    d.apply_update(bytes.fromhex(c["dep"]))
+    assert d.encode_state_as_update().hex() == c["state"]
+    assert d.encode_state_vector().hex() == c["sv"]
+    for root, kind in c["roots"].items():
+        assert json.loads(d.root_json(root, kind)) == c["json"][root]
 
 
 @pytest.mark.gpu

@@ -143,7 +143,7 @@ def _edges():
     with open(_os.path.join(_os.path.dirname(__file__), "golden", "edges.json")) as f:
         # (the "json" cases — ContentJSON texts Yjs rewrites with JSON.stringify — are pinned on the
         # GPU side against the fixture itself, test_gpu_json_rewrite.py; the oracle copies such texts)
-        return [c for c in _json.load(f)["cases"] if c["kind"] != "json"]
+        return [c for c in _json.load(f)["cases"] if not c["kind"].startswith("json")]
 
 
 def test_oracle_edge_fixtures_apply():
