@@ -856,7 +856,6 @@ constexpr uint32_t JARENA_WORDS = JSON_ARENA_WORDS;  // arena per lane (yc_parse
 constexpr uint32_t JLANES = 256;
 int json_rewrite(ycrdt_engine* e, ycrdt_batch* b, uint32_t n, const ShardSpec* sh, bool& restaged) {
   restaged = false;
-  if (sh) return fail(YCRDT_E_UNSUPPORTED, "a ContentJSON / Embed / Format value outside JSON.stringify's form in a sharded merge");
   if (++b->jpasses > 8) return fail(YCRDT_E_DEVICE, "internal: the JSON rewrite did not settle");
   Work& w = e->w;
   auto& V = e->bufs;
@@ -883,6 +882,13 @@ int json_rewrite(ycrdt_engine* e, ycrdt_batch* b, uint32_t n, const ShardSpec* s
   if (!ok) return fail(YCRDT_E_DEVICE, oom("JSON rewrite"));
   HIPCHK(hipMemcpyAsync(offs, off.data(), sizeof(unsigned long long) * n, hipMemcpyHostToDevice, s));
   launch_json_canon(w, w.jlist, n, items, arena, JARENA_WORDS, lanes, offs, cout, s);
+  HIPCHK(hipMemcpyAsync(it.data(), items, sizeof(JItem) * n, hipMemcpyDeviceToHost, s));
+  HIPCHK(hipStreamSynchronize(s));
+  bool any_diff = false;
+  for (uint32_t j = 0; j < n; ++j) any_diff |= it[j].pad != 0;
+  if (!any_diff) return YCRDT_OK;  // already in the form Yjs writes (compared on the device)
+  // (a sharded merge parses each update on one rank only: a rewrite would have to be agreed on)
+  if (sh) return fail(YCRDT_E_UNSUPPORTED, "a ContentJSON / Embed / Format or `any` value Yjs writes back differently, in a sharded merge");
   std::vector<uint8_t> canon(total);
   if (total) HIPCHK(hipMemcpyAsync(canon.data(), cout, total, hipMemcpyDeviceToHost, s));
   // the updates as staged (layout order), and which of them a content lies in
@@ -900,8 +906,7 @@ int json_rewrite(ycrdt_engine* e, ycrdt_batch* b, uint32_t n, const ShardSpec* s
     for (size_t v = 0; v < nu; ++v)
       if (it[j].cpos >= uabs(b, v) && it[j].cpos + it[j].clen <= uabs(b, v) + b->ulen[v]) { u = v; break; }
     if (u == nu) return fail(YCRDT_E_DEVICE, "internal: a JSON content outside every staged update");
-    const uint64_t rel = it[j].cpos - uabs(b, u);
-    if (it[j].len != it[j].clen || memcmp(ups[u].data() + rel, canon.data() + off[j], it[j].len) != 0) {
+    if (it[j].pad) {
       per[u].push_back(j);
       changed = true;
     }

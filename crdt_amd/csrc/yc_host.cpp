@@ -8,6 +8,7 @@
 // (Y@48365) + typeListInsertGenericsAfter (Y@47498) and typeListDelete (Y@48835): the new item's
 // origin / right origin are read off the view, and the struct is written as Item.write (Y@80416).
 #include "yc_host.h"
+#include "yc_parse.h"  // (yc_num.h: Number::toString for the JSON output)
 
 #include <algorithm>
 #include <array>
@@ -94,15 +95,13 @@ void put_json_str(std::string& o, const uint8_t* s, size_t n) {
   o.push_back('"');
 }
 
-void put_number(std::string& o, double x) {  // JSON.stringify(Number)
+void put_number(std::string& o, double x) {  // JSON.stringify(Number): Number::toString's text (yc_num.h)
   if (!std::isfinite(x)) { o += "null"; return; }
   if (x == 0) { o += "0"; return; }
-  char t[40];
-  for (int prec = 1; prec <= 17; ++prec) {  // shortest text that reads back to x
-    snprintf(t, sizeof t, "%.*g", prec, x);
-    if (strtod(t, nullptr) == x) break;
-  }
-  o += t;
+  char d[20], t[40];
+  int32_t n;
+  const uint32_t k = f64_shortest(x < 0 ? -x : x, d, n);
+  o.append(t, num_text(x < 0, d, k, n, t));
 }
 
 double be_f64(const uint8_t* p) {

@@ -219,6 +219,11 @@ YC_HDI int64_t key_index(const uint8_t* __restrict__ b, uint32_t p, uint32_t n) 
   }
   return v < 0xFFFFFFFFull ? (int64_t)v : -1;
 }
+YC_HDI uint32_t fnv_key(const uint8_t* __restrict__ b, uint32_t p, uint32_t n) {
+  uint32_t h = 2166136261u;
+  for (uint32_t i = 0; i < n; ++i) h = (h ^ b[p + i]) * 16777619u;
+  return h;
+}
 YC_HDI bool key_proto(const uint8_t* __restrict__ b, uint32_t p, uint32_t n) {
   const char* k = "__proto__";
   if (n != 9) return false;
@@ -235,6 +240,11 @@ YC_HD inline bool skip_any(const uint8_t* __restrict__ b, uint32_t& p, uint32_t 
   uint32_t cf = 0;                  // ANY_* flags (UTF8 mode: the exact parse checks the encoding)
   int64_t lastkey[UTF8 ? DEPTH + 1 : 1];  // per object level: the last array-index key, or -2 after a string key
   uint64_t keym[UTF8 ? DEPTH + 1 : 1];    // per object level: the repeat mask of its keys (key_bit)
+  // per object level: the FNV-32 hashes of its first KH keys (a repeat is a hash match: exact up to
+  // a 2^-32 false alarm, which costs a rewrite pass that changes nothing); past KH keys the mask
+  constexpr uint32_t KH = 8;
+  uint32_t keyh[UTF8 ? DEPTH + 1 : 1][UTF8 ? KH : 1];
+  uint32_t keyn[UTF8 ? DEPTH + 1 : 1];
   // A level is kept only while members FOLLOW the one being read (rem[d] >= 1): the last member of
   // a container is read in the container's place (a tail position), so nesting along last members
   // — [[[..]]], {a: {b: ..}}, however deep — takes no stack, and DEPTH bounds only containers
@@ -297,6 +307,8 @@ YC_HD inline bool skip_any(const uint8_t* __restrict__ b, uint32_t& p, uint32_t 
               if (n > 1) {
                 lastkey[d - 1] = ki >= 0 ? ki : -2;
                 keym[d - 1] = key_bit(k, k ? b[st] : 0u, k ? b[st + k - 1] : 0u);
+                keyh[d - 1][0] = fnv_key(b, st, k);
+                keyn[d - 1] = 1;
               }
             }
           }
@@ -330,7 +342,16 @@ YC_HD inline bool skip_any(const uint8_t* __restrict__ b, uint32_t& p, uint32_t 
         if (ki >= 0 && (prev == -2 || (prev >= 0 && ki <= prev))) cf |= ANY_KEYS;
         lastkey[lvl] = ki >= 0 ? ki : -2;
         const uint64_t kb = key_bit(k, k ? b[st] : 0u, k ? b[st + k - 1] : 0u);
-        if (keym[lvl] & kb) cf |= ANY_KEYS;
+        const uint32_t kn = keyn[lvl];
+        if (kn <= KH) {  // the hashes of every key so far: exact
+          const uint32_t h = fnv_key(b, st, k);
+          for (uint32_t j = 0; j < kn; ++j)
+            if (keyh[lvl][j] == h) cf |= ANY_KEYS;
+          if (kn < KH) keyh[lvl][kn] = h;
+          keyn[lvl] = kn + 1;
+        } else if (keym[lvl] & kb) {
+          cf |= ANY_KEYS;
+        }
         keym[lvl] |= kb;
       }
     }
@@ -385,6 +406,28 @@ YC_HDI void any_scalar(const S& b, uint32_t tag, uint32_t& p, uint32_t end, bool
   }
 }
 YC_HDI bool any_scalar_tag(uint32_t tag) { return tag >= 116u && tag <= 127u && tag != 117u && tag != 118u; }
+// whether one of the first `i` keys of a flat object (members from q: key, scalar value) equals the
+// key [ks, ks + k): the exact test behind a repeat-mask hit (rare; inline: a call from the struct
+// decoder would give it a stack frame)
+template <class S>
+YC_HDI bool key_repeats(const S& b, uint32_t q, uint32_t i, uint32_t ks, uint32_t k, uint32_t end) {
+  bool o = true;
+  for (uint32_t j = 0; j < i && o; ++j) {
+    const uint32_t kl = b.vu(q, end, o);
+    if (!o) return false;
+    if (kl == k) {
+      uint32_t x = 0;
+      while (x < k && b.u8(q + x) == b.u8(ks + x)) ++x;
+      if (x == k) return true;
+    }
+    skip_bytes(q, kl, end, o);
+    if (!o || q >= end) return false;
+    const uint32_t t = b.u8(q++);
+    uint32_t cf = 0;
+    any_scalar<false>(b, t, q, end, o, cf);
+  }
+  return false;
+}
 // A one-level array / object of at most 8 scalar members (C1's {name, v}, C2's {name}), inline:
 // true when it was one (p past it; ok false if malformed), false otherwise (p unchanged: the
 // container goes to skip_any_nl).
@@ -396,6 +439,7 @@ YC_HDI bool any_flat(const S& b, uint32_t& p, uint32_t end, uint32_t& steps, boo
   const uint32_t m = b.vu(q, end, o);
   if (!o || m > 8 || st < m + 1) return false;
   if (FULL) c |= vu_overlong_at(b, p0 + 1, q);
+  const uint32_t qm = q;  // the first member
   int64_t prev = -1;
   uint64_t km = 0;  // the keys' repeat mask
   for (uint32_t i = 0; i < m; ++i) {
@@ -413,7 +457,7 @@ YC_HDI bool any_flat(const S& b, uint32_t& p, uint32_t end, uint32_t& steps, boo
         if (ki >= 0 && (prev == -2 || (prev >= 0 && ki <= prev))) c |= ANY_KEYS;
         prev = ki >= 0 ? ki : -2;
         const uint64_t kb = key_bit(k, k ? b.u8(ks) : 0u, k ? b.u8(ks + k - 1) : 0u);
-        if (km & kb) c |= ANY_KEYS;
+        if ((km & kb) && key_repeats(b, qm, i, ks, k, end)) c |= ANY_KEYS;  // (a mask hit: tested exactly)
         km |= kb;
       }
       if (!o) { ok = false; p = q; return true; }
@@ -1073,8 +1117,8 @@ YC_HD inline __attribute__((noinline)) uint32_t json_canon(const uint8_t* __rest
 // for it (Y@71991 ContentJSON.write: the count, then each value's JSON.stringify, "undefined" as
 // is; ContentEmbed / ContentFormat: writeJSON, after Format's key) — into out (null: size only),
 // every length prefix in writeVarUint's shortest form. JSON_OK, JSON_BAD or JSON_ARENA.
-YC_HD inline uint32_t any_content_canon(const uint8_t* __restrict__ b, uint32_t p, uint32_t end, uint8_t* out,
-                                        uint32_t* arena, uint32_t acap, uint32_t& olen);
+YC_HD inline __attribute__((noinline)) uint32_t any_content_canon(const uint8_t* __restrict__ b, uint32_t p, uint32_t end, uint8_t* out,
+                                                                 uint32_t* arena, uint32_t acap, uint32_t& olen);
 YC_HD inline uint32_t json_content_canon(const uint8_t* __restrict__ b, uint32_t p, uint32_t end, uint32_t ref, uint8_t* out,
                                          uint32_t* arena, uint32_t acap, uint32_t& olen) {
   if (ref == REF_ANY) return any_content_canon(b, p, end, out, arena, acap, olen);  // (object key semantics, ANY_KEYS)

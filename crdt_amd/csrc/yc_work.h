@@ -733,7 +733,7 @@ struct JItem {
   uint32_t clen;            // its bytes in the update
   uint32_t len;             // its canonical bytes
   uint32_t res;             // JSON_OK / JSON_BAD / JSON_ARENA
-  uint32_t pad;
+  uint32_t pad;             // pass 1: the canonical bytes differ from the input
 };
 void launch_json_canon(const Work& w, const uint32_t* list, uint32_t n, JItem* items, uint32_t* arena, uint32_t acap,
                        uint32_t lanes, const unsigned long long* offs, uint8_t* out, hipStream_t s);

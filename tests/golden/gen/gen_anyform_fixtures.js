@@ -70,7 +70,10 @@ const values = {
   obj_many_keys_dup: [118, 10, ...[...Array(9).keys()].flatMap((i) => [...vs('m' + i), 125, i]), ...vs('m4'), 125, 44],
   obj_deep_dup: [118, 2, ...vs('d'), ...[...Array(24).keys()].flatMap(() => [117, 2]), 118, 2, ...vs('a'), 125, 1, ...vs('a'), 125, 2,
     ...[...Array(24).keys()].flatMap(() => [125, 0]), ...vs('d'), 125, 5],
-  obj_dup_keys_canon: [118, 2, ...vs('a'), 125, 1, ...vs('ab'), 125, 2],  // (a mask false alarm: left as is)
+  obj_dup_keys_canon: [118, 2, ...vs('a'), 125, 1, ...vs('ab'), 125, 2],
+  // keys whose repeat-mask bits collide ('ab', 'b_') without repeating: tested exactly, left as is
+  obj_mask_collision: [118, 2, ...vs('ab'), 125, 1, ...vs('b_'), 125, 2],
+  obj_mask_collision_nested: [118, 3, ...vs('ab'), 125, 1, ...vs('b_'), 117, 1, 125, 2, ...vs('z'), 118, 2, ...vs('ab'), 120, ...vs('b_'), 121],
   // still refused: writeVarInt garbles a negative integer past 2^32; a "__proto__" array makes the
   // object pass `instanceof Array` in writeAny
   f64_neg_5e9: [123, ...f64(-5e9)],

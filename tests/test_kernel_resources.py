@@ -17,11 +17,13 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LLVM = "/opt/rocm/lib/llvm/bin"
 LIB = os.path.join(ROOT, "crdt_amd", "libycrdt.so")
 
-# kernel (mangled-name fragment) -> scratch bytes per lane it may use
+# kernel (mangled-name fragment) -> scratch bytes per lane it may use (k_struct_decode: 16 -> 24 in
+# round 6 for the exact repeated-key test of flat `any` objects; its live time did not move, 4.25 vs
+# 4.33 ms on two boxes)
 BUDGET = {
     "7k_units": 0, "11k_seg_props": 0, "9k_resolve": 0, "13k_winner_walk": 0, "18k_merge_flags_scan": 0,
     "11k_out_sizes": 0, "15k_write_structs": 0, "6k_cuts": 0, "14k_struct_clock": 0, "13k_scatter_seg": 0,
-    "15k_struct_decode": 16, "8k_direct": 160, "6k_spec": 160,
+    "15k_struct_decode": 24, "8k_direct": 160, "6k_spec": 160,
 }
 
 
