@@ -3436,7 +3436,9 @@ __global__ __launch_bounds__(256) void k_json_structs(Work w, uint32_t nstructs)
   if (i >= nstructs) return;
   const uint8_t* __restrict__ bw = struct_bytes(w, i);
   const uint32_t ref = bw[w.s_pos[i]] & 31u;  // (the input's info byte: superseded sections' structs too)
+  if (w.ntrusted && w.sections[w.s_sec[i]].upd < w.ntrusted) return;  // a doc state: already what Yjs holds
   if (ref == REF_ANY && (w.s_pk[i] & 0x20u)) {  // `any` objects with keys JS treats specially: rewritten
+    if (w.jskip_any) return;
     const uint32_t k = atomicAdd(&w.ctr->njson, 1u);
     if (k < w.jcap) w.jlist[k] = i;
     return;

@@ -318,6 +318,7 @@ struct ycrdt_batch {
   // host copies the batch was re-staged from, and the rewrite passes so far
   std::vector<std::vector<uint8_t>> jstore;
   uint32_t jpasses = 0;
+  uint32_t ntrusted = 0;        // leading staged updates that are doc states the engine wrote (device sources)
   uint64_t nbytes = 0;          // span of the batch buffer (windows before the last are 2^32 bytes)
   uint64_t in_bytes = 0;
   bool merged = false;
@@ -587,6 +588,7 @@ int stage_srcs(ycrdt_batch* b, const std::vector<Src>& src, const uint32_t* doc_
   const size_t nu = b->ulen.size();
   size_t ndev = 0;
   while (ndev < nu && src[order[ndev]].dev) ++ndev;
+  b->ntrusted = (uint32_t)ndev;
   // staging runs on the copy stream (a host thread may stage the next batch while another merges
   // on the engine stream); device sources (doc states in HBM) are read after the engine stream's
   // work so far, which may still be writing them
@@ -851,7 +853,6 @@ int split_decode_exchange(ycrdt_engine* e, ycrdt_batch* b, const ShardSpec* sh) 
 // updates: byte moves only), so that every later pass sees what Yjs would hold. A pass whose
 // canonical contents all equal the input (a text json_check could not judge: nesting past its
 // level mask) keeps the batch as it is. Rare by construction: Yjs itself writes ContentAny.
-constexpr uint32_t JLIST_CAP = 1u << 16;     // structs per rewrite pass (more: another pass)
 constexpr uint32_t JARENA_WORDS = JSON_ARENA_WORDS;  // arena per lane (yc_parse.h json_canon): 256 KiB
 constexpr uint32_t JLANES = 256;
 int json_rewrite(ycrdt_engine* e, ycrdt_batch* b, uint32_t n, const ShardSpec* sh, bool& restaged) {
@@ -932,10 +933,11 @@ int json_rewrite(ycrdt_engine* e, ycrdt_batch* b, uint32_t n, const ShardSpec* s
     src[u] = Src{store[u].data(), store[u].size(), false};
   }
   const std::vector<uint32_t> udoc = b->udoc;
-  const uint32_t ndocs = b->ndocs;
+  const uint32_t ndocs = b->ndocs, ntrusted = b->ntrusted;
   b->pre_src = -1;  // (a doc state's marks no longer name a source: it is decoded like the others)
   b->pre_check = false;
   if (const int rc = stage_srcs(b, src, udoc.empty() ? nullptr : udoc.data(), ndocs)) return rc;
+  b->ntrusted = ntrusted;  // (the same updates in the same order, now all host copies)
   b->jstore = std::move(store);
   restaged = true;
   return YCRDT_OK;
@@ -1027,8 +1029,8 @@ int run_decode(ycrdt_engine* e, ycrdt_batch* b, bool lazy, Decoded& D, bool gene
   w.ds_count = take<uint32_t>(V, B_DSCNT, nu + 2, ok);
   w.ds_dense_off = take<uint32_t>(V, B_DSOFF, nu + 2, ok);
   w.ds_biglist = take<uint32_t>(V, B_DSBIGL, nu + 1, ok);
-  w.jcap = JLIST_CAP;
-  w.jlist = take<uint32_t>(V, B_JLIST, JLIST_CAP, ok);
+  w.jcap = 0;  // (sized when the decode saw a JSON-like content)
+  w.jlist = nullptr;
   w.cap_clients = w.cap_sections;
   w.scratch = take<uint32_t>(V, B_SCRATCH, std::max<uint64_t>({nwords + 2, (uint64_t)w.cap_sections + 66, (uint64_t)nu + 2}), ok);
   w.usec_start = take<uint32_t>(V, B_USEC, nu + 1, ok);
@@ -1253,6 +1255,12 @@ int run_decode(ycrdt_engine* e, ycrdt_batch* b, bool lazy, Decoded& D, bool gene
   if (rc) return rc;
   const uint32_t nstructs_q = quick ? c.nstructs : nstructs, nsections_q = quick ? c.nsections : nsections;
   if (c.any_json) {  // ContentJSON / Embed / Format values: JSON.parse (rare: one more pass and sync)
+    // room for every struct: one rewrite pass takes all of them (an `any` content is rewritten once)
+    w.jcap = std::max<uint32_t>(nstructs_q, 1);
+    w.jlist = take<uint32_t>(V, B_JLIST, w.jcap, ok);
+    if (!ok) return fail(YCRDT_E_DEVICE, oom("JSON list"));
+    w.ntrusted = b->ntrusted;
+    w.jskip_any = b->jpasses > 0 ? 1u : 0u;
     launch_json_structs(w, nstructs_q, s);
     rc = check(e, c, "JSON values");
     if (rc) return rc;

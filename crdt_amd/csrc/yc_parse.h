@@ -1212,6 +1212,44 @@ YC_HD inline bool any_skip_deep(const uint8_t* __restrict__ b, uint32_t& p, uint
     }
   }
 }
+// Whether the object at p (tag 118) still reaches Object.prototype's __proto__ accessor once readAny
+// has built it: its "__proto__" members assign its prototype in order while it does — null cuts the
+// chain (later "__proto__" keys are then own members), an object passes on ITS state. Explicit
+// stack of resume positions in arena[base, acap): 0 no, 1 yes, 2 past the arena / malformed.
+YC_HD inline uint32_t any_proto_state(const uint8_t* __restrict__ b, uint32_t p, uint32_t end, uint32_t* arena, uint32_t base, uint32_t acap) {
+  bool ok = true;
+  uint32_t d = 0;  // open objects: (resume position, members left) pairs at arena[base + 2 * i]
+  ++p;             // (the tag)
+  uint32_t left = rd_vu(b, p, end, ok);
+  for (;;) {
+    if (!ok) return 2;
+    if (left == 0) {  // the object keeps the accessor: its parent goes on after it
+      if (d == 0) return 1;
+      --d;
+      p = arena[base + 2 * d];
+      left = arena[base + 2 * d + 1];
+      continue;
+    }
+    --left;
+    const uint32_t kl = rd_vu(b, p, end, ok);
+    if (!ok || end - p < kl) return 2;
+    const bool proto = key_proto(b, p, kl);
+    p += kl;
+    if (proto && p < end && b[p] == 126) return 0;  // null: no accessor from here on (for every open level)
+    if (proto && p < end && b[p] == 118) {          // an object: its own state decides
+      uint32_t q = p;
+      if (!any_skip_deep(b, q, end, arena, base + 2 * d + 2, acap)) return 2;
+      if (base + 2 * d + 2 > acap) return 2;
+      arena[base + 2 * d] = q;
+      arena[base + 2 * d + 1] = left;
+      ++d;
+      ++p;
+      left = rd_vu(b, p, end, ok);
+      continue;
+    }
+    if (!any_skip_deep(b, p, end, arena, base + 2 * d, acap)) return 2;
+  }
+}
 YC_HD inline __attribute__((noinline)) uint32_t any_content_canon(const uint8_t* __restrict__ b, uint32_t p, uint32_t end, uint8_t* out,
                                                                  uint32_t* arena, uint32_t acap, uint32_t& olen) {
   olen = 0;
@@ -1303,6 +1341,7 @@ YC_HD inline __attribute__((noinline)) uint32_t any_content_canon(const uint8_t*
           const uint32_t f = used;
           if ((uint64_t)f + 5 + 5ull * m > acap) return JSON_ARENA;
           uint32_t k = 0;
+          bool acc = true;  // the object still reaches the __proto__ accessor (any_proto_state)
           for (uint32_t j = 0; j < m; ++j) {
             const uint32_t kl = rd_vu(b, p, end, ok);
             if (!ok || end - p < kl) return JSON_BAD;
@@ -1310,8 +1349,14 @@ YC_HD inline __attribute__((noinline)) uint32_t any_content_canon(const uint8_t*
             p += kl;
             const uint32_t vp = p;
             if (!any_skip_deep(b, p, end, arena, f + 5 + 5 * m, acap)) return JSON_ARENA;
-            if (key_proto(b, ks, kl)) {  // the prototype setter: no own member
+            if (acc && key_proto(b, ks, kl)) {  // the prototype setter: no own member
               if (b[vp] == 116 || b[vp] == 117) return JSON_ARENA;  // (instanceof Uint8Array / Array: refused)
+              if (b[vp] == 126) acc = false;                        // null: later "__proto__" keys are members
+              else if (b[vp] == 118) {
+                const uint32_t st = any_proto_state(b, vp, end, arena, f + 5 + 5 * m, acap);
+                if (st == 2) return JSON_ARENA;
+                acc = st == 1;
+              }
               continue;
             }
             uint32_t h = 2166136261u;

@@ -147,6 +147,9 @@ struct Work {
   uint32_t* ds_len = nullptr;      // [cap_ds+1] clipped lengths (scan input)
   uint32_t* jlist = nullptr;       // [jcap] structs whose JSON-like content Yjs would write back differently (k_json_structs)
   uint32_t jcap = 0;
+  uint32_t ntrusted = 0;           // the first ntrusted staged updates are doc states the engine wrote: never rewritten
+  uint32_t jskip_any = 0;          // 1: a rewrite pass ran: `any` contents are not rewritten again (readAny o writeAny
+                                   //    is not idempotent: an own "__proto__" member written by writeAny)
   uint32_t* ds_biglist = nullptr;  // [nupd] updates with more than DSA_WAVE ranges (ctr->ds_big of them): k_units spreads
                                    // their ranges past the first DSA_WAVE over extra workgroups, whichever decoder read them
   // large delete sets decoded grid-wide (yc_decode.hip k_dsp_*): per chunk of the large updates

@@ -80,6 +80,48 @@ const values = {
   obj_proto_array: [118, 1, ...vs('__proto__'), 117, 1, 125, 1],
 };
 const refused = new Set(['f64_neg_5e9', 'obj_proto_array']);
+// seeded random values in encodings writeAny never produces: objects with repeated keys, array-index
+// keys in any order and "__proto__" members (scalar / object / null values), nested up to 5 levels,
+// numbers as varint / float32 / float64 whether or not that is writeAny's form, overlong prefixes
+{
+  let a = 20240611;
+  const r = () => { a |= 0; a = (a + 0x6D2B79F5) | 0; let t = Math.imul(a ^ (a >>> 15), 1 | a); t = (t + Math.imul(t ^ (t >>> 7), 61 | t)) ^ t; return ((t ^ (t >>> 14)) >>> 0) / 4294967296; };
+  const pick = (xs) => xs[Math.floor(r() * xs.length)];
+  const vu = (n, over) => { const o = []; while (n > 127) { o.push(0x80 | (n & 127)); n = Math.floor(n / 128); } o.push(n); if (over) { o[o.length - 1] |= 0x80; o.push(0); } return o; };
+  const key = (k) => { const b = Buffer.from(k, 'utf8'); return [...vu(b.length, r() < 0.05), ...b]; };
+  const scalar = () => {
+    const x = r();
+    if (x < 0.15) return [125, ...vu(Math.floor(r() * 200))];
+    if (x < 0.3) return [123, ...f64(pick([0.5, 3, -7, 1e10, 0.1, 2147483648, -2147483649, 1.25, NaN, -0]))];
+    if (x < 0.4) return [124, ...f32(pick([1.5, 3, -0.25, 7]))];
+    if (x < 0.55) { const b = Buffer.from(pick(['', 'x', 'é', 'long string value', '0']), 'utf8'); return [119, ...vu(b.length, r() < 0.05), ...b]; }
+    if (x < 0.65) return [pick([126, 127, 120, 121])];
+    if (x < 0.7) return [116, 2, 9, 8];
+    return [125, ...vu(Math.floor(r() * 5))];
+  };
+  const value = (d) => {
+    const x = r();
+    if (d >= 5 || x < 0.4) return scalar();
+    const n = Math.floor(r() * 5);
+    if (x < 0.6) { const o = [117, ...vu(n)]; for (let i = 0; i < n; i++) o.push(...value(d + 1)); return o; }
+    const o = [118, ...vu(n)];
+    const used = [];
+    for (let i = 0; i < n; i++) {
+      let k;
+      const y = r();
+      if (used.length && y < 0.2) k = pick(used);                                // a repeated key
+      else if (y < 0.45) k = String(Math.floor(r() * 12));                        // an array index
+      else if (y < 0.5) k = '__proto__';
+      else k = pick(['a', 'b', 'name', 'v', 'é', '01', '4294967295', 'ab', 'b_', '']);
+      used.push(k);
+      let v = value(d + 1);
+      if (k === '__proto__' && (v[0] === 116 || v[0] === 117)) v = [126];         // (refused forms: see above)
+      o.push(...key(k), ...v);
+    }
+    return o;
+  };
+  for (let i = 0; i < 120; i++) values['fuzz_' + i] = value(0);
+}
 
 const cases = [];
 for (const [name, v] of Object.entries(values)) {
@@ -89,12 +131,14 @@ for (const [name, v] of Object.entries(values)) {
   const other = new Y.Doc(); other.clientID = 33; other.getMap('users').set('x', 1.5);
   const o = Y.encodeStateAsUpdate(other);
   const merged = Y.mergeUpdates([u, o]);
+  let st2 = null;
+  try { const d2 = new Y.Doc(); d2.clientID = 5; Y.applyUpdate(d2, u); Y.applyUpdate(d2, o); st2 = hex(canonicalUpdate(Y.encodeStateAsUpdate(d2))); } catch (e) { st2 = 'throws: ' + e.message; }
   const diff = Y.diffUpdate(u, new Uint8Array([0]));
   let st = null; let sv = null; let json = null;
   try { st = hex(canonicalUpdate(Y.encodeStateAsUpdate(d))); sv = hex(canonicalSv(Y.encodeStateVector(d)));
         json = name === 'bigint' ? null : JSON.parse(JSON.stringify(d.getMap('users').toJSON())); } catch (e) { st = 'throws: ' + e.message; }
   cases.push({ name, update: hex(u), other: hex(o), refused: refused.has(name),
-               state: st, sv, json, merged: hex(canonicalUpdate(merged)), diff: hex(canonicalUpdate(diff)) });
+               state: st, sv, json, merged: hex(canonicalUpdate(merged)), diff: hex(canonicalUpdate(diff)), state_with_other: st2 });
 }
 const outDir = process.argv[2] || path.join(__dirname, '..');
 fs.writeFileSync(path.join(outDir, 'anyform.json'), JSON.stringify({ yjs: '13.5.16', cases }, null, 0));

@@ -47,6 +47,20 @@ def test_anyform_apply(mode, monkeypatch):
         assert b.result()[0] == d2.encode_state_as_update(), c["name"]
 
 
+def test_anyform_doc_remerge():
+    """The doc's state holds what Yjs holds (writeAny of the values readAny built), and a later merge
+    into the doc keeps it: a doc state is never rewritten again (an own "__proto__" member that
+    writeAny wrote after a `"__proto__": null` would be read back as the prototype setter)."""
+    for c in _cases():
+        if c["refused"]:
+            continue
+        d = crdt_amd.Doc(client_id=5)
+        d.apply_update(bytes.fromhex(c["update"]))
+        assert d.encode_state_as_update().hex() == c["state"], c["name"]
+        d.apply_update(bytes.fromhex(c["other"]))
+        assert d.encode_state_as_update().hex() == c["state_with_other"], c["name"]
+
+
 def test_anyform_merge_and_diff():
     for c in _cases():
         if c["refused"]:
