@@ -3035,8 +3035,19 @@ __device__ __forceinline__ void ds_bound_at(const Work& w, uint32_t u) {  // reg
   // applyUpdate keeps only the LAST section of a client (readClientsStructRefs' Map.set, Y@19286):
   // an earlier one is marked superseded (pad = 1) and its structs decode as Skips
   const uint32_t a = w.usec_start[u], b = a + w.usec_n[u];
+  if (u == w.upre) return;  // a doc state decoded by its marks: its encode wrote descending clients
   bool canon = true;
-  for (uint32_t i = a + 1; i < b && canon; ++i) canon = w.sections[i].client < w.sections[i - 1].client;
+  // (eight sections' clients per round of loads: a full state's 1 001 sections one dependent load
+  // at a time held this pass for 0.13 ms)
+  uint32_t prev = b > a ? w.sections[a].client : 0u;
+  for (uint32_t i0 = a + 1; i0 < b && canon; i0 += 8) {
+    uint32_t c[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) c[k] = i0 + k < b ? w.sections[i0 + k].client : 0u;
+#pragma unroll
+    for (int k = 0; k < 8; ++k)
+      if (i0 + k < b) { canon = canon && c[k] < prev; prev = c[k]; }
+  }
   if (canon) return;
   w.ctr->noncanon = 1;
   if (w.lazy) return;

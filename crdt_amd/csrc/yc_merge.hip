@@ -258,18 +258,32 @@ __global__ __launch_bounds__(SEG_LANES) void k_segments_small(Work w, uint64_t n
 // extra workgroups). Any update can: a 16 KiB direct-path update of one transaction that deleted
 // ~8 000 scattered items carries that many 2-byte ranges, so the list is every such update the
 // decoders met (k_ds_decode, k_dsp_headers), not the chunk-path updates
+// A wavefront takes 64 consecutive ranges; a long range (a full state's delete set holds runs of
+// tens of thousands of units: C2's base client) is flagged by the whole wavefront, 64 units a step,
+// as in unit_ds_apply — one lane walking it alone held k_units for 0.8 ms on a C2 document's state.
 __device__ __forceinline__ void unit_ds_apply_big(const Work& w, uint32_t nclients, uint32_t blk, uint32_t nx) {
-  const uint32_t t = blk * blockDim.x + threadIdx.x, stride = nx * blockDim.x;
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t wave = (blk * blockDim.x + threadIdx.x) >> 6, nwaves = nx * blockDim.x / 64;
   const uint32_t nlist = min(w.ctr->ds_big, w.nupd);
   for (uint32_t bi = 0; bi < nlist; ++bi) {
     const uint32_t u = w.ds_biglist[bi];
     const uint32_t n = w.ds_count[u];
     if (n <= DSA_WAVE) continue;
     const uint32_t base = w.ds_region[u], doc = doc_of_update(w, u);
-    for (uint32_t i = DSA_WAVE + t; i < n; i += stride) {
-      uint64_t gb;
-      const uint32_t len = ds_range_units(w, nclients, doc, w.ds_tmp[base + i], gb);
-      for (uint32_t k = 0; k < len; ++k) unit_flag(w, (uint32_t)(gb + k), 1);
+    for (uint32_t i0 = DSA_WAVE + wave * 64; i0 < n; i0 += nwaves * 64) {  // (wave-uniform)
+      const uint32_t i = i0 + lane;
+      uint64_t gb = 0;
+      uint32_t len = 0;
+      if (i < n) len = ds_range_units(w, nclients, doc, w.ds_tmp[base + i], gb);
+      const bool lng = len > LONG_UNITS;
+      if (!lng)
+        for (uint32_t k = 0; k < len; ++k) unit_flag(w, (uint32_t)(gb + k), 1);
+      for (uint64_t m = __ballot(lng); m; m &= m - 1) {
+        const int L = __ffsll((long long)m) - 1;
+        const uint64_t g0 = shfl64(gb, L);
+        const uint32_t nl = __shfl(len, L);
+        for (uint32_t k = lane; k < nl; k += 64) unit_flag(w, (uint32_t)(g0 + k), 1);
+      }
     }
   }
 }
