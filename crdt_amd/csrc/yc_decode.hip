@@ -2940,6 +2940,108 @@ __global__ __launch_bounds__(256) void k_dsp_vals(Work w) {
     dsp_vals_group(w, i, lane);
   }
 }
+// The client blocks of a large delete set without hopping from header to header in one lane (a
+// full state's 1 001 blocks were 0.37 ms of dependent loads, on the path of every apply into a large
+// doc: crdt.js's sync reply carries the peer's whole delete set). The header after the one at value
+// index k is k + 2 + 2 (its run count); k_dsh_jump takes 32 such steps from EVERY value index at once
+// (garbage where k is no header, never read), k_dsh_base strides the real chain 32 headers a step
+// from value 1, k_dsh_fill walks each stride's 32 headers and writes their blocks, k_dsh_final
+// publishes them. Every check of the lane-serial walk (k_dsp_headers) is made on the real chain;
+// where one fails the update is left to the wavefront decoder, as there.
+__device__ __forceinline__ bool dsh_update(const Work& w, uint32_t bi, uint32_t& u, uint64_t& total, const uint32_t*& vals) {
+  u = w.ulist[bi];
+  if (!dsp_applies(w, u) || w.dsp_fail[u]) return false;
+  const uint32_t CH = w.schunk;
+  const uint32_t g0 = w.ugroup[u] + (w.dsstart[u] - w.uoff[u]) / CH, gl = w.ugroup[u] + (w.ulen[u] + CH - 1) / CH;
+  total = w.dsp_pre[gl] - w.dsp_pre[g0];
+  vals = w.dsp_val + 2ull * w.ds_region[u];
+  return total >= 1;
+}
+__global__ __launch_bounds__(256) void k_dsh_jump(Work w) {
+  const uint32_t bi = blockIdx.y;
+  uint32_t u;
+  uint64_t total;
+  const uint32_t* vals;
+  if (!dsh_update(w, bi, u, total, vals)) return;
+  uint32_t* __restrict__ J = w.dsp_j + 2ull * w.ds_region[u];
+  uint32_t* __restrict__ S = w.dsp_js + 2ull * w.ds_region[u];
+  for (uint64_t i = 1 + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (uint64_t)gridDim.x * blockDim.x) {
+    uint64_t k = i;
+    uint32_t sum = 0;
+    for (uint32_t h = 0; h < DSH_STRIDE; ++h) {
+      if (k + 2 > total) { k = NONE; break; }
+      const uint32_t nr = vals[k + 1];
+      if (nr > 0x7FFFFFFFu || k + 2 + 2ull * nr > total) { k = NONE; break; }
+      sum += nr;
+      k += 2 + 2ull * nr;
+    }
+    J[i] = (uint32_t)k;
+    S[i] = sum;
+  }
+}
+__global__ void k_dsh_base(Work w) {
+  const uint32_t bi = blockIdx.x * blockDim.x + threadIdx.x;
+  if (bi >= w.nbig) return;
+  uint2* __restrict__ H = w.dsp_h + (size_t)bi * (DSH_SEG + 1);
+  H[DSH_SEG] = make_uint2(1u, 0u);  // (failed until the chain is strided)
+  uint32_t u;
+  uint64_t total;
+  const uint32_t* vals;
+  if (!dsh_update(w, bi, u, total, vals)) return;
+  const uint32_t nb = vals[0];
+  if (nb > DSP_MAXBLK) return;  // (k_dsp_headers gives up there too: the wavefront decodes it)
+  const uint32_t* __restrict__ J = w.dsp_j + 2ull * w.ds_region[u];
+  const uint32_t* __restrict__ S = w.dsp_js + 2ull * w.ds_region[u];
+  const uint32_t nseg = (nb + DSH_STRIDE - 1) / DSH_STRIDE;
+  uint32_t k = 1, off = 0;
+  for (uint32_t sg = 0; sg < nseg; ++sg) {
+    H[sg] = make_uint2(k, off);
+    if (sg + 1 < nseg) {  // a full stride of 32 headers: its jump must be valid
+      if (k >= total) return;
+      const uint32_t j = J[k];
+      if (j == NONE) return;
+      off += S[k];
+      k = j;
+    }
+  }
+  H[DSH_SEG] = make_uint2(0u, 0u);
+}
+__global__ void k_dsh_fill(Work w) {
+  const uint32_t bi = blockIdx.y, sg = threadIdx.x + blockIdx.x * blockDim.x;
+  uint32_t u;
+  uint64_t total;
+  const uint32_t* vals;
+  if (!dsh_update(w, bi, u, total, vals)) return;
+  uint2* __restrict__ H = w.dsp_h + (size_t)bi * (DSH_SEG + 1);
+  const uint32_t nb = vals[0];
+  if (nb > DSP_MAXBLK || sg * DSH_STRIDE >= nb || H[DSH_SEG].x) return;
+  uint4* __restrict__ blk = w.dsp_blk + (size_t)bi * DSP_MAXBLK;
+  uint64_t k = H[sg].x;
+  uint32_t off = H[sg].y;
+  for (uint32_t c = sg * DSH_STRIDE; c < min(nb, (sg + 1) * DSH_STRIDE); ++c) {
+    if (k + 2 > total) { atomicOr(&H[DSH_SEG].x, 1u); return; }
+    const uint32_t client = vals[k], nr = vals[k + 1];
+    if (nr > 0x7FFFFFFFu || k + 2 + 2ull * nr > total) { atomicOr(&H[DSH_SEG].x, 1u); return; }
+    blk[c] = make_uint4((uint32_t)k, client, nr, off);
+    off += nr;
+    k += 2 + 2ull * nr;
+  }
+  if (min(nb, (sg + 1) * DSH_STRIDE) == nb) H[DSH_SEG].y = off;  // (the last stride: every run)
+}
+__global__ void k_dsh_final(Work w) {
+  const uint32_t bi = blockIdx.x * blockDim.x + threadIdx.x;
+  if (bi >= w.nbig) return;
+  uint32_t u;
+  uint64_t total;
+  const uint32_t* vals;
+  if (!dsh_update(w, bi, u, total, vals)) return;
+  const uint2 f = w.dsp_h[(size_t)bi * (DSH_SEG + 1) + DSH_SEG];
+  if (f.x) return;  // the wavefront decodes it (and reports what is wrong)
+  w.dsp_nb[bi] = vals[0];
+  w.ds_count[u] = f.y;
+  if (f.y > DSA_WAVE) w.ds_biglist[atomicAdd(&w.ctr->ds_big, 1u)] = u;
+  w.dsp_b[u] = bi;
+}
 __global__ void k_dsp_headers(Work w) {
   const uint32_t bi = blockIdx.x * blockDim.x + threadIdx.x;
   if (bi >= w.nbig) return;
@@ -3017,7 +3119,14 @@ void launch_ds_grid(const Work& w, hipStream_t s) {
   hipLaunchKernelGGL(k_dsp_count, dim3(DSP_GRID), dim3(256), 0, s, w);
   scan_u32(w.tmp, w.tmp_bytes, w.dsp_cnt, w.dsp_pre, (uint64_t)w.ngroups + 1, s);
   hipLaunchKernelGGL(k_dsp_vals, dim3(DSP_GRID), dim3(256), 0, s, w);
-  hipLaunchKernelGGL(k_dsp_headers, dim3(w.nbig / 64 + 1), dim3(64), 0, s, w);
+  if (w.dsp_j && !env_off("YCRDT_DS_JUMP")) {  // (YCRDT_DS_JUMP=0: the lane-serial header walk, A/B)
+    hipLaunchKernelGGL(k_dsh_jump, dim3(w.dsh_grid, w.nbig), dim3(256), 0, s, w);
+    hipLaunchKernelGGL(k_dsh_base, dim3(w.nbig / 64 + 1), dim3(64), 0, s, w);
+    hipLaunchKernelGGL(k_dsh_fill, dim3(1, w.nbig), dim3(DSH_SEG), 0, s, w);
+    hipLaunchKernelGGL(k_dsh_final, dim3(w.nbig / 64 + 1), dim3(64), 0, s, w);
+  } else {
+    hipLaunchKernelGGL(k_dsp_headers, dim3(w.nbig / 64 + 1), dim3(64), 0, s, w);
+  }
   hipLaunchKernelGGL(k_dsp_ranges, dim3(DSP_GRID), dim3(256), 0, s, w);
 }
 

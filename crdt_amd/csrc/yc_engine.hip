@@ -179,7 +179,7 @@ enum Buf {
   B_UOWN, B_UFLAG, B_UCUT, B_UWPRE,
   B_GSTART, B_GCIDX, B_GSRC, B_GFLAGS, B_GORIG, B_GRORIG, B_GLINK, B_GOSEG, B_GKEY, B_GMAXC, B_GNEXT, B_GOUTID, B_GTMP, B_GTMP2,
   B_KHASH, B_KROOT, B_KWIN, B_KPAR, B_KFLAG, B_SPK,
-  B_USEC, B_USECN, B_DBG, B_XTAB, B_UFAIL, B_FW, B_CCNT, B_TENTRY, B_XLIST, B_WLEN, B_FWSEC, B_DSPCNT, B_DSPPRE, B_DSPVAL, B_DSPBLK, B_DSPB, B_DSPNB, B_DSPFAIL, B_DSPGB, B_OGEN, B_SDDEFER, B_COFF, B_CPRE, B_OPRE, B_SECUEND, B_SECDOC, B_DSBIGL, B_FWC, B_FWCOFF, B_RTAB, B_RK, B_JLIST, B_JITEM, B_JARENA, B_JOFF, B_JOUT,
+  B_USEC, B_USECN, B_DBG, B_XTAB, B_UFAIL, B_FW, B_CCNT, B_TENTRY, B_XLIST, B_WLEN, B_FWSEC, B_DSPCNT, B_DSPPRE, B_DSPVAL, B_DSPBLK, B_DSPB, B_DSPNB, B_DSPFAIL, B_DSPGB, B_OGEN, B_SDDEFER, B_COFF, B_CPRE, B_OPRE, B_SECUEND, B_SECDOC, B_DSBIGL, B_FWC, B_FWCOFF, B_RTAB, B_RK, B_DSHJ, B_DSHS, B_DSHH, B_JLIST, B_JITEM, B_JARENA, B_JOFF, B_JOUT,
   B_LZKEY, B_LZKEYS, B_LZIOTA, B_LZSEC, B_LZRSTART, B_LZPREV, B_LZFIRST, B_LZCAP, B_LZEVBASE, B_LZEVN, B_LZFLAG,
   B_LZLHI, B_LZLLO, B_EVKIND, B_EVSRC, B_EVCLOCK, B_EVLEN, B_EVSIZE, B_EVPOS, B_BLKSIZE, B_BLKPOS, B_SVC, B_SVK,
   B_DSMKEY, B_DSMKEYS, B_DSMLEN, B_DSMLENS, B_DSMEND, B_DSMMAX, B_DSMFLAG, B_DSMRID, B_DRCLIENT, B_DRCLOCK, B_DREND,
@@ -1208,10 +1208,20 @@ int run_decode(ycrdt_engine* e, ycrdt_batch* b, bool lazy, Decoded& D, bool gene
       wd.dsp_gb = take<uint32_t>(V, B_DSPGB, (uint64_t)w.nbig + 1, okd);
       wd.dsp_b = take<uint32_t>(V, B_DSPB, (uint64_t)w.nupd + 1, okd);
       wd.dsp_fail = take<uint32_t>(V, B_DSPFAIL, (uint64_t)w.nupd + 1, okd);
+      wd.dsp_j = take<uint32_t>(V, B_DSHJ, 2ull * w.cap_ds + 2, okd);
+      wd.dsp_js = take<uint32_t>(V, B_DSHS, 2ull * w.cap_ds + 2, okd);
+      wd.dsp_h = take<uint2>(V, B_DSHH, (uint64_t)w.nbig * (DSH_SEG + 1), okd);
+      {  // k_dsh_jump: about one lane per delete-set value of the largest big update
+        uint64_t mx = 0;
+        for (uint32_t i = 0; i < b->nbig; ++i) mx = std::max<uint64_t>(mx, b->ulen[b->ulist[i]]);
+        wd.dsh_grid = (uint32_t)std::min<uint64_t>(4096, mx / 512 + 1);
+      }
       if (okd) fill_u32_multi({{wd.dsp_b, (uint64_t)w.nupd + 1, NONE}, {wd.dsp_fail, (uint64_t)w.nupd + 1, 0u}}, e->side);
     } else {
       wd.dsp_cnt = wd.dsp_pre = wd.dsp_val = wd.dsp_nb = wd.dsp_b = wd.dsp_fail = nullptr;
       wd.dsp_blk = nullptr;
+      wd.dsp_j = wd.dsp_js = nullptr;
+      wd.dsp_h = nullptr;
     }
     if (!okd) return fail(YCRDT_E_DEVICE, oom("delete-set scratch"));
     w.dsp_b = wd.dsp_b;  // (the range apply reads which updates took the grid path)

@@ -163,6 +163,10 @@ struct Work {
   uint32_t* dsp_nb = nullptr;      // [nbig] its client blocks
   uint32_t* dsp_gb = nullptr;      // [nbig+1] scan of the delete-set chunks of each big update (the grid's work list)
   uint32_t* dsp_fail = nullptr;    // [nupd] a varuint longer than 6 bytes: the wavefront decodes (and reports) it
+  uint32_t* dsp_j = nullptr;       // [2 cap_ds] per delete-set value index: where 32 header hops from it land (k_dsh_jump)
+  uint32_t* dsp_js = nullptr;      // [2 cap_ds] the run counts those hops pass
+  uint2* dsp_h = nullptr;          // [nbig x (DSH_SEG + 1)] every 32nd header (value index, runs before it); [DSH_SEG]: (failed, runs)
+  uint32_t dsh_grid = 0;           // k_dsh_jump's workgroups per big update
   uint64_t* ds_scan = nullptr;     // [cap_ds+1]
   uint32_t* dsclient_vals = nullptr; // [cap_dsclients] (client values seen in delete sets)
   // ---- per struct (S)
@@ -766,6 +770,7 @@ void launch_shard_export(const Work& w, uint32_t nsegs, const uint8_t* owner, ui
 void launch_merge_final(const Work& w, uint32_t nsegs, hipStream_t s);
 void run_dead_keys(const Work& w, uint32_t nsegs, hipStream_t s);
 constexpr uint32_t DSP_MAXBLK = 8192;  // client blocks of one delete set decoded grid-wide (yc_decode.hip)
+constexpr uint32_t DSH_STRIDE = 32, DSH_SEG = DSP_MAXBLK / DSH_STRIDE;  // header jumps (yc_decode.hip k_dsh_*)
 constexpr uint32_t LISTS_UNNUMBERED = 0xFFFFFFFFu;  // launch_yata: lists exist, launch_ylists numbers them
 uint32_t launch_yata(const Work& w, uint32_t nsegs, uint32_t narray, uint32_t nclients, hipStream_t s, hipStream_t side,
                      hipEvent_t ev_fork, hipEvent_t ev_join);

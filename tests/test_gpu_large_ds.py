@@ -4,7 +4,8 @@ extra workgroups of k_units past DSA_WAVE ranges) against the CPU oracle and the
 A delete set is a flat varuint stream (readDeleteSet, Y@11105); one of at least DSP_MIN bytes in a
 large update — a full state sent as one update, crdt.js:288,443 — is decoded by terminal-byte
 counts, a scan, a per-value decode and a walk over the client blocks. Every case is merged with
-the grid path on (the default) and off (YCRDT_DS_GRID=0: the wavefront per update) and must give
+the grid path on (the default; its client headers found by parallel 32-header jumps, and with
+YCRDT_DS_JUMP=0 by the lane-serial walk) and off (YCRDT_DS_GRID=0: the wavefront per update) and must give
 the oracle's bytes; corrupted and truncated delete sets must be refused (or accepted) exactly as
 the wavefront does, which tests/test_gpu_corrupt.py pins against Yjs.
 """
@@ -40,7 +41,10 @@ def _state_many(n_clients, n, step, seed):
 
 
 def _run(batch, monkeypatch, grid):
+    # grid True: the grid path with its parallel header jumps (k_dsh_*), "hop": the grid path with
+    # the lane-serial header walk (YCRDT_DS_JUMP=0), False: the wavefront per update
     monkeypatch.setenv("YCRDT_DS_GRID", "1" if grid else "0")
+    monkeypatch.setenv("YCRDT_DS_JUMP", "0" if grid == "hop" else "1")
     d = crdt_amd.Doc(client_id=0x7FFFFFF0)
     try:
         d.apply_updates(batch)
@@ -56,6 +60,7 @@ def _check(batch, monkeypatch):
         ref.apply_update(u)
     want = (None, ref.encode_state_as_update(), ref.encode_state_vector())
     assert _run(batch, monkeypatch, True) == want
+    assert _run(batch, monkeypatch, "hop") == want
     assert _run(batch, monkeypatch, False) == want
 
 
@@ -103,7 +108,9 @@ def test_corrupted_and_truncated_delete_sets_like_the_wavefront(monkeypatch):
     v[n - 200:n - 192] = b"\x80" * 8  # a varuint of more than 6 bytes
     cases.append(bytes(v))
     for c in cases:
-        assert _run([c], monkeypatch, True) == _run([c], monkeypatch, False)
+        w = _run([c], monkeypatch, False)
+        assert _run([c], monkeypatch, True) == w
+        assert _run([c], monkeypatch, "hop") == w
 
 
 def test_million_item_full_state_as_one_update(monkeypatch):
