@@ -686,11 +686,23 @@ void launch_write_structs(const Work& w, uint32_t nsegs, uint32_t nclients, hipS
 // struct's start (out_pos), every client block's section record and first struct, the delete set's
 // start. The bitmaps were zeroed by the caller; the count of sections is meta[0] (atomic).
 __global__ void k_state_marks(Work w, uint32_t nout, uint32_t nclients, PreMarks m) {
-  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x, lane = threadIdx.x & 63;
+  // struct starts: positions ascend with t, so a wavefront's bits fall into few words — OR'd across
+  // the lanes of a word first (segmented, by shuffles), one atomic per word and wavefront
+  uint32_t word = NONE;
+  uint64_t bit = 0;
   if (t < nout && w.o_size[t]) {
     const uint32_t p = (uint32_t)out_pos(w, t);
-    atomicOr((unsigned long long*)&m.fbits[p >> 6], 1ull << (p & 63));
+    word = p >> 6;
+    bit = 1ull << (p & 63);
   }
+  for (uint32_t d = 1; d < 64; d <<= 1) {
+    const uint32_t ow = (uint32_t)__shfl_down((int)word, d);
+    const uint64_t ob = ((uint64_t)(uint32_t)__shfl_down((int)(uint32_t)(bit >> 32), d) << 32) | (uint32_t)__shfl_down((int)(uint32_t)bit, d);
+    if (lane + d < 64 && ow == word) bit |= ob;
+  }
+  const uint32_t prev = (uint32_t)__shfl_up((int)word, 1);
+  if (word != NONE && (lane == 0 || prev != word)) atomicOr((unsigned long long*)&m.fbits[word], bit);
   // the client blocks: slot c holds client c's record (n = 0: no block); struct blocks are written
   // in descending client order (both compat modes), which k_predecoded restores when it compacts
   if (t < nclients && t < m.cap_secs) {

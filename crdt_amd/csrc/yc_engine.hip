@@ -179,7 +179,7 @@ enum Buf {
   B_UOWN, B_UFLAG, B_UCUT, B_UWPRE,
   B_GSTART, B_GCIDX, B_GSRC, B_GFLAGS, B_GORIG, B_GRORIG, B_GLINK, B_GOSEG, B_GKEY, B_GMAXC, B_GNEXT, B_GOUTID, B_GTMP, B_GTMP2,
   B_KHASH, B_KROOT, B_KWIN, B_KPAR, B_KFLAG, B_SPK,
-  B_USEC, B_USECN, B_DBG, B_XTAB, B_UFAIL, B_FW, B_CCNT, B_TENTRY, B_XLIST, B_WLEN, B_FWSEC, B_DSPCNT, B_DSPPRE, B_DSPVAL, B_DSPBLK, B_DSPB, B_DSPNB, B_DSPFAIL, B_DSPGB, B_OGEN, B_SDDEFER, B_COFF, B_CPRE, B_OPRE, B_SECUEND, B_SECDOC, B_DSBIGL, B_FWC, B_FWCOFF, B_RTAB, B_RK, B_DSHJ, B_DSHS, B_DSHH, B_JLIST, B_JITEM, B_JARENA, B_JOFF, B_JOUT,
+  B_USEC, B_USECN, B_DBG, B_XTAB, B_UFAIL, B_FW, B_CCNT, B_TENTRY, B_XLIST, B_WLEN, B_FWSEC, B_DSPCNT, B_DSPPRE, B_DSPVAL, B_DSPBLK, B_DSPB, B_DSPNB, B_DSPFAIL, B_DSPGB, B_OGEN, B_SDDEFER, B_COFF, B_CPRE, B_OPRE, B_SECUEND, B_SECDOC, B_DSBIGL, B_DSTAILS, B_FWC, B_FWCOFF, B_RTAB, B_RK, B_DSHJ, B_DSHS, B_DSHH, B_JLIST, B_JITEM, B_JARENA, B_JOFF, B_JOUT,
   B_LZKEY, B_LZKEYS, B_LZIOTA, B_LZSEC, B_LZRSTART, B_LZPREV, B_LZFIRST, B_LZCAP, B_LZEVBASE, B_LZEVN, B_LZFLAG,
   B_LZLHI, B_LZLLO, B_EVKIND, B_EVSRC, B_EVCLOCK, B_EVLEN, B_EVSIZE, B_EVPOS, B_BLKSIZE, B_BLKPOS, B_SVC, B_SVK,
   B_DSMKEY, B_DSMKEYS, B_DSMLEN, B_DSMLENS, B_DSMEND, B_DSMMAX, B_DSMFLAG, B_DSMRID, B_DRCLIENT, B_DRCLOCK, B_DREND,
@@ -1418,6 +1418,12 @@ int run_merge(ycrdt_engine* e, ycrdt_batch* b, const std::unordered_map<uint32_t
   if (U || nds) launch_units_fill(w, U, s);
   mark(e, "merge.units");  // k_units alone
   // with no units, delete-set ranges still have to be checked: each one is pending (pendingDs)
+  {  // long delete-set runs spread over the grid (k_ds_tails; YCRDT_DS_TAILS=0: A/B); without the
+     // buffer every run is flagged by the wavefront that met it
+    bool okt = true;
+    w.ds_tails = D.ds_big && !env_off("YCRDT_DS_TAILS") ? take<uint4>(V, B_DSTAILS, DS_TAILS_CAP, okt) : nullptr;
+    if (!okt) w.ds_tails = nullptr;
+  }
   if (U || nds) launch_units(w, nstructs, nclients, nds, U, D.ds_big, s);
   mark(e, "merge.segments");
   uint32_t nsegs = 0;

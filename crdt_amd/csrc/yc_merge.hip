@@ -116,13 +116,34 @@ __device__ __forceinline__ uint32_t ds_range_units(const Work& w, uint32_t nclie
   gb = w.cl_base[c] + r.clock;
   return len;
 }
+// a run of nl units from g0, by the whole wavefront: with ds_tails (a large delete set) a run past
+// DS_TAIL_MIN units flags its first DS_TAIL_MIN and hands the rest to k_ds_tails, which spreads it
+// over the grid (a C2 document's state holds runs of ~90 k units: 1 400 steps of one wavefront)
+__device__ __forceinline__ void ds_run_wave(const Work& w, uint64_t g0, uint32_t nl, uint32_t lane) {
+  if (w.ds_tails && nl > DS_TAIL_MIN) {
+    uint32_t slot = 0;
+    if (lane == 0) slot = atomicAdd(&w.ctr->ds_ntails, 1u);
+    slot = __shfl(slot, 0);
+    if (slot < DS_TAILS_CAP) {
+      if (lane == 0) {
+        const uint64_t gt = g0 + DS_TAIL_MIN;
+        w.ds_tails[slot] = make_uint4((uint32_t)gt, (uint32_t)(gt >> 32), nl - DS_TAIL_MIN, 0u);
+      }
+      nl = DS_TAIL_MIN;
+    }
+  }
+  for (uint32_t k = lane; k < nl; k += 64) unit_flag(w, (uint32_t)(g0 + k), 1);
+}
 // a wavefront applies the first DSA_WAVE ranges of its update; a large update's delete set (a
 // full state as one update: C3's 156 MB state holds a million ranges) is spread over the extra
 // workgroups of k_units (unit_ds_apply_big)
-__device__ __forceinline__ void unit_ds_apply(const Work& w, uint32_t nclients, uint32_t blk) {
+__device__ __forceinline__ void unit_ds_apply(const Work& w, uint32_t nclients, uint32_t blk, bool big) {
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t u = (blk * blockDim.x + threadIdx.x) >> 6;
   if (u >= w.nupd) return;
+  // (with the spread apply on, an update past DSA_WAVE ranges is applied by it whole: its first
+  // DSA_WAVE ranges were 64 dependent steps of this one wavefront, 0.15 ms on a C2 document's state)
+  if (big && w.ds_count[u] > DSA_WAVE) return;
   const uint32_t n = min(w.ds_count[u], DSA_WAVE), base = w.ds_region[u];
   const uint32_t doc = doc_of_update(w, u);
   for (uint32_t i0 = 0; i0 < n; i0 += 64) {
@@ -135,9 +156,7 @@ __device__ __forceinline__ void unit_ds_apply(const Work& w, uint32_t nclients, 
       for (uint32_t k = 0; k < len; ++k) unit_flag(w, (uint32_t)(gb + k), 1);
     for (uint64_t m = __ballot(lng); m; m &= m - 1) {
       const int L = __ffsll((long long)m) - 1;
-      const uint64_t g0 = shfl64(gb, L);
-      const uint32_t nl = __shfl(len, L);
-      for (uint32_t k = lane; k < nl; k += 64) unit_flag(w, (uint32_t)(g0 + k), 1);
+      ds_run_wave(w, shfl64(gb, L), __shfl(len, L), lane);
     }
   }
 }
@@ -254,7 +273,7 @@ __global__ __launch_bounds__(SEG_LANES) void k_segments_small(Work w, uint64_t n
 // references, every one of them a byte store or an atomic): workgroups [0, nb) take a struct each
 // lane (owner, then references — the struct's columns are loaded once), the rest one update per
 // wavefront (delete sets).
-// ranges DSA_WAVE.. of the delete sets that hold more, one lane per range (grid-stride over the
+// the delete sets that hold more than DSA_WAVE ranges, whole, one lane per range (grid-stride over the
 // extra workgroups). Any update can: a 16 KiB direct-path update of one transaction that deleted
 // ~8 000 scattered items carries that many 2-byte ranges, so the list is every such update the
 // decoders met (k_ds_decode, k_dsp_headers), not the chunk-path updates
@@ -270,7 +289,7 @@ __device__ __forceinline__ void unit_ds_apply_big(const Work& w, uint32_t nclien
     const uint32_t n = w.ds_count[u];
     if (n <= DSA_WAVE) continue;
     const uint32_t base = w.ds_region[u], doc = doc_of_update(w, u);
-    for (uint32_t i0 = DSA_WAVE + wave * 64; i0 < n; i0 += nwaves * 64) {  // (wave-uniform)
+    for (uint32_t i0 = wave * 64; i0 < n; i0 += nwaves * 64) {  // (wave-uniform; every range: unit_ds_apply left them)
       const uint32_t i = i0 + lane;
       uint64_t gb = 0;
       uint32_t len = 0;
@@ -280,11 +299,18 @@ __device__ __forceinline__ void unit_ds_apply_big(const Work& w, uint32_t nclien
         for (uint32_t k = 0; k < len; ++k) unit_flag(w, (uint32_t)(gb + k), 1);
       for (uint64_t m = __ballot(lng); m; m &= m - 1) {
         const int L = __ffsll((long long)m) - 1;
-        const uint64_t g0 = shfl64(gb, L);
-        const uint32_t nl = __shfl(len, L);
-        for (uint32_t k = lane; k < nl; k += 64) unit_flag(w, (uint32_t)(g0 + k), 1);
+        ds_run_wave(w, shfl64(gb, L), __shfl(len, L), lane);
       }
     }
+  }
+}
+// the tails of the long runs (ds_run_wave), every workgroup striding over each of them
+__global__ __launch_bounds__(256) void k_ds_tails(Work w) {
+  const uint32_t n = min(w.ctr->ds_ntails, DS_TAILS_CAP);
+  for (uint32_t t = 0; t < n; ++t) {
+    const uint4 T = w.ds_tails[t];
+    const uint64_t g0 = (uint64_t)T.x | ((uint64_t)T.y << 32);
+    for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < T.z; k += gridDim.x * blockDim.x) unit_flag(w, g0 + k, 1);
   }
 }
 __global__ __launch_bounds__(256) void k_units(Work w, uint32_t nstructs, uint32_t nclients, uint32_t nb, uint32_t nd, uint32_t nx) {
@@ -293,7 +319,7 @@ __global__ __launch_bounds__(256) void k_units(Work w, uint32_t nstructs, uint32
     unit_owner(w, nstructs, s);
     unit_refs(w, nstructs, s);
   } else if (blockIdx.x < nb + nd) {
-    unit_ds_apply(w, nclients, blockIdx.x - nb);
+    unit_ds_apply(w, nclients, blockIdx.x - nb, nx != 0);
   } else {
     unit_ds_apply_big(w, nclients, blockIdx.x - nb - nd, nx);
   }
@@ -305,6 +331,7 @@ void launch_units(const Work& w, uint32_t nstructs, uint32_t nclients, uint32_t 
   const uint32_t nb = (nstructs + 255) / 256, nd = nds && w.nupd ? (w.nupd + 3) / 4 : 0u;
   const uint32_t nx = nd && ds_big ? 256u : 0u;  // a delete set of more than DSA_WAVE ranges (k_dsp_headers says)
   if (nb + nd) hipLaunchKernelGGL(k_units, dim3(nb + nd + nx), dim3(256), 0, s, w, nstructs, nclients, nb, nd, nx);
+  if (nx && w.ds_tails) hipLaunchKernelGGL(k_ds_tails, dim3(512), dim3(256), 0, s, w);
 }
 
 void launch_segments(const Work& w, uint32_t nclients, uint64_t nunits, hipStream_t s) {

@@ -47,7 +47,7 @@ struct Counters {            // device-side counters, read back at the few host 
   uint32_t noncanon;          // lazy decode: an update's sections are not in strictly descending client order
   uint32_t lz_blocks;         // serial lazy merge: output sections
   uint32_t njson;             // JSON-like contents not in JSON.stringify's form (k_json_structs: listed in jlist)
-  uint32_t njson_pad;
+  uint32_t ds_ntails;         // long delete-set runs whose tails k_ds_tails flags (ds_tails)
   unsigned long long out_total; // encoded output size (integrate encoder; 64-bit)
   unsigned long long ds_base;   // integrate encoder: byte position of the delete-set section
   unsigned long long items;  // Σ clock lengths of Skip structs (items = Σ all lengths − this)
@@ -150,6 +150,8 @@ struct Work {
   uint32_t ntrusted = 0;           // the first ntrusted staged updates are doc states the engine wrote: never rewritten
   uint32_t jskip_any = 0;          // 1: a rewrite pass ran: `any` contents are not rewritten again (readAny o writeAny
                                    //    is not idempotent: an own "__proto__" member written by writeAny)
+  uint4* ds_tails = nullptr;       // [DS_TAILS_CAP] (first unit lo, hi, units) of long delete-set runs past their first
+                                   // DS_TAIL_MIN units: flagged grid-wide by k_ds_tails (set only with a large delete set)
   uint32_t* ds_biglist = nullptr;  // [nupd] updates with more than DSA_WAVE ranges (ctr->ds_big of them): k_units spreads
                                    // their ranges past the first DSA_WAVE over extra workgroups, whichever decoder read them
   // large delete sets decoded grid-wide (yc_decode.hip k_dsp_*): per chunk of the large updates
@@ -769,6 +771,7 @@ void launch_shard_mask(const Work& w, uint32_t nsegs, const uint8_t* owner, uint
 void launch_shard_export(const Work& w, uint32_t nsegs, const uint8_t* owner, uint32_t shard, uint32_t* acc, hipStream_t s);
 void launch_merge_final(const Work& w, uint32_t nsegs, hipStream_t s);
 void run_dead_keys(const Work& w, uint32_t nsegs, hipStream_t s);
+constexpr uint32_t DS_TAIL_MIN = 4096, DS_TAILS_CAP = 1u << 16;  // long delete-set runs (yc_merge.hip k_ds_tails)
 constexpr uint32_t DSP_MAXBLK = 8192;  // client blocks of one delete set decoded grid-wide (yc_decode.hip)
 constexpr uint32_t DSH_STRIDE = 32, DSH_SEG = DSP_MAXBLK / DSH_STRIDE;  // header jumps (yc_decode.hip k_dsh_*)
 constexpr uint32_t LISTS_UNNUMBERED = 0xFFFFFFFFu;  // launch_yata: lists exist, launch_ylists numbers them
