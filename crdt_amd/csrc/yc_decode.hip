@@ -2362,8 +2362,20 @@ __global__ void k_prewalk(Work w) {
   w.ufail[u] = UF_WALKED;
 }
 
+// walk_only: every large update must now be pre-decoded or pre-walked; one that is not (the host's
+// struct count and the pre-walk disagree) is a capacity error, and the decode reruns with the walk
+__global__ void k_prewalk_check(Work w) {
+  const uint32_t bi = blockIdx.x * blockDim.x + threadIdx.x;
+  if (bi >= w.nbig) return;
+  const uint32_t u = w.ulist[bi], f = w.ufail[u];
+  if (w.ulen[u] && f != UF_PRE && f != UF_WALKED) raise_err(&w.ctr->err, ERR_CAPACITY);
+}
 void launch_chunks(const Work& w, hipStream_t s) {
   if (w.nbig && !w.force_xtab && !env_off("YCRDT_PREWALK")) hipLaunchKernelGGL(k_prewalk, dim3(w.nbig / 64 + 1), dim3(64), 0, s, w);
+  if (w.walk_only) {  // (a sync reply's delta behind a doc state: the chunk kernels would find nothing to do)
+    hipLaunchKernelGGL(k_prewalk_check, dim3(w.nbig / 64 + 1), dim3(64), 0, s, w);
+    return;
+  }
   if (w.ngroups) {
     if (w.rtab) hipLaunchKernelGGL(k_rtab, dim3((uint32_t)std::min<uint64_t>((uint64_t)w.ngroups * w.schunk / 256 + 1, 16384)), dim3(256), 0, s, w);
     hipLaunchKernelGGL(k_spec, dim3((w.ngroups + DL - 1) / DL), dim3(DL), 0, s, w);

@@ -272,7 +272,7 @@ struct ycrdt_doc {
   bool wants_view = false;  // a view was read once: build it beside every merge (crdt.js reads after each op)
   // Y.applyUpdate is deferred: validated updates wait here and are merged in one
   // batch by the next read (encode*, toJSON, get, local op). n sequential applies cost one merge.
-  struct Queued { std::vector<uint8_t> bytes; bool local; bool ds_error = false; };  // ds_error: read_update
+  struct Queued { std::vector<uint8_t> bytes; bool local; bool ds_error = false; int32_t nst = -1, nsec = -1; };  // ds_error: read_update; nst / nsec: the scan's counts
   std::vector<Queued> queue;
   size_t queue_bytes = 0;
   IngestState ing;       // Yjs pendingStructs / pendingDs / store client order (yc_ingest.h)
@@ -319,6 +319,7 @@ struct ycrdt_batch {
   std::vector<std::vector<uint8_t>> jstore;
   uint32_t jpasses = 0;
   uint32_t ntrusted = 0;        // leading staged updates that are doc states the engine wrote (device sources)
+  bool walk_only = false;       // every large update is the doc state or pre-walked whole (layout): no chunk walk
   uint64_t nbytes = 0;          // span of the batch buffer (windows before the last are 2^32 bytes)
   uint64_t in_bytes = 0;
   bool merged = false;
@@ -372,6 +373,7 @@ struct Src {
   const uint8_t* p;
   size_t len;
   bool dev;
+  int32_t nst = -1, nsec = -1;  // structs / sections, when the host scan of Y.applyUpdate counted them
 };
 
 // Lays out the sources (64-byte aligned, so every update owns its bitmap words; device sources
@@ -448,6 +450,7 @@ void layout(ycrdt_batch* b, const std::vector<Src>& src, std::vector<uint32_t>& 
   }
   const uint64_t wuse = win_use(b->win_shift);
   uint64_t total = 0, win = 0;  // total: bytes used in window `win`
+  bool walk_all = true;
   for (const uint32_t i : order) {
     const size_t len = src[i].len, len64 = (len + 63) & ~size_t(63);
     if (total && total + len64 > wuse) { ++win; total = 0; }  // an update never straddles windows
@@ -470,6 +473,9 @@ void layout(ycrdt_batch* b, const std::vector<Src>& src, std::vector<uint32_t>& 
         b->fwc_off.back() = (uint32_t)b->fwc_recs;
         b->fwc_recs += (len + 63) & ~size_t(63);
       }
+      // (the chunk walk is needed unless every large update is the doc state or one whose struct
+      // section the pre-walk takes whole: <= 64 structs in <= 8 sections, as the host scan counted)
+      if ((int)i != pre && !(src[i].nst >= 0 && src[i].nst <= 64 && src[i].nsec >= 0 && src[i].nsec <= 8)) walk_all = false;
       b->ugroup.push_back((uint32_t)b->groups.size());
       b->ulist.push_back(u);
       for (size_t g = 0; g < len; g += b->schunk) {
@@ -485,6 +491,7 @@ void layout(ycrdt_batch* b, const std::vector<Src>& src, std::vector<uint32_t>& 
     total += len64;
   }
   b->nbig = (uint32_t)b->ulist.size();
+  b->walk_only = walk_all && b->nbig > 0;
   b->ulist.insert(b->ulist.end(), small.begin(), small.end());
   b->uoff.push_back((uint32_t)total);
   b->nwin = (uint32_t)win + 1;
@@ -657,14 +664,17 @@ int stage_srcs(ycrdt_batch* b, const std::vector<Src>& src, const uint32_t* doc_
 
 // n host updates, optionally behind a device-resident doc state (`prefix`, the first update)
 int stage(ycrdt_batch* b, const ycrdt_buf* ups, size_t n, const DevBuf* prefix, size_t prefix_len,
-          const uint32_t* doc_of = nullptr, uint32_t ndocs = 1) {
+          const uint32_t* doc_of = nullptr, uint32_t ndocs = 1, const int32_t* hints = nullptr) {
   if (prefix_len && doc_of && ndocs > 1) return fail(YCRDT_E_ARG, "internal: multi-document batch with a state prefix");
   b->jpasses = 0;
   b->jstore.clear();
   std::vector<Src> src;
   src.reserve(n + 1);
   if (prefix_len) src.push_back(Src{(const uint8_t*)prefix->p, prefix_len, true});
-  for (size_t i = 0; i < n; ++i) src.push_back(Src{ups[i].ptr, ups[i].len, false});
+  for (size_t i = 0; i < n; ++i) {
+    src.push_back(Src{ups[i].ptr, ups[i].len, false});
+    if (hints) { src.back().nst = hints[2 * i]; src.back().nsec = hints[2 * i + 1]; }
+  }
   return stage_srcs(b, src, doc_of, ndocs);
 }
 
@@ -982,6 +992,9 @@ int run_decode(ycrdt_engine* e, ycrdt_batch* b, bool lazy, Decoded& D, bool gene
   {
     const char* mode = getenv("YCRDT_DECODE");
     w.force_xtab = mode && !strcmp(mode, "xtab") ? 1u : 0u;
+    // the chunk walk skipped when the pre-walk takes every large update (YCRDT_WALK_ONLY=0: A/B);
+    // a pre-walk that stops short raises a capacity error and the generous rerun walks the chunks
+    w.walk_only = b->walk_only && !generous && !sh && !w.force_xtab && !env_off("YCRDT_PREWALK") && !env_off("YCRDT_WALK_ONLY") ? 1u : 0u;
     w.fwm_max = getenv("YCRDT_FWM_MAX") ? (uint32_t)atoi(getenv("YCRDT_FWM_MAX")) : 0u;
     const char* sh = getenv("YCRDT_SPEC_HINT");
     // chunk-start hints: single-section updates only by default (a C2 snapshot or replica update
@@ -2295,11 +2308,12 @@ void doc_marks(ycrdt_doc* d) {
 // Merges `extra` (host updates) behind the doc's state in one device pass and makes the result the
 // doc's state. caps: integrate only below the per-client caps (the pending path).
 int commit_merge(ycrdt_doc* d, const std::vector<ycrdt_buf>& extra, const ClockMap* caps,
-                 const std::vector<uint32_t>* order = nullptr) {
+                 const std::vector<uint32_t>* order = nullptr, const std::vector<int32_t>* hints = nullptr) {
   ycrdt_engine* e = d->e;
   ycrdt_batch& b = scratch_batch(e);  // engine-owned: no hipMalloc / hipFree per call
   doc_pre(d, b);
-  int rc = stage(&b, extra.data(), extra.size(), d->state_len ? &d->state : nullptr, d->state_len);
+  int rc = stage(&b, extra.data(), extra.size(), d->state_len ? &d->state : nullptr, d->state_len, nullptr, 1,
+                 hints && hints->size() == 2 * extra.size() ? hints->data() : nullptr);
   // The merged state goes to a block of its own (or the doc's, when it fits and is not the source
   // of this merge any more: the batch holds a copy once staged); the doc changes only once it is
   // there. A small merge queues the copies before its last synchronisation (run_merge's
@@ -2394,9 +2408,15 @@ int flush(ycrdt_doc* d) {
   HIPCHK(hipSetDevice(e->device));
   std::vector<ycrdt_buf> bufs;
   bool ds_errors = false;  // a cut-short delete set takes effect against the state of its time: replay
-  for (const auto& q : d->queue) { bufs.push_back(ycrdt_buf{q.bytes.data(), q.bytes.size()}); ds_errors |= q.ds_error; }
+  std::vector<int32_t> hints;  // the scan's struct / section counts (a large update with few structs: no chunk walk)
+  for (const auto& q : d->queue) {
+    bufs.push_back(ycrdt_buf{q.bytes.data(), q.bytes.size()});
+    ds_errors |= q.ds_error;
+    hints.push_back(q.nst);
+    hints.push_back(q.nsec);
+  }
   if (!d->ing.has_pending && !d->ing.has_ds && e->compat != 135 && !ds_errors) {
-    const int rc = commit_merge(d, bufs, nullptr);
+    const int rc = commit_merge(d, bufs, nullptr, nullptr, &hints);
     if (rc != YCRDT_E_PENDING) {
       if (rc == YCRDT_OK) { d->queue.clear(); d->queue_bytes = 0; }
       return rc;
@@ -2431,8 +2451,8 @@ int flush(ycrdt_doc* d) {
   return YCRDT_OK;
 }
 
-void enqueue(ycrdt_doc* d, const uint8_t* p, size_t n, bool local, bool ds_error = false) {
-  d->queue.push_back(ycrdt_doc::Queued{std::vector<uint8_t>(p, p + n), local, ds_error});
+void enqueue(ycrdt_doc* d, const uint8_t* p, size_t n, bool local, bool ds_error = false, int32_t nst = -1, int32_t nsec = -1) {
+  d->queue.push_back(ycrdt_doc::Queued{std::vector<uint8_t>(p, p + n), local, ds_error, nst, nsec});
   d->queue_bytes += n;
   d->view.valid = false;
 }
@@ -2586,7 +2606,7 @@ int ycrdt_apply_updates(ycrdt_doc* d, const ycrdt_buf* ups, size_t n) {
       }
       return fail(YCRDT_E_DECODE, "Integer out of range! (malformed update " + std::to_string(i) + ")");
     }
-    enqueue(d, ups[i].ptr, ups[i].len, false);
+    enqueue(d, ups[i].ptr, ups[i].len, false, false, (int32_t)std::min<uint64_t>(sc[i].nstructs, 0x7FFFFFFF), (int32_t)sc[i].secs.size());
   }
   if (d->queue_bytes > QUEUE_FLUSH_BYTES) return flush(d);
   return YCRDT_OK;

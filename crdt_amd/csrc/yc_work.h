@@ -130,6 +130,7 @@ struct Work {
                                    // 2 / 3 fast-walked, 4 / 5 resumed by k_walk, UF_PRE decoded by its marks,
                                    // UF_WALKED walked whole by k_prewalk
   uint32_t upre = 0xFFFFFFFFu;     // the update decoded by its marks (k_predecoded), NONE: none
+  uint32_t walk_only = 0;          // 1: every large update is pre-decoded or pre-walked whole (no chunk walk)
   uint64_t* final_bits = nullptr;  // [B/64] verified struct starts
   uint64_t* sec_bits = nullptr;    // [B/64] first struct of every non-empty section
   uint32_t* dsstart = nullptr;     // [nupd] byte position of the delete set
