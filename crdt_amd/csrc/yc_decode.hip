@@ -2967,7 +2967,9 @@ __device__ __forceinline__ bool dsh_update(const Work& w, uint32_t bi, uint32_t&
   const uint32_t g0 = w.ugroup[u] + (w.dsstart[u] - w.uoff[u]) / CH, gl = w.ugroup[u] + (w.ulen[u] + CH - 1) / CH;
   total = w.dsp_pre[gl] - w.dsp_pre[g0];
   vals = w.dsp_val + 2ull * w.ds_region[u];
-  return total >= 1;
+  // (a delete set of few client blocks — C2's snapshots hold one — is walked by k_dsp_headers: the
+  // jumps from every value index cost more than a short walk, and they compete with the struct decode)
+  return total >= 1 && vals[0] > DSH_MIN_BLOCKS;
 }
 __global__ __launch_bounds__(256) void k_dsh_jump(Work w) {
   const uint32_t bi = blockIdx.y;
@@ -3054,11 +3056,16 @@ __global__ void k_dsh_final(Work w) {
   if (f.y > DSA_WAVE) w.ds_biglist[atomicAdd(&w.ctr->ds_big, 1u)] = u;
   w.dsp_b[u] = bi;
 }
-__global__ void k_dsp_headers(Work w) {
+__global__ void k_dsp_headers(Work w, uint32_t jumps) {
   const uint32_t bi = blockIdx.x * blockDim.x + threadIdx.x;
   if (bi >= w.nbig) return;
   const uint32_t u = w.ulist[bi];
   if (!dsp_applies(w, u) || w.dsp_fail[u]) return;
+  if (jumps) {  // (the k_dsh_* kernels take the delete sets of many client blocks)
+    const uint32_t CH = w.schunk;
+    const uint32_t g0 = w.ugroup[u] + (w.dsstart[u] - w.uoff[u]) / CH, gl = w.ugroup[u] + (w.ulen[u] + CH - 1) / CH;
+    if (w.dsp_pre[gl] - w.dsp_pre[g0] >= 1 && w.dsp_val[2ull * w.ds_region[u]] > DSH_MIN_BLOCKS) return;
+  }
   const uint32_t CH = w.schunk;
   const uint32_t g0 = w.ugroup[u] + (w.dsstart[u] - w.uoff[u]) / CH, gl = w.ugroup[u] + (w.ulen[u] + CH - 1) / CH;
   const uint64_t total = w.dsp_pre[gl] - w.dsp_pre[g0];
@@ -3131,13 +3138,13 @@ void launch_ds_grid(const Work& w, hipStream_t s) {
   hipLaunchKernelGGL(k_dsp_count, dim3(DSP_GRID), dim3(256), 0, s, w);
   scan_u32(w.tmp, w.tmp_bytes, w.dsp_cnt, w.dsp_pre, (uint64_t)w.ngroups + 1, s);
   hipLaunchKernelGGL(k_dsp_vals, dim3(DSP_GRID), dim3(256), 0, s, w);
-  if (w.dsp_j && !env_off("YCRDT_DS_JUMP")) {  // (YCRDT_DS_JUMP=0: the lane-serial header walk, A/B)
+  const uint32_t jumps = w.dsp_j && !env_off("YCRDT_DS_JUMP") ? 1u : 0u;  // (YCRDT_DS_JUMP=0: the lane-serial walk, A/B)
+  hipLaunchKernelGGL(k_dsp_headers, dim3(w.nbig / 64 + 1), dim3(64), 0, s, w, jumps);
+  if (jumps) {
     hipLaunchKernelGGL(k_dsh_jump, dim3(w.dsh_grid, w.nbig), dim3(256), 0, s, w);
     hipLaunchKernelGGL(k_dsh_base, dim3(w.nbig / 64 + 1), dim3(64), 0, s, w);
     hipLaunchKernelGGL(k_dsh_fill, dim3(1, w.nbig), dim3(DSH_SEG), 0, s, w);
     hipLaunchKernelGGL(k_dsh_final, dim3(w.nbig / 64 + 1), dim3(64), 0, s, w);
-  } else {
-    hipLaunchKernelGGL(k_dsp_headers, dim3(w.nbig / 64 + 1), dim3(64), 0, s, w);
   }
   hipLaunchKernelGGL(k_dsp_ranges, dim3(DSP_GRID), dim3(256), 0, s, w);
 }
@@ -3571,6 +3578,7 @@ __global__ __launch_bounds__(256) void k_json_structs(Work w, uint32_t nstructs)
   if (w.ntrusted && w.sections[w.s_sec[i]].upd < w.ntrusted) return;  // a doc state: already what Yjs holds
   if (ref == REF_ANY && (w.s_pk[i] & 0x20u)) {  // `any` objects with keys JS treats specially: rewritten
     if (w.jskip_any) return;
+    if (!any_keys_exact(bw, w.s_cpos[i], w.s_cend[i])) return;  // (a repeat-mask false alarm)
     const uint32_t k = atomicAdd(&w.ctr->njson, 1u);
     if (k < w.jcap) w.jlist[k] = i;
     return;

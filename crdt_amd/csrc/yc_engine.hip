@@ -1227,7 +1227,7 @@ int run_decode(ycrdt_engine* e, ycrdt_batch* b, bool lazy, Decoded& D, bool gene
       {  // k_dsh_jump: about one lane per delete-set value of the largest big update
         uint64_t mx = 0;
         for (uint32_t i = 0; i < b->nbig; ++i) mx = std::max<uint64_t>(mx, b->ulen[b->ulist[i]]);
-        wd.dsh_grid = (uint32_t)std::min<uint64_t>(4096, mx / 512 + 1);
+        wd.dsh_grid = (uint32_t)std::min<uint64_t>(256, mx / 512 + 1);  // (grid-stride past 64 K values)
       }
       if (okd) fill_u32_multi({{wd.dsp_b, (uint64_t)w.nupd + 1, NONE}, {wd.dsp_fail, (uint64_t)w.nupd + 1, 0u}}, e->side);
     } else {

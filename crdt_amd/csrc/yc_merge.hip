@@ -284,13 +284,18 @@ __device__ __forceinline__ void unit_ds_apply_big(const Work& w, uint32_t nclien
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t wave = (blk * blockDim.x + threadIdx.x) >> 6, nwaves = nx * blockDim.x / 64;
   const uint32_t nlist = min(w.ctr->ds_big, w.nupd);
+  // the 64-range slices of all listed delete sets, dealt to the wavefronts round-robin across the
+  // updates (a wave per slice index within each update left most of the grid idle when many
+  // updates hold a few thousand ranges each: C2's 112 snapshots)
+  uint32_t gs = wave, before = 0;  // the next global slice of this wave; slices of the updates before bi
   for (uint32_t bi = 0; bi < nlist; ++bi) {
     const uint32_t u = w.ds_biglist[bi];
     const uint32_t n = w.ds_count[u];
     if (n <= DSA_WAVE) continue;
+    const uint32_t ns = (n + 63) / 64;
     const uint32_t base = w.ds_region[u], doc = doc_of_update(w, u);
-    for (uint32_t i0 = wave * 64; i0 < n; i0 += nwaves * 64) {  // (wave-uniform; every range: unit_ds_apply left them)
-      const uint32_t i = i0 + lane;
+    for (; gs < before + ns; gs += nwaves) {  // (wave-uniform; every range: unit_ds_apply left them)
+      const uint32_t i = (gs - before) * 64 + lane;
       uint64_t gb = 0;
       uint32_t len = 0;
       if (i < n) len = ds_range_units(w, nclients, doc, w.ds_tmp[base + i], gb);
@@ -302,6 +307,7 @@ __device__ __forceinline__ void unit_ds_apply_big(const Work& w, uint32_t nclien
         ds_run_wave(w, shfl64(gb, L), __shfl(len, L), lane);
       }
     }
+    before += ns;
   }
 }
 // the tails of the long runs (ds_run_wave), every workgroup striding over each of them

@@ -406,28 +406,6 @@ YC_HDI void any_scalar(const S& b, uint32_t tag, uint32_t& p, uint32_t end, bool
   }
 }
 YC_HDI bool any_scalar_tag(uint32_t tag) { return tag >= 116u && tag <= 127u && tag != 117u && tag != 118u; }
-// whether one of the first `i` keys of a flat object (members from q: key, scalar value) equals the
-// key [ks, ks + k): the exact test behind a repeat-mask hit (rare; inline: a call from the struct
-// decoder would give it a stack frame)
-template <class S>
-YC_HDI bool key_repeats(const S& b, uint32_t q, uint32_t i, uint32_t ks, uint32_t k, uint32_t end) {
-  bool o = true;
-  for (uint32_t j = 0; j < i && o; ++j) {
-    const uint32_t kl = b.vu(q, end, o);
-    if (!o) return false;
-    if (kl == k) {
-      uint32_t x = 0;
-      while (x < k && b.u8(q + x) == b.u8(ks + x)) ++x;
-      if (x == k) return true;
-    }
-    skip_bytes(q, kl, end, o);
-    if (!o || q >= end) return false;
-    const uint32_t t = b.u8(q++);
-    uint32_t cf = 0;
-    any_scalar<false>(b, t, q, end, o, cf);
-  }
-  return false;
-}
 // A one-level array / object of at most 8 scalar members (C1's {name, v}, C2's {name}), inline:
 // true when it was one (p past it; ok false if malformed), false otherwise (p unchanged: the
 // container goes to skip_any_nl).
@@ -439,7 +417,6 @@ YC_HDI bool any_flat(const S& b, uint32_t& p, uint32_t end, uint32_t& steps, boo
   const uint32_t m = b.vu(q, end, o);
   if (!o || m > 8 || st < m + 1) return false;
   if (FULL) c |= vu_overlong_at(b, p0 + 1, q);
-  const uint32_t qm = q;  // the first member
   int64_t prev = -1;
   uint64_t km = 0;  // the keys' repeat mask
   for (uint32_t i = 0; i < m; ++i) {
@@ -456,9 +433,13 @@ YC_HDI bool any_flat(const S& b, uint32_t& p, uint32_t end, uint32_t& steps, boo
         // Object.keys order: array-index keys first, ascending, then the others (skip_any)
         if (ki >= 0 && (prev == -2 || (prev >= 0 && ki <= prev))) c |= ANY_KEYS;
         prev = ki >= 0 ? ki : -2;
-        const uint64_t kb = key_bit(k, k ? b.u8(ks) : 0u, k ? b.u8(ks + k - 1) : 0u);
-        if ((km & kb) && key_repeats(b, qm, i, ks, k, end)) c |= ANY_KEYS;  // (a mask hit: tested exactly)
-        km |= kb;
+        if (m > 1) {  // (one member cannot repeat: C2's {name} values skip the mask)
+          // a mask hit is a possible repeat: flagged here, tested exactly by k_json_structs (the test
+          // inline cost the struct decode a spilled register: +0.5 ms on the C2 headline)
+          const uint64_t kb = key_bit(k, k ? b.u8(ks) : 0u, k ? b.u8(ks + k - 1) : 0u);
+          if (km & kb) c |= ANY_KEYS;
+          km |= kb;
+        }
       }
       if (!o) { ok = false; p = q; return true; }
     }
@@ -1439,6 +1420,20 @@ YC_HD inline __attribute__((noinline)) uint32_t any_content_canon(const uint8_t*
   if (p != end) return JSON_BAD;
   olen = o.n;
   return JSON_OK;
+}
+
+// Whether a ContentAny content [p, end) holds an object whose keys JS treats specially, exactly
+// (skip_any's per-level key hashes; the struct decoder only flags a possible repeat by a mask):
+// k_json_structs lists the struct for the rewrite when it does.
+YC_HD inline __attribute__((noinline)) bool any_keys_exact(const uint8_t* __restrict__ b, uint32_t p, uint32_t end) {
+  bool ok = true;
+  const uint32_t n = rd_vu(b, p, end, ok);
+  for (uint32_t i = 0; i < n && ok; ++i) {
+    uint32_t steps = 0xFFFFFFFFu, cf = 0;
+    if (!skip_any<32, true>(b, p, end, steps, &cf)) return true;  // (deeper than the reader: let the rewrite judge)
+    if (cf & ANY_KEYS) return true;
+  }
+  return false;
 }
 
 // Decoded view of one struct (Y@19286 readClientsStructRefs + readItemContent).

@@ -775,6 +775,7 @@ void run_dead_keys(const Work& w, uint32_t nsegs, hipStream_t s);
 constexpr uint32_t DS_TAIL_MIN = 4096, DS_TAILS_CAP = 1u << 16;  // long delete-set runs (yc_merge.hip k_ds_tails)
 constexpr uint32_t DSP_MAXBLK = 8192;  // client blocks of one delete set decoded grid-wide (yc_decode.hip)
 constexpr uint32_t DSH_STRIDE = 32, DSH_SEG = DSP_MAXBLK / DSH_STRIDE;  // header jumps (yc_decode.hip k_dsh_*)
+constexpr uint32_t DSH_MIN_BLOCKS = 32;  // delete sets of more client blocks take the jumps
 constexpr uint32_t LISTS_UNNUMBERED = 0xFFFFFFFFu;  // launch_yata: lists exist, launch_ylists numbers them
 uint32_t launch_yata(const Work& w, uint32_t nsegs, uint32_t narray, uint32_t nclients, hipStream_t s, hipStream_t side,
                      hipEvent_t ev_fork, hipEvent_t ev_join);
