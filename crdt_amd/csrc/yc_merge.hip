@@ -154,9 +154,11 @@ __device__ __forceinline__ void unit_ds_apply(const Work& w, uint32_t nclients, 
     const bool lng = len > LONG_UNITS;
     if (!lng)
       for (uint32_t k = 0; k < len; ++k) unit_flag(w, (uint32_t)(gb + k), 1);
-    for (uint64_t m = __ballot(lng); m; m &= m - 1) {
+    for (uint64_t m = __ballot(lng); m; m &= m - 1) {  // (a delete set this size: no tails, ds_run_wave)
       const int L = __ffsll((long long)m) - 1;
-      ds_run_wave(w, shfl64(gb, L), __shfl(len, L), lane);
+      const uint64_t g0 = shfl64(gb, L);
+      const uint32_t nl = __shfl(len, L);
+      for (uint32_t k = lane; k < nl; k += 64) unit_flag(w, (uint32_t)(g0 + k), 1);
     }
   }
 }
@@ -319,14 +321,18 @@ __global__ __launch_bounds__(256) void k_ds_tails(Work w) {
     for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < T.z; k += gridDim.x * blockDim.x) unit_flag(w, g0 + k, 1);
   }
 }
+// BIG: the batch holds a delete set of more than DSA_WAVE ranges (the spread workgroups exist). Two
+// builds: the spread apply's registers (it walks a list and hands runs to k_ds_tails) cost the
+// common case — the C2 headline, no such delete set — 0.15 ms of k_units when compiled in.
+template <bool BIG>
 __global__ __launch_bounds__(256) void k_units(Work w, uint32_t nstructs, uint32_t nclients, uint32_t nb, uint32_t nd, uint32_t nx) {
   if (blockIdx.x < nb) {
     const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
     unit_owner(w, nstructs, s);
     unit_refs(w, nstructs, s);
   } else if (blockIdx.x < nb + nd) {
-    unit_ds_apply(w, nclients, blockIdx.x - nb, nx != 0);
-  } else {
+    unit_ds_apply(w, nclients, blockIdx.x - nb, BIG);
+  } else if (BIG) {
     unit_ds_apply_big(w, nclients, blockIdx.x - nb - nd, nx);
   }
 }
@@ -336,7 +342,10 @@ void launch_units_fill(const Work& w, uint64_t nunits, hipStream_t s) {
 void launch_units(const Work& w, uint32_t nstructs, uint32_t nclients, uint32_t nds, uint64_t nunits, bool ds_big, hipStream_t s) {
   const uint32_t nb = (nstructs + 255) / 256, nd = nds && w.nupd ? (w.nupd + 3) / 4 : 0u;
   const uint32_t nx = nd && ds_big ? 256u : 0u;  // a delete set of more than DSA_WAVE ranges (k_dsp_headers says)
-  if (nb + nd) hipLaunchKernelGGL(k_units, dim3(nb + nd + nx), dim3(256), 0, s, w, nstructs, nclients, nb, nd, nx);
+  if (nb + nd) {
+    if (nx) hipLaunchKernelGGL(k_units<true>, dim3(nb + nd + nx), dim3(256), 0, s, w, nstructs, nclients, nb, nd, nx);
+    else hipLaunchKernelGGL(k_units<false>, dim3(nb + nd), dim3(256), 0, s, w, nstructs, nclients, nb, nd, 0u);
+  }
   if (nx && w.ds_tails) hipLaunchKernelGGL(k_ds_tails, dim3(512), dim3(256), 0, s, w);
 }
 
