@@ -60,22 +60,35 @@ bool scan_update(const uint8_t* b, size_t n, bool headers, UpdScan& o) {
   }
   o.struct_end = p;
   o.structs_ok = true;
-  // readAndApplyDeleteSet reads (and applies) range by range
-  const uint32_t nd = rd_vu(b, p, end, ok);
-  if (!ok) return false;
-  for (uint32_t i = 0; i < nd; ++i) {
-    const uint32_t client = rd_vu(b, p, end, ok);
-    const uint32_t nr = rd_vu(b, p, end, ok);
-    if (!ok) return false;
-    ScanDs e{client, (uint32_t)o.ranges.size(), 0};
-    for (uint32_t k = 0; k < nr; ++k) {
-      const uint32_t clock = rd_vu(b, p, end, ok);
-      const uint32_t len = rd_vu(b, p, end, ok);
-      if (!ok) { o.ds.push_back(e); return false; }
-      o.ranges.push_back({clock, len});
-      ++e.n;
+  // readAndApplyDeleteSet reads (and applies) range by range. The ranges are kept only where a
+  // caller reads them (headers: the pending emulation) or where the set is cut short (the part read
+  // before the error still applies: repaired_update); a valid set is only checked — a sync reply
+  // carries the peer's whole delete set, 70 k ranges for a C2 document, on every Y.applyUpdate
+  const uint32_t ds0 = p;
+  auto read_ds = [&](bool keep) -> bool {
+    uint32_t q = ds0;
+    bool okd = true;
+    const uint32_t nd = rd_vu(b, q, end, okd);
+    if (!okd) return false;
+    for (uint32_t i = 0; i < nd; ++i) {
+      const uint32_t client = rd_vu(b, q, end, okd);
+      const uint32_t nr = rd_vu(b, q, end, okd);
+      if (!okd) return false;
+      ScanDs e{client, (uint32_t)o.ranges.size(), 0};
+      for (uint32_t k = 0; k < nr; ++k) {
+        const uint32_t clock = rd_vu(b, q, end, okd);
+        const uint32_t len = rd_vu(b, q, end, okd);
+        if (!okd) { if (keep) o.ds.push_back(e); return false; }
+        if (keep) o.ranges.push_back({clock, len});
+        ++e.n;
+      }
+      if (keep) o.ds.push_back(e);
     }
-    o.ds.push_back(e);
+    return true;
+  };
+  if (!read_ds(headers)) {
+    if (!headers) read_ds(true);  // (again, keeping what was read before the error)
+    return false;
   }
   o.ds_ok = true;
   return true;
@@ -350,7 +363,7 @@ int read_update(IngestState& S, const uint8_t* u, size_t n, bool local, const Me
   const bool h1 = pending_ds_of(sc, S.state, ds1);
   if (S.has_ds) {
     UpdScan ps;
-    if (!scan_update(S.pending_ds.data(), S.pending_ds.size(), false, ps)) { err = "internal: pendingDs"; return YCRDT_E_DECODE; }
+    if (!scan_update(S.pending_ds.data(), S.pending_ds.size(), true, ps)) { err = "internal: pendingDs"; return YCRDT_E_DECODE; }
     const bool h2 = pending_ds_of(ps, S.state, ds2);
     if (h1 && h2) {
       std::vector<uint8_t> merged;
