@@ -65,6 +65,45 @@ bool scan_update(const uint8_t* b, size_t n, bool headers, UpdScan& o) {
   // before the error still applies: repaired_update); a valid set is only checked — a sync reply
   // carries the peer's whole delete set, 70 k ranges for a C2 document, on every Y.applyUpdate
   const uint32_t ds0 = p;
+  // Checking skips t varuints eight bytes a load: a byte below 0x80 ends one (rd_vu), so a word is
+  // passed whole while it ends at most t of them; rd_vu's only other error — a sixth continuation
+  // byte in a row — sends the set to the exact reader (it ends no valid set: u32 values take five)
+  auto skip_vus = [&](uint32_t& q, uint32_t t) -> bool {
+    uint32_t run = 0;  // continuation bytes carried over from the words passed
+    while (t && q + 8 <= end) {
+      uint64_t w;
+      std::memcpy(&w, b + q, 8);
+      const uint64_t cont = w & 0x8080808080808080ull;
+      const uint32_t ends = (uint32_t)(((~w & 0x8080808080808080ull) >> 7) * 0x0101010101010101ull >> 56);
+      if (ends > t) break;
+      if (cont & (cont >> 8) & (cont >> 16) & (cont >> 24) & (cont >> 32) & (cont >> 40)) return false;
+      const uint32_t lead = cont == 0x8080808080808080ull ? 8u : (uint32_t)__builtin_ctzll(~cont & 0x8080808080808080ull) >> 3;
+      if (run + lead >= 6) return false;
+      run = cont == 0x8080808080808080ull ? run + 8 : (uint32_t)__builtin_clzll(~cont & 0x8080808080808080ull) >> 3;
+      t -= ends;
+      q += 8;
+    }
+    q -= run;  // back to the start of the varuint the last word passed ended inside of
+    bool okd = true;
+    for (; t; --t) {
+      rd_vu(b, q, end, okd);
+      if (!okd) return false;
+    }
+    return true;
+  };
+  auto check_ds = [&]() -> bool {
+    uint32_t q = ds0;
+    bool okd = true;
+    const uint32_t nd = rd_vu(b, q, end, okd);
+    if (!okd) return false;
+    for (uint32_t i = 0; i < nd; ++i) {
+      rd_vu(b, q, end, okd);
+      const uint32_t nr = rd_vu(b, q, end, okd);
+      if (!okd) return false;
+      if (nr >= 0x80000000u || !skip_vus(q, 2 * nr)) return false;
+    }
+    return true;
+  };
   auto read_ds = [&](bool keep) -> bool {
     uint32_t q = ds0;
     bool okd = true;
@@ -86,7 +125,7 @@ bool scan_update(const uint8_t* b, size_t n, bool headers, UpdScan& o) {
     }
     return true;
   };
-  if (!read_ds(headers)) {
+  if (headers ? !read_ds(true) : !check_ds() && !read_ds(false)) {
     if (!headers) read_ds(true);  // (again, keeping what was read before the error)
     return false;
   }
