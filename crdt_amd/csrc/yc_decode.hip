@@ -2458,11 +2458,19 @@ __global__ __launch_bounds__(256) void k_wlen(Work w) {
 }
 constexpr uint32_t WR_LANES = 1024;
 constexpr uint16_t WR_INF = 0xFFFFu;
-__global__ __launch_bounds__(WR_LANES) void k_wrank(Work w) {
+// k_wrank's LDS for updates of at most `cap` bytes: the two jump tables and the distances (u16,
+// cap + 3 entries each), then the struct-start bitmap. Sized to the batch's longest small update
+// (Work::small_max), not to WD_MAX: at 16 KiB a workgroup takes 100 KB and one fits a CU; a
+// replica update of 11 KB takes 67 KB, and two share a CU.
+__host__ __device__ constexpr uint32_t wr_tab(uint32_t cap) { return (cap + 3 + 3) & ~3u; }  // (u16 entries, 8-byte multiple)
+__host__ __device__ constexpr size_t wr_lds(uint32_t cap) { return 3 * (size_t)wr_tab(cap) * 2 + ((cap + 63) / 64) * 8; }
+__global__ __launch_bounds__(WR_LANES) void k_wrank(Work w, uint32_t cap) {
   // [L]: the update end, [L + 1]: no struct parses, [L + 2]: a position k_wlen left unevaluated
-  __shared__ uint16_t ja[WD_MAX + 3], jb[WD_MAX + 3], dist[WD_MAX + 3];
-  __shared__ uint32_t sh_later;
-  __shared__ uint64_t bits[WD_WORDS];
+  extern __shared__ __attribute__((aligned(16))) uint64_t wr_smem[];
+  uint16_t* const ja = (uint16_t*)wr_smem;
+  uint16_t* const jb = ja + wr_tab(cap);
+  uint16_t* const dist = jb + wr_tab(cap);
+  uint64_t* const bits = (uint64_t*)(dist + wr_tab(cap));
   __shared__ uint32_t sh_base, sh_last;
   const uint32_t t = threadIdx.x, j = blockIdx.x;
   const uint32_t u = w.ulist[w.nbig + j];
@@ -2474,7 +2482,7 @@ __global__ __launch_bounds__(WR_LANES) void k_wrank(Work w) {
   uint16_t* __restrict__ dl = w.wlen + (size_t)j * WD_MAX;
   bool sized = false;  // every position sized (the rare kinds too)
   uint32_t* err = &w.ctr->err;
-  if (L > WD_MAX) { if (t == 0) raise_err(err, ERR_CAPACITY); return; }  // (the layout never sends one)
+  if (L > WD_MAX || L > cap) { if (t == 0) raise_err(err, ERR_CAPACITY); return; }  // (the layout never sends one)
   bool ok = true;
   uint32_t q = ustart;
   const uint32_t nsec = rd_vu(b, q, uend, ok);
@@ -2586,8 +2594,15 @@ void launch_direct(const Work& w, hipStream_t s) {
   // (a split decode's share may take this path where the whole batch did not: no rank tables)
   if (wave_decode(w) && ((wm && !strcmp(wm, "settle")) || !w.wlen)) hipLaunchKernelGGL(k_wdecode, dim3(w.nsmall), dim3(64), 0, s, w);
   else if (wave_decode(w)) {
-    hipLaunchKernelGGL(k_wlen, dim3(WD_MAX / WL_SPAN, w.nsmall), dim3(256), 0, s, w);
-    hipLaunchKernelGGL(k_wrank, dim3(w.nsmall), dim3(WR_LANES), 0, s, w);
+    const uint32_t cap = std::min(std::max(w.small_max, 1u), WD_MAX);
+    static const bool lds_set = [] {  // (dynamic LDS past 64 KB: up to the WD_MAX table set)
+      const bool r = hipFuncSetAttribute((const void*)k_wrank, hipFuncAttributeMaxDynamicSharedMemorySize, (int)wr_lds(WD_MAX)) == hipSuccess;
+      if (!r) (void)hipGetLastError();
+      return r;
+    }();
+    (void)lds_set;
+    hipLaunchKernelGGL(k_wlen, dim3((cap + WL_SPAN - 1) / WL_SPAN, w.nsmall), dim3(256), 0, s, w);
+    hipLaunchKernelGGL(k_wrank, dim3(w.nsmall), dim3(WR_LANES), wr_lds(cap), s, w, cap);
   } else if (w.nsmall) {
     // (one lane per update; 64 / 96 / 256 B windows and 2 / 4 / 8 lanes per update with a
     // wavefront-local chain sync were slower on C2: DESIGN.md §5.1)

@@ -988,6 +988,8 @@ int run_decode(ycrdt_engine* e, ycrdt_batch* b, bool lazy, Decoded& D, bool gene
   w.nbig = b->nbig;
   w.schunk = b->schunk;
   w.nsmall = (uint32_t)b->ulist.size() - b->nbig;
+  w.small_max = 0;
+  for (size_t i = b->nbig; i < b->ulist.size(); ++i) w.small_max = std::max(w.small_max, b->ulen[b->ulist[i]]);
   w.lazy = lazy ? 1u : 0u;
   {
     const char* mode = getenv("YCRDT_DECODE");

@@ -91,6 +91,7 @@ struct Work {
   uint32_t ndocs = 1;
   const uint32_t* ulist = nullptr; // [nbig] updates on the chunk path, then [nsmall] parsed directly
   uint32_t nbig = 0, nsmall = 0;
+  uint32_t small_max = 0;          // the longest of the [nsmall] updates (host-known: k_wlen's grid, k_wrank's LDS)
   uint32_t* fwsec = nullptr;       // [2 cap_sections] k_fastwalk_multi: each section's chain range [q, e)
   uint4* fwc = nullptr;            // record mode (k_fwc): per byte of a multi-section large update, the section
                                    // step from a header there {next header, chain range end, walked, why}
