@@ -98,6 +98,21 @@ def test_wave_periodic_streams(wave, capfd, n):
         _check([u], capfd)
 
 
+def test_wave_lds_sized_to_longest(wave, capfd):
+    """k_wrank's LDS is sized to the batch's longest small update (Work::small_max): an update at
+    the 16 KiB limit (100 KB of LDS) beside tiny ones, tiny ones alone, and a mid-size one."""
+    n = 812
+    while len(_periodic(n, 1)) > WAVE_MAX:
+        n -= 1
+    big = _periodic(n, 1)
+    assert len(big) > WAVE_MAX - 64
+    tiny = [_periodic(k, 2 + k) for k in (1, 3, 9)]
+    _check(tiny + [big], capfd)
+    _check([big] + tiny, capfd)
+    _check(tiny, capfd)
+    _check([_periodic(300, 5)] + tiny, capfd)
+
+
 def test_wave_long_delete_sets(wave, capfd):
     """An update whose delete set is most of its bytes: many (clock, len) ranges of many clients,
     byte patterns the lanes' chains parse as struct runs."""
